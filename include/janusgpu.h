@@ -1,0 +1,175 @@
+/*
+ * janusgpu.h — C-ABI of libjanusgpu, the MI355X (gfx950) OLAP graph-computer engine
+ * behind GpuGraphComputer, the drop-in for JanusGraph's FulgoraGraphComputer.
+ *
+ * Plain C: pointers + sizes, no torch / HIP / C++ types.  Every entry point returns an int
+ * status (JG_OK = 0, < 0 = error class) and never throws or aborts across the ABI; the message
+ * of the last failure on the calling thread is available from jg_last_error().
+ *
+ * What each entry point replaces in the reference (paths relative to
+ * /root/reference/janusgraph-core/src/main/java/org/janusgraph/):
+ *
+ *   jg_ctx_create / jg_ctx_create_rank
+ *       FulgoraGraphComputer(StandardJanusGraph, Configuration) + workers(n)
+ *       graphdb/olap/computer/FulgoraGraphComputer.java:101-106,134-139
+ *   jg_graph_build
+ *       the per-superstep edgestore scan: StandardScannerExecutor.run
+ *       (diskstorage/keycolumnvalue/scan/StandardScannerExecutor.java:97-216) feeding
+ *       VertexJobConverter.process (graphdb/olap/VertexJobConverter.java:122-151: ghost skip)
+ *       and the canonical-id map (graphdb/olap/computer/FulgoraVertexMemory.java:74-77).
+ *       Done ONCE per computer instead of once per superstep.
+ *   jg_pagerank (+ begin/step/end)
+ *       executeVertexProgram superstep loop (FulgoraGraphComputer.java:210-230) running
+ *       janusgraph-backend-testutils/.../olap/PageRankVertexProgram.java:89-110, with the gather of
+ *       VertexMemoryHandler.receiveMessages (graphdb/olap/computer/VertexMemoryHandler.java:121-151)
+ *   jg_shortest_distance
+ *       the same loop running ShortestDistanceVertexProgram.java:112-146 with
+ *       ShortestDistanceMessageCombiner.java:29-31 (min)
+ *   jg_bfs
+ *       TinkerPop ShortestPathVertexProgram under Fulgora's forced {Local(bothE), Global} scopes
+ *       (FulgoraGraphComputer.java:249-253): hop depth per source (paths are rebuilt host-side)
+ *   jg_connected_components
+ *       TinkerPop ConnectedComponentVertexProgram (String-min label over BOTH edges,
+ *       VertexProgramScanJob.java:113-135 loads BOTH); pinned by OLAPTest.java:736-762
+ *   jg_graph_info_get / jg_ctx_last_stats
+ *       ScanMetrics counters (StandardScanMetrics.java:28-88: ghost-vertices, truncated-results)
+ *       and memory().getIteration()/getRuntime() (FulgoraMemory.java:97-101)
+ *
+ * Ownership: host arrays passed in are caller-owned and read only during the call; outputs are
+ * caller-allocated.  Device memory is owned by the library (per jg_graph) and freed by
+ * jg_graph_destroy.  A jg_ctx is not re-entrant: one call in flight per context.
+ */
+#ifndef JANUSGPU_H
+#define JANUSGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JG_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define JG_OK               0
+#define JG_ERR_ARG         -1  /* bad argument (null pointer, size, unknown vertex id …)        */
+#define JG_ERR_OOM         -2  /* device or host allocation failed                                */
+#define JG_ERR_HIP         -3  /* HIP runtime error                                               */
+#define JG_ERR_RCCL        -4  /* RCCL communicator / collective error                            */
+#define JG_ERR_UNSUPPORTED -5  /* operation not available for this graph/context configuration  */
+#define JG_ERR_STATE       -6  /* call out of order (e.g. step before begin)                      */
+
+/* ---- adjacency requested at build time (bit flags) ---- */
+#define JG_ADJ_OUT  1u  /* out-adjacency: rows = source vertex (bottom-up of IN traversals)        */
+#define JG_ADJ_IN   2u  /* in-adjacency:  rows = target vertex (PageRank pull, SD push)           */
+#define JG_ADJ_BOTH 4u  /* symmetrised:   rows = every vertex, a self-loop appears twice (BOTH)   */
+
+/* ---- traversal direction (the MessageScope.Local incident traversal) ---- */
+#define JG_DIR_OUT  1   /* follow u->v edges from u          */
+#define JG_DIR_IN   2   /* follow u->v edges from v back to u */
+#define JG_DIR_BOTH 3
+
+/* Fulgora's hard limit on entries per non-BOTH slice (graphdb/olap/QueryContainer.java:42,133) */
+#define JG_FULGORA_HARD_QUERY_LIMIT 100000
+
+typedef struct jg_ctx jg_ctx;
+typedef struct jg_graph jg_graph;
+
+typedef struct jg_graph_info {
+    int64_t num_vertices;        /* |V| handed to the build (existing, non-ghost vertices)          */
+    int64_t num_edges;           /* edges kept: both endpoints in V                                  */
+    int64_t ghost_edges;         /* edges dropped because an endpoint is not in V                    */
+    int64_t self_loops;          /* kept edges with src == dst                                       */
+    int64_t truncated_vertices;  /* vertices with > JG_FULGORA_HARD_QUERY_LIMIT edge entries (in+out):
+                                    Fulgora would silently truncate their OUT/IN slices; we do not  */
+    int64_t max_in_degree;
+    int64_t max_out_degree;
+    int64_t device_bytes;        /* device memory held by this graph, summed over shards             */
+    int32_t num_shards;          /* 1D vertex partitions (one per device / rank)                    */
+    uint32_t flags;              /* JG_ADJ_* actually built                                          */
+} jg_graph_info;
+
+typedef struct jg_stats {
+    int32_t supersteps;          /* memory().getIteration() of the equivalent Fulgora run           */
+    int32_t levels;              /* BFS/SSSP levels or CC sweeps actually executed on the GPU       */
+    double  build_ms;            /* last jg_graph_build*: snapshot -> CSR on device                 */
+    double  compute_ms;          /* last program: HIP-event time of the superstep loop              */
+    double  exchange_ms;         /* part of compute_ms spent in RCCL / peer exchange                */
+    double  kernel_ms_total;     /* sum of HIP-event durations of the dominant kernel                */
+    int64_t kernel_launches;     /* number of launches of the dominant kernel that were timed       */
+    double  algorithmic_bytes;   /* SURVEY §8(d) byte model for the last program, whole run         */
+    double  edges_traversed;     /* adjacency entries examined (for TEPS)                           */
+} jg_stats;
+
+/* ---- library / context ---- */
+int         jg_abi_version(void);
+const char* jg_last_error(void);
+
+/* One process driving `ndev` devices (the JVM case).  ndev > 1 shards the graph 1D over the listed
+ * devices; distinct devices exchange through RCCL (ncclCommInitAll), a device listed more than once
+ * holds several logical shards that exchange by device copies (test mode). */
+int jg_ctx_create(const int* devices, int ndev, jg_ctx** out);
+
+/* One process per GPU (torch.distributed style): this process is `rank` of `nranks`, driving
+ * `device`.  `unique_id` is the JG_UNIQUE_ID_BYTES blob from jg_comm_unique_id() on rank 0,
+ * broadcast out-of-band by the caller.  nranks == 1 needs no unique_id (may be NULL). */
+#define JG_UNIQUE_ID_BYTES 128
+int jg_comm_unique_id(void* out /* JG_UNIQUE_ID_BYTES */);
+int jg_ctx_create_rank(int device, int nranks, int rank, const void* unique_id, jg_ctx** out);
+int jg_ctx_destroy(jg_ctx* ctx);
+int jg_ctx_last_stats(const jg_ctx* ctx, jg_stats* out);
+/* Record HIP events around every launch of the dominant kernel (costs ~1 us per launch). */
+int jg_ctx_set_profiling(jg_ctx* ctx, int enable);
+
+/* ---- graph snapshot ---- */
+/* vid[n]: the ids of the vertices the scan returned (unique, any order; outputs are indexed the same
+ * way).  src/dst[m]: edge endpoints as vertex ids; an edge whose endpoint is not in vid is a ghost
+ * edge and is dropped.  weight[m] (nullable): Integer edge property for jg_shortest_distance; NULL
+ * means unit weights.  Multi-edges and self-loops are kept (JanusGraph MULTI semantics). */
+int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n,
+                   const int64_t* src, const int64_t* dst, const int32_t* weight, int64_t m,
+                   uint32_t flags, jg_graph** out);
+
+/* Synthetic Graph500 Kronecker (RMAT a,b,c,d = .57,.19,.19,.05) graph generated on the device(s):
+ * n = 2^scale vertices with ids 0..n-1, m = edgefactor * n directed edges, seeded and
+ * bit-identical to oracle/jg_oracle.c:jo_rmat_edges. */
+int jg_graph_build_rmat(jg_ctx* ctx, int scale, int edgefactor, uint64_t seed, uint32_t flags,
+                        jg_graph** out);
+int jg_graph_info_get(const jg_graph* g, jg_graph_info* out);
+int jg_graph_destroy(jg_graph* g);
+
+/* ---- programs ---- */
+/* JanusGraph PageRankVertexProgram: `iterations` = maxIterations K (supersteps 0..K, i.e. K-1 power
+ * steps), `vertex_count` = the user-supplied vertexCount N (NOT |V|).  rank_out[n] / edge_count_out[n]
+ * (nullable) receive janusgraph.pageRank.pageRank / .edgeCount; with K == 0 no property is written
+ * and rank_out is filled with NaN. */
+int jg_pagerank(jg_graph* g, double damping, int64_t vertex_count, int32_t iterations,
+                double* rank_out, double* edge_count_out);
+/* The same run split for benchmarking: begin = supersteps 0 and 1, step = `nsteps` power supersteps
+ * enqueued asynchronously, end = synchronise + copy results (either pointer nullable). */
+int jg_pagerank_begin(jg_graph* g, double damping, int64_t vertex_count);
+int jg_pagerank_step(jg_graph* g, int32_t nsteps);
+int jg_pagerank_end(jg_graph* g, double* rank_out, double* edge_count_out);
+
+/* ShortestDistanceVertexProgram: dist_out[v] = min over paths v -> ... -> seed of <= max_depth hops
+ * of the summed edge weights (int64), or -1 where Fulgora leaves DISTANCE absent. */
+int jg_shortest_distance(jg_graph* g, int64_t seed_vid, int32_t max_depth, int64_t* dist_out);
+
+/* Hop depth from each of nsrc sources (nsrc <= 64 runs as one bit-parallel multi-source BFS);
+ * depth_out[s * n + v] = hops or -1 (unreached / beyond max_depth; max_depth < 0 = unbounded).
+ * depth_out may be NULL (benchmarking: results stay on the device). */
+int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction,
+           int32_t max_depth, int32_t* depth_out);
+
+/* ConnectedComponentVertexProgram: component_vid_out[v] = the vertex id whose decimal String is the
+ * component label (the String-minimum id of v's weakly connected component).  iterations_out
+ * (nullable) = supersteps of the synchronous program. */
+int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out);
+
+/* Block until all work enqueued on the graph's streams is complete. */
+int jg_graph_sync(jg_graph* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JANUSGPU_H */

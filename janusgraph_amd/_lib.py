@@ -1,0 +1,251 @@
+"""ctypes binding of libjanusgpu (include/janusgpu.h).
+
+The HIP library is the only compute path: if libjanusgpu.so is missing or fails to load, every
+entry point raises — there is no CPU fallback in the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjanusgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "janusgpu.h")
+
+JG_OK = 0
+JG_ERR_ARG = -1
+JG_ERR_OOM = -2
+JG_ERR_HIP = -3
+JG_ERR_RCCL = -4
+JG_ERR_UNSUPPORTED = -5
+JG_ERR_STATE = -6
+
+ADJ_OUT, ADJ_IN, ADJ_BOTH = 1, 2, 4
+DIR_OUT, DIR_IN, DIR_BOTH = 1, 2, 3
+FULGORA_HARD_QUERY_LIMIT = 100000
+UNIQUE_ID_BYTES = 128
+
+# every function the header declares (checked by tests/test_abi.py against include/janusgpu.h)
+EXPORTS = [
+    "jg_abi_version", "jg_last_error", "jg_ctx_create", "jg_comm_unique_id", "jg_ctx_create_rank",
+    "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_rmat",
+    "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
+    "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_graph_sync",
+]
+
+
+class GraphInfo(ctypes.Structure):
+    _fields_ = [
+        ("num_vertices", ctypes.c_int64), ("num_edges", ctypes.c_int64), ("ghost_edges", ctypes.c_int64),
+        ("self_loops", ctypes.c_int64), ("truncated_vertices", ctypes.c_int64),
+        ("max_in_degree", ctypes.c_int64), ("max_out_degree", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
+        ("num_shards", ctypes.c_int32), ("flags", ctypes.c_uint32),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("supersteps", ctypes.c_int32), ("levels", ctypes.c_int32), ("build_ms", ctypes.c_double),
+        ("compute_ms", ctypes.c_double), ("exchange_ms", ctypes.c_double), ("kernel_ms_total", ctypes.c_double),
+        ("kernel_launches", ctypes.c_int64), ("algorithmic_bytes", ctypes.c_double),
+        ("edges_traversed", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class JanusGpuError(RuntimeError):
+    """A non-zero status from libjanusgpu (the Java side wraps these in JanusGraphException)."""
+
+    def __init__(self, code, message):
+        super().__init__(f"libjanusgpu error {code}: {message}")
+        self.code = code
+
+
+_lib = None
+_P = ctypes.c_void_p
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+
+def load():
+    """Load libjanusgpu.so (raises if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libjanusgpu.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` (hipcc, gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "jg_abi_version": ([], ctypes.c_int),
+        "jg_last_error": ([], ctypes.c_char_p),
+        "jg_ctx_create": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int, _PP], ctypes.c_int),
+        "jg_comm_unique_id": ([_P], ctypes.c_int),
+        "jg_ctx_create_rank": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _PP], ctypes.c_int),
+        "jg_ctx_destroy": ([_P], ctypes.c_int),
+        "jg_ctx_last_stats": ([_P, ctypes.POINTER(Stats)], ctypes.c_int),
+        "jg_ctx_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
+        "jg_graph_build": ([_P, _P, _i64, _P, _P, _P, _i64, ctypes.c_uint32, _PP], ctypes.c_int),
+        "jg_graph_build_rmat": ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, _PP],
+                                ctypes.c_int),
+        "jg_graph_info_get": ([_P, ctypes.POINTER(GraphInfo)], ctypes.c_int),
+        "jg_graph_destroy": ([_P], ctypes.c_int),
+        "jg_pagerank": ([_P, ctypes.c_double, _i64, _i32, _P, _P], ctypes.c_int),
+        "jg_pagerank_begin": ([_P, ctypes.c_double, _i64], ctypes.c_int),
+        "jg_pagerank_step": ([_P, _i32], ctypes.c_int),
+        "jg_pagerank_end": ([_P, _P, _P], ctypes.c_int),
+        "jg_shortest_distance": ([_P, _i64, _i32, _P], ctypes.c_int),
+        "jg_bfs": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
+        "jg_connected_components": ([_P, _P, _P], ctypes.c_int),
+        "jg_graph_sync": ([_P], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(status):
+    if status != JG_OK:
+        msg = load().jg_last_error()
+        raise JanusGpuError(status, msg.decode() if msg else "")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    check(load().jg_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return buf.raw
+
+
+class Context:
+    """jg_ctx: one process driving `devices` (sharded 1D when several), or rank `rank` of `nranks`."""
+
+    def __init__(self, devices=(0,), rank=None, nranks=1, unique_id=None):
+        L = load()
+        self._h = ctypes.c_void_p()
+        if rank is None:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            check(L.jg_ctx_create(devs, len(devices), ctypes.byref(self._h)))
+        else:
+            uid = None
+            if unique_id is not None:
+                self._uid = ctypes.create_string_buffer(bytes(unique_id), UNIQUE_ID_BYTES)
+                uid = ctypes.cast(self._uid, ctypes.c_void_p)
+            check(L.jg_ctx_create_rank(int(devices[0]), int(nranks), int(rank), uid, ctypes.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            check(load().jg_ctx_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_profiling(self, on=True):
+        check(load().jg_ctx_set_profiling(self._h, 1 if on else 0))
+
+    def stats(self) -> dict:
+        s = Stats()
+        check(load().jg_ctx_last_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def build(self, vid, src, dst, weight=None, flags=ADJ_IN | ADJ_OUT | ADJ_BOTH) -> "Graph":
+        vid = np.ascontiguousarray(vid, np.int64)
+        src = np.ascontiguousarray(src, np.int64)
+        dst = np.ascontiguousarray(dst, np.int64)
+        if len(src) != len(dst):
+            raise ValueError("src and dst differ in length")
+        w = None if weight is None else np.ascontiguousarray(weight, np.int32)
+        if w is not None and len(w) != len(src):
+            raise ValueError("weight must have one entry per edge")
+        h = ctypes.c_void_p()
+        check(load().jg_graph_build(self._h, _ptr(vid), len(vid), _ptr(src), _ptr(dst), _ptr(w), len(src),
+                                    flags, ctypes.byref(h)))
+        return Graph(self, h, len(vid))
+
+    def build_rmat(self, scale, edgefactor=16, seed=1, flags=ADJ_IN) -> "Graph":
+        h = ctypes.c_void_p()
+        check(load().jg_graph_build_rmat(self._h, scale, edgefactor, seed, flags, ctypes.byref(h)))
+        return Graph(self, h, 1 << scale)
+
+
+class Graph:
+    """jg_graph: a device-resident CSR snapshot; outputs are indexed like the vid[] it was built from."""
+
+    def __init__(self, ctx: Context, handle, n):
+        self.ctx, self._h, self.n = ctx, handle, n
+
+    def close(self):
+        if self._h:
+            check(load().jg_graph_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        i = GraphInfo()
+        check(load().jg_graph_info_get(self._h, ctypes.byref(i)))
+        return i.as_dict()
+
+    def sync(self):
+        check(load().jg_graph_sync(self._h))
+
+    def pagerank(self, damping=0.85, vertex_count=1, iterations=10):
+        rank = np.empty(self.n, np.float64)
+        ec = np.empty(self.n, np.float64)
+        check(load().jg_pagerank(self._h, float(damping), int(vertex_count), int(iterations), _ptr(rank), _ptr(ec)))
+        return rank, ec
+
+    def pagerank_begin(self, damping=0.85, vertex_count=1):
+        check(load().jg_pagerank_begin(self._h, float(damping), int(vertex_count)))
+
+    def pagerank_step(self, nsteps=1):
+        check(load().jg_pagerank_step(self._h, int(nsteps)))
+
+    def pagerank_end(self, want=True):
+        rank = np.empty(self.n, np.float64) if want else None
+        ec = np.empty(self.n, np.float64) if want else None
+        check(load().jg_pagerank_end(self._h, _ptr(rank), _ptr(ec)))
+        return rank, ec
+
+    def shortest_distance(self, seed_vid, max_depth):
+        dist = np.empty(self.n, np.int64)
+        check(load().jg_shortest_distance(self._h, int(seed_vid), int(max_depth), _ptr(dist)))
+        return dist
+
+    def bfs(self, sources, direction=DIR_BOTH, max_depth=-1, want=True):
+        src = np.ascontiguousarray(np.atleast_1d(sources), np.int64)
+        depth = np.empty(len(src) * self.n, np.int32) if want else None
+        check(load().jg_bfs(self._h, _ptr(src), len(src), int(direction), int(max_depth), _ptr(depth)))
+        return None if depth is None else depth.reshape(len(src), self.n)
+
+    def connected_components(self):
+        comp = np.empty(self.n, np.int64)
+        it = ctypes.c_int32(0)
+        check(load().jg_connected_components(self._h, _ptr(comp), ctypes.byref(it)))
+        return comp, int(it.value)

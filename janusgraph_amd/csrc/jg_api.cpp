@@ -1,0 +1,514 @@
+// jg_api.cpp — the extern "C" boundary of libjanusgpu (include/janusgpu.h), contexts, the RCCL
+// exchange and profiling.  No exception or abort crosses the ABI: every entry point catches and
+// returns a status, with the message kept per thread for jg_last_error().
+//
+// Error style mirrors FulgoraGraphComputer's "Computer is aborting" failures
+// (janusgraph-core/.../olap/computer/FulgoraGraphComputer.java:269-286): any failure aborts the
+// whole program run; callers wrap a non-zero status in a JanusGraphException.
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+#include "jg_internal.h"
+
+namespace jg {
+
+namespace {
+thread_local std::string g_last_error;
+
+void rccl_check(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) fail(JG_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+}  // namespace
+
+void fail(int code, const std::string& msg) { throw Error(code, msg); }
+
+void hip_check(hipError_t e, const char* what, const char* file, int line) {
+    if (e != hipSuccess) {
+        const char* base = std::strrchr(file, '/');
+        fail(e == hipErrorOutOfMemory ? JG_ERR_OOM : JG_ERR_HIP,
+             std::string(what) + " failed: " + hipGetErrorString(e) + " (" + (base ? base + 1 : file) + ":" +
+                 std::to_string(line) + ")");
+    }
+}
+
+int64_t Graph::dense_of_vid(int64_t v) const {
+    if (sorted_vid.empty()) return (v >= 0 && v < n) ? v : -1;
+    auto it = std::lower_bound(sorted_vid.begin(), sorted_vid.end(), v);
+    if (it == sorted_vid.end() || *it != v) return -1;
+    return sorted_dense[(size_t)(it - sorted_vid.begin())];
+}
+
+void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
+    if (g.P == 1) return;
+    Ctx& c = *g.ctx;
+    const size_t slice = (size_t)g.S * elem_bytes;
+    if (c.logical) {  // all shards on one device and stream: device copies of the owned slices
+        Shard& s0 = *g.shards[0];
+        DeviceGuard dg(s0.device);
+        for (size_t dst = 0; dst < g.shards.size(); ++dst)
+            for (size_t src = 0; src < g.shards.size(); ++src) {
+                if (src == dst) continue;
+                const int r = g.shards[src]->index;
+                char* d = static_cast<char*>(bufs[dst]) + (size_t)r * slice;
+                const char* s = static_cast<const char*>(bufs[src]) + (size_t)r * slice;
+                JG_HIP(hipMemcpyAsync(d, s, slice, hipMemcpyDeviceToDevice, s0.stream));
+            }
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        char* base = static_cast<char*>(bufs[i]);
+        rccl_check(ncclAllGather(base + (size_t)sh.index * slice, base, (size_t)g.S,
+                                 type, sh.comm, sh.stream),
+                   "ncclAllGather");
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+int allreduce_or(Graph& g, int flag) {
+    Ctx& c = *g.ctx;
+    if (c.nranks == 1) return flag;  // in-process shards already combined by the caller
+    Shard& sh = *g.shards[0];
+    DeviceGuard dg(sh.device);
+    DevBuf<int32_t> d(1);
+    int32_t v = flag ? 1 : 0;
+    JG_HIP(hipMemcpyAsync(d.get(), &v, sizeof v, hipMemcpyHostToDevice, sh.stream));
+    rccl_check(ncclAllReduce(d.get(), d.get(), 1, ncclInt32, ncclMax, sh.comm, sh.stream), "ncclAllReduce");
+    JG_HIP(hipMemcpyAsync(&v, d.get(), sizeof v, hipMemcpyDeviceToHost, sh.stream));
+    JG_HIP(hipStreamSynchronize(sh.stream));
+    return v;
+}
+
+bool prof_enabled(const Ctx& c) { return c.profiling; }
+
+void prof_record_start(Ctx& c, Shard& sh) {
+    if (!c.profiling) return;
+    hipEvent_t e;
+    JG_HIP(hipEventCreate(&e));
+    JG_HIP(hipEventRecord(e, sh.stream));
+    sh.prof_events.push_back(e);
+}
+
+void prof_record_stop(Ctx& c, Shard& sh) { prof_record_start(c, sh); }
+
+void prof_collect(Ctx& c, Graph& g) {
+    double total = 0;
+    int64_t launches = 0;
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        DeviceGuard dg(sh.device);
+        for (size_t i = 0; i + 1 < sh.prof_events.size(); i += 2) {
+            JG_HIP(hipEventSynchronize(sh.prof_events[i + 1]));
+            float ms = 0;
+            JG_HIP(hipEventElapsedTime(&ms, sh.prof_events[i], sh.prof_events[i + 1]));
+            total += ms;
+            ++launches;
+        }
+        for (auto e : sh.prof_events) (void)hipEventDestroy(e);
+        sh.prof_events.clear();
+    }
+    c.last.kernel_ms_total += total;
+    c.last.kernel_launches += launches;
+}
+
+static void make_shards(Ctx& c, Graph& g) {
+    g.P = c.total_shards();
+    for (size_t i = 0; i < c.devices.size(); ++i) {
+        auto sh = std::make_unique<Shard>();
+        sh->device = c.devices[i];
+        sh->index = c.rank * (int)c.devices.size() + (int)i;
+        sh->stream = c.streams[i];
+        sh->comm = c.comms.empty() ? nullptr : c.comms[i];
+        g.shards.push_back(std::move(sh));
+    }
+}
+
+}  // namespace jg
+
+using jg::Error;
+
+#define JG_GUARD_BEGIN try {
+#define JG_GUARD_END                                       \
+    return JG_OK;                                          \
+    }                                                      \
+    catch (const Error& e) {                               \
+        jg::g_last_error_set(e.what());                    \
+        return e.code;                                     \
+    }                                                      \
+    catch (const std::bad_alloc&) {                        \
+        jg::g_last_error_set("host allocation failed");    \
+        return JG_ERR_OOM;                                 \
+    }                                                      \
+    catch (const std::exception& e) {                      \
+        jg::g_last_error_set(e.what());                    \
+        return JG_ERR_HIP;                                 \
+    }
+
+namespace jg {
+void g_last_error_set(const char* m) { g_last_error = m ? m : ""; }
+}  // namespace jg
+
+#define JG_ARG(cond, msg) \
+    if (!(cond)) jg::fail(JG_ERR_ARG, msg)
+
+extern "C" {
+
+int jg_abi_version(void) { return JG_ABI_VERSION; }
+
+const char* jg_last_error(void) { return jg::g_last_error.c_str(); }
+
+int jg_comm_unique_id(void* out) {
+    JG_GUARD_BEGIN
+    JG_ARG(out, "null output");
+    ncclUniqueId id;
+    jg::rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    static_assert(sizeof(ncclUniqueId) == JG_UNIQUE_ID_BYTES, "unique id size");
+    std::memcpy(out, &id, sizeof id);
+    JG_GUARD_END
+}
+
+int jg_ctx_create(const int* devices, int ndev, jg_ctx** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(out && devices && ndev > 0, "jg_ctx_create: need devices and an output pointer");
+    *out = nullptr;
+    int count = 0;
+    JG_HIP(hipGetDeviceCount(&count));
+    for (int i = 0; i < ndev; ++i)
+        JG_ARG(devices[i] >= 0 && devices[i] < count, "jg_ctx_create: device ordinal out of range");
+    auto ctx = std::make_unique<jg_ctx>();
+    jg::Ctx& c = ctx->impl;
+    c.devices.assign(devices, devices + ndev);
+    bool all_same = true;
+    for (int i = 1; i < ndev; ++i) all_same &= devices[i] == devices[0];
+    c.logical = ndev > 1 && all_same;
+    if (ndev > 1 && !all_same) {
+        std::vector<int> sorted(c.devices);
+        std::sort(sorted.begin(), sorted.end());
+        JG_ARG(std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end(),
+               "jg_ctx_create: mix of repeated and distinct devices");
+    }
+    for (int i = 0; i < ndev; ++i) {
+        jg::DeviceGuard dg(c.devices[i]);
+        hipStream_t s = nullptr;
+        if (c.logical && i > 0) s = c.streams[0];  // logical shards share one stream
+        else JG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        c.streams.push_back(s);
+    }
+    if (ndev > 1 && !c.logical) {
+        c.comms.resize(ndev);
+        jg::rccl_check(ncclCommInitAll(c.comms.data(), ndev, c.devices.data()), "ncclCommInitAll");
+    }
+    *out = ctx.release();
+    JG_GUARD_END
+}
+
+int jg_ctx_create_rank(int device, int nranks, int rank, const void* unique_id, jg_ctx** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(out && nranks >= 1 && rank >= 0 && rank < nranks, "jg_ctx_create_rank: bad rank arguments");
+    JG_ARG(nranks == 1 || unique_id, "jg_ctx_create_rank: unique_id required for nranks > 1");
+    *out = nullptr;
+    int count = 0;
+    JG_HIP(hipGetDeviceCount(&count));
+    JG_ARG(device >= 0 && device < count, "jg_ctx_create_rank: device ordinal out of range");
+    auto ctx = std::make_unique<jg_ctx>();
+    jg::Ctx& c = ctx->impl;
+    c.devices = {device};
+    c.nranks = nranks;
+    c.rank = rank;
+    jg::DeviceGuard dg(device);
+    hipStream_t s = nullptr;
+    JG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    c.streams.push_back(s);
+    if (nranks > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof id);
+        ncclComm_t comm;
+        jg::rccl_check(ncclCommInitRank(&comm, nranks, id, rank), "ncclCommInitRank");
+        c.comms.push_back(comm);
+    }
+    *out = ctx.release();
+    JG_GUARD_END
+}
+
+int jg_ctx_destroy(jg_ctx* ctx) {
+    JG_GUARD_BEGIN
+    if (!ctx) return JG_OK;
+    jg::Ctx& c = ctx->impl;
+    for (auto cm : c.comms) ncclCommDestroy(cm);
+    for (size_t i = 0; i < c.streams.size(); ++i) {
+        if (c.logical && i > 0) continue;
+        jg::DeviceGuard dg(c.devices[i]);
+        (void)hipStreamDestroy(c.streams[i]);
+    }
+    delete ctx;
+    JG_GUARD_END
+}
+
+int jg_ctx_last_stats(const jg_ctx* ctx, jg_stats* out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx && out, "null argument");
+    *out = ctx->impl.last;
+    JG_GUARD_END
+}
+
+int jg_ctx_set_profiling(jg_ctx* ctx, int enable) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx, "null context");
+    ctx->impl.profiling = enable != 0;
+    JG_GUARD_END
+}
+
+int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* src, const int64_t* dst,
+                   const int32_t* weight, int64_t m, uint32_t flags, jg_graph** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx && out, "null argument");
+    JG_ARG(n >= 0 && m >= 0, "negative size");
+    JG_ARG(n == 0 || vid, "vid is null");
+    JG_ARG(m == 0 || (src && dst), "src/dst is null");
+    JG_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 vertices");
+    JG_ARG(m < (int64_t)UINT32_MAX, "more than 2^32-1 edges");
+    JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
+    *out = nullptr;
+    jg::Ctx& c = ctx->impl;
+    auto gh = std::make_unique<jg_graph>();
+    jg::Graph& g = gh->impl;
+    g.ctx = &c;
+    g.n = n;
+    g.flags = flags;
+    g.has_weights = weight != nullptr;
+    jg::make_shards(c, g);
+    g.vid.assign(vid, vid + n);
+    {
+        std::vector<std::pair<int64_t, int64_t>> t(n);
+        for (int64_t i = 0; i < n; ++i) t[i] = {vid[i], i};
+        std::sort(t.begin(), t.end());
+        for (int64_t i = 1; i < n; ++i)
+            if (t[i].first == t[i - 1].first) jg::fail(JG_ERR_ARG, "duplicate vertex id in vid[]");
+        g.sorted_vid.resize(n);
+        g.sorted_dense.resize(n);
+        for (int64_t i = 0; i < n; ++i) {
+            g.sorted_vid[i] = t[i].first;
+            g.sorted_dense[i] = t[i].second;
+        }
+    }
+    hipEvent_t t0, t1;
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
+    }
+    std::vector<jg::DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size()), dw(g.shards.size());
+    jg::DenseEdges e;
+    e.m = m;
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        jg::Shard& sh = *g.shards[i];
+        jg::DeviceGuard dg(sh.device);
+        jg::DevBuf<int64_t> dvid(std::max<int64_t>(n, 1)), dsrc(std::max<int64_t>(m, 1)), ddst(std::max<int64_t>(m, 1));
+        if (n) JG_HIP(hipMemcpy(dvid.get(), vid, n * sizeof(int64_t), hipMemcpyHostToDevice));
+        if (m) {
+            JG_HIP(hipMemcpy(dsrc.get(), src, m * sizeof(int64_t), hipMemcpyHostToDevice));
+            JG_HIP(hipMemcpy(ddst.get(), dst, m * sizeof(int64_t), hipMemcpyHostToDevice));
+        }
+        ds[i].alloc(std::max<int64_t>(m, 1));
+        dd[i].alloc(std::max<int64_t>(m, 1));
+        jg::remap_ids_device(dvid.get(), n, dsrc.get(), ddst.get(), m, ds[i].get(), dd[i].get(), sh.stream);
+        e.src.push_back(ds[i].get());
+        e.dst.push_back(dd[i].get());
+        if (weight) {
+            dw[i].alloc(std::max<int64_t>(m, 1));
+            if (m) JG_HIP(hipMemcpy(dw[i].get(), weight, m * sizeof(int32_t), hipMemcpyHostToDevice));
+            e.weight.push_back(dw[i].get());
+        } else {
+            e.weight.push_back(nullptr);
+        }
+    }
+    jg::build_graph_from_dense(g, e);
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
+        JG_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        c.last = jg_stats{};
+        c.last.build_ms = ms;
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
+    *out = gh.release();
+    JG_GUARD_END
+}
+
+int jg_graph_build_rmat(jg_ctx* ctx, int scale, int edgefactor, uint64_t seed, uint32_t flags, jg_graph** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx && out, "null argument");
+    JG_ARG(scale >= 1 && scale <= 30 && edgefactor >= 1 && edgefactor <= 64, "bad RMAT scale/edgefactor");
+    JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
+    *out = nullptr;
+    const int64_t n = 1ll << scale, m = (int64_t)edgefactor << scale;
+    JG_ARG(m < (int64_t)UINT32_MAX, "too many edges");
+    jg::Ctx& c = ctx->impl;
+    auto gh = std::make_unique<jg_graph>();
+    jg::Graph& g = gh->impl;
+    g.ctx = &c;
+    g.n = n;
+    g.flags = flags;
+    jg::make_shards(c, g);
+    hipEvent_t t0, t1;
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
+    }
+    std::vector<jg::DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size());
+    jg::DenseEdges e;
+    e.m = m;
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        jg::Shard& sh = *g.shards[i];
+        jg::DeviceGuard dg(sh.device);
+        ds[i].alloc(m);
+        dd[i].alloc(m);
+        jg::generate_rmat_device(scale, seed, m, ds[i].get(), dd[i].get(), sh.stream);
+        e.src.push_back(ds[i].get());
+        e.dst.push_back(dd[i].get());
+        e.weight.push_back(nullptr);
+    }
+    jg::build_graph_from_dense(g, e);
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
+        JG_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        c.last = jg_stats{};
+        c.last.build_ms = ms;
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
+    *out = gh.release();
+    JG_GUARD_END
+}
+
+int jg_graph_info_get(const jg_graph* g, jg_graph_info* out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && out, "null argument");
+    *out = g->impl.info;
+    JG_GUARD_END
+}
+
+int jg_graph_destroy(jg_graph* g) {
+    JG_GUARD_BEGIN
+    if (!g) return JG_OK;
+    for (auto& sp : g->impl.shards) {
+        jg::DeviceGuard dg(sp->device);
+        (void)hipStreamSynchronize(sp->stream);
+    }
+    delete g;
+    JG_GUARD_END
+}
+
+int jg_graph_sync(jg_graph* g) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    for (auto& sp : g->impl.shards) {
+        jg::DeviceGuard dg(sp->device);
+        JG_HIP(hipStreamSynchronize(sp->stream));
+    }
+    JG_GUARD_END
+}
+
+int jg_pagerank_begin(jg_graph* g, double damping, int64_t vertex_count) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    g->impl.ctx->last = jg_stats{};
+    jg::pagerank_begin(g->impl, damping, vertex_count);
+    JG_GUARD_END
+}
+
+int jg_pagerank_step(jg_graph* g, int32_t nsteps) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && nsteps >= 0, "bad arguments");
+    jg::pagerank_steps(g->impl, nsteps);
+    JG_GUARD_END
+}
+
+int jg_pagerank_end(jg_graph* g, double* rank_out, double* edge_count_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    jg::pagerank_end(g->impl, rank_out, edge_count_out);
+    jg::Graph& gr = g->impl;
+    jg::Ctx& c = *gr.ctx;
+    c.last.supersteps = gr.pr_steps + 1;
+    double nnz = 0;
+    for (auto& sp : gr.shards) nnz += (double)sp->in.nnz;
+    c.last.edges_traversed = nnz * gr.pr_steps;
+    c.last.algorithmic_bytes = (12.0 * nnz + 32.0 * (double)gr.n) * gr.pr_steps;
+    JG_GUARD_END
+}
+
+int jg_pagerank(jg_graph* g, double damping, int64_t vertex_count, int32_t iterations, double* rank_out,
+                double* edge_count_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    JG_ARG(iterations >= 0, "negative iterations");
+    jg::Graph& gr = g->impl;
+    if (iterations == 0) {  // only superstep 0 runs: no property is written
+        if (rank_out) std::fill(rank_out, rank_out + gr.n, std::numeric_limits<double>::quiet_NaN());
+        if (edge_count_out) std::fill(edge_count_out, edge_count_out + gr.n, std::numeric_limits<double>::quiet_NaN());
+        gr.ctx->last = jg_stats{};
+        return JG_OK;
+    }
+    gr.ctx->last = jg_stats{};
+    jg::Shard& sh0 = *gr.shards[0];
+    jg::DeviceGuard dg(sh0.device);
+    hipEvent_t t0, t1;
+    JG_HIP(hipEventCreate(&t0));
+    JG_HIP(hipEventCreate(&t1));
+    JG_HIP(hipEventRecord(t0, sh0.stream));
+    jg::pagerank_begin(gr, damping, vertex_count);
+    jg::pagerank_steps(gr, iterations - 1);
+    JG_HIP(hipEventRecord(t1, sh0.stream));
+    jg::pagerank_end(gr, rank_out, edge_count_out);
+    float ms = 0;
+    JG_HIP(hipEventSynchronize(t1));
+    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    jg::Ctx& c = *gr.ctx;
+    c.last.compute_ms = ms;
+    c.last.supersteps = iterations;
+    double nnz = 0;
+    for (auto& sp : gr.shards) nnz += (double)sp->in.nnz;
+    c.last.edges_traversed = nnz * (iterations - 1);
+    c.last.algorithmic_bytes = (12.0 * nnz + 32.0 * (double)gr.n) * (iterations - 1);
+    JG_GUARD_END
+}
+
+int jg_shortest_distance(jg_graph* g, int64_t seed_vid, int32_t max_depth, int64_t* dist_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && dist_out, "null argument");
+    JG_ARG(max_depth >= 0, "negative maxDepth");
+    jg::shortest_distance_run(g->impl, seed_vid, max_depth, dist_out);
+    JG_GUARD_END
+}
+
+int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth,
+           int32_t* depth_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && source_vids, "null argument");
+    jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, depth_out);
+    JG_GUARD_END
+}
+
+int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    jg::cc_run(g->impl, component_vid_out, iterations_out);
+    JG_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,527 @@
+// jg_build.hip — the CSR snapshot that replaces Fulgora's per-superstep edgestore scan.
+//
+// Reference semantics (paths under /root/reference/janusgraph-core/src/main/java/org/janusgraph/):
+//   graphdb/olap/VertexJobConverter.java:122-151   ghost vertices never execute or send: an edge
+//                                                  counts only if both endpoints exist
+//   graphdb/olap/computer/FulgoraVertexMemory.java:74-77  canonical id per vertex
+//   graphdb/database/StandardJanusGraph.java:617-640       a self-loop has an OUT and an IN entry on
+//                                                  its row: once in OUT, once in IN, twice in BOTH
+//   graphdb/olap/QueryContainer.java:42,133        100000-entry hard limit (reported, not applied)
+//
+// Pipeline per shard (device): degrees -> degree-sorted relabel (radix sort) -> padded global ids ->
+// per-CSR key select (row<<cbits | col) -> stable radix sort -> row_ptr by boundary detection.
+#include <algorithm>
+#include <climits>
+
+#include "jg_internal.h"
+#include "jg_prim.h"
+
+namespace jg {
+
+namespace {
+
+// ---------------- Graph500 Kronecker generator (bit-identical to oracle jo_rmat_edges) ----------------
+struct RmatParams {
+    uint64_t seedmix;
+    uint32_t t_ab, t_anorm, t_cnorm;
+    int32_t scale;
+    uint64_t mask;
+    uint64_t k1, c1, k2, c2, k3, c3;
+    int32_t sh;
+};
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+RmatParams rmat_params(int scale, uint64_t seed) {
+    const double A = 0.57, B = 0.19, C = 0.19;
+    const double ab = A + B, c_norm = C / (1.0 - (A + B)), a_norm = A / (A + B);
+    RmatParams p;
+    p.seedmix = splitmix64(seed);
+    p.t_ab = (uint32_t)(ab * 4294967296.0);
+    p.t_anorm = (uint32_t)(a_norm * 4294967296.0);
+    p.t_cnorm = (uint32_t)(c_norm * 4294967296.0);
+    p.scale = scale;
+    p.mask = scale >= 64 ? ~0ull : ((1ull << scale) - 1ull);
+    p.k1 = splitmix64(seed ^ 0x1111111111111111ull) | 1ull;
+    p.c1 = splitmix64(seed ^ 0x2222222222222222ull);
+    p.k2 = splitmix64(seed ^ 0x3333333333333333ull) | 1ull;
+    p.c2 = splitmix64(seed ^ 0x4444444444444444ull);
+    p.k3 = splitmix64(seed ^ 0x5555555555555555ull) | 1ull;
+    p.c3 = splitmix64(seed ^ 0x6666666666666666ull);
+    p.sh = scale > 1 ? (scale + 1) / 2 : 1;
+    return p;
+}
+
+__device__ __forceinline__ uint64_t rmat_perm(const RmatParams& p, uint64_t x) {
+    x = (x * p.k1 + p.c1) & p.mask;
+    x ^= x >> p.sh;
+    x = (x * p.k2 + p.c2) & p.mask;
+    x ^= x >> p.sh;
+    x = (x * p.k3 + p.c3) & p.mask;
+    return x;
+}
+
+__global__ __launch_bounds__(kBlock) void rmat_kernel(RmatParams p, int64_t m, int32_t* __restrict__ src,
+                                                      int32_t* __restrict__ dst) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t i = 0, j = 0;
+        for (int l = 0; l < p.scale; ++l) {
+            const uint64_t h = splitmix64((((uint64_t)e << 6) | (uint64_t)l) ^ p.seedmix);
+            const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+            const uint64_t ii = lo >= p.t_ab;
+            const uint64_t jj = hi >= (ii ? p.t_cnorm : p.t_anorm);
+            i |= ii << l;
+            j |= jj << l;
+        }
+        src[e] = (int32_t)rmat_perm(p, i);
+        dst[e] = (int32_t)rmat_perm(p, j);
+    }
+}
+
+// ---------------- id remap ----------------
+__global__ void vid_keys_kernel(const int64_t* __restrict__ vid, int64_t n, uint64_t* __restrict__ keys,
+                                uint32_t* __restrict__ vals) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        keys[i] = (uint64_t)vid[i] ^ 0x8000000000000000ull;  // order-preserving for signed ids
+        vals[i] = (uint32_t)i;
+    }
+}
+
+__global__ void dup_check_kernel(const uint64_t* __restrict__ keys, int64_t n, int32_t* __restrict__ dup) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (keys[i] == keys[i - 1]) *dup = 1;
+}
+
+__device__ __forceinline__ int32_t lookup_dense(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                int64_t n, int64_t id) {
+    const uint64_t k = (uint64_t)id ^ 0x8000000000000000ull;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    return (lo < n && keys[lo] == k) ? (int32_t)vals[lo] : -1;
+}
+
+__global__ void remap_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n,
+                             const int64_t* __restrict__ s, const int64_t* __restrict__ d, int64_t m,
+                             int32_t* __restrict__ ds, int32_t* __restrict__ dd) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        ds[e] = lookup_dense(keys, vals, n, s[e]);
+        dd[e] = lookup_dense(keys, vals, n, d[e]);
+    }
+}
+
+// ---------------- degrees & relabel ----------------
+__global__ void degree_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m,
+                              int32_t* __restrict__ indeg, int32_t* __restrict__ outdeg,
+                              unsigned long long* __restrict__ counters /* kept, loops */) {
+    unsigned long long kept = 0, loops = 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t a = src[e], b = dst[e];
+        if (a < 0 || b < 0) continue;
+        atomicAdd(&outdeg[a], 1);
+        atomicAdd(&indeg[b], 1);
+        ++kept;
+        loops += (a == b);
+    }
+    kept = wave_reduce_add(kept);
+    loops = wave_reduce_add(loops);
+    if (lane_id() == 0) {
+        atomicAdd(&counters[0], kept);
+        atomicAdd(&counters[1], loops);
+    }
+}
+
+// key = (maxdeg - deg) << vbits | v  (ascending sort = degree descending, then id ascending)
+__global__ void relabel_keys_kernel(const int32_t* __restrict__ indeg, const int32_t* __restrict__ outdeg, int64_t n,
+                                    int mode, int64_t maxdeg, int vbits, uint64_t* __restrict__ keys) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        int64_t d = mode == 0 ? indeg[v] : mode == 1 ? (int64_t)indeg[v] + outdeg[v] : outdeg[v];
+        keys[v] = ((uint64_t)(maxdeg - d) << vbits) | (uint64_t)v;
+    }
+}
+
+__global__ void stats_kernel(const int32_t* __restrict__ indeg, const int32_t* __restrict__ outdeg, int64_t n,
+                             unsigned long long* __restrict__ out /* max_in, max_out, truncated */) {
+    unsigned long long mi = 0, mo = 0, tr = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long a = (unsigned)indeg[v], b = (unsigned)outdeg[v];
+        mi = a > mi ? a : mi;
+        mo = b > mo ? b : mo;
+        tr += (a + b) > (unsigned long long)JG_FULGORA_HARD_QUERY_LIMIT;
+    }
+    atomicMax(&out[0], mi);
+    atomicMax(&out[1], mo);
+    tr = wave_reduce_add(tr);
+    if (lane_id() == 0) atomicAdd(&out[2], tr);
+}
+
+// order[k] = dense vertex of degree rank k;  padded[v] = g(k) = (k % P) * S + k / P
+__global__ void padded_ids_kernel(const uint64_t* __restrict__ sorted_keys, int64_t n, uint64_t vmask, int P,
+                                  int64_t S, int32_t* __restrict__ order, int32_t* __restrict__ padded) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = (int32_t)(sorted_keys[k] & vmask);
+        order[k] = v;
+        padded[v] = (int32_t)((k % P) * S + k / P);
+    }
+}
+
+__global__ void local_outdeg_kernel(const int32_t* __restrict__ order, const int32_t* __restrict__ outdeg, int64_t n,
+                                    int P, int r, int64_t rows, int32_t* __restrict__ out) {
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = (int64_t)r + l * P;
+        out[l] = k < n ? outdeg[order[k]] : 0;
+    }
+}
+
+// ---------------- key select (stable) ----------------
+// Emits, in edge order, the keys of the CSR entries owned by shard r.
+//   which = 0: IN   row = dst, col = src
+//           1: OUT  row = src, col = dst
+//           2: BOTH both of the above (an edge contributes its OUT entry then its IN entry)
+constexpr int kSelItems = 8;
+constexpr int kSelTile = kBlock * kSelItems;
+
+struct SelectArgs {
+    const int32_t* src;
+    const int32_t* dst;
+    const int32_t* padded;
+    int64_t m;
+    int64_t S;
+    int r;
+    int which;
+    int cbits;
+};
+
+__device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
+    const int32_t s = a.src[e], d = a.dst[e];
+    if (s < 0 || d < 0) return 0;
+    const int32_t gs = a.padded[s], gd = a.padded[d];
+    const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
+    if (a.which == 0) return own_d;
+    if (a.which == 1) return own_s;
+    return (int)own_s + (int)own_d;
+}
+
+__global__ __launch_bounds__(kBlock) void select_count_kernel(SelectArgs a, int64_t* __restrict__ block_counts) {
+    __shared__ int64_t scratch[kBlock / kWave];
+    const int64_t base = (int64_t)blockIdx.x * kSelTile + (int64_t)threadIdx.x * kSelItems;
+    int64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kSelItems; ++k)
+        if (base + k < a.m) c += emit_count(a, base + k);
+    c = wave_reduce_add(c);
+    if (lane_id() == 0) scratch[wave_id()] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) t += scratch[w];
+        block_counts[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, const int64_t* __restrict__ block_off,
+                                                              uint64_t* __restrict__ keys, uint32_t* __restrict__ eidx) {
+    __shared__ int64_t scratch[kBlock / kWave];
+    const int64_t base = (int64_t)blockIdx.x * kSelTile + (int64_t)threadIdx.x * kSelItems;
+    int64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kSelItems; ++k)
+        if (base + k < a.m) c += emit_count(a, base + k);
+    int64_t total;
+    int64_t pos = block_exclusive_scan_add(c, scratch, &total) + block_off[blockIdx.x];
+    for (int k = 0; k < kSelItems; ++k) {
+        const int64_t e = base + k;
+        if (e >= a.m) break;
+        const int32_t s = a.src[e], d = a.dst[e];
+        if (s < 0 || d < 0) continue;
+        const int64_t gs = a.padded[s], gd = a.padded[d];
+        const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
+        if ((a.which == 1 || a.which == 2) && own_s) {
+            keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)gd;
+            if (eidx) eidx[pos] = (uint32_t)e;
+            ++pos;
+        }
+        if ((a.which == 0 || a.which == 2) && own_d) {
+            keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)gs;
+            if (eidx) eidx[pos] = (uint32_t)e;
+            ++pos;
+        }
+    }
+}
+
+__global__ void fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// row_ptr[rr] = first entry of row rr; rows without entries get the next row's start.
+__global__ void csr_from_sorted_kernel(const uint64_t* __restrict__ keys, int64_t nnz, int cbits,
+                                       int64_t* __restrict__ row_ptr, int32_t* __restrict__ col,
+                                       const uint32_t* __restrict__ eidx, const int32_t* __restrict__ w_in,
+                                       int32_t* __restrict__ w_out) {
+    const uint64_t cmask = (1ull << cbits) - 1ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const int64_t row = (int64_t)(k >> cbits);
+        const int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> cbits) : -1;
+        for (int64_t rr = prev + 1; rr <= row; ++rr) row_ptr[rr] = i;
+        col[i] = (int32_t)(k & cmask);
+        if (w_out) w_out[i] = w_in[eidx[i]];
+    }
+}
+
+// ---------------- pull plans ----------------
+__global__ void hub_flag_kernel(const int64_t* __restrict__ rp, int64_t rows, uint8_t* __restrict__ flag) {
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x)
+        flag[l] = (rp[l + 1] - rp[l]) >= kHubDegree;
+}
+
+__constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 0};
+
+__global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
+                                   unsigned long long* __restrict__ first_below /* [kNumClasses] */) {
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = rp[l + 1] - rp[l];
+#pragma unroll
+        for (int c = 1; c < kNumClasses - 1; ++c)
+            if (d < c_class_thr[c]) atomicMin(&first_below[c], (unsigned long long)l);
+    }
+}
+
+int64_t select_keys(const SelectArgs& a, DevBuf<uint64_t>& keys, DevBuf<uint32_t>& eidx, bool want_eidx,
+                    hipStream_t s) {
+    const int64_t nb = std::max<int64_t>(1, (a.m + kSelTile - 1) / kSelTile);
+    DevBuf<int64_t> counts(nb), off(nb + 1);
+    select_count_kernel<<<(unsigned)nb, kBlock, 0, s>>>(a, counts.get());
+    JG_LAUNCH_CHECK();
+    prim::exclusive_scan(counts.get(), off.get(), nb, s);
+    int64_t total = 0;
+    JG_HIP(hipMemcpyAsync(&total, off.get() + nb, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+    keys.alloc(std::max<int64_t>(total, 1));
+    if (want_eidx) eidx.alloc(std::max<int64_t>(total, 1));
+    select_write_kernel<<<(unsigned)nb, kBlock, 0, s>>>(a, off.get(), keys.get(), want_eidx ? eidx.get() : nullptr);
+    JG_LAUNCH_CHECK();
+    return total;
+}
+
+}  // namespace
+
+void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s) {
+    const RmatParams p = rmat_params(scale, seed);
+    rmat_kernel<<<grid_for(m, kBlock, 256 * 32), kBlock, 0, s>>>(p, m, src, dst);
+    JG_LAUNCH_CHECK();
+}
+
+void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
+                      int32_t* dsrc, int32_t* ddst, hipStream_t s) {
+    DevBuf<uint64_t> keys(std::max<int64_t>(n, 1));
+    DevBuf<uint32_t> vals(std::max<int64_t>(n, 1));
+    DevBuf<int32_t> dup(1);
+    JG_HIP(hipMemsetAsync(dup.get(), 0, sizeof(int32_t), s));
+    if (n > 0) {
+        vid_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(d_vid, n, keys.get(), vals.get());
+        JG_LAUNCH_CHECK();
+        prim::radix_sort(keys.get(), vals.get(), n, 64, s);
+        dup_check_kernel<<<grid_for(n), kBlock, 0, s>>>(keys.get(), n, dup.get());
+        JG_LAUNCH_CHECK();
+    }
+    int32_t has_dup = 0;
+    JG_HIP(hipMemcpyAsync(&has_dup, dup.get(), sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+    if (has_dup) fail(JG_ERR_ARG, "duplicate vertex id in vid[]");
+    if (m > 0) {
+        remap_kernel<<<grid_for(m), kBlock, 0, s>>>(keys.get(), vals.get(), n, d_src, d_dst, m, dsrc, ddst);
+        JG_LAUNCH_CHECK();
+    }
+    JG_HIP(hipStreamSynchronize(s));
+}
+
+static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr& csr, hipStream_t s) {
+    DevBuf<uint64_t> keys;
+    DevBuf<uint32_t> eidx;
+    const int64_t nnz = select_keys(a, keys, eidx, weight != nullptr, s);
+    const int rbits = bits_for((uint64_t)std::max<int64_t>(sh.rows - 1, 0));
+    prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits, s);
+    csr.rows = sh.rows;
+    csr.nnz = nnz;
+    csr.row_ptr.alloc(sh.rows + 1);
+    csr.col.alloc(std::max<int64_t>(nnz, 1));
+    if (weight) csr.weight.alloc(std::max<int64_t>(nnz, 1));
+    fill_i64_kernel<<<grid_for(sh.rows + 1), kBlock, 0, s>>>(csr.row_ptr.get(), sh.rows + 1, nnz);
+    JG_LAUNCH_CHECK();
+    if (nnz > 0) {
+        csr_from_sorted_kernel<<<grid_for(nnz), kBlock, 0, s>>>(keys.get(), nnz, a.cbits, csr.row_ptr.get(),
+                                                                csr.col.get(), weight ? eidx.get() : nullptr, weight,
+                                                                weight ? csr.weight.get() : nullptr);
+        JG_LAUNCH_CHECK();
+    }
+    JG_HIP(hipStreamSynchronize(s));
+}
+
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
+    hipStream_t s = sh.stream;
+    const int64_t rows = csr.rows;
+    // hub rows (any position) -> chunk table
+    std::vector<int64_t> hubs;
+    if (rows > 0) {
+        DevBuf<uint8_t> flag(rows);
+        DevBuf<int64_t> idx(rows);
+        hub_flag_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, flag.get());
+        JG_LAUNCH_CHECK();
+        const int64_t nh = prim::compact_indices(flag.get(), rows, idx.get(), s);
+        hubs.resize(nh);
+        if (nh) JG_HIP(hipMemcpy(hubs.data(), idx.get(), nh * sizeof(int64_t), hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> crow, cbeg, cend, hptr(1, 0);
+    for (int64_t r : hubs) {
+        int64_t b = 0, e = 0;
+        JG_HIP(hipMemcpy(&b, csr.row_ptr.get() + r, sizeof(int64_t), hipMemcpyDeviceToHost));
+        JG_HIP(hipMemcpy(&e, csr.row_ptr.get() + r + 1, sizeof(int64_t), hipMemcpyDeviceToHost));
+        for (int64_t p = b; p < e; p += kHubChunk) {
+            crow.push_back(r);
+            cbeg.push_back(p);
+            cend.push_back(std::min(e, p + kHubChunk));
+        }
+        hptr.push_back((int64_t)crow.size());
+    }
+    plan.num_hub_rows = (int64_t)hubs.size();
+    plan.num_chunks = (int64_t)crow.size();
+    auto upload = [&](DevBuf<int64_t>& d, const std::vector<int64_t>& h) {
+        d.alloc(std::max<size_t>(h.size(), 1));
+        if (!h.empty()) JG_HIP(hipMemcpy(d.get(), h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    };
+    upload(plan.chunk_row, crow);
+    upload(plan.chunk_begin, cbeg);
+    upload(plan.chunk_end, cend);
+    upload(plan.hub_chunk_ptr, hptr);
+    // class boundaries: first row whose degree falls below each class threshold
+    unsigned long long fb[kNumClasses];
+    for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
+    if (rows > 0) {
+        DevBuf<unsigned long long> d_fb(kNumClasses);
+        JG_HIP(hipMemcpy(d_fb.get(), fb, sizeof fb, hipMemcpyHostToDevice));
+        class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get());
+        JG_LAUNCH_CHECK();
+        JG_HIP(hipMemcpy(fb, d_fb.get(), sizeof fb, hipMemcpyDeviceToHost));
+    }
+    // class 1 (64 lanes) starts at row 0; class c ends where class c+1 begins
+    int64_t begin = 0;
+    plan.class_row_begin[0] = plan.class_row_end[0] = 0;  // hub class is the chunk table
+    plan.class_block_begin[0] = 0;
+    plan.class_block_begin[1] = plan.num_chunks;
+    for (int c = 1; c < kNumClasses; ++c) {
+        int64_t end = (c < kNumClasses - 1) ? (int64_t)fb[c] : rows;
+        end = std::max(end, begin);
+        plan.class_row_begin[c] = begin;
+        plan.class_row_end[c] = end;
+        const int lanes = 64 >> (c - 1);
+        const int64_t rows_per_block = kBlock / lanes;
+        plan.class_block_begin[c + 1] = plan.class_block_begin[c] + (end - begin + rows_per_block - 1) / rows_per_block;
+        begin = end;
+    }
+}
+
+void build_graph_from_dense(Graph& g, DenseEdges& e) {
+    const int64_t n = g.n, m = e.m;
+    const int P = g.P;
+    g.S = (n + P - 1) / P;
+    if (g.S < 1) g.S = 1;
+    if ((int64_t)P * g.S >= (int64_t)INT32_MAX) fail(JG_ERR_UNSUPPORTED, "graph too large for int32 vertex ids");
+    const int mode = (g.flags & JG_ADJ_IN) ? 0 : (g.flags & JG_ADJ_BOTH) ? 1 : 2;
+    const int vbits = bits_for((uint64_t)std::max<int64_t>(n - 1, 0));
+    const int cbits = std::max(1, bits_for((uint64_t)(g.padded_len() - 1)));
+    bool first = true;
+    for (size_t li = 0; li < g.shards.size(); ++li) {
+        Shard& sh = *g.shards[li];
+        DeviceGuard dg(sh.device);
+        hipStream_t s = sh.stream;
+        DevBuf<int32_t> indeg(std::max<int64_t>(n, 1)), outdeg(std::max<int64_t>(n, 1));
+        DevBuf<unsigned long long> cnt(5);
+        JG_HIP(hipMemsetAsync(indeg.get(), 0, indeg.bytes(), s));
+        JG_HIP(hipMemsetAsync(outdeg.get(), 0, outdeg.bytes(), s));
+        JG_HIP(hipMemsetAsync(cnt.get(), 0, cnt.bytes(), s));
+        if (m > 0) {
+            degree_kernel<<<grid_for(m, kBlock, 256 * 16), kBlock, 0, s>>>(e.src[li], e.dst[li], m, indeg.get(),
+                                                                           outdeg.get(), cnt.get());
+            JG_LAUNCH_CHECK();
+        }
+        if (n > 0) {
+            stats_kernel<<<grid_for(n, kBlock, 1024), kBlock, 0, s>>>(indeg.get(), outdeg.get(), n, cnt.get() + 2);
+            JG_LAUNCH_CHECK();
+        }
+        unsigned long long hc[5];
+        JG_HIP(hipMemcpyAsync(hc, cnt.get(), sizeof hc, hipMemcpyDeviceToHost, s));
+        JG_HIP(hipStreamSynchronize(s));
+        const int64_t maxdeg = mode == 0 ? (int64_t)hc[2] : mode == 1 ? (int64_t)(hc[2] + hc[3]) : (int64_t)hc[3];
+        if (first) {
+            g.info.num_vertices = n;
+            g.info.num_edges = (int64_t)hc[0];
+            g.info.ghost_edges = m - (int64_t)hc[0];
+            g.info.self_loops = (int64_t)hc[1];
+            g.info.max_in_degree = (int64_t)hc[2];
+            g.info.max_out_degree = (int64_t)hc[3];
+            g.info.truncated_vertices = (int64_t)hc[4];
+        }
+        // degree-sorted relabel
+        DevBuf<uint64_t> rkeys(std::max<int64_t>(n, 1));
+        DevBuf<int32_t> order(std::max<int64_t>(n, 1)), padded(std::max<int64_t>(n, 1));
+        if (n > 0) {
+            relabel_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(indeg.get(), outdeg.get(), n, mode, maxdeg, vbits,
+                                                               rkeys.get());
+            JG_LAUNCH_CHECK();
+            prim::radix_sort(rkeys.get(), nullptr, n, vbits + bits_for((uint64_t)maxdeg), s);
+            padded_ids_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, (1ull << vbits) - 1ull, P, g.S,
+                                                             order.get(), padded.get());
+            JG_LAUNCH_CHECK();
+        }
+        const int r = sh.index;
+        sh.rows = std::max<int64_t>(0, std::min<int64_t>(g.S, (n - r + P - 1) / P));
+        // host copies: dense index of each owned row, padded id of every vertex (once)
+        std::vector<int32_t> h_order(n);
+        if (n) JG_HIP(hipMemcpy(h_order.data(), order.get(), n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        sh.dense_of_local.resize(sh.rows);
+        for (int64_t l = 0; l < sh.rows; ++l) sh.dense_of_local[l] = h_order[(size_t)(r + l * P)];
+        if (first) {
+            g.padded_of_dense.resize(n);
+            for (int64_t k = 0; k < n; ++k) g.padded_of_dense[h_order[k]] = (k % P) * g.S + k / P;
+        }
+        sh.out_degree.alloc(std::max<int64_t>(sh.rows, 1));
+        if (sh.rows > 0) {
+            local_outdeg_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(order.get(), outdeg.get(), n, P, r, sh.rows,
+                                                                     sh.out_degree.get());
+            JG_LAUNCH_CHECK();
+        }
+        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits};
+        const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
+        if (g.flags & JG_ADJ_IN) {
+            a.which = 0;
+            build_csr(sh, a, w, sh.in, s);
+            build_pull_plan(sh, sh.in, sh.plan_in);
+        }
+        if (g.flags & JG_ADJ_OUT) {
+            a.which = 1;
+            build_csr(sh, a, w, sh.out, s);
+        }
+        if (g.flags & JG_ADJ_BOTH) {
+            a.which = 2;
+            build_csr(sh, a, nullptr, sh.both, s);
+            build_pull_plan(sh, sh.both, sh.plan_both);
+        }
+        JG_HIP(hipStreamSynchronize(s));
+        first = false;
+    }
+    int64_t bytes = 0;
+    for (auto& sp : g.shards) bytes += sp->in.bytes() + sp->out.bytes() + sp->both.bytes() + sp->out_degree.bytes();
+    g.info.device_bytes = bytes;
+    g.info.num_shards = P;
+    g.info.flags = g.flags;
+}
+
+}  // namespace jg

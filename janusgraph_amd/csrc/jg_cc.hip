@@ -1,0 +1,217 @@
+// jg_cc.hip — ConnectedComponentVertexProgram as synchronous min-label pull supersteps.
+//
+// Reference: TinkerPop 3.4.6 ConnectedComponentVertexProgram (not in the container; SURVEY.md A.3
+// [TP-recall]) run by Fulgora with BOTH edges loaded (janusgraph-core/.../olap/computer/
+// VertexProgramScanJob.java:113-135); label form pinned by janusgraph-backend-testutils/.../olap/
+// OLAPTest.java:736-762 (component == id().toString(), shared by a component).
+//   superstep 0: component = id().toString(); vertices with a BOTH edge send it
+//   superstep t: min by String.compareTo over messages pulled over BOTH edges from neighbours that
+//                sent in t-1; on improvement set + send; halt when nobody sent (or iteration >= 99)
+// Labels are carried as the rank of the id's decimal string in String order (bijective), so the
+// superstep is an int32 min-semiring pull: msg[g] = label if g sent in t-1, else INT32_MAX.
+// String order of non-negative ids: compare x*10^(19-digits(x)) (19-digit left-aligned decimal),
+// ties (a prefix such as "1" < "10") broken by fewer digits — computed with two stable radix sorts.
+#include <climits>
+
+#include "jg_pull.h"
+
+namespace jg {
+
+namespace {
+
+constexpr int kCcMaxIterations = 100;  // ConnectedComponentVertexProgram default maxIterations
+
+struct CcOp {
+    using T = int32_t;
+    const int32_t* __restrict__ msg;     // full length, previous superstep
+    int32_t* __restrict__ msg_out;       // full length (owned slice written)
+    int32_t* __restrict__ label;         // [rows]
+    int32_t* __restrict__ changed;
+    int64_t base;
+    __device__ __forceinline__ int32_t identity() const { return INT_MAX; }
+    __device__ __forceinline__ int32_t combine(int32_t a, int32_t b) const { return a < b ? a : b; }
+    __device__ __forceinline__ int32_t gather(int32_t c) const { return msg[c]; }
+    __device__ __forceinline__ int32_t shfl_xor(int32_t v, int o) const { return __shfl_xor(v, o, kWave); }
+    __device__ __forceinline__ bool active(int64_t) const { return true; }
+    __device__ __forceinline__ void finalize(int64_t row, int32_t m) const {
+        if (m < label[row]) {
+            label[row] = m;
+            msg_out[base + row] = m;
+            *changed = 1;
+        } else {
+            msg_out[base + row] = INT_MAX;
+        }
+    }
+};
+
+__device__ __forceinline__ int digits_of(uint64_t x) {
+    int d = 1;
+    while (d < 20 && x >= 10ull) { x /= 10ull; ++d; }
+    return d;
+}
+
+// pass 1 keys: digit count (tie-break, least significant)
+__global__ void lex_digits_kernel(const int64_t* __restrict__ vid, int64_t n, uint64_t* __restrict__ keys,
+                                  uint32_t* __restrict__ vals) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        keys[i] = (uint64_t)digits_of((uint64_t)vid[i]);
+        vals[i] = (uint32_t)i;
+    }
+}
+
+// pass 2 keys: left-aligned 19-digit decimal of the id (in pass-1 order)
+__global__ void lex_padded_kernel(const int64_t* __restrict__ vid, const uint32_t* __restrict__ vals, int64_t n,
+                                  uint64_t* __restrict__ keys) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t x = (uint64_t)vid[vals[i]];
+        for (int d = digits_of(x); d < 19; ++d) x *= 10ull;
+        keys[i] = x;
+    }
+}
+
+__global__ void lex_rank_scatter_kernel(const uint32_t* __restrict__ vals, int64_t n, int32_t* __restrict__ rank_of) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        rank_of[vals[r]] = (int32_t)r;
+}
+
+__global__ void cc_init_kernel(const int32_t* __restrict__ lab0, const int64_t* __restrict__ rp, int64_t rows,
+                               int64_t base, int32_t* __restrict__ label, int32_t* __restrict__ msg) {
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
+        label[l] = lab0[l];
+        msg[base + l] = (rp[l + 1] > rp[l]) ? lab0[l] : INT_MAX;  // only vertices with edges send
+    }
+}
+
+void exchange_msg(Graph& g, int which) {
+    std::vector<void*> bufs;
+    for (auto& sp : g.shards) bufs.push_back(sp->cc_msg[which].get());
+    exchange_allgather(g, bufs, sizeof(int32_t), ncclInt32);
+}
+
+}  // namespace
+
+void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
+    if (!(g.flags & JG_ADJ_BOTH)) fail(JG_ERR_UNSUPPORTED, "connected components need a graph built with JG_ADJ_BOTH");
+    Ctx& ctx = *g.ctx;
+    ctx.last = jg_stats{};
+    const int64_t n = g.n;
+    for (int64_t d = 0; d < n; ++d)
+        if (g.vid_of(d) < 0) fail(JG_ERR_UNSUPPORTED, "connected components need non-negative vertex ids");
+    // String-order rank of every vertex id (on the first shard's device)
+    std::vector<int32_t> rank_of(n);
+    std::vector<int64_t> vid_of_rank(n);
+    {
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh.device);
+        hipStream_t s = sh.stream;
+        std::vector<int64_t> hv(n);
+        for (int64_t d = 0; d < n; ++d) hv[d] = g.vid_of(d);
+        DevBuf<int64_t> vid(std::max<int64_t>(n, 1));
+        DevBuf<uint64_t> keys(std::max<int64_t>(n, 1));
+        DevBuf<uint32_t> vals(std::max<int64_t>(n, 1));
+        DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
+        if (n > 0) {
+            JG_HIP(hipMemcpy(vid.get(), hv.data(), n * sizeof(int64_t), hipMemcpyHostToDevice));
+            lex_digits_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n, keys.get(), vals.get());
+            JG_LAUNCH_CHECK();
+            prim::radix_sort(keys.get(), vals.get(), n, 5, s);
+            lex_padded_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), vals.get(), n, keys.get());
+            JG_LAUNCH_CHECK();
+            prim::radix_sort(keys.get(), vals.get(), n, 64, s);
+            lex_rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), n, rk.get());
+            JG_LAUNCH_CHECK();
+            JG_HIP(hipMemcpy(rank_of.data(), rk.get(), n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        }
+        for (int64_t d = 0; d < n; ++d) vid_of_rank[rank_of[d]] = hv[d];
+    }
+    const int64_t len = g.padded_len();
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        DeviceGuard dg(sh.device);
+        for (int k = 0; k < 2; ++k) {
+            if (sh.cc_msg[k].size() != (size_t)len) sh.cc_msg[k].alloc(len);
+            JG_HIP(hipMemsetAsync(sh.cc_msg[k].get(), 0x7F, sh.cc_msg[k].bytes(), sh.stream));  // ~INT_MAX
+        }
+        sh.cc_label.alloc(std::max<int64_t>(sh.rows, 1));
+        sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
+        sh.cc_changed.alloc(1);
+        std::vector<int32_t> lab0(sh.rows);
+        for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
+        DevBuf<int32_t> dlab0(std::max<int64_t>(sh.rows, 1));
+        if (sh.rows) {
+            JG_HIP(hipMemcpy(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), hipMemcpyHostToDevice));
+            cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
+                                                                        (int64_t)sh.index * g.S, sh.cc_label.get(),
+                                                                        sh.cc_msg[0].get());
+            JG_LAUNCH_CHECK();
+        }
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    exchange_msg(g, 0);
+    // superstep 0 votes: anyone with an edge sent
+    int any = 0;
+    for (auto& sp : g.shards) any |= sp->both.nnz > 0;
+    any = allreduce_or(g, any);
+
+    Shard& sh0 = *g.shards[0];
+    DeviceGuard dg0(sh0.device);
+    hipEvent_t t0, t1;
+    JG_HIP(hipEventCreate(&t0));
+    JG_HIP(hipEventCreate(&t1));
+    JG_HIP(hipEventRecord(t0, sh0.stream));
+    int iteration = 0, cur = 0;
+    while (any && iteration < kCcMaxIterations - 1) {
+        ++iteration;
+        for (auto& sp : g.shards) {
+            Shard& sh = *sp;
+            DeviceGuard dg(sh.device);
+            JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
+            CcOp op;
+            op.msg = sh.cc_msg[cur].get();
+            op.msg_out = sh.cc_msg[cur ^ 1].get();
+            op.label = sh.cc_label.get();
+            op.changed = sh.cc_changed.get();
+            op.base = (int64_t)sh.index * g.S;
+            launch_pull(sh.both, sh.plan_both, op, sh.cc_hub_partial.get(), sh.stream, ctx.profiling ? &ctx : nullptr,
+                        &sh);
+        }
+        exchange_msg(g, cur ^ 1);
+        any = 0;
+        for (auto& sp : g.shards) {
+            Shard& sh = *sp;
+            DeviceGuard dg(sh.device);
+            int32_t ch = 0;
+            JG_HIP(hipMemcpyAsync(&ch, sh.cc_changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
+            JG_HIP(hipStreamSynchronize(sh.stream));
+            any |= ch;
+        }
+        any = allreduce_or(g, any);
+        cur ^= 1;
+    }
+    JG_HIP(hipEventRecord(t1, sh0.stream));
+    JG_HIP(hipEventSynchronize(t1));
+    float ms = 0;
+    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+    JG_HIP(hipEventDestroy(t0));
+    JG_HIP(hipEventDestroy(t1));
+    ctx.last.compute_ms = ms;
+    ctx.last.supersteps = iteration;
+    ctx.last.levels = iteration;
+    double nnz = 0;
+    for (auto& sp : g.shards) nnz += (double)sp->both.nnz;
+    ctx.last.edges_traversed = nnz * iteration;
+    ctx.last.algorithmic_bytes = (8.0 * nnz + 16.0 * (double)n) * iteration;  // 16m + 16n per superstep
+    if (iterations_out) *iterations_out = iteration;
+    if (comp_out) {
+        for (auto& sp : g.shards) {
+            Shard& sh = *sp;
+            DeviceGuard dg(sh.device);
+            std::vector<int32_t> h(sh.rows);
+            if (sh.rows) JG_HIP(hipMemcpy(h.data(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+            for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local[l]] = vid_of_rank[h[l]];
+        }
+    }
+    prof_collect(ctx, g);
+}
+
+}  // namespace jg

@@ -1,0 +1,104 @@
+// jg_common.h — shared internals of libjanusgpu (gfx950 only; wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace jg {
+
+constexpr int kWave = 64;    // CDNA wavefront width
+constexpr int kBlock = 256;  // threads per workgroup for every kernel in the library
+
+// Internal failures travel as exceptions and are turned into status codes at the C-ABI
+// (jg_api.cpp); nothing crosses the ABI as an exception.
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void fail(int code, const std::string& msg);
+void hip_check(hipError_t e, const char* what, const char* file, int line);
+
+#define JG_HIP(call) ::jg::hip_check((call), #call, __FILE__, __LINE__)
+#define JG_LAUNCH_CHECK() ::jg::hip_check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)
+
+// Owning device allocation (hipMalloc on the current device).
+template <typename T>
+class DevBuf {
+   public:
+    DevBuf() = default;
+    explicit DevBuf(size_t n) { alloc(n); }
+    ~DevBuf() { reset(); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p_(o.p_), n_(o.n_), dev_(o.dev_) { o.p_ = nullptr; o.n_ = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; dev_ = o.dev_; o.p_ = nullptr; o.n_ = 0; }
+        return *this;
+    }
+    void alloc(size_t n) {
+        reset();
+        n_ = n;
+        JG_HIP(hipGetDevice(&dev_));
+        if (n) {
+            hipError_t e = hipMalloc(reinterpret_cast<void**>(&p_), n * sizeof(T));
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                p_ = nullptr;
+                n_ = 0;
+                fail(-2, "device allocation of " + std::to_string(n * sizeof(T)) + " bytes failed");
+            }
+        }
+    }
+    void reset() {
+        if (p_) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            if (cur != dev_) (void)hipSetDevice(dev_);
+            (void)hipFree(p_);
+            if (cur != dev_) (void)hipSetDevice(cur);
+        }
+        p_ = nullptr;
+        n_ = 0;
+    }
+    T* get() const { return p_; }
+    size_t size() const { return n_; }
+    size_t bytes() const { return n_ * sizeof(T); }
+    void swap(DevBuf& o) { std::swap(p_, o.p_); std::swap(n_, o.n_); std::swap(dev_, o.dev_); }
+
+   private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+    int dev_ = 0;
+};
+
+inline unsigned grid_for(int64_t work, int per_block = kBlock, int64_t cap = 256 * 16) {
+    int64_t b = (work + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (cap > 0 && b > cap) b = cap;
+    return static_cast<unsigned>(b);
+}
+
+inline int bits_for(uint64_t x) {  // number of bits to represent values in [0, x]
+    int b = 0;
+    while (b < 64 && (x >> b) != 0) ++b;
+    return b;
+}
+
+// RAII device switch.
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        JG_HIP(hipGetDevice(&prev));
+        if (prev != dev) JG_HIP(hipSetDevice(dev));
+    }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+}  // namespace jg

@@ -1,0 +1,155 @@
+// jg_internal.h — contexts, shards and graphs of libjanusgpu.
+//
+// HBM layout (per shard = per GPU or logical partition):
+//   vertices are relabelled once at build time: sorted by degree (descending; the degree of the
+//   adjacency the programs pull over) and dealt round-robin to the P shards, so every shard owns
+//   S = ceil(n/P) rows whose degrees are sorted inside the shard.  A vertex's global id is
+//   g = shard * S + local; every full-length vertex vector is P*S long, laid out shard-major, so an
+//   in-place allgather of the owned slices IS the exchange step (RCCL over xGMI).
+//   Csr: row_ptr int64 [rows+1], col int32 [nnz] (global ids), optional weight int32 [nnz].
+//   Pull programs stream col once per superstep and gather the source vector at col.
+#pragma once
+
+#include <memory>
+
+#include "jg_common.h"
+#include "janusgpu.h"
+
+#include <rccl/rccl.h>
+
+namespace jg {
+
+struct Csr {
+    int64_t rows = 0;
+    int64_t nnz = 0;
+    DevBuf<int64_t> row_ptr;
+    DevBuf<int32_t> col;
+    DevBuf<int32_t> weight;  // optional (SD weights)
+    bool present() const { return row_ptr.size() > 0; }
+    int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
+};
+
+// Degree-class plan for the pull kernels of one CSR on one shard.  Rows are sorted by degree
+// (descending), so each class is a contiguous row range.
+constexpr int kNumClasses = 8;  // 0: hub (chunked), 1..7: lanes per row 64,32,16,8,4,2,1
+constexpr int64_t kHubDegree = 8192;
+constexpr int64_t kHubChunk = 4096;
+
+struct PullPlan {
+    int64_t class_row_begin[kNumClasses];
+    int64_t class_row_end[kNumClasses];
+    int64_t class_block_begin[kNumClasses + 1];  // hub: one block per chunk
+    int64_t num_hub_rows = 0;
+    int64_t num_chunks = 0;
+    DevBuf<int64_t> chunk_row;    // [num_chunks] local row of each hub chunk
+    DevBuf<int64_t> chunk_begin;  // [num_chunks] first entry (CSR position)
+    DevBuf<int64_t> chunk_end;    // [num_chunks]
+    DevBuf<int64_t> hub_chunk_ptr;  // [num_hub_rows+1] chunks of hub row r: [ptr[r], ptr[r+1])
+    int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
+};
+
+struct Ctx;
+
+struct Shard {
+    int device = 0;
+    int index = 0;           // shard id r in [0, P)
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;  // borrowed from the context (may be null)
+    int64_t rows = 0;        // owned rows (<= S)
+    Csr in, out, both;
+    PullPlan plan_in, plan_both;
+    DevBuf<int32_t> out_degree;   // [rows] out-degree of owned vertices (PageRank edgeCount)
+    std::vector<int32_t> dense_of_local;  // host: caller's dense index of each owned row
+
+    // program state (allocated on demand)
+    DevBuf<double> pr_contrib[2];  // [P*S] full-length, ping-pong
+    DevBuf<double> pr_rank;        // [rows]
+    DevBuf<double> pr_hub_partial; // [num_chunks]
+    DevBuf<int32_t> cc_msg[2];     // [P*S] label if sent else INT32_MAX
+    DevBuf<int32_t> cc_label;      // [rows]
+    DevBuf<int32_t> cc_hub_partial;
+    DevBuf<int32_t> cc_changed;    // [1]
+
+    std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
+};
+
+struct Graph {
+    Ctx* ctx = nullptr;
+    int64_t n = 0;         // caller vertices
+    int P = 1;             // global shard count
+    int64_t S = 0;         // padded rows per shard
+    uint32_t flags = 0;
+    std::vector<std::unique_ptr<Shard>> shards;  // the shards this process drives
+    std::vector<int64_t> sorted_vid;    // host: caller vids sorted (for vid -> dense lookups)
+    std::vector<int64_t> sorted_dense;  // dense index of sorted_vid[i]
+    std::vector<int64_t> vid;           // host: vid[dense] (empty for RMAT graphs: vid == dense)
+    std::vector<int64_t> padded_of_dense;  // host: global padded id of each caller vertex
+    jg_graph_info info{};
+    bool has_weights = false;
+    // PageRank session
+    int pr_cur = 0;
+    bool pr_begun = false;
+    double pr_damping = 0.85;
+    int64_t pr_vertex_count = 1;
+    int pr_steps = 0;
+
+    int64_t vid_of(int64_t dense) const { return vid.empty() ? dense : vid[dense]; }
+    int64_t dense_of_vid(int64_t v) const;  // -1 if absent
+    int64_t padded_len() const { return (int64_t)P * S; }
+};
+
+struct Ctx {
+    std::vector<int> devices;   // devices this process drives (one shard each)
+    int nranks = 1;             // processes (rank mode) — total shards = nranks * devices.size()
+    int rank = 0;
+    bool logical = false;       // several shards on one device: exchange by device copies
+    std::vector<ncclComm_t> comms;
+    std::vector<hipStream_t> streams;
+    bool profiling = false;
+    jg_stats last{};
+    int total_shards() const { return nranks * (int)devices.size(); }
+};
+
+// ---- build (jg_build.hip) ----
+// Dense edge list already on every shard's device as int32 (src, dst) with ids in [0,n) — or -1
+// for a ghost endpoint; weights optional.  Builds relabelling, CSRs and pull plans.
+struct DenseEdges {
+    std::vector<int32_t*> src, dst;    // per local shard device pointers (size m)
+    std::vector<int32_t*> weight;      // may hold nullptr
+    int64_t m = 0;
+};
+void build_graph_from_dense(Graph& g, DenseEdges& e);
+void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s);
+void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
+                      int32_t* dsrc, int32_t* ddst, hipStream_t s);
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan);
+
+// ---- exchange (jg_api.cpp) ----
+// In-place allgather of every shard's owned slice [r*S, r*S+S) of a full-length vector.
+void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
+
+// ---- programs ----
+void pagerank_begin(Graph& g, double damping, int64_t vertex_count);
+void pagerank_steps(Graph& g, int nsteps);
+void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out);
+void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
+void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
+
+// Logical OR of a flag over all ranks (identity in single-process contexts).
+int allreduce_or(Graph& g, int flag);
+
+// Profiling of the dominant kernel (HIP events on the shard's stream).
+bool prof_enabled(const Ctx& c);
+void prof_record_start(Ctx& c, Shard& sh);
+void prof_record_stop(Ctx& c, Shard& sh);
+void prof_collect(Ctx& c, Graph& g);
+
+}  // namespace jg
+
+struct jg_ctx {
+    jg::Ctx impl;
+};
+struct jg_graph {
+    jg::Graph impl;
+};

@@ -1,0 +1,157 @@
+// jg_pull.h — the pull superstep engine: one launch streams a CSR's col[] once and folds the
+// gathered source values per row.  This is Fulgora's message gather
+// (graphdb/olap/computer/VertexMemoryHandler.java:121-151: for each reverse-incident edge, read the
+// neighbour's previous-superstep message) as a segmented reduction.
+//
+// Work decomposition (rows are degree-sorted, PullPlan classes are contiguous row ranges):
+//   class 0  hub rows (degree >= kHubDegree): one workgroup per kHubChunk entries, partial folds
+//            written to hub_partial[], combined in chunk order by pull_hub_finalize_kernel
+//   class c  (c = 1..7) L = 64 >> (c-1) lanes per row, 256/L rows per workgroup; lanes stride the
+//            row, fold, then a width-L xor-shuffle tree; lane 0 finalises the row
+// Every row is folded in a fixed order that does not depend on timing (bit-reproducible runs).
+// An Op supplies: T, identity(), combine(a,b), gather(col), shfl_xor(v,o), active(row) (false: the
+// row is not folded but still finalised with identity()), finalize(row, acc).
+#pragma once
+
+#include "jg_internal.h"
+#include "jg_prim.h"
+
+namespace jg {
+
+struct PullArgs {
+    const int64_t* __restrict__ row_ptr;
+    const int32_t* __restrict__ col;
+    const int64_t* __restrict__ chunk_row;
+    const int64_t* __restrict__ chunk_begin;
+    const int64_t* __restrict__ chunk_end;
+    const int64_t* __restrict__ hub_chunk_ptr;
+    int64_t num_chunks;
+    int64_t num_hub_rows;
+    int64_t class_row_begin[kNumClasses];
+    int64_t class_row_end[kNumClasses];
+    int64_t class_block_begin[kNumClasses + 1];
+};
+
+inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
+    PullArgs a;
+    a.row_ptr = csr.row_ptr.get();
+    a.col = csr.col.get();
+    a.chunk_row = p.chunk_row.get();
+    a.chunk_begin = p.chunk_begin.get();
+    a.chunk_end = p.chunk_end.get();
+    a.hub_chunk_ptr = p.hub_chunk_ptr.get();
+    a.num_chunks = p.num_chunks;
+    a.num_hub_rows = p.num_hub_rows;
+    for (int c = 0; c < kNumClasses; ++c) {
+        a.class_row_begin[c] = p.class_row_begin[c];
+        a.class_row_end[c] = p.class_row_end[c];
+    }
+    for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = p.class_block_begin[c];
+    return a;
+}
+
+// Fold col[j0..j1) with stride `stride` starting at j0 + first; 4 gathers in flight per lane,
+// folded in index order.
+template <class Op>
+__device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
+                                                       int64_t j1, int stride) {
+    using T = typename Op::T;
+    T acc = op.identity();
+    for (; j + 3 * (int64_t)stride < j1; j += 4 * (int64_t)stride) {
+        const int32_t c0 = col[j], c1 = col[j + stride], c2 = col[j + 2 * stride], c3 = col[j + 3 * stride];
+        const T v0 = op.gather(c0), v1 = op.gather(c1), v2 = op.gather(c2), v3 = op.gather(c3);
+        acc = op.combine(acc, v0);
+        acc = op.combine(acc, v1);
+        acc = op.combine(acc, v2);
+        acc = op.combine(acc, v3);
+    }
+    for (; j < j1; j += stride) acc = op.combine(acc, op.gather(col[j]));
+    return acc;
+}
+
+template <class Op, int L>
+__device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op, int c, int64_t local_block) {
+    using T = typename Op::T;
+    constexpr int kRowsPerBlock = kBlock / L;
+    const int sub = threadIdx.x % L;
+    const int64_t row = a.class_row_begin[c] + local_block * kRowsPerBlock + threadIdx.x / L;
+    const bool valid = row < a.class_row_end[c];
+    T acc = op.identity();
+    bool hub = false;
+    if (valid) {
+        const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
+        hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
+        if (!hub && op.active(row)) acc = fold_strided(op, a.col, j0 + sub, j1, L);
+    }
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
+    if (valid && !hub && sub == 0) op.finalize(row, acc);
+}
+
+template <class Op>
+__global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
+    using T = typename Op::T;
+    const int64_t b = blockIdx.x;
+    if (b < a.num_chunks) {
+        __shared__ T red[kBlock / kWave];
+        const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
+        T acc = op.active(a.chunk_row[b]) ? fold_strided(op, a.col, j0 + threadIdx.x, j1, kBlock) : op.identity();
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
+        if (lane_id() == 0) red[wave_id()] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            T t = red[0];
+#pragma unroll
+            for (int w = 1; w < kBlock / kWave; ++w) t = op.combine(t, red[w]);
+            hub_partial[b] = t;
+        }
+        return;
+    }
+    int c = 1;
+#pragma unroll
+    for (int k = 1; k < kNumClasses; ++k)
+        if (b >= a.class_block_begin[k + 1]) c = k + 1;
+    const int64_t lb = b - a.class_block_begin[c];
+    switch (c) {
+        case 1: pull_rows_class<Op, 64>(a, op, c, lb); break;
+        case 2: pull_rows_class<Op, 32>(a, op, c, lb); break;
+        case 3: pull_rows_class<Op, 16>(a, op, c, lb); break;
+        case 4: pull_rows_class<Op, 8>(a, op, c, lb); break;
+        case 5: pull_rows_class<Op, 4>(a, op, c, lb); break;
+        case 6: pull_rows_class<Op, 2>(a, op, c, lb); break;
+        default: pull_rows_class<Op, 1>(a, op, c, lb); break;
+    }
+}
+
+template <class Op>
+__global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T* __restrict__ hub_partial) {
+    using T = typename Op::T;
+    for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < a.num_hub_rows;
+         h += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c0 = a.hub_chunk_ptr[h], c1 = a.hub_chunk_ptr[h + 1];
+        T acc = op.identity();
+        for (int64_t k = c0; k < c1; ++k) acc = op.combine(acc, hub_partial[k]);
+        op.finalize(a.chunk_row[c0], acc);
+    }
+}
+
+// Enqueue one pull superstep on `s`.
+template <class Op>
+void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
+                 Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr) {
+    const PullArgs a = make_pull_args(csr, plan);
+    const int64_t blocks = plan.total_blocks();
+    if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
+    if (blocks > 0) {
+        pull_kernel<Op><<<(unsigned)blocks, kBlock, 0, s>>>(a, op, hub_partial);
+        JG_LAUNCH_CHECK();
+    }
+    if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
+    if (plan.num_hub_rows > 0) {
+        pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
+        JG_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace jg

@@ -1,0 +1,605 @@
+// jg_traverse.hip — hop-depth traversals and hop-bounded shortest distance.
+//
+// Reference semantics:
+//   SPVP depth (TinkerPop ShortestPathVertexProgram under Fulgora's forced {Local(bothE), Global}
+//   scopes, janusgraph-core/.../olap/computer/FulgoraGraphComputer.java:249-253): undirected hops.
+//   ShortestDistanceVertexProgram (janusgraph-backend-testutils/.../olap/
+//   ShortestDistanceVertexProgram.java:112-146, combiner ShortestDistanceMessageCombiner.java:29-31):
+//   v pulls over its OUT edges the targets' previous-superstep messages + edge weight, keeps the
+//   minimum, forwards on improvement; supersteps 0..maxDepth => min over paths of <= maxDepth hops.
+//
+// Kernels:
+//   single source, 1 shard: direction-optimising BFS (Beamer).  Top-down expands a queue with
+//     16 lanes per frontier vertex, claims targets with atomicCAS and appends them through one
+//     wave-ballot + one atomicAdd per wave; bottom-up gives each unvisited vertex one lane that
+//     scans its pull adjacency against a 64-bit-word frontier bitmap and stops at the first hit;
+//     the next bitmap word is the wave's ballot (no atomics).
+//   multi-source (<= 64) or sharded: bit-parallel BFS, one uint64 frontier word per vertex, as an
+//     OR-semiring pull superstep on the jg_pull.h engine, exchanged by allgather.
+//   weighted SD: frontier Bellman-Ford with exact snapshot semantics (messages of superstep t-1
+//     only): push over the in-CSR with 64-bit atomicMin into a scratch array, then apply.
+#include <climits>
+
+#include "jg_pull.h"
+
+namespace jg {
+
+namespace {
+
+constexpr int kTdLanes = 16;
+
+struct Counters {  // device-side level counters
+    unsigned long long next_size;  // vertices discovered this level
+    unsigned long long next_edges; // their push degrees (m_f of the next level)
+};
+
+__device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t* __restrict__ queue,
+                                            unsigned long long* __restrict__ size) {
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    unsigned long long base = 0;
+    if (lane_id() == leader) base = atomicAdd(size, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader, kWave);
+    if (take) queue[base + __popcll(mask & lanemask_lt())] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void td_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                    const int32_t* __restrict__ queue, int64_t qsize,
+                                                    int32_t* __restrict__ depth, int32_t next_depth,
+                                                    int32_t* __restrict__ next_queue, Counters* __restrict__ cnt) {
+    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
+    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
+    const int sub = threadIdx.x % kTdLanes;
+    unsigned long long edges = 0;
+    // all lanes of a wave iterate the same number of times (wave-uniform trip count for ballots)
+    const int64_t iters = (qsize + ngroups - 1) / ngroups;
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t qi = group + it * ngroups;
+        const bool have = qi < qsize;
+        const int32_t u = have ? queue[qi] : 0;
+        const int64_t j0 = have ? rp[u] : 0, j1 = have ? rp[u + 1] : 0;
+        int64_t len = j1 - j0;
+        // wave-uniform loop bound: max row length among the wave's groups
+        int64_t maxlen = len;
+#pragma unroll
+        for (int o = kTdLanes; o < kWave; o <<= 1) {
+            const int64_t t = __shfl_xor(maxlen, o, kWave);
+            maxlen = t > maxlen ? t : maxlen;
+        }
+        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
+            const int64_t k = k0 + sub;
+            bool won = false;
+            int32_t v = 0;
+            if (k < len) {
+                v = col[j0 + k];
+                if (depth[v] < 0) won = atomicCAS(&depth[v], -1, next_depth) == -1;
+            }
+            if (won) edges += (unsigned long long)(rp[v + 1] - rp[v]);
+            wave_append(won, v, next_queue, &cnt->next_size);
+        }
+    }
+    edges = wave_reduce_add(edges);
+    if (lane_id() == 0 && edges) atomicAdd(&cnt->next_edges, edges);
+}
+
+__global__ void queue_to_bitmap_kernel(const int32_t* __restrict__ queue, int64_t qsize,
+                                       unsigned long long* __restrict__ bm) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < qsize; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = queue[i];
+        atomicOr(&bm[u >> 6], 1ull << (u & 63));
+    }
+}
+
+// One lane per vertex; 64 consecutive vertices per wave so that the next frontier word is a ballot.
+__global__ __launch_bounds__(kBlock) void bu_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                    const int64_t* __restrict__ push_rp,
+                                                    const unsigned long long* __restrict__ frontier,
+                                                    int32_t* __restrict__ depth, int64_t rows, int32_t next_depth,
+                                                    unsigned long long* __restrict__ next_bm,
+                                                    int32_t* __restrict__ next_queue, Counters* __restrict__ cnt) {
+    const int64_t words = (rows + 63) / 64;
+    unsigned long long edges = 0;
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words;
+         w += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+        const int64_t v = w * 64 + lane_id();
+        bool found = false;
+        if (v < rows && depth[v] < 0) {
+            const int64_t j1 = rp[v + 1];
+            for (int64_t j = rp[v]; j < j1; ++j) {
+                const int32_t u = col[j];
+                if ((frontier[u >> 6] >> (u & 63)) & 1ull) { found = true; break; }
+            }
+            if (found) {
+                depth[v] = next_depth;
+                edges += (unsigned long long)(push_rp[v + 1] - push_rp[v]);
+            }
+        }
+        const uint64_t word = __ballot(found);
+        if (lane_id() == 0) next_bm[w] = word;
+        wave_append(found, (int32_t)v, next_queue, &cnt->next_size);
+    }
+    edges = wave_reduce_add(edges);
+    if (lane_id() == 0 && edges) atomicAdd(&cnt->next_edges, edges);
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+__global__ void set_source_kernel(int32_t* depth, int32_t* queue, int64_t v, const int64_t* rp, Counters* cnt) {
+    depth[v] = 0;
+    queue[0] = (int32_t)v;
+    cnt->next_size = 1;
+    cnt->next_edges = (unsigned long long)(rp[v + 1] - rp[v]);
+}
+
+// input edges inside the reached set: sum of row lengths of reached vertices (symmetric: / 2 later)
+__global__ void reached_edges_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ depth, int64_t rows,
+                                     unsigned long long* __restrict__ out) {
+    unsigned long long s = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        if (depth[v] >= 0) s += (unsigned long long)(rp[v + 1] - rp[v]);
+    s = wave_reduce_add(s);
+    if (lane_id() == 0 && s) atomicAdd(out, s);
+}
+
+// ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
+struct MsBfsOp {
+    using T = unsigned long long;
+    const T* __restrict__ F;    // frontier words of the previous level, full length
+    T* __restrict__ Fout;       // full length, owned slice written
+    T* __restrict__ visited;    // [rows]
+    int32_t* __restrict__ depth;  // [nsrc * rows]
+    int32_t* __restrict__ changed;
+    int64_t rows, base;
+    int32_t lvl;
+    T full;
+    __device__ __forceinline__ T identity() const { return 0ull; }
+    __device__ __forceinline__ T combine(T a, T b) const { return a | b; }
+    __device__ __forceinline__ T gather(int32_t c) const { return F[c]; }
+    __device__ __forceinline__ T shfl_xor(T v, int o) const { return __shfl_xor(v, o, kWave); }
+    __device__ __forceinline__ bool active(int64_t row) const { return visited[row] != full; }
+    __device__ __forceinline__ void finalize(int64_t row, T acc) const {
+        T nw = acc & ~visited[row] & full;
+        Fout[base + row] = nw;
+        if (nw) {
+            visited[row] |= nw;
+            *changed = 1;
+            while (nw) {
+                const int s = __ffsll(nw) - 1;
+                depth[(int64_t)s * rows + row] = lvl;
+                nw &= nw - 1;
+            }
+        }
+    }
+};
+
+__global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
+                                  unsigned long long* __restrict__ visited, int32_t* __restrict__ depth, int64_t rows,
+                                  int64_t base) {
+    // sequential over the (<= 64) sources: several sources may share a vertex
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int s = 0; s < nsrc; ++s) {
+        const int64_t l = local_src[s];
+        if (l < 0) continue;
+        F[base + l] |= 1ull << s;
+        visited[l] |= 1ull << s;
+        depth[(int64_t)s * rows + l] = 0;
+    }
+}
+
+// ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
+__global__ __launch_bounds__(kBlock) void sd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                         const int32_t* __restrict__ wt,
+                                                         const int32_t* __restrict__ frontier, int64_t fsize,
+                                                         const long long* __restrict__ msg, long long* __restrict__ best,
+                                                         int32_t* __restrict__ touched,
+                                                         unsigned long long* __restrict__ tsize) {
+    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
+    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
+    const int sub = threadIdx.x % kTdLanes;
+    const int64_t iters = (fsize + ngroups - 1) / ngroups;
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t qi = group + it * ngroups;
+        const bool have = qi < fsize;
+        const int32_t w = have ? frontier[qi] : 0;
+        const int64_t j0 = have ? rp[w] : 0, j1 = have ? rp[w + 1] : 0;
+        const long long mw = have ? msg[w] : 0;
+        const int64_t len = j1 - j0;
+        int64_t maxlen = len;
+#pragma unroll
+        for (int o = kTdLanes; o < kWave; o <<= 1) {
+            const int64_t t = __shfl_xor(maxlen, o, kWave);
+            maxlen = t > maxlen ? t : maxlen;
+        }
+        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
+            const int64_t k = k0 + sub;
+            bool first = false;
+            int32_t u = 0;
+            if (k < len) {
+                u = col[j0 + k];
+                const long long cand = mw + (long long)(wt ? wt[j0 + k] : 1);
+                const long long old = atomicMin(&best[u], cand);
+                first = old == LLONG_MAX;
+            }
+            wave_append(first, u, touched, tsize);
+        }
+    }
+}
+
+__global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsize, long long* __restrict__ best,
+                                long long* __restrict__ dist, long long* __restrict__ msg,
+                                int32_t* __restrict__ next_frontier, unsigned long long* __restrict__ nsize) {
+    const int64_t iters = (tsize + (int64_t)gridDim.x * blockDim.x - 1) / ((int64_t)gridDim.x * blockDim.x);
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + it * (int64_t)gridDim.x * blockDim.x;
+        bool improved = false;
+        int32_t u = 0;
+        if (i < tsize) {
+            u = touched[i];
+            const long long b = best[u];
+            best[u] = LLONG_MAX;
+            if (dist[u] == LLONG_MIN || dist[u] > b) {
+                dist[u] = b;
+                msg[u] = b;
+                improved = true;
+            }
+        }
+        wave_append(improved, u, next_frontier, nsize);
+    }
+}
+
+__global__ void fill_ll_kernel(long long* p, int64_t n, long long v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+struct BfsCsrs {
+    const Csr* push;
+    const Csr* pull;
+};
+
+BfsCsrs pick_csrs(const Shard& sh, int direction) {
+    if (direction == JG_DIR_BOTH) {
+        if (!sh.both.present()) fail(JG_ERR_UNSUPPORTED, "BOTH traversal needs a graph built with JG_ADJ_BOTH");
+        return {&sh.both, &sh.both};
+    }
+    // OUT traversal: push from u over out-rows; pull for v over in-rows (u -> v).  IN is the mirror.
+    const Csr* push = direction == JG_DIR_OUT ? &sh.out : &sh.in;
+    const Csr* pull = direction == JG_DIR_OUT ? &sh.in : &sh.out;
+    if (!push->present() && !pull->present())
+        fail(JG_ERR_UNSUPPORTED, "directed traversal needs JG_ADJ_OUT and/or JG_ADJ_IN");
+    return {push->present() ? push : nullptr, pull->present() ? pull : nullptr};
+}
+
+// Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
+// Returns levels run; *edges_out = adjacency entries of reached vertices (push CSR).
+int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
+                 double* edges_out) {
+    hipStream_t s = sh.stream;
+    const int64_t rows = sh.rows;
+    const Csr* push = c.push;
+    const Csr* pull = c.pull;
+    const Csr* degcsr = push ? push : pull;
+    const int64_t words = (rows + 63) / 64;
+    DevBuf<int32_t> qa(std::max<int64_t>(rows, 1)), qb(std::max<int64_t>(rows, 1));
+    DevBuf<unsigned long long> bma(std::max<int64_t>(words, 1)), bmb(std::max<int64_t>(words, 1));
+    DevBuf<Counters> cnt(1);
+    fill_i32_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, -1);
+    JG_LAUNCH_CHECK();
+    JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(Counters), s));
+    set_source_kernel<<<1, 1, 0, s>>>(depth, qa.get(), source, degcsr->row_ptr.get(), cnt.get());
+    JG_LAUNCH_CHECK();
+    Counters h{1, 0};
+    JG_HIP(hipMemcpyAsync(&h, cnt.get(), sizeof h, hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+    int64_t nf = 1, mf = (int64_t)h.next_edges;
+    int64_t mu = degcsr->nnz - mf;
+    bool bottom_up = false;
+    bool queue_valid = true;  // qa holds the frontier as a queue
+    const double alpha = 14.0, beta = 24.0;
+    int level = 0;
+    while (nf > 0 && (max_depth < 0 || level < max_depth)) {
+        // direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the
+        // unexplored edges / alpha, back top-down when the frontier shrinks below n / beta
+        if (!bottom_up && pull && (!push || (double)mf > (double)mu / alpha)) bottom_up = true;
+        else if (bottom_up && push && (double)nf < (double)rows / beta) bottom_up = false;
+        JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(Counters), s));
+        const int next_depth = level + 1;
+        if (bottom_up) {
+            if (queue_valid) {  // frontier queue -> bitmap
+                JG_HIP(hipMemsetAsync(bma.get(), 0, words * sizeof(unsigned long long), s));
+                queue_to_bitmap_kernel<<<grid_for(nf), kBlock, 0, s>>>(qa.get(), nf, bma.get());
+                JG_LAUNCH_CHECK();
+            }
+            if (prof_enabled(ctx)) prof_record_start(ctx, sh);
+            bu_kernel<<<grid_for(words * kWave, kBlock, 256 * 8), kBlock, 0, s>>>(
+                pull->row_ptr.get(), pull->col.get(), degcsr->row_ptr.get(), bma.get(), depth, rows, next_depth,
+                bmb.get(), qb.get(), cnt.get());
+            JG_LAUNCH_CHECK();
+            if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
+            bma.swap(bmb);
+            queue_valid = true;  // bu also appended the new frontier to qb
+        } else {
+            if (prof_enabled(ctx)) prof_record_start(ctx, sh);
+            td_kernel<<<grid_for(nf * kTdLanes, kBlock, 256 * 8), kBlock, 0, s>>>(
+                push->row_ptr.get(), push->col.get(), qa.get(), nf, depth, next_depth, qb.get(), cnt.get());
+            JG_LAUNCH_CHECK();
+            if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
+            queue_valid = true;
+        }
+        qa.swap(qb);
+        JG_HIP(hipMemcpyAsync(&h, cnt.get(), sizeof h, hipMemcpyDeviceToHost, s));
+        JG_HIP(hipStreamSynchronize(s));
+        nf = (int64_t)h.next_size;
+        mf = (int64_t)h.next_edges;
+        mu -= mf;
+        ++level;
+    }
+    if (edges_out) {
+        DevBuf<unsigned long long> e(1);
+        JG_HIP(hipMemsetAsync(e.get(), 0, sizeof(unsigned long long), s));
+        reached_edges_kernel<<<grid_for(rows, kBlock, 1024), kBlock, 0, s>>>(degcsr->row_ptr.get(), depth, rows,
+                                                                             e.get());
+        JG_LAUNCH_CHECK();
+        unsigned long long he = 0;
+        JG_HIP(hipMemcpyAsync(&he, e.get(), sizeof he, hipMemcpyDeviceToHost, s));
+        JG_HIP(hipStreamSynchronize(s));
+        *edges_out = (double)he;
+    }
+    return level;
+}
+
+int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
+    const int64_t d = g.dense_of_vid(vid);
+    if (d < 0) return -1;
+    const int64_t pg = g.padded_of_dense[d];
+    *shard_out = (int)(pg / g.S);
+    return pg % g.S;
+}
+
+}  // namespace
+
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out) {
+    if (nsrc <= 0) fail(JG_ERR_ARG, "nsrc must be positive");
+    if (direction < JG_DIR_OUT || direction > JG_DIR_BOTH) fail(JG_ERR_ARG, "bad direction");
+    Ctx& ctx = *g.ctx;
+    ctx.last = jg_stats{};
+    const bool single = nsrc == 1 && g.P == 1;
+    hipEvent_t t0, t1;
+    Shard& sh0 = *g.shards[0];
+    DeviceGuard dg0(sh0.device);
+    JG_HIP(hipEventCreate(&t0));
+    JG_HIP(hipEventCreate(&t1));
+    if (single) {
+        Shard& sh = sh0;
+        const BfsCsrs c = pick_csrs(sh, direction);
+        int shard = 0;
+        const int64_t l = local_of_vid(g, source_vids[0], &shard);
+        DevBuf<int32_t> depth(std::max<int64_t>(sh.rows, 1));
+        int levels = 0;
+        double edges = 0;
+        if (l < 0) {
+            fill_i32_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(depth.get(), sh.rows, -1);
+            JG_LAUNCH_CHECK();
+            JG_HIP(hipEventRecord(t0, sh.stream));
+            JG_HIP(hipEventRecord(t1, sh.stream));
+        } else {
+            JG_HIP(hipEventRecord(t0, sh.stream));
+            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges);
+            JG_HIP(hipEventRecord(t1, sh.stream));
+        }
+        JG_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        ctx.last.compute_ms = ms;
+        ctx.last.levels = levels;
+        ctx.last.supersteps = levels;
+        ctx.last.edges_traversed = direction == JG_DIR_BOTH ? edges / 2 : edges;
+        const Csr* degcsr = c.push ? c.push : c.pull;
+        ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
+        if (depth_out) {
+            std::vector<int32_t> h(sh.rows);
+            if (sh.rows) JG_HIP(hipMemcpy(h.data(), depth.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+            for (int64_t v = 0; v < sh.rows; ++v) depth_out[sh.dense_of_local[v]] = h[v];
+        }
+        prof_collect(ctx, g);
+    } else {
+        // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
+        const int64_t len = g.padded_len();
+        float total_ms = 0;
+        int max_levels = 0;
+        for (int b0 = 0; b0 < nsrc; b0 += 64) {
+            const int ns = std::min(64, nsrc - b0);
+            const unsigned long long full = ns == 64 ? ~0ull : ((1ull << ns) - 1ull);
+            struct St {
+                DevBuf<unsigned long long> F[2], vis;
+                DevBuf<int32_t> depth, changed;
+                DevBuf<unsigned long long> hub;
+            };
+            std::vector<St> st(g.shards.size());
+            for (size_t i = 0; i < g.shards.size(); ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh.device);
+                const BfsCsrs c = pick_csrs(sh, direction);
+                if (!c.pull) fail(JG_ERR_UNSUPPORTED, "multi-source BFS needs the pull adjacency");
+                const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
+                if (c.pull == &sh.out) fail(JG_ERR_UNSUPPORTED, "multi-source IN traversal is not supported");
+                (void)plan;
+                St& t = st[i];
+                t.F[0].alloc(len);
+                t.F[1].alloc(len);
+                t.vis.alloc(std::max<int64_t>(sh.rows, 1));
+                t.depth.alloc(std::max<int64_t>(sh.rows * ns, 1));
+                t.changed.alloc(1);
+                t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
+                JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.depth.get(), 0xFF, t.depth.bytes(), sh.stream));
+                std::vector<int64_t> loc(ns, -1);
+                for (int s = 0; s < ns; ++s) {
+                    int shard = -1;
+                    const int64_t l = local_of_vid(g, source_vids[b0 + s], &shard);
+                    if (l >= 0 && shard == sh.index) loc[s] = l;
+                }
+                DevBuf<int64_t> dloc(ns);
+                JG_HIP(hipMemcpy(dloc.get(), loc.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice));
+                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth.get(),
+                                                          sh.rows, (int64_t)sh.index * g.S);
+                JG_LAUNCH_CHECK();
+                JG_HIP(hipStreamSynchronize(sh.stream));
+            }
+            {
+                std::vector<void*> bufs;
+                for (auto& t : st) bufs.push_back(t.F[0].get());
+                exchange_allgather(g, bufs, sizeof(unsigned long long), ncclUint64);
+            }
+            JG_HIP(hipEventRecord(t0, sh0.stream));
+            int cur = 0, level = 0;
+            while (max_depth < 0 || level < max_depth) {
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    const BfsCsrs c = pick_csrs(sh, direction);
+                    const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
+                    St& t = st[i];
+                    JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
+                    MsBfsOp op;
+                    op.F = t.F[cur].get();
+                    op.Fout = t.F[cur ^ 1].get();
+                    op.visited = t.vis.get();
+                    op.depth = t.depth.get();
+                    op.changed = t.changed.get();
+                    op.rows = sh.rows;
+                    op.base = (int64_t)sh.index * g.S;
+                    op.lvl = level + 1;
+                    op.full = full;
+                    launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh);
+                }
+                {
+                    std::vector<void*> bufs;
+                    for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
+                    exchange_allgather(g, bufs, sizeof(unsigned long long), ncclUint64);
+                }
+                int32_t any = 0;
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    int32_t ch = 0;
+                    JG_HIP(hipMemcpyAsync(&ch, st[i].changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
+                    JG_HIP(hipStreamSynchronize(sh.stream));
+                    any |= ch;
+                }
+                any = allreduce_or(g, any);
+                cur ^= 1;
+                ++level;
+                if (!any) break;
+            }
+            JG_HIP(hipEventRecord(t1, sh0.stream));
+            JG_HIP(hipEventSynchronize(t1));
+            float ms = 0;
+            JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+            total_ms += ms;
+            max_levels = std::max(max_levels, level);
+            if (depth_out) {
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    std::vector<int32_t> h(sh.rows * ns);
+                    if (!h.empty())
+                        JG_HIP(hipMemcpy(h.data(), st[i].depth.get(), h.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+                    for (int s = 0; s < ns; ++s)
+                        for (int64_t l = 0; l < sh.rows; ++l)
+                            depth_out[(int64_t)(b0 + s) * g.n + sh.dense_of_local[l]] = h[(size_t)(s * sh.rows + l)];
+                }
+            }
+        }
+        ctx.last.compute_ms = total_ms;
+        ctx.last.levels = max_levels;
+        ctx.last.supersteps = max_levels;
+        prof_collect(ctx, g);
+    }
+    JG_HIP(hipEventDestroy(t0));
+    JG_HIP(hipEventDestroy(t1));
+}
+
+void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
+    Ctx& ctx = *g.ctx;
+    ctx.last = jg_stats{};
+    if (g.P != 1) fail(JG_ERR_UNSUPPORTED, "shortest distance runs on a single shard in this version");
+    if (!(g.flags & JG_ADJ_IN)) fail(JG_ERR_UNSUPPORTED, "shortest distance needs a graph built with JG_ADJ_IN");
+    Shard& sh = *g.shards[0];
+    DeviceGuard dg(sh.device);
+    hipStream_t s = sh.stream;
+    const int64_t rows = sh.rows;
+    int shard = 0;
+    const int64_t seed = local_of_vid(g, seed_vid, &shard);
+    std::vector<int64_t> host(rows, -1);
+    hipEvent_t t0, t1;
+    JG_HIP(hipEventCreate(&t0));
+    JG_HIP(hipEventCreate(&t1));
+    JG_HIP(hipEventRecord(t0, s));
+    int levels = 0;
+    if (seed >= 0 && !g.has_weights) {
+        // unit weights: min over <= maxDepth-hop paths == BFS depth along IN edges, capped
+        DevBuf<int32_t> depth(std::max<int64_t>(rows, 1));
+        BfsCsrs c{&sh.in, sh.out.present() ? &sh.out : nullptr};
+        levels = dobfs_single(ctx, sh, c, seed, max_depth, depth.get(), nullptr);
+        std::vector<int32_t> h(rows);
+        if (rows) JG_HIP(hipMemcpy(h.data(), depth.get(), rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int64_t l = 0; l < rows; ++l) host[l] = h[l];
+    } else if (seed >= 0) {
+        DevBuf<long long> dist(std::max<int64_t>(rows, 1)), msg(std::max<int64_t>(rows, 1)),
+            best(std::max<int64_t>(rows, 1));
+        DevBuf<int32_t> fa(std::max<int64_t>(rows, 1)), fb(std::max<int64_t>(rows, 1)),
+            touched(std::max<int64_t>(rows, 1));
+        DevBuf<unsigned long long> sizes(2);
+        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MIN);  // absent
+        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(best.get(), rows, LLONG_MAX);
+        JG_LAUNCH_CHECK();
+        const long long zero = 0;
+        const int32_t seed32 = (int32_t)seed;
+        JG_HIP(hipMemcpyAsync(dist.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+        JG_HIP(hipMemcpyAsync(msg.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+        JG_HIP(hipMemcpyAsync(fa.get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
+        int64_t fsize = 1;
+        for (int t = 1; t <= max_depth && fsize > 0; ++t) {
+            JG_HIP(hipMemsetAsync(sizes.get(), 0, 2 * sizeof(unsigned long long), s));
+            sd_push_kernel<<<grid_for(fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, s>>>(
+                sh.in.row_ptr.get(), sh.in.col.get(), sh.in.weight.get(), fa.get(), fsize, msg.get(), best.get(),
+                touched.get(), sizes.get());
+            JG_LAUNCH_CHECK();
+            unsigned long long ts = 0;
+            JG_HIP(hipMemcpyAsync(&ts, sizes.get(), sizeof ts, hipMemcpyDeviceToHost, s));
+            JG_HIP(hipStreamSynchronize(s));
+            if (ts > 0) {
+                sd_apply_kernel<<<grid_for((int64_t)ts, kBlock, 256 * 8), kBlock, 0, s>>>(
+                    touched.get(), (int64_t)ts, best.get(), dist.get(), msg.get(), fb.get(), sizes.get() + 1);
+                JG_LAUNCH_CHECK();
+            }
+            unsigned long long ns = 0;
+            JG_HIP(hipMemcpyAsync(&ns, sizes.get() + 1, sizeof ns, hipMemcpyDeviceToHost, s));
+            JG_HIP(hipStreamSynchronize(s));
+            fsize = (int64_t)ns;
+            fa.swap(fb);
+            levels = t;
+        }
+        std::vector<long long> h(rows);
+        if (rows) JG_HIP(hipMemcpy(h.data(), dist.get(), rows * sizeof(long long), hipMemcpyDeviceToHost));
+        for (int64_t l = 0; l < rows; ++l) host[l] = h[l] == LLONG_MIN ? -1 : h[l];
+    }
+    JG_HIP(hipEventRecord(t1, s));
+    JG_HIP(hipEventSynchronize(t1));
+    float ms = 0;
+    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+    JG_HIP(hipEventDestroy(t0));
+    JG_HIP(hipEventDestroy(t1));
+    ctx.last.compute_ms = ms;
+    ctx.last.levels = levels;
+    ctx.last.supersteps = max_depth;  // Fulgora always runs supersteps 0..maxDepth
+    for (int64_t l = 0; l < rows; ++l) dist_out[sh.dense_of_local[l]] = host[l];
+    prof_collect(ctx, g);
+}
+
+}  // namespace jg

@@ -1,0 +1,161 @@
+"""ctypes front-end of the CPU restatement in oracle/jg_oracle.c.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, never by janusgraph_amd/.  Semantics and reference citations live in jg_oracle.c.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libjg_oracle.so")
+_lib = None
+
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compile libjg_oracle.so (gcc, OpenMP) if missing or stale."""
+    src = os.path.join(_HERE, "jg_oracle.c")
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.jo_rmat_edges.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
+        L.jo_rmat_edges.restype = None
+        L.jo_remap.argtypes = [_i64p, ctypes.c_int64, _i64p, _i64p, ctypes.c_int64, _i32p, _i32p, _i64p]
+        L.jo_remap.restype = ctypes.c_int64
+        L.jo_pagerank.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_double,
+                                  ctypes.c_int64, ctypes.c_int, _f64p, _f64p]
+        L.jo_pagerank.restype = None
+        L.jo_pagerank_superstep_csr.argtypes = [ctypes.c_int64, _i64p, _i32p, _f64p, _f64p, ctypes.c_double,
+                                                ctypes.c_int64, _f64p, ctypes.c_void_p]
+        L.jo_pagerank_superstep_csr.restype = None
+        L.jo_build_in_csr.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, _i64p, _i32p]
+        L.jo_build_in_csr.restype = None
+        L.jo_shortest_distance.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int, _i64p]
+        L.jo_shortest_distance.restype = None
+        L.jo_bfs.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_int, ctypes.c_int64,
+                             ctypes.c_int, _i32p]
+        L.jo_bfs.restype = None
+        L.jo_lex_rank.argtypes = [_i64p, ctypes.c_int64, _i32p]
+        L.jo_lex_rank.restype = None
+        L.jo_connected_components.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, _i64p, ctypes.c_int,
+                                              _i64p]
+        L.jo_connected_components.restype = ctypes.c_int
+        L.jo_num_threads.argtypes = []
+        L.jo_num_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def num_threads() -> int:
+    return int(lib().jo_num_threads())
+
+
+def rmat_edges(scale: int, edgefactor: int, seed: int, e0: int = 0, count: int | None = None):
+    """Graph500 Kronecker edges e0..e0+count of RMAT(scale, seed); dense int64 ids."""
+    m = edgefactor << scale
+    if count is None:
+        count = m - e0
+    src = np.empty(count, np.int64)
+    dst = np.empty(count, np.int64)
+    lib().jo_rmat_edges(scale, seed, e0, count, src, dst)
+    return src, dst
+
+
+def remap(vid, src, dst):
+    """Sparse ids -> dense (caller order), ghost edges dropped.  Returns (dsrc, ddst, keep_idx)."""
+    vid, src, dst = _i64(vid), _i64(src), _i64(dst)
+    m = len(src)
+    dsrc = np.empty(max(m, 1), np.int32)
+    ddst = np.empty(max(m, 1), np.int32)
+    keep = np.empty(max(m, 1), np.int64)
+    k = lib().jo_remap(vid, len(vid), src, dst, m, dsrc, ddst, keep)
+    if k < 0:
+        raise ValueError("duplicate vertex id")
+    return dsrc[:k].copy(), ddst[:k].copy(), keep[:k].copy()
+
+
+def pagerank(n, src, dst, damping=0.85, vertex_count=1, iterations=10):
+    src, dst = _i32(src), _i32(dst)
+    rank = np.empty(max(n, 1), np.float64)
+    ec = np.empty(max(n, 1), np.float64)
+    lib().jo_pagerank(n, len(src), src, dst, float(damping), int(vertex_count), int(iterations), rank, ec)
+    return rank[:n], ec[:n]
+
+
+def build_in_csr(n, src, dst):
+    src, dst = _i32(src), _i32(dst)
+    ptr = np.empty(n + 1, np.int64)
+    col = np.empty(max(len(src), 1), np.int32)
+    lib().jo_build_in_csr(n, len(src), src, dst, ptr, col)
+    return ptr, col[: len(src)]
+
+
+def pagerank_superstep_csr(n, in_ptr, in_src, contrib_in, edge_count, damping, vertex_count, rank_out=None):
+    out = np.empty(n, np.float64)
+    rp = None
+    if rank_out is not None:
+        rp = rank_out.ctypes.data_as(ctypes.c_void_p)
+    lib().jo_pagerank_superstep_csr(n, _i64(in_ptr), _i32(in_src), np.ascontiguousarray(contrib_in, np.float64),
+                                    np.ascontiguousarray(edge_count, np.float64), float(damping),
+                                    int(vertex_count), out, rp)
+    return out
+
+
+def shortest_distance(n, src, dst, seed, max_depth, weight=None):
+    src, dst = _i32(src), _i32(dst)
+    dist = np.empty(max(n, 1), np.int64)
+    w = None
+    if weight is not None:
+        weight = _i32(weight)
+        w = weight.ctypes.data_as(ctypes.c_void_p)
+    lib().jo_shortest_distance(n, len(src), src, dst, w, int(seed), int(max_depth), dist)
+    return dist[:n]
+
+
+DIR_OUT, DIR_IN, DIR_BOTH = 1, 2, 3
+
+
+def bfs(n, src, dst, source, direction=DIR_BOTH, max_depth=-1):
+    src, dst = _i32(src), _i32(dst)
+    depth = np.empty(max(n, 1), np.int32)
+    lib().jo_bfs(n, len(src), src, dst, int(direction), int(source), int(max_depth), depth)
+    return depth[:n]
+
+
+def lex_rank(vid):
+    vid = _i64(vid)
+    r = np.empty(max(len(vid), 1), np.int32)
+    lib().jo_lex_rank(vid, len(vid), r)
+    return r[: len(vid)]
+
+
+def connected_components(n, src, dst, vid, max_iterations=100):
+    src, dst, vid = _i32(src), _i32(dst), _i64(vid)
+    comp = np.empty(max(n, 1), np.int64)
+    it = lib().jo_connected_components(n, len(src), src, dst, vid, int(max_iterations), comp)
+    return comp[:n], int(it)
