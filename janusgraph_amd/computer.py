@@ -1,0 +1,298 @@
+"""GpuGraphComputer — host-side mirror of the TinkerPop GraphComputer API over libjanusgpu.
+
+Mirrors FulgoraGraphComputer (janusgraph-core/src/main/java/org/janusgraph/graphdb/olap/computer/
+FulgoraGraphComputer.java):
+  vertices/edges (graph filters: stored, unsupported at submit)          :108-118, :522
+  result/persist/workers/program/mapReduce (+ JanusGraphComputer.resultMode) :120-152
+  submit(): single use, validation, async execution -> Future[ComputerResult] :154-208
+  memory().getIteration() == last superstep index, getRuntime() in ms        FulgoraMemory.java:97-101
+  map-reduce results under mr.memory_key                                      :288-357
+  write-back of computed keys (ORIGINAL -> the graph, NEW -> a result view)   :359-471
+The supersteps themselves run in libjanusgpu (HIP, gfx950): this module snapshots the graph once,
+calls the C-ABI, and shapes the outputs like Fulgora's.  There is no CPU execution path: programs
+the GPU does not run raise ProgramNotSupported (the Java side delegates those to Fulgora).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import math
+import time
+
+import numpy as np
+
+from . import _lib
+from .computer_types import (Persist, ProgramNotSupported, ResultGraph, ResultMode, computer_has_already_been_submitted,
+                             computer_has_no_vertex_program_nor_map_reducers, graph_filter_not_supported)
+from .graph import InMemoryGraph
+from .programs import (ConnectedComponentVertexProgram, PageRankVertexProgram, ShortestDistanceVertexProgram,
+                       ShortestPathVertexProgram)
+
+
+class Memory:
+    """Global memory of a finished computation (FulgoraMemory after complete())."""
+
+    def __init__(self):
+        self._map = {}
+        self._iteration = 0
+        self._runtime = 0
+
+    def get(self, key):
+        if key not in self._map:
+            raise KeyError(f"The memory does not contain the provided key: {key}")
+        return self._map[key]
+
+    def set(self, key, value):
+        self._map[key] = value
+
+    def exists(self, key):
+        return key in self._map
+
+    def keys(self):
+        return set(self._map)
+
+    def getIteration(self):  # noqa: N802
+        return self._iteration
+
+    def getRuntime(self):  # noqa: N802
+        return self._runtime
+
+    iteration = property(getIteration)
+    runtime = property(getRuntime)
+
+
+class ComputedGraph:
+    """ResultGraph.NEW view: the original vertices with the computed keys overlaid."""
+
+    def __init__(self, base: InMemoryGraph, props: dict):
+        self.base, self.props = base, props
+
+    def value(self, vid, key):
+        return self.props[int(vid)][key]
+
+    def properties(self, vid):
+        return self.props.get(int(vid), {})
+
+
+class ComputerResult:
+    def __init__(self, graph, memory: Memory):
+        self._graph, self._memory = graph, memory
+
+    def graph(self):
+        return self._graph
+
+    def memory(self) -> Memory:
+        return self._memory
+
+
+class GpuGraphComputer:
+    """graph.compute(GpuGraphComputer.class) for the programs of programs.RECOGNISED."""
+
+    def __init__(self, graph: InMemoryGraph, devices=(0,), context: _lib.Context | None = None):
+        self.graph = graph
+        self.devices = tuple(devices)
+        self._context = context
+        self.vertex_program = None
+        self.map_reduces = []
+        self.result_graph_mode = None
+        self.persist_mode = None
+        self.num_threads = 1
+        self.vertex_filter = None
+        self.edge_filter = None
+        self.executed = False
+
+    # ---- GraphComputer builder methods ----
+    def vertices(self, vertex_filter):
+        self.vertex_filter = vertex_filter
+        return self
+
+    def edges(self, edge_filter):
+        self.edge_filter = edge_filter
+        return self
+
+    def result(self, mode: ResultGraph):
+        if mode is None:
+            raise ValueError("Need to specify mode")
+        self.result_graph_mode = mode
+        return self
+
+    def persist(self, mode: Persist):
+        if mode is None:
+            raise ValueError("Need to specify mode")
+        self.persist_mode = mode
+        return self
+
+    def resultMode(self, mode: ResultMode):  # noqa: N802 (JanusGraphComputer.resultMode)
+        return self.result(mode.result_graph).persist(mode.persist)
+
+    def workers(self, threads: int):
+        if threads <= 0:
+            raise ValueError(f"Invalid number of threads: {threads}")
+        self.num_threads = threads  # GPU parallelism is internal; accepted for API parity
+        return self
+
+    def program(self, vertex_program):
+        if self.vertex_program is not None:
+            raise RuntimeError("A vertex program has already been set")
+        self.vertex_program = vertex_program
+        return self
+
+    def mapReduce(self, map_reduce):  # noqa: N802
+        self.map_reduces.append(map_reduce)
+        return self
+
+    @staticmethod
+    def features():
+        return {"supportsVertexAddition": False, "supportsVertexRemoval": False,
+                "supportsVertexPropertyAddition": True, "supportsVertexPropertyRemoval": False,
+                "supportsEdgeAddition": False, "supportsEdgeRemoval": False, "supportsEdgePropertyAddition": False,
+                "supportsEdgePropertyRemoval": False, "supportsGraphFilter": False}
+
+    # ---- submit ----
+    def submit(self) -> cf.Future:
+        if self.executed:
+            raise computer_has_already_been_submitted()
+        self.executed = True
+        if self.vertex_program is None and not self.map_reduces:
+            raise computer_has_no_vertex_program_nor_map_reducers()
+        if self.vertex_filter is not None or self.edge_filter is not None:
+            raise graph_filter_not_supported()
+        vp = self.vertex_program
+        if vp is not None:
+            if not isinstance(vp, (PageRankVertexProgram, ShortestDistanceVertexProgram,
+                                   ConnectedComponentVertexProgram, ShortestPathVertexProgram)):
+                raise ProgramNotSupported(f"{type(vp).__name__} is not run by GpuGraphComputer; "
+                                          f"delegate to FulgoraGraphComputer")
+            self.map_reduces.extend(vp.get_map_reducers())
+        if self.persist_mode is None:
+            self.persist_mode = vp.preferred_persist if vp is not None else Persist.NOTHING
+        if self.result_graph_mode is None:
+            self.result_graph_mode = vp.preferred_result_graph if vp is not None else ResultGraph.ORIGINAL
+        pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="GpuGraphComputer")
+        fut = pool.submit(self._submit_async)
+        pool.shutdown(wait=False)
+        return fut
+
+    # ---- execution ----
+    def _ctx(self) -> _lib.Context:
+        if self._context is None:
+            self._context = _lib.Context(self.devices)
+        return self._context
+
+    def _submit_async(self) -> ComputerResult:
+        t0 = time.perf_counter()
+        memory = Memory()
+        props = {}
+        vids = None
+        if self.vertex_program is not None:
+            vids, props, iteration, extra = self._execute_vertex_program(self.vertex_program)
+            memory._iteration = iteration
+            for k, v in extra.items():
+                memory.set(k, v)
+        for mr in self.map_reduces:
+            emitted = []
+            for vid in (vids if vids is not None else []):
+                mr.map(int(vid), props.get(int(vid), {}), lambda k, v: emitted.append((k, v)))
+            memory.set(mr.memory_key, iter(emitted))
+        result_graph = self._write_back(props)
+        memory._runtime = int(round((time.perf_counter() - t0) * 1000))
+        return ComputerResult(result_graph, memory)
+
+    def _execute_vertex_program(self, vp):
+        g0 = self.graph
+        ctx = self._ctx()
+        if isinstance(vp, PageRankVertexProgram):
+            vid, src, dst, _ = g0.snapshot()
+            if vp.max_iterations == 0:
+                return vid, {}, 0, {}
+            g = ctx.build(vid, src, dst, flags=_lib.ADJ_IN)
+            try:
+                rank, ec = g.pagerank(vp.damping_factor, vp.vertex_count, vp.max_iterations)
+            finally:
+                g.close()
+            props = {int(v): {vp.PAGE_RANK: float(r), vp.OUTGOING_EDGE_COUNT: float(c)}
+                     for v, r, c in zip(vid, rank, ec)}
+            return vid, props, vp.max_iterations, {}
+        if isinstance(vp, ShortestDistanceVertexProgram):
+            vid, src, dst, w = g0.snapshot(weight_property=vp.weight_property)
+            g = ctx.build(vid, src, dst, weight=w, flags=_lib.ADJ_IN | _lib.ADJ_OUT)
+            try:
+                dist = g.shortest_distance(vp.seed, vp.max_depth)
+            finally:
+                g.close()
+            props = {int(v): {vp.DISTANCE: int(d)} for v, d in zip(vid, dist) if d >= 0}
+            return vid, props, vp.max_depth, {}
+        if isinstance(vp, ConnectedComponentVertexProgram):
+            vid, src, dst, _ = g0.snapshot()
+            g = ctx.build(vid, src, dst, flags=_lib.ADJ_BOTH)
+            try:
+                comp, it = g.connected_components()
+            finally:
+                g.close()
+            props = {int(v): {vp.property: str(int(c))} for v, c in zip(vid, comp)}
+            return vid, props, it, {}
+        if isinstance(vp, ShortestPathVertexProgram):
+            return self._shortest_paths(ctx, vp)
+        raise ProgramNotSupported(type(vp).__name__)
+
+    def _shortest_paths(self, ctx, vp):
+        vid, src, dst, _ = self.graph.snapshot()
+        present = set(vid.tolist())
+        sources = [s for s in (vp.sources if vp.sources is not None else vid.tolist()) if s in present]
+        targets = set(vp.targets) if vp.targets is not None else None
+        g = ctx.build(vid, src, dst, flags=_lib.ADJ_BOTH)
+        paths, max_level = [], 0
+        try:
+            if sources:
+                depth = g.bfs(np.asarray(sources, np.int64), _lib.DIR_BOTH,
+                              -1 if vp.max_distance is None else vp.max_distance)
+                max_level = int(depth.max(initial=0))
+                adj = _undirected_adjacency(vid, src, dst)
+                index = {int(v): i for i, v in enumerate(vid.tolist())}
+                for si, s in enumerate(sources):
+                    d = depth[si]
+                    for ti in np.nonzero(d >= 0)[0]:
+                        t = int(vid[ti])
+                        if targets is not None and t not in targets:
+                            continue
+                        paths.extend(_all_shortest_paths(adj, index, d, vid, index[s], int(ti)))
+        finally:
+            g.close()
+        return vid, {}, max_level + 1, {vp.SHORTEST_PATHS: paths}
+
+    def _write_back(self, props):
+        if self.persist_mode is Persist.NOTHING:
+            return None if self.result_graph_mode is ResultGraph.NEW else self.graph
+        if self.result_graph_mode is ResultGraph.ORIGINAL:
+            for vid, kv in props.items():
+                v = self.graph.vertices.get(vid)
+                if v is not None:
+                    v.properties.update(kv)
+            return self.graph
+        return ComputedGraph(self.graph, props)
+
+
+def _undirected_adjacency(vid, src, dst):
+    index = {int(v): i for i, v in enumerate(vid.tolist())}
+    adj = [[] for _ in range(len(vid))]
+    for a, b in zip(src.tolist(), dst.tolist()):
+        if a in index and b in index:
+            adj[index[a]].append(index[b])
+            adj[index[b]].append(index[a])
+    return adj
+
+
+def _all_shortest_paths(adj, index, depth, vid, s, t):
+    """Every shortest s..t path (vertex ids) from a BFS depth array, walking back from t."""
+    out = []
+
+    def back(v, suffix):
+        if v == s:
+            out.append([int(vid[x]) for x in reversed(suffix + [v])])
+            return
+        for u in sorted(set(adj[v])):
+            if depth[u] == depth[v] - 1:
+                back(u, suffix + [v])
+
+    if depth[t] >= 0 and not math.isinf(depth[t]):
+        back(t, [])
+    return out

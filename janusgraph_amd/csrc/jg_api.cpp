@@ -6,6 +6,7 @@
 // (janusgraph-core/.../olap/computer/FulgoraGraphComputer.java:269-286): any failure aborts the
 // whole program run; callers wrap a non-zero status in a JanusGraphException.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -83,6 +84,19 @@ int allreduce_or(Graph& g, int flag) {
 }
 
 bool prof_enabled(const Ctx& c) { return c.profiling; }
+
+static bool env_flag(const char* name) {
+    const char* v = std::getenv(name);
+    return v && *v && std::strcmp(v, "0") != 0;
+}
+bool pull_split_launches() {
+    static const bool v = env_flag("JG_PULL_SPLIT");
+    return v;
+}
+bool debug_plan() {
+    static const bool v = env_flag("JG_DEBUG_PLAN");
+    return v;
+}
 
 void prof_record_start(Ctx& c, Shard& sh) {
     if (!c.profiling) return;
@@ -308,10 +322,10 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
         jg::Shard& sh = *g.shards[i];
         jg::DeviceGuard dg(sh.device);
         jg::DevBuf<int64_t> dvid(std::max<int64_t>(n, 1)), dsrc(std::max<int64_t>(m, 1)), ddst(std::max<int64_t>(m, 1));
-        if (n) JG_HIP(hipMemcpy(dvid.get(), vid, n * sizeof(int64_t), hipMemcpyHostToDevice));
+        if (n) jg::copy_h2d(dvid.get(), vid, n * sizeof(int64_t), sh.stream);
         if (m) {
-            JG_HIP(hipMemcpy(dsrc.get(), src, m * sizeof(int64_t), hipMemcpyHostToDevice));
-            JG_HIP(hipMemcpy(ddst.get(), dst, m * sizeof(int64_t), hipMemcpyHostToDevice));
+            jg::copy_h2d(dsrc.get(), src, m * sizeof(int64_t), sh.stream);
+            jg::copy_h2d(ddst.get(), dst, m * sizeof(int64_t), sh.stream);
         }
         ds[i].alloc(std::max<int64_t>(m, 1));
         dd[i].alloc(std::max<int64_t>(m, 1));
@@ -320,7 +334,7 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
         e.dst.push_back(dd[i].get());
         if (weight) {
             dw[i].alloc(std::max<int64_t>(m, 1));
-            if (m) JG_HIP(hipMemcpy(dw[i].get(), weight, m * sizeof(int32_t), hipMemcpyHostToDevice));
+            if (m) jg::copy_h2d(dw[i].get(), weight, m * sizeof(int32_t), sh.stream);
             e.weight.push_back(dw[i].get());
         } else {
             e.weight.push_back(nullptr);

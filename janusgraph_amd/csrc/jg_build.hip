@@ -377,13 +377,13 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
         JG_LAUNCH_CHECK();
         const int64_t nh = prim::compact_indices(flag.get(), rows, idx.get(), s);
         hubs.resize(nh);
-        if (nh) JG_HIP(hipMemcpy(hubs.data(), idx.get(), nh * sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (nh) copy_d2h(hubs.data(), idx.get(), nh * sizeof(int64_t), s);
     }
     std::vector<int64_t> crow, cbeg, cend, hptr(1, 0);
     for (int64_t r : hubs) {
         int64_t b = 0, e = 0;
-        JG_HIP(hipMemcpy(&b, csr.row_ptr.get() + r, sizeof(int64_t), hipMemcpyDeviceToHost));
-        JG_HIP(hipMemcpy(&e, csr.row_ptr.get() + r + 1, sizeof(int64_t), hipMemcpyDeviceToHost));
+        copy_d2h(&b, csr.row_ptr.get() + r, sizeof(int64_t), s);
+        copy_d2h(&e, csr.row_ptr.get() + r + 1, sizeof(int64_t), s);
         for (int64_t p = b; p < e; p += kHubChunk) {
             crow.push_back(r);
             cbeg.push_back(p);
@@ -395,7 +395,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
     plan.num_chunks = (int64_t)crow.size();
     auto upload = [&](DevBuf<int64_t>& d, const std::vector<int64_t>& h) {
         d.alloc(std::max<size_t>(h.size(), 1));
-        if (!h.empty()) JG_HIP(hipMemcpy(d.get(), h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+        if (!h.empty()) copy_h2d(d.get(), h.data(), h.size() * sizeof(int64_t), s);
     };
     upload(plan.chunk_row, crow);
     upload(plan.chunk_begin, cbeg);
@@ -406,10 +406,10 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
     if (rows > 0) {
         DevBuf<unsigned long long> d_fb(kNumClasses);
-        JG_HIP(hipMemcpy(d_fb.get(), fb, sizeof fb, hipMemcpyHostToDevice));
+        copy_h2d(d_fb.get(), fb, sizeof fb, s);
         class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get());
         JG_LAUNCH_CHECK();
-        JG_HIP(hipMemcpy(fb, d_fb.get(), sizeof fb, hipMemcpyDeviceToHost));
+        copy_d2h(fb, d_fb.get(), sizeof fb, s);
     }
     // class 1 (64 lanes) starts at row 0; class c ends where class c+1 begins
     int64_t begin = 0;
@@ -425,6 +425,18 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
         const int64_t rows_per_block = kBlock / lanes;
         plan.class_block_begin[c + 1] = plan.class_block_begin[c] + (end - begin + rows_per_block - 1) / rows_per_block;
         begin = end;
+    }
+    if (debug_plan()) {
+        std::vector<int64_t> rp(rows + 1);
+        copy_d2h(rp.data(), csr.row_ptr.get(), (rows + 1) * sizeof(int64_t), s);
+        std::fprintf(stderr, "[jg plan] shard %d rows %lld nnz %lld hubs %lld chunks %lld\n", sh.index, (long long)rows,
+                     (long long)csr.nnz, (long long)plan.num_hub_rows, (long long)plan.num_chunks);
+        for (int c = 1; c < kNumClasses; ++c) {
+            const int64_t b = plan.class_row_begin[c], e = plan.class_row_end[c];
+            std::fprintf(stderr, "[jg plan]   class %d lanes %2d rows [%lld,%lld) = %lld nnz %lld blocks %lld\n", c,
+                         64 >> (c - 1), (long long)b, (long long)e, (long long)(e - b), (long long)(rp[e] - rp[b]),
+                         (long long)(plan.class_block_begin[c + 1] - plan.class_block_begin[c]));
+        }
     }
 }
 
@@ -485,7 +497,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         sh.rows = std::max<int64_t>(0, std::min<int64_t>(g.S, (n - r + P - 1) / P));
         // host copies: dense index of each owned row, padded id of every vertex (once)
         std::vector<int32_t> h_order(n);
-        if (n) JG_HIP(hipMemcpy(h_order.data(), order.get(), n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (n) copy_d2h(h_order.data(), order.get(), n * sizeof(int32_t), s);
         sh.dense_of_local.resize(sh.rows);
         for (int64_t l = 0; l < sh.rows; ++l) sh.dense_of_local[l] = h_order[(size_t)(r + l * P)];
         if (first) {

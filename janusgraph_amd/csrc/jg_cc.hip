@@ -111,7 +111,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         DevBuf<uint32_t> vals(std::max<int64_t>(n, 1));
         DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
         if (n > 0) {
-            JG_HIP(hipMemcpy(vid.get(), hv.data(), n * sizeof(int64_t), hipMemcpyHostToDevice));
+            copy_h2d(vid.get(), hv.data(), n * sizeof(int64_t), s);
             lex_digits_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n, keys.get(), vals.get());
             JG_LAUNCH_CHECK();
             prim::radix_sort(keys.get(), vals.get(), n, 5, s);
@@ -120,7 +120,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             prim::radix_sort(keys.get(), vals.get(), n, 64, s);
             lex_rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), n, rk.get());
             JG_LAUNCH_CHECK();
-            JG_HIP(hipMemcpy(rank_of.data(), rk.get(), n * sizeof(int32_t), hipMemcpyDeviceToHost));
+            copy_d2h(rank_of.data(), rk.get(), n * sizeof(int32_t), s);
         }
         for (int64_t d = 0; d < n; ++d) vid_of_rank[rank_of[d]] = hv[d];
     }
@@ -139,7 +139,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
         DevBuf<int32_t> dlab0(std::max<int64_t>(sh.rows, 1));
         if (sh.rows) {
-            JG_HIP(hipMemcpy(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), hipMemcpyHostToDevice));
+            copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
             cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
                                                                         (int64_t)sh.index * g.S, sh.cc_label.get(),
                                                                         sh.cc_msg[0].get());
@@ -207,7 +207,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             Shard& sh = *sp;
             DeviceGuard dg(sh.device);
             std::vector<int32_t> h(sh.rows);
-            if (sh.rows) JG_HIP(hipMemcpy(h.data(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+            if (sh.rows) copy_d2h(h.data(), sh.cc_label.get(), sh.rows * sizeof(int32_t), sh.stream);
             for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local[l]] = vid_of_rank[h[l]];
         }
     }

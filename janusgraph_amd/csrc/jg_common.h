@@ -91,6 +91,19 @@ inline int bits_for(uint64_t x) {  // number of bits to represent values in [0, 
     return b;
 }
 
+// Host<->device copies ordered on the library's (non-blocking) stream `s`, then synchronised.
+// Plain hipMemcpy runs on the legacy stream, which does NOT wait for non-blocking streams.
+inline void copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    JG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+}
+inline void copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    JG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    JG_HIP(hipStreamSynchronize(s));
+}
+
 // RAII device switch.
 struct DeviceGuard {
     int prev = 0;

@@ -139,6 +139,11 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
 // Logical OR of a flag over all ranks (identity in single-process contexts).
 int allreduce_or(Graph& g, int flag);
 
+// Diagnostics from the environment: JG_PULL_SPLIT=1 launches each degree class separately,
+// JG_DEBUG_PLAN=1 prints every pull plan at build time.
+bool pull_split_launches();
+bool debug_plan();
+
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);
 void prof_record_start(Ctx& c, Shard& sh);

@@ -119,12 +119,12 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out) {
         if (sh.rows == 0) continue;
         if (rank_out) {
             std::vector<double> h(sh.rows);
-            JG_HIP(hipMemcpy(h.data(), sh.pr_rank.get(), sh.rows * sizeof(double), hipMemcpyDeviceToHost));
+            copy_d2h(h.data(), sh.pr_rank.get(), sh.rows * sizeof(double), sh.stream);
             for (int64_t l = 0; l < sh.rows; ++l) rank_out[sh.dense_of_local[l]] = h[l];
         }
         if (edge_count_out) {
             std::vector<int32_t> h(sh.rows);
-            JG_HIP(hipMemcpy(h.data(), sh.out_degree.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+            copy_d2h(h.data(), sh.out_degree.get(), sh.rows * sizeof(int32_t), sh.stream);
             for (int64_t l = 0; l < sh.rows; ++l) edge_count_out[sh.dense_of_local[l]] = (double)h[l];
         }
     }

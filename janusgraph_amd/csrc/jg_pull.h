@@ -30,6 +30,7 @@ struct PullArgs {
     int64_t class_row_begin[kNumClasses];
     int64_t class_row_end[kNumClasses];
     int64_t class_block_begin[kNumClasses + 1];
+    int64_t block_offset;  // diagnostic split launches (JG_PULL_SPLIT=1): first block of this launch
 };
 
 inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
@@ -47,6 +48,7 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
         a.class_row_end[c] = p.class_row_end[c];
     }
     for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = p.class_block_begin[c];
+    a.block_offset = 0;
     return a;
 }
 
@@ -91,7 +93,7 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
 template <class Op>
 __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
     using T = typename Op::T;
-    const int64_t b = blockIdx.x;
+    const int64_t b = (int64_t)blockIdx.x + a.block_offset;
     if (b < a.num_chunks) {
         __shared__ T red[kBlock / kWave];
         const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
@@ -140,10 +142,18 @@ __global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
                  Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr) {
-    const PullArgs a = make_pull_args(csr, plan);
+    PullArgs a = make_pull_args(csr, plan);
     const int64_t blocks = plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
-    if (blocks > 0) {
+    if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
+        for (int c = 0; c < kNumClasses; ++c) {
+            const int64_t b0 = plan.class_block_begin[c], b1 = plan.class_block_begin[c + 1];
+            if (b1 <= b0) continue;
+            a.block_offset = b0;
+            pull_kernel<Op><<<(unsigned)(b1 - b0), kBlock, 0, s>>>(a, op, hub_partial);
+            JG_LAUNCH_CHECK();
+        }
+    } else if (blocks > 0) {
         pull_kernel<Op><<<(unsigned)blocks, kBlock, 0, s>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }

@@ -400,7 +400,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
         if (depth_out) {
             std::vector<int32_t> h(sh.rows);
-            if (sh.rows) JG_HIP(hipMemcpy(h.data(), depth.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+            if (sh.rows) copy_d2h(h.data(), depth.get(), sh.rows * sizeof(int32_t), sh.stream);
             for (int64_t v = 0; v < sh.rows; ++v) depth_out[sh.dense_of_local[v]] = h[v];
         }
         prof_collect(ctx, g);
@@ -444,7 +444,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     if (l >= 0 && shard == sh.index) loc[s] = l;
                 }
                 DevBuf<int64_t> dloc(ns);
-                JG_HIP(hipMemcpy(dloc.get(), loc.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice));
+                copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
                 msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth.get(),
                                                           sh.rows, (int64_t)sh.index * g.S);
                 JG_LAUNCH_CHECK();
@@ -508,7 +508,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     DeviceGuard dg(sh.device);
                     std::vector<int32_t> h(sh.rows * ns);
                     if (!h.empty())
-                        JG_HIP(hipMemcpy(h.data(), st[i].depth.get(), h.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+                        copy_d2h(h.data(), st[i].depth.get(), h.size() * sizeof(int32_t), sh.stream);
                     for (int s = 0; s < ns; ++s)
                         for (int64_t l = 0; l < sh.rows; ++l)
                             depth_out[(int64_t)(b0 + s) * g.n + sh.dense_of_local[l]] = h[(size_t)(s * sh.rows + l)];
@@ -547,7 +547,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         BfsCsrs c{&sh.in, sh.out.present() ? &sh.out : nullptr};
         levels = dobfs_single(ctx, sh, c, seed, max_depth, depth.get(), nullptr);
         std::vector<int32_t> h(rows);
-        if (rows) JG_HIP(hipMemcpy(h.data(), depth.get(), rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (rows) copy_d2h(h.data(), depth.get(), rows * sizeof(int32_t), s);
         for (int64_t l = 0; l < rows; ++l) host[l] = h[l];
     } else if (seed >= 0) {
         DevBuf<long long> dist(std::max<int64_t>(rows, 1)), msg(std::max<int64_t>(rows, 1)),
@@ -586,7 +586,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
             levels = t;
         }
         std::vector<long long> h(rows);
-        if (rows) JG_HIP(hipMemcpy(h.data(), dist.get(), rows * sizeof(long long), hipMemcpyDeviceToHost));
+        if (rows) copy_d2h(h.data(), dist.get(), rows * sizeof(long long), s);
         for (int64_t l = 0; l < rows; ++l) host[l] = h[l] == LLONG_MIN ? -1 : h[l];
     }
     JG_HIP(hipEventRecord(t1, s));

@@ -1,0 +1,75 @@
+"""The C-ABI library loads here (no GPU) and exports exactly what include/janusgpu.h declares."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "janusgpu.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(jg_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_drop_in_surface():
+    fns = header_functions()
+    for f in ["jg_ctx_create", "jg_graph_build", "jg_pagerank", "jg_bfs", "jg_shortest_distance",
+              "jg_connected_components", "jg_graph_destroy", "jg_last_error", "jg_ctx_last_stats"]:
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    import janusgraph_amd._lib as L
+    lib = L.load()
+    fns = header_functions()
+    assert sorted(fns) == sorted(L.EXPORTS)
+    for f in fns:
+        assert hasattr(lib, f), f
+    out = subprocess.check_output(["nm", "-D", "--defined-only", L.LIB_PATH], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(fns) <= exported
+
+
+def test_abi_version_and_no_gpu_error_is_a_status():
+    import janusgraph_amd as jg
+    lib = jg.load()
+    assert lib.jg_abi_version() == 1
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("a GPU is present")
+    with pytest.raises(jg.JanusGpuError) as e:
+        jg.Context((0,))
+    assert e.value.code in (-3, -1)
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """sizeof/offsetof of jg_graph_info and jg_stats from gcc == the ctypes mirrors."""
+    import ctypes
+    import janusgraph_amd._lib as L
+    src = tmp_path / "layout.c"
+    fields_i = [f for f, _ in L.GraphInfo._fields_]
+    fields_s = [f for f, _ in L.Stats._fields_]
+    body = ["#include <stdio.h>", "#include <stddef.h>", '#include "janusgpu.h"', "int main(void){",
+            'printf("%zu\\n", sizeof(jg_graph_info));', 'printf("%zu\\n", sizeof(jg_stats));']
+    body += [f'printf("%zu\\n", offsetof(jg_graph_info, {f}));' for f in fields_i]
+    body += [f'printf("%zu\\n", offsetof(jg_stats, {f}));' for f in fields_s]
+    body += ["return 0;}"]
+    src.write_text("\n".join(body))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    vals = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
+    want = [ctypes.sizeof(L.GraphInfo), ctypes.sizeof(L.Stats)]
+    want += [getattr(L.GraphInfo, f).offset for f in fields_i] + [getattr(L.Stats, f).offset for f in fields_s]
+    assert vals == want
+
+
+def test_header_compiles_as_plain_c():
+    subprocess.check_call(["gcc", "-std=c99", "-fsyntax-only", "-Wall", "-Werror", "-x", "c", HEADER])
