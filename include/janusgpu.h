@@ -169,6 +169,10 @@ int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* it
 /* Block until all work enqueued on the graph's streams is complete. */
 int jg_graph_sync(jg_graph* g);
 
+/* Process-wide performance knobs (no effect on results): "pull_unroll" (4 | 8 gathers in flight per
+ * lane), "pull_nt" (0 | 1: non-temporal loads of the streamed adjacency).  Unknown key: JG_ERR_ARG. */
+int jg_tune_set(const char* key, int64_t value);
+
 #ifdef __cplusplus
 }
 #endif

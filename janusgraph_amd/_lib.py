@@ -33,6 +33,7 @@ EXPORTS = [
     "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_graph_sync",
+    "jg_tune_set",
 ]
 
 
@@ -106,6 +107,7 @@ def load():
         "jg_bfs": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
         "jg_connected_components": ([_P, _P, _P], ctypes.c_int),
         "jg_graph_sync": ([_P], ctypes.c_int),
+        "jg_tune_set": ([ctypes.c_char_p, _i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -123,6 +125,11 @@ def check(status):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def tune_set(key: str, value: int):
+    """Process-wide performance knob (results are unaffected): pull_unroll, pull_nt."""
+    check(load().jg_tune_set(key.encode(), int(value)))
 
 
 def comm_unique_id() -> bytes:

@@ -98,6 +98,11 @@ bool debug_plan() {
     return v;
 }
 
+Tune& tune() {
+    static Tune t;
+    return t;
+}
+
 void prof_record_start(Ctx& c, Shard& sh) {
     if (!c.profiling) return;
     hipEvent_t e;
@@ -171,6 +176,21 @@ void g_last_error_set(const char* m) { g_last_error = m ? m : ""; }
 extern "C" {
 
 int jg_abi_version(void) { return JG_ABI_VERSION; }
+
+int jg_tune_set(const char* key, int64_t value) {
+    JG_GUARD_BEGIN
+    JG_ARG(key, "null key");
+    const std::string k(key);
+    if (k == "pull_unroll") {
+        JG_ARG(value == 4 || value == 8, "pull_unroll must be 4 or 8");
+        jg::tune().pull_unroll = (int)value;
+    } else if (k == "pull_nt") {
+        jg::tune().pull_nt = value != 0;
+    } else {
+        jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
+    }
+    JG_GUARD_END
+}
 
 const char* jg_last_error(void) { return jg::g_last_error.c_str(); }
 

@@ -282,15 +282,28 @@ __global__ void hub_flag_kernel(const int64_t* __restrict__ rp, int64_t rows, ui
         flag[l] = (rp[l + 1] - rp[l]) >= kHubDegree;
 }
 
-__constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 0};
+// degree thresholds of the lane classes 1..6 (class 7 takes the rest, class 8 the empty suffix)
+__constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 1, 0};
 
+// first_below[c] = first row with degree < c_class_thr[c] (c = 1..6);
+// first_below[kZeroClass] = 1 + last row with any entry (rows after it are all empty)
 __global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
-                                   unsigned long long* __restrict__ first_below /* [kNumClasses] */) {
+                                   unsigned long long* __restrict__ first_below /* [kNumClasses] */,
+                                   unsigned long long* __restrict__ last_nonempty) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = rp[l + 1] - rp[l];
 #pragma unroll
-        for (int c = 1; c < kNumClasses - 1; ++c)
+        for (int c = 1; c < kNumClasses - 2; ++c)
             if (d < c_class_thr[c]) atomicMin(&first_below[c], (unsigned long long)l);
+        if (d > 0) atomicMax(last_nonempty, (unsigned long long)(l + 1));
+    }
+}
+
+__global__ void gather_row_bounds_kernel(const int64_t* __restrict__ rp, const int64_t* __restrict__ rows_idx,
+                                         int64_t nh, int64_t* __restrict__ out /* [2*nh] */) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
+        out[2 * i] = rp[rows_idx[i]];
+        out[2 * i + 1] = rp[rows_idx[i] + 1];
     }
 }
 
@@ -369,7 +382,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
     hipStream_t s = sh.stream;
     const int64_t rows = csr.rows;
     // hub rows (any position) -> chunk table
-    std::vector<int64_t> hubs;
+    std::vector<int64_t> hubs, bounds;
     if (rows > 0) {
         DevBuf<uint8_t> flag(rows);
         DevBuf<int64_t> idx(rows);
@@ -377,13 +390,18 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
         JG_LAUNCH_CHECK();
         const int64_t nh = prim::compact_indices(flag.get(), rows, idx.get(), s);
         hubs.resize(nh);
-        if (nh) copy_d2h(hubs.data(), idx.get(), nh * sizeof(int64_t), s);
+        bounds.resize(2 * nh);
+        if (nh) {
+            DevBuf<int64_t> db(2 * nh);
+            gather_row_bounds_kernel<<<grid_for(nh), kBlock, 0, s>>>(csr.row_ptr.get(), idx.get(), nh, db.get());
+            JG_LAUNCH_CHECK();
+            copy_d2h(hubs.data(), idx.get(), nh * sizeof(int64_t), s);
+            copy_d2h(bounds.data(), db.get(), 2 * nh * sizeof(int64_t), s);
+        }
     }
     std::vector<int64_t> crow, cbeg, cend, hptr(1, 0);
-    for (int64_t r : hubs) {
-        int64_t b = 0, e = 0;
-        copy_d2h(&b, csr.row_ptr.get() + r, sizeof(int64_t), s);
-        copy_d2h(&e, csr.row_ptr.get() + r + 1, sizeof(int64_t), s);
+    for (size_t h = 0; h < hubs.size(); ++h) {
+        const int64_t r = hubs[h], b = bounds[2 * h], e = bounds[2 * h + 1];
         for (int64_t p = b; p < e; p += kHubChunk) {
             crow.push_back(r);
             cbeg.push_back(p);
@@ -402,26 +420,31 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
     upload(plan.chunk_end, cend);
     upload(plan.hub_chunk_ptr, hptr);
     // class boundaries: first row whose degree falls below each class threshold
-    unsigned long long fb[kNumClasses];
+    unsigned long long fb[kNumClasses + 1];
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
+    fb[kNumClasses] = 0;  // 1 + last non-empty row
     if (rows > 0) {
-        DevBuf<unsigned long long> d_fb(kNumClasses);
+        DevBuf<unsigned long long> d_fb(kNumClasses + 1);
         copy_h2d(d_fb.get(), fb, sizeof fb, s);
-        class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get());
+        class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get(),
+                                                             d_fb.get() + kNumClasses);
         JG_LAUNCH_CHECK();
         copy_d2h(fb, d_fb.get(), sizeof fb, s);
     }
-    // class 1 (64 lanes) starts at row 0; class c ends where class c+1 begins
+    // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
+    // changes), but the empty class starts strictly after the last non-empty row (correctness).
+    const int64_t zero_begin = (int64_t)fb[kNumClasses];
     int64_t begin = 0;
     plan.class_row_begin[0] = plan.class_row_end[0] = 0;  // hub class is the chunk table
     plan.class_block_begin[0] = 0;
     plan.class_block_begin[1] = plan.num_chunks;
     for (int c = 1; c < kNumClasses; ++c) {
-        int64_t end = (c < kNumClasses - 1) ? (int64_t)fb[c] : rows;
+        int64_t end = c < kZeroClass - 1 ? (int64_t)fb[c] : c == kZeroClass - 1 ? zero_begin : rows;
+        end = std::min(std::max(end, begin), c < kZeroClass ? zero_begin : rows);
         end = std::max(end, begin);
         plan.class_row_begin[c] = begin;
         plan.class_row_end[c] = end;
-        const int lanes = 64 >> (c - 1);
+        const int lanes = c == kZeroClass ? 1 : 64 >> (c - 1);
         const int64_t rows_per_block = kBlock / lanes;
         plan.class_block_begin[c + 1] = plan.class_block_begin[c] + (end - begin + rows_per_block - 1) / rows_per_block;
         begin = end;

@@ -31,7 +31,8 @@ struct Csr {
 
 // Degree-class plan for the pull kernels of one CSR on one shard.  Rows are sorted by degree
 // (descending), so each class is a contiguous row range.
-constexpr int kNumClasses = 8;  // 0: hub (chunked), 1..7: lanes per row 64,32,16,8,4,2,1
+constexpr int kNumClasses = 9;  // 0: hub (chunked), 1..7: lanes per row 64,32,16,8,4,2,1, 8: empty rows
+constexpr int kZeroClass = kNumClasses - 1;
 constexpr int64_t kHubDegree = 8192;
 constexpr int64_t kHubChunk = 4096;
 
@@ -143,6 +144,14 @@ int allreduce_or(Graph& g, int flag);
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
 bool pull_split_launches();
 bool debug_plan();
+
+// Performance knobs (jg_tune_set): variants of the pull kernel selectable at run time so that they
+// can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).
+struct Tune {
+    int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
+    int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
+};
+Tune& tune();
 
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);

@@ -8,6 +8,7 @@
 //            written to hub_partial[], combined in chunk order by pull_hub_finalize_kernel
 //   class c  (c = 1..7) L = 64 >> (c-1) lanes per row, 256/L rows per workgroup; lanes stride the
 //            row, fold, then a width-L xor-shuffle tree; lane 0 finalises the row
+//   class 8  the suffix of rows without entries: finalised with the identity, row_ptr not read
 // Every row is folded in a fixed order that does not depend on timing (bit-reproducible runs).
 // An Op supplies: T, identity(), combine(a,b), gather(col), shfl_xor(v,o), active(row) (false: the
 // row is not folded but still finalised with identity()), finalize(row, acc).
@@ -52,26 +53,33 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
     return a;
 }
 
-// Fold col[j0..j1) with stride `stride` starting at j0 + first; 4 gathers in flight per lane,
-// folded in index order.
-template <class Op>
+template <bool NT>
+__device__ __forceinline__ int32_t load_col(const int32_t* __restrict__ col, int64_t j) {
+    if constexpr (NT) return __builtin_nontemporal_load(col + j);  // streamed once: don't keep it in cache
+    else return col[j];
+}
+
+// Fold col[j..j1) with stride `stride`; U gathers in flight per lane, folded in index order.
+template <class Op, int U, bool NT>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
                                                        int64_t j1, int stride) {
     using T = typename Op::T;
     T acc = op.identity();
-    for (; j + 3 * (int64_t)stride < j1; j += 4 * (int64_t)stride) {
-        const int32_t c0 = col[j], c1 = col[j + stride], c2 = col[j + 2 * stride], c3 = col[j + 3 * stride];
-        const T v0 = op.gather(c0), v1 = op.gather(c1), v2 = op.gather(c2), v3 = op.gather(c3);
-        acc = op.combine(acc, v0);
-        acc = op.combine(acc, v1);
-        acc = op.combine(acc, v2);
-        acc = op.combine(acc, v3);
+    for (; j + (U - 1) * (int64_t)stride < j1; j += U * (int64_t)stride) {
+        int32_t c[U];
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = load_col<NT>(col, j + u * (int64_t)stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = op.gather(c[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = op.combine(acc, v[u]);
     }
-    for (; j < j1; j += stride) acc = op.combine(acc, op.gather(col[j]));
+    for (; j < j1; j += stride) acc = op.combine(acc, op.gather(load_col<NT>(col, j)));
     return acc;
 }
 
-template <class Op, int L>
+template <class Op, int L, int U, bool NT>
 __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op, int c, int64_t local_block) {
     using T = typename Op::T;
     constexpr int kRowsPerBlock = kBlock / L;
@@ -83,21 +91,29 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
     if (valid) {
         const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
         hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
-        if (!hub && op.active(row)) acc = fold_strided(op, a.col, j0 + sub, j1, L);
+        if (!hub && op.active(row)) acc = fold_strided<Op, U, NT>(op, a.col, j0 + sub, j1, L);
     }
 #pragma unroll
     for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
     if (valid && !hub && sub == 0) op.finalize(row, acc);
 }
 
+// Rows known to have no entries (the degree-sorted suffix): finalise with the identity, no row_ptr.
 template <class Op>
+__device__ __forceinline__ void pull_rows_empty(const PullArgs& a, const Op& op, int64_t local_block) {
+    const int64_t row = a.class_row_begin[kZeroClass] + local_block * kBlock + threadIdx.x;
+    if (row < a.class_row_end[kZeroClass]) op.finalize(row, op.identity());
+}
+
+template <class Op, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
     using T = typename Op::T;
     const int64_t b = (int64_t)blockIdx.x + a.block_offset;
     if (b < a.num_chunks) {
         __shared__ T red[kBlock / kWave];
         const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
-        T acc = op.active(a.chunk_row[b]) ? fold_strided(op, a.col, j0 + threadIdx.x, j1, kBlock) : op.identity();
+        T acc = op.active(a.chunk_row[b]) ? fold_strided<Op, U, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock)
+                                          : op.identity();
 #pragma unroll
         for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
         if (lane_id() == 0) red[wave_id()] = acc;
@@ -116,13 +132,14 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typenam
         if (b >= a.class_block_begin[k + 1]) c = k + 1;
     const int64_t lb = b - a.class_block_begin[c];
     switch (c) {
-        case 1: pull_rows_class<Op, 64>(a, op, c, lb); break;
-        case 2: pull_rows_class<Op, 32>(a, op, c, lb); break;
-        case 3: pull_rows_class<Op, 16>(a, op, c, lb); break;
-        case 4: pull_rows_class<Op, 8>(a, op, c, lb); break;
-        case 5: pull_rows_class<Op, 4>(a, op, c, lb); break;
-        case 6: pull_rows_class<Op, 2>(a, op, c, lb); break;
-        default: pull_rows_class<Op, 1>(a, op, c, lb); break;
+        case 1: pull_rows_class<Op, 64, U, NT>(a, op, c, lb); break;
+        case 2: pull_rows_class<Op, 32, U, NT>(a, op, c, lb); break;
+        case 3: pull_rows_class<Op, 16, U, NT>(a, op, c, lb); break;
+        case 4: pull_rows_class<Op, 8, U, NT>(a, op, c, lb); break;
+        case 5: pull_rows_class<Op, 4, U, NT>(a, op, c, lb); break;
+        case 6: pull_rows_class<Op, 2, U, NT>(a, op, c, lb); break;
+        case 7: pull_rows_class<Op, 1, U, NT>(a, op, c, lb); break;
+        default: pull_rows_empty<Op>(a, op, lb); break;
     }
 }
 
@@ -145,17 +162,27 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     PullArgs a = make_pull_args(csr, plan);
     const int64_t blocks = plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
+    auto launch = [&](unsigned grid) {
+        const int u = tune().pull_unroll;
+        const bool nt = tune().pull_nt != 0;
+        if (u >= 8) {
+            if (nt) pull_kernel<Op, 8, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+            else pull_kernel<Op, 8, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+        } else {
+            if (nt) pull_kernel<Op, 4, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+            else pull_kernel<Op, 4, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+        }
+        JG_LAUNCH_CHECK();
+    };
     if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
         for (int c = 0; c < kNumClasses; ++c) {
             const int64_t b0 = plan.class_block_begin[c], b1 = plan.class_block_begin[c + 1];
             if (b1 <= b0) continue;
             a.block_offset = b0;
-            pull_kernel<Op><<<(unsigned)(b1 - b0), kBlock, 0, s>>>(a, op, hub_partial);
-            JG_LAUNCH_CHECK();
+            launch((unsigned)(b1 - b0));
         }
     } else if (blocks > 0) {
-        pull_kernel<Op><<<(unsigned)blocks, kBlock, 0, s>>>(a, op, hub_partial);
-        JG_LAUNCH_CHECK();
+        launch((unsigned)blocks);
     }
     if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
     if (plan.num_hub_rows > 0) {
