@@ -1,0 +1,111 @@
+/*
+ * janusgpu_jni.c — JNI shim between org.janusgraph.graphdb.olap.gpu.JanusGpu and libjanusgpu's
+ * C-ABI (include/janusgpu.h).  Pure pass-through: direct ByteBuffers are handed to the library as
+ * raw pointers (no copies), statuses are returned unchanged.
+ *
+ * Build (needs a JDK; none is installed in the build container):
+ *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
+ *       janusgpu_jni.c -L../../janusgraph_amd -ljanusgpu -Wl,-rpath,'$ORIGIN' -o libjanusgpu_jni.so
+ */
+#include <jni.h>
+#include <stddef.h>
+
+#include "janusgpu.h"
+
+#define FN(name) Java_org_janusgraph_graphdb_olap_gpu_JanusGpu_##name
+
+static void* buf(JNIEnv* env, jobject b) { return b ? (*env)->GetDirectBufferAddress(env, b) : NULL; }
+
+JNIEXPORT jint JNICALL FN(abiVersion)(JNIEnv* env, jclass c) { (void)env; (void)c; return jg_abi_version(); }
+
+JNIEXPORT jstring JNICALL FN(lastError)(JNIEnv* env, jclass c) {
+    (void)c;
+    return (*env)->NewStringUTF(env, jg_last_error());
+}
+
+JNIEXPORT jint JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jintArray devices, jlongArray out) {
+    (void)c;
+    jsize nd = (*env)->GetArrayLength(env, devices);
+    jint* d = (*env)->GetIntArrayElements(env, devices, NULL);
+    jg_ctx* ctx = NULL;
+    int st = jg_ctx_create((const int*)d, (int)nd, &ctx);
+    (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
+    jlong h = (jlong)(intptr_t)ctx;
+    (*env)->SetLongArrayRegion(env, out, 0, 1, &h);
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(ctxDestroy)(JNIEnv* env, jclass c, jlong ctx) {
+    (void)env; (void)c;
+    return jg_ctx_destroy((jg_ctx*)(intptr_t)ctx);
+}
+
+JNIEXPORT jint JNICALL FN(ctxLastStats)(JNIEnv* env, jclass c, jlong ctx, jdoubleArray out9) {
+    (void)c;
+    jg_stats s;
+    int st = jg_ctx_last_stats((const jg_ctx*)(intptr_t)ctx, &s);
+    if (st == JG_OK) {
+        jdouble v[9] = {s.supersteps, s.levels, s.build_ms, s.compute_ms, s.exchange_ms, s.kernel_ms_total,
+                        (jdouble)s.kernel_launches, s.algorithmic_bytes, s.edges_traversed};
+        (*env)->SetDoubleArrayRegion(env, out9, 0, 9, v);
+    }
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(graphBuild)(JNIEnv* env, jclass c, jlong ctx, jobject vid, jlong n, jobject src, jobject dst,
+                                      jobject weight, jlong m, jint flags, jlongArray out) {
+    (void)c;
+    jg_graph* g = NULL;
+    int st = jg_graph_build((jg_ctx*)(intptr_t)ctx, (const int64_t*)buf(env, vid), n, (const int64_t*)buf(env, src),
+                            (const int64_t*)buf(env, dst), (const int32_t*)buf(env, weight), m, (uint32_t)flags, &g);
+    jlong h = (jlong)(intptr_t)g;
+    (*env)->SetLongArrayRegion(env, out, 0, 1, &h);
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(graphDestroy)(JNIEnv* env, jclass c, jlong g) {
+    (void)env; (void)c;
+    return jg_graph_destroy((jg_graph*)(intptr_t)g);
+}
+
+JNIEXPORT jint JNICALL FN(graphInfo)(JNIEnv* env, jclass c, jlong g, jlongArray out8) {
+    (void)c;
+    jg_graph_info i;
+    int st = jg_graph_info_get((const jg_graph*)(intptr_t)g, &i);
+    if (st == JG_OK) {
+        jlong v[8] = {i.num_vertices, i.num_edges, i.ghost_edges, i.self_loops, i.truncated_vertices,
+                      i.max_in_degree, i.max_out_degree, i.device_bytes};
+        (*env)->SetLongArrayRegion(env, out8, 0, 8, v);
+    }
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(pageRank)(JNIEnv* env, jclass c, jlong g, jdouble damping, jlong vertex_count,
+                                    jint iterations, jobject rank_out, jobject edge_count_out) {
+    (void)c;
+    return jg_pagerank((jg_graph*)(intptr_t)g, damping, vertex_count, iterations, (double*)buf(env, rank_out),
+                       (double*)buf(env, edge_count_out));
+}
+
+JNIEXPORT jint JNICALL FN(shortestDistance)(JNIEnv* env, jclass c, jlong g, jlong seed, jint max_depth,
+                                            jobject dist_out) {
+    (void)c;
+    return jg_shortest_distance((jg_graph*)(intptr_t)g, seed, max_depth, (int64_t*)buf(env, dist_out));
+}
+
+JNIEXPORT jint JNICALL FN(bfs)(JNIEnv* env, jclass c, jlong g, jobject sources, jint nsrc, jint direction,
+                               jint max_depth, jobject depth_out) {
+    (void)c;
+    return jg_bfs((jg_graph*)(intptr_t)g, (const int64_t*)buf(env, sources), nsrc, direction, max_depth,
+                  (int32_t*)buf(env, depth_out));
+}
+
+JNIEXPORT jint JNICALL FN(connectedComponents)(JNIEnv* env, jclass c, jlong g, jobject comp_out,
+                                               jintArray iterations_out) {
+    (void)c;
+    int32_t it = 0;
+    int st = jg_connected_components((jg_graph*)(intptr_t)g, (int64_t*)buf(env, comp_out), &it);
+    jint v = it;
+    (*env)->SetIntArrayRegion(env, iterations_out, 0, 1, &v);
+    return st;
+}
