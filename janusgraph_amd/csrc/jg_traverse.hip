@@ -26,12 +26,10 @@ namespace jg {
 
 namespace {
 
-constexpr int kTdLanes = 16;
-
-struct Counters {  // device-side level counters
-    unsigned long long next_size;  // vertices discovered this level
-    unsigned long long next_edges; // their push degrees (m_f of the next level)
-};
+constexpr int kTdLanes = 16;         // lanes per frontier vertex in the weighted-SD push
+constexpr int kPackShift = 37;       // packed frontier counter: (vertices << 37) | push edges
+constexpr unsigned long long kEdgeMask = (1ull << kPackShift) - 1ull;
+constexpr int kTdEdgesPerThread = 4;
 
 __device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t* __restrict__ queue,
                                             unsigned long long* __restrict__ size) {
@@ -44,43 +42,76 @@ __device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t* __res
     if (take) queue[base + __popcll(mask & lanemask_lt())] = v;
 }
 
+// Append v (push degree deg) to a frontier queue whose entries also carry their first edge offset.
+// One packed 64-bit atomicAdd per wave reserves both the queue slots and the edge range, so queue
+// positions and edge offsets grow together (the offsets are monotone: top-down binary-searches them).
+// Must be reached by all 64 lanes (wave-uniform call sites).
+__device__ __forceinline__ void wave_append_frontier(bool take, int32_t v, int64_t deg, int32_t* __restrict__ queue,
+                                                     int64_t* __restrict__ qoff,
+                                                     unsigned long long* __restrict__ packed) {
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int64_t d = take ? deg : 0;
+    const int64_t dinc = wave_inclusive_scan_add(d);
+    const int64_t dtot = __shfl(dinc, kWave - 1, kWave);
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    unsigned long long base = 0;
+    if (lane_id() == leader)
+        base = atomicAdd(packed, ((unsigned long long)__popcll(mask) << kPackShift) | (unsigned long long)dtot);
+    base = __shfl(base, leader, kWave);
+    if (take) {
+        const uint64_t pos = (base >> kPackShift) + (uint64_t)__popcll(mask & lanemask_lt());
+        queue[pos] = v;
+        qoff[pos] = (int64_t)(base & kEdgeMask) + dinc - d;
+    }
+}
+
+// Edge-parallel top-down step: frontier edge e in [0, mf) belongs to the queue entry i with
+// qoff[i] <= e < qoff[i+1]; each thread walks kTdEdgesPerThread consecutive edges after one binary
+// search, so a hub in the frontier is spread over the whole grid.
 __global__ __launch_bounds__(kBlock) void td_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                    const int32_t* __restrict__ queue, int64_t qsize,
+                                                    const int32_t* __restrict__ queue,
+                                                    const int64_t* __restrict__ qoff, int64_t nf, int64_t mf,
                                                     int32_t* __restrict__ depth, int32_t next_depth,
-                                                    int32_t* __restrict__ next_queue, Counters* __restrict__ cnt) {
-    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
-    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
-    const int sub = threadIdx.x % kTdLanes;
-    unsigned long long edges = 0;
-    // all lanes of a wave iterate the same number of times (wave-uniform trip count for ballots)
-    const int64_t iters = (qsize + ngroups - 1) / ngroups;
-    for (int64_t it = 0; it < iters; ++it) {
-        const int64_t qi = group + it * ngroups;
-        const bool have = qi < qsize;
-        const int32_t u = have ? queue[qi] : 0;
-        const int64_t j0 = have ? rp[u] : 0, j1 = have ? rp[u + 1] : 0;
-        int64_t len = j1 - j0;
-        // wave-uniform loop bound: max row length among the wave's groups
-        int64_t maxlen = len;
-#pragma unroll
-        for (int o = kTdLanes; o < kWave; o <<= 1) {
-            const int64_t t = __shfl_xor(maxlen, o, kWave);
-            maxlen = t > maxlen ? t : maxlen;
+                                                    int32_t* __restrict__ next_queue, int64_t* __restrict__ next_qoff,
+                                                    unsigned long long* __restrict__ packed) {
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
+    for (int64_t t = 0; t < tiles; ++t) {
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < mf) {
+            int64_t lo = 0, hi = nf - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < nf ? qoff[i + 1] : mf;
         }
-        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
-            const int64_t k = k0 + sub;
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
             bool won = false;
             int32_t v = 0;
-            if (k < len) {
-                v = col[j0 + k];
-                if (depth[v] < 0) won = atomicCAS(&depth[v], -1, next_depth) == -1;
+            int64_t vdeg = 0;
+            if (e < mf) {
+                while (e >= next_bound) {  // skips zero-degree frontier entries too
+                    ++i;
+                    next_bound = i + 1 < nf ? qoff[i + 1] : mf;
+                }
+                const int32_t u = queue[i];
+                v = col[rp[u] + (e - qoff[i])];
+                if (depth[v] < 0 && atomicCAS(&depth[v], -1, next_depth) == -1) {
+                    won = true;
+                    vdeg = rp[v + 1] - rp[v];
+                }
             }
-            if (won) edges += (unsigned long long)(rp[v + 1] - rp[v]);
-            wave_append(won, v, next_queue, &cnt->next_size);
+            wave_append_frontier(won, v, vdeg, next_queue, next_qoff, packed);
         }
     }
-    edges = wave_reduce_add(edges);
-    if (lane_id() == 0 && edges) atomicAdd(&cnt->next_edges, edges);
 }
 
 __global__ void queue_to_bitmap_kernel(const int32_t* __restrict__ queue, int64_t qsize,
@@ -97,13 +128,14 @@ __global__ __launch_bounds__(kBlock) void bu_kernel(const int64_t* __restrict__ 
                                                     const unsigned long long* __restrict__ frontier,
                                                     int32_t* __restrict__ depth, int64_t rows, int32_t next_depth,
                                                     unsigned long long* __restrict__ next_bm,
-                                                    int32_t* __restrict__ next_queue, Counters* __restrict__ cnt) {
+                                                    int32_t* __restrict__ next_queue, int64_t* __restrict__ next_qoff,
+                                                    unsigned long long* __restrict__ packed) {
     const int64_t words = (rows + 63) / 64;
-    unsigned long long edges = 0;
-    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words;
-         w += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) / kWave;
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words; w += wstride) {
         const int64_t v = w * 64 + lane_id();
         bool found = false;
+        int64_t vdeg = 0;
         if (v < rows && depth[v] < 0) {
             const int64_t j1 = rp[v + 1];
             for (int64_t j = rp[v]; j < j1; ++j) {
@@ -112,26 +144,25 @@ __global__ __launch_bounds__(kBlock) void bu_kernel(const int64_t* __restrict__ 
             }
             if (found) {
                 depth[v] = next_depth;
-                edges += (unsigned long long)(push_rp[v + 1] - push_rp[v]);
+                vdeg = push_rp[v + 1] - push_rp[v];
             }
         }
         const uint64_t word = __ballot(found);
         if (lane_id() == 0) next_bm[w] = word;
-        wave_append(found, (int32_t)v, next_queue, &cnt->next_size);
+        wave_append_frontier(found, (int32_t)v, vdeg, next_queue, next_qoff, packed);
     }
-    edges = wave_reduce_add(edges);
-    if (lane_id() == 0 && edges) atomicAdd(&cnt->next_edges, edges);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-__global__ void set_source_kernel(int32_t* depth, int32_t* queue, int64_t v, const int64_t* rp, Counters* cnt) {
+__global__ void set_source_kernel(int32_t* depth, int32_t* queue, int64_t* qoff, int64_t v, const int64_t* rp,
+                                  unsigned long long* packed) {
     depth[v] = 0;
     queue[0] = (int32_t)v;
-    cnt->next_size = 1;
-    cnt->next_edges = (unsigned long long)(rp[v + 1] - rp[v]);
+    qoff[0] = 0;
+    *packed = (1ull << kPackShift) | (unsigned long long)(rp[v + 1] - rp[v]);
 }
 
 // input edges inside the reached set: sum of row lengths of reached vertices (symmetric: / 2 later)
@@ -283,56 +314,51 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     const Csr* degcsr = push ? push : pull;
     const int64_t words = (rows + 63) / 64;
     DevBuf<int32_t> qa(std::max<int64_t>(rows, 1)), qb(std::max<int64_t>(rows, 1));
+    DevBuf<int64_t> oa(std::max<int64_t>(rows, 1)), ob(std::max<int64_t>(rows, 1));
     DevBuf<unsigned long long> bma(std::max<int64_t>(words, 1)), bmb(std::max<int64_t>(words, 1));
-    DevBuf<Counters> cnt(1);
+    DevBuf<unsigned long long> packed(1);
     fill_i32_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, -1);
     JG_LAUNCH_CHECK();
-    JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(Counters), s));
-    set_source_kernel<<<1, 1, 0, s>>>(depth, qa.get(), source, degcsr->row_ptr.get(), cnt.get());
+    set_source_kernel<<<1, 1, 0, s>>>(depth, qa.get(), oa.get(), source, degcsr->row_ptr.get(), packed.get());
     JG_LAUNCH_CHECK();
-    Counters h{1, 0};
-    JG_HIP(hipMemcpyAsync(&h, cnt.get(), sizeof h, hipMemcpyDeviceToHost, s));
-    JG_HIP(hipStreamSynchronize(s));
-    int64_t nf = 1, mf = (int64_t)h.next_edges;
+    unsigned long long h = 0;
+    copy_d2h(&h, packed.get(), sizeof h, s);
+    int64_t nf = (int64_t)(h >> kPackShift), mf = (int64_t)(h & kEdgeMask);
     int64_t mu = degcsr->nnz - mf;
     bool bottom_up = false;
-    bool queue_valid = true;  // qa holds the frontier as a queue
     const double alpha = 14.0, beta = 24.0;
     int level = 0;
     while (nf > 0 && (max_depth < 0 || level < max_depth)) {
         // direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the
         // unexplored edges / alpha, back top-down when the frontier shrinks below n / beta
-        if (!bottom_up && pull && (!push || (double)mf > (double)mu / alpha)) bottom_up = true;
-        else if (bottom_up && push && (double)nf < (double)rows / beta) bottom_up = false;
-        JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(Counters), s));
+        if (!bottom_up && pull && (!push || (double)mf > (double)mu / alpha)) {
+            bottom_up = true;
+            JG_HIP(hipMemsetAsync(bma.get(), 0, words * sizeof(unsigned long long), s));  // queue -> bitmap
+            queue_to_bitmap_kernel<<<grid_for(nf), kBlock, 0, s>>>(qa.get(), nf, bma.get());
+            JG_LAUNCH_CHECK();
+        } else if (bottom_up && push && (double)nf < (double)rows / beta) {
+            bottom_up = false;  // the queue is always valid: both steps append to it
+        }
+        JG_HIP(hipMemsetAsync(packed.get(), 0, sizeof(unsigned long long), s));
         const int next_depth = level + 1;
+        if (prof_enabled(ctx)) prof_record_start(ctx, sh);
         if (bottom_up) {
-            if (queue_valid) {  // frontier queue -> bitmap
-                JG_HIP(hipMemsetAsync(bma.get(), 0, words * sizeof(unsigned long long), s));
-                queue_to_bitmap_kernel<<<grid_for(nf), kBlock, 0, s>>>(qa.get(), nf, bma.get());
-                JG_LAUNCH_CHECK();
-            }
-            if (prof_enabled(ctx)) prof_record_start(ctx, sh);
             bu_kernel<<<grid_for(words * kWave, kBlock, 256 * 8), kBlock, 0, s>>>(
                 pull->row_ptr.get(), pull->col.get(), degcsr->row_ptr.get(), bma.get(), depth, rows, next_depth,
-                bmb.get(), qb.get(), cnt.get());
-            JG_LAUNCH_CHECK();
-            if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
+                bmb.get(), qb.get(), ob.get(), packed.get());
             bma.swap(bmb);
-            queue_valid = true;  // bu also appended the new frontier to qb
-        } else {
-            if (prof_enabled(ctx)) prof_record_start(ctx, sh);
-            td_kernel<<<grid_for(nf * kTdLanes, kBlock, 256 * 8), kBlock, 0, s>>>(
-                push->row_ptr.get(), push->col.get(), qa.get(), nf, depth, next_depth, qb.get(), cnt.get());
-            JG_LAUNCH_CHECK();
-            if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
-            queue_valid = true;
+        } else if (mf > 0) {
+            td_kernel<<<grid_for((mf + kTdEdgesPerThread - 1) / kTdEdgesPerThread, kBlock, 256 * 8), kBlock, 0, s>>>(
+                push->row_ptr.get(), push->col.get(), qa.get(), oa.get(), nf, mf, depth, next_depth, qb.get(),
+                ob.get(), packed.get());
         }
+        JG_LAUNCH_CHECK();
+        if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
         qa.swap(qb);
-        JG_HIP(hipMemcpyAsync(&h, cnt.get(), sizeof h, hipMemcpyDeviceToHost, s));
-        JG_HIP(hipStreamSynchronize(s));
-        nf = (int64_t)h.next_size;
-        mf = (int64_t)h.next_edges;
+        oa.swap(ob);
+        copy_d2h(&h, packed.get(), sizeof h, s);
+        nf = (int64_t)(h >> kPackShift);
+        mf = (int64_t)(h & kEdgeMask);
         mu -= mf;
         ++level;
     }
