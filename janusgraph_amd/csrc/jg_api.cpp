@@ -186,6 +186,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().pull_unroll = (int)value;
     } else if (k == "pull_nt") {
         jg::tune().pull_nt = value != 0;
+    } else if (k == "pull_split") {
+        jg::tune().pull_split = value != 0;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }

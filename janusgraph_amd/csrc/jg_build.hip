@@ -307,6 +307,46 @@ __global__ void gather_row_bounds_kernel(const int64_t* __restrict__ rp, const i
     }
 }
 
+// ---------------- XCD split of the heavy rows ----------------
+__global__ void col_hist_kernel(const int32_t* __restrict__ col, int64_t n, int32_t* __restrict__ hist) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&hist[col[j]], 1);
+}
+
+// bounds[q] = first column g with prefix[g] >= q * total / 8 (q = 1..7)
+__global__ void col_bound_kernel(const int64_t* __restrict__ prefix, int64_t len, int64_t* __restrict__ bounds) {
+    const int q = threadIdx.x + 1;
+    if (q >= kXcds) return;
+    const int64_t total = prefix[len];
+    const int64_t target = total / kXcds * q + (total % kXcds) * q / kXcds;
+    int64_t lo = 0, hi = len;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (prefix[mid] < target) lo = mid + 1; else hi = mid;
+    }
+    bounds[q] = lo;
+}
+
+// split_off[r*8+q] = first entry of row r with col >= bounds[q], relative to row_ptr[r] (cols sorted)
+__global__ void split_off_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t heavy,
+                                 const int64_t* __restrict__ bounds, uint32_t* __restrict__ split_off) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < heavy * kXcds;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / kXcds;
+        const int q = (int)(i % kXcds);
+        const int64_t b = rp[r], e = rp[r + 1];
+        int64_t lo = b, hi = e;
+        if (q > 0) {
+            const int64_t target = bounds[q];
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((int64_t)col[mid] < target) lo = mid + 1; else hi = mid;
+            }
+        }
+        split_off[i] = (uint32_t)(lo - b);
+    }
+}
+
 int64_t select_keys(const SelectArgs& a, DevBuf<uint64_t>& keys, DevBuf<uint32_t>& eidx, bool want_eidx,
                     hipStream_t s) {
     const int64_t nb = std::max<int64_t>(1, (a.m + kSelTile - 1) / kSelTile);
@@ -378,7 +418,82 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     JG_HIP(hipStreamSynchronize(s));
 }
 
-void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
+// Tasks of the XCD split (shared by the 8 column ranges): a hub row alone (block-wide fold), or up to
+// 256/L consecutive heavy rows folded with L lanes each, L chosen from the per-range length ~deg/8.
+static void build_split_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t heavy) {
+    hipStream_t s = sh.stream;
+    plan.split_rows = 0;
+    plan.split_tasks = 0;
+    if (heavy <= 0) return;
+    std::vector<int64_t> rp(heavy + 1);
+    copy_d2h(rp.data(), csr.row_ptr.get(), (heavy + 1) * sizeof(int64_t), s);
+    plan.split_rows = heavy;
+    // tasks
+    std::vector<int32_t> trow, tmeta;
+    int64_t r = 0;
+    while (r < heavy) {
+        const int64_t d = rp[r + 1] - rp[r];
+        if (d >= kHubDegree) {
+            trow.push_back((int32_t)r);
+            tmeta.push_back(0 | (1 << 8));
+            ++r;
+            continue;
+        }
+        const int64_t per = d / kXcds;
+        const int lanes = per >= 256 ? 64 : per >= 128 ? 32 : per >= 64 ? 16 : per >= 32 ? 8 : per >= 16 ? 4 : 2;
+        const int64_t maxrows = kBlock / lanes;
+        int64_t k = 0;
+        while (k < maxrows && r + k < heavy) {
+            const int64_t dk = rp[r + k + 1] - rp[r + k];
+            const int64_t pk = dk / kXcds;
+            const int lk = dk >= kHubDegree ? 0
+                           : pk >= 256 ? 64 : pk >= 128 ? 32 : pk >= 64 ? 16 : pk >= 32 ? 8 : pk >= 16 ? 4 : 2;
+            if (lk != lanes) break;
+            ++k;
+        }
+        trow.push_back((int32_t)r);
+        tmeta.push_back(lanes | (int32_t)(k << 8));
+        r += k;
+    }
+    plan.split_tasks = (int64_t)trow.size();
+    plan.task_row.alloc(trow.size());
+    plan.task_meta.alloc(tmeta.size());
+    copy_h2d(plan.task_row.get(), trow.data(), trow.size() * sizeof(int32_t), s);
+    copy_h2d(plan.task_meta.get(), tmeta.data(), tmeta.size() * sizeof(int32_t), s);
+    plan.heads.alloc(kXcds);
+    plan.split_off.alloc(heavy * kXcds);
+}
+
+// Column bounds + per-row range offsets of the XCD split (needs the column space length).
+static void build_split_bounds(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
+    hipStream_t s = sh.stream;
+    const int64_t heavy = plan.split_rows;
+    if (heavy <= 0) return;
+    int64_t heavy_nnz = 0;
+    copy_d2h(&heavy_nnz, csr.row_ptr.get() + heavy, sizeof(int64_t), s);
+    DevBuf<int32_t> hist(col_space);
+    DevBuf<int64_t> prefix(col_space + 1);
+    JG_HIP(hipMemsetAsync(hist.get(), 0, hist.bytes(), s));
+    if (heavy_nnz > 0) {
+        col_hist_kernel<<<grid_for(heavy_nnz, kBlock, 4096), kBlock, 0, s>>>(csr.col.get(), heavy_nnz, hist.get());
+        JG_LAUNCH_CHECK();
+    }
+    prim::exclusive_scan(hist.get(), prefix.get(), col_space, s);
+    DevBuf<int64_t> bounds(kXcds + 1);
+    int64_t hb[kXcds + 1];
+    for (int q = 0; q <= kXcds; ++q) hb[q] = q == kXcds ? col_space : 0;
+    copy_h2d(bounds.get(), hb, sizeof hb, s);
+    col_bound_kernel<<<1, kXcds, 0, s>>>(prefix.get(), col_space, bounds.get());
+    JG_LAUNCH_CHECK();
+    copy_d2h(hb, bounds.get(), sizeof hb, s);
+    for (int q = 0; q <= kXcds; ++q) plan.col_bound[q] = hb[q];
+    split_off_kernel<<<grid_for(heavy * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), heavy, bounds.get(),
+                                                                plan.split_off.get());
+    JG_LAUNCH_CHECK();
+    JG_HIP(hipStreamSynchronize(s));
+}
+
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
     hipStream_t s = sh.stream;
     const int64_t rows = csr.rows;
     // hub rows (any position) -> chunk table
@@ -434,21 +549,33 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan) {
     // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
-    int64_t begin = 0;
-    plan.class_row_begin[0] = plan.class_row_end[0] = 0;  // hub class is the chunk table
-    plan.class_block_begin[0] = 0;
-    plan.class_block_begin[1] = plan.num_chunks;
-    for (int c = 1; c < kNumClasses; ++c) {
-        int64_t end = c < kZeroClass - 1 ? (int64_t)fb[c] : c == kZeroClass - 1 ? zero_begin : rows;
-        end = std::min(std::max(end, begin), c < kZeroClass ? zero_begin : rows);
-        end = std::max(end, begin);
-        plan.class_row_begin[c] = begin;
-        plan.class_row_end[c] = end;
-        const int lanes = c == kZeroClass ? 1 : 64 >> (c - 1);
-        const int64_t rows_per_block = kBlock / lanes;
-        plan.class_block_begin[c + 1] = plan.class_block_begin[c] + (end - begin + rows_per_block - 1) / rows_per_block;
-        begin = end;
-    }
+    // the heavy prefix split by XCD: rows before the first row of degree < kSplitMinDegree
+    const int64_t heavy = std::min<int64_t>((int64_t)fb[3], zero_begin);  // c_class_thr[3] == 64
+    static_assert(kSplitMinDegree == 64, "class 3 threshold is the split threshold");
+    auto make_classes = [&](int64_t first_row, int64_t chunks, int64_t* rb, int64_t* re, int64_t* bb) {
+        int64_t begin = first_row;
+        rb[0] = re[0] = 0;  // hub class is the chunk table
+        bb[0] = 0;
+        bb[1] = chunks;
+        for (int c = 1; c < kNumClasses; ++c) {
+            int64_t end = c < kZeroClass - 1 ? (int64_t)fb[c] : c == kZeroClass - 1 ? zero_begin : rows;
+            end = std::min(std::max(end, begin), c < kZeroClass ? zero_begin : rows);
+            end = std::max(end, begin);
+            rb[c] = begin;
+            re[c] = end;
+            const int lanes = c == kZeroClass ? 1 : 64 >> (c - 1);
+            const int64_t rows_per_block = kBlock / lanes;
+            bb[c + 1] = bb[c] + (end - begin + rows_per_block - 1) / rows_per_block;
+            begin = end;
+        }
+    };
+    make_classes(0, plan.num_chunks, plan.class_row_begin, plan.class_row_end, plan.class_block_begin);
+    build_split_plan(sh, csr, plan, heavy);
+    build_split_bounds(sh, csr, plan, col_space);
+    // light part: rows after the heavy prefix (hub rows are all heavy when rows are degree-sorted;
+    // any hub beyond the prefix keeps its chunks, so chunks stay in the light table too)
+    make_classes(plan.split_rows, plan.split_rows > 0 ? plan.num_chunks : plan.num_chunks, plan.light_row_begin,
+                 plan.light_row_end, plan.light_block_begin);
     if (debug_plan()) {
         std::vector<int64_t> rp(rows + 1);
         copy_d2h(rp.data(), csr.row_ptr.get(), (rows + 1) * sizeof(int64_t), s);
@@ -538,7 +665,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         if (g.flags & JG_ADJ_IN) {
             a.which = 0;
             build_csr(sh, a, w, sh.in, s);
-            build_pull_plan(sh, sh.in, sh.plan_in);
+            build_pull_plan(sh, sh.in, sh.plan_in, g.padded_len());
         }
         if (g.flags & JG_ADJ_OUT) {
             a.which = 1;
@@ -547,7 +674,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         if (g.flags & JG_ADJ_BOTH) {
             a.which = 2;
             build_csr(sh, a, nullptr, sh.both, s);
-            build_pull_plan(sh, sh.both, sh.plan_both);
+            build_pull_plan(sh, sh.both, sh.plan_both, g.padded_len());
         }
         JG_HIP(hipStreamSynchronize(s));
         first = false;

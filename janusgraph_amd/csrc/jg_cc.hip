@@ -134,6 +134,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         }
         sh.cc_label.alloc(std::max<int64_t>(sh.rows, 1));
         sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
+        sh.cc_split_partial.alloc(std::max<int64_t>(kXcds * sh.plan_both.split_rows, 1));
         sh.cc_changed.alloc(1);
         std::vector<int32_t> lab0(sh.rows);
         for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
@@ -173,7 +174,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             op.changed = sh.cc_changed.get();
             op.base = (int64_t)sh.index * g.S;
             launch_pull(sh.both, sh.plan_both, op, sh.cc_hub_partial.get(), sh.stream, ctx.profiling ? &ctx : nullptr,
-                        &sh);
+                        &sh, sh.cc_split_partial.get());
         }
         exchange_msg(g, cur ^ 1);
         any = 0;

@@ -47,7 +47,26 @@ struct PullPlan {
     DevBuf<int64_t> chunk_end;    // [num_chunks]
     DevBuf<int64_t> hub_chunk_ptr;  // [num_hub_rows+1] chunks of hub row r: [ptr[r], ptr[r+1])
     int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
+
+    // XCD split of the heavy rows [0, split_rows) (degree >= kSplitMinDegree): the entries of every
+    // heavy row are cut at 8 column bounds (equal-entry quantiles of the heavy part); range q of a
+    // task is folded by a workgroup that runs on XCD q (HW_REG_XCC_ID, per-XCD task queues with
+    // stealing), so each XCD's private 4 MiB L2 caches one eighth of the gathered vector.  Partials
+    // partial[q][row] are combined in q order by pull_split_finalize_kernel.  The light rows keep
+    // the degree classes above (class ranges start at split_rows).
+    int64_t split_rows = 0;
+    int64_t split_tasks = 0;
+    int64_t light_row_begin[kNumClasses] = {};  // the class table of rows [split_rows, rows)
+    int64_t light_row_end[kNumClasses] = {};
+    int64_t light_block_begin[kNumClasses + 1] = {};
+    int64_t col_bound[9] = {};
+    DevBuf<int32_t> task_row;            // first row of each task
+    DevBuf<int32_t> task_meta;           // lanes per row (0: block-wide hub row) | rows << 8
+    DevBuf<uint32_t> split_off;          // [split_rows * 8] start of range q, relative to row_ptr[row]
+    DevBuf<unsigned long long> heads;    // [8] per-XCD queue heads (reset before each launch)
 };
+constexpr int kXcds = 8;
+constexpr int64_t kSplitMinDegree = 64;
 
 struct Ctx;
 
@@ -66,6 +85,8 @@ struct Shard {
     DevBuf<double> pr_contrib[2];  // [P*S] full-length, ping-pong
     DevBuf<double> pr_rank;        // [rows]
     DevBuf<double> pr_hub_partial; // [num_chunks]
+    DevBuf<double> pr_split_partial;  // [8 * plan_in.split_rows]
+    DevBuf<int32_t> cc_split_partial; // [8 * plan_both.split_rows]
     DevBuf<int32_t> cc_msg[2];     // [P*S] label if sent else INT32_MAX
     DevBuf<int32_t> cc_label;      // [rows]
     DevBuf<int32_t> cc_hub_partial;
@@ -123,7 +144,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e);
 void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s);
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
                       int32_t* dsrc, int32_t* ddst, hipStream_t s);
-void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan);
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space);
 
 // ---- exchange (jg_api.cpp) ----
 // In-place allgather of every shard's owned slice [r*S, r*S+S) of a full-length vector.
@@ -150,6 +171,7 @@ bool debug_plan();
 struct Tune {
     int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
+    int pull_split = 1;   // 1: XCD column split of the heavy rows (PullPlan::split_*)
 };
 Tune& tune();
 

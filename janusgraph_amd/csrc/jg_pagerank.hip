@@ -69,6 +69,8 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
         if (sh.pr_rank.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.pr_hub_partial.size() != (size_t)std::max<int64_t>(sh.plan_in.num_chunks, 1))
             sh.pr_hub_partial.alloc(std::max<int64_t>(sh.plan_in.num_chunks, 1));
+        if (sh.pr_split_partial.size() != (size_t)std::max<int64_t>(kXcds * sh.plan_in.split_rows, 1))
+            sh.pr_split_partial.alloc(std::max<int64_t>(kXcds * sh.plan_in.split_rows, 1));
         const double initial = 1.0 / (double)vertex_count;
         if (sh.rows > 0) {
             pr_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.out_degree.get(), sh.rows,
@@ -102,7 +104,7 @@ void pagerank_steps(Graph& g, int nsteps) {
             op.base = (int64_t)sh.index * g.S;
             op.damping = g.pr_damping;
             op.teleport = teleport;
-            launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh);
+            launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get());
         }
         exchange_contrib(g, nxt);
         g.pr_cur = nxt;

@@ -32,9 +32,10 @@ struct PullArgs {
     int64_t class_row_end[kNumClasses];
     int64_t class_block_begin[kNumClasses + 1];
     int64_t block_offset;  // diagnostic split launches (JG_PULL_SPLIT=1): first block of this launch
+    int64_t skip_rows;     // rows [0, skip_rows) are folded by the XCD split: their hub chunks are skipped
 };
 
-inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
+inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = false) {
     PullArgs a;
     a.row_ptr = csr.row_ptr.get();
     a.col = csr.col.get();
@@ -45,11 +46,12 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p) {
     a.num_chunks = p.num_chunks;
     a.num_hub_rows = p.num_hub_rows;
     for (int c = 0; c < kNumClasses; ++c) {
-        a.class_row_begin[c] = p.class_row_begin[c];
-        a.class_row_end[c] = p.class_row_end[c];
+        a.class_row_begin[c] = light ? p.light_row_begin[c] : p.class_row_begin[c];
+        a.class_row_end[c] = light ? p.light_row_end[c] : p.class_row_end[c];
     }
-    for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = p.class_block_begin[c];
+    for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = light ? p.light_block_begin[c] : p.class_block_begin[c];
     a.block_offset = 0;
+    a.skip_rows = light ? p.split_rows : 0;
     return a;
 }
 
@@ -112,8 +114,9 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typenam
     if (b < a.num_chunks) {
         __shared__ T red[kBlock / kWave];
         const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
-        T acc = op.active(a.chunk_row[b]) ? fold_strided<Op, U, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock)
-                                          : op.identity();
+        const int64_t crow = a.chunk_row[b];
+        T acc = (crow >= a.skip_rows && op.active(crow)) ? fold_strided<Op, U, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock)
+                                                         : op.identity();
 #pragma unroll
         for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
         if (lane_id() == 0) red[wave_id()] = acc;
@@ -149,19 +152,151 @@ __global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T
     for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < a.num_hub_rows;
          h += (int64_t)gridDim.x * blockDim.x) {
         const int64_t c0 = a.hub_chunk_ptr[h], c1 = a.hub_chunk_ptr[h + 1];
+        if (a.chunk_row[c0] < a.skip_rows) continue;  // finalised by the XCD split
         T acc = op.identity();
         for (int64_t k = c0; k < c1; ++k) acc = op.combine(acc, hub_partial[k]);
         op.finalize(a.chunk_row[c0], acc);
     }
 }
 
+// ---------------- XCD column split of the heavy rows (PullPlan::split_*) ----------------
+struct SplitArgs {
+    const int64_t* __restrict__ row_ptr;
+    const int32_t* __restrict__ col;
+    const int32_t* __restrict__ task_row;
+    const int32_t* __restrict__ task_meta;
+    const uint32_t* __restrict__ split_off;
+    unsigned long long* __restrict__ heads;
+    int64_t ntasks;
+    int64_t rows;  // heavy rows
+};
+
+// XCD (0..7) the calling workgroup runs on.  Placement is only a speed hint: any XCD may take any
+// range (stealing), results do not depend on it.
+__device__ __forceinline__ int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7u);
+}
+
+__device__ __forceinline__ void split_segment(const SplitArgs& a, int64_t r, int q, int64_t& j0, int64_t& j1) {
+    const int64_t base = a.row_ptr[r];
+    j0 = base + a.split_off[r * kXcds + q];
+    j1 = q == kXcds - 1 ? a.row_ptr[r + 1] : base + a.split_off[r * kXcds + q + 1];
+}
+
+template <class Op, int L, bool NT>
+__device__ __forceinline__ void split_rows_task(const SplitArgs& a, const Op& op, int q, int64_t row0, int nrows,
+                                                typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    const int sub = threadIdx.x % L;
+    const int local = threadIdx.x / L;
+    const int64_t r = row0 + local;
+    const bool valid = local < nrows;
+    T acc = op.identity();
+    if (valid && op.active(r)) {
+        int64_t j0, j1;
+        split_segment(a, r, q, j0, j1);
+        acc = fold_strided<Op, 4, NT>(op, a.col, j0 + sub, j1, L);
+    }
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
+    if (valid && sub == 0) partial[(int64_t)q * a.rows + r] = acc;
+}
+
+template <class Op, bool NT>
+__device__ __forceinline__ void split_hub_task(const SplitArgs& a, const Op& op, int q, int64_t r,
+                                               typename Op::T* __restrict__ partial, typename Op::T* red) {
+    using T = typename Op::T;
+    T acc = op.identity();
+    if (op.active(r)) {
+        int64_t j0, j1;
+        split_segment(a, r, q, j0, j1);
+        acc = fold_strided<Op, 4, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
+    if (lane_id() == 0) red[wave_id()] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = red[0];
+#pragma unroll
+        for (int w = 1; w < kBlock / kWave; ++w) t = op.combine(t, red[w]);
+        partial[(int64_t)q * a.rows + r] = t;
+    }
+}
+
+// Workgroups loop over (task, range) items: their own XCD's queue first, then the others'.  Every
+// item is processed exactly once and written to its own partial slot, so the result is independent
+// of placement and timing.  Every workgroup exits once all eight queues are drained.
+template <class Op, bool NT>
+__global__ __launch_bounds__(kBlock) void pull_split_kernel(SplitArgs a, Op op, typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    __shared__ long long s_task;
+    __shared__ int s_q;
+    __shared__ T red[kBlock / kWave];
+    int q = xcc_id(), tried = 0;  // thread 0's dequeue state
+    for (;;) {
+        if (threadIdx.x == 0) {
+            long long t = -1;
+            while (tried < kXcds) {
+                const unsigned long long k = atomicAdd(&a.heads[q], 1ull);
+                if ((long long)k < a.ntasks) { t = (long long)k; break; }
+                ++tried;
+                q = (q + 1) & (kXcds - 1);
+            }
+            s_task = t;
+            s_q = q;
+        }
+        __syncthreads();
+        const long long t = s_task;
+        const int qq = s_q;
+        __syncthreads();
+        if (t < 0) break;
+        const int64_t row0 = a.task_row[t];
+        const int meta = a.task_meta[t];
+        const int nrows = meta >> 8;
+        switch (meta & 0xff) {
+            case 0: split_hub_task<Op, NT>(a, op, qq, row0, partial, red); __syncthreads(); break;
+            case 64: split_rows_task<Op, 64, NT>(a, op, qq, row0, nrows, partial); break;
+            case 32: split_rows_task<Op, 32, NT>(a, op, qq, row0, nrows, partial); break;
+            case 16: split_rows_task<Op, 16, NT>(a, op, qq, row0, nrows, partial); break;
+            case 8: split_rows_task<Op, 8, NT>(a, op, qq, row0, nrows, partial); break;
+            case 4: split_rows_task<Op, 4, NT>(a, op, qq, row0, nrows, partial); break;
+            default: split_rows_task<Op, 2, NT>(a, op, qq, row0, nrows, partial); break;
+        }
+    }
+}
+
+template <class Op>
+__global__ void pull_split_finalize_kernel(int64_t rows, Op op, const typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+        T acc = partial[r];
+#pragma unroll
+        for (int q = 1; q < kXcds; ++q) acc = op.combine(acc, partial[(int64_t)q * rows + r]);
+        op.finalize(r, acc);
+    }
+}
+
 // Enqueue one pull superstep on `s`.
+// `split_partial` ([8 * plan.split_rows], nullable) enables the XCD split of the heavy rows.
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
-                 Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr) {
-    PullArgs a = make_pull_args(csr, plan);
-    const int64_t blocks = plan.total_blocks();
+                 Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr) {
+    const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
+    PullArgs a = make_pull_args(csr, plan, split);
+    const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
+    if (split) {
+        SplitArgs sa{csr.row_ptr.get(), csr.col.get(), plan.task_row.get(), plan.task_meta.get(),
+                     plan.split_off.get(), plan.heads.get(), plan.split_tasks, plan.split_rows};
+        JG_HIP(hipMemsetAsync(plan.heads.get(), 0, kXcds * sizeof(unsigned long long), s));
+        const unsigned grid = (unsigned)std::min<int64_t>(plan.split_tasks * kXcds, 256 * 8);
+        if (tune().pull_nt) pull_split_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+        else pull_split_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+        JG_LAUNCH_CHECK();
+    }
     auto launch = [&](unsigned grid) {
         const int u = tune().pull_unroll;
         const bool nt = tune().pull_nt != 0;
@@ -176,7 +311,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     };
     if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
         for (int c = 0; c < kNumClasses; ++c) {
-            const int64_t b0 = plan.class_block_begin[c], b1 = plan.class_block_begin[c + 1];
+            const int64_t b0 = a.class_block_begin[c], b1 = a.class_block_begin[c + 1];
             if (b1 <= b0) continue;
             a.block_offset = b0;
             launch((unsigned)(b1 - b0));
@@ -187,6 +322,10 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
     if (plan.num_hub_rows > 0) {
         pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
+        JG_LAUNCH_CHECK();
+    }
+    if (split) {
+        pull_split_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, split_partial);
         JG_LAUNCH_CHECK();
     }
 }

@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--variants", default="4:0,8:0,4:1,8:1")
+    ap.add_argument("--variants", default="4:0:0,4:0:1,4:1:1,8:0:1")
     args = ap.parse_args()
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     ctx = jg.Context((0,))
@@ -33,6 +33,7 @@ def main():
         for v in variants:
             _lib.tune_set("pull_unroll", v[0])
             _lib.tune_set("pull_nt", v[1])
+            _lib.tune_set("pull_split", v[2] if len(v) > 2 else 1)
             g.pagerank_begin(0.85, n)
             g.pagerank_step(2)
             g.sync()
@@ -49,8 +50,9 @@ def main():
     out = {}
     for v in variants:
         t = np.array(times[v])
-        out[f"unroll{v[0]}_nt{v[1]}"] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
-                                         "identical": bool(np.array_equal(ranks[v], base))}
+        out[f"unroll{v[0]}_nt{v[1]}_split{v[2] if len(v) > 2 else 1}"] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
+                                         "identical": bool(np.array_equal(ranks[v], base)),
+                                         "max_rel_vs_first": float(np.max(np.abs(ranks[v] - base) / base))}
     print(json.dumps({"scale": args.scale, "steps": args.steps, "variants": out}))
 
 
