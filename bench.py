@@ -92,6 +92,30 @@ class Control:
             self.dist.destroy_process_group()
 
 
+def pmc_traffic(kernel_tag="PrOp", workload=None):
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
+    (profiles/<round>/summary.json, made by tools/profile_round.sh + tools/pmc_summary.py on the same
+    bench workload).  None when no summary exists."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None, None
+    for rnd in sorted(os.listdir(pdir), reverse=True):
+        path = os.path.join(pdir, rnd, "summary.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            s = json.load(f)
+        if kernel_tag not in s.get("kernel", "") or s.get("traffic_bytes_per_launch") is None:
+            continue
+        bj = os.path.join(pdir, rnd, "bench.json")
+        if workload and os.path.exists(bj):
+            with open(bj) as f:
+                if json.load(f).get("config", {}).get("workload") != workload:
+                    continue
+        return s["traffic_bytes_per_launch"], f"profiles/{rnd}/summary.json ({s.get('read_bytes_method', '')})"
+    return None, None
+
+
 def cpu_baseline(scale, ef, seed, steps):
     """The oracle's PageRank superstep (OpenMP) on the same RMAT graph, rank 0 only."""
     from oracle import oracle as o
@@ -155,9 +179,11 @@ def main():
     if ws == 1:
         alg_bytes_launch = 12.0 * m + 32.0 * n
     achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
+    workload = f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}"
+    traffic, traffic_src = pmc_traffic("PrOp", workload) if ws == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "pull_kernel<PrOp>", "kernel_ms": round(kern_ms, 4),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": "pull superstep (pull_split_kernel + pull_kernel<PrOp>)", "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": alg_bytes_launch}
     del local_nnz
 

@@ -98,6 +98,33 @@ bool debug_plan() {
     return v;
 }
 
+unsigned long long* split_debug_counters() {
+    static unsigned long long* p = nullptr;
+    static bool init = false;
+    if (!init) {
+        init = true;
+        if (env_flag("JG_DEBUG_SPLIT")) {
+            JG_HIP(hipMalloc(reinterpret_cast<void**>(&p), 64 * sizeof(unsigned long long)));
+            JG_HIP(hipMemset(p, 0, 64 * sizeof(unsigned long long)));
+        }
+    }
+    return p;
+}
+
+void split_debug_dump() {
+    unsigned long long* p = split_debug_counters();
+    if (!p) return;
+    unsigned long long h[64];
+    JG_HIP(hipDeviceSynchronize());
+    JG_HIP(hipMemcpy(h, p, sizeof h, hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[jg split] tasks by xcc (rows) x range (cols):\n");
+    for (int x = 0; x < 8; ++x) {
+        std::fprintf(stderr, "[jg split]  xcc %d:", x);
+        for (int q = 0; q < 8; ++q) std::fprintf(stderr, " %8llu", h[x * 8 + q]);
+        std::fprintf(stderr, "\n");
+    }
+}
+
 Tune& tune() {
     static Tune t;
     return t;
@@ -454,6 +481,7 @@ int jg_graph_sync(jg_graph* g) {
         jg::DeviceGuard dg(sp->device);
         JG_HIP(hipStreamSynchronize(sp->stream));
     }
+    jg::split_debug_dump();
     JG_GUARD_END
 }
 

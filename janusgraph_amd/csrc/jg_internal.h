@@ -165,6 +165,9 @@ int allreduce_or(Graph& g, int flag);
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
 bool pull_split_launches();
 bool debug_plan();
+// JG_DEBUG_SPLIT=1: device counters of (XCD, column range) split tasks, printed by jg_graph_sync.
+unsigned long long* split_debug_counters();
+void split_debug_dump();
 
 // Performance knobs (jg_tune_set): variants of the pull kernel selectable at run time so that they
 // can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).

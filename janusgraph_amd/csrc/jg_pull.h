@@ -169,6 +169,7 @@ struct SplitArgs {
     unsigned long long* __restrict__ heads;
     int64_t ntasks;
     int64_t rows;  // heavy rows
+    unsigned long long* __restrict__ dbg;  // JG_DEBUG_SPLIT: [8 xcc][8 ranges] task counts (nullable)
 };
 
 // XCD (0..7) the calling workgroup runs on.  Placement is only a speed hint: any XCD may take any
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(kBlock) void pull_split_kernel(SplitArgs a, Op op, 
         const int qq = s_q;
         __syncthreads();
         if (t < 0) break;
+        if (a.dbg && threadIdx.x == 0) atomicAdd(&a.dbg[xcc_id() * kXcds + qq], 1ull);
         const int64_t row0 = a.task_row[t];
         const int meta = a.task_meta[t];
         const int nrows = meta >> 8;
@@ -290,7 +292,8 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
     if (split) {
         SplitArgs sa{csr.row_ptr.get(), csr.col.get(), plan.task_row.get(), plan.task_meta.get(),
-                     plan.split_off.get(), plan.heads.get(), plan.split_tasks, plan.split_rows};
+                     plan.split_off.get(), plan.heads.get(), plan.split_tasks, plan.split_rows,
+                     split_debug_counters()};
         JG_HIP(hipMemsetAsync(plan.heads.get(), 0, kXcds * sizeof(unsigned long long), s));
         const unsigned grid = (unsigned)std::min<int64_t>(plan.split_tasks * kXcds, 256 * 8);
         if (tune().pull_nt) pull_split_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);

@@ -46,7 +46,7 @@ def main():
         c.update(per_kernel(os.path.join(src, sub), kernel))
     out["counters_per_launch"] = c
     rd = None
-    if "TCC_EA0_RDREQ_sum" in c and ("TCC_EA0_RDREQ_128B_sum" in c or "TCC_EA0_RDREQ_32B_sum" in c):
+    if "TCC_EA0_RDREQ_sum" in c and "TCC_EA0_RDREQ_128B_sum" in c:
         n = c["TCC_EA0_RDREQ_sum"]
         n32 = c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
         n128 = c.get("TCC_EA0_RDREQ_128B_sum", 0.0)
