@@ -214,7 +214,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "pull_nt") {
         jg::tune().pull_nt = value != 0;
     } else if (k == "pull_split") {
-        jg::tune().pull_split = value != 0;
+        JG_ARG(value >= 0 && value <= 2, "pull_split must be 0 (off), 1 (per-XCD queues) or 2 (static)");
+        jg::tune().pull_split = (int)value;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }

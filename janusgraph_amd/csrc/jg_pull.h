@@ -270,6 +270,32 @@ __global__ __launch_bounds__(kBlock) void pull_split_kernel(SplitArgs a, Op op, 
     }
 }
 
+// Static variant: block b folds range (b mod 8) of task (b div 8).  The dispatcher deals blocks
+// round-robin over the XCDs, so the blocks of one range share an XCD (speed only; any placement gives
+// the same result).  No queue atomics.
+template <class Op, bool NT>
+__global__ __launch_bounds__(kBlock) void pull_split_static_kernel(SplitArgs a, Op op,
+                                                                   typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    __shared__ T red[kBlock / kWave];
+    const int64_t b = blockIdx.x;
+    const int qq = (int)(b & (kXcds - 1));
+    const int64_t t = b >> 3;
+    if (a.dbg && threadIdx.x == 0) atomicAdd(&a.dbg[xcc_id() * kXcds + qq], 1ull);
+    const int64_t row0 = a.task_row[t];
+    const int meta = a.task_meta[t];
+    const int nrows = meta >> 8;
+    switch (meta & 0xff) {
+        case 0: split_hub_task<Op, NT>(a, op, qq, row0, partial, red); break;
+        case 64: split_rows_task<Op, 64, NT>(a, op, qq, row0, nrows, partial); break;
+        case 32: split_rows_task<Op, 32, NT>(a, op, qq, row0, nrows, partial); break;
+        case 16: split_rows_task<Op, 16, NT>(a, op, qq, row0, nrows, partial); break;
+        case 8: split_rows_task<Op, 8, NT>(a, op, qq, row0, nrows, partial); break;
+        case 4: split_rows_task<Op, 4, NT>(a, op, qq, row0, nrows, partial); break;
+        default: split_rows_task<Op, 2, NT>(a, op, qq, row0, nrows, partial); break;
+    }
+}
+
 template <class Op>
 __global__ void pull_split_finalize_kernel(int64_t rows, Op op, const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
@@ -294,10 +320,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         SplitArgs sa{csr.row_ptr.get(), csr.col.get(), plan.task_row.get(), plan.task_meta.get(),
                      plan.split_off.get(), plan.heads.get(), plan.split_tasks, plan.split_rows,
                      split_debug_counters()};
-        JG_HIP(hipMemsetAsync(plan.heads.get(), 0, kXcds * sizeof(unsigned long long), s));
-        const unsigned grid = (unsigned)std::min<int64_t>(plan.split_tasks * kXcds, 256 * 8);
-        if (tune().pull_nt) pull_split_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
-        else pull_split_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+        if (tune().pull_split == 2) {  // static blockIdx -> range mapping
+            const unsigned grid = (unsigned)(plan.split_tasks * kXcds);
+            if (tune().pull_nt) pull_split_static_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+            else pull_split_static_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+        } else {  // per-XCD dynamic queues
+            JG_HIP(hipMemsetAsync(plan.heads.get(), 0, kXcds * sizeof(unsigned long long), s));
+            const unsigned grid = (unsigned)std::min<int64_t>(plan.split_tasks * kXcds, 256 * 8);
+            if (tune().pull_nt) pull_split_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+            else pull_split_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
+        }
         JG_LAUNCH_CHECK();
     }
     auto launch = [&](unsigned grid) {
