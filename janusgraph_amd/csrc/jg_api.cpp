@@ -213,6 +213,9 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().pull_unroll = (int)value;
     } else if (k == "pull_nt") {
         jg::tune().pull_nt = value != 0;
+    } else if (k == "split_min_degree") {
+        JG_ARG(value >= 8, "split_min_degree must be >= 8");
+        jg::tune().split_min_degree = value;
     } else if (k == "pull_split") {
         JG_ARG(value >= 0 && value <= 2, "pull_split must be 0 (off), 1 (per-XCD queues) or 2 (static)");
         jg::tune().pull_split = (int)value;

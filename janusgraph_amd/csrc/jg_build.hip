@@ -289,13 +289,15 @@ __constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 1
 // first_below[kZeroClass] = 1 + last row with any entry (rows after it are all empty)
 __global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
                                    unsigned long long* __restrict__ first_below /* [kNumClasses] */,
-                                   unsigned long long* __restrict__ last_nonempty) {
+                                   unsigned long long* __restrict__ last_nonempty, int64_t split_thr,
+                                   unsigned long long* __restrict__ first_below_split) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = rp[l + 1] - rp[l];
 #pragma unroll
         for (int c = 1; c < kNumClasses - 2; ++c)
             if (d < c_class_thr[c]) atomicMin(&first_below[c], (unsigned long long)l);
         if (d > 0) atomicMax(last_nonempty, (unsigned long long)(l + 1));
+        if (d < split_thr) atomicMin(first_below_split, (unsigned long long)l);
     }
 }
 
@@ -535,23 +537,25 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     upload(plan.chunk_end, cend);
     upload(plan.hub_chunk_ptr, hptr);
     // class boundaries: first row whose degree falls below each class threshold
-    unsigned long long fb[kNumClasses + 1];
+    unsigned long long fb[kNumClasses + 2];
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
-    fb[kNumClasses] = 0;  // 1 + last non-empty row
+    fb[kNumClasses] = 0;                                 // 1 + last non-empty row
+    fb[kNumClasses + 1] = (unsigned long long)rows;      // first row below the split threshold
+    const int64_t split_thr = std::max<int64_t>(tune().split_min_degree, kXcds);
     if (rows > 0) {
-        DevBuf<unsigned long long> d_fb(kNumClasses + 1);
+        DevBuf<unsigned long long> d_fb(kNumClasses + 2);
         copy_h2d(d_fb.get(), fb, sizeof fb, s);
         class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get(),
-                                                             d_fb.get() + kNumClasses);
+                                                             d_fb.get() + kNumClasses, split_thr,
+                                                             d_fb.get() + kNumClasses + 1);
         JG_LAUNCH_CHECK();
         copy_d2h(fb, d_fb.get(), sizeof fb, s);
     }
     // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
-    // the heavy prefix split by XCD: rows before the first row of degree < kSplitMinDegree
-    const int64_t heavy = std::min<int64_t>((int64_t)fb[3], zero_begin);  // c_class_thr[3] == 64
-    static_assert(kSplitMinDegree == 64, "class 3 threshold is the split threshold");
+    // the heavy prefix split by XCD: rows before the first row of degree < split_min_degree
+    const int64_t heavy = std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin);
     auto make_classes = [&](int64_t first_row, int64_t chunks, int64_t* rb, int64_t* re, int64_t* bb) {
         int64_t begin = first_row;
         rb[0] = re[0] = 0;  // hub class is the chunk table

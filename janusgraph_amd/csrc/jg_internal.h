@@ -66,7 +66,6 @@ struct PullPlan {
     DevBuf<unsigned long long> heads;    // [8] per-XCD queue heads (reset before each launch)
 };
 constexpr int kXcds = 8;
-constexpr int64_t kSplitMinDegree = 64;
 
 struct Ctx;
 
@@ -174,7 +173,8 @@ void split_debug_dump();
 struct Tune {
     int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
-    int pull_split = 1;   // 1: XCD column split of the heavy rows (PullPlan::split_*)
+    int pull_split = 1;   // XCD column split of the heavy rows: 0 off, 1 per-XCD queues, 2 static map
+    int64_t split_min_degree = 2048;  // build time: rows of at least this degree are split
 };
 Tune& tune();
 
