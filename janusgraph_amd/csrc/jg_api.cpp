@@ -130,6 +130,15 @@ Tune& tune() {
     return t;
 }
 
+int device_cu_count() {
+    static int cache[64] = {0};
+    int dev = 0;
+    JG_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) JG_HIP(hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev));
+    return cache[dev];
+}
+
 void prof_record_start(Ctx& c, Shard& sh) {
     if (!c.profiling) return;
     hipEvent_t e;
@@ -213,6 +222,9 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().pull_unroll = (int)value;
     } else if (k == "pull_nt") {
         jg::tune().pull_nt = value != 0;
+    } else if (k == "pull_lds") {
+        JG_ARG(value >= 0, "pull_lds must be >= 0");
+        jg::tune().pull_lds = value;
     } else if (k == "split_min_degree") {
         JG_ARG(value >= 8, "split_min_degree must be >= 8");
         jg::tune().split_min_degree = value;

@@ -497,6 +497,7 @@ static void build_split_bounds(Shard& sh, const Csr& csr, PullPlan& plan, int64_
 
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
     hipStream_t s = sh.stream;
+    plan.lds_ok = col_space == csr.rows;  // one shard: the hot prefix of the gathered vector is [0, hot)
     const int64_t rows = csr.rows;
     // hub rows (any position) -> chunk table
     std::vector<int64_t> hubs, bounds;

@@ -31,6 +31,7 @@ struct CcOp {
     __device__ __forceinline__ int32_t identity() const { return INT_MAX; }
     __device__ __forceinline__ int32_t combine(int32_t a, int32_t b) const { return a < b ? a : b; }
     __device__ __forceinline__ int32_t gather(int32_t c) const { return msg[c]; }
+    __device__ __forceinline__ const int32_t* vec() const { return msg; }
     __device__ __forceinline__ int32_t shfl_xor(int32_t v, int o) const { return __shfl_xor(v, o, kWave); }
     __device__ __forceinline__ bool active(int64_t) const { return true; }
     __device__ __forceinline__ void finalize(int64_t row, int32_t m) const {

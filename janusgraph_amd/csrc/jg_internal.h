@@ -64,6 +64,7 @@ struct PullPlan {
     DevBuf<int32_t> task_meta;           // lanes per row (0: block-wide hub row) | rows << 8
     DevBuf<uint32_t> split_off;          // [split_rows * 8] start of range q, relative to row_ptr[row]
     DevBuf<unsigned long long> heads;    // [8] per-XCD queue heads (reset before each launch)
+    bool lds_ok = false;  // the gathered vector's hot prefix is [0, hot) (single shard)
 };
 constexpr int kXcds = 8;
 
@@ -175,8 +176,10 @@ struct Tune {
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
     int pull_split = 1;   // XCD column split of the heavy rows: 0 off, 1 per-XCD queues, 2 static map
     int64_t split_min_degree = 2048;  // build time: rows of at least this degree are split
+    int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
 };
 Tune& tune();
+int device_cu_count();  // compute units of the current device
 
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);

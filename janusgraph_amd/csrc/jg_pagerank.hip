@@ -28,6 +28,7 @@ struct PrOp {
     __device__ __forceinline__ double identity() const { return 0.0; }
     __device__ __forceinline__ double combine(double a, double b) const { return __dadd_rn(a, b); }
     __device__ __forceinline__ double gather(int32_t c) const { return x[c]; }
+    __device__ __forceinline__ const double* vec() const { return x; }
     __device__ __forceinline__ double shfl_xor(double v, int o) const { return __shfl_xor(v, o, kWave); }
     __device__ __forceinline__ bool active(int64_t) const { return true; }
     __device__ __forceinline__ void finalize(int64_t row, double s) const {

@@ -61,10 +61,25 @@ __device__ __forceinline__ int32_t load_col(const int32_t* __restrict__ col, int
     else return col[j];
 }
 
+// How a fold reads the gathered vector: straight from global memory, or from an LDS copy of its
+// hottest prefix (the degree-sorted first `hot` ids) with global memory for the rest.
+template <class Op>
+struct GlobalGather {
+    const Op& op;
+    __device__ __forceinline__ typename Op::T operator()(int32_t c) const { return op.gather(c); }
+};
+template <class Op>
+struct LdsGather {
+    const Op& op;
+    const typename Op::T* lds;
+    int32_t hot;
+    __device__ __forceinline__ typename Op::T operator()(int32_t c) const { return c < hot ? lds[c] : op.gather(c); }
+};
+
 // Fold col[j..j1) with stride `stride`; U gathers in flight per lane, folded in index order.
-template <class Op, int U, bool NT>
-__device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
-                                                       int64_t j1, int stride) {
+template <class Op, int U, bool NT, class G>
+__device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& gather, const int32_t* __restrict__ col,
+                                                       int64_t j, int64_t j1, int stride) {
     using T = typename Op::T;
     T acc = op.identity();
     for (; j + (U - 1) * (int64_t)stride < j1; j += U * (int64_t)stride) {
@@ -73,27 +88,35 @@ __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32
 #pragma unroll
         for (int u = 0; u < U; ++u) c[u] = load_col<NT>(col, j + u * (int64_t)stride);
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = op.gather(c[u]);
+        for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) acc = op.combine(acc, v[u]);
     }
-    for (; j < j1; j += stride) acc = op.combine(acc, op.gather(load_col<NT>(col, j)));
+    for (; j < j1; j += stride) acc = op.combine(acc, gather(load_col<NT>(col, j)));
     return acc;
 }
 
-template <class Op, int L, int U, bool NT>
-__device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op, int c, int64_t local_block) {
+template <class Op, int U, bool NT>
+__device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
+                                                       int64_t j1, int stride) {
+    return fold_strided<Op, U, NT>(op, GlobalGather<Op>{op}, col, j, j1, stride);
+}
+
+// `tid` is the thread's index inside its (virtual) 256-thread block.
+template <class Op, int L, int U, bool NT, class G>
+__device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op, const G& gather, int c,
+                                                int64_t local_block, int tid) {
     using T = typename Op::T;
     constexpr int kRowsPerBlock = kBlock / L;
-    const int sub = threadIdx.x % L;
-    const int64_t row = a.class_row_begin[c] + local_block * kRowsPerBlock + threadIdx.x / L;
+    const int sub = tid % L;
+    const int64_t row = a.class_row_begin[c] + local_block * kRowsPerBlock + tid / L;
     const bool valid = row < a.class_row_end[c];
     T acc = op.identity();
     bool hub = false;
     if (valid) {
         const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
         hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
-        if (!hub && op.active(row)) acc = fold_strided<Op, U, NT>(op, a.col, j0 + sub, j1, L);
+        if (!hub && op.active(row)) acc = fold_strided<Op, U, NT>(op, gather, a.col, j0 + sub, j1, L);
     }
 #pragma unroll
     for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
@@ -102,9 +125,29 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
 
 // Rows known to have no entries (the degree-sorted suffix): finalise with the identity, no row_ptr.
 template <class Op>
-__device__ __forceinline__ void pull_rows_empty(const PullArgs& a, const Op& op, int64_t local_block) {
-    const int64_t row = a.class_row_begin[kZeroClass] + local_block * kBlock + threadIdx.x;
+__device__ __forceinline__ void pull_rows_empty(const PullArgs& a, const Op& op, int64_t local_block, int tid) {
+    const int64_t row = a.class_row_begin[kZeroClass] + local_block * kBlock + tid;
     if (row < a.class_row_end[kZeroClass]) op.finalize(row, op.identity());
+}
+
+// Class dispatch of (virtual) block b >= num_chunks.
+template <class Op, int U, bool NT, class G>
+__device__ __forceinline__ void pull_block_rows(const PullArgs& a, const Op& op, const G& gather, int64_t b, int tid) {
+    int c = 1;
+#pragma unroll
+    for (int k = 1; k < kNumClasses; ++k)
+        if (b >= a.class_block_begin[k + 1]) c = k + 1;
+    const int64_t lb = b - a.class_block_begin[c];
+    switch (c) {
+        case 1: pull_rows_class<Op, 64, U, NT>(a, op, gather, c, lb, tid); break;
+        case 2: pull_rows_class<Op, 32, U, NT>(a, op, gather, c, lb, tid); break;
+        case 3: pull_rows_class<Op, 16, U, NT>(a, op, gather, c, lb, tid); break;
+        case 4: pull_rows_class<Op, 8, U, NT>(a, op, gather, c, lb, tid); break;
+        case 5: pull_rows_class<Op, 4, U, NT>(a, op, gather, c, lb, tid); break;
+        case 6: pull_rows_class<Op, 2, U, NT>(a, op, gather, c, lb, tid); break;
+        case 7: pull_rows_class<Op, 1, U, NT>(a, op, gather, c, lb, tid); break;
+        default: pull_rows_empty<Op>(a, op, lb, tid); break;
+    }
 }
 
 template <class Op, int U, bool NT>
@@ -129,21 +172,31 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typenam
         }
         return;
     }
-    int c = 1;
-#pragma unroll
-    for (int k = 1; k < kNumClasses; ++k)
-        if (b >= a.class_block_begin[k + 1]) c = k + 1;
-    const int64_t lb = b - a.class_block_begin[c];
-    switch (c) {
-        case 1: pull_rows_class<Op, 64, U, NT>(a, op, c, lb); break;
-        case 2: pull_rows_class<Op, 32, U, NT>(a, op, c, lb); break;
-        case 3: pull_rows_class<Op, 16, U, NT>(a, op, c, lb); break;
-        case 4: pull_rows_class<Op, 8, U, NT>(a, op, c, lb); break;
-        case 5: pull_rows_class<Op, 4, U, NT>(a, op, c, lb); break;
-        case 6: pull_rows_class<Op, 2, U, NT>(a, op, c, lb); break;
-        case 7: pull_rows_class<Op, 1, U, NT>(a, op, c, lb); break;
-        default: pull_rows_empty<Op>(a, op, lb); break;
-    }
+    pull_block_rows<Op, U, NT>(a, op, GlobalGather<Op>{op}, b, (int)threadIdx.x);
+}
+
+// LDS-cached variant (persistent, 1024 threads = 4 virtual 256-thread blocks, one workgroup per
+// CU): the gathered vector's hottest prefix [0, hot) — the highest-degree vertices after the
+// degree-sorted relabel — is staged once per superstep into LDS (up to 160 KiB), so those gathers
+// never become L2 requests (the pull superstep is bound by L2 request rate, not bytes:
+// tools/pr_locality.py).  Virtual blocks >= num_chunks are dealt round-robin; hub chunks stay with
+// pull_kernel.  No block-wide barrier after the staging one, so the four virtual blocks run freely.
+constexpr int kLdsThreads = 1024;
+template <class Op, int U, bool NT>
+__global__ __launch_bounds__(kLdsThreads) void pull_lds_kernel(PullArgs a, Op op, int32_t hot) {
+    using T = typename Op::T;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    T* lds = reinterpret_cast<T*>(lds_raw);
+    const T* src = op.vec();
+    for (int i = threadIdx.x; i < hot; i += kLdsThreads) lds[i] = src[i];
+    __syncthreads();
+    const LdsGather<Op> gather{op, lds, hot};
+    constexpr int kVirt = kLdsThreads / kBlock;
+    const int tid = threadIdx.x % kBlock;
+    const int64_t last = a.class_block_begin[kNumClasses];
+    for (int64_t b = a.class_block_begin[1] + (int64_t)blockIdx.x * kVirt + threadIdx.x / kBlock; b < last;
+         b += (int64_t)gridDim.x * kVirt)
+        pull_block_rows<Op, U, NT>(a, op, gather, b, tid);
 }
 
 template <class Op>
@@ -309,10 +362,13 @@ __global__ void pull_split_finalize_kernel(int64_t rows, Op op, const typename O
 
 // Enqueue one pull superstep on `s`.
 // `split_partial` ([8 * plan.split_rows], nullable) enables the XCD split of the heavy rows.
+constexpr int64_t kMaxLdsBytes = 160 * 1024;
+
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
                  Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr) {
-    const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
+    using T = typename Op::T;
+    const bool split = tune().pull_split && tune().pull_lds == 0 && plan.split_rows > 0 && split_partial != nullptr;
     PullArgs a = make_pull_args(csr, plan, split);
     const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
@@ -331,6 +387,40 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             else pull_split_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
         }
         JG_LAUNCH_CHECK();
+    }
+    if (!split && tune().pull_lds > 0 && plan.lds_ok) {  // LDS-cached hot prefix (single shard)
+        const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
+        if (plan.num_chunks > 0) {  // hub chunks keep the 256-thread kernel (block-wide reductions)
+            if (tune().pull_nt) pull_kernel<Op, 4, true><<<(unsigned)plan.num_chunks, kBlock, 0, s>>>(a, op, hub_partial);
+            else pull_kernel<Op, 4, false><<<(unsigned)plan.num_chunks, kBlock, 0, s>>>(a, op, hub_partial);
+            JG_LAUNCH_CHECK();
+        }
+        const size_t bytes = (size_t)hot * sizeof(T);
+        const unsigned grid = (unsigned)device_cu_count();
+        if (tune().pull_nt) {
+            static bool attr = false;
+            if (!attr) {
+                JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
+                attr = true;
+            }
+            pull_lds_kernel<Op, 4, true><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
+        } else {
+            static bool attr = false;
+            if (!attr) {
+                JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
+                attr = true;
+            }
+            pull_lds_kernel<Op, 4, false><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
+        }
+        JG_LAUNCH_CHECK();
+        if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
+        if (plan.num_hub_rows > 0) {
+            pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
+            JG_LAUNCH_CHECK();
+        }
+        return;
     }
     auto launch = [&](unsigned grid) {
         const int u = tune().pull_unroll;

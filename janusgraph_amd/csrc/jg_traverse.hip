@@ -189,6 +189,7 @@ struct MsBfsOp {
     __device__ __forceinline__ T identity() const { return 0ull; }
     __device__ __forceinline__ T combine(T a, T b) const { return a | b; }
     __device__ __forceinline__ T gather(int32_t c) const { return F[c]; }
+    __device__ __forceinline__ const T* vec() const { return F; }
     __device__ __forceinline__ T shfl_xor(T v, int o) const { return __shfl_xor(v, o, kWave); }
     __device__ __forceinline__ bool active(int64_t row) const { return visited[row] != full; }
     __device__ __forceinline__ void finalize(int64_t row, T acc) const {

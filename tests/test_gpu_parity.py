@@ -268,3 +268,37 @@ def test_errors_are_status_codes(ctx):
         g.pagerank(0.85, 2, 5)  # no in-adjacency built
     with pytest.raises(jg.JanusGpuError):
         g.pagerank_step(1)
+
+
+@pytest.mark.parametrize("mode", ["lds", "split_queue", "split_static"])
+def test_pull_engine_variants_match_oracle(oracle_lib, mode):
+    """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: LDS-staged hot prefix,
+    XCD column split with per-XCD queues, and with the static blockIdx mapping."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    knobs = {"lds": [("pull_split", 0), ("pull_lds", 20480)],
+             "split_queue": [("pull_lds", 0), ("split_min_degree", 64), ("pull_split", 1)],
+             "split_static": [("pull_lds", 0), ("split_min_degree", 64), ("pull_split", 2)]}[mode]
+    try:
+        for k, v in knobs:
+            _lib.tune_set(k, v)
+        c = jg.Context((0,))
+        n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 15)
+        g = c.build(vid, src, dst, flags=2 | 4)
+        rank, _ = g.pagerank(0.85, n, 12)
+        r_ref, _ = oracle_lib.pagerank(n, ds, dd, 0.85, n, 12)
+        assert_pr_close(rank, r_ref)
+        comp, it = g.connected_components()
+        ref, ref_it = oracle_lib.connected_components(n, ds, dd, vid)
+        np.testing.assert_array_equal(comp, ref)
+        assert it == ref_it
+        srcs = np.unique(ds)[:40]
+        depth = g.bfs(vid[srcs], 3)
+        for k in (0, 17, 39):
+            np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3))
+        g.close()
+        c.close()
+    finally:
+        _lib.tune_set("pull_lds", 0)
+        _lib.tune_set("pull_split", 1)
+        _lib.tune_set("split_min_degree", 2048)
