@@ -556,7 +556,8 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
     // the heavy prefix split by XCD: rows before the first row of degree < split_min_degree
-    const int64_t heavy = std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin);
+    // (built only when the split is enabled at build time: it measured slower on RMAT)
+    const int64_t heavy = tune().pull_split ? std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin) : 0;
     auto make_classes = [&](int64_t first_row, int64_t chunks, int64_t* rb, int64_t* re, int64_t* bb) {
         int64_t begin = first_row;
         rb[0] = re[0] = 0;  // hub class is the chunk table

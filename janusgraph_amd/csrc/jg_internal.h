@@ -91,6 +91,13 @@ struct Shard {
     DevBuf<int32_t> cc_label;      // [rows]
     DevBuf<int32_t> cc_hub_partial;
     DevBuf<int32_t> cc_changed;    // [1]
+    // single-source DO-BFS scratch, kept across calls (level-parity ping-pong)
+    DevBuf<int32_t> bfs_queue[2];            // [rows] frontier vertices
+    DevBuf<int64_t> bfs_qoff[2];             // [rows] first push edge of each queue entry
+    DevBuf<unsigned long long> bfs_bm[2];    // [ceil(rows/64)] frontier bitmaps (bottom-up)
+    DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
+    DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
+    DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
 };
@@ -174,7 +181,8 @@ void split_debug_dump();
 struct Tune {
     int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
-    int pull_split = 1;   // XCD column split of the heavy rows: 0 off, 1 per-XCD queues, 2 static map
+    int pull_split = 0;   // XCD column split of the heavy rows: 0 off, 1 per-XCD queues, 2 static map
+                          // (read at build time too: the split plan is only built when non-zero)
     int64_t split_min_degree = 2048;  // build time: rows of at least this degree are split
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
 };

@@ -9,11 +9,12 @@
 //   minimum, forwards on improvement; supersteps 0..maxDepth => min over paths of <= maxDepth hops.
 //
 // Kernels:
-//   single source, 1 shard: direction-optimising BFS (Beamer).  Top-down expands a queue with
-//     16 lanes per frontier vertex, claims targets with atomicCAS and appends them through one
-//     wave-ballot + one atomicAdd per wave; bottom-up gives each unvisited vertex one lane that
-//     scans its pull adjacency against a 64-bit-word frontier bitmap and stops at the first hit;
-//     the next bitmap word is the wave's ballot (no atomics).
+//   single source, 1 shard: direction-optimising BFS (Beamer), one kernel per level that picks its
+//     direction on the device from the counters of the previous level (no host round trip per
+//     level).  Top-down is edge-parallel over the frontier's edges, claims targets with atomicCAS
+//     and appends them through one wave-ballot + one packed atomicAdd per wave; bottom-up gives
+//     each unvisited vertex one lane that scans its pull adjacency against a 64-bit-word frontier
+//     bitmap and stops at the first hit; the next bitmap word is the wave's ballot (no atomics).
 //   multi-source (<= 64) or sharded: bit-parallel BFS, one uint64 frontier word per vertex, as an
 //     OR-semiring pull superstep on the jg_pull.h engine, exchanged by allgather.
 //   weighted SD: frontier Bellman-Ford with exact snapshot semantics (messages of superstep t-1
@@ -30,6 +31,7 @@ constexpr int kTdLanes = 16;         // lanes per frontier vertex in the weighte
 constexpr int kPackShift = 37;       // packed frontier counter: (vertices << 37) | push edges
 constexpr unsigned long long kEdgeMask = (1ull << kPackShift) - 1ull;
 constexpr int kTdEdgesPerThread = 4;
+constexpr int kBfsRing = 4;            // level-state ring: a level touches slots L-1, L, L+1
 
 __device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t* __restrict__ queue,
                                             unsigned long long* __restrict__ size) {
@@ -66,19 +68,76 @@ __device__ __forceinline__ void wave_append_frontier(bool take, int32_t v, int64
     }
 }
 
-// Edge-parallel top-down step: frontier edge e in [0, mf) belongs to the queue entry i with
+// Per-level device state of the single-source DO-BFS.  Level L's kernel derives its direction from
+// the state and frontier counter level L-1 left behind, so the host enqueues levels in batches and
+// reads the state back once per batch instead of once per level.
+struct BfsState {
+    long long mu;     // push edges not yet in any frontier (after this level's input frontier)
+    long long edges;  // push degree summed over every frontier so far = edges of reached vertices
+    int bottom_up;    // direction this level ran in
+    int done;         // traversal finished: this level and all later ones do nothing
+    int levels;       // levels run (valid once done)
+    int pad;
+};
+
+struct BfsLevel {
+    const int64_t* push_rp;  // null when there is no push adjacency
+    const int32_t* push_col;
+    const int64_t* pull_rp;  // null when there is no pull adjacency
+    const int32_t* pull_col;
+    const int64_t* deg_rp;   // push_rp, else pull_rp (frontier edge counts)
+    int32_t* depth;
+    int64_t rows;
+    const int32_t* queue_in;
+    const int64_t* qoff_in;
+    int32_t* queue_out;
+    int64_t* qoff_out;
+    const unsigned long long* bm_in;
+    unsigned long long* bm_out;
+    unsigned long long* ctr;  // [kBfsRing] packed frontier counters, slot = level % kBfsRing
+    BfsState* st;             // [kBfsRing]
+    int level, max_depth;
+    double alpha, beta;
+};
+
+// Direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the unexplored
+// edges / alpha, back top-down when the frontier shrinks below rows / beta.
+__device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_out, bool* switch_in) {
+    const int pl = (a.level + kBfsRing - 1) % kBfsRing;
+    const BfsState p = a.st[pl];
+    const unsigned long long h = a.ctr[pl];
+    BfsState c = p;
+    *switch_in = false;
+    *nf_out = *mf_out = 0;
+    if (p.done) return c;
+    const int64_t nf = (int64_t)(h >> kPackShift), mf = (int64_t)(h & kEdgeMask);
+    *nf_out = nf;
+    *mf_out = mf;
+    c.mu = p.mu - mf;
+    c.edges = p.edges + mf;
+    if (nf == 0 || (a.max_depth >= 0 && a.level >= a.max_depth)) {
+        c.done = 1;
+        c.levels = a.level;
+        return c;
+    }
+    if (!p.bottom_up && a.pull_rp && (!a.push_rp || (double)mf > (double)c.mu / a.alpha)) {
+        c.bottom_up = 1;
+        *switch_in = true;  // the previous frontier exists only as a queue: test depth == level instead
+    } else if (p.bottom_up && a.push_rp && (double)nf < (double)a.rows / a.beta) {
+        c.bottom_up = 0;  // the queue is always valid: both directions append to it
+    }
+    return c;
+}
+
+// Edge-parallel top-down: frontier edge e in [0, mf) belongs to the queue entry i with
 // qoff[i] <= e < qoff[i+1]; each thread walks kTdEdgesPerThread consecutive edges after one binary
 // search, so a hub in the frontier is spread over the whole grid.
-__global__ __launch_bounds__(kBlock) void td_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                    const int32_t* __restrict__ queue,
-                                                    const int64_t* __restrict__ qoff, int64_t nf, int64_t mf,
-                                                    int32_t* __restrict__ depth, int32_t next_depth,
-                                                    int32_t* __restrict__ next_queue, int64_t* __restrict__ next_qoff,
-                                                    unsigned long long* __restrict__ packed) {
+__device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
     const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
+    const int32_t next_depth = a.level + 1;
     for (int64_t t = 0; t < tiles; ++t) {
         const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
         int64_t i = 0, next_bound = 0;
@@ -86,10 +145,10 @@ __global__ __launch_bounds__(kBlock) void td_kernel(const int64_t* __restrict__ 
             int64_t lo = 0, hi = nf - 1;
             while (lo < hi) {
                 const int64_t mid = (lo + hi + 1) >> 1;
-                if (qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+                if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
             }
             i = lo;
-            next_bound = i + 1 < nf ? qoff[i + 1] : mf;
+            next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
         }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) {
@@ -100,79 +159,93 @@ __global__ __launch_bounds__(kBlock) void td_kernel(const int64_t* __restrict__ 
             if (e < mf) {
                 while (e >= next_bound) {  // skips zero-degree frontier entries too
                     ++i;
-                    next_bound = i + 1 < nf ? qoff[i + 1] : mf;
+                    next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
                 }
-                const int32_t u = queue[i];
-                v = col[rp[u] + (e - qoff[i])];
-                if (depth[v] < 0 && atomicCAS(&depth[v], -1, next_depth) == -1) {
+                const int32_t u = a.queue_in[i];
+                v = a.push_col[a.push_rp[u] + (e - a.qoff_in[i])];
+                if (a.depth[v] < 0 && atomicCAS(&a.depth[v], -1, next_depth) == -1) {
                     won = true;
-                    vdeg = rp[v + 1] - rp[v];
+                    vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
                 }
             }
-            wave_append_frontier(won, v, vdeg, next_queue, next_qoff, packed);
+            wave_append_frontier(won, v, vdeg, a.queue_out, a.qoff_out, packed);
         }
     }
 }
 
-__global__ void queue_to_bitmap_kernel(const int32_t* __restrict__ queue, int64_t qsize,
-                                       unsigned long long* __restrict__ bm) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < qsize; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t u = queue[i];
-        atomicOr(&bm[u >> 6], 1ull << (u & 63));
-    }
-}
-
-// One lane per vertex; 64 consecutive vertices per wave so that the next frontier word is a ballot.
-__global__ __launch_bounds__(kBlock) void bu_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                    const int64_t* __restrict__ push_rp,
-                                                    const unsigned long long* __restrict__ frontier,
-                                                    int32_t* __restrict__ depth, int64_t rows, int32_t next_depth,
-                                                    unsigned long long* __restrict__ next_bm,
-                                                    int32_t* __restrict__ next_queue, int64_t* __restrict__ next_qoff,
-                                                    unsigned long long* __restrict__ packed) {
-    const int64_t words = (rows + 63) / 64;
+// Bottom-up: one lane per unvisited vertex scans its pull row against the frontier and stops at the
+// first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
+template <bool kFromDepth>
+__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed) {
+    const int64_t words = (a.rows + 63) / 64;
     const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) / kWave;
+    const int32_t next_depth = a.level + 1;
     for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words; w += wstride) {
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t vdeg = 0;
-        if (v < rows && depth[v] < 0) {
-            const int64_t j1 = rp[v + 1];
-            for (int64_t j = rp[v]; j < j1; ++j) {
-                const int32_t u = col[j];
-                if ((frontier[u >> 6] >> (u & 63)) & 1ull) { found = true; break; }
+        if (v < a.rows && a.depth[v] < 0) {
+            const int64_t j1 = a.pull_rp[v + 1];
+            for (int64_t j = a.pull_rp[v]; j < j1; ++j) {
+                const int32_t u = a.pull_col[j];
+                const bool in_frontier = kFromDepth ? a.depth[u] == a.level : ((a.bm_in[u >> 6] >> (u & 63)) & 1ull);
+                if (in_frontier) { found = true; break; }
             }
             if (found) {
-                depth[v] = next_depth;
-                vdeg = push_rp[v + 1] - push_rp[v];
+                a.depth[v] = next_depth;
+                vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
             }
         }
         const uint64_t word = __ballot(found);
-        if (lane_id() == 0) next_bm[w] = word;
-        wave_append_frontier(found, (int32_t)v, vdeg, next_queue, next_qoff, packed);
+        if (lane_id() == 0) a.bm_out[w] = word;
+        wave_append_frontier(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed);
     }
+}
+
+__global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
+    __shared__ BfsState s_st;
+    __shared__ long long s_nf, s_mf;
+    __shared__ int s_switch;
+    if (threadIdx.x == 0) {
+        int64_t nf, mf;
+        bool sw;
+        const BfsState c = bfs_decide(a, &nf, &mf, &sw);
+        s_st = c;
+        s_nf = nf;
+        s_mf = mf;
+        s_switch = sw;
+        if (blockIdx.x == 0) {
+            a.st[a.level % kBfsRing] = c;
+            if (!c.done) a.ctr[(a.level + 1) % kBfsRing] = 0ull;  // counter of the next level
+        }
+    }
+    __syncthreads();
+    if (s_st.done) return;
+    unsigned long long* packed = a.ctr + a.level % kBfsRing;
+    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed);
+    else if (s_switch) bfs_bottom_up<true>(a, packed);
+    else bfs_bottom_up<false>(a, packed);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-__global__ void set_source_kernel(int32_t* depth, int32_t* queue, int64_t* qoff, int64_t v, const int64_t* rp,
-                                  unsigned long long* packed) {
-    depth[v] = 0;
-    queue[0] = (int32_t)v;
-    qoff[0] = 0;
-    *packed = (1ull << kPackShift) | (unsigned long long)(rp[v + 1] - rp[v]);
-}
-
-// input edges inside the reached set: sum of row lengths of reached vertices (symmetric: / 2 later)
-__global__ void reached_edges_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ depth, int64_t rows,
-                                     unsigned long long* __restrict__ out) {
-    unsigned long long s = 0;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
-        if (depth[v] >= 0) s += (unsigned long long)(rp[v + 1] - rp[v]);
-    s = wave_reduce_add(s);
-    if (lane_id() == 0 && s) atomicAdd(out, s);
+// depth = -1 except the source; level -1 state: nothing explored, the source is the frontier
+__global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64_t source, int32_t* queue,
+                                int64_t* qoff, const int64_t* __restrict__ deg_rp, long long total,
+                                unsigned long long* ctr, BfsState* st) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x)
+        depth[i] = i == source ? 0 : -1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        queue[0] = (int32_t)source;
+        qoff[0] = 0;
+        ctr[kBfsRing - 1] = (1ull << kPackShift) | (unsigned long long)(deg_rp[source + 1] - deg_rp[source]);
+        ctr[0] = 0ull;
+        BfsState s{};
+        s.mu = total;
+        st[kBfsRing - 1] = s;
+    }
 }
 
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
@@ -305,7 +378,7 @@ BfsCsrs pick_csrs(const Shard& sh, int direction) {
 }
 
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
-// Returns levels run; *edges_out = adjacency entries of reached vertices (push CSR).
+// Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
                  double* edges_out) {
     hipStream_t s = sh.stream;
@@ -314,67 +387,59 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     const Csr* pull = c.pull;
     const Csr* degcsr = push ? push : pull;
     const int64_t words = (rows + 63) / 64;
-    DevBuf<int32_t> qa(std::max<int64_t>(rows, 1)), qb(std::max<int64_t>(rows, 1));
-    DevBuf<int64_t> oa(std::max<int64_t>(rows, 1)), ob(std::max<int64_t>(rows, 1));
-    DevBuf<unsigned long long> bma(std::max<int64_t>(words, 1)), bmb(std::max<int64_t>(words, 1));
-    DevBuf<unsigned long long> packed(1);
-    fill_i32_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, -1);
+    const size_t r1 = (size_t)std::max<int64_t>(rows, 1), w1 = (size_t)std::max<int64_t>(words, 1);
+    for (int k = 0; k < 2; ++k) {
+        if (sh.bfs_queue[k].size() != r1) sh.bfs_queue[k].alloc(r1);
+        if (sh.bfs_qoff[k].size() != r1) sh.bfs_qoff[k].alloc(r1);
+        if (sh.bfs_bm[k].size() != w1) sh.bfs_bm[k].alloc(w1);
+    }
+    if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
+    if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
+    BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
+    bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
+                                                      degcsr->row_ptr.get(), (long long)degcsr->nnz,
+                                                      sh.bfs_ctr.get(), st);
     JG_LAUNCH_CHECK();
-    set_source_kernel<<<1, 1, 0, s>>>(depth, qa.get(), oa.get(), source, degcsr->row_ptr.get(), packed.get());
-    JG_LAUNCH_CHECK();
-    unsigned long long h = 0;
-    copy_d2h(&h, packed.get(), sizeof h, s);
-    int64_t nf = (int64_t)(h >> kPackShift), mf = (int64_t)(h & kEdgeMask);
-    int64_t mu = degcsr->nnz - mf;
-    bool bottom_up = false;
-    const double alpha = 14.0, beta = 24.0;
+    BfsLevel a{};
+    a.push_rp = push ? push->row_ptr.get() : nullptr;
+    a.push_col = push ? push->col.get() : nullptr;
+    a.pull_rp = pull ? pull->row_ptr.get() : nullptr;
+    a.pull_col = pull ? pull->col.get() : nullptr;
+    a.deg_rp = degcsr->row_ptr.get();
+    a.depth = depth;
+    a.rows = rows;
+    a.ctr = sh.bfs_ctr.get();
+    a.st = st;
+    a.max_depth = max_depth;
+    a.alpha = 14.0;
+    a.beta = 24.0;
+    // a fixed grid: bottom-up covers every word, top-down strides over the frontier's edges
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((words * kWave + kBlock - 1) / kBlock, 64),
+                                                      256 * 8);
+    BfsState hs{};
     int level = 0;
-    while (nf > 0 && (max_depth < 0 || level < max_depth)) {
-        // direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the
-        // unexplored edges / alpha, back top-down when the frontier shrinks below n / beta
-        if (!bottom_up && pull && (!push || (double)mf > (double)mu / alpha)) {
-            bottom_up = true;
-            JG_HIP(hipMemsetAsync(bma.get(), 0, words * sizeof(unsigned long long), s));  // queue -> bitmap
-            queue_to_bitmap_kernel<<<grid_for(nf), kBlock, 0, s>>>(qa.get(), nf, bma.get());
+    for (int batch = 8;; batch = 16) {
+        if (max_depth >= 0) batch = std::min(batch, max_depth + 1 - level);
+        if (batch <= 0) fail(JG_ERR_STATE, "BFS level control did not terminate");  // level max_depth stops
+        for (int k = 0; k < batch; ++k, ++level) {
+            const int p = level & 1;
+            a.level = level;
+            a.queue_in = sh.bfs_queue[p].get();
+            a.qoff_in = sh.bfs_qoff[p].get();
+            a.queue_out = sh.bfs_queue[p ^ 1].get();
+            a.qoff_out = sh.bfs_qoff[p ^ 1].get();
+            a.bm_in = sh.bfs_bm[p].get();
+            a.bm_out = sh.bfs_bm[p ^ 1].get();
+            if (prof_enabled(ctx)) prof_record_start(ctx, sh);
+            bfs_level_kernel<<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
-        } else if (bottom_up && push && (double)nf < (double)rows / beta) {
-            bottom_up = false;  // the queue is always valid: both steps append to it
+            if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
         }
-        JG_HIP(hipMemsetAsync(packed.get(), 0, sizeof(unsigned long long), s));
-        const int next_depth = level + 1;
-        if (prof_enabled(ctx)) prof_record_start(ctx, sh);
-        if (bottom_up) {
-            bu_kernel<<<grid_for(words * kWave, kBlock, 256 * 8), kBlock, 0, s>>>(
-                pull->row_ptr.get(), pull->col.get(), degcsr->row_ptr.get(), bma.get(), depth, rows, next_depth,
-                bmb.get(), qb.get(), ob.get(), packed.get());
-            bma.swap(bmb);
-        } else if (mf > 0) {
-            td_kernel<<<grid_for((mf + kTdEdgesPerThread - 1) / kTdEdgesPerThread, kBlock, 256 * 8), kBlock, 0, s>>>(
-                push->row_ptr.get(), push->col.get(), qa.get(), oa.get(), nf, mf, depth, next_depth, qb.get(),
-                ob.get(), packed.get());
-        }
-        JG_LAUNCH_CHECK();
-        if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
-        qa.swap(qb);
-        oa.swap(ob);
-        copy_d2h(&h, packed.get(), sizeof h, s);
-        nf = (int64_t)(h >> kPackShift);
-        mf = (int64_t)(h & kEdgeMask);
-        mu -= mf;
-        ++level;
+        copy_d2h(&hs, st + (level - 1) % kBfsRing, sizeof hs, s);
+        if (hs.done) break;
     }
-    if (edges_out) {
-        DevBuf<unsigned long long> e(1);
-        JG_HIP(hipMemsetAsync(e.get(), 0, sizeof(unsigned long long), s));
-        reached_edges_kernel<<<grid_for(rows, kBlock, 1024), kBlock, 0, s>>>(degcsr->row_ptr.get(), depth, rows,
-                                                                             e.get());
-        JG_LAUNCH_CHECK();
-        unsigned long long he = 0;
-        JG_HIP(hipMemcpyAsync(&he, e.get(), sizeof he, hipMemcpyDeviceToHost, s));
-        JG_HIP(hipStreamSynchronize(s));
-        *edges_out = (double)he;
-    }
-    return level;
+    if (edges_out) *edges_out = (double)hs.edges;
+    return hs.levels;
 }
 
 int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
@@ -403,7 +468,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         const BfsCsrs c = pick_csrs(sh, direction);
         int shard = 0;
         const int64_t l = local_of_vid(g, source_vids[0], &shard);
-        DevBuf<int32_t> depth(std::max<int64_t>(sh.rows, 1));
+        if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
+        DevBuf<int32_t>& depth = sh.bfs_depth;
         int levels = 0;
         double edges = 0;
         if (l < 0) {

@@ -300,5 +300,5 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         c.close()
     finally:
         _lib.tune_set("pull_lds", 0)
-        _lib.tune_set("pull_split", 1)
+        _lib.tune_set("pull_split", 0)
         _lib.tune_set("split_min_degree", 2048)

@@ -43,7 +43,7 @@ def main():
     out = {s: {"median_ms": round(float(np.median(v)), 4),
                "max_rel_vs_off": float(np.max(np.abs(ranks[s] - base) / base))} for s, v in res.items()}
     _lib.tune_set("pull_lds", 0)
-    _lib.tune_set("pull_split", 1)
+    _lib.tune_set("pull_split", 0)
     print(json.dumps({"scale": args.scale, "lds": out}))
 
 

@@ -40,6 +40,7 @@ def main():
     out = {}
     for d in [int(x) for x in args.degrees.split(",")]:
         _lib.tune_set("split_min_degree", d)
+        _lib.tune_set("pull_split", 1)  # build the split plan
         g = ctx.build_rmat(args.scale, 16, 0x5EED + args.scale, flags=jg.ADJ_IN)
         res = {0: [], 1: [], 2: []}
         for _ in range(args.rounds):
@@ -48,7 +49,7 @@ def main():
                 res[mode].append(time_steps(g, n, args.steps))
         out[d] = {f"split{m}": round(float(np.median(v)), 4) for m, v in res.items()}
         g.close()
-    _lib.tune_set("pull_split", 1)
+    _lib.tune_set("pull_split", 0)
     print(json.dumps({"scale": args.scale, "ms_per_step": out}))
 
 
