@@ -114,6 +114,10 @@ def load():
         f.argtypes = args
         f.restype = res
     _lib = L
+    # JG_TUNE="key=value,key=value": performance knobs for profiling runs (results are unaffected)
+    for item in filter(None, os.environ.get("JG_TUNE", "").split(",")):
+        k, v = item.split("=")
+        tune_set(k.strip(), int(v))
     return L
 
 
@@ -128,7 +132,8 @@ def _ptr(a):
 
 
 def tune_set(key: str, value: int):
-    """Process-wide performance knob (results are unaffected): pull_unroll, pull_nt."""
+    """Process-wide performance knob (results are unaffected): pull_unroll, pull_nt, pull_lds,
+    pull_split, split_min_degree (the last two are read at graph build time too)."""
     check(load().jg_tune_set(key.encode(), int(value)))
 
 

@@ -98,33 +98,6 @@ bool debug_plan() {
     return v;
 }
 
-unsigned long long* split_debug_counters() {
-    static unsigned long long* p = nullptr;
-    static bool init = false;
-    if (!init) {
-        init = true;
-        if (env_flag("JG_DEBUG_SPLIT")) {
-            JG_HIP(hipMalloc(reinterpret_cast<void**>(&p), 64 * sizeof(unsigned long long)));
-            JG_HIP(hipMemset(p, 0, 64 * sizeof(unsigned long long)));
-        }
-    }
-    return p;
-}
-
-void split_debug_dump() {
-    unsigned long long* p = split_debug_counters();
-    if (!p) return;
-    unsigned long long h[64];
-    JG_HIP(hipDeviceSynchronize());
-    JG_HIP(hipMemcpy(h, p, sizeof h, hipMemcpyDeviceToHost));
-    std::fprintf(stderr, "[jg split] tasks by xcc (rows) x range (cols):\n");
-    for (int x = 0; x < 8; ++x) {
-        std::fprintf(stderr, "[jg split]  xcc %d:", x);
-        for (int q = 0; q < 8; ++q) std::fprintf(stderr, " %8llu", h[x * 8 + q]);
-        std::fprintf(stderr, "\n");
-    }
-}
-
 Tune& tune() {
     static Tune t;
     return t;
@@ -228,9 +201,13 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "split_min_degree") {
         JG_ARG(value >= 8, "split_min_degree must be >= 8");
         jg::tune().split_min_degree = value;
+    } else if (k == "slice_mode") {
+        JG_ARG(value >= 0 && value <= 2, "slice_mode must be 0, 1 or 2");
+        jg::tune().slice_mode = (int)value;
     } else if (k == "pull_split") {
-        JG_ARG(value >= 0 && value <= 2, "pull_split must be 0 (off), 1 (per-XCD queues) or 2 (static)");
-        jg::tune().pull_split = (int)value;
+        jg::tune().pull_split = value != 0;
+    } else if (k == "slice_lds") {
+        jg::tune().slice_lds = value != 0;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }
@@ -497,7 +474,6 @@ int jg_graph_sync(jg_graph* g) {
         jg::DeviceGuard dg(sp->device);
         JG_HIP(hipStreamSynchronize(sp->stream));
     }
-    jg::split_debug_dump();
     JG_GUARD_END
 }
 

@@ -197,6 +197,8 @@ struct SelectArgs {
     int r;
     int which;
     int cbits;
+    int sbits;  // 0, or kSliceBits: entries of a row grouped by XCD slice of their column (then by column)
+    int smode;  // col_slice mode
 };
 
 __device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
@@ -244,12 +246,14 @@ __global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, cons
         const int64_t gs = a.padded[s], gd = a.padded[d];
         const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
         if ((a.which == 1 || a.which == 2) && own_s) {
-            keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)gd;
+            keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
+                        ((uint64_t)(a.sbits ? col_slice(gd, a.smode) : 0) << a.cbits) | (uint64_t)gd;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
         if ((a.which == 0 || a.which == 2) && own_d) {
-            keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)gs;
+            keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
+                        ((uint64_t)(a.sbits ? col_slice(gs, a.smode) : 0) << a.cbits) | (uint64_t)gs;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
@@ -261,15 +265,15 @@ __global__ void fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
 }
 
 // row_ptr[rr] = first entry of row rr; rows without entries get the next row's start.
-__global__ void csr_from_sorted_kernel(const uint64_t* __restrict__ keys, int64_t nnz, int cbits,
+__global__ void csr_from_sorted_kernel(const uint64_t* __restrict__ keys, int64_t nnz, int cbits, int rshift,
                                        int64_t* __restrict__ row_ptr, int32_t* __restrict__ col,
                                        const uint32_t* __restrict__ eidx, const int32_t* __restrict__ w_in,
                                        int32_t* __restrict__ w_out) {
     const uint64_t cmask = (1ull << cbits) - 1ull;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = keys[i];
-        const int64_t row = (int64_t)(k >> cbits);
-        const int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> cbits) : -1;
+        const int64_t row = (int64_t)(k >> rshift);
+        const int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> rshift) : -1;
         for (int64_t rr = prev + 1; rr <= row; ++rr) row_ptr[rr] = i;
         col[i] = (int32_t)(k & cmask);
         if (w_out) w_out[i] = w_in[eidx[i]];
@@ -310,40 +314,19 @@ __global__ void gather_row_bounds_kernel(const int64_t* __restrict__ rp, const i
 }
 
 // ---------------- XCD split of the heavy rows ----------------
-__global__ void col_hist_kernel(const int32_t* __restrict__ col, int64_t n, int32_t* __restrict__ hist) {
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&hist[col[j]], 1);
-}
-
-// bounds[q] = first column g with prefix[g] >= q * total / 8 (q = 1..7)
-__global__ void col_bound_kernel(const int64_t* __restrict__ prefix, int64_t len, int64_t* __restrict__ bounds) {
-    const int q = threadIdx.x + 1;
-    if (q >= kXcds) return;
-    const int64_t total = prefix[len];
-    const int64_t target = total / kXcds * q + (total % kXcds) * q / kXcds;
-    int64_t lo = 0, hi = len;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (prefix[mid] < target) lo = mid + 1; else hi = mid;
-    }
-    bounds[q] = lo;
-}
-
-// split_off[r*8+q] = first entry of row r with col >= bounds[q], relative to row_ptr[r] (cols sorted)
+// split_off[r*8+q] = first entry of row r in XCD slice q, relative to row_ptr[r].  Entries of a row
+// of a sliced CSR are ordered by (col_slice(col), col), so the slice is non-decreasing along the row.
 __global__ void split_off_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t heavy,
-                                 const int64_t* __restrict__ bounds, uint32_t* __restrict__ split_off) {
+                                 int smode, uint32_t* __restrict__ split_off) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < heavy * kXcds;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / kXcds;
         const int q = (int)(i % kXcds);
         const int64_t b = rp[r], e = rp[r + 1];
         int64_t lo = b, hi = e;
-        if (q > 0) {
-            const int64_t target = bounds[q];
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if ((int64_t)col[mid] < target) lo = mid + 1; else hi = mid;
-            }
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (col_slice(col[mid], smode) < q) lo = mid + 1; else hi = mid;
         }
         split_off[i] = (uint32_t)(lo - b);
     }
@@ -403,16 +386,19 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     DevBuf<uint32_t> eidx;
     const int64_t nnz = select_keys(a, keys, eidx, weight != nullptr, s);
     const int rbits = bits_for((uint64_t)std::max<int64_t>(sh.rows - 1, 0));
-    prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits, s);
+    prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits + a.sbits, s);
     csr.rows = sh.rows;
     csr.nnz = nnz;
+    csr.sliced = a.sbits != 0;
+    csr.slice_mode = a.smode;
     csr.row_ptr.alloc(sh.rows + 1);
     csr.col.alloc(std::max<int64_t>(nnz, 1));
     if (weight) csr.weight.alloc(std::max<int64_t>(nnz, 1));
     fill_i64_kernel<<<grid_for(sh.rows + 1), kBlock, 0, s>>>(csr.row_ptr.get(), sh.rows + 1, nnz);
     JG_LAUNCH_CHECK();
     if (nnz > 0) {
-        csr_from_sorted_kernel<<<grid_for(nnz), kBlock, 0, s>>>(keys.get(), nnz, a.cbits, csr.row_ptr.get(),
+        csr_from_sorted_kernel<<<grid_for(nnz), kBlock, 0, s>>>(keys.get(), nnz, a.cbits, a.cbits + a.sbits,
+                                                                csr.row_ptr.get(),
                                                                 csr.col.get(), weight ? eidx.get() : nullptr, weight,
                                                                 weight ? csr.weight.get() : nullptr);
         JG_LAUNCH_CHECK();
@@ -420,77 +406,98 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     JG_HIP(hipStreamSynchronize(s));
 }
 
-// Tasks of the XCD split (shared by the 8 column ranges): a hub row alone (block-wide fold), or up to
-// 256/L consecutive heavy rows folded with L lanes each, L chosen from the per-range length ~deg/8.
+// Tasks of the XCD-sliced split, shared by the 8 slices (pull_slice_kernel): rows whose per-slice
+// length d/8 exceeds 2 kSliceChunk are cut into K chunk tasks each (the degree-sorted prefix); the
+// rest are grouped 64/L consecutive rows to a wave, L lanes per row with ~4 entries per lane.
 static void build_split_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t heavy) {
     hipStream_t s = sh.stream;
-    plan.split_rows = 0;
-    plan.split_tasks = 0;
+    plan.split_rows = plan.split_tasks = plan.chunk_rows = plan.chunk_tasks = 0;
     if (heavy <= 0) return;
     std::vector<int64_t> rp(heavy + 1);
     copy_d2h(rp.data(), csr.row_ptr.get(), (heavy + 1) * sizeof(int64_t), s);
     plan.split_rows = heavy;
-    // tasks
-    std::vector<int32_t> trow, tmeta;
+    std::vector<int32_t> trow, tmeta, cptr(1, 0);
     int64_t r = 0;
-    while (r < heavy) {
-        const int64_t d = rp[r + 1] - rp[r];
-        if (d >= kHubDegree) {
+    for (; r < heavy; ++r) {
+        const int64_t per = (rp[r + 1] - rp[r]) / kXcds;
+        if (per <= 2 * kSliceChunk) break;
+        const int64_t K = std::min<int64_t>((per + kSliceChunk - 1) / kSliceChunk, 4095);
+        for (int64_t k = 0; k < K; ++k) {
             trow.push_back((int32_t)r);
-            tmeta.push_back(0 | (1 << 8));
-            ++r;
-            continue;
+            tmeta.push_back((int32_t)((k | (K << 12)) << 8));
         }
-        const int64_t per = d / kXcds;
-        const int lanes = per >= 256 ? 64 : per >= 128 ? 32 : per >= 64 ? 16 : per >= 32 ? 8 : per >= 16 ? 4 : 2;
-        const int64_t maxrows = kBlock / lanes;
-        int64_t k = 0;
-        while (k < maxrows && r + k < heavy) {
-            const int64_t dk = rp[r + k + 1] - rp[r + k];
-            const int64_t pk = dk / kXcds;
-            const int lk = dk >= kHubDegree ? 0
-                           : pk >= 256 ? 64 : pk >= 128 ? 32 : pk >= 64 ? 16 : pk >= 32 ? 8 : pk >= 16 ? 4 : 2;
-            if (lk != lanes) break;
-            ++k;
-        }
+        cptr.push_back((int32_t)trow.size());
+    }
+    plan.chunk_rows = r;
+    plan.chunk_tasks = (int64_t)trow.size();
+    auto lanes_for = [](int64_t per) {
+        int L = 1;
+        while (L < 64 && 4 * L < per) L *= 2;
+        return L;
+    };
+    while (r < heavy) {
+        const int L = lanes_for((rp[r + 1] - rp[r]) / kXcds);
+        int64_t k = 1;
+        while (k < kWave / L && r + k < heavy && lanes_for((rp[r + k + 1] - rp[r + k]) / kXcds) == L) ++k;
         trow.push_back((int32_t)r);
-        tmeta.push_back(lanes | (int32_t)(k << 8));
+        tmeta.push_back(L | (int32_t)(k << 8));
         r += k;
     }
     plan.split_tasks = (int64_t)trow.size();
     plan.task_row.alloc(trow.size());
     plan.task_meta.alloc(tmeta.size());
+    plan.chunk_ptr.alloc(cptr.size());
     copy_h2d(plan.task_row.get(), trow.data(), trow.size() * sizeof(int32_t), s);
     copy_h2d(plan.task_meta.get(), tmeta.data(), tmeta.size() * sizeof(int32_t), s);
-    plan.heads.alloc(kXcds);
-    plan.split_off.alloc(heavy * kXcds);
+    copy_h2d(plan.chunk_ptr.get(), cptr.data(), cptr.size() * sizeof(int32_t), s);
 }
 
-// Column bounds + per-row range offsets of the XCD split (needs the column space length).
-static void build_split_bounds(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
-    hipStream_t s = sh.stream;
-    const int64_t heavy = plan.split_rows;
-    if (heavy <= 0) return;
-    int64_t heavy_nnz = 0;
-    copy_d2h(&heavy_nnz, csr.row_ptr.get() + heavy, sizeof(int64_t), s);
-    DevBuf<int32_t> hist(col_space);
-    DevBuf<int64_t> prefix(col_space + 1);
-    JG_HIP(hipMemsetAsync(hist.get(), 0, hist.bytes(), s));
-    if (heavy_nnz > 0) {
-        col_hist_kernel<<<grid_for(heavy_nnz, kBlock, 4096), kBlock, 0, s>>>(csr.col.get(), heavy_nnz, hist.get());
-        JG_LAUNCH_CHECK();
+// Sub-row lengths in slice-major order: len[q * H + r] = entries of row r in slice q.
+__global__ void slice_len_kernel(const int64_t* __restrict__ rp, const uint32_t* __restrict__ off, int64_t H,
+                                 int32_t* __restrict__ len) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < H * kXcds; i += (int64_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i / H);
+        const int64_t r = i % H;
+        const int64_t b = off[r * kXcds + q];
+        const int64_t e = q == kXcds - 1 ? rp[r + 1] - rp[r] : (int64_t)off[r * kXcds + q + 1];
+        len[i] = (int32_t)(e - b);
     }
-    prim::exclusive_scan(hist.get(), prefix.get(), col_space, s);
-    DevBuf<int64_t> bounds(kXcds + 1);
-    int64_t hb[kXcds + 1];
-    for (int q = 0; q <= kXcds; ++q) hb[q] = q == kXcds ? col_space : 0;
-    copy_h2d(bounds.get(), hb, sizeof hb, s);
-    col_bound_kernel<<<1, kXcds, 0, s>>>(prefix.get(), col_space, bounds.get());
+}
+
+// slice_col[slice_ptr[q * H + r] ...] = the slice-q entries of row r (one wave per sub-row).
+__global__ void slice_copy_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                  const uint32_t* __restrict__ off, int64_t H, const int64_t* __restrict__ sp,
+                                  int32_t* __restrict__ scol) {
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; i < H * kXcds; i += waves) {
+        const int q = (int)(i / H);
+        const int64_t r = i % H;
+        const int64_t src = rp[r] + off[r * kXcds + q];
+        const int64_t dst = sp[i], n = sp[i + 1] - sp[i];
+        for (int64_t k = lane_id(); k < n; k += kWave) scol[dst + k] = col[src + k];
+    }
+}
+
+// Slice-major copy of the heavy rows (8 sub-CSRs over rows [0, H)): a wave folding consecutive rows
+// of one slice reads one contiguous col span.
+static void build_slice_csr(Shard& sh, const Csr& csr, PullPlan& plan) {
+    hipStream_t s = sh.stream;
+    const int64_t H = plan.split_rows;
+    if (H <= 0) return;
+    DevBuf<uint32_t> off(H * kXcds);
+    DevBuf<int32_t> len(H * kXcds);
+    split_off_kernel<<<grid_for(H * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), H, csr.slice_mode,
+                                                            off.get());
     JG_LAUNCH_CHECK();
-    copy_d2h(hb, bounds.get(), sizeof hb, s);
-    for (int q = 0; q <= kXcds; ++q) plan.col_bound[q] = hb[q];
-    split_off_kernel<<<grid_for(heavy * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), heavy, bounds.get(),
-                                                                plan.split_off.get());
+    slice_len_kernel<<<grid_for(H * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), off.get(), H, len.get());
+    JG_LAUNCH_CHECK();
+    plan.slice_ptr.alloc(H * kXcds + 1);
+    prim::exclusive_scan(len.get(), plan.slice_ptr.get(), H * kXcds, s);
+    int64_t nnz = 0;
+    copy_d2h(&nnz, plan.slice_ptr.get() + H * kXcds, sizeof(int64_t), s);
+    plan.slice_col.alloc(std::max<int64_t>(nnz, 1));
+    slice_copy_kernel<<<grid_for(H * kXcds * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), off.get(), H,
+                                                                     plan.slice_ptr.get(), plan.slice_col.get());
     JG_LAUNCH_CHECK();
     JG_HIP(hipStreamSynchronize(s));
 }
@@ -498,6 +505,7 @@ static void build_split_bounds(Shard& sh, const Csr& csr, PullPlan& plan, int64_
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
     hipStream_t s = sh.stream;
     plan.lds_ok = col_space == csr.rows;  // one shard: the hot prefix of the gathered vector is [0, hot)
+    plan.col_space = col_space;
     const int64_t rows = csr.rows;
     // hub rows (any position) -> chunk table
     std::vector<int64_t> hubs, bounds;
@@ -555,9 +563,10 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
-    // the heavy prefix split by XCD: rows before the first row of degree < split_min_degree
-    // (built only when the split is enabled at build time: it measured slower on RMAT)
-    const int64_t heavy = tune().pull_split ? std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin) : 0;
+    // the heavy prefix split by XCD slice: rows before the first row of degree < split_min_degree
+    // (only on a sliced CSR, and only when the split is enabled at build time)
+    const int64_t heavy = (tune().pull_split && csr.sliced && csr.slice_mode == 1)
+                              ? std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin) : 0;
     auto make_classes = [&](int64_t first_row, int64_t chunks, int64_t* rb, int64_t* re, int64_t* bb) {
         int64_t begin = first_row;
         rb[0] = re[0] = 0;  // hub class is the chunk table
@@ -577,7 +586,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     };
     make_classes(0, plan.num_chunks, plan.class_row_begin, plan.class_row_end, plan.class_block_begin);
     build_split_plan(sh, csr, plan, heavy);
-    build_split_bounds(sh, csr, plan, col_space);
+    build_slice_csr(sh, csr, plan);
     // light part: rows after the heavy prefix (hub rows are all heavy when rows are degree-sorted;
     // any hub beyond the prefix keeps its chunks, so chunks stay in the light table too)
     make_classes(plan.split_rows, plan.split_rows > 0 ? plan.num_chunks : plan.num_chunks, plan.light_row_begin,
@@ -666,11 +675,13 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                      sh.out_degree.get());
             JG_LAUNCH_CHECK();
         }
-        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits};
+        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0, tune().slice_mode};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
         if (g.flags & JG_ADJ_IN) {
             a.which = 0;
+            a.sbits = tune().pull_split ? kSliceBits : 0;  // PageRank's pull adjacency: XCD-sliced rows
             build_csr(sh, a, w, sh.in, s);
+            a.sbits = 0;
             build_pull_plan(sh, sh.in, sh.plan_in, g.padded_len());
         }
         if (g.flags & JG_ADJ_OUT) {

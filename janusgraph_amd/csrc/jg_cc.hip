@@ -23,6 +23,7 @@ constexpr int kCcMaxIterations = 100;  // ConnectedComponentVertexProgram defaul
 
 struct CcOp {
     using T = int32_t;
+    static constexpr bool kZeroIdentity = false;  // min: identity INT32_MAX
     const int32_t* __restrict__ msg;     // full length, previous superstep
     int32_t* __restrict__ msg_out;       // full length (owned slice written)
     int32_t* __restrict__ label;         // [rows]
@@ -135,7 +136,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         }
         sh.cc_label.alloc(std::max<int64_t>(sh.rows, 1));
         sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
-        sh.cc_split_partial.alloc(std::max<int64_t>(kXcds * sh.plan_both.split_rows, 1));
+        sh.cc_split_partial.alloc(sh.plan_both.split_partial_len());
         sh.cc_changed.alloc(1);
         std::vector<int32_t> lab0(sh.rows);
         for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];

@@ -25,6 +25,8 @@ struct Csr {
     DevBuf<int64_t> row_ptr;
     DevBuf<int32_t> col;
     DevBuf<int32_t> weight;  // optional (SD weights)
+    bool sliced = false;     // entries of each row ordered by (col_slice(col), col) instead of col
+    int slice_mode = 0;      // col_slice mode of a sliced CSR
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
 };
@@ -48,25 +50,47 @@ struct PullPlan {
     DevBuf<int64_t> hub_chunk_ptr;  // [num_hub_rows+1] chunks of hub row r: [ptr[r], ptr[r+1])
     int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
 
-    // XCD split of the heavy rows [0, split_rows) (degree >= kSplitMinDegree): the entries of every
-    // heavy row are cut at 8 column bounds (equal-entry quantiles of the heavy part); range q of a
-    // task is folded by a workgroup that runs on XCD q (HW_REG_XCC_ID, per-XCD task queues with
-    // stealing), so each XCD's private 4 MiB L2 caches one eighth of the gathered vector.  Partials
-    // partial[q][row] are combined in q order by pull_split_finalize_kernel.  The light rows keep
-    // the degree classes above (class ranges start at split_rows).
+    // XCD-sliced split of the heavy rows [0, split_rows) (degree >= split_min_degree) of a sliced
+    // CSR: see pull_slice_kernel (jg_pull.h).  The light rows keep the degree classes above (the
+    // light_* table covers rows [split_rows, rows)).
     int64_t split_rows = 0;
     int64_t split_tasks = 0;
+    int64_t chunk_rows = 0;    // rows [0, chunk_rows) are folded by chunk tasks (the task prefix)
+    int64_t chunk_tasks = 0;
+    int64_t col_space = 0;     // length of the gathered vector
     int64_t light_row_begin[kNumClasses] = {};  // the class table of rows [split_rows, rows)
     int64_t light_row_end[kNumClasses] = {};
     int64_t light_block_begin[kNumClasses + 1] = {};
-    int64_t col_bound[9] = {};
     DevBuf<int32_t> task_row;            // first row of each task
-    DevBuf<int32_t> task_meta;           // lanes per row (0: block-wide hub row) | rows << 8
-    DevBuf<uint32_t> split_off;          // [split_rows * 8] start of range q, relative to row_ptr[row]
-    DevBuf<unsigned long long> heads;    // [8] per-XCD queue heads (reset before each launch)
+    DevBuf<int32_t> task_meta;           // lanes per row | rows << 8, or 0 | (k | K << 12) << 8 (chunk)
+    DevBuf<int32_t> chunk_ptr;           // [chunk_rows + 1] first task of each chunked row
+    DevBuf<int64_t> slice_ptr;           // [8 * split_rows + 1] sub-row (q, r) = [ptr[q*H+r], ptr[q*H+r+1])
+    DevBuf<int32_t> slice_col;           // the heavy rows' entries, slice-major (8 sub-CSRs)
+    int64_t split_partial_len() const { return std::max<int64_t>(8 * (split_rows + chunk_tasks), 1); }
     bool lds_ok = false;  // the gathered vector's hot prefix is [0, hot) (single shard)
 };
 constexpr int kXcds = 8;
+// XCD slices of the column space: 128-byte lines of an fp64 vector (16 elements) are dealt to the 8
+// XCDs, so every slice holds an equal share of every hot region and one XCD's 4 MiB L2 only ever
+// caches its own eighth of the gathered vector.  Modes (Tune::slice_mode, fixed per CSR at build):
+//   0  slice = line mod 8 (every line of a slice has the same residue mod 8: few L2 channels)
+//   1  slice = xor of the line index's 3-bit groups (every residue appears in every slice)
+//   2  2 KiB blocks (16 lines) dealt round-robin
+constexpr int kSliceBits = 3;
+constexpr int64_t kSliceChunk = 1024;  // entries per chunk task of the sliced split (longer sub-rows are cut)
+__host__ __device__ __forceinline__ int col_slice(int64_t c, int mode) {
+    uint32_t line = (uint32_t)(c >> 4);
+    if (mode == 2) return (int)((line >> 4) & (kXcds - 1));
+    if (mode == 1) {
+        uint32_t x = line;
+        x ^= x >> 3;
+        x ^= x >> 6;
+        x ^= x >> 12;
+        x ^= x >> 24;
+        return (int)(x & (kXcds - 1));
+    }
+    return (int)(line & (kXcds - 1));
+}
 
 struct Ctx;
 
@@ -172,19 +196,18 @@ int allreduce_or(Graph& g, int flag);
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
 bool pull_split_launches();
 bool debug_plan();
-// JG_DEBUG_SPLIT=1: device counters of (XCD, column range) split tasks, printed by jg_graph_sync.
-unsigned long long* split_debug_counters();
-void split_debug_dump();
 
 // Performance knobs (jg_tune_set): variants of the pull kernel selectable at run time so that they
 // can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).
 struct Tune {
     int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
-    int pull_split = 0;   // XCD column split of the heavy rows: 0 off, 1 per-XCD queues, 2 static map
-                          // (read at build time too: the split plan is only built when non-zero)
-    int64_t split_min_degree = 2048;  // build time: rows of at least this degree are split
+    int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_slice_kernel): 0 off, 1 on
+                          // (read at build time too: the sliced in-CSR and split plan need it)
+    int64_t split_min_degree = 16;    // build time: rows of at least this degree are split
+    int slice_lds = 1;                // stage each slice's hottest lines in LDS (single shard)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
+    int slice_mode = 1;               // build time: col_slice mode of sliced CSRs
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

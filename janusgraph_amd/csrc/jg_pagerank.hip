@@ -19,6 +19,7 @@ namespace {
 
 struct PrOp {
     using T = double;
+    static constexpr bool kZeroIdentity = true;
     const double* __restrict__ x;      // contrib of the previous superstep, full length
     double* __restrict__ contrib_out;  // full length (owned slice written)
     double* __restrict__ rank;         // [rows]
@@ -70,8 +71,8 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
         if (sh.pr_rank.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.pr_hub_partial.size() != (size_t)std::max<int64_t>(sh.plan_in.num_chunks, 1))
             sh.pr_hub_partial.alloc(std::max<int64_t>(sh.plan_in.num_chunks, 1));
-        if (sh.pr_split_partial.size() != (size_t)std::max<int64_t>(kXcds * sh.plan_in.split_rows, 1))
-            sh.pr_split_partial.alloc(std::max<int64_t>(kXcds * sh.plan_in.split_rows, 1));
+        if (sh.pr_split_partial.size() != (size_t)sh.plan_in.split_partial_len())
+            sh.pr_split_partial.alloc(sh.plan_in.split_partial_len());
         const double initial = 1.0 / (double)vertex_count;
         if (sh.rows > 0) {
             pr_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.out_degree.get(), sh.rows,

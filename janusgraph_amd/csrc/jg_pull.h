@@ -68,31 +68,78 @@ struct GlobalGather {
     const Op& op;
     __device__ __forceinline__ typename Op::T operator()(int32_t c) const { return op.gather(c); }
 };
+// LDS pointers keep address space 3: through a generic pointer the compiler emits flat loads, which
+// go through the TA/TD like global loads and defeat the point of staging.
+template <class T>
+using lds_ptr = __attribute__((address_space(3))) T*;
+
 template <class Op>
 struct LdsGather {
     const Op& op;
-    const typename Op::T* lds;
+    lds_ptr<const typename Op::T> lds;
     int32_t hot;
     __device__ __forceinline__ typename Op::T operator()(int32_t c) const { return c < hot ? lds[c] : op.gather(c); }
 };
 
 // Fold col[j..j1) with stride `stride`; U gathers in flight per lane, folded in index order.
+// Software-pipelined: the col batch of iteration i+1 is loaded while the gathers of iteration i are
+// in flight, so a long row pays one round trip per batch instead of two.  The last, partial batch is
+// not walked one entry at a time: its out-of-range slots re-read the row's last entry (a cache hit)
+// and are dropped from the fold by a select, so every batch is branch-free.
+template <class Op, int U, bool NT>
+__device__ __forceinline__ void load_cols(const int32_t* __restrict__ col, int64_t j, int64_t j1, int stride,
+                                          int32_t (&c)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t k = j + u * (int64_t)stride;
+        c[u] = load_col<NT>(col, k < j1 ? k : j1 - 1);
+    }
+}
+
+template <class G, class = void>
+struct is_split_gather { static constexpr bool value = false; };
+template <class G>
+struct is_split_gather<G, decltype((void)G::kSplit)> { static constexpr bool value = G::kSplit; };
+
 template <class Op, int U, bool NT, class G>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& gather, const int32_t* __restrict__ col,
                                                        int64_t j, int64_t j1, int stride) {
     using T = typename Op::T;
     T acc = op.identity();
-    for (; j + (U - 1) * (int64_t)stride < j1; j += U * (int64_t)stride) {
-        int32_t c[U];
+    if (j >= j1) return acc;
+    int32_t c[U];
+    load_cols<Op, U, NT>(col, j, j1, stride, c);
+    for (;;) {
         T v[U];
+        const int64_t jn = j + U * (int64_t)stride;
+        if constexpr (is_split_gather<G>::value) {
+            // Wait for the whole col batch once (the empty asm needs every c[u] in a register), so
+            // the masked global loads below issue back to back: exec-masked, a hot lane costs the
+            // TA/TD nothing (an out-of-range buffer lane still costs a TD cycle).  The LDS reads are
+            // unconditional (cold lanes read the identity cell) and land in their own registers.
+            static_assert(U == 4, "split gathers are written for U == 4");
+            asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]));
+            T vg[U], vl[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) c[u] = load_col<NT>(col, j + u * (int64_t)stride);
+            for (int u = 0; u < U; ++u) vl[u] = gather.hot(c[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
+            for (int u = 0; u < U; ++u) vg[u] = gather.cold(c[u]);
+            load_cols<Op, U, NT>(col, jn, j1, stride, c);
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc = op.combine(acc, v[u]);
+            for (int u = 0; u < U; ++u) v[u] = op.combine(vl[u], vg[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
+            load_cols<Op, U, NT>(col, jn, j1, stride, c);  // clamped: unconditional keeps vmcnt counting exact
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const T t = op.combine(acc, v[u]);
+            acc = (j + u * (int64_t)stride < j1) ? t : acc;
+        }
+        j = jn;
+        if (j >= j1) break;
     }
-    for (; j < j1; j += stride) acc = op.combine(acc, gather(load_col<NT>(col, j)));
     return acc;
 }
 
@@ -186,7 +233,7 @@ template <class Op, int U, bool NT>
 __global__ __launch_bounds__(kLdsThreads) void pull_lds_kernel(PullArgs a, Op op, int32_t hot) {
     using T = typename Op::T;
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    T* lds = reinterpret_cast<T*>(lds_raw);
+    lds_ptr<T> lds = (lds_ptr<T>)lds_raw;
     const T* src = op.vec();
     for (int i = threadIdx.x; i < hot; i += kLdsThreads) lds[i] = src[i];
     __syncthreads();
@@ -212,150 +259,160 @@ __global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T
     }
 }
 
-// ---------------- XCD column split of the heavy rows (PullPlan::split_*) ----------------
-struct SplitArgs {
-    const int64_t* __restrict__ row_ptr;
-    const int32_t* __restrict__ col;
+// ---------------- XCD-sliced split of the heavy rows (PullPlan::split_*) ----------------
+// The entries of every heavy row of a sliced CSR are grouped by col_slice (mode 1: each aligned
+// group of 8 lines of the gathered vector gives one line to every slice).  A wave item is (task t,
+// slice q); every item of slice q runs in a workgroup b with b mod 8 == q, which the dispatcher
+// deals to one XCD (speed only: any placement gives the same result), so each XCD's L2 only ever
+// holds its own eighth of the vector.  On one shard the workgroup also stages the hottest lines of
+// its slice (the first kSliceLdsLines line groups, i.e. ids < 16 * 8 * kSliceLdsLines) in LDS, and
+// those gathers never leave the CU: the superstep is bound by TCP->L2 requests in flight
+// (PMC: TA/TD ~95% busy stalled on the TCP), not by bytes.
+//   task kind R (meta & 0xff = L lanes per row, meta >> 8 = rows): 64/L consecutive rows, sub-row
+//             (r, q) folded by L lanes, written to partial[q * split_rows + r]
+//   task kind C (meta & 0xff = 0, meta >> 8 = k | K << 12): chunk k of K of sub-row (r, q), folded by
+//             the wave, written to chunk_partial[t * 8 + q]; the chunked rows are the prefix
+//             [0, chunk_rows) and their tasks the prefix of the task list (chunk_ptr[r] = first task)
+// pull_slice_finalize_kernel folds the 8 slices (and the chunks of chunked rows) in fixed order.
+constexpr int kSliceThreads = 1024;                   // one workgroup per CU
+constexpr int kSliceLdsBytes = 160 * 1024;            // all of the CU's LDS
+
+struct SliceArgs {
+    const int64_t* __restrict__ slice_ptr;  // [8 * rows + 1], slice-major
+    const int32_t* __restrict__ col;        // slice_col
     const int32_t* __restrict__ task_row;
     const int32_t* __restrict__ task_meta;
-    const uint32_t* __restrict__ split_off;
-    unsigned long long* __restrict__ heads;
     int64_t ntasks;
-    int64_t rows;  // heavy rows
-    unsigned long long* __restrict__ dbg;  // JG_DEBUG_SPLIT: [8 xcc][8 ranges] task counts (nullable)
+    int64_t rows;       // split (heavy) rows
+    uint32_t vec_bytes;  // bytes of the gathered vector (buffer resource range)
 };
 
-// XCD (0..7) the calling workgroup runs on.  Placement is only a speed hint: any XCD may take any
-// range (stealing), results do not depend on it.
-__device__ __forceinline__ int xcc_id() {
-    unsigned v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return (int)(v & 7u);
+// Sub-row (r, q): [j0, j1) of col.
+__device__ __forceinline__ void slice_segment(const SliceArgs& a, int64_t r, int q, int64_t& j0, int64_t& j1) {
+    const int64_t i = (int64_t)q * a.rows + r;
+    j0 = a.slice_ptr[i];
+    j1 = a.slice_ptr[i + 1];
 }
 
-__device__ __forceinline__ void split_segment(const SplitArgs& a, int64_t r, int q, int64_t& j0, int64_t& j1) {
-    const int64_t base = a.row_ptr[r];
-    j0 = base + a.split_off[r * kXcds + q];
-    j1 = q == kXcds - 1 ? a.row_ptr[r + 1] : base + a.split_off[r * kXcds + q + 1];
-}
-
-template <class Op, int L, bool NT>
-__device__ __forceinline__ void split_rows_task(const SplitArgs& a, const Op& op, int q, int64_t row0, int nrows,
-                                                typename Op::T* __restrict__ partial) {
+// Gathers of slice q: ids below `hot` come from the LDS image of the slice's first lines (line group
+// c >> 7 holds one line of this slice; it sits at LDS line c >> 7), the rest from global memory.
+// Split form for fold_strided: hot(c) / cold(c) each return identity() for the other kind, and
+// combine(hot, cold) is the gathered value (exact: combine(x, identity) == x).
+template <class Op>
+struct SliceLdsGather {
+    static constexpr bool kSplit = true;
     using T = typename Op::T;
-    const int sub = threadIdx.x % L;
-    const int local = threadIdx.x / L;
+    const Op& op;
+    lds_ptr<const T> lds;
+    int32_t hot_ids;
+    // Cold lanes read the identity cell just past the staged lines: no select, so the compiler
+    // cannot turn the read into a branch.
+    __device__ __forceinline__ T hot(int32_t c) const {
+        return lds[c < hot_ids ? (((c >> 7) << 4) | (c & 15)) : (hot_ids >> 3)];
+    }
+    // Only cold lanes load (exec-masked); the others keep identity().
+    __device__ __forceinline__ T cold(int32_t c) const {
+        T v = op.identity();
+        if (c >= hot_ids) v = op.gather(c);
+        return v;
+    }
+};
+
+template <class Op, int L, int U, class G>
+__device__ __forceinline__ void slice_rows_item(const SliceArgs& a, const Op& op, const G& gather, int q, int64_t row0,
+                                                int nrows, int lane, typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    const int sub = lane % L;
+    const int local = lane / L;
     const int64_t r = row0 + local;
     const bool valid = local < nrows;
     T acc = op.identity();
     if (valid && op.active(r)) {
         int64_t j0, j1;
-        split_segment(a, r, q, j0, j1);
-        acc = fold_strided<Op, 4, NT>(op, a.col, j0 + sub, j1, L);
+        slice_segment(a, r, q, j0, j1);
+        acc = fold_strided<Op, U, false>(op, gather, a.col, j0 + sub, j1, L);
     }
 #pragma unroll
     for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
     if (valid && sub == 0) partial[(int64_t)q * a.rows + r] = acc;
 }
 
-template <class Op, bool NT>
-__device__ __forceinline__ void split_hub_task(const SplitArgs& a, const Op& op, int q, int64_t r,
-                                               typename Op::T* __restrict__ partial, typename Op::T* red) {
+template <class Op, int U, bool LDS>
+__global__ __launch_bounds__(kSliceThreads) void pull_slice_kernel(SliceArgs a, Op op, typename Op::T* __restrict__ partial,
+                                                                   typename Op::T* __restrict__ chunk_partial,
+                                                                   int32_t hot) {
     using T = typename Op::T;
-    T acc = op.identity();
-    if (op.active(r)) {
-        int64_t j0, j1;
-        split_segment(a, r, q, j0, j1);
-        acc = fold_strided<Op, 4, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock);
-    }
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
-    if (lane_id() == 0) red[wave_id()] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        T t = red[0];
-#pragma unroll
-        for (int w = 1; w < kBlock / kWave; ++w) t = op.combine(t, red[w]);
-        partial[(int64_t)q * a.rows + r] = t;
-    }
-}
-
-// Workgroups loop over (task, range) items: their own XCD's queue first, then the others'.  Every
-// item is processed exactly once and written to its own partial slot, so the result is independent
-// of placement and timing.  Every workgroup exits once all eight queues are drained.
-template <class Op, bool NT>
-__global__ __launch_bounds__(kBlock) void pull_split_kernel(SplitArgs a, Op op, typename Op::T* __restrict__ partial) {
-    using T = typename Op::T;
-    __shared__ long long s_task;
-    __shared__ int s_q;
-    __shared__ T red[kBlock / kWave];
-    int q = xcc_id(), tried = 0;  // thread 0's dequeue state
-    for (;;) {
-        if (threadIdx.x == 0) {
-            long long t = -1;
-            while (tried < kXcds) {
-                const unsigned long long k = atomicAdd(&a.heads[q], 1ull);
-                if ((long long)k < a.ntasks) { t = (long long)k; break; }
-                ++tried;
-                q = (q + 1) & (kXcds - 1);
-            }
-            s_task = t;
-            s_q = q;
+    extern __shared__ __align__(16) unsigned char slice_lds_raw[];
+    lds_ptr<T> lds = (lds_ptr<T>)slice_lds_raw;
+    const int q = (int)(blockIdx.x & (kXcds - 1));
+    const int64_t g = blockIdx.x >> 3, G = gridDim.x >> 3;
+    if constexpr (LDS) {
+        // LDS line i = the line of slice q in line group i (mode-1 slices permute each aligned group)
+        const T* src = op.vec();
+        const int nl = hot >> 7;  // line groups staged
+        for (int i = threadIdx.x; i < nl * 16; i += kSliceThreads) {
+            const int grp = i >> 4;
+            const int line = grp * 8 + (q ^ col_slice((int64_t)grp * 128, 1));
+            lds[i] = src[line * 16 + (i & 15)];
         }
+        if (threadIdx.x == 0) lds[nl * 16] = op.identity();  // the cold lanes' cell (SliceLdsGather::hot)
         __syncthreads();
-        const long long t = s_task;
-        const int qq = s_q;
-        __syncthreads();
-        if (t < 0) break;
-        if (a.dbg && threadIdx.x == 0) atomicAdd(&a.dbg[xcc_id() * kXcds + qq], 1ull);
+    }
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    constexpr int kWaves = kSliceThreads / kWave;
+    for (int64_t t = g * kWaves + wave; t < a.ntasks; t += G * kWaves) {
         const int64_t row0 = a.task_row[t];
         const int meta = a.task_meta[t];
-        const int nrows = meta >> 8;
-        switch (meta & 0xff) {
-            case 0: split_hub_task<Op, NT>(a, op, qq, row0, partial, red); __syncthreads(); break;
-            case 64: split_rows_task<Op, 64, NT>(a, op, qq, row0, nrows, partial); break;
-            case 32: split_rows_task<Op, 32, NT>(a, op, qq, row0, nrows, partial); break;
-            case 16: split_rows_task<Op, 16, NT>(a, op, qq, row0, nrows, partial); break;
-            case 8: split_rows_task<Op, 8, NT>(a, op, qq, row0, nrows, partial); break;
-            case 4: split_rows_task<Op, 4, NT>(a, op, qq, row0, nrows, partial); break;
-            default: split_rows_task<Op, 2, NT>(a, op, qq, row0, nrows, partial); break;
-        }
+        const int L = meta & 0xff;
+        const int arg = meta >> 8;
+        auto run = [&](const auto& gather) {
+            switch (L) {
+                case 0: {  // chunk k of K of sub-row (row0, q)
+                    const int k = arg & 0xfff, K = arg >> 12;
+                    int64_t j0, j1;
+                    slice_segment(a, row0, q, j0, j1);
+                    const int64_t len = j1 - j0;
+                    const int64_t c0 = j0 + len * k / K, c1 = j0 + len * (k + 1) / K;
+                    T acc = op.active(row0) ? fold_strided<Op, U, false>(op, gather, a.col, c0 + lane, c1, kWave)
+                                            : op.identity();
+#pragma unroll
+                    for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
+                    if (lane == 0) chunk_partial[t * kXcds + q] = acc;
+                    break;
+                }
+                case 64: slice_rows_item<Op, 64, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                case 32: slice_rows_item<Op, 32, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                case 16: slice_rows_item<Op, 16, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                case 8: slice_rows_item<Op, 8, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                case 4: slice_rows_item<Op, 4, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                case 2: slice_rows_item<Op, 2, U>(a, op, gather, q, row0, arg, lane, partial); break;
+                default: slice_rows_item<Op, 1, U>(a, op, gather, q, row0, arg, lane, partial); break;
+            }
+        };
+        if constexpr (LDS) run(SliceLdsGather<Op>{op, lds, hot});
+        else run(GlobalGather<Op>{op});
     }
 }
 
-// Static variant: block b folds range (b mod 8) of task (b div 8).  The dispatcher deals blocks
-// round-robin over the XCDs, so the blocks of one range share an XCD (speed only; any placement gives
-// the same result).  No queue atomics.
-template <class Op, bool NT>
-__global__ __launch_bounds__(kBlock) void pull_split_static_kernel(SplitArgs a, Op op,
-                                                                   typename Op::T* __restrict__ partial) {
-    using T = typename Op::T;
-    __shared__ T red[kBlock / kWave];
-    const int64_t b = blockIdx.x;
-    const int qq = (int)(b & (kXcds - 1));
-    const int64_t t = b >> 3;
-    if (a.dbg && threadIdx.x == 0) atomicAdd(&a.dbg[xcc_id() * kXcds + qq], 1ull);
-    const int64_t row0 = a.task_row[t];
-    const int meta = a.task_meta[t];
-    const int nrows = meta >> 8;
-    switch (meta & 0xff) {
-        case 0: split_hub_task<Op, NT>(a, op, qq, row0, partial, red); break;
-        case 64: split_rows_task<Op, 64, NT>(a, op, qq, row0, nrows, partial); break;
-        case 32: split_rows_task<Op, 32, NT>(a, op, qq, row0, nrows, partial); break;
-        case 16: split_rows_task<Op, 16, NT>(a, op, qq, row0, nrows, partial); break;
-        case 8: split_rows_task<Op, 8, NT>(a, op, qq, row0, nrows, partial); break;
-        case 4: split_rows_task<Op, 4, NT>(a, op, qq, row0, nrows, partial); break;
-        default: split_rows_task<Op, 2, NT>(a, op, qq, row0, nrows, partial); break;
-    }
-}
-
+// Row r: fold the 8 slices in q order; a chunked row folds each slice's chunks in k order first.
 template <class Op>
-__global__ void pull_split_finalize_kernel(int64_t rows, Op op, const typename Op::T* __restrict__ partial) {
+__global__ void pull_slice_finalize_kernel(int64_t rows, int64_t chunk_rows, const int32_t* __restrict__ chunk_ptr,
+                                           Op op, const typename Op::T* __restrict__ partial,
+                                           const typename Op::T* __restrict__ chunk_partial) {
     using T = typename Op::T;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
-        T acc = partial[r];
+        T acc = op.identity();
+        if (r < chunk_rows) {
+            const int t0 = chunk_ptr[r], t1 = chunk_ptr[r + 1];
+            for (int q = 0; q < kXcds; ++q) {
+                T sq = op.identity();
+                for (int t = t0; t < t1; ++t) sq = op.combine(sq, chunk_partial[(int64_t)t * kXcds + q]);
+                acc = op.combine(acc, sq);
+            }
+        } else {
 #pragma unroll
-        for (int q = 1; q < kXcds; ++q) acc = op.combine(acc, partial[(int64_t)q * rows + r]);
+            for (int q = 0; q < kXcds; ++q) acc = op.combine(acc, partial[(int64_t)q * rows + r]);
+        }
         op.finalize(r, acc);
     }
 }
@@ -368,59 +425,37 @@ template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
                  Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr) {
     using T = typename Op::T;
-    const bool split = tune().pull_split && tune().pull_lds == 0 && plan.split_rows > 0 && split_partial != nullptr;
+    const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
     PullArgs a = make_pull_args(csr, plan, split);
     const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
     if (split) {
-        SplitArgs sa{csr.row_ptr.get(), csr.col.get(), plan.task_row.get(), plan.task_meta.get(),
-                     plan.split_off.get(), plan.heads.get(), plan.split_tasks, plan.split_rows,
-                     split_debug_counters()};
-        if (tune().pull_split == 2) {  // static blockIdx -> range mapping
-            const unsigned grid = (unsigned)(plan.split_tasks * kXcds);
-            if (tune().pull_nt) pull_split_static_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
-            else pull_split_static_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
-        } else {  // per-XCD dynamic queues
-            JG_HIP(hipMemsetAsync(plan.heads.get(), 0, kXcds * sizeof(unsigned long long), s));
-            const unsigned grid = (unsigned)std::min<int64_t>(plan.split_tasks * kXcds, 256 * 8);
-            if (tune().pull_nt) pull_split_kernel<Op, true><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
-            else pull_split_kernel<Op, false><<<grid, kBlock, 0, s>>>(sa, op, split_partial);
-        }
-        JG_LAUNCH_CHECK();
-    }
-    if (!split && tune().pull_lds > 0 && plan.lds_ok) {  // LDS-cached hot prefix (single shard)
-        const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
-        if (plan.num_chunks > 0) {  // hub chunks keep the 256-thread kernel (block-wide reductions)
-            if (tune().pull_nt) pull_kernel<Op, 4, true><<<(unsigned)plan.num_chunks, kBlock, 0, s>>>(a, op, hub_partial);
-            else pull_kernel<Op, 4, false><<<(unsigned)plan.num_chunks, kBlock, 0, s>>>(a, op, hub_partial);
-            JG_LAUNCH_CHECK();
-        }
-        const size_t bytes = (size_t)hot * sizeof(T);
-        const unsigned grid = (unsigned)device_cu_count();
-        if (tune().pull_nt) {
-            static bool attr = false;
-            if (!attr) {
-                JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
-                attr = true;
+        SliceArgs sa{plan.slice_ptr.get(), plan.slice_col.get(), plan.task_row.get(), plan.task_meta.get(),
+                     plan.split_tasks, plan.split_rows,
+                     (uint32_t)std::min<int64_t>(plan.col_space * (int64_t)sizeof(T), 0xffffffffll)};
+        T* chunk_partial = split_partial + kXcds * plan.split_rows;
+        const unsigned grid = (unsigned)(device_cu_count() / kXcds * kXcds);
+        const int64_t hot_max = (int64_t)(kSliceLdsBytes / sizeof(T) - 16) * kXcds;  // full LDS, 1 identity line
+        const bool lds_ok = plan.lds_ok && tune().slice_lds && plan.col_space * (int64_t)sizeof(T) < (1ll << 32);
+        const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) >> 7 << 7) : 0;
+        bool launched = false;
+        if constexpr (Op::kZeroIdentity) {
+            if (hot > 0) {
+                static bool attr = false;
+                if (!attr) {
+                    JG_HIP(hipFuncSetAttribute((const void*)pull_slice_kernel<Op, 4, true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kSliceLdsBytes));
+                    attr = true;
+                }
+                const size_t bytes = (size_t)(hot / kXcds + 1) * sizeof(T);
+                pull_slice_kernel<Op, 4, true><<<grid, kSliceThreads, bytes, s>>>(sa, op, split_partial, chunk_partial,
+                                                                                 hot);
+                launched = true;
             }
-            pull_lds_kernel<Op, 4, true><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
-        } else {
-            static bool attr = false;
-            if (!attr) {
-                JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
-                attr = true;
-            }
-            pull_lds_kernel<Op, 4, false><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
         }
+        if (!launched)
+            pull_slice_kernel<Op, 4, false><<<grid, kSliceThreads, 0, s>>>(sa, op, split_partial, chunk_partial, 0);
         JG_LAUNCH_CHECK();
-        if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
-        if (plan.num_hub_rows > 0) {
-            pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
-            JG_LAUNCH_CHECK();
-        }
-        return;
     }
     auto launch = [&](unsigned grid) {
         const int u = tune().pull_unroll;
@@ -434,7 +469,20 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         }
         JG_LAUNCH_CHECK();
     };
-    if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
+    if (!split && tune().pull_lds > 0 && plan.lds_ok) {  // LDS-cached hot prefix (single shard, unsliced)
+        const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
+        if (plan.num_chunks > 0) launch((unsigned)plan.num_chunks);  // hub chunks: blocks [0, num_chunks)
+        const size_t bytes = (size_t)hot * sizeof(T);
+        const unsigned grid = (unsigned)device_cu_count();
+        static bool attr = false;
+        if (!attr) {
+            JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
+            attr = true;
+        }
+        pull_lds_kernel<Op, 4, false><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
+        JG_LAUNCH_CHECK();
+    } else if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
         for (int c = 0; c < kNumClasses; ++c) {
             const int64_t b0 = a.class_block_begin[c], b1 = a.class_block_begin[c + 1];
             if (b1 <= b0) continue;
@@ -450,7 +498,9 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         JG_LAUNCH_CHECK();
     }
     if (split) {
-        pull_split_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, split_partial);
+        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(
+            plan.split_rows, plan.chunk_rows, plan.chunk_ptr.get(), op, split_partial,
+            split_partial + kXcds * plan.split_rows);
         JG_LAUNCH_CHECK();
     }
 }

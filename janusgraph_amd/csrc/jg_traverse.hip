@@ -251,6 +251,7 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
 struct MsBfsOp {
     using T = unsigned long long;
+    static constexpr bool kZeroIdentity = true;  // OR: identity 0
     const T* __restrict__ F;    // frontier words of the previous level, full length
     T* __restrict__ Fout;       // full length, owned slice written
     T* __restrict__ visited;    // [rows]
@@ -526,7 +527,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.depth.alloc(std::max<int64_t>(sh.rows * ns, 1));
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
-                t.split.alloc(std::max<int64_t>(kXcds * plan.split_rows, 1));
+                t.split.alloc(plan.split_partial_len());
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));

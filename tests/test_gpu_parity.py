@@ -270,15 +270,17 @@ def test_errors_are_status_codes(ctx):
         g.pagerank_step(1)
 
 
-@pytest.mark.parametrize("mode", ["lds", "split_queue", "split_static"])
+@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_deg16"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
-    """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: LDS-staged hot prefix,
-    XCD column split with per-XCD queues, and with the static blockIdx mapping."""
+    """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
+    LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
-    knobs = {"lds": [("pull_split", 0), ("pull_lds", 20480)],
-             "split_queue": [("pull_lds", 0), ("split_min_degree", 64), ("pull_split", 1)],
-             "split_static": [("pull_lds", 0), ("split_min_degree", 64), ("pull_split", 2)]}[mode]
+    knobs = {"plain": [("pull_split", 0)],
+             "lds": [("pull_split", 0), ("pull_lds", 20480)],
+             "split_nolds": [("pull_split", 1), ("slice_lds", 0), ("split_min_degree", 64)],
+             "split_lds": [("pull_split", 1), ("slice_lds", 1), ("split_min_degree", 64)],
+             "split_deg16": [("pull_split", 1), ("slice_lds", 1), ("split_min_degree", 16)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -300,5 +302,6 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         c.close()
     finally:
         _lib.tune_set("pull_lds", 0)
-        _lib.tune_set("pull_split", 0)
-        _lib.tune_set("split_min_degree", 2048)
+        _lib.tune_set("pull_split", 1)
+        _lib.tune_set("slice_lds", 1)
+        _lib.tune_set("split_min_degree", 16)
