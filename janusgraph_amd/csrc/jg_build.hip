@@ -406,52 +406,6 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     JG_HIP(hipStreamSynchronize(s));
 }
 
-// Tasks of the XCD-sliced split, shared by the 8 slices (pull_slice_kernel): rows whose per-slice
-// length d/8 exceeds 2 kSliceChunk are cut into K chunk tasks each (the degree-sorted prefix); the
-// rest are grouped 64/L consecutive rows to a wave, L lanes per row with ~4 entries per lane.
-static void build_split_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t heavy) {
-    hipStream_t s = sh.stream;
-    plan.split_rows = plan.split_tasks = plan.chunk_rows = plan.chunk_tasks = 0;
-    if (heavy <= 0) return;
-    std::vector<int64_t> rp(heavy + 1);
-    copy_d2h(rp.data(), csr.row_ptr.get(), (heavy + 1) * sizeof(int64_t), s);
-    plan.split_rows = heavy;
-    std::vector<int32_t> trow, tmeta, cptr(1, 0);
-    int64_t r = 0;
-    for (; r < heavy; ++r) {
-        const int64_t per = (rp[r + 1] - rp[r]) / kXcds;
-        if (per <= 2 * kSliceChunk) break;
-        const int64_t K = std::min<int64_t>((per + kSliceChunk - 1) / kSliceChunk, 4095);
-        for (int64_t k = 0; k < K; ++k) {
-            trow.push_back((int32_t)r);
-            tmeta.push_back((int32_t)((k | (K << 12)) << 8));
-        }
-        cptr.push_back((int32_t)trow.size());
-    }
-    plan.chunk_rows = r;
-    plan.chunk_tasks = (int64_t)trow.size();
-    auto lanes_for = [](int64_t per) {
-        int L = 1;
-        while (L < 64 && 4 * L < per) L *= 2;
-        return L;
-    };
-    while (r < heavy) {
-        const int L = lanes_for((rp[r + 1] - rp[r]) / kXcds);
-        int64_t k = 1;
-        while (k < kWave / L && r + k < heavy && lanes_for((rp[r + k + 1] - rp[r + k]) / kXcds) == L) ++k;
-        trow.push_back((int32_t)r);
-        tmeta.push_back(L | (int32_t)(k << 8));
-        r += k;
-    }
-    plan.split_tasks = (int64_t)trow.size();
-    plan.task_row.alloc(trow.size());
-    plan.task_meta.alloc(tmeta.size());
-    plan.chunk_ptr.alloc(cptr.size());
-    copy_h2d(plan.task_row.get(), trow.data(), trow.size() * sizeof(int32_t), s);
-    copy_h2d(plan.task_meta.get(), tmeta.data(), tmeta.size() * sizeof(int32_t), s);
-    copy_h2d(plan.chunk_ptr.get(), cptr.data(), cptr.size() * sizeof(int32_t), s);
-}
-
 // Sub-row lengths in slice-major order: len[q * H + r] = entries of row r in slice q.
 __global__ void slice_len_kernel(const int64_t* __restrict__ rp, const uint32_t* __restrict__ off, int64_t H,
                                  int32_t* __restrict__ len) {
@@ -464,7 +418,23 @@ __global__ void slice_len_kernel(const int64_t* __restrict__ rp, const uint32_t*
     }
 }
 
-// slice_col[slice_ptr[q * H + r] ...] = the slice-q entries of row r (one wave per sub-row).
+struct SliceBases {
+    int64_t begin[kXcds];     // aligned first entry of each slice
+    int64_t end[kXcds];       // end entry of each slice
+    int64_t base[kXcds + 1];  // first task of each slice
+};
+
+// sp[q*(H+1) + r] = raw[q*H + r] - raw[q*H] + begin[q], r in [0, H] (raw[q*H + H] is slice q's end).
+__global__ void slice_ptr_kernel(const int64_t* __restrict__ raw, int64_t H, SliceBases b, int64_t* __restrict__ sp) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (H + 1) * kXcds;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i / (H + 1));
+        const int64_t r = i % (H + 1);
+        sp[i] = raw[(int64_t)q * H + r] - raw[(int64_t)q * H] + b.begin[q];
+    }
+}
+
+// slice_col[sp[q][r] ...] = the slice-q entries of row r (one wave per sub-row).
 __global__ void slice_copy_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                   const uint32_t* __restrict__ off, int64_t H, const int64_t* __restrict__ sp,
                                   int32_t* __restrict__ scol) {
@@ -473,32 +443,123 @@ __global__ void slice_copy_kernel(const int64_t* __restrict__ rp, const int32_t*
         const int q = (int)(i / H);
         const int64_t r = i % H;
         const int64_t src = rp[r] + off[r * kXcds + q];
-        const int64_t dst = sp[i], n = sp[i + 1] - sp[i];
+        const int64_t* p = sp + (int64_t)q * (H + 1) + r;
+        const int64_t dst = p[0], n = p[1] - p[0];
         for (int64_t k = lane_id(); k < n; k += kWave) scol[dst + k] = col[src + k];
     }
 }
 
-// Slice-major copy of the heavy rows (8 sub-CSRs over rows [0, H)): a wave folding consecutive rows
-// of one slice reads one contiguous col span.
-static void build_slice_csr(Shard& sh, const Csr& csr, PullPlan& plan) {
+__global__ void nonempty_kernel(const int32_t* __restrict__ len, int64_t n, int32_t* __restrict__ flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        flag[i] = len[i] > 0;
+}
+
+// Number the non-empty sub-rows slice-major: sub_index[q*H + r] = k (or -1), cstart[k] = first entry.
+__global__ void sub_number_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t H,
+                                  const int64_t* __restrict__ sp, int32_t* __restrict__ sub_index,
+                                  int64_t* __restrict__ cstart) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < H * kXcds; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = i / H, r = i % H;
+        if (len[i] > 0) {
+            sub_index[i] = (int32_t)num[i];
+            cstart[num[i]] = sp[q * (H + 1) + r];
+        } else {
+            sub_index[i] = -1;
+        }
+    }
+}
+
+// Per task: j0 = the non-empty sub-row holding its first entry, carry = it started earlier, and
+// heads[t][l] = row-start bits of lane l's kMergeEpl entries (bit 0 of lane 0 always set).
+__global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64_t* __restrict__ nzb, SliceBases b,
+                                 int32_t* __restrict__ meta, uint8_t* __restrict__ heads) {
+    constexpr int kEpl = kMergeTask / kWave;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < b.base[kXcds];
+         t += (int64_t)gridDim.x * blockDim.x) {
+        int q = 0;
+        while (q < kXcds - 1 && t >= b.base[q + 1]) ++q;
+        const int64_t e0 = b.begin[q] + (t - b.base[q]) * kMergeTask;
+        const int64_t e1 = min(e0 + kMergeTask, b.end[q]);
+        int64_t lo = nzb[q], hi = nzb[q + 1];  // first sub-row starting after e0
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (cstart[mid] <= e0) lo = mid + 1; else hi = mid;
+        }
+        const int64_t j0 = lo - 1;
+        meta[2 * t] = (int32_t)j0;
+        meta[2 * t + 1] = cstart[j0] < e0 ? 1 : 0;
+        uint8_t h[kWave];
+        for (int l = 0; l < kWave; ++l) h[l] = 0;
+        h[0] = 1;
+        for (int64_t j = j0 + 1; j < nzb[q + 1] && cstart[j] < e1; ++j) {
+            const int pos = (int)(cstart[j] - e0);
+            h[pos / kEpl] |= (uint8_t)(1u << (pos % kEpl));
+        }
+        for (int l = 0; l < kWave; ++l) heads[t * kWave + l] = h[l];
+    }
+}
+
+// The sliced split of the heavy rows [0, H): slice-major sub-CSRs, each slice's start aligned to a
+// merge task, so a task never spans two slices and its col loads are 16-byte aligned.
+static void build_slice_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t H) {
     hipStream_t s = sh.stream;
-    const int64_t H = plan.split_rows;
+    plan.split_rows = plan.split_tasks = plan.split_subrows = 0;
     if (H <= 0) return;
-    DevBuf<uint32_t> off(H * kXcds);
-    DevBuf<int32_t> len(H * kXcds);
-    split_off_kernel<<<grid_for(H * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), H, csr.slice_mode,
-                                                            off.get());
+    plan.split_rows = H;
+    const int64_t NS = H * kXcds;
+    DevBuf<uint32_t> off(NS);
+    DevBuf<int32_t> len(NS);
+    DevBuf<int64_t> raw(NS + 1);
+    split_off_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), H, csr.slice_mode, off.get());
     JG_LAUNCH_CHECK();
-    slice_len_kernel<<<grid_for(H * kXcds), kBlock, 0, s>>>(csr.row_ptr.get(), off.get(), H, len.get());
+    slice_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), off.get(), H, len.get());
     JG_LAUNCH_CHECK();
-    plan.slice_ptr.alloc(H * kXcds + 1);
-    prim::exclusive_scan(len.get(), plan.slice_ptr.get(), H * kXcds, s);
-    int64_t nnz = 0;
-    copy_d2h(&nnz, plan.slice_ptr.get() + H * kXcds, sizeof(int64_t), s);
-    plan.slice_col.alloc(std::max<int64_t>(nnz, 1));
-    slice_copy_kernel<<<grid_for(H * kXcds * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), off.get(), H,
-                                                                     plan.slice_ptr.get(), plan.slice_col.get());
+    prim::exclusive_scan(len.get(), raw.get(), NS, s);
+    int64_t bounds[kXcds + 1];
+    for (int q = 0; q <= kXcds; ++q) copy_d2h(&bounds[q], raw.get() + (int64_t)q * H, sizeof(int64_t), s);
+    SliceBases b{};
+    int64_t at = 0;
+    b.base[0] = 0;
+    for (int q = 0; q < kXcds; ++q) {
+        const int64_t n = bounds[q + 1] - bounds[q];
+        const int64_t tasks = (n + kMergeTask - 1) / kMergeTask;
+        b.begin[q] = plan.slice_begin[q] = at;
+        b.end[q] = plan.slice_end[q] = at + n;
+        b.base[q + 1] = b.base[q] + tasks;
+        at += tasks * kMergeTask;
+    }
+    for (int q = 0; q <= kXcds; ++q) plan.slice_task_base[q] = b.base[q];
+    plan.split_tasks = b.base[kXcds];
+    DevBuf<int64_t> sp((H + 1) * kXcds);
+    slice_ptr_kernel<<<grid_for((H + 1) * kXcds), kBlock, 0, s>>>(raw.get(), H, b, sp.get());
     JG_LAUNCH_CHECK();
+    plan.slice_col.alloc(at + kMergeTask);  // one task of padding: the last task's aligned loads
+    JG_HIP(hipMemsetAsync(plan.slice_col.get(), 0, plan.slice_col.bytes(), s));
+    slice_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), off.get(), H, sp.get(),
+                                                              plan.slice_col.get());
+    JG_LAUNCH_CHECK();
+    // number the non-empty sub-rows
+    DevBuf<int32_t> flag(NS);
+    DevBuf<int64_t> num(NS + 1);
+    nonempty_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), NS, flag.get());
+    JG_LAUNCH_CHECK();
+    prim::exclusive_scan(flag.get(), num.get(), NS, s);
+    int64_t nzb[kXcds + 1];
+    for (int q = 0; q <= kXcds; ++q) copy_d2h(&nzb[q], num.get() + (int64_t)q * H, sizeof(int64_t), s);
+    plan.split_subrows = nzb[kXcds];
+    DevBuf<int64_t> cstart(std::max<int64_t>(plan.split_subrows, 1)), d_nzb(kXcds + 1);
+    copy_h2d(d_nzb.get(), nzb, sizeof nzb, s);
+    plan.sub_index.alloc(NS);
+    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), H, sp.get(), plan.sub_index.get(),
+                                                      cstart.get());
+    JG_LAUNCH_CHECK();
+    plan.task_meta.alloc(std::max<int64_t>(2 * plan.split_tasks, 1));
+    plan.task_heads.alloc(std::max<int64_t>(kWave * plan.split_tasks, 1));
+    if (plan.split_tasks > 0) {
+        task_meta_kernel<<<grid_for(plan.split_tasks, 64), 64, 0, s>>>(cstart.get(), d_nzb.get(), b, plan.task_meta.get(),
+                                                                       plan.task_heads.get());
+        JG_LAUNCH_CHECK();
+    }
     JG_HIP(hipStreamSynchronize(s));
 }
 
@@ -585,8 +646,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         }
     };
     make_classes(0, plan.num_chunks, plan.class_row_begin, plan.class_row_end, plan.class_block_begin);
-    build_split_plan(sh, csr, plan, heavy);
-    build_slice_csr(sh, csr, plan);
+    build_slice_plan(sh, csr, plan, heavy);
     // light part: rows after the heavy prefix (hub rows are all heavy when rows are degree-sorted;
     // any hub beyond the prefix keeps its chunks, so chunks stay in the light table too)
     make_classes(plan.split_rows, plan.split_rows > 0 ? plan.num_chunks : plan.num_chunks, plan.light_row_begin,

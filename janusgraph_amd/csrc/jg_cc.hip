@@ -23,7 +23,6 @@ constexpr int kCcMaxIterations = 100;  // ConnectedComponentVertexProgram defaul
 
 struct CcOp {
     using T = int32_t;
-    static constexpr bool kZeroIdentity = false;  // min: identity INT32_MAX
     const int32_t* __restrict__ msg;     // full length, previous superstep
     int32_t* __restrict__ msg_out;       // full length (owned slice written)
     int32_t* __restrict__ label;         // [rows]
@@ -34,6 +33,7 @@ struct CcOp {
     __device__ __forceinline__ int32_t gather(int32_t c) const { return msg[c]; }
     __device__ __forceinline__ const int32_t* vec() const { return msg; }
     __device__ __forceinline__ int32_t shfl_xor(int32_t v, int o) const { return __shfl_xor(v, o, kWave); }
+    __device__ __forceinline__ int32_t shfl_up(int32_t v, int d) const { return __shfl_up(v, d, kWave); }
     __device__ __forceinline__ bool active(int64_t) const { return true; }
     __device__ __forceinline__ void finalize(int64_t row, int32_t m) const {
         if (m < label[row]) {

@@ -51,22 +51,28 @@ struct PullPlan {
     int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
 
     // XCD-sliced split of the heavy rows [0, split_rows) (degree >= split_min_degree) of a sliced
-    // CSR: see pull_slice_kernel (jg_pull.h).  The light rows keep the degree classes above (the
-    // light_* table covers rows [split_rows, rows)).
+    // CSR: see pull_merge_kernel (jg_pull.h).  The heavy rows' entries are kept slice-major (8
+    // sub-CSRs, each slice's start aligned to kMergeTask entries) and folded merge-path style in
+    // tasks of kMergeTask consecutive entries.  Non-empty sub-rows (q, r) are numbered slice-major
+    // (their partial slot); the light rows keep the degree classes above (the light_* table covers
+    // rows [split_rows, rows)).
     int64_t split_rows = 0;
-    int64_t split_tasks = 0;
-    int64_t chunk_rows = 0;    // rows [0, chunk_rows) are folded by chunk tasks (the task prefix)
-    int64_t chunk_tasks = 0;
+    int64_t split_tasks = 0;   // merge tasks over all 8 slices
+    int64_t split_subrows = 0; // non-empty sub-rows
     int64_t col_space = 0;     // length of the gathered vector
     int64_t light_row_begin[kNumClasses] = {};  // the class table of rows [split_rows, rows)
     int64_t light_row_end[kNumClasses] = {};
     int64_t light_block_begin[kNumClasses + 1] = {};
-    DevBuf<int32_t> task_row;            // first row of each task
-    DevBuf<int32_t> task_meta;           // lanes per row | rows << 8, or 0 | (k | K << 12) << 8 (chunk)
-    DevBuf<int32_t> chunk_ptr;           // [chunk_rows + 1] first task of each chunked row
-    DevBuf<int64_t> slice_ptr;           // [8 * split_rows + 1] sub-row (q, r) = [ptr[q*H+r], ptr[q*H+r+1])
-    DevBuf<int32_t> slice_col;           // the heavy rows' entries, slice-major (8 sub-CSRs)
-    int64_t split_partial_len() const { return std::max<int64_t>(8 * (split_rows + chunk_tasks), 1); }
+    int64_t slice_task_base[9] = {};      // first task of slice q; [8] = split_tasks
+    int64_t slice_begin[8] = {};          // first entry of slice q in slice_col (aligned)
+    int64_t slice_end[8] = {};            // one past the last entry of slice q
+    DevBuf<int32_t> slice_col;            // the heavy rows' entries, slice-major (+ one task of padding)
+    DevBuf<uint8_t> task_heads;           // [tasks][64]: byte l = row-start bits of lane l's entries
+    DevBuf<int32_t> task_meta;            // [tasks][2]: sub-row number of the task's first entry, and 1
+                                          // if that sub-row started in an earlier task (a carry)
+    DevBuf<int32_t> sub_index;            // [8][split_rows]: number of sub-row (q, r), -1 if empty
+    // program-owned fold buffer: [split_subrows] sub-row partials + [split_tasks] task carries
+    int64_t split_partial_len() const { return std::max<int64_t>(split_subrows + split_tasks, 1); }
     bool lds_ok = false;  // the gathered vector's hot prefix is [0, hot) (single shard)
 };
 constexpr int kXcds = 8;
@@ -77,7 +83,7 @@ constexpr int kXcds = 8;
 //   1  slice = xor of the line index's 3-bit groups (every residue appears in every slice)
 //   2  2 KiB blocks (16 lines) dealt round-robin
 constexpr int kSliceBits = 3;
-constexpr int64_t kSliceChunk = 1024;  // entries per chunk task of the sliced split (longer sub-rows are cut)
+constexpr int kMergeTask = 512;  // entries per merge task of the sliced split (one wave, 8 per lane)
 __host__ __device__ __forceinline__ int col_slice(int64_t c, int mode) {
     uint32_t line = (uint32_t)(c >> 4);
     if (mode == 2) return (int)((line >> 4) & (kXcds - 1));
@@ -204,7 +210,7 @@ struct Tune {
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
     int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_slice_kernel): 0 off, 1 on
                           // (read at build time too: the sliced in-CSR and split plan need it)
-    int64_t split_min_degree = 16;    // build time: rows of at least this degree are split
+    int64_t split_min_degree = 8;     // build time: rows of at least this degree are split
     int slice_lds = 1;                // stage each slice's hottest lines in LDS (single shard)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
     int slice_mode = 1;               // build time: col_slice mode of sliced CSRs

@@ -19,7 +19,6 @@ namespace {
 
 struct PrOp {
     using T = double;
-    static constexpr bool kZeroIdentity = true;
     const double* __restrict__ x;      // contrib of the previous superstep, full length
     double* __restrict__ contrib_out;  // full length (owned slice written)
     double* __restrict__ rank;         // [rows]
@@ -31,6 +30,7 @@ struct PrOp {
     __device__ __forceinline__ double gather(int32_t c) const { return x[c]; }
     __device__ __forceinline__ const double* vec() const { return x; }
     __device__ __forceinline__ double shfl_xor(double v, int o) const { return __shfl_xor(v, o, kWave); }
+    __device__ __forceinline__ double shfl_up(double v, int d) const { return __shfl_up(v, d, kWave); }
     __device__ __forceinline__ bool active(int64_t) const { return true; }
     __device__ __forceinline__ void finalize(int64_t row, double s) const {
         // (dampingFactor * newPageRank) + ((1D - dampingFactor) / vertexCount), no contraction
@@ -71,8 +71,9 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
         if (sh.pr_rank.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.pr_hub_partial.size() != (size_t)std::max<int64_t>(sh.plan_in.num_chunks, 1))
             sh.pr_hub_partial.alloc(std::max<int64_t>(sh.plan_in.num_chunks, 1));
-        if (sh.pr_split_partial.size() != (size_t)sh.plan_in.split_partial_len())
+        if (sh.pr_split_partial.size() != (size_t)sh.plan_in.split_partial_len()) {
             sh.pr_split_partial.alloc(sh.plan_in.split_partial_len());
+        }
         const double initial = 1.0 / (double)vertex_count;
         if (sh.rows > 0) {
             pr_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.out_degree.get(), sh.rows,

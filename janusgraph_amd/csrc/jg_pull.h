@@ -10,8 +10,9 @@
 //            row, fold, then a width-L xor-shuffle tree; lane 0 finalises the row
 //   class 8  the suffix of rows without entries: finalised with the identity, row_ptr not read
 // Every row is folded in a fixed order that does not depend on timing (bit-reproducible runs).
-// An Op supplies: T, identity(), combine(a,b), gather(col), shfl_xor(v,o), active(row) (false: the
-// row is not folded but still finalised with identity()), finalize(row, acc).
+// An Op supplies: T, identity(), combine(a,b), gather(col), vec(), shfl_xor(v,o),
+// shfl_up(v,d), active(row) (false: the row is not folded but still finalised with identity()),
+// finalize(row, acc).
 #pragma once
 
 #include "jg_internal.h"
@@ -96,11 +97,6 @@ __device__ __forceinline__ void load_cols(const int32_t* __restrict__ col, int64
     }
 }
 
-template <class G, class = void>
-struct is_split_gather { static constexpr bool value = false; };
-template <class G>
-struct is_split_gather<G, decltype((void)G::kSplit)> { static constexpr bool value = G::kSplit; };
-
 template <class Op, int U, bool NT, class G>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& gather, const int32_t* __restrict__ col,
                                                        int64_t j, int64_t j1, int stride) {
@@ -112,26 +108,9 @@ __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& ga
     for (;;) {
         T v[U];
         const int64_t jn = j + U * (int64_t)stride;
-        if constexpr (is_split_gather<G>::value) {
-            // Wait for the whole col batch once (the empty asm needs every c[u] in a register), so
-            // the masked global loads below issue back to back: exec-masked, a hot lane costs the
-            // TA/TD nothing (an out-of-range buffer lane still costs a TD cycle).  The LDS reads are
-            // unconditional (cold lanes read the identity cell) and land in their own registers.
-            static_assert(U == 4, "split gathers are written for U == 4");
-            asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]));
-            T vg[U], vl[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) vl[u] = gather.hot(c[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) vg[u] = gather.cold(c[u]);
-            load_cols<Op, U, NT>(col, jn, j1, stride, c);
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = op.combine(vl[u], vg[u]);
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
-            load_cols<Op, U, NT>(col, jn, j1, stride, c);  // clamped: unconditional keeps vmcnt counting exact
-        }
+        for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
+        load_cols<Op, U, NT>(col, jn, j1, stride, c);  // clamped: unconditional keeps vmcnt counting exact
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const T t = op.combine(acc, v[u]);
@@ -260,47 +239,42 @@ __global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T
 }
 
 // ---------------- XCD-sliced split of the heavy rows (PullPlan::split_*) ----------------
-// The entries of every heavy row of a sliced CSR are grouped by col_slice (mode 1: each aligned
-// group of 8 lines of the gathered vector gives one line to every slice).  A wave item is (task t,
-// slice q); every item of slice q runs in a workgroup b with b mod 8 == q, which the dispatcher
-// deals to one XCD (speed only: any placement gives the same result), so each XCD's L2 only ever
-// holds its own eighth of the vector.  On one shard the workgroup also stages the hottest lines of
-// its slice (the first kSliceLdsLines line groups, i.e. ids < 16 * 8 * kSliceLdsLines) in LDS, and
-// those gathers never leave the CU: the superstep is bound by TCP->L2 requests in flight
-// (PMC: TA/TD ~95% busy stalled on the TCP), not by bytes.
-//   task kind R (meta & 0xff = L lanes per row, meta >> 8 = rows): 64/L consecutive rows, sub-row
-//             (r, q) folded by L lanes, written to partial[q * split_rows + r]
-//   task kind C (meta & 0xff = 0, meta >> 8 = k | K << 12): chunk k of K of sub-row (r, q), folded by
-//             the wave, written to chunk_partial[t * 8 + q]; the chunked rows are the prefix
-//             [0, chunk_rows) and their tasks the prefix of the task list (chunk_ptr[r] = first task)
-// pull_slice_finalize_kernel folds the 8 slices (and the chunks of chunked rows) in fixed order.
-constexpr int kSliceThreads = 1024;                   // one workgroup per CU
-constexpr int kSliceLdsBytes = 160 * 1024;            // all of the CU's LDS
+// The entries of the heavy rows are kept slice-major: slice q (col_slice mode 1: each aligned group
+// of 8 lines of the gathered vector gives one line to every slice) is a sub-CSR over the heavy rows.
+// Each slice is folded merge-path style (CSR-stream): a wave task is kMergeTask consecutive entries
+// of one slice, kMergeEpl per lane, whatever the row boundaries, so col loads are whole 2 KiB spans
+// and no lane idles on short rows.  Every task of slice q runs in a workgroup b with b mod 8 == q,
+// which the dispatcher deals to one XCD (speed only: any placement gives the same result), so each
+// XCD's L2 only ever holds its own eighth of the vector; on one shard the workgroup also stages the
+// hottest lines of its slice in LDS, and those gathers never leave the CU (the superstep is bound by
+// TCP->L2 requests in flight, PMC: TA/TD ~95% busy, not by bytes).
+// Row boundaries come from build-time task metadata, so a task's only dependent loads are its
+// gathers: heads[t][l] holds the row-start bits of lane l's entries (entry 0 of a task is always a
+// head), meta[t] = (j0, carry): head h of the task is non-empty sub-row j0 + h, and with carry = 1
+// head 0 continues sub-row j0 from the previous task.  Sums are a deterministic segmented reduction:
+// sequential inside a lane, a fixed Hillis-Steele segmented scan across lanes.  A segment that starts
+// in the task goes to partial[j]; a continuation goes to carry[t], and pull_merge_fixup_kernel adds a
+// sub-row's carries in task order.  pull_slice_finalize_kernel folds every row's 8 slices in q order.
+constexpr int kMergeThreads = 1024;                    // one workgroup per CU
+constexpr int kMergeWaves = kMergeThreads / kWave;
+constexpr int kMergeEpl = kMergeTask / kWave;          // entries per lane
+constexpr int kMergeLdsBytes = 160 * 1024;
 
-struct SliceArgs {
-    const int64_t* __restrict__ slice_ptr;  // [8 * rows + 1], slice-major
+struct MergeArgs {
     const int32_t* __restrict__ col;        // slice_col
-    const int32_t* __restrict__ task_row;
-    const int32_t* __restrict__ task_meta;
-    int64_t ntasks;
-    int64_t rows;       // split (heavy) rows
-    uint32_t vec_bytes;  // bytes of the gathered vector (buffer resource range)
+    const uint8_t* __restrict__ heads;      // [tasks][64]
+    const int32_t* __restrict__ meta;       // [tasks][2]
+    const int32_t* __restrict__ sub_index;  // [8][H]
+    int64_t H;
+    int64_t base[kXcds + 1];
+    int64_t begin[kXcds];
+    int64_t end[kXcds];
 };
 
-// Sub-row (r, q): [j0, j1) of col.
-__device__ __forceinline__ void slice_segment(const SliceArgs& a, int64_t r, int q, int64_t& j0, int64_t& j1) {
-    const int64_t i = (int64_t)q * a.rows + r;
-    j0 = a.slice_ptr[i];
-    j1 = a.slice_ptr[i + 1];
-}
-
-// Gathers of slice q: ids below `hot` come from the LDS image of the slice's first lines (line group
-// c >> 7 holds one line of this slice; it sits at LDS line c >> 7), the rest from global memory.
-// Split form for fold_strided: hot(c) / cold(c) each return identity() for the other kind, and
-// combine(hot, cold) is the gathered value (exact: combine(x, identity) == x).
+// Gathers of slice q: ids below `hot_ids` come from the LDS image of the slice's first lines (line
+// group c >> 7 holds one line of this slice; it sits at LDS line c >> 7), the rest from global memory.
 template <class Op>
 struct SliceLdsGather {
-    static constexpr bool kSplit = true;
     using T = typename Op::T;
     const Op& op;
     lds_ptr<const T> lds;
@@ -318,100 +292,169 @@ struct SliceLdsGather {
     }
 };
 
-template <class Op, int L, int U, class G>
-__device__ __forceinline__ void slice_rows_item(const SliceArgs& a, const Op& op, const G& gather, int q, int64_t row0,
-                                                int nrows, int lane, typename Op::T* __restrict__ partial) {
+template <class Op, bool LDS>
+__global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
+                                                                   typename Op::T* __restrict__ carry, int32_t hot) {
     using T = typename Op::T;
-    const int sub = lane % L;
-    const int local = lane / L;
-    const int64_t r = row0 + local;
-    const bool valid = local < nrows;
-    T acc = op.identity();
-    if (valid && op.active(r)) {
-        int64_t j0, j1;
-        slice_segment(a, r, q, j0, j1);
-        acc = fold_strided<Op, U, false>(op, gather, a.col, j0 + sub, j1, L);
-    }
-#pragma unroll
-    for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
-    if (valid && sub == 0) partial[(int64_t)q * a.rows + r] = acc;
-}
-
-template <class Op, int U, bool LDS>
-__global__ __launch_bounds__(kSliceThreads) void pull_slice_kernel(SliceArgs a, Op op, typename Op::T* __restrict__ partial,
-                                                                   typename Op::T* __restrict__ chunk_partial,
-                                                                   int32_t hot) {
-    using T = typename Op::T;
-    extern __shared__ __align__(16) unsigned char slice_lds_raw[];
-    lds_ptr<T> lds = (lds_ptr<T>)slice_lds_raw;
+    extern __shared__ __align__(16) unsigned char merge_lds[];
     const int q = (int)(blockIdx.x & (kXcds - 1));
     const int64_t g = blockIdx.x >> 3, G = gridDim.x >> 3;
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    lds_ptr<T> hotv = (lds_ptr<T>)merge_lds;
     if constexpr (LDS) {
         // LDS line i = the line of slice q in line group i (mode-1 slices permute each aligned group)
         const T* src = op.vec();
-        const int nl = hot >> 7;  // line groups staged
-        for (int i = threadIdx.x; i < nl * 16; i += kSliceThreads) {
+        const int nl = hot >> 7;
+        for (int i = threadIdx.x; i < nl * 16; i += kMergeThreads) {
             const int grp = i >> 4;
             const int line = grp * 8 + (q ^ col_slice((int64_t)grp * 128, 1));
-            lds[i] = src[line * 16 + (i & 15)];
+            hotv[i] = src[line * 16 + (i & 15)];
         }
-        if (threadIdx.x == 0) lds[nl * 16] = op.identity();  // the cold lanes' cell (SliceLdsGather::hot)
+        if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
         __syncthreads();
     }
-    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    constexpr int kWaves = kSliceThreads / kWave;
-    for (int64_t t = g * kWaves + wave; t < a.ntasks; t += G * kWaves) {
-        const int64_t row0 = a.task_row[t];
-        const int meta = a.task_meta[t];
-        const int L = meta & 0xff;
-        const int arg = meta >> 8;
-        auto run = [&](const auto& gather) {
-            switch (L) {
-                case 0: {  // chunk k of K of sub-row (row0, q)
-                    const int k = arg & 0xfff, K = arg >> 12;
-                    int64_t j0, j1;
-                    slice_segment(a, row0, q, j0, j1);
-                    const int64_t len = j1 - j0;
-                    const int64_t c0 = j0 + len * k / K, c1 = j0 + len * (k + 1) / K;
-                    T acc = op.active(row0) ? fold_strided<Op, U, false>(op, gather, a.col, c0 + lane, c1, kWave)
-                                            : op.identity();
+    const SliceLdsGather<Op> lg{op, hotv, hot};
+    const int64_t ntask = a.base[q + 1] - a.base[q];
+    const int64_t step = G * kMergeWaves;
+    int64_t k = g * kMergeWaves + wave;
+    if (k >= ntask) return;
+    // cols of the current task (prefetched one task ahead)
+    auto load_cols = [&](int64_t kk, int32_t (&c)[kMergeEpl]) {
+        const int4* p = reinterpret_cast<const int4*>(a.col + a.begin[q] + kk * kMergeTask + kMergeEpl * lane);
 #pragma unroll
-                    for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
-                    if (lane == 0) chunk_partial[t * kXcds + q] = acc;
-                    break;
-                }
-                case 64: slice_rows_item<Op, 64, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                case 32: slice_rows_item<Op, 32, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                case 16: slice_rows_item<Op, 16, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                case 8: slice_rows_item<Op, 8, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                case 4: slice_rows_item<Op, 4, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                case 2: slice_rows_item<Op, 2, U>(a, op, gather, q, row0, arg, lane, partial); break;
-                default: slice_rows_item<Op, 1, U>(a, op, gather, q, row0, arg, lane, partial); break;
+        for (int h = 0; h < kMergeEpl / 4; ++h) {
+            const int4 v = p[h];
+            c[4 * h] = v.x;
+            c[4 * h + 1] = v.y;
+            c[4 * h + 2] = v.z;
+            c[4 * h + 3] = v.w;
+        }
+    };
+    int32_t c[kMergeEpl];
+    load_cols(k, c);
+    for (;;) {
+        const int64_t t = a.base[q] + k;
+        const int64_t e0 = a.begin[q] + k * kMergeTask;
+        const int n = (int)min((int64_t)kMergeTask, a.end[q] - e0);
+        const int32_t j0 = a.meta[2 * t];
+        const bool carry_in = a.meta[2 * t + 1] != 0;
+        const uint32_t hb = a.heads[t * kWave + lane];
+#pragma unroll
+        for (int u = 0; u < kMergeEpl; ++u)  // past the task end: cold id (identity cell, no load)
+            if (kMergeEpl * lane + u >= n) c[u] = INT32_MAX;
+        // gathers of this task, then the next task's cols: both round trips overlap
+        T v[kMergeEpl];
+        if constexpr (LDS) {
+            T vg[kMergeEpl], vl[kMergeEpl];
+#pragma unroll
+            for (int u = 0; u < kMergeEpl; ++u) vl[u] = lg.hot(c[u]);
+#pragma unroll
+            for (int u = 0; u < kMergeEpl; ++u) vg[u] = c[u] != INT32_MAX ? lg.cold(c[u]) : op.identity();
+#pragma unroll
+            for (int u = 0; u < kMergeEpl; ++u) v[u] = op.combine(vl[u], vg[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kMergeEpl; ++u) {
+                v[u] = op.identity();
+                if (c[u] != INT32_MAX) v[u] = op.gather(c[u]);
             }
+        }
+        const int64_t kn = k + step;
+        if (kn < ntask) load_cols(kn, c);
+        // head numbers: exclusive wave scan of the per-lane head counts
+        const int cnt = __builtin_popcount(hb);
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int o = __shfl_up(incl, d, kWave);
+            if (lane >= d) incl += o;
+        }
+        const int hbase = incl - cnt;  // head number of this lane's first head
+        const bool valid_lane = kMergeEpl * lane < n;
+        auto emit = [&](int h, T val) {  // segment of head h
+            if (h == 0 && carry_in) carry[t] = val;
+            else partial[j0 + h] = val;
         };
-        if constexpr (LDS) run(SliceLdsGather<Op>{op, lds, hot});
-        else run(GlobalGather<Op>{op});
+        // lane-local: the part before the first head (continues the segment on the left), inner
+        // segments (emitted here) and the segment of the last head (continues to the right)
+        const int fh = hb ? __builtin_ctz(hb) : kMergeEpl;
+        T pre = op.identity(), run = op.identity();
+        int run_h = hbase - 1;
+#pragma unroll
+        for (int u = 0; u < kMergeEpl; ++u) {
+            if (u < fh) {
+                pre = u == 0 ? v[u] : op.combine(pre, v[u]);
+            } else if ((hb >> u) & 1u) {
+                if (u > fh) emit(run_h, run);  // the previous head's segment ends here
+                run = v[u];
+                ++run_h;
+            } else {
+                run = op.combine(run, v[u]);
+            }
+        }
+        // segmented inclusive scan across lanes of (lane_out, has_head, head number)
+        T x = fh < kMergeEpl ? run : pre;
+        int f = fh < kMergeEpl ? 1 : 0;
+        int xh = run_h;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const T xu = op.shfl_up(x, d);
+            const int fu = __shfl_up(f, d, kWave);
+            const int hu = __shfl_up(xh, d, kWave);
+            if (lane >= d) {
+                if (!f) {
+                    x = op.combine(xu, x);
+                    xh = hu;
+                }
+                f |= fu;
+            }
+        }
+        const T in_x = op.shfl_up(x, 1);
+        const int in_h = __shfl_up(xh, 1, kWave);
+        if (valid_lane) {
+            if (lane > 0 && fh < kMergeEpl) emit(in_h, fh > 0 ? op.combine(in_x, pre) : in_x);
+            if (kMergeEpl * (lane + 1) >= n) {  // the task's last segment ends here
+                if (fh < kMergeEpl) emit(run_h, run);
+                else emit(in_h, lane > 0 ? op.combine(in_x, pre) : pre);
+            }
+        }
+        if (kn >= ntask) break;
+        k = kn;
     }
 }
 
-// Row r: fold the 8 slices in q order; a chunked row folds each slice's chunks in k order first.
+// Sub-rows that span tasks: the sub-row's first task wrote partial[j]; every later task it covers left
+// its segment in carry[t] (meta[t] = (j, 1)).  The first carry of each run adds the run in task order.
 template <class Op>
-__global__ void pull_slice_finalize_kernel(int64_t rows, int64_t chunk_rows, const int32_t* __restrict__ chunk_ptr,
-                                           Op op, const typename Op::T* __restrict__ partial,
-                                           const typename Op::T* __restrict__ chunk_partial) {
+__global__ void pull_merge_fixup_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
+                                        const typename Op::T* __restrict__ carry) {
+    using T = typename Op::T;
+    const int64_t tasks = a.base[kXcds];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += (int64_t)gridDim.x * blockDim.x) {
+        if (!a.meta[2 * t + 1]) continue;
+        const int32_t j = a.meta[2 * t];
+        if (a.meta[2 * (t - 1) + 1] && a.meta[2 * (t - 1)] == j) continue;  // not the first carry of the run
+        T acc = partial[j];
+        for (int64_t u = t; u < tasks && a.meta[2 * u + 1] && a.meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
+        partial[j] = acc;
+    }
+}
+
+// Row r: fold its non-empty slices in q order.
+template <class Op>
+__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, const int32_t* __restrict__ sub_index,
+                                           const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
         T acc = op.identity();
-        if (r < chunk_rows) {
-            const int t0 = chunk_ptr[r], t1 = chunk_ptr[r + 1];
-            for (int q = 0; q < kXcds; ++q) {
-                T sq = op.identity();
-                for (int t = t0; t < t1; ++t) sq = op.combine(sq, chunk_partial[(int64_t)t * kXcds + q]);
-                acc = op.combine(acc, sq);
-            }
-        } else {
+        bool first = true;
 #pragma unroll
-            for (int q = 0; q < kXcds; ++q) acc = op.combine(acc, partial[(int64_t)q * rows + r]);
+        for (int q = 0; q < kXcds; ++q) {
+            const int32_t j = sub_index[(int64_t)q * rows + r];
+            if (j >= 0) {
+                acc = first ? partial[j] : op.combine(acc, partial[j]);
+                first = false;
+            }
         }
         op.finalize(r, acc);
     }
@@ -430,31 +473,32 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
     if (split) {
-        SliceArgs sa{plan.slice_ptr.get(), plan.slice_col.get(), plan.task_row.get(), plan.task_meta.get(),
-                     plan.split_tasks, plan.split_rows,
-                     (uint32_t)std::min<int64_t>(plan.col_space * (int64_t)sizeof(T), 0xffffffffll)};
-        T* chunk_partial = split_partial + kXcds * plan.split_rows;
-        const unsigned grid = (unsigned)(device_cu_count() / kXcds * kXcds);
-        const int64_t hot_max = (int64_t)(kSliceLdsBytes / sizeof(T) - 16) * kXcds;  // full LDS, 1 identity line
-        const bool lds_ok = plan.lds_ok && tune().slice_lds && plan.col_space * (int64_t)sizeof(T) < (1ll << 32);
-        const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) >> 7 << 7) : 0;
-        bool launched = false;
-        if constexpr (Op::kZeroIdentity) {
-            if (hot > 0) {
-                static bool attr = false;
-                if (!attr) {
-                    JG_HIP(hipFuncSetAttribute((const void*)pull_slice_kernel<Op, 4, true>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, kSliceLdsBytes));
-                    attr = true;
-                }
-                const size_t bytes = (size_t)(hot / kXcds + 1) * sizeof(T);
-                pull_slice_kernel<Op, 4, true><<<grid, kSliceThreads, bytes, s>>>(sa, op, split_partial, chunk_partial,
-                                                                                 hot);
-                launched = true;
-            }
+        MergeArgs ma{plan.slice_col.get(), plan.task_heads.get(), plan.task_meta.get(), plan.sub_index.get(),
+                     plan.split_rows, {}, {}, {}};
+        for (int q = 0; q <= kXcds; ++q) ma.base[q] = plan.slice_task_base[q];
+        for (int q = 0; q < kXcds; ++q) {
+            ma.begin[q] = plan.slice_begin[q];
+            ma.end[q] = plan.slice_end[q];
         }
-        if (!launched)
-            pull_slice_kernel<Op, 4, false><<<grid, kSliceThreads, 0, s>>>(sa, op, split_partial, chunk_partial, 0);
+        T* carry = split_partial + plan.split_subrows;
+        const unsigned grid = (unsigned)(device_cu_count() / kXcds * kXcds);
+        const int64_t hot_max = (int64_t)(kMergeLdsBytes / sizeof(T) - 16) * kXcds;  // 1 identity line
+        const bool lds_ok = plan.lds_ok && tune().slice_lds;
+        const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) >> 7 << 7) : 0;
+        if (hot > 0) {
+            static bool attr = false;
+            if (!attr) {
+                JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
+                attr = true;
+            }
+            pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hot / kXcds + 1) * sizeof(T), s>>>(
+                ma, op, split_partial, carry, hot);
+        } else {
+            pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, split_partial, carry, 0);
+        }
+        JG_LAUNCH_CHECK();
+        pull_merge_fixup_kernel<Op><<<grid_for(plan.split_tasks), kBlock, 0, s>>>(ma, op, split_partial, carry);
         JG_LAUNCH_CHECK();
     }
     auto launch = [&](unsigned grid) {
@@ -492,17 +536,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     } else if (blocks > 0) {
         launch((unsigned)blocks);
     }
-    if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);
     if (plan.num_hub_rows > 0) {
         pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }
     if (split) {
-        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(
-            plan.split_rows, plan.chunk_rows, plan.chunk_ptr.get(), op, split_partial,
-            split_partial + kXcds * plan.split_rows);
+        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op,
+                                                                                   plan.sub_index.get(), split_partial);
         JG_LAUNCH_CHECK();
     }
+    if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);  // the whole superstep: every launch above
 }
 
 }  // namespace jg

@@ -251,7 +251,6 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
 struct MsBfsOp {
     using T = unsigned long long;
-    static constexpr bool kZeroIdentity = true;  // OR: identity 0
     const T* __restrict__ F;    // frontier words of the previous level, full length
     T* __restrict__ Fout;       // full length, owned slice written
     T* __restrict__ visited;    // [rows]
@@ -265,6 +264,7 @@ struct MsBfsOp {
     __device__ __forceinline__ T gather(int32_t c) const { return F[c]; }
     __device__ __forceinline__ const T* vec() const { return F; }
     __device__ __forceinline__ T shfl_xor(T v, int o) const { return __shfl_xor(v, o, kWave); }
+    __device__ __forceinline__ T shfl_up(T v, int d) const { return __shfl_up(v, d, kWave); }
     __device__ __forceinline__ bool active(int64_t row) const { return visited[row] != full; }
     __device__ __forceinline__ void finalize(int64_t row, T acc) const {
         T nw = acc & ~visited[row] & full;

@@ -304,4 +304,4 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("pull_lds", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("slice_lds", 1)
-        _lib.tune_set("split_min_degree", 16)
+        _lib.tune_set("split_min_degree", 8)

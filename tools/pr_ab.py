@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import janusgraph_amd as jg  # noqa: E402
 from janusgraph_amd import _lib  # noqa: E402
 
-DEFAULTS = {"pull_split": 1, "split_min_degree": 16, "slice_mode": 1, "slice_lds": 1, "pull_lds": 0,
+DEFAULTS = {"pull_split": 1, "split_min_degree": 8, "slice_mode": 1, "slice_lds": 1, "pull_lds": 0,
             "pull_unroll": 4, "pull_nt": 0}
 
 
