@@ -133,7 +133,7 @@ def _ptr(a):
 
 def tune_set(key: str, value: int):
     """Process-wide performance knob (results are unaffected): pull_unroll, pull_nt, pull_lds,
-    pull_split, split_min_degree (the last two are read at graph build time too)."""
+    slice_lds, pull_split, band<i>_deg, band<i>_bit (the last three are read at graph build time)."""
     check(load().jg_tune_set(key.encode(), int(value)))
 
 

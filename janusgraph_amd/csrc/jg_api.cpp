@@ -198,12 +198,16 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "pull_lds") {
         JG_ARG(value >= 0, "pull_lds must be >= 0");
         jg::tune().pull_lds = value;
-    } else if (k == "split_min_degree") {
-        JG_ARG(value >= 8, "split_min_degree must be >= 8");
-        jg::tune().split_min_degree = value;
-    } else if (k == "slice_mode") {
-        JG_ARG(value >= 0 && value <= 2, "slice_mode must be 0, 1 or 2");
-        jg::tune().slice_mode = (int)value;
+    } else if (k.rfind("band", 0) == 0 && k.size() == 9 && k[4] >= '0' && k[4] <= '3' &&
+               (k.substr(5) == "_deg" || k.substr(5) == "_bit")) {
+        const int i = k[4] - '0';  // band<i>_deg: minimum degree (0: band unused); band<i>_bit: log2 sub-slices
+        if (k.substr(5) == "_deg") {
+            JG_ARG(value >= 0, "band degree must be >= 0");
+            jg::tune().band_deg[i] = value;
+        } else {
+            JG_ARG(value >= 3 && value <= 8, "band bits must be in [3, 8]");
+            jg::tune().band_bits[i] = (int)value;
+        }
     } else if (k == "pull_split") {
         jg::tune().pull_split = value != 0;
     } else if (k == "slice_lds") {

@@ -197,8 +197,7 @@ struct SelectArgs {
     int r;
     int which;
     int cbits;
-    int sbits;  // 0, or kSliceBits: entries of a row grouped by XCD slice of their column (then by column)
-    int smode;  // col_slice mode
+    int sbits;  // 0, or 8: entries of a row ordered by (sub_key(col), col)
 };
 
 __device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
@@ -247,13 +246,13 @@ __global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, cons
         const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
         if ((a.which == 1 || a.which == 2) && own_s) {
             keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? col_slice(gd, a.smode) : 0) << a.cbits) | (uint64_t)gd;
+                        ((uint64_t)(a.sbits ? sub_key(gd) : 0) << a.cbits) | (uint64_t)gd;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
         if ((a.which == 0 || a.which == 2) && own_d) {
             keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? col_slice(gs, a.smode) : 0) << a.cbits) | (uint64_t)gs;
+                        ((uint64_t)(a.sbits ? sub_key(gs) : 0) << a.cbits) | (uint64_t)gs;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
@@ -290,18 +289,32 @@ __global__ void hub_flag_kernel(const int64_t* __restrict__ rp, int64_t rows, ui
 __constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 1, 0};
 
 // first_below[c] = first row with degree < c_class_thr[c] (c = 1..6);
-// first_below[kZeroClass] = 1 + last row with any entry (rows after it are all empty)
+// first_below[kZeroClass] = 1 + last row with any entry (rows after it are all empty);
+// band_below[i] = first row with degree < band_thr[i] (i < nbands).  Wave-reduced, one atomic per wave.
+struct BandThresholds {
+    int64_t thr[4];
+    int n;
+};
 __global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
                                    unsigned long long* __restrict__ first_below /* [kNumClasses] */,
-                                   unsigned long long* __restrict__ last_nonempty, int64_t split_thr,
-                                   unsigned long long* __restrict__ first_below_split) {
-    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t d = rp[l + 1] - rp[l];
+                                   unsigned long long* __restrict__ last_nonempty, BandThresholds bt,
+                                   unsigned long long* __restrict__ band_below /* [4] */) {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < rows; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t l = base + threadIdx.x;
+        const bool in = l < rows;
+        const int64_t d = in ? rp[l + 1] - rp[l] : 0;
+        const unsigned long long none = ~0ull;
 #pragma unroll
-        for (int c = 1; c < kNumClasses - 2; ++c)
-            if (d < c_class_thr[c]) atomicMin(&first_below[c], (unsigned long long)l);
-        if (d > 0) atomicMax(last_nonempty, (unsigned long long)(l + 1));
-        if (d < split_thr) atomicMin(first_below_split, (unsigned long long)l);
+        for (int c = 1; c < kNumClasses - 2; ++c) {
+            const unsigned long long v = wave_reduce_min(in && d < c_class_thr[c] ? (unsigned long long)l : none);
+            if (lane_id() == 0 && v != none) atomicMin(&first_below[c], v);
+        }
+        const unsigned long long ne = wave_reduce_max(in && d > 0 ? (unsigned long long)(l + 1) : 0ull);
+        if (lane_id() == 0 && ne) atomicMax(last_nonempty, ne);
+        for (int i = 0; i < bt.n; ++i) {
+            const unsigned long long v = wave_reduce_min(in && d < bt.thr[i] ? (unsigned long long)l : none);
+            if (lane_id() == 0 && v != none) atomicMin(&band_below[i], v);
+        }
     }
 }
 
@@ -314,24 +327,6 @@ __global__ void gather_row_bounds_kernel(const int64_t* __restrict__ rp, const i
 }
 
 // ---------------- XCD split of the heavy rows ----------------
-// split_off[r*8+q] = first entry of row r in XCD slice q, relative to row_ptr[r].  Entries of a row
-// of a sliced CSR are ordered by (col_slice(col), col), so the slice is non-decreasing along the row.
-__global__ void split_off_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t heavy,
-                                 int smode, uint32_t* __restrict__ split_off) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < heavy * kXcds;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / kXcds;
-        const int q = (int)(i % kXcds);
-        const int64_t b = rp[r], e = rp[r + 1];
-        int64_t lo = b, hi = e;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (col_slice(col[mid], smode) < q) lo = mid + 1; else hi = mid;
-        }
-        split_off[i] = (uint32_t)(lo - b);
-    }
-}
-
 int64_t select_keys(const SelectArgs& a, DevBuf<uint64_t>& keys, DevBuf<uint32_t>& eidx, bool want_eidx,
                     hipStream_t s) {
     const int64_t nb = std::max<int64_t>(1, (a.m + kSelTile - 1) / kSelTile);
@@ -390,7 +385,6 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     csr.rows = sh.rows;
     csr.nnz = nnz;
     csr.sliced = a.sbits != 0;
-    csr.slice_mode = a.smode;
     csr.row_ptr.alloc(sh.rows + 1);
     csr.col.alloc(std::max<int64_t>(nnz, 1));
     if (weight) csr.weight.alloc(std::max<int64_t>(nnz, 1));
@@ -406,46 +400,59 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     JG_HIP(hipStreamSynchronize(s));
 }
 
-// Sub-row lengths in slice-major order: len[q * H + r] = entries of row r in slice q.
-__global__ void slice_len_kernel(const int64_t* __restrict__ rp, const uint32_t* __restrict__ off, int64_t H,
-                                 int32_t* __restrict__ len) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < H * kXcds; i += (int64_t)gridDim.x * blockDim.x) {
-        const int q = (int)(i / H);
-        const int64_t r = i % H;
-        const int64_t b = off[r * kXcds + q];
-        const int64_t e = q == kXcds - 1 ? rp[r + 1] - rp[r] : (int64_t)off[r * kXcds + q + 1];
-        len[i] = (int32_t)(e - b);
+// ---------------- the sliced split (SliceBand) ----------------
+// len[h * NR + i] = entries of band row R0 + i in sub-slice h (the row's entries are ordered by
+// sub_key = bit-reversed hash, so sub-slice h of a 2^b band is the key range brev_b(h) << (8 - b)).
+__global__ void band_len_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t R0,
+                                int64_t NR, int bits, uint32_t* __restrict__ off, int32_t* __restrict__ len) {
+    const int64_t S = 1ll << bits;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < S * NR; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = x % NR;
+        const int h = (int)(x / NR);
+        const int64_t b = rp[R0 + i], e = rp[R0 + i + 1];
+        const uint32_t k0 = brev_bits((uint32_t)h, bits) << (8 - bits);
+        const uint32_t k1 = k0 + (1u << (8 - bits));
+        auto first_at_least = [&](uint32_t key) {
+            int64_t lo = b, hi = e;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (sub_key(col[mid]) < key) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        const int64_t j0 = first_at_least(k0);
+        const int64_t j1 = k1 >= 256 ? e : first_at_least(k1);
+        off[x] = (uint32_t)(j0 - b);
+        len[x] = (int32_t)(j1 - j0);
     }
 }
 
-struct SliceBases {
-    int64_t begin[kXcds];     // aligned first entry of each slice
-    int64_t end[kXcds];       // end entry of each slice
-    int64_t base[kXcds + 1];  // first task of each slice
-};
+// raw[h * NR] for h = 0..S (the sub-slice boundaries of the exclusive scan)
+__global__ void band_bounds_kernel(const int64_t* __restrict__ raw, int64_t NR, int S, int64_t* __restrict__ out) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h <= S) out[h] = raw[(int64_t)h * NR];
+}
 
-// sp[q*(H+1) + r] = raw[q*H + r] - raw[q*H] + begin[q], r in [0, H] (raw[q*H + H] is slice q's end).
-__global__ void slice_ptr_kernel(const int64_t* __restrict__ raw, int64_t H, SliceBases b, int64_t* __restrict__ sp) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (H + 1) * kXcds;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int q = (int)(i / (H + 1));
-        const int64_t r = i % (H + 1);
-        sp[i] = raw[(int64_t)q * H + r] - raw[(int64_t)q * H] + b.begin[q];
+// sp[h*(NR+1) + i] = raw[h*NR + i] - raw[h*NR] + begin[h], i in [0, NR] (raw[h*NR + NR] = its end)
+__global__ void band_ptr_kernel(const int64_t* __restrict__ raw, int64_t NR, int S, const int64_t* __restrict__ begin,
+                                int64_t* __restrict__ sp) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < (NR + 1) * S; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t h = x / (NR + 1), i = x % (NR + 1);
+        sp[x] = raw[h * NR + i] - raw[h * NR] + begin[h];
     }
 }
 
-// slice_col[sp[q][r] ...] = the slice-q entries of row r (one wave per sub-row).
-__global__ void slice_copy_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                  const uint32_t* __restrict__ off, int64_t H, const int64_t* __restrict__ sp,
-                                  int32_t* __restrict__ scol) {
+// band col[sp[h][i] ...] = the sub-slice-h entries of band row i (one wave per sub-row)
+__global__ void band_copy_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t R0,
+                                 int64_t NR, int S, const uint32_t* __restrict__ off, const int64_t* __restrict__ sp,
+                                 int32_t* __restrict__ bcol) {
     const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; i < H * kXcds; i += waves) {
-        const int q = (int)(i / H);
-        const int64_t r = i % H;
-        const int64_t src = rp[r] + off[r * kXcds + q];
-        const int64_t* p = sp + (int64_t)q * (H + 1) + r;
+    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; x < NR * S; x += waves) {
+        const int64_t h = x / NR, i = x % NR;
+        const int64_t src = rp[R0 + i] + off[x];
+        const int64_t* p = sp + h * (NR + 1) + i;
         const int64_t dst = p[0], n = p[1] - p[0];
-        for (int64_t k = lane_id(); k < n; k += kWave) scol[dst + k] = col[src + k];
+        for (int64_t k = lane_id(); k < n; k += kWave) bcol[dst + k] = col[src + k];
     }
 }
 
@@ -454,33 +461,37 @@ __global__ void nonempty_kernel(const int32_t* __restrict__ len, int64_t n, int3
         flag[i] = len[i] > 0;
 }
 
-// Number the non-empty sub-rows slice-major: sub_index[q*H + r] = k (or -1), cstart[k] = first entry.
-__global__ void sub_number_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t H,
+// Number the non-empty sub-rows sub-slice-major: sub_index[h*NR + i] = k (or -1), cstart[k] = first entry.
+__global__ void sub_number_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t NR, int S,
                                   const int64_t* __restrict__ sp, int32_t* __restrict__ sub_index,
                                   int64_t* __restrict__ cstart) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < H * kXcds; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t q = i / H, r = i % H;
-        if (len[i] > 0) {
-            sub_index[i] = (int32_t)num[i];
-            cstart[num[i]] = sp[q * (H + 1) + r];
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < NR * S; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t h = x / NR, i = x % NR;
+        if (len[x] > 0) {
+            sub_index[x] = (int32_t)num[x];
+            cstart[num[x]] = sp[h * (NR + 1) + i];
         } else {
-            sub_index[i] = -1;
+            sub_index[x] = -1;
         }
     }
 }
 
 // Per task: j0 = the non-empty sub-row holding its first entry, carry = it started earlier, and
 // heads[t][l] = row-start bits of lane l's kMergeEpl entries (bit 0 of lane 0 always set).
-__global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64_t* __restrict__ nzb, SliceBases b,
-                                 int32_t* __restrict__ meta, uint8_t* __restrict__ heads) {
+__global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64_t* __restrict__ nzb, int S,
+                                 const int64_t* __restrict__ begin, const int64_t* __restrict__ end,
+                                 const int64_t* __restrict__ base, int32_t* __restrict__ meta, uint8_t* __restrict__ heads) {
     constexpr int kEpl = kMergeTask / kWave;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < b.base[kXcds];
-         t += (int64_t)gridDim.x * blockDim.x) {
-        int q = 0;
-        while (q < kXcds - 1 && t >= b.base[q + 1]) ++q;
-        const int64_t e0 = b.begin[q] + (t - b.base[q]) * kMergeTask;
-        const int64_t e1 = min(e0 + kMergeTask, b.end[q]);
-        int64_t lo = nzb[q], hi = nzb[q + 1];  // first sub-row starting after e0
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < base[S]; t += (int64_t)gridDim.x * blockDim.x) {
+        int lo_h = 0, hi_h = S;  // sub-slice: last h with base[h] <= t
+        while (hi_h - lo_h > 1) {
+            const int mid = (lo_h + hi_h) >> 1;
+            if (base[mid] <= t) lo_h = mid; else hi_h = mid;
+        }
+        const int h = lo_h;
+        const int64_t e0 = begin[h] + (t - base[h]) * kMergeTask;
+        const int64_t e1 = min(e0 + kMergeTask, end[h]);
+        int64_t lo = nzb[h], hi = nzb[h + 1];  // first sub-row starting after e0
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             if (cstart[mid] <= e0) lo = mid + 1; else hi = mid;
@@ -488,55 +499,61 @@ __global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64
         const int64_t j0 = lo - 1;
         meta[2 * t] = (int32_t)j0;
         meta[2 * t + 1] = cstart[j0] < e0 ? 1 : 0;
-        uint8_t h[kWave];
-        for (int l = 0; l < kWave; ++l) h[l] = 0;
-        h[0] = 1;
-        for (int64_t j = j0 + 1; j < nzb[q + 1] && cstart[j] < e1; ++j) {
+        uint8_t hd[kWave];
+        for (int l = 0; l < kWave; ++l) hd[l] = 0;
+        hd[0] = 1;
+        for (int64_t j = j0 + 1; j < nzb[h + 1] && cstart[j] < e1; ++j) {
             const int pos = (int)(cstart[j] - e0);
-            h[pos / kEpl] |= (uint8_t)(1u << (pos % kEpl));
+            hd[pos / kEpl] |= (uint8_t)(1u << (pos % kEpl));
         }
-        for (int l = 0; l < kWave; ++l) heads[t * kWave + l] = h[l];
+        for (int l = 0; l < kWave; ++l) heads[t * kWave + l] = hd[l];
     }
 }
 
-// The sliced split of the heavy rows [0, H): slice-major sub-CSRs, each slice's start aligned to a
-// merge task, so a task never spans two slices and its col loads are 16-byte aligned.
-static void build_slice_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t H) {
+// One band: sub-slice-major sub-CSRs of rows [R0, R1), every sub-slice's start aligned to a merge
+// task (a task never spans two sub-slices and its col loads are 16-byte aligned).
+static void build_band(Shard& sh, const Csr& csr, SliceBand& bd) {
     hipStream_t s = sh.stream;
-    plan.split_rows = plan.split_tasks = plan.split_subrows = 0;
-    if (H <= 0) return;
-    plan.split_rows = H;
-    const int64_t NS = H * kXcds;
+    const int64_t R0 = bd.row_begin, NR = bd.rows();
+    const int S = 1 << bd.bits;
+    const int64_t NS = NR * S;
     DevBuf<uint32_t> off(NS);
     DevBuf<int32_t> len(NS);
     DevBuf<int64_t> raw(NS + 1);
-    split_off_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), H, csr.slice_mode, off.get());
-    JG_LAUNCH_CHECK();
-    slice_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), off.get(), H, len.get());
+    band_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, off.get(), len.get());
     JG_LAUNCH_CHECK();
     prim::exclusive_scan(len.get(), raw.get(), NS, s);
-    int64_t bounds[kXcds + 1];
-    for (int q = 0; q <= kXcds; ++q) copy_d2h(&bounds[q], raw.get() + (int64_t)q * H, sizeof(int64_t), s);
-    SliceBases b{};
+    std::vector<int64_t> bounds(S + 1), begin(S), end(S), base(S + 1);
+    {
+        DevBuf<int64_t> d_b(S + 1);
+        band_bounds_kernel<<<grid_for(S + 1), kBlock, 0, s>>>(raw.get(), NR, S, d_b.get());
+        JG_LAUNCH_CHECK();
+        copy_d2h(bounds.data(), d_b.get(), (S + 1) * sizeof(int64_t), s);
+    }
     int64_t at = 0;
-    b.base[0] = 0;
-    for (int q = 0; q < kXcds; ++q) {
-        const int64_t n = bounds[q + 1] - bounds[q];
+    base[0] = 0;
+    for (int h = 0; h < S; ++h) {
+        const int64_t n = bounds[h + 1] - bounds[h];
         const int64_t tasks = (n + kMergeTask - 1) / kMergeTask;
-        b.begin[q] = plan.slice_begin[q] = at;
-        b.end[q] = plan.slice_end[q] = at + n;
-        b.base[q + 1] = b.base[q] + tasks;
+        begin[h] = at;
+        end[h] = at + n;
+        base[h + 1] = base[h] + tasks;
         at += tasks * kMergeTask;
     }
-    for (int q = 0; q <= kXcds; ++q) plan.slice_task_base[q] = b.base[q];
-    plan.split_tasks = b.base[kXcds];
-    DevBuf<int64_t> sp((H + 1) * kXcds);
-    slice_ptr_kernel<<<grid_for((H + 1) * kXcds), kBlock, 0, s>>>(raw.get(), H, b, sp.get());
+    bd.tasks = base[S];
+    bd.sub_begin.alloc(S);
+    bd.sub_end.alloc(S);
+    bd.sub_base.alloc(S + 1);
+    copy_h2d(bd.sub_begin.get(), begin.data(), S * sizeof(int64_t), s);
+    copy_h2d(bd.sub_end.get(), end.data(), S * sizeof(int64_t), s);
+    copy_h2d(bd.sub_base.get(), base.data(), (S + 1) * sizeof(int64_t), s);
+    DevBuf<int64_t> sp((NR + 1) * S);
+    band_ptr_kernel<<<grid_for((NR + 1) * S), kBlock, 0, s>>>(raw.get(), NR, S, bd.sub_begin.get(), sp.get());
     JG_LAUNCH_CHECK();
-    plan.slice_col.alloc(at + kMergeTask);  // one task of padding: the last task's aligned loads
-    JG_HIP(hipMemsetAsync(plan.slice_col.get(), 0, plan.slice_col.bytes(), s));
-    slice_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), off.get(), H, sp.get(),
-                                                              plan.slice_col.get());
+    bd.col.alloc(at + kMergeTask);  // one task of padding: the last task's aligned loads
+    JG_HIP(hipMemsetAsync(bd.col.get(), 0, bd.col.bytes(), s));
+    band_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, S, off.get(),
+                                                             sp.get(), bd.col.get());
     JG_LAUNCH_CHECK();
     // number the non-empty sub-rows
     DevBuf<int32_t> flag(NS);
@@ -544,20 +561,21 @@ static void build_slice_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t 
     nonempty_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), NS, flag.get());
     JG_LAUNCH_CHECK();
     prim::exclusive_scan(flag.get(), num.get(), NS, s);
-    int64_t nzb[kXcds + 1];
-    for (int q = 0; q <= kXcds; ++q) copy_d2h(&nzb[q], num.get() + (int64_t)q * H, sizeof(int64_t), s);
-    plan.split_subrows = nzb[kXcds];
-    DevBuf<int64_t> cstart(std::max<int64_t>(plan.split_subrows, 1)), d_nzb(kXcds + 1);
-    copy_h2d(d_nzb.get(), nzb, sizeof nzb, s);
-    plan.sub_index.alloc(NS);
-    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), H, sp.get(), plan.sub_index.get(),
+    DevBuf<int64_t> nzb(S + 1);
+    band_bounds_kernel<<<grid_for(S + 1), kBlock, 0, s>>>(num.get(), NR, S, nzb.get());
+    JG_LAUNCH_CHECK();
+    copy_d2h(&bd.subrows, num.get() + NS, sizeof(int64_t), s);
+    DevBuf<int64_t> cstart(std::max<int64_t>(bd.subrows, 1));
+    bd.sub_index.alloc(NS);
+    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), NR, S, sp.get(), bd.sub_index.get(),
                                                       cstart.get());
     JG_LAUNCH_CHECK();
-    plan.task_meta.alloc(std::max<int64_t>(2 * plan.split_tasks, 1));
-    plan.task_heads.alloc(std::max<int64_t>(kWave * plan.split_tasks, 1));
-    if (plan.split_tasks > 0) {
-        task_meta_kernel<<<grid_for(plan.split_tasks, 64), 64, 0, s>>>(cstart.get(), d_nzb.get(), b, plan.task_meta.get(),
-                                                                       plan.task_heads.get());
+    bd.meta.alloc(std::max<int64_t>(2 * bd.tasks, 1));
+    bd.heads.alloc(std::max<int64_t>(kWave * bd.tasks, 1));
+    if (bd.tasks > 0) {
+        task_meta_kernel<<<grid_for(bd.tasks, 64), 64, 0, s>>>(cstart.get(), nzb.get(), S, bd.sub_begin.get(),
+                                                               bd.sub_end.get(), bd.sub_base.get(), bd.meta.get(),
+                                                               bd.heads.get());
         JG_LAUNCH_CHECK();
     }
     JG_HIP(hipStreamSynchronize(s));
@@ -606,28 +624,39 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     upload(plan.chunk_begin, cbeg);
     upload(plan.chunk_end, cend);
     upload(plan.hub_chunk_ptr, hptr);
-    // class boundaries: first row whose degree falls below each class threshold
-    unsigned long long fb[kNumClasses + 2];
+    // class boundaries: first row whose degree falls below each class threshold, and the band bounds
+    unsigned long long fb[kNumClasses + 1 + 4];
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
-    fb[kNumClasses] = 0;                                 // 1 + last non-empty row
-    fb[kNumClasses + 1] = (unsigned long long)rows;      // first row below the split threshold
-    const int64_t split_thr = std::max<int64_t>(tune().split_min_degree, kXcds);
+    fb[kNumClasses] = 0;  // 1 + last non-empty row
+    BandThresholds bt{};
+    // bands only on a sliced CSR, and only when the split is enabled at build time
+    if (tune().pull_split && csr.sliced)
+        for (int i = 0; i < 4 && tune().band_deg[i] > 0; ++i) bt.thr[bt.n++] = std::max<int64_t>(tune().band_deg[i], 1);
+    for (int i = 0; i < 4; ++i) fb[kNumClasses + 1 + i] = (unsigned long long)rows;
     if (rows > 0) {
-        DevBuf<unsigned long long> d_fb(kNumClasses + 2);
+        DevBuf<unsigned long long> d_fb(kNumClasses + 1 + 4);
         copy_h2d(d_fb.get(), fb, sizeof fb, s);
         class_bound_kernel<<<grid_for(rows), kBlock, 0, s>>>(csr.row_ptr.get(), rows, d_fb.get(),
-                                                             d_fb.get() + kNumClasses, split_thr,
-                                                             d_fb.get() + kNumClasses + 1);
+                                                             d_fb.get() + kNumClasses, bt, d_fb.get() + kNumClasses + 1);
         JG_LAUNCH_CHECK();
         copy_d2h(fb, d_fb.get(), sizeof fb, s);
     }
     // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
-    // the heavy prefix split by XCD slice: rows before the first row of degree < split_min_degree
-    // (only on a sliced CSR, and only when the split is enabled at build time)
-    const int64_t heavy = (tune().pull_split && csr.sliced && csr.slice_mode == 1)
-                              ? std::min<int64_t>((int64_t)fb[kNumClasses + 1], zero_begin) : 0;
+    plan.bands.clear();
+    int64_t row_at = 0;
+    for (int i = 0; i < bt.n; ++i) {
+        const int64_t end = std::min<int64_t>((int64_t)fb[kNumClasses + 1 + i], zero_begin);
+        if (end <= row_at) continue;
+        auto bd = std::make_unique<SliceBand>();
+        bd->bits = std::min(std::max(tune().band_bits[i], 3), 8);
+        bd->row_begin = row_at;
+        bd->row_end = end;
+        row_at = end;
+        plan.bands.push_back(std::move(bd));
+    }
+    plan.split_rows = row_at;
     auto make_classes = [&](int64_t first_row, int64_t chunks, int64_t* rb, int64_t* re, int64_t* bb) {
         int64_t begin = first_row;
         rb[0] = re[0] = 0;  // hub class is the chunk table
@@ -646,7 +675,15 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         }
     };
     make_classes(0, plan.num_chunks, plan.class_row_begin, plan.class_row_end, plan.class_block_begin);
-    build_slice_plan(sh, csr, plan, heavy);
+    {
+        int64_t part = 0;
+        for (auto& bd : plan.bands) {
+            build_band(sh, csr, *bd);
+            bd->part_off = part;
+            bd->carry_off = part + bd->subrows;
+            part += bd->subrows + bd->tasks;
+        }
+    }
     // light part: rows after the heavy prefix (hub rows are all heavy when rows are degree-sorted;
     // any hub beyond the prefix keeps its chunks, so chunks stay in the light table too)
     make_classes(plan.split_rows, plan.split_rows > 0 ? plan.num_chunks : plan.num_chunks, plan.light_row_begin,
@@ -735,11 +772,11 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                      sh.out_degree.get());
             JG_LAUNCH_CHECK();
         }
-        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0, tune().slice_mode};
+        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
         if (g.flags & JG_ADJ_IN) {
             a.which = 0;
-            a.sbits = tune().pull_split ? kSliceBits : 0;  // PageRank's pull adjacency: XCD-sliced rows
+            a.sbits = tune().pull_split ? 8 : 0;  // PageRank's pull adjacency: sub-slice-ordered rows
             build_csr(sh, a, w, sh.in, s);
             a.sbits = 0;
             build_pull_plan(sh, sh.in, sh.plan_in, g.padded_len());

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "jg_common.h"
 #include "janusgpu.h"
@@ -25,8 +26,7 @@ struct Csr {
     DevBuf<int64_t> row_ptr;
     DevBuf<int32_t> col;
     DevBuf<int32_t> weight;  // optional (SD weights)
-    bool sliced = false;     // entries of each row ordered by (col_slice(col), col) instead of col
-    int slice_mode = 0;      // col_slice mode of a sliced CSR
+    bool sliced = false;     // entries of each row ordered by (sub_key(col), col) instead of col
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
 };
@@ -37,6 +37,28 @@ constexpr int kNumClasses = 9;  // 0: hub (chunked), 1..7: lanes per row 64,32,1
 constexpr int kZeroClass = kNumClasses - 1;
 constexpr int64_t kHubDegree = 8192;
 constexpr int64_t kHubChunk = 4096;
+
+// One degree band of the sliced split: rows [row_begin, row_end), whose entries are dealt to
+// S = 2^bits sub-slices by sub_slice() (sub-slice h belongs to XCD h mod 8).  Each sub-slice is a
+// sub-CSR over the band's rows (entries slice-major in `col`, every sub-slice's start aligned to a
+// merge task) folded merge-path style in tasks of kMergeTask entries.  Non-empty sub-rows (h, r) are
+// numbered sub-slice-major: their partial slot (part_off + number); task carries follow at carry_off.
+struct SliceBand {
+    int bits = 3;
+    int64_t row_begin = 0, row_end = 0;
+    int64_t tasks = 0;      // merge tasks over all sub-slices
+    int64_t subrows = 0;    // non-empty sub-rows
+    int64_t part_off = 0;   // offset of the band's partials in the program's fold buffer
+    int64_t carry_off = 0;  // offset of the band's task carries
+    DevBuf<int32_t> col;        // entries, sub-slice-major (+ one task of padding)
+    DevBuf<int64_t> sub_begin;  // [S] first entry of sub-slice h in col (aligned)
+    DevBuf<int64_t> sub_end;    // [S] one past its last entry
+    DevBuf<int64_t> sub_base;   // [S+1] first task of sub-slice h
+    DevBuf<uint8_t> heads;      // [tasks][64]: byte l = row-start bits of lane l's entries
+    DevBuf<int32_t> meta;       // [tasks][2]: sub-row number of the task's first entry; 1 if it is a carry
+    DevBuf<int32_t> sub_index;  // [S][rows of the band]: number of sub-row (h, r), -1 if empty
+    int64_t rows() const { return row_end - row_begin; }
+};
 
 struct PullPlan {
     int64_t class_row_begin[kNumClasses];
@@ -50,53 +72,43 @@ struct PullPlan {
     DevBuf<int64_t> hub_chunk_ptr;  // [num_hub_rows+1] chunks of hub row r: [ptr[r], ptr[r+1])
     int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
 
-    // XCD-sliced split of the heavy rows [0, split_rows) (degree >= split_min_degree) of a sliced
-    // CSR: see pull_merge_kernel (jg_pull.h).  The heavy rows' entries are kept slice-major (8
-    // sub-CSRs, each slice's start aligned to kMergeTask entries) and folded merge-path style in
-    // tasks of kMergeTask consecutive entries.  Non-empty sub-rows (q, r) are numbered slice-major
-    // (their partial slot); the light rows keep the degree classes above (the light_* table covers
-    // rows [split_rows, rows)).
+    // XCD-sliced split of the heavy rows [0, split_rows) of a sliced CSR, in degree bands (rows are
+    // degree-sorted, so every band is a row range): see SliceBand and pull_merge_kernel (jg_pull.h).
+    // The light rows keep the degree classes above (the light_* table covers [split_rows, rows)).
     int64_t split_rows = 0;
-    int64_t split_tasks = 0;   // merge tasks over all 8 slices
-    int64_t split_subrows = 0; // non-empty sub-rows
     int64_t col_space = 0;     // length of the gathered vector
     int64_t light_row_begin[kNumClasses] = {};  // the class table of rows [split_rows, rows)
     int64_t light_row_end[kNumClasses] = {};
     int64_t light_block_begin[kNumClasses + 1] = {};
-    int64_t slice_task_base[9] = {};      // first task of slice q; [8] = split_tasks
-    int64_t slice_begin[8] = {};          // first entry of slice q in slice_col (aligned)
-    int64_t slice_end[8] = {};            // one past the last entry of slice q
-    DevBuf<int32_t> slice_col;            // the heavy rows' entries, slice-major (+ one task of padding)
-    DevBuf<uint8_t> task_heads;           // [tasks][64]: byte l = row-start bits of lane l's entries
-    DevBuf<int32_t> task_meta;            // [tasks][2]: sub-row number of the task's first entry, and 1
-                                          // if that sub-row started in an earlier task (a carry)
-    DevBuf<int32_t> sub_index;            // [8][split_rows]: number of sub-row (q, r), -1 if empty
-    // program-owned fold buffer: [split_subrows] sub-row partials + [split_tasks] task carries
-    int64_t split_partial_len() const { return std::max<int64_t>(split_subrows + split_tasks, 1); }
+    std::vector<std::unique_ptr<SliceBand>> bands;
+    // program-owned fold buffer: per band [subrows] sub-row partials + [tasks] task carries
+    int64_t split_partial_len() const {
+        int64_t n = 0;
+        for (const auto& b : bands) n += b->subrows + b->tasks;
+        return std::max<int64_t>(n, 1);
+    }
     bool lds_ok = false;  // the gathered vector's hot prefix is [0, hot) (single shard)
 };
 constexpr int kXcds = 8;
-// XCD slices of the column space: 128-byte lines of an fp64 vector (16 elements) are dealt to the 8
-// XCDs, so every slice holds an equal share of every hot region and one XCD's 4 MiB L2 only ever
-// caches its own eighth of the gathered vector.  Modes (Tune::slice_mode, fixed per CSR at build):
-//   0  slice = line mod 8 (every line of a slice has the same residue mod 8: few L2 channels)
-//   1  slice = xor of the line index's 3-bit groups (every residue appears in every slice)
-//   2  2 KiB blocks (16 lines) dealt round-robin
-constexpr int kSliceBits = 3;
+// Sub-slices of the column space: the 128-byte lines of an fp64 vector (16 elements) are hashed to
+// 8 bits (xor of the line index's byte groups); a band of 2^b sub-slices uses the low b bits, and
+// sub-slice h belongs to XCD h mod 8.  Inside any aligned group of 2^b lines the hash is a
+// permutation (low bits xor a constant of the group), so every sub-slice holds an equal share of
+// every hot region and one XCD's L2 only ever caches its own eighth of the gathered vector.  Rows
+// of a sliced CSR order their entries by (sub_key, col): sub_key is the bit-reversed hash, so the
+// entries of every sub-slice of every band are contiguous in the row.
 constexpr int kMergeTask = 512;  // entries per merge task of the sliced split (one wave, 8 per lane)
-__host__ __device__ __forceinline__ int col_slice(int64_t c, int mode) {
-    uint32_t line = (uint32_t)(c >> 4);
-    if (mode == 2) return (int)((line >> 4) & (kXcds - 1));
-    if (mode == 1) {
-        uint32_t x = line;
-        x ^= x >> 3;
-        x ^= x >> 6;
-        x ^= x >> 12;
-        x ^= x >> 24;
-        return (int)(x & (kXcds - 1));
-    }
-    return (int)(line & (kXcds - 1));
+__host__ __device__ __forceinline__ uint32_t sub_hash(int64_t c) {
+    const uint32_t x = (uint32_t)(c >> 4);
+    return (x ^ (x >> 8) ^ (x >> 16) ^ (x >> 24)) & 255u;
 }
+__host__ __device__ __forceinline__ uint32_t brev_bits(uint32_t v, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((v >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+__host__ __device__ __forceinline__ uint32_t sub_key(int64_t c) { return brev_bits(sub_hash(c), 8); }
+__host__ __device__ __forceinline__ int sub_slice(int64_t c, int bits) { return (int)(sub_hash(c) & ((1u << bits) - 1)); }
 
 struct Ctx;
 
@@ -208,12 +220,14 @@ bool debug_plan();
 struct Tune {
     int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
     int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
-    int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_slice_kernel): 0 off, 1 on
+    int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_merge_kernel): 0 off, 1 on
                           // (read at build time too: the sliced in-CSR and split plan need it)
-    int64_t split_min_degree = 8;     // build time: rows of at least this degree are split
-    int slice_lds = 1;                // stage each slice's hottest lines in LDS (single shard)
+    // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
+    // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light
+    int64_t band_deg[4] = {128, 8, 0, 0};
+    int band_bits[4] = {5, 3, 3, 3};
+    int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
-    int slice_mode = 1;               // build time: col_slice mode of sliced CSRs
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

@@ -31,6 +31,26 @@ __device__ __forceinline__ T wave_reduce_add(T v) {
     return v;
 }
 
+template <typename T>
+__device__ __forceinline__ T wave_reduce_min(T v) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const T u = __shfl_xor(v, o, kWave);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_reduce_max(T v) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const T u = __shfl_xor(v, o, kWave);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
 // Exclusive scan across a 256-thread block. `scratch` holds >= 4 elements. Returns the exclusive
 // prefix of the calling thread; *total receives the block sum.
 template <typename T>

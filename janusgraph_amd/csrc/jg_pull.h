@@ -238,51 +238,55 @@ __global__ void pull_hub_finalize_kernel(PullArgs a, Op op, const typename Op::T
     }
 }
 
-// ---------------- XCD-sliced split of the heavy rows (PullPlan::split_*) ----------------
-// The entries of the heavy rows are kept slice-major: slice q (col_slice mode 1: each aligned group
-// of 8 lines of the gathered vector gives one line to every slice) is a sub-CSR over the heavy rows.
-// Each slice is folded merge-path style (CSR-stream): a wave task is kMergeTask consecutive entries
-// of one slice, kMergeEpl per lane, whatever the row boundaries, so col loads are whole 2 KiB spans
-// and no lane idles on short rows.  Every task of slice q runs in a workgroup b with b mod 8 == q,
-// which the dispatcher deals to one XCD (speed only: any placement gives the same result), so each
-// XCD's L2 only ever holds its own eighth of the vector; on one shard the workgroup also stages the
-// hottest lines of its slice in LDS, and those gathers never leave the CU (the superstep is bound by
-// TCP->L2 requests in flight, PMC: TA/TD ~95% busy, not by bytes).
+// ---------------- XCD-sliced split of the heavy rows (PullPlan::bands) ----------------
+// A band's entries are kept sub-slice-major: sub-slice h (2^bits of them, sub_slice(): each aligned
+// group of 2^bits lines of the gathered vector gives one line to every sub-slice) is a sub-CSR over
+// the band's rows.  Each sub-slice is folded merge-path style (CSR-stream): a wave task is kMergeTask
+// consecutive entries of one sub-slice, kMergeEpl per lane, whatever the row boundaries, so col loads
+// are whole 2 KiB spans and no lane idles on short rows.  Workgroup b runs sub-slice
+// h = (b mod 8) | ((b / 8) mod 2^bits/8) << 3, so h's workgroups share the dispatcher's XCD b mod 8
+// (speed only: any placement gives the same result) and an XCD's L2 only ever holds its eighth of
+// the vector.  On one shard every workgroup also stages the hottest lines of its sub-slice in LDS:
+// with 2^bits sub-slices the CUs of one XCD hold different images, so the LDS-resident share of the
+// vector grows with bits.  The superstep is bound by TCP->L2 requests in flight (PMC: TA/TD ~90%
+// busy, TCP pending-stalled), so every gather served from LDS is one request fewer.
 // Row boundaries come from build-time task metadata, so a task's only dependent loads are its
 // gathers: heads[t][l] holds the row-start bits of lane l's entries (entry 0 of a task is always a
 // head), meta[t] = (j0, carry): head h of the task is non-empty sub-row j0 + h, and with carry = 1
 // head 0 continues sub-row j0 from the previous task.  Sums are a deterministic segmented reduction:
 // sequential inside a lane, a fixed Hillis-Steele segmented scan across lanes.  A segment that starts
 // in the task goes to partial[j]; a continuation goes to carry[t], and pull_merge_fixup_kernel adds a
-// sub-row's carries in task order.  pull_slice_finalize_kernel folds every row's 8 slices in q order.
+// sub-row's carries in task order.  pull_slice_finalize_kernel folds every row's sub-slices in order.
 constexpr int kMergeThreads = 1024;                    // one workgroup per CU
 constexpr int kMergeWaves = kMergeThreads / kWave;
 constexpr int kMergeEpl = kMergeTask / kWave;          // entries per lane
 constexpr int kMergeLdsBytes = 160 * 1024;
 
 struct MergeArgs {
-    const int32_t* __restrict__ col;        // slice_col
+    const int32_t* __restrict__ col;        // band col
     const uint8_t* __restrict__ heads;      // [tasks][64]
     const int32_t* __restrict__ meta;       // [tasks][2]
-    const int32_t* __restrict__ sub_index;  // [8][H]
-    int64_t H;
-    int64_t base[kXcds + 1];
-    int64_t begin[kXcds];
-    int64_t end[kXcds];
+    const int64_t* __restrict__ sub_begin;  // [S]
+    const int64_t* __restrict__ sub_end;    // [S]
+    const int64_t* __restrict__ sub_base;   // [S+1]
+    int64_t tasks;
+    int bits;
 };
 
-// Gathers of slice q: ids below `hot_ids` come from the LDS image of the slice's first lines (line
-// group c >> 7 holds one line of this slice; it sits at LDS line c >> 7), the rest from global memory.
+// Gathers of sub-slice h of a 2^bits band: ids below `hot_ids` come from the LDS image of the
+// sub-slice's first lines (line group c >> (4 + bits) holds one line of h; it sits at LDS line
+// c >> (4 + bits)), the rest from global memory.
 template <class Op>
 struct SliceLdsGather {
     using T = typename Op::T;
     const Op& op;
     lds_ptr<const T> lds;
     int32_t hot_ids;
+    int gshift;  // 4 + bits
     // Cold lanes read the identity cell just past the staged lines: no select, so the compiler
     // cannot turn the read into a branch.
     __device__ __forceinline__ T hot(int32_t c) const {
-        return lds[c < hot_ids ? (((c >> 7) << 4) | (c & 15)) : (hot_ids >> 3)];
+        return lds[c < hot_ids ? (((c >> gshift) << 4) | (c & 15)) : (hot_ids >> (gshift - 4))];
     }
     // Only cold lanes load (exec-masked); the others keep identity().
     __device__ __forceinline__ T cold(int32_t c) const {
@@ -297,52 +301,75 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
                                                                    typename Op::T* __restrict__ carry, int32_t hot) {
     using T = typename Op::T;
     extern __shared__ __align__(16) unsigned char merge_lds[];
-    const int q = (int)(blockIdx.x & (kXcds - 1));
-    const int64_t g = blockIdx.x >> 3, G = gridDim.x >> 3;
+    const int per = (1 << a.bits) >> 3;  // sub-slices per XCD
+    const int w = (int)(blockIdx.x >> 3);
+    const int h = (int)(blockIdx.x & (kXcds - 1)) | ((w % per) << 3);
+    const int64_t g = w / per, G = (gridDim.x >> 3) / per;  // this block's rank among h's blocks
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     lds_ptr<T> hotv = (lds_ptr<T>)merge_lds;
+    const int gshift = 4 + a.bits;
     if constexpr (LDS) {
-        // LDS line i = the line of slice q in line group i (mode-1 slices permute each aligned group)
+        // LDS line i = the line of sub-slice h in line group i (a permutation of each aligned group)
         const T* src = op.vec();
-        const int nl = hot >> 7;
-        for (int i = threadIdx.x; i < nl * 16; i += kMergeThreads) {
+        const int nl = hot >> gshift;
+        const uint32_t mask = (1u << a.bits) - 1;
+        // kStage loads in flight per thread: with 2^bits sub-slices the image lines are scattered over
+        // 2^bits x the image span, so a load-store-load loop would pay one memory round trip each
+        constexpr int kStage = 8;
+        auto src_of = [&](int i) {
             const int grp = i >> 4;
-            const int line = grp * 8 + (q ^ col_slice((int64_t)grp * 128, 1));
-            hotv[i] = src[line * 16 + (i & 15)];
+            const int64_t line = ((int64_t)grp << a.bits) + (int64_t)(h ^ (sub_hash((int64_t)grp << gshift) & mask));
+            return src + line * 16 + (i & 15);
+        };
+        const int total = nl * 16;
+        for (int i0 = 0; i0 < total; i0 += kStage * kMergeThreads) {
+            T buf[kStage];
+#pragma unroll
+            for (int u = 0; u < kStage; ++u) {
+                const int i = i0 + u * kMergeThreads + (int)threadIdx.x;
+                buf[u] = i < total ? *src_of(i) : op.identity();
+            }
+#pragma unroll
+            for (int u = 0; u < kStage; ++u) {
+                const int i = i0 + u * kMergeThreads + (int)threadIdx.x;
+                if (i < total) hotv[i] = buf[u];
+            }
         }
         if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
         __syncthreads();
     }
-    const SliceLdsGather<Op> lg{op, hotv, hot};
-    const int64_t ntask = a.base[q + 1] - a.base[q];
+    const SliceLdsGather<Op> lg{op, hotv, hot, gshift};
+    const int64_t base = a.sub_base[h];
+    const int64_t ntask = a.sub_base[h + 1] - base;
+    const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
     const int64_t step = G * kMergeWaves;
     int64_t k = g * kMergeWaves + wave;
     if (k >= ntask) return;
-    // cols of the current task (prefetched one task ahead)
-    auto load_cols = [&](int64_t kk, int32_t (&c)[kMergeEpl]) {
-        const int4* p = reinterpret_cast<const int4*>(a.col + a.begin[q] + kk * kMergeTask + kMergeEpl * lane);
-#pragma unroll
-        for (int h = 0; h < kMergeEpl / 4; ++h) {
-            const int4 v = p[h];
-            c[4 * h] = v.x;
-            c[4 * h + 1] = v.y;
-            c[4 * h + 2] = v.z;
-            c[4 * h + 3] = v.w;
-        }
+    // The next task's cols and metadata are loaded while this task's gathers are in flight.  The
+    // loop carries the raw load registers (int4 col vectors, head byte, meta word) and unpacks them at
+    // the top, so a prefetch writes straight into them and nothing waits on it until the next task.
+    // Metadata are vector loads (lane 0: j0, lane 1: carry flag; one head byte per lane): a scalar
+    // prefetch would hold up every LDS wait (lgkmcnt does not count SMEM in order).
+    static_assert(kMergeEpl == 8, "the loop carries two int4 col vectors per lane");
+    auto col_ptr = [&](int64_t kk) {
+        return reinterpret_cast<const int4*>(a.col + hbegin + kk * kMergeTask + kMergeEpl * lane);
     };
-    int32_t c[kMergeEpl];
-    load_cols(k, c);
+    auto meta_idx = [&](int64_t kk) { return 2 * (base + kk) + (lane & 1); };
+    auto head_idx = [&](int64_t kk) { return (base + kk) * kWave + lane; };
+    int4 cv0 = col_ptr(k)[0], cv1 = col_ptr(k)[1];
+    uint32_t hb = a.heads[head_idx(k)];
+    int32_t mw = a.meta[meta_idx(k)];
     for (;;) {
-        const int64_t t = a.base[q] + k;
-        const int64_t e0 = a.begin[q] + k * kMergeTask;
-        const int n = (int)min((int64_t)kMergeTask, a.end[q] - e0);
-        const int32_t j0 = a.meta[2 * t];
-        const bool carry_in = a.meta[2 * t + 1] != 0;
-        const uint32_t hb = a.heads[t * kWave + lane];
+        const int64_t t = base + k;
+        const int64_t e0 = hbegin + k * kMergeTask;
+        const int n = (int)min((int64_t)kMergeTask, hend - e0);
+        int32_t c[kMergeEpl] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+        const int32_t j0 = __builtin_amdgcn_readlane(mw, 0);
+        const bool carry_in = __builtin_amdgcn_readlane(mw, 1) != 0;
+        const uint32_t hbc = hb;
 #pragma unroll
         for (int u = 0; u < kMergeEpl; ++u)  // past the task end: cold id (identity cell, no load)
             if (kMergeEpl * lane + u >= n) c[u] = INT32_MAX;
-        // gathers of this task, then the next task's cols: both round trips overlap
         T v[kMergeEpl];
         if constexpr (LDS) {
             T vg[kMergeEpl], vl[kMergeEpl];
@@ -360,9 +387,14 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
             }
         }
         const int64_t kn = k + step;
-        if (kn < ntask) load_cols(kn, c);
+        if (kn < ntask) {
+            cv0 = col_ptr(kn)[0];
+            cv1 = col_ptr(kn)[1];
+            hb = a.heads[head_idx(kn)];
+            mw = a.meta[meta_idx(kn)];
+        }
         // head numbers: exclusive wave scan of the per-lane head counts
-        const int cnt = __builtin_popcount(hb);
+        const int cnt = __builtin_popcount(hbc);
         int incl = cnt;
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
@@ -371,20 +403,20 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         }
         const int hbase = incl - cnt;  // head number of this lane's first head
         const bool valid_lane = kMergeEpl * lane < n;
-        auto emit = [&](int h, T val) {  // segment of head h
-            if (h == 0 && carry_in) carry[t] = val;
-            else partial[j0 + h] = val;
+        auto emit = [&](int hh, T val) {  // segment of head hh
+            if (hh == 0 && carry_in) carry[t] = val;
+            else partial[j0 + hh] = val;
         };
         // lane-local: the part before the first head (continues the segment on the left), inner
         // segments (emitted here) and the segment of the last head (continues to the right)
-        const int fh = hb ? __builtin_ctz(hb) : kMergeEpl;
+        const int fh = hbc ? __builtin_ctz(hbc) : kMergeEpl;
         T pre = op.identity(), run = op.identity();
         int run_h = hbase - 1;
 #pragma unroll
         for (int u = 0; u < kMergeEpl; ++u) {
             if (u < fh) {
                 pre = u == 0 ? v[u] : op.combine(pre, v[u]);
-            } else if ((hb >> u) & 1u) {
+            } else if ((hbc >> u) & 1u) {
                 if (u > fh) emit(run_h, run);  // the previous head's segment ends here
                 run = v[u];
                 ++run_h;
@@ -425,34 +457,47 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 
 // Sub-rows that span tasks: the sub-row's first task wrote partial[j]; every later task it covers left
 // its segment in carry[t] (meta[t] = (j, 1)).  The first carry of each run adds the run in task order.
+// (The first task of a sub-slice is never a carry: sub-slices start at a sub-row start.)
 template <class Op>
 __global__ void pull_merge_fixup_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
                                         const typename Op::T* __restrict__ carry) {
     using T = typename Op::T;
-    const int64_t tasks = a.base[kXcds];
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.tasks; t += (int64_t)gridDim.x * blockDim.x) {
         if (!a.meta[2 * t + 1]) continue;
         const int32_t j = a.meta[2 * t];
         if (a.meta[2 * (t - 1) + 1] && a.meta[2 * (t - 1)] == j) continue;  // not the first carry of the run
         T acc = partial[j];
-        for (int64_t u = t; u < tasks && a.meta[2 * u + 1] && a.meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
+        for (int64_t u = t; u < a.tasks && a.meta[2 * u + 1] && a.meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
         partial[j] = acc;
     }
 }
 
-// Row r: fold its non-empty slices in q order.
+// Row r of the split: fold its non-empty sub-slices in h order.
+constexpr int kMaxBands = 4;
+struct FinalizeBands {
+    const int32_t* sub_index[kMaxBands];
+    int64_t row_begin[kMaxBands];
+    int64_t row_end[kMaxBands];
+    int64_t part_off[kMaxBands];
+    int bits[kMaxBands];
+    int n;
+};
 template <class Op>
-__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, const int32_t* __restrict__ sub_index,
-                                           const typename Op::T* __restrict__ partial) {
+__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb, const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+        int b = 0;
+        while (b < fb.n - 1 && r >= fb.row_end[b]) ++b;
+        const int64_t NR = fb.row_end[b] - fb.row_begin[b], i = r - fb.row_begin[b];
+        const int S = 1 << fb.bits[b];
+        const int32_t* __restrict__ si = fb.sub_index[b];
+        const T* __restrict__ part = partial + fb.part_off[b];
         T acc = op.identity();
         bool first = true;
-#pragma unroll
-        for (int q = 0; q < kXcds; ++q) {
-            const int32_t j = sub_index[(int64_t)q * rows + r];
+        for (int hh = 0; hh < S; ++hh) {
+            const int32_t j = si[(int64_t)hh * NR + i];
             if (j >= 0) {
-                acc = first ? partial[j] : op.combine(acc, partial[j]);
+                acc = first ? part[j] : op.combine(acc, part[j]);
                 first = false;
             }
         }
@@ -473,33 +518,35 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
     if (split) {
-        MergeArgs ma{plan.slice_col.get(), plan.task_heads.get(), plan.task_meta.get(), plan.sub_index.get(),
-                     plan.split_rows, {}, {}, {}};
-        for (int q = 0; q <= kXcds; ++q) ma.base[q] = plan.slice_task_base[q];
-        for (int q = 0; q < kXcds; ++q) {
-            ma.begin[q] = plan.slice_begin[q];
-            ma.end[q] = plan.slice_end[q];
+        static bool attr = false;
+        if (!attr) {
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
+            attr = true;
         }
-        T* carry = split_partial + plan.split_subrows;
-        const unsigned grid = (unsigned)(device_cu_count() / kXcds * kXcds);
-        const int64_t hot_max = (int64_t)(kMergeLdsBytes / sizeof(T) - 16) * kXcds;  // 1 identity line
-        const bool lds_ok = plan.lds_ok && tune().slice_lds;
-        const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) >> 7 << 7) : 0;
-        if (hot > 0) {
-            static bool attr = false;
-            if (!attr) {
-                JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-                attr = true;
-            }
-            pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hot / kXcds + 1) * sizeof(T), s>>>(
-                ma, op, split_partial, carry, hot);
-        } else {
-            pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, split_partial, carry, 0);
+        for (const auto& bp : plan.bands) {
+            const SliceBand& bd = *bp;
+            if (bd.tasks == 0) continue;
+            MergeArgs ma{bd.col.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(), bd.sub_end.get(),
+                         bd.sub_base.get(), bd.tasks, bd.bits};
+            T* part = split_partial + bd.part_off;
+            T* carry = split_partial + bd.carry_off;
+            // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
+            const int64_t S = 1ll << bd.bits, gsz = 16 * S;
+            // a multiple of S workgroups: every sub-slice gets grid / S of them
+            const unsigned grid = (unsigned)std::max<int64_t>(S, device_cu_count() / S * S);
+            const int64_t hot_max = (int64_t)(kMergeLdsBytes / sizeof(T) - 16) * S;
+            const bool lds_ok = plan.lds_ok && tune().slice_lds;
+            const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) / gsz * gsz) : 0;
+            if (hot > 0)
+                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hot / S + 1) * sizeof(T), s>>>(ma, op, part,
+                                                                                                       carry, hot);
+            else
+                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, 0);
+            JG_LAUNCH_CHECK();
+            pull_merge_fixup_kernel<Op><<<grid_for(bd.tasks), kBlock, 0, s>>>(ma, op, part, carry);
+            JG_LAUNCH_CHECK();
         }
-        JG_LAUNCH_CHECK();
-        pull_merge_fixup_kernel<Op><<<grid_for(plan.split_tasks), kBlock, 0, s>>>(ma, op, split_partial, carry);
-        JG_LAUNCH_CHECK();
     }
     auto launch = [&](unsigned grid) {
         const int u = tune().pull_unroll;
@@ -541,8 +588,17 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         JG_LAUNCH_CHECK();
     }
     if (split) {
-        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op,
-                                                                                   plan.sub_index.get(), split_partial);
+        FinalizeBands fb{};
+        for (const auto& bp : plan.bands) {
+            if (fb.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
+            fb.sub_index[fb.n] = bp->sub_index.get();
+            fb.row_begin[fb.n] = bp->row_begin;
+            fb.row_end[fb.n] = bp->row_end;
+            fb.part_off[fb.n] = bp->part_off;
+            fb.bits[fb.n] = bp->bits;
+            ++fb.n;
+        }
+        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, fb, split_partial);
         JG_LAUNCH_CHECK();
     }
     if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);  // the whole superstep: every launch above

@@ -1,7 +1,7 @@
 """A/B timing of PageRank pull-engine variants on one RMAT graph shape (diagnostic, not a benchmark).
 
 Each variant is "name:key=value,key=value" of jg_tune_set knobs, applied before its graph is built
-(build-time knobs: pull_split, split_min_degree, slice_mode) and while it runs.  All variants are
+(build-time knobs: pull_split, band<i>_deg, band<i>_bit) and while it runs.  All variants are
 built once and timed in interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
 Reports the median ms per superstep and the max relative difference of the ranks vs the first.
   python tools/pr_ab.py --scale 24 plain:pull_split=0 split:pull_split=1
@@ -18,8 +18,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import janusgraph_amd as jg  # noqa: E402
 from janusgraph_amd import _lib  # noqa: E402
 
-DEFAULTS = {"pull_split": 1, "split_min_degree": 8, "slice_mode": 1, "slice_lds": 1, "pull_lds": 0,
-            "pull_unroll": 4, "pull_nt": 0}
+DEFAULTS = {"pull_split": 1, "slice_lds": 1, "pull_lds": 0, "pull_unroll": 4, "pull_nt": 0,
+            "band0_deg": 128, "band0_bit": 5, "band1_deg": 8, "band1_bit": 3, "band2_deg": 0, "band2_bit": 3,
+            "band3_deg": 0, "band3_bit": 3}
 
 
 def apply(knobs):

@@ -36,7 +36,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--ks", default="14,18,20,22")
-    ap.add_argument("--min-degree", type=int, default=16)
     args = ap.parse_args()
     n = 1 << args.scale
     src, dst = o.rmat_edges(args.scale, 16, 0x5EED + args.scale)
@@ -45,7 +44,6 @@ def main():
     ctx = jg.Context((0,))
     rng = np.random.default_rng(1)
     out = {}
-    _lib.tune_set("split_min_degree", args.min_degree)
     for k in [int(x) for x in args.ks.split(",")]:
         s2 = order[rng.integers(0, 1 << k, len(dst))].astype(np.int64)
         r = {}
