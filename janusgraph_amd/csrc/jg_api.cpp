@@ -103,6 +103,19 @@ Tune& tune() {
     return t;
 }
 
+SideStream& side_stream() {
+    static SideStream cache[64];
+    int dev = 0;
+    JG_HIP(hipGetDevice(&dev));
+    SideStream& ss = cache[dev & 63];
+    if (!ss.stream) {
+        JG_HIP(hipStreamCreateWithFlags(&ss.stream, hipStreamNonBlocking));
+        JG_HIP(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+        JG_HIP(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
+    }
+    return ss;
+}
+
 int device_cu_count() {
     static int cache[64] = {0};
     int dev = 0;
@@ -210,6 +223,8 @@ int jg_tune_set(const char* key, int64_t value) {
         }
     } else if (k == "pull_split") {
         jg::tune().pull_split = value != 0;
+    } else if (k == "pull_overlap") {
+        jg::tune().pull_overlap = value != 0;
     } else if (k == "slice_lds") {
         jg::tune().slice_lds = value != 0;
     } else {

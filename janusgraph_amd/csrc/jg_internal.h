@@ -227,10 +227,19 @@ struct Tune {
     int64_t band_deg[4] = {128, 8, 0, 0};
     int band_bits[4] = {5, 3, 3, 3};
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
+    int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device
+// A second stream of the current device (created on first use, lives for the process) with a fork
+// and a join event: work independent of the main stream's runs beside it, e.g. the light rows of a
+// pull superstep next to the sliced split's merge kernels.
+struct SideStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+SideStream& side_stream();
 
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);

@@ -517,6 +517,17 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     PullArgs a = make_pull_args(csr, plan, split);
     const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
+    // With the split, the light rows (and hub finalize) run on the side stream beside the merge
+    // kernels: they touch other rows, and their 256-thread, LDS-free blocks fit next to a merge
+    // workgroup on every CU, filling its memory stalls.
+    hipStream_t ls = s;
+    SideStream* side = nullptr;
+    if (split && tune().pull_overlap) {
+        side = &side_stream();
+        JG_HIP(hipEventRecord(side->fork, s));
+        JG_HIP(hipStreamWaitEvent(side->stream, side->fork, 0));
+        ls = side->stream;
+    }
     if (split) {
         static bool attr = false;
         if (!attr) {
@@ -552,11 +563,11 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         const int u = tune().pull_unroll;
         const bool nt = tune().pull_nt != 0;
         if (u >= 8) {
-            if (nt) pull_kernel<Op, 8, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
-            else pull_kernel<Op, 8, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+            if (nt) pull_kernel<Op, 8, true><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
+            else pull_kernel<Op, 8, false><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
         } else {
-            if (nt) pull_kernel<Op, 4, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
-            else pull_kernel<Op, 4, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
+            if (nt) pull_kernel<Op, 4, true><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
+            else pull_kernel<Op, 4, false><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
         }
         JG_LAUNCH_CHECK();
     };
@@ -584,7 +595,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         launch((unsigned)blocks);
     }
     if (plan.num_hub_rows > 0) {
-        pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
+        pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, ls>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }
     if (split) {
@@ -600,6 +611,10 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         }
         pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, fb, split_partial);
         JG_LAUNCH_CHECK();
+    }
+    if (side) {
+        JG_HIP(hipEventRecord(side->join, side->stream));
+        JG_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
     if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);  // the whole superstep: every launch above
 }
