@@ -183,7 +183,7 @@ def main():
     traffic, traffic_src = pmc_traffic("PrOp", workload) if ws == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "pull superstep (pull_slice_kernel + pull_kernel + finalize kernels, PrOp)", "kernel_ms": round(kern_ms, 4),
+                "kernel": "PageRank superstep (pull_merge_kernel x bands + fixups + light-row pull_kernel + finalize kernels, PrOp)", "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": alg_bytes_launch}
     del local_nnz
 

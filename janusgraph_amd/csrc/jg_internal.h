@@ -127,8 +127,8 @@ struct Shard {
     DevBuf<double> pr_contrib[2];  // [P*S] full-length, ping-pong
     DevBuf<double> pr_rank;        // [rows]
     DevBuf<double> pr_hub_partial; // [num_chunks]
-    DevBuf<double> pr_split_partial;  // [8 * plan_in.split_rows]
-    DevBuf<int32_t> cc_split_partial; // [8 * plan_both.split_rows]
+    DevBuf<double> pr_split_partial;  // [plan_in.split_partial_len()]
+    DevBuf<int32_t> cc_split_partial; // [plan_both.split_partial_len()]
     DevBuf<int32_t> cc_msg[2];     // [P*S] label if sent else INT32_MAX
     DevBuf<int32_t> cc_label;      // [rows]
     DevBuf<int32_t> cc_hub_partial;
