@@ -223,6 +223,8 @@ int jg_tune_set(const char* key, int64_t value) {
         }
     } else if (k == "pull_split") {
         jg::tune().pull_split = value != 0;
+    } else if (k == "pull_short") {
+        jg::tune().pull_short = value != 0;
     } else if (k == "pull_overlap") {
         jg::tune().pull_overlap = value != 0;
     } else if (k == "slice_lds") {

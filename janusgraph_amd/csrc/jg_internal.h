@@ -227,6 +227,7 @@ struct Tune {
     int64_t band_deg[4] = {128, 8, 0, 0};
     int band_bits[4] = {5, 3, 3, 3};
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
+    int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
 };

@@ -34,6 +34,7 @@ struct PullArgs {
     int64_t class_block_begin[kNumClasses + 1];
     int64_t block_offset;  // diagnostic split launches (JG_PULL_SPLIT=1): first block of this launch
     int64_t skip_rows;     // rows [0, skip_rows) are folded by the XCD split: their hub chunks are skipped
+    int short_rows;        // 1-lane rows of <= 8 entries use fold_short (Tune::pull_short)
 };
 
 inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = false) {
@@ -53,6 +54,7 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = f
     for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = light ? p.light_block_begin[c] : p.class_block_begin[c];
     a.block_offset = 0;
     a.skip_rows = light ? p.split_rows : 0;
+    a.short_rows = tune().pull_short;
     return a;
 }
 
@@ -122,6 +124,34 @@ __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& ga
     return acc;
 }
 
+// Short rows (one lane per row, < 8 entries): all entries in one masked batch of 8.  Out-of-range
+// slots issue no load at all (exec-masked), instead of re-reading the last entry: a duplicate lane
+// still costs the TA/TD its cycles (tools/micro/td_mask.hip: cost scales with active lanes).
+template <class Op, bool NT, class G>
+__device__ __forceinline__ typename Op::T fold_short(const Op& op, const G& gather, const int32_t* __restrict__ col,
+                                                     int64_t j, int64_t j1) {
+    using T = typename Op::T;
+    constexpr int kMax = 8;
+    const int n = (int)(j1 - j);
+    int32_t c[kMax];
+#pragma unroll
+    for (int u = 0; u < kMax; ++u) {
+        c[u] = 0;
+        if (u < n) c[u] = load_col<NT>(col, j + u);
+    }
+    T v[kMax];
+#pragma unroll
+    for (int u = 0; u < kMax; ++u) {
+        v[u] = op.identity();
+        if (u < n) v[u] = gather(c[u]);
+    }
+    T acc = op.identity();
+#pragma unroll
+    for (int u = 0; u < kMax; ++u)
+        if (u < n) acc = op.combine(acc, v[u]);
+    return acc;
+}
+
 template <class Op, int U, bool NT>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
                                                        int64_t j1, int stride) {
@@ -142,7 +172,10 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
     if (valid) {
         const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
         hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
-        if (!hub && op.active(row)) acc = fold_strided<Op, U, NT>(op, gather, a.col, j0 + sub, j1, L);
+        if (!hub && op.active(row)) {
+            if (L == 1 && a.short_rows && j1 - j0 <= 8) acc = fold_short<Op, NT>(op, gather, a.col, j0, j1);
+            else acc = fold_strided<Op, U, NT>(op, gather, a.col, j0 + sub, j1, L);
+        }
     }
 #pragma unroll
     for (int o = L / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
