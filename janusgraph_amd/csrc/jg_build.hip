@@ -787,7 +787,9 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         }
         if (g.flags & JG_ADJ_BOTH) {
             a.which = 2;
+            a.sbits = tune().pull_split ? 8 : 0;  // CC's pull adjacency: sub-slice-ordered rows
             build_csr(sh, a, nullptr, sh.both, s);
+            a.sbits = 0;
             build_pull_plan(sh, sh.both, sh.plan_both, g.padded_len());
         }
         JG_HIP(hipStreamSynchronize(s));

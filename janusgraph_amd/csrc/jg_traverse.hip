@@ -509,7 +509,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             struct St {
                 DevBuf<unsigned long long> F[2], vis;
                 DevBuf<int32_t> depth, changed;
-                DevBuf<unsigned long long> hub, split;
+                DevBuf<unsigned long long> hub;
             };
             std::vector<St> st(g.shards.size());
             for (size_t i = 0; i < g.shards.size(); ++i) {
@@ -527,7 +527,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.depth.alloc(std::max<int64_t>(sh.rows * ns, 1));
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
-                t.split.alloc(plan.split_partial_len());
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
@@ -570,8 +569,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     op.base = (int64_t)sh.index * g.S;
                     op.lvl = level + 1;
                     op.full = full;
+                    // no sliced split (split_partial null): the class kernel skips fully visited rows
+                    // (MsBfsOp::active), which whole-entry merge tasks cannot
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                t.split.get());
+                                (unsigned long long*)nullptr);
                 }
                 {
                     std::vector<void*> bufs;

@@ -1,5 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/sw25
+mkdir -p gpurun_out/sw26
 export TMPDIR=/tmp
-timeout -k 10 500 python tools/pr_ab.py --rounds 7 ns_b8:pull_short=0 s_b16:pull_short=1,band1_deg=16 ns_b16:pull_short=0,band1_deg=16 s_b8:pull_short=1 s_b12:pull_short=1,band1_deg=12 > gpurun_out/sw25/ab.json 2> gpurun_out/sw25/ab.err || exit 5
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/sw26/pytest.log 2>&1 || exit 3
+timeout -k 10 400 python tools/big_configs.py --scale 22 --out gpurun_out/sw26/big22.json > gpurun_out/sw26/big22.log 2>&1 || exit 4
+timeout -k 10 900 python tools/big_configs.py --scale 26 --out gpurun_out/sw26/big26.json > gpurun_out/sw26/big26.log 2>&1 || exit 5
 echo done
