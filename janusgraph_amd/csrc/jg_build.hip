@@ -774,24 +774,25 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         }
         SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
-        if (g.flags & JG_ADJ_IN) {
-            a.which = 0;
-            a.sbits = tune().pull_split ? 8 : 0;  // PageRank's pull adjacency: sub-slice-ordered rows
-            build_csr(sh, a, w, sh.in, s);
-            a.sbits = 0;
-            build_pull_plan(sh, sh.in, sh.plan_in, g.padded_len());
-        }
+        // The pull adjacencies (IN: PageRank, BOTH: CC) are first built sub-slice-ordered, which the
+        // split bands are cut from (separate copies), then rebuilt column-ordered: traversals scan
+        // rows in column (degree-rank) order, and bottom-up BFS exits earlier that way.
+        auto build_pull_csr = [&](int which, const int32_t* wt, Csr& csr, PullPlan& plan) {
+            a.which = which;
+            a.sbits = tune().pull_split ? 8 : 0;
+            build_csr(sh, a, wt, csr, s);
+            build_pull_plan(sh, csr, plan, g.padded_len());
+            if (a.sbits) {
+                a.sbits = 0;
+                build_csr(sh, a, wt, csr, s);
+            }
+        };
+        if (g.flags & JG_ADJ_IN) build_pull_csr(0, w, sh.in, sh.plan_in);
         if (g.flags & JG_ADJ_OUT) {
             a.which = 1;
             build_csr(sh, a, w, sh.out, s);
         }
-        if (g.flags & JG_ADJ_BOTH) {
-            a.which = 2;
-            a.sbits = tune().pull_split ? 8 : 0;  // CC's pull adjacency: sub-slice-ordered rows
-            build_csr(sh, a, nullptr, sh.both, s);
-            a.sbits = 0;
-            build_pull_plan(sh, sh.both, sh.plan_both, g.padded_len());
-        }
+        if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, nullptr, sh.both, sh.plan_both);
         JG_HIP(hipStreamSynchronize(s));
         first = false;
     }
