@@ -16,11 +16,11 @@ namespace jg {
 
 namespace {
 thread_local std::string g_last_error;
+}  // namespace
 
 void rccl_check(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) fail(JG_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
-}  // namespace
 
 void fail(int code, const std::string& msg) { throw Error(code, msg); }
 
@@ -229,6 +229,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().pull_overlap = value != 0;
     } else if (k == "slice_lds") {
         jg::tune().slice_lds = value != 0;
+    } else if (k == "halo") {
+        jg::tune().halo = value != 0;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }

@@ -198,6 +198,7 @@ struct SelectArgs {
     int which;
     int cbits;
     int sbits;  // 0, or 8: entries of a row ordered by (sub_key(col), col)
+    CompactMap cm;  // sharded pull adjacency with a halo plan: columns become compact ids
 };
 
 __device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
@@ -245,14 +246,16 @@ __global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, cons
         const int64_t gs = a.padded[s], gd = a.padded[d];
         const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
         if ((a.which == 1 || a.which == 2) && own_s) {
+            const int64_t c = a.cm.on() ? (int64_t)a.cm(gd) : gd;
             keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? sub_key(gd) : 0) << a.cbits) | (uint64_t)gd;
+                        ((uint64_t)(a.sbits ? sub_key(c) : 0) << a.cbits) | (uint64_t)c;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
         if ((a.which == 0 || a.which == 2) && own_d) {
+            const int64_t c = a.cm.on() ? (int64_t)a.cm(gs) : gs;
             keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? sub_key(gs) : 0) << a.cbits) | (uint64_t)gs;
+                        ((uint64_t)(a.sbits ? sub_key(c) : 0) << a.cbits) | (uint64_t)c;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
@@ -381,6 +384,7 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     DevBuf<uint32_t> eidx;
     const int64_t nnz = select_keys(a, keys, eidx, weight != nullptr, s);
     const int rbits = bits_for((uint64_t)std::max<int64_t>(sh.rows - 1, 0));
+    if (rbits + a.cbits + a.sbits > 64) fail(JG_ERR_UNSUPPORTED, "CSR sort key exceeds 64 bits");
     prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits + a.sbits, s);
     csr.rows = sh.rows;
     csr.nnz = nnz;
@@ -772,29 +776,50 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                      sh.out_degree.get());
             JG_LAUNCH_CHECK();
         }
-        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0};
+        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0, CompactMap{}};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
         // The pull adjacencies (IN: PageRank, BOTH: CC) are first built sub-slice-ordered, which the
         // split bands are cut from (separate copies), then rebuilt column-ordered: traversals scan
         // rows in column (degree-rank) order, and bottom-up BFS exits earlier that way.
-        auto build_pull_csr = [&](int which, const int32_t* wt, Csr& csr, PullPlan& plan) {
+        // Sharded: a halo plan first, whose compact ids the CSR columns then hold.
+        auto build_pull_csr = [&](int which, const int32_t* wt, Csr& csr, PullPlan& plan, Halo& halo) {
             a.which = which;
+            a.cm = CompactMap{};
+            int64_t col_space = g.padded_len();
+            if (P > 1 && tune().halo) {
+                build_halo(g, sh, e.src[li], e.dst[li], padded.get(), m, which, halo, s);
+                a.cm = halo.map(g.S, r);
+                col_space = halo.C;
+            }
+            a.cbits = std::max(cbits, bits_for((uint64_t)(col_space - 1)));  // compact ids may exceed P*S
             a.sbits = tune().pull_split ? 8 : 0;
             build_csr(sh, a, wt, csr, s);
-            build_pull_plan(sh, csr, plan, g.padded_len());
+            build_pull_plan(sh, csr, plan, col_space);
+            if (halo.on) {  // segmented compact vector: every segment's hot entries are its prefix
+                plan.lds_ok = true;
+                plan.seg_tbits = halo.tbits;
+                plan.nseg = P;
+            }
             if (a.sbits) {
                 a.sbits = 0;
                 build_csr(sh, a, wt, csr, s);
             }
+            if (halo.on) release_halo_maps(halo);
+            a.cm = CompactMap{};
+            a.cbits = cbits;
         };
-        if (g.flags & JG_ADJ_IN) build_pull_csr(0, w, sh.in, sh.plan_in);
+        if (g.flags & JG_ADJ_IN) build_pull_csr(0, w, sh.in, sh.plan_in, sh.halo_in);
         if (g.flags & JG_ADJ_OUT) {
             a.which = 1;
             build_csr(sh, a, w, sh.out, s);
         }
-        if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, nullptr, sh.both, sh.plan_both);
+        if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, nullptr, sh.both, sh.plan_both, sh.halo_both);
         JG_HIP(hipStreamSynchronize(s));
         first = false;
+    }
+    if (P > 1 && tune().halo) {
+        if (g.flags & JG_ADJ_IN) check_halo_counts(g, JG_ADJ_IN);
+        if (g.flags & JG_ADJ_BOTH) check_halo_counts(g, JG_ADJ_BOTH);
     }
     int64_t bytes = 0;
     for (auto& sp : g.shards) bytes += sp->in.bytes() + sp->out.bytes() + sp->both.bytes() + sp->out_degree.bytes();

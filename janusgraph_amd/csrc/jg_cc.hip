@@ -27,7 +27,7 @@ struct CcOp {
     int32_t* __restrict__ msg_out;       // full length (owned slice written)
     int32_t* __restrict__ label;         // [rows]
     int32_t* __restrict__ changed;
-    int64_t base;
+    VecPos pos;                          // owned row -> its slot in the gathered vector
     __device__ __forceinline__ int32_t identity() const { return INT_MAX; }
     __device__ __forceinline__ int32_t combine(int32_t a, int32_t b) const { return a < b ? a : b; }
     __device__ __forceinline__ int32_t gather(int32_t c) const { return msg[c]; }
@@ -38,10 +38,10 @@ struct CcOp {
     __device__ __forceinline__ void finalize(int64_t row, int32_t m) const {
         if (m < label[row]) {
             label[row] = m;
-            msg_out[base + row] = m;
+            msg_out[pos(row)] = m;
             *changed = 1;
         } else {
-            msg_out[base + row] = INT_MAX;
+            msg_out[pos(row)] = INT_MAX;
         }
     }
 };
@@ -77,17 +77,17 @@ __global__ void lex_rank_scatter_kernel(const uint32_t* __restrict__ vals, int64
 }
 
 __global__ void cc_init_kernel(const int32_t* __restrict__ lab0, const int64_t* __restrict__ rp, int64_t rows,
-                               int64_t base, int32_t* __restrict__ label, int32_t* __restrict__ msg) {
+                               VecPos pos, int32_t* __restrict__ label, int32_t* __restrict__ msg) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
         label[l] = lab0[l];
-        msg[base + l] = (rp[l + 1] > rp[l]) ? lab0[l] : INT_MAX;  // only vertices with edges send
+        msg[pos(l)] = (rp[l + 1] > rp[l]) ? lab0[l] : INT_MAX;  // only vertices with edges send
     }
 }
 
 void exchange_msg(Graph& g, int which) {
     std::vector<void*> bufs;
     for (auto& sp : g.shards) bufs.push_back(sp->cc_msg[which].get());
-    exchange_allgather(g, bufs, sizeof(int32_t), ncclInt32);
+    exchange_vec(g, JG_ADJ_BOTH, bufs, sizeof(int32_t), ncclInt32);
 }
 
 }  // namespace
@@ -126,10 +126,10 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         }
         for (int64_t d = 0; d < n; ++d) vid_of_rank[rank_of[d]] = hv[d];
     }
-    const int64_t len = g.padded_len();
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
         DeviceGuard dg(sh.device);
+        const int64_t len = g.vec_len(sh, JG_ADJ_BOTH);
         for (int k = 0; k < 2; ++k) {
             if (sh.cc_msg[k].size() != (size_t)len) sh.cc_msg[k].alloc(len);
             JG_HIP(hipMemsetAsync(sh.cc_msg[k].get(), 0x7F, sh.cc_msg[k].bytes(), sh.stream));  // ~INT_MAX
@@ -144,7 +144,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         if (sh.rows) {
             copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
             cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
-                                                                        (int64_t)sh.index * g.S, sh.cc_label.get(),
+                                                                        g.vec_pos(sh, JG_ADJ_BOTH), sh.cc_label.get(),
                                                                         sh.cc_msg[0].get());
             JG_LAUNCH_CHECK();
         }
@@ -174,7 +174,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             op.msg_out = sh.cc_msg[cur ^ 1].get();
             op.label = sh.cc_label.get();
             op.changed = sh.cc_changed.get();
-            op.base = (int64_t)sh.index * g.S;
+            op.pos = g.vec_pos(sh, JG_ADJ_BOTH);
             launch_pull(sh.both, sh.plan_both, op, sh.cc_hub_partial.get(), sh.stream, ctx.profiling ? &ctx : nullptr,
                         &sh, sh.cc_split_partial.get());
         }

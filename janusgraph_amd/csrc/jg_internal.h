@@ -8,8 +8,15 @@
 //   in-place allgather of the owned slices IS the exchange step (RCCL over xGMI).
 //   Csr: row_ptr int64 [rows+1], col int32 [nnz] (global ids), optional weight int32 [nnz].
 //   Pull programs stream col once per superstep and gather the source vector at col.
+//   Sharded (P > 1, tune halo = 1): the pull adjacencies (IN, BOTH) instead hold COMPACT column ids:
+//   each shard's gathered vector holds its own rows, then one segment per peer with just the peer's
+//   vertices its rows read (CompactMap), each in degree order, so every segment's hottest entries are
+//   its prefix.  The exchange step is a sparse halo exchange (pack, RCCL send/recv per peer straight
+//   into the peer's segment) of the values each peer actually reads — ~21% of the dense allgather
+//   for RMAT-24 at P = 8.
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -87,7 +94,9 @@ struct PullPlan {
         for (const auto& b : bands) n += b->subrows + b->tasks;
         return std::max<int64_t>(n, 1);
     }
-    bool lds_ok = false;  // the gathered vector's hot prefix is [0, hot) (single shard)
+    bool lds_ok = false;  // the gathered vector's hot entries are segment prefixes (see seg_tbits)
+    int seg_tbits = 31;   // segmented compact vector (sharded, halo): nseg segments of stride 2^seg_tbits
+    int nseg = 1;         // one segment: the hot prefix is [0, hot)
 };
 constexpr int kXcds = 8;
 // Sub-slices of the column space: the 128-byte lines of an fp64 vector (16 elements) are hashed to
@@ -112,6 +121,54 @@ __host__ __device__ __forceinline__ int sub_slice(int64_t c, int bits) { return 
 
 struct Ctx;
 
+// Compact column ids of one shard's pull adjacency (sharded graphs).  The gathered vector is cut
+// into P segments of stride T = 2^tbits: segment 0 holds the shard's own rows [0, rows), segment
+// s(q) = q < r ? q + 1 : q the vertices of peer q that this shard reads, in the peer's local (degree)
+// order — exactly the run peer q sends, so it is received in place.  Every segment's hottest entries
+// are its prefix.
+struct CompactMap {
+    const uint32_t* bits = nullptr;   // [ceil(P*S/32)] needed remote vertices by global id
+    const int64_t* off = nullptr;     // [words + 1] exclusive popcount prefix of bits
+    const int64_t* qbase = nullptr;   // [P + 1] popcount prefix at q * S
+    int64_t S = 0;
+    int r = 0, tbits = 31;
+    __host__ __device__ bool on() const { return bits != nullptr; }
+    __device__ __forceinline__ int32_t operator()(int64_t g) const {
+        const int64_t q = g / S, l = g - q * S;
+        if (q == r) return (int32_t)l;
+        const uint32_t w = bits[g >> 5];
+        const int64_t rank = off[g >> 5] + __popc(w & ((1u << (g & 31)) - 1u)) - qbase[q];
+        return (int32_t)(((q < r ? q + 1 : q) << tbits) + rank);
+    }
+};
+
+// Halo plan of one shard's pull adjacency: which of its own values each peer reads (send lists, by
+// peer, ascending local ids) and how many values it reads from each peer (landing at the peer's
+// segment).  The lists are static, so a superstep moves values only, no indices.
+struct Halo {
+    bool on = false;
+    int tbits = 31;                      // segment stride 2^tbits
+    int64_t C = 0;                       // gathered vector length: P segments
+    DevBuf<uint32_t> bits;               // CompactMap storage
+    DevBuf<int64_t> off, qbase;
+    DevBuf<int32_t> send_src;            // [send_off[P]] own rows packed for the peers, by peer
+    std::vector<int64_t> send_off, recv_off;  // [P + 1] element offsets per peer
+    DevBuf<uint64_t> send_buf;           // 8-byte scratch elements (4-byte vectors use half)
+    int seg_of(int q, int r) const { return q < r ? q + 1 : q; }
+    CompactMap map(int64_t S, int r) const {
+        CompactMap m;
+        if (on) { m.bits = bits.get(); m.off = off.get(); m.qbase = qbase.get(); m.S = S; m.r = r; m.tbits = tbits; }
+        return m;
+    }
+};
+
+// Position of an owned row's value in a gathered vector: base + row (base = shard * S in the
+// full-length shard-major layout, 0 in a segmented compact vector).
+struct VecPos {
+    int64_t base = 0;
+    __device__ __forceinline__ int64_t operator()(int64_t row) const { return base + row; }
+};
+
 struct Shard {
     int device = 0;
     int index = 0;           // shard id r in [0, P)
@@ -120,6 +177,7 @@ struct Shard {
     int64_t rows = 0;        // owned rows (<= S)
     Csr in, out, both;
     PullPlan plan_in, plan_both;
+    Halo halo_in, halo_both;      // sharded graphs: compact vectors of the IN / BOTH pull adjacencies
     DevBuf<int32_t> out_degree;   // [rows] out-degree of owned vertices (PageRank edgeCount)
     std::vector<int32_t> dense_of_local;  // host: caller's dense index of each owned row
 
@@ -167,6 +225,17 @@ struct Graph {
     int64_t vid_of(int64_t dense) const { return vid.empty() ? dense : vid[dense]; }
     int64_t dense_of_vid(int64_t v) const;  // -1 if absent
     int64_t padded_len() const { return (int64_t)P * S; }
+    // adj: JG_ADJ_IN or JG_ADJ_BOTH — the pull adjacency whose gathered vector this is
+    const Halo& halo(const Shard& sh, uint32_t adj) const { return adj == JG_ADJ_BOTH ? sh.halo_both : sh.halo_in; }
+    int64_t vec_len(const Shard& sh, uint32_t adj) const {
+        const Halo& h = halo(sh, adj);
+        return h.on ? std::max<int64_t>(h.C, 1) : padded_len();
+    }
+    VecPos vec_pos(const Shard& sh, uint32_t adj) const {
+        VecPos p;
+        p.base = halo(sh, adj).on ? 0 : (int64_t)sh.index * S;
+        return p;
+    }
 };
 
 struct Ctx {
@@ -195,9 +264,22 @@ void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, con
                       int32_t* dsrc, int32_t* ddst, hipStream_t s);
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space);
 
-// ---- exchange (jg_api.cpp) ----
-// In-place allgather of every shard's owned slice [r*S, r*S+S) of a full-length vector.
+void rccl_check(ncclResult_t r, const char* what);
+
+// ---- exchange (jg_api.cpp, jg_halo.hip) ----
+// The exchange step of a gathered vector of the pull adjacency `adj` (JG_ADJ_IN / JG_ADJ_BOTH):
+// halo exchange when the shards hold compact vectors, else an in-place allgather of every shard's
+// owned slice [r*S, r*S+S) of the full-length vector.
+void exchange_vec(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
 void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
+void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
+// Builds shard sh's halo plan for adjacency `which` (0 IN, 2 BOTH) from the full edge list.
+void build_halo(Graph& g, Shard& sh, const int32_t* src, const int32_t* dst, const int32_t* padded, int64_t m,
+                int which, Halo& h, hipStream_t s);
+// The halo plans are a build-time structure only (the lists stay, the maps go).
+void release_halo_maps(Halo& h);
+// Checks that every shard's send counts equal its peers' receive counts (RCCL: count allgather).
+void check_halo_counts(Graph& g, uint32_t adj);
 
 // ---- programs ----
 void pagerank_begin(Graph& g, double damping, int64_t vertex_count);
@@ -230,6 +312,7 @@ struct Tune {
     int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
+    int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

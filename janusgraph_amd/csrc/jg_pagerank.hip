@@ -9,7 +9,8 @@
 // VertexMemoryHandler.java:121-151); pulling over the in-CSR is the same reverse-adjacency read.
 //
 // Per power superstep and shard: contrib_out[g] = rank/edgeCount for owned rows, gathered from the
-// full-length contrib_in at col[]; then the owned slices are allgathered (RCCL) into every shard.
+// contrib_in at col[] (full length, or the shard's compact vector); then the exchange step
+// (allgather or halo exchange, RCCL) refreshes every shard's copy.
 // Algorithmic bytes per superstep: 12*m + 32*n.
 #include "jg_pull.h"
 
@@ -23,7 +24,7 @@ struct PrOp {
     double* __restrict__ contrib_out;  // full length (owned slice written)
     double* __restrict__ rank;         // [rows]
     const int32_t* __restrict__ outdeg;
-    int64_t base;                      // shard * S
+    VecPos pos;                        // owned row -> its slot in the gathered vector
     double damping, teleport;
     __device__ __forceinline__ double identity() const { return 0.0; }
     __device__ __forceinline__ double combine(double a, double b) const { return __dadd_rn(a, b); }
@@ -36,23 +37,23 @@ struct PrOp {
         // (dampingFactor * newPageRank) + ((1D - dampingFactor) / vertexCount), no contraction
         const double r = __dadd_rn(__dmul_rn(damping, s), teleport);
         rank[row] = r;
-        contrib_out[base + row] = r / (double)outdeg[row];
+        contrib_out[pos(row)] = r / (double)outdeg[row];
     }
 };
 
 // superstep 1: rank = 1/N, contrib = rank / edgeCount (edgeCount = out-degree as a double)
-__global__ void pr_init_kernel(const int32_t* __restrict__ outdeg, int64_t rows, int64_t base, double initial,
+__global__ void pr_init_kernel(const int32_t* __restrict__ outdeg, int64_t rows, VecPos pos, double initial,
                                double* __restrict__ contrib, double* __restrict__ rank) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
         rank[l] = initial;
-        contrib[base + l] = initial / (double)outdeg[l];
+        contrib[pos(l)] = initial / (double)outdeg[l];
     }
 }
 
 void exchange_contrib(Graph& g, int which) {
     std::vector<void*> bufs;
     for (auto& sp : g.shards) bufs.push_back(sp->pr_contrib[which].get());
-    exchange_allgather(g, bufs, sizeof(double), ncclFloat64);
+    exchange_vec(g, JG_ADJ_IN, bufs, sizeof(double), ncclFloat64);
 }
 
 }  // namespace
@@ -60,10 +61,10 @@ void exchange_contrib(Graph& g, int which) {
 void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
     if (!(g.flags & JG_ADJ_IN)) fail(JG_ERR_UNSUPPORTED, "PageRank needs a graph built with JG_ADJ_IN");
     if (vertex_count == 0) fail(JG_ERR_ARG, "vertexCount must be non-zero");
-    const int64_t len = g.padded_len();
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
         DeviceGuard dg(sh.device);
+        const int64_t len = g.vec_len(sh, JG_ADJ_IN);
         for (int k = 0; k < 2; ++k) {
             if (sh.pr_contrib[k].size() != (size_t)len) sh.pr_contrib[k].alloc(len);
             JG_HIP(hipMemsetAsync(sh.pr_contrib[k].get(), 0, sh.pr_contrib[k].bytes(), sh.stream));
@@ -77,7 +78,7 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
         const double initial = 1.0 / (double)vertex_count;
         if (sh.rows > 0) {
             pr_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.out_degree.get(), sh.rows,
-                                                                        (int64_t)sh.index * g.S, initial,
+                                                                        g.vec_pos(sh, JG_ADJ_IN), initial,
                                                                         sh.pr_contrib[0].get(), sh.pr_rank.get());
             JG_LAUNCH_CHECK();
         }
@@ -104,7 +105,7 @@ void pagerank_steps(Graph& g, int nsteps) {
             op.contrib_out = sh.pr_contrib[nxt].get();
             op.rank = sh.pr_rank.get();
             op.outdeg = sh.out_degree.get();
-            op.base = (int64_t)sh.index * g.S;
+            op.pos = g.vec_pos(sh, JG_ADJ_IN);
             op.damping = g.pr_damping;
             op.teleport = teleport;
             launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get());

@@ -306,32 +306,44 @@ struct MergeArgs {
     int bits;
 };
 
-// Gathers of sub-slice h of a 2^bits band: ids below `hot_ids` come from the LDS image of the
-// sub-slice's first lines (line group c >> (4 + bits) holds one line of h; it sits at LDS line
-// c >> (4 + bits)), the rest from global memory.
+// The hot entries of a gathered vector: the first `hs` entries of each of its `nseg` segments
+// (stride 2^tbits; one segment of stride 2^31 on a single shard, a shard's own rows + one per peer
+// on a sharded compact vector).
+struct HotSegs {
+    int32_t hs = 0;
+    int tbits = 31;
+    int nseg = 1;
+};
+
+// Gathers of sub-slice h of a 2^bits band: hot ids come from the LDS image of the sub-slice's lines
+// in the hot entries (line group c >> (4 + bits) of a segment holds one line of h; segment s's group
+// j sits at LDS line s * hg + j), the rest from global memory.
 template <class Op>
 struct SliceLdsGather {
     using T = typename Op::T;
     const Op& op;
     lds_ptr<const T> lds;
-    int32_t hot_ids;
-    int gshift;  // 4 + bits
-    // Cold lanes read the identity cell just past the staged lines: no select, so the compiler
-    // cannot turn the read into a branch.
+    uint32_t hs, tmask, hg;
+    int tbits, gshift;  // gshift = 4 + bits
+    uint32_t idcell;    // the identity cell just past the staged lines
+    __device__ __forceinline__ bool is_hot(int32_t c) const { return ((uint32_t)c & tmask) < hs; }
+    // Cold lanes read the identity cell: no select, so the compiler cannot turn the read into a branch.
     __device__ __forceinline__ T hot(int32_t c) const {
-        return lds[c < hot_ids ? (((c >> gshift) << 4) | (c & 15)) : (hot_ids >> (gshift - 4))];
+        const uint32_t u = (uint32_t)c, off = u & tmask;
+        const uint32_t grp = (u >> tbits) * hg + (off >> gshift);
+        return lds[off < hs ? ((grp << 4) | (u & 15u)) : idcell];
     }
     // Only cold lanes load (exec-masked); the others keep identity().
     __device__ __forceinline__ T cold(int32_t c) const {
         T v = op.identity();
-        if (c >= hot_ids) v = op.gather(c);
+        if (!is_hot(c)) v = op.gather(c);
         return v;
     }
 };
 
 template <class Op, bool LDS>
 __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
-                                                                   typename Op::T* __restrict__ carry, int32_t hot) {
+                                                                   typename Op::T* __restrict__ carry, HotSegs hs) {
     using T = typename Op::T;
     extern __shared__ __align__(16) unsigned char merge_lds[];
     const int per = (1 << a.bits) >> 3;  // sub-slices per XCD
@@ -341,17 +353,19 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     lds_ptr<T> hotv = (lds_ptr<T>)merge_lds;
     const int gshift = 4 + a.bits;
+    const int hg = hs.hs >> gshift;  // hot line groups per segment
+    const int nl = hs.nseg * hg;     // LDS lines
     if constexpr (LDS) {
-        // LDS line i = the line of sub-slice h in line group i (a permutation of each aligned group)
+        // LDS line i = the line of sub-slice h in hot line group i (a permutation of each aligned group)
         const T* src = op.vec();
-        const int nl = hot >> gshift;
         const uint32_t mask = (1u << a.bits) - 1;
         // kStage loads in flight per thread: with 2^bits sub-slices the image lines are scattered over
         // 2^bits x the image span, so a load-store-load loop would pay one memory round trip each
         constexpr int kStage = 8;
         auto src_of = [&](int i) {
-            const int grp = i >> 4;
-            const int64_t line = ((int64_t)grp << a.bits) + (int64_t)(h ^ (sub_hash((int64_t)grp << gshift) & mask));
+            const int sg = i >> 4, seg = sg / hg;
+            const int64_t grp = ((int64_t)seg << (hs.tbits - gshift)) + (sg - seg * hg);
+            const int64_t line = (grp << a.bits) + (int64_t)(h ^ (sub_hash(grp << gshift) & mask));
             return src + line * 16 + (i & 15);
         };
         const int total = nl * 16;
@@ -371,7 +385,8 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
         __syncthreads();
     }
-    const SliceLdsGather<Op> lg{op, hotv, hot, gshift};
+    const SliceLdsGather<Op> lg{op, hotv, (uint32_t)hs.hs, (uint32_t)((hs.tbits >= 31) ? 0x7FFFFFFFu : ((1u << hs.tbits) - 1u)),
+                                (uint32_t)hg, hs.tbits, gshift, (uint32_t)nl * 16u};
     const int64_t base = a.sub_base[h];
     const int64_t ntask = a.sub_base[h + 1] - base;
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
@@ -491,22 +506,36 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 // Sub-rows that span tasks: the sub-row's first task wrote partial[j]; every later task it covers left
 // its segment in carry[t] (meta[t] = (j, 1)).  The first carry of each run adds the run in task order.
 // (The first task of a sub-slice is never a carry: sub-slices start at a sub-row start.)
+// Carries of every band in one launch: thread x of [0, sum of tasks) takes task x - task_begin[b] of
+// band b.
+constexpr int kMaxBands = 4;
+struct FixupBands {
+    const int32_t* meta[kMaxBands];
+    int64_t task_begin[kMaxBands + 1];
+    int64_t part_off[kMaxBands], carry_off[kMaxBands];
+    int n;
+};
 template <class Op>
-__global__ void pull_merge_fixup_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
-                                        const typename Op::T* __restrict__ carry) {
+__global__ void pull_merge_fixup_kernel(FixupBands fb, Op op, typename Op::T* __restrict__ split_partial) {
     using T = typename Op::T;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.tasks; t += (int64_t)gridDim.x * blockDim.x) {
-        if (!a.meta[2 * t + 1]) continue;
-        const int32_t j = a.meta[2 * t];
-        if (a.meta[2 * (t - 1) + 1] && a.meta[2 * (t - 1)] == j) continue;  // not the first carry of the run
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < fb.task_begin[fb.n];
+         x += (int64_t)gridDim.x * blockDim.x) {
+        int b = 0;
+        while (x >= fb.task_begin[b + 1]) ++b;
+        const int64_t t = x - fb.task_begin[b], tasks = fb.task_begin[b + 1] - fb.task_begin[b];
+        const int32_t* __restrict__ meta = fb.meta[b];
+        if (!meta[2 * t + 1]) continue;
+        const int32_t j = meta[2 * t];
+        if (meta[2 * (t - 1) + 1] && meta[2 * (t - 1)] == j) continue;  // not the first carry of the run
+        T* __restrict__ partial = split_partial + fb.part_off[b];
+        const T* __restrict__ carry = split_partial + fb.carry_off[b];
         T acc = partial[j];
-        for (int64_t u = t; u < a.tasks && a.meta[2 * u + 1] && a.meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
+        for (int64_t u = t; u < tasks && meta[2 * u + 1] && meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
         partial[j] = acc;
     }
 }
 
 // Row r of the split: fold its non-empty sub-slices in h order.
-constexpr int kMaxBands = 4;
 struct FinalizeBands {
     const int32_t* sub_index[kMaxBands];
     int64_t row_begin[kMaxBands];
@@ -527,12 +556,21 @@ __global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb
         const T* __restrict__ part = partial + fb.part_off[b];
         T acc = op.identity();
         bool first = true;
-        for (int hh = 0; hh < S; ++hh) {
-            const int32_t j = si[(int64_t)hh * NR + i];
-            if (j >= 0) {
-                acc = first ? part[j] : op.combine(acc, part[j]);
-                first = false;
-            }
+        // batches of 8 sub-slices (S >= 8): all index loads, then all partial loads, then the fold in
+        // h order, so a hub row's 32 sub-slices cost 4 round trips instead of 32 dependent pairs
+        for (int h0 = 0; h0 < S; h0 += 8) {
+            int32_t j[8];
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) j[u] = si[(int64_t)(h0 + u) * NR + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j[u] >= 0) {
+                    acc = first ? v[u] : op.combine(acc, v[u]);
+                    first = false;
+                }
         }
         op.finalize(r, acc);
     }
@@ -579,16 +617,33 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const int64_t S = 1ll << bd.bits, gsz = 16 * S;
             // a multiple of S workgroups: every sub-slice gets grid / S of them
             const unsigned grid = (unsigned)std::max<int64_t>(S, device_cu_count() / S * S);
+            // shared equally by the segments; a segment's hot part stays below its stride (the
+            // past-the-end sentinel INT32_MAX must test cold)
             const int64_t hot_max = (int64_t)(kMergeLdsBytes / sizeof(T) - 16) * S;
             const bool lds_ok = plan.lds_ok && tune().slice_lds;
-            const int32_t hot = lds_ok ? (int32_t)(std::min<int64_t>(hot_max, plan.col_space) / gsz * gsz) : 0;
-            if (hot > 0)
-                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hot / S + 1) * sizeof(T), s>>>(ma, op, part,
-                                                                                                       carry, hot);
+            HotSegs hs;
+            hs.tbits = plan.seg_tbits;
+            hs.nseg = plan.nseg;
+            const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
+            hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
+            if (hs.hs > 0)
+                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), s>>>(
+                    ma, op, part, carry, hs);
             else
-                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, 0);
+                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, hs);
             JG_LAUNCH_CHECK();
-            pull_merge_fixup_kernel<Op><<<grid_for(bd.tasks), kBlock, 0, s>>>(ma, op, part, carry);
+        }
+        FixupBands fx{};
+        for (const auto& bp : plan.bands) {
+            if (fx.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
+            fx.meta[fx.n] = bp->meta.get();
+            fx.part_off[fx.n] = bp->part_off;
+            fx.carry_off[fx.n] = bp->carry_off;
+            fx.task_begin[fx.n + 1] = fx.task_begin[fx.n] + bp->tasks;
+            ++fx.n;
+        }
+        if (fx.task_begin[fx.n] > 0) {
+            pull_merge_fixup_kernel<Op><<<grid_for(fx.task_begin[fx.n]), kBlock, 0, s>>>(fx, op, split_partial);
             JG_LAUNCH_CHECK();
         }
     }
@@ -604,7 +659,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         }
         JG_LAUNCH_CHECK();
     };
-    if (!split && tune().pull_lds > 0 && plan.lds_ok) {  // LDS-cached hot prefix (single shard, unsliced)
+    if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
         const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
         if (plan.num_chunks > 0) launch((unsigned)plan.num_chunks);  // hub chunks: blocks [0, num_chunks)
         const size_t bytes = (size_t)hot * sizeof(T);
@@ -627,7 +682,8 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     } else if (blocks > 0) {
         launch((unsigned)blocks);
     }
-    if (plan.num_hub_rows > 0) {
+    // hub rows are the first rows (degree order); with the split they are all its rows already
+    if (plan.num_hub_rows > 0 && !(split && plan.num_hub_rows <= plan.split_rows)) {
         pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, ls>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }

@@ -256,7 +256,8 @@ struct MsBfsOp {
     T* __restrict__ visited;    // [rows]
     int32_t* __restrict__ depth;  // [nsrc * rows]
     int32_t* __restrict__ changed;
-    int64_t rows, base;
+    int64_t rows;
+    VecPos pos;                 // owned row -> its slot in the gathered vector
     int32_t lvl;
     T full;
     __device__ __forceinline__ T identity() const { return 0ull; }
@@ -268,7 +269,7 @@ struct MsBfsOp {
     __device__ __forceinline__ bool active(int64_t row) const { return visited[row] != full; }
     __device__ __forceinline__ void finalize(int64_t row, T acc) const {
         T nw = acc & ~visited[row] & full;
-        Fout[base + row] = nw;
+        Fout[pos(row)] = nw;
         if (nw) {
             visited[row] |= nw;
             *changed = 1;
@@ -283,13 +284,13 @@ struct MsBfsOp {
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
                                   unsigned long long* __restrict__ visited, int32_t* __restrict__ depth, int64_t rows,
-                                  int64_t base) {
+                                  VecPos pos) {
     // sequential over the (<= 64) sources: several sources may share a vertex
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     for (int s = 0; s < nsrc; ++s) {
         const int64_t l = local_src[s];
         if (l < 0) continue;
-        F[base + l] |= 1ull << s;
+        F[pos(l)] |= 1ull << s;
         visited[l] |= 1ull << s;
         depth[(int64_t)s * rows + l] = 0;
     }
@@ -377,6 +378,9 @@ BfsCsrs pick_csrs(const Shard& sh, int direction) {
         fail(JG_ERR_UNSUPPORTED, "directed traversal needs JG_ADJ_OUT and/or JG_ADJ_IN");
     return {push->present() ? push : nullptr, pull->present() ? pull : nullptr};
 }
+
+// the pull adjacency of a traversal, as the key of its gathered vector's layout (Graph::vec_pos)
+uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ? JG_ADJ_BOTH : JG_ADJ_IN; }
 
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
 // Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
@@ -500,7 +504,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         prof_collect(ctx, g);
     } else {
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
-        const int64_t len = g.padded_len();
         float total_ms = 0;
         int max_levels = 0;
         for (int b0 = 0; b0 < nsrc; b0 += 64) {
@@ -521,6 +524,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 if (c.pull == &sh.out) fail(JG_ERR_UNSUPPORTED, "multi-source IN traversal is not supported");
                 (void)plan;
                 St& t = st[i];
+                const int64_t len = g.vec_len(sh, adj_of(sh, c));
                 t.F[0].alloc(len);
                 t.F[1].alloc(len);
                 t.vis.alloc(std::max<int64_t>(sh.rows, 1));
@@ -540,14 +544,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<int64_t> dloc(ns);
                 copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
                 msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth.get(),
-                                                          sh.rows, (int64_t)sh.index * g.S);
+                                                          sh.rows, g.vec_pos(sh, adj_of(sh, c)));
                 JG_LAUNCH_CHECK();
                 JG_HIP(hipStreamSynchronize(sh.stream));
             }
             {
                 std::vector<void*> bufs;
                 for (auto& t : st) bufs.push_back(t.F[0].get());
-                exchange_allgather(g, bufs, sizeof(unsigned long long), ncclUint64);
+                exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
             }
             JG_HIP(hipEventRecord(t0, sh0.stream));
             int cur = 0, level = 0;
@@ -566,7 +570,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     op.depth = t.depth.get();
                     op.changed = t.changed.get();
                     op.rows = sh.rows;
-                    op.base = (int64_t)sh.index * g.S;
+                    op.pos = g.vec_pos(sh, adj_of(sh, c));
                     op.lvl = level + 1;
                     op.full = full;
                     // no sliced split (split_partial null): the class kernel skips fully visited rows
@@ -577,7 +581,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 {
                     std::vector<void*> bufs;
                     for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
-                    exchange_allgather(g, bufs, sizeof(unsigned long long), ncclUint64);
+                    exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
                 }
                 int32_t any = 0;
                 for (size_t i = 0; i < g.shards.size(); ++i) {

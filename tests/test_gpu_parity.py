@@ -217,13 +217,19 @@ def test_graph_info_counts(ctx):
     assert info["num_shards"] == 1
 
 
-@pytest.mark.parametrize("shards", [2, 3, 4])
-def test_logical_shards_match_single(oracle_lib, shards):
-    """P logical shards on one device (exchange by device copies) == 1 shard == oracle."""
+@pytest.mark.parametrize("shards,scale,halo", [(2, 13, 1), (3, 13, 1), (4, 13, 1), (8, 15, 1),
+                                               (2, 13, 0), (3, 13, 0)])
+def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
+    """P logical shards on one device (exchange by device copies) == 1 shard == oracle; halo = 1 is
+    the compact-vector halo exchange, 0 the dense allgather."""
     import janusgraph_amd as jg
     c = jg.Context((0,) * shards)
-    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 13)
-    g = c.build(vid, src, dst, flags=2 | 4)
+    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, scale)
+    jg._lib.tune_set("halo", halo)
+    try:
+        g = c.build(vid, src, dst, flags=2 | 4)
+    finally:
+        jg._lib.tune_set("halo", 1)
     rank, _ = g.pagerank(0.85, n, 15)
     r_ref, _ = oracle_lib.pagerank(n, ds, dd, 0.85, n, 15)
     assert_pr_close(rank, r_ref)
@@ -234,6 +240,9 @@ def test_logical_shards_match_single(oracle_lib, shards):
     depth = g.bfs(vid[srcs], 3)
     for k in range(len(srcs)):
         np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3))
+    depth = g.bfs(vid[srcs], 1)  # OUT traversal: bit-parallel pull over the IN adjacency
+    for k in range(len(srcs)):
+        np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 1))
     assert g.info()["num_shards"] == shards
     g.close()
     c.close()
