@@ -6,6 +6,9 @@
    g = (k % P) * S + k / P), every rank folds only its own rows, then the owned slices of the
    full-length vector are allgathered (the RCCL in-place allgather of jg_api.cpp exchange_allgather).
    The sharded result must equal the single-rank oracle bit for bit (same fold order per row).
+3. The sparse halo exchange (jg_halo.hip) with world_size 3 over gloo point-to-point: segmented
+   compact vectors, per-peer send lists, receive in place; parity with the oracle and matching
+   per-peer counts.
 """
 import os
 import socket
@@ -123,3 +126,129 @@ def test_two_rank_gloo_partition_and_exchange(oracle_lib):
     assert e0 + e1 == 16 << 11  # every edge is owned by exactly one shard
     assert abs(e0 - e1) < 0.05 * (e0 + e1)  # degree-sorted round-robin balances entries
     assert rel <= 1e-12
+
+
+def _halo_worker(rank, ws, port, out_q):
+    """The sparse halo exchange of jg_halo.hip, modelled rank by rank over gloo point-to-point:
+    need / send bitmaps from the full edge list, the segmented compact vector (own rows, then one
+    segment of stride T per peer, peer order q < r ? q + 1 : q), columns remapped to compact ids, and
+    per superstep: pack the own values each peer reads, send/recv per peer straight into the peer's
+    segment (ncclSend/ncclRecv in exchange_halo)."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    import torch
+    import torch.distributed as dist
+
+    from oracle import oracle as o
+
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    scale, n = 10, 1 << 10
+    s, t = o.rmat_edges(scale, 16, 9)
+    s, t = s.astype(np.int32), t.astype(np.int32)
+    indeg = np.bincount(t, minlength=n)
+    outdeg = np.bincount(s, minlength=n).astype(np.float64)
+    padded, S = padded_layout(indeg, ws)
+    gs, gt = padded[s], padded[t]
+    P, r = ws, rank
+    # halo_mark_kernel (IN adjacency: row = target, col = source)
+    rq, cq = gt // S, gs // S
+    need = np.zeros(P * S, bool)
+    need[gs[(rq == r) & (cq != r)]] = True
+    send = np.zeros(P * S, bool)
+    sel = (cq == r) & (rq != r)
+    send[rq[sel] * S + gs[sel] % S] = True
+    recv_cnt = [int(need[q * S:(q + 1) * S].sum()) if q != r else 0 for q in range(P)]
+    send_lists = [np.flatnonzero(send[q * S:(q + 1) * S]) if q != r else np.zeros(0, np.int64) for q in range(P)]
+    rows_own = int(min(S, (n - r + P - 1) // P))
+    T = 1 << 13
+    while T < max([rows_own, 8192] + recv_cnt):
+        T <<= 1
+    seg = lambda q: q + 1 if q < r else q  # noqa: E731
+    prefix = np.concatenate([[0], np.cumsum(need)])
+
+    def compact(g):
+        q, l = g // S, g % S
+        rk = prefix[g] - prefix[q * S]
+        return np.where(q == r, l, np.where(q < r, q + 1, q) * T + rk)
+
+    mine = rq == r
+    rows = gt[mine] - r * S
+    cols = compact(gs[mine])
+    key = np.lexsort((cols, rows))
+    rows, cols = rows[key], cols[key]
+    ptr = np.searchsorted(rows, np.arange(S + 1))
+    dense_of_padded = np.full(P * S, -1, np.int64)
+    dense_of_padded[padded] = np.arange(n)
+    od = np.zeros(P * S)
+    od[padded] = outdeg
+    vec = np.zeros(P * T)  # the shard's gathered vector
+    own_g = r * S + np.arange(S)
+    valid = dense_of_padded[own_g] >= 0
+    vec[:S][valid] = (1.0 / n) / od[own_g][valid]
+
+    def exchange():
+        reqs, bufs = [], {}
+        for q in range(P):
+            if q == r:
+                continue
+            if len(send_lists[q]):
+                reqs.append(dist.isend(torch.from_numpy(vec[send_lists[q]].copy()), q))
+            if recv_cnt[q]:
+                bufs[q] = torch.zeros(recv_cnt[q], dtype=torch.float64)
+                reqs.append(dist.irecv(bufs[q], q))
+        for rq_ in reqs:
+            rq_.wait()
+        for q, b in bufs.items():
+            vec[seg(q) * T:seg(q) * T + recv_cnt[q]] = b.numpy()
+
+    exchange()
+    iters = 10
+    rank_local = np.full(S, 1.0 / n)
+    for _ in range(iters - 1):
+        nxt = np.zeros(S)
+        for row in range(S):
+            acc = 0.0
+            for j in range(ptr[row], ptr[row + 1]):
+                acc = acc + vec[cols[j]]
+            rank_local[row] = 0.85 * acc + 0.15 / n
+            g = r * S + row
+            nxt[row] = rank_local[row] / od[g] if dense_of_padded[g] >= 0 else 0.0
+        vec[:S] = nxt
+        exchange()
+    # every peer sends exactly what each receiver expects (check_halo_counts)
+    counts = [None] * ws
+    dist.all_gather_object(counts, (r, [len(x) for x in send_lists], recv_cnt))
+    ok_counts = all(counts[q][1][p] == counts[p][2][q] for p in range(P) for q in range(P) if p != q)
+    vol = sum(recv_cnt)
+    ranks_all = [None] * ws
+    dist.all_gather_object(ranks_all, (r, rank_local.tolist()))
+    full = np.zeros(ws * S)
+    for rr, vals in ranks_all:
+        full[rr * S:(rr + 1) * S] = vals
+    got = full[padded]
+    rel = None
+    if rank == 0:
+        ref, _ = o.pagerank(n, s, t, 0.85, n, iters)
+        rel = float(np.max(np.abs(got - ref) / ref))
+    out_q.put((rank, ok_counts, vol, (P - 1) * S, rel))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_three_rank_gloo_halo_exchange(oracle_lib):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_counts, vol, dense, _ in res:
+        assert ok_counts
+        assert 0 < vol < dense  # the halo is a strict subset of the dense allgather
+    assert res[0][4] <= 1e-12
