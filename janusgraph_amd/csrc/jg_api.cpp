@@ -218,7 +218,7 @@ int jg_tune_set(const char* key, int64_t value) {
             JG_ARG(value >= 0, "band degree must be >= 0");
             jg::tune().band_deg[i] = value;
         } else {
-            JG_ARG(value >= 3 && value <= 8, "band bits must be in [3, 8]");
+            JG_ARG(value == 0 || (value >= 3 && value <= 8), "band bits must be 0 (automatic) or in [3, 8]");
             jg::tune().band_bits[i] = (int)value;
         }
     } else if (k == "pull_split") {

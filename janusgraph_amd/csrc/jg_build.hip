@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <climits>
 
+#include <cmath>
+
 #include "jg_internal.h"
 #include "jg_prim.h"
 
@@ -585,7 +587,21 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd) {
     JG_HIP(hipStreamSynchronize(s));
 }
 
-void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space) {
+// Sub-slices of an automatic band (band<i>_bit = 0, the default for the hub band): the LDS-resident
+// share of the vector is 2^bits x one CU's image.  Measured best (tools/pr_ab.py, ms per superstep):
+//   RMAT-22: 0.236 / 0.221 / 0.237 at 3 / 4 / 5 bits     RMAT-24: 0.94 / 0.98 / 1.14 at 5 / 6 / 7
+//   RMAT-25: 2.18 / 2.14 / 2.36 at 5 / 6 / 7             RMAT-26: 5.29 / 5.05 / 4.88 / 5.48 at 5 / 6 / 7 / 8
+// so log2(entries) - 19, within [4, 7], for the 8-byte PageRank vector (IN adjacency).  CC's 4-byte
+// labels (BOTH adjacency; tools/cc_ab.py): RMAT-24 14.3 / 14.9 / 16.2 ms at 4 / 5 / 6 bits, RMAT-26
+// 56.3 / 58.0 / 67.3 ms at 5 / 6 / 7, so 4 + (log2(entries) - 24) / 2.
+int auto_band_bits(int64_t vec_entries, int elem_bytes) {
+    const int l2 = (int)std::lround(std::log2((double)std::max<int64_t>(vec_entries, 1)));
+    const int b = elem_bytes >= 8 ? l2 - 19 : 4 + (l2 - 24) / 2;
+    return std::min(std::max(b, 4), 7);
+}
+
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
+                     int elem_bytes) {
     hipStream_t s = sh.stream;
     plan.lds_ok = col_space == csr.rows;  // one shard: the hot prefix of the gathered vector is [0, hot)
     plan.col_space = col_space;
@@ -654,7 +670,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         const int64_t end = std::min<int64_t>((int64_t)fb[kNumClasses + 1 + i], zero_begin);
         if (end <= row_at) continue;
         auto bd = std::make_unique<SliceBand>();
-        bd->bits = std::min(std::max(tune().band_bits[i], 3), 8);
+        bd->bits = std::min(std::max(tune().band_bits[i] > 0 ? tune().band_bits[i] : auto_band_bits(vec_entries, elem_bytes), 3), 8);
         bd->row_begin = row_at;
         bd->row_end = end;
         row_at = end;
@@ -785,16 +801,18 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         auto build_pull_csr = [&](int which, const int32_t* wt, Csr& csr, PullPlan& plan, Halo& halo) {
             a.which = which;
             a.cm = CompactMap{};
-            int64_t col_space = g.padded_len();
+            int64_t col_space = g.padded_len(), vec_entries = g.padded_len();
             if (P > 1 && tune().halo) {
                 build_halo(g, sh, e.src[li], e.dst[li], padded.get(), m, which, halo, s);
                 a.cm = halo.map(g.S, r);
                 col_space = halo.C;
+                vec_entries = sh.rows + halo.recv_off[P];
             }
             a.cbits = std::max(cbits, bits_for((uint64_t)(col_space - 1)));  // compact ids may exceed P*S
             a.sbits = tune().pull_split ? 8 : 0;
             build_csr(sh, a, wt, csr, s);
-            build_pull_plan(sh, csr, plan, col_space);
+            // the gathered vector of the split: PageRank's fp64 contributions (IN), CC's int32 labels (BOTH)
+            build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 0 ? 8 : 4);
             if (halo.on) {  // segmented compact vector: every segment's hot entries are its prefix
                 plan.lds_ok = true;
                 plan.seg_tbits = halo.tbits;

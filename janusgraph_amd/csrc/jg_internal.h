@@ -262,7 +262,11 @@ void build_graph_from_dense(Graph& g, DenseEdges& e);
 void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s);
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
                       int32_t* dsrc, int32_t* ddst, hipStream_t s);
-void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space);
+// col_space: length of the gathered vector; vec_entries: entries actually in it, elem_bytes: their
+// size (automatic band widths)
+void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
+                     int elem_bytes);
+int auto_band_bits(int64_t vec_entries, int elem_bytes);
 
 void rccl_check(ncclResult_t r, const char* what);
 
@@ -307,7 +311,7 @@ struct Tune {
     // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
     // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light
     int64_t band_deg[4] = {128, 8, 0, 0};
-    int band_bits[4] = {5, 3, 3, 3};
+    int band_bits[4] = {0, 3, 3, 3};  // 0: automatic (auto_band_bits of the gathered vector's size)
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
     int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)

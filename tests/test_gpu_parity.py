@@ -315,5 +315,5 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("pull_lds", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("slice_lds", 1)
-        for k, v in (("band0_deg", 128), ("band0_bit", 5), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0)):
+        for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0)):
             _lib.tune_set(k, v)
