@@ -231,6 +231,10 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().slice_lds = value != 0;
     } else if (k == "halo") {
         jg::tune().halo = value != 0;
+    } else if (k == "relabel_ties") {
+        jg::tune().relabel_ties = value != 0;
+    } else if (k == "merge_temporal") {
+        jg::tune().merge_temporal = value != 0;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }

@@ -149,6 +149,52 @@ __global__ void relabel_keys_kernel(const int32_t* __restrict__ indeg, const int
     }
 }
 
+// Tie-break of the degree relabel (tune relabel_ties): rank1[v] = position of v in the (degree, id)
+// order; nbr_min[v] = smallest rank1 over v's pull neighbours (IN: sources of its in-edges; BOTH:
+// both ends), so rows of equal degree that gather the same hot vertex become neighbours.
+__global__ void rank_scatter_kernel(const uint64_t* __restrict__ sorted_keys, int64_t n, uint64_t vmask,
+                                    int32_t* __restrict__ rank1) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        rank1[sorted_keys[k] & vmask] = (int32_t)k;
+}
+
+__global__ void nbr_min_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m, int mode,
+                               const int32_t* __restrict__ rank1, int32_t* __restrict__ nbr_min) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t a = src[e], b = dst[e];
+        if (a < 0 || b < 0) continue;
+        atomicMin(&nbr_min[b], rank1[a]);
+        if (mode == 1) atomicMin(&nbr_min[a], rank1[b]);
+    }
+}
+
+// pass 1 of the tie-break sort: key = nbr_min << vbits | v (vertices without neighbours last; nbr_min
+// starts at 0x7F7F7F7F, above any rank)
+__global__ void tie_keys_kernel(const int32_t* __restrict__ nbr_min, int64_t n, int vbits, uint64_t* __restrict__ keys) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = nbr_min[v] >= n ? n : nbr_min[v];
+        keys[v] = ((uint64_t)t << vbits) | (uint64_t)v;
+    }
+}
+
+// pass 2: key = (maxdeg - deg(v)) << 32 | position in pass 1 (stable: ties keep the pass-1 order)
+__global__ void tie_deg_keys_kernel(const uint64_t* __restrict__ keys1, int64_t n, uint64_t vmask,
+                                    const int32_t* __restrict__ indeg, const int32_t* __restrict__ outdeg, int mode,
+                                    int64_t maxdeg, uint64_t* __restrict__ keys2) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = (int64_t)(keys1[i] & vmask);
+        const int64_t d = mode == 0 ? indeg[v] : mode == 1 ? (int64_t)indeg[v] + outdeg[v] : outdeg[v];
+        keys2[i] = ((uint64_t)(maxdeg - d) << 32) | (uint64_t)i;
+    }
+}
+
+// back to (degree, v) keys in the final order, for padded_ids_kernel
+__global__ void tie_final_kernel(const uint64_t* __restrict__ keys1, const uint64_t* __restrict__ keys2, int64_t n,
+                                 uint64_t vmask, uint64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = keys1[keys2[k] & 0xFFFFFFFFull] & vmask;
+}
+
 __global__ void stats_kernel(const int32_t* __restrict__ indeg, const int32_t* __restrict__ outdeg, int64_t n,
                              unsigned long long* __restrict__ out /* max_in, max_out, truncated */) {
     unsigned long long mi = 0, mo = 0, tr = 0;
@@ -467,18 +513,25 @@ __global__ void nonempty_kernel(const int32_t* __restrict__ len, int64_t n, int3
         flag[i] = len[i] > 0;
 }
 
-// Number the non-empty sub-rows sub-slice-major: sub_index[h*NR + i] = k (or -1), cstart[k] = first entry.
+// Non-empty sub-rows are numbered sub-slice-major (num = exclusive scan of the flags): cstart[k] =
+// first entry of sub-row k.
 __global__ void sub_number_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t NR, int S,
-                                  const int64_t* __restrict__ sp, int32_t* __restrict__ sub_index,
-                                  int64_t* __restrict__ cstart) {
+                                  const int64_t* __restrict__ sp, int64_t* __restrict__ cstart) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < NR * S; x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t h = x / NR, i = x % NR;
-        if (len[x] > 0) {
-            sub_index[x] = (int32_t)num[x];
-            cstart[num[x]] = sp[h * (NR + 1) + i];
-        } else {
-            sub_index[x] = -1;
-        }
+        if (len[x] > 0) cstart[num[x]] = sp[h * (NR + 1) + i];
+    }
+}
+
+// sub_word[h][w] = (non-empty flags of band rows 32w .. 32w+31 in sub-slice h, number of the first of
+// them) (SliceBand)
+__global__ void sub_word_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t NR, int S,
+                                int64_t W, uint2* __restrict__ word) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < W * S; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t h = x / W, w = x % W, i0 = w * 32;
+        uint32_t b = 0;
+        for (int k = 0; k < 32 && i0 + k < NR; ++k) b |= (len[h * NR + i0 + k] > 0 ? 1u : 0u) << k;
+        word[x] = make_uint2(b, (uint32_t)num[h * NR + i0]);
     }
 }
 
@@ -572,10 +625,15 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd) {
     JG_LAUNCH_CHECK();
     copy_d2h(&bd.subrows, num.get() + NS, sizeof(int64_t), s);
     DevBuf<int64_t> cstart(std::max<int64_t>(bd.subrows, 1));
-    bd.sub_index.alloc(NS);
-    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), NR, S, sp.get(), bd.sub_index.get(),
-                                                      cstart.get());
+    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), NR, S, sp.get(), cstart.get());
     JG_LAUNCH_CHECK();
+    if (bd.subrows >= (int64_t)INT32_MAX) fail(JG_ERR_UNSUPPORTED, "too many sub-rows in a split band");
+    const int64_t W = (NR + 31) / 32;
+    bd.sub_word.alloc(std::max<int64_t>(W * S, 1));
+    if (W > 0) {
+        sub_word_kernel<<<grid_for(W * S), kBlock, 0, s>>>(len.get(), num.get(), NR, S, W, bd.sub_word.get());
+        JG_LAUNCH_CHECK();
+    }
     bd.meta.alloc(std::max<int64_t>(2 * bd.tasks, 1));
     bd.heads.alloc(std::max<int64_t>(kWave * bd.tasks, 1));
     if (bd.tasks > 0) {
@@ -635,6 +693,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         hptr.push_back((int64_t)crow.size());
     }
     plan.num_hub_rows = (int64_t)hubs.size();
+    plan.max_hub_row = hubs.empty() ? -1 : *std::max_element(hubs.begin(), hubs.end());
     plan.num_chunks = (int64_t)crow.size();
     auto upload = [&](DevBuf<int64_t>& d, const std::vector<int64_t>& h) {
         d.alloc(std::max<size_t>(h.size(), 1));
@@ -719,6 +778,12 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
                          64 >> (c - 1), (long long)b, (long long)e, (long long)(e - b), (long long)(rp[e] - rp[b]),
                          (long long)(plan.class_block_begin[c + 1] - plan.class_block_begin[c]));
         }
+        for (size_t i = 0; i < plan.bands.size(); ++i) {
+            const SliceBand& bd = *plan.bands[i];
+            std::fprintf(stderr, "[jg plan]   band %zu bits %d rows [%lld,%lld) nnz %lld sub-rows %lld tasks %lld\n", i,
+                         bd.bits, (long long)bd.row_begin, (long long)bd.row_end,
+                         (long long)(rp[bd.row_end] - rp[bd.row_begin]), (long long)bd.subrows, (long long)bd.tasks);
+        }
     }
 }
 
@@ -771,6 +836,27 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                rkeys.get());
             JG_LAUNCH_CHECK();
             prim::radix_sort(rkeys.get(), nullptr, n, vbits + bits_for((uint64_t)maxdeg), s);
+            if (tune().relabel_ties && mode != 2 && m > 0) {
+                // equal-degree vertices ordered by their hottest pull neighbour (then id)
+                const uint64_t vmask = (1ull << vbits) - 1ull;
+                DevBuf<int32_t> rank1(n), nbr_min(n);
+                rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, vmask, rank1.get());
+                JG_LAUNCH_CHECK();
+                JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
+                nbr_min_kernel<<<grid_for(m, kBlock, 256 * 16), kBlock, 0, s>>>(e.src[li], e.dst[li], m, mode,
+                                                                                 rank1.get(), nbr_min.get());
+                JG_LAUNCH_CHECK();
+                DevBuf<uint64_t> k1(n), k2(n);
+                tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, k1.get());
+                JG_LAUNCH_CHECK();
+                prim::radix_sort(k1.get(), nullptr, n, vbits + bits_for((uint64_t)n), s);
+                tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, indeg.get(), outdeg.get(), mode,
+                                                                   maxdeg, k2.get());
+                JG_LAUNCH_CHECK();
+                prim::radix_sort(k2.get(), nullptr, n, 32 + bits_for((uint64_t)maxdeg), s);
+                tie_final_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), k2.get(), n, vmask, rkeys.get());
+                JG_LAUNCH_CHECK();
+            }
             padded_ids_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, (1ull << vbits) - 1ull, P, g.S,
                                                              order.get(), padded.get());
             JG_LAUNCH_CHECK();

@@ -63,7 +63,9 @@ struct SliceBand {
     DevBuf<int64_t> sub_base;   // [S+1] first task of sub-slice h
     DevBuf<uint8_t> heads;      // [tasks][64]: byte l = row-start bits of lane l's entries
     DevBuf<int32_t> meta;       // [tasks][2]: sub-row number of the task's first entry; 1 if it is a carry
-    DevBuf<int32_t> sub_index;  // [S][rows of the band]: number of sub-row (h, r), -1 if empty
+    // non-empty sub-rows, numbered sub-slice-major: for w = sub_word[h][i>>5], bit i&31 of w.x says
+    // whether band row i has entries in sub-slice h; its number is w.y + the set bits of w.x below it
+    DevBuf<uint2> sub_word;     // [S][words], words = ceil(rows of the band / 32)
     int64_t rows() const { return row_end - row_begin; }
 };
 
@@ -72,6 +74,7 @@ struct PullPlan {
     int64_t class_row_end[kNumClasses];
     int64_t class_block_begin[kNumClasses + 1];  // hub: one block per chunk
     int64_t num_hub_rows = 0;
+    int64_t max_hub_row = -1;    // hub rows need not be a prefix (rows follow the relabel's degree)
     int64_t num_chunks = 0;
     DevBuf<int64_t> chunk_row;    // [num_chunks] local row of each hub chunk
     DevBuf<int64_t> chunk_begin;  // [num_chunks] first entry (CSR position)
@@ -317,6 +320,8 @@ struct Tune {
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
+    int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
+    int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality)
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

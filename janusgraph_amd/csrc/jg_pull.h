@@ -343,19 +343,28 @@ struct SliceLdsGather {
 
 template <class Op, bool LDS>
 __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
-                                                                   typename Op::T* __restrict__ carry, HotSegs hs) {
+                                                                   typename Op::T* __restrict__ carry, HotSegs hs,
+                                                                   int temporal) {
     using T = typename Op::T;
     extern __shared__ __align__(16) unsigned char merge_lds[];
     const int per = (1 << a.bits) >> 3;  // sub-slices per XCD
-    const int w = (int)(blockIdx.x >> 3);
-    const int h = (int)(blockIdx.x & (kXcds - 1)) | ((w % per) << 3);
-    const int64_t g = w / per, G = (gridDim.x >> 3) / per;  // this block's rank among h's blocks
+    const int w = (int)(blockIdx.x >> 3), W = (int)(gridDim.x >> 3);
+    const int xcd = (int)(blockIdx.x & (kXcds - 1));
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     lds_ptr<T> hotv = (lds_ptr<T>)merge_lds;
     const int gshift = 4 + a.bits;
     const int hg = hs.hs >> gshift;  // hot line groups per segment
     const int nl = hs.nseg * hg;     // LDS lines
+    // Static: block w of an XCD folds sub-slice (w mod per) with the XCD's other W / per blocks of it.
+    // Temporal: every block of an XCD sweeps the XCD's per sub-slices in the same order, all W blocks
+    // on one sub-slice at a time, so the XCD's L2 holds one sub-slice's part of the vector instead
+    // of all of them at once (one image restaged per round).
+    const int rounds = temporal ? per : 1;
+    for (int rd = 0; rd < rounds; ++rd) {
+    const int h = xcd | ((temporal ? rd : w % per) << 3);
+    const int64_t g = temporal ? w : w / per, G = temporal ? W : W / per;  // this block's rank among h's blocks
     if constexpr (LDS) {
+        if (rd > 0) __syncthreads();  // every wave is done with the previous round's image
         // LDS line i = the line of sub-slice h in hot line group i (a permutation of each aligned group)
         const T* src = op.vec();
         const uint32_t mask = (1u << a.bits) - 1;
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
     const int64_t step = G * kMergeWaves;
     int64_t k = g * kMergeWaves + wave;
-    if (k >= ntask) return;
+    if (k >= ntask) continue;
     // The next task's cols and metadata are loaded while this task's gathers are in flight.  The
     // loop carries the raw load registers (int4 col vectors, head byte, meta word) and unpacks them at
     // the top, so a prefetch writes straight into them and nothing waits on it until the next task.
@@ -501,6 +510,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         if (kn >= ntask) break;
         k = kn;
     }
+    }  // rounds
 }
 
 // Sub-rows that span tasks: the sub-row's first task wrote partial[j]; every later task it covers left
@@ -535,9 +545,11 @@ __global__ void pull_merge_fixup_kernel(FixupBands fb, Op op, typename Op::T* __
     }
 }
 
-// Row r of the split: fold its non-empty sub-slices in h order.
+// Row r of the split: fold its non-empty sub-slices in h order.  One lane per row, so a wave reads
+// sub-slice h's partials of 64 consecutive rows (consecutive numbers: coalesced); several lanes per
+// row were measured slower (their partials of different sub-slices sit far apart).
 struct FinalizeBands {
-    const int32_t* sub_index[kMaxBands];
+    const uint2* sub_word[kMaxBands];
     int64_t row_begin[kMaxBands];
     int64_t row_end[kMaxBands];
     int64_t part_off[kMaxBands];
@@ -551,18 +563,24 @@ __global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb
         int b = 0;
         while (b < fb.n - 1 && r >= fb.row_end[b]) ++b;
         const int64_t NR = fb.row_end[b] - fb.row_begin[b], i = r - fb.row_begin[b];
+        const int64_t W = (NR + 31) / 32, wi = i >> 5;
+        const uint32_t below = (1u << (i & 31)) - 1u, me = 1u << (i & 31);
         const int S = 1 << fb.bits[b];
-        const int32_t* __restrict__ si = fb.sub_index[b];
+        const uint2* __restrict__ sw = fb.sub_word[b];
         const T* __restrict__ part = partial + fb.part_off[b];
         T acc = op.identity();
         bool first = true;
         // batches of 8 sub-slices (S >= 8): all index loads, then all partial loads, then the fold in
-        // h order, so a hub row's 32 sub-slices cost 4 round trips instead of 32 dependent pairs
+        // h order, so a hub row's 32 sub-slices cost 4 round trips instead of 32 dependent pairs.  The
+        // index words are shared by 32 rows (1/16 of the bytes of an int32 index per sub-row).
         for (int h0 = 0; h0 < S; h0 += 8) {
             int32_t j[8];
             T v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) j[u] = si[(int64_t)(h0 + u) * NR + i];
+            for (int u = 0; u < 8; ++u) {
+                const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
+                j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
 #pragma unroll
@@ -626,11 +644,12 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             hs.nseg = plan.nseg;
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
+            const int temporal = tune().merge_temporal;
             if (hs.hs > 0)
                 pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), s>>>(
-                    ma, op, part, carry, hs);
+                    ma, op, part, carry, hs, temporal);
             else
-                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, hs);
+                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, hs, temporal);
             JG_LAUNCH_CHECK();
         }
         FixupBands fx{};
@@ -682,8 +701,8 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     } else if (blocks > 0) {
         launch((unsigned)blocks);
     }
-    // hub rows are the first rows (degree order); with the split they are all its rows already
-    if (plan.num_hub_rows > 0 && !(split && plan.num_hub_rows <= plan.split_rows)) {
+    // with the split, hub rows inside it are finalised by it (skip the launch when that is all of them)
+    if (plan.num_hub_rows > 0 && !(split && plan.max_hub_row < plan.split_rows)) {
         pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, ls>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }
@@ -691,7 +710,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         FinalizeBands fb{};
         for (const auto& bp : plan.bands) {
             if (fb.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
-            fb.sub_index[fb.n] = bp->sub_index.get();
+            fb.sub_word[fb.n] = bp->sub_word.get();
             fb.row_begin[fb.n] = bp->row_begin;
             fb.row_end[fb.n] = bp->row_end;
             fb.part_off[fb.n] = bp->part_off;
