@@ -234,7 +234,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
     } else if (k == "merge_temporal") {
-        jg::tune().merge_temporal = value != 0;
+        JG_ARG(value >= 0 && value <= 2, "merge_temporal must be 0, 1 (automatic) or 2");
+        jg::tune().merge_temporal = (int)value;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }

@@ -661,8 +661,14 @@ int auto_band_bits(int64_t vec_entries, int elem_bytes) {
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
                      int elem_bytes) {
     hipStream_t s = sh.stream;
+    // a segmented (sharded) vector splits every LDS image over its segments: one more sub-slice bit
+    // (tools/shard_sim.py, RMAT-24 at P = 8: 0.163 vs 0.169 ms per shard superstep at 5 vs 4 bits)
+    const bool sharded_vec = col_space != vec_entries && col_space != csr.rows;
     plan.lds_ok = col_space == csr.rows;  // one shard: the hot prefix of the gathered vector is [0, hot)
     plan.col_space = col_space;
+    // temporal merge schedule only pays when an XCD's eighth of the vector overflows its 4 MB L2 well
+    // (tools/shard_sim.py, RMAT-24 at P = 8, 41 MB vector: 0.173 vs 0.168 ms per shard superstep)
+    plan.temporal = vec_entries * elem_bytes > (int64_t)64 << 20;
     const int64_t rows = csr.rows;
     // hub rows (any position) -> chunk table
     std::vector<int64_t> hubs, bounds;
@@ -729,7 +735,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         const int64_t end = std::min<int64_t>((int64_t)fb[kNumClasses + 1 + i], zero_begin);
         if (end <= row_at) continue;
         auto bd = std::make_unique<SliceBand>();
-        bd->bits = std::min(std::max(tune().band_bits[i] > 0 ? tune().band_bits[i] : auto_band_bits(vec_entries, elem_bytes), 3), 8);
+        bd->bits = std::min(std::max(tune().band_bits[i] > 0 ? tune().band_bits[i] : auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
         bd->row_begin = row_at;
         bd->row_end = end;
         row_at = end;

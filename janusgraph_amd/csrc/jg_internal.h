@@ -98,6 +98,7 @@ struct PullPlan {
         return std::max<int64_t>(n, 1);
     }
     bool lds_ok = false;  // the gathered vector's hot entries are segment prefixes (see seg_tbits)
+    bool temporal = false;  // the vector is large enough for the temporal merge schedule (tune merge_temporal = 1)
     int seg_tbits = 31;   // segmented compact vector (sharded, halo): nseg segments of stride 2^seg_tbits
     int nseg = 1;         // one segment: the hot prefix is [0, hot)
 };
@@ -321,7 +322,8 @@ struct Tune {
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
-    int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality)
+    int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
+                                      // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

@@ -644,7 +644,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             hs.nseg = plan.nseg;
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
-            const int temporal = tune().merge_temporal;
+            const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
             if (hs.hs > 0)
                 pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), s>>>(
                     ma, op, part, carry, hs, temporal);

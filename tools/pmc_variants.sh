@@ -2,6 +2,7 @@
 # PMC passes (one rocprofv3 run per pass, MI355X_MICROARCH.md §rocprofv3 slot limits) over PageRank
 # supersteps of bench.py for several pull-engine variants (JG_TUNE).  Usage on the GPU box:
 #   bash tools/pmc_variants.sh <outdir> "<name>:<JG_TUNE>" ...
+# BENCH_ARGS (env) adds bench.py arguments, e.g. BENCH_ARGS="--scale 26".
 set -o pipefail
 OUT=$1; shift
 mkdir -p $OUT
@@ -18,7 +19,7 @@ for v in "$@"; do
   name=${v%%:*}; tune=${v#*:}
   i=0; mkdir -p $OUT/$name
   for p in "${PASSES[@]}"; do
-    JG_TUNE="$tune" timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d $OUT/$name/p$i -o p -- python3 bench.py --no-cpu --no-bfs --steps 5 --warmup 1 > $OUT/$name/p$i.log 2>&1 || { echo "pass $i of $name failed"; exit 3; }
+    JG_TUNE="$tune" timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d $OUT/$name/p$i -o p -- python3 bench.py --no-cpu --no-bfs --steps 5 --warmup 1 $BENCH_ARGS > $OUT/$name/p$i.log 2>&1 || { echo "pass $i of $name failed"; exit 3; }
     i=$((i+1))
   done
 done
