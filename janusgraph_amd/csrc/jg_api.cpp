@@ -93,6 +93,10 @@ bool pull_split_launches() {
     static const bool v = env_flag("JG_PULL_SPLIT");
     return v;
 }
+bool debug_bfs() {
+    static const bool v = env_flag("JG_DEBUG_BFS");
+    return v;
+}
 bool debug_plan() {
     static const bool v = env_flag("JG_DEBUG_PLAN");
     return v;

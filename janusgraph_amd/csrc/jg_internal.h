@@ -304,6 +304,7 @@ int allreduce_or(Graph& g, int flag);
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
 bool pull_split_launches();
 bool debug_plan();
+bool debug_bfs();  // JG_DEBUG_BFS=1: synchronise and print every DO-BFS level's decision
 
 // Performance knobs (jg_tune_set): variants of the pull kernel selectable at run time so that they
 // can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).

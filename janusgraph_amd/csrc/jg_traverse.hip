@@ -21,6 +21,8 @@
 //     only): push over the in-CSR with 64-bit atomicMin into a scratch array, then apply.
 #include <climits>
 
+#include <cstdio>
+
 #include "jg_pull.h"
 
 namespace jg {
@@ -31,6 +33,7 @@ constexpr int kTdLanes = 16;         // lanes per frontier vertex in the weighte
 constexpr int kPackShift = 37;       // packed frontier counter: (vertices << 37) | push edges
 constexpr unsigned long long kEdgeMask = (1ull << kPackShift) - 1ull;
 constexpr int kTdEdgesPerThread = 4;
+constexpr int kBuBatch = 4;             // bottom-up: neighbours probed per step
 constexpr int kBfsRing = 4;            // level-state ring: a level touches slots L-1, L, L+1
 
 __device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t* __restrict__ queue,
@@ -129,10 +132,52 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
     return c;
 }
 
+// Block-aggregated form of wave_append_frontier: the block's waves combine their counts in LDS and
+// one thread reserves the block's range with a single atomic (a level that finds most of the graph
+// would otherwise put one atomic per wave on one address).  Must be reached by every thread of the
+// block (block-uniform call sites); queue positions and edge offsets stay monotone.
+struct AppendScratch {
+    unsigned long long cnt[kBlock / kWave], deg[kBlock / kWave];
+    unsigned long long base;
+};
+__device__ __forceinline__ void block_append_frontier(bool take, int32_t v, int64_t deg, int32_t* __restrict__ queue,
+                                                      int64_t* __restrict__ qoff, unsigned long long* __restrict__ packed,
+                                                      AppendScratch& sc) {
+    const uint64_t mask = __ballot(take);
+    const int64_t d = take ? deg : 0;
+    const int64_t dinc = wave_inclusive_scan_add(d);
+    const int wv = wave_id();
+    if (lane_id() == kWave - 1) {
+        sc.cnt[wv] = (unsigned long long)__popcll(mask);
+        sc.deg[wv] = (unsigned long long)dinc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = 0, e = 0;
+        for (int k = 0; k < kBlock / kWave; ++k) {
+            const unsigned long long ck = sc.cnt[k], ek = sc.deg[k];
+            sc.cnt[k] = c;  // exclusive prefixes
+            sc.deg[k] = e;
+            c += ck;
+            e += ek;
+        }
+        sc.base = c ? atomicAdd(packed, (c << kPackShift) | e) : 0ull;
+    }
+    __syncthreads();
+    if (take) {
+        const unsigned long long base = sc.base;
+        const uint64_t pos = (base >> kPackShift) + sc.cnt[wv] + (uint64_t)__popcll(mask & lanemask_lt());
+        queue[pos] = v;
+        qoff[pos] = (int64_t)(base & kEdgeMask) + (int64_t)sc.deg[wv] + dinc - d;
+    }
+    __syncthreads();  // the scratch is reused by the next call
+}
+
 // Edge-parallel top-down: frontier edge e in [0, mf) belongs to the queue entry i with
 // qoff[i] <= e < qoff[i+1]; each thread walks kTdEdgesPerThread consecutive edges after one binary
 // search, so a hub in the frontier is spread over the whole grid.
-__device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed) {
+__device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed,
+                                             AppendScratch& sc) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -168,7 +213,7 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
                     vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
                 }
             }
-            wave_append_frontier(won, v, vdeg, a.queue_out, a.qoff_out, packed);
+            block_append_frontier(won, v, vdeg, a.queue_out, a.qoff_out, packed, sc);
         }
     }
 }
@@ -176,20 +221,32 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
 // Bottom-up: one lane per unvisited vertex scans its pull row against the frontier and stops at the
 // first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
 template <bool kFromDepth>
-__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed) {
+__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, AppendScratch& sc) {
     const int64_t words = (a.rows + 63) / 64;
-    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) / kWave;
+    constexpr int kWpb = kBlock / kWave;
+    const int64_t wstride = (int64_t)gridDim.x * kWpb;
     const int32_t next_depth = a.level + 1;
-    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words; w += wstride) {
+    // block-uniform trip count (the append is block-wide); words past the end take nothing
+    for (int64_t w0 = (int64_t)blockIdx.x * kWpb; w0 < words; w0 += wstride) {
+        const int64_t w = w0 + wave_id();
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t vdeg = 0;
         if (v < a.rows && a.depth[v] < 0) {
+            // kBuBatch neighbours per step: all column loads, then all frontier probes, then the test,
+            // so a row scanned to its end pays two round trips per batch instead of per neighbour
+            // (which neighbour hits does not matter: the depth is level + 1 either way)
             const int64_t j1 = a.pull_rp[v + 1];
-            for (int64_t j = a.pull_rp[v]; j < j1; ++j) {
-                const int32_t u = a.pull_col[j];
-                const bool in_frontier = kFromDepth ? a.depth[u] == a.level : ((a.bm_in[u >> 6] >> (u & 63)) & 1ull);
-                if (in_frontier) { found = true; break; }
+            for (int64_t j = a.pull_rp[v]; j < j1 && !found; j += kBuBatch) {
+                int32_t u[kBuBatch];
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k) u[k] = a.pull_col[j + k < j1 ? j + k : j1 - 1];
+                bool hit[kBuBatch];
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k)
+                    hit[k] = kFromDepth ? a.depth[u[k]] == a.level : ((a.bm_in[u[k] >> 6] >> (u[k] & 63)) & 1ull);
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k) found |= hit[k];
             }
             if (found) {
                 a.depth[v] = next_depth;
@@ -197,8 +254,8 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
             }
         }
         const uint64_t word = __ballot(found);
-        if (lane_id() == 0) a.bm_out[w] = word;
-        wave_append_frontier(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed);
+        if (lane_id() == 0 && w < words) a.bm_out[w] = word;
+        block_append_frontier(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed, sc);
     }
 }
 
@@ -206,6 +263,7 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
     __shared__ long long s_nf, s_mf;
     __shared__ int s_switch;
+    __shared__ AppendScratch s_app;
     if (threadIdx.x == 0) {
         int64_t nf, mf;
         bool sw;
@@ -222,9 +280,9 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __syncthreads();
     if (s_st.done) return;
     unsigned long long* packed = a.ctr + a.level % kBfsRing;
-    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed);
-    else if (s_switch) bfs_bottom_up<true>(a, packed);
-    else bfs_bottom_up<false>(a, packed);
+    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed, s_app);
+    else if (s_switch) bfs_bottom_up<true>(a, packed, s_app);
+    else bfs_bottom_up<false>(a, packed, s_app);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -439,6 +497,14 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             bfs_level_kernel<<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
+            if (debug_bfs()) {
+                BfsState ds{};
+                unsigned long long dc = 0;
+                copy_d2h(&ds, st + level % kBfsRing, sizeof ds, s);
+                copy_d2h(&dc, sh.bfs_ctr.get() + level % kBfsRing, sizeof dc, s);
+                std::fprintf(stderr, "[jg bfs] level %d %s done %d next frontier %llu vertices %llu edges\n", level,
+                             ds.bottom_up ? "bottom-up" : "top-down", ds.done, dc >> kPackShift, dc & kEdgeMask);
+            }
         }
         copy_d2h(&hs, st + (level - 1) % kBfsRing, sizeof hs, s);
         if (hs.done) break;
