@@ -323,6 +323,8 @@ struct Tune {
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
+    int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
+    int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
 };

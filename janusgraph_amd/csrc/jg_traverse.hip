@@ -474,8 +474,8 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.ctr = sh.bfs_ctr.get();
     a.st = st;
     a.max_depth = max_depth;
-    a.alpha = 14.0;
-    a.beta = 24.0;
+    a.alpha = (double)tune().bfs_alpha;
+    a.beta = (double)tune().bfs_beta;
     // a fixed grid: bottom-up covers every word, top-down strides over the frontier's edges
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((words * kWave + kBlock - 1) / kBlock, 64),
                                                       256 * 8);
