@@ -238,6 +238,9 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "bfs_alpha" || k == "bfs_beta") {
         JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta must be in [1, 1e6]");
         (k == "bfs_alpha" ? jg::tune().bfs_alpha : jg::tune().bfs_beta) = (int)value;
+    } else if (k == "bfs_grid") {
+        JG_ARG(value >= 64 && value <= 65536, "bfs_grid must be in [64, 65536]");
+        jg::tune().bfs_grid = (int)value;
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
     } else if (k == "merge_temporal") {

@@ -325,6 +325,7 @@ struct Tune {
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
+    int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
 };

@@ -184,6 +184,9 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
     const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
     const int32_t next_depth = a.level + 1;
     for (int64_t t = 0; t < tiles; ++t) {
+        // block-uniform: a block whose slice of this tile is past the frontier's edges has nothing to
+        // claim or append (small frontiers leave most of the grid idle)
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= mf) break;
         const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
         int64_t i = 0, next_bound = 0;
         if (e0 < mf) {
@@ -478,7 +481,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.beta = (double)tune().bfs_beta;
     // a fixed grid: bottom-up covers every word, top-down strides over the frontier's edges
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((words * kWave + kBlock - 1) / kBlock, 64),
-                                                      256 * 8);
+                                                      tune().bfs_grid);
     BfsState hs{};
     int level = 0;
     for (int batch = 8;; batch = 16) {
