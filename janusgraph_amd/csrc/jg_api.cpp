@@ -241,6 +241,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "bfs_grid") {
         JG_ARG(value >= 64 && value <= 65536, "bfs_grid must be in [64, 65536]");
         jg::tune().bfs_grid = (int)value;
+    } else if (k == "fuse_finalize") {
+        jg::tune().fuse_finalize = value != 0;
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
     } else if (k == "merge_temporal") {

@@ -319,6 +319,7 @@ struct Tune {
     int band_bits[4] = {0, 3, 3, 3};  // 0: automatic (auto_band_bits of the gathered vector's size)
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
     int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
+    int fuse_finalize = 1;            // light rows and the split's finalize in one launch
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)

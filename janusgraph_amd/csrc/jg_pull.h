@@ -210,9 +210,9 @@ __device__ __forceinline__ void pull_block_rows(const PullArgs& a, const Op& op,
 }
 
 template <class Op, int U, bool NT>
-__global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
+__device__ __forceinline__ void pull_block(const PullArgs& a, const Op& op, typename Op::T* __restrict__ hub_partial,
+                                           int64_t b) {
     using T = typename Op::T;
-    const int64_t b = (int64_t)blockIdx.x + a.block_offset;
     if (b < a.num_chunks) {
         __shared__ T red[kBlock / kWave];
         const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
@@ -232,6 +232,11 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typenam
         return;
     }
     pull_block_rows<Op, U, NT>(a, op, GlobalGather<Op>{op}, b, (int)threadIdx.x);
+}
+
+template <class Op, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
+    pull_block<Op, U, NT>(a, op, hub_partial, (int64_t)blockIdx.x + a.block_offset);
 }
 
 // LDS-cached variant (persistent, 1024 threads = 4 virtual 256-thread blocks, one workgroup per
@@ -557,9 +562,10 @@ struct FinalizeBands {
     int n;
 };
 template <class Op>
-__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb, const typename Op::T* __restrict__ partial) {
+__device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, const FinalizeBands& fb,
+                                                   const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    {
         int b = 0;
         while (b < fb.n - 1 && r >= fb.row_end[b]) ++b;
         const int64_t NR = fb.row_end[b] - fb.row_begin[b], i = r - fb.row_begin[b];
@@ -592,6 +598,29 @@ __global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb
         }
         op.finalize(r, acc);
     }
+}
+
+template <class Op>
+__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb, const typename Op::T* __restrict__ partial) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
+        slice_finalize_row(r, op, fb, partial);
+}
+
+// The light rows and the split's finalize in one launch (tune fuse_finalize): blocks [0, fin_blocks)
+// finalise split rows (one per thread), the rest run light-row blocks.  Both are latency-bound and
+// independent, so interleaving their blocks hides one's stalls behind the other's.
+template <class Op, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a, Op op,
+                                                                     typename Op::T* __restrict__ hub_partial,
+                                                                     FinalizeBands fb,
+                                                                     const typename Op::T* __restrict__ partial,
+                                                                     int64_t split_rows, int64_t fin_blocks) {
+    if ((int64_t)blockIdx.x < fin_blocks) {
+        const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (r < split_rows) slice_finalize_row(r, op, fb, partial);
+        return;
+    }
+    pull_block<Op, U, NT>(a, op, hub_partial, (int64_t)blockIdx.x - fin_blocks + a.block_offset);
 }
 
 // Enqueue one pull superstep on `s`.
@@ -678,7 +707,30 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         }
         JG_LAUNCH_CHECK();
     };
-    if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
+    FinalizeBands fb{};
+    if (split) {
+        for (const auto& bp : plan.bands) {
+            if (fb.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
+            fb.sub_word[fb.n] = bp->sub_word.get();
+            fb.row_begin[fb.n] = bp->row_begin;
+            fb.row_end[fb.n] = bp->row_end;
+            fb.part_off[fb.n] = bp->part_off;
+            fb.bits[fb.n] = bp->bits;
+            ++fb.n;
+        }
+    }
+    const bool fuse = split && tune().fuse_finalize && !pull_split_launches() && side == nullptr;
+    if (fuse) {
+        const int64_t fin_blocks = (plan.split_rows + kBlock - 1) / kBlock;
+        const unsigned grid = (unsigned)(fin_blocks + blocks);
+        if (tune().pull_unroll >= 8)
+            pull_light_finalize_kernel<Op, 8, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
+                                                                            plan.split_rows, fin_blocks);
+        else
+            pull_light_finalize_kernel<Op, 4, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
+                                                                            plan.split_rows, fin_blocks);
+        JG_LAUNCH_CHECK();
+    } else if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
         const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
         if (plan.num_chunks > 0) launch((unsigned)plan.num_chunks);  // hub chunks: blocks [0, num_chunks)
         const size_t bytes = (size_t)hot * sizeof(T);
@@ -706,17 +758,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, ls>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }
-    if (split) {
-        FinalizeBands fb{};
-        for (const auto& bp : plan.bands) {
-            if (fb.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
-            fb.sub_word[fb.n] = bp->sub_word.get();
-            fb.row_begin[fb.n] = bp->row_begin;
-            fb.row_end[fb.n] = bp->row_end;
-            fb.part_off[fb.n] = bp->part_off;
-            fb.bits[fb.n] = bp->bits;
-            ++fb.n;
-        }
+    if (split && !fuse) {
         pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, fb, split_partial);
         JG_LAUNCH_CHECK();
     }
