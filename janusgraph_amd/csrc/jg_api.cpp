@@ -83,6 +83,18 @@ int allreduce_or(Graph& g, int flag) {
     return v;
 }
 
+void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
+    Ctx& c = *g.ctx;
+    if (c.nranks == 1) return;  // in-process shards already summed by the caller
+    Shard& sh = *g.shards[0];
+    DeviceGuard dg(sh.device);
+    DevBuf<int64_t> d(n);
+    JG_HIP(hipMemcpyAsync(d.get(), vals, n * sizeof(int64_t), hipMemcpyHostToDevice, sh.stream));
+    rccl_check(ncclAllReduce(d.get(), d.get(), (size_t)n, ncclInt64, ncclSum, sh.comm, sh.stream), "ncclAllReduce");
+    JG_HIP(hipMemcpyAsync(vals, d.get(), n * sizeof(int64_t), hipMemcpyDeviceToHost, sh.stream));
+    JG_HIP(hipStreamSynchronize(sh.stream));
+}
+
 bool prof_enabled(const Ctx& c) { return c.profiling; }
 
 static bool env_flag(const char* name) {
@@ -238,6 +250,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "bfs_alpha" || k == "bfs_beta") {
         JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta must be in [1, 1e6]");
         (k == "bfs_alpha" ? jg::tune().bfs_alpha : jg::tune().bfs_beta) = (int)value;
+    } else if (k == "sharded_bfs") {
+        jg::tune().sharded_bfs = value != 0;
     } else if (k == "bfs_grid") {
         JG_ARG(value >= 64 && value <= 65536, "bfs_grid must be in [64, 65536]");
         jg::tune().bfs_grid = (int)value;

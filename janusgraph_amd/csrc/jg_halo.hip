@@ -264,6 +264,53 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
+void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std::vector<void*>& rbufs,
+                           size_t elem_bytes, ncclDataType_t type) {
+    if (g.P == 1) return;
+    Ctx& c = *g.ctx;
+    // shard r's segment for peer q (the run q sent it) goes back to q, landing at q's send-list
+    // position for r
+    auto seg_ptr = [&](size_t i, int q) {
+        const Shard& sh = *g.shards[i];
+        const Halo& h = g.halo(sh, adj);
+        return static_cast<char*>(vecs[i]) + ((size_t)h.seg_of(q, sh.index) << h.tbits) * elem_bytes;
+    };
+    if (c.logical) {
+        Shard& s0 = *g.shards[0];
+        DeviceGuard dg(s0.device);
+        for (size_t di = 0; di < g.shards.size(); ++di) {  // receiver: the owner
+            const Halo& hd = g.halo(*g.shards[di], adj);
+            for (size_t si = 0; si < g.shards.size(); ++si) {
+                if (si == di) continue;
+                const Halo& hs = g.halo(*g.shards[si], adj);
+                const int q = g.shards[si]->index, r = g.shards[di]->index;
+                const int64_t n = hs.recv_off[r + 1] - hs.recv_off[r];
+                if (n == 0) continue;
+                JG_HIP(hipMemcpyAsync(static_cast<char*>(rbufs[di]) + hd.send_off[q] * elem_bytes, seg_ptr(si, r),
+                                      n * elem_bytes, hipMemcpyDeviceToDevice, s0.stream));
+            }
+        }
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh.device);
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t ns = h.recv_off[q + 1] - h.recv_off[q];  // my segment for q goes back to q
+            const int64_t nr = h.send_off[q + 1] - h.send_off[q];  // q's segment for me comes back
+            if (ns > 0) rccl_check(ncclSend(seg_ptr(i, q), (size_t)ns, type, q, sh.comm, sh.stream), "ncclSend");
+            if (nr > 0)
+                rccl_check(ncclRecv(static_cast<char*>(rbufs[i]) + h.send_off[q] * elem_bytes, (size_t)nr, type, q,
+                                    sh.comm, sh.stream),
+                           "ncclRecv");
+        }
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void exchange_vec(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
     if (g.P == 1) return;
     if (g.halo(*g.shards[0], adj).on)

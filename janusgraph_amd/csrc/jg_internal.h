@@ -281,6 +281,11 @@ void rccl_check(ncclResult_t r, const char* what);
 void exchange_vec(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
 void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
 void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type);
+// The transpose of the halo exchange: every shard's segment for peer q (values about q's vertices)
+// goes back to q, landing in rbufs[q] at q's send-list position for the sender (element j of a
+// shard's rbuf is about its own row send_src[j]).
+void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std::vector<void*>& rbufs,
+                           size_t elem_bytes, ncclDataType_t type);
 // Builds shard sh's halo plan for adjacency `which` (0 IN, 2 BOTH) from the full edge list.
 void build_halo(Graph& g, Shard& sh, const int32_t* src, const int32_t* dst, const int32_t* padded, int64_t m,
                 int which, Halo& h, hipStream_t s);
@@ -299,6 +304,8 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
 
 // Logical OR of a flag over all ranks (identity in single-process contexts).
 int allreduce_or(Graph& g, int flag);
+// Element-wise sum of vals[0..n) over all ranks, in place (identity in single-process contexts).
+void allreduce_sum_i64(Graph& g, int64_t* vals, int n);
 
 // Diagnostics from the environment: JG_PULL_SPLIT=1 launches each degree class separately,
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
@@ -326,6 +333,7 @@ struct Tune {
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
+    int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always

@@ -524,6 +524,308 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
     return pg % g.S;
 }
 
+// ---------------- sharded direction-optimising BFS (BOTH adjacency, halo plan) ----------------
+// Each shard owns its rows; dvec is its segmented compact vector of depths (own rows [0, rows), then
+// the peers' vertices its rows touch).  Bottom-up: a forward halo exchange refreshes the peers'
+// depths, then own unvisited rows probe their neighbours for depth == level.  Top-down: own frontier
+// rows claim own neighbours by CAS and stamp remote ones (stamp = level + 1) in their halo segments;
+// the reverse exchange hands the stamps to the owners, which claim them.  One packed counter per
+// shard and level ((vertices << 37) | degree sum), summed over shards and ranks, drives Beamer's
+// direction rule on the host.
+struct SBfsLevel {
+    const int64_t* rp;
+    const int32_t* col;
+    int64_t rows;
+    int32_t* dvec;
+    int32_t* stamp;
+    const int32_t* queue_in;
+    const int64_t* qoff_in;   // first frontier edge of each queue entry (edge-parallel top-down)
+    int64_t nq, mf;           // local frontier: vertices, entries
+    int32_t* queue_out;
+    int64_t* qoff_out;
+    const int32_t* rbuf;      // reverse-exchanged stamps, by send-list position
+    const int32_t* send_src;  // own row of each send-list position
+    int64_t nrecv;
+    unsigned long long* packed;
+    int32_t level;
+};
+
+// top-down, edge-parallel over the local frontier's entries (as bfs_top_down): own neighbours are
+// claimed by CAS, remote ones stamped in their halo segment
+__global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
+    __shared__ AppendScratch sc;
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    const int32_t nd = a.level + 1;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff_in[i + 1] : a.mf;
+        }
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
+            bool take = false;
+            int32_t u = 0;
+            int64_t deg = 0;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff_in[i + 1] : a.mf;
+                }
+                const int32_t v = a.queue_in[i];
+                u = a.col[a.rp[v] + (e - a.qoff_in[i])];
+                if (u < a.rows) {
+                    if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                        take = true;
+                        deg = a.rp[u + 1] - a.rp[u];
+                    }
+                } else if (a.dvec[u] < 0) {  // halo copy: visited stays visited, so skip those
+                    a.stamp[u] = nd;
+                }
+            }
+            block_append_frontier(take, u, deg, a.queue_out, a.qoff_out, a.packed, sc);
+        }
+    }
+}
+
+// top-down, owner side: claim the own rows the peers stamped this level
+__global__ __launch_bounds__(kBlock) void sbfs_td_apply_kernel(SBfsLevel a) {
+    __shared__ AppendScratch sc;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int32_t nd = a.level + 1;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < a.nrecv; x0 += stride) {  // block-uniform trips
+        const int64_t x = x0 + threadIdx.x;
+        bool take = false;
+        int32_t u = 0;
+        int64_t deg = 0;
+        if (x < a.nrecv && a.rbuf[x] == nd) {
+            u = a.send_src[x];
+            if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                take = true;
+                deg = a.rp[u + 1] - a.rp[u];
+            }
+        }
+        block_append_frontier(take, u, deg, a.queue_out, a.qoff_out, a.packed, sc);
+    }
+}
+
+// bottom-up over own rows (the halo segments hold the peers' depths of the previous level)
+__global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
+    __shared__ AppendScratch sc;
+    const int64_t words = (a.rows + 63) / 64;
+    constexpr int kWpb = kBlock / kWave;
+    const int64_t wstride = (int64_t)gridDim.x * kWpb;
+    const int32_t nd = a.level + 1;
+    for (int64_t w0 = (int64_t)blockIdx.x * kWpb; w0 < words; w0 += wstride) {
+        const int64_t v = (w0 + wave_id()) * 64 + lane_id();
+        bool found = false;
+        int64_t deg = 0;
+        if (v < a.rows && a.dvec[v] < 0) {
+            const int64_t j1 = a.rp[v + 1];
+            for (int64_t j = a.rp[v]; j < j1 && !found; j += kBuBatch) {
+                int32_t u[kBuBatch];
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k) u[k] = a.col[j + k < j1 ? j + k : j1 - 1];
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k) found |= a.dvec[u[k]] == a.level;
+            }
+            if (found) {
+                a.dvec[v] = nd;
+                deg = j1 - a.rp[v];
+            }
+        }
+        block_append_frontier(found, (int32_t)v, deg, a.queue_out, a.qoff_out, a.packed, sc);
+    }
+}
+
+__global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t C, int32_t* __restrict__ stamp, int64_t src,
+                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (int64_t)gridDim.x * blockDim.x) {
+        dvec[i] = i == src ? 0 : -1;
+        stamp[i] = 0;
+    }
+    if (src >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        queue[0] = (int32_t)src;
+        qoff[0] = 0;
+    }
+}
+
+// Sharded single-source DO-BFS over BOTH; returns levels run, *edges_out = entries of reached rows.
+int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth, double* edges_out, float* ms_out) {
+    const size_t ns = g.shards.size();
+    struct St {
+        DevBuf<int32_t> dvec, stamp, rbuf, queue[2];
+        DevBuf<int64_t> qoff[2];
+        DevBuf<unsigned long long> ctr;
+        int64_t nq = 0, mf = 0;
+    };
+    std::vector<St> st(ns);
+    int64_t tot[2] = {0, 0};  // entries of all shards, rows of all shards
+    int64_t src_deg = 0;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        const Halo& h = sh.halo_both;
+        St& t = st[i];
+        t.dvec.alloc(h.C);
+        t.stamp.alloc(h.C);
+        t.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
+        t.queue[0].alloc(std::max<int64_t>(sh.rows, 1));
+        t.queue[1].alloc(std::max<int64_t>(sh.rows, 1));
+        t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
+        t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
+        t.ctr.alloc(1);
+        const int64_t src = sh.index == src_shard ? src_local : -1;
+        sbfs_init_kernel<<<grid_for(h.C), kBlock, 0, sh.stream>>>(t.dvec.get(), h.C, t.stamp.get(), src,
+                                                                  t.queue[0].get(), t.qoff[0].get());
+        JG_LAUNCH_CHECK();
+        t.nq = src >= 0 ? 1 : 0;
+        if (src >= 0) {
+            int64_t b[2];
+            copy_d2h(b, sh.both.row_ptr.get() + src, 2 * sizeof(int64_t), sh.stream);
+            src_deg = b[1] - b[0];
+            t.mf = src_deg;
+        }
+        tot[0] += sh.both.nnz;
+        tot[1] += sh.rows;
+    }
+    int64_t init[3] = {tot[0], tot[1], src_deg};
+    allreduce_sum_i64(g, init, 3);
+    int64_t mu = init[0] - init[2], nf = 1, mf = init[2], edges = init[2];
+    const int64_t nrows = init[1];
+    const double alpha = (double)tune().bfs_alpha, beta = (double)tune().bfs_beta;
+    bool bu = false;
+    int level = 0, cur = 0;
+    Shard& sh0 = *g.shards[0];
+    hipEvent_t t0, t1;
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, sh0.stream));
+    }
+    std::vector<void*> dv, sv, rv;
+    for (auto& t : st) {
+        dv.push_back(t.dvec.get());
+        sv.push_back(t.stamp.get());
+        rv.push_back(t.rbuf.get());
+    }
+    while (nf > 0 && (max_depth < 0 || level < max_depth)) {
+        if (!bu && (double)mf > (double)mu / alpha) bu = true;
+        else if (bu && (double)nf < (double)nrows / beta) bu = false;
+        if (bu) exchange_halo(g, JG_ADJ_BOTH, dv, sizeof(int32_t), ncclInt32);  // the peers' depths
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
+            SBfsLevel a{};
+            a.rp = sh.both.row_ptr.get();
+            a.col = sh.both.col.get();
+            a.rows = sh.rows;
+            a.dvec = t.dvec.get();
+            a.stamp = t.stamp.get();
+            a.queue_in = t.queue[cur].get();
+            a.qoff_in = t.qoff[cur].get();
+            a.nq = t.nq;
+            a.mf = t.mf;
+            a.queue_out = t.queue[cur ^ 1].get();
+            a.qoff_out = t.qoff[cur ^ 1].get();
+            a.rbuf = t.rbuf.get();
+            a.send_src = sh.halo_both.send_src.get();
+            a.nrecv = sh.halo_both.send_off[g.P];
+            a.packed = t.ctr.get();
+            a.level = level;
+            const unsigned grid = (unsigned)std::min<int64_t>(
+                std::max<int64_t>((((sh.rows + 63) / 64) * kWave + kBlock - 1) / kBlock, 64), tune().bfs_grid);
+            if (bu) {
+                sbfs_bu_kernel<<<grid, kBlock, 0, sh.stream>>>(a);
+            } else if (t.mf > 0) {
+                sbfs_td_push_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
+                                          (t.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
+                                      kBlock, 0, sh.stream>>>(a);
+            }
+            JG_LAUNCH_CHECK();
+        }
+        if (!bu) {
+            exchange_halo_reverse(g, JG_ADJ_BOTH, sv, rv, sizeof(int32_t), ncclInt32);
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh.device);
+                St& t = st[i];
+                SBfsLevel a{};
+                a.rp = sh.both.row_ptr.get();
+                a.rows = sh.rows;
+                a.dvec = t.dvec.get();
+                a.queue_out = t.queue[cur ^ 1].get();
+                a.qoff_out = t.qoff[cur ^ 1].get();
+                a.rbuf = t.rbuf.get();
+                a.send_src = sh.halo_both.send_src.get();
+                a.nrecv = sh.halo_both.send_off[g.P];
+                a.packed = t.ctr.get();
+                a.level = level;
+                if (a.nrecv > 0) {
+                    sbfs_td_apply_kernel<<<(unsigned)std::min<int64_t>((a.nrecv + kBlock - 1) / kBlock, tune().bfs_grid),
+                                           kBlock, 0, sh.stream>>>(a);
+                    JG_LAUNCH_CHECK();
+                }
+            }
+        }
+        int64_t sums[2] = {0, 0};
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            unsigned long long c = 0;
+            copy_d2h(&c, st[i].ctr.get(), sizeof c, sh.stream);
+            st[i].nq = (int64_t)(c >> kPackShift);
+            st[i].mf = (int64_t)(c & kEdgeMask);
+            sums[0] += st[i].nq;
+            sums[1] += st[i].mf;
+        }
+        allreduce_sum_i64(g, sums, 2);
+        nf = sums[0];
+        mf = sums[1];
+        mu -= mf;
+        edges += mf;
+        cur ^= 1;
+        ++level;
+        if (debug_bfs())
+            std::fprintf(stderr, "[jg sbfs] level %d %s next frontier %lld vertices %lld entries\n", level - 1,
+                         bu ? "bottom-up" : "top-down", (long long)nf, (long long)mf);
+    }
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventRecord(t1, sh0.stream));
+        JG_HIP(hipEventSynchronize(t1));
+        JG_HIP(hipEventElapsedTime(ms_out, t0, t1));
+        JG_HIP(hipEventDestroy(t0));
+        JG_HIP(hipEventDestroy(t1));
+    }
+    // depths of the own rows: the compact vector's own segment
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
+        if (sh.rows)
+            JG_HIP(hipMemcpyAsync(sh.bfs_depth.get(), st[i].dvec.get(), sh.rows * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, sh.stream));
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    *edges_out = (double)edges;
+    return level;  // levels run, as dobfs_single counts them
+}
+
 }  // namespace
 
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out) {
@@ -532,12 +834,34 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
     const bool single = nsrc == 1 && g.P == 1;
+    const bool sharded_do = nsrc == 1 && g.P > 1 && direction == JG_DIR_BOTH && g.shards[0]->halo_both.on &&
+                            tune().sharded_bfs;
     hipEvent_t t0, t1;
     Shard& sh0 = *g.shards[0];
     DeviceGuard dg0(sh0.device);
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
-    if (single) {
+    if (sharded_do) {
+        int shard = -1;
+        const int64_t l = local_of_vid(g, source_vids[0], &shard);
+        double edges = 0;
+        float ms = 0;
+        const int levels = dobfs_sharded(g, l >= 0 ? shard : -1, l, max_depth, &edges, &ms);
+        ctx.last.compute_ms = ms;
+        ctx.last.levels = levels;
+        ctx.last.supersteps = levels;
+        ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
+        if (depth_out) {
+            for (auto& sp : g.shards) {
+                Shard& sh = *sp;
+                DeviceGuard dg(sh.device);
+                std::vector<int32_t> h(sh.rows);
+                if (sh.rows) copy_d2h(h.data(), sh.bfs_depth.get(), sh.rows * sizeof(int32_t), sh.stream);
+                for (int64_t v = 0; v < sh.rows; ++v) depth_out[sh.dense_of_local[v]] = h[v];
+            }
+        }
+        prof_collect(ctx, g);
+    } else if (single) {
         Shard& sh = sh0;
         const BfsCsrs c = pick_csrs(sh, direction);
         int shard = 0;

@@ -243,6 +243,11 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     depth = g.bfs(vid[srcs], 1)  # OUT traversal: bit-parallel pull over the IN adjacency
     for k in range(len(srcs)):
         np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 1))
+    # single source, BOTH: the sharded direction-optimising BFS (halo plans), unbounded and bounded
+    for k in range(3):
+        for md in (-1, 2):
+            d1 = g.bfs(vid[srcs[k:k + 1]], 3, md)[0]
+            np.testing.assert_array_equal(d1, oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3, md))
     assert g.info()["num_shards"] == shards
     g.close()
     c.close()

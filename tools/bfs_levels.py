@@ -12,8 +12,9 @@ import janusgraph_amd as jg  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--scale", type=int, default=20)
 ap.add_argument("--runs", type=int, default=4)
+ap.add_argument("--shards", type=int, default=1, help="logical shards on device 0 (sharded DO-BFS when > 1)")
 a = ap.parse_args()
-ctx = jg.Context((0,))
+ctx = jg.Context((0,) * a.shards)
 g = ctx.build_rmat(a.scale, 16, 0x5EED + a.scale, flags=jg.ADJ_BOTH)
 rng = np.random.default_rng(1)
 for k in range(a.runs):
