@@ -357,6 +357,100 @@ __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsr
     }
 }
 
+// Top-down levels of the bit-parallel BFS (one shard): the frontier is a queue of vertices with a
+// nonzero word and their push-edge offsets.  Each frontier edge v -> u ORs F[v]'s unvisited bits into
+// Fnext[u] (OR is order-independent: deterministic); the first toucher of u queues it; the apply pass
+// turns the touched words into the next frontier.
+__global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned long long* __restrict__ F, int64_t rows,
+                                                                const int64_t* __restrict__ push_rp,
+                                                                int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                                unsigned long long* __restrict__ packed) {
+    __shared__ AppendScratch sc;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t v = x0 + threadIdx.x;
+        const bool take = v < rows && F[v] != 0ull;
+        const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
+        block_append_frontier(take, (int32_t)v, deg, queue, qoff, packed, sc);
+    }
+}
+
+struct MsTd {
+    const int32_t* queue;
+    const int64_t* qoff;
+    int64_t nq, mf;
+    const int64_t* push_rp;
+    const int32_t* push_col;
+    const unsigned long long* F;
+    const unsigned long long* visited;
+    unsigned long long* Fnext;
+    int32_t* touched;
+    int64_t* touched_off;  // scratch (block_append_frontier writes edge offsets)
+    unsigned long long* tpacked;
+};
+
+__global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
+    __shared__ AppendScratch sc;
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+        }
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
+            bool take = false;
+            int32_t u = 0;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                }
+                const int32_t v = a.queue[i];
+                u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
+                const unsigned long long w = a.F[v] & ~a.visited[u];
+                if (w) take = atomicOr(&a.Fnext[u], w) == 0ull;
+            }
+            block_append_frontier(take, u, 0, a.touched, a.touched_off, a.tpacked, sc);
+        }
+    }
+}
+
+// touched vertex u: its new bits become its next-frontier word (and the visited / depth updates)
+__global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* __restrict__ touched, int64_t nt,
+                                                                MsBfsOp op, const int64_t* __restrict__ push_rp,
+                                                                int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                                unsigned long long* __restrict__ packed) {
+    __shared__ AppendScratch sc;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nt; x0 += stride) {  // block-uniform trips
+        const int64_t x = x0 + threadIdx.x;
+        bool take = false;
+        int32_t u = 0;
+        int64_t deg = 0;
+        if (x < nt) {
+            u = touched[x];
+            const unsigned long long acc = op.Fout[u];  // the ORed words (finalize overwrites Fout[u])
+            op.finalize(u, acc);
+            take = op.Fout[u] != 0ull;
+            if (take) deg = push_rp[u + 1] - push_rp[u];
+        }
+        block_append_frontier(take, u, deg, queue, qoff, packed, sc);
+    }
+}
+
 // ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
 __global__ __launch_bounds__(kBlock) void sd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ wt,
@@ -947,8 +1041,81 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
             }
             JG_HIP(hipEventRecord(t0, sh0.stream));
+            // one shard with a push adjacency: levels whose frontier has few edges run top-down
+            const BfsCsrs c0 = pick_csrs(sh0, direction);
+            const bool td_ok = g.shards.size() == 1 && g.P == 1 && c0.push != nullptr && tune().msbfs_td;
+            struct Td {
+                DevBuf<int32_t> queue[2], touched;
+                DevBuf<int64_t> qoff[2], touched_off;
+                DevBuf<unsigned long long> ctr;  // [0] frontier, [1] touched
+                int64_t nq = 0, mf = 0;
+                int qc = 0;
+            } td;
+            auto read_frontier = [&]() {
+                unsigned long long h = 0;
+                copy_d2h(&h, td.ctr.get(), sizeof h, sh0.stream);
+                td.nq = (int64_t)(h >> kPackShift);
+                td.mf = (int64_t)(h & kEdgeMask);
+            };
+            auto build_frontier = [&](const unsigned long long* F, int qslot) {
+                JG_HIP(hipMemsetAsync(td.ctr.get(), 0, sizeof(unsigned long long), sh0.stream));
+                msbfs_frontier_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
+                    F, sh0.rows, c0.push->row_ptr.get(), td.queue[qslot].get(), td.qoff[qslot].get(), td.ctr.get());
+                JG_LAUNCH_CHECK();
+                read_frontier();
+            };
+            if (td_ok) {
+                const size_t r1 = (size_t)std::max<int64_t>(sh0.rows, 1);
+                for (int k = 0; k < 2; ++k) {
+                    td.queue[k].alloc(r1);
+                    td.qoff[k].alloc(r1);
+                }
+                td.touched.alloc(r1);
+                td.touched_off.alloc(r1);
+                td.ctr.alloc(2);
+                build_frontier(st[0].F[0].get(), 0);
+            }
             int cur = 0, level = 0;
             while (max_depth < 0 || level < max_depth) {
+                const bool td_level =
+                    td_ok && (double)td.mf < (double)c0.push->nnz / (double)tune().bfs_alpha;
+                if (td_level) {
+                    Shard& sh = sh0;
+                    St& t = st[0];
+                    JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
+                    JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, t.F[cur ^ 1].bytes(), sh.stream));
+                    JG_HIP(hipMemsetAsync(td.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+                    if (td.mf > 0) {
+                        MsTd a{td.queue[td.qc].get(), td.qoff[td.qc].get(), td.nq, td.mf, c0.push->row_ptr.get(),
+                               c0.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
+                               td.touched_off.get(), td.ctr.get() + 1};
+                        msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
+                                              (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
+                                          kBlock, 0, sh.stream>>>(a);
+                        JG_LAUNCH_CHECK();
+                    }
+                    unsigned long long th = 0;
+                    copy_d2h(&th, td.ctr.get() + 1, sizeof th, sh.stream);
+                    const int64_t nt = (int64_t)(th >> kPackShift);
+                    if (nt > 0) {
+                        MsBfsOp op;
+                        op.F = t.F[cur].get();
+                        op.Fout = t.F[cur ^ 1].get();
+                        op.visited = t.vis.get();
+                        op.depth = t.depth.get();
+                        op.changed = t.changed.get();
+                        op.rows = sh.rows;
+                        op.pos = g.vec_pos(sh, adj_of(sh, c0));
+                        op.lvl = level + 1;
+                        op.full = full;
+                        msbfs_td_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(
+                            td.touched.get(), nt, op, c0.push->row_ptr.get(), td.queue[td.qc ^ 1].get(),
+                            td.qoff[td.qc ^ 1].get(), td.ctr.get());
+                        JG_LAUNCH_CHECK();
+                    }
+                    read_frontier();
+                    td.qc ^= 1;
+                } else
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
                     DeviceGuard dg(sh.device);
@@ -970,8 +1137,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     // (MsBfsOp::active), which whole-entry merge tasks cannot
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                 (unsigned long long*)nullptr);
+                    if (td_ok) {  // the next level may run top-down: queue this level's frontier
+                        build_frontier(t.F[cur ^ 1].get(), td.qc ^ 1);
+                        td.qc ^= 1;
+                    }
                 }
-                {
+                if (!td_level) {
                     std::vector<void*> bufs;
                     for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
                     exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
