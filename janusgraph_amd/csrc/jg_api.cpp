@@ -250,6 +250,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "bfs_alpha" || k == "bfs_beta") {
         JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta must be in [1, 1e6]");
         (k == "bfs_alpha" ? jg::tune().bfs_alpha : jg::tune().bfs_beta) = (int)value;
+    } else if (k == "cc_push") {
+        jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {
         jg::tune().msbfs_td = value != 0;
     } else if (k == "sharded_bfs") {

@@ -13,6 +13,7 @@
 // ties (a prefix such as "1" < "10") broken by fewer digits — computed with two stable radix sorts.
 #include <climits>
 
+#include "jg_frontier.h"
 #include "jg_pull.h"
 
 namespace jg {
@@ -81,6 +82,86 @@ __global__ void cc_init_kernel(const int32_t* __restrict__ lab0, const int64_t* 
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
         label[l] = lab0[l];
         msg[pos(l)] = (rp[l + 1] > rp[l]) ? lab0[l] : INT_MAX;  // only vertices with edges send
+    }
+}
+
+// Sparse supersteps on one shard run push-style: only the vertices that sent a label (changed in
+// the previous superstep) are visited; each takes the min into its neighbours' candidates
+// (atomicMin: order-independent, so the result equals the pull superstep's), the first toucher of a
+// neighbour queues it, and the apply pass keeps the improvements.  No-message cells are any value
+// >= kNoMsg (INT_MAX from finalize, 0x7F7F7F7F from a memset); labels are ranks < n.
+constexpr int32_t kNoMsg = 0x7F7F7F7F;
+
+__global__ __launch_bounds__(kBlock) void cc_senders_kernel(const int32_t* __restrict__ msg, int64_t rows,
+                                                            const int64_t* __restrict__ rp, int32_t* __restrict__ queue,
+                                                            int64_t* __restrict__ qoff,
+                                                            unsigned long long* __restrict__ packed) {
+    __shared__ AppendScratch sc;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t v = x0 + threadIdx.x;
+        const bool take = v < rows && msg[v] < kNoMsg;
+        block_append_frontier(take, (int32_t)v, take ? rp[v + 1] - rp[v] : 0, queue, qoff, packed, sc);
+    }
+}
+
+struct CcPush {
+    const int32_t* queue;
+    const int64_t* qoff;
+    int64_t nq, mf;
+    const int64_t* rp;
+    const int32_t* col;
+    const int32_t* msg;
+    int32_t* cand;  // the next superstep's message vector, preset to kNoMsg
+    int32_t* touched;
+    int64_t* touched_off;
+    unsigned long long* tpacked;
+};
+
+__global__ __launch_bounds__(kBlock) void cc_push_kernel(CcPush a) {
+    __shared__ AppendScratch sc;
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * 4;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * 4 >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * 4;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t e = e0 + k;
+            bool take = false;
+            int32_t v = 0;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                }
+                const int32_t u = a.queue[i];
+                v = a.col[a.rp[u] + (e - a.qoff[i])];
+                const int32_t m = a.msg[u];
+                if (m < a.cand[v]) take = atomicMin(&a.cand[v], m) == kNoMsg;
+            }
+            block_append_frontier(take, v, 0, a.touched, a.touched_off, a.tpacked, sc);
+        }
+    }
+}
+
+// touched vertex v: the pull superstep's finalize with the pushed minimum
+__global__ void cc_push_apply_kernel(const int32_t* __restrict__ touched, int64_t nt, CcOp op) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nt; x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = touched[x];
+        op.finalize(v, op.msg_out[v]);  // msg_out holds the candidate; finalize rewrites it
     }
 }
 
@@ -163,8 +244,62 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     JG_HIP(hipEventCreate(&t1));
     JG_HIP(hipEventRecord(t0, sh0.stream));
     int iteration = 0, cur = 0;
+    // one shard: supersteps whose senders have few edges run push-style
+    const bool push_ok = g.shards.size() == 1 && g.P == 1 && tune().cc_push;
+    struct Push {
+        DevBuf<int32_t> queue, touched;
+        DevBuf<int64_t> qoff, touched_off;
+        DevBuf<unsigned long long> ctr;
+    } pu;
+    if (push_ok) {
+        const size_t r1 = (size_t)std::max<int64_t>(sh0.rows, 1);
+        pu.queue.alloc(r1);
+        pu.touched.alloc(r1);
+        pu.qoff.alloc(r1);
+        pu.touched_off.alloc(r1);
+        pu.ctr.alloc(2);
+    }
     while (any && iteration < kCcMaxIterations - 1) {
         ++iteration;
+        bool pushed = false;
+        if (push_ok) {
+            Shard& sh = sh0;
+            JG_HIP(hipMemsetAsync(pu.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+            cc_senders_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.cc_msg[cur].get(), sh.rows,
+                                                                           sh.both.row_ptr.get(), pu.queue.get(),
+                                                                           pu.qoff.get(), pu.ctr.get());
+            JG_LAUNCH_CHECK();
+            unsigned long long h = 0;
+            copy_d2h(&h, pu.ctr.get(), sizeof h, sh.stream);
+            const int64_t nq = (int64_t)(h >> kPackShift), mf = (int64_t)(h & kEdgeMask);
+            if ((double)mf < (double)sh.both.nnz / (double)tune().bfs_alpha) {
+                pushed = true;
+                JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
+                JG_HIP(hipMemsetAsync(sh.cc_msg[cur ^ 1].get(), 0x7F, sh.cc_msg[cur ^ 1].bytes(), sh.stream));
+                if (mf > 0) {
+                    CcPush a{pu.queue.get(), pu.qoff.get(), nq, mf, sh.both.row_ptr.get(), sh.both.col.get(),
+                             sh.cc_msg[cur].get(), sh.cc_msg[cur ^ 1].get(), pu.touched.get(), pu.touched_off.get(),
+                             pu.ctr.get() + 1};
+                    cc_push_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>((mf / 4 + kBlock - 1) / kBlock, 1),
+                                                                  4096),
+                                     kBlock, 0, sh.stream>>>(a);
+                    JG_LAUNCH_CHECK();
+                    copy_d2h(&h, pu.ctr.get() + 1, sizeof h, sh.stream);
+                    const int64_t nt = (int64_t)(h >> kPackShift);
+                    if (nt > 0) {
+                        CcOp op;
+                        op.msg = sh.cc_msg[cur].get();
+                        op.msg_out = sh.cc_msg[cur ^ 1].get();
+                        op.label = sh.cc_label.get();
+                        op.changed = sh.cc_changed.get();
+                        op.pos = g.vec_pos(sh, JG_ADJ_BOTH);
+                        cc_push_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(pu.touched.get(), nt, op);
+                        JG_LAUNCH_CHECK();
+                    }
+                }
+            }
+        }
+        if (!pushed)
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
             DeviceGuard dg(sh.device);

@@ -333,6 +333,7 @@ struct Tune {
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
+    int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)

@@ -23,6 +23,7 @@
 
 #include <cstdio>
 
+#include "jg_frontier.h"
 #include "jg_pull.h"
 
 namespace jg {
@@ -30,8 +31,6 @@ namespace jg {
 namespace {
 
 constexpr int kTdLanes = 16;         // lanes per frontier vertex in the weighted-SD push
-constexpr int kPackShift = 37;       // packed frontier counter: (vertices << 37) | push edges
-constexpr unsigned long long kEdgeMask = (1ull << kPackShift) - 1ull;
 constexpr int kTdEdgesPerThread = 4;
 constexpr int kBuBatch = 4;             // bottom-up: neighbours probed per step
 constexpr int kBfsRing = 4;            // level-state ring: a level touches slots L-1, L, L+1
@@ -130,47 +129,6 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
         c.bottom_up = 0;  // the queue is always valid: both directions append to it
     }
     return c;
-}
-
-// Block-aggregated form of wave_append_frontier: the block's waves combine their counts in LDS and
-// one thread reserves the block's range with a single atomic (a level that finds most of the graph
-// would otherwise put one atomic per wave on one address).  Must be reached by every thread of the
-// block (block-uniform call sites); queue positions and edge offsets stay monotone.
-struct AppendScratch {
-    unsigned long long cnt[kBlock / kWave], deg[kBlock / kWave];
-    unsigned long long base;
-};
-__device__ __forceinline__ void block_append_frontier(bool take, int32_t v, int64_t deg, int32_t* __restrict__ queue,
-                                                      int64_t* __restrict__ qoff, unsigned long long* __restrict__ packed,
-                                                      AppendScratch& sc) {
-    const uint64_t mask = __ballot(take);
-    const int64_t d = take ? deg : 0;
-    const int64_t dinc = wave_inclusive_scan_add(d);
-    const int wv = wave_id();
-    if (lane_id() == kWave - 1) {
-        sc.cnt[wv] = (unsigned long long)__popcll(mask);
-        sc.deg[wv] = (unsigned long long)dinc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long c = 0, e = 0;
-        for (int k = 0; k < kBlock / kWave; ++k) {
-            const unsigned long long ck = sc.cnt[k], ek = sc.deg[k];
-            sc.cnt[k] = c;  // exclusive prefixes
-            sc.deg[k] = e;
-            c += ck;
-            e += ek;
-        }
-        sc.base = c ? atomicAdd(packed, (c << kPackShift) | e) : 0ull;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long base = sc.base;
-        const uint64_t pos = (base >> kPackShift) + sc.cnt[wv] + (uint64_t)__popcll(mask & lanemask_lt());
-        queue[pos] = v;
-        qoff[pos] = (int64_t)(base & kEdgeMask) + (int64_t)sc.deg[wv] + dinc - d;
-    }
-    __syncthreads();  // the scratch is reused by the next call
 }
 
 // Edge-parallel top-down: frontier edge e in [0, mf) belongs to the queue entry i with
