@@ -166,6 +166,19 @@ int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direct
  * (nullable) = supersteps of the synchronous program. */
 int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out);
 
+/* Decode n edgestore entries on the context's first GPU, as EdgeSerializer.parseRelation does
+ * (core/graphdb/database/EdgeSerializer.java:86-122; header: IDHandler.readRelationType,
+ * idhandling/IDHandler.java:130-141; varints: idhandling/VariableLong.java:44-52,193-208,276-294).
+ * Entry i is bytes[entry_off[i] .. entry_off[i+1]) (column then value), value_pos[i] its value
+ * position (the column length).  type_ids / type_mult (ntypes, may be 0) give the multiplicity of
+ * edge labels: 0 MULTI, 1 SIMPLE, 2 ONE2MANY, 3 MANY2ONE, 4 ONE2ONE (core/core/Multiplicity.java);
+ * labels absent from the table are MULTI.  Outputs per entry (each nullable): the relation type id,
+ * dir_out = 0 OUT edge, 1 IN edge, 2 property, 3 system relation, -1 malformed; the other vertex id
+ * and the relation id (-1 unless a user edge).  Stats: compute_ms = kernel time. */
+int jg_decode_edges(jg_ctx* ctx, const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off,
+                    const int32_t* value_pos, int64_t n, const int64_t* type_ids, const int8_t* type_mult,
+                    int32_t ntypes, int64_t* type_out, int8_t* dir_out, int64_t* other_out, int64_t* relation_out);
+
 /* Block until all work enqueued on the graph's streams is complete. */
 int jg_graph_sync(jg_graph* g);
 

@@ -32,7 +32,7 @@ EXPORTS = [
     "jg_abi_version", "jg_last_error", "jg_ctx_create", "jg_comm_unique_id", "jg_ctx_create_rank",
     "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
-    "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_graph_sync",
+    "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set",
 ]
 
@@ -106,6 +106,7 @@ def load():
         "jg_shortest_distance": ([_P, _i64, _i32, _P], ctypes.c_int),
         "jg_bfs": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
         "jg_connected_components": ([_P, _P, _P], ctypes.c_int),
+        "jg_decode_edges": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i32, _P, _P, _P, _P], ctypes.c_int),
         "jg_graph_sync": ([_P], ctypes.c_int),
         "jg_tune_set": ([ctypes.c_char_p, _i64], ctypes.c_int),
     }
@@ -182,6 +183,27 @@ class Context:
         s = Stats()
         check(load().jg_ctx_last_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
+
+    def decode_edges(self, data, entry_off, value_pos, type_ids=(), type_mult=()):
+        """jg_decode_edges: decode edgestore entries (column + value bytes) on the GPU.
+        Returns (type_id, dir, other_vertex_id, relation_id); dir 0 OUT, 1 IN, 2 property, 3 system
+        relation, -1 malformed."""
+        data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                    np.uint8)
+        off = np.ascontiguousarray(entry_off, np.int64)
+        vpos = np.ascontiguousarray(value_pos, np.int32)
+        n = len(vpos)
+        if len(off) != n + 1:
+            raise ValueError("entry_off needs n + 1 offsets")
+        tid = np.ascontiguousarray(type_ids, np.int64)
+        tm = np.ascontiguousarray(type_mult, np.int8)
+        if len(tid) != len(tm):
+            raise ValueError("type_ids and type_mult differ in length")
+        t, d, o, r = (np.empty(max(n, 1), np.int64), np.empty(max(n, 1), np.int8), np.empty(max(n, 1), np.int64),
+                      np.empty(max(n, 1), np.int64))
+        check(load().jg_decode_edges(self._h, _ptr(data), len(data), _ptr(off), _ptr(vpos), n, _ptr(tid), _ptr(tm),
+                                     len(tid), _ptr(t), _ptr(d), _ptr(o), _ptr(r)))
+        return t[:n], d[:n], o[:n], r[:n]
 
     def build(self, vid, src, dst, weight=None, flags=ADJ_IN | ADJ_OUT | ADJ_BOTH) -> "Graph":
         vid = np.ascontiguousarray(vid, np.int64)

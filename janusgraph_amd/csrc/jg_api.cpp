@@ -618,6 +618,16 @@ int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direct
     JG_GUARD_END
 }
 
+int jg_decode_edges(jg_ctx* ctx, const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off,
+                    const int32_t* value_pos, int64_t n, const int64_t* type_ids, const int8_t* type_mult,
+                    int32_t ntypes, int64_t* type_out, int8_t* dir_out, int64_t* other_out, int64_t* relation_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx, "null context");
+    jg::decode_edges(ctx->impl, bytes, nbytes, entry_off, value_pos, n, type_ids, type_mult, ntypes, type_out, dir_out,
+                     other_out, relation_out);
+    JG_GUARD_END
+}
+
 int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out) {
     JG_GUARD_BEGIN
     JG_ARG(g, "null graph");

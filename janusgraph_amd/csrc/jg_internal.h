@@ -294,6 +294,11 @@ void release_halo_maps(Halo& h);
 // Checks that every shard's send counts equal its peers' receive counts (RCCL: count allgather).
 void check_halo_counts(Graph& g, uint32_t adj);
 
+// ---- edgestore decode (jg_decode.hip) ----
+void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* off, const int32_t* vpos, int64_t n,
+                  const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int64_t* type_out,
+                  int8_t* dir_out, int64_t* other_out, int64_t* rel_out);
+
 // ---- programs ----
 void pagerank_begin(Graph& g, double damping, int64_t vertex_count);
 void pagerank_steps(Graph& g, int nsteps);

@@ -1,0 +1,172 @@
+"""Writer side of JanusGraph's edgestore entry format, restated in Python (TEST INFRASTRUCTURE ONLY:
+imported by tests/ to build encoded inputs for the decoders; never by janusgraph_amd/).
+
+Reference paths are relative to /root/reference/janusgraph-core/src/main/java/org/janusgraph/:
+  graphdb/database/idhandling/VariableLong.java   writeUnsigned :55-69, writePositive :99-102,
+      positiveLength :124-127, writePositiveWithPrefix :159-185, readPositiveWithPrefix :193-208,
+      writeUnsignedBackward :257-268, unsignedBackwardLength :270-274, readUnsignedBackward :276-294
+  graphdb/database/idhandling/IDHandler.java      DirectionID :38-98, writeRelationType :117-122
+  graphdb/idmanagement/IDManager.java             VertexIDType suffixes :210-300, getSchemaId :650-653
+  graphdb/database/EdgeSerializer.java            writeRelation :239-303 (column / value layout)
+  core/Multiplicity.java                          isUnique :80-90
+"""
+from __future__ import annotations
+
+MULTI, SIMPLE, ONE2MANY, MANY2ONE, ONE2ONE = 0, 1, 2, 3, 4
+OUT, IN = 0, 1
+SUFFIX = {"user_edge": 21, "system_edge": 53, "user_key": 5, "system_key": 37}
+
+
+def _bit_length(v: int) -> int:
+    return 1 if v == 0 else v.bit_length()
+
+
+def write_unsigned(v: int, nbits: int | None = None) -> bytes:
+    """VariableLong.writeUnsigned: 7-bit groups, most significant first, stop bit on the last byte."""
+    if nbits is None:
+        nbits = ((_bit_length(v) - 1) // 7 + 1) * 7
+    out = bytearray()
+    off = nbits
+    while off > 0:
+        off -= 7
+        b = (v >> off) & 0x7F
+        if off == 0:
+            b |= 0x80
+        out.append(b)
+    return bytes(out)
+
+
+def read_unsigned(b: bytes, pos: int) -> tuple[int, int]:
+    v = 0
+    while True:
+        c = b[pos]
+        pos += 1
+        v = (v << 7) | (c & 0x7F)
+        if c & 0x80:
+            return v, pos
+
+
+def write_positive(v: int) -> bytes:
+    assert v >= 0
+    return write_unsigned(v)
+
+
+def positive_length(v: int) -> int:
+    return (_bit_length(v) - 1) // 7 + 1
+
+
+def backward_length(v: int) -> int:
+    """VariableLong.unsignedBackwardLength."""
+    bl = _bit_length(v)
+    return max(3, 1 + (0 if bl <= 4 else 1 + (bl - 5) // 7))
+
+
+def write_positive_backward(v: int) -> bytes:
+    """VariableLong.writeUnsignedBackward: first byte = stop marker | (length - 3) << 4 | top 4 bits."""
+    assert v >= 0
+    n = backward_length(v)
+    out = bytearray()
+    b = ((n - 3) << 4) | 0x80
+    for i in range(n - 1, -1, -1):
+        b |= 0x7F & (v >> (i * 7))
+        out.append(b & 0xFF)
+        b = 0
+    return bytes(out)
+
+
+def read_positive_backward(b: bytes, pos: int) -> tuple[int, int]:
+    """VariableLong.readUnsignedBackward from position pos (exclusive end); returns (value, new pos)."""
+    v = 0
+    n = 0
+    while True:
+        pos -= 1
+        c = b[pos]
+        if c & 0x80:
+            v |= (c & 0x0F) << (7 * n)
+            assert ((c >> 4) & 7) + 3 == n + 1
+            return v, pos
+        v |= c << (7 * n)
+        n += 1
+
+
+def write_positive_with_prefix(v: int, prefix: int, prefix_len: int) -> bytes:
+    """VariableLong.writePositiveWithPrefix."""
+    assert v >= 0 and 0 < prefix_len < 6 and prefix < (1 << prefix_len)
+    delta = 8 - prefix_len
+    first = (prefix << delta) & 0xFF
+    vlen = _bit_length(v)
+    mod = vlen % 7
+    if mod <= delta - 1:
+        off = vlen - mod
+        first |= v >> off
+        v &= (1 << off) - 1
+        vlen -= mod
+    else:
+        vlen += 7 - mod
+    if vlen > 0:
+        first |= 1 << (delta - 1)
+    out = bytes([first & 0xFF])
+    if vlen > 0:
+        out += write_unsigned(v, vlen)
+    return out
+
+
+def read_positive_with_prefix(b: bytes, pos: int, prefix_len: int) -> tuple[int, int, int]:
+    """VariableLong.readPositiveWithPrefix; returns (value, prefix, new pos)."""
+    first = b[pos]
+    pos += 1
+    delta = 8 - prefix_len
+    prefix = first >> delta
+    v = first & ((1 << (delta - 1)) - 1)
+    if (first >> (delta - 1)) & 1:
+        p0 = pos
+        rem, pos = read_unsigned(b, pos)
+        v = (v << ((pos - p0) * 7)) + rem
+    return v, prefix, pos
+
+
+def schema_id(count: int, kind: str) -> int:
+    """IDManager.getSchemaId: count << 6 | the type's suffix."""
+    return (count << 6) | SUFFIX[kind]
+
+
+def write_relation_type(type_id: int, is_edge: bool, direction: int, invisible: bool = False) -> bytes:
+    """IDHandler.writeRelationType (PREFIX_BIT_LEN = 3)."""
+    system = (type_id & 63) in (SUFFIX["system_edge"], SUFFIX["system_key"])
+    rel_type = 1 if is_edge else 0
+    dir_int = direction if is_edge else 0
+    prefix = ((0 if system else (2 if invisible else 1)) << 1) + rel_type
+    stripped = ((type_id >> 6) << 1) + dir_int
+    return write_positive_with_prefix(stripped, prefix, 3)
+
+
+def is_unique(mult: int, direction: int) -> bool:
+    if direction == IN:
+        return mult in (ONE2MANY, ONE2ONE)
+    return mult in (MANY2ONE, ONE2ONE)
+
+
+def encode_edge(type_id: int, direction: int, other: int, rel: int, mult: int = MULTI, sort_key: bytes = b"",
+                value: bytes = b"", invisible: bool = False) -> tuple[bytes, int]:
+    """EdgeSerializer.writeRelation for an edge: (entry bytes = column + value, value position)."""
+    col = bytearray(write_relation_type(type_id, True, direction, invisible))
+    if mult == MULTI:
+        col += sort_key
+        col += write_positive_backward(other)
+        col += write_positive_backward(rel)
+        vpos = len(col)
+        tail = b""
+    elif is_unique(mult, direction):
+        vpos = len(col)
+        tail = write_positive(other) + write_positive(rel)
+    else:
+        col += write_positive_backward(other)
+        vpos = len(col)
+        tail = write_positive(rel)
+    return bytes(col) + tail + value, vpos
+
+
+def encode_property(type_id: int, rel: int, value: bytes = b"\x00") -> tuple[bytes, int]:
+    """A LIST-cardinality property entry: [header][relation backward] | value."""
+    col = write_relation_type(type_id, False, OUT) + write_positive_backward(rel)
+    return col + value, len(col)

@@ -426,3 +426,93 @@ JO_API int jo_num_threads(void) {
     return 1;
 #endif
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Edgestore entry decode: one adjacency column of a vertex row, as
+ * EdgeSerializer.parseRelation reads it (core/graphdb/database/EdgeSerializer.java:86-122).
+ *   header: IDHandler.readRelationType (core/graphdb/database/idhandling/IDHandler.java:130-141) =
+ *     VariableLong.readPositiveWithPrefix(in, 3) (idhandling/VariableLong.java:193-208): prefix bit 0 =
+ *     relation type (0 property, 1 edge), prefix >> 1 == 0 = system type; value bit 0 = direction
+ *     (0 OUT, 1 IN), value >> 1 = type count; type id = count << 6 | suffix (IDManager.getSchemaId,
+ *     core/graphdb/idmanagement/IDManager.java:650-653; suffixes :269-294 and the property keys).
+ *   edge, MULTI (unconstrained): [header][sort key][other backward][relation backward] | value, both
+ *     read backward from the value position (readUnsignedBackward, VariableLong.java:276-294);
+ *   edge, constrained, unique in this direction: | [other forward][relation forward] (readPositive,
+ *     VariableLong.java:44-52,93-97);
+ *   edge, constrained, not unique: [header][other backward] | [relation forward]
+ *   (EdgeSerializer.writeRelation :264-279 is the writer of all three).
+ * Multiplicity codes: 0 MULTI, 1 SIMPLE, 2 ONE2MANY (unique IN), 3 MANY2ONE (unique OUT), 4 ONE2ONE
+ * (core/core/Multiplicity.java:35-90); edge labels absent from the table are MULTI.
+ * dir_out: 0 OUT edge, 1 IN edge, 2 property entry, 3 system relation (ids not decoded: -1).
+ * ------------------------------------------------------------------------------------------ */
+static int64_t jo_read_unsigned(const uint8_t* b, int64_t* pos) {
+    int64_t v = 0;
+    int8_t c;
+    do {
+        c = (int8_t)b[(*pos)++];
+        v = (v << 7) | (c & 0x7F);
+    } while (c >= 0);
+    return v;
+}
+
+static int64_t jo_read_unsigned_backward(const uint8_t* b, int64_t* pos) {
+    int64_t v = 0;
+    int n = 0;
+    for (;;) {
+        const int8_t c = (int8_t)b[--(*pos)];
+        if (c < 0) {  /* first byte: stop marker, 3 length bits, 4 value bits */
+            v |= (int64_t)(c & 0x0F) << (7 * n);
+            break;
+        }
+        v |= (int64_t)c << (7 * n);
+        ++n;
+    }
+    return v;
+}
+
+JO_API void jo_decode_edges(const uint8_t* bytes, const int64_t* off, const int32_t* vpos, int64_t n,
+                            const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int64_t* type_out,
+                            int8_t* dir_out, int64_t* other_out, int64_t* rel_out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < n; ++e) {
+        const uint8_t* b = bytes + off[e];
+        /* readPositiveWithPrefix(in, 3) */
+        int64_t pos = 0;
+        const int first = b[pos++];
+        const int64_t prefix = first >> 5;
+        int64_t value = first & 0x0F;
+        if ((first >> 4) & 1) {
+            const int64_t p0 = pos;
+            const int64_t rem = jo_read_unsigned(b, &pos);
+            value = (value << (7 * (pos - p0))) + rem;
+        }
+        const int is_edge = (int)(prefix & 1), dirbit = (int)(value & 1), system = (prefix >> 1) == 0;
+        const int64_t count = value >> 1;
+        const int64_t suffix = is_edge ? (system ? 53 : 21) : (system ? 37 : 5);
+        const int64_t type_id = (count << 6) | suffix;
+        type_out[e] = type_id;
+        if (!is_edge || system) {
+            dir_out[e] = (int8_t)(is_edge ? 3 : 2);
+            other_out[e] = -1;
+            rel_out[e] = -1;
+            continue;
+        }
+        dir_out[e] = (int8_t)dirbit;
+        int mult = 0;
+        for (int32_t t = 0; t < ntypes; ++t)
+            if (type_ids[t] == type_id) { mult = type_mult[t]; break; }
+        const int unique = dirbit ? (mult == 2 || mult == 4) : (mult == 3 || mult == 4);
+        int64_t p = vpos[e];
+        if (mult == 0) {
+            rel_out[e] = jo_read_unsigned_backward(b, &p);
+            other_out[e] = jo_read_unsigned_backward(b, &p);
+        } else if (unique) {
+            other_out[e] = jo_read_unsigned(b, &p);
+            rel_out[e] = jo_read_unsigned(b, &p);
+        } else {
+            other_out[e] = jo_read_unsigned_backward(b, &p);
+            p = vpos[e];
+            rel_out[e] = jo_read_unsigned(b, &p);
+        }
+    }
+}

@@ -59,6 +59,11 @@ def lib():
         L.jo_connected_components.restype = ctypes.c_int
         L.jo_num_threads.argtypes = []
         L.jo_num_threads.restype = ctypes.c_int
+        _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+        _i8p = np.ctypeslib.ndpointer(dtype=np.int8, flags="C_CONTIGUOUS")
+        L.jo_decode_edges.argtypes = [_u8p, _i64p, _i32p, ctypes.c_int64, _i64p, _i8p, ctypes.c_int32, _i64p, _i8p,
+                                      _i64p, _i64p]
+        L.jo_decode_edges.restype = None
         _lib = L
     return _lib
 
@@ -159,3 +164,17 @@ def connected_components(n, src, dst, vid, max_iterations=100):
     comp = np.empty(max(n, 1), np.int64)
     it = lib().jo_connected_components(n, len(src), src, dst, vid, int(max_iterations), comp)
     return comp[:n], int(it)
+
+
+def decode_edges(data, off, vpos, type_ids=(), type_mult=()):
+    """Decode edgestore entries (jo_decode_edges): data[off[i]:off[i+1]] is entry i, vpos[i] its value
+    position.  Returns (type_id, dir, other, relation_id) arrays; dir 0 OUT, 1 IN, 2 property, 3 system."""
+    data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data,
+                                np.uint8)
+    off, vpos = _i64(off), _i32(vpos)
+    n = len(vpos)
+    t, d, o, r = (np.empty(n, np.int64), np.empty(n, np.int8), np.empty(n, np.int64), np.empty(n, np.int64))
+    tid = _i64(type_ids) if len(type_ids) else np.zeros(1, np.int64)
+    tm = np.ascontiguousarray(type_mult, np.int8) if len(type_mult) else np.zeros(1, np.int8)
+    lib().jo_decode_edges(data if len(data) else np.zeros(1, np.uint8), off, vpos, n, tid, tm, len(type_ids), t, d, o, r)
+    return t, d, o, r

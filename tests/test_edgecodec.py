@@ -1,0 +1,130 @@
+"""Edgestore entry codec, CPU side.
+
+1. The Python restatement of VariableLong (oracle/edgecodec.py) against the reference's own
+   known-answer tests, janusgraph-test/.../graphdb/idmanagement/VariableLongTest.java:
+   readWriteTest :42-94 (values written in sequence, read back in order — backward encodings from
+   the end — with the encoded length checked for every value, then the 0 / Long.MAX_VALUE
+   boundaries), at the ranges of testPosBackwardWrite{Small,Big} :129-137 and
+   testPrefix{1,2,3}Write* :149-167 (sampled with a coarser jump where a full Python walk would be
+   slow), and byteOrderPreservingPositiveBackward :287-300.
+2. The C oracle decoder (jo_decode_edges, EdgeSerializer.parseRelation :86-122) recovers every field
+   of entries the restated writer (EdgeSerializer.writeRelation :239-303) produced: every
+   multiplicity, both directions, sort keys, trailing values, property and system entries.
+"""
+import numpy as np
+
+from oracle import edgecodec as ec
+
+LONG_MAX = (1 << 63) - 1
+
+
+def _read_write_backward(max_value, jump):
+    values = list(range(0, max_value + 1, jump))
+    buf = b"".join(ec.write_positive_backward(v) for v in values)
+    pos = len(buf)
+    for v in reversed(values):
+        got, npos = ec.read_positive_backward(buf, pos)
+        assert got == v
+        assert pos - npos == ec.backward_length(v)
+        pos = npos
+    assert pos == 0
+    buf = ec.write_positive_backward(0) + ec.write_positive_backward(LONG_MAX)
+    got, pos = ec.read_positive_backward(buf, len(buf))
+    assert got == LONG_MAX
+    assert ec.read_positive_backward(buf, pos)[0] == 0
+
+
+def _read_write_prefix(max_value, jump, prefix_len, prefix):
+    values = list(range(0, max_value + 1, jump))
+    buf = b"".join(ec.write_positive_with_prefix(v, prefix, prefix_len) for v in values)
+    pos = 0
+    for v in values:
+        got, p, npos = ec.read_positive_with_prefix(buf, pos, prefix_len)
+        assert (got, p) == (v, prefix)
+        # positiveWithPrefixLength = numVariableBlocks(bitLength(v) + prefixLen)
+        assert npos - pos == (max(v.bit_length(), 1) + prefix_len - 1) // 7 + 1
+        pos = npos
+    buf = ec.write_positive_with_prefix(0, prefix, prefix_len) + ec.write_positive_with_prefix(LONG_MAX, prefix,
+                                                                                               prefix_len)
+    v0, _, pos = ec.read_positive_with_prefix(buf, 0, prefix_len)
+    v1, _, _ = ec.read_positive_with_prefix(buf, pos, prefix_len)
+    assert (v0, v1) == (0, LONG_MAX)
+
+
+def test_pos_backward_write_small():
+    _read_write_backward(1000000, 7)  # reference: jump 1
+
+
+def test_pos_backward_write_big():
+    _read_write_backward(10000000000000, 1000000000)  # reference: jump 1e6
+
+
+def test_prefix_writes():
+    _read_write_prefix(1000000000000, 100000000, 3, 4)  # testPrefix1WriteBig (jump 1e6 in the reference)
+    _read_write_prefix(130, 1, 2, 1)                     # testPrefix2WriteTiny
+    _read_write_prefix(100000, 1, 2, 1)                  # testPrefix2WriteSmall
+    _read_write_prefix(100000, 1, 2, 0)                  # testPrefix3WriteSmall
+
+
+def test_byte_order_preserving_positive_backward():
+    rng = np.random.default_rng(3)
+    vals = sorted(set(int(x) for x in rng.integers(0, 1 << 62, 2000)) | {0, 1, 127, 128, LONG_MAX})
+    enc = [ec.write_positive_backward(v) for v in vals]
+    assert enc == sorted(enc)
+    for v, b in zip(vals, enc):
+        assert ec.read_positive_backward(b, len(b)) == (v, 0)
+
+
+def random_entries(n, seed=0):
+    """n encoded entries of every kind; returns (bytes, off, vpos, type_ids, type_mult, expected)."""
+    rng = np.random.default_rng(seed)
+    labels = [ec.schema_id(int(c), "user_edge") for c in rng.integers(1, 1 << 20, 12)]
+    mults = [ec.MULTI, ec.MULTI, ec.SIMPLE, ec.ONE2MANY, ec.MANY2ONE, ec.ONE2ONE] * 2
+    keys = [ec.schema_id(int(c), "user_key") for c in rng.integers(1, 1 << 20, 4)]
+    sys_label = ec.schema_id(3, "system_edge")
+    data, off, vpos, exp = bytearray(), [0], [], []
+    for i in range(n):
+        kind = rng.integers(0, 20)
+        if kind == 0:
+            t = keys[int(rng.integers(0, len(keys)))]
+            rel = int(rng.integers(0, 1 << 40))
+            e, vp = ec.encode_property(t, rel, bytes(rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8)))
+            exp.append((t, 2, -1, -1))
+        elif kind == 1:
+            e, vp = ec.encode_edge(sys_label, ec.OUT, 5, 6)
+            exp.append((sys_label, 3, -1, -1))
+        else:
+            li = int(rng.integers(0, len(labels)))
+            t, m = labels[li], mults[li]
+            d = int(rng.integers(0, 2))
+            other = int(rng.integers(0, 1 << int(rng.integers(1, 62))))
+            rel = int(rng.integers(0, 1 << int(rng.integers(1, 62))))
+            sk = bytes(rng.integers(0, 256, int(rng.integers(0, 4)), dtype=np.uint8)) if m == ec.MULTI else b""
+            val = bytes(rng.integers(0, 256, int(rng.integers(0, 8)), dtype=np.uint8))
+            e, vp = ec.encode_edge(t, d, other, rel, m, sk, val, invisible=bool(rng.integers(0, 4) == 0))
+            exp.append((t, d, other, rel))
+        data += e
+        off.append(len(data))
+        vpos.append(vp)
+    return (bytes(data), np.array(off, np.int64), np.array(vpos, np.int32), np.array(labels, np.int64),
+            np.array(mults, np.int8), np.array(exp, dtype=object))
+
+
+def check_decoded(decoded, exp):
+    t, d, o, r = decoded
+    assert np.array_equal(t, np.array([x[0] for x in exp], np.int64))
+    assert np.array_equal(d, np.array([x[1] for x in exp], np.int8))
+    assert np.array_equal(o, np.array([x[2] for x in exp], np.int64))
+    assert np.array_equal(r, np.array([x[3] for x in exp], np.int64))
+
+
+def test_oracle_decodes_every_entry_kind(oracle_lib):
+    data, off, vpos, tids, tmult, exp = random_entries(4000, seed=1)
+    check_decoded(oracle_lib.decode_edges(data, off, vpos, tids, tmult), exp)
+
+
+def test_unlisted_labels_decode_as_multi(oracle_lib):
+    t = ec.schema_id(77, "user_edge")
+    e, vp = ec.encode_edge(t, ec.IN, 123456789, 42)
+    got = oracle_lib.decode_edges(e, [0, len(e)], [vp])
+    check_decoded(got, [(t, 1, 123456789, 42)])

@@ -322,3 +322,35 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("slice_lds", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0)):
             _lib.tune_set(k, v)
+
+
+@pytest.mark.gpu
+def test_decode_edges_matches_oracle(ctx, oracle_lib):
+    """GPU edgestore decode (jg_decode_edges) == the C oracle == the values the restated writer
+    encoded, over every entry kind (tests/test_edgecodec.py random_entries)."""
+    from test_edgecodec import check_decoded, random_entries
+    data, off, vpos, tids, tmult, exp = random_entries(20000, seed=7)
+    got = ctx.decode_edges(data, off, vpos, tids, tmult)
+    check_decoded(got, exp)
+    ref = oracle_lib.decode_edges(data, off, vpos, tids, tmult)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_decode_edges_edge_cases(ctx):
+    """Empty input; a truncated varint is reported as malformed (dir -1) without reading past it;
+    out-of-range offsets are rejected before any launch."""
+    import janusgraph_amd as jg
+    from oracle import edgecodec as ec
+    t, d, o, r = ctx.decode_edges(b"", [0], [])
+    assert len(t) == len(d) == len(o) == len(r) == 0
+    lab = ec.schema_id(9, "user_edge")
+    good, vp = ec.encode_edge(lab, ec.OUT, 1 << 40, 17)
+    hdr = ec.write_relation_type(lab, True, ec.OUT)
+    bad = hdr + b"\x01\x02"  # backward varint with no first (stop-marked) byte
+    data = good + bad
+    t, d, o, r = ctx.decode_edges(data, [0, len(good), len(data)], [vp, len(bad)])
+    assert list(d) == [0, -1] and o[0] == 1 << 40 and r[0] == 17 and o[1] == -1
+    with pytest.raises(jg.JanusGpuError):
+        ctx.decode_edges(data, [0, len(data) + 5], [1])
