@@ -18,6 +18,9 @@
  *       VertexJobConverter.process (graphdb/olap/VertexJobConverter.java:122-151: ghost skip)
  *       and the canonical-id map (graphdb/olap/computer/FulgoraVertexMemory.java:74-77).
  *       Done ONCE per computer instead of once per superstep.
+ *   jg_graph_build_edgestore
+ *       the same, from the raw rows: the row decode of VertexJobConverter.process and
+ *       EdgeSerializer.parseRelation (graphdb/database/EdgeSerializer.java:86-122) on the GPU
  *   jg_pagerank (+ begin/step/end)
  *       executeVertexProgram superstep loop (FulgoraGraphComputer.java:210-230) running
  *       janusgraph-backend-testutils/.../olap/PageRankVertexProgram.java:89-110, with the gather of
@@ -129,6 +132,25 @@ int jg_ctx_set_profiling(jg_ctx* ctx, int enable);
 int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n,
                    const int64_t* src, const int64_t* dst, const int32_t* weight, int64_t m,
                    uint32_t flags, jg_graph** out);
+
+/* The same snapshot straight from the edgestore rows the scan returns, decoded on the GPU
+ * (replaces VertexJobConverter.process + EdgeSerializer.parseRelation per row and entry:
+ * graphdb/olap/VertexJobConverter.java:122-151,169-181; graphdb/database/EdgeSerializer.java:86-122;
+ * graphdb/idmanagement/IDManager.java:496-506).  Row r has key row_keys[r] (the 8-byte big-endian
+ * StaticBuffer as an unsigned value) and entries [row_entry_off[r], row_entry_off[r+1]); entry e is
+ * bytes[entry_off[e] .. entry_off[e+1]) with its value at value_pos[e] (as jg_decode_edges; the
+ * type table gives edge-label multiplicities).  Rows with an odd key (schema / invisible vertices)
+ * are filtered; a row whose first entry is not the VertexExists property is a ghost; the kept rows
+ * are V (in row order, ids -> vid_out[nrows], count -> *num_vertices_out, both nullable) and their
+ * OUT entries of visible user edges are the edges (ghost endpoints dropped as in jg_graph_build).
+ * Unit weights.  Partitioned (vertex-cut) rows: JG_ERR_UNSUPPORTED; a malformed entry on a kept row
+ * or a key with no user vertex type: JG_ERR_ARG.  Stats: build_ms (whole snapshot), kernel_ms_total
+ * (the decode kernels). */
+int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
+                             const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
+                             int64_t nentries, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
+                             int32_t partition_bits, uint32_t flags, int64_t* vid_out, int64_t* num_vertices_out,
+                             jg_graph** out);
 
 /* Synthetic Graph500 Kronecker (RMAT a,b,c,d = .57,.19,.19,.05) graph generated on the device(s):
  * n = 2^scale vertices with ids 0..n-1, m = edgefactor * n directed edges, seeded and

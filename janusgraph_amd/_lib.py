@@ -30,7 +30,8 @@ UNIQUE_ID_BYTES = 128
 # every function the header declares (checked by tests/test_abi.py against include/janusgpu.h)
 EXPORTS = [
     "jg_abi_version", "jg_last_error", "jg_ctx_create", "jg_comm_unique_id", "jg_ctx_create_rank",
-    "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_rmat",
+    "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_edgestore",
+    "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set",
@@ -95,6 +96,8 @@ def load():
         "jg_ctx_last_stats": ([_P, ctypes.POINTER(Stats)], ctypes.c_int),
         "jg_ctx_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
         "jg_graph_build": ([_P, _P, _i64, _P, _P, _P, _i64, ctypes.c_uint32, _PP], ctypes.c_int),
+        "jg_graph_build_edgestore": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i64, _P, _P, _i32, _i32, ctypes.c_uint32,
+                                      _P, _P, _PP], ctypes.c_int),
         "jg_graph_build_rmat": ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, _PP],
                                 ctypes.c_int),
         "jg_graph_info_get": ([_P, ctypes.POINTER(GraphInfo)], ctypes.c_int),
@@ -218,6 +221,30 @@ class Context:
         check(load().jg_graph_build(self._h, _ptr(vid), len(vid), _ptr(src), _ptr(dst), _ptr(w), len(src),
                                     flags, ctypes.byref(h)))
         return Graph(self, h, len(vid))
+
+    def build_edgestore(self, row_keys, row_entry_off, data, entry_off, value_pos, type_ids=(), type_mult=(),
+                        partition_bits=5, flags=ADJ_IN | ADJ_OUT | ADJ_BOTH):
+        """jg_graph_build_edgestore: the CSR snapshot from raw edgestore rows, decoded on the GPU.
+        Returns (graph, vid): vid = ids of the non-ghost vertex rows, the order outputs are indexed in."""
+        keys = np.ascontiguousarray(row_keys, np.uint64)
+        roff = np.ascontiguousarray(row_entry_off, np.int64)
+        data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                    np.uint8)
+        off = np.ascontiguousarray(entry_off, np.int64)
+        vpos = np.ascontiguousarray(value_pos, np.int32)
+        if len(roff) != len(keys) + 1 or len(off) != len(vpos) + 1:
+            raise ValueError("row_entry_off needs nrows + 1 offsets, entry_off nentries + 1")
+        tid = np.ascontiguousarray(type_ids, np.int64)
+        tm = np.ascontiguousarray(type_mult, np.int8)
+        if len(tid) != len(tm):
+            raise ValueError("type_ids and type_mult differ in length")
+        vid = np.empty(max(len(keys), 1), np.int64)
+        nv = ctypes.c_int64(0)
+        h = ctypes.c_void_p()
+        check(load().jg_graph_build_edgestore(self._h, _ptr(keys), len(keys), _ptr(roff), _ptr(data), len(data),
+                                              _ptr(off), _ptr(vpos), len(vpos), _ptr(tid), _ptr(tm), len(tid),
+                                              partition_bits, flags, _ptr(vid), ctypes.byref(nv), ctypes.byref(h)))
+        return Graph(self, h, nv.value), vid[:nv.value].copy()
 
     def build_rmat(self, scale, edgefactor=16, seed=1, flags=ADJ_IN) -> "Graph":
         h = ctypes.c_void_p()

@@ -171,6 +171,22 @@ void prof_collect(Ctx& c, Graph& g) {
     c.last.kernel_launches += launches;
 }
 
+// Host copies of the vertex ids: outputs are indexed like vid[], lookups go through the sorted copy.
+static void set_vertex_ids(Graph& g, const int64_t* vid, int64_t n) {
+    g.vid.assign(vid, vid + n);
+    std::vector<std::pair<int64_t, int64_t>> t(n);
+    for (int64_t i = 0; i < n; ++i) t[i] = {vid[i], i};
+    std::sort(t.begin(), t.end());
+    for (int64_t i = 1; i < n; ++i)
+        if (t[i].first == t[i - 1].first) fail(JG_ERR_ARG, "duplicate vertex id in vid[]");
+    g.sorted_vid.resize(n);
+    g.sorted_dense.resize(n);
+    for (int64_t i = 0; i < n; ++i) {
+        g.sorted_vid[i] = t[i].first;
+        g.sorted_dense[i] = t[i].second;
+    }
+}
+
 static void make_shards(Ctx& c, Graph& g) {
     g.P = c.total_shards();
     for (size_t i = 0; i < c.devices.size(); ++i) {
@@ -394,20 +410,7 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
     g.flags = flags;
     g.has_weights = weight != nullptr;
     jg::make_shards(c, g);
-    g.vid.assign(vid, vid + n);
-    {
-        std::vector<std::pair<int64_t, int64_t>> t(n);
-        for (int64_t i = 0; i < n; ++i) t[i] = {vid[i], i};
-        std::sort(t.begin(), t.end());
-        for (int64_t i = 1; i < n; ++i)
-            if (t[i].first == t[i - 1].first) jg::fail(JG_ERR_ARG, "duplicate vertex id in vid[]");
-        g.sorted_vid.resize(n);
-        g.sorted_dense.resize(n);
-        for (int64_t i = 0; i < n; ++i) {
-            g.sorted_vid[i] = t[i].first;
-            g.sorted_dense[i] = t[i].second;
-        }
-    }
+    jg::set_vertex_ids(g, vid, n);
     hipEvent_t t0, t1;
     {
         jg::DeviceGuard dg(g.shards[0]->device);
@@ -452,6 +455,83 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
         (void)hipEventDestroy(t0);
         (void)hipEventDestroy(t1);
     }
+    *out = gh.release();
+    JG_GUARD_END
+}
+
+int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
+                             const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
+                             int64_t nentries, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
+                             int32_t partition_bits, uint32_t flags, int64_t* vid_out, int64_t* num_vertices_out,
+                             jg_graph** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx && out, "null argument");
+    JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
+    const jg::EdgestoreRows r{row_keys, nrows,     row_entry_off, bytes,    nbytes,        entry_off,
+                              value_pos, nentries, type_ids,      type_mult, ntypes,       partition_bits};
+    jg::edgestore_check(r);
+    *out = nullptr;
+    jg::Ctx& c = ctx->impl;
+    auto gh = std::make_unique<jg_graph>();
+    jg::Graph& g = gh->impl;
+    g.ctx = &c;
+    g.flags = flags;
+    g.has_weights = false;
+    jg::make_shards(c, g);
+    hipEvent_t t0, t1;
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
+    }
+    std::vector<jg::DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size());
+    jg::DenseEdges e;
+    float decode_ms = 0;
+    for (size_t i = 0; i < g.shards.size(); ++i) {  // every shard holds the whole edge list (as jg_graph_build)
+        jg::Shard& sh = *g.shards[i];
+        jg::DeviceGuard dg(sh.device);
+        jg::DevBuf<int64_t> dvid, dsrc, ddst;
+        int64_t n = 0, m = 0;
+        float ms = 0;
+        jg::edgestore_snapshot(r, sh.stream, dvid, n, dsrc, ddst, m, &ms);
+        if (i == 0) {
+            JG_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 vertices");
+            JG_ARG(m < (int64_t)UINT32_MAX, "more than 2^32-1 edges");
+            std::vector<int64_t> hv((size_t)n);
+            if (n) jg::copy_d2h(hv.data(), dvid.get(), (size_t)n * sizeof(int64_t), sh.stream);
+            g.n = n;
+            jg::set_vertex_ids(g, hv.data(), n);
+            e.m = m;
+            decode_ms = ms;
+        }
+        ds[i].alloc(std::max<int64_t>(m, 1));
+        dd[i].alloc(std::max<int64_t>(m, 1));
+        jg::remap_ids_device(dvid.get(), n, dsrc.get(), ddst.get(), m, ds[i].get(), dd[i].get(), sh.stream);
+        e.src.push_back(ds[i].get());
+        e.dst.push_back(dd[i].get());
+        e.weight.push_back(nullptr);
+    }
+    jg::build_graph_from_dense(g, e);
+    {
+        jg::DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
+        JG_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        c.last = jg_stats{};
+        c.last.build_ms = ms;
+        c.last.kernel_ms_total = decode_ms;  // the two decode kernels (rows, entries)
+        c.last.kernel_launches = 1;
+        // decode kernels: entry bytes + off/vpos/take (13 B) per entry, src/dst (16 B) per kept edge,
+        // key/row_off/row_vid/keep (25 B) per row
+        c.last.algorithmic_bytes =
+            (double)nbytes + 13.0 * (double)nentries + 16.0 * (double)e.m + 25.0 * (double)nrows;
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
+    if (vid_out && g.n) std::copy(g.vid.begin(), g.vid.end(), vid_out);
+    if (num_vertices_out) *num_vertices_out = g.n;
     *out = gh.release();
     JG_GUARD_END
 }

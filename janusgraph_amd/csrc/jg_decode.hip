@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "jg_internal.h"
+#include "jg_prim.h"
 
 namespace jg {
 
@@ -56,126 +57,292 @@ __device__ __forceinline__ int64_t read_unsigned_backward(const uint8_t* __restr
     }
 }
 
-struct DecodeArgs {
+// The entry stream: entry e is bytes[off[e] .. off[e+1]), its value at vpos[e]; edge-label
+// multiplicities from a sorted (type id, code) table.
+struct EntryView {
     const uint8_t* bytes;
     const int64_t* off;
     const int32_t* vpos;
-    int64_t n;
     const int64_t* type_ids;  // sorted
     const int8_t* type_mult;
     int32_t ntypes;
+};
+
+struct Decoded {
+    int64_t type_id, other, rel;
+    int8_t dir;    // 0 OUT edge, 1 IN edge, 2 property, 3 system relation, -1 malformed
+    bool visible;  // a user relation (header prefix >> 1 == 1), not system, not invisible
+};
+
+// EdgeSerializer.parseRelation (EdgeSerializer.java:86-122) of one entry, header and ids only.
+// b = the entry's bytes (global memory or the block's LDS stage), len its length, vpos its value
+// position.
+__device__ __forceinline__ Decoded decode_entry(const EntryView& a, const uint8_t* __restrict__ b, int64_t len,
+                                                int64_t vpos) {
+    bool bad = false;
+    int64_t pos = 0;
+    const int first = b[pos++];
+    const int prefix = first >> 5;
+    int64_t value = first & 0x0F;
+    if ((first >> 4) & 1) {
+        const int64_t p0 = pos;
+        const int64_t rem = read_unsigned(b, pos, len, bad);
+        value = (value << (7 * (pos - p0))) + rem;
+    }
+    const bool is_edge = prefix & 1, system = (prefix >> 1) == 0;
+    const int dirbit = (int)(value & 1);
+    const int64_t suffix = is_edge ? (system ? 53 : 21) : (system ? 37 : 5);
+    Decoded d;
+    d.type_id = ((value >> 1) << 6) | suffix;
+    d.other = d.rel = -1;
+    d.dir = (int8_t)(is_edge ? 3 : 2);
+    d.visible = (prefix >> 1) == 1;
+    if (is_edge && !system) {
+        d.dir = (int8_t)dirbit;
+        int mult = 0;
+        int lo = 0, hi = a.ntypes;  // lower bound of type_id
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (a.type_ids[mid] < d.type_id) lo = mid + 1; else hi = mid;
+        }
+        if (lo < a.ntypes && a.type_ids[lo] == d.type_id) mult = a.type_mult[lo];
+        const bool unique = dirbit ? (mult == 2 || mult == 4) : (mult == 3 || mult == 4);
+        int64_t p = vpos;
+        if (mult == 0) {
+            d.rel = read_unsigned_backward(b, p, bad);
+            d.other = read_unsigned_backward(b, p, bad);
+        } else if (unique) {
+            d.other = read_unsigned(b, p, len, bad);
+            d.rel = read_unsigned(b, p, len, bad);
+        } else {
+            d.other = read_unsigned_backward(b, p, bad);
+            p = vpos;
+            d.rel = read_unsigned(b, p, len, bad);
+        }
+    }
+    if (bad) {
+        d.dir = -1;
+        d.other = d.rel = -1;
+    }
+    return d;
+}
+
+struct DecodeOut {
     int64_t* type_out;
     int8_t* dir_out;
     int64_t* other_out;
     int64_t* rel_out;
 };
 
-__global__ __launch_bounds__(kBlock) void decode_edges_kernel(DecodeArgs a) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += (int64_t)gridDim.x * blockDim.x) {
-        const uint8_t* __restrict__ b = a.bytes + a.off[e];
-        const int64_t len = a.off[e + 1] - a.off[e];
-        bool bad = false;
-        int64_t pos = 0;
-        const int first = b[pos++];
-        const int prefix = first >> 5;
-        int64_t value = first & 0x0F;
-        if ((first >> 4) & 1) {
-            const int64_t p0 = pos;
-            const int64_t rem = read_unsigned(b, pos, len, bad);
-            value = (value << (7 * (pos - p0))) + rem;
+// Block-staged entries: a block decodes kBlock consecutive entries, whose bytes are one contiguous
+// range; it is streamed into LDS with coalesced dword loads, then every thread parses its entry
+// there (the varint walks are dependent byte loads: from HBM they serialise on memory latency).
+// A block whose range exceeds the stage (entries with long property values) reads global memory.
+// The byte array is allocated with kBytePad slack, so the dword loads may run past its end.
+constexpr int kStageWords = 4096;  // 16 KB of LDS per block
+constexpr int64_t kBytePad = 16;
+
+struct Stage {
+    const uint8_t* base;  // where entry bytes are read from
+    int64_t origin;       // byte offset of base[0] in the array
+};
+
+__device__ __forceinline__ Stage stage_entries(const EntryView& a, int64_t e0, int64_t e_end, uint32_t* lds) {
+    const int64_t b0 = a.off[e0] & ~(int64_t)3, b1 = a.off[e_end];
+    const int64_t words = (b1 - b0 + 3) >> 2;
+    if (words > kStageWords) return Stage{a.bytes, 0};
+    const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(a.bytes + b0);
+    for (int64_t w = threadIdx.x; w < words; w += kBlock) lds[w] = __builtin_nontemporal_load(src + w);
+    __syncthreads();
+    return Stage{reinterpret_cast<const uint8_t*>(lds), b0};
+}
+
+__global__ __launch_bounds__(kBlock) void decode_edges_kernel(EntryView a, int64_t n, DecodeOut o) {
+    __shared__ uint32_t lds[kStageWords];
+    for (int64_t e0 = (int64_t)blockIdx.x * kBlock; e0 < n; e0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t e_end = e0 + kBlock < n ? e0 + kBlock : n;
+        const Stage st = stage_entries(a, e0, e_end, lds);
+        const int64_t e = e0 + threadIdx.x;
+        if (e < e_end) {
+            const int64_t o0 = a.off[e];
+            const Decoded d = decode_entry(a, st.base + (o0 - st.origin), a.off[e + 1] - o0, a.vpos[e]);
+            if (o.type_out) o.type_out[e] = d.type_id;
+            if (o.dir_out) o.dir_out[e] = d.dir;
+            if (o.other_out) o.other_out[e] = d.other;
+            if (o.rel_out) o.rel_out[e] = d.rel;
         }
-        const bool is_edge = prefix & 1, system = (prefix >> 1) == 0;
-        const int dirbit = (int)(value & 1);
-        const int64_t suffix = is_edge ? (system ? 53 : 21) : (system ? 37 : 5);
-        const int64_t type_id = ((value >> 1) << 6) | suffix;
-        int64_t other = -1, rel = -1;
-        int8_t dir = (int8_t)(is_edge ? 3 : 2);
-        if (is_edge && !system) {
-            dir = (int8_t)dirbit;
-            int mult = 0;
-            int lo = 0, hi = a.ntypes;  // lower bound of type_id
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (a.type_ids[mid] < type_id) lo = mid + 1; else hi = mid;
-            }
-            if (lo < a.ntypes && a.type_ids[lo] == type_id) mult = a.type_mult[lo];
-            const bool unique = dirbit ? (mult == 2 || mult == 4) : (mult == 3 || mult == 4);
-            int64_t p = a.vpos[e];
-            if (mult == 0) {
-                rel = read_unsigned_backward(b, p, bad);
-                other = read_unsigned_backward(b, p, bad);
-            } else if (unique) {
-                other = read_unsigned(b, p, len, bad);
-                rel = read_unsigned(b, p, len, bad);
-            } else {
-                other = read_unsigned_backward(b, p, bad);
-                p = a.vpos[e];
-                rel = read_unsigned(b, p, len, bad);
-            }
-        }
-        if (bad) {
-            dir = -1;
-            other = rel = -1;
-        }
-        if (a.type_out) a.type_out[e] = type_id;
-        if (a.dir_out) a.dir_out[e] = dir;
-        if (a.other_out) a.other_out[e] = other;
-        if (a.rel_out) a.rel_out[e] = rel;
+        __syncthreads();  // the stage is reused by the next block-iteration
     }
+}
+
+// ---------------- CSR snapshot straight from edgestore rows ----------------
+// IDManager.getKeyID (idmanagement/IDManager.java:496-506) of a user row key: partition in the top
+// pbits, count above the 3-bit type suffix; id = (count << pbits | partition) << 3 | suffix.
+// Returns -1 for an odd key (schema / invisible row: VertexJobConverter.getKeyFilter, :174-177
+// drops it) and -2 for a suffix that is no user vertex type (getUserVertexIDType throws).
+__device__ __forceinline__ int64_t key_to_vertex_id(uint64_t key, int pbits) {
+    if (key & 1) return -1;
+    const uint64_t suffix = key & 7;
+    if (suffix == 6) return -2;
+    const int poff = 64 - pbits;
+    const uint64_t partition = poff < 64 ? key >> poff : 0;
+    const uint64_t count = (key >> 3) & ((1ull << (poff - 3)) - 1ull);
+    return (int64_t)((((count << pbits) + partition) << 3) | suffix);
+}
+
+constexpr int64_t kVertexExistsId = (1 << 6) | 37;  // BaseKey.VertexExists: SystemPropertyKey count 1
+
+// Error bits of the snapshot (any set bit fails the build before the CSR is cut)
+enum : int32_t { kErrBadKey = 1, kErrPartitioned = 2, kErrMalformed = 4 };
+
+// One thread per row: vertex id, key filter, ghost rule (VertexJobConverter.process / isGhostVertex,
+// olap/VertexJobConverter.java:122-151: the row's first entry must be the VertexExists property;
+// system properties sort first, so it is entry 0 of the row when present).
+__global__ __launch_bounds__(kBlock) void edgestore_rows_kernel(EntryView a, const uint64_t* __restrict__ keys,
+                                                                 const int64_t* __restrict__ row_off, int64_t nrows,
+                                                                 int pbits, uint8_t* __restrict__ keep,
+                                                                 int64_t* __restrict__ row_vid, int32_t* __restrict__ err) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t vid = key_to_vertex_id(keys[r], pbits);
+        uint8_t k = 0;
+        if (vid == -2) {
+            atomicOr(err, kErrBadKey);
+        } else if (vid >= 0) {
+            if ((vid & 7) == 2) {  // vertex-cut representatives need canonical-id aggregation
+                atomicOr(err, kErrPartitioned);
+            } else if (row_off[r + 1] > row_off[r]) {
+                const int64_t e = row_off[r];
+                const Decoded d = decode_entry(a, a.bytes + a.off[e], a.off[e + 1] - a.off[e], a.vpos[e]);
+                if (d.dir < 0) atomicOr(err, kErrMalformed);
+                k = (d.dir == 2 && d.type_id == kVertexExistsId) ? 1 : 0;
+            }
+        }
+        keep[r] = k;
+        row_vid[r] = vid;
+    }
+}
+
+// One thread per entry: the row (binary search of row_off), then the entry's OUT edge.  Every edge
+// is stored twice, OUT on its source row and IN on its target row (a self-loop: both on one row,
+// StandardJanusGraph.java:617-640), so the OUT entries of the kept rows are the edge list exactly
+// once.  Visible user edges only (bothE() of a PreloadedVertex sees no system or invisible type).
+__device__ __forceinline__ int64_t row_of_entry(const int64_t* __restrict__ row_off, int64_t lo, int64_t hi, int64_t e) {
+    while (hi - lo > 1) {  // last row r in [lo, hi) with row_off[r] <= e
+        const int64_t mid = (lo + hi) >> 1;
+        if (row_off[mid] <= e) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void edgestore_edges_kernel(EntryView a, const int64_t* __restrict__ row_off,
+                                                                  int64_t nrows, int64_t nent,
+                                                                  const uint8_t* __restrict__ keep,
+                                                                  const int64_t* __restrict__ row_vid,
+                                                                  uint8_t* __restrict__ take, int64_t* __restrict__ src,
+                                                                  int64_t* __restrict__ dst, int32_t* __restrict__ err) {
+    __shared__ uint32_t lds[kStageWords];
+    __shared__ int64_t span[2];
+    for (int64_t e0 = (int64_t)blockIdx.x * kBlock; e0 < nent; e0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t e_end = e0 + kBlock < nent ? e0 + kBlock : nent;
+        // the rows the block's entries fall in: two searches per block, then short ones per thread
+        if (threadIdx.x == 0) span[0] = row_of_entry(row_off, 0, nrows, e0);
+        if (threadIdx.x == kBlock - 1) span[1] = row_of_entry(row_off, 0, nrows, e_end - 1);
+        const Stage st = stage_entries(a, e0, e_end, lds);  // synchronises the block
+        __syncthreads();
+        const int64_t e = e0 + threadIdx.x;
+        if (e < e_end) {
+            const int64_t r = row_of_entry(row_off, span[0], span[1] + 1, e);
+            uint8_t t = 0;
+            if (keep[r]) {
+                const int64_t o0 = a.off[e];
+                const Decoded d = decode_entry(a, st.base + (o0 - st.origin), a.off[e + 1] - o0, a.vpos[e]);
+                if (d.dir < 0) atomicOr(err, kErrMalformed);
+                if (d.dir == 0 && d.visible) {
+                    t = 1;
+                    src[e] = row_vid[r];
+                    dst[e] = d.other;
+                }
+            }
+            take[e] = t;
+        }
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ void gather_kernel(const T* __restrict__ in, const int64_t* __restrict__ idx, int64_t n, T* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[idx[i]];
 }
 
 }  // namespace
 
-void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* off, const int32_t* vpos, int64_t n,
-                  const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int64_t* type_out,
-                  int8_t* dir_out, int64_t* other_out, int64_t* rel_out) {
-    if (n < 0 || nbytes < 0 || ntypes < 0) fail(JG_ERR_ARG, "negative size");
+// Every entry inside the byte array, its value position inside the entry (checked before any launch).
+static void check_entries(const uint8_t* bytes, int64_t nbytes, const int64_t* off, const int32_t* vpos, int64_t n) {
+    if (n < 0 || nbytes < 0) fail(JG_ERR_ARG, "negative size");
     if (n > 0 && (!bytes || !off || !vpos)) fail(JG_ERR_ARG, "null entry arrays");
-    if (ntypes > 0 && (!type_ids || !type_mult)) fail(JG_ERR_ARG, "null type table");
-    // every entry must lie inside the byte array, with its value position inside the entry
     for (int64_t e = 0; e < n; ++e) {
         const int64_t len = off[e + 1] - off[e];
         if (off[e] < 0 || len < 1 || off[e + 1] > nbytes || vpos[e] < 1 || vpos[e] > len)
             fail(JG_ERR_ARG, "entry " + std::to_string(e) + " out of range");
     }
-    std::vector<std::pair<int64_t, int8_t>> tt((size_t)ntypes);
-    for (int32_t t = 0; t < ntypes; ++t) {
-        if (type_mult[t] < 0 || type_mult[t] > 4) fail(JG_ERR_ARG, "multiplicity code must be in [0, 4]");
-        tt[(size_t)t] = {type_ids[t], type_mult[t]};
+}
+
+// The multiplicity table sorted by type id, on the device.
+struct TypeTable {
+    DevBuf<int64_t> ids;
+    DevBuf<int8_t> mult;
+    int32_t n = 0;
+    TypeTable(const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, hipStream_t s)
+        : ids(std::max<int32_t>(ntypes, 1)), mult(std::max<int32_t>(ntypes, 1)), n(ntypes) {
+        if (ntypes < 0) fail(JG_ERR_ARG, "negative size");
+        if (ntypes > 0 && (!type_ids || !type_mult)) fail(JG_ERR_ARG, "null type table");
+        std::vector<std::pair<int64_t, int8_t>> tt((size_t)ntypes);
+        for (int32_t t = 0; t < ntypes; ++t) {
+            if (type_mult[t] < 0 || type_mult[t] > 4) fail(JG_ERR_ARG, "multiplicity code must be in [0, 4]");
+            tt[(size_t)t] = {type_ids[t], type_mult[t]};
+        }
+        std::sort(tt.begin(), tt.end());
+        std::vector<int64_t> tid(tt.size());
+        std::vector<int8_t> tm(tt.size());
+        for (size_t t = 0; t < tt.size(); ++t) {
+            tid[t] = tt[t].first;
+            tm[t] = tt[t].second;
+        }
+        if (ntypes) {
+            copy_h2d(ids.get(), tid.data(), tid.size() * sizeof(int64_t), s);
+            copy_h2d(mult.get(), tm.data(), tm.size(), s);
+        }
     }
-    std::sort(tt.begin(), tt.end());
-    std::vector<int64_t> tid(tt.size());
-    std::vector<int8_t> tm(tt.size());
-    for (size_t t = 0; t < tt.size(); ++t) {
-        tid[t] = tt[t].first;
-        tm[t] = tt[t].second;
-    }
+};
+
+void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* off, const int32_t* vpos, int64_t n,
+                  const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int64_t* type_out,
+                  int8_t* dir_out, int64_t* other_out, int64_t* rel_out) {
+    check_entries(bytes, nbytes, off, vpos, n);
     const int dev = c.devices.empty() ? 0 : c.devices[0];
     DeviceGuard dg(dev);
     hipStream_t s = c.streams.empty() ? nullptr : c.streams[0];
-    DevBuf<uint8_t> d_bytes(std::max<int64_t>(nbytes, 1));
+    TypeTable tt(type_ids, type_mult, ntypes, s);
+    DevBuf<uint8_t> d_bytes(nbytes + kBytePad);
     DevBuf<int64_t> d_off(n + 1), d_type(std::max<int64_t>(n, 1)), d_other(std::max<int64_t>(n, 1)),
-        d_rel(std::max<int64_t>(n, 1)), d_tid(std::max<int32_t>(ntypes, 1));
+        d_rel(std::max<int64_t>(n, 1));
     DevBuf<int32_t> d_vpos(std::max<int64_t>(n, 1));
-    DevBuf<int8_t> d_dir(std::max<int64_t>(n, 1)), d_tm(std::max<int32_t>(ntypes, 1));
+    DevBuf<int8_t> d_dir(std::max<int64_t>(n, 1));
     if (nbytes) copy_h2d(d_bytes.get(), bytes, (size_t)nbytes, s);
     if (n) {
         copy_h2d(d_off.get(), off, (size_t)(n + 1) * sizeof(int64_t), s);
         copy_h2d(d_vpos.get(), vpos, (size_t)n * sizeof(int32_t), s);
     }
-    if (ntypes) {
-        copy_h2d(d_tid.get(), tid.data(), tid.size() * sizeof(int64_t), s);
-        copy_h2d(d_tm.get(), tm.data(), tm.size(), s);
-    }
-    DecodeArgs a{d_bytes.get(), d_off.get(), d_vpos.get(), n, d_tid.get(), d_tm.get(), ntypes,
-                 type_out ? d_type.get() : nullptr, dir_out ? d_dir.get() : nullptr,
-                 other_out ? d_other.get() : nullptr, rel_out ? d_rel.get() : nullptr};
+    const EntryView a{d_bytes.get(), d_off.get(), d_vpos.get(), tt.ids.get(), tt.mult.get(), ntypes};
+    const DecodeOut o{type_out ? d_type.get() : nullptr, dir_out ? d_dir.get() : nullptr,
+                      other_out ? d_other.get() : nullptr, rel_out ? d_rel.get() : nullptr};
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
     JG_HIP(hipEventRecord(t0, s));
     if (n > 0) {
-        decode_edges_kernel<<<grid_for(n, kBlock, 256 * 64), kBlock, 0, s>>>(a);
+        decode_edges_kernel<<<grid_for(n, kBlock, 256 * 64), kBlock, 0, s>>>(a, n, o);
         JG_LAUNCH_CHECK();
     }
     JG_HIP(hipEventRecord(t1, s));
@@ -195,6 +362,81 @@ void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* o
     if (n && dir_out) copy_d2h(dir_out, d_dir.get(), (size_t)n, s);
     if (n && other_out) copy_d2h(other_out, d_other.get(), (size_t)n * sizeof(int64_t), s);
     if (n && rel_out) copy_d2h(rel_out, d_rel.get(), (size_t)n * sizeof(int64_t), s);
+}
+
+void edgestore_check(const EdgestoreRows& r) {
+    if (r.nrows < 0 || r.nentries < 0) fail(JG_ERR_ARG, "negative size");
+    if (r.pbits < 0 || r.pbits > 16) fail(JG_ERR_ARG, "partition bits must be in [0, 16]");
+    if (r.nrows > 0 && (!r.keys || !r.row_off)) fail(JG_ERR_ARG, "null row arrays");
+    if (r.nrows == 0 ? r.nentries != 0 : (r.row_off[0] != 0 || r.row_off[r.nrows] != r.nentries))
+        fail(JG_ERR_ARG, "row offsets must run from 0 to the entry count");
+    for (int64_t i = 0; i < r.nrows; ++i)
+        if (r.row_off[i + 1] < r.row_off[i]) fail(JG_ERR_ARG, "row offsets must be non-decreasing");
+    check_entries(r.bytes, r.nbytes, r.entry_off, r.vpos, r.nentries);
+}
+
+void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
+                        DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms) {
+    TypeTable tt(r.type_ids, r.type_mult, r.ntypes, s);
+    const int64_t R = r.nrows, E = r.nentries;
+    DevBuf<uint8_t> d_bytes(r.nbytes + kBytePad), keep(std::max<int64_t>(R, 1)),
+        take(std::max<int64_t>(E, 1));
+    DevBuf<int64_t> d_off(E + 1), d_roff(R + 1), row_vid(std::max<int64_t>(R, 1)), esrc(std::max<int64_t>(E, 1)),
+        edst(std::max<int64_t>(E, 1)), idx(std::max<int64_t>(std::max(R, E), 1));
+    DevBuf<uint64_t> d_keys(std::max<int64_t>(R, 1));
+    DevBuf<int32_t> d_vpos(std::max<int64_t>(E, 1)), err(1);
+    if (r.nbytes) copy_h2d(d_bytes.get(), r.bytes, (size_t)r.nbytes, s);
+    copy_h2d(d_off.get(), r.entry_off, (size_t)(E + 1) * sizeof(int64_t), s);
+    if (E) copy_h2d(d_vpos.get(), r.vpos, (size_t)E * sizeof(int32_t), s);
+    if (R) {
+        copy_h2d(d_keys.get(), r.keys, (size_t)R * sizeof(uint64_t), s);
+        copy_h2d(d_roff.get(), r.row_off, (size_t)(R + 1) * sizeof(int64_t), s);
+    }
+    JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
+    const EntryView a{d_bytes.get(), d_off.get(), d_vpos.get(), tt.ids.get(), tt.mult.get(), tt.n};
+    hipEvent_t t0, t1;
+    JG_HIP(hipEventCreate(&t0));
+    JG_HIP(hipEventCreate(&t1));
+    JG_HIP(hipEventRecord(t0, s));
+    if (R) {
+        edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, d_keys.get(), d_roff.get(), R, r.pbits, keep.get(),
+                                                            row_vid.get(), err.get());
+        JG_LAUNCH_CHECK();
+    }
+    if (E) {
+        edgestore_edges_kernel<<<grid_for(E, kBlock, 256 * 64), kBlock, 0, s>>>(
+            a, d_roff.get(), R, E, keep.get(), row_vid.get(), take.get(), esrc.get(), edst.get(), err.get());
+        JG_LAUNCH_CHECK();
+    }
+    JG_HIP(hipEventRecord(t1, s));
+    int32_t herr = 0;
+    JG_HIP(hipMemcpyAsync(&herr, err.get(), sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+    float ms = 0;
+    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+    JG_HIP(hipEventDestroy(t0));
+    JG_HIP(hipEventDestroy(t1));
+    if (kernel_ms) *kernel_ms = ms;
+    if (herr & kErrBadKey) fail(JG_ERR_ARG, "row key with an unrecognized vertex id type");
+    if (herr & kErrPartitioned)
+        fail(JG_ERR_UNSUPPORTED, "partitioned (vertex-cut) vertex rows: build from canonical ids with jg_graph_build");
+    if (herr & kErrMalformed) fail(JG_ERR_ARG, "malformed edgestore entry on a vertex row");
+    n = prim::compact_indices(keep.get(), R, idx.get(), s);
+    vid.alloc(std::max<int64_t>(n, 1));
+    if (n) {
+        gather_kernel<int64_t><<<grid_for(n), kBlock, 0, s>>>(row_vid.get(), idx.get(), n, vid.get());
+        JG_LAUNCH_CHECK();
+    }
+    m = prim::compact_indices(take.get(), E, idx.get(), s);
+    src.alloc(std::max<int64_t>(m, 1));
+    dst.alloc(std::max<int64_t>(m, 1));
+    if (m) {
+        gather_kernel<int64_t><<<grid_for(m), kBlock, 0, s>>>(esrc.get(), idx.get(), m, src.get());
+        JG_LAUNCH_CHECK();
+        gather_kernel<int64_t><<<grid_for(m), kBlock, 0, s>>>(edst.get(), idx.get(), m, dst.get());
+        JG_LAUNCH_CHECK();
+    }
+    JG_HIP(hipStreamSynchronize(s));
 }
 
 }  // namespace jg

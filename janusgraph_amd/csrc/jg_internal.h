@@ -298,6 +298,25 @@ void check_halo_counts(Graph& g, uint32_t adj);
 void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* off, const int32_t* vpos, int64_t n,
                   const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int64_t* type_out,
                   int8_t* dir_out, int64_t* other_out, int64_t* rel_out);
+// The scan's rows as the edgestore holds them (jg_graph_build_edgestore).
+struct EdgestoreRows {
+    const uint64_t* keys;      // nrows row keys (the 8-byte big-endian key as an unsigned value)
+    int64_t nrows;
+    const int64_t* row_off;    // nrows + 1: entries of row r are [row_off[r], row_off[r+1])
+    const uint8_t* bytes;
+    int64_t nbytes;
+    const int64_t* entry_off;  // nentries + 1
+    const int32_t* vpos;       // nentries
+    int64_t nentries;
+    const int64_t* type_ids;
+    const int8_t* type_mult;
+    int32_t ntypes;
+    int pbits;                 // cluster.max-partitions = 2^pbits
+};
+void edgestore_check(const EdgestoreRows& r);
+// On the current device and stream: vid = ids of the kept rows (row order), src/dst = their OUT edges.
+void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
+                        DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms);
 
 // ---- programs ----
 void pagerank_begin(Graph& g, double damping, int64_t vertex_count);

@@ -178,3 +178,57 @@ def decode_edges(data, off, vpos, type_ids=(), type_mult=()):
     tm = np.ascontiguousarray(type_mult, np.int8) if len(type_mult) else np.zeros(1, np.int8)
     lib().jo_decode_edges(data if len(data) else np.zeros(1, np.uint8), off, vpos, n, tid, tm, len(type_ids), t, d, o, r)
     return t, d, o, r
+
+
+VERTEX_EXISTS_ID = (1 << 6) | 37  # BaseKey.VertexExists (types/system/BaseKey.java:40-41): SystemPropertyKey count 1
+
+
+def key_to_vertex_id(keys, partition_bits=5):
+    """IDManager.getKeyID (graphdb/idmanagement/IDManager.java:496-506) over uint64 row keys.
+    Odd keys (schema / invisible rows) come back as -1, keys with no user vertex type as -2."""
+    k = np.asarray(keys, np.uint64)
+    poff = 64 - partition_bits
+    part = (k >> np.uint64(poff)) if poff < 64 else np.zeros_like(k)
+    count = (k >> np.uint64(3)) & np.uint64((1 << (poff - 3)) - 1)
+    suffix = k & np.uint64(7)
+    vid = ((((count << np.uint64(partition_bits)) + part) << np.uint64(3)) | suffix).astype(np.int64)
+    vid[(k & np.uint64(1)) == 1] = -1
+    vid[suffix == 6] = -2
+    return vid
+
+
+def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=(), partition_bits=5):
+    """The scan -> snapshot step restated row by row (the checker of jg_graph_build_edgestore):
+    VertexJobConverter.getKeyFilter drops invisible rows (olap/VertexJobConverter.java:174-177);
+    process/isGhostVertex keep a row only if its first entry is the VertexExists property (:122-151);
+    the kept rows' OUT entries of visible user edges are the edges (each edge is stored OUT on its
+    source row and IN on its target row, graphdb/database/StandardJanusGraph.java:617-640).
+    Returns (vid of kept rows in row order, src ids, dst ids); raises ValueError where Java throws."""
+    data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    off, row_off = _i64(off), _i64(row_off)
+    t, d, o, _ = decode_edges(data, off, vpos, type_ids, type_mult)
+    vids = key_to_vertex_id(keys, partition_bits)
+    keep_v, src, dst = [], [], []
+    for r, vid in enumerate(vids):
+        e0, e1 = int(row_off[r]), int(row_off[r + 1])
+        if vid == -1:
+            continue
+        if vid == -2:
+            raise ValueError("row key with an unrecognized vertex id type")
+        if vid & 7 == 2:
+            raise NotImplementedError("partitioned (vertex-cut) vertex rows")
+        if e0 == e1:
+            continue
+        if d[e0] < 0:
+            raise ValueError("malformed entry")
+        if not (d[e0] == 2 and t[e0] == VERTEX_EXISTS_ID):
+            continue  # ghost vertex
+        keep_v.append(int(vid))
+        for e in range(e0, e1):
+            if d[e] < 0:
+                raise ValueError("malformed entry")
+            visible = (int(data[off[e]]) >> 6) == 1  # relation-type header prefix >> 1: 1 = user, visible
+            if d[e] == 0 and visible:
+                src.append(int(vid))
+                dst.append(int(o[e]))
+    return np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64)
