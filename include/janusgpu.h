@@ -34,6 +34,9 @@
  *   jg_connected_components
  *       TinkerPop ConnectedComponentVertexProgram (String-min label over BOTH edges,
  *       VertexProgramScanJob.java:113-135 loads BOTH); pinned by OLAPTest.java:736-762
+ *   jg_combine_steps
+ *       the same loop for sum/min/max MessageCombiner programs (OLAPTest.DegreeCounter,
+ *       janusgraph-test/.../olap/OLAPTest.java:424-503; VertexState.java:85-114)
  *   jg_graph_info_get / jg_ctx_last_stats
  *       ScanMetrics counters (StandardScanMetrics.java:28-88: ghost-vertices, truncated-results)
  *       and memory().getIteration()/getRuntime() (FulgoraMemory.java:97-101)
@@ -187,6 +190,20 @@ int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direct
  * component label (the String-minimum id of v's weakly connected component).  iterations_out
  * (nullable) = supersteps of the synchronous program. */
 int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out);
+
+/* Combiner vertex programs (the DegreeCounter family, janusgraph-test/.../olap/OLAPTest.java:424-503):
+ * x_0 = init[v] (NULL: every vertex sends 1), then `steps` supersteps of
+ *     x_t[v] = COMBINE over the entries (v, w) of v's `direction` adjacency of x_{t-1}[w]
+ * (JG_DIR_OUT: v's out-edges, i.e. messages sent on Local.of(inE); one term per edge).  COMBINE is
+ * JG_COMBINE_SUM (a vertex with no entries gets 0, as reduce(0, +)), _MIN or _MAX (no entries: the
+ * identity, and received_out[v] = 0).  int32_wrap != 0: Java Integer values (inputs truncated to
+ * int32, sums modulo 2^32).  out[n] = x_steps; received_out[n] (nullable) = v had at least one term
+ * in the last superstep.  Needs the matching adjacency at build time; single-shard graphs only. */
+#define JG_COMBINE_SUM 0
+#define JG_COMBINE_MIN 1
+#define JG_COMBINE_MAX 2
+int jg_combine_steps(jg_graph* g, int32_t direction, int32_t combiner, int32_t int32_wrap, const int64_t* init,
+                     int32_t steps, int64_t* out, uint8_t* received_out);
 
 /* Decode n edgestore entries on the context's first GPU, as EdgeSerializer.parseRelation does
  * (core/graphdb/database/EdgeSerializer.java:86-122; header: IDHandler.readRelationType,

@@ -24,6 +24,7 @@ JG_ERR_STATE = -6
 
 ADJ_OUT, ADJ_IN, ADJ_BOTH = 1, 2, 4
 DIR_OUT, DIR_IN, DIR_BOTH = 1, 2, 3
+COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
 FULGORA_HARD_QUERY_LIMIT = 100000
 UNIQUE_ID_BYTES = 128
 
@@ -33,7 +34,7 @@ EXPORTS = [
     "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_edgestore",
     "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
-    "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_decode_edges", "jg_graph_sync",
+    "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_combine_steps", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set",
 ]
 
@@ -109,6 +110,7 @@ def load():
         "jg_shortest_distance": ([_P, _i64, _i32, _P], ctypes.c_int),
         "jg_bfs": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
         "jg_connected_components": ([_P, _P, _P], ctypes.c_int),
+        "jg_combine_steps": ([_P, _i32, _i32, _i32, _P, _i32, _P, _P], ctypes.c_int),
         "jg_decode_edges": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i32, _P, _P, _P, _P], ctypes.c_int),
         "jg_graph_sync": ([_P], ctypes.c_int),
         "jg_tune_set": ([ctypes.c_char_p, _i64], ctypes.c_int),
@@ -305,6 +307,18 @@ class Graph:
         depth = np.empty(len(src) * self.n, np.int32) if want else None
         check(load().jg_bfs(self._h, _ptr(src), len(src), int(direction), int(max_depth), _ptr(depth)))
         return None if depth is None else depth.reshape(len(src), self.n)
+
+    def combine_steps(self, direction, combiner=COMBINE_SUM, steps=1, init=None, int32_wrap=True):
+        """jg_combine_steps: `steps` supersteps of x[v] = COMBINE over v's `direction` entries of x[w].
+        Returns (x, received) indexed like vid[]."""
+        x0 = None if init is None else np.ascontiguousarray(init, np.int64)
+        if x0 is not None and len(x0) != self.n:
+            raise ValueError("init needs one value per vertex")
+        out = np.empty(max(self.n, 1), np.int64)
+        rec = np.empty(max(self.n, 1), np.uint8)
+        check(load().jg_combine_steps(self._h, int(direction), int(combiner), 1 if int32_wrap else 0, _ptr(x0),
+                                      int(steps), _ptr(out), _ptr(rec)))
+        return out[:self.n], rec[:self.n].astype(bool)
 
     def connected_components(self):
         comp = np.empty(self.n, np.int64)

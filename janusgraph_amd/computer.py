@@ -24,8 +24,8 @@ from . import _lib
 from .computer_types import (Persist, ProgramNotSupported, ResultGraph, ResultMode, computer_has_already_been_submitted,
                              computer_has_no_vertex_program_nor_map_reducers, graph_filter_not_supported)
 from .graph import InMemoryGraph
-from .programs import (ConnectedComponentVertexProgram, PageRankVertexProgram, ShortestDistanceVertexProgram,
-                       ShortestPathVertexProgram)
+from .programs import (CombinerVertexProgram, ConnectedComponentVertexProgram, PageRankVertexProgram,
+                       ShortestDistanceVertexProgram, ShortestPathVertexProgram)
 
 
 class Memory:
@@ -159,7 +159,8 @@ class GpuGraphComputer:
         vp = self.vertex_program
         if vp is not None:
             if not isinstance(vp, (PageRankVertexProgram, ShortestDistanceVertexProgram,
-                                   ConnectedComponentVertexProgram, ShortestPathVertexProgram)):
+                                   ConnectedComponentVertexProgram, ShortestPathVertexProgram,
+                                   CombinerVertexProgram)):
                 raise ProgramNotSupported(f"{type(vp).__name__} is not run by GpuGraphComputer; "
                                           f"delegate to FulgoraGraphComputer")
             self.map_reduces.extend(vp.get_map_reducers())
@@ -192,7 +193,8 @@ class GpuGraphComputer:
             emitted = []
             for vid in (vids if vids is not None else []):
                 mr.map(int(vid), props.get(int(vid), {}), lambda k, v: emitted.append((k, v)))
-            memory.set(mr.memory_key, iter(emitted))
+            final = getattr(mr, "generate_final_result", None)
+            memory.set(mr.memory_key, final(emitted) if final else iter(emitted))
         result_graph = self._write_back(props)
         memory._runtime = int(round((time.perf_counter() - t0) * 1000))
         return ComputerResult(result_graph, memory)
@@ -232,6 +234,20 @@ class GpuGraphComputer:
             return vid, props, it, {}
         if isinstance(vp, ShortestPathVertexProgram):
             return self._shortest_paths(ctx, vp)
+        if isinstance(vp, CombinerVertexProgram):
+            vid, src, dst, _ = g0.snapshot()
+            direction = CombinerVertexProgram.SCOPES[vp.scope]
+            adj = {_lib.DIR_OUT: _lib.ADJ_OUT, _lib.DIR_IN: _lib.ADJ_IN, _lib.DIR_BOTH: _lib.ADJ_BOTH}[direction]
+            g = ctx.build(vid, src, dst, flags=adj)
+            try:
+                x, received = g.combine_steps(direction, CombinerVertexProgram.COMBINERS.index(vp.combiner), vp.length,
+                                              np.full(len(vid), vp.initial_message, np.int64), vp.int32)
+            finally:
+                g.close()
+            # a sum always sets the key (reduce(0, +)); min/max only where a message arrived
+            keep = np.ones(len(vid), bool) if vp.combiner == "sum" else received
+            props = {int(v): {vp.property_key: int(d)} for v, d, k in zip(vid, x, keep) if k}
+            return vid, props, vp.length, {}
         raise ProgramNotSupported(type(vp).__name__)
 
     def _shortest_paths(self, ctx, vp):

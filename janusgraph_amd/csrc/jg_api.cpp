@@ -708,6 +708,15 @@ int jg_decode_edges(jg_ctx* ctx, const uint8_t* bytes, int64_t nbytes, const int
     JG_GUARD_END
 }
 
+int jg_combine_steps(jg_graph* g, int32_t direction, int32_t combiner, int32_t int32_wrap, const int64_t* init,
+                     int32_t steps, int64_t* out, uint8_t* received_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    JG_ARG(out || g->impl.n == 0, "null output");
+    jg::combine_run(g->impl, direction, combiner, int32_wrap, init, steps, out, received_out);
+    JG_GUARD_END
+}
+
 int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* iterations_out) {
     JG_GUARD_BEGIN
     JG_ARG(g, "null graph");

@@ -181,6 +181,8 @@ struct Shard {
     int64_t rows = 0;        // owned rows (<= S)
     Csr in, out, both;
     PullPlan plan_in, plan_both;
+    PullPlan plan_out;            // built on first use (combiner programs over the OUT adjacency)
+    bool plan_out_built = false;
     Halo halo_in, halo_both;      // sharded graphs: compact vectors of the IN / BOTH pull adjacencies
     DevBuf<int32_t> out_degree;   // [rows] out-degree of owned vertices (PageRank edgeCount)
     std::vector<int32_t> dense_of_local;  // host: caller's dense index of each owned row
@@ -325,6 +327,8 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out);
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
+void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
+                 uint8_t* received_out);
 
 // Logical OR of a flag over all ranks (identity in single-process contexts).
 int allreduce_or(Graph& g, int flag);

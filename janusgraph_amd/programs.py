@@ -9,6 +9,10 @@ Same names, configuration keys, builders and output keys as the reference:
       ShortestDistanceMapReduce.java:29-64
   ConnectedComponentVertexProgram, ShortestPathVertexProgram
       TinkerPop 3.4.6 gremlin-core (third party, not in the container; SURVEY.md A.3/A.4 [TP-recall])
+  CombinerVertexProgram / DegreeCounter / DegreeMapper
+      a superstep loop with a sum / min / max MessageCombiner over one Local scope, as
+      janusgraph-test/src/main/java/org/janusgraph/olap/OLAPTest.java:424-540 (DegreeCounter,
+      DegreeMapper) writes it; message combining per VertexState.java:85-114
 Any other program is not recognised: the computer refuses it with ProgramNotSupported so that the
 caller (the Java GpuGraphComputer) delegates it to FulgoraGraphComputer unchanged.
 """
@@ -177,6 +181,39 @@ class ShortestPathVertexProgram(VertexProgram):
         return cls.Builder()
 
 
+class CombinerVertexProgram(VertexProgram):
+    """A program whose every superstep is x_t[v] = COMBINE of the messages v receives, each neighbour
+    sending its x_{t-1}: superstep 0 sends `initial_message`, supersteps 1..length store the combined
+    value under `property_key` and send it on while t < length; terminate at iteration >= length.
+    `scope` is the send scope's direction: "inE" (DegreeCounter's DEG_MSG, OLAPTest.java:429) reaches
+    the sources of a vertex's in-edges, so a vertex receives from its out-neighbours."""
+
+    preferred_result_graph = ResultGraph.NEW
+    preferred_persist = Persist.VERTEX_PROPERTIES
+    COMBINERS = ("sum", "min", "max")
+    SCOPES = {"inE": 1, "outE": 2, "bothE": 3}  # -> the receiver's pull direction (DIR_OUT/IN/BOTH)
+
+    def __init__(self, length=1, property_key="degree", combiner="sum", scope="inE", initial_message=1,
+                 int32=True):
+        if length <= 0:
+            raise ValueError("length must be positive")  # Preconditions.checkArgument(length>0), :438
+        if combiner not in self.COMBINERS or scope not in self.SCOPES:
+            raise ValueError("unknown combiner or scope")
+        self.length, self.property_key, self.combiner, self.scope = length, property_key, combiner, scope
+        self.initial_message, self.int32 = initial_message, int32
+        self.compute_keys = (property_key,)
+        super().__init__({"length": length})
+
+
+class DegreeCounter(CombinerVertexProgram):
+    """OLAPTest.DegreeCounter (OLAPTest.java:424-503): k-hop out-path counts, Integer sums."""
+
+    DEGREE = "degree"
+
+    def __init__(self, length=1):
+        super().__init__(length, self.DEGREE, "sum", "inE", 1, True)
+
+
 class MapReduce:
     memory_key = None
 
@@ -216,6 +253,21 @@ class ShortestDistanceMapReduce(MapReduce):
             emit(vid, v)
 
 
+class DegreeMapper(MapReduce):
+    """OLAPTest.DegreeMapper (OLAPTest.java:505-540): memory["degrees"] = {vertex id: degree}."""
+
+    DEGREE_RESULT = "degrees"
+    memory_key = DEGREE_RESULT
+
+    def map(self, vid, props, emit):
+        v = props.get(DegreeCounter.DEGREE)
+        if v is not None:
+            emit(vid, v)
+
+    def generate_final_result(self, key_values):
+        return {k: v for k, v in key_values}
+
+
 class _MrBuilder:
     def __init__(self, cls):
         self.cls, self.key = cls, cls.DEFAULT_MEMORY_KEY
@@ -229,4 +281,4 @@ class _MrBuilder:
 
 
 RECOGNISED = (PageRankVertexProgram, ShortestDistanceVertexProgram, ConnectedComponentVertexProgram,
-              ShortestPathVertexProgram)
+              ShortestPathVertexProgram, CombinerVertexProgram)

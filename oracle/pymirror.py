@@ -105,11 +105,15 @@ class Engine:
         self.props = {v: {} for v in g.vertices}
         self.prev_msgs, self.cur_msgs = {}, {}
         program.setup(mem)
+        self.prev_scopes = []
         while True:
-            self.prev_scopes = program.message_scopes(mem)
+            # nextIteration(getMessageScopes(memory)) sets the scopes this superstep SENDS on; messages
+            # are received over the previous superstep's (FulgoraVertexMemory.java:101-112)
+            cur_scopes = program.message_scopes(mem)
             for v in g.vertices:
                 program.execute(v, self.props[v], Messenger(self, v), mem, g)
             self.prev_msgs, self.cur_msgs = self.cur_msgs, {}
+            self.prev_scopes = cur_scopes
             if program.terminate(mem):
                 break
             mem.iteration += 1
@@ -241,3 +245,47 @@ def bfs_depth(graph: MiniGraph, source, direction=BOTH, max_depth=-1):
                     nxt.append(w)
         frontier = nxt
     return depth
+
+
+class DegreeCounterProgram:
+    """janusgraph-test/.../olap/OLAPTest.java:424-503 (DegreeCounter): Integer sums, Local.of(inE),
+    combiner (a, b) -> a + b.  The general form takes the combiner and scope (CombinerVertexProgram)."""
+
+    def __init__(self, length=1, combine=lambda a, b: a + b, direction=IN, initial=1, key="degree", int32=True):
+        self.length, self.combine, self.initial, self.key, self.int32 = length, combine, initial, key, int32
+        self.scope = LocalScope(direction, "deg")
+        self.sum = combine(2, 3) == 5
+
+    def setup(self, mem):
+        pass
+
+    def message_scopes(self, mem):
+        return [self.scope] if mem.iteration < self.length else []
+
+    def _int(self, x):
+        if not self.int32:
+            return x
+        x &= 0xFFFFFFFF
+        return x - (1 << 32) if x >> 31 else x
+
+    def execute(self, v, props, msgr, mem, g):
+        if mem.is_initial_iteration():
+            msgr.send_message(self.scope, self.initial)
+            return
+        msgs = msgr.receive_messages()
+        if self.sum:
+            degree = 0  # IteratorUtils.stream(...).reduce(0, (a, b) -> a + b)
+            for m in msgs:
+                degree = self._int(degree + m)
+        else:
+            if not msgs:
+                return
+            degree = msgs[0]
+            for m in msgs[1:]:
+                degree = self.combine(degree, m)
+        props[self.key] = degree
+        if mem.iteration < self.length:
+            msgr.send_message(self.scope, degree)
+
+    def terminate(self, mem):
+        return mem.iteration >= self.length
