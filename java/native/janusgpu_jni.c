@@ -109,3 +109,39 @@ JNIEXPORT jint JNICALL FN(connectedComponents)(JNIEnv* env, jclass c, jlong g, j
     (*env)->SetIntArrayRegion(env, iterations_out, 0, 1, &v);
     return st;
 }
+
+JNIEXPORT jint JNICALL FN(graphBuildEdgestore)(JNIEnv* env, jclass c, jlong ctx, jobject row_keys, jlong nrows,
+                                               jobject row_entry_off, jobject bytes, jlong nbytes, jobject entry_off,
+                                               jobject value_pos, jlong nentries, jobject type_ids, jobject type_mult,
+                                               jint ntypes, jint partition_bits, jint flags, jobject vid_out,
+                                               jlongArray out2) {
+    (void)c;
+    jg_graph* g = NULL;
+    int64_t nv = 0;
+    int st = jg_graph_build_edgestore((jg_ctx*)(intptr_t)ctx, (const uint64_t*)buf(env, row_keys), nrows,
+                                      (const int64_t*)buf(env, row_entry_off), (const uint8_t*)buf(env, bytes), nbytes,
+                                      (const int64_t*)buf(env, entry_off), (const int32_t*)buf(env, value_pos),
+                                      nentries, (const int64_t*)buf(env, type_ids), (const int8_t*)buf(env, type_mult),
+                                      ntypes, partition_bits, (uint32_t)flags, (int64_t*)buf(env, vid_out), &nv, &g);
+    jlong v[2] = {(jlong)(intptr_t)g, (jlong)nv};
+    (*env)->SetLongArrayRegion(env, out2, 0, 2, v);
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(combineSteps)(JNIEnv* env, jclass c, jlong g, jint direction, jint combiner,
+                                        jint int32_wrap, jobject init, jint steps, jobject out, jobject received_out) {
+    (void)c;
+    return jg_combine_steps((jg_graph*)(intptr_t)g, direction, combiner, int32_wrap, (const int64_t*)buf(env, init),
+                            steps, (int64_t*)buf(env, out), (uint8_t*)buf(env, received_out));
+}
+
+JNIEXPORT jint JNICALL FN(decodeEdges)(JNIEnv* env, jclass c, jlong ctx, jobject bytes, jlong nbytes, jobject entry_off,
+                                       jobject value_pos, jlong n, jobject type_ids, jobject type_mult, jint ntypes,
+                                       jobject type_out, jobject dir_out, jobject other_out, jobject relation_out) {
+    (void)c;
+    return jg_decode_edges((jg_ctx*)(intptr_t)ctx, (const uint8_t*)buf(env, bytes), nbytes,
+                           (const int64_t*)buf(env, entry_off), (const int32_t*)buf(env, value_pos), n,
+                           (const int64_t*)buf(env, type_ids), (const int8_t*)buf(env, type_mult), ntypes,
+                           (int64_t*)buf(env, type_out), (int8_t*)buf(env, dir_out), (int64_t*)buf(env, other_out),
+                           (int64_t*)buf(env, relation_out));
+}

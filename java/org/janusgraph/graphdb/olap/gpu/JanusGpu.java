@@ -47,6 +47,20 @@ final class JanusGpu {
     static native int bfs(long graph, ByteBuffer sourceVids, int nsrc, int direction, int maxDepth, ByteBuffer depthOut);
     static native int connectedComponents(long graph, ByteBuffer componentVidOut, int[] iterationsOut);
 
+    /** jg_graph_build_edgestore: the snapshot from the scan's raw rows (StaticBuffer keys as longs, the
+     *  EntryLists' bytes, entry offsets and value positions); out2 = {graph handle, |V|}. */
+    static native int graphBuildEdgestore(long ctx, ByteBuffer rowKeys, long nrows, ByteBuffer rowEntryOff,
+                                          ByteBuffer bytes, long nbytes, ByteBuffer entryOff, ByteBuffer valuePos,
+                                          long nentries, ByteBuffer typeIds, ByteBuffer typeMult, int ntypes,
+                                          int partitionBits, int flags, ByteBuffer vidOut, long[] out2);
+    /** jg_combine_steps: sum/min/max MessageCombiner programs (OLAPTest.DegreeCounter family). */
+    static native int combineSteps(long graph, int direction, int combiner, int int32Wrap, ByteBuffer init, int steps,
+                                   ByteBuffer out, ByteBuffer receivedOut);
+    /** jg_decode_edges: EdgeSerializer.parseRelation of raw entries on the GPU. */
+    static native int decodeEdges(long ctx, ByteBuffer bytes, long nbytes, ByteBuffer entryOff, ByteBuffer valuePos,
+                                  long n, ByteBuffer typeIds, ByteBuffer typeMult, int ntypes, ByteBuffer typeOut,
+                                  ByteBuffer dirOut, ByteBuffer otherOut, ByteBuffer relationOut);
+
     static void check(int status) {
         if (status != 0) {
             throw new org.janusgraph.core.JanusGraphException(
