@@ -163,8 +163,14 @@ __global__ void nbr_min_kernel(const int32_t* __restrict__ src, const int32_t* _
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
         const int32_t a = src[e], b = dst[e];
         if (a < 0 || b < 0) continue;
-        atomicMin(&nbr_min[b], rank1[a]);
-        if (mode == 1) atomicMin(&nbr_min[a], rank1[b]);
+        // plain read first: the minimum only falls, so a value not below the current one is done
+        // (hub rows otherwise serialise millions of atomics on one word)
+        const int32_t ra = rank1[a];
+        if (ra < __atomic_load_n(&nbr_min[b], __ATOMIC_RELAXED)) atomicMin(&nbr_min[b], ra);
+        if (mode == 1) {
+            const int32_t rb = rank1[b];
+            if (rb < __atomic_load_n(&nbr_min[a], __ATOMIC_RELAXED)) atomicMin(&nbr_min[a], rb);
+        }
     }
 }
 
@@ -249,8 +255,25 @@ struct SelectArgs {
     CompactMap cm;  // sharded pull adjacency with a halo plan: columns become compact ids
 };
 
-__device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
-    const int32_t s = a.src[e], d = a.dst[e];
+// The block's tile of kSelTile edges is staged through LDS with coalesced loads, so each thread's
+// kSelItems consecutive edges (kept consecutive for the stable order) come from LDS instead of
+// stride-kSelItems global loads.  Padded by one word per kSelItems against bank conflicts.
+constexpr int kSelPad = kSelTile + kSelTile / kSelItems;
+__device__ __forceinline__ int sel_slot(int i) { return i + i / kSelItems; }
+
+__device__ __forceinline__ void stage_tile(const SelectArgs& a, int32_t* ts, int32_t* td) {
+    const int64_t t0 = (int64_t)blockIdx.x * kSelTile;
+#pragma unroll
+    for (int u = 0; u < kSelItems; ++u) {
+        const int i = threadIdx.x + u * kBlock;
+        const int64_t e = t0 + i;
+        ts[sel_slot(i)] = e < a.m ? a.src[e] : -1;
+        td[sel_slot(i)] = e < a.m ? a.dst[e] : -1;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int emit_count(const SelectArgs& a, int32_t s, int32_t d) {
     if (s < 0 || d < 0) return 0;
     const int32_t gs = a.padded[s], gd = a.padded[d];
     const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
@@ -261,11 +284,14 @@ __device__ __forceinline__ int emit_count(const SelectArgs& a, int64_t e) {
 
 __global__ __launch_bounds__(kBlock) void select_count_kernel(SelectArgs a, int64_t* __restrict__ block_counts) {
     __shared__ int64_t scratch[kBlock / kWave];
-    const int64_t base = (int64_t)blockIdx.x * kSelTile + (int64_t)threadIdx.x * kSelItems;
+    __shared__ int32_t ts[kSelPad], td[kSelPad];
+    stage_tile(a, ts, td);
     int64_t c = 0;
 #pragma unroll
-    for (int k = 0; k < kSelItems; ++k)
-        if (base + k < a.m) c += emit_count(a, base + k);
+    for (int k = 0; k < kSelItems; ++k) {
+        const int i = sel_slot(threadIdx.x * kSelItems + k);
+        c += emit_count(a, ts[i], td[i]);
+    }
     c = wave_reduce_add(c);
     if (lane_id() == 0) scratch[wave_id()] = c;
     __syncthreads();
@@ -279,17 +305,22 @@ __global__ __launch_bounds__(kBlock) void select_count_kernel(SelectArgs a, int6
 __global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, const int64_t* __restrict__ block_off,
                                                               uint64_t* __restrict__ keys, uint32_t* __restrict__ eidx) {
     __shared__ int64_t scratch[kBlock / kWave];
+    __shared__ int32_t ts[kSelPad], td[kSelPad];
+    stage_tile(a, ts, td);
     const int64_t base = (int64_t)blockIdx.x * kSelTile + (int64_t)threadIdx.x * kSelItems;
     int64_t c = 0;
 #pragma unroll
-    for (int k = 0; k < kSelItems; ++k)
-        if (base + k < a.m) c += emit_count(a, base + k);
+    for (int k = 0; k < kSelItems; ++k) {
+        const int i = sel_slot(threadIdx.x * kSelItems + k);
+        c += emit_count(a, ts[i], td[i]);
+    }
     int64_t total;
     int64_t pos = block_exclusive_scan_add(c, scratch, &total) + block_off[blockIdx.x];
     for (int k = 0; k < kSelItems; ++k) {
         const int64_t e = base + k;
         if (e >= a.m) break;
-        const int32_t s = a.src[e], d = a.dst[e];
+        const int i = sel_slot(threadIdx.x * kSelItems + k);
+        const int32_t s = ts[i], d = td[i];
         if (s < 0 || d < 0) continue;
         const int64_t gs = a.padded[s], gd = a.padded[d];
         const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
@@ -358,13 +389,17 @@ __global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
 #pragma unroll
         for (int c = 1; c < kNumClasses - 2; ++c) {
             const unsigned long long v = wave_reduce_min(in && d < c_class_thr[c] ? (unsigned long long)l : none);
-            if (lane_id() == 0 && v != none) atomicMin(&first_below[c], v);
+            // a plain read first: once a low row has set the bound, later waves skip the atomic
+            // (every wave's atomic on the same few words serialised at L2: 9 ms at RMAT-24)
+            if (lane_id() == 0 && v != none && v < __atomic_load_n(&first_below[c], __ATOMIC_RELAXED))
+                atomicMin(&first_below[c], v);
         }
         const unsigned long long ne = wave_reduce_max(in && d > 0 ? (unsigned long long)(l + 1) : 0ull);
-        if (lane_id() == 0 && ne) atomicMax(last_nonempty, ne);
+        if (lane_id() == 0 && ne && ne > __atomic_load_n(last_nonempty, __ATOMIC_RELAXED)) atomicMax(last_nonempty, ne);
         for (int i = 0; i < bt.n; ++i) {
             const unsigned long long v = wave_reduce_min(in && d < bt.thr[i] ? (unsigned long long)l : none);
-            if (lane_id() == 0 && v != none) atomicMin(&band_below[i], v);
+            if (lane_id() == 0 && v != none && v < __atomic_load_n(&band_below[i], __ATOMIC_RELAXED))
+                atomicMin(&band_below[i], v);
         }
     }
 }
