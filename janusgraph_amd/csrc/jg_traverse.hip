@@ -470,6 +470,67 @@ __global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsi
     }
 }
 
+// Sharded SD push: like sd_push_kernel, but the columns are compact ids of the IN halo plan (own rows
+// in segment 0, peers' vertices in their segments): only own rows enter the touched list; remote
+// candidates wait in the halo slots for the reverse exchange.
+__global__ __launch_bounds__(kBlock) void ssd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                          const int32_t* __restrict__ wt,
+                                                          const int32_t* __restrict__ frontier, int64_t fsize,
+                                                          const long long* __restrict__ msg, long long* __restrict__ best,
+                                                          int tbits, int32_t* __restrict__ touched,
+                                                          unsigned long long* __restrict__ tsize) {
+    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
+    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
+    const int sub = threadIdx.x % kTdLanes;
+    const int64_t iters = (fsize + ngroups - 1) / ngroups;
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t qi = group + it * ngroups;
+        const bool have = qi < fsize;
+        const int32_t w = have ? frontier[qi] : 0;
+        const int64_t j0 = have ? rp[w] : 0, j1 = have ? rp[w + 1] : 0;
+        const long long mw = have ? msg[w] : 0;
+        const int64_t len = j1 - j0;
+        int64_t maxlen = len;
+#pragma unroll
+        for (int o = kTdLanes; o < kWave; o <<= 1) {
+            const int64_t t = __shfl_xor(maxlen, o, kWave);
+            maxlen = t > maxlen ? t : maxlen;
+        }
+        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
+            const int64_t k = k0 + sub;
+            bool first = false;
+            int32_t u = 0;
+            if (k < len) {
+                u = col[j0 + k];
+                const long long cand = mw + (long long)(wt ? wt[j0 + k] : 1);
+                const long long old = atomicMin(&best[u], cand);
+                first = old == LLONG_MAX && (u >> tbits) == 0;
+            }
+            wave_append(first, u, touched, tsize);
+        }
+    }
+}
+
+// The peers' candidates for own rows, received at the send-list positions (send_src[k] = own row)
+__global__ void ssd_recv_kernel(const long long* __restrict__ rbuf, const int32_t* __restrict__ send_src, int64_t nrecv,
+                                long long* __restrict__ best, int32_t* __restrict__ touched,
+                                unsigned long long* __restrict__ tsize) {
+    const int64_t iters = (nrecv + (int64_t)gridDim.x * blockDim.x - 1) / ((int64_t)gridDim.x * blockDim.x);
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + it * (int64_t)gridDim.x * blockDim.x;
+        bool first = false;
+        int32_t u = 0;
+        if (k < nrecv) {
+            const long long v = rbuf[k];
+            if (v != LLONG_MAX) {
+                u = send_src[k];
+                first = atomicMin(&best[u], v) == LLONG_MAX;
+            }
+        }
+        wave_append(first, u, touched, tsize);
+    }
+}
+
 __global__ void fill_ll_kernel(long long* p, int64_t n, long long v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -1147,11 +1208,145 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
     JG_HIP(hipEventDestroy(t1));
 }
 
+// Sharded ShortestDistanceVertexProgram (weighted or unit): the same exact supersteps as the single
+// shard (push from the rows whose distance fell last superstep, min into `best`, apply), over the IN
+// adjacency's halo plan.  Candidates for remote vertices collect in their halo slots and go to the
+// owners by the reverse halo exchange (the transpose of the PageRank/CC exchange), which take their
+// min; frontier sizes are summed over shards and ranks every superstep.
+static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
+    Ctx& ctx = *g.ctx;
+    const size_t ns = g.shards.size();
+    for (auto& sp : g.shards)
+        if (!sp->halo_in.on)
+            fail(JG_ERR_UNSUPPORTED, "sharded shortest distance needs the halo plan (tune \"halo\" = 1 at build)");
+    int seed_shard = -1;
+    const int64_t seed_local = local_of_vid(g, seed_vid, &seed_shard);
+    struct St {
+        DevBuf<long long> best, dist, msg, rbuf;
+        DevBuf<int32_t> fa, fb, touched;
+        DevBuf<unsigned long long> sizes;
+        int64_t fsize = 0;
+    };
+    std::vector<St> st(ns);
+    std::vector<void*> bv, rv;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        const Halo& h = sh.halo_in;
+        St& t = st[i];
+        const int64_t rows = std::max<int64_t>(sh.rows, 1);
+        t.best.alloc(std::max<int64_t>(h.C, 1));
+        t.dist.alloc(rows);
+        t.msg.alloc(rows);
+        t.fa.alloc(rows);
+        t.fb.alloc(rows);
+        t.touched.alloc(rows);
+        t.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
+        t.sizes.alloc(2);
+        fill_ll_kernel<<<grid_for(h.C), kBlock, 0, sh.stream>>>(t.best.get(), h.C, LLONG_MAX);
+        fill_ll_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.dist.get(), sh.rows, LLONG_MIN);  // absent
+        JG_LAUNCH_CHECK();
+        if (seed_local >= 0 && sh.index == seed_shard) {
+            const long long zero = 0;
+            const int32_t seed32 = (int32_t)seed_local;
+            copy_h2d(t.dist.get() + seed_local, &zero, sizeof zero, sh.stream);
+            copy_h2d(t.msg.get() + seed_local, &zero, sizeof zero, sh.stream);
+            copy_h2d(t.fa.get(), &seed32, sizeof seed32, sh.stream);
+            t.fsize = 1;
+        }
+        bv.push_back(t.best.get());
+        rv.push_back(t.rbuf.get());
+    }
+    int64_t total = seed_local >= 0 ? 1 : 0;
+    allreduce_sum_i64(g, &total, 1);
+    Shard& sh0 = *g.shards[0];
+    hipEvent_t t0, t1;
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, sh0.stream));
+    }
+    int levels = 0;
+    for (int lv = 1; lv <= max_depth && total > 0; ++lv) {
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            JG_HIP(hipMemsetAsync(t.sizes.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+            if (t.fsize > 0) {
+                ssd_push_kernel<<<grid_for(t.fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
+                    sh.in.row_ptr.get(), sh.in.col.get(), g.has_weights ? sh.in.weight.get() : nullptr, t.fa.get(),
+                    t.fsize, t.msg.get(), t.best.get(), sh.halo_in.tbits, t.touched.get(), t.sizes.get());
+                JG_LAUNCH_CHECK();
+            }
+        }
+        exchange_halo_reverse(g, JG_ADJ_IN, bv, rv, sizeof(long long), ncclInt64);
+        int64_t next = 0;
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            const Halo& h = sh.halo_in;
+            const int64_t nrecv = h.send_off[g.P];
+            if (nrecv > 0) {
+                ssd_recv_kernel<<<grid_for(nrecv, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
+                    t.rbuf.get(), h.send_src.get(), nrecv, t.best.get(), t.touched.get(), t.sizes.get());
+                JG_LAUNCH_CHECK();
+            }
+            for (int q = 0; q < g.P; ++q) {  // the halo slots are sent: back to "no candidate"
+                const int64_t nr = h.recv_off[q + 1] - h.recv_off[q];
+                if (q == sh.index || nr == 0) continue;
+                fill_ll_kernel<<<grid_for(nr), kBlock, 0, sh.stream>>>(
+                    t.best.get() + ((int64_t)h.seg_of(q, sh.index) << h.tbits), nr, LLONG_MAX);
+                JG_LAUNCH_CHECK();
+            }
+            unsigned long long ts = 0;
+            copy_d2h(&ts, t.sizes.get(), sizeof ts, sh.stream);
+            if (ts > 0) {
+                sd_apply_kernel<<<grid_for((int64_t)ts, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
+                    t.touched.get(), (int64_t)ts, t.best.get(), t.dist.get(), t.msg.get(), t.fb.get(), t.sizes.get() + 1);
+                JG_LAUNCH_CHECK();
+            }
+            unsigned long long nn = 0;
+            copy_d2h(&nn, t.sizes.get() + 1, sizeof nn, sh.stream);
+            t.fsize = (int64_t)nn;
+            t.fa.swap(t.fb);
+            next += t.fsize;
+        }
+        allreduce_sum_i64(g, &next, 1);
+        total = next;
+        levels = lv;
+    }
+    float ms = 0;
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventRecord(t1, sh0.stream));
+        JG_HIP(hipEventSynchronize(t1));
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        std::vector<long long> h((size_t)sh.rows);
+        if (sh.rows) copy_d2h(h.data(), st[i].dist.get(), sh.rows * sizeof(long long), sh.stream);
+        for (int64_t l = 0; l < sh.rows; ++l) dist_out[sh.dense_of_local[l]] = h[l] == LLONG_MIN ? -1 : h[l];
+    }
+    ctx.last.compute_ms = ms;
+    ctx.last.levels = levels;
+    ctx.last.supersteps = max_depth;
+}
+
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
-    if (g.P != 1) fail(JG_ERR_UNSUPPORTED, "shortest distance runs on a single shard in this version");
     if (!(g.flags & JG_ADJ_IN)) fail(JG_ERR_UNSUPPORTED, "shortest distance needs a graph built with JG_ADJ_IN");
+    if (g.P != 1) {
+        shortest_distance_sharded(g, seed_vid, max_depth, dist_out);
+        return;
+    }
     Shard& sh = *g.shards[0];
     DeviceGuard dg(sh.device);
     hipStream_t s = sh.stream;

@@ -253,6 +253,27 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     c.close()
 
 
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_logical_shards_shortest_distance(oracle_lib, shards):
+    """Sharded ShortestDistanceVertexProgram (weighted and unit) over the IN halo plan: push into own
+    rows and halo slots, reverse halo exchange to the owners == the oracle, for several hop bounds."""
+    import janusgraph_amd as jg
+    c = jg.Context((0,) * shards)
+    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 13)
+    w = (np.arange(len(src)) % 3 + 1).astype(np.int32)
+    g = c.build(vid, src, dst, weight=w, flags=2)
+    gu = c.build(vid, src, dst, flags=2)
+    for seed in (int(dd[0]), int(dd[7])):
+        for md in (1, 3, 6, 30):
+            np.testing.assert_array_equal(g.shortest_distance(vid[seed], md),
+                                          oracle_lib.shortest_distance(n, ds, dd, seed, md, w))
+            np.testing.assert_array_equal(gu.shortest_distance(vid[seed], md),
+                                          oracle_lib.shortest_distance(n, ds, dd, seed, md))
+    g.close()
+    gu.close()
+    c.close()
+
+
 def test_hub_rows_chunked(ctx, oracle_lib):
     """A star with hubs above the chunking threshold (8192) in and out."""
     n = 40000
