@@ -198,7 +198,7 @@ int jg_connected_components(jg_graph* g, int64_t* component_vid_out, int32_t* it
  * JG_COMBINE_SUM (a vertex with no entries gets 0, as reduce(0, +)), _MIN or _MAX (no entries: the
  * identity, and received_out[v] = 0).  int32_wrap != 0: Java Integer values (inputs truncated to
  * int32, sums modulo 2^32).  out[n] = x_steps; received_out[n] (nullable) = v had at least one term
- * in the last superstep.  Needs the matching adjacency at build time; single-shard graphs only. */
+ * in the last superstep.  Needs the matching adjacency at build time; sharded graphs exchange the messages every superstep. */
 #define JG_COMBINE_SUM 0
 #define JG_COMBINE_MIN 1
 #define JG_COMBINE_MAX 2

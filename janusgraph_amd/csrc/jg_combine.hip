@@ -50,8 +50,9 @@ __device__ __forceinline__ int64_t finish(int64_t acc, int wrap32) {
 template <int OP>
 struct CombOp {
     using T = long long;
-    const long long* __restrict__ x;  // previous superstep, one value per row (one shard: column space)
-    long long* __restrict__ x_out;
+    const long long* __restrict__ x;  // previous superstep, gathered vector (compact or full length)
+    long long* __restrict__ x_out;    // next superstep's gathered vector (owned slots written)
+    VecPos pos;                       // owned row -> its slot
     int wrap32;
     __device__ __forceinline__ long long identity() const { return Combine<OP>::identity(); }
     __device__ __forceinline__ long long combine(long long a, long long b) const { return Combine<OP>::apply(a, b); }
@@ -60,7 +61,9 @@ struct CombOp {
     __device__ __forceinline__ long long shfl_xor(long long v, int o) const { return __shfl_xor(v, o, kWave); }
     __device__ __forceinline__ long long shfl_up(long long v, int d) const { return __shfl_up(v, d, kWave); }
     __device__ __forceinline__ bool active(int64_t) const { return true; }
-    __device__ __forceinline__ void finalize(int64_t row, long long acc) const { x_out[row] = finish<OP>(acc, wrap32); }
+    __device__ __forceinline__ void finalize(int64_t row, long long acc) const {
+        x_out[pos(row)] = finish<OP>(acc, wrap32);
+    }
 };
 
 // received = the row has at least one entry (static over the supersteps)
@@ -71,70 +74,117 @@ __global__ void has_entries_kernel(const int64_t* __restrict__ row_ptr, int64_t 
 
 template <int OP>
 void launch_step(const Csr& c, const PullPlan& plan, long long* hub_partial, const int64_t* x_in, int64_t* x_out,
-                 int wrap32, hipStream_t s) {
-    const CombOp<OP> op{reinterpret_cast<const long long*>(x_in), reinterpret_cast<long long*>(x_out), wrap32};
+                 VecPos pos, int wrap32, hipStream_t s) {
+    const CombOp<OP> op{reinterpret_cast<const long long*>(x_in), reinterpret_cast<long long*>(x_out), pos, wrap32};
     launch_pull(c, plan, op, hub_partial, s);
 }
 
 }  // namespace
 
+// Sharded graphs: the gathered vector is the adjacency's own layout: IN / BOTH use their halo plans
+// (compact vectors, refreshed by the sparse halo exchange, or full length under "halo" = 0); OUT has
+// no halo plan and its columns are global padded ids, so its vector is full length and refreshed by
+// the dense allgather of the owned slices.
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
                  uint8_t* received_out) {
     if (direction < JG_DIR_OUT || direction > JG_DIR_BOTH) fail(JG_ERR_ARG, "direction must be JG_DIR_OUT/IN/BOTH");
     if (combiner < JG_COMBINE_SUM || combiner > JG_COMBINE_MAX) fail(JG_ERR_ARG, "unknown combiner");
     if (steps < 0) fail(JG_ERR_ARG, "negative step count");
-    if (g.P != 1) fail(JG_ERR_UNSUPPORTED, "combiner programs run on single-shard graphs");
-    Shard& sh = *g.shards[0];
-    // the receiver pulls over the reverse of the send scope: v's out-neighbours are its OUT row
-    const Csr& c = direction == JG_DIR_OUT ? sh.out : direction == JG_DIR_IN ? sh.in : sh.both;
-    if (!c.present())
+    const uint32_t adj = direction == JG_DIR_OUT ? JG_ADJ_OUT : direction == JG_DIR_IN ? JG_ADJ_IN : JG_ADJ_BOTH;
+    if (!(g.flags & adj))
         fail(JG_ERR_UNSUPPORTED, std::string("graph was built without the ") +
                                      (direction == JG_DIR_OUT ? "OUT" : direction == JG_DIR_IN ? "IN" : "BOTH") +
                                      " adjacency");
-    DeviceGuard dg(sh.device);
-    hipStream_t s = sh.stream;
-    const int64_t n = sh.rows;
-    // rows are degree-ranked vertices; the CSR's columns index the same order (one shard)
-    std::vector<int64_t> h(std::max<int64_t>(n, 1));
-    for (int64_t l = 0; l < n; ++l) {
-        const int64_t v = init ? init[sh.dense_of_local[l]] : 1;
-        h[l] = wrap32 ? (int64_t)(int32_t)v : v;
+    const size_t ns = g.shards.size();
+    struct St {
+        DevBuf<int64_t> x[2];
+        DevBuf<uint8_t> recv;
+        DevBuf<long long> hub_partial;
+        int64_t len = 0;
+        VecPos pos;
+    };
+    std::vector<St> st(ns);
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        hipStream_t s = sh.stream;
+        St& t = st[i];
+        const Csr& c = adj == JG_ADJ_OUT ? sh.out : adj == JG_ADJ_IN ? sh.in : sh.both;
+        if (adj == JG_ADJ_OUT) {
+            t.len = g.padded_len();
+            t.pos.base = (int64_t)sh.index * g.S;
+            if (!sh.plan_out_built) {
+                build_pull_plan(sh, sh.out, sh.plan_out, g.padded_len(), g.padded_len(), 8);
+                sh.plan_out_built = true;
+            }
+        } else {
+            t.len = g.vec_len(sh, adj);
+            t.pos = g.vec_pos(sh, adj);
+        }
+        const PullPlan& plan = adj == JG_ADJ_OUT ? sh.plan_out : adj == JG_ADJ_IN ? sh.plan_in : sh.plan_both;
+        const int64_t n = sh.rows;
+        t.x[0].alloc(std::max<int64_t>(t.len, 1));
+        t.x[1].alloc(std::max<int64_t>(t.len, 1));
+        t.recv.alloc(std::max<int64_t>(n, 1));
+        t.hub_partial.alloc(std::max<int64_t>(plan.num_chunks, 1));
+        // owned rows' initial messages at their slots (vertex order: sh.dense_of_local)
+        std::vector<int64_t> h(std::max<int64_t>(n, 1));
+        for (int64_t l = 0; l < n; ++l) {
+            const int64_t v = init ? init[sh.dense_of_local[l]] : 1;
+            h[l] = wrap32 ? (int64_t)(int32_t)v : v;
+        }
+        if (n) {
+            copy_h2d(t.x[0].get() + t.pos.base, h.data(), n * sizeof(int64_t), s);
+            has_entries_kernel<<<grid_for(n), kBlock, 0, s>>>(c.row_ptr.get(), n, t.recv.get());
+            JG_LAUNCH_CHECK();
+        }
     }
-    DevBuf<int64_t> x[2] = {DevBuf<int64_t>(std::max<int64_t>(n, 1)), DevBuf<int64_t>(std::max<int64_t>(n, 1))};
-    DevBuf<uint8_t> recv(std::max<int64_t>(n, 1));
-    if (n) copy_h2d(x[0].get(), h.data(), n * sizeof(int64_t), s);
-    if (n) {
-        has_entries_kernel<<<grid_for(n), kBlock, 0, s>>>(c.row_ptr.get(), n, recv.get());
-        JG_LAUNCH_CHECK();
-    }
-    PullPlan& plan = direction == JG_DIR_OUT ? sh.plan_out : direction == JG_DIR_IN ? sh.plan_in : sh.plan_both;
-    if (direction == JG_DIR_OUT && !sh.plan_out_built) {
-        build_pull_plan(sh, sh.out, sh.plan_out, g.padded_len(), g.padded_len(), 8);
-        sh.plan_out_built = true;
-    }
-    DevBuf<long long> hub_partial(std::max<int64_t>(plan.num_chunks, 1));
-    hipEvent_t t0, t1;
-    JG_HIP(hipEventCreate(&t0));
-    JG_HIP(hipEventCreate(&t1));
-    JG_HIP(hipEventRecord(t0, s));
-    int cur = 0;
-    for (int t = 0; t < steps && n > 0; ++t) {
-        const int64_t* xi = x[cur].get();
-        int64_t* xo = x[cur ^ 1].get();
-        if (combiner == JG_COMBINE_SUM)
-            launch_step<JG_COMBINE_SUM>(c, plan, hub_partial.get(), xi, xo, wrap32, s);
-        else if (combiner == JG_COMBINE_MIN)
-            launch_step<JG_COMBINE_MIN>(c, plan, hub_partial.get(), xi, xo, wrap32, s);
+    auto exchange = [&](int which) {
+        std::vector<void*> bufs;
+        for (auto& t : st) bufs.push_back(t.x[which].get());
+        if (adj == JG_ADJ_OUT)
+            exchange_allgather(g, bufs, sizeof(int64_t), ncclInt64);
         else
-            launch_step<JG_COMBINE_MAX>(c, plan, hub_partial.get(), xi, xo, wrap32, s);
+            exchange_vec(g, adj, bufs, sizeof(int64_t), ncclInt64);
+    };
+    Shard& sh0 = *g.shards[0];
+    hipEvent_t t0, t1;
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, sh0.stream));
+    }
+    int cur = 0;
+    for (int t = 0; t < steps; ++t) {
+        exchange(cur);  // the senders' previous-superstep messages reach every reader
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            if (sh.rows == 0) continue;
+            DeviceGuard dg(sh.device);
+            St& s_ = st[i];
+            const Csr& c = adj == JG_ADJ_OUT ? sh.out : adj == JG_ADJ_IN ? sh.in : sh.both;
+            const PullPlan& plan = adj == JG_ADJ_OUT ? sh.plan_out : adj == JG_ADJ_IN ? sh.plan_in : sh.plan_both;
+            const int64_t* xi = s_.x[cur].get();
+            int64_t* xo = s_.x[cur ^ 1].get();
+            if (combiner == JG_COMBINE_SUM)
+                launch_step<JG_COMBINE_SUM>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+            else if (combiner == JG_COMBINE_MIN)
+                launch_step<JG_COMBINE_MIN>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+            else
+                launch_step<JG_COMBINE_MAX>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+        }
         cur ^= 1;
     }
-    JG_HIP(hipEventRecord(t1, s));
-    JG_HIP(hipEventSynchronize(t1));
     float ms = 0;
-    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventRecord(t1, sh0.stream));
+        JG_HIP(hipEventSynchronize(t1));
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
     Ctx& cx = *g.ctx;
     cx.last = jg_stats{};
     cx.last.supersteps = steps;
@@ -142,14 +192,27 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
     cx.last.compute_ms = ms;
     cx.last.kernel_ms_total = ms;
     cx.last.kernel_launches = steps;
-    cx.last.algorithmic_bytes = (double)steps * (12.0 * (double)c.nnz + 16.0 * (double)n);
-    cx.last.edges_traversed = (double)steps * (double)c.nnz;
-    if (n) {
-        copy_d2h(h.data(), x[cur].get(), n * sizeof(int64_t), s);
+    double nnz = 0, rows = 0;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        const Csr& c = adj == JG_ADJ_OUT ? sh.out : adj == JG_ADJ_IN ? sh.in : sh.both;
+        nnz += (double)c.nnz;
+        rows += (double)sh.rows;
+    }
+    cx.last.algorithmic_bytes = (double)steps * (12.0 * nnz + 16.0 * rows);
+    cx.last.edges_traversed = (double)steps * nnz;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        const int64_t n = sh.rows;
+        if (n == 0) continue;
+        DeviceGuard dg(sh.device);
+        St& t = st[i];
+        std::vector<int64_t> h((size_t)n);
+        copy_d2h(h.data(), t.x[cur].get() + t.pos.base, n * sizeof(int64_t), sh.stream);
         for (int64_t l = 0; l < n; ++l) out[sh.dense_of_local[l]] = h[l];
         if (received_out) {
-            std::vector<uint8_t> rc(n);
-            copy_d2h(rc.data(), recv.get(), n, s);
+            std::vector<uint8_t> rc((size_t)n);
+            copy_d2h(rc.data(), t.recv.get(), n, sh.stream);
             for (int64_t l = 0; l < n; ++l) received_out[sh.dense_of_local[l]] = steps > 0 ? rc[l] : 0;
         }
     }

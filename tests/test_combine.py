@@ -163,3 +163,30 @@ def test_gpu_degree_counting_distance(mode):  # OLAPTest.degreeCountingDistance 
         want = sum(len(out[w]) for w in out[i])
         got = view.value(vs[i].id, "degree") if mode == "LOCALTX" else g.vertex(vs[i].id).value("degree")
         assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,halo", [(2, 1), (3, 1), (8, 1), (3, 0)])
+def test_gpu_combine_logical_shards(oracle_lib, shards, halo):
+    """Sharded combiner supersteps (IN / BOTH through the halo exchange or the dense allgather, OUT
+    through the allgather of owned slices) == the oracle."""
+    import janusgraph_amd as jg
+    scale = 12
+    n = 1 << scale
+    s, t = oracle_lib.rmat_edges(scale, 16, 21)
+    vid = (np.random.default_rng(4).permutation(n).astype(np.int64) + 1) << 8
+    init = np.random.default_rng(9).integers(-(1 << 31), 1 << 31, n)
+    ctx = jg.Context((0,) * shards)
+    jg._lib.tune_set("halo", halo)
+    try:
+        g = ctx.build(vid, vid[s], vid[t], flags=jg.ADJ_IN | jg.ADJ_OUT | jg.ADJ_BOTH)
+    finally:
+        jg._lib.tune_set("halo", 1)
+    for direction in (1, 2, 3):
+        for combiner in (0, 1):
+            x, rec = g.combine_steps(direction, combiner, 3, init, True)
+            ref, rref = oracle_lib.combine_steps(n, s, t, direction, combiner, 3, init, True)
+            np.testing.assert_array_equal(x, ref)
+            np.testing.assert_array_equal(rec, rref)
+    g.close()
+    ctx.close()
