@@ -146,8 +146,10 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n,
  * are filtered; a row whose first entry is not the VertexExists property is a ghost; the kept rows
  * are V (in row order, ids -> vid_out[nrows], count -> *num_vertices_out, both nullable) and their
  * OUT entries of visible user edges are the edges (ghost endpoints dropped as in jg_graph_build).
- * Unit weights.  Partitioned (vertex-cut) rows: JG_ERR_UNSUPPORTED; a malformed entry on a kept row
- * or a key with no user vertex type: JG_ERR_ARG.  Stats: build_ms (whole snapshot), kernel_ms_total
+ * Unit weights.  Partitioned (vertex-cut) vertices are one vertex, the canonical id
+ * (IDManager.java:525-551): every representative row adds its edges, only the canonical row's
+ * VertexExists decides the ghost rule (VertexProgramScanJob.java:88-102).  A malformed entry on a
+ * kept row or a key with no user vertex type: JG_ERR_ARG.  Stats: build_ms (whole snapshot), kernel_ms_total
  * (the decode kernels). */
 int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                              const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,

@@ -195,29 +195,58 @@ constexpr int64_t kVertexExistsId = (1 << 6) | 37;  // BaseKey.VertexExists: Sys
 // Error bits of the snapshot (any set bit fails the build before the CSR is cut)
 enum : int32_t { kErrBadKey = 1, kErrPartitioned = 2, kErrMalformed = 4 };
 
+// IDManager.getCanonicalVertexId (idmanagement/IDManager.java:525-547): a partitioned (vertex-cut)
+// vertex's representatives share its count; the canonical one sits in the partition hashed from it.
+__device__ __forceinline__ int64_t canonical_vertex_id(int64_t vid, int pbits) {
+    const uint64_t count = (uint64_t)vid >> (pbits + 3);
+    uint64_t h = 0;
+    for (int off = 0; off < 64; off += pbits) h ^= (count >> off) & ((1ull << pbits) - 1ull);
+    return (int64_t)((((count << pbits) + h) << 3) | 2u);
+}
+
+__device__ __forceinline__ bool is_partitioned(int64_t vid, int pbits) {
+    return vid > 0 && (vid & 7) == 2 && ((uint64_t)vid >> (pbits + 3)) > 0;
+}
+
 // One thread per row: vertex id, key filter, ghost rule (VertexJobConverter.process / isGhostVertex,
 // olap/VertexJobConverter.java:122-151: the row's first entry must be the VertexExists property;
-// system properties sort first, so it is entry 0 of the row when present).
+// system properties sort first, so it is entry 0 of the row when present).  Partitioned vertices
+// (VertexProgramScanJob.java:88-102; FulgoraVertexMemory.getCanonicalId): every representative row
+// contributes its edges to the canonical vertex; a non-canonical representative is never a ghost
+// and adds no vertex of its own.
+//   keep_edges[r]: the row's OUT entries are edges; keep_vertex[r]: the row is a vertex of V.
 __global__ __launch_bounds__(kBlock) void edgestore_rows_kernel(EntryView a, const uint64_t* __restrict__ keys,
                                                                  const int64_t* __restrict__ row_off, int64_t nrows,
-                                                                 int pbits, uint8_t* __restrict__ keep,
+                                                                 int pbits, uint8_t* __restrict__ keep_edges,
+                                                                 uint8_t* __restrict__ keep_vertex,
                                                                  int64_t* __restrict__ row_vid, int32_t* __restrict__ err) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t vid = key_to_vertex_id(keys[r], pbits);
-        uint8_t k = 0;
+        int64_t vid = key_to_vertex_id(keys[r], pbits);
+        uint8_t ke = 0, kv = 0;
         if (vid == -2) {
             atomicOr(err, kErrBadKey);
         } else if (vid >= 0) {
-            if ((vid & 7) == 2) {  // vertex-cut representatives need canonical-id aggregation
-                atomicOr(err, kErrPartitioned);
+            bool canonical = true;
+            if ((vid & 7) == 2) {
+                if (pbits == 0) {  // getPartitionHashForId: "no partition bits"
+                    atomicOr(err, kErrPartitioned);
+                } else {
+                    const int64_t c = canonical_vertex_id(vid, pbits);
+                    canonical = c == vid;
+                    vid = c;
+                }
+            }
+            if (!canonical) {
+                ke = 1;
             } else if (row_off[r + 1] > row_off[r]) {
                 const int64_t e = row_off[r];
                 const Decoded d = decode_entry(a, a.bytes + a.off[e], a.off[e + 1] - a.off[e], a.vpos[e]);
                 if (d.dir < 0) atomicOr(err, kErrMalformed);
-                k = (d.dir == 2 && d.type_id == kVertexExistsId) ? 1 : 0;
+                ke = kv = (d.dir == 2 && d.type_id == kVertexExistsId) ? 1 : 0;
             }
         }
-        keep[r] = k;
+        keep_edges[r] = ke;
+        keep_vertex[r] = kv;
         row_vid[r] = vid;
     }
 }
@@ -253,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void edgestore_edges_kernel(EntryView a, co
                                                                   const int64_t* __restrict__ block_row,
                                                                   int64_t nrows, int64_t nent,
                                                                   const uint8_t* __restrict__ keep,
-                                                                  const int64_t* __restrict__ row_vid,
+                                                                  const int64_t* __restrict__ row_vid, int pbits,
                                                                   uint8_t* __restrict__ take, int64_t* __restrict__ src,
                                                                   int64_t* __restrict__ dst, int32_t* __restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kStageWords];
@@ -317,7 +346,8 @@ __global__ __launch_bounds__(kBlock) void edgestore_edges_kernel(EntryView a, co
                 if (d.dir == 0 && d.visible) {
                     t = 1;
                     src[e] = row_vid[r];
-                    dst[e] = d.other;
+                    dst[e] = pbits > 0 && is_partitioned(d.other, pbits) ? canonical_vertex_id(d.other, pbits)
+                                                                        : d.other;
                 }
             }
             take[e] = t;
@@ -436,7 +466,7 @@ void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& 
                         DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms) {
     TypeTable tt(r.type_ids, r.type_mult, r.ntypes, s);
     const int64_t R = r.nrows, E = r.nentries;
-    DevBuf<uint8_t> d_bytes(r.nbytes + kBytePad), keep(std::max<int64_t>(R, 1)),
+    DevBuf<uint8_t> d_bytes(r.nbytes + kBytePad), keep(std::max<int64_t>(R, 1)), keep_v(std::max<int64_t>(R, 1)),
         take(std::max<int64_t>(E, 1));
     DevBuf<int64_t> d_off(E + 1), d_roff(R + 1), row_vid(std::max<int64_t>(R, 1)), esrc(std::max<int64_t>(E, 1)),
         edst(std::max<int64_t>(E, 1)), idx(std::max<int64_t>(std::max(R, E), 1));
@@ -458,14 +488,15 @@ void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& 
     JG_HIP(hipEventRecord(t0, s));
     if (R) {
         edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, d_keys.get(), d_roff.get(), R, r.pbits, keep.get(),
-                                                            row_vid.get(), err.get());
+                                                            keep_v.get(), row_vid.get(), err.get());
         JG_LAUNCH_CHECK();
     }
     if (E) {
         block_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(d_roff.get(), R, block_row.get());
         JG_LAUNCH_CHECK();
         edgestore_edges_kernel<<<grid_for((E + kEpt - 1) / kEpt, kBlock, 256 * 16), kBlock, 0, s>>>(
-            a, d_roff.get(), block_row.get(), R, E, keep.get(), row_vid.get(), take.get(), esrc.get(), edst.get(), err.get());
+            a, d_roff.get(), block_row.get(), R, E, keep.get(), row_vid.get(), r.pbits, take.get(), esrc.get(), edst.get(),
+            err.get());
         JG_LAUNCH_CHECK();
     }
     JG_HIP(hipEventRecord(t1, s));
@@ -478,10 +509,9 @@ void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& 
     JG_HIP(hipEventDestroy(t1));
     if (kernel_ms) *kernel_ms = ms;
     if (herr & kErrBadKey) fail(JG_ERR_ARG, "row key with an unrecognized vertex id type");
-    if (herr & kErrPartitioned)
-        fail(JG_ERR_UNSUPPORTED, "partitioned (vertex-cut) vertex rows: build from canonical ids with jg_graph_build");
+    if (herr & kErrPartitioned) fail(JG_ERR_ARG, "partitioned vertex row with no partition bits");
     if (herr & kErrMalformed) fail(JG_ERR_ARG, "malformed edgestore entry on a vertex row");
-    n = prim::compact_indices(keep.get(), R, idx.get(), s);
+    n = prim::compact_indices(keep_v.get(), R, idx.get(), s);
     vid.alloc(std::max<int64_t>(n, 1));
     if (n) {
         gather_kernel<int64_t><<<grid_for(n), kBlock, 0, s>>>(row_vid.get(), idx.get(), n, vid.get());

@@ -197,78 +197,60 @@ def key_to_vertex_id(keys, partition_bits=5):
     return vid
 
 
+def canonical_vertex_id(vid, partition_bits=5):
+    """IDManager.getCanonicalVertexId (graphdb/idmanagement/IDManager.java:525-547)."""
+    count = vid >> (partition_bits + 3)
+    h, off = 0, 0
+    while off < 64:
+        h ^= (count >> off) & ((1 << partition_bits) - 1)
+        off += partition_bits
+    return (((count << partition_bits) + h) << 3) | 2
+
+
 def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=(), partition_bits=5):
     """The scan -> snapshot step restated row by row (the checker of jg_graph_build_edgestore):
     VertexJobConverter.getKeyFilter drops invisible rows (olap/VertexJobConverter.java:174-177);
-    process/isGhostVertex keep a row only if its first entry is the VertexExists property (:122-151);
-    the kept rows' OUT entries of visible user edges are the edges (each edge is stored OUT on its
-    source row and IN on its target row, graphdb/database/StandardJanusGraph.java:617-640).
-    Returns (vid of kept rows in row order, src ids, dst ids); raises ValueError where Java throws."""
+    process/isGhostVertex keep a row only if its first entry is the VertexExists property (:122-151),
+    except a non-canonical representative of a partitioned vertex, which is never a ghost; the rows'
+    OUT entries of visible user edges are the edges (each edge is stored OUT on its source row and IN
+    on its target row, graphdb/database/StandardJanusGraph.java:617-640).  Partitioned vertices
+    (comp/VertexProgramScanJob.java:88-102, FulgoraVertexMemory.getCanonicalId) are one vertex: the
+    canonical id, whose edges are the union over its representative rows.
+    Returns (vid of kept vertices in row order, src ids, dst ids); raises ValueError where Java throws."""
     data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
     off, row_off = _i64(off), _i64(row_off)
     t, d, o, _ = decode_edges(data, off, vpos, type_ids, type_mult)
     vids = key_to_vertex_id(keys, partition_bits)
+
+    def canon(v):
+        if v > 0 and v & 7 == 2 and v >> (partition_bits + 3) > 0:
+            if partition_bits == 0:
+                raise ValueError("no partition bits")
+            return canonical_vertex_id(v, partition_bits)
+        return v
+
     keep_v, src, dst = [], [], []
     for r, vid in enumerate(vids):
+        vid = int(vid)
         e0, e1 = int(row_off[r]), int(row_off[r + 1])
         if vid == -1:
             continue
         if vid == -2:
             raise ValueError("row key with an unrecognized vertex id type")
-        if vid & 7 == 2:
-            raise NotImplementedError("partitioned (vertex-cut) vertex rows")
-        if e0 == e1:
-            continue
-        if d[e0] < 0:
-            raise ValueError("malformed entry")
-        if not (d[e0] == 2 and t[e0] == VERTEX_EXISTS_ID):
-            continue  # ghost vertex
-        keep_v.append(int(vid))
+        cv = canon(vid)
+        if cv == vid:  # a normal vertex, or the canonical representative: the ghost rule
+            if e0 == e1:
+                continue
+            if d[e0] < 0:
+                raise ValueError("malformed entry")
+            if not (d[e0] == 2 and t[e0] == VERTEX_EXISTS_ID):
+                continue  # ghost vertex
+            keep_v.append(cv)
         for e in range(e0, e1):
             if d[e] < 0:
                 raise ValueError("malformed entry")
             visible = (int(data[off[e]]) >> 6) == 1  # relation-type header prefix >> 1: 1 = user, visible
             if d[e] == 0 and visible:
-                src.append(int(vid))
-                dst.append(int(o[e]))
+                src.append(cv)
+                dst.append(canon(int(o[e])))
     return np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64)
-
-
-COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
-
-
-def combine_steps(n, src, dst, direction, combiner, steps, init=None, int32_wrap=True):
-    """Combiner vertex programs restated with numpy (checker of jg_combine_steps): `steps` supersteps
-    of x[v] = COMBINE over v's `direction` adjacency entries (v, w) of x[w]; DIR_OUT = v's out-edges
-    (messages sent on Local.of(inE), OLAPTest.java:429), BOTH = out- and in-entries (a self-loop
-    twice).  SUM of nothing is 0 (reduce(0, +)); MIN/MAX of nothing keeps the identity with
-    received = False.  Returns (x, received)."""
-    src, dst = np.asarray(src, np.int64), np.asarray(dst, np.int64)
-    x = np.ones(n, np.int64) if init is None else np.asarray(init, np.int64).copy()
-    if int32_wrap:
-        x = x.astype(np.int32).astype(np.int64)
-    rows, cols = [], []
-    if direction in (DIR_OUT, DIR_BOTH):
-        rows.append(src)
-        cols.append(dst)
-    if direction in (DIR_IN, DIR_BOTH):
-        rows.append(dst)
-        cols.append(src)
-    r = np.concatenate(rows) if rows else np.zeros(0, np.int64)
-    c = np.concatenate(cols) if cols else np.zeros(0, np.int64)
-    received = np.bincount(r, minlength=n)[:n] > 0 if len(r) else np.zeros(n, bool)
-    ident = {COMBINE_SUM: 0, COMBINE_MIN: np.iinfo(np.int64).max, COMBINE_MAX: np.iinfo(np.int64).min}[combiner]
-    for _ in range(steps):
-        y = np.full(n, ident, np.int64)
-        if combiner == COMBINE_SUM:
-            np.add.at(y, r, x[c])  # int64 wraps modulo 2^64; truncating to int32 gives the Java int sum
-            if int32_wrap:
-                y = y.astype(np.int32).astype(np.int64)
-        elif combiner == COMBINE_MIN:
-            np.minimum.at(y, r, x[c])
-        else:
-            np.maximum.at(y, r, x[c])
-        x = y
-    if steps == 0:
-        received = np.zeros(n, bool)
-    return x, received

@@ -16,7 +16,9 @@ from janusgraph_amd.idmanager import IDManager
 from oracle import edgecodec as ec
 
 
-def make_edgestore(n=300, m=2000, seed=0, ghosts=0.08, partition_bits=5):
+def make_edgestore(n=300, m=2000, seed=0, ghosts=0.08, partition_bits=5, partitioned=4):
+    """Returns (store arrays, (V, src, dst) by construction, OUT entries on live rows to ghosts)."""
+    from oracle.oracle import canonical_vertex_id
     rng = np.random.default_rng(seed)
     idm = IDManager(partition_bits)
     vids = []
@@ -29,7 +31,18 @@ def make_edgestore(n=300, m=2000, seed=0, ghosts=0.08, partition_bits=5):
         if v not in seen:
             seen.add(v)
             vids.append(v)
+    # vertex-cut vertices: the last `partitioned` indices get canonical ids and 3 representative rows
+    reps = {}
+    for i in range(n - partitioned, n):
+        count = int(rng.integers(1, 1 << 30))
+        canon = canonical_vertex_id((count << (partition_bits + 3)) | 2, partition_bits)
+        others = [(((count << partition_bits) + p) << 3) | 2 for p in range(1 << partition_bits)]
+        others = [x for x in others if x != canon]
+        pick = [others[int(k)] for k in rng.choice(len(others), 2, replace=False)]
+        vids[i] = canon
+        reps[i] = [canon] + pick
     ghost = rng.random(n) < ghosts
+    ghost[n - partitioned:] = False
     labels = [ec.schema_id(c, "user_edge") for c in (11, 12, 13, 14)]
     mults = [ec.MULTI, ec.SIMPLE, ec.ONE2MANY, ec.MANY2ONE]
     tids = np.array(labels[1:], np.int64)
@@ -42,40 +55,51 @@ def make_edgestore(n=300, m=2000, seed=0, ghosts=0.08, partition_bits=5):
     s[m // 50: m // 25] = s[0]   # a hub with multi-edges
     t[m // 50: m // 25] = t[0]
     lab = rng.integers(0, len(labels), m)
-    rows = [[] for _ in range(n)]  # (entry bytes, value position)
+    rows = {}  # row vertex id -> [(entry bytes, value position)]
+
+    def row_of(i):  # the row an entry of vertex i goes to (any representative of a partitioned one)
+        return reps[i][int(rng.integers(0, 3))] if i in reps else vids[i]
+
     rel = 1000
     for i in range(n):
-        if not ghost[i]:
-            rows[i].append(ec.encode_property(ec.schema_id(1, "system_key"), rel, b"\x01"))
+        for rv in reps.get(i, [vids[i]]):
+            rows.setdefault(rv, [])
+        if not ghost[i]:  # VertexExists lives on the (canonical) vertex row
+            rows[vids[i]].append(ec.encode_property(ec.schema_id(1, "system_key"), rel, b"\x01"))
             rel += 1
-        rows[i].append(ec.encode_property(name_key, rel, b"name%d" % i))
+        rows[vids[i]].append(ec.encode_property(name_key, rel, b"name%d" % i))
         rel += 1
         if rng.integers(0, 10) == 0:
-            rows[i].append(ec.encode_edge(sys_edge, ec.OUT, vids[int(rng.integers(0, n))], rel))
+            rows[vids[i]].append(ec.encode_edge(sys_edge, ec.OUT, vids[int(rng.integers(0, n))], rel))
             rel += 1
         if rng.integers(0, 10) == 0:  # an invisible user edge
-            rows[i].append(ec.encode_edge(labels[0], ec.OUT, vids[int(rng.integers(0, n))], rel, invisible=True))
+            rows[vids[i]].append(ec.encode_edge(labels[0], ec.OUT, vids[int(rng.integers(0, n))], rel,
+                                                invisible=True))
             rel += 1
     for e in range(m):
         a, b, L = int(s[e]), int(t[e]), int(lab[e])
-        rows[a].append(ec.encode_edge(labels[L], ec.OUT, vids[b], rel, mults[L]))
-        rows[b].append(ec.encode_edge(labels[L], ec.IN, vids[a], rel, mults[L]))
+        ra, rb = row_of(a), row_of(b)
+        rows[ra].append(ec.encode_edge(labels[L], ec.OUT, rb, rel, mults[L]))  # other = a representative id
+        rows[rb].append(ec.encode_edge(labels[L], ec.IN, ra, rel, mults[L]))
         rel += 1
-    keys = [idm.get_key(v) for v in vids]
+    row_ids = list(rows)
+    keys = [idm.get_key(v) for v in row_ids]
+    ents = [rows[v] for v in row_ids]
     # schema rows (odd keys) holding entries of their own, never decoded
     for c in (3, 7, 9):
         keys.append(ec.schema_id(c, "user_edge"))
-        rows.append([(b"\xff\xff\xff", 1)])
+        ents.append([(b"\xff\xff\xff", 1)])
+        row_ids.append(None)
     order = sorted(range(len(keys)), key=lambda r: keys[r])  # the scan is key-ordered
     data, off, vpos, roff = bytearray(), [0], [], [0]
     for r in order:
-        ents = sorted(rows[r], key=lambda ev: ev[0][: ev[1]])  # columns in byte order
-        for b, vp in ents:
+        for b, vp in sorted(ents[r], key=lambda ev: ev[0][: ev[1]]):  # columns in byte order
             data += b
             off.append(len(data))
             vpos.append(vp)
         roff.append(len(vpos))
-    live = [vids[r] for r in order if r < n and not ghost[r]]
+    index = {v: i for i, v in enumerate(vids)}
+    live = [row_ids[r] for r in order if row_ids[r] in index and not ghost[index[row_ids[r]]]]
     keep = [(e_s, e_t) for e_s, e_t in zip(s, t) if not ghost[e_s] and not ghost[e_t]]
     truth = (np.array(live, np.int64), np.array([vids[a] for a, _ in keep], np.int64),
              np.array([vids[b] for _, b in keep], np.int64))
@@ -154,13 +178,9 @@ def test_gpu_edgestore_edge_cases():
     g, vid = ctx.build_edgestore(np.zeros(0, np.uint64), [0], b"", [0], [])
     assert len(vid) == 0 and g.info()["num_edges"] == 0
     g.close()
-    # a partitioned (vertex-cut) row is refused, a malformed entry on a live row too
+    # a malformed entry on a live row is refused
     idm = IDManager(5)
     exists, vp = ec.encode_property(ec.schema_id(1, "system_key"), 1, b"\x01")
-    pv = (((5 << 5) + 1) << 3) | 0b010
-    with pytest.raises(jg.JanusGpuError) as ei:
-        ctx.build_edgestore([idm.get_key(pv)], [0, 1], exists, [0, len(exists)], [vp])
-    assert ei.value.code == -5
     lab = ec.schema_id(9, "user_edge")
     bad = ec.write_relation_type(lab, True, ec.OUT) + b"\x01\x02"
     v1 = idm.to_vertex_id(1)
