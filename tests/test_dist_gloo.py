@@ -252,3 +252,124 @@ def test_three_rank_gloo_halo_exchange(oracle_lib):
         assert ok_counts
         assert 0 < vol < dense  # the halo is a strict subset of the dense allgather
     assert res[0][4] <= 1e-12
+
+
+def _sd_worker(rank, ws, port, out_q):
+    """Sharded ShortestDistanceVertexProgram (jg_traverse.hip shortest_distance_sharded) modelled rank
+    by rank over gloo: the IN adjacency's halo layout as in _halo_worker; per superstep each rank
+    pushes min(msg[w] + weight) from its frontier rows into own rows and halo slots, the REVERSE
+    halo exchange (exchange_halo_reverse: segment for peer q goes back to q, landing at q's send-list
+    positions) hands remote candidates to their owners, owners take the min and apply; frontier
+    sizes are summed over ranks (allreduce_sum_i64)."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    import torch
+    import torch.distributed as dist
+
+    from oracle import oracle as o
+
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    scale, n = 9, 1 << 9
+    s, t = o.rmat_edges(scale, 8, 3)
+    s, t = s.astype(np.int32), t.astype(np.int32)
+    wt = (np.arange(len(s)) % 3 + 1).astype(np.int64)
+    indeg = np.bincount(t, minlength=n)
+    padded, S = padded_layout(indeg, ws)
+    gs, gt = padded[s], padded[t]
+    P, r = ws, rank
+    rq, cq = gt // S, gs // S
+    need = np.zeros(P * S, bool)
+    need[gs[(rq == r) & (cq != r)]] = True
+    send = np.zeros(P * S, bool)
+    sel = (cq == r) & (rq != r)
+    send[rq[sel] * S + gs[sel] % S] = True
+    recv_cnt = [int(need[q * S:(q + 1) * S].sum()) if q != r else 0 for q in range(P)]
+    send_lists = [np.flatnonzero(send[q * S:(q + 1) * S]) if q != r else np.zeros(0, np.int64) for q in range(P)]
+    T = 1 << 12
+    seg = lambda q: q + 1 if q < r else q  # noqa: E731
+    prefix = np.concatenate([[0], np.cumsum(need)])
+
+    def compact(g):
+        q, l = g // S, g % S
+        rk = prefix[g] - prefix[q * S]
+        return np.where(q == r, l, np.where(q < r, q + 1, q) * T + rk)
+
+    mine = rq == r
+    rows, cols, ws_ = gt[mine] - r * S, compact(gs[mine]), wt[mine]
+    key = np.lexsort((cols, rows))
+    rows, cols, ws_ = rows[key], cols[key], ws_[key]
+    ptr = np.searchsorted(rows, np.arange(S + 1))
+    INF, ABSENT = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+    seed_dense, max_depth = int(t[0]), 5
+    seed_g = int(padded[seed_dense])
+    best = np.full(P * T, INF, np.int64)
+    dist_ = np.full(S, ABSENT, np.int64)
+    msg = np.zeros(S, np.int64)
+    frontier = []
+    if seed_g // S == r:
+        dist_[seed_g % S] = 0
+        frontier = [seed_g % S]
+    total = torch.tensor([len(frontier)], dtype=torch.int64)
+    dist.all_reduce(total)
+    for _ in range(max_depth):
+        if int(total) == 0:
+            break
+        for w in frontier:  # ssd_push_kernel
+            for j in range(ptr[w], ptr[w + 1]):
+                best[cols[j]] = min(best[cols[j]], msg[w] + ws_[j])
+        reqs, bufs = [], {}  # exchange_halo_reverse
+        for q in range(P):
+            if q == r:
+                continue
+            if recv_cnt[q]:
+                reqs.append(dist.isend(torch.from_numpy(best[seg(q) * T:seg(q) * T + recv_cnt[q]].copy()), q))
+            if len(send_lists[q]):
+                bufs[q] = torch.zeros(len(send_lists[q]), dtype=torch.int64)
+                reqs.append(dist.irecv(bufs[q], q))
+        for x in reqs:
+            x.wait()
+        for q, b in bufs.items():  # ssd_recv_kernel
+            np.minimum.at(best, send_lists[q], b.numpy())
+        for q in range(P):
+            if q != r:
+                best[seg(q) * T:seg(q) * T + recv_cnt[q]] = INF
+        nxt = []  # sd_apply_kernel
+        for u in np.flatnonzero(best[:S] != INF):
+            b = best[u]
+            best[u] = INF
+            if dist_[u] == ABSENT or dist_[u] > b:
+                dist_[u] = b
+                msg[u] = b
+                nxt.append(int(u))
+        frontier = nxt
+        total = torch.tensor([len(frontier)], dtype=torch.int64)
+        dist.all_reduce(total)
+    parts = [None] * ws
+    dist.all_gather_object(parts, (r, dist_.tolist()))
+    full = np.zeros(ws * S, np.int64)
+    for rr, vals in parts:
+        full[rr * S:(rr + 1) * S] = vals
+    got = np.where(full[padded] == ABSENT, -1, full[padded])
+    ok = None
+    if rank == 0:
+        ref = o.shortest_distance(n, s, t, seed_dense, max_depth, wt.astype(np.int32))
+        ok = bool(np.array_equal(got, ref)) and int((ref >= 0).sum()) > 1
+    out_q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_sharded_shortest_distance(oracle_lib):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sd_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] is True
