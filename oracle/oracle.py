@@ -254,3 +254,43 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
                 src.append(cv)
                 dst.append(canon(int(o[e])))
     return np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64)
+
+
+COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
+
+
+def combine_steps(n, src, dst, direction, combiner, steps, init=None, int32_wrap=True):
+    """Combiner vertex programs restated with numpy (checker of jg_combine_steps): `steps` supersteps
+    of x[v] = COMBINE over v's `direction` adjacency entries (v, w) of x[w]; DIR_OUT = v's out-edges
+    (messages sent on Local.of(inE), OLAPTest.java:429), BOTH = out- and in-entries (a self-loop
+    twice).  SUM of nothing is 0 (reduce(0, +)); MIN/MAX of nothing keeps the identity with
+    received = False.  Returns (x, received)."""
+    src, dst = np.asarray(src, np.int64), np.asarray(dst, np.int64)
+    x = np.ones(n, np.int64) if init is None else np.asarray(init, np.int64).copy()
+    if int32_wrap:
+        x = x.astype(np.int32).astype(np.int64)
+    rows, cols = [], []
+    if direction in (DIR_OUT, DIR_BOTH):
+        rows.append(src)
+        cols.append(dst)
+    if direction in (DIR_IN, DIR_BOTH):
+        rows.append(dst)
+        cols.append(src)
+    r = np.concatenate(rows) if rows else np.zeros(0, np.int64)
+    c = np.concatenate(cols) if cols else np.zeros(0, np.int64)
+    received = np.bincount(r, minlength=n)[:n] > 0 if len(r) else np.zeros(n, bool)
+    ident = {COMBINE_SUM: 0, COMBINE_MIN: np.iinfo(np.int64).max, COMBINE_MAX: np.iinfo(np.int64).min}[combiner]
+    for _ in range(steps):
+        y = np.full(n, ident, np.int64)
+        if combiner == COMBINE_SUM:
+            np.add.at(y, r, x[c])  # int64 wraps modulo 2^64; truncating to int32 gives the Java int sum
+            if int32_wrap:
+                y = y.astype(np.int32).astype(np.int64)
+        elif combiner == COMBINE_MIN:
+            np.minimum.at(y, r, x[c])
+        else:
+            np.maximum.at(y, r, x[c])
+        x = y
+    if steps == 0:
+        received = np.zeros(n, bool)
+    return x, received
