@@ -1,3 +1,6 @@
+#!/bin/bash
+# Round validation on the GPU box: the whole -m gpu suite, smoke(), the bench line and the rocprofv3
+# kernel stats of the same bench command.  Usage: bash tools/gpu_final.sh <tag> -> gpurun_out/<tag>/
 set -o pipefail
 OUT=gpurun_out/${1:-f1}
 mkdir -p $OUT
