@@ -939,7 +939,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
             a.sbits = tune().pull_split ? 8 : 0;
             build_csr(sh, a, wt, csr, s);
             // the gathered vector of the split: PageRank's fp64 contributions (IN), CC's int32 labels (BOTH)
-            build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 0 ? 8 : 4);
+            build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 2 ? 4 : 8);
             if (halo.on) {  // segmented compact vector: every segment's hot entries are its prefix
                 plan.lds_ok = true;
                 plan.seg_tbits = halo.tbits;
@@ -955,8 +955,14 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         };
         if (g.flags & JG_ADJ_IN) build_pull_csr(0, w, sh.in, sh.plan_in, sh.halo_in);
         if (g.flags & JG_ADJ_OUT) {
-            a.which = 1;
-            build_csr(sh, a, w, sh.out, s);
+            if (P == 1) {  // one shard: OUT gets the sliced split too (combiner programs over out-edges)
+                Halo none;
+                build_pull_csr(1, w, sh.out, sh.plan_out, none);
+                sh.plan_out_built = true;
+            } else {  // sharded OUT has no halo plan: global columns, class plan built on first use
+                a.which = 1;
+                build_csr(sh, a, w, sh.out, s);
+            }
         }
         if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, nullptr, sh.both, sh.plan_both, sh.halo_both);
         JG_HIP(hipStreamSynchronize(s));

@@ -72,11 +72,12 @@ __global__ void has_entries_kernel(const int64_t* __restrict__ row_ptr, int64_t 
         f[r] = row_ptr[r + 1] > row_ptr[r];
 }
 
+// split_partial (nullable): the IN / BOTH plans' XCD-sliced merge bands, as PageRank and CC use them
 template <int OP>
-void launch_step(const Csr& c, const PullPlan& plan, long long* hub_partial, const int64_t* x_in, int64_t* x_out,
-                 VecPos pos, int wrap32, hipStream_t s) {
+void launch_step(const Csr& c, const PullPlan& plan, long long* hub_partial, long long* split_partial,
+                 const int64_t* x_in, int64_t* x_out, VecPos pos, int wrap32, hipStream_t s) {
     const CombOp<OP> op{reinterpret_cast<const long long*>(x_in), reinterpret_cast<long long*>(x_out), pos, wrap32};
-    launch_pull(c, plan, op, hub_partial, s);
+    launch_pull(c, plan, op, hub_partial, s, nullptr, nullptr, split_partial);
 }
 
 }  // namespace
@@ -99,7 +100,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
     struct St {
         DevBuf<int64_t> x[2];
         DevBuf<uint8_t> recv;
-        DevBuf<long long> hub_partial;
+        DevBuf<long long> hub_partial, split_partial;
         int64_t len = 0;
         VecPos pos;
     };
@@ -127,6 +128,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
         t.x[1].alloc(std::max<int64_t>(t.len, 1));
         t.recv.alloc(std::max<int64_t>(n, 1));
         t.hub_partial.alloc(std::max<int64_t>(plan.num_chunks, 1));
+        if (plan.split_rows > 0) t.split_partial.alloc(plan.split_partial_len());
         // owned rows' initial messages at their slots (vertex order: sh.dense_of_local)
         std::vector<int64_t> h(std::max<int64_t>(n, 1));
         for (int64_t l = 0; l < n; ++l) {
@@ -168,11 +170,14 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
             const int64_t* xi = s_.x[cur].get();
             int64_t* xo = s_.x[cur ^ 1].get();
             if (combiner == JG_COMBINE_SUM)
-                launch_step<JG_COMBINE_SUM>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+                launch_step<JG_COMBINE_SUM>(c, plan, s_.hub_partial.get(), s_.split_partial.get(), xi, xo, s_.pos, wrap32,
+                                            sh.stream);
             else if (combiner == JG_COMBINE_MIN)
-                launch_step<JG_COMBINE_MIN>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+                launch_step<JG_COMBINE_MIN>(c, plan, s_.hub_partial.get(), s_.split_partial.get(), xi, xo, s_.pos, wrap32,
+                                            sh.stream);
             else
-                launch_step<JG_COMBINE_MAX>(c, plan, s_.hub_partial.get(), xi, xo, s_.pos, wrap32, sh.stream);
+                launch_step<JG_COMBINE_MAX>(c, plan, s_.hub_partial.get(), s_.split_partial.get(), xi, xo, s_.pos, wrap32,
+                                            sh.stream);
         }
         cur ^= 1;
     }
