@@ -127,7 +127,8 @@ def cpu_baseline(scale, ef, seed, steps):
     ptr, col = o.build_in_csr(n, s32, d32)
     outdeg = np.bincount(s32, minlength=n).astype(np.float64)
     del s32, d32
-    contrib = (1.0 / n) / outdeg
+    with np.errstate(divide="ignore"):  # sinks: never gathered (no out-edges), as in the kernels
+        contrib = (1.0 / n) / outdeg
     t0 = time.perf_counter()
     for _ in range(steps):
         contrib = o.pagerank_superstep_csr(n, ptr, col, contrib, outdeg, 0.85, n)
