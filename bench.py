@@ -175,7 +175,6 @@ def main():
     # roofline of the dominant kernel (pull SpMV), HIP events on its stream, this rank's launches
     launches = max(st["kernel_launches"], 1)
     kern_ms = st["kernel_ms_total"] / launches
-    local_nnz = m if ws == 1 else None
     alg_bytes_launch = 12.0 * m / ws + 32.0 * n / ws  # SURVEY §8d per-edge/per-vertex bytes x this rank's share
     if ws == 1:
         alg_bytes_launch = 12.0 * m + 32.0 * n
@@ -186,7 +185,6 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "PageRank superstep (pull_merge_kernel x bands + fixups + light-row pull_kernel + finalize kernels, PrOp)", "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": alg_bytes_launch}
-    del local_nnz
 
     bfs = None
     if not args.no_bfs and ws == 1:
@@ -218,7 +216,7 @@ def main():
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (Graph500 Kronecker RMAT, on-device generator)",
             "config": {"workload": f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}", "n": n, "m": m,
-                       "parallelism": f"1d-vertex-partition x{ws}, RCCL allgather" if ws > 1 else "single GPU",
+                       "parallelism": f"1d-vertex-partition x{ws}, RCCL halo send/recv" if ws > 1 else "single GPU",
                        "build_ms": round(build_ms, 1), "truncated_vertices": info["truncated_vertices"]},
             "roofline": roofline, "cpu_baseline": cpu, "bfs": bfs,
         }
