@@ -224,8 +224,8 @@ int jg_decode_edges(jg_ctx* ctx, const uint8_t* bytes, int64_t nbytes, const int
 int jg_graph_sync(jg_graph* g);
 
 /* Process-wide performance knobs (no effect on results): "pull_unroll" (4 | 8 gathers in flight per
- * lane), "pull_nt" (0 | 1: non-temporal loads of the streamed adjacency), "pull_lds", "slice_lds",
- * "pull_short", "pull_overlap"; read when a graph is built: "pull_split", "band<i>_deg",
+ * lane), "pull_nt" (0 | 1: non-temporal loads of the streamed adjacency), "pull_lds", "light_lds",
+ * "slice_lds", "pull_short", "pull_overlap"; read when a graph is built: "pull_split", "band<i>_deg",
  * "band<i>_bit", "halo" (sharded graphs: sparse halo exchange, 0 = dense allgather).
  * Unknown key: JG_ERR_ARG. */
 int jg_tune_set(const char* key, int64_t value);

@@ -243,6 +243,9 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "pull_lds") {
         JG_ARG(value >= 0, "pull_lds must be >= 0");
         jg::tune().pull_lds = value;
+    } else if (k == "light_lds") {
+        JG_ARG(value >= 0, "light_lds must be >= 0");
+        jg::tune().light_lds = value;
     } else if (k.rfind("band", 0) == 0 && k.size() == 9 && k[4] >= '0' && k[4] <= '3' &&
                (k.substr(5) == "_deg" || k.substr(5) == "_bit")) {
         const int i = k[4] - '0';  // band<i>_deg: minimum degree (0: band unused); band<i>_bit: log2 sub-slices

@@ -357,6 +357,9 @@ struct Tune {
     int fuse_finalize = 1;            // light rows and the split's finalize in one launch
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
+    int64_t light_lds = 0;            // >0, with the split: the light rows run persistent with this many
+                                      // hottest elements in LDS (unfused from the split's finalize;
+                                      // measured: 5% slower than the fused launch at RMAT-24 and 26)
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha

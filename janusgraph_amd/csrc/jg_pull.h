@@ -719,8 +719,24 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             ++fb.n;
         }
     }
-    const bool fuse = split && tune().fuse_finalize && !pull_split_launches() && side == nullptr;
-    if (fuse) {
+    // light rows through the persistent LDS-prefix kernel (every hub row is inside the split, so the
+    // light args hold no chunk work)
+    const bool light_lds = split && tune().light_lds > 0 && plan.lds_ok && plan.nseg == 1 &&
+                           plan.max_hub_row < plan.split_rows && !pull_split_launches() && side == nullptr;
+    const bool fuse = split && tune().fuse_finalize && !pull_split_launches() && side == nullptr && !light_lds;
+    if (light_lds) {
+        const int32_t hot = (int32_t)std::min<int64_t>(tune().light_lds, kMaxLdsBytes / (int64_t)sizeof(T));
+        static bool attr_l = false;
+        if (!attr_l) {
+            JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
+            attr_l = true;
+        }
+        if (a.class_block_begin[kNumClasses] > a.class_block_begin[1])
+            pull_lds_kernel<Op, 4, false><<<(unsigned)device_cu_count() * (hot <= 8192 ? 2u : 1u), kLdsThreads,
+                                            (size_t)hot * sizeof(T), s>>>(a, op, hot);
+        JG_LAUNCH_CHECK();
+    } else if (fuse) {
         const int64_t fin_blocks = (plan.split_rows + kBlock - 1) / kBlock;
         const unsigned grid = (unsigned)(fin_blocks + blocks);
         if (tune().pull_unroll >= 8)

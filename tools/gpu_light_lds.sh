@@ -1,0 +1,9 @@
+# light_lds knob: parity of the variant, then A/B at RMAT-24 and RMAT-26 -> gpurun_out/ll/
+set -o pipefail
+mkdir -p gpurun_out/ll
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "pull_engine_variants" > gpurun_out/ll/pytest.log 2>&1 || exit 3
+V="base: l4k:light_lds=4096 l8k:light_lds=8192 l20k:light_lds=20480"
+timeout -k 10 300 python -u tools/pr_ab.py --scale 24 --steps 20 --rounds 4 $V > gpurun_out/ll/s24.json 2> gpurun_out/ll/s24.err || exit 4
+timeout -k 10 400 python -u tools/pr_ab.py --scale 26 --steps 10 --rounds 3 $V > gpurun_out/ll/s26.json 2> gpurun_out/ll/s26.err || exit 5
+echo ok
