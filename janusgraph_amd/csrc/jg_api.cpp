@@ -149,7 +149,11 @@ void prof_record_start(Ctx& c, Shard& sh) {
     sh.prof_events.push_back(e);
 }
 
-void prof_record_stop(Ctx& c, Shard& sh) { prof_record_start(c, sh); }
+void prof_record_stop(Ctx& c, Shard& sh, int units) {
+    if (!c.profiling) return;
+    prof_record_start(c, sh);
+    sh.prof_units.push_back(units);
+}
 
 void prof_collect(Ctx& c, Graph& g) {
     double total = 0;
@@ -162,10 +166,11 @@ void prof_collect(Ctx& c, Graph& g) {
             float ms = 0;
             JG_HIP(hipEventElapsedTime(&ms, sh.prof_events[i], sh.prof_events[i + 1]));
             total += ms;
-            ++launches;
+            launches += i / 2 < sh.prof_units.size() ? sh.prof_units[i / 2] : 1;
         }
         for (auto e : sh.prof_events) (void)hipEventDestroy(e);
         sh.prof_events.clear();
+        sh.prof_units.clear();
     }
     c.last.kernel_ms_total += total;
     c.last.kernel_launches += launches;

@@ -206,6 +206,7 @@ struct Shard {
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
+    std::vector<int> prof_units;          // supersteps each pair spans
 };
 
 struct Graph {
@@ -385,7 +386,7 @@ SideStream& side_stream();
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);
 void prof_record_start(Ctx& c, Shard& sh);
-void prof_record_stop(Ctx& c, Shard& sh);
+void prof_record_stop(Ctx& c, Shard& sh, int units = 1);
 void prof_collect(Ctx& c, Graph& g);
 
 }  // namespace jg
