@@ -73,3 +73,16 @@ def test_struct_layouts_match_the_header(tmp_path):
 
 def test_header_compiles_as_plain_c():
     subprocess.check_call(["gcc", "-std=c99", "-fsyntax-only", "-Wall", "-Werror", "-x", "c", HEADER])
+
+
+def test_tune_keys_validate_without_a_gpu():
+    """jg_tune_set accepts every documented knob and reports bad keys / values as JG_ERR_ARG."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    jg.load()
+    for k, v in (("pull_lds", 0), ("light_lds", 0), ("pull_unroll", 4), ("merge_temporal", 1), ("band1_bit", 3)):
+        _lib.tune_set(k, v)
+    for k, v in (("light_lds", -1), ("pull_unroll", 5), ("band1_bit", 2), ("no_such_knob", 1)):
+        with pytest.raises(jg.JanusGpuError) as e:
+            _lib.tune_set(k, v)
+        assert e.value.code == -1
