@@ -248,6 +248,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "pull_lds") {
         JG_ARG(value >= 0, "pull_lds must be >= 0");
         jg::tune().pull_lds = value;
+    } else if (k == "merge_overlap") {
+        jg::tune().merge_overlap = value != 0;
     } else if (k == "light_lds") {
         JG_ARG(value >= 0, "light_lds must be >= 0");
         jg::tune().light_lds = value;

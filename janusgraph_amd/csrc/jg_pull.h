@@ -653,9 +653,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
             attr = true;
         }
-        for (const auto& bp : plan.bands) {
-            const SliceBand& bd = *bp;
+        SideStream* mside = nullptr;
+        if (tune().merge_overlap && side == nullptr && plan.bands.size() > 1) {
+            mside = &side_stream();
+            JG_HIP(hipEventRecord(mside->fork, s));
+            JG_HIP(hipStreamWaitEvent(mside->stream, mside->fork, 0));
+        }
+        for (size_t bi = 0; bi < plan.bands.size(); ++bi) {
+            const SliceBand& bd = *plan.bands[bi];
             if (bd.tasks == 0) continue;
+            const hipStream_t ms = (mside && bi > 0) ? mside->stream : s;
             MergeArgs ma{bd.col.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(), bd.sub_end.get(),
                          bd.sub_base.get(), bd.tasks, bd.bits};
             T* part = split_partial + bd.part_off;
@@ -675,11 +682,15 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
             const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
             if (hs.hs > 0)
-                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), s>>>(
+                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), ms>>>(
                     ma, op, part, carry, hs, temporal);
             else
-                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, s>>>(ma, op, part, carry, hs, temporal);
+                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, ms>>>(ma, op, part, carry, hs, temporal);
             JG_LAUNCH_CHECK();
+        }
+        if (mside) {
+            JG_HIP(hipEventRecord(mside->join, mside->stream));
+            JG_HIP(hipStreamWaitEvent(s, mside->join, 0));
         }
         FixupBands fx{};
         for (const auto& bp : plan.bands) {
