@@ -670,10 +670,11 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
             const int64_t S = 1ll << bd.bits, gsz = 16 * S;
             // a multiple of S workgroups: every sub-slice gets grid / S of them
-            const unsigned grid = (unsigned)std::max<int64_t>(S, device_cu_count() / S * S);
+            const int wpc = tune().merge_wgs;
+            const unsigned grid = (unsigned)std::max<int64_t>(S, (int64_t)device_cu_count() * wpc / S * S);
             // shared equally by the segments; a segment's hot part stays below its stride (the
             // past-the-end sentinel INT32_MAX must test cold)
-            const int64_t hot_max = (int64_t)(kMergeLdsBytes / sizeof(T) - 16) * S;
+            const int64_t hot_max = (int64_t)(kMergeLdsBytes / wpc / sizeof(T) - 16) * S;
             const bool lds_ok = plan.lds_ok && tune().slice_lds;
             HotSegs hs;
             hs.tbits = plan.seg_tbits;
