@@ -248,6 +248,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "pull_lds") {
         JG_ARG(value >= 0, "pull_lds must be >= 0");
         jg::tune().pull_lds = value;
+    } else if (k == "fin_last") {
+        jg::tune().fin_last = value != 0;
     } else if (k == "merge_wgs") {
         JG_ARG(value == 1 || value == 2, "merge_wgs must be 1 or 2");
         jg::tune().merge_wgs = (int)value;

@@ -358,6 +358,8 @@ struct Tune {
     int fuse_finalize = 1;            // light rows and the split's finalize in one launch
     int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
     int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
+    int fin_last = 0;                 // fused light+finalize launch: light-row blocks first (1) or last (0)
+                                      // (measured: no difference at RMAT-24 or 26)
     int merge_wgs = 1;                // merge workgroups per CU (1 or 2): 2 halves each one's LDS image
                                       // (measured: 2 is 17% slower at RMAT-24, 11% at RMAT-26)
     int merge_overlap = 0;            // with the split: band i > 0 merge launches run on the side stream

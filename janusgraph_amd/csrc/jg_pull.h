@@ -614,13 +614,18 @@ __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a,
                                                                      typename Op::T* __restrict__ hub_partial,
                                                                      FinalizeBands fb,
                                                                      const typename Op::T* __restrict__ partial,
-                                                                     int64_t split_rows, int64_t fin_blocks) {
-    if ((int64_t)blockIdx.x < fin_blocks) {
-        const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+                                                                     int64_t split_rows, int64_t fin_blocks,
+                                                                     int fin_last) {
+    // fin_last: the light-row blocks first, the finalize blocks after them (Tune::fin_last)
+    const int64_t light_blocks = (int64_t)gridDim.x - fin_blocks;
+    const int64_t fb0 = fin_last ? light_blocks : 0;
+    const int64_t b = blockIdx.x;
+    if (b >= fb0 && b < fb0 + fin_blocks) {
+        const int64_t r = (b - fb0) * kBlock + threadIdx.x;
         if (r < split_rows) slice_finalize_row(r, op, fb, partial);
         return;
     }
-    pull_block<Op, U, NT>(a, op, hub_partial, (int64_t)blockIdx.x - fin_blocks + a.block_offset);
+    pull_block<Op, U, NT>(a, op, hub_partial, (fin_last ? b : b - fin_blocks) + a.block_offset);
 }
 
 // Enqueue one pull superstep on `s`.
@@ -753,10 +758,10 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         const unsigned grid = (unsigned)(fin_blocks + blocks);
         if (tune().pull_unroll >= 8)
             pull_light_finalize_kernel<Op, 8, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                            plan.split_rows, fin_blocks);
+                                                                            plan.split_rows, fin_blocks, tune().fin_last);
         else
             pull_light_finalize_kernel<Op, 4, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                            plan.split_rows, fin_blocks);
+                                                                            plan.split_rows, fin_blocks, tune().fin_last);
         JG_LAUNCH_CHECK();
     } else if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
         const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));

@@ -305,7 +305,7 @@ def test_errors_are_status_codes(ctx):
         g.pagerank_step(1)
 
 
-@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2"])
+@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -320,7 +320,8 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "split_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
              "split_light_lds": [("pull_split", 1), ("light_lds", 8192)],
              "split_merge_overlap": [("pull_split", 1), ("merge_overlap", 1)],
-             "split_merge_wgs2": [("pull_split", 1), ("merge_wgs", 2)]}[mode]
+             "split_merge_wgs2": [("pull_split", 1), ("merge_wgs", 2)],
+             "split_fin_last": [("pull_split", 1), ("fin_last", 1)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -345,6 +346,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("light_lds", 0)
         _lib.tune_set("merge_overlap", 0)
         _lib.tune_set("merge_wgs", 1)
+        _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("slice_lds", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0)):
