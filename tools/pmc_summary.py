@@ -1,7 +1,7 @@
 """Summarise a tools/profile_round.sh output directory into profiles/<tag>/summary.json.
 
 Traffic per PageRank superstep = the sum over every kernel of the superstep (pull_merge_kernel,
-pull_merge_fixup_kernel, pull_kernel, the finalize kernels; PrOp instantiations) of the L2 <-> fabric
+pull_merge_fixup_kernel, pull_kernel, the fused light+finalize and the finalize kernels; PrOp instantiations) of the L2 <-> fabric
 bytes, from rocprofv3 PMC passes (MI355X_MICROARCH.md §HBM: FETCH_SIZE = TCC_EA0_RDREQ x 64 B on
 gfx950 and under-counts 128-B requests by 2x, so the reads are recomputed from the request-size
 split: 32*n32 + 64*n64 + 128*n128; writes: 64*n64 + 32*(n - n64)).  Infinity-Cache hits are counted
@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 SUPERSTEP = ("pull_merge_kernel", "pull_merge_fixup_kernel", "pull_kernel", "pull_slice_finalize_kernel",
-             "pull_hub_finalize_kernel", "pull_lds_kernel")
+             "pull_hub_finalize_kernel", "pull_lds_kernel", "pull_light_finalize_kernel")
 
 
 def counters(path):
