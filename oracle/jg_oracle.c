@@ -376,22 +376,19 @@ JO_API void jo_lex_rank(const int64_t* vid, int64_t n, int32_t* rank) {
  *   (maxIterations = 100).
  * Labels are carried as lex ranks (bijective with the strings).  Returns memory().getIteration().
  * ------------------------------------------------------------------------------------------ */
-JO_API int jo_connected_components(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
-                                   const int64_t* vid, int max_iterations, int64_t* comp_vid) {
-    int32_t* rank = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-    int64_t* vid_of_rank = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
-    jo_lex_rank(vid, n, rank);
-    for (int64_t v = 0; v < n; ++v) vid_of_rank[rank[v]] = vid[v];
-    jo_csr c;
-    jo_csr_build_both(n, m, src, dst, &c);
-    int32_t* label = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+/* The superstep loop of the restatement above over a BOTH adjacency given as CSR (rows = vertices,
+ * entries = neighbours, any order inside a row: the String-min fold does not depend on it) and the
+ * lex rank of every vertex.  label[v] = the rank of v's component label.  Returns getIteration(). */
+JO_API int jo_cc_csr(int64_t n, const int64_t* ptr, const int32_t* other, const int32_t* rank,
+                     int max_iterations, int32_t* label) {
     int32_t* label_prev = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     unsigned char* sent = (unsigned char*)malloc((size_t)(n > 0 ? n : 1));
     unsigned char* sent_next = (unsigned char*)malloc((size_t)(n > 0 ? n : 1));
     int any = 0;
+#pragma omp parallel for schedule(static) reduction(| : any)
     for (int64_t v = 0; v < n; ++v) {
         label[v] = rank[v];
-        sent[v] = c.ptr[v + 1] > c.ptr[v];
+        sent[v] = ptr[v + 1] > ptr[v];
         any |= sent[v];
     }
     int iteration = 0;
@@ -404,8 +401,8 @@ JO_API int jo_connected_components(int64_t n, int64_t m, const int32_t* src, con
         for (int64_t v = 0; v < n; ++v) {
             int32_t cur = label_prev[v];
             int diff = 0;
-            for (int64_t k = c.ptr[v]; k < c.ptr[v + 1]; ++k) {
-                const int32_t u = c.other[k];
+            for (int64_t k = ptr[v]; k < ptr[v + 1]; ++k) {
+                const int32_t u = other[k];
                 if (sent[u] && label_prev[u] < cur) { cur = label_prev[u]; diff = 1; }
             }
             sent_next[v] = (unsigned char)diff;
@@ -413,10 +410,229 @@ JO_API int jo_connected_components(int64_t n, int64_t m, const int32_t* src, con
         }
         unsigned char* t = sent; sent = sent_next; sent_next = t;
     }
+    free(label_prev); free(sent); free(sent_next);
+    return iteration;
+}
+
+JO_API int jo_connected_components(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
+                                   const int64_t* vid, int max_iterations, int64_t* comp_vid) {
+    int32_t* rank = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int64_t* vid_of_rank = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    jo_lex_rank(vid, n, rank);
+    for (int64_t v = 0; v < n; ++v) vid_of_rank[rank[v]] = vid[v];
+    jo_csr c;
+    jo_csr_build_both(n, m, src, dst, &c);
+    int32_t* label = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    const int iteration = jo_cc_csr(n, c.ptr, c.other, rank, max_iterations, label);
     for (int64_t v = 0; v < n; ++v) comp_vid[v] = vid_of_rank[label[v]];
-    free(rank); free(vid_of_rank); free(label); free(label_prev); free(sent); free(sent_next);
+    free(rank); free(vid_of_rank); free(label);
     jo_csr_free(&c);
     return iteration;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Full-size checkers (BASELINE.json configs at RMAT scale 20-26; tests/test_gpu_configs.py).
+ * The restatements above build ordered CSRs serially, which is minutes at 2^26 vertices; these
+ * build the same adjacency in parallel and run the same semantics on it.
+ * ------------------------------------------------------------------------------------------ */
+
+/* CSR with rows = key[e], entries = other[e] (both = 1: also rows = other, entries = key, so a
+ * self-loop appears twice, as jo_csr_build_both).  Entry order inside a row is unspecified (atomic
+ * fill): use only where the result does not depend on it (BFS depth, CC labels) or where it
+ * changes rounding only (PageRank sums, far below the 1e-9 bar).  ptr[n+1], out[m or 2m]. */
+JO_API void jo_csr_unordered(int64_t n, int64_t m, const int32_t* key, const int32_t* other, int both,
+                             int64_t* ptr, int32_t* out) {
+    int64_t* fill = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+#pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < m; ++e) {
+        __atomic_fetch_add(&fill[key[e]], 1, __ATOMIC_RELAXED);
+        if (both) __atomic_fetch_add(&fill[other[e]], 1, __ATOMIC_RELAXED);
+    }
+    ptr[0] = 0;
+    for (int64_t v = 0; v < n; ++v) ptr[v + 1] = ptr[v] + fill[v];
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < n; ++v) fill[v] = ptr[v];
+#pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < m; ++e) {
+        out[__atomic_fetch_add(&fill[key[e]], 1, __ATOMIC_RELAXED)] = other[e];
+        if (both) out[__atomic_fetch_add(&fill[other[e]], 1, __ATOMIC_RELAXED)] = key[e];
+    }
+    free(fill);
+}
+
+/* Hop depth from `source` over a CSR (jo_bfs semantics: -1 unreached or beyond max_depth, max_depth
+ * < 0 unbounded), level-synchronous and parallel: the depth of a vertex is the level it is first
+ * reached at, whatever thread claims it, so the result is deterministic. */
+JO_API void jo_bfs_csr(int64_t n, const int64_t* ptr, const int32_t* other, int64_t source, int max_depth,
+                       int32_t* depth) {
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < n; ++v) depth[v] = -1;
+    if (source < 0 || source >= n) return;
+    int32_t* q = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    int32_t* qn = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    int64_t len = 1, len_next = 0;
+    q[0] = (int32_t)source;
+    depth[source] = 0;
+    for (int32_t level = 0; len > 0 && (max_depth < 0 || level < max_depth); ++level) {
+        len_next = 0;
+#pragma omp parallel
+        {
+            int32_t buf[1024];
+            int nb = 0;
+#pragma omp for schedule(dynamic, 64)
+            for (int64_t i = 0; i < len; ++i) {
+                const int32_t u = q[i];
+                for (int64_t k = ptr[u]; k < ptr[u + 1]; ++k) {
+                    const int32_t v = other[k];
+                    int32_t expect = -1;
+                    if (__atomic_load_n(&depth[v], __ATOMIC_RELAXED) == -1 &&
+                        __atomic_compare_exchange_n(&depth[v], &expect, level + 1, 0, __ATOMIC_RELAXED,
+                                                    __ATOMIC_RELAXED)) {
+                        buf[nb++] = v;
+                        if (nb == 1024) {
+                            const int64_t at = __atomic_fetch_add(&len_next, nb, __ATOMIC_RELAXED);
+                            memcpy(qn + at, buf, sizeof(int32_t) * 1024);
+                            nb = 0;
+                        }
+                    }
+                }
+            }
+            if (nb) {
+                const int64_t at = __atomic_fetch_add(&len_next, nb, __ATOMIC_RELAXED);
+                memcpy(qn + at, buf, sizeof(int32_t) * (size_t)nb);
+            }
+        }
+        int32_t* t = q; q = qn; qn = t;
+        len = len_next;
+    }
+    free(q); free(qn);
+}
+
+/* Rank of every id 0..n-1 in String order (the lex rank of jo_lex_rank for vid = 0..n-1, in O(n)):
+ * String order of decimal numbers is the preorder of the decimal trie ("0", "1", "10", "100", ...,
+ * "101", ..., "11", ...). */
+JO_API void jo_lex_rank_iota(int64_t n, int32_t* rank) {
+    if (n <= 0) return;
+    int32_t r = 0;
+    rank[0] = r++;
+    int64_t x = 1;
+    while (r < n) {
+        rank[x] = r++;
+        if (x * 10 < n) { x *= 10; continue; }        /* first child */
+        while (x % 10 == 9 || x + 1 >= n) x /= 10;    /* climb while no next sibling */
+        ++x;                                          /* next sibling */
+    }
+}
+
+/* Graph500-style validation of a BFS depth vector over the undirected edge list (src, dst):
+ * bit 0: depth[source] != 0; bit 1: an edge with exactly one reached endpoint; bit 2: an edge whose
+ * endpoint depths differ by more than one; bit 3: a reached vertex other than the source without a
+ * neighbour one level up; bit 4 (comp != NULL): the reached set is not the source's component.
+ * Returns the error bits (0 = valid); *edges_out = edges with a reached endpoint (Graph500 TEPS). */
+JO_API int jo_bfs_validate(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* depth,
+                           int64_t source, const int32_t* comp, int64_t* edges_out) {
+    int err = 0;
+    if (source < 0 || source >= n || depth[source] != 0) err |= 1;
+    unsigned char* has_parent = (unsigned char*)calloc((size_t)(n > 0 ? n : 1), 1);
+    int64_t edges = 0;
+#pragma omp parallel for schedule(static) reduction(| : err) reduction(+ : edges)
+    for (int64_t e = 0; e < m; ++e) {
+        const int32_t du = depth[src[e]], dv = depth[dst[e]];
+        if ((du >= 0) != (dv >= 0)) { err |= 2; continue; }
+        if (du < 0) continue;
+        ++edges;
+        if (du - dv > 1 || dv - du > 1) err |= 4;
+        if (du == dv - 1) __atomic_store_n(&has_parent[dst[e]], 1, __ATOMIC_RELAXED);
+        if (dv == du - 1) __atomic_store_n(&has_parent[src[e]], 1, __ATOMIC_RELAXED);
+    }
+#pragma omp parallel for schedule(static) reduction(| : err)
+    for (int64_t v = 0; v < n; ++v) {
+        if (depth[v] > 0 && !has_parent[v]) err |= 8;
+        if (comp && source >= 0 && source < n && ((depth[v] >= 0) != (comp[v] == comp[source]))) err |= 16;
+    }
+    free(has_parent);
+    if (edges_out) *edges_out = edges;
+    return err;
+}
+
+/* Hop depth from up to 64 sources at once (jo_bfs semantics per source), bit-parallel: bit k of
+ * visited[v] / frontier[v] is source k.  A level either pushes from the frontier (few frontier
+ * vertices: atomic OR into the neighbours' next words) or pulls over every unfinished vertex's
+ * neighbours (OR of their frontier words); both give next[v] = the OR of the frontier words of v's
+ * neighbours, so depth_out[k * n + v] is the level bit k first reaches v, whatever the order.
+ * Duplicate sources each get their own row.  -1 = unreached or beyond max_depth (< 0: unbounded). */
+JO_API void jo_msbfs_csr(int64_t n, const int64_t* ptr, const int32_t* other, const int64_t* sources, int nsrc,
+                         int max_depth, int32_t* depth_out) {
+    if (nsrc <= 0 || nsrc > 64) return;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)nsrc * n; ++i) depth_out[i] = -1;
+    uint64_t* visited = (uint64_t*)calloc((size_t)(n > 0 ? n : 1), 8);
+    uint64_t* front = (uint64_t*)calloc((size_t)(n > 0 ? n : 1), 8);
+    uint64_t* next = (uint64_t*)calloc((size_t)(n > 0 ? n : 1), 8);
+    const uint64_t all = nsrc == 64 ? ~0ull : ((1ull << nsrc) - 1ull);
+    int64_t nfront = 0;
+    for (int k = 0; k < nsrc; ++k) {
+        const int64_t s = sources[k];
+        if (s < 0 || s >= n) continue;
+        if (!front[s]) ++nfront;
+        front[s] |= 1ull << k;
+        visited[s] |= 1ull << k;
+        depth_out[(int64_t)k * n + s] = 0;
+    }
+    for (int32_t level = 0; nfront > 0 && (max_depth < 0 || level < max_depth); ++level) {
+        if (nfront < n / 32) { /* push */
+#pragma omp parallel for schedule(dynamic, 64)
+            for (int64_t u = 0; u < n; ++u) {
+                const uint64_t f = front[u];
+                if (!f) continue;
+                for (int64_t k = ptr[u]; k < ptr[u + 1]; ++k) {
+                    const int32_t v = other[k];
+                    const uint64_t add = f & ~visited[v];
+                    if (add && (__atomic_load_n(&next[v], __ATOMIC_RELAXED) & add) != add)
+                        __atomic_fetch_or(&next[v], add, __ATOMIC_RELAXED);
+                }
+            }
+        } else { /* pull */
+#pragma omp parallel for schedule(dynamic, 1024)
+            for (int64_t v = 0; v < n; ++v) {
+                if ((visited[v] & all) == all) continue;
+                uint64_t acc = 0;
+                for (int64_t k = ptr[v]; k < ptr[v + 1]; ++k) acc |= front[other[k]];
+                next[v] = acc;
+            }
+        }
+        nfront = 0;
+#pragma omp parallel for schedule(static) reduction(+ : nfront)
+        for (int64_t v = 0; v < n; ++v) {
+            const uint64_t nw = next[v] & ~visited[v] & all;
+            next[v] = 0;
+            front[v] = nw;
+            if (!nw) continue;
+            visited[v] |= nw;
+            ++nfront;
+            for (uint64_t b = nw; b; b &= b - 1) depth_out[(int64_t)__builtin_ctzll(b) * n + v] = level + 1;
+        }
+    }
+    free(visited); free(front); free(next);
+}
+
+/* JanusGraph PageRank (jo_pagerank's semantics) over CSRs built by jo_csr_unordered: out_ptr gives
+ * the out-degree (edgeCount: one message per out-edge, a sum of 1.0s, exact), in_ptr/in_src the
+ * gather.  Same superstep loop; only the summation order inside a row may differ (rounding). */
+JO_API void jo_pagerank_csr(int64_t n, const int64_t* in_ptr, const int32_t* in_src, const double* edge_count,
+                            double damping, int64_t vertex_count, int iterations, double* rank) {
+    for (int64_t v = 0; v < n; ++v) rank[v] = NAN;
+    if (iterations <= 0) return;
+    double* msg = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double* msg_next = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    const double initial = 1.0 / (double)vertex_count;
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < n; ++v) { rank[v] = initial; msg[v] = initial / edge_count[v]; }
+    for (int t = 2; t <= iterations; ++t) {
+        jo_pagerank_superstep_csr(n, in_ptr, in_src, msg, edge_count, damping, vertex_count, msg_next, rank);
+        double* tmp = msg; msg = msg_next; msg_next = tmp;
+    }
+    free(msg); free(msg_next);
 }
 
 JO_API int jo_num_threads(void) {

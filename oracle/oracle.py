@@ -57,6 +57,22 @@ def lib():
         L.jo_connected_components.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, _i64p, ctypes.c_int,
                                               _i64p]
         L.jo_connected_components.restype = ctypes.c_int
+        L.jo_cc_csr.argtypes = [ctypes.c_int64, _i64p, _i32p, _i32p, ctypes.c_int, _i32p]
+        L.jo_cc_csr.restype = ctypes.c_int
+        L.jo_csr_unordered.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_int, _i64p, _i32p]
+        L.jo_csr_unordered.restype = None
+        L.jo_bfs_csr.argtypes = [ctypes.c_int64, _i64p, _i32p, ctypes.c_int64, ctypes.c_int, _i32p]
+        L.jo_bfs_csr.restype = None
+        L.jo_lex_rank_iota.argtypes = [ctypes.c_int64, _i32p]
+        L.jo_lex_rank_iota.restype = None
+        L.jo_bfs_validate.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, _i32p, ctypes.c_int64,
+                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+        L.jo_bfs_validate.restype = ctypes.c_int
+        L.jo_pagerank_csr.argtypes = [ctypes.c_int64, _i64p, _i32p, _f64p, ctypes.c_double, ctypes.c_int64,
+                                      ctypes.c_int, _f64p]
+        L.jo_pagerank_csr.restype = None
+        L.jo_msbfs_csr.argtypes = [ctypes.c_int64, _i64p, _i32p, _i64p, ctypes.c_int, ctypes.c_int, _i32p]
+        L.jo_msbfs_csr.restype = None
         L.jo_num_threads.argtypes = []
         L.jo_num_threads.restype = ctypes.c_int
         _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -294,3 +310,64 @@ def combine_steps(n, src, dst, direction, combiner, steps, init=None, int32_wrap
     if steps == 0:
         received = np.zeros(n, bool)
     return x, received
+
+
+# ---- full-size checkers (parallel CSR builds; tests/test_gpu_configs.py) ----
+
+def csr_unordered(n, key, other, both=False):
+    """CSR rows = key, entries = other (both: symmetrised, a self-loop twice); entry order inside a
+    row unspecified.  Returns (ptr int64[n+1], adj int32)."""
+    key, other = _i32(key), _i32(other)
+    m = len(key)
+    ptr = np.empty(n + 1, np.int64)
+    adj = np.empty(max((2 if both else 1) * m, 1), np.int32)
+    lib().jo_csr_unordered(n, m, key, other, 1 if both else 0, ptr, adj)
+    return ptr, adj[: (2 if both else 1) * m]
+
+
+def bfs_csr(n, ptr, adj, source, max_depth=-1):
+    depth = np.empty(max(n, 1), np.int32)
+    lib().jo_bfs_csr(n, _i64(ptr), _i32(adj), int(source), int(max_depth), depth)
+    return depth[:n]
+
+
+def msbfs_csr(n, ptr, adj, sources, max_depth=-1):
+    """Bit-parallel hop depth from up to 64 sources (jo_msbfs_csr).  Returns int32 [nsrc, n]."""
+    src = _i64(np.atleast_1d(sources))
+    depth = np.empty(max(len(src) * n, 1), np.int32)
+    lib().jo_msbfs_csr(n, _i64(ptr), _i32(adj), src, len(src), int(max_depth), depth)
+    return depth[: len(src) * n].reshape(len(src), n)
+
+
+def lex_rank_iota(n):
+    """jo_lex_rank of vid = 0..n-1 (String order of the decimal ids), in O(n)."""
+    r = np.empty(max(n, 1), np.int32)
+    lib().jo_lex_rank_iota(n, r)
+    return r[:n]
+
+
+def cc_csr(n, ptr, adj, rank, max_iterations=100):
+    """jo_connected_components' superstep loop on a BOTH CSR with given lex ranks.
+    Returns (label rank per vertex, iterations)."""
+    label = np.empty(max(n, 1), np.int32)
+    it = lib().jo_cc_csr(n, _i64(ptr), _i32(adj), _i32(rank), int(max_iterations), label)
+    return label[:n], int(it)
+
+
+def bfs_validate(n, src, dst, depth, source, comp=None):
+    """Graph500 validation (jo_bfs_validate).  Returns (error bits, edges with a reached endpoint)."""
+    comp_p = None
+    if comp is not None:
+        comp = _i32(comp)
+        comp_p = comp.ctypes.data_as(ctypes.c_void_p)
+    edges = ctypes.c_int64(0)
+    err = lib().jo_bfs_validate(n, len(src), _i32(src), _i32(dst), _i32(depth), int(source), comp_p,
+                                ctypes.byref(edges))
+    return int(err), int(edges.value)
+
+
+def pagerank_csr(n, in_ptr, in_src, edge_count, damping=0.85, vertex_count=1, iterations=10):
+    rank = np.empty(max(n, 1), np.float64)
+    lib().jo_pagerank_csr(n, _i64(in_ptr), _i32(in_src), np.ascontiguousarray(edge_count, np.float64),
+                          float(damping), int(vertex_count), int(iterations), rank)
+    return rank[:n]

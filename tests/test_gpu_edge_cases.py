@@ -1,0 +1,101 @@
+"""GPU edge cases of the programs, each against the oracle (the restatement of the reference's
+semantics) on the same graph:
+  * PageRank with vertexCount at its default of 1 and with vertexCount != |V|
+    (PageRankVertexProgram.java:64-69: N is the user's parameter, not the measured count), and
+    K = 0 / 1 / 2 supersteps (:107-110: K - 1 power steps; K = 0 writes no property);
+  * ShortestDistance with maxDepth = 0 (ShortestDistanceVertexProgram.java:144-146: only the seed);
+  * CC, BFS, PageRank and ShortestDistance on an edgeless graph and on a graph whose every edge is a
+    ghost edge (VertexJobConverter.java:126-129).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PR_RTOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import janusgraph_amd as jg
+    c = jg.Context((0,))
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def rmat12(oracle_lib):
+    o = oracle_lib
+    n = 1 << 12
+    s, t = o.rmat_edges(12, 16, 21)
+    vid = (np.random.default_rng(3).permutation(n).astype(np.int64) + 1) << 8
+    return n, vid, s.astype(np.int32), t.astype(np.int32)
+
+
+def assert_pr(got, want):
+    nan = np.isnan(want)
+    assert (np.isnan(got) == nan).all()
+    rel = np.abs(got[~nan] - want[~nan]) / np.maximum(np.abs(want[~nan]), 1e-300)
+    assert rel.max(initial=0.0) <= PR_RTOL, f"max rel err {rel.max()}"
+
+
+@pytest.mark.parametrize("vertex_count,iterations", [(1, 10), (1, 0), (1, 1), (1, 2), (7, 30), ("n+1000", 12),
+                                                     ("n", 0), ("n", 1), ("n", 2)])
+def test_pagerank_vertex_count_and_iterations(ctx, oracle_lib, rmat12, vertex_count, iterations):
+    import janusgraph_amd as jg
+    n, vid, s, t = rmat12
+    N = {"n": n, "n+1000": n + 1000}.get(vertex_count, vertex_count)
+    g = ctx.build(vid, vid[s], vid[t], flags=jg.ADJ_IN)
+    rank, ec = g.pagerank(0.85, N, iterations)
+    want, ec_want = oracle_lib.pagerank(n, s, t, 0.85, N, iterations)
+    assert_pr(rank, want)
+    assert_pr(ec, ec_want)
+    assert ctx.stats()["supersteps"] == iterations
+    g.close()
+
+
+@pytest.mark.parametrize("max_depth", [0, 1])
+def test_shortest_distance_max_depth_small(ctx, oracle_lib, rmat12, max_depth):
+    import janusgraph_amd as jg
+    n, vid, s, t = rmat12
+    w = (np.arange(len(s)) % 3 + 1).astype(np.int32)
+    g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN | jg.ADJ_OUT)
+    seed = int(t[0])
+    got = g.shortest_distance(vid[seed], max_depth)
+    want = oracle_lib.shortest_distance(n, s, t, seed, max_depth, w)
+    np.testing.assert_array_equal(got, want)
+    assert got[seed] == 0
+    if max_depth == 0:
+        assert (got >= 0).sum() == 1
+    g.close()
+
+
+@pytest.mark.parametrize("case", ["edgeless", "all_ghost"])
+def test_programs_without_edges(ctx, oracle_lib, case):
+    import janusgraph_amd as jg
+    o = oracle_lib
+    n = 37
+    vid = ((np.arange(n, dtype=np.int64) * 7 + 3) << 8)
+    if case == "edgeless":
+        src = dst = np.zeros(0, np.int64)
+    else:  # every edge has an endpoint the scan did not return (ghost): all dropped
+        src = vid[:10]
+        dst = np.full(10, (1 << 40) << 8, np.int64)
+    g = ctx.build(vid, src, dst, flags=jg.ADJ_IN | jg.ADJ_OUT | jg.ADJ_BOTH)
+    info = g.info()
+    assert info["num_edges"] == 0 and info["num_vertices"] == n
+    empty = np.zeros(0, np.int32)
+    comp, it = g.connected_components()
+    want, it_want = o.connected_components(n, empty, empty, vid)
+    np.testing.assert_array_equal(comp, want)
+    np.testing.assert_array_equal(comp, vid)  # every vertex is its own component
+    assert it == it_want
+    rank, ec = g.pagerank(0.85, n, 10)
+    r_want, ec_want = o.pagerank(n, empty, empty, 0.85, n, 10)
+    assert_pr(rank, r_want)
+    assert_pr(ec, ec_want)
+    depth = g.bfs([vid[5]], jg.DIR_BOTH)[0]
+    np.testing.assert_array_equal(depth, o.bfs(n, empty, empty, 5, o.DIR_BOTH))
+    dist = g.shortest_distance(vid[5], 10)
+    np.testing.assert_array_equal(dist, o.shortest_distance(n, empty, empty, 5, 10))
+    g.close()
