@@ -157,6 +157,31 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
                              int32_t partition_bits, uint32_t flags, int64_t* vid_out, int64_t* num_vertices_out,
                              jg_graph** out);
 
+/* ---- chunked snapshot ----
+ * The same two snapshots fed in chunks as the scan produces them (Java direct ByteBuffers hold at most
+ * 2 GiB, and the scan is a stream: StandardScannerExecutor.java:141-174 hands rows to the processors
+ * in key order).  Either ids (add_vertices / add_edges, any interleaving; edge weights on every
+ * add_edges call or on none) or raw rows (set_schema once, then add_rows; a row never spans two
+ * chunks), not both.  Each add_rows call stages its chunk and returns while the chunk is copied and
+ * decoded on the GPU, so the decode overlaps the caller's scan of the next chunk.  finish builds the
+ * graph exactly as jg_graph_build / jg_graph_build_edgestore would from the concatenated chunks
+ * (vertex order = the order added; read it back with jg_graph_vertex_ids).  The builder is single-use;
+ * destroy it after finish (or instead of it).  Stats of finish: build_ms, kernel_ms_total = copy +
+ * decode time of the rows, kernel_launches = number of row chunks. */
+typedef struct jg_builder jg_builder;
+int jg_builder_create(jg_ctx* ctx, jg_builder** out);
+int jg_builder_add_vertices(jg_builder* b, const int64_t* vid, int64_t n);
+int jg_builder_add_edges(jg_builder* b, const int64_t* src, const int64_t* dst, const int32_t* weight, int64_t m);
+int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
+                          int32_t partition_bits);
+int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
+                        const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
+                        int64_t nentries);
+int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out);
+int jg_builder_destroy(jg_builder* b);
+/* vid_out[i] = the id of vertex offset + i in output order (the order vid[] / the kept rows were given). */
+int jg_graph_vertex_ids(const jg_graph* g, int64_t offset, int64_t count, int64_t* vid_out);
+
 /* Synthetic Graph500 Kronecker (RMAT a,b,c,d = .57,.19,.19,.05) graph generated on the device(s):
  * n = 2^scale vertices with ids 0..n-1, m = edgefactor * n directed edges, seeded and
  * bit-identical to oracle/jg_oracle.c:jo_rmat_edges. */

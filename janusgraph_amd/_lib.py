@@ -35,7 +35,8 @@ EXPORTS = [
     "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_combine_steps", "jg_decode_edges", "jg_graph_sync",
-    "jg_tune_set",
+    "jg_tune_set", "jg_builder_create", "jg_builder_add_vertices", "jg_builder_add_edges", "jg_builder_set_schema",
+    "jg_builder_add_rows", "jg_builder_finish", "jg_builder_destroy", "jg_graph_vertex_ids",
 ]
 
 
@@ -114,6 +115,14 @@ def load():
         "jg_decode_edges": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i32, _P, _P, _P, _P], ctypes.c_int),
         "jg_graph_sync": ([_P], ctypes.c_int),
         "jg_tune_set": ([ctypes.c_char_p, _i64], ctypes.c_int),
+        "jg_builder_create": ([_P, _PP], ctypes.c_int),
+        "jg_builder_add_vertices": ([_P, _P, _i64], ctypes.c_int),
+        "jg_builder_add_edges": ([_P, _P, _P, _P, _i64], ctypes.c_int),
+        "jg_builder_set_schema": ([_P, _P, _P, _i32, _i32], ctypes.c_int),
+        "jg_builder_add_rows": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i64], ctypes.c_int),
+        "jg_builder_finish": ([_P, ctypes.c_uint32, _PP], ctypes.c_int),
+        "jg_builder_destroy": ([_P], ctypes.c_int),
+        "jg_graph_vertex_ids": ([_P, _i64, _i64, _P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -248,10 +257,75 @@ class Context:
                                               partition_bits, flags, _ptr(vid), ctypes.byref(nv), ctypes.byref(h)))
         return Graph(self, h, nv.value), vid[:nv.value].copy()
 
+    def builder(self) -> "Builder":
+        """jg_builder: the snapshot fed in chunks (ids, or raw edgestore rows decoded as they arrive)."""
+        return Builder(self)
+
     def build_rmat(self, scale, edgefactor=16, seed=1, flags=ADJ_IN) -> "Graph":
         h = ctypes.c_void_p()
         check(load().jg_graph_build_rmat(self._h, scale, edgefactor, seed, flags, ctypes.byref(h)))
         return Graph(self, h, 1 << scale)
+
+
+class Builder:
+    """jg_builder_*: add_vertices / add_edges chunks, or set_schema then add_rows chunks, then finish()."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        check(load().jg_builder_create(ctx.handle, ctypes.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            check(load().jg_builder_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_vertices(self, vid):
+        vid = np.ascontiguousarray(vid, np.int64)
+        check(load().jg_builder_add_vertices(self._h, _ptr(vid), len(vid)))
+
+    def add_edges(self, src, dst, weight=None):
+        src = np.ascontiguousarray(src, np.int64)
+        dst = np.ascontiguousarray(dst, np.int64)
+        if len(src) != len(dst):
+            raise ValueError("src and dst differ in length")
+        w = None if weight is None else np.ascontiguousarray(weight, np.int32)
+        if w is not None and len(w) != len(src):
+            raise ValueError("weight must have one entry per edge")
+        check(load().jg_builder_add_edges(self._h, _ptr(src), _ptr(dst), _ptr(w), len(src)))
+
+    def set_schema(self, type_ids=(), type_mult=(), partition_bits=5):
+        tid = np.ascontiguousarray(type_ids, np.int64)
+        tm = np.ascontiguousarray(type_mult, np.int8)
+        if len(tid) != len(tm):
+            raise ValueError("type_ids and type_mult differ in length")
+        self._schema = (tid, tm)
+        check(load().jg_builder_set_schema(self._h, _ptr(tid), _ptr(tm), len(tid), int(partition_bits)))
+
+    def add_rows(self, row_keys, row_entry_off, data, entry_off, value_pos):
+        keys = np.ascontiguousarray(row_keys, np.uint64)
+        roff = np.ascontiguousarray(row_entry_off, np.int64)
+        data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                    np.uint8)
+        off = np.ascontiguousarray(entry_off, np.int64)
+        vpos = np.ascontiguousarray(value_pos, np.int32)
+        if len(roff) != len(keys) + 1 or len(off) != len(vpos) + 1:
+            raise ValueError("row_entry_off needs nrows + 1 offsets, entry_off nentries + 1")
+        check(load().jg_builder_add_rows(self._h, _ptr(keys), len(keys), _ptr(roff), _ptr(data), len(data), _ptr(off),
+                                         _ptr(vpos), len(vpos)))
+
+    def finish(self, flags=ADJ_IN | ADJ_OUT | ADJ_BOTH) -> "Graph":
+        h = ctypes.c_void_p()
+        check(load().jg_builder_finish(self._h, flags, ctypes.byref(h)))
+        g = Graph(self.ctx, h, 0)
+        g.n = g.info()["num_vertices"]
+        return g
 
 
 class Graph:
@@ -278,6 +352,13 @@ class Graph:
 
     def sync(self):
         check(load().jg_graph_sync(self._h))
+
+    def vertex_ids(self, offset=0, count=None):
+        """jg_graph_vertex_ids: the vertex ids in output order."""
+        count = self.n - offset if count is None else count
+        out = np.empty(max(count, 1), np.int64)
+        check(load().jg_graph_vertex_ids(self._h, int(offset), int(count), _ptr(out)))
+        return out[:count]
 
     def pagerank(self, damping=0.85, vertex_count=1, iterations=10):
         rank = np.empty(self.n, np.float64)

@@ -204,7 +204,103 @@ static void make_shards(Ctx& c, Graph& g) {
     }
 }
 
+// Builds g (shards made) from vertex / edge ids already on device `dev0` (written on stream `s0`):
+// vid[n] int64, src/dst[m] int64, weight[m] int32 (nullable).  Every shard remaps the whole edge list
+// (shards on other devices get a peer copy first), then the CSRs and plans are built.
+static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int64_t* d_vid, int64_t n,
+                                  const int64_t* d_src, const int64_t* d_dst, const int32_t* d_w, int64_t m) {
+    if (n >= (int64_t)INT32_MAX) fail(JG_ERR_ARG, "more than 2^31-1 vertices");
+    if (m >= (int64_t)UINT32_MAX) fail(JG_ERR_ARG, "more than 2^32-1 edges");
+    {
+        DeviceGuard dg(dev0);
+        JG_HIP(hipStreamSynchronize(s0));
+        std::vector<int64_t> hv((size_t)n);
+        if (n) copy_d2h(hv.data(), d_vid, (size_t)n * sizeof(int64_t), s0);
+        g.n = n;
+        set_vertex_ids(g, hv.data(), n);
+    }
+    g.has_weights = d_w != nullptr;
+    std::vector<DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size()), dw(g.shards.size());
+    std::vector<DevBuf<int64_t>> pv(g.shards.size()), ps(g.shards.size()), pd(g.shards.size());
+    DenseEdges e;
+    e.m = m;
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        const int64_t *v = d_vid, *a = d_src, *b = d_dst;
+        auto peer = [&](void* dst, const void* src, size_t bytes) {
+            if (bytes) JG_HIP(hipMemcpyPeerAsync(dst, sh.device, src, dev0, bytes, sh.stream));
+        };
+        if (sh.device != dev0) {
+            pv[i].alloc(std::max<int64_t>(n, 1));
+            ps[i].alloc(std::max<int64_t>(m, 1));
+            pd[i].alloc(std::max<int64_t>(m, 1));
+            peer(pv[i].get(), d_vid, (size_t)n * sizeof(int64_t));
+            peer(ps[i].get(), d_src, (size_t)m * sizeof(int64_t));
+            peer(pd[i].get(), d_dst, (size_t)m * sizeof(int64_t));
+            v = pv[i].get();
+            a = ps[i].get();
+            b = pd[i].get();
+        }
+        ds[i].alloc(std::max<int64_t>(m, 1));
+        dd[i].alloc(std::max<int64_t>(m, 1));
+        remap_ids_device(v, n, a, b, m, ds[i].get(), dd[i].get(), sh.stream);
+        e.src.push_back(ds[i].get());
+        e.dst.push_back(dd[i].get());
+        if (d_w) {
+            dw[i].alloc(std::max<int64_t>(m, 1));
+            if (sh.device != dev0) peer(dw[i].get(), d_w, (size_t)m * sizeof(int32_t));
+            else if (m) JG_HIP(hipMemcpyAsync(dw[i].get(), d_w, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToDevice, sh.stream));
+            e.weight.push_back(dw[i].get());
+        } else {
+            e.weight.push_back(nullptr);
+        }
+    }
+    build_graph_from_dense(g, e);
+}
+
+// HIP-event timer on the first shard's stream.
+struct BuildTimer {
+    Graph& g;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    explicit BuildTimer(Graph& gr) : g(gr) {
+        DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
+    }
+    float stop() {
+        DeviceGuard dg(g.shards[0]->device);
+        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
+        JG_HIP(hipEventSynchronize(t1));
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
+        return ms;
+    }
+    ~BuildTimer() {
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
+};
+
 }  // namespace jg
+
+// The chunked snapshot (jg_builder_*): ids accumulate on the first device as they arrive, raw rows are
+// decoded there chunk by chunk (EdgestoreDecoder: copy and decode overlap the caller's next chunk).
+struct jg_builder {
+    jg::Ctx* ctx = nullptr;
+    int mode = 0;  // 0 empty, 1 ids (vertices / edges), 2 edgestore rows
+    int weights = -1;  // ids mode: -1 unknown, 0 no edge weights, 1 every edge weighted
+    bool finished = false;
+    jg::DevBuf<int64_t> vid, src, dst;
+    jg::DevBuf<int32_t> w;
+    int64_t n = 0, m = 0, mw = 0;
+    std::unique_ptr<jg::EdgestoreDecoder> dec;
+    std::vector<int64_t> type_ids;
+    std::vector<int8_t> type_mult;
+    int pbits = 5;
+    bool schema_set = false;
+};
 
 using jg::Error;
 
@@ -259,15 +355,25 @@ int jg_tune_set(const char* key, int64_t value) {
         JG_ARG(value >= 0, "light_lds must be >= 0");
         jg::tune().light_lds = value;
     } else if (k.rfind("band", 0) == 0 && k.size() == 9 && k[4] >= '0' && k[4] <= '3' &&
-               (k.substr(5) == "_deg" || k.substr(5) == "_bit")) {
-        const int i = k[4] - '0';  // band<i>_deg: minimum degree (0: band unused); band<i>_bit: log2 sub-slices
+               (k.substr(5) == "_deg" || k.substr(5) == "_bit" || k.substr(5) == "_sub")) {
+        // band<i>_deg: minimum degree (0: band unused); band<i>_bit: log2 sub-slices (0: automatic);
+        // band<i>_sub: sub-slices, a power of two in [1, 256]
+        const int i = k[4] - '0';
         if (k.substr(5) == "_deg") {
             JG_ARG(value >= 0, "band degree must be >= 0");
             jg::tune().band_deg[i] = value;
-        } else {
+        } else if (k.substr(5) == "_bit") {
             JG_ARG(value == 0 || (value >= 3 && value <= 8), "band bits must be 0 (automatic) or in [3, 8]");
-            jg::tune().band_bits[i] = (int)value;
+            jg::tune().band_bits[i] = value == 0 ? -1 : (int)value;
+        } else {
+            JG_ARG(value >= 1 && value <= 256 && (value & (value - 1)) == 0, "band sub-slices must be a power of two in [1, 256]");
+            int b = 0;
+            while ((1 << b) < value) ++b;
+            jg::tune().band_bits[i] = b;
         }
+    } else if (k == "merge_nt") {
+        JG_ARG(value >= 0 && value <= 3, "merge_nt must be in [0, 3]");
+        jg::tune().merge_nt = (int)value;
     } else if (k == "pull_split") {
         jg::tune().pull_split = value != 0;
     } else if (k == "pull_short") {
@@ -294,6 +400,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().fuse_finalize = value != 0;
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
+    } else if (k == "pr_skip_empty") {
+        jg::tune().pr_skip_empty = value != 0;
     } else if (k == "merge_temporal") {
         JG_ARG(value >= 0 && value <= 2, "merge_temporal must be 0, 1 (automatic) or 2");
         jg::tune().merge_temporal = (int)value;
@@ -421,55 +529,29 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
     auto gh = std::make_unique<jg_graph>();
     jg::Graph& g = gh->impl;
     g.ctx = &c;
-    g.n = n;
     g.flags = flags;
-    g.has_weights = weight != nullptr;
     jg::make_shards(c, g);
-    jg::set_vertex_ids(g, vid, n);
-    hipEvent_t t0, t1;
+    jg::BuildTimer timer(g);
+    jg::Shard& sh0 = *g.shards[0];
     {
-        jg::DeviceGuard dg(g.shards[0]->device);
-        JG_HIP(hipEventCreate(&t0));
-        JG_HIP(hipEventCreate(&t1));
-        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
-    }
-    std::vector<jg::DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size()), dw(g.shards.size());
-    jg::DenseEdges e;
-    e.m = m;
-    for (size_t i = 0; i < g.shards.size(); ++i) {
-        jg::Shard& sh = *g.shards[i];
-        jg::DeviceGuard dg(sh.device);
+        jg::DeviceGuard dg(sh0.device);
         jg::DevBuf<int64_t> dvid(std::max<int64_t>(n, 1)), dsrc(std::max<int64_t>(m, 1)), ddst(std::max<int64_t>(m, 1));
-        if (n) jg::copy_h2d(dvid.get(), vid, n * sizeof(int64_t), sh.stream);
+        jg::DevBuf<int32_t> dw;
+        if (n) jg::copy_h2d(dvid.get(), vid, n * sizeof(int64_t), sh0.stream);
         if (m) {
-            jg::copy_h2d(dsrc.get(), src, m * sizeof(int64_t), sh.stream);
-            jg::copy_h2d(ddst.get(), dst, m * sizeof(int64_t), sh.stream);
+            jg::copy_h2d(dsrc.get(), src, m * sizeof(int64_t), sh0.stream);
+            jg::copy_h2d(ddst.get(), dst, m * sizeof(int64_t), sh0.stream);
         }
-        ds[i].alloc(std::max<int64_t>(m, 1));
-        dd[i].alloc(std::max<int64_t>(m, 1));
-        jg::remap_ids_device(dvid.get(), n, dsrc.get(), ddst.get(), m, ds[i].get(), dd[i].get(), sh.stream);
-        e.src.push_back(ds[i].get());
-        e.dst.push_back(dd[i].get());
         if (weight) {
-            dw[i].alloc(std::max<int64_t>(m, 1));
-            if (m) jg::copy_h2d(dw[i].get(), weight, m * sizeof(int32_t), sh.stream);
-            e.weight.push_back(dw[i].get());
-        } else {
-            e.weight.push_back(nullptr);
+            dw.alloc(std::max<int64_t>(m, 1));
+            if (m) jg::copy_h2d(dw.get(), weight, m * sizeof(int32_t), sh0.stream);
         }
+        jg::build_from_device_ids(g, sh0.device, sh0.stream, dvid.get(), n, dsrc.get(), ddst.get(),
+                                  weight ? dw.get() : nullptr, m);
     }
-    jg::build_graph_from_dense(g, e);
-    {
-        jg::DeviceGuard dg(g.shards[0]->device);
-        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
-        JG_HIP(hipEventSynchronize(t1));
-        float ms = 0;
-        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
-        c.last = jg_stats{};
-        c.last.build_ms = ms;
-        (void)hipEventDestroy(t0);
-        (void)hipEventDestroy(t1);
-    }
+    const float ms = timer.stop();
+    c.last = jg_stats{};
+    c.last.build_ms = ms;
     *out = gh.release();
     JG_GUARD_END
 }
@@ -491,63 +573,180 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
     jg::Graph& g = gh->impl;
     g.ctx = &c;
     g.flags = flags;
-    g.has_weights = false;
     jg::make_shards(c, g);
-    hipEvent_t t0, t1;
+    jg::BuildTimer timer(g);
+    jg::Shard& sh0 = *g.shards[0];
+    jg::EdgestoreDecoder dec(type_ids, type_mult, ntypes, partition_bits, sh0.device);
+    dec.add(r);
+    dec.finish();
     {
-        jg::DeviceGuard dg(g.shards[0]->device);
-        JG_HIP(hipEventCreate(&t0));
-        JG_HIP(hipEventCreate(&t1));
-        JG_HIP(hipEventRecord(t0, g.shards[0]->stream));
+        jg::DeviceGuard dg(sh0.device);
+        jg::build_from_device_ids(g, sh0.device, sh0.stream, dec.vid.get(), dec.n, dec.src.get(), dec.dst.get(), nullptr,
+                                  dec.m);
     }
-    std::vector<jg::DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size());
-    jg::DenseEdges e;
-    float decode_ms = 0;
-    for (size_t i = 0; i < g.shards.size(); ++i) {  // every shard holds the whole edge list (as jg_graph_build)
-        jg::Shard& sh = *g.shards[i];
-        jg::DeviceGuard dg(sh.device);
-        jg::DevBuf<int64_t> dvid, dsrc, ddst;
-        int64_t n = 0, m = 0;
-        float ms = 0;
-        jg::edgestore_snapshot(r, sh.stream, dvid, n, dsrc, ddst, m, &ms);
-        if (i == 0) {
-            JG_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 vertices");
-            JG_ARG(m < (int64_t)UINT32_MAX, "more than 2^32-1 edges");
-            std::vector<int64_t> hv((size_t)n);
-            if (n) jg::copy_d2h(hv.data(), dvid.get(), (size_t)n * sizeof(int64_t), sh.stream);
-            g.n = n;
-            jg::set_vertex_ids(g, hv.data(), n);
-            e.m = m;
-            decode_ms = ms;
-        }
-        ds[i].alloc(std::max<int64_t>(m, 1));
-        dd[i].alloc(std::max<int64_t>(m, 1));
-        jg::remap_ids_device(dvid.get(), n, dsrc.get(), ddst.get(), m, ds[i].get(), dd[i].get(), sh.stream);
-        e.src.push_back(ds[i].get());
-        e.dst.push_back(dd[i].get());
-        e.weight.push_back(nullptr);
-    }
-    jg::build_graph_from_dense(g, e);
-    {
-        jg::DeviceGuard dg(g.shards[0]->device);
-        JG_HIP(hipEventRecord(t1, g.shards[0]->stream));
-        JG_HIP(hipEventSynchronize(t1));
-        float ms = 0;
-        JG_HIP(hipEventElapsedTime(&ms, t0, t1));
-        c.last = jg_stats{};
-        c.last.build_ms = ms;
-        c.last.kernel_ms_total = decode_ms;  // the two decode kernels (rows, entries)
-        c.last.kernel_launches = 1;
-        // decode kernels: entry bytes + off/vpos/take (13 B) per entry, src/dst (16 B) per kept edge,
-        // key/row_off/row_vid/keep (25 B) per row
-        c.last.algorithmic_bytes =
-            (double)nbytes + 13.0 * (double)nentries + 16.0 * (double)e.m + 25.0 * (double)nrows;
-        (void)hipEventDestroy(t0);
-        (void)hipEventDestroy(t1);
-    }
+    const float ms = timer.stop();
+    c.last = jg_stats{};
+    c.last.build_ms = ms;
+    c.last.kernel_ms_total = dec.kernel_ms;  // copy + decode of the rows
+    c.last.kernel_launches = 1;
+    // decode kernels: entry bytes + off/vpos/take (13 B) per entry, src/dst (16 B) per kept edge,
+    // key/row_off/row_vid/keep (25 B) per row
+    c.last.algorithmic_bytes = (double)nbytes + 13.0 * (double)nentries + 16.0 * (double)dec.m + 25.0 * (double)nrows;
     if (vid_out && g.n) std::copy(g.vid.begin(), g.vid.end(), vid_out);
     if (num_vertices_out) *num_vertices_out = g.n;
     *out = gh.release();
+    JG_GUARD_END
+}
+
+int jg_builder_create(jg_ctx* ctx, jg_builder** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx && out, "null argument");
+    *out = nullptr;
+    auto b = std::make_unique<jg_builder>();
+    b->ctx = &ctx->impl;
+    *out = b.release();
+    JG_GUARD_END
+}
+
+int jg_builder_destroy(jg_builder* b) {
+    JG_GUARD_BEGIN
+    delete b;
+    JG_GUARD_END
+}
+
+extern "C++" {
+namespace {
+int builder_device(const jg_builder* b) { return b->ctx->devices.empty() ? 0 : b->ctx->devices[0]; }
+hipStream_t builder_stream(const jg_builder* b) { return b->ctx->streams.empty() ? nullptr : b->ctx->streams[0]; }
+template <class T>
+void builder_append(jg::DevBuf<T>& acc, int64_t& len, const T* host, int64_t k, hipStream_t s) {
+    if (k <= 0) return;
+    if ((int64_t)acc.size() < len + k) {
+        jg::DevBuf<T> bigger(std::max<int64_t>(len + k, 2 * (int64_t)acc.size()));
+        if (len) JG_HIP(hipMemcpyAsync(bigger.get(), acc.get(), (size_t)len * sizeof(T), hipMemcpyDeviceToDevice, s));
+        JG_HIP(hipStreamSynchronize(s));
+        acc.swap(bigger);
+    }
+    jg::copy_h2d(acc.get() + len, host, (size_t)k * sizeof(T), s);
+    len += k;
+}
+}  // namespace
+}  // extern "C++"
+
+int jg_builder_add_vertices(jg_builder* b, const int64_t* vid, int64_t n) {
+    JG_GUARD_BEGIN
+    JG_ARG(b && n >= 0 && (n == 0 || vid), "bad arguments");
+    if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
+    if (b->mode == 2) jg::fail(JG_ERR_STATE, "builder holds edgestore rows: vertices come from the rows");
+    b->mode = 1;
+    jg::DeviceGuard dg(builder_device(b));
+    builder_append(b->vid, b->n, vid, n, builder_stream(b));
+    JG_GUARD_END
+}
+
+int jg_builder_add_edges(jg_builder* b, const int64_t* src, const int64_t* dst, const int32_t* weight, int64_t m) {
+    JG_GUARD_BEGIN
+    JG_ARG(b && m >= 0 && (m == 0 || (src && dst)), "bad arguments");
+    if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
+    if (b->mode == 2) jg::fail(JG_ERR_STATE, "builder holds edgestore rows: edges come from the rows");
+    if (m == 0) return JG_OK;
+    const int wmode = weight ? 1 : 0;
+    if (b->weights >= 0 && b->weights != wmode) jg::fail(JG_ERR_ARG, "edge weights must be given for every chunk or none");
+    b->weights = wmode;
+    b->mode = 1;
+    jg::DeviceGuard dg(builder_device(b));
+    hipStream_t s = builder_stream(b);
+    int64_t m2 = b->m;
+    builder_append(b->src, b->m, src, m, s);
+    builder_append(b->dst, m2, dst, m, s);
+    if (weight) builder_append(b->w, b->mw, weight, m, s);
+    JG_GUARD_END
+}
+
+int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
+                          int32_t partition_bits) {
+    JG_GUARD_BEGIN
+    JG_ARG(b && ntypes >= 0 && (ntypes == 0 || (type_ids && type_mult)), "bad arguments");
+    JG_ARG(partition_bits >= 0 && partition_bits <= 16, "partition bits must be in [0, 16]");
+    if (b->finished || b->mode != 0) jg::fail(JG_ERR_STATE, "jg_builder_set_schema must precede every chunk");
+    b->type_ids.assign(type_ids, type_ids + ntypes);
+    b->type_mult.assign(type_mult, type_mult + ntypes);
+    b->pbits = partition_bits;
+    b->schema_set = true;
+    JG_GUARD_END
+}
+
+int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
+                        const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
+                        int64_t nentries) {
+    JG_GUARD_BEGIN
+    JG_ARG(b, "null builder");
+    if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
+    if (b->mode == 1) jg::fail(JG_ERR_STATE, "builder holds vertex / edge ids: rows cannot be mixed in");
+    b->mode = 2;
+    if (!b->dec)
+        b->dec = std::make_unique<jg::EdgestoreDecoder>(b->type_ids.data(), b->type_mult.data(),
+                                                        (int32_t)b->type_ids.size(), b->pbits, builder_device(b));
+    const jg::EdgestoreRows r{row_keys, nrows,      row_entry_off, bytes,
+                              nbytes,   entry_off,  value_pos,     nentries,
+                              b->type_ids.data(), b->type_mult.data(), (int32_t)b->type_ids.size(), b->pbits};
+    b->dec->add(r);
+    JG_GUARD_END
+}
+
+int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(b && out, "null argument");
+    JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
+    if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
+    *out = nullptr;
+    jg::Ctx& c = *b->ctx;
+    auto gh = std::make_unique<jg_graph>();
+    jg::Graph& g = gh->impl;
+    g.ctx = &c;
+    g.flags = flags;
+    jg::make_shards(c, g);
+    jg::BuildTimer timer(g);
+    const int dev0 = builder_device(b);
+    float decode_ms = 0;
+    int64_t chunks = 0;
+    if (b->mode == 2) {
+        b->dec->finish();
+        decode_ms = b->dec->kernel_ms;
+        chunks = b->dec->chunks_added_;
+        jg::build_from_device_ids(g, dev0, builder_stream(b), b->dec->vid.get(), b->dec->n, b->dec->src.get(),
+                                  b->dec->dst.get(), nullptr, b->dec->m);
+    } else {
+        jg::DeviceGuard dg(dev0);
+        if (b->vid.size() == 0) b->vid.alloc(1);
+        if (b->src.size() == 0) { b->src.alloc(1); b->dst.alloc(1); }
+        jg::build_from_device_ids(g, dev0, builder_stream(b), b->vid.get(), b->n, b->src.get(), b->dst.get(),
+                                  b->weights == 1 ? b->w.get() : nullptr, b->m);
+    }
+    const float ms = timer.stop();
+    b->finished = true;
+    b->dec.reset();
+    {
+        jg::DeviceGuard dg(dev0);
+        b->vid.reset();
+        b->src.reset();
+        b->dst.reset();
+        b->w.reset();
+    }
+    c.last = jg_stats{};
+    c.last.build_ms = ms;
+    c.last.kernel_ms_total = decode_ms;
+    c.last.kernel_launches = chunks;
+    *out = gh.release();
+    JG_GUARD_END
+}
+
+int jg_graph_vertex_ids(const jg_graph* g, int64_t offset, int64_t count, int64_t* vid_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && (count == 0 || vid_out), "null argument");
+    const jg::Graph& gr = g->impl;
+    JG_ARG(offset >= 0 && count >= 0 && offset + count <= gr.n, "range outside [0, num_vertices)");
+    for (int64_t i = 0; i < count; ++i) vid_out[i] = gr.vid_of(offset + i);
     JG_GUARD_END
 }
 

@@ -770,7 +770,9 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         const int64_t end = std::min<int64_t>((int64_t)fb[kNumClasses + 1 + i], zero_begin);
         if (end <= row_at) continue;
         auto bd = std::make_unique<SliceBand>();
-        bd->bits = std::min(std::max(tune().band_bits[i] > 0 ? tune().band_bits[i] : auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
+        bd->bits = tune().band_bits[i] >= 0
+                       ? std::min(tune().band_bits[i], 8)
+                       : std::min(std::max(auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
         bd->row_begin = row_at;
         bd->row_end = end;
         row_at = end;

@@ -15,6 +15,7 @@
 // absent labels are MULTI.  One thread per entry, every entry independent: byte-level work bound by
 // HBM (a few loads per entry; neighbouring threads read neighbouring entries).
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "jg_internal.h"
@@ -462,71 +463,206 @@ void edgestore_check(const EdgestoreRows& r) {
     check_entries(r.bytes, r.nbytes, r.entry_off, r.vpos, r.nentries);
 }
 
-void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
-                        DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms) {
-    TypeTable tt(r.type_ids, r.type_mult, r.ntypes, s);
-    const int64_t R = r.nrows, E = r.nentries;
-    DevBuf<uint8_t> d_bytes(r.nbytes + kBytePad), keep(std::max<int64_t>(R, 1)), keep_v(std::max<int64_t>(R, 1)),
-        take(std::max<int64_t>(E, 1));
-    DevBuf<int64_t> d_off(E + 1), d_roff(R + 1), row_vid(std::max<int64_t>(R, 1)), esrc(std::max<int64_t>(E, 1)),
-        edst(std::max<int64_t>(E, 1)), idx(std::max<int64_t>(std::max(R, E), 1));
-    DevBuf<uint64_t> d_keys(std::max<int64_t>(R, 1));
-    DevBuf<int64_t> block_row((E + kChunk - 1) / kChunk + 1);
-    DevBuf<int32_t> d_vpos(std::max<int64_t>(E, 1)), err(1);
-    if (r.nbytes) copy_h2d(d_bytes.get(), r.bytes, (size_t)r.nbytes, s);
-    copy_h2d(d_off.get(), r.entry_off, (size_t)(E + 1) * sizeof(int64_t), s);
-    if (E) copy_h2d(d_vpos.get(), r.vpos, (size_t)E * sizeof(int32_t), s);
-    if (R) {
-        copy_h2d(d_keys.get(), r.keys, (size_t)R * sizeof(uint64_t), s);
-        copy_h2d(d_roff.get(), r.row_off, (size_t)(R + 1) * sizeof(int64_t), s);
+// ---- the snapshot decoder: chunks of rows, two in flight ----
+// A chunk's arrays are staged in pinned host memory, so the call that adds it returns once they are
+// copied there; the H2D copy and the two decode kernels then run on the chunk's stream while the caller
+// scans the next chunk.  Completing a chunk (at the next add, or at finish) checks its error flags,
+// compacts the kept rows and edges and appends them to the device accumulators.
+struct EdgestoreChunk {
+    int64_t R = 0, E = 0, nbytes = 0;
+    PinnedBuf staging;
+    DevBuf<uint8_t> d_bytes, keep, keep_v, take;
+    DevBuf<int64_t> d_off, d_roff, row_vid, esrc, edst, block_row;
+    DevBuf<uint64_t> d_keys;
+    DevBuf<int32_t> d_vpos, err;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool pending = false;
+};
+
+namespace {
+template <class T>
+void grow_append(DevBuf<T>& acc, int64_t& len, const T* src, int64_t k, hipStream_t s) {
+    if (k <= 0) return;
+    if ((int64_t)acc.size() < len + k) {
+        DevBuf<T> bigger(std::max<int64_t>(len + k, 2 * (int64_t)acc.size()));
+        if (len) JG_HIP(hipMemcpyAsync(bigger.get(), acc.get(), (size_t)len * sizeof(T), hipMemcpyDeviceToDevice, s));
+        acc.swap(bigger);
+        JG_HIP(hipStreamSynchronize(s));  // the old buffer is freed on return
     }
-    JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
-    const EntryView a{d_bytes.get(), d_off.get(), d_vpos.get(), tt.ids.get(), tt.mult.get(), tt.n};
-    hipEvent_t t0, t1;
-    JG_HIP(hipEventCreate(&t0));
-    JG_HIP(hipEventCreate(&t1));
-    JG_HIP(hipEventRecord(t0, s));
+    JG_HIP(hipMemcpyAsync(acc.get() + len, src, (size_t)k * sizeof(T), hipMemcpyDeviceToDevice, s));
+    len += k;
+}
+}  // namespace
+
+PinnedBuf::~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+}
+void PinnedBuf::reserve(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        fail(JG_ERR_OOM, "pinned host allocation of " + std::to_string(n) + " bytes failed");
+    }
+    cap = n;
+}
+
+EdgestoreDecoder::EdgestoreDecoder(const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int pbits,
+                                   int device)
+    : pbits_(pbits), device_(device) {
+    if (pbits < 0 || pbits > 16) fail(JG_ERR_ARG, "partition bits must be in [0, 16]");
+    DeviceGuard dg(device_);
+    for (int i = 0; i < 2; ++i) {
+        JG_HIP(hipStreamCreateWithFlags(&streams_[i], hipStreamNonBlocking));
+        chunks_[i] = std::make_unique<EdgestoreChunk>();
+        JG_HIP(hipEventCreate(&chunks_[i]->t0));
+        JG_HIP(hipEventCreate(&chunks_[i]->t1));
+    }
+    types_ = std::make_unique<TypeTable>(type_ids, type_mult, ntypes, streams_[0]);
+}
+
+EdgestoreDecoder::~EdgestoreDecoder() {
+    DeviceGuard dg(device_);
+    for (int i = 0; i < 2; ++i) {
+        if (streams_[i]) (void)hipStreamSynchronize(streams_[i]);
+        if (chunks_[i]) {
+            (void)hipEventDestroy(chunks_[i]->t0);
+            (void)hipEventDestroy(chunks_[i]->t1);
+        }
+        chunks_[i].reset();
+        if (streams_[i]) (void)hipStreamDestroy(streams_[i]);
+    }
+}
+
+void EdgestoreDecoder::add(const EdgestoreRows& r) {
+    edgestore_check(r);
+    DeviceGuard dg(device_);
+    const int slot = next_;
+    next_ ^= 1;
+    EdgestoreChunk& c = *chunks_[slot];
+    if (c.pending) complete(slot);  // its buffers are reused below
+    hipStream_t s = streams_[slot];
+    const int64_t R = r.nrows, E = r.nentries;
+    c.R = R;
+    c.E = E;
+    c.nbytes = r.nbytes;
+    // staging layout: off [E+1] i64 | roff [R+1] i64 | keys [R] u64 | vpos [E] i32 | bytes
+    const size_t o_off = 0, o_roff = o_off + (size_t)(E + 1) * 8, o_keys = o_roff + (size_t)(R + 1) * 8,
+                 o_vpos = o_keys + (size_t)R * 8, o_bytes = o_vpos + (size_t)E * 4;
+    c.staging.reserve(o_bytes + (size_t)r.nbytes + 1);
+    char* st = (char*)c.staging.p;
+    std::memcpy(st + o_off, r.entry_off, (size_t)(E + 1) * 8);
     if (R) {
-        edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, d_keys.get(), d_roff.get(), R, r.pbits, keep.get(),
-                                                            keep_v.get(), row_vid.get(), err.get());
+        std::memcpy(st + o_roff, r.row_off, (size_t)(R + 1) * 8);
+        std::memcpy(st + o_keys, r.keys, (size_t)R * 8);
+    }
+    if (E) std::memcpy(st + o_vpos, r.vpos, (size_t)E * 4);
+    if (r.nbytes) std::memcpy(st + o_bytes, r.bytes, (size_t)r.nbytes);
+    auto fit = [](auto& buf, int64_t n) {
+        if ((int64_t)buf.size() < std::max<int64_t>(n, 1)) buf.alloc(std::max<int64_t>(n, 1));
+    };
+    fit(c.d_bytes, r.nbytes + kBytePad);
+    fit(c.keep, R);
+    fit(c.keep_v, R);
+    fit(c.take, E);
+    fit(c.d_off, E + 1);
+    fit(c.d_roff, R + 1);
+    fit(c.row_vid, R);
+    fit(c.esrc, E);
+    fit(c.edst, E);
+    fit(c.block_row, (E + kChunk - 1) / kChunk + 1);
+    fit(c.d_keys, R);
+    fit(c.d_vpos, E);
+    fit(c.err, 1);
+    auto h2d = [&](void* d, size_t off, size_t bytes) {
+        if (bytes) JG_HIP(hipMemcpyAsync(d, st + off, bytes, hipMemcpyHostToDevice, s));
+    };
+    JG_HIP(hipEventRecord(c.t0, s));
+    h2d(c.d_bytes.get(), o_bytes, (size_t)r.nbytes);
+    h2d(c.d_off.get(), o_off, (size_t)(E + 1) * 8);
+    h2d(c.d_vpos.get(), o_vpos, (size_t)E * 4);
+    h2d(c.d_keys.get(), o_keys, (size_t)R * 8);
+    h2d(c.d_roff.get(), o_roff, (size_t)(R + 1) * 8);
+    JG_HIP(hipMemsetAsync(c.err.get(), 0, sizeof(int32_t), s));
+    const EntryView a{c.d_bytes.get(), c.d_off.get(), c.d_vpos.get(), types_->ids.get(), types_->mult.get(), types_->n};
+    if (R) {
+        edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, c.d_keys.get(), c.d_roff.get(), R, pbits_, c.keep.get(),
+                                                            c.keep_v.get(), c.row_vid.get(), c.err.get());
         JG_LAUNCH_CHECK();
     }
     if (E) {
-        block_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(d_roff.get(), R, block_row.get());
+        block_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(c.d_roff.get(), R, c.block_row.get());
         JG_LAUNCH_CHECK();
         edgestore_edges_kernel<<<grid_for((E + kEpt - 1) / kEpt, kBlock, 256 * 16), kBlock, 0, s>>>(
-            a, d_roff.get(), block_row.get(), R, E, keep.get(), row_vid.get(), r.pbits, take.get(), esrc.get(), edst.get(),
-            err.get());
+            a, c.d_roff.get(), c.block_row.get(), R, E, c.keep.get(), c.row_vid.get(), pbits_, c.take.get(),
+            c.esrc.get(), c.edst.get(), c.err.get());
         JG_LAUNCH_CHECK();
     }
-    JG_HIP(hipEventRecord(t1, s));
+    JG_HIP(hipEventRecord(c.t1, s));
+    c.pending = true;
+    ++chunks_added_;
+    rows_ += R;
+    entries_ += E;
+    bytes_ += r.nbytes;
+}
+
+void EdgestoreDecoder::complete(int slot) {
+    EdgestoreChunk& c = *chunks_[slot];
+    if (!c.pending) return;
+    c.pending = false;
+    hipStream_t s = streams_[slot];
     int32_t herr = 0;
-    JG_HIP(hipMemcpyAsync(&herr, err.get(), sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    JG_HIP(hipMemcpyAsync(&herr, c.err.get(), sizeof(int32_t), hipMemcpyDeviceToHost, s));
     JG_HIP(hipStreamSynchronize(s));
     float ms = 0;
-    JG_HIP(hipEventElapsedTime(&ms, t0, t1));
-    JG_HIP(hipEventDestroy(t0));
-    JG_HIP(hipEventDestroy(t1));
-    if (kernel_ms) *kernel_ms = ms;
+    JG_HIP(hipEventElapsedTime(&ms, c.t0, c.t1));
+    kernel_ms += ms;  // copy + decode of the chunk
     if (herr & kErrBadKey) fail(JG_ERR_ARG, "row key with an unrecognized vertex id type");
     if (herr & kErrPartitioned) fail(JG_ERR_ARG, "partitioned vertex row with no partition bits");
     if (herr & kErrMalformed) fail(JG_ERR_ARG, "malformed edgestore entry on a vertex row");
-    n = prim::compact_indices(keep_v.get(), R, idx.get(), s);
-    vid.alloc(std::max<int64_t>(n, 1));
-    if (n) {
-        gather_kernel<int64_t><<<grid_for(n), kBlock, 0, s>>>(row_vid.get(), idx.get(), n, vid.get());
+    const int64_t cap = std::max<int64_t>(std::max(c.R, c.E), 1);
+    if ((int64_t)idx_.size() < cap) idx_.alloc(cap);
+    if ((int64_t)tmp_.size() < cap) tmp_.alloc(cap);
+    const int64_t nk = prim::compact_indices(c.keep_v.get(), c.R, idx_.get(), s);
+    if (nk) {
+        gather_kernel<int64_t><<<grid_for(nk), kBlock, 0, s>>>(c.row_vid.get(), idx_.get(), nk, tmp_.get());
         JG_LAUNCH_CHECK();
+        grow_append(vid, n, tmp_.get(), nk, s);
     }
-    m = prim::compact_indices(take.get(), E, idx.get(), s);
-    src.alloc(std::max<int64_t>(m, 1));
-    dst.alloc(std::max<int64_t>(m, 1));
-    if (m) {
-        gather_kernel<int64_t><<<grid_for(m), kBlock, 0, s>>>(esrc.get(), idx.get(), m, src.get());
+    const int64_t mk = prim::compact_indices(c.take.get(), c.E, idx_.get(), s);
+    if (mk) {
+        int64_t m2 = m;
+        gather_kernel<int64_t><<<grid_for(mk), kBlock, 0, s>>>(c.esrc.get(), idx_.get(), mk, tmp_.get());
         JG_LAUNCH_CHECK();
-        gather_kernel<int64_t><<<grid_for(m), kBlock, 0, s>>>(edst.get(), idx.get(), m, dst.get());
+        grow_append(src, m, tmp_.get(), mk, s);
+        gather_kernel<int64_t><<<grid_for(mk), kBlock, 0, s>>>(c.edst.get(), idx_.get(), mk, tmp_.get());
         JG_LAUNCH_CHECK();
+        grow_append(dst, m2, tmp_.get(), mk, s);
     }
     JG_HIP(hipStreamSynchronize(s));
+}
+
+void EdgestoreDecoder::finish() {
+    DeviceGuard dg(device_);
+    // chunks complete in the order they were added
+    complete(next_);
+    complete(next_ ^ 1);
+}
+
+void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
+                        DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms) {
+    EdgestoreDecoder dec(r.type_ids, r.type_mult, r.ntypes, r.pbits, device);
+    dec.add(r);
+    dec.finish();
+    vid.swap(dec.vid);
+    src.swap(dec.src);
+    dst.swap(dec.dst);
+    n = dec.n;
+    m = dec.m;
+    if (kernel_ms) *kernel_ms = dec.kernel_ms;
 }
 
 }  // namespace jg

@@ -317,8 +317,44 @@ struct EdgestoreRows {
     int pbits;                 // cluster.max-partitions = 2^pbits
 };
 void edgestore_check(const EdgestoreRows& r);
-// On the current device and stream: vid = ids of the kept rows (row order), src/dst = their OUT edges.
-void edgestore_snapshot(const EdgestoreRows& r, hipStream_t s, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
+// Page-locked host memory (async H2D staging).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf();
+    void reserve(size_t bytes);
+};
+struct TypeTable;
+struct EdgestoreChunk;
+// The snapshot decoder on `device`: add() takes one chunk of rows (a row never spans chunks), stages it
+// in pinned memory and enqueues its copy and decode on one of two streams, then returns; the chunk
+// before it completes meanwhile (error check, compaction).  After finish(): vid[0, n) = ids of the
+// kept rows in the order added, src/dst[0, m) = their OUT edges (vertex ids; ghosts dropped later).
+struct EdgestoreDecoder {
+    EdgestoreDecoder(const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes, int pbits, int device);
+    ~EdgestoreDecoder();
+    void add(const EdgestoreRows& r);
+    void finish();
+    DevBuf<int64_t> vid, src, dst;
+    int64_t n = 0, m = 0;
+    float kernel_ms = 0;  // copy + decode time of every chunk (HIP events)
+    int64_t chunks_added_ = 0, rows_ = 0, entries_ = 0, bytes_ = 0;
+    int device() const { return device_; }
+
+   private:
+    void complete(int slot);
+    int pbits_, device_;
+    int next_ = 0;
+    hipStream_t streams_[2] = {nullptr, nullptr};
+    std::unique_ptr<EdgestoreChunk> chunks_[2];
+    std::unique_ptr<TypeTable> types_;
+    DevBuf<int64_t> idx_, tmp_;
+};
+// One-shot: vid = ids of the kept rows (row order), src/dst = their OUT edges, on `device`.
+void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
                         DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms);
 
 // ---- programs ----
@@ -352,7 +388,7 @@ struct Tune {
     // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
     // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light
     int64_t band_deg[4] = {128, 8, 0, 0};
-    int band_bits[4] = {0, 3, 3, 3};  // 0: automatic (auto_band_bits of the gathered vector's size)
+    int band_bits[4] = {-1, 3, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits of the vector)
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
     int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
     int fuse_finalize = 1;            // light rows and the split's finalize in one launch
@@ -376,6 +412,9 @@ struct Tune {
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)
+    int merge_nt = 0;                 // merge kernel: bit 0 non-temporal band loads, bit 1 non-temporal partial stores
+    int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power
+                                      // steps only (their rank and contribution are constant after that)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
 };

@@ -117,7 +117,12 @@ void pagerank_steps(Graph& g, int nsteps) {
             op.pos = g.vec_pos(sh, JG_ADJ_IN);
             op.damping = g.pr_damping;
             op.teleport = teleport;
-            launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get());
+            // Rows without in-edges: rank = (1-d)/N and contrib = rank/edgeCount from the first power step
+            // on.  Steps 0 and 1 write that constant into both contrib buffers (step 0 must still gather
+            // the initial values), later steps leave those rows alone.
+            const bool skip_empty = g.pr_steps >= 2 && tune().pr_skip_empty;
+            launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get(),
+                        skip_empty);
         }
         exchange_contrib(g, nxt);
         g.pr_cur = nxt;

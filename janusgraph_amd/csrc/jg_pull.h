@@ -346,13 +346,25 @@ struct SliceLdsGather {
     }
 };
 
-template <class Op, bool LDS>
+// NT: bit 0 = the streamed band arrays (col, heads, meta) are loaded non-temporally, bit 1 = the
+// partials are stored non-temporally (both are touched once per superstep; keep L2 / MALL for the
+// gathered vector).  Bands of fewer than 8 sub-slices (2^bits < 8) share each sub-slice among
+// 8 / 2^bits XCDs.
+template <class T>
+__device__ __forceinline__ void store_nt(T* p, T v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <class Op, bool LDS, int NT>
 __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
                                                                    typename Op::T* __restrict__ carry, HotSegs hs,
                                                                    int temporal) {
     using T = typename Op::T;
     extern __shared__ __align__(16) unsigned char merge_lds[];
-    const int per = (1 << a.bits) >> 3;  // sub-slices per XCD
+    const int S = 1 << a.bits;
+    const int xs = S < kXcds ? S : kXcds;  // sub-slice residues: h mod xs is fixed by the XCD
+    const int rep = kXcds / xs;            // XCDs sharing each sub-slice
+    const int per = S / xs;                // sub-slices per XCD
     const int w = (int)(blockIdx.x >> 3), W = (int)(gridDim.x >> 3);
     const int xcd = (int)(blockIdx.x & (kXcds - 1));
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -366,8 +378,10 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     // of all of them at once (one image restaged per round).
     const int rounds = temporal ? per : 1;
     for (int rd = 0; rd < rounds; ++rd) {
-    const int h = xcd | ((temporal ? rd : w % per) << 3);
-    const int64_t g = temporal ? w : w / per, G = temporal ? W : W / per;  // this block's rank among h's blocks
+    const int h = (xcd % xs) | ((temporal ? rd : w % per) << 3);
+    // this block's rank among h's blocks
+    const int64_t g = (int64_t)(temporal ? w : w / per) * rep + xcd / xs;
+    const int64_t G = (int64_t)(temporal ? W : W / per) * rep;
     if constexpr (LDS) {
         if (rd > 0) __syncthreads();  // every wave is done with the previous round's image
         // LDS line i = the line of sub-slice h in hot line group i (a permutation of each aligned group)
@@ -418,9 +432,18 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     };
     auto meta_idx = [&](int64_t kk) { return 2 * (base + kk) + (lane & 1); };
     auto head_idx = [&](int64_t kk) { return (base + kk) * kWave + lane; };
-    int4 cv0 = col_ptr(k)[0], cv1 = col_ptr(k)[1];
-    uint32_t hb = a.heads[head_idx(k)];
-    int32_t mw = a.meta[meta_idx(k)];
+    auto ld = [](const auto* p) {
+        if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(p);
+        else return *p;
+    };
+    auto ld4 = [&](const int4* p) {
+        using v4i = int __attribute__((ext_vector_type(4)));
+        const v4i x = ld(reinterpret_cast<const v4i*>(p));
+        return make_int4(x.x, x.y, x.z, x.w);
+    };
+    int4 cv0 = ld4(col_ptr(k)), cv1 = ld4(col_ptr(k) + 1);
+    uint32_t hb = ld(a.heads + head_idx(k));
+    int32_t mw = ld(a.meta + meta_idx(k));
     for (;;) {
         const int64_t t = base + k;
         const int64_t e0 = hbegin + k * kMergeTask;
@@ -450,10 +473,10 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         }
         const int64_t kn = k + step;
         if (kn < ntask) {
-            cv0 = col_ptr(kn)[0];
-            cv1 = col_ptr(kn)[1];
-            hb = a.heads[head_idx(kn)];
-            mw = a.meta[meta_idx(kn)];
+            cv0 = ld4(col_ptr(kn));
+            cv1 = ld4(col_ptr(kn) + 1);
+            hb = ld(a.heads + head_idx(kn));
+            mw = ld(a.meta + meta_idx(kn));
         }
         // head numbers: exclusive wave scan of the per-lane head counts
         const int cnt = __builtin_popcount(hbc);
@@ -466,8 +489,8 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         const int hbase = incl - cnt;  // head number of this lane's first head
         const bool valid_lane = kMergeEpl * lane < n;
         auto emit = [&](int hh, T val) {  // segment of head hh
-            if (hh == 0 && carry_in) carry[t] = val;
-            else partial[j0 + hh] = val;
+            if (hh == 0 && carry_in) store_nt(carry + t, val, (NT & 2) != 0);
+            else store_nt(partial + j0 + hh, val, (NT & 2) != 0);
         };
         // lane-local: the part before the first head (continues the segment on the left), inner
         // segments (emitted here) and the segment of the last head (continues to the right)
@@ -584,8 +607,11 @@ __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, cons
             T v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
-                j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
+                j[u] = -1;
+                if (h0 + u < S) {  // bands of fewer than 8 sub-slices
+                    const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
+                    j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
+                }
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
@@ -632,13 +658,17 @@ __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a,
 // `split_partial` ([8 * plan.split_rows], nullable) enables the XCD split of the heavy rows.
 constexpr int64_t kMaxLdsBytes = 160 * 1024;
 
+// `skip_empty`: the rows without entries (the degree-sorted suffix, class kZeroClass) are not
+// finalised, for programs whose value there no longer changes (PageRank after two power steps).
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
-                 Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr) {
+                 Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr,
+                 bool skip_empty = false) {
     using T = typename Op::T;
     const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
     PullArgs a = make_pull_args(csr, plan, split);
-    const int64_t blocks = split ? plan.light_block_begin[kNumClasses] : plan.total_blocks();
+    if (skip_empty) a.class_block_begin[kNumClasses] = a.class_block_begin[kZeroClass];
+    const int64_t blocks = a.class_block_begin[kNumClasses];
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
     // With the split, the light rows (and hub finalize) run on the side stream beside the merge
     // kernels: they touch other rows, and their 256-thread, LDS-free blocks fit next to a merge
@@ -654,7 +684,13 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     if (split) {
         static bool attr = false;
         if (!attr) {
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 1>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 2>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
             attr = true;
         }
@@ -687,11 +723,17 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
             const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
-            if (hs.hs > 0)
-                pull_merge_kernel<Op, true><<<grid, kMergeThreads, (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T), ms>>>(
-                    ma, op, part, carry, hs, temporal);
-            else
-                pull_merge_kernel<Op, false><<<grid, kMergeThreads, 0, ms>>>(ma, op, part, carry, hs, temporal);
+            const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) : 0;
+            auto go = [&](auto kern) { kern<<<grid, kMergeThreads, lds, ms>>>(ma, op, part, carry, hs, temporal); };
+            const int nt = tune().merge_nt & 3;
+            if (hs.hs > 0) {
+                if (nt == 0) go(pull_merge_kernel<Op, true, 0>);
+                else if (nt == 1) go(pull_merge_kernel<Op, true, 1>);
+                else if (nt == 2) go(pull_merge_kernel<Op, true, 2>);
+                else go(pull_merge_kernel<Op, true, 3>);
+            } else {
+                go(pull_merge_kernel<Op, false, 0>);
+            }
             JG_LAUNCH_CHECK();
         }
         if (mside) {

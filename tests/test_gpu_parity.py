@@ -305,7 +305,8 @@ def test_errors_are_status_codes(ctx):
         g.pagerank_step(1)
 
 
-@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last"])
+@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
+                                  "split_sub1", "split_sub2_4", "split_nt", "pr_noskip"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -321,7 +322,12 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "split_light_lds": [("pull_split", 1), ("light_lds", 8192)],
              "split_merge_overlap": [("pull_split", 1), ("merge_overlap", 1)],
              "split_merge_wgs2": [("pull_split", 1), ("merge_wgs", 2)],
-             "split_fin_last": [("pull_split", 1), ("fin_last", 1)]}[mode]
+             "split_fin_last": [("pull_split", 1), ("fin_last", 1)],
+             "split_sub1": [("band1_sub", 1)],
+             "split_sub2_4": [("band0_deg", 64), ("band0_sub", 4), ("band1_deg", 16), ("band1_sub", 2),
+                              ("band2_deg", 4), ("band2_sub", 1)],
+             "split_nt": [("merge_nt", 3)],
+             "pr_noskip": [("pr_skip_empty", 0)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -349,7 +355,10 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("slice_lds", 1)
-        for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0)):
+        _lib.tune_set("merge_nt", 0)
+        _lib.tune_set("pr_skip_empty", 1)
+        for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
+                     ("band2_bit", 3)):
             _lib.tune_set(k, v)
 
 
