@@ -174,9 +174,12 @@ int jg_builder_add_vertices(jg_builder* b, const int64_t* vid, int64_t n);
 int jg_builder_add_edges(jg_builder* b, const int64_t* src, const int64_t* dst, const int32_t* weight, int64_t m);
 int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
                           int32_t partition_bits);
+/* entry_weight[nentries] (nullable; on every chunk or none): the Integer weight property of each
+ * entry's edge for jg_shortest_distance (JG_WEIGHT_ABSENT: the edge has none), read by the caller
+ * with the edge's own serializer; ignored for entries that are not kept edges. */
 int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                         const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
-                        int64_t nentries);
+                        const int32_t* entry_weight, int64_t nentries);
 int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out);
 int jg_builder_destroy(jg_builder* b);
 /* vid_out[i] = the id of vertex offset + i in output order (the order vid[] / the kept rows were given). */
@@ -204,7 +207,12 @@ int jg_pagerank_step(jg_graph* g, int32_t nsteps);
 int jg_pagerank_end(jg_graph* g, double* rank_out, double* edge_count_out);
 
 /* ShortestDistanceVertexProgram: dist_out[v] = min over paths v -> ... -> seed of <= max_depth hops
- * of the summed edge weights (int64), or -1 where Fulgora leaves DISTANCE absent. */
+ * of the summed edge weights (int64; weights may be negative), or JG_DIST_ABSENT where Fulgora leaves
+ * DISTANCE absent.  A weight of JG_WEIGHT_ABSENT marks an edge without the weight property: if a
+ * message crosses one, the run fails with JG_ERR_ARG (Fulgora's edge function throws there,
+ * ShortestDistanceVertexProgram.java:69); untraversed ones are harmless. */
+#define JG_DIST_ABSENT INT64_MIN
+#define JG_WEIGHT_ABSENT INT32_MIN
 int jg_shortest_distance(jg_graph* g, int64_t seed_vid, int32_t max_depth, int64_t* dist_out);
 
 /* Hop depth from each of nsrc sources (nsrc <= 64 runs as one bit-parallel multi-source BFS);

@@ -26,6 +26,8 @@ ADJ_OUT, ADJ_IN, ADJ_BOTH = 1, 2, 4
 DIR_OUT, DIR_IN, DIR_BOTH = 1, 2, 3
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
 FULGORA_HARD_QUERY_LIMIT = 100000
+DIST_ABSENT = np.iinfo(np.int64).min   # JG_DIST_ABSENT: DISTANCE never written
+WEIGHT_ABSENT = np.iinfo(np.int32).min  # JG_WEIGHT_ABSENT: the edge has no weight property
 UNIQUE_ID_BYTES = 128
 
 # every function the header declares (checked by tests/test_abi.py against include/janusgpu.h)
@@ -119,7 +121,7 @@ def load():
         "jg_builder_add_vertices": ([_P, _P, _i64], ctypes.c_int),
         "jg_builder_add_edges": ([_P, _P, _P, _P, _i64], ctypes.c_int),
         "jg_builder_set_schema": ([_P, _P, _P, _i32, _i32], ctypes.c_int),
-        "jg_builder_add_rows": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _i64], ctypes.c_int),
+        "jg_builder_add_rows": ([_P, _P, _i64, _P, _P, _i64, _P, _P, _P, _i64], ctypes.c_int),
         "jg_builder_finish": ([_P, ctypes.c_uint32, _PP], ctypes.c_int),
         "jg_builder_destroy": ([_P], ctypes.c_int),
         "jg_graph_vertex_ids": ([_P, _i64, _i64, _P], ctypes.c_int),
@@ -308,7 +310,7 @@ class Builder:
         self._schema = (tid, tm)
         check(load().jg_builder_set_schema(self._h, _ptr(tid), _ptr(tm), len(tid), int(partition_bits)))
 
-    def add_rows(self, row_keys, row_entry_off, data, entry_off, value_pos):
+    def add_rows(self, row_keys, row_entry_off, data, entry_off, value_pos, entry_weight=None):
         keys = np.ascontiguousarray(row_keys, np.uint64)
         roff = np.ascontiguousarray(row_entry_off, np.int64)
         data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data,
@@ -317,8 +319,11 @@ class Builder:
         vpos = np.ascontiguousarray(value_pos, np.int32)
         if len(roff) != len(keys) + 1 or len(off) != len(vpos) + 1:
             raise ValueError("row_entry_off needs nrows + 1 offsets, entry_off nentries + 1")
+        w = None if entry_weight is None else np.ascontiguousarray(entry_weight, np.int32)
+        if w is not None and len(w) != len(vpos):
+            raise ValueError("entry_weight needs one value per entry")
         check(load().jg_builder_add_rows(self._h, _ptr(keys), len(keys), _ptr(roff), _ptr(data), len(data), _ptr(off),
-                                         _ptr(vpos), len(vpos)))
+                                         _ptr(vpos), _ptr(w), len(vpos)))
 
     def finish(self, flags=ADJ_IN | ADJ_OUT | ADJ_BOTH) -> "Graph":
         h = ctypes.c_void_p()

@@ -221,7 +221,7 @@ class GpuGraphComputer:
                 dist = g.shortest_distance(vp.seed, vp.max_depth)
             finally:
                 g.close()
-            props = {int(v): {vp.DISTANCE: int(d)} for v, d in zip(vid, dist) if d >= 0}
+            props = {int(v): {vp.DISTANCE: int(d)} for v, d in zip(vid, dist) if d != _lib.DIST_ABSENT}
             return vid, props, vp.max_depth, {}
         if isinstance(vp, ConnectedComponentVertexProgram):
             vid, src, dst, _ = g0.snapshot()

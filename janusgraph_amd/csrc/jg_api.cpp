@@ -678,7 +678,7 @@ int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* 
 
 int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                         const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
-                        int64_t nentries) {
+                        const int32_t* entry_weight, int64_t nentries) {
     JG_GUARD_BEGIN
     JG_ARG(b, "null builder");
     if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
@@ -687,9 +687,10 @@ int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, 
     if (!b->dec)
         b->dec = std::make_unique<jg::EdgestoreDecoder>(b->type_ids.data(), b->type_mult.data(),
                                                         (int32_t)b->type_ids.size(), b->pbits, builder_device(b));
-    const jg::EdgestoreRows r{row_keys, nrows,      row_entry_off, bytes,
-                              nbytes,   entry_off,  value_pos,     nentries,
-                              b->type_ids.data(), b->type_mult.data(), (int32_t)b->type_ids.size(), b->pbits};
+    jg::EdgestoreRows r{row_keys, nrows,      row_entry_off, bytes,
+                        nbytes,   entry_off,  value_pos,     nentries,
+                        b->type_ids.data(), b->type_mult.data(), (int32_t)b->type_ids.size(), b->pbits};
+    r.weight = entry_weight;
     b->dec->add(r);
     JG_GUARD_END
 }
@@ -714,8 +715,9 @@ int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
         b->dec->finish();
         decode_ms = b->dec->kernel_ms;
         chunks = b->dec->chunks_added_;
+        if (b->dec->weighted == 1 && b->dec->w.size() == 0) b->dec->w.alloc(1);
         jg::build_from_device_ids(g, dev0, builder_stream(b), b->dec->vid.get(), b->dec->n, b->dec->src.get(),
-                                  b->dec->dst.get(), nullptr, b->dec->m);
+                                  b->dec->dst.get(), b->dec->weighted == 1 ? b->dec->w.get() : nullptr, b->dec->m);
     } else {
         jg::DeviceGuard dg(dev0);
         if (b->vid.size() == 0) b->vid.alloc(1);

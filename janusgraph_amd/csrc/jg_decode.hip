@@ -474,7 +474,8 @@ struct EdgestoreChunk {
     DevBuf<uint8_t> d_bytes, keep, keep_v, take;
     DevBuf<int64_t> d_off, d_roff, row_vid, esrc, edst, block_row;
     DevBuf<uint64_t> d_keys;
-    DevBuf<int32_t> d_vpos, err;
+    DevBuf<int32_t> d_vpos, err, d_w;
+    bool weighted = false;
     hipEvent_t t0 = nullptr, t1 = nullptr;
     bool pending = false;
 };
@@ -539,6 +540,9 @@ EdgestoreDecoder::~EdgestoreDecoder() {
 
 void EdgestoreDecoder::add(const EdgestoreRows& r) {
     edgestore_check(r);
+    const int wmode = r.weight ? 1 : 0;
+    if (weighted >= 0 && weighted != wmode) fail(JG_ERR_ARG, "entry weights must be given for every chunk or none");
+    weighted = wmode;
     DeviceGuard dg(device_);
     const int slot = next_;
     next_ ^= 1;
@@ -549,9 +553,11 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     c.R = R;
     c.E = E;
     c.nbytes = r.nbytes;
-    // staging layout: off [E+1] i64 | roff [R+1] i64 | keys [R] u64 | vpos [E] i32 | bytes
+    // staging layout: off [E+1] i64 | roff [R+1] i64 | keys [R] u64 | vpos [E] i32 | weight [E] i32 | bytes
     const size_t o_off = 0, o_roff = o_off + (size_t)(E + 1) * 8, o_keys = o_roff + (size_t)(R + 1) * 8,
-                 o_vpos = o_keys + (size_t)R * 8, o_bytes = o_vpos + (size_t)E * 4;
+                 o_vpos = o_keys + (size_t)R * 8, o_w = o_vpos + (size_t)E * 4,
+                 o_bytes = o_w + (r.weight ? (size_t)E * 4 : 0);
+    c.weighted = r.weight != nullptr;
     c.staging.reserve(o_bytes + (size_t)r.nbytes + 1);
     char* st = (char*)c.staging.p;
     std::memcpy(st + o_off, r.entry_off, (size_t)(E + 1) * 8);
@@ -560,6 +566,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
         std::memcpy(st + o_keys, r.keys, (size_t)R * 8);
     }
     if (E) std::memcpy(st + o_vpos, r.vpos, (size_t)E * 4);
+    if (E && r.weight) std::memcpy(st + o_w, r.weight, (size_t)E * 4);
     if (r.nbytes) std::memcpy(st + o_bytes, r.bytes, (size_t)r.nbytes);
     auto fit = [](auto& buf, int64_t n) {
         if ((int64_t)buf.size() < std::max<int64_t>(n, 1)) buf.alloc(std::max<int64_t>(n, 1));
@@ -577,6 +584,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     fit(c.d_keys, R);
     fit(c.d_vpos, E);
     fit(c.err, 1);
+    if (r.weight) fit(c.d_w, E);
     auto h2d = [&](void* d, size_t off, size_t bytes) {
         if (bytes) JG_HIP(hipMemcpyAsync(d, st + off, bytes, hipMemcpyHostToDevice, s));
     };
@@ -586,6 +594,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     h2d(c.d_vpos.get(), o_vpos, (size_t)E * 4);
     h2d(c.d_keys.get(), o_keys, (size_t)R * 8);
     h2d(c.d_roff.get(), o_roff, (size_t)(R + 1) * 8);
+    if (r.weight) h2d(c.d_w.get(), o_w, (size_t)E * 4);
     JG_HIP(hipMemsetAsync(c.err.get(), 0, sizeof(int32_t), s));
     const EntryView a{c.d_bytes.get(), c.d_off.get(), c.d_vpos.get(), types_->ids.get(), types_->mult.get(), types_->n};
     if (R) {
@@ -626,6 +635,7 @@ void EdgestoreDecoder::complete(int slot) {
     const int64_t cap = std::max<int64_t>(std::max(c.R, c.E), 1);
     if ((int64_t)idx_.size() < cap) idx_.alloc(cap);
     if ((int64_t)tmp_.size() < cap) tmp_.alloc(cap);
+    if (c.weighted && (int64_t)tmpw_.size() < cap) tmpw_.alloc(cap);
     const int64_t nk = prim::compact_indices(c.keep_v.get(), c.R, idx_.get(), s);
     if (nk) {
         gather_kernel<int64_t><<<grid_for(nk), kBlock, 0, s>>>(c.row_vid.get(), idx_.get(), nk, tmp_.get());
@@ -641,6 +651,11 @@ void EdgestoreDecoder::complete(int slot) {
         gather_kernel<int64_t><<<grid_for(mk), kBlock, 0, s>>>(c.edst.get(), idx_.get(), mk, tmp_.get());
         JG_LAUNCH_CHECK();
         grow_append(dst, m2, tmp_.get(), mk, s);
+        if (c.weighted) {  // kept entries are edges: their weights follow the same compaction
+            gather_kernel<int32_t><<<grid_for(mk), kBlock, 0, s>>>(c.d_w.get(), idx_.get(), mk, tmpw_.get());
+            JG_LAUNCH_CHECK();
+            grow_append(w, mw, tmpw_.get(), mk, s);
+        }
     }
     JG_HIP(hipStreamSynchronize(s));
 }

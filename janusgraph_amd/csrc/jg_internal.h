@@ -315,6 +315,7 @@ struct EdgestoreRows {
     const int8_t* type_mult;
     int32_t ntypes;
     int pbits;                 // cluster.max-partitions = 2^pbits
+    const int32_t* weight = nullptr;  // nentries, nullable: the Integer weight property of each entry's edge
 };
 void edgestore_check(const EdgestoreRows& r);
 // Page-locked host memory (async H2D staging).
@@ -339,7 +340,9 @@ struct EdgestoreDecoder {
     void add(const EdgestoreRows& r);
     void finish();
     DevBuf<int64_t> vid, src, dst;
-    int64_t n = 0, m = 0;
+    DevBuf<int32_t> w;    // weights of the kept edges (when every chunk carried entry weights)
+    int64_t n = 0, m = 0, mw = 0;
+    int weighted = -1;    // -1 no chunk yet, 0 / 1: the chunks carry no / per-entry weights
     float kernel_ms = 0;  // copy + decode time of every chunk (HIP events)
     int64_t chunks_added_ = 0, rows_ = 0, entries_ = 0, bytes_ = 0;
     int device() const { return device_; }
@@ -352,6 +355,7 @@ struct EdgestoreDecoder {
     std::unique_ptr<EdgestoreChunk> chunks_[2];
     std::unique_ptr<TypeTable> types_;
     DevBuf<int64_t> idx_, tmp_;
+    DevBuf<int32_t> tmpw_;
 };
 // One-shot: vid = ids of the kept rows (row order), src/dst = their OUT edges, on `device`.
 void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,

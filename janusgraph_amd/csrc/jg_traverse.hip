@@ -410,12 +410,16 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
 }
 
 // ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
+// An edge without the weight property carries kWeightAbsent: a message crossing it is an error, as
+// in Fulgora; distances may be negative, so an absent DISTANCE is reported as INT64_MIN.
+constexpr int32_t kWeightAbsent = INT32_MIN;
 __global__ __launch_bounds__(kBlock) void sd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ wt,
                                                          const int32_t* __restrict__ frontier, int64_t fsize,
                                                          const long long* __restrict__ msg, long long* __restrict__ best,
                                                          int32_t* __restrict__ touched,
-                                                         unsigned long long* __restrict__ tsize) {
+                                                         unsigned long long* __restrict__ tsize,
+                                                         int32_t* __restrict__ err) {
     const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
     const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
     const int sub = threadIdx.x % kTdLanes;
@@ -439,9 +443,13 @@ __global__ __launch_bounds__(kBlock) void sd_push_kernel(const int64_t* __restri
             int32_t u = 0;
             if (k < len) {
                 u = col[j0 + k];
-                const long long cand = mw + (long long)(wt ? wt[j0 + k] : 1);
-                const long long old = atomicMin(&best[u], cand);
-                first = old == LLONG_MAX;
+                const int32_t wk = wt ? wt[j0 + k] : 1;
+                if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
+                    *err = 1;
+                } else {
+                    const long long old = atomicMin(&best[u], mw + (long long)wk);
+                    first = old == LLONG_MAX;
+                }
             }
             wave_append(first, u, touched, tsize);
         }
@@ -478,7 +486,8 @@ __global__ __launch_bounds__(kBlock) void ssd_push_kernel(const int64_t* __restr
                                                           const int32_t* __restrict__ frontier, int64_t fsize,
                                                           const long long* __restrict__ msg, long long* __restrict__ best,
                                                           int tbits, int32_t* __restrict__ touched,
-                                                          unsigned long long* __restrict__ tsize) {
+                                                          unsigned long long* __restrict__ tsize,
+                                                          int32_t* __restrict__ err) {
     const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
     const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
     const int sub = threadIdx.x % kTdLanes;
@@ -502,9 +511,13 @@ __global__ __launch_bounds__(kBlock) void ssd_push_kernel(const int64_t* __restr
             int32_t u = 0;
             if (k < len) {
                 u = col[j0 + k];
-                const long long cand = mw + (long long)(wt ? wt[j0 + k] : 1);
-                const long long old = atomicMin(&best[u], cand);
-                first = old == LLONG_MAX && (u >> tbits) == 0;
+                const int32_t wk = wt ? wt[j0 + k] : 1;
+                if (wk == kWeightAbsent) {
+                    *err = 1;
+                } else {
+                    const long long old = atomicMin(&best[u], mw + (long long)wk);
+                    first = old == LLONG_MAX && (u >> tbits) == 0;
+                }
             }
             wave_append(first, u, touched, tsize);
         }
@@ -1213,6 +1226,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
 // adjacency's halo plan.  Candidates for remote vertices collect in their halo slots and go to the
 // owners by the reverse halo exchange (the transpose of the PageRank/CC exchange), which take their
 // min; frontier sizes are summed over shards and ranks every superstep.
+static const char* const kMissingWeight =
+    "a message crossed an edge without the weight property (ShortestDistanceVertexProgram.java:69 "
+    "edge.value(weightProperty) throws)";
+
 static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
     Ctx& ctx = *g.ctx;
     const size_t ns = g.shards.size();
@@ -1225,6 +1242,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         DevBuf<long long> best, dist, msg, rbuf;
         DevBuf<int32_t> fa, fb, touched;
         DevBuf<unsigned long long> sizes;
+        DevBuf<int32_t> err;
         int64_t fsize = 0;
     };
     std::vector<St> st(ns);
@@ -1243,6 +1261,8 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         t.touched.alloc(rows);
         t.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
         t.sizes.alloc(2);
+        t.err.alloc(1);
+        JG_HIP(hipMemsetAsync(t.err.get(), 0, sizeof(int32_t), sh.stream));
         fill_ll_kernel<<<grid_for(h.C), kBlock, 0, sh.stream>>>(t.best.get(), h.C, LLONG_MAX);
         fill_ll_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.dist.get(), sh.rows, LLONG_MIN);  // absent
         JG_LAUNCH_CHECK();
@@ -1277,7 +1297,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
             if (t.fsize > 0) {
                 ssd_push_kernel<<<grid_for(t.fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
                     sh.in.row_ptr.get(), sh.in.col.get(), g.has_weights ? sh.in.weight.get() : nullptr, t.fa.get(),
-                    t.fsize, t.msg.get(), t.best.get(), sh.halo_in.tbits, t.touched.get(), t.sizes.get());
+                    t.fsize, t.msg.get(), t.best.get(), sh.halo_in.tbits, t.touched.get(), t.sizes.get(), t.err.get());
                 JG_LAUNCH_CHECK();
             }
         }
@@ -1327,13 +1347,18 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         (void)hipEventDestroy(t0);
         (void)hipEventDestroy(t1);
     }
+    int missing = 0;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh.device);
+        int32_t e = 0;
+        copy_d2h(&e, st[i].err.get(), sizeof e, sh.stream);
+        missing |= e;
         std::vector<long long> h((size_t)sh.rows);
         if (sh.rows) copy_d2h(h.data(), st[i].dist.get(), sh.rows * sizeof(long long), sh.stream);
-        for (int64_t l = 0; l < sh.rows; ++l) dist_out[sh.dense_of_local[l]] = h[l] == LLONG_MIN ? -1 : h[l];
+        for (int64_t l = 0; l < sh.rows; ++l) dist_out[sh.dense_of_local[l]] = h[l];  // LLONG_MIN: absent
     }
+    if (allreduce_or(g, missing)) fail(JG_ERR_ARG, kMissingWeight);
     ctx.last.compute_ms = ms;
     ctx.last.levels = levels;
     ctx.last.supersteps = max_depth;
@@ -1353,7 +1378,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
     const int64_t rows = sh.rows;
     int shard = 0;
     const int64_t seed = local_of_vid(g, seed_vid, &shard);
-    std::vector<int64_t> host(rows, -1);
+    std::vector<int64_t> host(rows, LLONG_MIN);  // absent
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
@@ -1366,13 +1391,15 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         levels = dobfs_single(ctx, sh, c, seed, max_depth, depth.get(), nullptr);
         std::vector<int32_t> h(rows);
         if (rows) copy_d2h(h.data(), depth.get(), rows * sizeof(int32_t), s);
-        for (int64_t l = 0; l < rows; ++l) host[l] = h[l];
+        for (int64_t l = 0; l < rows; ++l) host[l] = h[l] >= 0 ? h[l] : LLONG_MIN;
     } else if (seed >= 0) {
         DevBuf<long long> dist(std::max<int64_t>(rows, 1)), msg(std::max<int64_t>(rows, 1)),
             best(std::max<int64_t>(rows, 1));
         DevBuf<int32_t> fa(std::max<int64_t>(rows, 1)), fb(std::max<int64_t>(rows, 1)),
             touched(std::max<int64_t>(rows, 1));
         DevBuf<unsigned long long> sizes(2);
+        DevBuf<int32_t> err(1);
+        JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
         fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MIN);  // absent
         fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(best.get(), rows, LLONG_MAX);
         JG_LAUNCH_CHECK();
@@ -1386,7 +1413,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
             JG_HIP(hipMemsetAsync(sizes.get(), 0, 2 * sizeof(unsigned long long), s));
             sd_push_kernel<<<grid_for(fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, s>>>(
                 sh.in.row_ptr.get(), sh.in.col.get(), sh.in.weight.get(), fa.get(), fsize, msg.get(), best.get(),
-                touched.get(), sizes.get());
+                touched.get(), sizes.get(), err.get());
             JG_LAUNCH_CHECK();
             unsigned long long ts = 0;
             JG_HIP(hipMemcpyAsync(&ts, sizes.get(), sizeof ts, hipMemcpyDeviceToHost, s));
@@ -1405,7 +1432,10 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         }
         std::vector<long long> h(rows);
         if (rows) copy_d2h(h.data(), dist.get(), rows * sizeof(long long), s);
-        for (int64_t l = 0; l < rows; ++l) host[l] = h[l] == LLONG_MIN ? -1 : h[l];
+        for (int64_t l = 0; l < rows; ++l) host[l] = h[l];
+        int32_t e = 0;
+        copy_d2h(&e, err.get(), sizeof e, s);
+        if (e) fail(JG_ERR_ARG, kMissingWeight);
     }
     JG_HIP(hipEventRecord(t1, s));
     JG_HIP(hipEventSynchronize(t1));

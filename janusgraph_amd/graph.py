@@ -76,17 +76,16 @@ class InMemoryGraph:
     # --- OLAP snapshot ---
     def snapshot(self, weight_property: str | None = None):
         """(vid, src, dst, weight): existing vertices + every stored edge (ghost endpoints included;
-        the library drops them).  weight: int32 edge property per edge, or None."""
+        the library drops them).  weight: int32 edge property per edge (WEIGHT_ABSENT where the edge
+        has none: Fulgora only fails if a message crosses such an edge), or None."""
         vid = np.fromiter((v.id for v in self.vertices.values() if not v.ghost), dtype=np.int64)
         src = np.fromiter((e.out_id for e in self.edges), dtype=np.int64, count=len(self.edges))
         dst = np.fromiter((e.in_id for e in self.edges), dtype=np.int64, count=len(self.edges))
         weight = None
         if weight_property is not None:
-            w = []
-            for e in self.edges:
-                if weight_property not in e.properties:
-                    raise KeyError(f"edge {e.out_id}->{e.in_id} has no property '{weight_property}'")
-                w.append(int(e.properties[weight_property]))
+            from ._lib import WEIGHT_ABSENT
+            w = [int(e.properties[weight_property]) if weight_property in e.properties else int(WEIGHT_ABSENT)
+                 for e in self.edges]
             weight = np.asarray(w, dtype=np.int32)
         return vid, src, dst, weight
 

@@ -274,12 +274,15 @@ JO_API void jo_build_in_csr(int64_t n, int64_t m, const int32_t* src, const int3
  *                t-1, each + weight; min-combined (ShortestDistanceMessageCombiner.java:29-31);
  *                if DISTANCE absent or larger: set it and send (:123-140)
  *   terminate at iteration >= maxDepth (:144-146)
- * weight == NULL means weight 1 on every edge.  dist[v] = -1 where DISTANCE stays absent.
+ * weight == NULL means weight 1 on every edge.  dist[v] = INT64_MIN where DISTANCE stays absent (any
+ * long is a valid distance: weights may be negative).  weight[e] == INT32_MIN marks an edge without
+ * the weight property: Fulgora's edge function (:69, edge.<Integer>value(weightProperty)) throws
+ * when a message crosses it, so the run returns -1 if one does (0 otherwise).
  * ------------------------------------------------------------------------------------------ */
-JO_API void jo_shortest_distance(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
-                                 const int32_t* weight, int64_t seed, int max_depth, int64_t* dist) {
-    for (int64_t v = 0; v < n; ++v) dist[v] = -1;
-    if (seed < 0 || seed >= n) return;
+JO_API int jo_shortest_distance(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
+                                const int32_t* weight, int64_t seed, int max_depth, int64_t* dist) {
+    for (int64_t v = 0; v < n; ++v) dist[v] = INT64_MIN;
+    if (seed < 0 || seed >= n) return 0;
     jo_csr out;
     jo_csr_build(n, m, src, dst, &out);
     const int64_t NONE = INT64_MIN; /* absent message / absent DISTANCE */
@@ -289,14 +292,16 @@ JO_API void jo_shortest_distance(int64_t n, int64_t m, const int32_t* src, const
     for (int64_t v = 0; v < n; ++v) msg[v] = NONE;
     dist[seed] = 0;
     msg[seed] = 0;
+    int missing = 0;
     for (int t = 1; t <= max_depth; ++t) {
         int any = 0;
-#pragma omp parallel for schedule(dynamic, 4096) reduction(| : any)
+#pragma omp parallel for schedule(dynamic, 4096) reduction(| : any, missing)
         for (int64_t v = 0; v < n; ++v) {
             int64_t best = NONE;
             for (int64_t k = out.ptr[v]; k < out.ptr[v + 1]; ++k) {
                 const int64_t mw = msg[out.other[k]];
                 if (mw == NONE) continue;
+                if (weight && weight[out.eidx[k]] == INT32_MIN) { missing = 1; continue; }
                 const int64_t cand = mw + (weight ? (int64_t)weight[out.eidx[k]] : 1);
                 if (best == NONE || cand < best) best = cand;
             }
@@ -310,10 +315,9 @@ JO_API void jo_shortest_distance(int64_t n, int64_t m, const int32_t* src, const
         int64_t* tmp = msg; msg = msg_next; msg_next = tmp;
         if (!any) break; /* nothing sent: later supersteps change nothing */
     }
-    for (int64_t v = 0; v < n; ++v)
-        if (dist[v] == NONE) dist[v] = -1; /* -1 = DISTANCE absent */
     free(msg); free(msg_next);
     jo_csr_free(&out);
+    return missing ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------------------------------

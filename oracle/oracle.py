@@ -48,7 +48,7 @@ def lib():
         L.jo_build_in_csr.restype = None
         L.jo_shortest_distance.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_void_p,
                                            ctypes.c_int64, ctypes.c_int, _i64p]
-        L.jo_shortest_distance.restype = None
+        L.jo_shortest_distance.restype = ctypes.c_int
         L.jo_bfs.argtypes = [ctypes.c_int64, ctypes.c_int64, _i32p, _i32p, ctypes.c_int, ctypes.c_int64,
                              ctypes.c_int, _i32p]
         L.jo_bfs.restype = None
@@ -147,15 +147,29 @@ def pagerank_superstep_csr(n, in_ptr, in_src, contrib_in, edge_count, damping, v
     return out
 
 
+DIST_ABSENT = np.iinfo(np.int64).min  # DISTANCE never written (jg_shortest_distance's marker too)
+WEIGHT_ABSENT = np.iinfo(np.int32).min  # an edge without the weight property
+
+
 def shortest_distance(n, src, dst, seed, max_depth, weight=None):
+    """dist[v], DIST_ABSENT where the property stays absent; ValueError if a message crosses an edge
+    whose weight is WEIGHT_ABSENT (Fulgora: edge.value(weightProperty) throws)."""
     src, dst = _i32(src), _i32(dst)
     dist = np.empty(max(n, 1), np.int64)
     w = None
     if weight is not None:
         weight = _i32(weight)
         w = weight.ctypes.data_as(ctypes.c_void_p)
-    lib().jo_shortest_distance(n, len(src), src, dst, w, int(seed), int(max_depth), dist)
+    if lib().jo_shortest_distance(n, len(src), src, dst, w, int(seed), int(max_depth), dist) != 0:
+        raise ValueError("a traversed edge has no weight property")
     return dist[:n]
+
+
+def golden_distance(d):
+    """The golden fixtures write an absent DISTANCE as -1 (their weights are positive)."""
+    d = np.asarray(d, np.int64).copy()
+    d[d == -1] = DIST_ABSENT
+    return d
 
 
 DIR_OUT, DIR_IN, DIR_BOTH = 1, 2, 3

@@ -349,7 +349,7 @@ def _sd_worker(rank, ws, port, out_q):
     full = np.zeros(ws * S, np.int64)
     for rr, vals in parts:
         full[rr * S:(rr + 1) * S] = vals
-    got = np.where(full[padded] == ABSENT, -1, full[padded])
+    got = full[padded]  # ABSENT == the oracle's DIST_ABSENT
     ok = None
     if rank == 0:
         ref = o.shortest_distance(n, s, t, seed_dense, max_depth, wt.astype(np.int32))

@@ -147,13 +147,24 @@ def test_ghost_vertices_do_not_count(ctx):
 
 
 def test_exception_propagates_to_caller(ctx):  # OLAPTest.vertexProgramExceptionPropagatesToCaller :312-329
+    """A message crossing an edge without the weight property fails the run through the Future, as
+    edge.value(weightProperty) throws in Fulgora (ShortestDistanceVertexProgram.java:69); an edge no
+    message crosses is harmless (VertexMemoryHandler.java:136-138 applies the edge function to
+    present messages only)."""
     g = jg.InMemoryGraph()
-    a, b = g.add_vertex(), g.add_vertex()
-    g.add_edge(a, b)  # no "distance" property
+    a, b, c = g.add_vertex(), g.add_vertex(), g.add_vertex()
+    g.add_edge(a, b)               # never crossed: a pulls over a->b, b never sends
+    g.add_edge(c, a, distance=-4)  # a negative distance is a distance, not "absent"
+    vp = jg.ShortestDistanceVertexProgram.build().seed(a.id).maxDepth(3).create(g)
+    view = jg.GpuGraphComputer(g, context=ctx).program(vp).resultMode(jg.ResultMode.LOCALTX).submit().result().graph()
+    assert view.value(a.id, vp.DISTANCE) == 0 and view.value(c.id, vp.DISTANCE) == -4
+    assert vp.DISTANCE not in view.properties(b.id)
+    g.add_edge(b, a)               # crossed at superstep 1: b pulls a's message over b->a
     vp = jg.ShortestDistanceVertexProgram.build().seed(a.id).maxDepth(3).create(g)
     fut = jg.GpuGraphComputer(g, context=ctx).program(vp).submit()
-    with pytest.raises(KeyError):
+    with pytest.raises(jg.JanusGpuError) as e:
         fut.result()
+    assert "weight property" in str(e.value)
 
 
 def test_rmat_pagerank_through_computer(ctx, oracle_lib):
