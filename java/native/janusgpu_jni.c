@@ -1,20 +1,28 @@
 /*
- * janusgpu_jni.c — JNI shim between org.janusgraph.graphdb.olap.gpu.JanusGpu and libjanusgpu's
+ * janusgpu_jni.c — JNI shim between org.janusgraph.graphdb.olap.computer.JanusGpu and libjanusgpu's
  * C-ABI (include/janusgpu.h).  Pure pass-through: direct ByteBuffers are handed to the library as
- * raw pointers (no copies), statuses are returned unchanged.
+ * raw pointers (no copies), statuses are returned unchanged.  tests/test_jni_shim.py checks that every
+ * native method of JanusGpu.java has its function here with the same arity, and
+ * tests/test_jni_sequence.py replays GpuGraphComputer's call sequences through ctypes.
  *
  * Build (needs a JDK; none is installed in the build container):
- *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
- *       janusgpu_jni.c -L../../janusgraph_amd -ljanusgpu -Wl,-rpath,'$ORIGIN' -o libjanusgpu_jni.so
+ *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
+ *       java/native/janusgpu_jni.c -Ljanusgraph_amd -ljanusgpu -Wl,-rpath,'$ORIGIN' -o libjanusgpu_jni.so
  */
 #include <jni.h>
 #include <stddef.h>
+#include <stdint.h>
 
 #include "janusgpu.h"
 
-#define FN(name) Java_org_janusgraph_graphdb_olap_gpu_JanusGpu_##name
+#define FN(name) Java_org_janusgraph_graphdb_olap_computer_JanusGpu_##name
 
 static void* buf(JNIEnv* env, jobject b) { return b ? (*env)->GetDirectBufferAddress(env, b) : NULL; }
+
+static void put_handle(JNIEnv* env, jlongArray out, const void* h) {
+    jlong v = (jlong)(intptr_t)h;
+    (*env)->SetLongArrayRegion(env, out, 0, 1, &v);
+}
 
 JNIEXPORT jint JNICALL FN(abiVersion)(JNIEnv* env, jclass c) { (void)env; (void)c; return jg_abi_version(); }
 
@@ -30,8 +38,7 @@ JNIEXPORT jint JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jintArray devices, j
     jg_ctx* ctx = NULL;
     int st = jg_ctx_create((const int*)d, (int)nd, &ctx);
     (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
-    jlong h = (jlong)(intptr_t)ctx;
-    (*env)->SetLongArrayRegion(env, out, 0, 1, &h);
+    put_handle(env, out, ctx);
     return st;
 }
 
@@ -52,14 +59,53 @@ JNIEXPORT jint JNICALL FN(ctxLastStats)(JNIEnv* env, jclass c, jlong ctx, jdoubl
     return st;
 }
 
-JNIEXPORT jint JNICALL FN(graphBuild)(JNIEnv* env, jclass c, jlong ctx, jobject vid, jlong n, jobject src, jobject dst,
-                                      jobject weight, jlong m, jint flags, jlongArray out) {
+JNIEXPORT jint JNICALL FN(builderCreate)(JNIEnv* env, jclass c, jlong ctx, jlongArray out) {
+    (void)c;
+    jg_builder* b = NULL;
+    int st = jg_builder_create((jg_ctx*)(intptr_t)ctx, &b);
+    put_handle(env, out, b);
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(builderDestroy)(JNIEnv* env, jclass c, jlong b) {
+    (void)env; (void)c;
+    return jg_builder_destroy((jg_builder*)(intptr_t)b);
+}
+
+JNIEXPORT jint JNICALL FN(builderAddVertices)(JNIEnv* env, jclass c, jlong b, jobject vid, jlong n) {
+    (void)c;
+    return jg_builder_add_vertices((jg_builder*)(intptr_t)b, (const int64_t*)buf(env, vid), n);
+}
+
+JNIEXPORT jint JNICALL FN(builderAddEdges)(JNIEnv* env, jclass c, jlong b, jobject src, jobject dst, jobject weight,
+                                           jlong m) {
+    (void)c;
+    return jg_builder_add_edges((jg_builder*)(intptr_t)b, (const int64_t*)buf(env, src), (const int64_t*)buf(env, dst),
+                                (const int32_t*)buf(env, weight), m);
+}
+
+JNIEXPORT jint JNICALL FN(builderSetSchema)(JNIEnv* env, jclass c, jlong b, jobject type_ids, jobject type_mult,
+                                            jint ntypes, jint partition_bits) {
+    (void)c;
+    return jg_builder_set_schema((jg_builder*)(intptr_t)b, (const int64_t*)buf(env, type_ids),
+                                 (const int8_t*)buf(env, type_mult), ntypes, partition_bits);
+}
+
+JNIEXPORT jint JNICALL FN(builderAddRows)(JNIEnv* env, jclass c, jlong b, jobject row_keys, jlong nrows,
+                                          jobject row_entry_off, jobject bytes, jlong nbytes, jobject entry_off,
+                                          jobject value_pos, jobject entry_weight, jlong nentries) {
+    (void)c;
+    return jg_builder_add_rows((jg_builder*)(intptr_t)b, (const uint64_t*)buf(env, row_keys), nrows,
+                               (const int64_t*)buf(env, row_entry_off), (const uint8_t*)buf(env, bytes), nbytes,
+                               (const int64_t*)buf(env, entry_off), (const int32_t*)buf(env, value_pos),
+                               (const int32_t*)buf(env, entry_weight), nentries);
+}
+
+JNIEXPORT jint JNICALL FN(builderFinish)(JNIEnv* env, jclass c, jlong b, jint flags, jlongArray out) {
     (void)c;
     jg_graph* g = NULL;
-    int st = jg_graph_build((jg_ctx*)(intptr_t)ctx, (const int64_t*)buf(env, vid), n, (const int64_t*)buf(env, src),
-                            (const int64_t*)buf(env, dst), (const int32_t*)buf(env, weight), m, (uint32_t)flags, &g);
-    jlong h = (jlong)(intptr_t)g;
-    (*env)->SetLongArrayRegion(env, out, 0, 1, &h);
+    int st = jg_builder_finish((jg_builder*)(intptr_t)b, (uint32_t)flags, &g);
+    put_handle(env, out, g);
     return st;
 }
 
@@ -78,6 +124,11 @@ JNIEXPORT jint JNICALL FN(graphInfo)(JNIEnv* env, jclass c, jlong g, jlongArray 
         (*env)->SetLongArrayRegion(env, out8, 0, 8, v);
     }
     return st;
+}
+
+JNIEXPORT jint JNICALL FN(graphVertexIds)(JNIEnv* env, jclass c, jlong g, jlong offset, jlong count, jobject vid_out) {
+    (void)c;
+    return jg_graph_vertex_ids((const jg_graph*)(intptr_t)g, offset, count, (int64_t*)buf(env, vid_out));
 }
 
 JNIEXPORT jint JNICALL FN(pageRank)(JNIEnv* env, jclass c, jlong g, jdouble damping, jlong vertex_count,
@@ -110,38 +161,9 @@ JNIEXPORT jint JNICALL FN(connectedComponents)(JNIEnv* env, jclass c, jlong g, j
     return st;
 }
 
-JNIEXPORT jint JNICALL FN(graphBuildEdgestore)(JNIEnv* env, jclass c, jlong ctx, jobject row_keys, jlong nrows,
-                                               jobject row_entry_off, jobject bytes, jlong nbytes, jobject entry_off,
-                                               jobject value_pos, jlong nentries, jobject type_ids, jobject type_mult,
-                                               jint ntypes, jint partition_bits, jint flags, jobject vid_out,
-                                               jlongArray out2) {
-    (void)c;
-    jg_graph* g = NULL;
-    int64_t nv = 0;
-    int st = jg_graph_build_edgestore((jg_ctx*)(intptr_t)ctx, (const uint64_t*)buf(env, row_keys), nrows,
-                                      (const int64_t*)buf(env, row_entry_off), (const uint8_t*)buf(env, bytes), nbytes,
-                                      (const int64_t*)buf(env, entry_off), (const int32_t*)buf(env, value_pos),
-                                      nentries, (const int64_t*)buf(env, type_ids), (const int8_t*)buf(env, type_mult),
-                                      ntypes, partition_bits, (uint32_t)flags, (int64_t*)buf(env, vid_out), &nv, &g);
-    jlong v[2] = {(jlong)(intptr_t)g, (jlong)nv};
-    (*env)->SetLongArrayRegion(env, out2, 0, 2, v);
-    return st;
-}
-
 JNIEXPORT jint JNICALL FN(combineSteps)(JNIEnv* env, jclass c, jlong g, jint direction, jint combiner,
                                         jint int32_wrap, jobject init, jint steps, jobject out, jobject received_out) {
     (void)c;
     return jg_combine_steps((jg_graph*)(intptr_t)g, direction, combiner, int32_wrap, (const int64_t*)buf(env, init),
                             steps, (int64_t*)buf(env, out), (uint8_t*)buf(env, received_out));
-}
-
-JNIEXPORT jint JNICALL FN(decodeEdges)(JNIEnv* env, jclass c, jlong ctx, jobject bytes, jlong nbytes, jobject entry_off,
-                                       jobject value_pos, jlong n, jobject type_ids, jobject type_mult, jint ntypes,
-                                       jobject type_out, jobject dir_out, jobject other_out, jobject relation_out) {
-    (void)c;
-    return jg_decode_edges((jg_ctx*)(intptr_t)ctx, (const uint8_t*)buf(env, bytes), nbytes,
-                           (const int64_t*)buf(env, entry_off), (const int32_t*)buf(env, value_pos), n,
-                           (const int64_t*)buf(env, type_ids), (const int8_t*)buf(env, type_mult), ntypes,
-                           (int64_t*)buf(env, type_out), (int8_t*)buf(env, dir_out), (int64_t*)buf(env, other_out),
-                           (int64_t*)buf(env, relation_out));
 }

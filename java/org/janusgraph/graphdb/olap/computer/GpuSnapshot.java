@@ -1,0 +1,248 @@
+// Copyright 2026 JanusGraph Authors
+// SPDX-License-Identifier: Apache-2.0
+package org.janusgraph.graphdb.olap.computer;
+
+import org.apache.tinkerpop.gremlin.structure.Direction;
+import org.janusgraph.core.EdgeLabel;
+import org.janusgraph.core.JanusGraphException;
+import org.janusgraph.core.schema.JanusGraphManagement;
+import org.janusgraph.diskstorage.Entry;
+import org.janusgraph.diskstorage.EntryList;
+import org.janusgraph.diskstorage.StaticBuffer;
+import org.janusgraph.diskstorage.keycolumnvalue.SliceQuery;
+import org.janusgraph.diskstorage.keycolumnvalue.scan.ScanJob;
+import org.janusgraph.diskstorage.keycolumnvalue.scan.ScanMetrics;
+import org.janusgraph.diskstorage.keycolumnvalue.scan.StandardScanner;
+import org.janusgraph.diskstorage.util.BufferUtil;
+import org.janusgraph.graphdb.database.EdgeSerializer;
+import org.janusgraph.graphdb.database.StandardJanusGraph;
+import org.janusgraph.graphdb.olap.VertexJobConverter;
+import org.janusgraph.graphdb.relations.RelationCache;
+import org.janusgraph.graphdb.transaction.StandardJanusGraphTx;
+
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+import java.util.ArrayList;
+import java.util.Collections;
+import java.util.List;
+import java.util.Map;
+import java.util.concurrent.atomic.AtomicInteger;
+
+/**
+ * The once-per-computer CSR snapshot, taken with the same edgestore scan Fulgora runs every superstep
+ * (Backend.buildEdgeScanJob, janusgraph-core/.../diskstorage/Backend.java:377-396, driving
+ * StandardScannerExecutor.run, diskstorage/keycolumnvalue/scan/StandardScannerExecutor.java:97-216).
+ * Rows are NOT decoded here: each row key and the raw bytes of its EntryList are packed into direct
+ * buffers and handed to libjanusgpu in chunks (jg_builder_add_rows), which decodes them on the GPU
+ * (EdgeSerializer.parseRelation, key filter and ghost rule of VertexJobConverter.process,
+ * graphdb/olap/VertexJobConverter.java:122-151,174-177) while this thread scans the next chunk.
+ *
+ * ShortestDistanceVertexProgram also needs the Integer edge weight, which lives in the entry's value
+ * with a type-dependent encoding: for that program every entry is additionally parsed here with the
+ * graph's own EdgeSerializer and its weight sent along (JanusGpu.WEIGHT_ABSENT if the edge has none,
+ * which fails the run only if a message crosses the edge, as Fulgora's edge function does).
+ */
+final class GpuSnapshot implements ScanJob {
+
+    /** Every column of a row: the VertexExists property first, then the other relations. */
+    static final SliceQuery ALL_ENTRIES = new SliceQuery(BufferUtil.zeroBuffer(1), BufferUtil.oneBuffer(4));
+
+    // Chunk limits: direct buffers stay far below 2 GiB, and a chunk's copy and decode on the GPU
+    // overlap the scan of the next one.  A single row larger than a chunk gets a chunk of its own.
+    private static final int CHUNK_BYTES = 64 << 20;
+    private static final int CHUNK_ENTRIES = 4 << 20;
+    private static final int CHUNK_ROWS = 1 << 20;
+
+    private static final AtomicInteger JOBS = new AtomicInteger();
+
+    private final long builder;
+    private final WeightReader weights;
+    private ByteBuffer keys, rowOff, bytes, entryOff, valuePos, entryWeight;
+    private int nrows, nentries, nbytes;
+
+    private GpuSnapshot(long builder, WeightReader weights) {
+        this.builder = builder;
+        this.weights = weights;
+        allocate(CHUNK_BYTES, CHUNK_ENTRIES, CHUNK_ROWS);
+    }
+
+    private static ByteBuffer direct(long bytes) {
+        if (bytes > Integer.MAX_VALUE) throw new JanusGraphException("GPU snapshot chunk above 2 GiB");
+        return ByteBuffer.allocateDirect((int) Math.max(bytes, 8)).order(ByteOrder.nativeOrder());
+    }
+
+    private void allocate(int maxBytes, int maxEntries, int maxRows) {
+        keys = direct(8L * maxRows);
+        rowOff = direct(8L * (maxRows + 1));
+        bytes = direct(maxBytes);
+        entryOff = direct(8L * (maxEntries + 1));
+        valuePos = direct(4L * maxEntries);
+        entryWeight = weights == null ? null : direct(4L * maxEntries);
+        reset();
+    }
+
+    private void reset() {
+        keys.clear();
+        rowOff.clear();
+        bytes.clear();
+        entryOff.clear();
+        valuePos.clear();
+        if (entryWeight != null) entryWeight.clear();
+        nrows = nentries = nbytes = 0;
+        rowOff.putLong(0L);
+        entryOff.putLong(0L);
+    }
+
+    @Override
+    public List<SliceQuery> getQueries() {
+        return Collections.singletonList(ALL_ENTRIES); // one query: no grounding slice needed (:104-116)
+    }
+
+    @Override
+    public void process(StaticBuffer key, Map<SliceQuery, EntryList> entries, ScanMetrics metrics) {
+        final EntryList row = entries.get(ALL_ENTRIES);
+        if (row == null || row.isEmpty()) return;
+        int rowBytes = 0;
+        for (Entry e : row) rowBytes += e.length();
+        final int rowEntries = row.size();
+        if (nrows > 0 && (nbytes + rowBytes > bytes.capacity() || nentries + rowEntries > valuePos.capacity() / 4
+                || nrows + 1 > keys.capacity() / 8)) {
+            flush();
+        }
+        if (rowBytes > bytes.capacity() || rowEntries > valuePos.capacity() / 4) { // a hub row: a chunk of its own
+            allocate(Math.max(rowBytes, CHUNK_BYTES), Math.max(rowEntries, CHUNK_ENTRIES), CHUNK_ROWS);
+        }
+        keys.putLong(key.getLong(0)); // the 8-byte big-endian row key as an unsigned value (IDManager.getKey)
+        for (Entry e : row) {
+            final byte[] b = e.as(StaticBuffer.ARRAY_FACTORY); // column then value
+            bytes.put(b);
+            nbytes += b.length;
+            entryOff.putLong(nbytes);
+            valuePos.putInt(e.getValuePosition());
+            if (entryWeight != null) entryWeight.putInt(weights.weight(e));
+        }
+        nentries += rowEntries;
+        ++nrows;
+        rowOff.putLong(nentries);
+    }
+
+    /** Hands the packed rows to the library (it copies them before returning). */
+    void flush() {
+        if (nrows == 0) return;
+        JanusGpu.check(JanusGpu.builderAddRows(builder, keys, nrows, rowOff, bytes, nbytes, entryOff, valuePos,
+            entryWeight, nentries));
+        if (bytes.capacity() > CHUNK_BYTES || valuePos.capacity() > 4 * CHUNK_ENTRIES) {
+            allocate(CHUNK_BYTES, CHUNK_ENTRIES, CHUNK_ROWS); // back to regular chunks after a hub row
+        } else {
+            reset();
+        }
+    }
+
+    @Override
+    public GpuSnapshot clone() {
+        return this; // one processor thread (setNumProcessingThreads(1)): rows arrive in key order
+    }
+
+    /** Reads the Integer weight property of the edge an entry stores (ShortestDistanceVertexProgram.java:69). */
+    static final class WeightReader {
+        private final StandardJanusGraphTx tx;
+        private final EdgeSerializer serializer;
+        private final long keyId;
+
+        WeightReader(StandardJanusGraph graph, String weightProperty) {
+            tx = VertexJobConverter.startTransaction(graph);
+            serializer = graph.getEdgeSerializer();
+            keyId = tx.containsPropertyKey(weightProperty) ? tx.getPropertyKey(weightProperty).longId() : -1L;
+        }
+
+        int weight(Entry e) {
+            final RelationCache rc = serializer.parseRelation(e, false, tx);
+            if (rc.direction != Direction.OUT || keyId < 0) return JanusGpu.WEIGHT_ABSENT;
+            final Object v = rc.get(keyId);
+            return v == null ? JanusGpu.WEIGHT_ABSENT : ((Number) v).intValue();
+        }
+
+        void close() {
+            if (tx.isOpen()) tx.rollback();
+        }
+    }
+
+    /** Multiplicity codes of include/janusgpu.h (jg_decode_edges): 0 MULTI, 1 SIMPLE, 2 ONE2MANY,
+     *  3 MANY2ONE, 4 ONE2ONE (core/Multiplicity.java:35-90). */
+    private static byte multiplicityCode(EdgeLabel label) {
+        switch (label.multiplicity()) {
+            case SIMPLE: return 1;
+            case ONE2MANY: return 2;
+            case MANY2ONE: return 3;
+            case ONE2ONE: return 4;
+            default: return 0;
+        }
+    }
+
+    /**
+     * Scans the edgestore into a device graph with the adjacencies `flags`. weightProperty != null
+     * also sends every entry's edge weight (ShortestDistanceVertexProgram). Returns the graph handle;
+     * its vertex order is the scan's row order (read it with JanusGpu.graphVertexIds).
+     */
+    static long scan(StandardJanusGraph graph, long ctx, int flags, String weightProperty) {
+        final long[] h = new long[1];
+        JanusGpu.check(JanusGpu.builderCreate(ctx, h));
+        final long builder = h[0];
+        WeightReader weights = null;
+        try {
+            final List<EdgeLabel> labels = new ArrayList<>();
+            final JanusGraphManagement mgmt = graph.openManagement();
+            try {
+                for (EdgeLabel l : mgmt.getRelationTypes(EdgeLabel.class)) labels.add(l);
+                final ByteBuffer typeIds = direct(8L * labels.size());
+                final ByteBuffer typeMult = direct(labels.size());
+                for (EdgeLabel l : labels) {
+                    typeIds.putLong(l.longId());
+                    typeMult.put(multiplicityCode(l));
+                }
+                final int partitionBits = Long.numberOfTrailingZeros(graph.getIDManager().getPartitionBound());
+                JanusGpu.check(JanusGpu.builderSetSchema(builder, typeIds, typeMult, labels.size(), partitionBits));
+            } finally {
+                mgmt.rollback();
+            }
+            if (weightProperty != null) weights = new WeightReader(graph, weightProperty);
+            final GpuSnapshot job = new GpuSnapshot(builder, weights);
+            final StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
+            scan.setJobId("gpu-snapshot#" + JOBS.incrementAndGet());
+            scan.setNumProcessingThreads(1);
+            scan.setJob(job);
+            final ScanMetrics metrics = scan.execute().get();
+            if (metrics.get(ScanMetrics.Metric.FAILURE) > 0) {
+                throw new JanusGraphException("Failed to snapshot [" + metrics.get(ScanMetrics.Metric.FAILURE)
+                    + "] vertex rows for the GPU. Computer is aborting.");
+            }
+            job.flush(); // the scan's last partial chunk (the scan thread is done: Future.get())
+            JanusGpu.check(JanusGpu.builderFinish(builder, flags, h));
+            return h[0];
+        } catch (JanusGraphException e) {
+            throw e;
+        } catch (Exception e) {
+            throw new JanusGraphException("GPU snapshot scan failed. Computer is aborting.", e);
+        } finally {
+            if (weights != null) weights.close();
+            JanusGpu.builderDestroy(builder);
+        }
+    }
+
+    /** The graph's vertex ids in output order, as one long[] (n < 2^31 by the library's limit). */
+    static long[] vertexIds(long graph) {
+        final long[] info = new long[8];
+        JanusGpu.check(JanusGpu.graphInfo(graph, info));
+        final long n = info[0];
+        final long[] vid = new long[(int) n];
+        final int chunk = 1 << 24;
+        final ByteBuffer buf = direct(8L * Math.min(n, chunk));
+        for (long off = 0; off < n; off += chunk) {
+            final int cnt = (int) Math.min(chunk, n - off);
+            buf.clear();
+            JanusGpu.check(JanusGpu.graphVertexIds(graph, off, cnt, buf));
+            buf.asLongBuffer().get(vid, (int) off, cnt);
+        }
+        return vid;
+    }
+}

@@ -237,7 +237,8 @@ def canonical_vertex_id(vid, partition_bits=5):
     return (((count << partition_bits) + h) << 3) | 2
 
 
-def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=(), partition_bits=5):
+def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=(), partition_bits=5,
+                       return_entries=False):
     """The scan -> snapshot step restated row by row (the checker of jg_graph_build_edgestore):
     VertexJobConverter.getKeyFilter drops invisible rows (olap/VertexJobConverter.java:174-177);
     process/isGhostVertex keep a row only if its first entry is the VertexExists property (:122-151),
@@ -246,7 +247,8 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
     on its target row, graphdb/database/StandardJanusGraph.java:617-640).  Partitioned vertices
     (comp/VertexProgramScanJob.java:88-102, FulgoraVertexMemory.getCanonicalId) are one vertex: the
     canonical id, whose edges are the union over its representative rows.
-    Returns (vid of kept vertices in row order, src ids, dst ids); raises ValueError where Java throws."""
+    Returns (vid of kept vertices in row order, src ids, dst ids[, entry index of each edge]); raises
+    ValueError where Java throws."""
     data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
     off, row_off = _i64(off), _i64(row_off)
     t, d, o, _ = decode_edges(data, off, vpos, type_ids, type_mult)
@@ -259,7 +261,7 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
             return canonical_vertex_id(v, partition_bits)
         return v
 
-    keep_v, src, dst = [], [], []
+    keep_v, src, dst, ent = [], [], [], []
     for r, vid in enumerate(vids):
         vid = int(vid)
         e0, e1 = int(row_off[r]), int(row_off[r + 1])
@@ -283,7 +285,9 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
             if d[e] == 0 and visible:
                 src.append(cv)
                 dst.append(canon(int(o[e])))
-    return np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64)
+                ent.append(e)
+    out = (np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64))
+    return out + (np.array(ent, np.int64),) if return_entries else out
 
 
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
