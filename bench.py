@@ -4,8 +4,10 @@ Headline (value): PageRank fp64 on RMAT scale-24 edgefactor-16 (BASELINE.json co
 "step" = one power superstep of JanusGraph's PageRankVertexProgram over the whole graph (pull SpMV
 over the in-CSR + contribution write + RCCL allgather of the rank-contribution vector when N > 1).
 value = directed edges processed per second over all GPUs (GTEPS), inputs resident in HBM.
-Secondary (same JSON line): BFS (SPVP depth, undirected) from one source on RMAT scale-20
-(configs[1]) as Graph500 TEPS.
+Secondary blocks (same JSON line, one GPU): "bfs" = DO-BFS (SPVP depth, undirected) from one source on
+RMAT scale-20 (configs[1]) as Graph500 TEPS with its roofline and CPU baseline; "rmat26" = PageRank
+(with roofline), DO-BFS, ConnectedComponent (configs[3]) and 64-source MS-BFS (configs[4]) at scale 26.
+With N > 1: "per_rank" = each rank's superstep kernel time, exchange time, halo volume and roofline.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -38,6 +40,9 @@ def parse():
     p.add_argument("--no-bfs", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--no-big", action="store_true", help="skip the RMAT-26 blocks (PageRank, BFS, CC, MS-BFS)")
+    p.add_argument("--big-scale", type=int, default=26)
+    p.add_argument("--big-steps", type=int, default=10)
     return p.parse_args()
 
 
@@ -86,6 +91,16 @@ class Control:
         t = torch.tensor([x], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+    def gather(self, row):
+        """Every rank's list of floats, on every rank (rank order)."""
+        if not self.dist:
+            return [row]
+        import torch
+        t = torch.tensor(row, dtype=torch.float64)
+        out = [torch.zeros_like(t) for _ in range(self.ws)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
 
     def close(self):
         if self.dist:
@@ -138,6 +153,112 @@ def cpu_baseline(scale, ef, seed, steps):
                       f"the same RMAT-{scale} ef{ef} graph (seed {seed}); CSR build untimed"}
 
 
+def cpu_baseline_bfs(scale, ef, seed, sources):
+    """The oracle's level-synchronous parallel BFS (jo_bfs_csr, OpenMP) from the bench's sources on the same
+    symmetrised RMAT graph, Graph500 TEPS (input edges of the source's component / time)."""
+    from oracle import oracle as o
+    o.build()
+    n = 1 << scale
+    s, d = o.rmat_edges(scale, ef, seed)
+    s, d = s.astype(np.int32), d.astype(np.int32)
+    ptr, adj = o.csr_unordered(n, s, d, both=True)
+    teps, total = [], 0.0
+    for sv in sources:
+        t0 = time.perf_counter()
+        depth = o.bfs_csr(n, ptr, adj, int(sv))
+        dt = time.perf_counter() - t0
+        total += dt
+        teps.append(int(np.count_nonzero(depth[s] >= 0)) / dt / 1e9)
+    return {"value": round(float(np.median(teps)), 4), "unit": "GTEPS", "cores": o.num_threads(), "kind": "port",
+            "sample": f"oracle/jg_oracle.c jo_bfs_csr (OpenMP, top-down level-synchronous), the {len(sources)} bench "
+                      f"sources on the same RMAT-{scale} ef{ef} graph, {total:.2f} s of CPU BFS; CSR build untimed"}
+
+
+def hbm_roofline(alg_bytes, ms, kernel, traffic=None, traffic_src=None):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": kernel, "kernel_ms": round(ms, 4), "bytes_per_launch": alg_bytes}
+
+
+def bfs_block(jg, ctx, scale, ef, nsrc=6, cpu=True):
+    """Single-source DO-BFS (SPVP depth, BOTH edges) from seeded sources of degree > 0, Graph500 TEPS;
+    roofline of one traversal: 8*m + 12*n algorithmic bytes / its HIP-event time."""
+    n, m = 1 << scale, ef << scale
+    gb = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
+    rng = np.random.default_rng(1)
+    times, teps, srcs = [], [], []
+    while len(srcs) < nsrc:
+        sv = int(rng.integers(0, n))
+        gb.bfs([sv], jg.DIR_BOTH, want=False)
+        st = ctx.stats()
+        if st["edges_traversed"] < m // 100:
+            continue  # a source in a tiny component: Graph500 resamples
+        gb.bfs([sv], jg.DIR_BOTH, want=False)  # timed run (the first touched cold pages)
+        st = ctx.stats()
+        srcs.append(sv)
+        times.append(st["compute_ms"])
+        teps.append(st["edges_traversed"] / (st["compute_ms"] * 1e-3) / 1e9)
+    gb.close()
+    ms = float(np.median(times))
+    blk = {"workload": f"bfs_spvp_rmat{scale}_ef{ef}", "gteps_median": round(float(np.median(teps)), 3),
+           "ms_median": round(ms, 4), "runs": len(times),
+           "roofline": hbm_roofline(8.0 * m + 12.0 * n, ms, "direction-optimising BFS, one traversal "
+                                    "(bfs_level_kernel launches)")}
+    if cpu:
+        blk["cpu_baseline"] = cpu_baseline_bfs(scale, ef, 0x5EED + scale, srcs[:3])
+    return blk
+
+
+def pagerank_block(jg, ctx, scale, ef, steps, warmup):
+    n, m = 1 << scale, ef << scale
+    g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_IN)
+    build_ms = ctx.stats()["build_ms"]
+    g.pagerank_begin(0.85, n)
+    g.pagerank_step(warmup)
+    g.sync()
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    g.pagerank_step(steps)
+    g.sync()
+    dt = time.perf_counter() - t0
+    g.pagerank_end(want=False)
+    st = ctx.stats()
+    ctx.set_profiling(False)
+    g.close()
+    kern_ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
+    return {"workload": f"pagerank_fp64_rmat{scale}_ef{ef}", "ms_per_step": round(dt / steps * 1e3, 4),
+            "gteps": round(m * steps / dt / 1e9, 3), "steps": steps, "build_ms": round(build_ms, 1),
+            "roofline": hbm_roofline(12.0 * m + 32.0 * n, kern_ms, "PageRank superstep (same launch sequence "
+                                     "as the headline)")}
+
+
+def rmat26_both_blocks(jg, ctx, scale, ef):
+    """CC (configs[3]) and 64-source MS-BFS (configs[4], one GPU here) on the BOTH adjacency."""
+    n, m = 1 << scale, ef << scale
+    g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
+    build_ms = ctx.stats()["build_ms"]
+    g.connected_components()  # warm
+    comp, it = g.connected_components()
+    st = ctx.stats()
+    cc_ms = st["compute_ms"]
+    cc = {"workload": f"cc_rmat{scale}_ef{ef}", "ms": round(cc_ms, 3), "iterations": it,
+          "components": int(len(np.unique(comp))), "build_ms": round(build_ms, 1),
+          "gteps_per_iteration": round(2 * m * it / (cc_ms * 1e-3) / 1e9, 2),
+          "note": "push supersteps visit only the senders' edges: per-iteration GTEPS is an equivalent rate"}
+    del comp
+    rng = np.random.default_rng(7)
+    cand = rng.integers(0, n, 4 * 64)
+    srcs = np.unique(cand)[:64]
+    g.bfs(srcs, jg.DIR_BOTH, want=False)  # warm
+    g.bfs(srcs, jg.DIR_BOTH, want=False)
+    st = ctx.stats()
+    ms = {"workload": f"msbfs64_rmat{scale}_ef{ef}", "sources": int(len(srcs)), "ms": round(st["compute_ms"], 3),
+          "levels": st["levels"]}
+    g.close()
+    return cc, ms
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -172,38 +293,39 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = m * args.steps / elapsed / 1e9  # GTEPS, all ranks
 
-    # roofline of the dominant kernel (pull SpMV), HIP events on its stream, this rank's launches
+    # roofline of the dominant kernel (the superstep's launch sequence), HIP events on its stream, this
+    # rank's launches; with N > 1 the exchange step is outside these events
     launches = max(st["kernel_launches"], 1)
     kern_ms = st["kernel_ms_total"] / launches
-    alg_bytes_launch = 12.0 * m / ws + 32.0 * n / ws  # SURVEY §8d per-edge/per-vertex bytes x this rank's share
-    if ws == 1:
-        alg_bytes_launch = 12.0 * m + 32.0 * n
-    achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
+    in_nnz = info["num_edges"] if ws == 1 else None
+    alg_bytes_launch = 12.0 * m + 32.0 * n  # SURVEY §8d per-edge/per-vertex bytes
+    if ws > 1:
+        alg_bytes_launch = (12.0 * m + 32.0 * n) / ws  # this rank's share (rows and entries are balanced)
     workload = f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}"
     traffic, traffic_src = pmc_traffic("PrOp", workload) if ws == 1 else (None, None)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "PageRank superstep (pull_merge_kernel x bands + fixups + light-row pull_kernel + finalize kernels, PrOp)", "kernel_ms": round(kern_ms, 4),
-                "bytes_per_launch": alg_bytes_launch}
+    roofline = hbm_roofline(alg_bytes_launch, kern_ms, "PageRank superstep (pull_merge_kernel x bands + fixup + "
+                            "fused light-row/finalize kernel, PrOp)", traffic, traffic_src)
+    per_rank = None
+    if ws > 1:
+        # every rank's own numbers, gathered on rank 0: superstep kernel time, exchange time, halo volume
+        mine = [float(rank), kern_ms, st["exchange_ms"] / max(args.steps, 1), float(info["exchange_values"]),
+                alg_bytes_launch / (kern_ms * 1e-3) / 1e9]
+        rows = ctl.gather(mine)
+        per_rank = [{"rank": int(r[0]), "kernel_ms": round(r[1], 4), "exchange_ms": round(r[2], 4),
+                     "halo_values": int(r[3]), "halo_bytes": int(r[3]) * 8,
+                     "roofline_frac": round(r[4] / HBM_PEAK_GBS, 4)} for r in rows]
+    g.close()
 
-    bfs = None
-    if not args.no_bfs and ws == 1:
-        gb = ctx.build_rmat(args.bfs_scale, args.edgefactor, 0x5EED + args.bfs_scale, flags=jg.ADJ_BOTH)
-        rng = np.random.default_rng(1)
-        times, teps = [], []
-        for k in range(6):
-            srcv = int(rng.integers(0, 1 << args.bfs_scale))
-            gb.bfs([srcv], jg.DIR_BOTH, want=False)
-            s = ctx.stats()
-            if s["edges_traversed"] < (args.edgefactor << args.bfs_scale) // 100:
-                continue  # source in a tiny component: Graph500 resamples
-            if k == 0:
-                continue
-            times.append(s["compute_ms"])
-            teps.append(s["edges_traversed"] / (s["compute_ms"] * 1e-3) / 1e9)
-        bfs = {"workload": f"bfs_spvp_rmat{args.bfs_scale}_ef{args.edgefactor}", "gteps_median": round(float(np.median(teps)), 3) if teps else None,
-               "ms_median": round(float(np.median(times)), 4) if times else None, "runs": len(times)}
-        gb.close()
+    extra = {}
+    if ws == 1 and not args.no_bfs:
+        extra["bfs"] = bfs_block(jg, ctx, args.bfs_scale, args.edgefactor, cpu=not args.no_cpu)
+    if ws == 1 and not args.no_big:
+        big = args.big_scale
+        extra[f"rmat{big}"] = {"pagerank": pagerank_block(jg, ctx, big, args.edgefactor, args.big_steps, 3),
+                               "bfs": bfs_block(jg, ctx, big, args.edgefactor, nsrc=4, cpu=False)}
+        cc, msbfs = rmat26_both_blocks(jg, ctx, big, args.edgefactor)
+        extra[f"rmat{big}"]["cc"] = cc
+        extra[f"rmat{big}"]["msbfs64"] = msbfs
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
@@ -215,13 +337,16 @@ def main():
             "value": round(value, 3), "unit": "GTEPS", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (Graph500 Kronecker RMAT, on-device generator)",
-            "config": {"workload": f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}", "n": n, "m": m,
+            "config": {"workload": workload, "n": n, "m": m,
                        "parallelism": f"1d-vertex-partition x{ws}, RCCL halo send/recv" if ws > 1 else "single GPU",
-                       "build_ms": round(build_ms, 1), "truncated_vertices": info["truncated_vertices"]},
-            "roofline": roofline, "cpu_baseline": cpu, "bfs": bfs,
+                       "build_ms": round(build_ms, 1), "truncated_vertices": info["truncated_vertices"],
+                       "in_entries": in_nnz},
+            "roofline": roofline, "cpu_baseline": cpu,
         }
+        if per_rank is not None:
+            line["per_rank"] = per_rank
+        line.update(extra)
         print(json.dumps(line), flush=True)
-    g.close()
     ctx.close()
     ctl.close()
 

@@ -93,6 +93,10 @@ typedef struct jg_graph_info {
     int64_t device_bytes;        /* device memory held by this graph, summed over shards             */
     int32_t num_shards;          /* 1D vertex partitions (one per device / rank)                    */
     uint32_t flags;              /* JG_ADJ_* actually built                                          */
+    int64_t exchange_values;     /* vertex values this process's shards receive from peers per
+                                    exchange step of the pull vector (IN adjacency if built, else
+                                    BOTH): the sparse halo, or (P-1)*S each for the dense allgather;
+                                    0 on one shard                                                   */
 } jg_graph_info;
 
 typedef struct jg_stats {
@@ -100,7 +104,7 @@ typedef struct jg_stats {
     int32_t levels;              /* BFS/SSSP levels or CC sweeps actually executed on the GPU       */
     double  build_ms;            /* last jg_graph_build*: snapshot -> CSR on device                 */
     double  compute_ms;          /* last program: HIP-event time of the superstep loop              */
-    double  exchange_ms;         /* part of compute_ms spent in RCCL / peer exchange                */
+    double  exchange_ms;         /* HIP-event time of the exchange steps (profiling on, sharded)    */
     double  kernel_ms_total;     /* sum of HIP-event durations of the dominant kernel                */
     int64_t kernel_launches;     /* number of launches of the dominant kernel that were timed       */
     double  algorithmic_bytes;   /* SURVEY §8(d) byte model for the last program, whole run         */

@@ -47,7 +47,7 @@ class GraphInfo(ctypes.Structure):
         ("num_vertices", ctypes.c_int64), ("num_edges", ctypes.c_int64), ("ghost_edges", ctypes.c_int64),
         ("self_loops", ctypes.c_int64), ("truncated_vertices", ctypes.c_int64),
         ("max_in_degree", ctypes.c_int64), ("max_out_degree", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
-        ("num_shards", ctypes.c_int32), ("flags", ctypes.c_uint32),
+        ("num_shards", ctypes.c_int32), ("flags", ctypes.c_uint32), ("exchange_values", ctypes.c_int64),
     ]
 
     def as_dict(self):

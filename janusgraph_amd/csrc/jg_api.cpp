@@ -155,12 +155,30 @@ void prof_record_stop(Ctx& c, Shard& sh, int units) {
     sh.prof_units.push_back(units);
 }
 
+void exch_record(Ctx& c, Shard& sh) {
+    if (!c.profiling) return;
+    hipEvent_t e;
+    JG_HIP(hipEventCreate(&e));
+    JG_HIP(hipEventRecord(e, sh.stream));
+    sh.exch_events.push_back(e);
+}
+
 void prof_collect(Ctx& c, Graph& g) {
     double total = 0;
     int64_t launches = 0;
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
         DeviceGuard dg(sh.device);
+        double ex = 0;
+        for (size_t i = 0; i + 1 < sh.exch_events.size(); i += 2) {
+            JG_HIP(hipEventSynchronize(sh.exch_events[i + 1]));
+            float ms = 0;
+            JG_HIP(hipEventElapsedTime(&ms, sh.exch_events[i], sh.exch_events[i + 1]));
+            ex += ms;
+        }
+        for (auto e : sh.exch_events) (void)hipEventDestroy(e);
+        sh.exch_events.clear();
+        c.last.exchange_ms = std::max(c.last.exchange_ms, ex);  // the slowest shard of this process
         for (size_t i = 0; i + 1 < sh.prof_events.size(); i += 2) {
             JG_HIP(hipEventSynchronize(sh.prof_events[i + 1]));
             float ms = 0;
@@ -400,6 +418,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().fuse_finalize = value != 0;
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
+    } else if (k == "pr_rank_last") {
+        jg::tune().pr_rank_last = value != 0;
     } else if (k == "pr_skip_empty") {
         jg::tune().pr_skip_empty = value != 0;
     } else if (k == "merge_temporal") {
@@ -807,6 +827,20 @@ int jg_graph_info_get(const jg_graph* g, jg_graph_info* out) {
     JG_GUARD_BEGIN
     JG_ARG(g && out, "null argument");
     *out = g->impl.info;
+    const jg::Graph& gr = g->impl;
+    out->exchange_values = 0;
+    if (gr.P > 1) {
+        const uint32_t adj = (gr.flags & JG_ADJ_IN) ? JG_ADJ_IN : JG_ADJ_BOTH;
+        for (const auto& sp : gr.shards) {
+            const jg::Halo& h = gr.halo(*sp, adj);
+            if (!h.on) {
+                out->exchange_values += (int64_t)(gr.P - 1) * gr.S;
+                continue;
+            }
+            for (int q = 0; q < gr.P; ++q)
+                if (q != sp->index) out->exchange_values += h.recv_off[q + 1] - h.recv_off[q];
+        }
+    }
     JG_GUARD_END
 }
 

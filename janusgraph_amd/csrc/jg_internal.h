@@ -206,6 +206,7 @@ struct Shard {
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
+    std::vector<hipEvent_t> exch_events;  // start/stop pairs around the exchange steps
     std::vector<int> prof_units;          // supersteps each pair spans
 };
 
@@ -417,6 +418,7 @@ struct Tune {
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)
     int merge_nt = 0;                 // merge kernel: bit 0 non-temporal band loads, bit 1 non-temporal partial stores
+    int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
     int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power
                                       // steps only (their rank and contribution are constant after that)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
@@ -438,6 +440,8 @@ bool prof_enabled(const Ctx& c);
 void prof_record_start(Ctx& c, Shard& sh);
 void prof_record_stop(Ctx& c, Shard& sh, int units = 1);
 void prof_collect(Ctx& c, Graph& g);
+// Event pair around an exchange step on the shard's stream (profiling only): exchange_ms.
+void exch_record(Ctx& c, Shard& sh);
 
 }  // namespace jg
 

@@ -26,6 +26,7 @@ struct PrOp {
     const int32_t* __restrict__ outdeg;
     VecPos pos;                        // owned row -> its slot in the gathered vector
     double damping, teleport;
+    bool write_rank;                   // the rank vector is stored on the last superstep of a call only
     __device__ __forceinline__ double identity() const { return 0.0; }
     __device__ __forceinline__ double combine(double a, double b) const { return __dadd_rn(a, b); }
     __device__ __forceinline__ double gather(int32_t c) const { return x[c]; }
@@ -36,7 +37,7 @@ struct PrOp {
     __device__ __forceinline__ void finalize(int64_t row, double s) const {
         // (dampingFactor * newPageRank) + ((1D - dampingFactor) / vertexCount), no contraction
         const double r = __dadd_rn(__dmul_rn(damping, s), teleport);
-        rank[row] = r;
+        if (write_rank) rank[row] = r;
         contrib_out[pos(row)] = r / (double)outdeg[row];
     }
 };
@@ -117,6 +118,9 @@ void pagerank_steps(Graph& g, int nsteps) {
             op.pos = g.vec_pos(sh, JG_ADJ_IN);
             op.damping = g.pr_damping;
             op.teleport = teleport;
+            // the rank property is read only after the call (jg_pagerank_end): earlier supersteps' ranks
+            // are dead stores, except on steps 0 and 1, which also write the rows later steps skip
+            op.write_rank = t == nsteps - 1 || g.pr_steps < 2 || !tune().pr_rank_last;
             // Rows without in-edges: rank = (1-d)/N and contrib = rank/edgeCount from the first power step
             // on.  Steps 0 and 1 write that constant into both contrib buffers (step 0 must still gather
             // the initial values), later steps leave those rows alone.
@@ -124,7 +128,17 @@ void pagerank_steps(Graph& g, int nsteps) {
             launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get(),
                         skip_empty);
         }
+        if (pc)
+            for (auto& sp : g.shards) {
+                DeviceGuard dg(sp->device);
+                exch_record(*pc, *sp);
+            }
         exchange_contrib(g, nxt);
+        if (pc)
+            for (auto& sp : g.shards) {
+                DeviceGuard dg(sp->device);
+                exch_record(*pc, *sp);
+            }
         g.pr_cur = nxt;
         ++g.pr_steps;
     }

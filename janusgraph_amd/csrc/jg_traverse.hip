@@ -132,50 +132,62 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
 }
 
 // Edge-parallel top-down: frontier edge e in [0, mf) belongs to the queue entry i with
-// qoff[i] <= e < qoff[i+1]; each thread walks kTdEdgesPerThread consecutive edges after one binary
-// search, so a hub in the frontier is spread over the whole grid.
+// qoff[i] <= e < qoff[i+1]; each thread takes `ept` consecutive edges after one binary search (one
+// edge per thread while the frontier's edges fit the grid, kTdEdgesPerThread beyond), so a hub in
+// the frontier is spread over the whole grid.  A thread's edges are processed in phases (all target
+// loads, then all depth probes and claims, then the degree loads) so its dependent memory round trips
+// do not multiply with the edges it holds; one block-wide append per edge slot follows.
 __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed,
                                              AppendScratch& sc) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int ept = mf <= nthreads ? 1 : kTdEdgesPerThread;  // grid-uniform
+    const int64_t per_tile = nthreads * ept;
     const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
     const int32_t next_depth = a.level + 1;
     for (int64_t t = 0; t < tiles; ++t) {
         // block-uniform: a block whose slice of this tile is past the frontier's edges has nothing to
         // claim or append (small frontiers leave most of the grid idle)
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= mf) break;
-        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
-        int64_t i = 0, next_bound = 0;
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * ept >= mf) break;
+        const int64_t e0 = (t * nthreads + tid) * ept;
+        int32_t v[kTdEdgesPerThread];
+        bool have[kTdEdgesPerThread], won[kTdEdgesPerThread];
+        int64_t vdeg[kTdEdgesPerThread];
         if (e0 < mf) {
             int64_t lo = 0, hi = nf - 1;
             while (lo < hi) {
                 const int64_t mid = (lo + hi + 1) >> 1;
                 if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
             }
-            i = lo;
-            next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
-        }
+            int64_t i = lo;
+            int64_t next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
 #pragma unroll
-        for (int k = 0; k < kTdEdgesPerThread; ++k) {
-            const int64_t e = e0 + k;
-            bool won = false;
-            int32_t v = 0;
-            int64_t vdeg = 0;
-            if (e < mf) {
-                while (e >= next_bound) {  // skips zero-degree frontier entries too
-                    ++i;
-                    next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
-                }
-                const int32_t u = a.queue_in[i];
-                v = a.push_col[a.push_rp[u] + (e - a.qoff_in[i])];
-                if (a.depth[v] < 0 && atomicCAS(&a.depth[v], -1, next_depth) == -1) {
-                    won = true;
-                    vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
+            for (int k = 0; k < kTdEdgesPerThread; ++k) {
+                const int64_t e = e0 + k;
+                have[k] = k < ept && e < mf;
+                v[k] = 0;
+                if (have[k]) {
+                    while (e >= next_bound) {  // skips zero-degree frontier entries too
+                        ++i;
+                        next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
+                    }
+                    const int32_t u = a.queue_in[i];
+                    v[k] = a.push_col[a.push_rp[u] + (e - a.qoff_in[i])];
                 }
             }
-            block_append_frontier(won, v, vdeg, a.queue_out, a.qoff_out, packed, sc);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kTdEdgesPerThread; ++k) have[k] = false, v[k] = 0;
         }
+        int32_t dv[kTdEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) dv[k] = have[k] ? a.depth[v[k]] : 0;
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k)
+            won[k] = have[k] && dv[k] < 0 && atomicCAS(&a.depth[v[k]], -1, next_depth) == -1;
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) vdeg[k] = won[k] ? a.deg_rp[v[k] + 1] - a.deg_rp[v[k]] : 0;
+        for (int k = 0; k < ept; ++k) block_append_frontier(won[k], v[k], vdeg[k], a.queue_out, a.qoff_out, packed, sc);
     }
 }
 

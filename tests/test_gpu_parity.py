@@ -329,7 +329,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "split_sub2_4": [("band0_deg", 64), ("band0_sub", 4), ("band1_deg", 16), ("band1_sub", 2),
                               ("band2_deg", 4), ("band2_sub", 1)],
              "split_nt": [("merge_nt", 3)],
-             "pr_noskip": [("pr_skip_empty", 0)]}[mode]
+             "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -359,6 +359,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("slice_lds", 1)
         _lib.tune_set("merge_nt", 0)
         _lib.tune_set("pr_skip_empty", 1)
+        _lib.tune_set("pr_rank_last", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
                      ("band2_bit", 3)):
             _lib.tune_set(k, v)

@@ -9,8 +9,8 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 3
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o bench -- python3 bench.py --no-cpu > $OUT/stats.log 2>&1 || exit 4
-timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --output-format csv -d $OUT/pmc_rd -o rd -- python3 bench.py --no-cpu --no-bfs --steps 5 --warmup 1 > $OUT/pmc_rd.log 2>&1 || exit 5
-timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/pmc_wr -o wr -- python3 bench.py --no-cpu --no-bfs --steps 5 --warmup 1 > $OUT/pmc_wr.log 2>&1 || exit 6
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --no-cpu --no-bfs --steps 5 --warmup 1 > $OUT/pmc_fetch.log 2>&1 || exit 7
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o bench -- python3 bench.py --no-cpu --no-big > $OUT/stats.log 2>&1 || exit 4
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --output-format csv -d $OUT/pmc_rd -o rd -- python3 bench.py --no-cpu --no-bfs --no-big --steps 10 --warmup 2 > $OUT/pmc_rd.log 2>&1 || exit 5
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/pmc_wr -o wr -- python3 bench.py --no-cpu --no-bfs --no-big --steps 10 --warmup 2 > $OUT/pmc_wr.log 2>&1 || exit 6
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --no-cpu --no-bfs --no-big --steps 10 --warmup 2 > $OUT/pmc_fetch.log 2>&1 || exit 7
 echo done
