@@ -49,4 +49,69 @@ __device__ __forceinline__ void block_append_frontier(bool take, int32_t v, int6
     __syncthreads();  // the scratch is reused by the next call
 }
 
+// LDS-staged frontier append: a block collects its appends in LDS (positions and edge offsets
+// relative to the block's staged run) and reserves global queue space with ONE atomic per flush —
+// normally once per kernel, at the end.  A single device-scope counter saturates near 90 atomics
+// per microsecond (MI355X_MICROARCH.md price list, dequeue row), so one atomic per block and wave
+// iteration made the frontier counter the bottleneck of large levels (RMAT-26 level 2: ~230 K appends).
+// Calls must be block-uniform; staged_flush must be called by the whole block before it exits.
+struct StagedAppend {
+    static constexpr int kCap = 2048;  // at least one full block of appends fits after a flush check
+    int32_t v[kCap];
+    int64_t off[kCap];                 // edge offset of entry i inside the staged run
+    unsigned long long wcnt[kBlock / kWave], wdeg[kBlock / kWave];
+    unsigned long long n, dsum, base;
+};
+__device__ __forceinline__ void staged_init(StagedAppend& sa) {
+    if (threadIdx.x == 0) sa.n = sa.dsum = 0;
+    __syncthreads();
+}
+__device__ __forceinline__ void staged_flush(StagedAppend& sa, int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                             unsigned long long* __restrict__ packed) {
+    __syncthreads();
+    if (threadIdx.x == 0) sa.base = sa.n ? atomicAdd(packed, (sa.n << kPackShift) | sa.dsum) : 0ull;
+    __syncthreads();
+    const unsigned long long n = sa.n, qb = sa.base >> kPackShift, eb = sa.base & kEdgeMask;
+    for (unsigned long long i = threadIdx.x; i < n; i += blockDim.x) {
+        queue[qb + i] = sa.v[i];
+        qoff[qb + i] = (int64_t)eb + sa.off[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sa.n = sa.dsum = 0;
+    __syncthreads();
+}
+__device__ __forceinline__ void staged_append(bool take, int32_t v, int64_t deg, StagedAppend& sa,
+                                              int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                              unsigned long long* __restrict__ packed) {
+    const uint64_t mask = __ballot(take);
+    const int64_t d = take ? deg : 0;
+    const int64_t dinc = wave_inclusive_scan_add(d);
+    const int wv = wave_id();
+    if (lane_id() == kWave - 1) {
+        sa.wcnt[wv] = (unsigned long long)__popcll(mask);
+        sa.wdeg[wv] = (unsigned long long)dinc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = sa.n, e = sa.dsum;
+        for (int k = 0; k < kBlock / kWave; ++k) {
+            const unsigned long long ck = sa.wcnt[k], ek = sa.wdeg[k];
+            sa.wcnt[k] = c;  // positions and offsets after the staged run
+            sa.wdeg[k] = e;
+            c += ck;
+            e += ek;
+        }
+        sa.n = c;
+        sa.dsum = e;
+    }
+    __syncthreads();
+    if (take) {
+        const unsigned long long p = sa.wcnt[wv] + (unsigned long long)__popcll(mask & lanemask_lt());
+        sa.v[p] = v;
+        sa.off[p] = (int64_t)sa.wdeg[wv] + dinc - d;
+    }
+    __syncthreads();
+    if (sa.n > (unsigned long long)(StagedAppend::kCap - kBlock)) staged_flush(sa, queue, qoff, packed);
+}
+
 }  // namespace jg

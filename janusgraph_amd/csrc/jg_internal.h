@@ -201,6 +201,7 @@ struct Shard {
     DevBuf<int32_t> bfs_queue[2];            // [rows] frontier vertices
     DevBuf<int64_t> bfs_qoff[2];             // [rows] first push edge of each queue entry
     DevBuf<unsigned long long> bfs_bm[2];    // [ceil(rows/64)] frontier bitmaps (bottom-up)
+    DevBuf<uint8_t> bfs_seen;                // [rows] depth-is-set byte map (filters depth probes)
     DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal

@@ -96,6 +96,8 @@ struct BfsLevel {
     int64_t* qoff_out;
     const unsigned long long* bm_in;
     unsigned long long* bm_out;
+    uint8_t* seen;  // seen[v] != 0: depth[v] is set (a 64 MB byte map at 2^26 vertices stays in the
+                    // Infinity Cache where the 268 MB depth array does not; bytes need no atomics)
     unsigned long long* ctr;  // [kBfsRing] packed frontier counters, slot = level % kBfsRing
     BfsState* st;             // [kBfsRing]
     int level, max_depth;
@@ -138,7 +140,7 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
 // loads, then all depth probes and claims, then the degree loads) so its dependent memory round trips
 // do not multiply with the edges it holds; one block-wide append per edge slot follows.
 __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed,
-                                             AppendScratch& sc) {
+                                             StagedAppend& sc) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int ept = mf <= nthreads ? 1 : kTdEdgesPerThread;  // grid-uniform
@@ -179,22 +181,25 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
 #pragma unroll
             for (int k = 0; k < kTdEdgesPerThread; ++k) have[k] = false, v[k] = 0;
         }
-        int32_t dv[kTdEdgesPerThread];
+        uint8_t sv[kTdEdgesPerThread];
 #pragma unroll
-        for (int k = 0; k < kTdEdgesPerThread; ++k) dv[k] = have[k] ? a.depth[v[k]] : 0;
+        for (int k = 0; k < kTdEdgesPerThread; ++k) sv[k] = have[k] ? a.seen[v[k]] : 1;
 #pragma unroll
-        for (int k = 0; k < kTdEdgesPerThread; ++k)
-            won[k] = have[k] && dv[k] < 0 && atomicCAS(&a.depth[v[k]], -1, next_depth) == -1;
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            // the byte map filters; the CAS on depth decides (a stale byte only costs a failed CAS)
+            won[k] = !sv[k] && atomicCAS(&a.depth[v[k]], -1, next_depth) == -1;
+            if (won[k]) a.seen[v[k]] = 1;
+        }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) vdeg[k] = won[k] ? a.deg_rp[v[k] + 1] - a.deg_rp[v[k]] : 0;
-        for (int k = 0; k < ept; ++k) block_append_frontier(won[k], v[k], vdeg[k], a.queue_out, a.qoff_out, packed, sc);
+        for (int k = 0; k < ept; ++k) staged_append(won[k], v[k], vdeg[k], sc, a.queue_out, a.qoff_out, packed);
     }
 }
 
 // Bottom-up: one lane per unvisited vertex scans its pull row against the frontier and stops at the
 // first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
 template <bool kFromDepth>
-__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, AppendScratch& sc) {
+__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, StagedAppend& sc) {
     const int64_t words = (a.rows + 63) / 64;
     constexpr int kWpb = kBlock / kWave;
     const int64_t wstride = (int64_t)gridDim.x * kWpb;
@@ -205,7 +210,7 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t vdeg = 0;
-        if (v < a.rows && a.depth[v] < 0) {
+        if (v < a.rows && !a.seen[v]) {
             // kBuBatch neighbours per step: all column loads, then all frontier probes, then the test,
             // so a row scanned to its end pays two round trips per batch instead of per neighbour
             // (which neighbour hits does not matter: the depth is level + 1 either way)
@@ -223,12 +228,13 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
             }
             if (found) {
                 a.depth[v] = next_depth;
+                a.seen[v] = 1;
                 vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
             }
         }
         const uint64_t word = __ballot(found);
         if (lane_id() == 0 && w < words) a.bm_out[w] = word;
-        block_append_frontier(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed, sc);
+        staged_append(found, (int32_t)v, vdeg, sc, a.queue_out, a.qoff_out, packed);
     }
 }
 
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
     __shared__ long long s_nf, s_mf;
     __shared__ int s_switch;
-    __shared__ AppendScratch s_app;
+    __shared__ StagedAppend s_app;
     if (threadIdx.x == 0) {
         int64_t nf, mf;
         bool sw;
@@ -253,9 +259,11 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __syncthreads();
     if (s_st.done) return;
     unsigned long long* packed = a.ctr + a.level % kBfsRing;
+    staged_init(s_app);
     if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed, s_app);
     else if (s_switch) bfs_bottom_up<true>(a, packed, s_app);
     else bfs_bottom_up<false>(a, packed, s_app);
+    staged_flush(s_app, a.queue_out, a.qoff_out, packed);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -265,9 +273,11 @@ __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
 // depth = -1 except the source; level -1 state: nothing explored, the source is the frontier
 __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64_t source, int32_t* queue,
                                 int64_t* qoff, const int64_t* __restrict__ deg_rp, long long total,
-                                unsigned long long* ctr, BfsState* st) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x)
+                                unsigned long long* ctr, BfsState* st, uint8_t* __restrict__ seen) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
         depth[i] = i == source ? 0 : -1;
+        seen[i] = i == source;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         queue[0] = (int32_t)source;
         qoff[0] = 0;
@@ -597,12 +607,13 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         if (sh.bfs_qoff[k].size() != r1) sh.bfs_qoff[k].alloc(r1);
         if (sh.bfs_bm[k].size() != w1) sh.bfs_bm[k].alloc(w1);
     }
+    if (sh.bfs_seen.size() != r1) sh.bfs_seen.alloc(r1);
     if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
     if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
     BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
     bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
                                                       degcsr->row_ptr.get(), (long long)degcsr->nnz,
-                                                      sh.bfs_ctr.get(), st);
+                                                      sh.bfs_ctr.get(), st, sh.bfs_seen.get());
     JG_LAUNCH_CHECK();
     BfsLevel a{};
     a.push_rp = push ? push->row_ptr.get() : nullptr;
@@ -612,6 +623,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.deg_rp = degcsr->row_ptr.get();
     a.depth = depth;
     a.rows = rows;
+    a.seen = sh.bfs_seen.get();
     a.ctr = sh.bfs_ctr.get();
     a.st = st;
     a.max_depth = max_depth;
