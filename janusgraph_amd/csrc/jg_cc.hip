@@ -96,13 +96,15 @@ __global__ __launch_bounds__(kBlock) void cc_senders_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ rp, int32_t* __restrict__ queue,
                                                             int64_t* __restrict__ qoff,
                                                             unsigned long long* __restrict__ packed) {
-    __shared__ AppendScratch sc;
+    __shared__ StagedAppend sc;
+    staged_init(sc);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
         const bool take = v < rows && msg[v] < kNoMsg;
-        block_append_frontier(take, (int32_t)v, take ? rp[v + 1] - rp[v] : 0, queue, qoff, packed, sc);
+        staged_append(take, (int32_t)v, take ? rp[v + 1] - rp[v] : 0, sc, queue, qoff, packed);
     }
+    staged_flush(sc, queue, qoff, packed);
 }
 
 struct CcPush {
@@ -119,7 +121,8 @@ struct CcPush {
 };
 
 __global__ __launch_bounds__(kBlock) void cc_push_kernel(CcPush a) {
-    __shared__ AppendScratch sc;
+    __shared__ StagedAppend sc;
+    staged_init(sc);
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * 4;
@@ -152,9 +155,10 @@ __global__ __launch_bounds__(kBlock) void cc_push_kernel(CcPush a) {
                 const int32_t m = a.msg[u];
                 if (m < a.cand[v]) take = atomicMin(&a.cand[v], m) == kNoMsg;
             }
-            block_append_frontier(take, v, 0, a.touched, a.touched_off, a.tpacked, sc);
+            staged_append(take, v, 0, sc, a.touched, a.touched_off, a.tpacked);
         }
     }
+    staged_flush(sc, a.touched, a.touched_off, a.tpacked);
 }
 
 // touched vertex v: the pull superstep's finalize with the pushed minimum

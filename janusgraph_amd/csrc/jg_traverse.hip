@@ -345,14 +345,16 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned l
                                                                 const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
                                                                 unsigned long long* __restrict__ packed) {
-    __shared__ AppendScratch sc;
+    __shared__ StagedAppend sc;
+    staged_init(sc);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
         const bool take = v < rows && F[v] != 0ull;
         const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
-        block_append_frontier(take, (int32_t)v, deg, queue, qoff, packed, sc);
+        staged_append(take, (int32_t)v, deg, sc, queue, qoff, packed);
     }
+    staged_flush(sc, queue, qoff, packed);
 }
 
 struct MsTd {
@@ -370,7 +372,8 @@ struct MsTd {
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
-    __shared__ AppendScratch sc;
+    __shared__ StagedAppend sc;
+    staged_init(sc);
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -403,9 +406,10 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 const unsigned long long w = a.F[v] & ~a.visited[u];
                 if (w) take = atomicOr(&a.Fnext[u], w) == 0ull;
             }
-            block_append_frontier(take, u, 0, a.touched, a.touched_off, a.tpacked, sc);
+            staged_append(take, u, 0, sc, a.touched, a.touched_off, a.tpacked);
         }
     }
+    staged_flush(sc, a.touched, a.touched_off, a.tpacked);
 }
 
 // touched vertex u: its new bits become its next-frontier word (and the visited / depth updates)
@@ -413,7 +417,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
                                                                 MsBfsOp op, const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
                                                                 unsigned long long* __restrict__ packed) {
-    __shared__ AppendScratch sc;
+    __shared__ StagedAppend sc;
+    staged_init(sc);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nt; x0 += stride) {  // block-uniform trips
         const int64_t x = x0 + threadIdx.x;
@@ -427,8 +432,9 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
             take = op.Fout[u] != 0ull;
             if (take) deg = push_rp[u + 1] - push_rp[u];
         }
-        block_append_frontier(take, u, deg, queue, qoff, packed, sc);
+        staged_append(take, u, deg, sc, queue, qoff, packed);
     }
+    staged_flush(sc, queue, qoff, packed);
 }
 
 // ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
