@@ -417,7 +417,7 @@ struct Tune {
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
-    int bfs_grid = 4096;              //         most workgroups of a level launch (grid-stride beyond)
+    int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int merge_nt = 0;                 // merge kernel: bit 0 non-temporal band loads, bit 1 non-temporal partial stores
     int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
     int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power

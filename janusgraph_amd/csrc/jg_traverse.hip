@@ -635,9 +635,12 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.max_depth = max_depth;
     a.alpha = (double)tune().bfs_alpha;
     a.beta = (double)tune().bfs_beta;
-    // a fixed grid: bottom-up covers every word, top-down strides over the frontier's edges
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((words * kWave + kBlock - 1) / kBlock, 64),
-                                                      tune().bfs_grid);
+    // a fixed grid, both directions grid-stride: ~sqrt(rows) workgroups (tools/bfs_sweep.py, ms per
+    // traversal: RMAT-20 0.164 / 0.141 / 0.140 / 0.157 at 256 / 512 / 1024 / 4096; RMAT-22 0.311 /
+    // 0.310 / 0.412 at 1024 / 2048 / 8192; RMAT-26 3.46 / 2.45 / 2.19 / 2.11 / 2.14 / 2.76 at 512 / 1024
+    // / 4096 / 8192 / 16384 / 65536): small levels pay less per block, big ones need the parallelism
+    const int64_t sq = 1ll << ((bits_for((uint64_t)std::max<int64_t>(rows - 1, 1)) + 1) / 2);
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sq, 64), tune().bfs_grid);
     BfsState hs{};
     int level = 0;
     for (int batch = 8;; batch = 16) {

@@ -1,6 +1,6 @@
 """Sweep a BFS knob on the bench's RMAT-20 single-source BFS (bench.py's procedure: 6 sources,
 Graph500 resampling of tiny components, first run dropped).  Usage: python tools/bfs_sweep.py
-bfs_grid 1024 2048 4096"""
+[--scale S] bfs_grid 1024 2048 4096"""
 import json
 import os
 import sys
@@ -12,19 +12,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     import janusgraph_amd as jg
-    key, values = sys.argv[1], [int(v) for v in sys.argv[2:]]
+    args = sys.argv[1:]
+    scale = 20
+    if args[0] == "--scale":
+        scale, args = int(args[1]), args[2:]
+    key, values = args[0], [int(v) for v in args[1:]]
     ctx = jg.Context((0,))
-    g = ctx.build_rmat(20, 16, 0x5EED + 20, flags=jg.ADJ_BOTH)
+    g = ctx.build_rmat(scale, 16, 0x5EED + scale, flags=jg.ADJ_BOTH)
     for v in values:
         jg._lib.tune_set(key, v)
         ms = []
         rng = np.random.default_rng(1)
         for rep in range(3):
             for k in range(6):
-                src = int(rng.integers(0, 1 << 20))
+                src = int(rng.integers(0, 1 << scale))
                 g.bfs([src], jg.DIR_BOTH, want=False)
                 s = ctx.stats()
-                if s["edges_traversed"] < (16 << 20) // 100 or (rep == 0 and k == 0):
+                if s["edges_traversed"] < (16 << scale) // 100 or (rep == 0 and k == 0):
                     continue
                 ms.append((s["compute_ms"], s["edges_traversed"] / (s["compute_ms"] * 1e-3) / 1e9))
         ms = np.array(ms)
