@@ -86,8 +86,11 @@ typedef struct jg_graph_info {
     int64_t num_edges;           /* edges kept: both endpoints in V                                  */
     int64_t ghost_edges;         /* edges dropped because an endpoint is not in V                    */
     int64_t self_loops;          /* kept edges with src == dst                                       */
-    int64_t truncated_vertices;  /* vertices with > JG_FULGORA_HARD_QUERY_LIMIT edge entries (in+out):
-                                    Fulgora would silently truncate their OUT/IN slices; we do not  */
+    int64_t truncated_vertices;  /* without a query limit: vertices with > JG_FULGORA_HARD_QUERY_LIMIT
+                                    edge entries (in+out), whose OUT/IN slices Fulgora truncates and
+                                    this graph does not.  Built with jg_builder_set_query_limit: the
+                                    rows whose edge slice reached the limit (Fulgora's
+                                    truncated-results metric, VertexJobConverter.java:139)          */
     int64_t max_in_degree;
     int64_t max_out_degree;
     int64_t device_bytes;        /* device memory held by this graph, summed over shards             */
@@ -184,6 +187,20 @@ int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* 
 int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                         const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
                         const int32_t* entry_weight, int64_t nentries);
+/* Fulgora's per-row slice cap (graphdb/olap/QueryContainer.java:42,121-146): an untyped OUT or IN edge
+ * scope is not a fitted query (query/vertex/BasicVertexCentricQueryBuilder.java:451-456), so the scan
+ * loads each row's EDGE slice (IDHandler.getBounds(EDGE), idhandling/IDHandler.java:172-193: the visible
+ * user edges of both directions, contiguous in column order) with at most `limit` entries
+ * (inmemory/SinglePageEntryBuffer.java:54-77 stops there), and a program reads only the entries of its
+ * direction among them.  With limit > 0 (JG_FULGORA_HARD_QUERY_LIMIT reproduces Fulgora) the graph is
+ * built from what the programs would read: the OUT adjacency and out-degrees (PageRank's edgeCount)
+ * from the OUT entries within their row's first `limit`; the IN adjacency, for in_entries = JG_DIR_IN,
+ * from the IN entries within their row's first `limit` (PageRank's gather and a combiner over IN:
+ * receivers read their own IN entries) or, for JG_DIR_OUT, as the transpose of the capped OUT entries
+ * (ShortestDistance: a receiver reads its OUT entries, the IN adjacency is pushed along); BOTH is a
+ * fitted query and never capped.  limit = 0 (the default) builds the untruncated graph.  Rows only
+ * (jg_builder_add_rows); call before the first chunk. */
+int jg_builder_set_query_limit(jg_builder* b, int64_t limit, int32_t in_entries);
 int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out);
 int jg_builder_destroy(jg_builder* b);
 /* vid_out[i] = the id of vertex offset + i in output order (the order vid[] / the kept rows were given). */

@@ -4,7 +4,8 @@ The compute path is libjanusgpu.so (hand-written HIP for gfx950, C-ABI in includ
 this package is its host-side mirror of the TinkerPop GraphComputer API.
 """
 from ._lib import (ADJ_BOTH, ADJ_IN, ADJ_OUT, COMBINE_MAX, COMBINE_MIN, COMBINE_SUM, DIR_BOTH, DIR_IN,  # noqa: F401
-                   DIR_OUT, DIST_ABSENT, LIB_PATH, WEIGHT_ABSENT, Builder, Context, Graph, JanusGpuError, load)
+                   DIR_OUT, DIST_ABSENT, FULGORA_HARD_QUERY_LIMIT, LIB_PATH, WEIGHT_ABSENT, Builder, Context,
+                   Graph, JanusGpuError, load)
 from .computer import ComputedGraph, ComputerResult, GpuGraphComputer, Memory  # noqa: F401
 from .computer_types import (GraphComputerError, Persist, ProgramNotSupported, ResultGraph,  # noqa: F401
                              ResultMode)

@@ -39,6 +39,7 @@ EXPORTS = [
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_combine_steps", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set", "jg_builder_create", "jg_builder_add_vertices", "jg_builder_add_edges", "jg_builder_set_schema",
     "jg_builder_add_rows", "jg_builder_finish", "jg_builder_destroy", "jg_graph_vertex_ids",
+    "jg_builder_set_query_limit",
 ]
 
 
@@ -125,6 +126,7 @@ def load():
         "jg_builder_finish": ([_P, ctypes.c_uint32, _PP], ctypes.c_int),
         "jg_builder_destroy": ([_P], ctypes.c_int),
         "jg_graph_vertex_ids": ([_P, _i64, _i64, _P], ctypes.c_int),
+        "jg_builder_set_query_limit": ([_P, _i64, _i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -309,6 +311,13 @@ class Builder:
             raise ValueError("type_ids and type_mult differ in length")
         self._schema = (tid, tm)
         check(load().jg_builder_set_schema(self._h, _ptr(tid), _ptr(tm), len(tid), int(partition_bits)))
+
+    def set_query_limit(self, limit=FULGORA_HARD_QUERY_LIMIT, in_entries=DIR_IN):
+        """Fulgora's per-row slice cap (jg_builder_set_query_limit; QueryContainer.java:42,133): the
+        directed adjacencies hold only what Fulgora's programs would read.  in_entries=DIR_IN: the IN
+        adjacency from the rows' IN entries (PageRank, combiners over IN); DIR_OUT: the transpose of the
+        capped OUT entries (ShortestDistance).  Call before the first add_rows."""
+        check(load().jg_builder_set_query_limit(self._h, int(limit), int(in_entries)))
 
     def add_rows(self, row_keys, row_entry_off, data, entry_off, value_pos, entry_weight=None):
         keys = np.ascontiguousarray(row_keys, np.uint64)

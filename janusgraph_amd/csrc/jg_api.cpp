@@ -225,8 +225,18 @@ static void make_shards(Ctx& c, Graph& g) {
 // Builds g (shards made) from vertex / edge ids already on device `dev0` (written on stream `s0`):
 // vid[n] int64, src/dst[m] int64, weight[m] int32 (nullable).  Every shard remaps the whole edge list
 // (shards on other devices get a peer copy first), then the CSRs and plans are built.
+// The capped edge lists of a snapshot built under Fulgora's slice cap (device pointers on dev0):
+// osrc[m] pairs with d_dst (-1 beyond the cap), (isrc, idst)[mi] the IN entries within the cap.
+struct CappedIds {
+    const int64_t *osrc = nullptr, *isrc = nullptr, *idst = nullptr;
+    int64_t mi = 0;
+    bool in_from_in = false;
+    int64_t truncated_rows = 0;
+};
+
 static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int64_t* d_vid, int64_t n,
-                                  const int64_t* d_src, const int64_t* d_dst, const int32_t* d_w, int64_t m) {
+                                  const int64_t* d_src, const int64_t* d_dst, const int32_t* d_w, int64_t m,
+                                  const CappedIds* cap = nullptr) {
     if (n >= (int64_t)INT32_MAX) fail(JG_ERR_ARG, "more than 2^31-1 vertices");
     if (m >= (int64_t)UINT32_MAX) fail(JG_ERR_ARG, "more than 2^32-1 edges");
     {
@@ -240,8 +250,16 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
     g.has_weights = d_w != nullptr;
     std::vector<DevBuf<int32_t>> ds(g.shards.size()), dd(g.shards.size()), dw(g.shards.size());
     std::vector<DevBuf<int64_t>> pv(g.shards.size()), ps(g.shards.size()), pd(g.shards.size());
+    std::vector<DevBuf<int32_t>> dos(g.shards.size()), dis(g.shards.size()), did(g.shards.size());
     DenseEdges e;
     e.m = m;
+    if (cap) {
+        if (cap->mi >= (int64_t)UINT32_MAX) fail(JG_ERR_ARG, "more than 2^32-1 edges");
+        e.capped = true;
+        e.in_from_in = cap->in_from_in;
+        e.m_in = cap->in_from_in ? cap->mi : 0;
+        e.truncated_rows = cap->truncated_rows;
+    }
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh.device);
@@ -265,6 +283,35 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
         remap_ids_device(v, n, a, b, m, ds[i].get(), dd[i].get(), sh.stream);
         e.src.push_back(ds[i].get());
         e.dst.push_back(dd[i].get());
+        if (cap) {
+            DevBuf<int64_t> po, pis, pid;
+            const int64_t *o = cap->osrc, *is = cap->isrc, *id = cap->idst;
+            if (sh.device != dev0) {
+                po.alloc(std::max<int64_t>(m, 1));
+                peer(po.get(), cap->osrc, (size_t)m * sizeof(int64_t));
+                o = po.get();
+            }
+            dos[i].alloc(std::max<int64_t>(m, 1));
+            mask_ids_device(o, ds[i].get(), m, dos[i].get(), sh.stream);
+            e.out_src.push_back(dos[i].get());
+            if (cap->in_from_in) {
+                const int64_t mi = cap->mi;
+                if (sh.device != dev0) {
+                    pis.alloc(std::max<int64_t>(mi, 1));
+                    pid.alloc(std::max<int64_t>(mi, 1));
+                    peer(pis.get(), cap->isrc, (size_t)mi * sizeof(int64_t));
+                    peer(pid.get(), cap->idst, (size_t)mi * sizeof(int64_t));
+                    is = pis.get();
+                    id = pid.get();
+                }
+                dis[i].alloc(std::max<int64_t>(mi, 1));
+                did[i].alloc(std::max<int64_t>(mi, 1));
+                remap_ids_device(v, n, is, id, mi, dis[i].get(), did[i].get(), sh.stream);
+                e.in_src.push_back(dis[i].get());
+                e.in_dst.push_back(did[i].get());
+            }
+            JG_HIP(hipStreamSynchronize(sh.stream));  // the peer staging buffers are freed here
+        }
         if (d_w) {
             dw[i].alloc(std::max<int64_t>(m, 1));
             if (sh.device != dev0) peer(dw[i].get(), d_w, (size_t)m * sizeof(int32_t));
@@ -318,6 +365,8 @@ struct jg_builder {
     std::vector<int8_t> type_mult;
     int pbits = 5;
     bool schema_set = false;
+    int64_t query_limit = 0;  // jg_builder_set_query_limit
+    int32_t in_entries = JG_DIR_IN;
 };
 
 using jg::Error;
@@ -696,6 +745,18 @@ int jg_builder_set_schema(jg_builder* b, const int64_t* type_ids, const int8_t* 
     JG_GUARD_END
 }
 
+int jg_builder_set_query_limit(jg_builder* b, int64_t limit, int32_t in_entries) {
+    JG_GUARD_BEGIN
+    JG_ARG(b, "null builder");
+    JG_ARG(limit >= 0, "the query limit must be >= 0 (0: no limit)");
+    JG_ARG(in_entries == JG_DIR_IN || in_entries == JG_DIR_OUT, "in_entries must be JG_DIR_IN or JG_DIR_OUT");
+    if (b->finished || b->mode == 2) jg::fail(JG_ERR_STATE, "jg_builder_set_query_limit must precede every chunk");
+    if (b->mode == 1) jg::fail(JG_ERR_STATE, "a query limit applies to edgestore rows, not to vertex / edge ids");
+    b->query_limit = limit;
+    b->in_entries = in_entries;
+    JG_GUARD_END
+}
+
 int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                         const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
                         const int32_t* entry_weight, int64_t nentries) {
@@ -704,9 +765,11 @@ int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, 
     if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
     if (b->mode == 1) jg::fail(JG_ERR_STATE, "builder holds vertex / edge ids: rows cannot be mixed in");
     b->mode = 2;
-    if (!b->dec)
+    if (!b->dec) {
         b->dec = std::make_unique<jg::EdgestoreDecoder>(b->type_ids.data(), b->type_mult.data(),
                                                         (int32_t)b->type_ids.size(), b->pbits, builder_device(b));
+        b->dec->set_query_limit(b->query_limit);
+    }
     jg::EdgestoreRows r{row_keys, nrows,      row_entry_off, bytes,
                         nbytes,   entry_off,  value_pos,     nentries,
                         b->type_ids.data(), b->type_mult.data(), (int32_t)b->type_ids.size(), b->pbits};
@@ -735,9 +798,24 @@ int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
         b->dec->finish();
         decode_ms = b->dec->kernel_ms;
         chunks = b->dec->chunks_added_;
-        if (b->dec->weighted == 1 && b->dec->w.size() == 0) b->dec->w.alloc(1);
-        jg::build_from_device_ids(g, dev0, builder_stream(b), b->dec->vid.get(), b->dec->n, b->dec->src.get(),
-                                  b->dec->dst.get(), b->dec->weighted == 1 ? b->dec->w.get() : nullptr, b->dec->m);
+        jg::EdgestoreDecoder& d = *b->dec;
+        if (d.weighted == 1 && d.w.size() == 0) d.w.alloc(1);
+        jg::CappedIds cap;
+        if (d.query_limit() > 0 && d.weighted == 1 && b->in_entries == JG_DIR_IN)
+            jg::fail(JG_ERR_ARG, "entry weights under a query limit need in_entries = JG_DIR_OUT (ShortestDistance "
+                                 "reads its OUT entries)");
+        if (d.query_limit() > 0) {
+            for (auto* buf : {&d.osrc, &d.isrc, &d.idst})
+                if (buf->size() == 0) buf->alloc(1);
+            cap.osrc = d.osrc.get();
+            cap.isrc = d.isrc.get();
+            cap.idst = d.idst.get();
+            cap.mi = d.mi;
+            cap.in_from_in = b->in_entries == JG_DIR_IN;
+            cap.truncated_rows = d.truncated_rows;
+        }
+        jg::build_from_device_ids(g, dev0, builder_stream(b), d.vid.get(), d.n, d.src.get(), d.dst.get(),
+                                  d.weighted == 1 ? d.w.get() : nullptr, d.m, d.query_limit() > 0 ? &cap : nullptr);
     } else {
         jg::DeviceGuard dg(dev0);
         if (b->vid.size() == 0) b->vid.alloc(1);

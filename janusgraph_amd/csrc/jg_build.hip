@@ -438,6 +438,18 @@ void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int
     JG_LAUNCH_CHECK();
 }
 
+__global__ void mask_ids_kernel(const int64_t* __restrict__ masked, const int32_t* __restrict__ dense, int64_t m,
+                                int32_t* __restrict__ out) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x)
+        out[e] = masked[e] < 0 ? -1 : dense[e];
+}
+
+void mask_ids_device(const int64_t* masked, const int32_t* dense, int64_t m, int32_t* out, hipStream_t s) {
+    if (m <= 0) return;
+    mask_ids_kernel<<<grid_for(m), kBlock, 0, s>>>(masked, dense, m, out);
+    JG_LAUNCH_CHECK();
+}
+
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
                       int32_t* dsrc, int32_t* ddst, hipStream_t s) {
     DevBuf<uint64_t> keys(std::max<int64_t>(n, 1));
@@ -830,6 +842,14 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     }
 }
 
+namespace {
+struct EdgeList {
+    const int32_t* src;
+    const int32_t* dst;
+    int64_t m;
+};
+}  // namespace
+
 void build_graph_from_dense(Graph& g, DenseEdges& e) {
     const int64_t n = g.n, m = e.m;
     const int P = g.P;
@@ -844,6 +864,11 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         Shard& sh = *g.shards[li];
         DeviceGuard dg(sh.device);
         hipStream_t s = sh.stream;
+        // The edge list of each adjacency: all of them, unless the snapshot was taken under Fulgora's
+        // slice cap (then OUT: the capped OUT entries; IN: the capped IN entries or the capped OUT list).
+        const EdgeList all{e.src[li], e.dst[li], m};
+        const EdgeList outl = e.capped ? EdgeList{e.out_src[li], e.dst[li], m} : all;
+        const EdgeList inl = !e.capped ? all : e.in_from_in ? EdgeList{e.in_src[li], e.in_dst[li], e.m_in} : outl;
         DevBuf<int32_t> indeg(std::max<int64_t>(n, 1)), outdeg(std::max<int64_t>(n, 1));
         DevBuf<unsigned long long> cnt(5);
         JG_HIP(hipMemsetAsync(indeg.get(), 0, indeg.bytes(), s));
@@ -861,7 +886,6 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         unsigned long long hc[5];
         JG_HIP(hipMemcpyAsync(hc, cnt.get(), sizeof hc, hipMemcpyDeviceToHost, s));
         JG_HIP(hipStreamSynchronize(s));
-        const int64_t maxdeg = mode == 0 ? (int64_t)hc[2] : mode == 1 ? (int64_t)(hc[2] + hc[3]) : (int64_t)hc[3];
         if (first) {
             g.info.num_vertices = n;
             g.info.num_edges = (int64_t)hc[0];
@@ -869,32 +893,64 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
             g.info.self_loops = (int64_t)hc[1];
             g.info.max_in_degree = (int64_t)hc[2];
             g.info.max_out_degree = (int64_t)hc[3];
-            g.info.truncated_vertices = (int64_t)hc[4];
+            g.info.truncated_vertices = e.capped ? e.truncated_rows : (int64_t)hc[4];
         }
+        // Under the cap the directed adjacencies see capped degrees: in-degree from the IN list,
+        // out-degree (PageRank's edgeCount) from the OUT list.  BOTH keeps the uncapped sums.
+        DevBuf<int32_t> cin, cout_;
+        const int32_t *din = indeg.get(), *dout = outdeg.get();
+        if (e.capped && mode != 1) {
+            cin.alloc(std::max<int64_t>(n, 1));
+            cout_.alloc(std::max<int64_t>(n, 1));
+            DevBuf<int32_t> scratch(std::max<int64_t>(n, 1));
+            DevBuf<unsigned long long> c2(5);
+            JG_HIP(hipMemsetAsync(cin.get(), 0, cin.bytes(), s));
+            JG_HIP(hipMemsetAsync(cout_.get(), 0, cout_.bytes(), s));
+            JG_HIP(hipMemsetAsync(c2.get(), 0, c2.bytes(), s));
+            if (inl.m > 0) {
+                degree_kernel<<<grid_for(inl.m, kBlock, 256 * 16), kBlock, 0, s>>>(inl.src, inl.dst, inl.m, cin.get(),
+                                                                                   scratch.get(), c2.get());
+                JG_LAUNCH_CHECK();
+            }
+            if (outl.m > 0) {
+                degree_kernel<<<grid_for(outl.m, kBlock, 256 * 16), kBlock, 0, s>>>(outl.src, outl.dst, outl.m,
+                                                                                    scratch.get(), cout_.get(), c2.get());
+                JG_LAUNCH_CHECK();
+            }
+            if (n > 0) {
+                stats_kernel<<<grid_for(n, kBlock, 1024), kBlock, 0, s>>>(cin.get(), cout_.get(), n, c2.get() + 2);
+                JG_LAUNCH_CHECK();
+            }
+            JG_HIP(hipMemcpyAsync(hc, c2.get(), sizeof hc, hipMemcpyDeviceToHost, s));
+            JG_HIP(hipStreamSynchronize(s));
+            din = cin.get();
+            dout = cout_.get();
+        }
+        const int64_t maxdeg = mode == 0 ? (int64_t)hc[2] : mode == 1 ? (int64_t)(hc[2] + hc[3]) : (int64_t)hc[3];
+        const EdgeList& pull = mode == 0 ? inl : all;  // the tie-break's pull neighbours (modes 0 and 1)
         // degree-sorted relabel
         DevBuf<uint64_t> rkeys(std::max<int64_t>(n, 1));
         DevBuf<int32_t> order(std::max<int64_t>(n, 1)), padded(std::max<int64_t>(n, 1));
         if (n > 0) {
-            relabel_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(indeg.get(), outdeg.get(), n, mode, maxdeg, vbits,
-                                                               rkeys.get());
+            relabel_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(din, dout, n, mode, maxdeg, vbits, rkeys.get());
             JG_LAUNCH_CHECK();
             prim::radix_sort(rkeys.get(), nullptr, n, vbits + bits_for((uint64_t)maxdeg), s);
-            if (tune().relabel_ties && mode != 2 && m > 0) {
+            if (tune().relabel_ties && mode != 2 && pull.m > 0) {
                 // equal-degree vertices ordered by their hottest pull neighbour (then id)
                 const uint64_t vmask = (1ull << vbits) - 1ull;
                 DevBuf<int32_t> rank1(n), nbr_min(n);
                 rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, vmask, rank1.get());
                 JG_LAUNCH_CHECK();
                 JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
-                nbr_min_kernel<<<grid_for(m, kBlock, 256 * 16), kBlock, 0, s>>>(e.src[li], e.dst[li], m, mode,
-                                                                                 rank1.get(), nbr_min.get());
+                nbr_min_kernel<<<grid_for(pull.m, kBlock, 256 * 16), kBlock, 0, s>>>(pull.src, pull.dst, pull.m, mode,
+                                                                                      rank1.get(), nbr_min.get());
                 JG_LAUNCH_CHECK();
                 DevBuf<uint64_t> k1(n), k2(n);
                 tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, k1.get());
                 JG_LAUNCH_CHECK();
                 prim::radix_sort(k1.get(), nullptr, n, vbits + bits_for((uint64_t)n), s);
-                tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, indeg.get(), outdeg.get(), mode,
-                                                                   maxdeg, k2.get());
+                tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, din, dout, mode, maxdeg,
+                                                                   k2.get());
                 JG_LAUNCH_CHECK();
                 prim::radix_sort(k2.get(), nullptr, n, 32 + bits_for((uint64_t)maxdeg), s);
                 tie_final_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), k2.get(), n, vmask, rkeys.get());
@@ -917,22 +973,29 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         }
         sh.out_degree.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.rows > 0) {
-            local_outdeg_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(order.get(), outdeg.get(), n, P, r, sh.rows,
-                                                                     sh.out_degree.get());
+            local_outdeg_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(order.get(), e.capped ? dout : outdeg.get(), n, P,
+                                                                     r, sh.rows, sh.out_degree.get());
             JG_LAUNCH_CHECK();
         }
         SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0, CompactMap{}};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
+        auto use = [&](const EdgeList& l) {
+            a.src = l.src;
+            a.dst = l.dst;
+            a.m = l.m;
+        };
         // The pull adjacencies (IN: PageRank, BOTH: CC) are first built sub-slice-ordered, which the
         // split bands are cut from (separate copies), then rebuilt column-ordered: traversals scan
         // rows in column (degree-rank) order, and bottom-up BFS exits earlier that way.
         // Sharded: a halo plan first, whose compact ids the CSR columns then hold.
-        auto build_pull_csr = [&](int which, const int32_t* wt, Csr& csr, PullPlan& plan, Halo& halo) {
+        auto build_pull_csr = [&](int which, const EdgeList& l, const int32_t* wt, Csr& csr, PullPlan& plan,
+                                  Halo& halo) {
+            use(l);
             a.which = which;
             a.cm = CompactMap{};
             int64_t col_space = g.padded_len(), vec_entries = g.padded_len();
             if (P > 1 && tune().halo) {
-                build_halo(g, sh, e.src[li], e.dst[li], padded.get(), m, which, halo, s);
+                build_halo(g, sh, l.src, l.dst, padded.get(), l.m, which, halo, s);
                 a.cm = halo.map(g.S, r);
                 col_space = halo.C;
                 vec_entries = sh.rows + halo.recv_off[P];
@@ -955,18 +1018,20 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
             a.cm = CompactMap{};
             a.cbits = cbits;
         };
-        if (g.flags & JG_ADJ_IN) build_pull_csr(0, w, sh.in, sh.plan_in, sh.halo_in);
+        // (the IN entries of a capped snapshot carry no weights: ShortestDistance builds IN from OUT)
+        if (g.flags & JG_ADJ_IN) build_pull_csr(0, inl, e.capped && e.in_from_in ? nullptr : w, sh.in, sh.plan_in, sh.halo_in);
         if (g.flags & JG_ADJ_OUT) {
             if (P == 1) {  // one shard: OUT gets the sliced split too (combiner programs over out-edges)
                 Halo none;
-                build_pull_csr(1, w, sh.out, sh.plan_out, none);
+                build_pull_csr(1, outl, w, sh.out, sh.plan_out, none);
                 sh.plan_out_built = true;
             } else {  // sharded OUT has no halo plan: global columns, class plan built on first use
+                use(outl);
                 a.which = 1;
                 build_csr(sh, a, w, sh.out, s);
             }
         }
-        if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, nullptr, sh.both, sh.plan_both, sh.halo_both);
+        if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, all, nullptr, sh.both, sh.plan_both, sh.halo_both);
         JG_HIP(hipStreamSynchronize(s));
         first = false;
     }

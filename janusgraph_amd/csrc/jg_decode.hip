@@ -284,8 +284,9 @@ __global__ __launch_bounds__(kBlock) void edgestore_edges_kernel(EntryView a, co
                                                                   int64_t nrows, int64_t nent,
                                                                   const uint8_t* __restrict__ keep,
                                                                   const int64_t* __restrict__ row_vid, int pbits,
-                                                                  uint8_t* __restrict__ take, int64_t* __restrict__ src,
-                                                                  int64_t* __restrict__ dst, int32_t* __restrict__ err) {
+                                                                  bool with_in, uint8_t* __restrict__ take,
+                                                                  int64_t* __restrict__ src, int64_t* __restrict__ dst,
+                                                                  int32_t* __restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kStageWords];
     __shared__ int64_t win_off[kRowWin + 1];
     __shared__ uint8_t win_keep[kRowWin];
@@ -344,16 +345,67 @@ __global__ __launch_bounds__(kBlock) void edgestore_edges_kernel(EntryView a, co
             if (kp) {
                 const Decoded d = decode_entry(a, st.base + (o[j] - st.origin), o_next[j] - o[j], vp[j]);
                 if (d.dir < 0) atomicOr(err, kErrMalformed);
+                const int64_t other = pbits > 0 && d.dir >= 0 && is_partitioned(d.other, pbits)
+                                          ? canonical_vertex_id(d.other, pbits) : d.other;
                 if (d.dir == 0 && d.visible) {
                     t = 1;
                     src[e] = row_vid[r];
-                    dst[e] = pbits > 0 && is_partitioned(d.other, pbits) ? canonical_vertex_id(d.other, pbits)
-                                                                        : d.other;
+                    dst[e] = other;
+                } else if (with_in && d.dir == 1 && d.visible) {  // the IN entry of edge other -> row
+                    t = 2;
+                    src[e] = other;
+                    dst[e] = row_vid[r];
                 }
             }
             take[e] = t;
         }
         __syncthreads();
+    }
+}
+
+// ---- Fulgora's slice cap (jg_builder_set_query_limit) ----
+// take[e] != 0 exactly for the entries of the EDGE slice on processed rows (visible user edges, both
+// directions: the slice IDHandler.getBounds(EDGE) delimits).  pre = exclusive scan of that flag; an
+// entry's rank in its row's slice is pre[e] - pre[row start].  A row whose slice holds more than
+// `limit` entries marks the ones of rank >= limit (bit 2): the scan never returned them
+// (SinglePageEntryBuffer.getSlice stops at the limit).  Rows reaching the limit are counted, as
+// VertexJobConverter.process counts truncated-results (:139: entryList.size() >= limit).
+__global__ void slice_flag_kernel(const uint8_t* __restrict__ take, int64_t n, uint32_t* __restrict__ f) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        f[i] = take[i] ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void slice_cap_kernel(const int64_t* __restrict__ row_off, int64_t nrows,
+                                                            const int64_t* __restrict__ pre, int64_t limit,
+                                                            uint8_t* __restrict__ take,
+                                                            unsigned long long* __restrict__ truncated) {
+    for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {  // block-uniform: one row per iteration
+        const int64_t e0 = row_off[r], e1 = row_off[r + 1];
+        const int64_t base = pre[e0], cnt = pre[e1] - base;
+        if (cnt >= limit && threadIdx.x == 0) atomicAdd(truncated, 1ull);
+        if (cnt <= limit) continue;
+        for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock)
+            if (take[e] && pre[e] - base >= limit) take[e] |= 4;
+    }
+}
+
+// out_flag: OUT entries (every one: the uncapped list BOTH is built from); in_flag: IN entries within
+// the cap
+__global__ void split_flags_kernel(const uint8_t* __restrict__ take, int64_t n, uint8_t* __restrict__ out_flag,
+                                   uint8_t* __restrict__ in_flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t t = take[i];
+        out_flag[i] = t & 1;
+        in_flag[i] = (t & 6) == 2 ? 1 : 0;
+    }
+}
+
+// out[i] = in[idx[i]], or -1 where that OUT entry is beyond its row's cap
+__global__ void capped_gather_kernel(const int64_t* __restrict__ in, const uint8_t* __restrict__ take,
+                                     const int64_t* __restrict__ idx, int64_t n, int64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = idx[i];
+        out[i] = (take[e] & 4) ? -1 : in[e];
     }
 }
 
@@ -471,8 +523,10 @@ void edgestore_check(const EdgestoreRows& r) {
 struct EdgestoreChunk {
     int64_t R = 0, E = 0, nbytes = 0;
     PinnedBuf staging;
-    DevBuf<uint8_t> d_bytes, keep, keep_v, take;
-    DevBuf<int64_t> d_off, d_roff, row_vid, esrc, edst, block_row;
+    DevBuf<uint8_t> d_bytes, keep, keep_v, take, out_flag, in_flag;
+    DevBuf<int64_t> d_off, d_roff, row_vid, esrc, edst, block_row, pre;
+    DevBuf<uint32_t> slice;
+    DevBuf<unsigned long long> truncated;
     DevBuf<uint64_t> d_keys;
     DevBuf<int32_t> d_vpos, err, d_w;
     bool weighted = false;
@@ -585,6 +639,14 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     fit(c.d_vpos, E);
     fit(c.err, 1);
     if (r.weight) fit(c.d_w, E);
+    const bool capped = limit_ > 0;
+    if (capped) {
+        fit(c.slice, E + 1);
+        fit(c.pre, E + 1);
+        fit(c.out_flag, E);
+        fit(c.in_flag, E);
+        fit(c.truncated, 1);
+    }
     auto h2d = [&](void* d, size_t off, size_t bytes) {
         if (bytes) JG_HIP(hipMemcpyAsync(d, st + off, bytes, hipMemcpyHostToDevice, s));
     };
@@ -606,9 +668,24 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
         block_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(c.d_roff.get(), R, c.block_row.get());
         JG_LAUNCH_CHECK();
         edgestore_edges_kernel<<<grid_for((E + kEpt - 1) / kEpt, kBlock, 256 * 16), kBlock, 0, s>>>(
-            a, c.d_roff.get(), c.block_row.get(), R, E, c.keep.get(), c.row_vid.get(), pbits_, c.take.get(),
+            a, c.d_roff.get(), c.block_row.get(), R, E, c.keep.get(), c.row_vid.get(), pbits_, capped, c.take.get(),
             c.esrc.get(), c.edst.get(), c.err.get());
         JG_LAUNCH_CHECK();
+    }
+    if (capped) {
+        JG_HIP(hipMemsetAsync(c.truncated.get(), 0, sizeof(unsigned long long), s));
+        JG_HIP(hipMemsetAsync(c.slice.get() + E, 0, sizeof(uint32_t), s));
+        if (E) {
+            slice_flag_kernel<<<grid_for(E), kBlock, 0, s>>>(c.take.get(), E, c.slice.get());
+            JG_LAUNCH_CHECK();
+        }
+        prim::exclusive_scan(c.slice.get(), c.pre.get(), E + 1, s);
+        if (R) {
+            slice_cap_kernel<<<(unsigned)std::min<int64_t>(R, 4096), kBlock, 0, s>>>(c.d_roff.get(), R, c.pre.get(),
+                                                                                     limit_, c.take.get(),
+                                                                                     c.truncated.get());
+            JG_LAUNCH_CHECK();
+        }
     }
     JG_HIP(hipEventRecord(c.t1, s));
     c.pending = true;
@@ -642,8 +719,34 @@ void EdgestoreDecoder::complete(int slot) {
         JG_LAUNCH_CHECK();
         grow_append(vid, n, tmp_.get(), nk, s);
     }
-    const int64_t mk = prim::compact_indices(c.take.get(), c.E, idx_.get(), s);
+    const bool capped = limit_ > 0;
+    if (capped && c.E) {
+        split_flags_kernel<<<grid_for(c.E), kBlock, 0, s>>>(c.take.get(), c.E, c.out_flag.get(), c.in_flag.get());
+        JG_LAUNCH_CHECK();
+    }
+    if (capped) {
+        unsigned long long tr = 0;
+        JG_HIP(hipMemcpyAsync(&tr, c.truncated.get(), sizeof tr, hipMemcpyDeviceToHost, s));
+        JG_HIP(hipStreamSynchronize(s));
+        truncated_rows += (int64_t)tr;
+        const int64_t ki = prim::compact_indices(c.in_flag.get(), c.E, idx_.get(), s);
+        if (ki) {
+            int64_t m2 = mi;
+            gather_kernel<int64_t><<<grid_for(ki), kBlock, 0, s>>>(c.esrc.get(), idx_.get(), ki, tmp_.get());
+            JG_LAUNCH_CHECK();
+            grow_append(isrc, mi, tmp_.get(), ki, s);
+            gather_kernel<int64_t><<<grid_for(ki), kBlock, 0, s>>>(c.edst.get(), idx_.get(), ki, tmp_.get());
+            JG_LAUNCH_CHECK();
+            grow_append(idst, m2, tmp_.get(), ki, s);
+        }
+    }
+    const int64_t mk = prim::compact_indices(capped ? c.out_flag.get() : c.take.get(), c.E, idx_.get(), s);
     if (mk) {
+        if (capped) {  // the capped OUT list: the same edges, -1 sources beyond the cap
+            capped_gather_kernel<<<grid_for(mk), kBlock, 0, s>>>(c.esrc.get(), c.take.get(), idx_.get(), mk, tmp_.get());
+            JG_LAUNCH_CHECK();
+            grow_append(osrc, mo, tmp_.get(), mk, s);
+        }
         int64_t m2 = m;
         gather_kernel<int64_t><<<grid_for(mk), kBlock, 0, s>>>(c.esrc.get(), idx_.get(), mk, tmp_.get());
         JG_LAUNCH_CHECK();

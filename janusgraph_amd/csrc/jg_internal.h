@@ -266,11 +266,20 @@ struct DenseEdges {
     std::vector<int32_t*> src, dst;    // per local shard device pointers (size m)
     std::vector<int32_t*> weight;      // may hold nullptr
     int64_t m = 0;
+    // Fulgora's slice cap (jg_builder_set_query_limit): the OUT adjacency and out-degrees come from
+    // (out_src, dst), -1 where the OUT entry lies beyond its row's limit; the IN adjacency from
+    // (in_src, in_dst)[m_in] if in_from_in, else from the capped OUT list; BOTH from (src, dst).
+    bool capped = false, in_from_in = false;
+    std::vector<int32_t*> out_src, in_src, in_dst;
+    int64_t m_in = 0;
+    int64_t truncated_rows = 0;
 };
 void build_graph_from_dense(Graph& g, DenseEdges& e);
 void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s);
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
                       int32_t* dsrc, int32_t* ddst, hipStream_t s);
+// out[e] = -1 where masked[e] < 0, else dense[e]
+void mask_ids_device(const int64_t* masked, const int32_t* dense, int64_t m, int32_t* out, hipStream_t s);
 // col_space: length of the gathered vector; vec_entries: entries actually in it, elem_bytes: their
 // size (automatic band widths)
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
@@ -344,6 +353,12 @@ struct EdgestoreDecoder {
     DevBuf<int64_t> vid, src, dst;
     DevBuf<int32_t> w;    // weights of the kept edges (when every chunk carried entry weights)
     int64_t n = 0, m = 0, mw = 0;
+    // Slice cap (set_query_limit before the first add): osrc[m] = src, or -1 where the edge's OUT entry
+    // is beyond its row's limit; (isrc, idst)[mi] = the edges whose IN entry is within its row's limit.
+    void set_query_limit(int64_t limit) { limit_ = limit; }
+    int64_t query_limit() const { return limit_; }
+    DevBuf<int64_t> osrc, isrc, idst;
+    int64_t mo = 0, mi = 0, mi2 = 0, truncated_rows = 0;
     int weighted = -1;    // -1 no chunk yet, 0 / 1: the chunks carry no / per-entry weights
     float kernel_ms = 0;  // copy + decode time of every chunk (HIP events)
     int64_t chunks_added_ = 0, rows_ = 0, entries_ = 0, bytes_ = 0;
@@ -352,6 +367,7 @@ struct EdgestoreDecoder {
    private:
     void complete(int slot);
     int pbits_, device_;
+    int64_t limit_ = 0;
     int next_ = 0;
     hipStream_t streams_[2] = {nullptr, nullptr};
     std::unique_ptr<EdgestoreChunk> chunks_[2];

@@ -101,6 +101,11 @@ JNIEXPORT jint JNICALL FN(builderAddRows)(JNIEnv* env, jclass c, jlong b, jobjec
                                (const int32_t*)buf(env, entry_weight), nentries);
 }
 
+JNIEXPORT jint JNICALL FN(builderSetQueryLimit)(JNIEnv* env, jclass c, jlong b, jlong limit, jint in_entries) {
+    (void)env; (void)c;
+    return jg_builder_set_query_limit((jg_builder*)(intptr_t)b, limit, in_entries);
+}
+
 JNIEXPORT jint JNICALL FN(builderFinish)(JNIEnv* env, jclass c, jlong b, jint flags, jlongArray out) {
     (void)c;
     jg_graph* g = NULL;

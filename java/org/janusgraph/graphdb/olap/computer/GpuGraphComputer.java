@@ -34,6 +34,7 @@ import org.janusgraph.diskstorage.keycolumnvalue.scan.ScanMetrics;
 import org.janusgraph.diskstorage.keycolumnvalue.scan.StandardScanner;
 import org.janusgraph.graphdb.configuration.GraphDatabaseConfiguration;
 import org.janusgraph.graphdb.database.StandardJanusGraph;
+import org.janusgraph.graphdb.olap.QueryContainer;
 import org.janusgraph.graphdb.util.WorkerPool;
 
 import java.lang.reflect.Field;
@@ -188,7 +189,8 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         final long ctx = h[0];
         final Results res;
         try {
-            final long g = GpuSnapshot.scan(graph, ctx, run.adjacency(), run.weightProperty());
+            final long g = GpuSnapshot.scan(graph, ctx, run.adjacency(), run.weightProperty(), queryLimit(),
+                run.inEntries());
             try {
                 final long[] vid = GpuSnapshot.vertexIds(g);
                 res = run.execute(g, vid, graph, memory);
@@ -205,6 +207,16 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         memory.setRuntime(System.currentTimeMillis() - time);
         memory.complete();
         return new DefaultComputerResult(resultGraph, memory);
+    }
+
+    /**
+     * Fulgora's hard limit on the entries of a non-fitted slice (QueryContainer.DEFAULT_HARD_QUERY_LIMIT,
+     * olap/QueryContainer.java:42,133): the snapshot reproduces it, so vertices with more than 100000
+     * edge entries get exactly the truncated adjacency Fulgora computes on.  The system property
+     * janusgraph.computer.gpu.untruncated=true computes on every entry instead.
+     */
+    private static long queryLimit() {
+        return Boolean.getBoolean("janusgraph.computer.gpu.untruncated") ? 0L : QueryContainer.DEFAULT_HARD_QUERY_LIMIT;
     }
 
     private static int[] devices() {
@@ -436,6 +448,12 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
             return null;
         }
 
+        /** Under the slice cap: the entries a receiver reads for the IN adjacency (jg_builder_set_query_limit).
+         *  PageRank's gather reads its IN entries; ShortestDistance overrides (its OUT entries). */
+        int inEntries() {
+            return JanusGpu.DIR_IN;
+        }
+
         abstract Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory);
 
         static GpuProgram recognise(VertexProgram<?> vp, StandardJanusGraph graph) {
@@ -535,6 +553,11 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         @Override
         String weightProperty() {
             return weight;
+        }
+
+        @Override
+        int inEntries() {
+            return JanusGpu.DIR_OUT; // messages on Local.of(inE): the receiver reads its OUT entries
         }
 
         @Override

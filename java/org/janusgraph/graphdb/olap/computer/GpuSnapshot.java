@@ -181,15 +181,20 @@ final class GpuSnapshot implements ScanJob {
 
     /**
      * Scans the edgestore into a device graph with the adjacencies `flags`. weightProperty != null
-     * also sends every entry's edge weight (ShortestDistanceVertexProgram). Returns the graph handle;
-     * its vertex order is the scan's row order (read it with JanusGpu.graphVertexIds).
+     * also sends every entry's edge weight (ShortestDistanceVertexProgram). queryLimit > 0 builds what
+     * Fulgora's programs read under its slice cap (inEntries: JanusGpu.DIR_IN or DIR_OUT, see
+     * jg_builder_set_query_limit). Returns the graph handle; its vertex order is the scan's row order
+     * (read it with JanusGpu.graphVertexIds).
      */
-    static long scan(StandardJanusGraph graph, long ctx, int flags, String weightProperty) {
+    static long scan(StandardJanusGraph graph, long ctx, int flags, String weightProperty, long queryLimit,
+                     int inEntries) {
         final long[] h = new long[1];
         JanusGpu.check(JanusGpu.builderCreate(ctx, h));
         final long builder = h[0];
         WeightReader weights = null;
         try {
+            // Fulgora's per-row slice cap (QueryContainer.java:42,133), reproduced in the decode
+            JanusGpu.check(JanusGpu.builderSetQueryLimit(builder, queryLimit, inEntries));
             final List<EdgeLabel> labels = new ArrayList<>();
             final JanusGraphManagement mgmt = graph.openManagement();
             try {

@@ -52,6 +52,8 @@ final class JanusGpu {
     static native int builderAddRows(long builder, ByteBuffer rowKeys, long nrows, ByteBuffer rowEntryOff,
                                      ByteBuffer bytes, long nbytes, ByteBuffer entryOff, ByteBuffer valuePos,
                                      ByteBuffer entryWeight, long nentries);
+    /** jg_builder_set_query_limit: Fulgora's per-row slice cap (0: none); inEntries DIR_IN or DIR_OUT. */
+    static native int builderSetQueryLimit(long builder, long limit, int inEntries);
     /** jg_builder_finish; graph handle written to out[0]. */
     static native int builderFinish(long builder, int flags, long[] out);
 

@@ -238,7 +238,7 @@ def canonical_vertex_id(vid, partition_bits=5):
 
 
 def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=(), partition_bits=5,
-                       return_entries=False):
+                       return_entries=False, query_limit=0):
     """The scan -> snapshot step restated row by row (the checker of jg_graph_build_edgestore):
     VertexJobConverter.getKeyFilter drops invisible rows (olap/VertexJobConverter.java:174-177);
     process/isGhostVertex keep a row only if its first entry is the VertexExists property (:122-151),
@@ -248,7 +248,15 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
     (comp/VertexProgramScanJob.java:88-102, FulgoraVertexMemory.getCanonicalId) are one vertex: the
     canonical id, whose edges are the union over its representative rows.
     Returns (vid of kept vertices in row order, src ids, dst ids[, entry index of each edge]); raises
-    ValueError where Java throws."""
+    ValueError where Java throws.
+
+    query_limit > 0 restates Fulgora's slice cap (olap/QueryContainer.java:42,121-146: an untyped OUT/IN
+    edge scope is not fitted, BasicVertexCentricQueryBuilder.java:451-456, so each processed row's EDGE
+    slice, IDHandler.getBounds(EDGE) = the visible user edges of both directions in column order, is
+    read with that limit, SinglePageEntryBuffer.getSlice :54-77) and appends a dict: out_keep[i] = edge
+    i's OUT entry is among its row's first query_limit slice entries; in_src/in_dst = the edges whose
+    IN entry is (other endpoint -> row vertex); truncated_rows = rows whose slice reached the limit
+    (VertexJobConverter.java:139)."""
     data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
     off, row_off = _i64(off), _i64(row_off)
     t, d, o, _ = decode_edges(data, off, vpos, type_ids, type_mult)
@@ -262,6 +270,7 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
         return v
 
     keep_v, src, dst, ent = [], [], [], []
+    out_keep, in_src, in_dst, truncated = [], [], [], 0
     for r, vid in enumerate(vids):
         vid = int(vid)
         e0, e1 = int(row_off[r]), int(row_off[r + 1])
@@ -278,16 +287,30 @@ def edgestore_snapshot(keys, row_off, data, off, vpos, type_ids=(), type_mult=()
             if not (d[e0] == 2 and t[e0] == VERTEX_EXISTS_ID):
                 continue  # ghost vertex
             keep_v.append(cv)
+        rank = 0  # slice entries of this row so far
         for e in range(e0, e1):
             if d[e] < 0:
                 raise ValueError("malformed entry")
             visible = (int(data[off[e]]) >> 6) == 1  # relation-type header prefix >> 1: 1 = user, visible
+            in_slice = visible and d[e] in (0, 1)
+            within = query_limit <= 0 or rank < query_limit
+            rank += in_slice
             if d[e] == 0 and visible:
                 src.append(cv)
                 dst.append(canon(int(o[e])))
                 ent.append(e)
+                out_keep.append(within)
+            elif d[e] == 1 and visible and within:
+                in_src.append(canon(int(o[e])))
+                in_dst.append(cv)
+        truncated += query_limit > 0 and rank >= query_limit
     out = (np.array(keep_v, np.int64), np.array(src, np.int64), np.array(dst, np.int64))
-    return out + (np.array(ent, np.int64),) if return_entries else out
+    if return_entries:
+        out = out + (np.array(ent, np.int64),)
+    if query_limit > 0:
+        out = out + ({"out_keep": np.array(out_keep, bool), "in_src": np.array(in_src, np.int64),
+                      "in_dst": np.array(in_dst, np.int64), "truncated_rows": int(truncated)},)
+    return out
 
 
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2

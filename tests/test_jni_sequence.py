@@ -2,7 +2,8 @@
 no JDK). java/native/janusgpu_jni.c is a pass-through (tests/test_jni_shim.py), so each JanusGpu
 native below is the C-ABI call the shim makes, with the buffers GpuSnapshot / GpuGraphComputer build:
 
-  ctxCreate -> builderCreate -> builderSetSchema -> builderAddRows (one per scan chunk of whole rows,
+  ctxCreate -> builderCreate -> builderSetQueryLimit (100000: Fulgora's slice cap) -> builderSetSchema ->
+  builderAddRows (one per scan chunk of whole rows,
   entry weights for ShortestDistance) -> builderFinish -> builderDestroy -> graphInfo ->
   graphVertexIds (chunks) -> pageRank | shortestDistance | connectedComponents | bfs (64 sources per
   call, ShortestPathVertexProgram) -> graphDestroy -> ctxDestroy
@@ -34,7 +35,7 @@ def _ok(status):
 class JavaRun:
     """GpuSnapshot.scan + GpuSnapshot.vertexIds as the Java code issues them."""
 
-    def __init__(self, store, flags, entry_weight=None, nchunks=4, vid_chunk=97):
+    def __init__(self, store, flags, entry_weight=None, nchunks=4, vid_chunk=97, in_entries=2, limit=100000):
         from janusgraph_amd import _lib
         L = _lib.load()
         self.L = L
@@ -45,6 +46,7 @@ class JavaRun:
         b = ctypes.c_void_p()
         _ok(L.jg_builder_create(self.ctx, ctypes.byref(b)))
         try:
+            _ok(L.jg_builder_set_query_limit(b, limit, in_entries))  # GpuGraphComputer.queryLimit(), inEntries()
             _ok(L.jg_builder_set_schema(b, _p(tids), _p(tmult), len(tids), 5))
             bounds = np.linspace(0, len(keys), nchunks + 1).astype(int)
             for ch in row_chunks(store, bounds):
@@ -112,7 +114,7 @@ def test_shortest_distance_sequence_with_entry_weights(oracle_lib, store):
     ew = np.array([weight_of_rel.get(int(x), int(_lib.WEIGHT_ABSENT)) if dd == 0 else int(_lib.WEIGHT_ABSENT)
                    for x, dd in zip(rel, d)], np.int32)
     ov, os_, ot, ent = oracle_lib.edgestore_snapshot(keys, roff, data, off, vpos, tids, tmult, return_entries=True)
-    r = JavaRun(store[0], flags=2 | 1, entry_weight=ew)
+    r = JavaRun(store[0], flags=2 | 1, entry_weight=ew, in_entries=1)  # ShortestDistance: JanusGpu.DIR_OUT
     n = len(r.vid)
     index = {int(v): i for i, v in enumerate(ov)}
     live = np.array([int(a) in index and int(b) in index for a, b in zip(os_, ot)])
