@@ -156,8 +156,8 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n,
  * Unit weights.  Partitioned (vertex-cut) vertices are one vertex, the canonical id
  * (IDManager.java:525-551): every representative row adds its edges, only the canonical row's
  * VertexExists decides the ghost rule (VertexProgramScanJob.java:88-102).  A malformed entry on a
- * kept row or a key with no user vertex type: JG_ERR_ARG.  Stats: build_ms (whole snapshot), kernel_ms_total
- * (the decode kernels). */
+ * kept row or a key with no user vertex type: JG_ERR_ARG.  Stats: build_ms (whole snapshot),
+ * exchange_ms (the row copies), kernel_ms_total (copies + decode kernels). */
 int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                              const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
                              int64_t nentries, const int64_t* type_ids, const int8_t* type_mult, int32_t ntypes,
@@ -174,7 +174,9 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
  * graph exactly as jg_graph_build / jg_graph_build_edgestore would from the concatenated chunks
  * (vertex order = the order added; read it back with jg_graph_vertex_ids).  The builder is single-use;
  * destroy it after finish (or instead of it).  Stats of finish: build_ms, kernel_ms_total = copy +
- * decode time of the rows, kernel_launches = number of row chunks. */
+ * decode time of the rows (HIP events per chunk, summed), exchange_ms = their host -> device copies
+ * alone, kernel_launches = number of row chunks.  Chunks whose entries are all shorter than 256 bytes
+ * cross PCIe with 1-byte lengths and value positions instead of the int64 offsets and int32 positions. */
 typedef struct jg_builder jg_builder;
 int jg_builder_create(jg_ctx* ctx, jg_builder** out);
 int jg_builder_add_vertices(jg_builder* b, const int64_t* vid, int64_t n);

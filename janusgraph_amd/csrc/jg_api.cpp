@@ -635,8 +635,7 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
     JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
     const jg::EdgestoreRows r{row_keys, nrows,     row_entry_off, bytes,    nbytes,        entry_off,
                               value_pos, nentries, type_ids,      type_mult, ntypes,       partition_bits};
-    jg::edgestore_check(r);
-    *out = nullptr;
+    *out = nullptr;  // the decoder validates the rows and entries as it stages them
     jg::Ctx& c = ctx->impl;
     auto gh = std::make_unique<jg_graph>();
     jg::Graph& g = gh->impl;
@@ -646,7 +645,9 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
     jg::BuildTimer timer(g);
     jg::Shard& sh0 = *g.shards[0];
     jg::EdgestoreDecoder dec(type_ids, type_mult, ntypes, partition_bits, sh0.device);
-    dec.add(r);
+    // Fed in chunks of whole rows, as the builder is: the pinned staging stays small, and staging a
+    // chunk on the host overlaps the copy and decode of the one before.
+    jg::add_in_chunks(dec, r);
     dec.finish();
     {
         jg::DeviceGuard dg(sh0.device);
@@ -657,6 +658,7 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
     c.last = jg_stats{};
     c.last.build_ms = ms;
     c.last.kernel_ms_total = dec.kernel_ms;  // copy + decode of the rows
+    c.last.exchange_ms = dec.copy_ms;        // the host -> device copies alone
     c.last.kernel_launches = 1;
     // decode kernels: entry bytes + off/vpos/take (13 B) per entry, src/dst (16 B) per kept edge,
     // key/row_off/row_vid/keep (25 B) per row
@@ -792,11 +794,12 @@ int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
     jg::make_shards(c, g);
     jg::BuildTimer timer(g);
     const int dev0 = builder_device(b);
-    float decode_ms = 0;
+    float decode_ms = 0, copy_ms = 0;
     int64_t chunks = 0;
     if (b->mode == 2) {
         b->dec->finish();
         decode_ms = b->dec->kernel_ms;
+        copy_ms = b->dec->copy_ms;
         chunks = b->dec->chunks_added_;
         jg::EdgestoreDecoder& d = *b->dec;
         if (d.weighted == 1 && d.w.size() == 0) d.w.alloc(1);
@@ -836,6 +839,7 @@ int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
     c.last = jg_stats{};
     c.last.build_ms = ms;
     c.last.kernel_ms_total = decode_ms;
+    c.last.exchange_ms = copy_ms;
     c.last.kernel_launches = chunks;
     *out = gh.release();
     JG_GUARD_END

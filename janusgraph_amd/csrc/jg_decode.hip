@@ -15,7 +15,12 @@
 // absent labels are MULTI.  One thread per entry, every entry independent: byte-level work bound by
 // HBM (a few loads per entry; neighbouring threads read neighbouring entries).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "jg_internal.h"
@@ -400,6 +405,15 @@ __global__ void split_flags_kernel(const uint8_t* __restrict__ take, int64_t n, 
     }
 }
 
+// Narrow staging: off[i] += base (i <= n: off[n] is the scan's total), vpos[i] = the u8 position
+__global__ void widen_entries_kernel(const uint8_t* __restrict__ vp8, int64_t n, int64_t base,
+                                     int64_t* __restrict__ off, int32_t* __restrict__ vpos) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (base) off[i] += base;
+        if (i < n) vpos[i] = vp8[i];
+    }
+}
+
 // out[i] = in[idx[i]], or -1 where that OUT entry is beyond its row's cap
 __global__ void capped_gather_kernel(const int64_t* __restrict__ in, const uint8_t* __restrict__ take,
                                      const int64_t* __restrict__ idx, int64_t n, int64_t* __restrict__ out) {
@@ -504,14 +518,56 @@ void decode_edges(Ctx& c, const uint8_t* bytes, int64_t nbytes, const int64_t* o
     if (n && rel_out) copy_d2h(rel_out, d_rel.get(), (size_t)n * sizeof(int64_t), s);
 }
 
-void edgestore_check(const EdgestoreRows& r) {
-    if (r.nrows < 0 || r.nentries < 0) fail(JG_ERR_ARG, "negative size");
+// Host work over n items split into up to kHostThreads ranges: f(lo, hi, t) on threads of its own
+// (the caller's thread takes range 0).  Staging a chunk is a few passes over memory the caller just
+// wrote; one thread streams them at a fraction of the socket's bandwidth.
+constexpr int kHostThreads = 8;
+template <class F>
+void parallel_ranges(int64_t n, int64_t grain, F f) {
+    const int nt = (int)std::min<int64_t>(kHostThreads, std::max<int64_t>(1, n / std::max<int64_t>(grain, 1)));
+    if (nt <= 1) {
+        f((int64_t)0, n, 0);
+        return;
+    }
+    std::vector<std::thread> ts;
+    ts.reserve(nt - 1);
+    for (int t = 1; t < nt; ++t) ts.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
+    f((int64_t)0, n / nt, 0);
+    for (auto& th : ts) th.join();
+}
+
+void copy_parallel(void* dst, const void* src, size_t bytes) {
+    parallel_ranges((int64_t)bytes, (int64_t)4 << 20, [&](int64_t lo, int64_t hi, int) {
+        std::memcpy((char*)dst + lo, (const char*)src + lo, (size_t)(hi - lo));
+    });
+}
+
+// dst[i] = src[i] - base (offsets of a chunk cut out of larger arrays)
+void copy_rebased(int64_t* dst, const int64_t* src, int64_t n, int64_t base) {
+    if (base == 0) {
+        copy_parallel(dst, src, (size_t)n * sizeof(int64_t));
+        return;
+    }
+    parallel_ranges(n, (int64_t)1 << 18, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) dst[i] = src[i] - base;
+    });
+}
+
+// The row arrays (the entries are validated while they are staged, EdgestoreDecoder::add).
+static void check_rows(const EdgestoreRows& r) {
+    if (r.nrows < 0 || r.nentries < 0 || r.nbytes < 0) fail(JG_ERR_ARG, "negative size");
     if (r.pbits < 0 || r.pbits > 16) fail(JG_ERR_ARG, "partition bits must be in [0, 16]");
     if (r.nrows > 0 && (!r.keys || !r.row_off)) fail(JG_ERR_ARG, "null row arrays");
-    if (r.nrows == 0 ? r.nentries != 0 : (r.row_off[0] != 0 || r.row_off[r.nrows] != r.nentries))
+    if (r.nentries > 0 && (!r.bytes || !r.entry_off || !r.vpos)) fail(JG_ERR_ARG, "null entry arrays");
+    if (r.nrows == 0 ? r.nentries != 0
+                     : (r.row_off[0] != r.entry_base || r.row_off[r.nrows] - r.entry_base != r.nentries))
         fail(JG_ERR_ARG, "row offsets must run from 0 to the entry count");
     for (int64_t i = 0; i < r.nrows; ++i)
         if (r.row_off[i + 1] < r.row_off[i]) fail(JG_ERR_ARG, "row offsets must be non-decreasing");
+}
+
+void edgestore_check(const EdgestoreRows& r) {
+    check_rows(r);
     check_entries(r.bytes, r.nbytes, r.entry_off, r.vpos, r.nentries);
 }
 
@@ -527,6 +583,10 @@ struct EdgestoreChunk {
     DevBuf<int64_t> d_off, d_roff, row_vid, esrc, edst, block_row, pre;
     DevBuf<uint32_t> slice;
     DevBuf<unsigned long long> truncated;
+    DevBuf<uint8_t> d_meta8;   // narrow staging: entry lengths then value positions
+    DevBuf<int64_t> scan_tmp;  // scratch of the stream-ordered scans
+    bool narrow = false;
+    hipEvent_t tc = nullptr;   // after the chunk's copies
     DevBuf<uint64_t> d_keys;
     DevBuf<int32_t> d_vpos, err, d_w;
     bool weighted = false;
@@ -549,14 +609,56 @@ void grow_append(DevBuf<T>& acc, int64_t& len, const T* src, int64_t k, hipStrea
 }
 }  // namespace
 
-PinnedBuf::~PinnedBuf() {
-    if (p) (void)hipHostFree(p);
+// Pinning host memory costs ~10 ms per 50 MB, more than staging a chunk.  Released staging buffers
+// stay pinned in a small process-wide pool, so the next snapshot (the next computer run in the same
+// JVM, the next build) reuses them.  The pool is never torn down: the HIP runtime may be gone at exit.
+namespace {
+struct PinnedPool {
+    std::mutex mu;
+    std::vector<std::pair<void*, size_t>> free;
+};
+PinnedPool& pinned_pool() {
+    static PinnedPool* pool = new PinnedPool();
+    return *pool;
 }
+constexpr size_t kPoolKeep = 4;                     // buffers kept
+constexpr size_t kPoolMaxBytes = (size_t)1 << 30;   // larger ones are freed
+void pinned_release(void* p, size_t cap) {
+    if (!p) return;
+    PinnedPool& pool = pinned_pool();
+    {
+        std::lock_guard<std::mutex> lk(pool.mu);
+        if (cap <= kPoolMaxBytes && pool.free.size() < kPoolKeep) {
+            pool.free.emplace_back(p, cap);
+            return;
+        }
+    }
+    (void)hipHostFree(p);
+}
+}  // namespace
+
+PinnedBuf::~PinnedBuf() { pinned_release(p, cap); }
+
 void PinnedBuf::reserve(size_t n) {
     if (n <= cap) return;
-    if (p) (void)hipHostFree(p);
+    pinned_release(p, cap);
     p = nullptr;
     cap = 0;
+    {  // the smallest pooled buffer that fits
+        PinnedPool& pool = pinned_pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        size_t best = pool.free.size();
+        for (size_t i = 0; i < pool.free.size(); ++i)
+            if (pool.free[i].second >= n && (best == pool.free.size() || pool.free[i].second < pool.free[best].second))
+                best = i;
+        if (best < pool.free.size()) {
+            p = pool.free[best].first;
+            cap = pool.free[best].second;
+            pool.free.erase(pool.free.begin() + (std::ptrdiff_t)best);
+            return;
+        }
+    }
+    n = std::max<size_t>(n + n / 4, (size_t)1 << 20);  // headroom: chunks vary a little in size
     if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
@@ -575,6 +677,7 @@ EdgestoreDecoder::EdgestoreDecoder(const int64_t* type_ids, const int8_t* type_m
         chunks_[i] = std::make_unique<EdgestoreChunk>();
         JG_HIP(hipEventCreate(&chunks_[i]->t0));
         JG_HIP(hipEventCreate(&chunks_[i]->t1));
+        JG_HIP(hipEventCreate(&chunks_[i]->tc));
     }
     types_ = std::make_unique<TypeTable>(type_ids, type_mult, ntypes, streams_[0]);
 }
@@ -586,14 +689,27 @@ EdgestoreDecoder::~EdgestoreDecoder() {
         if (chunks_[i]) {
             (void)hipEventDestroy(chunks_[i]->t0);
             (void)hipEventDestroy(chunks_[i]->t1);
+            (void)hipEventDestroy(chunks_[i]->tc);
         }
         chunks_[i].reset();
         if (streams_[i]) (void)hipStreamDestroy(streams_[i]);
     }
 }
 
+namespace {
+using HostClock = std::chrono::steady_clock;
+double ms_since(HostClock::time_point t) {
+    return std::chrono::duration<double, std::milli>(HostClock::now() - t).count();
+}
+bool decode_trace() {
+    static const bool on = std::getenv("JG_DECODE_TRACE") != nullptr;
+    return on;
+}
+}  // namespace
+
 void EdgestoreDecoder::add(const EdgestoreRows& r) {
-    edgestore_check(r);
+    const auto h0 = HostClock::now();
+    check_rows(r);
     const int wmode = r.weight ? 1 : 0;
     if (weighted >= 0 && weighted != wmode) fail(JG_ERR_ARG, "entry weights must be given for every chunk or none");
     weighted = wmode;
@@ -601,27 +717,80 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     const int slot = next_;
     next_ ^= 1;
     EdgestoreChunk& c = *chunks_[slot];
+    const auto h1 = HostClock::now();
     if (c.pending) complete(slot);  // its buffers are reused below
+    const double t_complete = ms_since(h1);
     hipStream_t s = streams_[slot];
     const int64_t R = r.nrows, E = r.nentries;
     c.R = R;
     c.E = E;
     c.nbytes = r.nbytes;
-    // staging layout: off [E+1] i64 | roff [R+1] i64 | keys [R] u64 | vpos [E] i32 | weight [E] i32 | bytes
-    const size_t o_off = 0, o_roff = o_off + (size_t)(E + 1) * 8, o_keys = o_roff + (size_t)(R + 1) * 8,
-                 o_vpos = o_keys + (size_t)R * 8, o_w = o_vpos + (size_t)E * 4,
+    // Staging layout (pinned), in the order the copies go out:
+    //   narrow (every entry < 256 bytes, the usual case): len [E] u8 | vpos [E] u8 | ...
+    //   wide: off [E+1] i64 | vpos [E] i32 | ...
+    //   ... | roff [R+1] i64 | keys [R] u64 | weight [E] i32 (optional) | bytes
+    // Narrow entries cross PCIe with 2 bytes of offsets and value positions instead of 12; the device
+    // rebuilds the offsets with a scan of the lengths.
+    // One parallel pass validates every entry (inside the bytes, value position within it) and writes
+    // the narrow metadata; a chunk with a long entry is then staged wide instead.
+    const size_t narrow_meta = (size_t)E * 2, wide_meta = (size_t)(E + 1) * 8 + (size_t)E * 4;
+    const size_t tail = (size_t)(R + 1) * 8 + (size_t)R * 8 + (r.weight ? (size_t)E * 4 : 0) + (size_t)r.nbytes + 1;
+    const auto h2 = HostClock::now();
+    c.staging.reserve(narrow_meta + tail);
+    const double t_reserve = ms_since(h2);
+    const auto h3 = HostClock::now();
+    int64_t bad[kHostThreads];
+    bool wide[kHostThreads];
+    for (int t = 0; t < kHostThreads; ++t) {
+        bad[t] = -1;
+        wide[t] = false;
+    }
+    {
+        uint8_t* len8 = (uint8_t*)c.staging.p;
+        uint8_t* vp8 = len8 + E;
+        const int64_t* off = r.entry_off;
+        const int32_t* vpos = r.vpos;
+        const int64_t nbytes = r.nbytes, b0 = r.byte_base;
+        parallel_ranges(E, (int64_t)1 << 18, [&](int64_t lo, int64_t hi, int t) {
+            bool w = false;
+            for (int64_t e = lo; e < hi; ++e) {
+                const int64_t o0 = off[e] - b0, o1 = off[e + 1] - b0, len = o1 - o0;
+                const int32_t vp = vpos[e];
+                if (o0 < 0 || len < 1 || o1 > nbytes || vp < 1 || vp > len) {
+                    bad[t] = e;
+                    return;
+                }
+                if (len >= 256) w = true;
+                len8[e] = (uint8_t)len;
+                vp8[e] = (uint8_t)vp;
+            }
+            wide[t] = w;
+        });
+    }
+    bool narrow = true;
+    for (int t = 0; t < kHostThreads; ++t) {
+        if (bad[t] >= 0) fail(JG_ERR_ARG, "entry " + std::to_string(bad[t]) + " out of range");
+        narrow = narrow && !wide[t];
+    }
+    c.narrow = narrow;
+    const size_t meta = narrow ? narrow_meta : wide_meta;
+    const size_t o_roff = meta, o_keys = o_roff + (size_t)(R + 1) * 8, o_w = o_keys + (size_t)R * 8,
                  o_bytes = o_w + (r.weight ? (size_t)E * 4 : 0);
     c.weighted = r.weight != nullptr;
-    c.staging.reserve(o_bytes + (size_t)r.nbytes + 1);
+    if (!narrow) c.staging.reserve(meta + tail);  // rare: a chunk holding an entry of 256 bytes or more
     char* st = (char*)c.staging.p;
-    std::memcpy(st + o_off, r.entry_off, (size_t)(E + 1) * 8);
-    if (R) {
-        std::memcpy(st + o_roff, r.row_off, (size_t)(R + 1) * 8);
-        std::memcpy(st + o_keys, r.keys, (size_t)R * 8);
+    if (!narrow) {
+        copy_rebased(reinterpret_cast<int64_t*>(st), r.entry_off, E + 1, r.byte_base);
+        if (E) copy_parallel(st + (size_t)(E + 1) * 8, r.vpos, (size_t)E * 4);
     }
-    if (E) std::memcpy(st + o_vpos, r.vpos, (size_t)E * 4);
-    if (E && r.weight) std::memcpy(st + o_w, r.weight, (size_t)E * 4);
-    if (r.nbytes) std::memcpy(st + o_bytes, r.bytes, (size_t)r.nbytes);
+    if (R) {
+        copy_rebased(reinterpret_cast<int64_t*>(st + o_roff), r.row_off, R + 1, r.entry_base);
+        copy_parallel(st + o_keys, r.keys, (size_t)R * 8);
+    }
+    if (E && r.weight) copy_parallel(st + o_w, r.weight, (size_t)E * 4);
+    if (r.nbytes) copy_parallel(st + o_bytes, r.bytes, (size_t)r.nbytes);
+    const double t_stage = ms_since(h3);
+    const auto h4 = HostClock::now();
     auto fit = [](auto& buf, int64_t n) {
         if ((int64_t)buf.size() < std::max<int64_t>(n, 1)) buf.alloc(std::max<int64_t>(n, 1));
     };
@@ -639,6 +808,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     fit(c.d_vpos, E);
     fit(c.err, 1);
     if (r.weight) fit(c.d_w, E);
+    if (narrow) fit(c.d_meta8, 2 * E);
     const bool capped = limit_ > 0;
     if (capped) {
         fit(c.slice, E + 1);
@@ -647,17 +817,31 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
         fit(c.in_flag, E);
         fit(c.truncated, 1);
     }
+    if (narrow || capped) fit(c.scan_tmp, prim::scan_scratch_size(E + 1));
     auto h2d = [&](void* d, size_t off, size_t bytes) {
         if (bytes) JG_HIP(hipMemcpyAsync(d, st + off, bytes, hipMemcpyHostToDevice, s));
     };
     JG_HIP(hipEventRecord(c.t0, s));
-    h2d(c.d_bytes.get(), o_bytes, (size_t)r.nbytes);
-    h2d(c.d_off.get(), o_off, (size_t)(E + 1) * 8);
-    h2d(c.d_vpos.get(), o_vpos, (size_t)E * 4);
-    h2d(c.d_keys.get(), o_keys, (size_t)R * 8);
+    if (narrow) {
+        h2d(c.d_meta8.get(), 0, (size_t)E * 2);
+    } else {
+        h2d(c.d_off.get(), 0, (size_t)(E + 1) * 8);
+        h2d(c.d_vpos.get(), (size_t)(E + 1) * 8, (size_t)E * 4);
+    }
     h2d(c.d_roff.get(), o_roff, (size_t)(R + 1) * 8);
+    h2d(c.d_keys.get(), o_keys, (size_t)R * 8);
     if (r.weight) h2d(c.d_w.get(), o_w, (size_t)E * 4);
+    h2d(c.d_bytes.get(), o_bytes, (size_t)r.nbytes);
+    JG_HIP(hipEventRecord(c.tc, s));
     JG_HIP(hipMemsetAsync(c.err.get(), 0, sizeof(int32_t), s));
+    if (narrow) {  // off = entry_off[0] + exclusive scan of the lengths; value positions widened
+        prim::exclusive_scan_async(c.d_meta8.get(), c.d_off.get(), E, c.scan_tmp.get(), s);
+        if (E) {
+            widen_entries_kernel<<<grid_for(E + 1), kBlock, 0, s>>>(c.d_meta8.get() + E, E, r.entry_off[0] - r.byte_base,
+                                                                  c.d_off.get(), c.d_vpos.get());
+            JG_LAUNCH_CHECK();
+        }
+    }
     const EntryView a{c.d_bytes.get(), c.d_off.get(), c.d_vpos.get(), types_->ids.get(), types_->mult.get(), types_->n};
     if (R) {
         edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, c.d_keys.get(), c.d_roff.get(), R, pbits_, c.keep.get(),
@@ -679,7 +863,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
             slice_flag_kernel<<<grid_for(E), kBlock, 0, s>>>(c.take.get(), E, c.slice.get());
             JG_LAUNCH_CHECK();
         }
-        prim::exclusive_scan(c.slice.get(), c.pre.get(), E + 1, s);
+        prim::exclusive_scan_async(c.slice.get(), c.pre.get(), E + 1, c.scan_tmp.get(), s);
         if (R) {
             slice_cap_kernel<<<(unsigned)std::min<int64_t>(R, 4096), kBlock, 0, s>>>(c.d_roff.get(), R, c.pre.get(),
                                                                                      limit_, c.take.get(),
@@ -693,6 +877,12 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     rows_ += R;
     entries_ += E;
     bytes_ += r.nbytes;
+    h2d_bytes_ += (int64_t)(o_bytes + (size_t)r.nbytes);
+    if (decode_trace())
+        std::fprintf(stderr, "[jg decode] chunk %lld: R %lld E %lld bytes %lld | host ms: total %.2f complete(prev) %.2f "
+                             "pinned reserve %.2f stage %.2f launch %.2f\n",
+                     (long long)chunks_added_, (long long)R, (long long)E, (long long)r.nbytes, ms_since(h0),
+                     t_complete, t_reserve, t_stage, ms_since(h4));
 }
 
 void EdgestoreDecoder::complete(int slot) {
@@ -703,9 +893,11 @@ void EdgestoreDecoder::complete(int slot) {
     int32_t herr = 0;
     JG_HIP(hipMemcpyAsync(&herr, c.err.get(), sizeof(int32_t), hipMemcpyDeviceToHost, s));
     JG_HIP(hipStreamSynchronize(s));
-    float ms = 0;
+    float ms = 0, cms = 0;
     JG_HIP(hipEventElapsedTime(&ms, c.t0, c.t1));
+    JG_HIP(hipEventElapsedTime(&cms, c.t0, c.tc));
     kernel_ms += ms;  // copy + decode of the chunk
+    copy_ms += cms;
     if (herr & kErrBadKey) fail(JG_ERR_ARG, "row key with an unrecognized vertex id type");
     if (herr & kErrPartitioned) fail(JG_ERR_ARG, "partitioned vertex row with no partition bits");
     if (herr & kErrMalformed) fail(JG_ERR_ARG, "malformed edgestore entry on a vertex row");
@@ -713,7 +905,7 @@ void EdgestoreDecoder::complete(int slot) {
     if ((int64_t)idx_.size() < cap) idx_.alloc(cap);
     if ((int64_t)tmp_.size() < cap) tmp_.alloc(cap);
     if (c.weighted && (int64_t)tmpw_.size() < cap) tmpw_.alloc(cap);
-    const int64_t nk = prim::compact_indices(c.keep_v.get(), c.R, idx_.get(), s);
+    const int64_t nk = prim::compact_indices(c.keep_v.get(), c.R, idx_.get(), cpos_, cscan_, s);
     if (nk) {
         gather_kernel<int64_t><<<grid_for(nk), kBlock, 0, s>>>(c.row_vid.get(), idx_.get(), nk, tmp_.get());
         JG_LAUNCH_CHECK();
@@ -729,7 +921,7 @@ void EdgestoreDecoder::complete(int slot) {
         JG_HIP(hipMemcpyAsync(&tr, c.truncated.get(), sizeof tr, hipMemcpyDeviceToHost, s));
         JG_HIP(hipStreamSynchronize(s));
         truncated_rows += (int64_t)tr;
-        const int64_t ki = prim::compact_indices(c.in_flag.get(), c.E, idx_.get(), s);
+        const int64_t ki = prim::compact_indices(c.in_flag.get(), c.E, idx_.get(), cpos_, cscan_, s);
         if (ki) {
             int64_t m2 = mi;
             gather_kernel<int64_t><<<grid_for(ki), kBlock, 0, s>>>(c.esrc.get(), idx_.get(), ki, tmp_.get());
@@ -740,7 +932,7 @@ void EdgestoreDecoder::complete(int slot) {
             grow_append(idst, m2, tmp_.get(), ki, s);
         }
     }
-    const int64_t mk = prim::compact_indices(capped ? c.out_flag.get() : c.take.get(), c.E, idx_.get(), s);
+    const int64_t mk = prim::compact_indices(capped ? c.out_flag.get() : c.take.get(), c.E, idx_.get(), cpos_, cscan_, s);
     if (mk) {
         if (capped) {  // the capped OUT list: the same edges, -1 sources beyond the cap
             capped_gather_kernel<<<grid_for(mk), kBlock, 0, s>>>(c.esrc.get(), c.take.get(), idx_.get(), mk, tmp_.get());
@@ -765,15 +957,52 @@ void EdgestoreDecoder::complete(int slot) {
 
 void EdgestoreDecoder::finish() {
     DeviceGuard dg(device_);
+    const auto h0 = HostClock::now();
     // chunks complete in the order they were added
     complete(next_);
     complete(next_ ^ 1);
+    if (decode_trace()) std::fprintf(stderr, "[jg decode] finish: last chunks completed in %.2f ms\n", ms_since(h0));
+}
+
+void add_in_chunks(EdgestoreDecoder& dec, const EdgestoreRows& r) {
+    check_rows(r);
+    constexpr int64_t kChunkEntries = (int64_t)4 << 20, kChunkBytes = (int64_t)64 << 20;
+    // chunk boundaries are cut at entry offsets: the first and last must lie inside the bytes (each
+    // chunk then checks its own entries)
+    if (r.nentries > 0 && (r.entry_off[0] < 0 || r.entry_off[r.nentries] > r.nbytes))
+        fail(JG_ERR_ARG, "entry offsets run outside the byte array");
+    const bool has_entries = r.nentries > 0;
+    int64_t lo = 0;
+    while (lo < r.nrows || (lo == 0 && r.nrows == 0)) {
+        int64_t hi = lo + 1;
+        const int64_t e0 = r.nrows ? r.row_off[lo] : 0;
+        while (hi < r.nrows && r.row_off[hi + 1] - e0 <= kChunkEntries &&
+               (!has_entries || r.entry_off[r.row_off[hi + 1]] - r.entry_off[e0] <= kChunkBytes))
+            ++hi;
+        if (r.nrows == 0) hi = 0;
+        EdgestoreRows c = r;
+        c.keys = r.keys + lo;
+        c.nrows = hi - lo;
+        c.row_off = r.row_off + lo;
+        c.entry_base = e0;
+        const int64_t e1 = r.nrows ? r.row_off[hi] : 0;
+        c.nentries = e1 - e0;
+        c.entry_off = has_entries ? r.entry_off + e0 : r.entry_off;
+        c.vpos = has_entries ? r.vpos + e0 : r.vpos;
+        c.byte_base = has_entries ? r.entry_off[e0] : 0;
+        c.bytes = has_entries ? r.bytes + c.byte_base : r.bytes;
+        c.nbytes = has_entries ? r.entry_off[e1] - c.byte_base : 0;
+        if (r.weight) c.weight = r.weight + e0;
+        dec.add(c);
+        if (r.nrows == 0) break;
+        lo = hi;
+    }
 }
 
 void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
                         DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms) {
     EdgestoreDecoder dec(r.type_ids, r.type_mult, r.ntypes, r.pbits, device);
-    dec.add(r);
+    add_in_chunks(dec, r);
     dec.finish();
     vid.swap(dec.vid);
     src.swap(dec.src);

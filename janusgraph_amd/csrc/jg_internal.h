@@ -327,6 +327,9 @@ struct EdgestoreRows {
     int32_t ntypes;
     int pbits;                 // cluster.max-partitions = 2^pbits
     const int32_t* weight = nullptr;  // nentries, nullable: the Integer weight property of each entry's edge
+    // A chunk cut out of larger arrays: row_off values count from entry_base, entry_off values from
+    // byte_base (bytes points at the chunk's first byte).
+    int64_t entry_base = 0, byte_base = 0;
 };
 void edgestore_check(const EdgestoreRows& r);
 // Page-locked host memory (async H2D staging).
@@ -361,7 +364,8 @@ struct EdgestoreDecoder {
     int64_t mo = 0, mi = 0, mi2 = 0, truncated_rows = 0;
     int weighted = -1;    // -1 no chunk yet, 0 / 1: the chunks carry no / per-entry weights
     float kernel_ms = 0;  // copy + decode time of every chunk (HIP events)
-    int64_t chunks_added_ = 0, rows_ = 0, entries_ = 0, bytes_ = 0;
+    float copy_ms = 0;    // its host -> device copies alone
+    int64_t chunks_added_ = 0, rows_ = 0, entries_ = 0, bytes_ = 0, h2d_bytes_ = 0;
     int device() const { return device_; }
 
    private:
@@ -372,9 +376,11 @@ struct EdgestoreDecoder {
     hipStream_t streams_[2] = {nullptr, nullptr};
     std::unique_ptr<EdgestoreChunk> chunks_[2];
     std::unique_ptr<TypeTable> types_;
-    DevBuf<int64_t> idx_, tmp_;
+    DevBuf<int64_t> idx_, tmp_, cpos_, cscan_;
     DevBuf<int32_t> tmpw_;
 };
+// Feeds one whole snapshot to the decoder in chunks of whole rows (<= 4 M entries / 64 MB each).
+void add_in_chunks(EdgestoreDecoder& dec, const EdgestoreRows& r);
 // One-shot: vid = ids of the kept rows (row order), src/dst = their OUT edges, on `device`.
 void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid, int64_t& n, DevBuf<int64_t>& src,
                         DevBuf<int64_t>& dst, int64_t& m, float* kernel_ms);

@@ -76,6 +76,11 @@ namespace prim {
 void exclusive_scan(const int32_t* in, int64_t* out, int64_t n, hipStream_t s);
 void exclusive_scan(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
 void exclusive_scan(const uint32_t* in, int64_t* out, int64_t n, hipStream_t s);
+// The same, queued on s without synchronising: scratch holds scan_scratch_size(n) elements and must
+// outlive the stream's work.
+int64_t scan_scratch_size(int64_t n);
+void exclusive_scan_async(const uint8_t* in, int64_t* out, int64_t n, int64_t* scratch, hipStream_t s);
+void exclusive_scan_async(const uint32_t* in, int64_t* out, int64_t n, int64_t* scratch, hipStream_t s);
 
 // Stable LSD radix sort of keys[0..n) on bits [0, bits), carrying vals (nullable).  Sorted data is
 // returned in keys/vals (temporaries are allocated internally).
@@ -84,6 +89,9 @@ void radix_sort(uint64_t* keys, uint32_t* vals, int64_t n, int bits, hipStream_t
 // Count elements of flags[0..n) that are nonzero, and write their indices (stable) into idx_out.
 // Returns the count (synchronises the stream).
 int64_t compact_indices(const uint8_t* flags, int64_t n, int64_t* idx_out, hipStream_t s);
+// The same with reusable scratch (grown on demand, no allocation after that); flags must be 0 or 1.
+int64_t compact_indices(const uint8_t* flags, int64_t n, int64_t* idx_out, DevBuf<int64_t>& pos,
+                        DevBuf<int64_t>& scan, hipStream_t s);
 
 }  // namespace prim
 }  // namespace jg

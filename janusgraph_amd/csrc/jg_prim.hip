@@ -195,7 +195,40 @@ __global__ void u8_to_u32_kernel(const uint8_t* __restrict__ f, uint32_t* __rest
         o[i] = f[i] ? 1u : 0u;
 }
 
+// The same scan without a synchronisation: block sums and offsets of every level live in `scratch`.
+template <typename Tin>
+void exclusive_scan_async_impl(const Tin* in, int64_t* out, int64_t n, int64_t* scratch, hipStream_t s) {
+    if (n <= 0) {
+        scan_single_total_kernel<<<1, 1, 0, s>>>(out, 0);
+        JG_LAUNCH_CHECK();
+        return;
+    }
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    int64_t *sums = scratch, *offs = scratch + nb;
+    scan_reduce_kernel<Tin><<<(unsigned)nb, kBlock, 0, s>>>(in, n, sums);
+    JG_LAUNCH_CHECK();
+    if (nb == 1) {
+        JG_HIP(hipMemsetAsync(offs, 0, sizeof(int64_t), s));
+    } else {
+        exclusive_scan_async_impl<int64_t>(sums, offs, nb, scratch + 2 * nb + 1, s);
+    }
+    scan_apply_kernel<Tin><<<(unsigned)nb, kBlock, 0, s>>>(in, out, n, offs);
+    JG_LAUNCH_CHECK();
+}
+
 }  // namespace
+
+int64_t scan_scratch_size(int64_t n) {
+    if (n <= 0) return 1;
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    return 2 * nb + 1 + (nb > 1 ? scan_scratch_size(nb) : 0);
+}
+void exclusive_scan_async(const uint8_t* in, int64_t* out, int64_t n, int64_t* scratch, hipStream_t s) {
+    exclusive_scan_async_impl(in, out, n, scratch, s);
+}
+void exclusive_scan_async(const uint32_t* in, int64_t* out, int64_t n, int64_t* scratch, hipStream_t s) {
+    exclusive_scan_async_impl(in, out, n, scratch, s);
+}
 
 void exclusive_scan(const int32_t* in, int64_t* out, int64_t n, hipStream_t s) { exclusive_scan_impl(in, out, n, s); }
 void exclusive_scan(const int64_t* in, int64_t* out, int64_t n, hipStream_t s) { exclusive_scan_impl(in, out, n, s); }
@@ -230,6 +263,20 @@ void radix_sort(uint64_t* keys, uint32_t* vals, int64_t n, int bits, hipStream_t
         if (vals) JG_HIP(hipMemcpyAsync(vals, vin, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     }
     JG_HIP(hipStreamSynchronize(s));
+}
+
+int64_t compact_indices(const uint8_t* flags, int64_t n, int64_t* idx_out, DevBuf<int64_t>& pos,
+                        DevBuf<int64_t>& scan, hipStream_t s) {
+    if (n <= 0) return 0;
+    if ((int64_t)pos.size() < n + 1) pos.alloc(n + 1);
+    if ((int64_t)scan.size() < scan_scratch_size(n)) scan.alloc(scan_scratch_size(n));
+    exclusive_scan_async_impl<uint8_t>(flags, pos.get(), n, scan.get(), s);  // flags are 0 / 1
+    flag_scan_kernel<<<grid_for(n), kBlock, 0, s>>>(flags, n, idx_out, pos.get());
+    JG_LAUNCH_CHECK();
+    int64_t total = 0;
+    JG_HIP(hipMemcpyAsync(&total, pos.get() + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    JG_HIP(hipStreamSynchronize(s));
+    return total;
 }
 
 int64_t compact_indices(const uint8_t* flags, int64_t n, int64_t* idx_out, hipStream_t s) {

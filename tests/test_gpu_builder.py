@@ -155,3 +155,39 @@ def test_builder_ids_past_2gib_rmat24(oracle_lib):
     ctx.close()
     np.testing.assert_array_equal(ec, ec2)
     np.testing.assert_array_equal(r, r2)
+
+
+def test_builder_wide_and_narrow_chunks(oracle_lib):
+    """A chunk holding an entry of 256 bytes or more is staged with int64 offsets; the others with
+    1-byte lengths and value positions.  Both decode to the oracle's snapshot."""
+    import janusgraph_amd as jg
+    from oracle import edgecodec as ec
+    from test_slice_cap import Rows
+    rng = np.random.default_rng(8)
+    g = Rows(300)
+    for _ in range(2500):
+        g.edge(int(rng.integers(0, 300)), int(rng.integers(0, 300)))
+    g.rows[g.vid[150]].append(ec.encode_property(ec.schema_id(5, "user_key"), 77, bytes(range(256)) * 2))
+    store = g.store()
+    keys, roff, data, off, vpos, tids, tmult = store
+    assert np.max(np.diff(off)) >= 256
+    ov, os_, ot = oracle_lib.edgestore_snapshot(keys, roff, data, off, vpos, tids, tmult)
+    ds, dd = _dense(ov, os_, ot)
+    n = len(ov)
+    ref, ref_e = oracle_lib.pagerank(n, ds, dd, 0.85, n, 10)
+    ctx = jg.Context((0,))
+    for nchunks in (1, 4):
+        b = ctx.builder()
+        b.set_schema(tids, tmult, 5)
+        for ch in row_chunks(store, np.linspace(0, len(keys), nchunks + 1).astype(int)):
+            b.add_rows(*ch)
+        gg = b.finish(jg.ADJ_IN)
+        b.close()
+        st = ctx.stats()
+        assert st["exchange_ms"] > 0 and st["kernel_ms_total"] >= st["exchange_ms"]
+        assert np.array_equal(gg.vertex_ids(), ov)
+        rank, ecount = gg.pagerank(0.85, n, 10)
+        assert np.max(np.abs(rank - ref) / np.abs(ref)) <= 1e-9
+        np.testing.assert_array_equal(ecount, ref_e)
+        gg.close()
+    ctx.close()
