@@ -254,7 +254,9 @@ def rmat26_both_blocks(jg, ctx, scale, ef):
     g.bfs(srcs, jg.DIR_BOTH, want=False)
     st = ctx.stats()
     ms = {"workload": f"msbfs64_rmat{scale}_ef{ef}", "sources": int(len(srcs)), "ms": round(st["compute_ms"], 3),
-          "levels": st["levels"]}
+          "levels": st["levels"],
+          "gteps": round(len(srcs) * m / (st["compute_ms"] * 1e-3) / 1e9, 1),
+          "gteps_note": "sources x m input edges / time (Graph500 convention, the giant component holds ~all edges)"}
     g.close()
     return cc, ms
 

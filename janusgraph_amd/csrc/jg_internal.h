@@ -438,6 +438,7 @@ struct Tune {
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
+    int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int merge_nt = 0;                 // merge kernel: bit 0 non-temporal band loads, bit 1 non-temporal partial stores

@@ -1064,7 +1064,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             struct St {
                 DevBuf<unsigned long long> F[2], vis;
                 DevBuf<int32_t> depth, changed;
-                DevBuf<unsigned long long> hub;
+                DevBuf<unsigned long long> hub, split;
             };
             std::vector<St> st(g.shards.size());
             for (size_t i = 0; i < g.shards.size(); ++i) {
@@ -1083,6 +1083,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.depth.alloc(std::max<int64_t>(sh.rows * ns, 1));
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
+                if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
@@ -1198,10 +1199,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     op.pos = g.vec_pos(sh, adj_of(sh, c));
                     op.lvl = level + 1;
                     op.full = full;
-                    // no sliced split (split_partial null): the class kernel skips fully visited rows
-                    // (MsBfsOp::active), which whole-entry merge tasks cannot
+                    // Pull levels come after the top-down ones, when most rows still miss sources: the
+                    // sliced split (XCD sub-slices, LDS-resident hot words) folds every entry of the
+                    // split rows, fully visited or not (MsBfsOp::finalize masks with ~visited); the
+                    // light rows' class kernel still skips fully visited rows (MsBfsOp::active).
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                (unsigned long long*)nullptr);
+                                t.split.size() ? t.split.get() : (unsigned long long*)nullptr);
                     if (td_ok) {  // the next level may run top-down: queue this level's frontier
                         build_frontier(t.F[cur ^ 1].get(), td.qc ^ 1);
                         td.qc ^= 1;

@@ -134,21 +134,25 @@ def test_config3_cc_rmat26(rmat26):
     ctx.close()
 
 
-def test_config4_msbfs64_rmat26_8shards(oracle_lib, rmat26):
+def test_config4_msbfs64_rmat26(oracle_lib, rmat26):
+    """8 logical shards (every level pulls through the sharded split) and one shard (top-down levels
+    for small frontiers, split pull levels between them)."""
     import janusgraph_amd as jg
     o = oracle_lib
     r = rmat26
     n = r["n"]
     srcs = pick_sources(r["ptr"], 64, 26)
-    ctx = jg.Context((0,) * 8)
-    g = ctx.build_rmat(26, EF, seed_of(26), flags=jg.ADJ_BOTH)
-    assert g.info()["num_shards"] == 8
-    got = g.bfs(srcs, jg.DIR_BOTH)
-    g.close()
-    ctx.close()
     want = o.msbfs_csr(n, r["ptr"], r["adj"], srcs)
-    for k in range(64):
-        assert np.array_equal(got[k], want[k]), f"source {k} ({srcs[k]}) differs"
-    for k in (0, 31, 63):
-        err, _ = o.bfs_validate(n, r["s"], r["d"], got[k], int(srcs[k]), r["label"])
-        assert err == 0, f"Graph500 validation bits {err} for source {k}"
+    for shards in (8, 1):
+        ctx = jg.Context((0,) * shards)
+        g = ctx.build_rmat(26, EF, seed_of(26), flags=jg.ADJ_BOTH)
+        assert g.info()["num_shards"] == shards
+        got = g.bfs(srcs, jg.DIR_BOTH)
+        g.close()
+        ctx.close()
+        for k in range(64):
+            assert np.array_equal(got[k], want[k]), f"{shards} shards: source {k} ({srcs[k]}) differs"
+        for k in (0, 31, 63):
+            err, _ = o.bfs_validate(n, r["s"], r["d"], got[k], int(srcs[k]), r["label"])
+            assert err == 0, f"{shards} shards: Graph500 validation bits {err} for source {k}"
+        del got
