@@ -458,6 +458,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {
         jg::tune().msbfs_td = value != 0;
+    } else if (k == "cc_uf") {
+        jg::tune().cc_uf = value != 0;
     } else if (k == "msbfs_split") {
         jg::tune().msbfs_split = value != 0;
     } else if (k == "sharded_bfs") {

@@ -169,6 +169,175 @@ __global__ void cc_push_apply_kernel(const int32_t* __restrict__ touched, int64_
     }
 }
 
+// ---- one shard: the fixed point by union-find, the superstep count by BFS ----
+// Synchronous min-label propagation gives vertex v after t supersteps the minimum rank within t hops
+// (a vertex that did not change sends nothing new, and what it sent before already arrived), so v's
+// label is final exactly at t = dist(v, c(v)), c(v) the minimum-rank vertex of its component, and
+// the last change anywhere is at D = max dist(v, c(v)).  The loop then stops one superstep later:
+// iterations = D + 1 when any vertex has an edge (0 otherwise; cc_run's loop, jo_cc_csr), unless that
+// reaches the 99-superstep cap, where the propagation itself runs.  The labels come from a union-find
+// whose roots are each component's minimum-rank vertex (a root is only ever hooked under a vertex of
+// smaller rank), D from a BFS started at every root.
+//
+// Union-find under MI355X's memory model: the hooks are atomicCAS (performed at the memory side, so
+// every XCD sees them); finds read with plain loads that may be stale inside a kernel, which is safe
+// because every vertex's parent chain only ever gains ancestors of strictly smaller rank: a stale
+// read yields an ancestor, a CAS against a stale root fails and returns the current parent.  Path
+// compression writes parents only in kernels of its own (no concurrent hooks), after the boundary.
+__device__ __forceinline__ int32_t uf_find(const int32_t* __restrict__ parent, int32_t x) {
+    for (;;) {
+        const int32_t p = parent[x];
+        if (p == x) return x;
+        x = p;
+    }
+}
+
+__device__ __forceinline__ void uf_link(int32_t* parent, const int32_t* __restrict__ rank, int32_t a, int32_t b) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    while (a != b) {
+        if (rank[a] > rank[b]) {  // hook the root of larger rank (b) under the smaller (a)
+            const int32_t t = a;
+            a = b;
+            b = t;
+        }
+        const int32_t old = atomicCAS(&parent[b], b, a);
+        if (old == b) return;
+        b = uf_find(parent, old);
+        a = uf_find(parent, a);
+    }
+}
+
+__global__ void uf_init_kernel(int32_t* __restrict__ parent, int64_t rows) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        parent[v] = (int32_t)v;
+}
+
+// Afforest's first round: every vertex links to its first k neighbours.
+__global__ void uf_link_first_kernel(int32_t* parent, const int32_t* __restrict__ rank, const int64_t* __restrict__ rp,
+                                     const int32_t* __restrict__ col, int64_t rows, int k) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e0 = rp[v], e1 = rp[v + 1] < rp[v] + k ? rp[v + 1] : rp[v] + k;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int32_t u = col[e];
+            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+        }
+    }
+}
+
+// Vertices outside the sampled giant component link their remaining neighbours (an edge between the
+// giant component and another vertex is linked from the other side).  Rows are degree-sorted: rows
+// below `heavy` (degree >= 64) take a wave each, the others a thread.
+__global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, const int32_t* __restrict__ rank,
+                                                               const int64_t* __restrict__ rp,
+                                                               const int32_t* __restrict__ col, int64_t rows,
+                                                               int64_t heavy, int k, int32_t giant) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
+    for (int64_t v = wave; v < heavy; v += nwaves) {  // wave-uniform
+        if (uf_find(parent, (int32_t)v) == giant) continue;
+        for (int64_t e = rp[v] + k + lane; e < rp[v + 1]; e += kWave) {
+            const int32_t u = col[e];
+            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+        }
+    }
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = heavy + tid; v < rows; v += nt) {
+        if (rp[v + 1] - rp[v] <= k || uf_find(parent, (int32_t)v) == giant) continue;
+        for (int64_t e = rp[v] + k; e < rp[v + 1]; ++e) {
+            const int32_t u = col[e];
+            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+        }
+    }
+}
+
+__global__ void uf_compress_kernel(int32_t* parent, int64_t rows) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        parent[v] = uf_find(parent, (int32_t)v);
+}
+
+__global__ void uf_sample_kernel(const int32_t* __restrict__ parent, int64_t rows, int n, int32_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = parent[(int64_t)(((uint64_t)i * 0x9E3779B97F4A7C15ull) % (uint64_t)rows)];
+}
+
+__global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, unsigned long long* __restrict__ cnt) {
+    unsigned long long c = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        c += rp[v + 1] - rp[v] >= kWave;
+    c = wave_reduce_add(c);
+    if (lane_id() == 0 && c) atomicAdd(cnt, c);
+}
+
+// label[v] = rank of v's root; msg = the final labels of vertices that had an edge (the propagation's
+// last message vector is never read after the fixed point)
+__global__ void uf_labels_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ rank, int64_t rows,
+                                 int32_t* __restrict__ label) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        label[v] = rank[parent[v]];
+}
+
+// Union-find labels and the BFS superstep count on one shard; false (labels untouched) if the count
+// reaches the superstep cap.
+bool cc_union_find(Ctx& ctx, Graph& g, Shard& sh, int* iterations) {
+    hipStream_t s = sh.stream;
+    const int64_t rows = sh.rows;
+    const Csr& c = sh.both;
+    constexpr int kFirst = 2;
+    DevBuf<int32_t> parent(std::max<int64_t>(rows, 1)), sample(1024), label(std::max<int64_t>(rows, 1));
+    DevBuf<unsigned long long> cnt(1);
+    if (rows == 0) {
+        *iterations = 0;
+        return true;
+    }
+    const int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
+    uf_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    JG_LAUNCH_CHECK();
+    uf_link_first_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, c.row_ptr.get(), c.col.get(), rows,
+                                                           kFirst);
+    JG_LAUNCH_CHECK();
+    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    JG_LAUNCH_CHECK();
+    // the most frequent root among 1024 sampled vertices: the giant component's
+    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent.get(), rows, 1024, sample.get());
+    JG_LAUNCH_CHECK();
+    std::vector<int32_t> hs(1024);
+    copy_d2h(hs.data(), sample.get(), hs.size() * sizeof(int32_t), s);
+    std::sort(hs.begin(), hs.end());
+    int32_t giant = hs[0];
+    size_t best = 0;
+    for (size_t i = 0; i < hs.size();) {
+        size_t j = i;
+        while (j < hs.size() && hs[j] == hs[i]) ++j;
+        if (j - i > best) {
+            best = j - i;
+            giant = hs[i];
+        }
+        i = j;
+    }
+    JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned long long), s));
+    heavy_rows_kernel<<<grid_for(rows), kBlock, 0, s>>>(c.row_ptr.get(), rows, cnt.get());
+    JG_LAUNCH_CHECK();
+    unsigned long long heavy = 0;
+    copy_d2h(&heavy, cnt.get(), sizeof heavy, s);
+    uf_link_rest_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, c.row_ptr.get(), c.col.get(), rows,
+                                                          (int64_t)heavy, kFirst, giant);
+    JG_LAUNCH_CHECK();
+    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    JG_LAUNCH_CHECK();
+    const int d = cc_root_eccentricity(ctx, sh, parent.get());
+    const int it = c.nnz > 0 ? d + 1 : 0;
+    if (it > kCcMaxIterations - 1) return false;
+    uf_labels_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, rows, label.get());
+    JG_LAUNCH_CHECK();
+    JG_HIP(hipMemcpyAsync(sh.cc_label.get(), label.get(), rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    JG_HIP(hipStreamSynchronize(s));
+    (void)g;
+    *iterations = it;
+    return true;
+}
+
 void exchange_msg(Graph& g, int which) {
     std::vector<void*> bufs;
     for (auto& sp : g.shards) bufs.push_back(sp->cc_msg[which].get());
@@ -263,7 +432,10 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         pu.touched_off.alloc(r1);
         pu.ctr.alloc(2);
     }
-    while (any && iteration < kCcMaxIterations - 1) {
+    // One shard: the same labels and superstep count from a union-find and one BFS (cc_union_find).
+    bool solved = false;
+    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) solved = cc_union_find(ctx, g, sh0, &iteration);
+    while (!solved && any && iteration < kCcMaxIterations - 1) {
         ++iteration;
         bool pushed = false;
         if (push_ok) {

@@ -392,6 +392,10 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out);
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
+// One shard, BOTH adjacency: the largest hop distance of a vertex from its component's root
+// (parent[v] == v), by a direction-optimising BFS started at every root that has an edge; -1 if no
+// vertex has an edge (jg_traverse.hip).
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* parent);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
                  uint8_t* received_out);
 
@@ -438,6 +442,7 @@ struct Tune {
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
+    int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)

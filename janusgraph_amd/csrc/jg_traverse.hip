@@ -289,6 +289,38 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
     }
 }
 
+// Multi-source start (cc_root_eccentricity): every component root with an edge is a level-0 source.
+__global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restrict__ depth, int64_t rows,
+                                                                const int32_t* __restrict__ parent,
+                                                                const int64_t* __restrict__ deg_rp, int32_t* queue,
+                                                                int64_t* qoff, unsigned long long* packed,
+                                                                uint8_t* __restrict__ seen) {
+    __shared__ StagedAppend sc;
+    staged_init(sc);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t v = x0 + threadIdx.x;
+        bool take = false;
+        int64_t deg = 0;
+        if (v < rows) {
+            deg = deg_rp[v + 1] - deg_rp[v];
+            take = parent[v] == (int32_t)v && deg > 0;
+            depth[v] = take ? 0 : -1;
+            seen[v] = take;
+        }
+        staged_append(take, (int32_t)v, deg, sc, queue, qoff, packed);
+    }
+    staged_flush(sc, queue, qoff, packed);
+}
+
+__global__ void depth_max_kernel(const int32_t* __restrict__ depth, int64_t n, int32_t* __restrict__ out) {
+    int32_t m = -1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = depth[i] > m ? depth[i] : m;
+    m = wave_reduce_max(m);
+    if (lane_id() == 0) atomicMax(out, m);
+}
+
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
 struct MsBfsOp {
     using T = unsigned long long;
@@ -600,7 +632,7 @@ uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ?
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
 // Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out) {
+                 double* edges_out, const int32_t* roots = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr* push = c.push;
@@ -617,9 +649,20 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
     if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
     BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
-    bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
-                                                      degcsr->row_ptr.get(), (long long)degcsr->nnz,
-                                                      sh.bfs_ctr.get(), st, sh.bfs_seen.get());
+    if (roots) {  // every root (parent[v] == v) with an edge starts at depth 0
+        JG_HIP(hipMemsetAsync(sh.bfs_ctr.get(), 0, kBfsRing * sizeof(unsigned long long), s));
+        BfsState s0{};
+        s0.mu = (long long)degcsr->nnz;
+        copy_h2d(st + kBfsRing - 1, &s0, sizeof s0, s);
+        bfs_init_roots_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, roots, degcsr->row_ptr.get(),
+                                                                sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
+                                                                sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
+    } else {
+        bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(),
+                                                          sh.bfs_qoff[0].get(), degcsr->row_ptr.get(),
+                                                          (long long)degcsr->nnz, sh.bfs_ctr.get(), st,
+                                                          sh.bfs_seen.get());
+    }
     JG_LAUNCH_CHECK();
     BfsLevel a{};
     a.push_rp = push ? push->row_ptr.get() : nullptr;
@@ -986,6 +1029,21 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
 }
 
 }  // namespace
+
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* parent) {
+    const int64_t rows = sh.rows;
+    if (rows == 0) return 0;
+    DevBuf<int32_t> depth(rows), dmax(1);
+    const BfsCsrs c{&sh.both, &sh.both};
+    dobfs_single(ctx, sh, c, -1, -1, depth.get(), nullptr, parent);
+    JG_HIP(hipMemsetAsync(dmax.get(), 0xFF, sizeof(int32_t), sh.stream));  // -1
+    depth_max_kernel<<<grid_for(rows), kBlock, 0, sh.stream>>>(depth.get(), rows, dmax.get());
+    JG_LAUNCH_CHECK();
+    int32_t d = -1;
+    copy_d2h(&d, dmax.get(), sizeof d, sh.stream);
+    return d;
+}
+
 
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out) {
     if (nsrc <= 0) fail(JG_ERR_ARG, "nsrc must be positive");

@@ -139,3 +139,34 @@ def test_shortest_distance_negative_and_absent_weights(oracle_lib, rmat12, shard
         np.testing.assert_array_equal(g.shortest_distance(vid[seed], 5), o.shortest_distance(n, s, t, seed, 5, harmless))
         g.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("uf", [1, 0])
+def test_connected_components_union_find_and_propagation(ctx, oracle_lib, uf):
+    """One shard: union-find labels + BFS superstep count (cc_uf=1), or the propagation (cc_uf=0), on
+    a graph with components of every kind, a path at the cap (150 vertices, minimum at one end: Fulgora
+    stops at 99 supersteps unconverged, and the union-find path hands it to the propagation) and
+    without it."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    rng = np.random.default_rng(11)
+    cases = []
+    n = 400
+    s, d = rng.integers(0, n, 300), rng.integers(0, n, 300)
+    s[:5] = d[:5] = 7  # self-loops
+    cases.append((n, s, d))
+    n = 150
+    cases.append((n, np.arange(n - 1), np.arange(1, n)))  # a path past the cap
+    cases.append((60, np.arange(59), np.arange(1, 60)))     # a path below it
+    try:
+        _lib.tune_set("cc_uf", uf)
+        for n, s, d in cases:
+            vid = np.arange(10, 10 + n, dtype=np.int64)
+            g = ctx.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
+            comp, it = g.connected_components()
+            want, want_it = oracle_lib.connected_components(n, s, d, vid)
+            assert it == want_it
+            np.testing.assert_array_equal(comp, want)
+            g.close()
+    finally:
+        _lib.tune_set("cc_uf", 1)
