@@ -244,8 +244,10 @@ def rmat26_both_blocks(jg, ctx, scale, ef):
     cc_ms = st["compute_ms"]
     cc = {"workload": f"cc_rmat{scale}_ef{ef}", "ms": round(cc_ms, 3), "iterations": it,
           "components": int(len(np.unique(comp))), "build_ms": round(build_ms, 1),
-          "gteps_per_iteration": round(2 * m * it / (cc_ms * 1e-3) / 1e9, 2),
-          "note": "push supersteps visit only the senders' edges: per-iteration GTEPS is an equivalent rate"}
+          "equivalent_gteps_per_iteration": round(2 * m * it / (cc_ms * 1e-3) / 1e9, 2),
+          "note": "one shard: union-find labels + BFS superstep count (jg_cc.hip cc_union_find), identical labels "
+                  "and iterations to the label propagation; the per-iteration rate counts 2m entries per superstep "
+                  "of the equivalent propagation"}
     del comp
     rng = np.random.default_rng(7)
     cand = rng.integers(0, n, 4 * 64)

@@ -175,15 +175,17 @@ __global__ void cc_push_apply_kernel(const int32_t* __restrict__ touched, int64_
 // label is final exactly at t = dist(v, c(v)), c(v) the minimum-rank vertex of its component, and
 // the last change anywhere is at D = max dist(v, c(v)).  The loop then stops one superstep later:
 // iterations = D + 1 when any vertex has an edge (0 otherwise; cc_run's loop, jo_cc_csr), unless that
-// reaches the 99-superstep cap, where the propagation itself runs.  The labels come from a union-find
-// whose roots are each component's minimum-rank vertex (a root is only ever hooked under a vertex of
-// smaller rank), D from a BFS started at every root.
+// reaches the 99-superstep cap, where the propagation itself runs (tests/test_cc_iterations.py pins
+// the identity on the oracle).  So: components by union-find, each component's minimum rank, then
+// one BFS started at every component's minimum-rank vertex for D.
 //
-// Union-find under MI355X's memory model: the hooks are atomicCAS (performed at the memory side, so
-// every XCD sees them); finds read with plain loads that may be stale inside a kernel, which is safe
-// because every vertex's parent chain only ever gains ancestors of strictly smaller rank: a stale
-// read yields an ancestor, a CAS against a stale root fails and returns the current parent.  Path
-// compression writes parents only in kernels of its own (no concurrent hooks), after the boundary.
+// The union-find hooks the root of larger index under the smaller (rows are degree-sorted, so hubs
+// become roots at once and every other vertex hooks under them without contention; hooking by rank
+// instead made every link of the first round fight over the giant component's current root: 6.7 ms
+// of CAS retries at RMAT-26).  Hooks are atomicCAS, performed at the memory side, so every XCD sees
+// them; finds use plain loads that may be stale inside a kernel, which is safe because a parent chain
+// only ever gains ancestors of strictly smaller index: a stale read yields an ancestor, a CAS against
+// a stale root fails and returns the current parent.  Path compression runs in kernels of its own.
 __device__ __forceinline__ int32_t uf_find(const int32_t* __restrict__ parent, int32_t x) {
     for (;;) {
         const int32_t p = parent[x];
@@ -192,11 +194,11 @@ __device__ __forceinline__ int32_t uf_find(const int32_t* __restrict__ parent, i
     }
 }
 
-__device__ __forceinline__ void uf_link(int32_t* parent, const int32_t* __restrict__ rank, int32_t a, int32_t b) {
+__device__ __forceinline__ void uf_link(int32_t* parent, int32_t a, int32_t b) {
     a = uf_find(parent, a);
     b = uf_find(parent, b);
     while (a != b) {
-        if (rank[a] > rank[b]) {  // hook the root of larger rank (b) under the smaller (a)
+        if (a > b) {  // hook the root of larger index (b) under the smaller (a)
             const int32_t t = a;
             a = b;
             b = t;
@@ -208,19 +210,21 @@ __device__ __forceinline__ void uf_link(int32_t* parent, const int32_t* __restri
     }
 }
 
-__global__ void uf_init_kernel(int32_t* __restrict__ parent, int64_t rows) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+__global__ void uf_init_kernel(int32_t* __restrict__ parent, int32_t* __restrict__ minr, int64_t rows) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         parent[v] = (int32_t)v;
+        minr[v] = INT_MAX;
+    }
 }
 
 // Afforest's first round: every vertex links to its first k neighbours.
-__global__ void uf_link_first_kernel(int32_t* parent, const int32_t* __restrict__ rank, const int64_t* __restrict__ rp,
-                                     const int32_t* __restrict__ col, int64_t rows, int k) {
+__global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                     int64_t rows, int k) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = rp[v], e1 = rp[v + 1] < rp[v] + k ? rp[v + 1] : rp[v] + k;
         for (int64_t e = e0; e < e1; ++e) {
             const int32_t u = col[e];
-            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+            if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
 }
@@ -228,8 +232,7 @@ __global__ void uf_link_first_kernel(int32_t* parent, const int32_t* __restrict_
 // Vertices outside the sampled giant component link their remaining neighbours (an edge between the
 // giant component and another vertex is linked from the other side).  Rows are degree-sorted: rows
 // below `heavy` (degree >= 64) take a wave each, the others a thread.
-__global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, const int32_t* __restrict__ rank,
-                                                               const int64_t* __restrict__ rp,
+__global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, const int64_t* __restrict__ rp,
                                                                const int32_t* __restrict__ col, int64_t rows,
                                                                int64_t heavy, int k, int32_t giant) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, c
         if (uf_find(parent, (int32_t)v) == giant) continue;
         for (int64_t e = rp[v] + k + lane; e < rp[v + 1]; e += kWave) {
             const int32_t u = col[e];
-            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+            if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, c
         if (rp[v + 1] - rp[v] <= k || uf_find(parent, (int32_t)v) == giant) continue;
         for (int64_t e = rp[v] + k; e < rp[v + 1]; ++e) {
             const int32_t u = col[e];
-            if (u != (int32_t)v) uf_link(parent, rank, (int32_t)v, u);
+            if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
 }
@@ -262,45 +265,80 @@ __global__ void uf_sample_kernel(const int32_t* __restrict__ parent, int64_t row
     if (i < n) out[i] = parent[(int64_t)(((uint64_t)i * 0x9E3779B97F4A7C15ull) % (uint64_t)rows)];
 }
 
-__global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, unsigned long long* __restrict__ cnt) {
-    unsigned long long c = 0;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
-        c += rp[v + 1] - rp[v] >= kWave;
-    c = wave_reduce_add(c);
-    if (lane_id() == 0 && c) atomicAdd(cnt, c);
+// minr[root] = the smallest rank of the root's component: the giant component through a block
+// reduction (one atomic per block), the others with an atomicMin each (small components).
+__global__ __launch_bounds__(kBlock) void uf_minrank_kernel(const int32_t* __restrict__ parent,
+                                                             const int32_t* __restrict__ rank, int64_t rows,
+                                                             int32_t giant, int32_t* __restrict__ minr) {
+    __shared__ int32_t red[kBlock / kWave];
+    int32_t g = INT_MAX;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = parent[v], k = rank[v];
+        if (r == giant) g = k < g ? k : g;
+        else atomicMin(&minr[r], k);
+    }
+    g = wave_reduce_min(g);
+    if (lane_id() == 0) red[wave_id()] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) g = red[w] < g ? red[w] : g;
+        if (g != INT_MAX) atomicMin(&minr[giant], g);
+    }
 }
 
-// label[v] = rank of v's root; msg = the final labels of vertices that had an edge (the propagation's
-// last message vector is never read after the fixed point)
-__global__ void uf_labels_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ rank, int64_t rows,
+// src[v] = v for its component's minimum-rank vertex (the BFS sources), -1 otherwise
+__global__ void uf_sources_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ rank,
+                                  const int32_t* __restrict__ minr, int64_t rows, int32_t* __restrict__ src) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        src[v] = rank[v] == minr[parent[v]] ? (int32_t)v : -1;
+}
+
+// label[v] = its component's minimum rank (in place over the ranks)
+__global__ void uf_labels_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ minr, int64_t rows,
                                  int32_t* __restrict__ label) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
-        label[v] = rank[parent[v]];
+        label[v] = minr[parent[v]];
+}
+
+// the number of rows of degree >= 64 (rows are degree-sorted: a binary search of the row offsets)
+__global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, unsigned long long* __restrict__ out) {
+    int64_t lo = 0, hi = rows;  // first row of degree < 64
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (rp[mid + 1] - rp[mid] >= kWave) lo = mid + 1; else hi = mid;
+    }
+    *out = (unsigned long long)lo;
 }
 
 // Union-find labels and the BFS superstep count on one shard; false (labels untouched) if the count
 // reaches the superstep cap.
-bool cc_union_find(Ctx& ctx, Graph& g, Shard& sh, int* iterations) {
+bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
     constexpr int kFirst = 2;
-    DevBuf<int32_t> parent(std::max<int64_t>(rows, 1)), sample(1024), label(std::max<int64_t>(rows, 1));
-    DevBuf<unsigned long long> cnt(1);
     if (rows == 0) {
         *iterations = 0;
         return true;
     }
-    const int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
-    uf_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    // scratch: the message vectors (re-initialised if the propagation has to run), two rows arrays
+    // kept with the shard
+    int32_t* parent = sh.cc_msg[0].get();
+    int32_t* minr = sh.cc_msg[1].get();
+    for (auto& b : sh.cc_aux)
+        if ((int64_t)b.size() < rows) b.alloc(rows);
+    int32_t* src = sh.cc_aux[0].get();
+    DevBuf<int32_t> sample(1024);
+    DevBuf<unsigned long long> cnt(1);
+    int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
+    uf_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, minr, rows);
     JG_LAUNCH_CHECK();
-    uf_link_first_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, c.row_ptr.get(), c.col.get(), rows,
-                                                           kFirst);
+    uf_link_first_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), rows, kFirst);
     JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rows);
     JG_LAUNCH_CHECK();
     // the most frequent root among 1024 sampled vertices: the giant component's
-    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent.get(), rows, 1024, sample.get());
+    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, rows, 1024, sample.get());
     JG_LAUNCH_CHECK();
     std::vector<int32_t> hs(1024);
     copy_d2h(hs.data(), sample.get(), hs.size() * sizeof(int32_t), s);
@@ -316,24 +354,25 @@ bool cc_union_find(Ctx& ctx, Graph& g, Shard& sh, int* iterations) {
         }
         i = j;
     }
-    JG_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned long long), s));
-    heavy_rows_kernel<<<grid_for(rows), kBlock, 0, s>>>(c.row_ptr.get(), rows, cnt.get());
+    heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), rows, cnt.get());
     JG_LAUNCH_CHECK();
     unsigned long long heavy = 0;
     copy_d2h(&heavy, cnt.get(), sizeof heavy, s);
-    uf_link_rest_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, c.row_ptr.get(), c.col.get(), rows,
-                                                          (int64_t)heavy, kFirst, giant);
+    uf_link_rest_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), rows, (int64_t)heavy,
+                                                          kFirst, giant);
     JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rows);
+    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rows);
     JG_LAUNCH_CHECK();
-    const int d = cc_root_eccentricity(ctx, sh, parent.get());
+    uf_minrank_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rank, rows, giant, minr);
+    JG_LAUNCH_CHECK();
+    uf_sources_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rank, minr, rows, src);
+    JG_LAUNCH_CHECK();
+    const int d = cc_root_eccentricity(ctx, sh, src, sh.cc_aux[1].get());
     const int it = c.nnz > 0 ? d + 1 : 0;
     if (it > kCcMaxIterations - 1) return false;
-    uf_labels_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent.get(), rank, rows, label.get());
+    uf_labels_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, minr, rows, rank);
     JG_LAUNCH_CHECK();
-    JG_HIP(hipMemcpyAsync(sh.cc_label.get(), label.get(), rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     JG_HIP(hipStreamSynchronize(s));
-    (void)g;
     *iterations = it;
     return true;
 }
@@ -434,7 +473,16 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     }
     // One shard: the same labels and superstep count from a union-find and one BFS (cc_union_find).
     bool solved = false;
-    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) solved = cc_union_find(ctx, g, sh0, &iteration);
+    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) {
+        solved = cc_union_find(ctx, sh0, &iteration);
+        if (!solved && sh0.rows) {  // the cap binds: the propagation runs, from fresh message vectors
+            for (auto& m : sh0.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh0.stream));
+            cc_init_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
+                sh0.cc_label.get(), sh0.both.row_ptr.get(), sh0.rows, g.vec_pos(sh0, JG_ADJ_BOTH), sh0.cc_label.get(),
+                sh0.cc_msg[0].get());
+            JG_LAUNCH_CHECK();
+        }
+    }
     while (!solved && any && iteration < kCcMaxIterations - 1) {
         ++iteration;
         bool pushed = false;

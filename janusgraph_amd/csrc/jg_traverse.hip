@@ -1030,14 +1030,14 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
 
 }  // namespace
 
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* parent) {
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* src, int32_t* depth) {
     const int64_t rows = sh.rows;
     if (rows == 0) return 0;
-    DevBuf<int32_t> depth(rows), dmax(1);
+    DevBuf<int32_t> dmax(1);
     const BfsCsrs c{&sh.both, &sh.both};
-    dobfs_single(ctx, sh, c, -1, -1, depth.get(), nullptr, parent);
+    dobfs_single(ctx, sh, c, -1, -1, depth, nullptr, src);
     JG_HIP(hipMemsetAsync(dmax.get(), 0xFF, sizeof(int32_t), sh.stream));  // -1
-    depth_max_kernel<<<grid_for(rows), kBlock, 0, sh.stream>>>(depth.get(), rows, dmax.get());
+    depth_max_kernel<<<grid_for(rows), kBlock, 0, sh.stream>>>(depth, rows, dmax.get());
     JG_LAUNCH_CHECK();
     int32_t d = -1;
     copy_d2h(&d, dmax.get(), sizeof d, sh.stream);
