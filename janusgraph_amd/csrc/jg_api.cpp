@@ -451,9 +451,10 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().slice_lds = value != 0;
     } else if (k == "halo") {
         jg::tune().halo = value != 0;
-    } else if (k == "bfs_alpha" || k == "bfs_beta") {
-        JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta must be in [1, 1e6]");
-        (k == "bfs_alpha" ? jg::tune().bfs_alpha : jg::tune().bfs_beta) = (int)value;
+    } else if (k == "bfs_alpha" || k == "bfs_beta" || k == "dobfs_alpha") {
+        JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta / dobfs_alpha must be in [1, 1e6]");
+        (k == "bfs_alpha" ? jg::tune().bfs_alpha : k == "bfs_beta" ? jg::tune().bfs_beta : jg::tune().dobfs_alpha) =
+            (int)value;
     } else if (k == "cc_push") {
         jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {

@@ -440,6 +440,10 @@ struct Tune {
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
+                                      // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)
+    int dobfs_alpha = 30;             // the same for single-source traversals (tools/bfs_sweep.py, RMAT-20:
+                                      // 0.147 / 0.146 / 0.137 / 0.136 / 0.137 ms at 14 / 20 / 30 / 45 / 70;
+                                      // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers

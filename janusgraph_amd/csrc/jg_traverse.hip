@@ -270,13 +270,16 @@ __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-// depth = -1 except the source; level -1 state: nothing explored, the source is the frontier
+// depth = -1 except the source; level -1 state: nothing explored, the source is the frontier.
+// A vertex with an empty pull row can never be reached: its seen byte starts set, so no bottom-up
+// level looks at it again (its depth stays -1).
 __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64_t source, int32_t* queue,
                                 int64_t* qoff, const int64_t* __restrict__ deg_rp, long long total,
-                                unsigned long long* ctr, BfsState* st, uint8_t* __restrict__ seen) {
+                                unsigned long long* ctr, BfsState* st, uint8_t* __restrict__ seen,
+                                const int64_t* __restrict__ pull_rp) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
         depth[i] = i == source ? 0 : -1;
-        seen[i] = i == source;
+        seen[i] = i == source || (pull_rp && pull_rp[i + 1] == pull_rp[i]);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         queue[0] = (int32_t)source;
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
             deg = deg_rp[v + 1] - deg_rp[v];
             take = parent[v] == (int32_t)v && deg > 0;
             depth[v] = take ? 0 : -1;
-            seen[v] = take;
+            seen[v] = take || deg == 0;  // BOTH: push and pull rows are the same (bfs_init_kernel)
         }
         staged_append(take, (int32_t)v, deg, sc, queue, qoff, packed);
     }
@@ -661,7 +664,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(),
                                                           sh.bfs_qoff[0].get(), degcsr->row_ptr.get(),
                                                           (long long)degcsr->nnz, sh.bfs_ctr.get(), st,
-                                                          sh.bfs_seen.get());
+                                                          sh.bfs_seen.get(), pull ? pull->row_ptr.get() : nullptr);
     }
     JG_LAUNCH_CHECK();
     BfsLevel a{};
@@ -676,7 +679,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.ctr = sh.bfs_ctr.get();
     a.st = st;
     a.max_depth = max_depth;
-    a.alpha = (double)tune().bfs_alpha;
+    a.alpha = (double)(roots ? tune().bfs_alpha : tune().dobfs_alpha);
     a.beta = (double)tune().bfs_beta;
     // a fixed grid, both directions grid-stride: ~sqrt(rows) workgroups (tools/bfs_sweep.py, ms per
     // traversal: RMAT-20 0.164 / 0.141 / 0.140 / 0.157 at 256 / 512 / 1024 / 4096; RMAT-22 0.311 /
