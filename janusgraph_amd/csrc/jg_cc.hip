@@ -77,6 +77,30 @@ __global__ void lex_rank_scatter_kernel(const uint32_t* __restrict__ vals, int64
         rank_of[vals[r]] = (int32_t)r;
 }
 
+__global__ void iota_i64_kernel(int64_t* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = i;
+}
+
+// vor[r] = id of the vertex of rank r (vals: the dense vertex of each rank, after the sorts)
+__global__ void vid_of_rank_kernel(const uint32_t* __restrict__ vals, const int64_t* __restrict__ vid, int64_t n,
+                                   int64_t* __restrict__ vor) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        vor[r] = vid[vals[r]];
+}
+
+__global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ idx, int64_t n,
+                                  int32_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = src[idx[i]];
+}
+
+// comp[dense[l]] = vor[label[l]]: each row's component id, in caller order
+__global__ void cc_output_kernel(const int32_t* __restrict__ label, const int32_t* __restrict__ dense,
+                                 const int64_t* __restrict__ vor, int64_t rows, int64_t* __restrict__ comp) {
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x)
+        comp[dense[l]] = vor[label[l]];
+}
+
 __global__ void cc_init_kernel(const int32_t* __restrict__ lab0, const int64_t* __restrict__ rp, int64_t rows,
                                VecPos pos, int32_t* __restrict__ label, int32_t* __restrict__ msg) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x) {
@@ -390,23 +414,30 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
     const int64_t n = g.n;
-    for (int64_t d = 0; d < n; ++d)
-        if (g.vid_of(d) < 0) fail(JG_ERR_UNSUPPORTED, "connected components need non-negative vertex ids");
-    // String-order rank of every vertex id (on the first shard's device)
-    std::vector<int32_t> rank_of(n);
-    std::vector<int64_t> vid_of_rank(n);
+    for (int64_t d = 0; d < (int64_t)g.vid.size(); ++d)
+        if (g.vid[d] < 0) fail(JG_ERR_UNSUPPORTED, "connected components need non-negative vertex ids");
+    // String-order rank of every vertex id, on the first shard's device.  One shard keeps everything
+    // there (rank of each vertex, vertex id of each rank, the rows' initial labels and the result in
+    // caller order); sharded graphs take host copies of the two maps.
+    Shard& shr = *g.shards[0];
+    const bool dev_maps = g.shards.size() == 1 && shr.rows == n && shr.dense_rows.size() >= (size_t)n;
+    std::vector<int32_t> rank_of(dev_maps ? 0 : n);
+    std::vector<int64_t> vid_of_rank(dev_maps ? 0 : n);
+    DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
+    DevBuf<int64_t> vor(std::max<int64_t>(n, 1));  // vertex id of each rank
     {
-        Shard& sh = *g.shards[0];
-        DeviceGuard dg(sh.device);
-        hipStream_t s = sh.stream;
-        std::vector<int64_t> hv(n);
-        for (int64_t d = 0; d < n; ++d) hv[d] = g.vid_of(d);
+        DeviceGuard dg(shr.device);
+        hipStream_t s = shr.stream;
         DevBuf<int64_t> vid(std::max<int64_t>(n, 1));
         DevBuf<uint64_t> keys(std::max<int64_t>(n, 1));
         DevBuf<uint32_t> vals(std::max<int64_t>(n, 1));
-        DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
         if (n > 0) {
-            copy_h2d(vid.get(), hv.data(), n * sizeof(int64_t), s);
+            if (g.vid.empty()) {
+                iota_i64_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n);
+                JG_LAUNCH_CHECK();
+            } else {
+                copy_h2d(vid.get(), g.vid.data(), n * sizeof(int64_t), s);
+            }
             lex_digits_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n, keys.get(), vals.get());
             JG_LAUNCH_CHECK();
             prim::radix_sort(keys.get(), vals.get(), n, 5, s);
@@ -415,9 +446,13 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             prim::radix_sort(keys.get(), vals.get(), n, 64, s);
             lex_rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), n, rk.get());
             JG_LAUNCH_CHECK();
-            copy_d2h(rank_of.data(), rk.get(), n * sizeof(int32_t), s);
+            vid_of_rank_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), vid.get(), n, vor.get());
+            JG_LAUNCH_CHECK();
+            if (!dev_maps) {
+                copy_d2h(rank_of.data(), rk.get(), n * sizeof(int32_t), s);
+                copy_d2h(vid_of_rank.data(), vor.get(), n * sizeof(int64_t), s);
+            }
         }
-        for (int64_t d = 0; d < n; ++d) vid_of_rank[rank_of[d]] = hv[d];
     }
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
@@ -431,11 +466,17 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
         sh.cc_split_partial.alloc(sh.plan_both.split_partial_len());
         sh.cc_changed.alloc(1);
-        std::vector<int32_t> lab0(sh.rows);
-        for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
         DevBuf<int32_t> dlab0(std::max<int64_t>(sh.rows, 1));
         if (sh.rows) {
-            copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
+            if (dev_maps) {  // the rows' ranks, gathered on the device
+                gather_i32_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(rk.get(), sh.dense_rows.get(), sh.rows,
+                                                                               dlab0.get());
+                JG_LAUNCH_CHECK();
+            } else {
+                std::vector<int32_t> lab0(sh.rows);
+                for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
+                copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
+            }
             cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
                                                                         g.vec_pos(sh, JG_ADJ_BOTH), sh.cc_label.get(),
                                                                         sh.cc_msg[0].get());
@@ -564,7 +605,15 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     ctx.last.edges_traversed = nnz * iteration;
     ctx.last.algorithmic_bytes = (8.0 * nnz + 16.0 * (double)n) * iteration;  // 16m + 16n per superstep
     if (iterations_out) *iterations_out = iteration;
-    if (comp_out) {
+    if (comp_out && dev_maps && n > 0) {  // comp[dense of row l] = id of rank label[l], on the device
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh.device);
+        DevBuf<int64_t> out(n);
+        cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(sh.cc_label.get(), sh.dense_rows.get(), vor.get(), n,
+                                                                out.get());
+        JG_LAUNCH_CHECK();
+        copy_d2h(comp_out, out.get(), n * sizeof(int64_t), sh.stream);
+    } else if (comp_out) {
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
             DeviceGuard dg(sh.device);

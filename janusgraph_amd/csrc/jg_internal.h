@@ -186,6 +186,7 @@ struct Shard {
     Halo halo_in, halo_both;      // sharded graphs: compact vectors of the IN / BOTH pull adjacencies
     DevBuf<int32_t> out_degree;   // [rows] out-degree of owned vertices (PageRank edgeCount)
     std::vector<int32_t> dense_of_local;  // host: caller's dense index of each owned row
+    DevBuf<int32_t> dense_rows;           // the same on the device (jg_scatter.h)
 
     // program state (allocated on demand)
     DevBuf<double> pr_contrib[2];  // [P*S] full-length, ping-pong
@@ -222,7 +223,7 @@ struct Graph {
     std::vector<int64_t> sorted_vid;    // host: caller vids sorted (for vid -> dense lookups)
     std::vector<int64_t> sorted_dense;  // dense index of sorted_vid[i]
     std::vector<int64_t> vid;           // host: vid[dense] (empty for RMAT graphs: vid == dense)
-    std::vector<int64_t> padded_of_dense;  // host: global padded id of each caller vertex
+    std::vector<int32_t> padded_of_dense;  // host: global padded id of each caller vertex (P*S < 2^31)
     jg_graph_info info{};
     bool has_weights = false;
     // PageRank session

@@ -13,6 +13,7 @@
 // (allgather or halo exchange, RCCL) refreshes every shard's copy.
 // Algorithmic bytes per superstep: 12*m + 32*n.
 #include "jg_pull.h"
+#include "jg_scatter.h"
 
 namespace jg {
 
@@ -155,16 +156,8 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out) {
         DeviceGuard dg(sh.device);
         JG_HIP(hipStreamSynchronize(sh.stream));
         if (sh.rows == 0) continue;
-        if (rank_out) {
-            std::vector<double> h(sh.rows);
-            copy_d2h(h.data(), sh.pr_rank.get(), sh.rows * sizeof(double), sh.stream);
-            for (int64_t l = 0; l < sh.rows; ++l) rank_out[sh.dense_of_local[l]] = h[l];
-        }
-        if (edge_count_out) {
-            std::vector<int32_t> h(sh.rows);
-            copy_d2h(h.data(), sh.out_degree.get(), sh.rows * sizeof(int32_t), sh.stream);
-            for (int64_t l = 0; l < sh.rows; ++l) edge_count_out[sh.dense_of_local[l]] = (double)h[l];
-        }
+        if (rank_out) rows_to_dense(g, sh, sh.pr_rank.get(), rank_out);
+        if (edge_count_out) rows_to_dense(g, sh, sh.out_degree.get(), edge_count_out);  // int32 -> double
     }
     prof_collect(*g.ctx, g);
 }

@@ -25,6 +25,7 @@
 
 #include "jg_frontier.h"
 #include "jg_pull.h"
+#include "jg_scatter.h"
 
 namespace jg {
 
@@ -1071,15 +1072,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.levels = levels;
         ctx.last.supersteps = levels;
         ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
-        if (depth_out) {
-            for (auto& sp : g.shards) {
-                Shard& sh = *sp;
-                DeviceGuard dg(sh.device);
-                std::vector<int32_t> h(sh.rows);
-                if (sh.rows) copy_d2h(h.data(), sh.bfs_depth.get(), sh.rows * sizeof(int32_t), sh.stream);
-                for (int64_t v = 0; v < sh.rows; ++v) depth_out[sh.dense_of_local[v]] = h[v];
-            }
-        }
+        if (depth_out)
+            for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.get(), depth_out);
         prof_collect(ctx, g);
     } else if (single) {
         Shard& sh = sh0;
@@ -1109,11 +1103,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.edges_traversed = direction == JG_DIR_BOTH ? edges / 2 : edges;
         const Csr* degcsr = c.push ? c.push : c.pull;
         ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
-        if (depth_out) {
-            std::vector<int32_t> h(sh.rows);
-            if (sh.rows) copy_d2h(h.data(), depth.get(), sh.rows * sizeof(int32_t), sh.stream);
-            for (int64_t v = 0; v < sh.rows; ++v) depth_out[sh.dense_of_local[v]] = h[v];
-        }
+        if (depth_out) rows_to_dense(g, sh, depth.get(), depth_out);
         prof_collect(ctx, g);
     } else {
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
@@ -1296,18 +1286,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventElapsedTime(&ms, t0, t1));
             total_ms += ms;
             max_levels = std::max(max_levels, level);
-            if (depth_out) {
-                for (size_t i = 0; i < g.shards.size(); ++i) {
-                    Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
-                    std::vector<int32_t> h(sh.rows * ns);
-                    if (!h.empty())
-                        copy_d2h(h.data(), st[i].depth.get(), h.size() * sizeof(int32_t), sh.stream);
+            if (depth_out)
+                for (size_t i = 0; i < g.shards.size(); ++i)
                     for (int s = 0; s < ns; ++s)
-                        for (int64_t l = 0; l < sh.rows; ++l)
-                            depth_out[(int64_t)(b0 + s) * g.n + sh.dense_of_local[l]] = h[(size_t)(s * sh.rows + l)];
-                }
-            }
+                        rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
+                                      depth_out + (int64_t)(b0 + s) * g.n);
         }
         ctx.last.compute_ms = total_ms;
         ctx.last.levels = max_levels;
@@ -1451,9 +1434,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         int32_t e = 0;
         copy_d2h(&e, st[i].err.get(), sizeof e, sh.stream);
         missing |= e;
-        std::vector<long long> h((size_t)sh.rows);
-        if (sh.rows) copy_d2h(h.data(), st[i].dist.get(), sh.rows * sizeof(long long), sh.stream);
-        for (int64_t l = 0; l < sh.rows; ++l) dist_out[sh.dense_of_local[l]] = h[l];  // LLONG_MIN: absent
+        rows_to_dense(g, sh, st[i].dist.get(), reinterpret_cast<long long*>(dist_out));  // LLONG_MIN: absent
     }
     if (allreduce_or(g, missing)) fail(JG_ERR_ARG, kMissingWeight);
     ctx.last.compute_ms = ms;
