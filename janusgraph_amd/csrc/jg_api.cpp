@@ -438,9 +438,6 @@ int jg_tune_set(const char* key, int64_t value) {
             while ((1 << b) < value) ++b;
             jg::tune().band_bits[i] = b;
         }
-    } else if (k == "merge_nt") {
-        JG_ARG(value >= 0 && value <= 3, "merge_nt must be in [0, 3]");
-        jg::tune().merge_nt = (int)value;
     } else if (k == "pull_split") {
         jg::tune().pull_split = value != 0;
     } else if (k == "pull_short") {
@@ -476,6 +473,18 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().pr_rank_last = value != 0;
     } else if (k == "pr_skip_empty") {
         jg::tune().pr_skip_empty = value != 0;
+    } else if (k.size() == 12 && k.compare(0, 11, "merge_stage") == 0 && k[11] >= '0' && k[11] <= '3') {
+        JG_ARG(value == -1 || value == 0 || value == 64 || value == 128 || value == 256 || value == 512,
+               "merge_stage<i> must be -1 (automatic), 0, 64, 128, 256 or 512");
+        jg::tune().merge_stage[k[11] - '0'] = (int)value;
+    } else if (k == "merge_pack") {
+        JG_ARG(value == 0 || value == 1 || value == 24, "merge_pack must be 0 (32 bits), 1 (automatic) or 24 (at least 24)");
+        jg::tune().merge_pack = (int)value;
+    } else if (k == "light_runs") {
+        jg::tune().light_runs = value != 0;
+    } else if (k == "merge_diag") {
+        JG_ARG(value >= 0 && value <= 3, "merge_diag must be in [0, 3]");
+        jg::tune().merge_diag = (int)value;
     } else if (k == "merge_temporal") {
         JG_ARG(value >= 0 && value <= 2, "merge_temporal must be 0, 1 (automatic) or 2");
         jg::tune().merge_temporal = (int)value;

@@ -369,6 +369,7 @@ __global__ void hub_flag_kernel(const int64_t* __restrict__ rp, int64_t rows, ui
 
 // degree thresholds of the lane classes 1..6 (class 7 takes the rest, class 8 the empty suffix)
 __constant__ int64_t c_class_thr[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 1, 0};
+constexpr int64_t c_class_thr_host[kNumClasses] = {kHubDegree, 256, 128, 64, 32, 16, 8, 1, 0};
 
 // first_below[c] = first row with degree < c_class_thr[c] (c = 1..6);
 // first_below[kZeroClass] = 1 + last row with any entry (rows after it are all empty);
@@ -400,6 +401,24 @@ __global__ void class_bound_kernel(const int64_t* __restrict__ rp, int64_t rows,
             const unsigned long long v = wave_reduce_min(in && d < bt.thr[i] ? (unsigned long long)l : none);
             if (lane_id() == 0 && v != none && v < __atomic_load_n(&band_below[i], __ATOMIC_RELAXED))
                 atomicMin(&band_below[i], v);
+        }
+    }
+}
+
+// Degree runs of rows [lo, hi): st[0] = 1 if a row's degree is 0, above kRunMax or above its
+// predecessor's; st[1 + d] = first row of degree d (d = 1..kRunMax), st[9 + d] = its row_ptr.
+__global__ void degree_run_kernel(const int64_t* __restrict__ rp, int64_t lo, int64_t hi, int64_t* __restrict__ st) {
+    for (int64_t l = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < hi; l += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = rp[l], d = rp[l + 1] - j;
+        if (d < 1 || d > kRunMax) {
+            st[0] = 1;
+            continue;
+        }
+        const int64_t dp = l > lo ? j - rp[l - 1] : kRunMax + 1;
+        if (d > dp) st[0] = 1;
+        else if (d < dp) {  // a run starts here (one row per degree when the order holds)
+            st[1 + d] = l;
+            st[9 + d] = j;
         }
     }
 }
@@ -616,9 +635,45 @@ __global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64
     }
 }
 
+// Lane chunk x of a band (entries [8x, 8x + 8) of its col): sub-slice-local indices packed in W bits
+// each, bit stream over W / 4 dwords, dwords 0..3 to pa[x], the rest to pb (SliceBand::pack_a/_b).
+template <int W>
+__global__ void band_pack_kernel(const int32_t* __restrict__ col, int64_t chunks, int gshift, uint4* __restrict__ pa,
+                                 uint32_t* __restrict__ pb) {
+    constexpr int D = W / 4, DB = D - 4;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < chunks; x += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t d[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) d[i] = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t c = (uint32_t)col[8 * x + u];
+            const uint64_t loc = (uint64_t)(((c >> gshift) << 4) | (c & 15u));
+            const int o = W * u, i = o >> 5, sh = o & 31;
+            d[i] |= (uint32_t)(loc << sh);
+            if (sh + W > 32) d[i + 1] |= (uint32_t)(loc >> (32 - sh));
+        }
+        pa[x] = make_uint4(d[0], d[1], d[2], d[3]);
+#pragma unroll
+        for (int i = 0; i < DB; ++i) pb[x * DB + i] = d[4 + i];
+    }
+}
+
+// Bits of the largest sub-slice-local index of a vector of col_space entries in 2^bits sub-slices:
+// the packed width 20, 24 or 32 (Tune::merge_pack = 0: always 32, 24: at least 24).
+static int band_width(int64_t col_space, int bits) {
+    const uint64_t cmax = (uint64_t)std::max<int64_t>(col_space - 1, 0);
+    const uint64_t loc = ((cmax >> (4 + bits)) << 4) | 15u;
+    int need = 1;
+    while (need < 64 && (loc >> need) != 0) ++need;
+    if (!tune().merge_pack) return 32;
+    if (tune().merge_pack == 24) need = std::max(need, 21);  // test knob: at least 24 bits
+    return need <= 20 ? 20 : need <= 24 ? 24 : 32;
+}
+
 // One band: sub-slice-major sub-CSRs of rows [R0, R1), every sub-slice's start aligned to a merge
 // task (a task never spans two sub-slices and its col loads are 16-byte aligned).
-static void build_band(Shard& sh, const Csr& csr, SliceBand& bd) {
+static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_space) {
     hipStream_t s = sh.stream;
     const int64_t R0 = bd.row_begin, NR = bd.rows();
     const int S = 1 << bd.bits;
@@ -689,7 +744,24 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd) {
                                                                bd.heads.get());
         JG_LAUNCH_CHECK();
     }
+    // the streamed form: packed sub-slice-local indices (the col copy is not kept)
+    bd.width = band_width(col_space, bd.bits);
+    const int64_t chunks = (at + kMergeTask) / 8;
+    const int DB = bd.width / 4 - 4;
+    bd.pack_a.alloc(std::max<int64_t>(chunks, 1));
+    bd.pack_b.alloc(std::max<int64_t>(chunks * DB, 1));
+    if (chunks > 0) {
+        const int gshift = 4 + bd.bits;
+        if (bd.width == 20)
+            band_pack_kernel<20><<<grid_for(chunks), kBlock, 0, s>>>(bd.col.get(), chunks, gshift, bd.pack_a.get(), bd.pack_b.get());
+        else if (bd.width == 24)
+            band_pack_kernel<24><<<grid_for(chunks), kBlock, 0, s>>>(bd.col.get(), chunks, gshift, bd.pack_a.get(), bd.pack_b.get());
+        else
+            band_pack_kernel<32><<<grid_for(chunks), kBlock, 0, s>>>(bd.col.get(), chunks, gshift, bd.pack_a.get(), bd.pack_b.get());
+        JG_LAUNCH_CHECK();
+    }
     JG_HIP(hipStreamSynchronize(s));
+    bd.col.reset();
 }
 
 // Sub-slices of an automatic band (band<i>_bit = 0, the default for the hub band): the LDS-resident
@@ -812,7 +884,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     {
         int64_t part = 0;
         for (auto& bd : plan.bands) {
-            build_band(sh, csr, *bd);
+            build_band(sh, csr, *bd, col_space);
             bd->part_off = part;
             bd->carry_off = part + bd->subrows;
             part += bd->subrows + bd->tasks;
@@ -822,6 +894,35 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     // any hub beyond the prefix keeps its chunks, so chunks stay in the light table too)
     make_classes(plan.split_rows, plan.split_rows > 0 ? plan.num_chunks : plan.num_chunks, plan.light_row_begin,
                  plan.light_row_end, plan.light_block_begin);
+    // degree runs of the 1-lane light rows (their class starts at the first row below 8 entries)
+    plan.runs = false;
+    {
+        const int64_t lo = plan.light_row_begin[kZeroClass - 1], hi = plan.light_row_end[kZeroClass - 1];
+        if (tune().light_runs && hi > lo && c_class_thr_host[kZeroClass - 2] == kRunMax + 1) {
+            int64_t st[17];
+            for (int i = 0; i < 17; ++i) st[i] = -1;
+            st[0] = 0;
+            DevBuf<int64_t> d_st(17);
+            copy_h2d(d_st.get(), st, sizeof st, s);
+            degree_run_kernel<<<grid_for(hi - lo), kBlock, 0, s>>>(csr.row_ptr.get(), lo, hi, d_st.get());
+            JG_LAUNCH_CHECK();
+            copy_d2h(st, d_st.get(), sizeof st, s);
+            if (st[0] == 0) {
+                // absent degrees get an empty run at the start of the next smaller present one
+                int64_t next = hi, next_ptr = -1;
+                plan.run_begin[0] = hi;
+                for (int d = 1; d <= kRunMax; ++d) {
+                    if (st[1 + d] >= 0) {
+                        next = st[1 + d];
+                        next_ptr = st[9 + d];
+                    }
+                    plan.run_begin[d] = next;
+                    plan.run_ptr[d] = st[1 + d] >= 0 ? st[9 + d] : next_ptr;
+                }
+                plan.runs = plan.run_begin[kRunMax] == lo;
+            }
+        }
+    }
     if (debug_plan()) {
         std::vector<int64_t> rp(rows + 1);
         copy_d2h(rp.data(), csr.row_ptr.get(), (rows + 1) * sizeof(int64_t), s);

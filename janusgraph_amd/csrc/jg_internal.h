@@ -43,6 +43,7 @@ struct Csr {
 constexpr int kNumClasses = 9;  // 0: hub (chunked), 1..7: lanes per row 64,32,16,8,4,2,1, 8: empty rows
 constexpr int kZeroClass = kNumClasses - 1;
 constexpr int64_t kHubDegree = 8192;
+constexpr int kRunMax = 7;  // light rows of degree 1..kRunMax may be addressed by degree run (PullPlan::runs)
 constexpr int64_t kHubChunk = 4096;
 
 // One degree band of the sliced split: rows [row_begin, row_end), whose entries are dealt to
@@ -57,7 +58,15 @@ struct SliceBand {
     int64_t subrows = 0;    // non-empty sub-rows
     int64_t part_off = 0;   // offset of the band's partials in the program's fold buffer
     int64_t carry_off = 0;  // offset of the band's task carries
-    DevBuf<int32_t> col;        // entries, sub-slice-major (+ one task of padding)
+    DevBuf<int32_t> col;        // entries, sub-slice-major (+ one task of padding); freed once packed
+    // The entries as the merge kernel streams them: lane chunk x = entries [8x, 8x + 8) of `col`, each
+    // as its sub-slice-local index loc = (c >> (4 + bits)) << 4 | (c & 15) (the sub-slice's hash bits
+    // of the line dropped; SliceBand::decode restores them), packed in `width` bits (20, 24 or 32:
+    // the fewest that hold the vector's largest loc) as a bit stream over width / 4 dwords, planar:
+    // dwords 0..3 in pack_a[x], the rest in pack_b[x * (width / 4 - 4) ...].  RMAT-26 band 0: 20 bits.
+    int width = 32;
+    DevBuf<uint4> pack_a;
+    DevBuf<uint32_t> pack_b;
     DevBuf<int64_t> sub_begin;  // [S] first entry of sub-slice h in col (aligned)
     DevBuf<int64_t> sub_end;    // [S] one past its last entry
     DevBuf<int64_t> sub_base;   // [S+1] first task of sub-slice h
@@ -101,6 +110,13 @@ struct PullPlan {
     bool temporal = false;  // the vector is large enough for the temporal merge schedule (tune merge_temporal = 1)
     int seg_tbits = 31;   // segmented compact vector (sharded, halo): nseg segments of stride 2^seg_tbits
     int nseg = 1;         // one segment: the hot prefix is [0, hot)
+    // Degree runs of the light rows: when rows [run_begin[kRunMax], zero rows) hold degrees
+    // kRunMax, ..., 1 in non-increasing order (a degree-sorted shard), rows of degree d are
+    // [run_begin[d], run_begin[d-1]) (run_begin[0] = first empty row) and row r of that run starts at
+    // run_ptr[d] + (r - run_begin[d]) * d: the 1-lane class needs no row_ptr load.
+    bool runs = false;
+    int64_t run_begin[kRunMax + 1] = {};
+    int64_t run_ptr[kRunMax + 1] = {};
 };
 constexpr int kXcds = 8;
 // Sub-slices of the column space: the 128-byte lines of an fp64 vector (16 elements) are hashed to
@@ -452,12 +468,19 @@ struct Tune {
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
-    int merge_nt = 0;                 // merge kernel: bit 0 non-temporal band loads, bit 1 non-temporal partial stores
     int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
     int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power
                                       // steps only (their rank and contribution are constant after that)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
+    int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
+                                          // stores, -1 = automatic from the band's heads per task)
+    int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
+                                      // (0: 32 bits, 24: at least 24; tests)
+    int light_runs = 1;               // build time: light rows of degree 1..7 addressed by degree run (no row_ptr load)
+    int merge_diag = 0;               // diagnostic timing of the merge kernel (wrong results for 1 and 3):
+                                      // 1 staging only, 3 no partial stores (round 2: a second col-sized
+                                      // stream cost +28% / +10% in the band 0 / 1 merges at RMAT-26)
 };
 Tune& tune();
 int device_cu_count();  // compute units of the current device

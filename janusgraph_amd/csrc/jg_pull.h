@@ -35,6 +35,9 @@ struct PullArgs {
     int64_t block_offset;  // diagnostic split launches (JG_PULL_SPLIT=1): first block of this launch
     int64_t skip_rows;     // rows [0, skip_rows) are folded by the XCD split: their hub chunks are skipped
     int short_rows;        // 1-lane rows of <= 8 entries use fold_short (Tune::pull_short)
+    int runs;              // 1-lane rows from run_begin[kRunMax] on are addressed by degree run (PullPlan::runs)
+    int64_t run_begin[kRunMax + 1];
+    int64_t run_ptr[kRunMax + 1];
 };
 
 inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = false) {
@@ -55,6 +58,11 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = f
     a.block_offset = 0;
     a.skip_rows = light ? p.split_rows : 0;
     a.short_rows = tune().pull_short;
+    a.runs = p.runs && a.short_rows;
+    for (int d = 0; d <= kRunMax; ++d) {
+        a.run_begin[d] = p.run_begin[d];
+        a.run_ptr[d] = p.run_ptr[d];
+    }
     return a;
 }
 
@@ -169,6 +177,19 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
     const bool valid = row < a.class_row_end[c];
     T acc = op.identity();
     bool hub = false;
+    if (L == 1 && valid && a.runs && row >= a.run_begin[kRunMax]) {
+        // degree run: rows of degree d are consecutive, so the entries follow from the row number
+        int64_t d = kRunMax, j0 = a.run_ptr[kRunMax] + (row - a.run_begin[kRunMax]) * kRunMax;
+#pragma unroll
+        for (int k = kRunMax - 1; k >= 1; --k)
+            if (row >= a.run_begin[k]) {
+                d = k;
+                j0 = a.run_ptr[k] + (row - a.run_begin[k]) * k;
+            }
+        if (op.active(row)) acc = fold_short<Op, NT>(op, gather, a.col, j0, j0 + d);
+        op.finalize(row, acc);
+        return;
+    }
     if (valid) {
         const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
         hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
@@ -301,7 +322,8 @@ constexpr int kMergeEpl = kMergeTask / kWave;          // entries per lane
 constexpr int kMergeLdsBytes = 160 * 1024;
 
 struct MergeArgs {
-    const int32_t* __restrict__ col;        // band col
+    const uint4* __restrict__ pack_a;       // band entries, packed (SliceBand::pack_a/_b)
+    const uint32_t* __restrict__ pack_b;
     const uint8_t* __restrict__ heads;      // [tasks][64]
     const int32_t* __restrict__ meta;       // [tasks][2]
     const int64_t* __restrict__ sub_begin;  // [S]
@@ -309,6 +331,8 @@ struct MergeArgs {
     const int64_t* __restrict__ sub_base;   // [S+1]
     int64_t tasks;
     int bits;
+    int stage;         // LDS staging slots per wave for a task's partials (0: direct stores)
+    int diag;          // Tune::merge_diag (diagnostic timing variants; 0 in production)
 };
 
 // The hot entries of a gathered vector: the first `hs` entries of each of its `nseg` segments
@@ -320,42 +344,60 @@ struct HotSegs {
     int nseg = 1;
 };
 
-// Gathers of sub-slice h of a 2^bits band: hot ids come from the LDS image of the sub-slice's lines
-// in the hot entries (line group c >> (4 + bits) of a segment holds one line of h; segment s's group
-// j sits at LDS line s * hg + j), the rest from global memory.
+// Gathers of sub-slice h of a 2^bits band from the entries' sub-slice-local indices
+// (SliceBand::pack_a/_b): loc = g << 4 | lane16, g = the line group (c >> (4 + bits)).  Hot ids come
+// from the LDS image of the sub-slice's lines in the hot entries (segment s = g >> (tbits - gshift),
+// its group j = the rest; hot when j < hg, at LDS line s * hg + j), the rest from global memory at
+// the column restored from loc: line = g << bits | (h ^ the hash bits of the group's first line).
 template <class Op>
-struct SliceLdsGather {
+struct SliceGather {
     using T = typename Op::T;
     const Op& op;
     lds_ptr<const T> lds;
-    uint32_t hs, tmask, hg;
-    int tbits, gshift;  // gshift = 4 + bits
+    uint32_t hg;        // hot line groups per segment
+    int sb;             // tbits - gshift: group bits inside a segment
+    int bits;
+    uint32_t hmask, h;  // 2^bits - 1, the sub-slice
     uint32_t idcell;    // the identity cell just past the staged lines
-    __device__ __forceinline__ bool is_hot(int32_t c) const { return ((uint32_t)c & tmask) < hs; }
-    // Cold lanes read the identity cell: no select, so the compiler cannot turn the read into a branch.
-    __device__ __forceinline__ T hot(int32_t c) const {
-        const uint32_t u = (uint32_t)c, off = u & tmask;
-        const uint32_t grp = (u >> tbits) * hg + (off >> gshift);
-        return lds[off < hs ? ((grp << 4) | (u & 15u)) : idcell];
+    __device__ __forceinline__ bool is_hot(uint32_t loc) const { return ((loc >> 4) & ((1u << sb) - 1u)) < hg; }
+    // Cold and invalid lanes read the identity cell: no select, so the read cannot become a branch.
+    __device__ __forceinline__ T hot(uint32_t loc, bool valid) const {
+        const uint32_t g = loc >> 4, j = g & ((1u << sb) - 1u), seg = g >> sb;
+        return lds[valid && j < hg ? (((seg * hg + j) << 4) | (loc & 15u)) : idcell];
     }
-    // Only cold lanes load (exec-masked); the others keep identity().
-    __device__ __forceinline__ T cold(int32_t c) const {
+    __device__ __forceinline__ int32_t col(uint32_t loc) const {
+        const uint32_t x = (loc >> 4) << bits;  // the group's first line
+        const uint32_t hx = (x ^ (x >> 8) ^ (x >> 16) ^ (x >> 24)) & hmask;
+        return (int32_t)(((x | (h ^ hx)) << 4) | (loc & 15u));
+    }
+    // Only valid cold lanes load (exec-masked); the others keep identity().
+    __device__ __forceinline__ T cold(uint32_t loc, bool valid, bool lds_on) const {
         T v = op.identity();
-        if (!is_hot(c)) v = op.gather(c);
+        if (valid && !(lds_on && is_hot(loc))) v = op.gather(col(loc));
         return v;
     }
 };
 
-// NT: bit 0 = the streamed band arrays (col, heads, meta) are loaded non-temporally, bit 1 = the
-// partials are stored non-temporally (both are touched once per superstep; keep L2 / MALL for the
-// gathered vector).  Bands of fewer than 8 sub-slices (2^bits < 8) share each sub-slice among
+// Entry u of a lane chunk packed in W bits (bit stream over the chunk's dwords).
+template <int W>
+__device__ __forceinline__ uint32_t unpack_entry(const uint32_t (&d)[W / 4], int u) {
+    const int o = W * u, i = o >> 5, sh = o & 31;
+    uint32_t v = d[i] >> sh;
+    if (sh + W > 32) v |= d[i + 1] << (32 - sh);
+    if constexpr (W < 32) v &= (1u << W) - 1u;
+    return v;
+}
+
+// NT: bit 0 = the streamed band arrays are loaded non-temporally, bit 1 = the partials are stored
+// non-temporally.  Every launch uses 0: the merge_nt knob measured no gain at RMAT-24/26 (round 2,
+// 4.12-4.25 vs 4.12 ms) and was removed; the parameter stays for such experiments.  Bands of fewer than 8 sub-slices (2^bits < 8) share each sub-slice among
 // 8 / 2^bits XCDs.
 template <class T>
 __device__ __forceinline__ void store_nt(T* p, T v, bool nt) {
     if (nt) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
-template <class Op, bool LDS, int NT>
+template <class Op, bool LDS, int NT, int PW>
 __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
                                                                    typename Op::T* __restrict__ carry, HotSegs hs,
                                                                    int temporal) {
@@ -372,6 +414,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int gshift = 4 + a.bits;
     const int hg = hs.hs >> gshift;  // hot line groups per segment
     const int nl = hs.nseg * hg;     // LDS lines
+    lds_ptr<T> stg = hotv + (nl * 16 + 1) + wave * a.stage;  // this wave's partial window (after the image)
     // Static: block w of an XCD folds sub-slice (w mod per) with the XCD's other W / per blocks of it.
     // Temporal: every block of an XCD sweeps the XCD's per sub-slices in the same order, all W blocks
     // on one sub-slice at a time, so the XCD's L2 holds one sub-slice's part of the vector instead
@@ -413,68 +456,74 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
         __syncthreads();
     }
-    const SliceLdsGather<Op> lg{op, hotv, (uint32_t)hs.hs, (uint32_t)((hs.tbits >= 31) ? 0x7FFFFFFFu : ((1u << hs.tbits) - 1u)),
-                                (uint32_t)hg, hs.tbits, gshift, (uint32_t)nl * 16u};
+    const SliceGather<Op> lg{op,       hotv, (uint32_t)hg, hs.tbits - gshift, a.bits, (1u << a.bits) - 1u, (uint32_t)h,
+                             (uint32_t)nl * 16u};
     const int64_t base = a.sub_base[h];
     const int64_t ntask = a.sub_base[h + 1] - base;
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
     const int64_t step = G * kMergeWaves;
     int64_t k = g * kMergeWaves + wave;
-    if (k >= ntask) continue;
-    // The next task's cols and metadata are loaded while this task's gathers are in flight.  The
-    // loop carries the raw load registers (int4 col vectors, head byte, meta word) and unpacks them at
-    // the top, so a prefetch writes straight into them and nothing waits on it until the next task.
-    // Metadata are vector loads (lane 0: j0, lane 1: carry flag; one head byte per lane): a scalar
-    // prefetch would hold up every LDS wait (lgkmcnt does not count SMEM in order).
-    static_assert(kMergeEpl == 8, "the loop carries two int4 col vectors per lane");
-    auto col_ptr = [&](int64_t kk) {
-        return reinterpret_cast<const int4*>(a.col + hbegin + kk * kMergeTask + kMergeEpl * lane);
-    };
+    if (k >= ntask || a.diag == 1) continue;
+    // The next task's entries and metadata are loaded while this task's gathers are in flight.  The
+    // loop carries the raw load registers (the packed lane chunk, head byte, meta word) and unpacks
+    // them at the top, so a prefetch writes straight into them and nothing waits on it until the next
+    // task.  Metadata are vector loads (lane 0: j0, lane 1: carry flag; one head byte per lane): a
+    // scalar prefetch would hold up every LDS wait (lgkmcnt does not count SMEM in order).
+    static_assert(kMergeEpl == 8, "a lane chunk is 8 entries");
+    constexpr int DB = PW / 4 - 4;  // dwords of a chunk in pack_b
+    auto chunk = [&](int64_t kk) { return (hbegin >> 3) + kk * kWave + lane; };
     auto meta_idx = [&](int64_t kk) { return 2 * (base + kk) + (lane & 1); };
     auto head_idx = [&](int64_t kk) { return (base + kk) * kWave + lane; };
     auto ld = [](const auto* p) {
         if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(p);
         else return *p;
     };
-    auto ld4 = [&](const int4* p) {
-        using v4i = int __attribute__((ext_vector_type(4)));
-        const v4i x = ld(reinterpret_cast<const v4i*>(p));
-        return make_int4(x.x, x.y, x.z, x.w);
+    using v4u = uint32_t __attribute__((ext_vector_type(4)));
+    using v2u = uint32_t __attribute__((ext_vector_type(2)));
+    auto load_chunk = [&](int64_t kk, uint32_t (&d)[PW / 4]) {
+        const int64_t x = chunk(kk);
+        const v4u va = ld(reinterpret_cast<const v4u*>(a.pack_a) + x);
+        d[0] = va.x, d[1] = va.y, d[2] = va.z, d[3] = va.w;
+        if constexpr (DB == 1) {
+            d[4] = ld(a.pack_b + x);
+        } else if constexpr (DB == 2) {
+            const v2u vb = ld(reinterpret_cast<const v2u*>(a.pack_b) + x);
+            d[4] = vb.x, d[5] = vb.y;
+        } else {
+            const v4u vb = ld(reinterpret_cast<const v4u*>(a.pack_b) + x);
+            d[4] = vb.x, d[5] = vb.y, d[6] = vb.z, d[7] = vb.w;
+        }
     };
-    int4 cv0 = ld4(col_ptr(k)), cv1 = ld4(col_ptr(k) + 1);
+    uint32_t cd[PW / 4];
+    load_chunk(k, cd);
     uint32_t hb = ld(a.heads + head_idx(k));
     int32_t mw = ld(a.meta + meta_idx(k));
     for (;;) {
         const int64_t t = base + k;
         const int64_t e0 = hbegin + k * kMergeTask;
         const int n = (int)min((int64_t)kMergeTask, hend - e0);
-        int32_t c[kMergeEpl] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+        uint32_t loc[kMergeEpl];
+#pragma unroll
+        for (int u = 0; u < kMergeEpl; ++u) loc[u] = unpack_entry<PW>(cd, u);
         const int32_t j0 = __builtin_amdgcn_readlane(mw, 0);
         const bool carry_in = __builtin_amdgcn_readlane(mw, 1) != 0;
         const uint32_t hbc = hb;
-#pragma unroll
-        for (int u = 0; u < kMergeEpl; ++u)  // past the task end: cold id (identity cell, no load)
-            if (kMergeEpl * lane + u >= n) c[u] = INT32_MAX;
         T v[kMergeEpl];
         if constexpr (LDS) {
             T vg[kMergeEpl], vl[kMergeEpl];
 #pragma unroll
-            for (int u = 0; u < kMergeEpl; ++u) vl[u] = lg.hot(c[u]);
+            for (int u = 0; u < kMergeEpl; ++u) vl[u] = lg.hot(loc[u], kMergeEpl * lane + u < n);
 #pragma unroll
-            for (int u = 0; u < kMergeEpl; ++u) vg[u] = c[u] != INT32_MAX ? lg.cold(c[u]) : op.identity();
+            for (int u = 0; u < kMergeEpl; ++u) vg[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, true);
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) v[u] = op.combine(vl[u], vg[u]);
         } else {
 #pragma unroll
-            for (int u = 0; u < kMergeEpl; ++u) {
-                v[u] = op.identity();
-                if (c[u] != INT32_MAX) v[u] = op.gather(c[u]);
-            }
+            for (int u = 0; u < kMergeEpl; ++u) v[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, false);
         }
         const int64_t kn = k + step;
         if (kn < ntask) {
-            cv0 = ld4(col_ptr(kn));
-            cv1 = ld4(col_ptr(kn) + 1);
+            load_chunk(kn, cd);
             hb = ld(a.heads + head_idx(kn));
             mw = ld(a.meta + meta_idx(kn));
         }
@@ -488,7 +537,17 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         }
         const int hbase = incl - cnt;  // head number of this lane's first head
         const bool valid_lane = kMergeEpl * lane < n;
+        // A task's partials are consecutive slots: with at most `stage` heads they are collected in the
+        // wave's LDS window and written by one coalesced store per 64, instead of up to 10 exec-masked
+        // scattered stores per lane (the stores cost ~20% of the merge kernel: merge_diag 3).
+        const int H = __builtin_amdgcn_readlane(incl, kWave - 1);
+        const bool staged = LDS && H <= a.stage;
         auto emit = [&](int hh, T val) {  // segment of head hh
+            if (a.diag == 3) return;  // diag 3: no partial stores (timing only)
+            if (staged) {
+                stg[hh] = val;
+                return;
+            }
             if (hh == 0 && carry_in) store_nt(carry + t, val, (NT & 2) != 0);
             else store_nt(partial + j0 + hh, val, (NT & 2) != 0);
         };
@@ -534,6 +593,22 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
                 if (fh < kMergeEpl) emit(run_h, run);
                 else emit(in_h, lane > 0 ? op.combine(in_x, pre) : pre);
             }
+        }
+        if (staged && a.diag != 3) {
+            // the window is wave-private and LDS runs a wave's instructions in order: the fences only
+            // keep the compiler from moving these reads above the writes (or the next task's writes
+            // above these reads)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = lane; i < H; i += kWave) {
+                const T val = stg[i];
+                if (i == 0 && carry_in) store_nt(carry + t, val, (NT & 2) != 0);
+                else store_nt(partial + j0 + i, val, (NT & 2) != 0);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (kn >= ntask) break;
         k = kn;
@@ -684,13 +759,11 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     if (split) {
         static bool attr = false;
         if (!attr) {
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 20>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 1>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 24>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 2>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 3>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
             attr = true;
         }
@@ -704,8 +777,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const SliceBand& bd = *plan.bands[bi];
             if (bd.tasks == 0) continue;
             const hipStream_t ms = (mside && bi > 0) ? mside->stream : s;
-            MergeArgs ma{bd.col.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(), bd.sub_end.get(),
-                         bd.sub_base.get(), bd.tasks, bd.bits};
+            // staging window: -1 = automatic, the power of two >= twice the band's mean heads per task
+            // (RMAT-24 band 0 ~21 heads: 64; RMAT-26 band 0 ~73 and band 1 ~110: 256), within [64, 256]
+            int stage = tune().merge_stage[std::min<size_t>(bi, 3)];
+            if (stage < 0) {
+                const double heads = (double)bd.subrows / (double)std::max<int64_t>(bd.tasks, 1);
+                stage = 64;
+                while (stage < 2.0 * heads && stage < 256) stage *= 2;
+            }
+            MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
+                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_diag};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
@@ -713,9 +794,9 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             // a multiple of S workgroups: every sub-slice gets grid / S of them
             const int wpc = tune().merge_wgs;
             const unsigned grid = (unsigned)std::max<int64_t>(S, (int64_t)device_cu_count() * wpc / S * S);
-            // shared equally by the segments; a segment's hot part stays below its stride (the
-            // past-the-end sentinel INT32_MAX must test cold)
-            const int64_t hot_max = (int64_t)(kMergeLdsBytes / wpc / sizeof(T) - 16) * S;
+            // shared equally by the segments; a segment's hot part stays below its stride
+            const int64_t stage_bytes = (int64_t)kMergeWaves * stage * (int64_t)sizeof(T);
+            const int64_t hot_max = (int64_t)((kMergeLdsBytes / wpc - stage_bytes) / (int64_t)sizeof(T) - 16) * S;
             const bool lds_ok = plan.lds_ok && tune().slice_lds;
             HotSegs hs;
             hs.tbits = plan.seg_tbits;
@@ -723,16 +804,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
             const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
-            const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) : 0;
+            const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) + (size_t)stage_bytes : 0;
             auto go = [&](auto kern) { kern<<<grid, kMergeThreads, lds, ms>>>(ma, op, part, carry, hs, temporal); };
-            const int nt = tune().merge_nt & 3;
             if (hs.hs > 0) {
-                if (nt == 0) go(pull_merge_kernel<Op, true, 0>);
-                else if (nt == 1) go(pull_merge_kernel<Op, true, 1>);
-                else if (nt == 2) go(pull_merge_kernel<Op, true, 2>);
-                else go(pull_merge_kernel<Op, true, 3>);
+                if (bd.width == 20) go(pull_merge_kernel<Op, true, 0, 20>);
+                else if (bd.width == 24) go(pull_merge_kernel<Op, true, 0, 24>);
+                else go(pull_merge_kernel<Op, true, 0, 32>);
             } else {
-                go(pull_merge_kernel<Op, false, 0>);
+                if (bd.width == 20) go(pull_merge_kernel<Op, false, 0, 20>);
+                else if (bd.width == 24) go(pull_merge_kernel<Op, false, 0, 24>);
+                else go(pull_merge_kernel<Op, false, 0, 32>);
             }
             JG_LAUNCH_CHECK();
         }

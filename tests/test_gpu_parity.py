@@ -308,7 +308,8 @@ def test_errors_are_status_codes(ctx):
 
 
 @pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
-                                  "split_sub1", "split_sub2_4", "split_nt", "pr_noskip"])
+                                  "split_sub1", "split_sub2_4", "split_w24", "split_w32", "split_stage_off",
+                                  "split_stage512", "light_noruns", "pr_noskip"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -328,7 +329,11 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "split_sub1": [("band1_sub", 1)],
              "split_sub2_4": [("band0_deg", 64), ("band0_sub", 4), ("band1_deg", 16), ("band1_sub", 2),
                               ("band2_deg", 4), ("band2_sub", 1)],
-             "split_nt": [("merge_nt", 3)],
+             "split_w24": [("merge_pack", 24)],
+             "split_w32": [("merge_pack", 0)],
+             "split_stage_off": [("merge_stage0", 0), ("merge_stage1", 0)],
+             "split_stage512": [("merge_stage0", 512), ("merge_stage1", 512)],
+             "light_noruns": [("light_runs", 0)],
              "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)]}[mode]
     try:
         for k, v in knobs:
@@ -357,7 +362,10 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("slice_lds", 1)
-        _lib.tune_set("merge_nt", 0)
+        _lib.tune_set("merge_pack", 1)
+        _lib.tune_set("merge_stage0", -1)
+        _lib.tune_set("merge_stage1", -1)
+        _lib.tune_set("light_runs", 1)
         _lib.tune_set("pr_skip_empty", 1)
         _lib.tune_set("pr_rank_last", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
