@@ -420,6 +420,12 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     // on one sub-slice at a time, so the XCD's L2 holds one sub-slice's part of the vector instead
     // of all of them at once (one image restaged per round).
     const int rounds = temporal ? per : 1;
+    const uint32_t hmask = (1u << a.bits) - 1u;
+    // the vector line held by LDS line j of segment seg in sub-slice hh's image
+    auto image_line = [&](int seg, int j, int hh) {
+        const int64_t grp = ((int64_t)seg << (hs.tbits - gshift)) + j;
+        return (grp << a.bits) + (int64_t)(hh ^ (sub_hash(grp << gshift) & hmask));
+    };
     for (int rd = 0; rd < rounds; ++rd) {
     const int h = (xcd % xs) | ((temporal ? rd : w % per) << 3);
     // this block's rank among h's blocks
@@ -427,30 +433,36 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int64_t G = (int64_t)(temporal ? W : W / per) * rep;
     if constexpr (LDS) {
         if (rd > 0) __syncthreads();  // every wave is done with the previous round's image
-        // LDS line i = the line of sub-slice h in hot line group i (a permutation of each aligned group)
-        const T* src = op.vec();
-        const uint32_t mask = (1u << a.bits) - 1;
-        // kStage loads in flight per thread: with 2^bits sub-slices the image lines are scattered over
-        // 2^bits x the image span, so a load-store-load loop would pay one memory round trip each
+        // LDS line i = the line of sub-slice h in hot line group i (a permutation of each aligned group).
+        // 16-byte units (16 / sizeof(T) elements of one line), kStage loads in flight per thread: with
+        // 2^bits sub-slices the image lines are scattered over 2^bits x the image span, so a
+        // load-store-load loop would pay one memory round trip each.
         constexpr int kStage = 8;
-        auto src_of = [&](int i) {
-            const int sg = i >> 4, seg = sg / hg;
-            const int64_t grp = ((int64_t)seg << (hs.tbits - gshift)) + (sg - seg * hg);
-            const int64_t line = (grp << a.bits) + (int64_t)(h ^ (sub_hash(grp << gshift) & mask));
-            return src + line * 16 + (i & 15);
-        };
-        const int total = nl * 16;
-        for (int i0 = 0; i0 < total; i0 += kStage * kMergeThreads) {
-            T buf[kStage];
+        constexpr int kUnit = 16 / (int)sizeof(T);
+        static_assert(16 % sizeof(T) == 0 && kUnit <= 16, "16-byte staging units");
+        const unsigned char* src = reinterpret_cast<const unsigned char*>(op.vec());
+        const int units = nl * 16 / kUnit;
+        using u4 = uint32_t __attribute__((ext_vector_type(4)));
+        lds_ptr<u4> hv4 = (lds_ptr<u4>)merge_lds;
+        for (int q0 = 0; q0 < units; q0 += kStage * kMergeThreads) {
+            u4 buf[kStage];
 #pragma unroll
             for (int u = 0; u < kStage; ++u) {
-                const int i = i0 + u * kMergeThreads + (int)threadIdx.x;
-                buf[u] = i < total ? *src_of(i) : op.identity();
+                const int q = q0 + u * kMergeThreads + (int)threadIdx.x;
+                const int i = q * kUnit, sg = i >> 4;
+                int seg = 0, j = sg;
+                if (hs.nseg > 1) {
+                    seg = sg / hg;
+                    j = sg - seg * hg;
+                }
+                buf[u] = u4{0, 0, 0, 0};
+                if (q < units)
+                    buf[u] = *reinterpret_cast<const u4*>(src + (image_line(seg, j, h) * 16 + (i & 15)) * (int64_t)sizeof(T));
             }
 #pragma unroll
             for (int u = 0; u < kStage; ++u) {
-                const int i = i0 + u * kMergeThreads + (int)threadIdx.x;
-                if (i < total) hotv[i] = buf[u];
+                const int q = q0 + u * kMergeThreads + (int)threadIdx.x;
+                if (q < units) hv4[q] = buf[u];
             }
         }
         if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
@@ -637,13 +649,21 @@ __global__ void pull_merge_fixup_kernel(FixupBands fb, Op op, typename Op::T* __
         while (x >= fb.task_begin[b + 1]) ++b;
         const int64_t t = x - fb.task_begin[b], tasks = fb.task_begin[b + 1] - fb.task_begin[b];
         const int32_t* __restrict__ meta = fb.meta[b];
-        if (!meta[2 * t + 1]) continue;
-        const int32_t j = meta[2 * t];
-        if (meta[2 * (t - 1) + 1] && meta[2 * (t - 1)] == j) continue;  // not the first carry of the run
         T* __restrict__ partial = split_partial + fb.part_off[b];
         const T* __restrict__ carry = split_partial + fb.carry_off[b];
-        T acc = partial[j];
-        for (int64_t u = t; u < tasks && meta[2 * u + 1] && meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
+        // one round trip for this task, its predecessor and its successor (most runs are one task
+        // long), then the sub-row's partial
+        const int64_t tp = t > 0 ? t - 1 : 0, tn = t + 1 < tasks ? t + 1 : t;
+        const int32_t f = meta[2 * t + 1], j = meta[2 * t];
+        const int32_t pf = meta[2 * tp + 1], pj = meta[2 * tp];
+        const int32_t nf = meta[2 * tn + 1], nj = meta[2 * tn];
+        const T c = carry[t], cn = carry[tn];
+        if (!f || (t > 0 && pf && pj == j)) continue;  // no carry, or not the first carry of the run
+        T acc = op.combine(partial[j], c);
+        if (tn != t && nf && nj == j) {
+            acc = op.combine(acc, cn);
+            for (int64_t u = t + 2; u < tasks && meta[2 * u + 1] && meta[2 * u] == j; ++u) acc = op.combine(acc, carry[u]);
+        }
         partial[j] = acc;
     }
 }
@@ -659,7 +679,7 @@ struct FinalizeBands {
     int bits[kMaxBands];
     int n;
 };
-template <class Op>
+template <class Op, bool PIPE = true>
 __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, const FinalizeBands& fb,
                                                    const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
@@ -674,28 +694,56 @@ __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, cons
         const T* __restrict__ part = partial + fb.part_off[b];
         T acc = op.identity();
         bool first = true;
-        // batches of 8 sub-slices (S >= 8): all index loads, then all partial loads, then the fold in
-        // h order, so a hub row's 32 sub-slices cost 4 round trips instead of 32 dependent pairs.  The
-        // index words are shared by 32 rows (1/16 of the bytes of an int32 index per sub-row).
-        for (int h0 = 0; h0 < S; h0 += 8) {
-            int32_t j[8];
-            T v[8];
+        // batches of 8 sub-slices: all index loads, then all partial loads, then the fold in h order,
+        // and the next batch's index words are loaded with this batch's partials, so a hub row's 128
+        // sub-slices cost 17 round trips instead of 128 dependent pairs.  The index words are shared by
+        // 32 rows (1/16 of the bytes of an int32 index per sub-row).
+        if constexpr (PIPE) {
+            uint2 wc[8], wn[8];
+            auto load_words = [&](int h0, uint2 (&wd)[8]) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                j[u] = -1;
-                if (h0 + u < S) {  // bands of fewer than 8 sub-slices
-                    const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
-                    j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
-                }
+                for (int u = 0; u < 8; ++u)  // bands of fewer than 8 sub-slices: empty words
+                    wd[u] = h0 + u < S ? sw[(int64_t)(h0 + u) * W + wi] : make_uint2(0u, 0u);
+            };
+            load_words(0, wc);
+            for (int h0 = 0; h0 < S; h0 += 8) {
+                int32_t j[8];
+                T v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) j[u] = (wc[u].x & me) ? (int32_t)wc[u].y + __popc(wc[u].x & below) : -1;
+                if (h0 + 8 < S) load_words(h0 + 8, wn);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (j[u] >= 0) {
+                        acc = first ? v[u] : op.combine(acc, v[u]);
+                        first = false;
+                    }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) wc[u] = wn[u];
             }
+        } else {  // round 1: index loads and partial loads of one batch, then the next batch
+            for (int h0 = 0; h0 < S; h0 += 8) {
+                int32_t j[8];
+                T v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (j[u] >= 0) {
-                    acc = first ? v[u] : op.combine(acc, v[u]);
-                    first = false;
+                for (int u = 0; u < 8; ++u) {
+                    j[u] = -1;
+                    if (h0 + u < S) {
+                        const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
+                        j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
+                    }
                 }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (j[u] >= 0) {
+                        acc = first ? v[u] : op.combine(acc, v[u]);
+                        first = false;
+                    }
+            }
         }
         op.finalize(r, acc);
     }
@@ -710,7 +758,7 @@ __global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb
 // The light rows and the split's finalize in one launch (tune fuse_finalize): blocks [0, fin_blocks)
 // finalise split rows (one per thread), the rest run light-row blocks.  Both are latency-bound and
 // independent, so interleaving their blocks hides one's stalls behind the other's.
-template <class Op, int U, bool NT>
+template <class Op, int U, bool NT, bool PIPE>
 __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a, Op op,
                                                                      typename Op::T* __restrict__ hub_partial,
                                                                      FinalizeBands fb,
@@ -723,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a,
     const int64_t b = blockIdx.x;
     if (b >= fb0 && b < fb0 + fin_blocks) {
         const int64_t r = (b - fb0) * kBlock + threadIdx.x;
-        if (r < split_rows) slice_finalize_row(r, op, fb, partial);
+        if (r < split_rows) slice_finalize_row<Op, PIPE>(r, op, fb, partial);
         return;
     }
     pull_block<Op, U, NT>(a, op, hub_partial, (fin_last ? b : b - fin_blocks) + a.block_offset);
@@ -831,7 +879,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             ++fx.n;
         }
         if (fx.task_begin[fx.n] > 0) {
-            pull_merge_fixup_kernel<Op><<<grid_for(fx.task_begin[fx.n]), kBlock, 0, s>>>(fx, op, split_partial);
+            pull_merge_fixup_kernel<Op><<<grid_for(fx.task_begin[fx.n], kBlock, 0), kBlock, 0, s>>>(fx, op, split_partial);
             JG_LAUNCH_CHECK();
         }
     }
@@ -880,11 +928,14 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         const int64_t fin_blocks = (plan.split_rows + kBlock - 1) / kBlock;
         const unsigned grid = (unsigned)(fin_blocks + blocks);
         if (tune().pull_unroll >= 8)
-            pull_light_finalize_kernel<Op, 8, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
+            pull_light_finalize_kernel<Op, 8, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
                                                                             plan.split_rows, fin_blocks, tune().fin_last);
+        else if (tune().fin_pipe)
+            pull_light_finalize_kernel<Op, 4, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
+                                                                                  plan.split_rows, fin_blocks, tune().fin_last);
         else
-            pull_light_finalize_kernel<Op, 4, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                            plan.split_rows, fin_blocks, tune().fin_last);
+            pull_light_finalize_kernel<Op, 4, false, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
+                                                                                   plan.split_rows, fin_blocks, tune().fin_last);
         JG_LAUNCH_CHECK();
     } else if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
         const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
