@@ -332,6 +332,7 @@ struct MergeArgs {
     int64_t tasks;
     int bits;
     int stage;         // LDS staging slots per wave for a task's partials (0: direct stores)
+    int dynamic;       // LDS image kernels: waves take their block's tasks from an LDS counter
     int diag;          // Tune::merge_diag (diagnostic timing variants; 0 in production)
 };
 
@@ -415,6 +416,8 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int hg = hs.hs >> gshift;  // hot line groups per segment
     const int nl = hs.nseg * hg;     // LDS lines
     lds_ptr<T> stg = hotv + (nl * 16 + 1) + wave * a.stage;  // this wave's partial window (after the image)
+    // the block's task counter (dynamic assignment), after every wave's window
+    lds_ptr<uint32_t> tctr = (lds_ptr<uint32_t>)(hotv + (nl * 16 + 1) + kMergeWaves * a.stage);
     // Static: block w of an XCD folds sub-slice (w mod per) with the XCD's other W / per blocks of it.
     // Temporal: every block of an XCD sweeps the XCD's per sub-slices in the same order, all W blocks
     // on one sub-slice at a time, so the XCD's L2 holds one sub-slice's part of the vector instead
@@ -465,7 +468,10 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
                 if (q < units) hv4[q] = buf[u];
             }
         }
-        if (threadIdx.x == 0) hotv[nl * 16] = op.identity();  // the cold lanes' cell
+        if (threadIdx.x == 0) {
+            hotv[nl * 16] = op.identity();  // the cold lanes' cell
+            *tctr = 0u;                     // this round's task counter (dynamic)
+        }
         __syncthreads();
     }
     const SliceGather<Op> lg{op,       hotv, (uint32_t)hg, hs.tbits - gshift, a.bits, (1u << a.bits) - 1u, (uint32_t)h,
@@ -474,7 +480,19 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int64_t ntask = a.sub_base[h + 1] - base;
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
     const int64_t step = G * kMergeWaves;
-    int64_t k = g * kMergeWaves + wave;
+    // The block's tasks are k = g * 16 + (j mod 16) + (j / 16) * step, j = 0, 1, ...  Static: wave w
+    // takes j = w, w + 16, ...; dynamic (LDS image kernels, a.dynamic): the waves take j from the
+    // block's LDS counter, so a wave that drew cheaper tasks takes more and the round's barrier waits
+    // less for the slowest wave.  Any order gives the same result (tasks are independent).
+    const bool dyn = LDS && a.dynamic;
+    auto task_of = [&](int64_t j) { return (j / kMergeWaves) * step + g * kMergeWaves + (j % kMergeWaves); };
+    auto grab = [&]() -> int64_t {
+        uint32_t j = 0;
+        if (lane == 0) j = __hip_atomic_fetch_add(tctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return task_of((int64_t)__builtin_amdgcn_readfirstlane(j));
+    };
+    int64_t jstat = wave;
+    int64_t k = dyn ? grab() : task_of(jstat);
     if (k >= ntask || a.diag == 1) continue;
     // The next task's entries and metadata are loaded while this task's gathers are in flight.  The
     // loop carries the raw load registers (the packed lane chunk, head byte, meta word) and unpacks
@@ -533,7 +551,13 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) v[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, false);
         }
-        const int64_t kn = k + step;
+        int64_t kn;
+        if (dyn) {
+            kn = grab();
+        } else {
+            jstat += kMergeWaves;
+            kn = task_of(jstat);
+        }
         if (kn < ntask) {
             load_chunk(kn, cd);
             hb = ld(a.heads + head_idx(kn));
@@ -834,7 +858,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                 while (stage < 2.0 * heads && stage < 256) stage *= 2;
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
-                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_diag};
+                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_diag};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
@@ -844,7 +868,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const unsigned grid = (unsigned)std::max<int64_t>(S, (int64_t)device_cu_count() * wpc / S * S);
             // shared equally by the segments; a segment's hot part stays below its stride
             const int64_t stage_bytes = (int64_t)kMergeWaves * stage * (int64_t)sizeof(T);
-            const int64_t hot_max = (int64_t)((kMergeLdsBytes / wpc - stage_bytes) / (int64_t)sizeof(T) - 16) * S;
+            const int64_t hot_max = (int64_t)((kMergeLdsBytes / wpc - stage_bytes - 16) / (int64_t)sizeof(T) - 16) * S;
             const bool lds_ok = plan.lds_ok && tune().slice_lds;
             HotSegs hs;
             hs.tbits = plan.seg_tbits;
@@ -852,7 +876,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
             hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
             const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
-            const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) + (size_t)stage_bytes : 0;
+            const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) + (size_t)stage_bytes + 16 : 0;
             auto go = [&](auto kern) { kern<<<grid, kMergeThreads, lds, ms>>>(ma, op, part, carry, hs, temporal); };
             if (hs.hs > 0) {
                 if (bd.width == 20) go(pull_merge_kernel<Op, true, 0, 20>);

@@ -7,7 +7,7 @@ OUT=gpurun_out/${1:-pack}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || exit 3
-V="auto: nopipe:fin_pipe=0 b1s16:band1_bit=4 b0s64:band0_bit=6 b0s256:band0_bit=8"
+V="auto: static:merge_dynamic=0"
 for S in 24 26; do
   timeout -k 10 300 python -u tools/pr_ab.py --scale $S --steps 10 --rounds 3 $V > $OUT/ab_s$S.json 2> $OUT/ab_s$S.err || exit 4
 done
