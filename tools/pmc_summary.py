@@ -45,7 +45,10 @@ def main():
                                     "avg_us": round(float(r["AverageNs"]) / 1e3, 2), "pct": float(r["Percentage"])}
                                    for r in rows[:14]]
         ss = [r for r in rows if "PrOp" in r["Name"] and any(s in r["Name"] for s in SUPERSTEP)]
-        out["superstep_kernel_avg_us"] = {r["Name"].split("(")[0][:80]: round(float(r["AverageNs"]) / 1e3, 2) for r in ss}
+        # template instantiations (e.g. the merge kernel's packed widths, one per band) stay apart:
+        # the kernel name plus its template arguments
+        out["superstep_kernel_avg_us"] = {r["Name"].replace("(anonymous namespace)::", "").split("(")[0][:90]:
+                                          round(float(r["AverageNs"]) / 1e3, 2) for r in ss}
         shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     rd, rd_calls = counters(os.path.join(src, "pmc_rd"))
     wr, _ = counters(os.path.join(src, "pmc_wr"))
