@@ -114,4 +114,81 @@ __device__ __forceinline__ void staged_append(bool take, int32_t v, int64_t deg,
     if (sa.n > (unsigned long long)(StagedAppend::kCap - kBlock)) staged_flush(sa, queue, qoff, packed);
 }
 
+// Wave-staged frontier append: every wave collects its appends in its own LDS region and keeps its
+// count in registers, so appending needs no block barrier and the waves of a block run their loops
+// independently (a block-wide append made every wave wait, every iteration, for the block's slowest
+// lane scan).  Global queue space is still reserved with one atomic per block at the end
+// (wave_stage_final, block-uniform); a wave whose region fills up reserves for itself.
+struct WaveStage {
+    static constexpr int kCap = 512;  // entries per wave
+    int32_t v[kBlock / kWave][kCap];
+    int64_t off[kBlock / kWave][kCap];  // edge offset inside the wave's staged run
+    unsigned long long cnt[kBlock / kWave], dsum[kBlock / kWave];
+    unsigned long long base;
+};
+struct WaveRun {  // a wave's staged run (wave-uniform registers)
+    unsigned long long n = 0, ds = 0;
+};
+__device__ __forceinline__ void wave_stage_flush(WaveStage& sa, WaveRun& run, int32_t* __restrict__ queue,
+                                                 int64_t* __restrict__ qoff, unsigned long long* __restrict__ packed) {
+    if (run.n == 0) return;
+    const int wv = wave_id();
+    unsigned long long base = 0;
+    if (lane_id() == 0) base = atomicAdd(packed, (run.n << kPackShift) | run.ds);
+    base = __shfl(base, 0, kWave);
+    const unsigned long long qb = base >> kPackShift, eb = base & kEdgeMask;
+    for (unsigned long long i = lane_id(); i < run.n; i += kWave) {
+        queue[qb + i] = sa.v[wv][i];
+        qoff[qb + i] = (int64_t)eb + sa.off[wv][i];
+    }
+    run.n = run.ds = 0;
+}
+// Wave-uniform call: lanes with `take` append v (push degree deg).
+__device__ __forceinline__ void wave_stage_append(bool take, int32_t v, int64_t deg, WaveStage& sa, WaveRun& run,
+                                                  int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                  unsigned long long* __restrict__ packed) {
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int64_t d = take ? deg : 0;
+    const int64_t dinc = wave_inclusive_scan_add(d);
+    const int64_t tot = __shfl(dinc, kWave - 1, kWave);
+    const int wv = wave_id();
+    if (take) {
+        const unsigned long long p = run.n + (unsigned long long)__popcll(mask & lanemask_lt());
+        sa.v[wv][p] = v;
+        sa.off[wv][p] = (int64_t)run.ds + dinc - d;
+    }
+    run.n += (unsigned long long)__popcll(mask);
+    run.ds += (unsigned long long)tot;
+    if (run.n > (unsigned long long)(WaveStage::kCap - kWave)) wave_stage_flush(sa, run, queue, qoff, packed);
+}
+// Block-uniform: the block's remaining runs reserve their space with one atomic and are written out.
+__device__ __forceinline__ void wave_stage_final(WaveStage& sa, WaveRun& run, int32_t* __restrict__ queue,
+                                                 int64_t* __restrict__ qoff, unsigned long long* __restrict__ packed) {
+    const int wv = wave_id();
+    if (lane_id() == 0) {
+        sa.cnt[wv] = run.n;
+        sa.dsum[wv] = run.ds;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = 0, e = 0;
+        for (int k = 0; k < kBlock / kWave; ++k) {
+            const unsigned long long ck = sa.cnt[k], ek = sa.dsum[k];
+            sa.cnt[k] = c;  // exclusive prefixes
+            sa.dsum[k] = e;
+            c += ck;
+            e += ek;
+        }
+        sa.base = c ? atomicAdd(packed, (c << kPackShift) | e) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long qb = (sa.base >> kPackShift) + sa.cnt[wv], eb = (sa.base & kEdgeMask) + sa.dsum[wv];
+    for (unsigned long long i = lane_id(); i < run.n; i += kWave) {
+        queue[qb + i] = sa.v[wv][i];
+        qoff[qb + i] = (int64_t)eb + sa.off[wv][i];
+    }
+    run.n = run.ds = 0;
+}
+
 }  // namespace jg

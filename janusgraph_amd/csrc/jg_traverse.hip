@@ -20,6 +20,7 @@
 //   weighted SD: frontier Bellman-Ford with exact snapshot semantics (messages of superstep t-1
 //     only): push over the in-CSR with 64-bit atomicMin into a scratch array, then apply.
 #include <climits>
+#include <type_traits>
 
 #include <cstdio>
 
@@ -140,8 +141,9 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
 // the frontier is spread over the whole grid.  A thread's edges are processed in phases (all target
 // loads, then all depth probes and claims, then the degree loads) so its dependent memory round trips
 // do not multiply with the edges it holds; one block-wide append per edge slot follows.
+template <class App>
 __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed,
-                                             StagedAppend& sc) {
+                                             App& app) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int ept = mf <= nthreads ? 1 : kTdEdgesPerThread;  // grid-uniform
@@ -149,9 +151,10 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
     const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
     const int32_t next_depth = a.level + 1;
     for (int64_t t = 0; t < tiles; ++t) {
-        // block-uniform: a block whose slice of this tile is past the frontier's edges has nothing to
-        // claim or append (small frontiers leave most of the grid idle)
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * ept >= mf) break;
+        // a block (a wave, with wave-staged appends) whose slice of this tile is past the frontier's
+        // edges has nothing to claim or append (small frontiers leave most of the grid idle)
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x + (App::kWaveUniform ? wave_id() * kWave : 0)) * ept >= mf)
+            break;
         const int64_t e0 = (t * nthreads + tid) * ept;
         int32_t v[kTdEdgesPerThread];
         bool have[kTdEdgesPerThread], won[kTdEdgesPerThread];
@@ -193,21 +196,23 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
         }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) vdeg[k] = won[k] ? a.deg_rp[v[k] + 1] - a.deg_rp[v[k]] : 0;
-        for (int k = 0; k < ept; ++k) staged_append(won[k], v[k], vdeg[k], sc, a.queue_out, a.qoff_out, packed);
+        for (int k = 0; k < ept; ++k) app.append(won[k], v[k], vdeg[k], a.queue_out, a.qoff_out, packed);
     }
 }
 
 // Bottom-up: one lane per unvisited vertex scans its pull row against the frontier and stops at the
 // first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
-template <bool kFromDepth>
-__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, StagedAppend& sc) {
+template <bool kFromDepth, class App>
+__device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, App& app) {
     const int64_t words = (a.rows + 63) / 64;
     constexpr int kWpb = kBlock / kWave;
     const int64_t wstride = (int64_t)gridDim.x * kWpb;
     const int32_t next_depth = a.level + 1;
-    // block-uniform trip count (the append is block-wide); words past the end take nothing
-    for (int64_t w0 = (int64_t)blockIdx.x * kWpb; w0 < words; w0 += wstride) {
-        const int64_t w = w0 + wave_id();
+    // block-uniform trip count when the append is block-wide (words past the end take nothing);
+    // wave-staged appends let every wave run its own words
+    const int64_t wv0 = App::kWaveUniform ? wave_id() : 0;
+    for (int64_t w0 = (int64_t)blockIdx.x * kWpb + wv0; w0 < words; w0 += wstride) {
+        const int64_t w = App::kWaveUniform ? w0 : w0 + wave_id();
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t vdeg = 0;
@@ -235,15 +240,40 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
         }
         const uint64_t word = __ballot(found);
         if (lane_id() == 0 && w < words) a.bm_out[w] = word;
-        staged_append(found, (int32_t)v, vdeg, sc, a.queue_out, a.qoff_out, packed);
+        app.append(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed);
     }
 }
 
+// The two frontier appenders behind one interface: block-staged (every call block-uniform) and
+// wave-staged (every call wave-uniform; Tune::bfs_wave_stage).
+struct BlockApp {
+    static constexpr bool kWaveUniform = false;
+    StagedAppend& sa;
+    __device__ void init() { staged_init(sa); }
+    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
+        staged_append(take, v, deg, sa, q, qo, packed);
+    }
+    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { staged_flush(sa, q, qo, packed); }
+};
+struct WaveApp {
+    static constexpr bool kWaveUniform = true;
+    WaveStage& sa;
+    WaveRun run;
+    __device__ void init() {}
+    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
+        wave_stage_append(take, v, deg, sa, run, q, qo, packed);
+    }
+    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { wave_stage_final(sa, run, q, qo, packed); }
+};
+
+template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
     __shared__ long long s_nf, s_mf;
     __shared__ int s_switch;
-    __shared__ StagedAppend s_app;
+    using Stage = std::conditional_t<WAVE, WaveStage, StagedAppend>;
+    using App = std::conditional_t<WAVE, WaveApp, BlockApp>;
+    __shared__ Stage s_app;
     if (threadIdx.x == 0) {
         int64_t nf, mf;
         bool sw;
@@ -260,11 +290,12 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __syncthreads();
     if (s_st.done) return;
     unsigned long long* packed = a.ctr + a.level % kBfsRing;
-    staged_init(s_app);
-    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed, s_app);
-    else if (s_switch) bfs_bottom_up<true>(a, packed, s_app);
-    else bfs_bottom_up<false>(a, packed, s_app);
-    staged_flush(s_app, a.queue_out, a.qoff_out, packed);
+    App app{s_app};
+    app.init();
+    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed, app);
+    else if (s_switch) bfs_bottom_up<true>(a, packed, app);
+    else bfs_bottom_up<false>(a, packed, app);
+    app.final(a.queue_out, a.qoff_out, packed);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -703,7 +734,8 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             a.bm_in = sh.bfs_bm[p].get();
             a.bm_out = sh.bfs_bm[p ^ 1].get();
             if (prof_enabled(ctx)) prof_record_start(ctx, sh);
-            bfs_level_kernel<<<grid, kBlock, 0, s>>>(a);
+            if (tune().bfs_wave_stage) bfs_level_kernel<true><<<grid, kBlock, 0, s>>>(a);
+            else bfs_level_kernel<false><<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
             if (debug_bfs()) {

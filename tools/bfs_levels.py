@@ -13,7 +13,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scale", type=int, default=20)
 ap.add_argument("--runs", type=int, default=4)
 ap.add_argument("--shards", type=int, default=1, help="logical shards on device 0 (sharded DO-BFS when > 1)")
+ap.add_argument("--tune", nargs="*", default=[], help="jg_tune_set knobs, key=value")
 a = ap.parse_args()
+for kv in a.tune:
+    k, v = kv.split("=")
+    jg._lib.tune_set(k, int(v))
 ctx = jg.Context((0,) * a.shards)
 g = ctx.build_rmat(a.scale, 16, 0x5EED + a.scale, flags=jg.ADJ_BOTH)
 rng = np.random.default_rng(1)
