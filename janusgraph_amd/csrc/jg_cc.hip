@@ -120,15 +120,15 @@ __global__ __launch_bounds__(kBlock) void cc_senders_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ rp, int32_t* __restrict__ queue,
                                                             int64_t* __restrict__ qoff,
                                                             unsigned long long* __restrict__ packed) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
         const bool take = v < rows && msg[v] < kNoMsg;
-        staged_append(take, (int32_t)v, take ? rp[v + 1] - rp[v] : 0, sc, queue, qoff, packed);
+        app.append(take, (int32_t)v, take ? rp[v + 1] - rp[v] : 0, queue, qoff, packed);
     }
-    staged_flush(sc, queue, qoff, packed);
+    app.final(queue, qoff, packed);
 }
 
 struct CcPush {
@@ -145,8 +145,8 @@ struct CcPush {
 };
 
 __global__ __launch_bounds__(kBlock) void cc_push_kernel(CcPush a) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * 4;
@@ -179,10 +179,10 @@ __global__ __launch_bounds__(kBlock) void cc_push_kernel(CcPush a) {
                 const int32_t m = a.msg[u];
                 if (m < a.cand[v]) take = atomicMin(&a.cand[v], m) == kNoMsg;
             }
-            staged_append(take, v, 0, sc, a.touched, a.touched_off, a.tpacked);
+            app.append(take, v, 0, a.touched, a.touched_off, a.tpacked);
         }
     }
-    staged_flush(sc, a.touched, a.touched_off, a.tpacked);
+    app.final(a.touched, a.touched_off, a.tpacked);
 }
 
 // touched vertex v: the pull superstep's finalize with the pushed minimum

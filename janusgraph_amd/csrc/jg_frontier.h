@@ -191,4 +191,26 @@ __device__ __forceinline__ void wave_stage_final(WaveStage& sa, WaveRun& run, in
     run.n = run.ds = 0;
 }
 
+// The two frontier appenders behind one interface: block-staged (every call block-uniform) and
+// wave-staged (every call wave-uniform; Tune::bfs_wave_stage).
+struct BlockApp {
+    static constexpr bool kWaveUniform = false;
+    StagedAppend& sa;
+    __device__ void init() { staged_init(sa); }
+    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
+        staged_append(take, v, deg, sa, q, qo, packed);
+    }
+    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { staged_flush(sa, q, qo, packed); }
+};
+struct WaveApp {
+    static constexpr bool kWaveUniform = true;
+    WaveStage& sa;
+    WaveRun run;
+    __device__ void init() {}
+    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
+        wave_stage_append(take, v, deg, sa, run, q, qo, packed);
+    }
+    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { wave_stage_final(sa, run, q, qo, packed); }
+};
+
 }  // namespace jg

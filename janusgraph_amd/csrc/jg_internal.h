@@ -467,6 +467,7 @@ struct Tune {
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
+    int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
     int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only

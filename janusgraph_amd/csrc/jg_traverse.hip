@@ -244,28 +244,6 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
     }
 }
 
-// The two frontier appenders behind one interface: block-staged (every call block-uniform) and
-// wave-staged (every call wave-uniform; Tune::bfs_wave_stage).
-struct BlockApp {
-    static constexpr bool kWaveUniform = false;
-    StagedAppend& sa;
-    __device__ void init() { staged_init(sa); }
-    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
-        staged_append(take, v, deg, sa, q, qo, packed);
-    }
-    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { staged_flush(sa, q, qo, packed); }
-};
-struct WaveApp {
-    static constexpr bool kWaveUniform = true;
-    WaveStage& sa;
-    WaveRun run;
-    __device__ void init() {}
-    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
-        wave_stage_append(take, v, deg, sa, run, q, qo, packed);
-    }
-    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { wave_stage_final(sa, run, q, qo, packed); }
-};
-
 template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
@@ -330,8 +308,8 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
                                                                 const int64_t* __restrict__ deg_rp, int32_t* queue,
                                                                 int64_t* qoff, unsigned long long* packed,
                                                                 uint8_t* __restrict__ seen) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
@@ -343,9 +321,9 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
             depth[v] = take ? 0 : -1;
             seen[v] = take || deg == 0;  // BOTH: push and pull rows are the same (bfs_init_kernel)
         }
-        staged_append(take, (int32_t)v, deg, sc, queue, qoff, packed);
+        app.append(take, (int32_t)v, deg, queue, qoff, packed);
     }
-    staged_flush(sc, queue, qoff, packed);
+    app.final(queue, qoff, packed);
 }
 
 __global__ void depth_max_kernel(const int32_t* __restrict__ depth, int64_t n, int32_t* __restrict__ out) {
@@ -412,16 +390,16 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned l
                                                                 const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
                                                                 unsigned long long* __restrict__ packed) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
         const bool take = v < rows && F[v] != 0ull;
         const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
-        staged_append(take, (int32_t)v, deg, sc, queue, qoff, packed);
+        app.append(take, (int32_t)v, deg, queue, qoff, packed);
     }
-    staged_flush(sc, queue, qoff, packed);
+    app.final(queue, qoff, packed);
 }
 
 struct MsTd {
@@ -439,8 +417,8 @@ struct MsTd {
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -473,10 +451,10 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 const unsigned long long w = a.F[v] & ~a.visited[u];
                 if (w) take = atomicOr(&a.Fnext[u], w) == 0ull;
             }
-            staged_append(take, u, 0, sc, a.touched, a.touched_off, a.tpacked);
+            app.append(take, u, 0, a.touched, a.touched_off, a.tpacked);
         }
     }
-    staged_flush(sc, a.touched, a.touched_off, a.tpacked);
+    app.final(a.touched, a.touched_off, a.tpacked);
 }
 
 // touched vertex u: its new bits become its next-frontier word (and the visited / depth updates)
@@ -484,8 +462,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
                                                                 MsBfsOp op, const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
                                                                 unsigned long long* __restrict__ packed) {
-    __shared__ StagedAppend sc;
-    staged_init(sc);
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nt; x0 += stride) {  // block-uniform trips
         const int64_t x = x0 + threadIdx.x;
@@ -499,9 +477,9 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
             take = op.Fout[u] != 0ull;
             if (take) deg = push_rp[u + 1] - push_rp[u];
         }
-        staged_append(take, u, deg, sc, queue, qoff, packed);
+        app.append(take, u, deg, queue, qoff, packed);
     }
-    staged_flush(sc, queue, qoff, packed);
+    app.final(queue, qoff, packed);
 }
 
 // ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
@@ -718,7 +696,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     // 0.310 / 0.412 at 1024 / 2048 / 8192; RMAT-26 3.46 / 2.45 / 2.19 / 2.11 / 2.14 / 2.76 at 512 / 1024
     // / 4096 / 8192 / 16384 / 65536): small levels pay less per block, big ones need the parallelism
     const int64_t sq = 1ll << ((bits_for((uint64_t)std::max<int64_t>(rows - 1, 1)) + 1) / 2);
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sq, 64), tune().bfs_grid);
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sq * tune().bfs_grid_mult / 4, 64), tune().bfs_grid);
     BfsState hs{};
     int level = 0;
     for (int batch = 8;; batch = 16) {
