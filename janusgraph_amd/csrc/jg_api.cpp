@@ -482,6 +482,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().bfs_grid_mult = (int)value;
     } else if (k == "bfs_wave_stage") {
         jg::tune().bfs_wave_stage = value != 0;
+    } else if (k == "merge_interleave") {
+        jg::tune().merge_interleave = value != 0;
     } else if (k == "merge_dynamic") {
         jg::tune().merge_dynamic = value != 0;
     } else if (k == "fin_pipe") {

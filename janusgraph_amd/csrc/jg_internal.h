@@ -477,6 +477,7 @@ struct Tune {
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
                                           // stores, -1 = automatic from the band's heads per task)
+    int merge_interleave = 1;         // merge blocks take interleaved single tasks, rotating per round (0: chunks of 16)
     int merge_dynamic = 1;            // merge waves take their block's tasks from an LDS counter (0: static)
     int fin_pipe = 1;                 // split finalize: next batch's index words loaded with this batch's partials
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows

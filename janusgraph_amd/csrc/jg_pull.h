@@ -333,6 +333,7 @@ struct MergeArgs {
     int bits;
     int stage;         // LDS staging slots per wave for a task's partials (0: direct stores)
     int dynamic;       // LDS image kernels: waves take their block's tasks from an LDS counter
+    int interleave;    // a block's tasks interleaved with its sub-slice's other blocks (rotating per round)
     int diag;          // Tune::merge_diag (diagnostic timing variants; 0 in production)
 };
 
@@ -480,12 +481,19 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int64_t ntask = a.sub_base[h + 1] - base;
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
     const int64_t step = G * kMergeWaves;
-    // The block's tasks are k = g * 16 + (j mod 16) + (j / 16) * step, j = 0, 1, ...  Static: wave w
-    // takes j = w, w + 16, ...; dynamic (LDS image kernels, a.dynamic): the waves take j from the
-    // block's LDS counter, so a wave that drew cheaper tasks takes more and the round's barrier waits
-    // less for the slowest wave.  Any order gives the same result (tasks are independent).
+    // The block's j-th task, j = 0, 1, ...: interleaved (a.interleave), k = j * G + (g + rd) mod G, so
+    // the G blocks of a sub-slice differ by at most one task per round and the rotation spreads the
+    // extra tasks over the blocks round by round; otherwise chunks of 16, k = g * 16 + (j mod 16) +
+    // (j / 16) * step, which gave the low blocks up to one more chunk in every round (~4% more work
+    // by the kernel's end).  Static: wave w takes j = w, w + 16, ...; dynamic (LDS image kernels,
+    // a.dynamic): the waves take j from the block's LDS counter, so a wave that drew cheaper tasks takes
+    // more and the round's barrier waits less for the slowest wave.  Any order gives the same result
+    // (tasks are independent).
     const bool dyn = LDS && a.dynamic;
-    auto task_of = [&](int64_t j) { return (j / kMergeWaves) * step + g * kMergeWaves + (j % kMergeWaves); };
+    const int64_t grot = (g + rd) % G;
+    auto task_of = [&](int64_t j) {
+        return a.interleave ? j * G + grot : (j / kMergeWaves) * step + g * kMergeWaves + (j % kMergeWaves);
+    };
     auto grab = [&]() -> int64_t {
         uint32_t j = 0;
         if (lane == 0) j = __hip_atomic_fetch_add(tctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -858,7 +866,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                 while (stage < 2.0 * heads && stage < 256) stage *= 2;
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
-                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_diag};
+                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_interleave, tune().merge_diag};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice

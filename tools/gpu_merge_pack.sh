@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 if [ "$2" != nopytest ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || exit 3
 fi
-V="auto: b0s64:band0_bit=6 b0s16:band0_bit=4 st128:merge_stage0=128 b1s16:band1_bit=4"
+V="auto: chunk16:merge_interleave=0"
 for S in 24 26; do
   timeout -k 10 300 python -u tools/pr_ab.py --scale $S --steps 10 --rounds 3 $V > $OUT/ab_s$S.json 2> $OUT/ab_s$S.err || exit 4
 done
