@@ -857,13 +857,16 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             const SliceBand& bd = *plan.bands[bi];
             if (bd.tasks == 0) continue;
             const hipStream_t ms = (mside && bi > 0) ? mside->stream : s;
-            // staging window: -1 = automatic, the power of two >= twice the band's mean heads per task
-            // (RMAT-24 band 0 ~21 heads: 64; RMAT-26 band 0 ~73 and band 1 ~110: 256), within [64, 256]
+            // staging window: -1 = automatic, the power of two >= 4x the band's mean heads per task,
+            // within [128, 256] (RMAT-24 band 0 ~21 heads: 128; RMAT-26 band 0 ~73 and band 1 ~110:
+            // 256).  Heads per task are heavy-tailed (tasks of short sub-rows near the band's degree
+            // floor), and a task over the window stores directly: at RMAT-24 a 64-slot window was
+            // 1.6% slower than 128 although the mean is 21.
             int stage = tune().merge_stage[std::min<size_t>(bi, 3)];
             if (stage < 0) {
                 const double heads = (double)bd.subrows / (double)std::max<int64_t>(bd.tasks, 1);
-                stage = 64;
-                while (stage < 2.0 * heads && stage < 256) stage *= 2;
+                stage = 128;
+                while (stage < 4.0 * heads && stage < 256) stage *= 2;
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
                          bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_interleave, tune().merge_diag};

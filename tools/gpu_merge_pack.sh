@@ -9,10 +9,11 @@ export TMPDIR=/tmp
 if [ "$2" != nopytest ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || exit 3
 fi
-V="auto: chunk16:merge_interleave=0"
+SHARED=--shared-graph
+V="auto: s64:merge_stage0=64 s128:merge_stage0=128 s256:merge_stage0=256 auto2:"
 for S in 24 26; do
-  timeout -k 10 300 python -u tools/pr_ab.py --scale $S --steps 10 --rounds 3 $V > $OUT/ab_s$S.json 2> $OUT/ab_s$S.err || exit 4
+  timeout -k 10 300 python -u tools/pr_ab.py --scale $S --steps 10 --rounds 3 $SHARED $V > $OUT/ab_s$S.json 2> $OUT/ab_s$S.err || exit 4
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o ab -- python3 tools/pr_ab.py --scale 26 --steps 10 --rounds 1 $V > $OUT/stats.log 2>&1 || exit 5
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o ab -- python3 tools/pr_ab.py --scale 26 --steps 10 --rounds 1 $SHARED $V > $OUT/stats.log 2>&1 || exit 5
 #timeout -k 10 400 python bench.py --no-cpu > $OUT/bench.json 2> $OUT/bench.err || exit 6
 echo done

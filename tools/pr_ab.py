@@ -33,16 +33,24 @@ def main():
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shared-graph", action="store_true",
+                    help="one graph built with the defaults for every variant (run-time knobs only): the "
+                         "variants then differ by nothing but their knobs, not by the graph's memory placement")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     ctx = jg.Context((0,))
     n = 1 << args.scale
     vs = []
+    shared = None
+    if args.shared_graph:
+        apply({})
+        shared = ctx.build_rmat(args.scale, 16, 0x5EED + args.scale, flags=jg.ADJ_IN)
     for spec in args.variants:
         name, _, kv = spec.partition(":")
         knobs = {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}
         apply(knobs)
-        vs.append((name, knobs, ctx.build_rmat(args.scale, 16, 0x5EED + args.scale, flags=jg.ADJ_IN)))
+        vs.append((name, knobs, shared if shared is not None else ctx.build_rmat(args.scale, 16, 0x5EED + args.scale,
+                                                                                  flags=jg.ADJ_IN)))
     times = {name: [] for name, _, _ in vs}
     ranks = {}
     for r in range(args.rounds):
