@@ -477,6 +477,13 @@ int jg_tune_set(const char* key, int64_t value) {
         JG_ARG(value == -1 || value == 0 || value == 64 || value == 128 || value == 256 || value == 512,
                "merge_stage<i> must be -1 (automatic), 0, 64, 128, 256 or 512");
         jg::tune().merge_stage[k[11] - '0'] = (int)value;
+    } else if (k == "bfs_init_suffix") {
+        jg::tune().bfs_init_suffix = value != 0;
+    } else if (k == "bfs_grow_rule") {
+        jg::tune().bfs_grow_rule = value != 0;
+    } else if (k == "bfs_batch0") {
+        JG_ARG(value >= 1 && value <= 64, "bfs_batch0 must be in [1, 64]");
+        jg::tune().bfs_batch0 = (int)value;
     } else if (k == "bfs_grid_mult") {
         JG_ARG(value >= 1 && value <= 64, "bfs_grid_mult must be in [1, 64]");
         jg::tune().bfs_grid_mult = (int)value;

@@ -848,6 +848,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     // Classes are consecutive row ranges; any row may sit in a "wrong" lane class (only speed
     // changes), but the empty class starts strictly after the last non-empty row (correctness).
     const int64_t zero_begin = (int64_t)fb[kNumClasses];
+    csr.empty_from = zero_begin;
     plan.bands.clear();
     int64_t row_at = 0;
     for (int i = 0; i < bt.n; ++i) {

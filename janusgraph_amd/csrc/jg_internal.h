@@ -34,6 +34,9 @@ struct Csr {
     DevBuf<int32_t> col;
     DevBuf<int32_t> weight;  // optional (SD weights)
     bool sliced = false;     // entries of each row ordered by (sub_key(col), col) instead of col
+    // rows [empty_from, rows) have no entries (set with the pull plan: 1 + the last non-empty row;
+    // -1 when unknown)
+    mutable int64_t empty_from = -1;
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
 };
@@ -467,6 +470,10 @@ struct Tune {
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
+    int bfs_init_suffix = 1;          //         DO-BFS init: empty rows from the plan's empty suffix (no row_ptr reads)
+    int bfs_grow_rule = 0;            //         DO-BFS: top-down -> bottom-up only while the frontier grows
+                                      //         (measured: RMAT-26 -0.6%, RMAT-20 +2.5%; off)
+    int bfs_batch0 = 10;              //         DO-BFS: levels in the first batch (then 4, 8, 16, ...)
     int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
     int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)

@@ -104,6 +104,7 @@ struct BfsLevel {
     BfsState* st;             // [kBfsRing]
     int level, max_depth;
     double alpha, beta;
+    int grow_rule;  // switch to bottom-up only while the frontier grows (Tune::bfs_grow_rule)
 };
 
 // Direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the unexplored
@@ -126,7 +127,12 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
         c.levels = a.level;
         return c;
     }
-    if (!p.bottom_up && a.pull_rp && (!a.push_rp || (double)mf > (double)c.mu / a.alpha)) {
+    // top-down -> bottom-up only while the frontier grows (Beamer et al.: a small, shrinking frontier
+    // late in the traversal has few unexplored edges left, yet a bottom-up level would scan every
+    // unvisited row: RMAT-26's 4-vertex level took 83 us bottom-up)
+    const int64_t nf_prev = a.level >= 1 ? (int64_t)(a.ctr[(a.level + kBfsRing - 2) % kBfsRing] >> kPackShift) : 0;
+    const bool growing = !a.grow_rule || nf > nf_prev;
+    if (!p.bottom_up && a.pull_rp && (!a.push_rp || ((double)mf > (double)c.mu / a.alpha && growing))) {
         c.bottom_up = 1;
         *switch_in = true;  // the previous frontier exists only as a queue: test depth == level instead
     } else if (p.bottom_up && a.push_rp && (double)nf < (double)a.rows / a.beta) {
@@ -283,13 +289,16 @@ __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
 // depth = -1 except the source; level -1 state: nothing explored, the source is the frontier.
 // A vertex with an empty pull row can never be reached: its seen byte starts set, so no bottom-up
 // level looks at it again (its depth stays -1).
+// empty_from >= 0: rows from there on are the empty suffix (no row_ptr reads; at RMAT-26 reading the
+// 537 MB row_ptr made this kernel 158 us of a 2.1 ms traversal).
 __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64_t source, int32_t* queue,
                                 int64_t* qoff, const int64_t* __restrict__ deg_rp, long long total,
                                 unsigned long long* ctr, BfsState* st, uint8_t* __restrict__ seen,
-                                const int64_t* __restrict__ pull_rp) {
+                                const int64_t* __restrict__ pull_rp, int64_t empty_from) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
         depth[i] = i == source ? 0 : -1;
-        seen[i] = i == source || (pull_rp && pull_rp[i + 1] == pull_rp[i]);
+        const bool empty = empty_from >= 0 ? i >= empty_from : (pull_rp && pull_rp[i + 1] == pull_rp[i]);
+        seen[i] = i == source || empty;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         queue[0] = (int32_t)source;
@@ -674,7 +683,8 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(),
                                                           sh.bfs_qoff[0].get(), degcsr->row_ptr.get(),
                                                           (long long)degcsr->nnz, sh.bfs_ctr.get(), st,
-                                                          sh.bfs_seen.get(), pull ? pull->row_ptr.get() : nullptr);
+                                                          sh.bfs_seen.get(), pull ? pull->row_ptr.get() : nullptr,
+                                                          pull && tune().bfs_init_suffix ? pull->empty_from : -1);
     }
     JG_LAUNCH_CHECK();
     BfsLevel a{};
@@ -691,6 +701,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.max_depth = max_depth;
     a.alpha = (double)(roots ? tune().bfs_alpha : tune().dobfs_alpha);
     a.beta = (double)tune().bfs_beta;
+    a.grow_rule = tune().bfs_grow_rule;
     // a fixed grid, both directions grid-stride: ~sqrt(rows) workgroups (tools/bfs_sweep.py, ms per
     // traversal: RMAT-20 0.164 / 0.141 / 0.140 / 0.157 at 256 / 512 / 1024 / 4096; RMAT-22 0.311 /
     // 0.310 / 0.412 at 1024 / 2048 / 8192; RMAT-26 3.46 / 2.45 / 2.19 / 2.11 / 2.14 / 2.76 at 512 / 1024
@@ -699,7 +710,12 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sq * tune().bfs_grid_mult / 4, 64), tune().bfs_grid);
     BfsState hs{};
     int level = 0;
-    for (int batch = 8;; batch = 16) {
+    // Levels are enqueued in batches, the host reading the device state once per batch: first
+    // bfs_batch0 (RMAT traversals end within ~10 levels plus the one that finds the frontier empty),
+    // then 4, 8, 16, ... (levels past the end are launched anyway and cost ~4 us each: a second batch
+    // of 16 after 8 wasted ~14 of them at RMAT-26)
+    int next_batch = 4;
+    for (int batch = std::max(1, tune().bfs_batch0);; batch = next_batch, next_batch = std::min(next_batch * 2, 64)) {
         if (max_depth >= 0) batch = std::min(batch, max_depth + 1 - level);
         if (batch <= 0) fail(JG_ERR_STATE, "BFS level control did not terminate");  // level max_depth stops
         for (int k = 0; k < batch; ++k, ++level) {
