@@ -48,6 +48,7 @@
 #ifndef JANUSGPU_H
 #define JANUSGPU_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -129,6 +130,21 @@ int jg_ctx_create(const int* devices, int ndev, jg_ctx** out);
 #define JG_UNIQUE_ID_BYTES 128
 int jg_comm_unique_id(void* out /* JG_UNIQUE_ID_BYTES */);
 int jg_ctx_create_rank(int device, int nranks, int rank, const void* unique_id, jg_ctx** out);
+/* The same rank mode over a caller-supplied host transport instead of RCCL: every exchange step is
+ * staged through host memory and handed to these callbacks (synchronous, called by every rank in
+ * the same order).  For tests of the multi-process control flow where RCCL cannot run (two ranks
+ * on one GPU); the same code paths build, plan, pack and place the data as with RCCL.
+ *   allgather: out[r * bytes .. (r + 1) * bytes) = rank r's `in`, for every rank r.
+ *   exchange:  send[i] (send_bytes[i] bytes) to rank send_peer[i]; receive recv_bytes[i] bytes from
+ *              rank recv_peer[i] into recv[i].  Zero-byte transfers are not listed.
+ * Callbacks return 0 on success.  `t` is copied; `t->user` is passed back untouched. */
+typedef struct jg_transport {
+    void* user;
+    int (*allgather)(void* user, const void* in, void* out, size_t bytes);
+    int (*exchange)(void* user, int nsend, const int* send_peer, const void* const* send, const size_t* send_bytes,
+                    int nrecv, const int* recv_peer, void* const* recv, const size_t* recv_bytes);
+} jg_transport;
+int jg_ctx_create_rank_transport(int device, int nranks, int rank, const jg_transport* t, jg_ctx** out);
 int jg_ctx_destroy(jg_ctx* ctx);
 int jg_ctx_last_stats(const jg_ctx* ctx, jg_stats* out);
 /* Record HIP events around every launch of the dominant kernel (costs ~1 us per launch). */

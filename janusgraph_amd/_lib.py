@@ -33,6 +33,7 @@ UNIQUE_ID_BYTES = 128
 # every function the header declares (checked by tests/test_abi.py against include/janusgpu.h)
 EXPORTS = [
     "jg_abi_version", "jg_last_error", "jg_ctx_create", "jg_comm_unique_id", "jg_ctx_create_rank",
+    "jg_ctx_create_rank_transport",
     "jg_ctx_destroy", "jg_ctx_last_stats", "jg_ctx_set_profiling", "jg_graph_build", "jg_graph_build_edgestore",
     "jg_graph_build_rmat",
     "jg_graph_info_get", "jg_graph_destroy", "jg_pagerank", "jg_pagerank_begin", "jg_pagerank_step",
@@ -67,6 +68,53 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+# jg_transport (include/janusgpu.h): a host transport for rank mode without RCCL (tests)
+_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
+                                ctypes.POINTER(ctypes.c_size_t))
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", _ALLGATHER_FN), ("exchange", _EXCHANGE_FN)]
+
+
+def _make_transport(obj):
+    """Wrap an object with allgather(data: bytes) -> bytes (every rank's data, rank order) and
+    exchange(sends: [(peer, bytes)], recvs: [(peer, nbytes)]) -> [bytes] into a jg_transport.
+    Returns (struct, keep-alive references)."""
+    import traceback
+
+    def allgather(user, inp, out, nbytes):
+        try:
+            got = obj.allgather(ctypes.string_at(inp, nbytes) if nbytes else b"")
+            if len(got) % max(nbytes, 1) != 0:
+                return 2
+            ctypes.memmove(out, got, len(got))
+            return 0
+        except Exception:  # an exception must not cross the C frames
+            traceback.print_exc()
+            return 1
+
+    def exchange(user, ns, sp, sbuf, sbytes, nr, rp, rbuf, rbytes):
+        try:
+            sends = [(int(sp[i]), ctypes.string_at(sbuf[i], sbytes[i])) for i in range(ns)]
+            recvs = [(int(rp[i]), int(rbytes[i])) for i in range(nr)]
+            got = obj.exchange(sends, recvs)
+            for i in range(nr):
+                if len(got[i]) != rbytes[i]:
+                    return 2
+                ctypes.memmove(rbuf[i], got[i], rbytes[i])
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    fa, fe = _ALLGATHER_FN(allgather), _EXCHANGE_FN(exchange)
+    return Transport(None, fa, fe), (fa, fe, obj)
+
+
 class JanusGpuError(RuntimeError):
     """A non-zero status from libjanusgpu (the Java side wraps these in JanusGraphException)."""
 
@@ -97,6 +145,8 @@ def load():
         "jg_ctx_create": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int, _PP], ctypes.c_int),
         "jg_comm_unique_id": ([_P], ctypes.c_int),
         "jg_ctx_create_rank": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _PP], ctypes.c_int),
+        "jg_ctx_create_rank_transport": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Transport), _PP],
+                                         ctypes.c_int),
         "jg_ctx_destroy": ([_P], ctypes.c_int),
         "jg_ctx_last_stats": ([_P, ctypes.POINTER(Stats)], ctypes.c_int),
         "jg_ctx_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
@@ -164,12 +214,22 @@ def comm_unique_id() -> bytes:
 
 
 class Context:
-    """jg_ctx: one process driving `devices` (sharded 1D when several), or rank `rank` of `nranks`."""
+    """jg_ctx: one process driving `devices` (sharded 1D when several), or rank `rank` of `nranks`
+    (over RCCL with `unique_id`, or over a host `transport`: see _make_transport).  In rank mode every
+    per-vertex output holds this rank's vertices only; the others keep NaN / the integer fill
+    (INT32_MIN for depths, INT64_MAX for int64 outputs)."""
 
-    def __init__(self, devices=(0,), rank=None, nranks=1, unique_id=None):
+    def __init__(self, devices=(0,), rank=None, nranks=1, unique_id=None, transport=None):
         L = load()
         self._h = ctypes.c_void_p()
-        if rank is None:
+        self.nranks = int(nranks) if rank is not None else 1
+        if transport is not None:
+            if rank is None:
+                raise ValueError("a transport needs rank and nranks")
+            self._tr, self._tr_keep = _make_transport(transport)
+            check(L.jg_ctx_create_rank_transport(int(devices[0]), int(nranks), int(rank), ctypes.byref(self._tr),
+                                                 ctypes.byref(self._h)))
+        elif rank is None:
             devs = (ctypes.c_int * len(devices))(*devices)
             check(L.jg_ctx_create(devs, len(devices), ctypes.byref(self._h)))
         else:
@@ -348,6 +408,14 @@ class Graph:
     def __init__(self, ctx: Context, handle, n):
         self.ctx, self._h, self.n = ctx, handle, n
 
+    def _out(self, size, dtype):
+        """An output array; in rank mode pre-filled so the other ranks' vertices are recognisable."""
+        if getattr(self.ctx, "nranks", 1) <= 1:
+            return np.empty(size, dtype)
+        fill = np.nan if np.issubdtype(dtype, np.floating) else (
+            np.iinfo(dtype).min if np.dtype(dtype) == np.int32 else np.iinfo(dtype).max)
+        return np.full(size, fill, dtype)
+
     def close(self):
         if self._h:
             check(load().jg_graph_destroy(self._h))
@@ -375,8 +443,8 @@ class Graph:
         return out[:count]
 
     def pagerank(self, damping=0.85, vertex_count=1, iterations=10):
-        rank = np.empty(self.n, np.float64)
-        ec = np.empty(self.n, np.float64)
+        rank = self._out(self.n, np.float64)
+        ec = self._out(self.n, np.float64)
         check(load().jg_pagerank(self._h, float(damping), int(vertex_count), int(iterations), _ptr(rank), _ptr(ec)))
         return rank, ec
 
@@ -387,19 +455,19 @@ class Graph:
         check(load().jg_pagerank_step(self._h, int(nsteps)))
 
     def pagerank_end(self, want=True):
-        rank = np.empty(self.n, np.float64) if want else None
-        ec = np.empty(self.n, np.float64) if want else None
+        rank = self._out(self.n, np.float64) if want else None
+        ec = self._out(self.n, np.float64) if want else None
         check(load().jg_pagerank_end(self._h, _ptr(rank), _ptr(ec)))
         return rank, ec
 
     def shortest_distance(self, seed_vid, max_depth):
-        dist = np.empty(self.n, np.int64)
+        dist = self._out(self.n, np.int64)
         check(load().jg_shortest_distance(self._h, int(seed_vid), int(max_depth), _ptr(dist)))
         return dist
 
     def bfs(self, sources, direction=DIR_BOTH, max_depth=-1, want=True):
         src = np.ascontiguousarray(np.atleast_1d(sources), np.int64)
-        depth = np.empty(len(src) * self.n, np.int32) if want else None
+        depth = self._out(len(src) * self.n, np.int32) if want else None
         check(load().jg_bfs(self._h, _ptr(src), len(src), int(direction), int(max_depth), _ptr(depth)))
         return None if depth is None else depth.reshape(len(src), self.n)
 
@@ -416,7 +484,7 @@ class Graph:
         return out[:self.n], rec[:self.n].astype(bool)
 
     def connected_components(self):
-        comp = np.empty(self.n, np.int64)
+        comp = self._out(self.n, np.int64)
         it = ctypes.c_int32(0)
         check(load().jg_connected_components(self._h, _ptr(comp), ctypes.byref(it)))
         return comp, int(it.value)

@@ -40,10 +40,37 @@ int64_t Graph::dense_of_vid(int64_t v) const {
     return sorted_dense[(size_t)(it - sorted_vid.begin())];
 }
 
+void transport_check(int rc, const char* what) {
+    if (rc != 0) fail(JG_ERR_RCCL, std::string("host transport ") + what + " failed (" + std::to_string(rc) + ")");
+}
+
+void host_allgather(Ctx& c, const void* in, void* out, size_t bytes) {
+    transport_check(c.transport.allgather(c.transport.user, in, out, bytes), "allgather");
+}
+
+void host_exchange(Ctx& c, const std::vector<int>& speer, const std::vector<const void*>& sbuf,
+                   const std::vector<size_t>& sbytes, const std::vector<int>& rpeer, const std::vector<void*>& rbuf,
+                   const std::vector<size_t>& rbytes) {
+    transport_check(c.transport.exchange(c.transport.user, (int)speer.size(), speer.data(), sbuf.data(), sbytes.data(),
+                                         (int)rpeer.size(), rpeer.data(), rbuf.data(), rbytes.data()),
+                    "exchange");
+}
+
 void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
     if (g.P == 1) return;
     Ctx& c = *g.ctx;
     const size_t slice = (size_t)g.S * elem_bytes;
+    if (c.host_transport) {  // rank mode over host callbacks: one shard per process
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh.device);
+        std::vector<char> mine(slice), all(slice * (size_t)c.nranks);
+        char* base = static_cast<char*>(bufs[0]);
+        copy_d2h(mine.data(), base + (size_t)sh.index * slice, slice, sh.stream);
+        host_allgather(c, mine.data(), all.data(), slice);
+        for (int r = 0; r < c.nranks; ++r)
+            if (r != sh.index) copy_h2d(base + (size_t)r * slice, all.data() + (size_t)r * slice, slice, sh.stream);
+        return;
+    }
     if (c.logical) {  // all shards on one device and stream: device copies of the owned slices
         Shard& s0 = *g.shards[0];
         DeviceGuard dg(s0.device);
@@ -74,6 +101,12 @@ int allreduce_or(Graph& g, int flag) {
     if (c.nranks == 1) return flag;  // in-process shards already combined by the caller
     Shard& sh = *g.shards[0];
     DeviceGuard dg(sh.device);
+    if (c.host_transport) {
+        const int32_t mine = flag ? 1 : 0;
+        std::vector<int32_t> all((size_t)c.nranks);
+        host_allgather(c, &mine, all.data(), sizeof mine);
+        return *std::max_element(all.begin(), all.end());
+    }
     DevBuf<int32_t> d(1);
     int32_t v = flag ? 1 : 0;
     JG_HIP(hipMemcpyAsync(d.get(), &v, sizeof v, hipMemcpyHostToDevice, sh.stream));
@@ -88,6 +121,16 @@ void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
     if (c.nranks == 1) return;  // in-process shards already summed by the caller
     Shard& sh = *g.shards[0];
     DeviceGuard dg(sh.device);
+    if (c.host_transport) {
+        std::vector<int64_t> all((size_t)n * c.nranks);
+        host_allgather(c, vals, all.data(), (size_t)n * sizeof(int64_t));
+        for (int i = 0; i < n; ++i) {
+            int64_t t = 0;
+            for (int r = 0; r < c.nranks; ++r) t += all[(size_t)r * n + i];
+            vals[i] = t;
+        }
+        return;
+    }
     DevBuf<int64_t> d(n);
     JG_HIP(hipMemcpyAsync(d.get(), vals, n * sizeof(int64_t), hipMemcpyHostToDevice, sh.stream));
     rccl_check(ncclAllReduce(d.get(), d.get(), (size_t)n, ncclInt64, ncclSum, sh.comm, sh.stream), "ncclAllReduce");
@@ -583,6 +626,29 @@ int jg_ctx_create_rank(int device, int nranks, int rank, const void* unique_id, 
         jg::rccl_check(ncclCommInitRank(&comm, nranks, id, rank), "ncclCommInitRank");
         c.comms.push_back(comm);
     }
+    *out = ctx.release();
+    JG_GUARD_END
+}
+
+int jg_ctx_create_rank_transport(int device, int nranks, int rank, const jg_transport* t, jg_ctx** out) {
+    JG_GUARD_BEGIN
+    JG_ARG(out && nranks >= 1 && rank >= 0 && rank < nranks, "jg_ctx_create_rank_transport: bad rank arguments");
+    JG_ARG(t && t->allgather && t->exchange, "jg_ctx_create_rank_transport: transport callbacks required");
+    *out = nullptr;
+    int count = 0;
+    JG_HIP(hipGetDeviceCount(&count));
+    JG_ARG(device >= 0 && device < count, "jg_ctx_create_rank_transport: device ordinal out of range");
+    auto ctx = std::make_unique<jg_ctx>();
+    jg::Ctx& c = ctx->impl;
+    c.devices = {device};
+    c.nranks = nranks;
+    c.rank = rank;
+    c.host_transport = nranks > 1;
+    c.transport = *t;
+    jg::DeviceGuard dg(device);
+    hipStream_t s = nullptr;
+    JG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    c.streams.push_back(s);
     *out = ctx.release();
     JG_GUARD_END
 }

@@ -184,11 +184,15 @@ void check_halo_counts(Graph& g, uint32_t adj) {
             const Halo& h = g.halo(*g.shards[i], adj);
             for (int p = 0; p < P; ++p) mine[i * P + p] = h.send_off[p + 1] - h.send_off[p];
         }
+        if (c.host_transport) {
+            host_allgather(c, mine.data(), counts.data(), per * sizeof(int64_t));
+        } else {
         DevBuf<int64_t> d(per * c.nranks);
         copy_h2d(d.get() + (size_t)c.rank * per, mine.data(), per * sizeof(int64_t), sh0.stream);
         rccl_check(ncclAllGather(d.get() + (size_t)c.rank * per, d.get(), per, ncclInt64, sh0.comm, sh0.stream),
                    "ncclAllGather(halo counts)");
         copy_d2h(counts.data(), d.get(), counts.size() * sizeof(int64_t), sh0.stream);
+        }
     }
     for (auto& sp : g.shards) {
         const Halo& h = g.halo(*sp, adj);
@@ -245,6 +249,37 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
         }
         return;
     }
+    if (c.host_transport) {  // rank mode over host callbacks (one shard per process): staged runs
+        Shard& sh = *g.shards[0];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh.device);
+        std::vector<char> sbuf((size_t)h.send_off[g.P] * elem_bytes);
+        copy_d2h(sbuf.data(), h.send_buf.get(), sbuf.size(), sh.stream);  // after the pack kernel
+        std::vector<int> sp, rp;
+        std::vector<const void*> sv;
+        std::vector<void*> rv;
+        std::vector<size_t> sb, rb;
+        std::vector<std::vector<char>> rbufs;
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t ns = h.send_off[q + 1] - h.send_off[q];
+            const int64_t nr = h.recv_off[q + 1] - h.recv_off[q];
+            if (ns > 0) {
+                sp.push_back(q);
+                sv.push_back(sbuf.data() + h.send_off[q] * elem_bytes);
+                sb.push_back((size_t)ns * elem_bytes);
+            }
+            if (nr > 0) {
+                rp.push_back(q);
+                rbufs.emplace_back((size_t)nr * elem_bytes);
+                rb.push_back((size_t)nr * elem_bytes);
+            }
+        }
+        for (auto& b : rbufs) rv.push_back(b.data());
+        host_exchange(c, sp, sv, sb, rp, rv, rb);
+        for (size_t k = 0; k < rp.size(); ++k) copy_h2d(seg_ptr(0, rp[k]), rv[k], rb[k], sh.stream);
+        return;
+    }
     rccl_check(ncclGroupStart(), "ncclGroupStart");
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
@@ -290,6 +325,38 @@ void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std
                                       n * elem_bytes, hipMemcpyDeviceToDevice, s0.stream));
             }
         }
+        return;
+    }
+    if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
+        Shard& sh = *g.shards[0];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh.device);
+        std::vector<int> sp, rp;
+        std::vector<const void*> sv;
+        std::vector<void*> rv;
+        std::vector<size_t> sb, rb;
+        std::vector<std::vector<char>> sbufs, hrecv;
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t ns = h.recv_off[q + 1] - h.recv_off[q];  // my segment for q goes back to q
+            const int64_t nr = h.send_off[q + 1] - h.send_off[q];  // q's segment for me comes back
+            if (ns > 0) {
+                sp.push_back(q);
+                sbufs.emplace_back((size_t)ns * elem_bytes);
+                copy_d2h(sbufs.back().data(), seg_ptr(0, q), sbufs.back().size(), sh.stream);
+                sb.push_back(sbufs.back().size());
+            }
+            if (nr > 0) {
+                rp.push_back(q);
+                hrecv.emplace_back((size_t)nr * elem_bytes);
+                rb.push_back((size_t)nr * elem_bytes);
+            }
+        }
+        for (auto& b : sbufs) sv.push_back(b.data());
+        for (auto& b : hrecv) rv.push_back(b.data());
+        host_exchange(c, sp, sv, sb, rp, rv, rb);
+        for (size_t k = 0; k < rp.size(); ++k)
+            copy_h2d(static_cast<char*>(rbufs[0]) + h.send_off[rp[k]] * elem_bytes, rv[k], rb[k], sh.stream);
         return;
     }
     rccl_check(ncclGroupStart(), "ncclGroupStart");

@@ -274,6 +274,8 @@ struct Ctx {
     int rank = 0;
     bool logical = false;       // several shards on one device: exchange by device copies
     std::vector<ncclComm_t> comms;
+    bool host_transport = false;  // rank mode over jg_transport callbacks (tests) instead of RCCL
+    jg_transport transport{};
     std::vector<hipStream_t> streams;
     bool profiling = false;
     jg_stats last{};
@@ -495,6 +497,11 @@ struct Tune {
                                       // stream cost +28% / +10% in the band 0 / 1 merges at RMAT-26)
 };
 Tune& tune();
+// rank mode over jg_transport callbacks (jg_api.cpp)
+void host_allgather(Ctx& c, const void* in, void* out, size_t bytes);
+void host_exchange(Ctx& c, const std::vector<int>& speer, const std::vector<const void*>& sbuf,
+                   const std::vector<size_t>& sbytes, const std::vector<int>& rpeer, const std::vector<void*>& rbuf,
+                   const std::vector<size_t>& rbytes);
 int device_cu_count();  // compute units of the current device
 // A second stream of the current device (created on first use, lives for the process) with a fork
 // and a join event: work independent of the main stream's runs beside it, e.g. the light rows of a

@@ -1,0 +1,139 @@
+"""Rank mode (one process per shard) driven through the library's multi-process code paths on one GPU.
+
+RCCL refuses two ranks on one device, so the driver's 8-GPU run is the only place its send/recv can
+execute.  Here two processes share device 0 and the library's exchanges go through a host transport
+(jg_ctx_create_rank_transport, gloo underneath): the same rank-mode build (each process builds only
+its shard), halo-plan count check, pack kernels, segment placement, reverse exchange and all-reduces
+as with RCCL, checked against the oracle.  Per-vertex outputs hold each rank's own vertices; rank 0
+combines them.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class GlooTransport:
+    """allgather / exchange of the jg_transport contract over torch.distributed (gloo, CPU)."""
+
+    def __init__(self, dist, world):
+        self.dist, self.world = dist, world
+
+    def allgather(self, data):
+        import torch
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else torch.empty(0, dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return b"".join(o.numpy().tobytes() for o in out)
+
+    def exchange(self, sends, recvs):
+        import torch
+        reqs, outs = [], []
+        for peer, b in sends:
+            reqs.append(self.dist.isend(torch.frombuffer(bytearray(b), dtype=torch.uint8), peer))
+        for peer, nbytes in recvs:
+            t = torch.empty(nbytes, dtype=torch.uint8)
+            reqs.append(self.dist.irecv(t, peer))
+            outs.append(t)
+        for r in reqs:
+            r.wait()
+        return [t.numpy().tobytes() for t in outs]
+
+
+def _combine(dist, world, a, fill):
+    """Every rank's array element-wise: each vertex is filled by exactly one rank."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    out = np.array(a, copy=True)
+    owned = np.zeros(len(a), np.int32)
+    for p in parts:
+        p = p.numpy()
+        mine = ~np.isnan(p) if np.issubdtype(p.dtype, np.floating) else p != fill
+        out[mine] = p[mine]
+        owned += mine
+    return out, owned
+
+
+def _worker(rank, world, port, halo, errfile):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import janusgraph_amd as jg
+        from janusgraph_amd import _lib
+        from oracle import oracle as o
+        _lib.tune_set("halo", halo)
+        scale = 12
+        n = 1 << scale
+        s, d = o.rmat_edges(scale, 16, 7)
+        vid = (np.arange(n, dtype=np.int64) + 1) << 8
+        ctx = jg.Context((0,), rank=rank, nranks=world, transport=GlooTransport(dist, world))
+        w = (np.arange(len(s)) % 5 + 1).astype(np.int32)
+        g = ctx.build(vid, vid[s], vid[d], weight=w, flags=jg.ADJ_IN | jg.ADJ_OUT | jg.ADJ_BOTH)
+        assert g.info()["num_shards"] == world
+        pr, _ = g.pagerank(0.85, n, 12)
+        pr, own_pr = _combine(dist, world, pr, None)
+        comp, it = g.connected_components()
+        comp, own_cc = _combine(dist, world, comp, np.iinfo(np.int64).max)
+        src = int(s[0])
+        depth = g.bfs([vid[src]], jg.DIR_BOTH)[0]
+        depth, own_d = _combine(dist, world, depth, np.iinfo(np.int32).min)
+        sd = own_sd = None
+        if halo:  # sharded shortest distance runs over the halo plan only
+            sd = g.shortest_distance(vid[src], 6)
+            sd, own_sd = _combine(dist, world, sd, np.iinfo(np.int64).max)
+        if rank == 0:
+            assert (own_pr == 1).all() and (own_cc == 1).all() and (own_d == 1).all(), "every vertex owned once"
+            ds, dd = s.astype(np.int32), d.astype(np.int32)
+            ref, _ = o.pagerank(n, ds, dd, 0.85, n, 12)
+            rel = np.abs(pr - ref) / np.abs(ref)
+            assert rel.max() <= 1e-9, f"PageRank parity {rel.max()}"
+            cref, cit = o.connected_components(n, ds, dd, vid)
+            np.testing.assert_array_equal(comp, cref)
+            assert it == cit, (it, cit)
+            np.testing.assert_array_equal(depth, o.bfs(n, ds, dd, src, o.DIR_BOTH))
+            if sd is not None:
+                assert (own_sd == 1).all()
+                np.testing.assert_array_equal(sd, o.shortest_distance(n, ds, dd, src, 6, w))
+        g.close()
+        ctx.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}:\n" + traceback.format_exc())
+        raise
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,halo", [(2, 1), (2, 0), (3, 1)])
+def test_ranks_over_host_transport(tmp_path, world, halo):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errfile = str(tmp_path / "err.txt")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, halo, errfile)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    err = open(errfile).read() if os.path.exists(errfile) else ""
+    assert all(p.exitcode == 0 for p in procs), f"exit codes {[p.exitcode for p in procs]}\n{err}"
