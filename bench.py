@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--no-big", action="store_true", help="skip the RMAT-26 blocks (PageRank, BFS, CC, MS-BFS)")
     p.add_argument("--big-scale", type=int, default=26)
     p.add_argument("--big-steps", type=int, default=10)
+    p.add_argument("--host-transport", action="store_true",
+                   help="N > 1 rehearsal on one GPU: every rank on device 0, exchanges over gloo through the "
+                        "library's host transport instead of RCCL (not a performance measurement)")
     return p.parse_args()
 
 
@@ -271,9 +274,13 @@ def main():
     ctl = Control(ws, rank)
     import janusgraph_amd as jg
 
-    uid = jg._lib.comm_unique_id() if (ws > 1 and rank == 0) else None
-    uid = ctl.bcast_bytes(uid)
-    ctx = jg.Context((local,), rank=rank if ws > 1 else None, nranks=ws, unique_id=uid)
+    if ws > 1 and args.host_transport:
+        from janusgraph_amd.transport import GlooTransport
+        ctx = jg.Context((0,), rank=rank, nranks=ws, transport=GlooTransport(ctl.dist, ws))
+    else:
+        uid = jg._lib.comm_unique_id() if (ws > 1 and rank == 0) else None
+        uid = ctl.bcast_bytes(uid)
+        ctx = jg.Context((local,), rank=rank if ws > 1 else None, nranks=ws, unique_id=uid)
     n = 1 << args.scale
     m = args.edgefactor << args.scale
 
@@ -342,7 +349,9 @@ def main():
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (Graph500 Kronecker RMAT, on-device generator)",
             "config": {"workload": workload, "n": n, "m": m,
-                       "parallelism": f"1d-vertex-partition x{ws}, RCCL halo send/recv" if ws > 1 else "single GPU",
+                       "parallelism": (f"1d-vertex-partition x{ws}, " + ("host-transport rehearsal on one GPU (not a "
+                                       "measurement)" if args.host_transport else "RCCL halo send/recv"))
+                       if ws > 1 else "single GPU",
                        "build_ms": round(build_ms, 1), "truncated_vertices": info["truncated_vertices"],
                        "in_entries": in_nnz},
             "roofline": roofline, "cpu_baseline": cpu,

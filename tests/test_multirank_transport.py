@@ -17,33 +17,6 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-class GlooTransport:
-    """allgather / exchange of the jg_transport contract over torch.distributed (gloo, CPU)."""
-
-    def __init__(self, dist, world):
-        self.dist, self.world = dist, world
-
-    def allgather(self, data):
-        import torch
-        t = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else torch.empty(0, dtype=torch.uint8)
-        out = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t)
-        return b"".join(o.numpy().tobytes() for o in out)
-
-    def exchange(self, sends, recvs):
-        import torch
-        reqs, outs = [], []
-        for peer, b in sends:
-            reqs.append(self.dist.isend(torch.frombuffer(bytearray(b), dtype=torch.uint8), peer))
-        for peer, nbytes in recvs:
-            t = torch.empty(nbytes, dtype=torch.uint8)
-            reqs.append(self.dist.irecv(t, peer))
-            outs.append(t)
-        for r in reqs:
-            r.wait()
-        return [t.numpy().tobytes() for t in outs]
-
-
 def _combine(dist, world, a, fill):
     """Every rank's array element-wise: each vertex is filled by exactly one rank."""
     import torch
@@ -69,6 +42,7 @@ def _worker(rank, world, port, halo, errfile):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import janusgraph_amd as jg
         from janusgraph_amd import _lib
+        from janusgraph_amd.transport import GlooTransport
         from oracle import oracle as o
         _lib.tune_set("halo", halo)
         scale = 12

@@ -1,0 +1,11 @@
+#!/bin/bash
+# bench.py's N > 1 path rehearsed on one GPU: N ranks under torch.distributed.run, every rank on
+# device 0, exchanges over gloo through the library's host transport (not a measurement).
+set -o pipefail
+OUT=gpurun_out/${1:-rehearsal}
+mkdir -p $OUT
+export TMPDIR=/tmp
+for N in 2 8; do
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29500 + N)) bench.py --gpus $N --steps 3 --warmup 1 --host-transport --no-cpu > $OUT/bench_n$N.json 2> $OUT/bench_n$N.err || exit 3
+done
+echo ok
