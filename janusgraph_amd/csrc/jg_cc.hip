@@ -310,62 +310,53 @@ __global__ __launch_bounds__(kBlock) void uf_minrank_kernel(const int32_t* __res
     }
 }
 
-// src[v] = v for its component's minimum-rank vertex (the BFS sources), -1 otherwise
-__global__ void uf_sources_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ rank,
-                                  const int32_t* __restrict__ minr, int64_t rows, int32_t* __restrict__ src) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
-        src[v] = rank[v] == minr[parent[v]] ? (int32_t)v : -1;
-}
-
-// label[v] = its component's minimum rank (in place over the ranks)
-__global__ void uf_labels_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ minr, int64_t rows,
-                                 int32_t* __restrict__ label) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
-        label[v] = minr[parent[v]];
-}
-
 // the number of rows of degree >= 64 (rows are degree-sorted: a binary search of the row offsets)
-__global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, unsigned long long* __restrict__ out) {
+__global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, int32_t* __restrict__ out) {
     int64_t lo = 0, hi = rows;  // first row of degree < 64
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         if (rp[mid + 1] - rp[mid] >= kWave) lo = mid + 1; else hi = mid;
     }
-    *out = (unsigned long long)lo;
+    *out = (int32_t)lo;
 }
 
 // Union-find labels and the BFS superstep count on one shard; false (labels untouched) if the count
-// reaches the superstep cap.
-bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations) {
+// reaches the superstep cap.  On success *labels points at the labels (the parent array, rewritten).
+// The union-find runs over the rows that have an edge (those before Csr::empty_from): an edgeless row
+// is its own component, with its own rank as label, and is never linked.
+bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
     constexpr int kFirst = 2;
     if (rows == 0) {
         *iterations = 0;
+        *labels = sh.cc_label.get();
         return true;
     }
-    // scratch: the message vectors (re-initialised if the propagation has to run), two rows arrays
-    // kept with the shard
+    const int64_t ne = c.empty_from >= 0 ? std::min(c.empty_from, rows) : rows;
+    // scratch: the message vectors (re-initialised if the propagation has to run), a rows array kept
+    // with the shard
     int32_t* parent = sh.cc_msg[0].get();
     int32_t* minr = sh.cc_msg[1].get();
-    for (auto& b : sh.cc_aux)
-        if ((int64_t)b.size() < rows) b.alloc(rows);
-    int32_t* src = sh.cc_aux[0].get();
-    DevBuf<int32_t> sample(1024);
-    DevBuf<unsigned long long> cnt(1);
-    int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
-    uf_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, minr, rows);
+    if ((int64_t)sh.cc_depth.size() < rows) sh.cc_depth.alloc(rows);
+    DevBuf<int32_t> sample(1025);  // 1024 sampled roots, then the heavy-row count
+    const int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
+    uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
     JG_LAUNCH_CHECK();
-    uf_link_first_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), rows, kFirst);
+    uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, kFirst);
     JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rows);
+    uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
     JG_LAUNCH_CHECK();
     // the most frequent root among 1024 sampled vertices: the giant component's
-    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, rows, 1024, sample.get());
+    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, std::max<int64_t>(ne, 1), 1024, sample.get());
     JG_LAUNCH_CHECK();
-    std::vector<int32_t> hs(1024);
+    heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), ne, sample.get() + 1024);
+    JG_LAUNCH_CHECK();
+    std::vector<int32_t> hs(1025);
     copy_d2h(hs.data(), sample.get(), hs.size() * sizeof(int32_t), s);
+    const int64_t heavy = hs[1024];
+    hs.pop_back();
     std::sort(hs.begin(), hs.end());
     int32_t giant = hs[0];
     size_t best = 0;
@@ -378,26 +369,20 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations) {
         }
         i = j;
     }
-    heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), rows, cnt.get());
+    uf_link_rest_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
+                                                        giant);
     JG_LAUNCH_CHECK();
-    unsigned long long heavy = 0;
-    copy_d2h(&heavy, cnt.get(), sizeof heavy, s);
-    uf_link_rest_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), rows, (int64_t)heavy,
-                                                          kFirst, giant);
+    uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
     JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rows);
+    uf_minrank_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
-    uf_minrank_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rank, rows, giant, minr);
-    JG_LAUNCH_CHECK();
-    uf_sources_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, rank, minr, rows, src);
-    JG_LAUNCH_CHECK();
-    const int d = cc_root_eccentricity(ctx, sh, src, sh.cc_aux[1].get());
+    // the BFS start picks the sources and rewrites parent into the labels
+    const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get());
     const int it = c.nnz > 0 ? d + 1 : 0;
     if (it > kCcMaxIterations - 1) return false;
-    uf_labels_kernel<<<grid_for(rows), kBlock, 0, s>>>(parent, minr, rows, rank);
-    JG_LAUNCH_CHECK();
     JG_HIP(hipStreamSynchronize(s));
     *iterations = it;
+    *labels = parent;
     return true;
 }
 
@@ -514,8 +499,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     }
     // One shard: the same labels and superstep count from a union-find and one BFS (cc_union_find).
     bool solved = false;
+    const int32_t* uf_labels = nullptr;  // the union-find's labels of shard 0 (when solved)
     if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) {
-        solved = cc_union_find(ctx, sh0, &iteration);
+        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels);
         if (!solved && sh0.rows) {  // the cap binds: the propagation runs, from fresh message vectors
             for (auto& m : sh0.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh0.stream));
             cc_init_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
@@ -609,8 +595,8 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         Shard& sh = *g.shards[0];
         DeviceGuard dg(sh.device);
         DevBuf<int64_t> out(n);
-        cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(sh.cc_label.get(), sh.dense_rows.get(), vor.get(), n,
-                                                                out.get());
+        cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(solved ? uf_labels : sh.cc_label.get(),
+                                                                sh.dense_rows.get(), vor.get(), n, out.get());
         JG_LAUNCH_CHECK();
         copy_d2h(comp_out, out.get(), n * sizeof(int64_t), sh.stream);
     } else if (comp_out) {
@@ -618,7 +604,8 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             Shard& sh = *sp;
             DeviceGuard dg(sh.device);
             std::vector<int32_t> h(sh.rows);
-            if (sh.rows) copy_d2h(h.data(), sh.cc_label.get(), sh.rows * sizeof(int32_t), sh.stream);
+            const int32_t* lab = solved && &sh == &sh0 ? uf_labels : sh.cc_label.get();
+            if (sh.rows) copy_d2h(h.data(), lab, sh.rows * sizeof(int32_t), sh.stream);
             for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local[l]] = vid_of_rank[h[l]];
         }
     }

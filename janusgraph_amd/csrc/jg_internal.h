@@ -215,7 +215,7 @@ struct Shard {
     DevBuf<int32_t> cc_split_partial; // [plan_both.split_partial_len()]
     DevBuf<int32_t> cc_msg[2];     // [P*S] label if sent else INT32_MAX
     DevBuf<int32_t> cc_label;      // [rows]
-    DevBuf<int32_t> cc_aux[2];     // [rows] one shard's union-find path: BFS sources, BFS depths
+    DevBuf<int32_t> cc_depth;      // [rows] one shard's union-find path: the BFS depths
     DevBuf<int32_t> cc_hub_partial;
     DevBuf<int32_t> cc_changed;    // [1]
     // single-source DO-BFS scratch, kept across calls (level-parity ping-pong)
@@ -415,10 +415,18 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out);
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
-// One shard, BOTH adjacency: the largest hop distance of a vertex from the source of its component
-// (src[v] == v marks the sources), by a direction-optimising BFS started at every source that has an
-// edge; -1 if no vertex has an edge (jg_traverse.hip).
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* src, int32_t* depth);
+// The union-find's result on one shard (jg_cc.hip): parent[v] is v's root for v < ne, minr[root] the
+// smallest rank in the root's component; rows [ne, rows) have no edge (Csr::empty_from).
+struct CcRoots {
+    int32_t* parent;  // overwritten with the labels (each row's component minimum rank)
+    const int32_t* rank;
+    const int32_t* minr;
+    int64_t ne;
+};
+// One shard, BOTH adjacency: the largest hop distance of a vertex from the minimum-rank vertex of its
+// component, by a direction-optimising BFS started at every such vertex that has an edge; -1 if no
+// vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
                  uint8_t* received_out);
 

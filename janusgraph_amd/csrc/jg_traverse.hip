@@ -311,9 +311,12 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
     }
 }
 
-// Multi-source start (cc_root_eccentricity): every component root with an edge is a level-0 source.
-__global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restrict__ depth, int64_t rows,
-                                                                const int32_t* __restrict__ parent,
+// Multi-source start (cc_root_eccentricity), fused with the union-find's last per-row pass: a row with
+// an edge whose rank is its component's minimum is a level-0 source, and every row's label (that
+// minimum) replaces its parent.  Rows from r.ne on have no edge: no row_ptr, parent or minr reads
+// (their label is their own rank).  At RMAT-26 this one pass replaced three (sources, init, labels:
+// 530 us).
+__global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restrict__ depth, int64_t rows, CcRoots r,
                                                                 const int64_t* __restrict__ deg_rp, int32_t* queue,
                                                                 int64_t* qoff, unsigned long long* packed,
                                                                 uint8_t* __restrict__ seen) {
@@ -325,22 +328,20 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
         bool take = false;
         int64_t deg = 0;
         if (v < rows) {
-            deg = deg_rp[v + 1] - deg_rp[v];
-            take = parent[v] == (int32_t)v && deg > 0;
-            depth[v] = take ? 0 : -1;
+            int32_t lab = r.rank[v];
+            if (v < r.ne) {
+                deg = deg_rp[v + 1] - deg_rp[v];
+                const int32_t m = r.minr[r.parent[v]];
+                take = deg > 0 && lab == m;
+                lab = m;
+                depth[v] = take ? 0 : -1;  // only the traversal reads the depths: the edgeless rows need none
+            }
+            r.parent[v] = lab;
             seen[v] = take || deg == 0;  // BOTH: push and pull rows are the same (bfs_init_kernel)
         }
         app.append(take, (int32_t)v, deg, queue, qoff, packed);
     }
     app.final(queue, qoff, packed);
-}
-
-__global__ void depth_max_kernel(const int32_t* __restrict__ depth, int64_t n, int32_t* __restrict__ out) {
-    int32_t m = -1;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        m = depth[i] > m ? depth[i] : m;
-    m = wave_reduce_max(m);
-    if (lane_id() == 0) atomicMax(out, m);
 }
 
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
@@ -654,7 +655,7 @@ uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ?
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
 // Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out, const int32_t* roots = nullptr) {
+                 double* edges_out, const CcRoots* roots = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr* push = c.push;
@@ -671,12 +672,12 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
     if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
     BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
-    if (roots) {  // every root (parent[v] == v) with an edge starts at depth 0
+    if (roots) {  // every component's minimum-rank vertex with an edge starts at depth 0
         JG_HIP(hipMemsetAsync(sh.bfs_ctr.get(), 0, kBfsRing * sizeof(unsigned long long), s));
         BfsState s0{};
         s0.mu = (long long)degcsr->nnz;
         copy_h2d(st + kBfsRing - 1, &s0, sizeof s0, s);
-        bfs_init_roots_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, roots, degcsr->row_ptr.get(),
+        bfs_init_roots_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, *roots, degcsr->row_ptr.get(),
                                                                 sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
                                                                 sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
     } else {
@@ -1060,18 +1061,12 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
 
 }  // namespace
 
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const int32_t* src, int32_t* depth) {
-    const int64_t rows = sh.rows;
-    if (rows == 0) return 0;
-    DevBuf<int32_t> dmax(1);
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth) {
+    if (sh.rows == 0) return -1;
     const BfsCsrs c{&sh.both, &sh.both};
-    dobfs_single(ctx, sh, c, -1, -1, depth, nullptr, src);
-    JG_HIP(hipMemsetAsync(dmax.get(), 0xFF, sizeof(int32_t), sh.stream));  // -1
-    depth_max_kernel<<<grid_for(rows), kBlock, 0, sh.stream>>>(depth, rows, dmax.get());
-    JG_LAUNCH_CHECK();
-    int32_t d = -1;
-    copy_d2h(&d, dmax.get(), sizeof d, sh.stream);
-    return d;
+    // the traversal stops at the first level with an empty frontier, which it counts: the deepest
+    // depth is the one before (no depth-max pass over the rows)
+    return dobfs_single(ctx, sh, c, -1, -1, depth, nullptr, &r) - 1;
 }
 
 
