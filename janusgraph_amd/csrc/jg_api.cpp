@@ -499,6 +499,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {
         jg::tune().msbfs_td = value != 0;
+    } else if (k == "msbfs_skip") {
+        jg::tune().msbfs_skip = value != 0;
     } else if (k == "cc_uf") {
         jg::tune().cc_uf = value != 0;
     } else if (k == "msbfs_split") {

@@ -580,12 +580,16 @@ __global__ void nonempty_kernel(const int32_t* __restrict__ len, int64_t n, int3
 }
 
 // Non-empty sub-rows are numbered sub-slice-major (num = exclusive scan of the flags): cstart[k] =
-// first entry of sub-row k.
+// first entry of sub-row k, srow[k] = its band row.
 __global__ void sub_number_kernel(const int32_t* __restrict__ len, const int64_t* __restrict__ num, int64_t NR, int S,
-                                  const int64_t* __restrict__ sp, int64_t* __restrict__ cstart) {
+                                  const int64_t* __restrict__ sp, int64_t* __restrict__ cstart,
+                                  int32_t* __restrict__ srow) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < NR * S; x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t h = x / NR, i = x % NR;
-        if (len[x] > 0) cstart[num[x]] = sp[h * (NR + 1) + i];
+        if (len[x] > 0) {
+            cstart[num[x]] = sp[h * (NR + 1) + i];
+            srow[num[x]] = (int32_t)i;
+        }
     }
 }
 
@@ -601,11 +605,13 @@ __global__ void sub_word_kernel(const int32_t* __restrict__ len, const int64_t* 
     }
 }
 
-// Per task: j0 = the non-empty sub-row holding its first entry, carry = it started earlier, and
-// heads[t][l] = row-start bits of lane l's kMergeEpl entries (bit 0 of lane 0 always set).
-__global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64_t* __restrict__ nzb, int S,
-                                 const int64_t* __restrict__ begin, const int64_t* __restrict__ end,
-                                 const int64_t* __restrict__ base, int32_t* __restrict__ meta, uint8_t* __restrict__ heads) {
+// Per task: j0 = the non-empty sub-row holding its first entry, carry = it started earlier,
+// heads[t][l] = row-start bits of lane l's kMergeEpl entries (bit 0 of lane 0 always set), and the
+// band rows of its first and last sub-row.
+__global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int32_t* __restrict__ srow,
+                                 const int64_t* __restrict__ nzb, int S, const int64_t* __restrict__ begin,
+                                 const int64_t* __restrict__ end, const int64_t* __restrict__ base,
+                                 int32_t* __restrict__ meta, uint8_t* __restrict__ heads, int32_t* __restrict__ trows) {
     constexpr int kEpl = kMergeTask / kWave;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < base[S]; t += (int64_t)gridDim.x * blockDim.x) {
         int lo_h = 0, hi_h = S;  // sub-slice: last h with base[h] <= t
@@ -627,11 +633,14 @@ __global__ void task_meta_kernel(const int64_t* __restrict__ cstart, const int64
         uint8_t hd[kWave];
         for (int l = 0; l < kWave; ++l) hd[l] = 0;
         hd[0] = 1;
-        for (int64_t j = j0 + 1; j < nzb[h + 1] && cstart[j] < e1; ++j) {
+        int64_t j = j0 + 1;
+        for (; j < nzb[h + 1] && cstart[j] < e1; ++j) {
             const int pos = (int)(cstart[j] - e0);
             hd[pos / kEpl] |= (uint8_t)(1u << (pos % kEpl));
         }
         for (int l = 0; l < kWave; ++l) heads[t * kWave + l] = hd[l];
+        trows[2 * t] = srow[j0];
+        trows[2 * t + 1] = srow[j - 1];
     }
 }
 
@@ -727,7 +736,8 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     JG_LAUNCH_CHECK();
     copy_d2h(&bd.subrows, num.get() + NS, sizeof(int64_t), s);
     DevBuf<int64_t> cstart(std::max<int64_t>(bd.subrows, 1));
-    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), NR, S, sp.get(), cstart.get());
+    DevBuf<int32_t> srow(std::max<int64_t>(bd.subrows, 1));
+    sub_number_kernel<<<grid_for(NS), kBlock, 0, s>>>(len.get(), num.get(), NR, S, sp.get(), cstart.get(), srow.get());
     JG_LAUNCH_CHECK();
     if (bd.subrows >= (int64_t)INT32_MAX) fail(JG_ERR_UNSUPPORTED, "too many sub-rows in a split band");
     const int64_t W = (NR + 31) / 32;
@@ -738,10 +748,12 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     }
     bd.meta.alloc(std::max<int64_t>(2 * bd.tasks, 1));
     bd.heads.alloc(std::max<int64_t>(kWave * bd.tasks, 1));
+    bd.task_rows.alloc(std::max<int64_t>(2 * bd.tasks, 1));
     if (bd.tasks > 0) {
-        task_meta_kernel<<<grid_for(bd.tasks, 64), 64, 0, s>>>(cstart.get(), nzb.get(), S, bd.sub_begin.get(),
-                                                               bd.sub_end.get(), bd.sub_base.get(), bd.meta.get(),
-                                                               bd.heads.get());
+        task_meta_kernel<<<grid_for(bd.tasks, 64), 64, 0, s>>>(cstart.get(), srow.get(), nzb.get(), S,
+                                                               bd.sub_begin.get(), bd.sub_end.get(),
+                                                               bd.sub_base.get(), bd.meta.get(), bd.heads.get(),
+                                                               bd.task_rows.get());
         JG_LAUNCH_CHECK();
     }
     // the streamed form: packed sub-slice-local indices (the col copy is not kept)

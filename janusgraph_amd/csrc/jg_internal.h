@@ -78,6 +78,7 @@ struct SliceBand {
     // non-empty sub-rows, numbered sub-slice-major: for w = sub_word[h][i>>5], bit i&31 of w.x says
     // whether band row i has entries in sub-slice h; its number is w.y + the set bits of w.x below it
     DevBuf<uint2> sub_word;     // [S][words], words = ceil(rows of the band / 32)
+    DevBuf<int32_t> task_rows;  // [tasks][2]: band rows of the task's first and last entry
     int64_t rows() const { return row_end - row_begin; }
 };
 
@@ -477,6 +478,7 @@ struct Tune {
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
+    int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo

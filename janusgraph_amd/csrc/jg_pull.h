@@ -335,6 +335,10 @@ struct MergeArgs {
     int dynamic;       // LDS image kernels: waves take their block's tasks from an LDS counter
     int interleave;    // a block's tasks interleaved with its sub-slice's other blocks (rotating per round)
     int diag;          // Tune::merge_diag (diagnostic timing variants; 0 in production)
+    // nullable: bit t (of the band's tasks) clear = task t is skipped, its partials and carry left as
+    // they are.  A program passes it only when every row the task touches would discard what the task
+    // folds (the multi-source BFS: rows that can gain no bit; see msbfs_task_live_kernel).
+    const uint32_t* __restrict__ live;
 };
 
 // The hot entries of a gathered vector: the first `hs` entries of each of its `nseg` segments
@@ -500,7 +504,21 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         return task_of((int64_t)__builtin_amdgcn_readfirstlane(j));
     };
     int64_t jstat = wave;
+    auto advance = [&]() -> int64_t {
+        if (dyn) return grab();
+        jstat += kMergeWaves;
+        return task_of(jstat);
+    };
+    // a skipped task (a.live): a scalar load of its bit (waiting on it does not wait for the vector
+    // gathers in flight), then the next task
+    auto dead = [&](int64_t kk) -> bool {
+        if (a.live == nullptr || kk >= ntask) return false;
+        const uint64_t tt = (uint64_t)(base + kk);
+        const uint32_t wd = __builtin_amdgcn_readfirstlane(a.live[tt >> 5]);
+        return ((wd >> (tt & 31)) & 1u) == 0;
+    };
     int64_t k = dyn ? grab() : task_of(jstat);
+    while (dead(k)) k = advance();
     if (k >= ntask || a.diag == 1) continue;
     // The next task's entries and metadata are loaded while this task's gathers are in flight.  The
     // loop carries the raw load registers (the packed lane chunk, head byte, meta word) and unpacks
@@ -559,13 +577,8 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) v[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, false);
         }
-        int64_t kn;
-        if (dyn) {
-            kn = grab();
-        } else {
-            jstat += kMergeWaves;
-            kn = task_of(jstat);
-        }
+        int64_t kn = advance();
+        while (dead(kn)) kn = advance();
         if (kn < ntask) {
             load_chunk(kn, cd);
             hb = ld(a.heads + head_idx(kn));
@@ -815,10 +828,11 @@ constexpr int64_t kMaxLdsBytes = 160 * 1024;
 
 // `skip_empty`: the rows without entries (the degree-sorted suffix, class kZeroClass) are not
 // finalised, for programs whose value there no longer changes (PageRank after two power steps).
+// `task_live` (nullable): per band, the MergeArgs::live bitmap of its tasks.
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
                  Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr,
-                 bool skip_empty = false) {
+                 bool skip_empty = false, const uint32_t* const* task_live = nullptr) {
     using T = typename Op::T;
     const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
     PullArgs a = make_pull_args(csr, plan, split);
@@ -869,7 +883,8 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                 while (stage < 4.0 * heads && stage < 256) stage *= 2;
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
-                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_interleave, tune().merge_diag};
+                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_interleave, tune().merge_diag,
+                         task_live ? task_live[bi] : nullptr};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice

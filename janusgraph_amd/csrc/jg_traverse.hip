@@ -355,16 +355,19 @@ struct MsBfsOp {
     int64_t rows;
     VecPos pos;                 // owned row -> its slot in the gathered vector
     int32_t lvl;
-    T full;
+    // the sources whose bits are in some word of the gathered vector F (msbfs_live_kernel; device
+    // word): no other bit can arrive this level, so a row whose unvisited bits miss them all is done
+    const T* live;
     __device__ __forceinline__ T identity() const { return 0ull; }
     __device__ __forceinline__ T combine(T a, T b) const { return a | b; }
     __device__ __forceinline__ T gather(int32_t c) const { return F[c]; }
     __device__ __forceinline__ const T* vec() const { return F; }
     __device__ __forceinline__ T shfl_xor(T v, int o) const { return __shfl_xor(v, o, kWave); }
     __device__ __forceinline__ T shfl_up(T v, int d) const { return __shfl_up(v, d, kWave); }
-    __device__ __forceinline__ bool active(int64_t row) const { return visited[row] != full; }
+    __device__ __forceinline__ bool active(int64_t row) const { return (~visited[row] & *live) != 0ull; }
+    // masking with live also discards what a done row's skipped merge tasks left in its partials
     __device__ __forceinline__ void finalize(int64_t row, T acc) const {
-        T nw = acc & ~visited[row] & full;
+        T nw = acc & ~visited[row] & *live;
         Fout[pos(row)] = nw;
         if (nw) {
             visited[row] |= nw;
@@ -377,6 +380,60 @@ struct MsBfsOp {
         }
     }
 };
+
+// *live |= the OR of every word of F (one atomic per block)
+__global__ __launch_bounds__(kBlock) void msbfs_live_kernel(const unsigned long long* __restrict__ F, int64_t len,
+                                                            unsigned long long* __restrict__ live) {
+    __shared__ unsigned long long red[kBlock / kWave];
+    unsigned long long m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x)
+        m |= F[i];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) m |= __shfl_xor(m, o, kWave);
+    if (lane_id() == 0) red[wave_id()] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) m |= red[w];
+        if (m) atomicOr(live, m);
+    }
+}
+
+// bit i of todo: band row i (row0 + i) can still gain a bit this level
+__global__ __launch_bounds__(kBlock) void msbfs_todo_kernel(const unsigned long long* __restrict__ visited,
+                                                            int64_t row0, int64_t nrows,
+                                                            const unsigned long long* __restrict__ live,
+                                                            unsigned long long* __restrict__ todo) {
+    const unsigned long long lv = *live;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nrows; x0 += stride) {  // block-uniform trips
+        const int64_t i = x0 + threadIdx.x;
+        const bool b = i < nrows && (~visited[row0 + i] & lv) != 0ull;
+        const unsigned long long word = __ballot(b);
+        if (lane_id() == 0 && i < nrows) todo[i >> 6] = word;
+    }
+}
+
+// bit t of tlive (MergeArgs::live): merge task t touches a band row that can still gain a bit
+__global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* __restrict__ task_rows, int64_t tasks,
+                                                                 const unsigned long long* __restrict__ todo,
+                                                                 unsigned long long* __restrict__ tlive) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tasks; x0 += stride) {  // block-uniform trips
+        const int64_t t = x0 + threadIdx.x;
+        bool b = false;
+        if (t < tasks) {
+            const int32_t lo = task_rows[2 * t], hi = task_rows[2 * t + 1];
+            for (int32_t w = lo >> 6; w <= (hi >> 6) && !b; ++w) {
+                unsigned long long m = todo[w];
+                if (w == (lo >> 6)) m &= ~0ull << (lo & 63);
+                if (w == (hi >> 6) && (hi & 63) != 63) m &= (2ull << (hi & 63)) - 1ull;
+                b = m != 0ull;
+            }
+        }
+        const unsigned long long word = __ballot(b);
+        if (lane_id() == 0 && t < tasks) tlive[t >> 6] = word;
+    }
+}
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
                                   unsigned long long* __restrict__ visited, int32_t* __restrict__ depth, int64_t rows,
@@ -1137,6 +1194,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> F[2], vis;
                 DevBuf<int32_t> depth, changed;
                 DevBuf<unsigned long long> hub, split;
+                DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
+                std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
             };
             std::vector<St> st(g.shards.size());
             for (size_t i = 0; i < g.shards.size(); ++i) {
@@ -1156,6 +1215,17 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
+                t.live.alloc(2);
+                const unsigned long long lw[2] = {full, full};
+                copy_h2d(t.live.get(), lw, sizeof lw, sh.stream);
+                if (t.split.size() && tune().msbfs_skip) {
+                    t.todo.resize(plan.bands.size());
+                    t.tlive.resize(plan.bands.size());
+                    for (size_t b = 0; b < plan.bands.size(); ++b) {
+                        t.todo[b].alloc(std::max<int64_t>((plan.bands[b]->rows() + 63) / 64, 1));
+                        t.tlive[b].alloc(std::max<int64_t>((plan.bands[b]->tasks + 63) / 64, 1));
+                    }
+                }
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
@@ -1245,7 +1315,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.rows = sh.rows;
                         op.pos = g.vec_pos(sh, adj_of(sh, c0));
                         op.lvl = level + 1;
-                        op.full = full;
+                        op.live = t.live.get() + 1;
                         msbfs_td_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(
                             td.touched.get(), nt, op, c0.push->row_ptr.get(), td.queue[td.qc ^ 1].get(),
                             td.qoff[td.qc ^ 1].get(), td.ctr.get());
@@ -1270,13 +1340,35 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     op.rows = sh.rows;
                     op.pos = g.vec_pos(sh, adj_of(sh, c));
                     op.lvl = level + 1;
-                    op.full = full;
-                    // Pull levels come after the top-down ones, when most rows still miss sources: the
-                    // sliced split (XCD sub-slices, LDS-resident hot words) folds every entry of the
-                    // split rows, fully visited or not (MsBfsOp::finalize masks with ~visited); the
-                    // light rows' class kernel still skips fully visited rows (MsBfsOp::active).
+                    // Live bits: the sources present in some word of this level's gathered vector.  A row
+                    // none of whose unvisited bits is live gains nothing, so the light rows skip it
+                    // (MsBfsOp::active) and the split skips every merge task whose rows are all such
+                    // (their partials are then stale, and finalize's live mask discards them).  At
+                    // RMAT-26 the last pull level has ~all rows done and the one before ~40% of band 0.
+                    unsigned long long* lw = t.live.get();
+                    const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
+                    JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
+                    msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
+                    JG_LAUNCH_CHECK();
+                    op.live = lw;
+                    std::vector<const uint32_t*> tl;
+                    for (size_t b = 0; b < t.todo.size(); ++b) {
+                        const SliceBand& bd = *plan.bands[b];
+                        if (bd.tasks == 0 || bd.rows() == 0) {
+                            tl.push_back(nullptr);
+                            continue;
+                        }
+                        msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
+                            t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
+                        JG_LAUNCH_CHECK();
+                        msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
+                            bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get());
+                        JG_LAUNCH_CHECK();
+                        tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                    }
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                t.split.size() ? t.split.get() : (unsigned long long*)nullptr);
+                                t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
+                                tl.empty() ? nullptr : tl.data());
                     if (td_ok) {  // the next level may run top-down: queue this level's frontier
                         build_frontier(t.F[cur ^ 1].get(), td.qc ^ 1);
                         td.qc ^= 1;

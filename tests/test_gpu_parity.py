@@ -180,6 +180,46 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
         np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3))
 
 
+@pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
+                                         ("skip_wide", 1), ("skip", 3), ("skip_dense", 2)])
+def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
+    """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
+    (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
+    isolated vertex and a vertex of a small component (their bits never reach the rest, so no row ever
+    holds every source), on one shard and on logical shards (halo and dense vectors)."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
+             "skip_bands3": [("band0_deg", 64), ("band0_bit", 8), ("band1_deg", 16), ("band1_bit", 5),
+                             ("band2_deg", 4), ("band2_bit", 3)],
+             "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
+             "skip_dense": [("halo", 0)]}[mode]
+    n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
+    n = n0 + 3  # + an isolated vertex and a two-vertex component
+    vid = np.concatenate([vid0, (np.arange(3, dtype=np.int64) + n0 + 1) << 8 | 7])
+    ds = np.concatenate([ds0, np.array([n0 + 1], ds0.dtype)])
+    dd = np.concatenate([dd0, np.array([n0 + 2], dd0.dtype)])
+    try:
+        for k, v in knobs:
+            _lib.tune_set(k, v)
+        c = jg.Context((0,) * shards)
+        g = c.build(vid, vid[ds], vid[dd], flags=2 | 4)
+        rng = np.random.default_rng(11)
+        srcs = np.concatenate([rng.choice(np.unique(ds0), 62, replace=False), [n0, n0 + 2]])
+        depth = g.bfs(vid[srcs], 3)
+        for k in range(len(srcs)):
+            np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3), err_msg=f"source {k}")
+        g.close()
+        c.close()
+    finally:
+        _lib.tune_set("msbfs_skip", 1)
+        _lib.tune_set("msbfs_td", 1)
+        _lib.tune_set("halo", 1)
+        for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
+                     ("band2_bit", 3)):  # the defaults (Tune::band_deg / band_bits)
+            _lib.tune_set(k, v)
+
+
 @pytest.mark.parametrize("direction", [1, 2])
 def test_directed_bfs(ctx, oracle_lib, direction):
     n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 12)
