@@ -398,6 +398,43 @@ __global__ __launch_bounds__(kBlock) void msbfs_live_kernel(const unsigned long 
     }
 }
 
+// After a pull level (one shard): the next level's live bits and its packed frontier counter
+// ((vertices << kPackShift) | push-edge sum: the direction rule's input) in one read of F, without the
+// top-down queue, which msbfs_frontier_kernel builds only if the next level runs top-down
+// (the queue build cost 750 us at RMAT-26's first two pull levels, whose successors pull).
+__global__ __launch_bounds__(kBlock) void msbfs_scan_kernel(const unsigned long long* __restrict__ F, int64_t rows,
+                                                            const int64_t* __restrict__ push_rp,
+                                                            unsigned long long* __restrict__ live,
+                                                            unsigned long long* __restrict__ packed) {
+    __shared__ unsigned long long red_or[kBlock / kWave], red_n[kBlock / kWave];
+    unsigned long long m = 0, cnt = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long w = F[v];
+        if (w) {
+            m |= w;
+            cnt += (1ull << kPackShift) + (unsigned long long)(push_rp[v + 1] - push_rp[v]);
+        }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        m |= __shfl_xor(m, o, kWave);
+        cnt += __shfl_xor(cnt, o, kWave);
+    }
+    if (lane_id() == 0) {
+        red_or[wave_id()] = m;
+        red_n[wave_id()] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) {
+            m |= red_or[w];
+            cnt += red_n[w];
+        }
+        if (m) atomicOr(live, m);
+        if (cnt) atomicAdd(packed, cnt);
+    }
+}
+
 // bit i of todo: band row i (row0 + i) can still gain a bit this level
 __global__ __launch_bounds__(kBlock) void msbfs_todo_kernel(const unsigned long long* __restrict__ visited,
                                                             int64_t row0, int64_t nrows,
@@ -1283,10 +1320,19 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 td.ctr.alloc(2);
                 build_frontier(st[0].F[0].get(), 0);
             }
+            // queued: td.queue[td.qc] holds the current frontier; live_ready: st[0].live[0] holds its live
+            // bits (both from the previous level's end)
+            bool queued = td_ok, live_ready = false;
             int cur = 0, level = 0;
             while (max_depth < 0 || level < max_depth) {
                 const bool td_level =
                     td_ok && (double)td.mf < (double)c0.push->nnz / (double)tune().bfs_alpha;
+                if (td_level && !queued) {
+                    build_frontier(st[0].F[cur].get(), td.qc ^ 1);
+                    td.qc ^= 1;
+                }
+                const bool have_live = live_ready;
+                queued = live_ready = false;
                 if (td_level) {
                     Shard& sh = sh0;
                     St& t = st[0];
@@ -1323,6 +1369,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                     read_frontier();
                     td.qc ^= 1;
+                    queued = true;
                 } else
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
@@ -1346,10 +1393,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     // (their partials are then stale, and finalize's live mask discards them).  At
                     // RMAT-26 the last pull level has ~all rows done and the one before ~40% of band 0.
                     unsigned long long* lw = t.live.get();
-                    const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
-                    JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
-                    msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
-                    JG_LAUNCH_CHECK();
+                    if (!have_live) {
+                        const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
+                        JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
+                        msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
+                        JG_LAUNCH_CHECK();
+                    }
                     op.live = lw;
                     std::vector<const uint32_t*> tl;
                     for (size_t b = 0; b < t.todo.size(); ++b) {
@@ -1369,9 +1418,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                 t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
                                 tl.empty() ? nullptr : tl.data());
-                    if (td_ok) {  // the next level may run top-down: queue this level's frontier
-                        build_frontier(t.F[cur ^ 1].get(), td.qc ^ 1);
-                        td.qc ^= 1;
+                    if (td_ok) {  // the next level's live bits and frontier counter (its direction)
+                        JG_HIP(hipMemsetAsync(td.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
+                        JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
+                        msbfs_scan_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                            t.F[cur ^ 1].get(), sh.rows, c0.push->row_ptr.get(), lw, td.ctr.get());
+                        JG_LAUNCH_CHECK();
+                        read_frontier();
+                        live_ready = true;
                     }
                 }
                 if (!td_level) {
