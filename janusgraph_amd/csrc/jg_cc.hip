@@ -480,6 +480,10 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
+    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf && sh0.rows > 0) {  // the union-find path's scratch
+        if ((int64_t)sh0.cc_depth.size() < sh0.rows) sh0.cc_depth.alloc(sh0.rows);
+        bfs_buffers(sh0);
+    }
     JG_HIP(hipEventRecord(t0, sh0.stream));
     int iteration = 0, cur = 0;
     // one shard: supersteps whose senders have few edges run push-style

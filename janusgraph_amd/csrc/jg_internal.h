@@ -428,6 +428,8 @@ struct CcRoots {
 // component, by a direction-optimising BFS started at every such vertex that has an edge; -1 if no
 // vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).
 int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth);
+// Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
+void bfs_buffers(Shard& sh);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
                  uint8_t* received_out);
 

@@ -748,13 +748,12 @@ uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ?
 
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
 // Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
-int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out, const CcRoots* roots = nullptr) {
-    hipStream_t s = sh.stream;
+}  // namespace
+
+// The single-shard traversal's scratch, kept with the shard (callers allocate it before their timed
+// region: a first call would otherwise time ~1 ms of allocations at RMAT-26).
+void bfs_buffers(Shard& sh) {
     const int64_t rows = sh.rows;
-    const Csr* push = c.push;
-    const Csr* pull = c.pull;
-    const Csr* degcsr = push ? push : pull;
     const int64_t words = (rows + 63) / 64;
     const size_t r1 = (size_t)std::max<int64_t>(rows, 1), w1 = (size_t)std::max<int64_t>(words, 1);
     for (int k = 0; k < 2; ++k) {
@@ -765,6 +764,18 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     if (sh.bfs_seen.size() != r1) sh.bfs_seen.alloc(r1);
     if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
     if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
+}
+
+namespace {
+
+int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
+                 double* edges_out, const CcRoots* roots = nullptr) {
+    hipStream_t s = sh.stream;
+    const int64_t rows = sh.rows;
+    const Csr* push = c.push;
+    const Csr* pull = c.pull;
+    const Csr* degcsr = push ? push : pull;
+    bfs_buffers(sh);
     BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
     if (roots) {  // every component's minimum-rank vertex with an edge starts at depth 0
         JG_HIP(hipMemsetAsync(sh.bfs_ctr.get(), 0, kBfsRing * sizeof(unsigned long long), s));
@@ -1205,6 +1216,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventRecord(t0, sh.stream));
             JG_HIP(hipEventRecord(t1, sh.stream));
         } else {
+            bfs_buffers(sh);
             JG_HIP(hipEventRecord(t0, sh.stream));
             levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges);
             JG_HIP(hipEventRecord(t1, sh.stream));
@@ -1285,7 +1297,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 for (auto& t : st) bufs.push_back(t.F[0].get());
                 exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
             }
-            JG_HIP(hipEventRecord(t0, sh0.stream));
             // one shard with a push adjacency: levels whose frontier has few edges run top-down
             const BfsCsrs c0 = pick_csrs(sh0, direction);
             const bool td_ok = g.shards.size() == 1 && g.P == 1 && c0.push != nullptr && tune().msbfs_td;
@@ -1309,7 +1320,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_LAUNCH_CHECK();
                 read_frontier();
             };
-            if (td_ok) {
+            if (td_ok) {  // allocated before the timed region (~2.3 GB at RMAT-26)
                 const size_t r1 = (size_t)std::max<int64_t>(sh0.rows, 1);
                 for (int k = 0; k < 2; ++k) {
                     td.queue[k].alloc(r1);
@@ -1318,8 +1329,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 td.touched.alloc(r1);
                 td.touched_off.alloc(r1);
                 td.ctr.alloc(2);
-                build_frontier(st[0].F[0].get(), 0);
             }
+            JG_HIP(hipEventRecord(t0, sh0.stream));
+            if (td_ok) build_frontier(st[0].F[0].get(), 0);
             // queued: td.queue[td.qc] holds the current frontier; live_ready: st[0].live[0] holds its live
             // bits (both from the previous level's end)
             bool queued = td_ok, live_ready = false;
@@ -1627,6 +1639,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
+    if (seed >= 0 && !g.has_weights) bfs_buffers(sh);
     JG_HIP(hipEventRecord(t0, s));
     int levels = 0;
     if (seed >= 0 && !g.has_weights) {
