@@ -553,7 +553,9 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 const int32_t v = a.queue[i];
                 u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
                 const unsigned long long w = a.F[v] & ~a.visited[u];
-                if (w) take = atomicOr(&a.Fnext[u], w) == 0ull;
+                // a plain read first: a hub neighbour already holding these bits takes no atomic (the
+                // atomics on one word serialise at the memory side); a stale read only costs the atomic
+                if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull;
             }
             app.append(take, u, 0, a.touched, a.touched_off, a.tpacked);
         }
