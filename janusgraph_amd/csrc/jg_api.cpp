@@ -499,6 +499,9 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {
         jg::tune().msbfs_td = value != 0;
+    } else if (k == "cc_first") {
+        JG_ARG(value >= 1 && value <= 64, "cc_first must be in [1, 64]");
+        jg::tune().cc_first = (int)value;
     } else if (k == "msbfs_skip") {
         jg::tune().msbfs_skip = value != 0;
     } else if (k == "cc_uf") {

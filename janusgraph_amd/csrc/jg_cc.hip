@@ -328,7 +328,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels)
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
-    constexpr int kFirst = 2;
+    const int kFirst = std::max(1, tune().cc_first);  // neighbours each vertex links in the first round
     if (rows == 0) {
         *iterations = 0;
         *labels = sh.cc_label.get();

@@ -480,6 +480,8 @@ struct Tune {
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
+    int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
+                                      //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)

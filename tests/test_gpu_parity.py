@@ -349,7 +349,7 @@ def test_errors_are_status_codes(ctx):
 
 @pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
                                   "split_sub1", "split_sub2_4", "split_w24", "split_w32", "split_stage_off",
-                                  "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip"])
+                                  "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip", "cc_first3"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -376,7 +376,8 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "light_noruns": [("light_runs", 0)],
              "merge_static": [("merge_dynamic", 0)],
              "merge_chunks16": [("merge_interleave", 0)],
-             "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)]}[mode]
+             "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)],
+             "cc_first3": [("cc_first", 3)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -412,6 +413,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("merge_interleave", 1)
         _lib.tune_set("pr_skip_empty", 1)
         _lib.tune_set("pr_rank_last", 1)
+        _lib.tune_set("cc_first", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
                      ("band2_bit", 3)):
             _lib.tune_set(k, v)
