@@ -506,6 +506,22 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned l
     app.final(queue, qoff, packed);
 }
 
+// The first top-down queue: the distinct source rows with their push-edge offsets, and the packed
+// frontier counter (one thread: at most 64 sources)
+__global__ void msbfs_source_queue_kernel(const int64_t* __restrict__ rows, int cnt, const int64_t* __restrict__ push_rp,
+                                          int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                          unsigned long long* __restrict__ packed) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int64_t off = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const int64_t v = rows[i];
+        queue[i] = (int32_t)v;
+        qoff[i] = off;
+        off += push_rp[v + 1] - push_rp[v];
+    }
+    packed[0] = ((unsigned long long)cnt << kPackShift) | (unsigned long long)off;
+}
+
 struct MsTd {
     const int32_t* queue;
     const int64_t* qoff;
@@ -1249,6 +1265,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
             };
             std::vector<St> st(g.shards.size());
+            std::vector<int64_t> src_rows;
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
@@ -1287,6 +1304,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     const int64_t l = local_of_vid(g, source_vids[b0 + s], &shard);
                     if (l >= 0 && shard == sh.index) loc[s] = l;
                 }
+                if (i == 0) {  // shard 0's distinct source rows: the first top-down queue (msbfs_source_queue_kernel)
+                    src_rows.clear();
+                    for (int64_t l : loc)
+                        if (l >= 0 && std::find(src_rows.begin(), src_rows.end(), l) == src_rows.end()) src_rows.push_back(l);
+                }
                 DevBuf<int64_t> dloc(ns);
                 copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
                 msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth.get(),
@@ -1306,6 +1328,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<int32_t> queue[2], touched;
                 DevBuf<int64_t> qoff[2], touched_off;
                 DevBuf<unsigned long long> ctr;  // [0] frontier, [1] touched
+                DevBuf<int64_t> srcs;            // shard 0's distinct source rows
                 int64_t nq = 0, mf = 0;
                 int qc = 0;
             } td;
@@ -1331,9 +1354,18 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 td.touched.alloc(r1);
                 td.touched_off.alloc(r1);
                 td.ctr.alloc(2);
+                td.srcs.alloc(std::max<size_t>(src_rows.size(), 1));
+                if (!src_rows.empty())
+                    copy_h2d(td.srcs.get(), src_rows.data(), src_rows.size() * sizeof(int64_t), sh0.stream);
             }
             JG_HIP(hipEventRecord(t0, sh0.stream));
-            if (td_ok) build_frontier(st[0].F[0].get(), 0);
+            if (td_ok) {  // the level-0 frontier is the source rows: queued directly, no scan of F
+                msbfs_source_queue_kernel<<<1, 1, 0, sh0.stream>>>(td.srcs.get(), (int)src_rows.size(),
+                                                                   c0.push->row_ptr.get(), td.queue[0].get(),
+                                                                   td.qoff[0].get(), td.ctr.get());
+                JG_LAUNCH_CHECK();
+                read_frontier();
+            }
             // queued: td.queue[td.qc] holds the current frontier; live_ready: st[0].live[0] holds its live
             // bits (both from the previous level's end)
             bool queued = td_ok, live_ready = false;
