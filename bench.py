@@ -118,19 +118,28 @@ def pmc_traffic(kernel_tag="PrOp", workload=None):
     if not os.path.isdir(pdir):
         return None, None
     for rnd in sorted(os.listdir(pdir), reverse=True):
-        path = os.path.join(pdir, rnd, "summary.json")
-        if not os.path.exists(path):
+        rdir = os.path.join(pdir, rnd)
+        if not os.path.isdir(rdir):
             continue
-        with open(path) as f:
-            s = json.load(f)
-        if kernel_tag not in s.get("kernel", "") or s.get("traffic_bytes_per_launch") is None:
-            continue
-        bj = os.path.join(pdir, rnd, "bench.json")
-        if workload and os.path.exists(bj):
-            with open(bj) as f:
-                if json.load(f).get("config", {}).get("workload") != workload:
+        # the round's own summary first, then its per-workload ones (e.g. profiles/r02/pmc26/)
+        subs = [""] + sorted(d for d in os.listdir(rdir) if os.path.isdir(os.path.join(rdir, d)))
+        for sub in subs:
+            path = os.path.join(rdir, sub, "summary.json")
+            if not os.path.exists(path):
+                continue
+            with open(path) as f:
+                s = json.load(f)
+            if kernel_tag not in s.get("kernel", "") or s.get("traffic_bytes_per_launch") is None:
+                continue
+            bj = os.path.join(rdir, sub, "bench.json")
+            if workload:
+                if not os.path.exists(bj):
                     continue
-        return s["traffic_bytes_per_launch"], f"profiles/{rnd}/summary.json ({s.get('read_bytes_method', '')})"
+                with open(bj) as f:
+                    if json.load(f).get("config", {}).get("workload") != workload:
+                        continue
+            rel = "/".join(x for x in ("profiles", rnd, sub, "summary.json") if x)
+            return s["traffic_bytes_per_launch"], f"{rel} ({s.get('read_bytes_method', '')})"
     return None, None
 
 
@@ -230,10 +239,12 @@ def pagerank_block(jg, ctx, scale, ef, steps, warmup):
     ctx.set_profiling(False)
     g.close()
     kern_ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
-    return {"workload": f"pagerank_fp64_rmat{scale}_ef{ef}", "ms_per_step": round(dt / steps * 1e3, 4),
+    workload = f"pagerank_fp64_rmat{scale}_ef{ef}"
+    traffic, traffic_src = pmc_traffic("PrOp", workload)
+    return {"workload": workload, "ms_per_step": round(dt / steps * 1e3, 4),
             "gteps": round(m * steps / dt / 1e9, 3), "steps": steps, "build_ms": round(build_ms, 1),
             "roofline": hbm_roofline(12.0 * m + 32.0 * n, kern_ms, "PageRank superstep (same launch sequence "
-                                     "as the headline)")}
+                                     "as the headline)", traffic, traffic_src)}
 
 
 def rmat26_both_blocks(jg, ctx, scale, ef):
