@@ -298,7 +298,9 @@ int jg_graph_sync(jg_graph* g);
 /* Process-wide performance knobs (no effect on results): "pull_unroll" (4 | 8 gathers in flight per
  * lane), "pull_nt" (0 | 1: non-temporal loads of the streamed adjacency), "pull_lds", "light_lds",
  * "slice_lds", "pull_short", "pull_overlap"; read when a graph is built: "pull_split", "band<i>_deg",
- * "band<i>_bit", "halo" (sharded graphs: sparse halo exchange, 0 = dense allgather).
+ * "band<i>_bit", "halo" (sharded graphs: sparse halo exchange, 0 = dense allgather).  Every key with
+ * its default and measurement is listed in `struct Tune` (janusgraph_amd/csrc/jg_internal.h), e.g.
+ * "msbfs_skip" (bit-parallel BFS merge-task skip), "cc_first" (CC union-find first-round links).
  * Unknown key: JG_ERR_ARG. */
 int jg_tune_set(const char* key, int64_t value);
 
