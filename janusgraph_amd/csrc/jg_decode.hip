@@ -811,8 +811,8 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     if (narrow) fit(c.d_meta8, 2 * E);
     const bool capped = limit_ > 0;
     if (capped) {
-        fit(c.slice, E + 1);
-        fit(c.pre, E + 1);
+        fit(c.slice, E);
+        fit(c.pre, E + 1);  // the scan of E flags writes pre[0..E]; pre[E] = total (read at pre[row_off[R]])
         fit(c.out_flag, E);
         fit(c.in_flag, E);
         fit(c.truncated, 1);
@@ -858,12 +858,11 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     }
     if (capped) {
         JG_HIP(hipMemsetAsync(c.truncated.get(), 0, sizeof(unsigned long long), s));
-        JG_HIP(hipMemsetAsync(c.slice.get() + E, 0, sizeof(uint32_t), s));
         if (E) {
             slice_flag_kernel<<<grid_for(E), kBlock, 0, s>>>(c.take.get(), E, c.slice.get());
             JG_LAUNCH_CHECK();
         }
-        prim::exclusive_scan_async(c.slice.get(), c.pre.get(), E + 1, c.scan_tmp.get(), s);
+        prim::exclusive_scan_async(c.slice.get(), c.pre.get(), E, c.scan_tmp.get(), s);
         if (R) {
             slice_cap_kernel<<<(unsigned)std::min<int64_t>(R, 4096), kBlock, 0, s>>>(c.d_roff.get(), R, c.pre.get(),
                                                                                      limit_, c.take.get(),
