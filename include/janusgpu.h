@@ -55,7 +55,9 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 1
+/* 2: jg_graph_info.exchange_values appended; jg_bfs_rows, jg_graph_neighbors added.  Callers must check
+ * jg_abi_version() == JG_ABI_VERSION before passing any struct across the ABI. */
+#define JG_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define JG_OK               0
@@ -259,6 +261,23 @@ int jg_shortest_distance(jg_graph* g, int64_t seed_vid, int32_t max_depth, int64
  * depth_out may be NULL (benchmarking: results stay on the device). */
 int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction,
            int32_t max_depth, int32_t* depth_out);
+
+/* The same traversal with one output row per source: depth_rows[s] (nullable, and the array itself)
+ * receives n int32 depths.  A Java direct buffer holds at most 2 GiB, so the 64 rows of one
+ * bit-parallel batch cannot share one buffer past 2^23 vertices (ShortestPathVertexProgram batches,
+ * java/.../GpuGraphComputer.java ShortestPaths). */
+int jg_bfs_rows(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth,
+                int32_t* const* depth_rows);
+
+/* Adjacency of vertices rows[0, nrows) (output-order indices), in output-order indices: the host copy
+ * of the snapshot a path walk-back reads where Fulgora re-reads each vertex's preloaded BOTH slice
+ * (graphdb/olap/computer/VertexProgramScanJob.java:113-135).  direction JG_DIR_BOTH (a self-loop
+ * appears twice, multi-edges repeat), JG_DIR_OUT or JG_DIR_IN (the adjacency must have been built).
+ * off_out[nrows + 1] = exclusive prefix of the rows' entry counts; nbr_out[off_out[nrows]] (nullable:
+ * size first, then fill) = the neighbours.  Every shard must live in this process (not rank mode:
+ * JG_ERR_UNSUPPORTED). */
+int jg_graph_neighbors(const jg_graph* g, int32_t direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
+                       int64_t* nbr_out);
 
 /* ConnectedComponentVertexProgram: component_vid_out[v] = the vertex id whose decimal String is the
  * component label (the String-minimum id of v's weakly connected component).  iterations_out

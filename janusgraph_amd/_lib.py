@@ -40,8 +40,9 @@ EXPORTS = [
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_combine_steps", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set", "jg_builder_create", "jg_builder_add_vertices", "jg_builder_add_edges", "jg_builder_set_schema",
     "jg_builder_add_rows", "jg_builder_finish", "jg_builder_destroy", "jg_graph_vertex_ids",
-    "jg_builder_set_query_limit",
+    "jg_builder_set_query_limit", "jg_bfs_rows", "jg_graph_neighbors",
 ]
+ABI_VERSION = 2  # JG_ABI_VERSION of include/janusgpu.h this binding's structs follow
 
 
 class GraphInfo(ctypes.Structure):
@@ -177,11 +178,15 @@ def load():
         "jg_builder_destroy": ([_P], ctypes.c_int),
         "jg_graph_vertex_ids": ([_P, _i64, _i64, _P], ctypes.c_int),
         "jg_builder_set_query_limit": ([_P, _i64, _i32], ctypes.c_int),
+        "jg_bfs_rows": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
+        "jg_graph_neighbors": ([_P, _i32, _P, _i64, _P, _P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if L.jg_abi_version() != ABI_VERSION:
+        raise ImportError(f"libjanusgpu.so has ABI {L.jg_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     # JG_TUNE="key=value,key=value": performance knobs for profiling runs (results are unaffected)
     for item in filter(None, os.environ.get("JG_TUNE", "").split(",")):
@@ -470,6 +475,31 @@ class Graph:
         depth = self._out(len(src) * self.n, np.int32) if want else None
         check(load().jg_bfs(self._h, _ptr(src), len(src), int(direction), int(max_depth), _ptr(depth)))
         return None if depth is None else depth.reshape(len(src), self.n)
+
+    def bfs_rows(self, sources, direction=DIR_BOTH, max_depth=-1, want=None):
+        """jg_bfs_rows: one depth array per source (want[s] False: that row stays on the device)."""
+        src = np.ascontiguousarray(np.atleast_1d(sources), np.int64)
+        want = [True] * len(src) if want is None else list(want)
+        rows = [self._out(self.n, np.int32) if w else None for w in want]
+        ptrs = (ctypes.c_void_p * len(src))(*[None if r is None else r.ctypes.data for r in rows])
+        check(load().jg_bfs_rows(self._h, _ptr(src), len(src), int(direction), int(max_depth), ptrs))
+        return rows
+
+    def neighbors(self, rows, direction=DIR_BOTH):
+        """jg_graph_neighbors: (off, nbr) CSR of the given output-order rows, in output-order indices."""
+        r = np.ascontiguousarray(np.atleast_1d(rows), np.int64)
+        off = np.empty(len(r) + 1, np.int64)
+        check(load().jg_graph_neighbors(self._h, int(direction), _ptr(r), len(r), _ptr(off), None))
+        nbr = np.empty(max(int(off[-1]), 1), np.int64)
+        check(load().jg_graph_neighbors(self._h, int(direction), _ptr(r), len(r), _ptr(off), _ptr(nbr)))
+        return off, nbr[:int(off[-1])]
+
+    def degrees(self, direction=DIR_BOTH, rows=None):
+        """Entries per row of the `direction` adjacency (jg_graph_neighbors' offsets only), all rows by default."""
+        r = np.arange(self.n, dtype=np.int64) if rows is None else np.ascontiguousarray(rows, np.int64)
+        off = np.empty(len(r) + 1, np.int64)
+        check(load().jg_graph_neighbors(self._h, int(direction), _ptr(r), len(r), _ptr(off), None))
+        return np.diff(off)
 
     def combine_steps(self, direction, combiner=COMBINE_SUM, steps=1, init=None, int32_wrap=True):
         """jg_combine_steps: `steps` supersteps of x[v] = COMBINE over v's `direction` entries of x[w].

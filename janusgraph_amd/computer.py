@@ -15,7 +15,6 @@ the GPU does not run raise ProgramNotSupported (the Java side delegates those to
 from __future__ import annotations
 
 import concurrent.futures as cf
-import math
 import time
 
 import numpy as np
@@ -251,26 +250,26 @@ class GpuGraphComputer:
         raise ProgramNotSupported(type(vp).__name__)
 
     def _shortest_paths(self, ctx, vp):
+        """ShortestPaths.execute of the Java drop-in: one depth row per source (jg_bfs_rows, 64 sources
+        per bit-parallel pass), paths rebuilt by PathDag over the snapshot's BOTH adjacency."""
         vid, src, dst, _ = self.graph.snapshot()
-        present = set(vid.tolist())
-        sources = [s for s in (vp.sources if vp.sources is not None else vid.tolist()) if s in present]
-        targets = set(vp.targets) if vp.targets is not None else None
+        index = {int(v): i for i, v in enumerate(vid.tolist())}
+        sources = [index[s] for s in (vp.sources if vp.sources is not None else vid.tolist()) if s in index]
+        target = None
+        if vp.targets is not None:
+            target = np.zeros(len(vid), bool)
+            target[[index[t] for t in vp.targets if t in index]] = True
         g = ctx.build(vid, src, dst, flags=_lib.ADJ_BOTH)
         paths, max_level = [], 0
         try:
-            if sources:
-                depth = g.bfs(np.asarray(sources, np.int64), _lib.DIR_BOTH,
-                              -1 if vp.max_distance is None else vp.max_distance)
-                max_level = int(depth.max(initial=0))
-                adj = _undirected_adjacency(vid, src, dst)
-                index = {int(v): i for i, v in enumerate(vid.tolist())}
-                for si, s in enumerate(sources):
-                    d = depth[si]
-                    for ti in np.nonzero(d >= 0)[0]:
-                        t = int(vid[ti])
-                        if targets is not None and t not in targets:
-                            continue
-                        paths.extend(_all_shortest_paths(adj, index, d, vid, index[s], int(ti)))
+            dag = PathDag(g.neighbors, len(vid))
+            for b0 in range(0, len(sources), SOURCES_PER_BFS):
+                batch = sources[b0:b0 + SOURCES_PER_BFS]
+                rows = g.bfs_rows(vid[batch], _lib.DIR_BOTH, -1 if vp.max_distance is None else vp.max_distance)
+                for s, depth in zip(batch, rows):
+                    got, deepest = dag.paths(depth, s, target)
+                    max_level = max(max_level, deepest)
+                    paths.extend([int(vid[x]) for x in p] for p in got)
         finally:
             g.close()
         return vid, {}, max_level + 1, {vp.SHORTEST_PATHS: paths}
@@ -287,28 +286,65 @@ class GpuGraphComputer:
         return ComputedGraph(self.graph, props)
 
 
-def _undirected_adjacency(vid, src, dst):
-    index = {int(v): i for i, v in enumerate(vid.tolist())}
-    adj = [[] for _ in range(len(vid))]
-    for a, b in zip(src.tolist(), dst.tolist()):
-        if a in index and b in index:
-            adj[index[a]].append(index[b])
-            adj[index[b]].append(index[a])
-    return adj
+SOURCES_PER_BFS = 64  # jg_bfs_rows: one bit-parallel pass per 64 sources
 
 
-def _all_shortest_paths(adj, index, depth, vid, s, t):
-    """Every shortest s..t path (vertex ids) from a BFS depth array, walking back from t."""
-    out = []
+class PathDag:
+    """Every shortest path from one source to the targets it reaches, rebuilt from its depth row (mirror
+    of GpuGraphComputer.PathDag, java/.../GpuGraphComputer.java): the predecessors of a vertex at depth d
+    are its BOTH neighbours at depth d - 1, read level by level from the device snapshot
+    (jg_graph_neighbors), deepest targets first, so each vertex on some path is expanded once; paths are
+    then enumerated from each target (ascending) back to the source.  `neighbors(rows)` -> (off, nbr)."""
 
-    def back(v, suffix):
-        if v == s:
-            out.append([int(vid[x]) for x in reversed(suffix + [v])])
-            return
-        for u in sorted(set(adj[v])):
-            if depth[u] == depth[v] - 1:
-                back(u, suffix + [v])
+    ROWS_PER_CALL = 1 << 14
 
-    if depth[t] >= 0 and not math.isinf(depth[t]):
-        back(t, [])
-    return out
+    def __init__(self, neighbors, n):
+        self.neighbors = neighbors
+        self.n = n
+
+    def predecessors(self, depth, target=None):
+        """{vertex: predecessor array} for every vertex on a shortest path to a target; and the targets."""
+        depth = np.asarray(depth)
+        reached = depth >= 0
+        if target is not None:
+            reached &= target
+        targets = np.flatnonzero(reached)
+        if len(targets) == 0:
+            return {}, targets, -1
+        deepest = int(depth[targets].max())
+        level = [[] for _ in range(deepest + 1)]
+        for d in range(deepest + 1):
+            level[d] = list(targets[depth[targets] == d])
+        queued = np.zeros(self.n, bool)
+        queued[targets] = True
+        pred = {}
+        for d in range(deepest, 0, -1):
+            cur = np.asarray(level[d], np.int64)
+            for f in range(0, len(cur), self.ROWS_PER_CALL):
+                rows = cur[f:f + self.ROWS_PER_CALL]
+                off, nbr = self.neighbors(rows)
+                for i, v in enumerate(rows.tolist()):
+                    nb = nbr[off[i]:off[i + 1]]
+                    nb = nb[depth[nb] == d - 1]
+                    _, first = np.unique(nb, return_index=True)
+                    p = nb[np.sort(first)]  # distinct, in adjacency order
+                    pred[v] = p
+                    new = p[~queued[p]]
+                    queued[new] = True
+                    level[d - 1].extend(new.tolist())
+        return pred, targets, deepest
+
+    def paths(self, depth, s, target=None):
+        """(paths as vertex-index lists, deepest target depth (0 if none))."""
+        pred, targets, deepest = self.predecessors(depth, target)
+        out = []
+        for t in targets.tolist():
+            stack = [(t, [t])]
+            while stack:
+                v, suffix = stack.pop()
+                if v == s:
+                    out.append(list(reversed(suffix)))
+                    continue
+                for u in reversed(pred[v].tolist()):  # first predecessor first, as the Java recursion
+                    stack.append((u, suffix + [u]))
+        return out, max(deepest, 0)

@@ -1129,7 +1129,27 @@ int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direct
            int32_t* depth_out) {
     JG_GUARD_BEGIN
     JG_ARG(g && source_vids, "null argument");
-    jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, depth_out);
+    JG_ARG(nsrc > 0, "nsrc must be positive");
+    std::vector<int32_t*> rows;
+    if (depth_out)
+        for (int32_t s = 0; s < nsrc; ++s) rows.push_back(depth_out + (int64_t)s * g->impl.n);
+    jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, depth_out ? rows.data() : nullptr);
+    JG_GUARD_END
+}
+
+int jg_bfs_rows(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth,
+                int32_t* const* depth_rows) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && source_vids, "null argument");
+    jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, depth_rows);
+    JG_GUARD_END
+}
+
+int jg_graph_neighbors(const jg_graph* g, int32_t direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
+                       int64_t* nbr_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    jg::graph_neighbors(g->impl, direction, rows, nrows, off_out, nbr_out);
     JG_GUARD_END
 }
 

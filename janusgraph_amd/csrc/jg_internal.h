@@ -413,7 +413,11 @@ void edgestore_snapshot(const EdgestoreRows& r, int device, DevBuf<int64_t>& vid
 void pagerank_begin(Graph& g, double damping, int64_t vertex_count);
 void pagerank_steps(Graph& g, int nsteps);
 void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
-void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out);
+// depth_rows[s] (each nullable, the array too): source s's depths in caller order (n int32)
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows);
+// jg_graph_neighbors: the adjacency `direction` of caller vertices rows[0, nrows) in caller order
+void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
+                     int64_t* nbr_out);
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
 // The union-find's result on one shard (jg_cc.hip): parent[v] is v's root for v < ne, minr[root] the

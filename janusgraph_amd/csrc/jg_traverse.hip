@@ -1193,7 +1193,7 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth) 
 }
 
 
-void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* depth_out) {
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows) {
     if (nsrc <= 0) fail(JG_ERR_ARG, "nsrc must be positive");
     if (direction < JG_DIR_OUT || direction > JG_DIR_BOTH) fail(JG_ERR_ARG, "bad direction");
     Ctx& ctx = *g.ctx;
@@ -1216,8 +1216,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.levels = levels;
         ctx.last.supersteps = levels;
         ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
-        if (depth_out)
-            for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.get(), depth_out);
+        if (depth_rows && depth_rows[0])
+            for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.get(), depth_rows[0]);
         prof_collect(ctx, g);
     } else if (single) {
         Shard& sh = sh0;
@@ -1248,7 +1248,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.edges_traversed = direction == JG_DIR_BOTH ? edges / 2 : edges;
         const Csr* degcsr = c.push ? c.push : c.pull;
         ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
-        if (depth_out) rows_to_dense(g, sh, depth.get(), depth_out);
+        if (depth_rows && depth_rows[0]) rows_to_dense(g, sh, depth.get(), depth_rows[0]);
         prof_collect(ctx, g);
     } else {
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
@@ -1499,11 +1499,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventElapsedTime(&ms, t0, t1));
             total_ms += ms;
             max_levels = std::max(max_levels, level);
-            if (depth_out)
+            if (depth_rows)
                 for (size_t i = 0; i < g.shards.size(); ++i)
                     for (int s = 0; s < ns; ++s)
-                        rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
-                                      depth_out + (int64_t)(b0 + s) * g.n);
+                        if (depth_rows[b0 + s])
+                            rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
+                                          depth_rows[b0 + s]);
         }
         ctx.last.compute_ms = total_ms;
         ctx.last.levels = max_levels;

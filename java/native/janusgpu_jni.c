@@ -12,6 +12,7 @@
 #include <jni.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "janusgpu.h"
 
@@ -22,6 +23,13 @@ static void* buf(JNIEnv* env, jobject b) { return b ? (*env)->GetDirectBufferAdd
 static void put_handle(JNIEnv* env, jlongArray out, const void* h) {
     jlong v = (jlong)(intptr_t)h;
     (*env)->SetLongArrayRegion(env, out, 0, 1, &v);
+}
+
+/* Refuse to load against a libjanusgpu whose structs and entry points differ from the header this shim
+ * was compiled with (JanusGpu.java checks the same number from the Java side). */
+JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void* reserved) {
+    (void)vm; (void)reserved;
+    return jg_abi_version() == JG_ABI_VERSION ? JNI_VERSION_1_8 : JNI_ERR;
 }
 
 JNIEXPORT jint JNICALL FN(abiVersion)(JNIEnv* env, jclass c) { (void)env; (void)c; return jg_abi_version(); }
@@ -154,6 +162,29 @@ JNIEXPORT jint JNICALL FN(bfs)(JNIEnv* env, jclass c, jlong g, jobject sources, 
     (void)c;
     return jg_bfs((jg_graph*)(intptr_t)g, (const int64_t*)buf(env, sources), nsrc, direction, max_depth,
                   (int32_t*)buf(env, depth_out));
+}
+
+JNIEXPORT jint JNICALL FN(bfsRows)(JNIEnv* env, jclass c, jlong g, jobject sources, jint nsrc, jint direction,
+                                   jint max_depth, jobjectArray depth_rows) {
+    (void)c;
+    if (nsrc <= 0 || (*env)->GetArrayLength(env, depth_rows) < nsrc) return JG_ERR_ARG;
+    int32_t** rows = (int32_t**)malloc(sizeof(int32_t*) * (size_t)nsrc);
+    if (!rows) return JG_ERR_OOM;
+    for (jint s = 0; s < nsrc; ++s) {
+        jobject b = (*env)->GetObjectArrayElement(env, depth_rows, s);
+        rows[s] = (int32_t*)buf(env, b);
+        if (b) (*env)->DeleteLocalRef(env, b);
+    }
+    int st = jg_bfs_rows((jg_graph*)(intptr_t)g, (const int64_t*)buf(env, sources), nsrc, direction, max_depth, rows);
+    free(rows);
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(graphNeighbors)(JNIEnv* env, jclass c, jlong g, jint direction, jobject rows, jlong nrows,
+                                          jobject off_out, jobject nbr_out) {
+    (void)c;
+    return jg_graph_neighbors((const jg_graph*)(intptr_t)g, direction, (const int64_t*)buf(env, rows), nrows,
+                              (int64_t*)buf(env, off_out), (int64_t*)buf(env, nbr_out));
 }
 
 JNIEXPORT jint JNICALL FN(connectedComponents)(JNIEnv* env, jclass c, jlong g, jobject comp_out,

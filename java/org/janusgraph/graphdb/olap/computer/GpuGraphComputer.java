@@ -11,49 +11,49 @@ import org.apache.tinkerpop.gremlin.process.computer.VertexProgram;
 import org.apache.tinkerpop.gremlin.process.computer.clustering.connected.ConnectedComponentVertexProgram;
 import org.apache.tinkerpop.gremlin.process.computer.search.path.ShortestPathVertexProgram;
 import org.apache.tinkerpop.gremlin.process.computer.util.DefaultComputerResult;
-import org.apache.tinkerpop.gremlin.process.computer.util.GraphComputerHelper;
 import org.apache.tinkerpop.gremlin.process.computer.util.VertexProgramHelper;
 import org.apache.tinkerpop.gremlin.process.traversal.Path;
 import org.apache.tinkerpop.gremlin.process.traversal.Traversal;
 import org.apache.tinkerpop.gremlin.process.traversal.step.util.ImmutablePath;
 import org.apache.tinkerpop.gremlin.process.traversal.util.PureTraversal;
 import org.apache.tinkerpop.gremlin.process.traversal.util.TraversalUtil;
-import org.apache.tinkerpop.gremlin.structure.Direction;
 import org.apache.tinkerpop.gremlin.structure.Edge;
 import org.apache.tinkerpop.gremlin.structure.Graph;
 import org.apache.tinkerpop.gremlin.structure.Vertex;
 import org.apache.tinkerpop.gremlin.structure.VertexProperty;
 import org.apache.tinkerpop.gremlin.structure.util.empty.EmptyGraph;
 import org.apache.tinkerpop.gremlin.structure.util.reference.ReferenceFactory;
-import org.janusgraph.core.JanusGraphComputer;
 import org.janusgraph.core.JanusGraphException;
 import org.janusgraph.core.JanusGraphTransaction;
 import org.janusgraph.core.schema.JanusGraphManagement;
 import org.janusgraph.diskstorage.configuration.Configuration;
-import org.janusgraph.diskstorage.keycolumnvalue.scan.ScanMetrics;
-import org.janusgraph.diskstorage.keycolumnvalue.scan.StandardScanner;
 import org.janusgraph.graphdb.configuration.GraphDatabaseConfiguration;
 import org.janusgraph.graphdb.database.StandardJanusGraph;
 import org.janusgraph.graphdb.olap.QueryContainer;
 import org.janusgraph.graphdb.util.WorkerPool;
+import org.slf4j.Logger;
+import org.slf4j.LoggerFactory;
 
 import java.lang.reflect.Field;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.nio.DoubleBuffer;
+import java.nio.IntBuffer;
+import java.nio.LongBuffer;
 import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.BitSet;
 import java.util.Collections;
 import java.util.HashMap;
 import java.util.HashSet;
-import java.util.Iterator;
-import java.util.LinkedHashMap;
 import java.util.List;
 import java.util.Map;
 import java.util.Objects;
-import java.util.Optional;
 import java.util.Set;
 import java.util.concurrent.CompletableFuture;
 import java.util.concurrent.Future;
 import java.util.concurrent.atomic.AtomicInteger;
+import java.util.function.IntFunction;
 
 /**
  * Drop-in for {@link FulgoraGraphComputer} that runs the superstep loop of the recognised programs on
@@ -69,21 +69,26 @@ import java.util.concurrent.atomic.AtomicInteger;
  *       component property key);</li>
  *   <li>TinkerPop ShortestPathVertexProgram with its default edge and distance traversals (any source /
  *       target filter, any maxDistance; includeEdges off): hop depths on the GPU (BOTH edges, as
- *       FulgoraGraphComputer.java:249-253 forces), paths rebuilt from the depths.</li>
+ *       FulgoraGraphComputer.java:249-253 forces), paths rebuilt from the depths over the snapshot's
+ *       own BOTH adjacency.</li>
  * </ul>
  * The edgestore is scanned ONCE into a device CSR (GpuSnapshot) instead of once per superstep. The
- * results then go through Fulgora's own machinery where it applies: the FulgoraMemory of the run,
- * the map phase (columnar emission for PageRankMapReduce / ShortestDistanceMapReduce, otherwise
- * Fulgora's VertexMapJob scan over a FulgoraVertexMemory holding the results), the reduce phase
- * (FulgoraGraphComputer.java:331-357) and the write-back of the non-transient compute keys
- * (:359-471: ORIGINAL in batch transactions, NEW in an uncommitted transaction).
+ * results then go through Fulgora's own machinery, opened to subclasses by
+ * java/patches/0002-FulgoraGraphComputer-protected-phases.patch: the settings check and FulgoraMemory
+ * of submit() (FulgoraGraphComputer.java:154-193), the map phase (columnar emission for
+ * PageRankMapReduce / ShortestDistanceMapReduce, otherwise Fulgora's executeMapJobs VertexMapJob scan
+ * over a FulgoraVertexMemory holding the results) and executeReducePhase (:331-357). The write-back
+ * of the non-transient compute keys goes straight from the result columns (:359-471 semantics:
+ * ORIGINAL in batch transactions, NEW in an uncommitted transaction).
  *
  * Entry: {@code graph.compute(GpuGraphComputer.class)} once JanusGraphBlueprintsGraph.compute(Class)
  * (janusgraph-core/.../tinkerpop/JanusGraphBlueprintsGraph.java:155-161) whitelists this class
- * (java/patches/); the transaction variant delegates to it. Devices: system property
+ * (java/patches/0001); the transaction variant delegates to it. Devices: system property
  * janusgraph.computer.gpu.devices (comma list, default "0"); several devices shard the graph 1D.
  */
 public class GpuGraphComputer extends FulgoraGraphComputer {
+
+    private static final Logger log = LoggerFactory.getLogger(GpuGraphComputer.class);
 
     static final String PR = "org.janusgraph.olap.PageRankVertexProgram";
     static final String SD = "org.janusgraph.olap.ShortestDistanceVertexProgram";
@@ -92,19 +97,12 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
     static final String PAGE_RANK = "janusgraph.pageRank.pageRank";
     static final String EDGE_COUNT = "janusgraph.pageRank.edgeCount";
     static final String DISTANCE = "janusgraph.shortestDistanceVertexProgram.distance";
-    static final int SOURCES_PER_BFS = 64; // jg_bfs: one bit-parallel pass per 64 sources
-
-    private static final AtomicInteger COMPUTERS = new AtomicInteger();
+    static final int SOURCES_PER_BFS = 64; // jg_bfs_rows: one bit-parallel pass per 64 sources
 
     private final StandardJanusGraph graph;
     private final int writeBatchSize;
     private VertexProgram<?> vertexProgram;
-    private final Set<MapReduce> mapReduces = new HashSet<>();
-    private ResultGraph resultGraphMode;
-    private Persist persistMode;
-    private int numThreads = 1;
     private boolean filtered;
-    private boolean executed;
 
     public GpuGraphComputer(final StandardJanusGraph graph, final Configuration configuration) {
         super(graph, configuration);
@@ -112,7 +110,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         this.writeBatchSize = configuration.get(GraphDatabaseConfiguration.BUFFER_SIZE);
     }
 
-    // ---- the GraphComputer builder: recorded here and passed on to Fulgora (the delegate path) ----
+    // ---- the GraphComputer builder: Fulgora records the settings; the GPU path reads them back ----
 
     @Override
     public GraphComputer vertices(final Traversal<Vertex, Vertex> vertexFilter) {
@@ -127,37 +125,9 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
     }
 
     @Override
-    public GraphComputer result(final ResultGraph resultGraph) {
-        super.result(resultGraph);
-        resultGraphMode = resultGraph;
-        return this;
-    }
-
-    @Override
-    public GraphComputer persist(final Persist persist) {
-        super.persist(persist);
-        persistMode = persist;
-        return this;
-    }
-
-    @Override
-    public JanusGraphComputer workers(final int threads) {
-        super.workers(threads);
-        numThreads = threads;
-        return this;
-    }
-
-    @Override
     public GraphComputer program(final VertexProgram program) {
         super.program(program);
         vertexProgram = program;
-        return this;
-    }
-
-    @Override
-    public GraphComputer mapReduce(final MapReduce mapReduce) {
-        super.mapReduce(mapReduce);
-        mapReduces.add(mapReduce);
         return this;
     }
 
@@ -167,21 +137,14 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
     public Future<ComputerResult> submit() {
         final GpuProgram run = (vertexProgram == null || filtered) ? null : GpuProgram.recognise(vertexProgram, graph);
         if (run == null) return super.submit(); // everything else stays on Fulgora, unchanged
-        if (executed) throw Exceptions.computerHasAlreadyBeenSubmittedAVertexProgram();
-        executed = true;
-        // FulgoraGraphComputer.ensureSettingsAreValid (:171-190)
-        GraphComputerHelper.validateProgramOnComputer(this, vertexProgram);
-        mapReduces.addAll(vertexProgram.getMapReducers());
-        persistMode = GraphComputerHelper.getPersistState(Optional.of(vertexProgram), Optional.ofNullable(persistMode));
-        resultGraphMode = GraphComputerHelper.getResultGraphState(Optional.of(vertexProgram),
-            Optional.ofNullable(resultGraphMode));
-        if (!features().supportsResultGraphPersistCombination(resultGraphMode, persistMode))
-            throw Exceptions.resultGraphPersistCombinationNotSupported(resultGraphMode, persistMode);
-        final FulgoraMemory memory = new FulgoraMemory(vertexProgram, mapReduces);
-        return CompletableFuture.supplyAsync(() -> submitAsync(run, memory));
+        // FulgoraGraphComputer.submit (:154-162) up to the superstep loop
+        guardAgainstDuplicateSubmission();
+        ensureSettingsAreValid();
+        initializeMemory();
+        return CompletableFuture.supplyAsync(() -> submitAsync(run));
     }
 
-    private ComputerResult submitAsync(final GpuProgram run, final FulgoraMemory memory) {
+    private ComputerResult submitAsync(final GpuProgram run) {
         final long time = System.currentTimeMillis();
         vertexProgram.setup(memory);
         final long[] h = new long[1];
@@ -202,7 +165,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
         // supersteps 0..K ran: Fulgora's memory counts K + 1 and complete() reports K (FulgoraMemory.java:97-101)
         memory.setIteration(res.iteration + 1);
-        executeMapReduce(res, memory);
+        executeMapReduce(res);
         final Graph resultGraph = writeBack(res);
         memory.setRuntime(System.currentTimeMillis() - time);
         memory.complete();
@@ -226,85 +189,45 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         return d;
     }
 
+    /** One direct buffer: at most 2 GiB (per-vertex 8-byte columns: up to 2^28 vertices). */
     static ByteBuffer direct(long bytes) {
         if (bytes > Integer.MAX_VALUE)
-            throw new JanusGraphException("GPU computer: " + bytes + " bytes exceed one direct buffer; the graph has "
-                + "more than 2^28 vertices");
+            throw new JanusGraphException("GPU computer: " + bytes + " bytes exceed one direct buffer (2 GiB)");
         return ByteBuffer.allocateDirect((int) Math.max(bytes, 8)).order(ByteOrder.nativeOrder());
     }
 
-    // ---- map / reduce (FulgoraGraphComputer.java:288-357) ----
+    // ---- map / reduce: Fulgora's phases (FulgoraGraphComputer.java:288-357) ----
 
-    private void executeMapReduce(final Results res, final FulgoraMemory memory) {
-        final Map<MapReduce, FulgoraMapEmitter> mapJobs = new LinkedHashMap<>();
-        for (MapReduce mr : mapReduces)
-            if (mr.doStage(MapReduce.Stage.MAP)) mapJobs.put(mr, new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE)));
+    private void executeMapReduce(final Results res) {
+        final Map<MapReduce, FulgoraMapEmitter> mapJobs = collectMapJobs();
         if (mapJobs.isEmpty()) return;
         boolean columnar = true;
         for (MapReduce mr : mapJobs.keySet()) {
             final String name = mr.getClass().getName();
             columnar &= name.equals(PR_MAP) || name.equals(SD_MAP);
         }
-        if (columnar) {
-            // PageRankMapReduce / ShortestDistanceMapReduce.map emit (vertex.id(), the compute key's value)
-            // where it is present (PageRankMapReduce.java:62-67, ShortestDistanceMapReduce.java:59-64):
-            // emitted straight from the result columns, without a second edgestore scan.
-            for (Map.Entry<MapReduce, FulgoraMapEmitter> job : mapJobs.entrySet()) {
-                final Column col = res.column(job.getKey().getClass().getName().equals(PR_MAP) ? PAGE_RANK : DISTANCE);
-                final FulgoraMapEmitter emitter = job.getValue();
-                job.getKey().workerStart(MapReduce.Stage.MAP);
-                for (int i = 0; i < res.vid.length; i++) {
-                    final Object v = col == null ? null : col.get(i);
-                    if (v != null) emitter.emit(res.vid[i], v);
-                }
-                job.getKey().workerEnd(MapReduce.Stage.MAP);
-            }
-        } else {
-            // any other MapReduce sees what Fulgora gives it: the scanned vertices with the compute keys
-            // mixed in from a FulgoraVertexMemory (VertexMapJob.java:107-130)
-            final FulgoraVertexMemory vertexMemory = res.toVertexMemory(graph, vertexProgram);
-            try (VertexMapJob.Executor job = VertexMapJob.getVertexMapJob(graph, vertexMemory, mapJobs)) {
-                final StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
-                scan.setJobId("gpu" + COMPUTERS.incrementAndGet() + "#map");
-                scan.setNumProcessingThreads(numThreads);
-                scan.setWorkBlockSize(writeBatchSize * 10);
-                scan.setJob(job);
-                final ScanMetrics metrics = scan.execute().get();
-                if (metrics.get(ScanMetrics.Metric.FAILURE) > 0)
-                    throw new JanusGraphException("Failed to process [" + metrics.get(ScanMetrics.Metric.FAILURE)
-                        + "] vertices in map phase. Computer is aborting.");
-                if (metrics.getCustom(VertexMapJob.MAP_JOB_FAILURE) > 0)
-                    throw new JanusGraphException("Failed to process [" + metrics.getCustom(VertexMapJob.MAP_JOB_FAILURE)
-                        + "] individual map jobs. Computer is aborting.");
-            } catch (JanusGraphException e) {
-                throw e;
-            } catch (Exception e) {
-                throw new JanusGraphException(e);
-            }
+        if (!columnar) {
+            // any other MapReduce sees what Fulgora gives it: Fulgora's VertexMapJob scan over the vertex
+            // memory it would hold after the supersteps (VertexMapJob.java:107-130), then its reduce phase
+            vertexMemory = res.toVertexMemory(graph, vertexProgram);
+            executeMapJobs(mapJobs);
+            return;
         }
-        for (Map.Entry<MapReduce, FulgoraMapEmitter> mapJob : mapJobs.entrySet()) {
-            final FulgoraMapEmitter<?, ?> mapEmitter = mapJob.getValue();
-            final MapReduce mapReduce = mapJob.getKey();
-            mapEmitter.complete(mapReduce);
-            if (mapReduce.doStage(MapReduce.Stage.REDUCE)) {
-                final FulgoraReduceEmitter<?, ?> reduceEmitter = new FulgoraReduceEmitter<>();
-                try (WorkerPool workers = new WorkerPool(numThreads)) {
-                    workers.submit(() -> mapReduce.workerStart(MapReduce.Stage.REDUCE));
-                    for (final Map.Entry queueEntry : mapEmitter.reduceMap.entrySet()) {
-                        if (null == queueEntry) break;
-                        workers.submit(() -> mapReduce.reduce(queueEntry.getKey(),
-                            ((Iterable) queueEntry.getValue()).iterator(), reduceEmitter));
-                    }
-                    workers.submit(() -> mapReduce.workerEnd(MapReduce.Stage.REDUCE));
-                } catch (Exception e) {
-                    throw new JanusGraphException("Exception while executing reduce phase", e);
-                }
-                reduceEmitter.complete(mapReduce);
-                mapReduce.addResultToMemory(memory, reduceEmitter.reduceQueue.iterator());
-            } else {
-                mapReduce.addResultToMemory(memory, mapEmitter.mapQueue.iterator());
+        // PageRankMapReduce / ShortestDistanceMapReduce.map emit (vertex.id(), the compute key's value)
+        // where it is present (PageRankMapReduce.java:62-67, ShortestDistanceMapReduce.java:59-64):
+        // emitted straight from the result columns, without a second edgestore scan
+        for (Map.Entry<MapReduce, FulgoraMapEmitter> job : mapJobs.entrySet()) {
+            final Column col = res.column(job.getKey().getClass().getName().equals(PR_MAP) ? PAGE_RANK : DISTANCE);
+            final FulgoraMapEmitter emitter = job.getValue();
+            job.getKey().workerStart(MapReduce.Stage.MAP);
+            for (int i = 0; i < res.vid.length; i++) {
+                final Object v = col == null ? null : col.get(i);
+                if (v != null) emitter.emit(res.vid[i], v);
             }
+            job.getKey().workerEnd(MapReduce.Stage.MAP);
         }
+        executeReducePhase(mapJobs);
+        memory.attachReferenceElements(graph);
     }
 
     // ---- write-back (FulgoraGraphComputer.java:359-471) ----
@@ -355,6 +278,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
                         }
                         tx.commit();
                     } catch (Throwable e) {
+                        log.error("Encountered exception while trying to write properties: ", e);
                         failures.incrementAndGet();
                     } finally {
                         if (tx.isOpen()) tx.rollback();
@@ -409,31 +333,36 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
     }
 
+    // Columns read the output buffers through typed views: element indices, no byte offsets.
+
     static Column doubles(String key, ByteBuffer buf) {
+        final DoubleBuffer d = buf.asDoubleBuffer();
         return new Column(key) {
             @Override
             Object get(int i) {
-                final double d = buf.getDouble(8 * i);
-                return Double.isNaN(d) ? null : d; // NaN: no superstep wrote the property (K == 0)
+                final double x = d.get(i);
+                return Double.isNaN(x) ? null : x; // NaN: no superstep wrote the property (K == 0)
             }
         };
     }
 
     static Column distances(String key, ByteBuffer buf) {
+        final LongBuffer d = buf.asLongBuffer();
         return new Column(key) {
             @Override
             Object get(int i) {
-                final long l = buf.getLong(8 * i);
+                final long l = d.get(i);
                 return l == JanusGpu.DIST_ABSENT ? null : l;
             }
         };
     }
 
     static Column components(String key, ByteBuffer buf) {
+        final LongBuffer d = buf.asLongBuffer();
         return new Column(key) {
             @Override
             Object get(int i) {
-                return Long.toString(buf.getLong(8 * i)); // the label is the id's String form
+                return Long.toString(d.get(i)); // the label is the id's String form
             }
         };
     }
@@ -589,8 +518,9 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
             final VertexProgram<?> defaults = ConnectedComponentVertexProgram.build().create(graph);
             final BaseConfiguration conf = state(vp), def = state(defaults);
             final Set<String> free = new HashSet<>();
+            final String key = property;
             conf.getKeys().forEachRemaining(k -> {
-                if (property.equals(String.valueOf(conf.getProperty(k)))) free.add(k);
+                if (key.equals(String.valueOf(conf.getProperty(k)))) free.add(k);
             });
             def.getKeys().forEachRemaining(k -> {
                 if (ConnectedComponentVertexProgram.COMPONENT.equals(String.valueOf(def.getProperty(k)))) free.add(k);
@@ -617,8 +547,9 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
     /**
      * ShortestPathVertexProgram with its default edge (bothE) and distance (unit) traversals and no
      * edges in the paths: every shortest path from each source to each target, as the program's
-     * shortestPaths memory key. Depths come from the GPU (DIR_BOTH, the forced scope); paths are
-     * walked back from each target over neighbours one level closer.
+     * shortestPaths memory key. Depths come from the GPU (DIR_BOTH, the forced scope), one depth row
+     * per source (jg_bfs_rows: 64 rows of n int32 do not fit one direct buffer past 2^23 vertices);
+     * paths are rebuilt from each row by {@link PathDag} over the snapshot's BOTH adjacency.
      */
     static final class ShortestPaths extends GpuProgram {
         final BaseConfiguration conf;
@@ -667,33 +598,43 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
 
         @Override
         Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory) {
+            final int n = vid.length;
             final JanusGraphTransaction tx = graph.buildTransaction().readOnly().start();
             try {
-                final List<Integer> sources = new ArrayList<>();
-                final boolean[] target = new boolean[vid.length];
-                final Map<Long, Integer> index = new HashMap<>();
-                for (int i = 0; i < vid.length; i++) {
-                    index.put(vid[i], i);
-                    final Vertex v = (sourceFilter == null && targetFilter == null) ? null : tx.getVertex(vid[i]);
-                    if (sourceFilter == null || TraversalUtil.test(v, sourceFilter.clone())) sources.add(i);
-                    target[i] = targetFilter == null || TraversalUtil.test(v, targetFilter.clone());
+                final int[] sources;
+                BitSet target = null; // null: every vertex is a target
+                if (sourceFilter == null && targetFilter == null) {
+                    sources = new int[n];
+                    for (int i = 0; i < n; i++) sources[i] = i;
+                } else {
+                    final PathDag.IntArray s = new PathDag.IntArray();
+                    if (targetFilter != null) target = new BitSet(n);
+                    for (int i = 0; i < n; i++) {
+                        final Vertex v = tx.getVertex(vid[i]);
+                        if (sourceFilter == null || TraversalUtil.test(v, sourceFilter.clone())) s.add(i);
+                        if (target != null && TraversalUtil.test(v, targetFilter.clone())) target.set(i);
+                    }
+                    sources = s.toArray();
                 }
+                final Map<Integer, Vertex> detached = new HashMap<>(); // path elements, detached once each
+                final IntFunction<Vertex> element =
+                    i -> detached.computeIfAbsent(i, x -> ReferenceFactory.detach(tx.getVertex(vid[x])));
+                final PathDag dag = new PathDag(g, n);
                 final List<Path> paths = new ArrayList<>();
                 int maxLevel = 0;
-                for (int b = 0; b < sources.size(); b += SOURCES_PER_BFS) {
-                    final int k = Math.min(SOURCES_PER_BFS, sources.size() - b);
-                    final ByteBuffer src = direct(8L * k), depth = direct(4L * k * vid.length);
-                    for (int j = 0; j < k; j++) src.putLong(vid[sources.get(b + j)]);
-                    JanusGpu.check(JanusGpu.bfs(g, src, k, JanusGpu.DIR_BOTH, maxDistance, depth));
+                for (int b = 0; b < sources.length; b += SOURCES_PER_BFS) {
+                    final int k = Math.min(SOURCES_PER_BFS, sources.length - b);
+                    final ByteBuffer src = direct(8L * k);
+                    final ByteBuffer[] rows = new ByteBuffer[k];
                     for (int j = 0; j < k; j++) {
-                        final int s = sources.get(b + j);
-                        final int base = 4 * j * vid.length;
-                        for (int t = 0; t < vid.length; t++) {
-                            final int d = depth.getInt(base + 4 * t);
-                            if (d < 0 || !target[t]) continue;
-                            maxLevel = Math.max(maxLevel, d);
-                            walkBack(tx, vid, index, depth, base, s, t, new ArrayList<>(), paths);
-                        }
+                        src.putLong(vid[sources[b + j]]);
+                        rows[j] = direct(4L * n);
+                    }
+                    JanusGpu.check(JanusGpu.bfsRows(g, src, k, JanusGpu.DIR_BOTH, maxDistance, rows));
+                    for (int j = 0; j < k; j++) {
+                        final IntBuffer depth = rows[j].asIntBuffer();
+                        rows[j] = null;
+                        maxLevel = Math.max(maxLevel, dag.paths(depth, sources[b + j], target, element, paths));
                     }
                 }
                 memory.set(ShortestPathVertexProgram.SHORTEST_PATHS, paths);
@@ -702,26 +643,133 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
                 tx.rollback();
             }
         }
+    }
 
-        /** Every shortest s..t path, walking from t to neighbours one level closer to s. */
-        private static void walkBack(JanusGraphTransaction tx, long[] vid, Map<Long, Integer> index, ByteBuffer depth,
-                                     int base, int s, int t, List<Integer> suffix, List<Path> out) {
-            suffix.add(t);
-            if (t == s) {
-                Path p = ImmutablePath.make();
-                for (int i = suffix.size() - 1; i >= 0; i--)
-                    p = p.extend(ReferenceFactory.detach(tx.getVertex(vid[suffix.get(i)])), Collections.emptySet());
-                out.add(p);
-            } else {
-                final int dt = depth.getInt(base + 4 * t);
-                final Set<Integer> seen = new HashSet<>();
-                for (Iterator<Vertex> it = tx.getVertex(vid[t]).vertices(Direction.BOTH); it.hasNext(); ) {
-                    final Integer u = index.get((Long) it.next().id());
-                    if (u != null && seen.add(u) && depth.getInt(base + 4 * u) == dt - 1)
-                        walkBack(tx, vid, index, depth, base, s, u, suffix, out);
+    /**
+     * Every shortest path from one source to the targets it reaches, rebuilt from its depth row: the
+     * predecessors of a vertex at depth d are its BOTH neighbours at depth d - 1. They are read level by
+     * level from the device snapshot (jg_graph_neighbors), deepest targets first, so each vertex on some
+     * path is expanded once and no OLTP transaction is touched; the paths are then enumerated from each
+     * target (ascending) back to the source.
+     */
+    static final class PathDag {
+        private static final int ROWS_PER_CALL = 1 << 14;
+        private final long graph;
+        private final int[] mark; // de-duplicates a vertex's neighbours (multi-edges, self-loops)
+        private int stamp;
+
+        PathDag(long graph, int n) {
+            this.graph = graph;
+            this.mark = new int[n];
+        }
+
+        /** Adds the source's paths to `out`; returns the deepest target depth (0 when none). */
+        int paths(IntBuffer depth, int s, BitSet target, IntFunction<Vertex> element, List<Path> out) {
+            final int n = mark.length;
+            final List<IntArray> level = new ArrayList<>();
+            final BitSet queued = new BitSet(n);
+            final IntArray targets = new IntArray();
+            int deepest = -1;
+            for (int t = 0; t < n; t++) {
+                final int d = depth.get(t);
+                if (d < 0 || (target != null && !target.get(t))) continue;
+                while (level.size() <= d) level.add(new IntArray());
+                level.get(d).add(t);
+                queued.set(t);
+                targets.add(t);
+                deepest = Math.max(deepest, d);
+            }
+            if (deepest < 0) return 0;
+            final Map<Integer, int[]> pred = new HashMap<>();
+            for (int d = deepest; d >= 1; d--) {
+                final int[] cur = level.get(d).toArray();
+                for (int from = 0; from < cur.length; from += ROWS_PER_CALL) {
+                    final int to = Math.min(cur.length, from + ROWS_PER_CALL);
+                    final long[][] adj = neighbors(cur, from, to);
+                    for (int i = from; i < to; i++) {
+                        final IntArray p = new IntArray();
+                        ++stamp;
+                        for (long e = adj[0][i - from]; e < adj[0][i - from + 1]; e++) {
+                            final int u = (int) adj[1][(int) e];
+                            if (mark[u] == stamp || depth.get(u) != d - 1) continue;
+                            mark[u] = stamp;
+                            p.add(u);
+                            if (!queued.get(u)) {
+                                queued.set(u);
+                                level.get(d - 1).add(u);
+                            }
+                        }
+                        pred.put(cur[i], p.toArray());
+                    }
                 }
             }
-            suffix.remove(suffix.size() - 1);
+            final IntArray suffix = new IntArray();
+            for (int t : targets.toArray()) walk(pred, s, t, suffix, element, out);
+            return deepest;
+        }
+
+        private static void walk(Map<Integer, int[]> pred, int s, int v, IntArray suffix, IntFunction<Vertex> element,
+                                 List<Path> out) {
+            suffix.add(v);
+            if (v == s) {
+                Path p = ImmutablePath.make();
+                for (int i = suffix.size() - 1; i >= 0; i--) p = p.extend(element.apply(suffix.get(i)), Collections.emptySet());
+                out.add(p);
+            } else {
+                for (int u : pred.get(v)) walk(pred, s, u, suffix, element, out);
+            }
+            suffix.pop();
+        }
+
+        /** {offsets[to - from + 1], neighbours} of rows[from, to): two jg_graph_neighbors calls (size, fill). */
+        private long[][] neighbors(int[] rows, int from, int to) {
+            final int k = to - from;
+            final ByteBuffer r = direct(8L * k), off = direct(8L * (k + 1));
+            for (int i = from; i < to; i++) r.putLong(rows[i]);
+            JanusGpu.check(JanusGpu.graphNeighbors(graph, JanusGpu.DIR_BOTH, r, k, off, null));
+            final long[] o = new long[k + 1];
+            off.asLongBuffer().get(o);
+            if (8L * o[k] > Integer.MAX_VALUE && k > 1) { // a hub-heavy batch: split it
+                final int mid = from + k / 2;
+                final long[][] a = neighbors(rows, from, mid), b = neighbors(rows, mid, to);
+                final long[] oo = Arrays.copyOf(a[0], k + 1);
+                for (int i = 1; i < b[0].length; i++) oo[mid - from + i] = a[0][mid - from] + b[0][i];
+                final long[] nn = Arrays.copyOf(a[1], a[1].length + b[1].length);
+                System.arraycopy(b[1], 0, nn, a[1].length, b[1].length);
+                return new long[][] {oo, nn};
+            }
+            final ByteBuffer nb = direct(8L * o[k]);
+            JanusGpu.check(JanusGpu.graphNeighbors(graph, JanusGpu.DIR_BOTH, r, k, off, nb));
+            final long[] nbr = new long[(int) o[k]];
+            nb.asLongBuffer().get(nbr);
+            return new long[][] {o, nbr};
+        }
+
+        /** A growable int list. */
+        static final class IntArray {
+            private int[] a = new int[8];
+            private int size;
+
+            void add(int v) {
+                if (size == a.length) a = Arrays.copyOf(a, 2 * size);
+                a[size++] = v;
+            }
+
+            int get(int i) {
+                return a[i];
+            }
+
+            void pop() {
+                --size;
+            }
+
+            int size() {
+                return size;
+            }
+
+            int[] toArray() {
+                return Arrays.copyOf(a, size);
+            }
         }
     }
 }

@@ -18,8 +18,14 @@ import java.nio.ByteBuffer;
  * per-vertex arrays (n * 8 bytes). Java 8 target (pom.xml:112-113): JNI, not Panama.
  */
 final class JanusGpu {
+    /** JG_ABI_VERSION of include/janusgpu.h that these natives and their array layouts follow. */
+    static final int ABI_VERSION = 2;
+
     static {
         System.loadLibrary("janusgpu_jni"); // links libjanusgpu.so
+        if (abiVersion() != ABI_VERSION)
+            throw new ExceptionInInitializerError("libjanusgpu ABI " + abiVersion() + ", GpuGraphComputer needs "
+                + ABI_VERSION + ": rebuild libjanusgpu and libjanusgpu_jni");
     }
 
     static final int ADJ_OUT = 1, ADJ_IN = 2, ADJ_BOTH = 4;
@@ -67,6 +73,13 @@ final class JanusGpu {
                                ByteBuffer edgeCountOut);
     static native int shortestDistance(long graph, long seedVid, int maxDepth, ByteBuffer distOut);
     static native int bfs(long graph, ByteBuffer sourceVids, int nsrc, int direction, int maxDepth, ByteBuffer depthOut);
+    /** jg_bfs_rows: one int32 direct buffer of n depths per source (null: not wanted). */
+    static native int bfsRows(long graph, ByteBuffer sourceVids, int nsrc, int direction, int maxDepth,
+                              ByteBuffer[] depthRows);
+    /** jg_graph_neighbors: rows (int64 output-order indices) -> offsets (int64, nrows + 1) and neighbours
+     *  (int64 output-order indices; null: offsets only). */
+    static native int graphNeighbors(long graph, int direction, ByteBuffer rows, long nrows, ByteBuffer offOut,
+                                     ByteBuffer nbrOut);
     static native int connectedComponents(long graph, ByteBuffer componentVidOut, int[] iterationsOut);
     /** jg_combine_steps: sum/min/max MessageCombiner programs (OLAPTest.DegreeCounter family). */
     static native int combineSteps(long graph, int direction, int combiner, int int32Wrap, ByteBuffer init, int steps,

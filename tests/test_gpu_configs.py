@@ -5,8 +5,12 @@ Every result is checked against the CPU restatement in oracle/ on the same Graph
 (the device generator is bit-identical to oracle.rmat_edges):
   configs[1]  SPVP BFS, RMAT-20 ef16, 1 GPU: depths from 3 sources (and depth-bounded) bit-exact.
   configs[2]  PageRank fp64, RMAT-24 ef16, K = 30 (29 power steps), vertexCount = |V|: per-vertex
-              relative error <= 1e-9, edgeCount exact; on 1 shard and on 8 logical shards.
-  configs[3]  ConnectedComponent, RMAT-26 ef16: every String-min label and the iteration count exact.
+              relative error <= 1e-9, edgeCount exact; on 1 shard and on 2, 4 and 8 logical shards (the
+              1/2/4/8-GPU layouts and halo exchanges on one device).
+  configs[3]  ConnectedComponent, RMAT-26 ef16: every String-min label and the iteration count exact, on
+              1 shard (union-find + root BFS) and on 2 and 8 logical shards (the label propagation with
+              its halo exchange that 2..8 GPUs run), plus the sharded single-source DO-BFS (dobfs_sharded,
+              what a BFS on 2..8 GPUs runs) from 3 degree > 0 sources on the same sharded graphs.
   configs[4]  64-source MS-BFS, RMAT-26 ef16 on 8 logical shards (the 8-GPU layout and halo exchange on
               one device): all 64 depth rows bit-exact, plus Graph500 validation of 3 of them.
 The oracle side uses the parallel checkers of jg_oracle.c (jo_csr_unordered, jo_bfs_csr,
@@ -90,7 +94,7 @@ def assert_pr(rank, ec, want, ec_want):
     assert rel.max() <= PR_RTOL, f"max rel err {rel.max()}"
 
 
-@pytest.mark.parametrize("shards", [1, 8])
+@pytest.mark.parametrize("shards", [1, 2, 4, 8])
 def test_config2_pagerank_rmat24(pr24, shards):
     import janusgraph_amd as jg
     n, ec_want, want = pr24
@@ -130,6 +134,31 @@ def test_config3_cc_rmat26(rmat26):
     assert it == r["cc_it"]
     assert it < 99  # Fulgora's 100-iteration cap does not bind
     np.testing.assert_array_equal(comp, r["vid_of_rank"][r["label"]])
+    g.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_config3_sharded_cc_and_dobfs_rmat26(oracle_lib, rmat26, shards):
+    """The code paths 2..8 GPUs run at configs[3]'s size: CC by label propagation over the BOTH halo
+    (not the one-shard union-find), and single-source DO-BFS by dobfs_sharded (halo refresh for
+    bottom-up levels, stamps and the reverse exchange for top-down levels)."""
+    import janusgraph_amd as jg
+    o = oracle_lib
+    r = rmat26
+    n = r["n"]
+    ctx = jg.Context((0,) * shards)
+    g = ctx.build_rmat(26, EF, seed_of(26), flags=jg.ADJ_BOTH)
+    assert g.info()["num_shards"] == shards and g.info()["exchange_values"] > 0
+    comp, it = g.connected_components()
+    assert it == r["cc_it"], f"{shards} shards: {it} supersteps, oracle {r['cc_it']}"
+    np.testing.assert_array_equal(comp, r["vid_of_rank"][r["label"]])
+    del comp
+    for sv in pick_sources(r["ptr"], 3, 126 + shards):
+        got = g.bfs([int(sv)], jg.DIR_BOTH)[0]
+        np.testing.assert_array_equal(got, o.bfs_csr(n, r["ptr"], r["adj"], int(sv)),
+                                      err_msg=f"{shards} shards: DO-BFS from {sv}")
+        assert ctx.stats()["levels"] > 2
     g.close()
     ctx.close()
 

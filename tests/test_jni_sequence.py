@@ -5,8 +5,9 @@ native below is the C-ABI call the shim makes, with the buffers GpuSnapshot / Gp
   ctxCreate -> builderCreate -> builderSetQueryLimit (100000: Fulgora's slice cap) -> builderSetSchema ->
   builderAddRows (one per scan chunk of whole rows,
   entry weights for ShortestDistance) -> builderFinish -> builderDestroy -> graphInfo ->
-  graphVertexIds (chunks) -> pageRank | shortestDistance | connectedComponents | bfs (64 sources per
-  call, ShortestPathVertexProgram) -> graphDestroy -> ctxDestroy
+  graphVertexIds (chunks) -> pageRank | shortestDistance | connectedComponents | bfsRows (64 sources
+  per call, one 4n-byte buffer per source, ShortestPathVertexProgram) + graphNeighbors (PathDag: the
+  size call, then the fill call) -> graphDestroy -> ctxDestroy
 
 Results are checked against the oracle's restatement of the scan (oracle.edgestore_snapshot) and
 programs.
@@ -146,6 +147,27 @@ def test_connected_components_sequence(oracle_lib, store):
     r.close()
 
 
+def jni_bfs_rows(L, g, src_vids, n, max_depth):
+    """JanusGpu.bfsRows as ShortestPaths.execute calls it: one direct(4L * n) buffer per source."""
+    src = np.ascontiguousarray(src_vids, np.int64)
+    rows = [np.empty(n, np.int32) for _ in range(len(src))]
+    ptrs = (ctypes.c_void_p * len(src))(*[r.ctypes.data for r in rows])
+    _ok(L.jg_bfs_rows(g, _p(src), len(src), 3, max_depth, ptrs))  # JanusGpu.DIR_BOTH
+    return rows
+
+
+def jni_neighbors(L, g):
+    """PathDag.neighbors: JanusGpu.graphNeighbors once for the offsets, once more for the neighbours."""
+    def call(rows):
+        r = np.ascontiguousarray(rows, np.int64)
+        off = np.empty(len(r) + 1, np.int64)
+        _ok(L.jg_graph_neighbors(g, 3, _p(r), len(r), _p(off), None))
+        nbr = np.empty(max(int(off[-1]), 1), np.int64)
+        _ok(L.jg_graph_neighbors(g, 3, _p(r), len(r), _p(off), _p(nbr)))
+        return off, nbr[:int(off[-1])]
+    return call
+
+
 def all_shortest_paths(adj, s, t):
     """Every shortest s..t path by plain BFS (the check, not the Java walk-back)."""
     dist = {s: 0}
@@ -172,8 +194,9 @@ def all_shortest_paths(adj, s, t):
 
 
 def test_shortest_path_sequence_batches_of_64(oracle_lib, store):
-    """ShortestPaths.execute: 70 sources -> two jg_bfs calls (64 + 6), DIR_BOTH, maxDistance; paths
-    rebuilt by walking back over neighbours one level closer."""
+    """ShortestPaths.execute: 70 sources -> two jg_bfs_rows calls (64 + 6), DIR_BOTH, maxDistance; paths
+    rebuilt by PathDag (predecessors read through jg_graph_neighbors) -> every shortest path."""
+    from janusgraph_amd.computer import PathDag
     ov, ds, dd = oracle_graph(oracle_lib, store)
     r = JavaRun(store[0], flags=4)
     n = len(r.vid)
@@ -182,35 +205,84 @@ def test_shortest_path_sequence_batches_of_64(oracle_lib, store):
         adj[a].append(b)
         adj[b].append(a)
     sources = list(range(70))
-    targets = set(range(0, n, 9))
+    target = np.zeros(n, bool)
+    target[::9] = True
     max_distance = 3
+    dag = PathDag(jni_neighbors(r.L, r.g), n)
     got = set()
     for b0 in range(0, len(sources), 64):
-        k = min(64, len(sources) - b0)
-        src = np.array([ov[s] for s in sources[b0:b0 + k]], np.int64)
-        depth = np.empty(k * n, np.int32)
-        _ok(r.L.jg_bfs(r.g, _p(src), k, 3, max_distance, _p(depth)))
-        depth = depth.reshape(k, n)
-        for j in range(k):
-            s = sources[b0 + j]
-            for t in range(n):
-                if depth[j, t] < 0 or t not in targets:
-                    continue
-
-                def walk(v, suffix):
-                    suffix = suffix + [v]
-                    if v == s:
-                        got.add(tuple(reversed(suffix)))
-                        return
-                    for u in sorted(set(adj[v])):
-                        if depth[j, u] == depth[j, v] - 1:
-                            walk(u, suffix)
-                walk(t, [])
+        batch = sources[b0:b0 + 64]
+        rows = jni_bfs_rows(r.L, r.g, ov[batch], n, max_distance)
+        for s, depth in zip(batch, rows):
+            paths, _ = dag.paths(depth, s, target)
+            got |= {tuple(p) for p in paths}
     want = set()
     for s in sources:
-        for t in targets:
+        for t in np.flatnonzero(target).tolist():
             for p in all_shortest_paths(adj, s, t):
                 if len(p) - 1 <= max_distance:
                     want.add(p)
     assert got == want and len(got) > 70
     r.close()
+
+
+def test_shortest_path_sequence_rmat24(oracle_lib):
+    """ShortestPaths.execute at BASELINE scale (configs[4]'s program on RMAT-24, n = 2^24): a 64-source
+    batch as 64 separate 4n-byte depth buffers (one 64 x n buffer would be 4 GiB, past Java's 2 GiB
+    direct-buffer limit), vertex ids read back in GpuSnapshot.vertexIds chunks of 2^24; three depth rows
+    against oracle.bfs_csr, and PathDag's predecessor lists and path counts against the oracle's CSR."""
+    from janusgraph_amd import _lib
+    from janusgraph_amd.computer import PathDag
+    from test_gpu_configs import host_edges, pick_sources
+    o = oracle_lib
+    scale = 24
+    n = 1 << scale
+    s, d = host_edges(o, scale)
+    vid = (np.arange(n, dtype=np.int64) + 1) << 8  # graph.set-vertex-id ids (IDManager.toVertexId)
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    _ok(L.jg_ctx_create((ctypes.c_int * 1)(0), 1, ctypes.byref(ctx)))
+    b = ctypes.c_void_p()
+    _ok(L.jg_builder_create(ctx, ctypes.byref(b)))
+    _ok(L.jg_builder_add_vertices(b, _p(vid), n))
+    step = 1 << 26  # 512 MB int64 chunks: each under a direct buffer's 2 GiB
+    for e0 in range(0, len(s), step):
+        cs = np.ascontiguousarray(vid[s[e0:e0 + step]])
+        cd = np.ascontiguousarray(vid[d[e0:e0 + step]])
+        _ok(L.jg_builder_add_edges(b, _p(cs), _p(cd), None, len(cs)))
+    g = ctypes.c_void_p()
+    _ok(L.jg_builder_finish(b, 4, ctypes.byref(g)))  # JanusGpu.ADJ_BOTH
+    _ok(L.jg_builder_destroy(b))
+    chunk = 1 << 24
+    got_vid = np.empty(n, np.int64)
+    for off in range(0, n, chunk):
+        _ok(L.jg_graph_vertex_ids(g, off, min(chunk, n - off), _p(got_vid[off:])))
+    np.testing.assert_array_equal(got_vid, vid)
+    ptr, adj = o.csr_unordered(n, s, d, both=True)
+    del s, d
+    srcs = pick_sources(ptr, 64, scale)
+    rows = jni_bfs_rows(L, g, vid[srcs], n, -1)
+    for k in (0, 31, 63):
+        np.testing.assert_array_equal(rows[k], o.bfs_csr(n, ptr, adj, int(srcs[k])))
+    depth = rows[0]
+    del rows[1:]
+    rng = np.random.default_rng(5)
+    reached = np.flatnonzero(depth >= 1)
+    target = np.zeros(n, bool)
+    target[rng.choice(reached, 60, replace=False)] = True
+    dag = PathDag(jni_neighbors(L, g), n)
+    pred, targets, _ = dag.predecessors(depth, target)
+    assert len(targets) == 60 and len(pred) >= 60
+    for v, p in pred.items():
+        nb = adj[ptr[v]:ptr[v + 1]]
+        np.testing.assert_array_equal(np.sort(p), np.unique(nb[depth[nb] == depth[v] - 1]))
+    # path counts of depth-2 targets: one path per distinct depth-1 neighbour
+    near = np.flatnonzero(depth == 2)[:20]
+    tmask = np.zeros(n, bool)
+    tmask[near] = True
+    paths, deepest = dag.paths(depth, int(srcs[0]), tmask)
+    assert deepest == 2
+    want = sum(len(np.unique(adj[ptr[t]:ptr[t + 1]][depth[adj[ptr[t]:ptr[t + 1]]] == 1])) for t in near.tolist())
+    assert len(paths) == want and all(p[0] == srcs[0] and len(p) == 3 for p in paths)
+    _ok(L.jg_graph_destroy(g))
+    _ok(L.jg_ctx_destroy(ctx))

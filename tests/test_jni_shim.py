@@ -11,7 +11,8 @@ SHIM = os.path.join(ROOT, "java", "native", "janusgpu_jni.c")
 HEADER = os.path.join(ROOT, "include", "janusgpu.h")
 
 JNI_TYPE = {"int": "jint", "long": "jlong", "double": "jdouble", "ByteBuffer": "jobject", "int[]": "jintArray",
-            "long[]": "jlongArray", "double[]": "jdoubleArray", "String": "jstring"}
+            "long[]": "jlongArray", "double[]": "jdoubleArray", "String": "jstring",
+            "ByteBuffer[]": "jobjectArray"}
 
 
 def java_natives():
