@@ -95,6 +95,22 @@ class Control:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def sum_array(self, a):
+        if not self.dist:
+            return a
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a, np.int64))
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.numpy()
+
+    def min_array(self, a):
+        if not self.dist:
+            return a
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a, np.int64))
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return t.numpy()
+
     def gather(self, row):
         """Every rank's list of floats, on every rank (rank order)."""
         if not self.dist:
@@ -110,10 +126,10 @@ class Control:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(kernel_tag="PrOp", workload=None):
-    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
-    (profiles/<round>/summary.json, made by tools/profile_round.sh + tools/pmc_summary.py on the same
-    bench workload).  None when no summary exists."""
+def pmc_traffic(workload):
+    """Fabric bytes per run of a workload from the newest committed rocprofv3 PMC summary whose "workload"
+    matches (profiles/<round>/**/summary.json, made by tools/pmc_workloads.sh + tools/pmc_summary.py from
+    runs of tools/workload.py / bench.py on the same workload).  (None, None) when there is none."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
         return None, None
@@ -121,24 +137,18 @@ def pmc_traffic(kernel_tag="PrOp", workload=None):
         rdir = os.path.join(pdir, rnd)
         if not os.path.isdir(rdir):
             continue
-        # the round's own summary first, then its per-workload ones (e.g. profiles/r02/pmc26/)
-        subs = [""] + sorted(d for d in os.listdir(rdir) if os.path.isdir(os.path.join(rdir, d)))
-        for sub in subs:
-            path = os.path.join(rdir, sub, "summary.json")
-            if not os.path.exists(path):
+        for dirpath, _, files in sorted(os.walk(rdir)):
+            if "summary.json" not in files:
                 continue
-            with open(path) as f:
+            with open(os.path.join(dirpath, "summary.json")) as f:
                 s = json.load(f)
-            if kernel_tag not in s.get("kernel", "") or s.get("traffic_bytes_per_launch") is None:
+            wl = s.get("workload")
+            if wl is None and os.path.exists(os.path.join(dirpath, "bench.json")):
+                with open(os.path.join(dirpath, "bench.json")) as f:
+                    wl = json.load(f).get("config", {}).get("workload")  # round-2 summaries
+            if wl != workload or s.get("traffic_bytes_per_launch") is None:
                 continue
-            bj = os.path.join(rdir, sub, "bench.json")
-            if workload:
-                if not os.path.exists(bj):
-                    continue
-                with open(bj) as f:
-                    if json.load(f).get("config", {}).get("workload") != workload:
-                        continue
-            rel = "/".join(x for x in ("profiles", rnd, sub, "summary.json") if x)
+            rel = os.path.relpath(os.path.join(dirpath, "summary.json"), ROOT)
             return s["traffic_bytes_per_launch"], f"{rel} ({s.get('read_bytes_method', '')})"
     return None, None
 
@@ -186,46 +196,77 @@ def cpu_baseline_bfs(scale, ef, seed, sources):
                       f"sources on the same RMAT-{scale} ef{ef} graph, {total:.2f} s of CPU BFS; CSR build untimed"}
 
 
-def hbm_roofline(alg_bytes, ms, kernel, traffic=None, traffic_src=None):
+def hbm_roofline(alg_bytes, ms, kernel, workload=None, model=None):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": kernel, "kernel_ms": round(ms, 4), "bytes_per_launch": alg_bytes}
+    traffic, traffic_src = pmc_traffic(workload) if workload else (None, None)
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+         "kernel": kernel, "kernel_ms": round(ms, 4), "bytes_per_launch": alg_bytes}
+    if model:
+        r["model"] = model
+    return r
 
 
-def bfs_block(jg, ctx, scale, ef, nsrc=6, cpu=True):
-    """Single-source DO-BFS (SPVP depth, BOTH edges) from seeded sources of degree > 0, Graph500 TEPS;
-    roofline of one traversal: 8*m + 12*n algorithmic bytes / its HIP-event time."""
+def pick_sources(degree, k, seed):
+    """Seeded uniform pick among vertices with at least one BOTH entry."""
+    cand = np.flatnonzero(degree > 0)
+    return np.random.default_rng(seed).choice(cand, min(k, len(cand)), replace=False).astype(np.int64)
+
+
+def both_degrees(jg, ctl, g):
+    """Entries per vertex of the BOTH adjacency (rank mode: each rank's rows, summed over ranks)."""
+    deg = g.degrees(jg.DIR_BOTH)
+    return ctl.sum_array(deg) if ctl.ws > 1 else deg
+
+
+def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
+    """Single-source DO-BFS (SPVP depth, BOTH edges) from seeded sources of degree > 0, Graph500 TEPS (input
+    edges of the source's component / time); roofline of one traversal: 8*m + 12*n algorithmic bytes
+    (one full pass) / its HIP-event time.  N > 1: the sharded DO-BFS (dobfs_sharded)."""
     n, m = 1 << scale, ef << scale
     gb = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
-    rng = np.random.default_rng(1)
-    times, teps, srcs = [], [], []
-    while len(srcs) < nsrc:
-        sv = int(rng.integers(0, n))
+    deg = both_degrees(jg, ctl, gb)
+    cand = pick_sources(deg, 4 * nsrc, scale)
+    times, teps, srcs, ranks = [], [], [], []
+    for sv in cand.tolist():
+        if len(srcs) == nsrc:
+            break
         gb.bfs([sv], jg.DIR_BOTH, want=False)
-        st = ctx.stats()
-        if st["edges_traversed"] < m // 100:
+        if ctx.stats()["edges_traversed"] < m // 100:
             continue  # a source in a tiny component: Graph500 resamples
         gb.bfs([sv], jg.DIR_BOTH, want=False)  # timed run (the first touched cold pages)
         st = ctx.stats()
+        ms = ctl.max(st["compute_ms"])
         srcs.append(sv)
-        times.append(st["compute_ms"])
-        teps.append(st["edges_traversed"] / (st["compute_ms"] * 1e-3) / 1e9)
+        times.append(ms)
+        teps.append(st["edges_traversed"] / (ms * 1e-3) / 1e9)
+        ranks.append(ctl.gather([st["compute_ms"], st["exchange_ms"]]))
     gb.close()
     ms = float(np.median(times))
-    blk = {"workload": f"bfs_spvp_rmat{scale}_ef{ef}", "gteps_median": round(float(np.median(teps)), 3),
-           "ms_median": round(ms, 4), "runs": len(times),
-           "roofline": hbm_roofline(8.0 * m + 12.0 * n, ms, "direction-optimising BFS, one traversal "
-                                    "(bfs_level_kernel launches)")}
-    if cpu:
+    workload = f"bfs_spvp_rmat{scale}_ef{ef}"
+    blk = {"workload": workload, "gteps_median": round(float(np.median(teps)), 3), "ms_median": round(ms, 4),
+           "runs": len(times), "sources": [int(x) for x in srcs]}
+    if ctl.ws == 1:
+        blk["roofline"] = hbm_roofline(8.0 * m + 12.0 * n, ms, "direction-optimising BFS, one traversal "
+                                       "(bfs_init_kernel + bfs_level_kernel launches)", workload,
+                                       "8*m + 12*n: every symmetrised entry (4 B) once, row_ptr (8 B) and depth "
+                                       "(4 B) per vertex (SURVEY.md 8d)")
+    else:
+        blk["per_rank"] = per_rank_rows(ranks[len(ranks) // 2])
+    if cpu and ctl.ws == 1:
         blk["cpu_baseline"] = cpu_baseline_bfs(scale, ef, 0x5EED + scale, srcs[:3])
     return blk
+
+
+def per_rank_rows(rows):
+    return [{"rank": r, "compute_ms": round(x[0], 4), "exchange_ms": round(x[1], 4)} for r, x in enumerate(rows)]
 
 
 def pagerank_block(jg, ctx, scale, ef, steps, warmup):
     n, m = 1 << scale, ef << scale
     g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_IN)
     build_ms = ctx.stats()["build_ms"]
+    live = int(np.count_nonzero(g.degrees(jg.DIR_IN)))
     g.pagerank_begin(0.85, n)
     g.pagerank_step(warmup)
     g.sync()
@@ -240,41 +281,80 @@ def pagerank_block(jg, ctx, scale, ef, steps, warmup):
     g.close()
     kern_ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
     workload = f"pagerank_fp64_rmat{scale}_ef{ef}"
-    traffic, traffic_src = pmc_traffic("PrOp", workload)
     return {"workload": workload, "ms_per_step": round(dt / steps * 1e3, 4),
             "gteps": round(m * steps / dt / 1e9, 3), "steps": steps, "build_ms": round(build_ms, 1),
             "roofline": hbm_roofline(12.0 * m + 32.0 * n, kern_ms, "PageRank superstep (same launch sequence "
-                                     "as the headline)", traffic, traffic_src)}
+                                     "as the headline)", workload, PR_MODEL),
+            "required": required_roofline(m, live, kern_ms)}
 
 
-def rmat26_both_blocks(jg, ctx, scale, ef):
-    """CC (configs[3]) and 64-source MS-BFS (configs[4], one GPU here) on the BOTH adjacency."""
+PR_MODEL = ("12*m + 32*n per superstep (SURVEY.md 8d): col (4 B) and gathered contribution (8 B) per edge; "
+            "row_ptr, 1/outdeg, rank write, contribution write (8 B each) per vertex")
+
+
+def required_roofline(m, live, ms):
+    """The bytes a superstep needs once the rows without in-edges are constant (written in the first two
+    power steps only) and the rank is stored on the last superstep only: 12*m + 24*live (row_ptr,
+    1/outdeg and the contribution write per row with an in-edge)."""
+    b = 12.0 * m + 24.0 * live
+    a = b / (ms * 1e-3) / 1e9
+    return {"bytes_per_launch": b, "rows_with_in_edges": live, "achieved": round(a, 1),
+            "frac": round(a / HBM_PEAK_GBS, 4)}
+
+
+def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
+    """CC (configs[3]) and 64-source MS-BFS (configs[4]) on the BOTH adjacency.  N > 1: every rank holds
+    its shard; CC runs the label propagation over the halo, MS-BFS the sharded bit-parallel pull."""
     n, m = 1 << scale, ef << scale
     g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
     build_ms = ctx.stats()["build_ms"]
+    deg = both_degrees(jg, ctl, g)
     g.connected_components()  # warm
     comp, it = g.connected_components()
     st = ctx.stats()
-    cc_ms = st["compute_ms"]
-    cc = {"workload": f"cc_rmat{scale}_ef{ef}", "ms": round(cc_ms, 3), "iterations": it,
-          "components": int(len(np.unique(comp))), "build_ms": round(build_ms, 1),
-          "equivalent_gteps_per_iteration": round(2 * m * it / (cc_ms * 1e-3) / 1e9, 2),
-          "note": "one shard: union-find labels + BFS superstep count (jg_cc.hip cc_union_find), identical labels "
-                  "and iterations to the label propagation; the per-iteration rate counts 2m entries per superstep "
-                  "of the equivalent propagation"}
-    del comp
-    rng = np.random.default_rng(7)
-    cand = rng.integers(0, n, 4 * 64)
-    srcs = np.unique(cand)[:64]
+    cc_ms = ctl.max(st["compute_ms"])
+    cc_rank = ctl.gather([st["compute_ms"], st["exchange_ms"]])
+    if ctl.ws > 1:
+        comp = ctl.min_array(comp)  # each rank filled its own rows (the others hold INT64_MAX)
+    counts = np.bincount(comp, minlength=n)  # RMAT ids are 0..n-1: labels are vertex ids
+    wl_cc = f"cc_rmat{scale}_ef{ef}"
+    cc = {"workload": wl_cc, "ms": round(cc_ms, 3), "iterations": it,
+          "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
+          "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
+                       "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"
+          if ctl.ws == 1 else "label propagation supersteps over the BOTH halo exchange"}
+    if ctl.ws == 1:
+        cc["roofline"] = hbm_roofline(st["algorithmic_bytes"], cc_ms, "ConnectedComponent run (uf_* kernels + "
+                                      "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
+                                      "98 B per row with an edge (union-find passes + BFS start), 12 B per entry "
+                                      "linked in the second round, 4 B per entry of the rows the BFS reached "
+                                      "(jg_cc.hip cc_union_find)")
+    else:
+        cc["per_rank"] = per_rank_rows(cc_rank)
+    # 64 sources among the degree > 0 vertices; TEPS counts each source's component edges
+    srcs = pick_sources(deg, 64, 7)
+    comp_edges = np.bincount(comp, weights=deg.astype(np.float64), minlength=n) / 2.0
+    edges = float(comp_edges[comp[srcs]].sum())
+    del comp, counts, comp_edges
     g.bfs(srcs, jg.DIR_BOTH, want=False)  # warm
     g.bfs(srcs, jg.DIR_BOTH, want=False)
     st = ctx.stats()
-    ms = {"workload": f"msbfs64_rmat{scale}_ef{ef}", "sources": int(len(srcs)), "ms": round(st["compute_ms"], 3),
-          "levels": st["levels"],
-          "gteps": round(len(srcs) * m / (st["compute_ms"] * 1e-3) / 1e9, 1),
-          "gteps_note": "sources x m input edges / time (Graph500 convention, the giant component holds ~all edges)"}
+    ms = ctl.max(st["compute_ms"])
+    wl_ms = f"msbfs64_rmat{scale}_ef{ef}"
+    msb = {"workload": wl_ms, "sources": int(len(srcs)), "ms": round(ms, 3), "levels": st["levels"],
+           "gteps": round(edges / (ms * 1e-3) / 1e9, 1),
+           "gteps_note": "sum over the 64 sources (degree > 0) of the input edges in the source's component / time"}
+    if ctl.ws == 1:
+        msb["roofline"] = hbm_roofline(st["algorithmic_bytes"], ms, "64-source bit-parallel BFS (MsBfsOp merge / "
+                                       "light kernels + msbfs_* kernels)", wl_ms,
+                                       "per pull level 12 B per entry of a live merge task and of the light rows "
+                                       "+ 24 B per row; per top-down level 12 B per frontier entry + 16 B per "
+                                       "touched word + 8 B per queued vertex; 4 B per reached (source, row) depth")
+        msb["entries_examined"] = st["edges_traversed"]
+    else:
+        msb["per_rank"] = per_rank_rows(ctl.gather([st["compute_ms"], st["exchange_ms"]]))
     g.close()
-    return cc, ms
+    return cc, msb
 
 
 def main():
@@ -298,6 +378,7 @@ def main():
     g = ctx.build_rmat(args.scale, args.edgefactor, args.seed, flags=jg.ADJ_IN)
     build_ms = ctx.stats()["build_ms"]
     info = g.info()
+    live = int(ctl.sum(float(np.count_nonzero(g.degrees(jg.DIR_IN)))))  # rows with an in-edge, all ranks
     g.pagerank_begin(0.85, n)
     g.pagerank_step(args.warmup)
     g.sync()
@@ -324,9 +405,10 @@ def main():
     if ws > 1:
         alg_bytes_launch = (12.0 * m + 32.0 * n) / ws  # this rank's share (rows and entries are balanced)
     workload = f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}"
-    traffic, traffic_src = pmc_traffic("PrOp", workload) if ws == 1 else (None, None)
     roofline = hbm_roofline(alg_bytes_launch, kern_ms, "PageRank superstep (pull_merge_kernel x bands + fixup + "
-                            "fused light-row/finalize kernel, PrOp)", traffic, traffic_src)
+                            "fused light-row/finalize kernel, PrOp)", workload if ws == 1 else None, PR_MODEL)
+    if ws == 1:
+        roofline["required"] = required_roofline(m, live, kern_ms)
     per_rank = None
     if ws > 1:
         # every rank's own numbers, gathered on rank 0: superstep kernel time, exchange time, halo volume
@@ -339,15 +421,17 @@ def main():
     g.close()
 
     extra = {}
-    if ws == 1 and not args.no_bfs:
-        extra["bfs"] = bfs_block(jg, ctx, args.bfs_scale, args.edgefactor, cpu=not args.no_cpu)
-    if ws == 1 and not args.no_big:
+    if not args.no_bfs and ws == 1:
+        extra["bfs"] = bfs_block(jg, ctx, ctl, args.bfs_scale, args.edgefactor, cpu=not args.no_cpu)
+    if not args.no_big:
+        # N > 1: the configs[3] / [4] workloads on N GPUs (sharded DO-BFS, CC propagation, sharded MS-BFS)
         big = args.big_scale
-        extra[f"rmat{big}"] = {"pagerank": pagerank_block(jg, ctx, big, args.edgefactor, args.big_steps, 3),
-                               "bfs": bfs_block(jg, ctx, big, args.edgefactor, nsrc=4, cpu=False)}
-        cc, msbfs = rmat26_both_blocks(jg, ctx, big, args.edgefactor)
-        extra[f"rmat{big}"]["cc"] = cc
-        extra[f"rmat{big}"]["msbfs64"] = msbfs
+        blk = {}
+        if ws == 1:
+            blk["pagerank"] = pagerank_block(jg, ctx, big, args.edgefactor, args.big_steps, 3)
+        blk["bfs"] = bfs_block(jg, ctx, ctl, big, args.edgefactor, nsrc=4, cpu=False)
+        blk["cc"], blk["msbfs64"] = rmat26_both_blocks(jg, ctx, ctl, big, args.edgefactor)
+        extra[f"rmat{big}"] = blk
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

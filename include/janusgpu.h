@@ -221,6 +221,31 @@ int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, 
  * fitted query and never capped.  limit = 0 (the default) builds the untruncated graph.  Rows only
  * (jg_builder_add_rows); call before the first chunk. */
 int jg_builder_set_query_limit(jg_builder* b, int64_t limit, int32_t in_entries);
+/* Edge weights decoded on the GPU from the rows (ShortestDistanceVertexProgram's Integer property,
+ * ShortestDistanceVertexProgram.java:69) instead of per-entry host weights: an edge's properties follow
+ * its ids in its value as (inline key id, value) pairs in ascending key-id order
+ * (graphdb/database/EdgeSerializer.java:294-302; inline id = IDManager.stripRelationTypePadding(key id),
+ * VariableLong.writePositive, idhandling/IDHandler.java:155-158; values per StandardSerializer.writeObject:
+ * a null flag byte unless String, then the attribute serializer's bytes).  weight_key = the inline id of the
+ * weight key; key_ids / key_types (nkeys) = every property key an edge may carry before it, with its
+ * JG_PROP_* type (an edge holding a key of unknown type before the weight: JG_ERR_UNSUPPORTED at finish).
+ * The weight is JG_WEIGHT_ABSENT where the edge has no non-null Integer value for the key; a stored
+ * Integer.MIN_VALUE collides with that marker and fails the build (JG_ERR_UNSUPPORTED).  The edge labels
+ * must have no signature keys (their values precede the inline pairs without ids): the caller checks.
+ * Rows only, before the first chunk; add_rows then takes no entry_weight. */
+#define JG_PROP_BYTE   1
+#define JG_PROP_SHORT  2
+#define JG_PROP_INT    3
+#define JG_PROP_LONG   4
+#define JG_PROP_CHAR   5
+#define JG_PROP_BOOL   6
+#define JG_PROP_DATE   7
+#define JG_PROP_FLOAT  8
+#define JG_PROP_DOUBLE 9
+#define JG_PROP_UUID   10
+#define JG_PROP_STRING 11
+int jg_builder_set_weight_key(jg_builder* b, int64_t weight_key, const int64_t* key_ids, const int8_t* key_types,
+                              int32_t nkeys);
 int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out);
 int jg_builder_destroy(jg_builder* b);
 /* vid_out[i] = the id of vertex offset + i in output order (the order vid[] / the kept rows were given). */
@@ -274,8 +299,8 @@ int jg_bfs_rows(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t d
  * (graphdb/olap/computer/VertexProgramScanJob.java:113-135).  direction JG_DIR_BOTH (a self-loop
  * appears twice, multi-edges repeat), JG_DIR_OUT or JG_DIR_IN (the adjacency must have been built).
  * off_out[nrows + 1] = exclusive prefix of the rows' entry counts; nbr_out[off_out[nrows]] (nullable:
- * size first, then fill) = the neighbours.  Every shard must live in this process (not rank mode:
- * JG_ERR_UNSUPPORTED). */
+ * size first, then fill) = the neighbours.  Rank mode (jg_ctx_create_rank*): entry counts only
+ * (nbr_out must be NULL, else JG_ERR_UNSUPPORTED), and rows of other ranks count 0 entries. */
 int jg_graph_neighbors(const jg_graph* g, int32_t direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
                        int64_t* nbr_out);
 

@@ -40,8 +40,11 @@ EXPORTS = [
     "jg_pagerank_end", "jg_shortest_distance", "jg_bfs", "jg_connected_components", "jg_combine_steps", "jg_decode_edges", "jg_graph_sync",
     "jg_tune_set", "jg_builder_create", "jg_builder_add_vertices", "jg_builder_add_edges", "jg_builder_set_schema",
     "jg_builder_add_rows", "jg_builder_finish", "jg_builder_destroy", "jg_graph_vertex_ids",
-    "jg_builder_set_query_limit", "jg_bfs_rows", "jg_graph_neighbors",
+    "jg_builder_set_query_limit", "jg_bfs_rows", "jg_graph_neighbors", "jg_builder_set_weight_key",
 ]
+# JG_PROP_* property value types (jg_builder_set_weight_key)
+PROP_BYTE, PROP_SHORT, PROP_INT, PROP_LONG, PROP_CHAR, PROP_BOOL, PROP_DATE, PROP_FLOAT, PROP_DOUBLE, PROP_UUID, \
+    PROP_STRING = range(1, 12)
 ABI_VERSION = 2  # JG_ABI_VERSION of include/janusgpu.h this binding's structs follow
 
 
@@ -180,6 +183,7 @@ def load():
         "jg_builder_set_query_limit": ([_P, _i64, _i32], ctypes.c_int),
         "jg_bfs_rows": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
         "jg_graph_neighbors": ([_P, _i32, _P, _i64, _P, _P], ctypes.c_int),
+        "jg_builder_set_weight_key": ([_P, _i64, _P, _P, _i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -383,6 +387,15 @@ class Builder:
         adjacency from the rows' IN entries (PageRank, combiners over IN); DIR_OUT: the transpose of the
         capped OUT entries (ShortestDistance).  Call before the first add_rows."""
         check(load().jg_builder_set_query_limit(self._h, int(limit), int(in_entries)))
+
+    def set_weight_key(self, weight_key, key_ids=(), key_types=()):
+        """jg_builder_set_weight_key: the edges' Integer weight decoded on the GPU from their values.
+        weight_key / key_ids are inline ids (the key id without its 4 padding bits); key_types JG_PROP_*."""
+        ids = np.ascontiguousarray(key_ids, np.int64)
+        types = np.ascontiguousarray(key_types, np.int8)
+        if len(ids) != len(types):
+            raise ValueError("key_ids and key_types differ in length")
+        check(load().jg_builder_set_weight_key(self._h, int(weight_key), _ptr(ids), _ptr(types), len(ids)))
 
     def add_rows(self, row_keys, row_entry_off, data, entry_off, value_pos, entry_weight=None):
         keys = np.ascontiguousarray(row_keys, np.uint64)

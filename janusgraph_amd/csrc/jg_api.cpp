@@ -410,6 +410,10 @@ struct jg_builder {
     bool schema_set = false;
     int64_t query_limit = 0;  // jg_builder_set_query_limit
     int32_t in_entries = JG_DIR_IN;
+    bool weight_key = false;  // jg_builder_set_weight_key
+    int64_t wkey = -1;
+    std::vector<int64_t> wkey_ids;
+    std::vector<int8_t> wkey_types;
 };
 
 using jg::Error;
@@ -862,6 +866,21 @@ int jg_builder_set_query_limit(jg_builder* b, int64_t limit, int32_t in_entries)
     JG_GUARD_END
 }
 
+int jg_builder_set_weight_key(jg_builder* b, int64_t weight_key, const int64_t* key_ids, const int8_t* key_types,
+                              int32_t nkeys) {
+    JG_GUARD_BEGIN
+    JG_ARG(b, "null builder");
+    JG_ARG(weight_key >= 0 && nkeys >= 0 && (nkeys == 0 || (key_ids && key_types)), "bad weight key arguments");
+    for (int32_t i = 0; i < nkeys; ++i)
+        JG_ARG(key_types[i] >= 0 && key_types[i] <= JG_PROP_STRING, "property type outside JG_PROP_*");
+    if (b->finished || b->mode != 0) jg::fail(JG_ERR_STATE, "jg_builder_set_weight_key must precede every chunk");
+    b->weight_key = true;
+    b->wkey = weight_key;
+    b->wkey_ids.assign(key_ids, key_ids + nkeys);
+    b->wkey_types.assign(key_types, key_types + nkeys);
+    JG_GUARD_END
+}
+
 int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, const int64_t* row_entry_off,
                         const uint8_t* bytes, int64_t nbytes, const int64_t* entry_off, const int32_t* value_pos,
                         const int32_t* entry_weight, int64_t nentries) {
@@ -874,6 +893,8 @@ int jg_builder_add_rows(jg_builder* b, const uint64_t* row_keys, int64_t nrows, 
         b->dec = std::make_unique<jg::EdgestoreDecoder>(b->type_ids.data(), b->type_mult.data(),
                                                         (int32_t)b->type_ids.size(), b->pbits, builder_device(b));
         b->dec->set_query_limit(b->query_limit);
+        if (b->weight_key)
+            b->dec->set_weight_key(b->wkey, b->wkey_ids.data(), b->wkey_types.data(), (int32_t)b->wkey_ids.size());
     }
     jg::EdgestoreRows r{row_keys, nrows,      row_entry_off, bytes,
                         nbytes,   entry_off,  value_pos,     nentries,

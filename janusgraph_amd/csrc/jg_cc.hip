@@ -256,14 +256,18 @@ __global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict_
 // Vertices outside the sampled giant component link their remaining neighbours (an edge between the
 // giant component and another vertex is linked from the other side).  Rows are degree-sorted: rows
 // below `heavy` (degree >= 64) take a wave each, the others a thread.
+// *linked += the entries linked (one atomic per wave; the work counter of jg_stats.algorithmic_bytes)
 __global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, const int64_t* __restrict__ rp,
                                                                const int32_t* __restrict__ col, int64_t rows,
-                                                               int64_t heavy, int k, int32_t giant) {
+                                                               int64_t heavy, int k, int32_t giant,
+                                                               unsigned long long* __restrict__ linked) {
     const int lane = threadIdx.x & (kWave - 1);
+    unsigned long long count = 0;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
     for (int64_t v = wave; v < heavy; v += nwaves) {  // wave-uniform
         if (uf_find(parent, (int32_t)v) == giant) continue;
+        if (lane == 0) count += (unsigned long long)(rp[v + 1] - rp[v] - k);
         for (int64_t e = rp[v] + k + lane; e < rp[v + 1]; e += kWave) {
             const int32_t u = col[e];
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
@@ -272,11 +276,14 @@ __global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, c
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
     for (int64_t v = heavy + tid; v < rows; v += nt) {
         if (rp[v + 1] - rp[v] <= k || uf_find(parent, (int32_t)v) == giant) continue;
+        count += (unsigned long long)(rp[v + 1] - rp[v] - k);
         for (int64_t e = rp[v] + k; e < rp[v + 1]; ++e) {
             const int32_t u = col[e];
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
+    count = wave_reduce_add(count);
+    if (lane == 0 && count) atomicAdd(linked, count);
 }
 
 __global__ void uf_compress_kernel(int32_t* parent, int64_t rows) {
@@ -324,7 +331,11 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // reaches the superstep cap.  On success *labels points at the labels (the parent array, rewritten).
 // The union-find runs over the rows that have an edge (those before Csr::empty_from): an edgeless row
 // is its own component, with its own rank as label, and is never linked.
-bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels) {
+// *work_bytes: the bytes the passes need (the §8d-style model of this algorithm): per row
+// with an edge 98 B (init 8, first links 20, two compressions 16, rest-link scan 12, minimum rank 8, BFS
+// start 29, BFS depth and seen 5), 12 B per entry linked in the second round (col, both finds) and 4 B
+// per adjacency entry of the rows the BFS reached.
+bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, double* work_bytes) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
@@ -341,6 +352,8 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels)
     int32_t* minr = sh.cc_msg[1].get();
     if ((int64_t)sh.cc_depth.size() < rows) sh.cc_depth.alloc(rows);
     DevBuf<int32_t> sample(1025);  // 1024 sampled roots, then the heavy-row count
+    DevBuf<unsigned long long> linked(1);
+    JG_HIP(hipMemsetAsync(linked.get(), 0, sizeof(unsigned long long), s));
     const int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
     uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
     JG_LAUNCH_CHECK();
@@ -370,17 +383,20 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels)
         i = j;
     }
     uf_link_rest_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
-                                                        giant);
+                                                        giant, linked.get());
     JG_LAUNCH_CHECK();
     uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
     JG_LAUNCH_CHECK();
     uf_minrank_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
     // the BFS start picks the sources and rewrites parent into the labels
-    const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get());
+    double reached = 0;
+    const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get(), &reached);
     const int it = c.nnz > 0 ? d + 1 : 0;
     if (it > kCcMaxIterations - 1) return false;
-    JG_HIP(hipStreamSynchronize(s));
+    unsigned long long rest = 0;
+    copy_d2h(&rest, linked.get(), sizeof rest, s);
+    *work_bytes = 98.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
     *iterations = it;
     *labels = parent;
     return true;
@@ -504,8 +520,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     // One shard: the same labels and superstep count from a union-find and one BFS (cc_union_find).
     bool solved = false;
     const int32_t* uf_labels = nullptr;  // the union-find's labels of shard 0 (when solved)
+    double uf_bytes = 0;
     if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) {
-        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels);
+        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_bytes);
         if (!solved && sh0.rows) {  // the cap binds: the propagation runs, from fresh message vectors
             for (auto& m : sh0.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh0.stream));
             cc_init_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
@@ -593,7 +610,8 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     double nnz = 0;
     for (auto& sp : g.shards) nnz += (double)sp->both.nnz;
     ctx.last.edges_traversed = nnz * iteration;
-    ctx.last.algorithmic_bytes = (8.0 * nnz + 16.0 * (double)n) * iteration;  // 16m + 16n per superstep
+    // the propagation: 16m + 16n per superstep; the union-find: its own pass model
+    ctx.last.algorithmic_bytes = solved ? uf_bytes : (8.0 * nnz + 16.0 * (double)n) * iteration;
     if (iterations_out) *iterations_out = iteration;
     if (comp_out && dev_maps && n > 0) {  // comp[dense of row l] = id of rank label[l], on the device
         Shard& sh = *g.shards[0];

@@ -76,6 +76,7 @@ struct EntryView {
 
 struct Decoded {
     int64_t type_id, other, rel;
+    int64_t vstart;  // user edges: first byte after the ids (signature values, then inline properties)
     int8_t dir;    // 0 OUT edge, 1 IN edge, 2 property, 3 system relation, -1 malformed
     bool visible;  // a user relation (header prefix >> 1 == 1), not system, not invisible
 };
@@ -101,6 +102,7 @@ __device__ __forceinline__ Decoded decode_entry(const EntryView& a, const uint8_
     Decoded d;
     d.type_id = ((value >> 1) << 6) | suffix;
     d.other = d.rel = -1;
+    d.vstart = vpos;
     d.dir = (int8_t)(is_edge ? 3 : 2);
     d.visible = (prefix >> 1) == 1;
     if (is_edge && !system) {
@@ -120,10 +122,12 @@ __device__ __forceinline__ Decoded decode_entry(const EntryView& a, const uint8_
         } else if (unique) {
             d.other = read_unsigned(b, p, len, bad);
             d.rel = read_unsigned(b, p, len, bad);
+            d.vstart = p;
         } else {
             d.other = read_unsigned_backward(b, p, bad);
             p = vpos;
             d.rel = read_unsigned(b, p, len, bad);
+            d.vstart = p;
         }
     }
     if (bad) {
@@ -131,6 +135,113 @@ __device__ __forceinline__ Decoded decode_entry(const EntryView& a, const uint8_
         d.other = d.rel = -1;
     }
     return d;
+}
+
+// ---- the Integer weight property of an edge, read from its value (ShortestDistanceVertexProgram.java:69)
+// EdgeSerializer.writeRelation (:294-302) stores an edge's properties after its ids: the label's
+// signature values (none: the caller checks), then each other property as its inline key id
+// (IDHandler.writeInlineRelationType: VariableLong.writePositive of the id without its 4 padding bits)
+// and its value (StandardSerializer.writeObject: a null flag byte 0 / -1 unless the serializer takes
+// nulls itself, then the serializer's bytes), in ascending key-id order.  Key types (JG_PROP_*):
+// the fixed widths of ByteSerializer 1, ShortSerializer 2, LongSerializer 8, CharacterSerializer 2,
+// BooleanSerializer 1, DateSerializer 8, FloatSerializer 4, DoubleSerializer 8, UUIDSerializer 16;
+// IntegerSerializer a signed VariableLong; StringSerializer (no flag byte) its own length header.
+// Error bits of the snapshot (any set bit fails the build before the CSR is cut)
+enum : int32_t { kErrBadKey = 1, kErrPartitioned = 2, kErrMalformed = 4, kErrWeightType = 8, kErrWeightValue = 16 };
+
+// VariableLong.read: the zig-zag-free sign encoding |v| << 1 | sign (VariableLong.java:133-152)
+__device__ __forceinline__ int64_t read_signed(const uint8_t* __restrict__ b, int64_t& pos, int64_t len, bool& bad) {
+    const uint64_t u = (uint64_t)read_unsigned(b, pos, len, bad);
+    return (u & 1) ? -(int64_t)(u >> 1) : (int64_t)(u >> 1);
+}
+
+// StringSerializer.read (StringSerializer.java:98-151), skipping the characters
+__device__ __forceinline__ void skip_string(const uint8_t* __restrict__ b, int64_t& pos, int64_t len, bool& bad) {
+    const int64_t h = read_unsigned(b, pos, len, bad);
+    if (bad || h == 0) return;  // 0: null
+    int64_t l = h >> 3;
+    if ((h & 7) != 0) {  // compressed: l bytes
+        pos += l;
+    } else if ((l & 1) == 0) {  // ASCII: one byte per character, the last one marked
+        l >>= 1;
+        if (l == 2) {
+            for (;;) {
+                if (pos >= len) { bad = true; return; }
+                if (b[pos++] & 0x80) break;
+            }
+        } else if (l != 1) {
+            bad = true;
+        }
+    } else {  // full UTF: l >> 1 characters of 1 to 3 bytes
+        for (int64_t i = 0, nc = l >> 1; i < nc; ++i) {
+            if (pos >= len) { bad = true; return; }
+            const int hi = b[pos] >> 4;
+            pos += hi < 8 ? 1 : hi == 14 ? 3 : 2;
+        }
+    }
+    if (pos > len) bad = true;
+}
+
+// The weight of one entry: JG_WEIGHT_ABSENT when the edge has no (non-null Integer) weight; *err gets
+// kErrWeightType when a property of an unknown type precedes the weight key (its length is unknown).
+__device__ __forceinline__ int32_t decode_weight(const uint8_t* __restrict__ b, int64_t pos, int64_t len,
+                                                 const WeightSchema& w, int32_t* err) {
+    bool bad = false;
+    while (pos < len) {
+        const int64_t kid = read_unsigned(b, pos, len, bad);
+        if (bad || kid > w.key) break;  // ascending ids: the weight key is not on this edge
+        int lo = 0, hi = w.n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (w.ids[mid] < kid) lo = mid + 1; else hi = mid;
+        }
+        const int type = lo < w.n && w.ids[lo] == kid ? w.types[lo] : 0;
+        if (type == JG_PROP_STRING) {
+            skip_string(b, pos, len, bad);
+            continue;
+        }
+        if (type <= 0 || type > JG_PROP_UUID) {
+            atomicOr(err, kErrWeightType);
+            return JG_WEIGHT_ABSENT;
+        }
+        if (pos >= len) { bad = true; break; }
+        const uint8_t flag = b[pos++];
+        if (flag == 0xFF) {  // a null value
+            if (kid == w.key) return JG_WEIGHT_ABSENT;
+            continue;
+        }
+        if (flag != 0) { bad = true; break; }
+        if (type == JG_PROP_INT) {
+            const int64_t v = read_signed(b, pos, len, bad);
+            if (kid == w.key) {
+                if (bad || v < INT32_MIN || v > INT32_MAX) break;
+                if (v == INT32_MIN) {  // the absent marker itself: refuse rather than drop the weight
+                    atomicOr(err, kErrWeightValue);
+                    return JG_WEIGHT_ABSENT;
+                }
+                return (int32_t)v;
+            }
+            continue;
+        }
+        if (kid == w.key) return JG_WEIGHT_ABSENT;  // not an Integer: Fulgora's <Integer> cast throws
+        constexpr int8_t kWidth[JG_PROP_UUID + 1] = {0, 1, 2, 0, 8, 2, 1, 8, 4, 8, 16};  // by JG_PROP_*
+        pos += kWidth[type];
+    }
+    if (bad || pos > len) atomicOr(err, kErrMalformed);
+    return JG_WEIGHT_ABSENT;
+}
+
+// One thread per entry: the weight of every OUT user edge (the kept entries' weights are compacted
+// with the edges, as host-given weights are).
+__global__ __launch_bounds__(kBlock) void edgestore_weight_kernel(EntryView a, int64_t nentries, WeightSchema w,
+                                                                  int32_t* __restrict__ weight,
+                                                                  int32_t* __restrict__ err) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nentries; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t* b = a.bytes + a.off[e];
+        const int64_t len = a.off[e + 1] - a.off[e];
+        const Decoded d = decode_entry(a, b, len, a.vpos[e]);
+        weight[e] = d.dir == 0 && d.visible ? decode_weight(b, d.vstart, len, w, err) : JG_WEIGHT_ABSENT;
+    }
 }
 
 struct DecodeOut {
@@ -198,8 +309,6 @@ __device__ __forceinline__ int64_t key_to_vertex_id(uint64_t key, int pbits) {
 
 constexpr int64_t kVertexExistsId = (1 << 6) | 37;  // BaseKey.VertexExists: SystemPropertyKey count 1
 
-// Error bits of the snapshot (any set bit fails the build before the CSR is cut)
-enum : int32_t { kErrBadKey = 1, kErrPartitioned = 2, kErrMalformed = 4 };
 
 // IDManager.getCanonicalVertexId (idmanagement/IDManager.java:525-547): a partitioned (vertex-cut)
 // vertex's representatives share its count; the canonical one sits in the partition hashed from it.
@@ -611,25 +720,29 @@ void grow_append(DevBuf<T>& acc, int64_t& len, const T* src, int64_t k, hipStrea
 
 // Pinning host memory costs ~10 ms per 50 MB, more than staging a chunk.  Released staging buffers
 // stay pinned in a small process-wide pool, so the next snapshot (the next computer run in the same
-// JVM, the next build) reuses them.  The pool is never torn down: the HIP runtime may be gone at exit.
+// JVM, the next build) reuses them.  The pool keeps only buffers of a regular chunk's size (a hub-row
+// chunk's staging is freed) and at most kPoolTotalBytes together: a JVM that ran one GPU computer keeps
+// ~2 chunk buffers page-locked, not gigabytes.  It is never torn down: the HIP runtime may be gone at exit.
 namespace {
 struct PinnedPool {
     std::mutex mu;
     std::vector<std::pair<void*, size_t>> free;
+    size_t bytes = 0;
 };
 PinnedPool& pinned_pool() {
     static PinnedPool* pool = new PinnedPool();
     return *pool;
 }
-constexpr size_t kPoolKeep = 4;                     // buffers kept
-constexpr size_t kPoolMaxBytes = (size_t)1 << 30;   // larger ones are freed
+constexpr size_t kPoolMaxBytes = (size_t)160 << 20;    // one regular chunk's staging (64 MB bytes + metadata, +25%)
+constexpr size_t kPoolTotalBytes = (size_t)320 << 20;  // the two chunks the decoder keeps in flight
 void pinned_release(void* p, size_t cap) {
     if (!p) return;
     PinnedPool& pool = pinned_pool();
     {
         std::lock_guard<std::mutex> lk(pool.mu);
-        if (cap <= kPoolMaxBytes && pool.free.size() < kPoolKeep) {
+        if (cap <= kPoolMaxBytes && pool.bytes + cap <= kPoolTotalBytes) {
             pool.free.emplace_back(p, cap);
+            pool.bytes += cap;
             return;
         }
     }
@@ -654,6 +767,7 @@ void PinnedBuf::reserve(size_t n) {
         if (best < pool.free.size()) {
             p = pool.free[best].first;
             cap = pool.free[best].second;
+            pool.bytes -= cap;
             pool.free.erase(pool.free.begin() + (std::ptrdiff_t)best);
             return;
         }
@@ -680,6 +794,32 @@ EdgestoreDecoder::EdgestoreDecoder(const int64_t* type_ids, const int8_t* type_m
         JG_HIP(hipEventCreate(&chunks_[i]->tc));
     }
     types_ = std::make_unique<TypeTable>(type_ids, type_mult, ntypes, streams_[0]);
+}
+
+void EdgestoreDecoder::set_weight_key(int64_t key, const int64_t* ids, const int8_t* types, int32_t n) {
+    if (chunks_added_) fail(JG_ERR_STATE, "the weight key must be set before the first chunk");
+    if (key < 0 || n < 0 || (n && (!ids || !types))) fail(JG_ERR_ARG, "bad weight key arguments");
+    std::vector<std::pair<int64_t, int8_t>> t((size_t)n);
+    for (int32_t i = 0; i < n; ++i) t[i] = {ids[i], types[i]};
+    std::sort(t.begin(), t.end());
+    std::vector<int64_t> hid((size_t)std::max(n, 1));
+    std::vector<int8_t> hty((size_t)std::max(n, 1));
+    wschema_ = WeightSchema{};
+    wschema_.key = key;
+    for (int32_t i = 0; i < n; ++i) {
+        if (i && t[i].first == t[i - 1].first) fail(JG_ERR_ARG, "duplicate property key id");
+        hid[i] = t[i].first;
+        hty[i] = t[i].second;
+        if (t[i].first == key) wschema_.key_type = t[i].second;
+    }
+    if (wschema_.key_type != JG_PROP_INT) wschema_.key = -1;  // no Integer weight on any edge: all absent
+    wschema_.n = n;
+    DeviceGuard dg(device_);
+    wkeys_.alloc(std::max(n, 1));
+    wtypes_.alloc(std::max(n, 1));
+    copy_h2d(wkeys_.get(), hid.data(), hid.size() * sizeof(int64_t), streams_[0]);
+    copy_h2d(wtypes_.get(), hty.data(), hty.size() * sizeof(int8_t), streams_[0]);
+    weight_key_set_ = true;
 }
 
 EdgestoreDecoder::~EdgestoreDecoder() {
@@ -710,7 +850,9 @@ bool decode_trace() {
 void EdgestoreDecoder::add(const EdgestoreRows& r) {
     const auto h0 = HostClock::now();
     check_rows(r);
-    const int wmode = r.weight ? 1 : 0;
+    const bool dev_w = weight_key_set_;  // weights decoded here from the rows (set_weight_key; key -1: all absent)
+    if (dev_w && r.weight) fail(JG_ERR_ARG, "entry weights given while the weight key decodes them on the GPU");
+    const int wmode = (r.weight || dev_w) ? 1 : 0;
     if (weighted >= 0 && weighted != wmode) fail(JG_ERR_ARG, "entry weights must be given for every chunk or none");
     weighted = wmode;
     DeviceGuard dg(device_);
@@ -776,7 +918,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     const size_t meta = narrow ? narrow_meta : wide_meta;
     const size_t o_roff = meta, o_keys = o_roff + (size_t)(R + 1) * 8, o_w = o_keys + (size_t)R * 8,
                  o_bytes = o_w + (r.weight ? (size_t)E * 4 : 0);
-    c.weighted = r.weight != nullptr;
+    c.weighted = r.weight != nullptr || dev_w;
     if (!narrow) c.staging.reserve(meta + tail);  // rare: a chunk holding an entry of 256 bytes or more
     char* st = (char*)c.staging.p;
     if (!narrow) {
@@ -807,7 +949,7 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
     fit(c.d_keys, R);
     fit(c.d_vpos, E);
     fit(c.err, 1);
-    if (r.weight) fit(c.d_w, E);
+    if (c.weighted) fit(c.d_w, E);
     if (narrow) fit(c.d_meta8, 2 * E);
     const bool capped = limit_ > 0;
     if (capped) {
@@ -843,6 +985,13 @@ void EdgestoreDecoder::add(const EdgestoreRows& r) {
         }
     }
     const EntryView a{c.d_bytes.get(), c.d_off.get(), c.d_vpos.get(), types_->ids.get(), types_->mult.get(), types_->n};
+    if (dev_w && E) {
+        WeightSchema w = wschema_;
+        w.ids = wkeys_.get();
+        w.types = wtypes_.get();
+        edgestore_weight_kernel<<<grid_for(E), kBlock, 0, s>>>(a, E, w, c.d_w.get(), c.err.get());
+        JG_LAUNCH_CHECK();
+    }
     if (R) {
         edgestore_rows_kernel<<<grid_for(R), kBlock, 0, s>>>(a, c.d_keys.get(), c.d_roff.get(), R, pbits_, c.keep.get(),
                                                             c.keep_v.get(), c.row_vid.get(), c.err.get());
@@ -900,6 +1049,10 @@ void EdgestoreDecoder::complete(int slot) {
     if (herr & kErrBadKey) fail(JG_ERR_ARG, "row key with an unrecognized vertex id type");
     if (herr & kErrPartitioned) fail(JG_ERR_ARG, "partitioned vertex row with no partition bits");
     if (herr & kErrMalformed) fail(JG_ERR_ARG, "malformed edgestore entry on a vertex row");
+    if (herr & kErrWeightType)
+        fail(JG_ERR_UNSUPPORTED, "an edge carries a property of unknown type before the weight key");
+    if (herr & kErrWeightValue)
+        fail(JG_ERR_UNSUPPORTED, "an edge weight equals Integer.MIN_VALUE (the absent-weight marker)");
     const int64_t cap = std::max<int64_t>(std::max(c.R, c.E), 1);
     if ((int64_t)idx_.size() < cap) idx_.alloc(cap);
     if ((int64_t)tmp_.size() < cap) tmp_.alloc(cap);

@@ -368,6 +368,14 @@ struct PinnedBuf {
 };
 struct TypeTable;
 struct EdgestoreChunk;
+// The property keys an edge value may hold before the weight key (jg_builder_set_weight_key)
+struct WeightSchema {
+    int64_t key = -1;              // inline id of the weight key (-1: none)
+    int8_t key_type = 0;           // its JG_PROP_* type (weights are read only for JG_PROP_INT)
+    const int64_t* ids = nullptr;  // sorted inline ids of the property keys (device)
+    const int8_t* types = nullptr;
+    int32_t n = 0;
+};
 // The snapshot decoder on `device`: add() takes one chunk of rows (a row never spans chunks), stages it
 // in pinned memory and enqueues its copy and decode on one of two streams, then returns; the chunk
 // before it completes meanwhile (error check, compaction).  After finish(): vid[0, n) = ids of the
@@ -383,6 +391,8 @@ struct EdgestoreDecoder {
     // Slice cap (set_query_limit before the first add): osrc[m] = src, or -1 where the edge's OUT entry
     // is beyond its row's limit; (isrc, idst)[mi] = the edges whose IN entry is within its row's limit.
     void set_query_limit(int64_t limit) { limit_ = limit; }
+    // jg_builder_set_weight_key: decode every OUT edge's Integer weight from its value on the GPU
+    void set_weight_key(int64_t key, const int64_t* ids, const int8_t* types, int32_t n);
     int64_t query_limit() const { return limit_; }
     DevBuf<int64_t> osrc, isrc, idst;
     int64_t mo = 0, mi = 0, mi2 = 0, truncated_rows = 0;
@@ -402,6 +412,10 @@ struct EdgestoreDecoder {
     std::unique_ptr<TypeTable> types_;
     DevBuf<int64_t> idx_, tmp_, cpos_, cscan_;
     DevBuf<int32_t> tmpw_;
+    WeightSchema wschema_;         // key < 0: no device weight decode
+    bool weight_key_set_ = false;  // set_weight_key was called (even if no Integer key exists)
+    DevBuf<int64_t> wkeys_;
+    DevBuf<int8_t> wtypes_;
 };
 // Feeds one whole snapshot to the decoder in chunks of whole rows (<= 4 M entries / 64 MB each).
 void add_in_chunks(EdgestoreDecoder& dec, const EdgestoreRows& r);
@@ -430,8 +444,9 @@ struct CcRoots {
 };
 // One shard, BOTH adjacency: the largest hop distance of a vertex from the minimum-rank vertex of its
 // component, by a direction-optimising BFS started at every such vertex that has an edge; -1 if no
-// vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth);
+// vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).  *edges_out =
+// adjacency entries of the rows the traversal reached.
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out);
 // Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
 void bfs_buffers(Shard& sh);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,

@@ -43,8 +43,13 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
                      int64_t* nbr_out) {
     if (direction < JG_DIR_OUT || direction > JG_DIR_BOTH) fail(JG_ERR_ARG, "bad direction");
     if (nrows < 0 || (nrows > 0 && !rows) || !off_out) fail(JG_ERR_ARG, "bad arguments");
-    if ((int)g.shards.size() != g.P)
-        fail(JG_ERR_UNSUPPORTED, "jg_graph_neighbors needs every shard in this process (not rank mode)");
+    // rank mode: only this process's rows are here; their entry counts can be read (the others count 0),
+    // their neighbours cannot (a compact id maps back through a peer's send list)
+    const bool all_local = (int)g.shards.size() == g.P;
+    if (!all_local && nbr_out)
+        fail(JG_ERR_UNSUPPORTED, "jg_graph_neighbors in rank mode: entry counts only (nbr_out must be NULL)");
+    std::vector<const Shard*> local((size_t)g.P, nullptr);
+    for (const auto& sp : g.shards) local[(size_t)sp->index] = sp.get();
     const uint32_t adj = direction == JG_DIR_BOTH ? JG_ADJ_BOTH : direction == JG_DIR_OUT ? JG_ADJ_OUT : JG_ADJ_IN;
     if (!(g.flags & adj)) fail(JG_ERR_UNSUPPORTED, "the graph was built without this adjacency");
     // rows grouped by owning shard, keeping their request position
@@ -54,6 +59,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
         if (d < 0 || d >= g.n) fail(JG_ERR_ARG, "row outside [0, num_vertices)");
         const int64_t pg = g.padded_of_dense[(size_t)d];
         const int q = (int)(pg / g.S);
+        if (!local[q]) continue;  // another rank's row: no entries here
         loc[q].push_back(pg - (int64_t)q * g.S);
         pos[q].push_back(k);
     }
@@ -63,7 +69,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
     for (int q = 0; q < g.P; ++q) {
         const int64_t k = (int64_t)loc[q].size();
         if (!k) continue;
-        const Shard& sh = *g.shards[q];
+        const Shard& sh = *local[q];
         const Csr& c = pick(sh, direction);
         DeviceGuard dg(sh.device);
         DevBuf<int64_t> drows(k), dlen(k);

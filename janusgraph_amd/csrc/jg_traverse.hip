@@ -450,10 +450,13 @@ __global__ __launch_bounds__(kBlock) void msbfs_todo_kernel(const unsigned long 
     }
 }
 
-// bit t of tlive (MergeArgs::live): merge task t touches a band row that can still gain a bit
+// bit t of tlive (MergeArgs::live): merge task t touches a band row that can still gain a bit;
+// *nlive += the live tasks (one atomic per wave; the work counter of jg_stats.algorithmic_bytes)
 __global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* __restrict__ task_rows, int64_t tasks,
                                                                  const unsigned long long* __restrict__ todo,
-                                                                 unsigned long long* __restrict__ tlive) {
+                                                                 unsigned long long* __restrict__ tlive,
+                                                                 unsigned long long* __restrict__ nlive) {
+    unsigned long long count = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tasks; x0 += stride) {  // block-uniform trips
         const int64_t t = x0 + threadIdx.x;
@@ -469,7 +472,19 @@ __global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* 
         }
         const unsigned long long word = __ballot(b);
         if (lane_id() == 0 && t < tasks) tlive[t >> 6] = word;
+        count += (unsigned long long)__popcll(word);
     }
+    if (lane_id() == 0 && count) atomicAdd(nlive, count);
+}
+
+// pairs += the set bits of visited[0, rows) (sources x reached rows: the depth entries written)
+__global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long long* __restrict__ visited, int64_t rows,
+                                                             unsigned long long* __restrict__ pairs) {
+    unsigned long long c = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
+        c += (unsigned long long)__popcll(visited[v]);
+    c = wave_reduce_add(c);
+    if (lane_id() == 0 && c) atomicAdd(pairs, c);
 }
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
@@ -1184,12 +1199,13 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
 
 }  // namespace
 
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth) {
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out) {
+    *edges_out = 0;
     if (sh.rows == 0) return -1;
     const BfsCsrs c{&sh.both, &sh.both};
     // the traversal stops at the first level with an empty frontier, which it counts: the deepest
     // depth is the one before (no depth-max pass over the rows)
-    return dobfs_single(ctx, sh, c, -1, -1, depth, nullptr, &r) - 1;
+    return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r) - 1;
 }
 
 
@@ -1254,6 +1270,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
         float total_ms = 0;
         int max_levels = 0;
+        double work_bytes = 0, work_entries = 0;
         for (int b0 = 0; b0 < nsrc; b0 += 64) {
             const int ns = std::min(64, nsrc - b0);
             const unsigned long long full = ns == 64 ? ~0ull : ((1ull << ns) - 1ull);
@@ -1263,6 +1280,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
+                DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs
+                int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
             };
             std::vector<St> st(g.shards.size());
             std::vector<int64_t> src_rows;
@@ -1284,6 +1303,15 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
                 t.live.alloc(2);
+                t.work.alloc(2);
+                JG_HIP(hipMemsetAsync(t.work.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+                t.light_nnz = c.pull->nnz;
+                if (t.split.size() && plan.split_rows > 0) {
+                    int64_t split_nnz = 0;
+                    copy_d2h(&split_nnz, c.pull->row_ptr.get() + plan.split_rows, sizeof split_nnz, sh.stream);
+                    t.light_nnz -= split_nnz;
+                    for (const auto& bd : plan.bands) t.all_tasks += bd->tasks;
+                }
                 const unsigned long long lw[2] = {full, full};
                 copy_h2d(t.live.get(), lw, sizeof lw, sh.stream);
                 if (t.split.size() && tune().msbfs_skip) {
@@ -1370,6 +1398,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // bits (both from the previous level's end)
             bool queued = td_ok, live_ready = false;
             int cur = 0, level = 0;
+            // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
+            // counted on the device, or every task when the skip is off) and top-down frontier entries
+            int pull_levels = 0;
+            double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
                 const bool td_level =
                     td_ok && (double)td.mf < (double)c0.push->nnz / (double)tune().bfs_alpha;
@@ -1397,6 +1429,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     unsigned long long th = 0;
                     copy_d2h(&th, td.ctr.get() + 1, sizeof th, sh.stream);
                     const int64_t nt = (int64_t)(th >> kPackShift);
+                    td_entries += (double)td.mf;
+                    td_touched += (double)nt;
+                    td_queued += (double)td.nq;
                     if (nt > 0) {
                         MsBfsOp op;
                         op.F = t.F[cur].get();
@@ -1457,7 +1492,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                         JG_LAUNCH_CHECK();
                         msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
-                            bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get());
+                            bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
                         JG_LAUNCH_CHECK();
                         tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
                     }
@@ -1475,6 +1510,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                 }
                 if (!td_level) {
+                    ++pull_levels;
                     std::vector<void*> bufs;
                     for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
                     exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
@@ -1499,6 +1535,26 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventElapsedTime(&ms, t0, t1));
             total_ms += ms;
             max_levels = std::max(max_levels, level);
+            // the work of this batch, counted after its timed region: per pull level 12 B per entry of a
+            // live merge task (col + gathered frontier word; a task streams its 512 slots) and of the light
+            // rows, 24 B per row (visited, the new word, the next level's live scan); per top-down level
+            // 12 B per frontier entry, 16 B per touched word and 8 B per queued vertex; 4 B per reached
+            // (source, row) pair: its depth entry
+            for (size_t i = 0; i < g.shards.size(); ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh.device);
+                St& t = st[i];
+                msbfs_pairs_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.vis.get(), sh.rows, t.work.get() + 1);
+                JG_LAUNCH_CHECK();
+                unsigned long long w[2] = {0, 0};
+                copy_d2h(w, t.work.get(), sizeof w, sh.stream);
+                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels : (double)w[0];
+                const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels;
+                work_entries += entries;
+                work_bytes += 12.0 * entries + 24.0 * (double)sh.rows * pull_levels + 4.0 * (double)w[1];
+            }
+            work_entries += td_entries;
+            work_bytes += 12.0 * td_entries + 16.0 * td_touched + 8.0 * td_queued;
             if (depth_rows)
                 for (size_t i = 0; i < g.shards.size(); ++i)
                     for (int s = 0; s < ns; ++s)
@@ -1509,6 +1565,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.compute_ms = total_ms;
         ctx.last.levels = max_levels;
         ctx.last.supersteps = max_levels;
+        ctx.last.algorithmic_bytes = work_bytes;
+        ctx.last.edges_traversed = work_entries;  // adjacency entries the levels examined
         prof_collect(ctx, g);
     }
     JG_HIP(hipEventDestroy(t0));

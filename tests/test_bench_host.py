@@ -1,4 +1,6 @@
-"""bench.py host helpers (CPU): the CPU-baseline leg and the PMC traffic lookup."""
+"""bench.py host helpers (CPU): the CPU-baseline leg, the PMC traffic lookup and the source pick."""
+import numpy as np
+
 import bench
 
 
@@ -9,7 +11,23 @@ def test_cpu_baseline_small():
 
 
 def test_pmc_traffic_lookup():
-    t, src = bench.pmc_traffic("PrOp", "pagerank_fp64_rmat24_ef16")
-    if t is not None:
-        assert t > 1e9 and src.startswith("profiles/")
-    assert bench.pmc_traffic("NoSuchKernel")[0] is None
+    """Every committed summary is found by its workload (round-2 ones through their bench.json)."""
+    t, src = bench.pmc_traffic("pagerank_fp64_rmat24_ef16")
+    assert t is not None and t > 1e9 and src.startswith("profiles/")
+    t26, src26 = bench.pmc_traffic("pagerank_fp64_rmat26_ef16")
+    assert t26 is not None and t26 > t and src26 != src
+    assert bench.pmc_traffic("no_such_workload") == (None, None)
+
+
+def test_sources_have_edges():
+    deg = np.array([0, 3, 0, 1, 5, 0, 2], np.int64)
+    s = bench.pick_sources(deg, 3, 1)
+    assert len(set(s.tolist())) == 3 and (deg[s] > 0).all()
+    assert len(bench.pick_sources(deg, 10, 1)) == 4  # all candidates when fewer than asked
+
+
+def test_required_bytes_below_model():
+    m, n, live = 16 << 24, 1 << 24, 9_000_000
+    r = bench.required_roofline(m, live, 0.8)
+    assert r["bytes_per_launch"] == 12.0 * m + 24.0 * live < 12.0 * m + 32.0 * n
+    assert abs(r["frac"] - r["bytes_per_launch"] / 0.8e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-4

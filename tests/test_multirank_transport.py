@@ -4,7 +4,8 @@ RCCL refuses two ranks on one device, so the driver's 8-GPU run is the only plac
 execute.  Here two processes share device 0 and the library's exchanges go through a host transport
 (jg_ctx_create_rank_transport, gloo underneath): the same rank-mode build (each process builds only
 its shard), halo-plan count check, pack kernels, segment placement, reverse exchange and all-reduces
-as with RCCL, checked against the oracle.  Per-vertex outputs hold each rank's own vertices; rank 0
+as with RCCL, checked against the oracle: PageRank, CC, single-source DO-BFS, the 8-source bit-parallel
+BFS, weighted shortest distance, and jg_graph_neighbors' entry counts (bench.py's source pick).  Per-vertex outputs hold each rank's own vertices; rank 0
 combines them.
 """
 import os
@@ -60,6 +61,13 @@ def _worker(rank, world, port, halo, errfile):
         src = int(s[0])
         depth = g.bfs([vid[src]], jg.DIR_BOTH)[0]
         depth, own_d = _combine(dist, world, depth, np.iinfo(np.int32).min)
+        msrc = [int(x) for x in s[:8]]
+        ms = g.bfs(vid[msrc], jg.DIR_BOTH, max_depth=5).ravel()  # the sharded bit-parallel pull (rank mode)
+        ms, own_ms = _combine(dist, world, ms, np.iinfo(np.int32).min)
+        import torch
+        deg = torch.from_numpy(g.degrees(jg.DIR_BOTH))  # rank mode: own rows' entry counts, 0 for the others
+        dist.all_reduce(deg)
+        deg = deg.numpy()
         sd = own_sd = None
         if halo:  # sharded shortest distance runs over the halo plan only
             sd = g.shortest_distance(vid[src], 6)
@@ -74,6 +82,10 @@ def _worker(rank, world, port, halo, errfile):
             np.testing.assert_array_equal(comp, cref)
             assert it == cit, (it, cit)
             np.testing.assert_array_equal(depth, o.bfs(n, ds, dd, src, o.DIR_BOTH))
+            assert (own_ms == 1).all()
+            for k, sv in enumerate(msrc):
+                np.testing.assert_array_equal(ms[k * n:(k + 1) * n], o.bfs(n, ds, dd, sv, o.DIR_BOTH, 5))
+            np.testing.assert_array_equal(deg, np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n))
             if sd is not None:
                 assert (own_sd == 1).all()
                 np.testing.assert_array_equal(sd, o.shortest_distance(n, ds, dd, src, 6, w))
