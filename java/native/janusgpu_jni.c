@@ -109,6 +109,13 @@ JNIEXPORT jint JNICALL FN(builderAddRows)(JNIEnv* env, jclass c, jlong b, jobjec
                                (const int32_t*)buf(env, entry_weight), nentries);
 }
 
+JNIEXPORT jint JNICALL FN(builderSetWeightKey)(JNIEnv* env, jclass c, jlong b, jlong weight_key, jobject key_ids,
+                                               jobject key_types, jint nkeys) {
+    (void)c;
+    return jg_builder_set_weight_key((jg_builder*)(intptr_t)b, weight_key, (const int64_t*)buf(env, key_ids),
+                                     (const int8_t*)buf(env, key_types), nkeys);
+}
+
 JNIEXPORT jint JNICALL FN(builderSetQueryLimit)(JNIEnv* env, jclass c, jlong b, jlong limit, jint in_entries) {
     (void)env; (void)c;
     return jg_builder_set_query_limit((jg_builder*)(intptr_t)b, limit, in_entries);

@@ -5,6 +5,7 @@ package org.janusgraph.graphdb.olap.computer;
 import org.apache.tinkerpop.gremlin.structure.Direction;
 import org.janusgraph.core.EdgeLabel;
 import org.janusgraph.core.JanusGraphException;
+import org.janusgraph.core.PropertyKey;
 import org.janusgraph.core.schema.JanusGraphManagement;
 import org.janusgraph.diskstorage.Entry;
 import org.janusgraph.diskstorage.EntryList;
@@ -16,6 +17,8 @@ import org.janusgraph.diskstorage.keycolumnvalue.scan.StandardScanner;
 import org.janusgraph.diskstorage.util.BufferUtil;
 import org.janusgraph.graphdb.database.EdgeSerializer;
 import org.janusgraph.graphdb.database.StandardJanusGraph;
+import org.janusgraph.graphdb.idmanagement.IDManager;
+import org.janusgraph.graphdb.internal.InternalRelationType;
 import org.janusgraph.graphdb.olap.VertexJobConverter;
 import org.janusgraph.graphdb.relations.RelationCache;
 import org.janusgraph.graphdb.transaction.StandardJanusGraphTx;
@@ -24,8 +27,10 @@ import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
 import java.util.Collections;
+import java.util.Date;
 import java.util.List;
 import java.util.Map;
+import java.util.UUID;
 import java.util.concurrent.atomic.AtomicInteger;
 
 /**
@@ -38,9 +43,13 @@ import java.util.concurrent.atomic.AtomicInteger;
  * graphdb/olap/VertexJobConverter.java:122-151,174-177) while this thread scans the next chunk.
  *
  * ShortestDistanceVertexProgram also needs the Integer edge weight, which lives in the entry's value
- * with a type-dependent encoding: for that program every entry is additionally parsed here with the
- * graph's own EdgeSerializer and its weight sent along (JanusGpu.WEIGHT_ABSENT if the edge has none,
- * which fails the run only if a message crosses the edge, as Fulgora's edge function does).
+ * after the ids as (inline key id, value) pairs in key-id order (EdgeSerializer.writeRelation,
+ * graphdb/database/EdgeSerializer.java:294-302). Where the schema allows (no edge label with signature
+ * keys, the weight key in no sort key, every property key below the weight key of a type with a known
+ * length) the weight is decoded on the GPU too (jg_builder_set_weight_key). Otherwise every OUT edge entry
+ * of a visible row is parsed here with the graph's own EdgeSerializer and its weight sent along
+ * (WeightReader). Either way an edge without an Integer weight gets JanusGpu.WEIGHT_ABSENT, which fails the
+ * run only if a message crosses the edge, as Fulgora's edge function does.
  */
 final class GpuSnapshot implements ScanJob {
 
@@ -113,13 +122,16 @@ final class GpuSnapshot implements ScanJob {
             allocate(Math.max(rowBytes, CHUNK_BYTES), Math.max(rowEntries, CHUNK_ENTRIES), CHUNK_ROWS);
         }
         keys.putLong(key.getLong(0)); // the 8-byte big-endian row key as an unsigned value (IDManager.getKey)
+        // host weights only for rows the decoder keeps: VertexJobConverter.getKeyFilter drops invisible rows
+        // (olap/VertexJobConverter.java:169-171) before anything is parsed
+        final boolean parseWeights = entryWeight != null && weights.visible(key);
         for (Entry e : row) {
             final byte[] b = e.as(StaticBuffer.ARRAY_FACTORY); // column then value
             bytes.put(b);
             nbytes += b.length;
             entryOff.putLong(nbytes);
             valuePos.putInt(e.getValuePosition());
-            if (entryWeight != null) entryWeight.putInt(weights.weight(e));
+            if (entryWeight != null) entryWeight.putInt(parseWeights ? weights.weight(e) : JanusGpu.WEIGHT_ABSENT);
         }
         nentries += rowEntries;
         ++nrows;
@@ -143,28 +155,87 @@ final class GpuSnapshot implements ScanJob {
         return this; // one processor thread (setNumProcessingThreads(1)): rows arrive in key order
     }
 
-    /** Reads the Integer weight property of the edge an entry stores (ShortestDistanceVertexProgram.java:69). */
+    /** Reads the Integer weight property of the edge an entry stores (ShortestDistanceVertexProgram.java:69),
+     *  on the host: the fallback when the schema rules out the GPU decode (see the class comment). */
     static final class WeightReader {
         private final StandardJanusGraphTx tx;
         private final EdgeSerializer serializer;
+        private final IDManager idManager;
         private final long keyId;
 
         WeightReader(StandardJanusGraph graph, String weightProperty) {
             tx = VertexJobConverter.startTransaction(graph);
             serializer = graph.getEdgeSerializer();
+            idManager = graph.getIDManager();
             keyId = tx.containsPropertyKey(weightProperty) ? tx.getPropertyKey(weightProperty).longId() : -1L;
         }
 
+        boolean visible(StaticBuffer key) {
+            return !IDManager.VertexIDType.Invisible.is(idManager.getKeyID(key));
+        }
+
         int weight(Entry e) {
+            if (serializer.parseDirection(e) != Direction.OUT) return JanusGpu.WEIGHT_ABSENT; // header only
             final RelationCache rc = serializer.parseRelation(e, false, tx);
-            if (rc.direction != Direction.OUT || keyId < 0) return JanusGpu.WEIGHT_ABSENT;
+            if (keyId < 0 || !tx.getExistingRelationType(rc.typeId).isEdgeLabel()) return JanusGpu.WEIGHT_ABSENT;
             final Object v = rc.get(keyId);
-            return v == null ? JanusGpu.WEIGHT_ABSENT : ((Number) v).intValue();
+            if (!(v instanceof Integer)) return JanusGpu.WEIGHT_ABSENT; // absent, or not an Integer: the <Integer> cast throws when crossed
+            final int w = (Integer) v;
+            if (w == JanusGpu.WEIGHT_ABSENT)
+                throw new JanusGraphException("GPU computer: an edge weight equals Integer.MIN_VALUE, the absent-weight marker");
+            return w;
         }
 
         void close() {
             if (tx.isOpen()) tx.rollback();
         }
+    }
+
+    /** JG_PROP_* codes of include/janusgpu.h for a property key's data type; 0: length unknown to the GPU. */
+    static byte propertyType(PropertyKey key) {
+        final Class<?> t = key.dataType();
+        if (t == Byte.class) return 1;
+        if (t == Short.class) return 2;
+        if (t == Integer.class) return 3;
+        if (t == Long.class) return 4;
+        if (t == Character.class) return 5;
+        if (t == Boolean.class) return 6;
+        if (t == Date.class) return 7;
+        if (t == Float.class) return 8;
+        if (t == Double.class) return 9;
+        if (t == UUID.class) return 10;
+        if (t == String.class) return 11;
+        return 0;
+    }
+
+    /**
+     * Sends the weight key and the property-key table for the GPU weight decode and returns true, or
+     * returns false when the schema needs the host parse: an edge label with signature keys (their values
+     * precede the inline pairs without ids), the weight key in a label's sort key (stored in the column),
+     * or a key of unknown value length below the weight key.
+     */
+    private static boolean deviceWeights(long builder, JanusGraphManagement mgmt, List<EdgeLabel> labels,
+                                         String weightProperty) {
+        final PropertyKey wk = mgmt.getPropertyKey(weightProperty);
+        for (EdgeLabel l : labels) {
+            final InternalRelationType t = (InternalRelationType) l;
+            if (t.getSignature().length > 0) return false;
+            if (wk != null) for (long k : t.getSortKey()) if (k == wk.longId()) return false;
+        }
+        final List<PropertyKey> keys = new ArrayList<>();
+        for (PropertyKey k : mgmt.getRelationTypes(PropertyKey.class)) {
+            if (wk != null && k.longId() < wk.longId() && propertyType(k) == 0) return false;
+            keys.add(k);
+        }
+        final ByteBuffer ids = direct(8L * keys.size()), types = direct(keys.size());
+        for (PropertyKey k : keys) {
+            ids.putLong(IDManager.stripRelationTypePadding(k.longId()));
+            types.put(propertyType(k));
+        }
+        // no such key: inline id 0 with an empty table, every weight absent
+        final long weightKey = wk == null ? 0L : IDManager.stripRelationTypePadding(wk.longId());
+        JanusGpu.check(JanusGpu.builderSetWeightKey(builder, weightKey, ids, types, wk == null ? 0 : keys.size()));
+        return true;
     }
 
     /** Multiplicity codes of include/janusgpu.h (jg_decode_edges): 0 MULTI, 1 SIMPLE, 2 ONE2MANY,
@@ -181,7 +252,7 @@ final class GpuSnapshot implements ScanJob {
 
     /**
      * Scans the edgestore into a device graph with the adjacencies `flags`. weightProperty != null
-     * also sends every entry's edge weight (ShortestDistanceVertexProgram). queryLimit > 0 builds what
+     * also gives every edge its weight (ShortestDistanceVertexProgram): decoded on the GPU, or parsed here. queryLimit > 0 builds what
      * Fulgora's programs read under its slice cap (inEntries: JanusGpu.DIR_IN or DIR_OUT, see
      * jg_builder_set_query_limit). Returns the graph handle; its vertex order is the scan's row order
      * (read it with JanusGpu.graphVertexIds).
@@ -207,10 +278,11 @@ final class GpuSnapshot implements ScanJob {
                 }
                 final int partitionBits = Long.numberOfTrailingZeros(graph.getIDManager().getPartitionBound());
                 JanusGpu.check(JanusGpu.builderSetSchema(builder, typeIds, typeMult, labels.size(), partitionBits));
+                if (weightProperty != null && !deviceWeights(builder, mgmt, labels, weightProperty))
+                    weights = new WeightReader(graph, weightProperty);
             } finally {
                 mgmt.rollback();
             }
-            if (weightProperty != null) weights = new WeightReader(graph, weightProperty);
             final GpuSnapshot job = new GpuSnapshot(builder, weights);
             final StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
             scan.setJobId("gpu-snapshot#" + JOBS.incrementAndGet());

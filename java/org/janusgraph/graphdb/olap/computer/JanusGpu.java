@@ -58,6 +58,10 @@ final class JanusGpu {
     static native int builderAddRows(long builder, ByteBuffer rowKeys, long nrows, ByteBuffer rowEntryOff,
                                      ByteBuffer bytes, long nbytes, ByteBuffer entryOff, ByteBuffer valuePos,
                                      ByteBuffer entryWeight, long nentries);
+    /** jg_builder_set_weight_key: the edges' Integer weight decoded on the GPU. weightKey and keyIds are inline
+     *  ids (IDManager.stripRelationTypePadding), keyTypes the JG_PROP_* codes (int8). */
+    static native int builderSetWeightKey(long builder, long weightKey, ByteBuffer keyIds, ByteBuffer keyTypes,
+                                          int nkeys);
     /** jg_builder_set_query_limit: Fulgora's per-row slice cap (0: none); inEntries DIR_IN or DIR_OUT. */
     static native int builderSetQueryLimit(long builder, long limit, int inEntries);
     /** jg_builder_finish; graph handle written to out[0]. */

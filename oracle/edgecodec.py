@@ -170,3 +170,133 @@ def encode_property(type_id: int, rel: int, value: bytes = b"\x00") -> tuple[byt
     """A LIST-cardinality property entry: [header][relation backward] | value."""
     col = write_relation_type(type_id, False, OUT) + write_positive_backward(rel)
     return col + value, len(col)
+
+
+# ---- edge properties in the value (EdgeSerializer.writeRelation :294-302, parseRelation :159-171) ----
+# JG_PROP_* codes of include/janusgpu.h
+BYTE, SHORT, INT, LONG, CHAR, BOOL, DATE, FLOAT, DOUBLE, UUID, STRING = range(1, 12)
+_FIXED = {BYTE: 1, SHORT: 2, LONG: 8, CHAR: 2, BOOL: 1, DATE: 8, FLOAT: 4, DOUBLE: 8, UUID: 16}
+
+
+def inline_id(key_id: int) -> int:
+    """IDManager.stripRelationTypePadding: the key id without its 4 RelationType padding bits."""
+    return key_id >> 4
+
+
+def write_signed(v: int) -> bytes:
+    """VariableLong.write: |v| << 1 | sign, then writeUnsigned (VariableLong.java:133-148)."""
+    return write_unsigned((abs(v) << 1) | (1 if v < 0 else 0))
+
+
+def read_signed(b: bytes, pos: int) -> tuple[int, int]:
+    u, pos = read_unsigned(b, pos)
+    return (-(u >> 1) if u & 1 else u >> 1), pos
+
+
+def write_string(s: str | None) -> bytes:
+    """StringSerializer.write (StringSerializer.java:154-205), uncompressed forms (< 16000 characters)."""
+    if s is None:
+        return write_positive(0)
+    if all(ord(c) < 128 for c in s):
+        if not s:
+            return write_positive(1 << 4)
+        body = bytearray(s.encode("ascii"))
+        body[-1] |= 0x80
+        return write_positive(2 << 4) + bytes(body)
+    out = bytearray(write_positive((len(s) << 4) + (1 << 3)))
+    for ch in s:
+        c = ord(ch)
+        if c <= 0x7F:
+            out.append(c)
+        elif c > 0x7FF:
+            out += bytes([0xE0 | (c >> 12) & 0x0F, 0x80 | (c >> 6) & 0x3F, 0x80 | c & 0x3F])
+        else:
+            out += bytes([0xC0 | (c >> 6) & 0x1F, 0x80 | c & 0x3F])
+    return bytes(out)
+
+
+def write_gzip_string_header(nbytes: int) -> bytes:
+    """The header of a compressed String (GZIP, compressor id 1) whose payload is nbytes long."""
+    return write_positive((nbytes << 3) + 1)
+
+
+def write_value(ptype: int, v) -> bytes:
+    """StandardSerializer.writeObject: a null flag (0 / -1) unless String, then the serializer's bytes."""
+    if ptype == STRING:
+        return write_string(v)
+    if v is None:
+        return b"\xff"
+    if ptype == INT:
+        return b"\x00" + write_signed(v)
+    raw = v if isinstance(v, (bytes, bytearray)) else int(v).to_bytes(_FIXED[ptype], "big", signed=False)
+    assert len(raw) == _FIXED[ptype]
+    return b"\x00" + bytes(raw)
+
+
+def write_properties(props: list[tuple[int, int, object]]) -> bytes:
+    """An edge's non-signature properties [(key id, JG_PROP_* type, value)] in ascending key-id order."""
+    out = bytearray()
+    for kid, ptype, v in sorted(props, key=lambda p: p[0]):
+        out += write_positive(inline_id(kid)) + write_value(ptype, v)
+    return bytes(out)
+
+
+WEIGHT_ABSENT = -(1 << 31)
+
+
+def _skip_string(b: bytes, pos: int) -> int:
+    h, pos = read_unsigned(b, pos)
+    if h == 0:
+        return pos
+    n = h >> 3
+    if h & 7:
+        return pos + n
+    if n & 1 == 0:
+        if n >> 1 == 2:
+            while not b[pos] & 0x80:
+                pos += 1
+            pos += 1
+        return pos
+    for _ in range(n >> 1):
+        hi = b[pos] >> 4
+        pos += 1 if hi < 8 else 3 if hi == 14 else 2
+    return pos
+
+
+def edge_weight(entry: bytes, vpos: int, mult: int, direction: int, weight_key: int, key_types: dict) -> int:
+    """The Integer weight property of an edge entry (parseRelation's property loop, restated): its value
+    section after the ids, then (inline id, value) pairs; WEIGHT_ABSENT when the edge has no non-null
+    Integer value for weight_key (a key id).  key_types: {key id: JG_PROP_*}; raises KeyError for an
+    unknown key before the weight."""
+    if mult == MULTI:
+        pos = vpos
+    else:
+        pos = vpos
+        if is_unique(mult, direction):
+            _, pos = read_unsigned(entry, pos)
+        _, pos = read_unsigned(entry, pos)
+    want = inline_id(weight_key)
+    types = {inline_id(k): t for k, t in key_types.items()}
+    while pos < len(entry):
+        kid, pos = read_unsigned(entry, pos)
+        if kid > want:
+            break
+        t = types[kid]
+        if t == STRING:
+            pos = _skip_string(entry, pos)
+            continue
+        flag = entry[pos]
+        pos += 1
+        if flag == 0xFF:
+            if kid == want:
+                return WEIGHT_ABSENT
+            continue
+        if t == INT:
+            v, pos = read_signed(entry, pos)
+            if kid == want:
+                return v
+            continue
+        if kid == want:
+            return WEIGHT_ABSENT
+        pos += _FIXED[t]
+    return WEIGHT_ABSENT

@@ -128,3 +128,51 @@ def test_unlisted_labels_decode_as_multi(oracle_lib):
     e, vp = ec.encode_edge(t, ec.IN, 123456789, 42)
     got = oracle_lib.decode_edges(e, [0, len(e)], [vp])
     check_decoded(got, [(t, 1, 123456789, 42)])
+
+
+# ---- edge properties in the value (the weight the GPU decodes, tests/test_gpu_weights.py) ----
+
+def test_property_value_formats():
+    """StandardSerializer.writeObject + the attribute serializers, pinned byte for byte: a null flag
+    then IntegerSerializer's VariableLong.write (|v| << 1 | sign); StringSerializer's header
+    (length << 3 | compressor: ASCII 2 << 4 with the last byte marked, UTF (chars << 4) + 8, null 0)."""
+    assert ec.write_value(ec.INT, 5) == b"\x00\x8a"
+    assert ec.write_value(ec.INT, -3) == b"\x00\x87"
+    assert ec.write_value(ec.INT, 0) == b"\x00\x80"
+    assert ec.write_value(ec.INT, None) == b"\xff"
+    assert ec.write_value(ec.LONG, 1) == b"\x00" + (1).to_bytes(8, "big")
+    assert ec.write_string("ab") == bytes([0xA0, ord("a"), ord("b") | 0x80])
+    assert ec.write_string(None) == b"\x80" and ec.write_string("") == b"\x90"
+    assert ec.write_string("é") == bytes([0x98, 0xC3, 0xA9])
+    assert ec.read_signed(ec.write_signed(-(1 << 31)), 0) == (-(1 << 31), 5)
+
+
+def test_edge_weight_parser_round_trip():
+    """edge_weight (parseRelation's property loop restated) finds the weight among random properties of
+    every type, on entries of every multiplicity and direction layout."""
+    import numpy as np
+    rng = np.random.default_rng(0)
+    keys = {ec.schema_id(c, "user_key"): t for c, t in
+            zip(range(3, 14), (ec.BYTE, ec.SHORT, ec.LONG, ec.CHAR, ec.BOOL, ec.INT, ec.DATE, ec.FLOAT, ec.DOUBLE,
+                               ec.UUID, ec.STRING))}
+    wkey = ec.schema_id(8, "user_key")  # the INT key
+    width = {ec.BYTE: 1, ec.SHORT: 2, ec.LONG: 8, ec.CHAR: 2, ec.BOOL: 1, ec.DATE: 8, ec.FLOAT: 4, ec.DOUBLE: 8,
+             ec.UUID: 16}
+    for trial in range(300):
+        props, want = [], ec.WEIGHT_ABSENT
+        for k, t in keys.items():
+            if rng.random() < 0.5:
+                continue
+            if t == ec.STRING:
+                v = ["", "q", "hello", "ünï", None][int(rng.integers(0, 5))]
+            elif t == ec.INT:
+                v = None if rng.random() < 0.2 else int(rng.integers(-(1 << 31) + 1, 1 << 31))
+                if k == wkey:
+                    want = ec.WEIGHT_ABSENT if v is None else v
+            else:
+                v = None if rng.random() < 0.1 else bytes(rng.integers(0, 256, width[t], dtype=np.uint8))
+            props.append((k, t, v))
+        mult = int(rng.integers(0, 5))
+        entry, vpos = ec.encode_edge(ec.schema_id(20, "user_edge"), ec.OUT, 12345 << 8, 777 + trial, mult,
+                                     value=ec.write_properties(props))
+        assert ec.edge_weight(entry, vpos, mult, ec.OUT, wkey, keys) == want, (trial, props)
