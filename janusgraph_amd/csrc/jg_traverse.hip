@@ -350,7 +350,11 @@ struct MsBfsOp {
     const T* __restrict__ F;    // frontier words of the previous level, full length
     T* __restrict__ Fout;       // full length, owned slice written
     T* __restrict__ visited;    // [rows]
-    int32_t* __restrict__ depth;  // [nsrc * rows]
+    int32_t* __restrict__ depth;  // [nsrc * rows] int32 planes (used when depth8 is null)
+    // [nsrc * rows] byte planes, 255 = unreached: the levels 0..254 of a traversal, a quarter of the
+    // scattered depth writes (RMAT-26, 64 sources: 2.1 instead of 8.6 GB); widened to int32 planes on the
+    // host's request (output) or when a traversal reaches level 255 (msbfs_widen_kernel)
+    uint8_t* __restrict__ depth8;
     int32_t* __restrict__ changed;
     int64_t rows;
     VecPos pos;                 // owned row -> its slot in the gathered vector
@@ -374,7 +378,8 @@ struct MsBfsOp {
             *changed = 1;
             while (nw) {
                 const int s = __ffsll(nw) - 1;
-                depth[(int64_t)s * rows + row] = lvl;
+                if (depth8) depth8[(int64_t)s * rows + row] = (uint8_t)lvl;
+                else depth[(int64_t)s * rows + row] = lvl;
                 nw &= nw - 1;
             }
         }
@@ -477,6 +482,14 @@ __global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* 
     if (lane_id() == 0 && count) atomicAdd(nlive, count);
 }
 
+// int32 planes from byte planes (255 = unreached -> -1)
+__global__ void msbfs_widen_kernel(const uint8_t* __restrict__ d8, int64_t n, int32_t* __restrict__ d32) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t v = d8[i];
+        d32[i] = v == 255 ? -1 : (int32_t)v;
+    }
+}
+
 // pairs += the set bits of visited[0, rows) (sources x reached rows: the depth entries written)
 __global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long long* __restrict__ visited, int64_t rows,
                                                              unsigned long long* __restrict__ pairs) {
@@ -488,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long
 }
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
-                                  unsigned long long* __restrict__ visited, int32_t* __restrict__ depth, int64_t rows,
+                                  unsigned long long* __restrict__ visited, uint8_t* __restrict__ depth, int64_t rows,
                                   VecPos pos) {
     // sequential over the (<= 64) sources: several sources may share a vertex
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -854,6 +867,9 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     // then 4, 8, 16, ... (levels past the end are launched anyway and cost ~4 us each: a second batch
     // of 16 after 8 wasted ~14 of them at RMAT-26)
     int next_batch = 4;
+    // (A first batch sized from the previous traversal's level count, to drop the 2-4 no-op levels of
+    // ~4.6 us that end a 6-8-level RMAT-20 traversal, measured slower: 0.154 / 0.157 vs 0.140 / 0.128 ms,
+    // since a deeper traversal then pays a host read and a second batch; profiles/r03/bfs/.)
     for (int batch = std::max(1, tune().bfs_batch0);; batch = next_batch, next_batch = std::min(next_batch * 2, 64)) {
         if (max_depth >= 0) batch = std::min(batch, max_depth + 1 - level);
         if (batch <= 0) fail(JG_ERR_STATE, "BFS level control did not terminate");  // level max_depth stops
@@ -1276,7 +1292,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             const unsigned long long full = ns == 64 ? ~0ull : ((1ull << ns) - 1ull);
             struct St {
                 DevBuf<unsigned long long> F[2], vis;
-                DevBuf<int32_t> depth, changed;
+                DevBuf<int32_t> depth, changed;  // depth: int32 planes once widened
+                DevBuf<uint8_t> depth8;           // byte planes while every level is below 255
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
@@ -1298,7 +1315,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.F[0].alloc(len);
                 t.F[1].alloc(len);
                 t.vis.alloc(std::max<int64_t>(sh.rows, 1));
-                t.depth.alloc(std::max<int64_t>(sh.rows * ns, 1));
+                t.depth8.alloc(std::max<int64_t>(sh.rows * ns, 1));
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
@@ -1325,7 +1342,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.depth.get(), 0xFF, t.depth.bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.depth8.get(), 0xFF, t.depth8.bytes(), sh.stream));
                 std::vector<int64_t> loc(ns, -1);
                 for (int s = 0; s < ns; ++s) {
                     int shard = -1;
@@ -1339,7 +1356,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
                 DevBuf<int64_t> dloc(ns);
                 copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
-                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth.get(),
+                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth8.get(),
                                                           sh.rows, g.vec_pos(sh, adj_of(sh, c)));
                 JG_LAUNCH_CHECK();
                 JG_HIP(hipStreamSynchronize(sh.stream));
@@ -1396,6 +1413,21 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             // queued: td.queue[td.qc] holds the current frontier; live_ready: st[0].live[0] holds its live
             // bits (both from the previous level's end)
+            // byte depth planes hold levels 0..254: a traversal about to write level 255 widens them first
+            auto widen = [&]() {
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    if (!t.depth8.size()) continue;
+                    DeviceGuard dg(sh.device);
+                    const int64_t total = std::max<int64_t>(sh.rows * ns, 1);
+                    t.depth.alloc(total);
+                    msbfs_widen_kernel<<<grid_for(total), kBlock, 0, sh.stream>>>(t.depth8.get(), total, t.depth.get());
+                    JG_LAUNCH_CHECK();
+                    JG_HIP(hipStreamSynchronize(sh.stream));
+                    t.depth8.reset();
+                }
+            };
             bool queued = td_ok, live_ready = false;
             int cur = 0, level = 0;
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
@@ -1403,6 +1435,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int pull_levels = 0;
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
+                if (level + 1 >= 255) widen();
                 const bool td_level =
                     td_ok && (double)td.mf < (double)c0.push->nnz / (double)tune().bfs_alpha;
                 if (td_level && !queued) {
@@ -1438,6 +1471,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.Fout = t.F[cur ^ 1].get();
                         op.visited = t.vis.get();
                         op.depth = t.depth.get();
+                        op.depth8 = t.depth8.get();
                         op.changed = t.changed.get();
                         op.rows = sh.rows;
                         op.pos = g.vec_pos(sh, adj_of(sh, c0));
@@ -1464,6 +1498,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     op.Fout = t.F[cur ^ 1].get();
                     op.visited = t.vis.get();
                     op.depth = t.depth.get();
+                    op.depth8 = t.depth8.get();
                     op.changed = t.changed.get();
                     op.rows = sh.rows;
                     op.pos = g.vec_pos(sh, adj_of(sh, c));
@@ -1555,12 +1590,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             work_entries += td_entries;
             work_bytes += 12.0 * td_entries + 16.0 * td_touched + 8.0 * td_queued;
-            if (depth_rows)
+            if (depth_rows) {
+                widen();  // the caller's int32 rows
                 for (size_t i = 0; i < g.shards.size(); ++i)
                     for (int s = 0; s < ns; ++s)
                         if (depth_rows[b0 + s])
                             rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
                                           depth_rows[b0 + s]);
+            }
         }
         ctx.last.compute_ms = total_ms;
         ctx.last.levels = max_levels;

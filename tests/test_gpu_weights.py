@@ -126,18 +126,20 @@ def test_device_weights_equal_host_weights(oracle_lib, seed):
     ds = np.array([index[int(a)] for a in os_], np.int32)
     dd = np.array([index[int(b)] for b in ot], np.int32)
     w = hw[ent].astype(np.int32)
-    failures = 0
-    for s in range(0, len(vid), 37):
-        got_d, got_h = sd_or_error(gd, vid, s, 5), sd_or_error(gh, vid, s, 5)
-        try:
-            want = oracle_lib.shortest_distance(len(vid), ds, dd, s, 5, w)
-        except ValueError:  # a message crosses an edge without the weight: Fulgora's edge function throws
-            failures += 1
-            assert got_d == got_h == -1, (got_d, got_h)  # JG_ERR_ARG
-            continue
-        np.testing.assert_array_equal(got_d, want)
-        np.testing.assert_array_equal(got_h, want)
-    assert 0 < failures < len(range(0, len(vid), 37))  # both outcomes exercised
+    failures = runs = 0
+    for s in range(0, len(vid), 13):
+        for depth in (1, 2):  # deeper runs almost always cross an edge without the weight
+            runs += 1
+            got_d, got_h = sd_or_error(gd, vid, s, depth), sd_or_error(gh, vid, s, depth)
+            try:
+                want = oracle_lib.shortest_distance(len(vid), ds, dd, s, depth, w)
+            except ValueError:  # a message crosses an edge without the weight: Fulgora's edge function throws
+                failures += 1
+                assert isinstance(got_d, int) and got_d == got_h == -1, (got_d, got_h)  # JG_ERR_ARG
+                continue
+            np.testing.assert_array_equal(got_d, want)
+            np.testing.assert_array_equal(got_h, want)
+    assert 0 < failures < runs  # both outcomes exercised
     for g, c in ((gd, ctx_d), (gh, ctx_h)):
         g.close()
         c.close()
