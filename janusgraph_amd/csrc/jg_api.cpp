@@ -506,6 +506,12 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "cc_first") {
         JG_ARG(value >= 1 && value <= 64, "cc_first must be in [1, 64]");
         jg::tune().cc_first = (int)value;
+    } else if (k == "msbfs_bu") {
+        JG_ARG(value >= 0 && value <= 2, "msbfs_bu must be 0, 1 or 2");
+        jg::tune().msbfs_bu = (int)value;
+    } else if (k == "msbfs_bu_frac") {
+        JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_frac must be in [0, 1000]");
+        jg::tune().msbfs_bu_frac = (int)value;
     } else if (k == "msbfs_skip") {
         jg::tune().msbfs_skip = value != 0;
     } else if (k == "cc_uf") {
@@ -533,6 +539,18 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().bfs_init_suffix = value != 0;
     } else if (k == "bfs_grow_rule") {
         jg::tune().bfs_grow_rule = value != 0;
+    } else if (k == "bfs_td_split") {
+        JG_ARG(value >= 0 && value <= 2, "bfs_td_split must be 0, 1 or 2");
+        jg::tune().bfs_td_split = (int)value;
+    } else if (k == "bfs_td_split_levels") {
+        JG_ARG(value >= 0 && value <= 0xffff, "bfs_td_split_levels must be a mask of levels 0..15");
+        jg::tune().bfs_td_split_levels = (int)value;
+    } else if (k == "bfs_td_split_min") {
+        JG_ARG(value >= 1 && value <= INT32_MAX, "bfs_td_split_min must be in [1, 2^31)");
+        jg::tune().bfs_td_split_min = value;
+    } else if (k == "bfs_td_split_max") {
+        JG_ARG(value >= 1 && value <= INT32_MAX, "bfs_td_split_max must be in [1, 2^31)");
+        jg::tune().bfs_td_split_max = value;
     } else if (k == "bfs_batch0") {
         JG_ARG(value >= 1 && value <= 64, "bfs_batch0 must be in [1, 64]");
         jg::tune().bfs_batch0 = (int)value;

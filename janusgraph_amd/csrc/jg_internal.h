@@ -224,6 +224,7 @@ struct Shard {
     DevBuf<int64_t> bfs_qoff[2];             // [rows] first push edge of each queue entry
     DevBuf<unsigned long long> bfs_bm[2];    // [ceil(rows/64)] frontier bitmaps (bottom-up)
     DevBuf<uint8_t> bfs_seen;                // [rows] depth-is-set byte map (filters depth probes)
+    DevBuf<int32_t> bfs_owner;               // [rows] split top-down levels: claiming edge of each target
     DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
@@ -502,12 +503,24 @@ struct Tune {
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
                                       //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
+    int msbfs_bu = 0;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
+                                      //         (0 never, 1 every pull level, 2 when the frontier holds >= msbfs_bu_frac;
+                                      //         measured 2-4x slower than the merge-engine pull: RMAT-26 81.0 / 21.7 ms,
+                                      //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
+    int msbfs_bu_frac = 100;          //         permille of the rows
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_init_suffix = 1;          //         DO-BFS init: empty rows from the plan's empty suffix (no row_ptr reads)
     int bfs_grow_rule = 0;            //         DO-BFS: top-down -> bottom-up only while the frontier grows
                                       //         (measured: RMAT-26 -0.6%, RMAT-20 +2.5%; off)
+    int bfs_td_split = 2;             //         DO-BFS top-down levels of >= bfs_td_split_min frontier entries in two
+                                      //         launches (targets' owner written, then claimed) instead of one CAS
+                                      //         per entry: 0 never, 1 every level, 2 the level(s) in bfs_td_split_levels
+    int bfs_td_split_levels = 2;      //         bit mask of the levels mode 2 splits (default: level 1)
+    int64_t bfs_td_split_min = 65536; //         frontier entries outside [min, max] claim by CAS anyway (the split
+    int64_t bfs_td_split_max = 1 << 20;  //       walks the entries twice: RMAT-26 levels of tens of millions lost
+                                      //         1.2 ms; RMAT-20's 329 K-entry level 1 went 64 -> 26 us)
     int bfs_batch0 = 10;              //         DO-BFS: levels in the first batch (then 4, 8, 16, ...)
     int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
     int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)

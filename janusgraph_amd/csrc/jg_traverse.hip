@@ -100,6 +100,9 @@ struct BfsLevel {
     unsigned long long* bm_out;
     uint8_t* seen;  // seen[v] != 0: depth[v] is set (a 64 MB byte map at 2^26 vertices stays in the
                     // Infinity Cache where the 268 MB depth array does not; bytes need no atomics)
+    int32_t* owner;           // [rows] split top-down levels (kTdOwner / kTdClaim)
+    long long split_min, split_max;  // split: frontier entries for which the level is split (max < 2^31)
+    int split;                // this launch is followed by bfs_td_claim_kernel
     unsigned long long* ctr;  // [kBfsRing] packed frontier counters, slot = level % kBfsRing
     BfsState* st;             // [kBfsRing]
     int level, max_depth;
@@ -147,15 +150,57 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
 // the frontier is spread over the whole grid.  A thread's edges are processed in phases (all target
 // loads, then all depth probes and claims, then the degree loads) so its dependent memory round trips
 // do not multiply with the edges it holds; one block-wide append per edge slot follows.
-template <class App>
+// Claims (kMode): kTdCas one CAS on the target's depth per entry; a split level runs kTdOwner (every
+// entry whose target is unvisited stores its index in owner[target], a plain store) and, in a second
+// launch, kTdClaim (the entry whose index survived claims the target).  Device-scope CAS runs at the
+// memory side, so the ~100 entries of one level that reach the same hub target queue behind each other
+// (RMAT-20 level 1: 329 K entries, 107 K targets, 64 us); plain stores to one address do not.
+enum TdMode { kTdCas = 0, kTdOwner = 1, kTdClaim = 2 };
+
+// Queue-entry search of the edge-parallel top-down: every stride-th edge offset of the input queue
+// (stride = ceil(nf / kQoffSamples)) is staged in LDS by each block with work, the
+// search runs there and then over at most `qs` global offsets.  The offsets were appended by every XCD
+// in the previous launch, so each global probe misses the reading XCD's L2: a 22.6 K-entry queue cost
+// 15 dependent probes (RMAT-20 level 4, a 24.9 K-entry top-down level: 12.4 us).
+constexpr int kQoffSamples = 1024;
+struct QoffIndex {
+    const int64_t* lds;  // samples: lds[j] = qoff_in[j * stride]
+    int64_t stride, count;
+};
+__device__ __forceinline__ QoffIndex stage_qoff(const BfsLevel& a, int64_t nf, int64_t mf, int ept, int64_t* s_qs) {
+    QoffIndex q{s_qs, (nf + kQoffSamples - 1) / kQoffSamples, 0};
+    q.count = (nf + q.stride - 1) / q.stride;
+    if ((int64_t)blockIdx.x * blockDim.x * ept < mf)  // block-uniform: blocks past the frontier's edges skip it
+        for (int64_t j = threadIdx.x; j < q.count; j += blockDim.x) s_qs[j] = a.qoff_in[j * q.stride];
+    __syncthreads();
+    return q;
+}
+// the queue entry i with qoff_in[i] <= e < qoff_in[i + 1] (offsets are monotone; zero-degree entries
+// share their successor's offset and the search returns the last of them)
+__device__ __forceinline__ int64_t find_entry(const BfsLevel& a, const QoffIndex& q, int64_t nf, int64_t e) {
+    int64_t lo = 0, hi = q.count - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (q.lds[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    int64_t g0 = lo * q.stride, g1 = std::min(g0 + q.stride, nf) - 1;
+    while (g0 < g1) {
+        const int64_t mid = (g0 + g1 + 1) >> 1;
+        if (a.qoff_in[mid] <= e) g0 = mid; else g1 = mid - 1;
+    }
+    return g0;
+}
+
+template <int kMode, class App>
 __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int64_t mf, unsigned long long* packed,
-                                             App& app) {
+                                             App& app, int64_t* s_qs) {
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int ept = mf <= nthreads ? 1 : kTdEdgesPerThread;  // grid-uniform
     const int64_t per_tile = nthreads * ept;
     const int64_t tiles = (mf + per_tile - 1) / per_tile;  // wave-uniform
     const int32_t next_depth = a.level + 1;
+    const QoffIndex qi = stage_qoff(a, nf, mf, ept, s_qs);
     for (int64_t t = 0; t < tiles; ++t) {
         // a block (a wave, with wave-staged appends) whose slice of this tile is past the frontier's
         // edges has nothing to claim or append (small frontiers leave most of the grid idle)
@@ -166,12 +211,7 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
         bool have[kTdEdgesPerThread], won[kTdEdgesPerThread];
         int64_t vdeg[kTdEdgesPerThread];
         if (e0 < mf) {
-            int64_t lo = 0, hi = nf - 1;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) >> 1;
-                if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
-            }
-            int64_t i = lo;
+            int64_t i = find_entry(a, qi, nf, e0);
             int64_t next_bound = i + 1 < nf ? a.qoff_in[i + 1] : mf;
 #pragma unroll
             for (int k = 0; k < kTdEdgesPerThread; ++k) {
@@ -194,11 +234,32 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
         uint8_t sv[kTdEdgesPerThread];
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) sv[k] = have[k] ? a.seen[v[k]] : 1;
+        if constexpr (kMode == kTdOwner) {
 #pragma unroll
-        for (int k = 0; k < kTdEdgesPerThread; ++k) {
-            // the byte map filters; the CAS on depth decides (a stale byte only costs a failed CAS)
-            won[k] = !sv[k] && atomicCAS(&a.depth[v[k]], -1, next_depth) == -1;
-            if (won[k]) a.seen[v[k]] = 1;
+            for (int k = 0; k < kTdEdgesPerThread; ++k)
+                if (!sv[k]) a.owner[v[k]] = (int32_t)(e0 + k);  // td_split: mf < 2^31
+            continue;
+        }
+        if constexpr (kMode == kTdClaim) {
+            // the seen bytes are the ones the owner pass read: only the claiming entry changes them
+            int32_t ow[kTdEdgesPerThread];
+#pragma unroll
+            for (int k = 0; k < kTdEdgesPerThread; ++k) ow[k] = sv[k] ? -1 : a.owner[v[k]];
+#pragma unroll
+            for (int k = 0; k < kTdEdgesPerThread; ++k) {
+                won[k] = !sv[k] && ow[k] == (int32_t)(e0 + k);
+                if (won[k]) {
+                    a.depth[v[k]] = next_depth;
+                    a.seen[v[k]] = 1;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kTdEdgesPerThread; ++k) {
+                // the byte map filters; the CAS on depth decides (a stale byte only costs a failed CAS)
+                won[k] = !sv[k] && atomicCAS(&a.depth[v[k]], -1, next_depth) == -1;
+                if (won[k]) a.seen[v[k]] = 1;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) vdeg[k] = won[k] ? a.deg_rp[v[k] + 1] - a.deg_rp[v[k]] : 0;
@@ -250,6 +311,12 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
     }
 }
 
+// a top-down level runs split when its launch is followed by the claim launch and its input frontier's
+// entries are in [split_min, split_max] (split_max < 2^31: the owner map holds int32 entry indices)
+__device__ __forceinline__ bool td_split(const BfsLevel& a, long long mf) {
+    return a.split && mf >= a.split_min && mf <= a.split_max;
+}
+
 template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
@@ -276,10 +343,41 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     unsigned long long* packed = a.ctr + a.level % kBfsRing;
     App app{s_app};
     app.init();
-    if (!s_st.bottom_up) bfs_top_down(a, s_nf, s_mf, packed, app);
-    else if (s_switch) bfs_bottom_up<true>(a, packed, app);
-    else bfs_bottom_up<false>(a, packed, app);
+    if (!s_st.bottom_up) {
+        __shared__ int64_t s_qs[kQoffSamples];
+        if (td_split(a, s_mf)) bfs_top_down<kTdOwner>(a, s_nf, s_mf, packed, app, s_qs);  // the claim launch appends
+        else bfs_top_down<kTdCas>(a, s_nf, s_mf, packed, app, s_qs);
+    } else if (s_switch) {
+        bfs_bottom_up<true>(a, packed, app);
+    } else {
+        bfs_bottom_up<false>(a, packed, app);
+    }
     app.final(a.queue_out, a.qoff_out, packed);
+}
+
+// Second launch of a split top-down level: the level's state (bfs_level_kernel wrote it) and input
+// frontier counter say whether the level was split; if so, every entry re-reads its target's owner.
+template <bool WAVE>
+__global__ __launch_bounds__(kBlock) void bfs_td_claim_kernel(BfsLevel a) {
+    __shared__ long long s_nf, s_mf;
+    __shared__ int s_run;
+    using Stage = std::conditional_t<WAVE, WaveStage, StagedAppend>;
+    using App = std::conditional_t<WAVE, WaveApp, BlockApp>;
+    __shared__ Stage s_app;
+    if (threadIdx.x == 0) {
+        const BfsState c = a.st[a.level % kBfsRing];
+        const unsigned long long h = a.ctr[(a.level + kBfsRing - 1) % kBfsRing];
+        s_nf = (long long)(h >> kPackShift);
+        s_mf = (long long)(h & kEdgeMask);
+        s_run = !c.done && !c.bottom_up && td_split(a, s_mf);
+    }
+    __syncthreads();
+    if (!s_run) return;
+    App app{s_app};
+    app.init();
+    __shared__ int64_t s_qs[kQoffSamples];
+    bfs_top_down<kTdClaim>(a, s_nf, s_mf, a.ctr + a.level % kBfsRing, app, s_qs);
+    app.final(a.queue_out, a.qoff_out, a.ctr + a.level % kBfsRing);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -550,6 +648,135 @@ __global__ void msbfs_source_queue_kernel(const int64_t* __restrict__ rows, int 
     packed[0] = ((unsigned long long)cnt << kPackShift) | (unsigned long long)off;
 }
 
+// ---- bottom-up pull levels of the bit-parallel BFS with early exit (one shard) ----
+// A row's gain this level is the OR of its neighbours' frontier words masked by need = ~visited & live;
+// once the OR covers need, no further entry can add a bit, so the scan stops (Beamer's bottom-up
+// early exit, per 64-bit word).  On a level whose frontier is large (most sources reach most rows)
+// nearly every row stops within its first entries (the CSR rows are column-ordered, hubs first):
+// RMAT-22, the level after the frontier's peak: 53 M -> 2.4 M entries (tools/msbfs_bu_sim).
+// The result equals the merge engine's: the same OR, the same finalize.  Rows [0, hub) take a
+// workgroup each (4 x 1024 entries in flight per step, a block-wide OR), [hub, wave) a wave each
+// (4 x 64), [wave, ne) a lane each (4 at a time), [ne, rows) have no entries and gain nothing.
+struct MsBu {
+    const int64_t* rp;
+    const int32_t* col;
+    int64_t rows, hub, wave, ne;
+    int64_t blocks_hub, blocks_wave;  // first blocks of the wave and lane roles
+    unsigned long long* examined;     // += the entries scanned (work counter, jg_stats.algorithmic_bytes)
+};
+constexpr int kMsBuUnroll = 4;
+
+__device__ __forceinline__ unsigned long long wave_or(unsigned long long m) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) m |= __shfl_xor(m, o, kWave);
+    return m;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp op) {
+    __shared__ unsigned long long red[kMergeWaves];
+    __shared__ int stop;
+    const unsigned long long live = *op.live;
+    const int lane = lane_id(), wv = threadIdx.x / kWave;
+    if ((int64_t)blockIdx.x < a.blocks_hub) {  // hub rows: a workgroup each
+        for (int64_t v = blockIdx.x; v < a.hub; v += a.blocks_hub) {
+            const unsigned long long need = ~op.visited[v] & live;  // block-uniform
+            unsigned long long acc = 0;
+            if (need) {
+                const int64_t e1 = a.rp[v + 1];
+                for (int64_t j = a.rp[v]; j < e1; j += kMsBuUnroll * kMergeThreads) {
+                    int32_t c[kMsBuUnroll];
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) {
+                        const int64_t e = j + u * kMergeThreads + threadIdx.x;
+                        c[u] = e < e1 ? a.col[e] : -1;
+                    }
+                    unsigned long long m = 0;
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
+                    m = wave_or(m & need);
+                    if (lane == 0) red[wv] = m;
+                    __syncthreads();
+                    if (threadIdx.x == 0) {
+                        unsigned long long t = acc;
+                        for (int w = 0; w < kMergeWaves; ++w) t |= red[w];
+                        red[0] = t;
+                        stop = t == need;
+                    }
+                    __syncthreads();
+                    acc = red[0];
+                    const int done = stop;
+                    __syncthreads();  // red / stop are rewritten by the next step
+                    if (threadIdx.x == 0)
+                        atomicAdd(a.examined, (unsigned long long)min((int64_t)kMsBuUnroll * kMergeThreads, e1 - j));
+                    if (done) break;
+                }
+            }
+            if (threadIdx.x == 0) op.finalize(v, acc);
+        }
+        return;
+    }
+    if ((int64_t)blockIdx.x < a.blocks_wave) {  // rows of 64 .. hub entries: a wave each
+        const int64_t nw = (a.blocks_wave - a.blocks_hub) * kMergeWaves;
+        for (int64_t v = a.hub + ((int64_t)blockIdx.x - a.blocks_hub) * kMergeWaves + wv; v < a.wave; v += nw) {
+            const unsigned long long need = ~op.visited[v] & live;  // wave-uniform
+            unsigned long long acc = 0;
+            if (need) {
+                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
+                int64_t j = e0;
+                for (; j < e1 && acc != need; j += kMsBuUnroll * kWave) {
+                    int32_t c[kMsBuUnroll];
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) {
+                        const int64_t e = j + u * kWave + lane;
+                        c[u] = e < e1 ? a.col[e] : -1;
+                    }
+                    unsigned long long m = 0;
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
+                    acc |= wave_or(m & need);
+                }
+                if (lane == 0) atomicAdd(a.examined, (unsigned long long)(min(j, e1) - e0));
+            }
+            if (lane == 0) op.finalize(v, acc);
+        }
+        return;
+    }
+    // light rows: a lane each; rows past ne have no entries
+    const int64_t nt = ((int64_t)gridDim.x - a.blocks_wave) * kMergeThreads;
+    unsigned long long scanned = 0;
+    for (int64_t v = a.wave + ((int64_t)blockIdx.x - a.blocks_wave) * kMergeThreads + threadIdx.x; v < a.rows; v += nt) {
+        unsigned long long acc = 0;
+        if (v < a.ne) {
+            const unsigned long long need = ~op.visited[v] & live;
+            if (need) {
+                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
+                int64_t j = e0;
+                for (; j < e1 && acc != need; j += kMsBuUnroll) {
+                    int32_t c[kMsBuUnroll];
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) c[u] = a.col[j + u < e1 ? j + u : e1 - 1];
+#pragma unroll
+                    for (int u = 0; u < kMsBuUnroll; ++u) acc |= op.F[c[u]] & need;
+                }
+                scanned += (unsigned long long)(min(j, e1) - e0);
+            }
+        }
+        op.finalize(v, acc);
+    }
+    scanned = wave_reduce_add(scanned);
+    if (lane == 0 && scanned) atomicAdd(a.examined, scanned);
+}
+
+// the first row whose degree is below d (rows are degree-sorted, descending)
+__global__ void degree_bound_kernel(const int64_t* __restrict__ rp, int64_t rows, int64_t d, int64_t* __restrict__ out) {
+    int64_t lo = 0, hi = rows;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (rp[mid + 1] - rp[mid] >= d) lo = mid + 1; else hi = mid;
+    }
+    *out = lo;
+}
+
 struct MsTd {
     const int32_t* queue;
     const int64_t* qoff;
@@ -808,6 +1035,7 @@ void bfs_buffers(Shard& sh) {
         if (sh.bfs_bm[k].size() != w1) sh.bfs_bm[k].alloc(w1);
     }
     if (sh.bfs_seen.size() != r1) sh.bfs_seen.alloc(r1);
+    if (tune().bfs_td_split && sh.bfs_owner.size() != r1) sh.bfs_owner.alloc(r1);
     if (sh.bfs_ctr.size() != (size_t)kBfsRing) sh.bfs_ctr.alloc(kBfsRing);
     if (sh.bfs_state.size() != kBfsRing * sizeof(BfsState)) sh.bfs_state.alloc(kBfsRing * sizeof(BfsState));
 }
@@ -854,6 +1082,10 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.alpha = (double)(roots ? tune().bfs_alpha : tune().dobfs_alpha);
     a.beta = (double)tune().bfs_beta;
     a.grow_rule = tune().bfs_grow_rule;
+    a.owner = sh.bfs_owner.get();
+    a.split_min = (long long)tune().bfs_td_split_min;
+    a.split_max = (long long)tune().bfs_td_split_max;
+    const int split_mode = tune().bfs_td_split, split_levels = tune().bfs_td_split_levels;
     // a fixed grid, both directions grid-stride: ~sqrt(rows) workgroups (tools/bfs_sweep.py, ms per
     // traversal: RMAT-20 0.164 / 0.141 / 0.140 / 0.157 at 256 / 512 / 1024 / 4096; RMAT-22 0.311 /
     // 0.310 / 0.412 at 1024 / 2048 / 8192; RMAT-26 3.46 / 2.45 / 2.19 / 2.11 / 2.14 / 2.76 at 512 / 1024
@@ -882,10 +1114,16 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             a.qoff_out = sh.bfs_qoff[p ^ 1].get();
             a.bm_in = sh.bfs_bm[p].get();
             a.bm_out = sh.bfs_bm[p ^ 1].get();
+            a.split = a.owner && (split_mode == 1 || (split_mode == 2 && level < 16 && ((split_levels >> level) & 1)));
             if (prof_enabled(ctx)) prof_record_start(ctx, sh);
             if (tune().bfs_wave_stage) bfs_level_kernel<true><<<grid, kBlock, 0, s>>>(a);
             else bfs_level_kernel<false><<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
+            if (a.split) {
+                if (tune().bfs_wave_stage) bfs_td_claim_kernel<true><<<grid, kBlock, 0, s>>>(a);
+                else bfs_td_claim_kernel<false><<<grid, kBlock, 0, s>>>(a);
+                JG_LAUNCH_CHECK();
+            }
             if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
             if (debug_bfs()) {
                 BfsState ds{};
@@ -1297,7 +1535,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
-                DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs
+                DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs,
+                                                  // [2] entries the early-exit bottom-up levels scanned
                 int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
             };
             std::vector<St> st(g.shards.size());
@@ -1320,8 +1559,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
                 t.live.alloc(2);
-                t.work.alloc(2);
-                JG_HIP(hipMemsetAsync(t.work.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+                t.work.alloc(3);
+                JG_HIP(hipMemsetAsync(t.work.get(), 0, 3 * sizeof(unsigned long long), sh.stream));
                 t.light_nnz = c.pull->nnz;
                 if (t.split.size() && plan.split_rows > 0) {
                     int64_t split_nnz = 0;
@@ -1428,6 +1667,29 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.depth8.reset();
                 }
             };
+            // one shard: pull levels whose frontier holds at least msbfs_bu_frac / 1000 of the rows run
+            // bottom-up with early exit (msbfs_bu_kernel) instead of through the merge engine
+            MsBu bu{};
+            const bool bu_ok = td_ok && c0.pull == c0.push && tune().msbfs_bu > 0;
+            if (bu_ok) {
+                DevBuf<int64_t> bnd(2);
+                degree_bound_kernel<<<1, 1, 0, sh0.stream>>>(c0.pull->row_ptr.get(), sh0.rows, 4096, bnd.get());
+                degree_bound_kernel<<<1, 1, 0, sh0.stream>>>(c0.pull->row_ptr.get(), sh0.rows, kWave, bnd.get() + 1);
+                JG_LAUNCH_CHECK();
+                int64_t hb[2] = {0, 0};
+                copy_d2h(hb, bnd.get(), sizeof hb, sh0.stream);
+                bu.rp = c0.pull->row_ptr.get();
+                bu.col = c0.pull->col.get();
+                bu.rows = sh0.rows;
+                bu.hub = hb[0];
+                bu.wave = hb[1];
+                bu.ne = c0.pull->empty_from >= 0 ? std::min(c0.pull->empty_from, sh0.rows) : sh0.rows;
+                bu.blocks_hub = std::min<int64_t>(bu.hub, 256);
+                bu.blocks_wave = bu.blocks_hub + std::min<int64_t>((bu.wave - bu.hub + kMergeWaves - 1) / kMergeWaves, 2048);
+                bu.examined = st[0].work.get() + 2;
+            }
+            const int64_t bu_rows = bu_ok ? sh0.rows * (int64_t)tune().msbfs_bu_frac / 1000 : 0;
+            int bu_levels = 0;
             bool queued = td_ok, live_ready = false;
             int cur = 0, level = 0;
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
@@ -1444,6 +1706,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
                 const bool have_live = live_ready;
                 queued = live_ready = false;
+                bool level_bu = false;  // this pull level ran msbfs_bu_kernel
                 if (td_level) {
                     Shard& sh = sh0;
                     St& t = st[0];
@@ -1516,6 +1779,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         JG_LAUNCH_CHECK();
                     }
                     op.live = lw;
+                    if (bu_ok && (tune().msbfs_bu == 1 || td.nq >= bu_rows)) {
+                        const int64_t light = sh.rows - bu.wave;
+                        const unsigned grid = (unsigned)(bu.blocks_wave +
+                                                         std::max<int64_t>(std::min<int64_t>((light + kMergeThreads - 1) / kMergeThreads, 4096), 1));
+                        msbfs_bu_kernel<<<grid, kMergeThreads, 0, sh.stream>>>(bu, op);
+                        JG_LAUNCH_CHECK();
+                        level_bu = true;
+                    } else {
                     std::vector<const uint32_t*> tl;
                     for (size_t b = 0; b < t.todo.size(); ++b) {
                         const SliceBand& bd = *plan.bands[b];
@@ -1534,6 +1805,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                 t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
                                 tl.empty() ? nullptr : tl.data());
+                    }
                     if (td_ok) {  // the next level's live bits and frontier counter (its direction)
                         JG_HIP(hipMemsetAsync(td.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
                         JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
@@ -1545,7 +1817,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                 }
                 if (!td_level) {
-                    ++pull_levels;
+                    ++(level_bu ? bu_levels : pull_levels);
                     std::vector<void*> bufs;
                     for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
                     exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
@@ -1581,12 +1853,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 St& t = st[i];
                 msbfs_pairs_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.vis.get(), sh.rows, t.work.get() + 1);
                 JG_LAUNCH_CHECK();
-                unsigned long long w[2] = {0, 0};
+                unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels : (double)w[0];
-                const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels;
+                const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
                 work_entries += entries;
-                work_bytes += 12.0 * entries + 24.0 * (double)sh.rows * pull_levels + 4.0 * (double)w[1];
+                work_bytes += 12.0 * entries + 24.0 * (double)sh.rows * (pull_levels + bu_levels) + 4.0 * (double)w[1];
             }
             work_entries += td_entries;
             work_bytes += 12.0 * td_entries + 16.0 * td_touched + 8.0 * td_queued;

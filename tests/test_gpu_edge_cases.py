@@ -170,3 +170,27 @@ def test_connected_components_union_find_and_propagation(ctx, oracle_lib, uf):
             g.close()
     finally:
         _lib.tune_set("cc_uf", 1)
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_multi_source_bfs_past_255_levels(oracle_lib, shards):
+    """The bit-parallel BFS keeps depths in byte planes for levels 0..254 and widens them to int32 when a
+    traversal reaches level 255: a 700-vertex path (plus a few chords and an isolated vertex) from 5
+    sources, unbounded and bounded at 300, on 1 and 2 shards, every depth row against the oracle."""
+    import janusgraph_amd as jg
+    n = 702
+    s = list(range(699)) + [10, 400, 650]
+    t = list(range(1, 700)) + [12, 405, 651]
+    s, t = np.array(s, np.int32), np.array(t, np.int32)
+    vid = (np.arange(n, dtype=np.int64) + 1) << 8
+    c = jg.Context((0,) * shards)
+    g = c.build(vid, vid[s], vid[t], flags=jg.ADJ_BOTH)
+    srcs = [0, 3, 350, 699, 701]
+    for max_depth in (-1, 300):
+        got = g.bfs(vid[srcs], jg.DIR_BOTH, max_depth=max_depth)
+        for k, sv in enumerate(srcs):
+            np.testing.assert_array_equal(got[k], oracle_lib.bfs(n, s, t, sv, oracle_lib.DIR_BOTH, max_depth),
+                                          err_msg=f"shards {shards} max_depth {max_depth} source {sv}")
+        assert got[0].max() > 255
+    g.close()
+    c.close()

@@ -150,6 +150,46 @@ def test_bfs_rmat_vs_oracle(ctx, oracle_lib, scale):
         np.testing.assert_array_equal(depth, ref)
 
 
+@pytest.mark.parametrize("mode,split_min", [(0, 65536), (1, 1), (1, 4096), (2, 1)])
+def test_bfs_split_top_down_matches_oracle(oracle_lib, mode, split_min):
+    """Split top-down levels (owner store + claim launch, Tune::bfs_td_split) against the CAS claims:
+    identical depths, edge counts and CC superstep counts (the eccentricity BFS shares the level code),
+    for every level split (mode 1) and level 1 only (mode 2)."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    c = jg.Context((0,))
+    try:
+        _lib.tune_set("bfs_td_split", mode)
+        _lib.tune_set("bfs_td_split_min", split_min)
+        for scale in (14, 17):
+            n, vid, src, dst, ds, dd = rmat_case(oracle_lib, scale)
+            g = c.build(vid, src, dst, flags=ALL)
+            deg = np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n)
+            cand = np.nonzero(deg)[0]
+            for k in range(3):
+                s = int(cand[(k * 7919) % len(cand)])
+                _lib.tune_set("bfs_td_split", 0)
+                g.bfs([vid[s]], 3, want=False)
+                edges_cas = c.stats()["edges_traversed"]
+                _lib.tune_set("bfs_td_split", mode)
+                got = g.bfs([vid[s]], 3)[0]
+                np.testing.assert_array_equal(got, oracle_lib.bfs(n, ds, dd, s, 3))
+                # each reached vertex claimed exactly once: the same frontier degree sums as the CAS claims
+                assert c.stats()["edges_traversed"] == edges_cas
+                for direction in (1, 2):
+                    np.testing.assert_array_equal(g.bfs([vid[s]], direction)[0],
+                                                  oracle_lib.bfs(n, ds, dd, s, direction))
+            comp, it = g.connected_components()
+            comp_ref, it_ref = oracle_lib.connected_components(n, ds, dd, vid)
+            np.testing.assert_array_equal(comp, comp_ref)
+            assert it == it_ref
+            g.close()
+    finally:
+        _lib.tune_set("bfs_td_split", 2)
+        _lib.tune_set("bfs_td_split_min", 65536)
+        c.close()
+
+
 def test_bfs_isolated_and_missing_source(ctx, oracle_lib):
     n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 10)
     g = ctx.build(vid, src, dst, flags=4)

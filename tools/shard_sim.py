@@ -1,9 +1,14 @@
-"""Sharded PageRank on ONE GPU: P logical shards (exchange by device copies), halo exchange vs the
-dense allgather.  Estimates the per-shard superstep compute of a P-GPU run (the shards run one after
-another on one stream) and prints the halo volume each shard would receive over xGMI.
+"""Sharded programs on ONE GPU: P logical shards (exchange by device copies) to estimate a P-GPU run.
+The shards run one after another on one stream, so the kernel time per shard is the P-GPU compute
+estimate; the halo volume is what each shard would receive over xGMI per exchange step.
 
-    python tools/shard_sim.py --scale 22 --shards 8 [--steps 10]
-Run with JG_DEBUG_PLAN=1 2> file to also get the per-shard halo sizes from the build.
+    python tools/shard_sim.py --scale 26 --shards 1 8 [--program pr|bfs|cc|msbfs] [--steps 10]
+
+pr:    PageRank supersteps (halo vs the dense allgather layout), per-shard superstep kernel time
+bfs:   sharded single-source DO-BFS from the bench's sources: levels, exchange steps, kernel time
+cc:    the sharded CC propagation (one shard: the union-find path), supersteps and time
+msbfs: the 64-source bit-parallel BFS, levels and time
+Each line carries exchange_values (values all shards receive per exchange step) and its bytes.
 """
 from __future__ import annotations
 
@@ -13,11 +18,13 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(jg, scale, shards, halo, steps, warmup):
+def run_pr(jg, scale, shards, halo, steps, warmup):
     jg._lib.tune_set("halo", halo)
     ctx = jg.Context((0,) * shards)
     try:
@@ -25,6 +32,7 @@ def run(jg, scale, shards, halo, steps, warmup):
     finally:
         jg._lib.tune_set("halo", 1)
     build_ms = ctx.stats()["build_ms"]
+    xv = g.info()["exchange_values"]
     n, m = 1 << scale, 16 << scale
     g.pagerank_begin(0.85, n)
     g.pagerank_step(warmup)
@@ -40,27 +48,76 @@ def run(jg, scale, shards, halo, steps, warmup):
     g.close()
     ctx.close()
     launches = max(st["kernel_launches"], 1)
-    return {"shards": shards, "halo": halo, "build_ms": round(build_ms, 1),
+    return {"program": "pr", "shards": shards, "halo": halo, "build_ms": round(build_ms, 1),
             "ms_per_step_all_shards": round(dt / steps * 1e3, 4),
             "compute_ms_per_shard_step": round(st["kernel_ms_total"] / launches, 4),
             "exchange_ms_per_step": round(dt / steps * 1e3 - st["kernel_ms_total"] / steps, 4),
+            "exchange_values_all_shards": xv, "exchange_bytes_per_shard": 8 * xv / max(shards, 1),
             "gteps_single_gpu_equiv": round(m / (dt / steps) / 1e9, 2)}, rank
+
+
+def run_both(jg, program, scale, shards, reps):
+    import bench
+    ctx = jg.Context((0,) * shards)
+    g = ctx.build_rmat(scale, 16, 0x5EED + scale, flags=jg.ADJ_BOTH)
+    xv = g.info()["exchange_values"]
+    deg = g.degrees(jg.DIR_BOTH)
+    out = {"program": program, "shards": shards, "exchange_values_all_shards": xv,
+           "exchange_values_per_shard": xv / max(shards, 1)}
+    rows = []
+    if program == "bfs":
+        m = 16 << scale
+        for sv in bench.pick_sources(deg, 16, scale).tolist():
+            g.bfs([sv], jg.DIR_BOTH, want=False)
+            if ctx.stats()["edges_traversed"] < m // 100:
+                continue
+            for _ in range(reps):
+                ctx.set_profiling(True)
+                g.bfs([sv], jg.DIR_BOTH, want=False)
+                st = ctx.stats()
+                ctx.set_profiling(False)
+                rows.append((st["compute_ms"], st["exchange_ms"], st["levels"]))
+            if len(rows) >= 3 * reps:
+                break
+    else:
+        call = g.connected_components if program == "cc" else (
+            lambda: g.bfs(bench.pick_sources(deg, 64, 7), jg.DIR_BOTH, want=False))
+        call()
+        for _ in range(reps):
+            ctx.set_profiling(True)
+            call()
+            st = ctx.stats()
+            ctx.set_profiling(False)
+            rows.append((st["compute_ms"], st["exchange_ms"], st["levels"]))
+    g.close()
+    ctx.close()
+    r = np.array(rows)
+    out.update({"runs": len(rows), "compute_ms_all_shards": round(float(np.median(r[:, 0])), 4),
+                "exchange_ms_all_shards": round(float(np.median(r[:, 1])), 4),
+                "levels": int(np.median(r[:, 2])),
+                "kernel_ms_per_shard": round(float(np.median(r[:, 0] - r[:, 1])) / shards, 4)})
+    return out
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=22)
     p.add_argument("--shards", type=int, nargs="+", default=[1, 8])
+    p.add_argument("--program", default="pr", choices=["pr", "bfs", "cc", "msbfs"])
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--halo", type=int, nargs="+", default=[1, 0], help="halo settings tried for P > 1")
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--halo", type=int, nargs="+", default=[1, 0], help="halo settings tried for P > 1 (pr)")
     a = p.parse_args()
-    import numpy as np
     import janusgraph_amd as jg
+    if a.program != "pr":
+        for P in a.shards:
+            print(json.dumps(run_both(jg, a.program, a.scale, P, a.reps)), flush=True)
+        return
     ref = None
     for P in a.shards:
         for halo in (a.halo if P > 1 else [1]):
-            r, rank = run(jg, a.scale, P, halo, a.steps, a.warmup)
+            r, rank = run_pr(jg, a.scale, P, halo, a.steps, a.warmup)
             if ref is None:
                 ref = rank
             r["max_rel_vs_first"] = float(np.max(np.abs(rank - ref) / np.maximum(np.abs(ref), 1e-300)))
