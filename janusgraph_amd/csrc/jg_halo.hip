@@ -378,6 +378,103 @@ void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
+std::vector<int64_t> halo_word_offsets(const Halo& h, int P) {
+    std::vector<int64_t> w((size_t)P + 1, 0);
+    for (int q = 0; q < P; ++q) w[(size_t)q + 1] = w[(size_t)q] + (h.send_off[(size_t)q + 1] - h.send_off[(size_t)q] + 63) / 64;
+    return w;
+}
+
+void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, std::vector<uint64_t*>& bitmaps,
+                        bool reverse) {
+    if (g.P == 1) return;
+    Ctx& c = *g.ctx;
+    constexpr size_t W = sizeof(uint64_t);
+    // shard i's words about peer q's vertices: its segment for q (receiver side of the forward run)
+    auto seg_words = [&](size_t i, int q) {
+        const Shard& sh = *g.shards[i];
+        const Halo& h = g.halo(sh, adj);
+        return bitmaps[i] + (((int64_t)h.seg_of(q, sh.index) << h.tbits) >> 6);
+    };
+    auto nwords = [](int64_t bits) { return (bits + 63) / 64; };
+    if (c.logical) {
+        Shard& s0 = *g.shards[0];
+        DeviceGuard dg(s0.device);
+        for (size_t oi = 0; oi < g.shards.size(); ++oi) {  // the owner of the vertices
+            const Halo& ho = g.halo(*g.shards[oi], adj);
+            const std::vector<int64_t> woff = halo_word_offsets(ho, g.P);
+            for (size_t ri = 0; ri < g.shards.size(); ++ri) {  // the shard that reads them
+                if (ri == oi) continue;
+                const int q = g.shards[oi]->index, r = g.shards[ri]->index;
+                const int64_t n = nwords(ho.send_off[(size_t)r + 1] - ho.send_off[(size_t)r]);
+                if (n == 0) continue;
+                uint64_t* own = sends[oi] + woff[(size_t)r];
+                uint64_t* seg = seg_words(ri, q);
+                JG_HIP(hipMemcpyAsync(reverse ? own : seg, reverse ? seg : own, (size_t)n * W, hipMemcpyDeviceToDevice,
+                                      s0.stream));
+            }
+        }
+        return;
+    }
+    if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
+        Shard& sh = *g.shards[0];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh.device);
+        const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
+        std::vector<int> sp, rp;
+        std::vector<const void*> sv;
+        std::vector<void*> rv;
+        std::vector<size_t> sb, rb;
+        std::vector<std::vector<uint64_t>> out, in;
+        std::vector<uint64_t*> dst;
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t mine = nwords(h.send_off[(size_t)q + 1] - h.send_off[(size_t)q]);  // my vertices q reads
+            const int64_t theirs = nwords(h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q]);  // q's vertices I read
+            const int64_t ns = reverse ? theirs : mine, nr = reverse ? mine : theirs;
+            if (ns > 0) {
+                sp.push_back(q);
+                out.emplace_back((size_t)ns);
+                copy_d2h(out.back().data(), reverse ? seg_words(0, q) : sends[0] + woff[(size_t)q], (size_t)ns * W,
+                         sh.stream);
+                sb.push_back((size_t)ns * W);
+            }
+            if (nr > 0) {
+                rp.push_back(q);
+                in.emplace_back((size_t)nr);
+                rb.push_back((size_t)nr * W);
+                dst.push_back(reverse ? sends[0] + woff[(size_t)q] : seg_words(0, q));
+            }
+        }
+        for (auto& b : out) sv.push_back(b.data());
+        for (auto& b : in) rv.push_back(b.data());
+        host_exchange(c, sp, sv, sb, rp, rv, rb);
+        for (size_t k = 0; k < rp.size(); ++k) copy_h2d(dst[k], rv[k], rb[k], sh.stream);
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh.device);
+        const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t mine = nwords(h.send_off[(size_t)q + 1] - h.send_off[(size_t)q]);
+            const int64_t theirs = nwords(h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q]);
+            uint64_t* own = sends[i] + woff[(size_t)q];
+            uint64_t* seg = seg_words(i, q);
+            if (!reverse) {
+                if (mine > 0) rccl_check(ncclSend(own, (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
+                if (theirs > 0) rccl_check(ncclRecv(seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
+            } else {
+                if (theirs > 0) rccl_check(ncclSend(seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
+                if (mine > 0) rccl_check(ncclRecv(own, (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
+            }
+        }
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void exchange_vec(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
     if (g.P == 1) return;
     if (g.halo(*g.shards[0], adj).on)

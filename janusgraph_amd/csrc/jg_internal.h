@@ -325,6 +325,15 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
 // shard's rbuf is about its own row send_src[j]).
 void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std::vector<void*>& rbufs,
                            size_t elem_bytes, ncclDataType_t type);
+// Bit-packed halo exchange (the sharded DO-BFS frontiers): peer q's run of n bits travels as
+// ceil(n / 64) words.  A shard's send-list bits sit in `sends[i]` at word woff(h, q) for peer q; the
+// receiver's bits about q's vertices sit in its compact bitmap `bitmaps[i]` (one bit per compact-vector
+// position) at its segment for q, which starts on a word (stride 2^tbits, tbits >= 13).  Forward: send
+// lists -> segments; reverse: segments -> the owners' send-list words.
+void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, std::vector<uint64_t*>& bitmaps,
+                        bool reverse);
+// word offsets of the per-peer send-list runs of exchange_halo_bits ([P + 1])
+std::vector<int64_t> halo_word_offsets(const Halo& h, int P);
 // Builds shard sh's halo plan for adjacency `which` (0 IN, 2 BOTH) from the full edge list.
 void build_halo(Graph& g, Shard& sh, const int32_t* src, const int32_t* dst, const int32_t* padded, int64_t m,
                 int which, Halo& h, hipStream_t s);

@@ -1150,42 +1150,89 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
 }
 
 // ---------------- sharded direction-optimising BFS (BOTH adjacency, halo plan) ----------------
-// Each shard owns its rows; dvec is its segmented compact vector of depths (own rows [0, rows), then
-// the peers' vertices its rows touch).  Bottom-up: a forward halo exchange refreshes the peers'
-// depths, then own unvisited rows probe their neighbours for depth == level.  Top-down: own frontier
-// rows claim own neighbours by CAS and stamp remote ones (stamp = level + 1) in their halo segments;
-// the reverse exchange hands the stamps to the owners, which claim them.  One packed counter per
-// shard and level ((vertices << 37) | degree sum), summed over shards and ranks, drives Beamer's
-// direction rule on the host.
+// Each shard owns its rows and their depths (dvec, [rows]).  Column ids of the BOTH CSR are compact:
+// own rows [0, rows), then one segment per peer (its vertices this shard's rows touch).  Frontiers cross
+// shards as bits (exchange_halo_bits: a 14.7 M-vertex halo per shard at RMAT-26, P = 8, is 1.8 MB of
+// words instead of 59 MB of int32 depths, moved every level):
+//  * bottom-up: each owner packs "depth == level" of its send lists into words, the forward exchange
+//    lands them in the readers' compact bitmaps, and own unvisited rows probe own depths and those bits;
+//  * top-down: edge-parallel over the local frontier; own targets are claimed by CAS, remote ones are
+//    stamped with the level (a plain store: same-address CAS or atomicOr would queue at the memory side
+//    behind the hub targets every shard's frontier reaches), the stamps are packed into the compact
+//    bitmap's segment words, and the reverse exchange hands those to the owners, which claim the marked
+//    send-list rows.
+// One packed counter per shard and level ((vertices << 37) | degree sum), summed over shards and ranks,
+// drives Beamer's direction rule on the host.  Appends are wave-staged (WaveApp), as in the one-shard
+// traversal; a block-wide append cost three barriers per 256 rows or words.
 struct SBfsLevel {
     const int64_t* rp;
     const int32_t* col;
     int64_t rows;
-    int32_t* dvec;
-    int32_t* stamp;
+    int32_t* dvec;                  // [rows] own depths
+    int32_t* stamp;                 // [C] top-down: level + 1 on the halo vertices this level reached
+    unsigned long long* hb;         // compact bitmap: halo frontier bits (bottom-up) / remote marks (top-down)
     const int32_t* queue_in;
     const int64_t* qoff_in;   // first frontier edge of each queue entry (edge-parallel top-down)
     int64_t nq, mf;           // local frontier: vertices, entries
     int32_t* queue_out;
     int64_t* qoff_out;
-    const int32_t* rbuf;      // reverse-exchanged stamps, by send-list position
+    unsigned long long* sw;         // send-list words (packed bottom-up bits / received top-down marks)
+    const int64_t* send_off;        // [P + 1] send-list element offsets per peer
+    const int64_t* woff;            // [P + 1] send-list word offsets per peer
+    const int64_t* rwoff;           // [P + 1] receive-run word offsets per peer (segment words, packed)
+    const int64_t* rseg;            // [P] first position of each peer's segment in the compact vector
+    const int64_t* rlen;            // [P] length of each peer's run in this shard's segment
+    int P;
     const int32_t* send_src;  // own row of each send-list position
-    int64_t nrecv;
     unsigned long long* packed;
     int32_t level;
 };
 
+// The per-peer tables of a level (send offsets, word offsets, segment starts and lengths), staged in
+// LDS by every block: a word's peer is a scan over them, and from global memory that scan was up to
+// P dependent loads per word (the pack and apply kernels ran 60-100 us per launch at RMAT-26).
+constexpr int kMaxShardsBfs = 64;
+struct PeerTables {
+    int64_t send_off[kMaxShardsBfs + 1], woff[kMaxShardsBfs + 1], rwoff[kMaxShardsBfs + 1];
+    int64_t rseg[kMaxShardsBfs], rlen[kMaxShardsBfs];
+};
+__device__ __forceinline__ void stage_peer_tables(const SBfsLevel& a, PeerTables& t) {
+    for (int i = threadIdx.x; i <= a.P; i += blockDim.x) {
+        t.send_off[i] = a.send_off[i];
+        t.woff[i] = a.woff[i];
+        t.rwoff[i] = a.rwoff[i];
+        if (i < a.P) {
+            t.rseg[i] = a.rseg[i];
+            t.rlen[i] = a.rlen[i];
+        }
+    }
+    __syncthreads();
+}
+// the peer q with offs[q] <= w < offs[q + 1] (offs in LDS)
+__device__ __forceinline__ int peer_of(const int64_t* offs, int P, int64_t w) {
+    int q = 0;
+    while (q + 1 < P && offs[q + 1] <= w) ++q;
+    return q;
+}
+
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+    const int lo = __shfl((int)(uint32_t)v, src, kWave), hi = __shfl((int)(uint32_t)(v >> 32), src, kWave);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
 // top-down, edge-parallel over the local frontier's entries (as bfs_top_down): own neighbours are
-// claimed by CAS, remote ones stamped in their halo segment
+// claimed by CAS, remote ones stamped
 __global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
-    __shared__ AppendScratch sc;
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
     const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
     const int32_t nd = a.level + 1;
     for (int64_t t = 0; t < tiles; ++t) {
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x + wave_id() * kWave) * kTdEdgesPerThread >= a.mf)
+            break;  // wave-uniform
         const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
         int64_t i = 0, next_bound = 0;
         if (e0 < a.mf) {
@@ -1215,45 +1262,97 @@ __global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
                         take = true;
                         deg = a.rp[u + 1] - a.rp[u];
                     }
-                } else if (a.dvec[u] < 0) {  // halo copy: visited stays visited, so skip those
+                } else {
                     a.stamp[u] = nd;
                 }
             }
-            block_append_frontier(take, u, deg, a.queue_out, a.qoff_out, a.packed, sc);
+            app.append(take, u, deg, a.queue_out, a.qoff_out, a.packed);
         }
     }
+    app.final(a.queue_out, a.qoff_out, a.packed);
 }
 
-// top-down, owner side: claim the own rows the peers stamped this level
-__global__ __launch_bounds__(kBlock) void sbfs_td_apply_kernel(SBfsLevel a) {
-    __shared__ AppendScratch sc;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+// top-down, reader side: this level's stamps of every peer segment into its compact bitmap words (one
+// wave per word)
+__global__ __launch_bounds__(kBlock) void sbfs_pack_marks_kernel(SBfsLevel a) {
+    __shared__ PeerTables pt;
+    stage_peer_tables(a, pt);
+    const int64_t words = pt.rwoff[a.P];
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
     const int32_t nd = a.level + 1;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < a.nrecv; x0 += stride) {  // block-uniform trips
-        const int64_t x = x0 + threadIdx.x;
-        bool take = false;
-        int32_t u = 0;
-        int64_t deg = 0;
-        if (x < a.nrecv && a.rbuf[x] == nd) {
-            u = a.send_src[x];
-            if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
-                take = true;
-                deg = a.rp[u + 1] - a.rp[u];
-            }
-        }
-        block_append_frontier(take, u, deg, a.queue_out, a.qoff_out, a.packed, sc);
+    for (int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w < words; w += nwaves) {
+        const int q = peer_of(pt.rwoff, a.P, w);
+        const int64_t j = (w - pt.rwoff[q]) * 64 + lane_id();
+        const bool bit = j < pt.rlen[q] && a.stamp[pt.rseg[q] + j] == nd;
+        const uint64_t word = __ballot(bit);
+        if (lane_id() == 0) a.hb[(pt.rseg[q] >> 6) + (w - pt.rwoff[q])] = word;
     }
 }
 
-// bottom-up over own rows (the halo segments hold the peers' depths of the previous level)
+// top-down, owner side: lanes load consecutive received words; the wave walks the non-zero ones, lane
+// b claiming the row of the word's bit b
+__global__ __launch_bounds__(kBlock) void sbfs_td_apply_kernel(SBfsLevel a) {
+    __shared__ WaveStage ws;
+    __shared__ PeerTables pt;
+    stage_peer_tables(a, pt);
+    WaveApp app{ws};
+    constexpr int kWpb = kBlock / kWave;
+    const int64_t words = pt.woff[a.P];
+    const int32_t nd = a.level + 1;
+    for (int64_t base = ((int64_t)blockIdx.x * kWpb + wave_id()) * kWave; base < words;
+         base += (int64_t)gridDim.x * kWpb * kWave) {  // wave-uniform
+        const int64_t w = base + lane_id();
+        const unsigned long long mine = w < words ? a.sw[w] : 0ull;
+        uint64_t nz = __ballot(mine != 0ull);
+        while (nz) {  // wave-uniform
+            const int l = __ffsll((unsigned long long)nz) - 1;
+            nz &= nz - 1;
+            const unsigned long long word = shfl_u64(mine, l);
+            bool take = false;
+            int32_t u = 0;
+            int64_t deg = 0;
+            if ((word >> lane_id()) & 1ull) {
+                const int64_t ww = base + l;
+                const int q = peer_of(pt.woff, a.P, ww);
+                // bits past a run's end are never set: x < send_off[q + 1]
+                u = a.send_src[pt.send_off[q] + (ww - pt.woff[q]) * 64 + lane_id()];
+                if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                    take = true;
+                    deg = a.rp[u + 1] - a.rp[u];
+                }
+            }
+            app.append(take, u, deg, a.queue_out, a.qoff_out, a.packed);
+        }
+    }
+    app.final(a.queue_out, a.qoff_out, a.packed);
+}
+
+// bottom-up, owner side before the forward exchange: one wave per send-list word, bit b = the depth of
+// the word's row b is this level's
+__global__ __launch_bounds__(kBlock) void sbfs_pack_bits_kernel(SBfsLevel a) {
+    __shared__ PeerTables pt;
+    stage_peer_tables(a, pt);
+    const int64_t words = pt.woff[a.P];
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+    for (int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w < words; w += nwaves) {
+        const int q = peer_of(pt.woff, a.P, w);
+        const int64_t x = pt.send_off[q] + (w - pt.woff[q]) * 64 + lane_id();
+        const bool bit = x < pt.send_off[q + 1] && a.dvec[a.send_src[x]] == a.level;
+        const uint64_t word = __ballot(bit);
+        if (lane_id() == 0) a.sw[w] = word;
+    }
+}
+
+// bottom-up over own rows: a neighbour is in the frontier if its depth (own) or bit (halo) says so
 __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
-    __shared__ AppendScratch sc;
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
     const int64_t words = (a.rows + 63) / 64;
     constexpr int kWpb = kBlock / kWave;
     const int64_t wstride = (int64_t)gridDim.x * kWpb;
     const int32_t nd = a.level + 1;
-    for (int64_t w0 = (int64_t)blockIdx.x * kWpb; w0 < words; w0 += wstride) {
-        const int64_t v = (w0 + wave_id()) * 64 + lane_id();
+    for (int64_t w = (int64_t)blockIdx.x * kWpb + wave_id(); w < words; w += wstride) {  // wave-uniform
+        const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t deg = 0;
         if (v < a.rows && a.dvec[v] < 0) {
@@ -1263,23 +1362,23 @@ __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
 #pragma unroll
                 for (int k = 0; k < kBuBatch; ++k) u[k] = a.col[j + k < j1 ? j + k : j1 - 1];
 #pragma unroll
-                for (int k = 0; k < kBuBatch; ++k) found |= a.dvec[u[k]] == a.level;
+                for (int k = 0; k < kBuBatch; ++k)
+                    found |= u[k] < a.rows ? a.dvec[u[k]] == a.level : (bool)((a.hb[u[k] >> 6] >> (u[k] & 63)) & 1ull);
             }
             if (found) {
                 a.dvec[v] = nd;
                 deg = j1 - a.rp[v];
             }
         }
-        block_append_frontier(found, (int32_t)v, deg, a.queue_out, a.qoff_out, a.packed, sc);
+        app.append(found, (int32_t)v, deg, a.queue_out, a.qoff_out, a.packed);
     }
+    app.final(a.queue_out, a.qoff_out, a.packed);
 }
 
-__global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t C, int32_t* __restrict__ stamp, int64_t src,
-                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (int64_t)gridDim.x * blockDim.x) {
+__global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t rows, int64_t src, int32_t* __restrict__ queue,
+                                 int64_t* __restrict__ qoff) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x)
         dvec[i] = i == src ? 0 : -1;
-        stamp[i] = 0;
-    }
     if (src >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         queue[0] = (int32_t)src;
         qoff[0] = 0;
@@ -1290,10 +1389,10 @@ __global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t C, int32_t*
 int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth, double* edges_out, float* ms_out) {
     const size_t ns = g.shards.size();
     struct St {
-        DevBuf<int32_t> dvec, stamp, rbuf, queue[2];
-        DevBuf<int64_t> qoff[2];
-        DevBuf<unsigned long long> ctr;
-        int64_t nq = 0, mf = 0;
+        DevBuf<int32_t> dvec, stamp, queue[2];
+        DevBuf<int64_t> qoff[2], send_off, woff, rwoff, rseg, rlen;
+        DevBuf<unsigned long long> ctr, hb, sw;
+        int64_t nq = 0, mf = 0, hb_words = 0, sw_words = 0, rw_words = 0;
     };
     std::vector<St> st(ns);
     int64_t tot[2] = {0, 0};  // entries of all shards, rows of all shards
@@ -1303,17 +1402,40 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         DeviceGuard dg(sh.device);
         const Halo& h = sh.halo_both;
         St& t = st[i];
-        t.dvec.alloc(h.C);
-        t.stamp.alloc(h.C);
-        t.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
+        const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
+        t.hb_words = (h.C + 63) / 64;
+        t.sw_words = woff[(size_t)g.P];
+        // this shard's segments (receive runs): first position, length, packed word offsets
+        std::vector<int64_t> rwoff((size_t)g.P + 1, 0), rseg((size_t)g.P, 0), rlen((size_t)g.P, 0);
+        for (int q = 0; q < g.P; ++q) {
+            rlen[(size_t)q] = q == sh.index ? 0 : h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q];
+            rseg[(size_t)q] = (int64_t)h.seg_of(q, sh.index) << h.tbits;
+            rwoff[(size_t)q + 1] = rwoff[(size_t)q] + (rlen[(size_t)q] + 63) / 64;
+        }
+        t.rw_words = rwoff[(size_t)g.P];
+        t.rwoff.alloc(g.P + 1);
+        t.rseg.alloc(g.P);
+        t.rlen.alloc(g.P);
+        copy_h2d(t.rwoff.get(), rwoff.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
+        copy_h2d(t.rseg.get(), rseg.data(), g.P * sizeof(int64_t), sh.stream);
+        copy_h2d(t.rlen.get(), rlen.data(), g.P * sizeof(int64_t), sh.stream);
+        t.dvec.alloc(std::max<int64_t>(sh.rows, 1));
+        t.stamp.alloc(std::max<int64_t>(h.C, 1));
+        JG_HIP(hipMemsetAsync(t.stamp.get(), 0, (size_t)h.C * sizeof(int32_t), sh.stream));  // no level stamps 0
+        t.hb.alloc(std::max<int64_t>(t.hb_words, 1));
+        t.sw.alloc(std::max<int64_t>(t.sw_words, 1));
+        t.send_off.alloc(g.P + 1);
+        t.woff.alloc(g.P + 1);
+        copy_h2d(t.send_off.get(), h.send_off.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
+        copy_h2d(t.woff.get(), woff.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
         t.queue[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.queue[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.ctr.alloc(1);
         const int64_t src = sh.index == src_shard ? src_local : -1;
-        sbfs_init_kernel<<<grid_for(h.C), kBlock, 0, sh.stream>>>(t.dvec.get(), h.C, t.stamp.get(), src,
-                                                                  t.queue[0].get(), t.qoff[0].get());
+        sbfs_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.dvec.get(), sh.rows, src, t.queue[0].get(),
+                                                                      t.qoff[0].get());
         JG_LAUNCH_CHECK();
         t.nq = src >= 0 ? 1 : 0;
         if (src >= 0) {
@@ -1340,38 +1462,62 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         JG_HIP(hipEventCreate(&t1));
         JG_HIP(hipEventRecord(t0, sh0.stream));
     }
-    std::vector<void*> dv, sv, rv;
+    std::vector<uint64_t*> swv, hbv;
     for (auto& t : st) {
-        dv.push_back(t.dvec.get());
-        sv.push_back(t.stamp.get());
-        rv.push_back(t.rbuf.get());
+        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.get()));
+        hbv.push_back(reinterpret_cast<uint64_t*>(t.hb.get()));
     }
+    auto level_args = [&](size_t i) {
+        Shard& sh = *g.shards[i];
+        St& t = st[i];
+        SBfsLevel a{};
+        a.rp = sh.both.row_ptr.get();
+        a.col = sh.both.col.get();
+        a.rows = sh.rows;
+        a.dvec = t.dvec.get();
+        a.stamp = t.stamp.get();
+        a.hb = t.hb.get();
+        a.queue_in = t.queue[cur].get();
+        a.qoff_in = t.qoff[cur].get();
+        a.nq = t.nq;
+        a.mf = t.mf;
+        a.queue_out = t.queue[cur ^ 1].get();
+        a.qoff_out = t.qoff[cur ^ 1].get();
+        a.sw = t.sw.get();
+        a.send_off = t.send_off.get();
+        a.woff = t.woff.get();
+        a.rwoff = t.rwoff.get();
+        a.rseg = t.rseg.get();
+        a.rlen = t.rlen.get();
+        a.P = g.P;
+        a.send_src = sh.halo_both.send_src.get();
+        a.packed = t.ctr.get();
+        a.level = level;
+        return a;
+    };
+    auto word_grid = [](int64_t words) {  // one wave per word (per 64 words in the apply), no grid-stride cap
+        return (unsigned)std::min<int64_t>(std::max<int64_t>((words + kBlock / kWave - 1) / (kBlock / kWave), 1),
+                                           1 << 20);
+    };
     while (nf > 0 && (max_depth < 0 || level < max_depth)) {
         if (!bu && (double)mf > (double)mu / alpha) bu = true;
         else if (bu && (double)nf < (double)nrows / beta) bu = false;
-        if (bu) exchange_halo(g, JG_ADJ_BOTH, dv, sizeof(int32_t), ncclInt32);  // the peers' depths
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            if (bu && t.sw_words > 0) {  // this level's frontier bits of the send lists (before the forward exchange)
+                sbfs_pack_bits_kernel<<<word_grid(t.sw_words), kBlock, 0, sh.stream>>>(level_args(i));
+                JG_LAUNCH_CHECK();
+            }
+        }
+        if (bu) exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, false);
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh.device);
             St& t = st[i];
             JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
-            SBfsLevel a{};
-            a.rp = sh.both.row_ptr.get();
-            a.col = sh.both.col.get();
-            a.rows = sh.rows;
-            a.dvec = t.dvec.get();
-            a.stamp = t.stamp.get();
-            a.queue_in = t.queue[cur].get();
-            a.qoff_in = t.qoff[cur].get();
-            a.nq = t.nq;
-            a.mf = t.mf;
-            a.queue_out = t.queue[cur ^ 1].get();
-            a.qoff_out = t.qoff[cur ^ 1].get();
-            a.rbuf = t.rbuf.get();
-            a.send_src = sh.halo_both.send_src.get();
-            a.nrecv = sh.halo_both.send_off[g.P];
-            a.packed = t.ctr.get();
-            a.level = level;
+            const SBfsLevel a = level_args(i);
             const unsigned grid = (unsigned)std::min<int64_t>(
                 std::max<int64_t>((((sh.rows + 63) / 64) * kWave + kBlock - 1) / kBlock, 64), tune().bfs_grid);
             if (bu) {
@@ -1384,25 +1530,21 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             JG_LAUNCH_CHECK();
         }
         if (!bu) {
-            exchange_halo_reverse(g, JG_ADJ_BOTH, sv, rv, sizeof(int32_t), ncclInt32);
+            for (size_t i = 0; i < ns; ++i) {  // the stamps of this level into the segment words
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh.device);
+                if (st[i].rw_words > 0) {
+                    sbfs_pack_marks_kernel<<<word_grid(st[i].rw_words), kBlock, 0, sh.stream>>>(level_args(i));
+                    JG_LAUNCH_CHECK();
+                }
+            }
+            exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, true);
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
                 St& t = st[i];
-                SBfsLevel a{};
-                a.rp = sh.both.row_ptr.get();
-                a.rows = sh.rows;
-                a.dvec = t.dvec.get();
-                a.queue_out = t.queue[cur ^ 1].get();
-                a.qoff_out = t.qoff[cur ^ 1].get();
-                a.rbuf = t.rbuf.get();
-                a.send_src = sh.halo_both.send_src.get();
-                a.nrecv = sh.halo_both.send_off[g.P];
-                a.packed = t.ctr.get();
-                a.level = level;
-                if (a.nrecv > 0) {
-                    sbfs_td_apply_kernel<<<(unsigned)std::min<int64_t>((a.nrecv + kBlock - 1) / kBlock, tune().bfs_grid),
-                                           kBlock, 0, sh.stream>>>(a);
+                if (t.sw_words > 0) {
+                    sbfs_td_apply_kernel<<<word_grid((t.sw_words + kWave - 1) / kWave), kBlock, 0, sh.stream>>>(level_args(i));
                     JG_LAUNCH_CHECK();
                 }
             }
@@ -1437,7 +1579,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         JG_HIP(hipEventDestroy(t0));
         JG_HIP(hipEventDestroy(t1));
     }
-    // depths of the own rows: the compact vector's own segment
+    // depths of the own rows
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh.device);
@@ -1469,8 +1611,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
     const bool single = nsrc == 1 && g.P == 1;
-    const bool sharded_do = nsrc == 1 && g.P > 1 && direction == JG_DIR_BOTH && g.shards[0]->halo_both.on &&
-                            tune().sharded_bfs;
+    const bool sharded_do = nsrc == 1 && g.P > 1 && g.P <= kMaxShardsBfs && direction == JG_DIR_BOTH &&
+                            g.shards[0]->halo_both.on && tune().sharded_bfs;
     hipEvent_t t0, t1;
     Shard& sh0 = *g.shards[0];
     DeviceGuard dg0(sh0.device);
