@@ -571,7 +571,7 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "light_runs") {
         jg::tune().light_runs = value != 0;
     } else if (k == "merge_diag") {
-        JG_ARG(value >= 0 && value <= 3, "merge_diag must be in [0, 3]");
+        JG_ARG(value >= 0 && value <= 4, "merge_diag must be in [0, 4]");
         jg::tune().merge_diag = (int)value;
     } else if (k == "merge_temporal") {
         JG_ARG(value >= 0 && value <= 2, "merge_temporal must be 0, 1 (automatic) or 2");

@@ -547,8 +547,9 @@ struct Tune {
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
                                       // (0: 32 bits, 24: at least 24; tests)
     int light_runs = 1;               // build time: light rows of degree 1..7 addressed by degree run (no row_ptr load)
-    int merge_diag = 0;               // diagnostic timing of the merge kernel (wrong results for 1 and 3):
-                                      // 1 staging only, 3 no partial stores (round 2: a second col-sized
+    int merge_diag = 0;               // diagnostic timing of the merge kernel (wrong results for 1, 3, 4):
+                                      // 1 staging only, 3 no partial stores, 4 no cold (non-LDS) gathers
+                                      // (round 2: a second col-sized
                                       // stream cost +28% / +10% in the band 0 / 1 merges at RMAT-26)
 };
 Tune& tune();

@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) vl[u] = lg.hot(loc[u], kMergeEpl * lane + u < n);
 #pragma unroll
-            for (int u = 0; u < kMergeEpl; ++u) vg[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, true);
+            for (int u = 0; u < kMergeEpl; ++u) vg[u] = lg.cold(loc[u], a.diag != 4 && kMergeEpl * lane + u < n, true);
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) v[u] = op.combine(vl[u], vg[u]);
         } else {
