@@ -138,6 +138,30 @@ void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
     JG_HIP(hipStreamSynchronize(sh.stream));
 }
 
+uint64_t allreduce_or_u64(Graph& g, uint64_t v) {
+    Ctx& c = *g.ctx;
+    if (c.nranks == 1) return v;
+    Shard& sh = *g.shards[0];
+    DeviceGuard dg(sh.device);
+    if (c.host_transport) {
+        std::vector<uint64_t> all((size_t)c.nranks);
+        host_allgather(c, &v, all.data(), sizeof v);
+        uint64_t r = 0;
+        for (uint64_t w : all) r |= w;
+        return r;
+    }
+    uint8_t bytes[64];
+    for (int b = 0; b < 64; ++b) bytes[b] = (uint8_t)((v >> b) & 1u);
+    DevBuf<uint8_t> d(64);
+    JG_HIP(hipMemcpyAsync(d.get(), bytes, sizeof bytes, hipMemcpyHostToDevice, sh.stream));
+    rccl_check(ncclAllReduce(d.get(), d.get(), 64, ncclUint8, ncclMax, sh.comm, sh.stream), "ncclAllReduce");
+    JG_HIP(hipMemcpyAsync(bytes, d.get(), sizeof bytes, hipMemcpyDeviceToHost, sh.stream));
+    JG_HIP(hipStreamSynchronize(sh.stream));
+    uint64_t r = 0;
+    for (int b = 0; b < 64; ++b) r |= (uint64_t)(bytes[b] != 0) << b;
+    return r;
+}
+
 bool prof_enabled(const Ctx& c) { return c.profiling; }
 
 static bool env_flag(const char* name) {
@@ -502,7 +526,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "cc_push") {
         jg::tune().cc_push = value != 0;
     } else if (k == "msbfs_td") {
-        jg::tune().msbfs_td = value != 0;
+        JG_ARG(value >= 0 && value <= 2, "msbfs_td must be 0 (off), 1 (one shard and sharded) or 2 (one shard only)");
+        jg::tune().msbfs_td = (int)value;
     } else if (k == "cc_first") {
         JG_ARG(value >= 1 && value <= 64, "cc_first must be in [1, 64]");
         jg::tune().cc_first = (int)value;

@@ -466,6 +466,9 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
 int allreduce_or(Graph& g, int flag);
 // Element-wise sum of vals[0..n) over all ranks, in place (identity in single-process contexts).
 void allreduce_sum_i64(Graph& g, int64_t* vals, int n);
+// bitwise OR of a 64-bit word over the ranks (rank mode; the caller combines its in-process shards):
+// RCCL has no bitwise reduction, so each bit travels as a byte under ncclMax
+uint64_t allreduce_or_u64(Graph& g, uint64_t v);
 
 // Diagnostics from the environment: JG_PULL_SPLIT=1 launches each degree class separately,
 // JG_DEBUG_PLAN=1 prints every pull plan at build time.
@@ -508,7 +511,8 @@ struct Tune {
                                       // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
-    int msbfs_td = 1;                 //         bit-parallel BFS on one shard: top-down levels for small frontiers
+    int msbfs_td = 1;                 //         bit-parallel BFS: top-down levels for small frontiers (1: one shard
+                                      //         and sharded over the BOTH halo, 2: one shard only, 0: off)
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
                                       //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit

@@ -789,11 +789,18 @@ struct MsTd {
     int32_t* touched;
     int64_t* touched_off;  // scratch (block_append_frontier writes edge offsets)
     unsigned long long* tpacked;
+    int tbits;             // sharded (compact BOTH columns): u >> tbits != 0 is a peer's vertex; 31 on one shard
+    // sharded: the halo staging vector (compact positions; zero outside a level) and the list of its
+    // slots this level set first, so they can be cleared without a pass over the whole vector
+    unsigned long long* hstage;
+    int32_t* hlist;
+    int64_t* hlist_off;        // scratch of the appender
+    unsigned long long* hpacked;
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
-    __shared__ WaveStage ws;
-    WaveApp app{ws};
+    __shared__ WaveStage ws, hws;
+    WaveApp app{ws}, happ{hws};
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -814,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) {
             const int64_t e = e0 + k;
-            bool take = false;
+            bool take = false, hfirst = false;
             int32_t u = 0;
             if (e < a.mf) {
                 while (e >= next_bound) {
@@ -823,24 +830,83 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 }
                 const int32_t v = a.queue[i];
                 u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
-                const unsigned long long w = a.F[v] & ~a.visited[u];
-                // a plain read first: a hub neighbour already holding these bits takes no atomic (the
-                // atomics on one word serialise at the memory side); a stale read only costs the atomic
-                if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull;
+                const unsigned long long fv = a.F[v];
+                if ((u >> a.tbits) == 0) {
+                    const unsigned long long w = fv & ~a.visited[u];
+                    // a plain read first: a hub neighbour already holding these bits takes no atomic (the
+                    // atomics on one word serialise at the memory side); a stale read only costs the atomic
+                    if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull;
+                } else if (fv & ~a.hstage[u]) {
+                    // a peer's vertex: its halo slot collects the bits; the reverse exchange takes them to
+                    // the owner, which masks them with its visited bits (msbfs_td_recv_kernel)
+                    hfirst = atomicOr(&a.hstage[u], fv) == 0ull;
+                }
             }
             app.append(take, u, 0, a.touched, a.touched_off, a.tpacked);
+            if (a.hstage) happ.append(hfirst, u, 0, a.hlist, a.hlist_off, a.hpacked);
         }
     }
     app.final(a.touched, a.touched_off, a.tpacked);
+    if (a.hstage) happ.final(a.hlist, a.hlist_off, a.hpacked);
 }
 
-// touched vertex u: its new bits become its next-frontier word (and the visited / depth updates)
+// v[list[i]] = 0 for i < n: clears the words a level set (its frontier rows, or its halo staging slots)
+// without a pass over the whole vector
+__global__ void msbfs_zero_list_kernel(unsigned long long* __restrict__ v, const int32_t* __restrict__ list, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[list[i]] = 0ull;
+}
+
+// Sharded top-down level, owner side: the peers' halo slots for own rows, received at the send-list
+// positions (rbuf[k] is about own row send_src[k]); own rows that gain a bit join the touched list
+// the local top-down kernel started (the first toucher of a word appends it, as there)
+__global__ __launch_bounds__(kBlock) void msbfs_td_recv_kernel(const unsigned long long* __restrict__ rbuf,
+                                                               const int32_t* __restrict__ send_src, int64_t nrecv,
+                                                               const unsigned long long* __restrict__ visited,
+                                                               unsigned long long* __restrict__ Fnext,
+                                                               int32_t* __restrict__ touched,
+                                                               int64_t* __restrict__ touched_off,
+                                                               unsigned long long* __restrict__ tpacked) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    // four words per thread and trip, loaded together (a sparse level's words are mostly zero: the
+    // kernel is a stream of rbuf, latency-bound one word at a time)
+    constexpr int kU = 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * kU;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x * kU; x0 < nrecv; x0 += stride) {  // block-uniform trips
+        unsigned long long r[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            const int64_t k = x0 + (int64_t)j * blockDim.x + threadIdx.x;
+            r[j] = k < nrecv ? rbuf[k] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            const int64_t k = x0 + (int64_t)j * blockDim.x + threadIdx.x;
+            bool take = false;
+            int32_t u = 0;
+            if (r[j]) {
+                u = send_src[k];
+                const unsigned long long w = r[j] & ~visited[u];
+                if (w && (w & ~Fnext[u])) take = atomicOr(&Fnext[u], w) == 0ull;
+            }
+            app.append(take, u, 0, touched, touched_off, tpacked);
+        }
+    }
+    app.final(touched, touched_off, tpacked);
+}
+
+// touched vertex u: its new bits become its next-frontier word (and the visited / depth updates);
+// *live_out |= the OR of the new words (the next pull level's live bits: untouched rows hold zero)
 __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* __restrict__ touched, int64_t nt,
                                                                 MsBfsOp op, const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
-                                                                unsigned long long* __restrict__ packed) {
+                                                                unsigned long long* __restrict__ packed,
+                                                                unsigned long long* __restrict__ live_out) {
     __shared__ WaveStage ws;
+    __shared__ unsigned long long red[kBlock / kWave];
     WaveApp app{ws};
+    unsigned long long lv = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nt; x0 += stride) {  // block-uniform trips
         const int64_t x = x0 + threadIdx.x;
@@ -851,12 +917,24 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
             u = touched[x];
             const unsigned long long acc = op.Fout[u];  // the ORed words (finalize overwrites Fout[u])
             op.finalize(u, acc);
-            take = op.Fout[u] != 0ull;
+            const unsigned long long nw = op.Fout[u];
+            lv |= nw;
+            take = nw != 0ull;
             if (take) deg = push_rp[u + 1] - push_rp[u];
         }
         app.append(take, u, deg, queue, qoff, packed);
     }
     app.final(queue, qoff, packed);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) lv |= __shfl_xor(lv, o, kWave);
+    if (lane_id() == 0) red[wave_id()] = lv;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) lv |= red[w];
+        // a plain read first: once every source is live (most levels) no block takes the atomic, which
+        // serialises at the memory side (one per block was +1.5 ms over a sharded RMAT-26 traversal)
+        if (lv & ~*(volatile unsigned long long*)live_out) atomicOr(live_out, lv);
+    }
 }
 
 // ---------------- weighted shortest distance (frontier Bellman-Ford) ----------------
@@ -1682,7 +1760,30 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
             };
             std::vector<St> st(g.shards.size());
-            std::vector<int64_t> src_rows;
+            const BfsCsrs c0 = pick_csrs(sh0, direction);
+            const uint32_t adj0 = adj_of(sh0, c0);
+            // Levels whose frontier has few edges run top-down: on one shard with a push adjacency, and
+            // on a sharded BOTH traversal over the halo plan (msbfs_td 1; 2 = one shard only).  Sharded,
+            // a shard pushes its own frontier rows; bits for a peer's vertex collect in its halo slot and
+            // go to the owner by the reverse halo exchange (msbfs_td_recv_kernel).
+            const bool td_one = g.shards.size() == 1 && g.P == 1 && c0.push != nullptr && tune().msbfs_td != 0;
+            const bool td_shard = g.P > 1 && direction == JG_DIR_BOTH && sh0.halo_both.on && tune().msbfs_td == 1;
+            const bool td_ok = td_one || td_shard;
+            struct Td {
+                DevBuf<int32_t> queue[2], touched;
+                DevBuf<int64_t> qoff[2], touched_off;
+                DevBuf<unsigned long long> ctr;   // [0] frontier, [1] touched, [2] halo slots set
+                DevBuf<int64_t> srcs;             // the shard's distinct source rows
+                DevBuf<unsigned long long> rbuf;  // sharded: the peers' halo slots for own rows (send-list order)
+                DevBuf<unsigned long long> hs;    // sharded: halo staging (compact positions), zero between levels
+                DevBuf<int32_t> hlist;            // sharded: the staging slots a level set
+                DevBuf<int64_t> hlist_off;        // appender scratch
+                std::vector<int64_t> src_rows;
+                int64_t nq = 0, mf = 0;
+                int64_t nq_in = 0;                // the last top-down level's input frontier (its queue)
+            };
+            std::vector<Td> tds(g.shards.size());
+            int64_t push_nnz = 0;  // entries of the push adjacency, all shards and ranks (the direction rule)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
@@ -1690,7 +1791,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 if (!c.pull) fail(JG_ERR_UNSUPPORTED, "multi-source BFS needs the pull adjacency");
                 const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
                 if (c.pull == &sh.out) fail(JG_ERR_UNSUPPORTED, "multi-source IN traversal is not supported");
-                (void)plan;
+                if (c.push) push_nnz += c.push->nnz;
                 St& t = st[i];
                 const int64_t len = g.vec_len(sh, adj_of(sh, c));
                 t.F[0].alloc(len);
@@ -1730,11 +1831,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     const int64_t l = local_of_vid(g, source_vids[b0 + s], &shard);
                     if (l >= 0 && shard == sh.index) loc[s] = l;
                 }
-                if (i == 0) {  // shard 0's distinct source rows: the first top-down queue (msbfs_source_queue_kernel)
-                    src_rows.clear();
-                    for (int64_t l : loc)
-                        if (l >= 0 && std::find(src_rows.begin(), src_rows.end(), l) == src_rows.end()) src_rows.push_back(l);
-                }
+                // the shard's distinct source rows: its first top-down queue (msbfs_source_queue_kernel)
+                for (int64_t l : loc)
+                    if (l >= 0 && std::find(tds[i].src_rows.begin(), tds[i].src_rows.end(), l) == tds[i].src_rows.end())
+                        tds[i].src_rows.push_back(l);
                 DevBuf<int64_t> dloc(ns);
                 copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
                 msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth8.get(),
@@ -1742,58 +1842,108 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_LAUNCH_CHECK();
                 JG_HIP(hipStreamSynchronize(sh.stream));
             }
-            {
+            allreduce_sum_i64(g, &push_nnz, 1);
+            // need_fwd: the current F's halo segments are stale.  The forward exchange runs lazily, before a
+            // pull level: a top-down level reads own frontier words only (and writes own rows only)
+            bool need_fwd = g.P > 1;
+            if (!td_ok) {
                 std::vector<void*> bufs;
                 for (auto& t : st) bufs.push_back(t.F[0].get());
-                exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
+                exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
+                need_fwd = false;
             }
-            // one shard with a push adjacency: levels whose frontier has few edges run top-down
-            const BfsCsrs c0 = pick_csrs(sh0, direction);
-            const bool td_ok = g.shards.size() == 1 && g.P == 1 && c0.push != nullptr && tune().msbfs_td;
-            struct Td {
-                DevBuf<int32_t> queue[2], touched;
-                DevBuf<int64_t> qoff[2], touched_off;
-                DevBuf<unsigned long long> ctr;  // [0] frontier, [1] touched
-                DevBuf<int64_t> srcs;            // shard 0's distinct source rows
-                int64_t nq = 0, mf = 0;
-                int qc = 0;
-            } td;
+            int cur = 0, level = 0, qc = 0;
+            int64_t g_nq = 0, g_mf = 0;  // the current frontier's vertices and push entries, all shards and ranks
             auto read_frontier = [&]() {
-                unsigned long long h = 0;
-                copy_d2h(&h, td.ctr.get(), sizeof h, sh0.stream);
-                td.nq = (int64_t)(h >> kPackShift);
-                td.mf = (int64_t)(h & kEdgeMask);
+                int64_t v[2] = {0, 0};
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    unsigned long long h = 0;
+                    copy_d2h(&h, tds[i].ctr.get(), sizeof h, sh.stream);
+                    tds[i].nq = (int64_t)(h >> kPackShift);
+                    tds[i].mf = (int64_t)(h & kEdgeMask);
+                    v[0] += tds[i].nq;
+                    v[1] += tds[i].mf;
+                }
+                allreduce_sum_i64(g, v, 2);
+                g_nq = v[0];
+                g_mf = v[1];
             };
-            auto build_frontier = [&](const unsigned long long* F, int qslot) {
-                JG_HIP(hipMemsetAsync(td.ctr.get(), 0, sizeof(unsigned long long), sh0.stream));
-                msbfs_frontier_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
-                    F, sh0.rows, c0.push->row_ptr.get(), td.queue[qslot].get(), td.qoff[qslot].get(), td.ctr.get());
-                JG_LAUNCH_CHECK();
+            // live bits of the next pull level from every shard's own rows (the top-down apply or the scan
+            // after a pull level ORed them into live[0]): OR over the local shards and the ranks, a superset
+            // of what the shard's gathered vector holds, which is all the task skip needs
+            auto combine_live = [&]() {
+                if (g.shards.size() == 1 && ctx.nranks == 1) return;
+                uint64_t v = 0;
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    uint64_t w = 0;
+                    copy_d2h(&w, st[i].live.get(), sizeof w, sh.stream);
+                    v |= w;
+                }
+                v = allreduce_or_u64(g, v);
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    copy_h2d(st[i].live.get(), &v, sizeof v, sh.stream);
+                }
+            };
+            auto build_frontier = [&](int qslot) {
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    const BfsCsrs c = pick_csrs(sh, direction);
+                    JG_HIP(hipMemsetAsync(tds[i].ctr.get(), 0, sizeof(unsigned long long), sh.stream));
+                    msbfs_frontier_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                        st[i].F[cur].get(), sh.rows, c.push->row_ptr.get(), tds[i].queue[qslot].get(),
+                        tds[i].qoff[qslot].get(), tds[i].ctr.get());
+                    JG_LAUNCH_CHECK();
+                }
                 read_frontier();
             };
-            if (td_ok) {  // allocated before the timed region (~2.3 GB at RMAT-26)
-                const size_t r1 = (size_t)std::max<int64_t>(sh0.rows, 1);
-                for (int k = 0; k < 2; ++k) {
-                    td.queue[k].alloc(r1);
-                    td.qoff[k].alloc(r1);
+            if (td_ok) {  // allocated before the timed region (~2.3 GB at RMAT-26 on one shard)
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    Td& td = tds[i];
+                    const size_t r1 = (size_t)std::max<int64_t>(sh.rows, 1);
+                    for (int k = 0; k < 2; ++k) {
+                        td.queue[k].alloc(r1);
+                        td.qoff[k].alloc(r1);
+                    }
+                    td.touched.alloc(r1);
+                    td.touched_off.alloc(r1);
+                    td.ctr.alloc(3);
+                    td.srcs.alloc(std::max<size_t>(td.src_rows.size(), 1));
+                    if (!td.src_rows.empty())
+                        copy_h2d(td.srcs.get(), td.src_rows.data(), td.src_rows.size() * sizeof(int64_t), sh.stream);
+                    if (td_shard) {
+                        const Halo& h = sh.halo_both;
+                        td.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
+                        td.hs.alloc(g.vec_len(sh, JG_ADJ_BOTH));
+                        JG_HIP(hipMemsetAsync(td.hs.get(), 0, td.hs.bytes(), sh.stream));
+                        td.hlist.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
+                        td.hlist_off.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
+                    }
                 }
-                td.touched.alloc(r1);
-                td.touched_off.alloc(r1);
-                td.ctr.alloc(2);
-                td.srcs.alloc(std::max<size_t>(src_rows.size(), 1));
-                if (!src_rows.empty())
-                    copy_h2d(td.srcs.get(), src_rows.data(), src_rows.size() * sizeof(int64_t), sh0.stream);
             }
             JG_HIP(hipEventRecord(t0, sh0.stream));
             if (td_ok) {  // the level-0 frontier is the source rows: queued directly, no scan of F
-                msbfs_source_queue_kernel<<<1, 1, 0, sh0.stream>>>(td.srcs.get(), (int)src_rows.size(),
-                                                                   c0.push->row_ptr.get(), td.queue[0].get(),
-                                                                   td.qoff[0].get(), td.ctr.get());
-                JG_LAUNCH_CHECK();
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    DeviceGuard dg(sh.device);
+                    const BfsCsrs c = pick_csrs(sh, direction);
+                    msbfs_source_queue_kernel<<<1, 1, 0, sh.stream>>>(tds[i].srcs.get(), (int)tds[i].src_rows.size(),
+                                                                       c.push->row_ptr.get(), tds[i].queue[0].get(),
+                                                                       tds[i].qoff[0].get(), tds[i].ctr.get());
+                    JG_LAUNCH_CHECK();
+                }
                 read_frontier();
             }
-            // queued: td.queue[td.qc] holds the current frontier; live_ready: st[0].live[0] holds its live
-            // bits (both from the previous level's end)
+            // queued: tds[i].queue[qc] holds the current frontier; live_ready: live[0] holds its live bits
+            // (both from the previous level's end)
             // byte depth planes hold levels 0..254: a traversal about to write level 255 widens them first
             auto widen = [&]() {
                 for (size_t i = 0; i < g.shards.size(); ++i) {
@@ -1812,7 +1962,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // one shard: pull levels whose frontier holds at least msbfs_bu_frac / 1000 of the rows run
             // bottom-up with early exit (msbfs_bu_kernel) instead of through the merge engine
             MsBu bu{};
-            const bool bu_ok = td_ok && c0.pull == c0.push && tune().msbfs_bu > 0;
+            const bool bu_ok = td_one && c0.pull == c0.push && tune().msbfs_bu > 0;
             if (bu_ok) {
                 DevBuf<int64_t> bnd(2);
                 degree_bound_kernel<<<1, 1, 0, sh0.stream>>>(c0.pull->row_ptr.get(), sh0.rows, 4096, bnd.get());
@@ -1833,44 +1983,129 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             const int64_t bu_rows = bu_ok ? sh0.rows * (int64_t)tune().msbfs_bu_frac / 1000 : 0;
             int bu_levels = 0;
             bool queued = td_ok, live_ready = false;
-            int cur = 0, level = 0;
+            bool prev_td = false;  // the previous level ran top-down: F[cur ^ 1]'s nonzero own words are
+                                   // exactly its input queue (tds[i].queue[qc ^ 1][0, nq_in))
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
             // counted on the device, or every task when the skip is off) and top-down frontier entries
             int pull_levels = 0;
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
                 if (level + 1 >= 255) widen();
-                const bool td_level =
-                    td_ok && (double)td.mf < (double)c0.push->nnz / (double)tune().bfs_alpha;
+                const bool td_level = td_ok && (double)g_mf < (double)push_nnz / (double)tune().bfs_alpha;
                 if (td_level && !queued) {
-                    build_frontier(st[0].F[cur].get(), td.qc ^ 1);
-                    td.qc ^= 1;
+                    build_frontier(qc ^ 1);
+                    qc ^= 1;
                 }
                 const bool have_live = live_ready;
                 queued = live_ready = false;
                 bool level_bu = false;  // this pull level ran msbfs_bu_kernel
                 if (td_level) {
-                    Shard& sh = sh0;
-                    St& t = st[0];
-                    JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
-                    JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, t.F[cur ^ 1].bytes(), sh.stream));
-                    JG_HIP(hipMemsetAsync(td.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
-                    if (td.mf > 0) {
-                        MsTd a{td.queue[td.qc].get(), td.qoff[td.qc].get(), td.nq, td.mf, c0.push->row_ptr.get(),
-                               c0.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
-                               td.touched_off.get(), td.ctr.get() + 1};
-                        msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
-                                              (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
-                                          kBlock, 0, sh.stream>>>(a);
-                        JG_LAUNCH_CHECK();
+                    std::vector<void*> fv, rv;
+                    for (size_t i = 0; i < g.shards.size(); ++i) {
+                        Shard& sh = *g.shards[i];
+                        DeviceGuard dg(sh.device);
+                        const BfsCsrs c = pick_csrs(sh, direction);
+                        St& t = st[i];
+                        Td& td = tds[i];
+                        JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
+                        // the output's own words start at zero (the first toucher of a word queues it): after a
+                        // top-down level only its input queue's words are set, otherwise clear every own row
+                        if (prev_td) {
+                            if (td.nq_in > 0) {
+                                msbfs_zero_list_kernel<<<grid_for(td.nq_in), kBlock, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), td.queue[qc ^ 1].get(), td.nq_in);
+                                JG_LAUNCH_CHECK();
+                            }
+                        } else {
+                            JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, (size_t)sh.rows * sizeof(unsigned long long),
+                                                  sh.stream));
+                        }
+                        JG_HIP(hipMemsetAsync(td.ctr.get(), 0, 3 * sizeof(unsigned long long), sh.stream));
+                        JG_HIP(hipMemsetAsync(t.live.get(), 0, sizeof(unsigned long long), sh.stream));
+                        td.nq_in = td.nq;
+                        if (td.mf > 0) {
+                            MsTd a{td.queue[qc].get(), td.qoff[qc].get(), td.nq, td.mf, c.push->row_ptr.get(),
+                                   c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
+                                   td.touched_off.get(), td.ctr.get() + 1, td_shard ? sh.halo_both.tbits : 31,
+                                   td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2};
+                            msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
+                                                  (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
+                                              kBlock, 0, sh.stream>>>(a);
+                            JG_LAUNCH_CHECK();
+                        }
+                        fv.push_back(td.hs.get());
+                        rv.push_back(td.rbuf.get());
                     }
-                    unsigned long long th = 0;
-                    copy_d2h(&th, td.ctr.get() + 1, sizeof th, sh.stream);
-                    const int64_t nt = (int64_t)(th >> kPackShift);
-                    td_entries += (double)td.mf;
-                    td_touched += (double)nt;
-                    td_queued += (double)td.nq;
-                    if (nt > 0) {
+                    if (td_shard) {
+                        exchange_halo_reverse(g, JG_ADJ_BOTH, fv, rv, sizeof(unsigned long long), ncclUint64);
+                        for (size_t i = 0; i < g.shards.size(); ++i) {
+                            Shard& sh = *g.shards[i];
+                            DeviceGuard dg(sh.device);
+                            const int64_t nrecv = sh.halo_both.send_off[g.P];
+                            if (nrecv > 0) {
+                                msbfs_td_recv_kernel<<<grid_for(nrecv, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
+                                    tds[i].rbuf.get(), sh.halo_both.send_src.get(), nrecv, st[i].vis.get(),
+                                    st[i].F[cur ^ 1].get(), tds[i].touched.get(), tds[i].touched_off.get(),
+                                    tds[i].ctr.get() + 1);
+                                JG_LAUNCH_CHECK();
+                            }
+                        }
+                    }
+                    for (size_t i = 0; i < g.shards.size(); ++i) {
+                        Shard& sh = *g.shards[i];
+                        DeviceGuard dg(sh.device);
+                        const BfsCsrs c = pick_csrs(sh, direction);
+                        St& t = st[i];
+                        Td& td = tds[i];
+                        unsigned long long th[2] = {0, 0};
+                        copy_d2h(th, td.ctr.get() + 1, sizeof th, sh.stream);
+                        const int64_t nt = (int64_t)(th[0] >> kPackShift), nh = (int64_t)(th[1] >> kPackShift);
+                        if (nh > 0) {  // the staging slots went out with the reverse exchange: back to zero
+                            msbfs_zero_list_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(td.hs.get(), td.hlist.get(), nh);
+                            JG_LAUNCH_CHECK();
+                        }
+                        td_entries += (double)td.mf;
+                        td_touched += (double)nt;
+                        td_queued += (double)td.nq;
+                        if (nt > 0) {
+                            MsBfsOp op;
+                            op.F = t.F[cur].get();
+                            op.Fout = t.F[cur ^ 1].get();
+                            op.visited = t.vis.get();
+                            op.depth = t.depth.get();
+                            op.depth8 = t.depth8.get();
+                            op.changed = t.changed.get();
+                            op.rows = sh.rows;
+                            op.pos = g.vec_pos(sh, adj_of(sh, c));
+                            op.lvl = level + 1;
+                            op.live = t.live.get() + 1;
+                            msbfs_td_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(
+                                td.touched.get(), nt, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
+                                td.qoff[qc ^ 1].get(), td.ctr.get(), t.live.get());
+                            JG_LAUNCH_CHECK();
+                        }
+                    }
+                    read_frontier();
+                    combine_live();
+                    qc ^= 1;
+                    queued = live_ready = true;
+                    need_fwd = td_shard;
+                    prev_td = true;
+                } else {
+                    prev_td = false;
+                    if (need_fwd) {  // stale halo segments: the lazy forward exchange
+                        std::vector<void*> bufs;
+                        for (auto& t : st) bufs.push_back(t.F[cur].get());
+                        exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
+                        need_fwd = false;
+                    }
+                    for (size_t i = 0; i < g.shards.size(); ++i) {
+                        Shard& sh = *g.shards[i];
+                        DeviceGuard dg(sh.device);
+                        const BfsCsrs c = pick_csrs(sh, direction);
+                        const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
+                        St& t = st[i];
+                        JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
                         MsBfsOp op;
                         op.F = t.F[cur].get();
                         op.Fout = t.F[cur ^ 1].get();
@@ -1879,90 +2114,63 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.depth8 = t.depth8.get();
                         op.changed = t.changed.get();
                         op.rows = sh.rows;
-                        op.pos = g.vec_pos(sh, adj_of(sh, c0));
+                        op.pos = g.vec_pos(sh, adj_of(sh, c));
                         op.lvl = level + 1;
-                        op.live = t.live.get() + 1;
-                        msbfs_td_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(
-                            td.touched.get(), nt, op, c0.push->row_ptr.get(), td.queue[td.qc ^ 1].get(),
-                            td.qoff[td.qc ^ 1].get(), td.ctr.get());
-                        JG_LAUNCH_CHECK();
-                    }
-                    read_frontier();
-                    td.qc ^= 1;
-                    queued = true;
-                } else
-                for (size_t i = 0; i < g.shards.size(); ++i) {
-                    Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
-                    const BfsCsrs c = pick_csrs(sh, direction);
-                    const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
-                    St& t = st[i];
-                    JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
-                    MsBfsOp op;
-                    op.F = t.F[cur].get();
-                    op.Fout = t.F[cur ^ 1].get();
-                    op.visited = t.vis.get();
-                    op.depth = t.depth.get();
-                    op.depth8 = t.depth8.get();
-                    op.changed = t.changed.get();
-                    op.rows = sh.rows;
-                    op.pos = g.vec_pos(sh, adj_of(sh, c));
-                    op.lvl = level + 1;
-                    // Live bits: the sources present in some word of this level's gathered vector.  A row
-                    // none of whose unvisited bits is live gains nothing, so the light rows skip it
-                    // (MsBfsOp::active) and the split skips every merge task whose rows are all such
-                    // (their partials are then stale, and finalize's live mask discards them).  At
-                    // RMAT-26 the last pull level has ~all rows done and the one before ~40% of band 0.
-                    unsigned long long* lw = t.live.get();
-                    if (!have_live) {
-                        const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
-                        JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
-                        msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
-                        JG_LAUNCH_CHECK();
-                    }
-                    op.live = lw;
-                    if (bu_ok && (tune().msbfs_bu == 1 || td.nq >= bu_rows)) {
-                        const int64_t light = sh.rows - bu.wave;
-                        const unsigned grid = (unsigned)(bu.blocks_wave +
-                                                         std::max<int64_t>(std::min<int64_t>((light + kMergeThreads - 1) / kMergeThreads, 4096), 1));
-                        msbfs_bu_kernel<<<grid, kMergeThreads, 0, sh.stream>>>(bu, op);
-                        JG_LAUNCH_CHECK();
-                        level_bu = true;
-                    } else {
-                    std::vector<const uint32_t*> tl;
-                    for (size_t b = 0; b < t.todo.size(); ++b) {
-                        const SliceBand& bd = *plan.bands[b];
-                        if (bd.tasks == 0 || bd.rows() == 0) {
-                            tl.push_back(nullptr);
-                            continue;
+                        // Live bits: the sources present in some word of this level's gathered vector.  A row
+                        // none of whose unvisited bits is live gains nothing, so the light rows skip it
+                        // (MsBfsOp::active) and the split skips every merge task whose rows are all such
+                        // (their partials are then stale, and finalize's live mask discards them).  At
+                        // RMAT-26 the last pull level has ~all rows done and the one before ~40% of band 0.
+                        unsigned long long* lw = t.live.get();
+                        if (!have_live) {
+                            const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
+                            JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
+                            msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
+                            JG_LAUNCH_CHECK();
                         }
-                        msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
-                            t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
-                        JG_LAUNCH_CHECK();
-                        msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
-                            bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
-                        JG_LAUNCH_CHECK();
-                        tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                        op.live = lw;
+                        if (bu_ok && (tune().msbfs_bu == 1 || g_nq >= bu_rows)) {
+                            const int64_t light = sh.rows - bu.wave;
+                            const unsigned grid = (unsigned)(bu.blocks_wave +
+                                                             std::max<int64_t>(std::min<int64_t>((light + kMergeThreads - 1) / kMergeThreads, 4096), 1));
+                            msbfs_bu_kernel<<<grid, kMergeThreads, 0, sh.stream>>>(bu, op);
+                            JG_LAUNCH_CHECK();
+                            level_bu = true;
+                        } else {
+                        std::vector<const uint32_t*> tl;
+                        for (size_t b = 0; b < t.todo.size(); ++b) {
+                            const SliceBand& bd = *plan.bands[b];
+                            if (bd.tasks == 0 || bd.rows() == 0) {
+                                tl.push_back(nullptr);
+                                continue;
+                            }
+                            msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
+                                t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
+                            JG_LAUNCH_CHECK();
+                            msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
+                                bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
+                            JG_LAUNCH_CHECK();
+                            tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                        }
+                        launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
+                                    t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
+                                    tl.empty() ? nullptr : tl.data());
+                        }
+                        if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
+                            JG_HIP(hipMemsetAsync(tds[i].ctr.get(), 0, sizeof(unsigned long long), sh.stream));
+                            JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
+                            msbfs_scan_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), lw, tds[i].ctr.get());
+                            JG_LAUNCH_CHECK();
+                        }
                     }
-                    launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
-                                tl.empty() ? nullptr : tl.data());
-                    }
-                    if (td_ok) {  // the next level's live bits and frontier counter (its direction)
-                        JG_HIP(hipMemsetAsync(td.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
-                        JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
-                        msbfs_scan_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                            t.F[cur ^ 1].get(), sh.rows, c0.push->row_ptr.get(), lw, td.ctr.get());
-                        JG_LAUNCH_CHECK();
+                    if (td_ok) {
                         read_frontier();
+                        combine_live();
                         live_ready = true;
                     }
-                }
-                if (!td_level) {
                     ++(level_bu ? bu_levels : pull_levels);
-                    std::vector<void*> bufs;
-                    for (auto& t : st) bufs.push_back(t.F[cur ^ 1].get());
-                    exchange_vec(g, adj_of(sh0, pick_csrs(sh0, direction)), bufs, sizeof(unsigned long long), ncclUint64);
+                    need_fwd = g.P > 1;
                 }
                 int32_t any = 0;
                 for (size_t i = 0; i < g.shards.size(); ++i) {

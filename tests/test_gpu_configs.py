@@ -164,8 +164,8 @@ def test_config3_sharded_cc_and_dobfs_rmat26(oracle_lib, rmat26, shards):
 
 
 def test_config4_msbfs64_rmat26(oracle_lib, rmat26):
-    """8 logical shards (every level pulls through the sharded split) and one shard (top-down levels
-    for small frontiers, split pull levels between them)."""
+    """8 logical shards and one shard: top-down levels for small frontiers (sharded: own frontier rows
+    pushed, the peers' bits returned by the reverse halo exchange), split pull levels between them."""
     import janusgraph_amd as jg
     o = oracle_lib
     r = rmat26

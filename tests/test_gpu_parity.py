@@ -221,19 +221,22 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
 
 
 @pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
-                                         ("skip_wide", 1), ("skip", 3), ("skip_dense", 2)])
+                                         ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
+                                         ("skip_dense", 2)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
     isolated vertex and a vertex of a small component (their bits never reach the rest, so no row ever
-    holds every source), on one shard and on logical shards (halo and dense vectors)."""
+    holds every source), on one shard and on logical shards (halo and dense vectors).  On sharded halo
+    plans the small-frontier levels run top-down (own rows pushed, peers' bits returned by the reverse
+    halo exchange); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2)."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
              "skip_bands3": [("band0_deg", 64), ("band0_bit", 8), ("band1_deg", 16), ("band1_bit", 5),
                              ("band2_deg", 4), ("band2_bit", 3)],
              "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
-             "skip_dense": [("halo", 0)]}[mode]
+             "skip_dense": [("halo", 0)], "skip_sharded_pull_only": [("msbfs_td", 2)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
     vid = np.concatenate([vid0, (np.arange(3, dtype=np.int64) + n0 + 1) << 8 | 7])
@@ -249,6 +252,10 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         depth = g.bfs(vid[srcs], 3)
         for k in range(len(srcs)):
             np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3), err_msg=f"source {k}")
+        bounded = g.bfs(vid[srcs[:5]], 3, 3)
+        for k in range(5):
+            np.testing.assert_array_equal(bounded[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 3, 3),
+                                          err_msg=f"source {k}, max_depth 3")
         g.close()
         c.close()
     finally:

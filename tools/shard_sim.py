@@ -108,8 +108,12 @@ def main():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--halo", type=int, nargs="+", default=[1, 0], help="halo settings tried for P > 1 (pr)")
+    p.add_argument("--tune", nargs="*", default=[], help="jg_tune_set knobs key=value applied first")
     a = p.parse_args()
     import janusgraph_amd as jg
+    for kv in a.tune:
+        k, v = kv.split("=")
+        jg._lib.tune_set(k, int(v))
     if a.program != "pr":
         for P in a.shards:
             print(json.dumps(run_both(jg, a.program, a.scale, P, a.reps)), flush=True)
