@@ -9,6 +9,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <map>
+#include <mutex>
 
 #include "jg_internal.h"
 
@@ -136,6 +138,140 @@ void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
     rccl_check(ncclAllReduce(d.get(), d.get(), (size_t)n, ncclInt64, ncclSum, sh.comm, sh.stream), "ncclAllReduce");
     JG_HIP(hipMemcpyAsync(vals, d.get(), n * sizeof(int64_t), hipMemcpyDeviceToHost, sh.stream));
     JG_HIP(hipStreamSynchronize(sh.stream));
+}
+
+// ---- the caching device allocator behind DevBuf (jg_common.h) ----
+namespace {
+constexpr size_t kCacheBlockMax = 1ull << 30;  // larger blocks go straight to hipMalloc / hipFree
+constexpr size_t kCacheBytesMax = 16ull << 30; // per device: beyond it, synchronise and free half
+struct DevCache {
+    std::multimap<size_t, void*> ready;           // synchronised since their free: reusable
+    std::vector<std::pair<size_t, void*>> pending; // freed since the device's last synchronisation
+    size_t bytes = 0;                              // ready + pending
+};
+// never destroyed: a DevBuf released during process exit (after static destructors) still finds them
+std::mutex& g_cache_mu = *new std::mutex;
+std::map<int, DevCache>& g_cache = *new std::map<int, DevCache>;
+bool cache_off() {
+    static const bool off = std::getenv("JG_NO_DEVCACHE") != nullptr;
+    return off;
+}
+// size class: at most 1/8 above the request (granularity = a power of two >= 4 KiB, 1/8 of the
+// request's leading power of two)
+size_t cache_round(size_t b) {
+    size_t top = 1;
+    while (top * 2 <= b) top *= 2;
+    const size_t g = std::max<size_t>(4096, top / 8);
+    return (b + g - 1) / g * g;
+}
+void free_on(int dev, void* p) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    (void)hipFree(p);
+    if (cur != dev) (void)hipSetDevice(cur);
+}
+// synchronise dev and move the pending blocks taken before the synchronisation to ready; with `trim`,
+// free ready blocks until the cache holds at most half its cap
+void cache_sync_dev(int dev, bool trim) {
+    std::vector<std::pair<size_t, void*>> snap;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        snap.swap(g_cache[dev].pending);
+    }
+    if (snap.empty() && !trim) return;
+    {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        (void)hipDeviceSynchronize();
+        if (cur != dev) (void)hipSetDevice(cur);
+    }
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        DevCache& c = g_cache[dev];
+        for (auto& b : snap) c.ready.emplace(b.first, b.second);
+        while (trim && c.bytes > kCacheBytesMax / 2 && !c.ready.empty()) {
+            auto it = std::prev(c.ready.end());  // the largest first
+            c.bytes -= it->first;
+            drop.push_back(it->second);
+            c.ready.erase(it);
+        }
+    }
+    for (void* p : drop) free_on(dev, p);
+}
+}  // namespace
+
+void* dev_alloc(size_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const bool cached = !cache_off() && bytes <= kCacheBlockMax;
+    const size_t rb = cached ? cache_round(bytes) : bytes;
+    if (cached) {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        DevCache& c = g_cache[dev];
+        auto it = c.ready.find(rb);
+        if (it != c.ready.end()) {
+            void* p = it->second;
+            c.ready.erase(it);
+            c.bytes -= rb;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, rb) != hipSuccess) {
+        (void)hipGetLastError();
+        dev_cache_release(dev);  // hand the cached blocks back, then try once more
+        p = nullptr;
+        if (hipMalloc(&p, rb) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    return p;
+}
+
+void dev_free(void* p, size_t bytes, int dev) {
+    if (!p) return;
+    if (cache_off() || bytes > kCacheBlockMax) {
+        free_on(dev, p);
+        return;
+    }
+    bool over = false;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        DevCache& c = g_cache[dev];
+        const size_t rb = cache_round(bytes);
+        c.pending.emplace_back(rb, p);
+        c.bytes += rb;
+        over = c.bytes > kCacheBytesMax;
+    }
+    if (over) cache_sync_dev(dev, true);
+}
+
+void dev_cache_sync() {
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        for (auto& kv : g_cache)
+            if (!kv.second.pending.empty()) devs.push_back(kv.first);
+    }
+    for (int d : devs) cache_sync_dev(d, false);
+}
+
+void dev_cache_release(int dev) {
+    cache_sync_dev(dev, false);
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        DevCache& c = g_cache[dev];
+        for (auto& kv : c.ready) drop.push_back(kv.second);
+        c.ready.clear();
+        c.bytes = 0;
+        for (auto& b : c.pending) c.bytes += b.first;
+    }
+    for (void* p : drop) free_on(dev, p);
 }
 
 uint64_t allreduce_or_u64(Graph& g, uint64_t v) {
@@ -444,6 +580,7 @@ using jg::Error;
 
 #define JG_GUARD_BEGIN try {
 #define JG_GUARD_END                                       \
+    jg::dev_cache_sync();                                  \
     return JG_OK;                                          \
     }                                                      \
     catch (const Error& e) {                               \
@@ -715,6 +852,8 @@ int jg_ctx_destroy(jg_ctx* ctx) {
         jg::DeviceGuard dg(c.devices[i]);
         (void)hipStreamDestroy(c.streams[i]);
     }
+    for (size_t i = 0; i < c.devices.size(); ++i)  // the cached device memory goes back with the context
+        if (!(c.logical && i > 0)) jg::dev_cache_release(c.devices[i]);
     delete ctx;
     JG_GUARD_END
 }

@@ -28,7 +28,19 @@ void hip_check(hipError_t e, const char* what, const char* file, int line);
 #define JG_HIP(call) ::jg::hip_check((call), #call, __FILE__, __LINE__)
 #define JG_LAUNCH_CHECK() ::jg::hip_check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)
 
-// Owning device allocation (hipMalloc on the current device).
+// Device memory behind DevBuf (jg_api.cpp).  hipFree synchronises the whole device, and a snapshot
+// build frees ~240 temporaries (RMAT-20: 9.6 ms of a 49 ms build went to hipFree), so freed blocks of
+// up to 1 GiB are kept per device and size class instead.  A freed block is "pending" until the
+// device has been synchronised once after its free (dev_cache_sync: at the end of every entry point
+// that left blocks pending); only synchronised blocks are handed out again, so a block is never reused
+// while work queued before its free may still touch it (what hipFree guaranteed per call).
+// JG_NO_DEVCACHE=1 in the environment restores plain hipMalloc / hipFree.
+void* dev_alloc(size_t bytes);                 // current device; nullptr when the device is out of memory
+void dev_free(void* p, size_t bytes, int dev);
+void dev_cache_sync();                          // pending blocks of every device become reusable
+void dev_cache_release(int dev);                // synchronise and return every cached block of dev
+
+// Owning device allocation (dev_alloc on the current device).
 template <typename T>
 class DevBuf {
    public:
@@ -47,23 +59,15 @@ class DevBuf {
         n_ = n;
         JG_HIP(hipGetDevice(&dev_));
         if (n) {
-            hipError_t e = hipMalloc(reinterpret_cast<void**>(&p_), n * sizeof(T));
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                p_ = nullptr;
+            p_ = static_cast<T*>(dev_alloc(n * sizeof(T)));
+            if (!p_) {
                 n_ = 0;
                 fail(-2, "device allocation of " + std::to_string(n * sizeof(T)) + " bytes failed");
             }
         }
     }
     void reset() {
-        if (p_) {
-            int cur = 0;
-            (void)hipGetDevice(&cur);
-            if (cur != dev_) (void)hipSetDevice(dev_);
-            (void)hipFree(p_);
-            if (cur != dev_) (void)hipSetDevice(cur);
-        }
+        if (p_) dev_free(p_, n_ * sizeof(T), dev_);
         p_ = nullptr;
         n_ = 0;
     }
