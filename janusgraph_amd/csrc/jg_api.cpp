@@ -35,12 +35,6 @@ void hip_check(hipError_t e, const char* what, const char* file, int line) {
     }
 }
 
-int64_t Graph::dense_of_vid(int64_t v) const {
-    if (sorted_vid.empty()) return (v >= 0 && v < n) ? v : -1;
-    auto it = std::lower_bound(sorted_vid.begin(), sorted_vid.end(), v);
-    if (it == sorted_vid.end() || *it != v) return -1;
-    return sorted_dense[(size_t)(it - sorted_vid.begin())];
-}
 
 void transport_check(int rc, const char* what) {
     if (rc != 0) fail(JG_ERR_RCCL, std::string("host transport ") + what + " failed (" + std::to_string(rc) + ")");
@@ -171,21 +165,26 @@ void free_on(int dev, void* p) {
     (void)hipFree(p);
     if (cur != dev) (void)hipSetDevice(cur);
 }
-// synchronise dev and move the pending blocks taken before the synchronisation to ready; with `trim`,
-// free ready blocks until the cache holds at most half its cap
+// synchronise every device that holds cached memory (a block of one device may be read by another's
+// peer copy) and move dev's pending blocks taken before the synchronisation to ready; with `trim`, free
+// ready blocks until the cache holds at most half its cap
 void cache_sync_dev(int dev, bool trim) {
     std::vector<std::pair<size_t, void*>> snap;
+    std::vector<int> devs;
     {
         std::lock_guard<std::mutex> lk(g_cache_mu);
         snap.swap(g_cache[dev].pending);
+        for (auto& kv : g_cache) devs.push_back(kv.first);
     }
     if (snap.empty() && !trim) return;
     {
         int cur = 0;
         (void)hipGetDevice(&cur);
-        if (cur != dev) (void)hipSetDevice(dev);
-        (void)hipDeviceSynchronize();
-        if (cur != dev) (void)hipSetDevice(cur);
+        for (int d : devs) {
+            (void)hipSetDevice(d);
+            (void)hipDeviceSynchronize();
+        }
+        (void)hipSetDevice(cur);
     }
     std::vector<void*> drop;
     {
@@ -397,21 +396,9 @@ void prof_collect(Ctx& c, Graph& g) {
     c.last.kernel_launches += launches;
 }
 
-// Host copies of the vertex ids: outputs are indexed like vid[], lookups go through the sorted copy.
-static void set_vertex_ids(Graph& g, const int64_t* vid, int64_t n) {
-    g.vid.assign(vid, vid + n);
-    std::vector<std::pair<int64_t, int64_t>> t(n);
-    for (int64_t i = 0; i < n; ++i) t[i] = {vid[i], i};
-    std::sort(t.begin(), t.end());
-    for (int64_t i = 1; i < n; ++i)
-        if (t[i].first == t[i - 1].first) fail(JG_ERR_ARG, "duplicate vertex id in vid[]");
-    g.sorted_vid.resize(n);
-    g.sorted_dense.resize(n);
-    for (int64_t i = 0; i < n; ++i) {
-        g.sorted_vid[i] = t[i].first;
-        g.sorted_dense[i] = t[i].second;
-    }
-}
+// Host copy of the vertex ids: outputs are indexed like vid[] (vid -> dense lookups and the duplicate
+// check go through the device table the id remap builds: dense_of_vids).
+static void set_vertex_ids(Graph& g, const int64_t* vid, int64_t n) { g.vid.assign(vid, vid + n); }
 
 static void make_shards(Ctx& c, Graph& g) {
     g.P = c.total_shards();
@@ -483,7 +470,12 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
         }
         ds[i].alloc(std::max<int64_t>(m, 1));
         dd[i].alloc(std::max<int64_t>(m, 1));
-        remap_ids_device(v, n, a, b, m, ds[i].get(), dd[i].get(), sh.stream);
+        // shard 0's vid table stays with the graph (vid -> dense lookups) and serves every shard on its
+        // device; shards on other devices build a temporary one
+        if (i == 0) g.id_dev = sh.device;
+        DevBuf<IdSlot> tmp_table;
+        DevBuf<IdSlot>& table = sh.device == g.id_dev ? g.id_table : tmp_table;
+        remap_ids_device(v, n, a, b, m, ds[i].get(), dd[i].get(), sh.stream, &table);
         e.src.push_back(ds[i].get());
         e.dst.push_back(dd[i].get());
         if (cap) {
@@ -509,7 +501,7 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
                 }
                 dis[i].alloc(std::max<int64_t>(mi, 1));
                 did[i].alloc(std::max<int64_t>(mi, 1));
-                remap_ids_device(v, n, is, id, mi, dis[i].get(), did[i].get(), sh.stream);
+                remap_ids_device(v, n, is, id, mi, dis[i].get(), did[i].get(), sh.stream, &table);
                 e.in_src.push_back(dis[i].get());
                 e.in_dst.push_back(did[i].get());
             }

@@ -188,6 +188,13 @@ struct Halo {
 
 // Position of an owned row's value in a gathered vector: base + row (base = shard * S in the
 // full-length shard-major layout, 0 in a segmented compact vector).
+// Slot of the device vid -> dense hash table (jg_build.hip remap_ids_device): open addressing, linear
+// probing, key INT64_MIN = empty.
+struct alignas(16) IdSlot {
+    unsigned long long key;
+    uint32_t val, pad;
+};
+
 struct VecPos {
     int64_t base = 0;
     __device__ __forceinline__ int64_t operator()(int64_t row) const { return base + row; }
@@ -241,8 +248,10 @@ struct Graph {
     int64_t S = 0;         // padded rows per shard
     uint32_t flags = 0;
     std::vector<std::unique_ptr<Shard>> shards;  // the shards this process drives
-    std::vector<int64_t> sorted_vid;    // host: caller vids sorted (for vid -> dense lookups)
-    std::vector<int64_t> sorted_dense;  // dense index of sorted_vid[i]
+    // caller vid -> dense index: the device hash table the build's id remap made (on shard 0's device;
+    // empty for RMAT graphs, whose vid == dense).  Lookups go through dense_of_vids (batched).
+    DevBuf<IdSlot> id_table;
+    int id_dev = 0;
     std::vector<int64_t> vid;           // host: vid[dense] (empty for RMAT graphs: vid == dense)
     std::vector<int32_t> padded_of_dense;  // host: global padded id of each caller vertex (P*S < 2^31)
     jg_graph_info info{};
@@ -255,7 +264,6 @@ struct Graph {
     int pr_steps = 0;
 
     int64_t vid_of(int64_t dense) const { return vid.empty() ? dense : vid[dense]; }
-    int64_t dense_of_vid(int64_t v) const;  // -1 if absent
     int64_t padded_len() const { return (int64_t)P * S; }
     // adj: JG_ADJ_IN or JG_ADJ_BOTH — the pull adjacency whose gathered vector this is
     const Halo& halo(const Shard& sh, uint32_t adj) const { return adj == JG_ADJ_BOTH ? sh.halo_both : sh.halo_in; }
@@ -301,8 +309,12 @@ struct DenseEdges {
 };
 void build_graph_from_dense(Graph& g, DenseEdges& e);
 void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int32_t* dst, hipStream_t s);
+// dsrc/ddst = the dense index of each endpoint (-1: not in vid, a ghost).  table: where the vid table is
+// built (nullptr: a temporary); a table that already holds this vid list (size != 0) is reused.
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
-                      int32_t* dsrc, int32_t* ddst, hipStream_t s);
+                      int32_t* dsrc, int32_t* ddst, hipStream_t s, DevBuf<IdSlot>* table = nullptr);
+// out[i] = the dense index of vids[i] (-1 if absent), k host values, one device lookup
+void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out);
 // out[e] = -1 where masked[e] < 0, else dense[e]
 void mask_ids_device(const int64_t* masked, const int32_t* dense, int64_t m, int32_t* out, hipStream_t s);
 // col_space: length of the gathered vector; vec_entries: entries actually in it, elem_bytes: their

@@ -1219,12 +1219,27 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     return hs.levels;
 }
 
+// The owning shard and local row of each caller vid (local -1: not a vertex of the graph), one
+// device lookup for the batch
+void locals_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* local, int* shard) {
+    std::vector<int64_t> d((size_t)k);
+    dense_of_vids(g, vids, k, d.data());
+    for (int64_t i = 0; i < k; ++i) {
+        local[i] = -1;
+        shard[i] = -1;
+        if (d[(size_t)i] < 0) continue;
+        const int64_t pg = g.padded_of_dense[(size_t)d[(size_t)i]];
+        shard[i] = (int)(pg / g.S);
+        local[i] = pg % g.S;
+    }
+}
+
 int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
-    const int64_t d = g.dense_of_vid(vid);
-    if (d < 0) return -1;
-    const int64_t pg = g.padded_of_dense[d];
-    *shard_out = (int)(pg / g.S);
-    return pg % g.S;
+    int64_t l = -1;
+    int sh = -1;
+    locals_of_vids(g, &vid, 1, &l, &sh);
+    if (l >= 0) *shard_out = sh;
+    return l;
 }
 
 // ---------------- sharded direction-optimising BFS (BOTH adjacency, halo plan) ----------------
@@ -1783,6 +1798,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 int64_t nq_in = 0;                // the last top-down level's input frontier (its queue)
             };
             std::vector<Td> tds(g.shards.size());
+            std::vector<int64_t> src_local((size_t)ns);
+            std::vector<int> src_shard((size_t)ns);
+            locals_of_vids(g, source_vids + b0, ns, src_local.data(), src_shard.data());
             int64_t push_nnz = 0;  // entries of the push adjacency, all shards and ranks (the direction rule)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
@@ -1826,11 +1844,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.depth8.get(), 0xFF, t.depth8.bytes(), sh.stream));
                 std::vector<int64_t> loc(ns, -1);
-                for (int s = 0; s < ns; ++s) {
-                    int shard = -1;
-                    const int64_t l = local_of_vid(g, source_vids[b0 + s], &shard);
-                    if (l >= 0 && shard == sh.index) loc[s] = l;
-                }
+                for (int s = 0; s < ns; ++s)
+                    if (src_local[(size_t)s] >= 0 && src_shard[(size_t)s] == sh.index) loc[s] = src_local[(size_t)s];
                 // the shard's distinct source rows: its first top-down queue (msbfs_source_queue_kernel)
                 for (int64_t l : loc)
                     if (l >= 0 && std::find(tds[i].src_rows.begin(), tds[i].src_rows.end(), l) == tds[i].src_rows.end())

@@ -194,3 +194,38 @@ def test_multi_source_bfs_past_255_levels(oracle_lib, shards):
         assert got[0].max() > 255
     g.close()
     c.close()
+
+
+def test_vertex_id_remap_arbitrary_ids(ctx, oracle_lib, rmat12):
+    """The device id table (jg_build.hip remap_ids_device): arbitrary int64 ids (negative, huge, clustered
+    in a few high-bit groups like JanusGraph's partitioned ids), ghost endpoints among them, a duplicate
+    id and the reserved INT64_MIN rejected with JG_ERR_ARG."""
+    import janusgraph_amd as jg
+    o = oracle_lib
+    n, _, s, t = rmat12
+    rng = np.random.default_rng(17)
+    vid = rng.choice(np.iinfo(np.int64).max, n, replace=False).astype(np.int64)
+    vid[: n // 4] = -vid[: n // 4]                            # negative ids
+    vid[n // 4: n // 2] = (np.arange(n // 4, dtype=np.int64) << 8) | (3 << 60)  # a dense high-bit cluster
+    assert len(np.unique(vid)) == n
+    assert 12345 not in set(vid.tolist())
+    src = vid[s].copy()
+    dst = vid[t].copy()
+    dst[np.arange(len(dst)) % 97 == 0] = 12345                # edges to an id outside vid: ghosts, dropped
+    keep = dst != 12345
+    g = ctx.build(vid, src, dst, flags=jg.ADJ_BOTH)
+    assert g.info()["ghost_edges"] == int((~keep).sum())
+    sv = int(s[0])
+    np.testing.assert_array_equal(g.bfs([vid[sv]], jg.DIR_BOTH)[0],
+                                  o.bfs(n, s[keep], t[keep], sv, o.DIR_BOTH))
+    g.close()
+    dup = vid.copy()
+    dup[7] = dup[3]
+    with pytest.raises(jg.JanusGpuError) as e:
+        ctx.build(dup, src, dst, flags=jg.ADJ_BOTH)
+    assert e.value.code == -1 and "duplicate" in str(e.value)
+    bad = vid.copy()
+    bad[5] = np.iinfo(np.int64).min
+    with pytest.raises(jg.JanusGpuError) as e:
+        ctx.build(bad, src, dst, flags=jg.ADJ_BOTH)
+    assert e.value.code == -1

@@ -4,7 +4,7 @@ set -o pipefail
 OUT=gpurun_out/r03x
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_edge_cases.py tests/test_gpu_parity.py tests/test_gpu_builder.py -x -v --timeout 120 --timeout-method thread > $OUT/pytest_quick.log 2>&1 || exit 3
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || exit 3
 timeout -k 10 300 python tools/build_trace.py --scale 20 --flags 4 --reps 4 > $OUT/build20.json 2> $OUT/build20.err || exit 4
 timeout -k 10 300 python tools/build_trace.py --scale 24 --flags 2 --reps 3 > $OUT/build24.json 2> $OUT/build24.err || exit 5
 timeout -k 10 300 python tools/edgestore_bench.py --scale 20 --chunks 1,8 > $OUT/edgestore20.json 2> $OUT/edgestore20.err || exit 6
