@@ -654,6 +654,8 @@ int jg_tune_set(const char* key, int64_t value) {
             (int)value;
     } else if (k == "cc_push") {
         jg::tune().cc_push = value != 0;
+    } else if (k == "msbfs_sparse") {
+        jg::tune().msbfs_sparse = value != 0;
     } else if (k == "msbfs_td") {
         JG_ARG(value >= 0 && value <= 2, "msbfs_td must be 0 (off), 1 (one shard and sharded) or 2 (one shard only)");
         jg::tune().msbfs_td = (int)value;

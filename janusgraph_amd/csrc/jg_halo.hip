@@ -475,6 +475,76 @@ void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, s
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
+void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::vector<std::vector<int64_t>>& soff,
+                   const std::vector<std::vector<int64_t>>& scount, const std::vector<char*>& recv,
+                   const std::vector<std::vector<int64_t>>& roff, const std::vector<std::vector<int64_t>>& rcount,
+                   size_t eb, ncclDataType_t type) {
+    if (g.P == 1) return;
+    Ctx& c = *g.ctx;
+    const size_t ns = g.shards.size();
+    if (c.logical) {  // every shard here, one device and stream: device copies
+        Shard& s0 = *g.shards[0];
+        DeviceGuard dg(s0.device);
+        for (size_t i = 0; i < ns; ++i)
+            for (size_t j = 0; j < ns; ++j) {
+                if (i == j) continue;
+                const int qi = g.shards[i]->index, qj = g.shards[j]->index;
+                const int64_t n = scount[i][(size_t)qj];
+                if (n != rcount[j][(size_t)qi]) fail(JG_ERR_HIP, "exchange_runs: send and receive counts differ");
+                if (n > 0)
+                    JG_HIP(hipMemcpyAsync(recv[j] + (size_t)roff[j][(size_t)qi] * eb, send[i] + (size_t)soff[i][(size_t)qj] * eb,
+                                          (size_t)n * eb, hipMemcpyDeviceToDevice, s0.stream));
+            }
+        return;
+    }
+    if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh.device);
+        std::vector<int> sp, rp;
+        std::vector<const void*> sv;
+        std::vector<void*> rv;
+        std::vector<size_t> sb, rb;
+        std::vector<std::vector<char>> out, in;
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t n_s = scount[0][(size_t)q], n_r = rcount[0][(size_t)q];
+            if (n_s > 0) {
+                sp.push_back(q);
+                out.emplace_back((size_t)n_s * eb);
+                copy_d2h(out.back().data(), send[0] + (size_t)soff[0][(size_t)q] * eb, out.back().size(), sh.stream);
+                sb.push_back(out.back().size());
+            }
+            if (n_r > 0) {
+                rp.push_back(q);
+                in.emplace_back((size_t)n_r * eb);
+                rb.push_back(in.back().size());
+            }
+        }
+        for (auto& b : out) sv.push_back(b.data());
+        for (auto& b : in) rv.push_back(b.data());
+        host_exchange(c, sp, sv, sb, rp, rv, rb);
+        for (size_t k = 0; k < rp.size(); ++k)
+            copy_h2d(recv[0] + (size_t)roff[0][(size_t)rp[k]] * eb, rv[k], rb[k], sh.stream);
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t n_s = scount[i][(size_t)q], n_r = rcount[i][(size_t)q];
+            if (n_s > 0)
+                rccl_check(ncclSend(send[i] + (size_t)soff[i][(size_t)q] * eb, (size_t)n_s, type, q, sh.comm, sh.stream),
+                           "ncclSend");
+            if (n_r > 0)
+                rccl_check(ncclRecv(recv[i] + (size_t)roff[i][(size_t)q] * eb, (size_t)n_r, type, q, sh.comm, sh.stream),
+                           "ncclRecv");
+        }
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void exchange_vec(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
     if (g.P == 1) return;
     if (g.halo(*g.shards[0], adj).on)

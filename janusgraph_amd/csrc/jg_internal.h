@@ -344,6 +344,13 @@ void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std
 // lists -> segments; reverse: segments -> the owners' send-list words.
 void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, std::vector<uint64_t*>& bitmaps,
                         bool reverse);
+// Per-peer runs whose lengths both sides know (the sparse reverse exchange of the sharded bit-parallel
+// BFS): local shard i sends scount[i][q] elements from send[i] + soff[i][q] to peer q and receives
+// rcount[i][q] elements from q at recv[i] + roff[i][q] (offsets and counts in elements of eb bytes).
+void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::vector<std::vector<int64_t>>& soff,
+                   const std::vector<std::vector<int64_t>>& scount, const std::vector<char*>& recv,
+                   const std::vector<std::vector<int64_t>>& roff, const std::vector<std::vector<int64_t>>& rcount,
+                   size_t eb, ncclDataType_t type);
 // word offsets of the per-peer send-list runs of exchange_halo_bits ([P + 1])
 std::vector<int64_t> halo_word_offsets(const Halo& h, int P);
 // Builds shard sh's halo plan for adjacency `which` (0 IN, 2 BOTH) from the full edge list.
@@ -523,6 +530,8 @@ struct Tune {
                                       // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
+    int msbfs_sparse = 1;             //         sharded bit-parallel BFS: top-down levels send only the set halo
+                                      //         staging slots when they are under half the halo (0: always dense)
     int msbfs_td = 1;                 //         bit-parallel BFS: top-down levels for small frontiers (1: one shard
                                       //         and sharded over the BOTH halo, 2: one shard only, 0: off)
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round

@@ -850,6 +850,100 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
     if (a.hstage) happ.final(a.hlist, a.hlist_off, a.hpacked);
 }
 
+// ---- sparse reverse exchange of a sharded top-down level (only the staging slots the level set) ----
+// A staging slot u (compact position, segment u >> tbits >= 1) is about peer q = seg - 1 if seg <= r,
+// else seg (the inverse of Halo::seg_of for shard r); it travels as (offset in the segment, word): the
+// offset is the slot's position in q's send list for r, so q finds its own row as send_src[send_off[r] + o].
+constexpr int kMaxPeersMs = 64;
+__device__ __forceinline__ int slot_peer(int32_t u, int tbits, int r) {
+    const int seg = (int)((uint32_t)u >> tbits);
+    return seg <= r ? seg - 1 : seg;
+}
+
+// cnt[q] += the slots of hlist[0, nh) about peer q (LDS histogram, one global atomic per block and peer)
+__global__ __launch_bounds__(kBlock) void msbfs_pair_count_kernel(const int32_t* __restrict__ hlist, int64_t nh,
+                                                                  int tbits, int r, int P,
+                                                                  unsigned long long* __restrict__ cnt) {
+    __shared__ unsigned int lc[kMaxPeersMs];
+    for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+    __syncthreads();
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nh; k += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&lc[slot_peer(hlist[k], tbits, r)], 1u);
+    __syncthreads();
+    for (int q = threadIdx.x; q < P; q += blockDim.x)
+        if (lc[q]) atomicAdd(&cnt[q], (unsigned long long)lc[q]);
+}
+
+struct PairRuns {
+    int64_t off[kMaxPeersMs + 1];       // pack: the run of peer q starts at pair off[q]; receive: from q at off[q]
+    int64_t send_off[kMaxPeersMs + 1];  // receive: the owner's send-list offsets (Halo::send_off)
+    int P;
+};
+
+// the (offset, word) pairs of every set staging slot, grouped by peer (order inside a run is free: the
+// receiver ORs); cursor[P] zeroed by the caller
+__global__ __launch_bounds__(kBlock) void msbfs_pair_pack_kernel(const int32_t* __restrict__ hlist, int64_t nh,
+                                                                 const unsigned long long* __restrict__ hs, int tbits,
+                                                                 int r, PairRuns pr,
+                                                                 unsigned long long* __restrict__ cursor,
+                                                                 unsigned long long* __restrict__ pairs) {
+    __shared__ unsigned int lc[kMaxPeersMs];
+    __shared__ unsigned long long base[kMaxPeersMs];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < nh; k0 += stride) {  // block-uniform trips
+        for (int q = threadIdx.x; q < pr.P; q += blockDim.x) lc[q] = 0u;
+        __syncthreads();
+        const int64_t k = k0 + threadIdx.x;
+        int q = 0;
+        unsigned int p = 0;
+        int32_t u = 0;
+        if (k < nh) {
+            u = hlist[k];
+            q = slot_peer(u, tbits, r);
+            p = atomicAdd(&lc[q], 1u);
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < pr.P; x += blockDim.x)
+            base[x] = lc[x] ? atomicAdd(&cursor[x], (unsigned long long)lc[x]) : 0ull;
+        __syncthreads();
+        if (k < nh) {
+            const int64_t j = pr.off[q] + (int64_t)(base[q] + p);
+            pairs[2 * j] = (unsigned long long)((uint32_t)u & ((1u << tbits) - 1u));
+            pairs[2 * j + 1] = hs[u];
+        }
+        __syncthreads();
+    }
+}
+
+// owner side of the sparse exchange: like msbfs_td_recv_kernel, over the received pairs
+__global__ __launch_bounds__(kBlock) void msbfs_td_recv_pairs_kernel(const unsigned long long* __restrict__ rpairs,
+                                                                     int64_t total, PairRuns pr,
+                                                                     const int32_t* __restrict__ send_src,
+                                                                     const unsigned long long* __restrict__ visited,
+                                                                     unsigned long long* __restrict__ Fnext,
+                                                                     int32_t* __restrict__ touched,
+                                                                     int64_t* __restrict__ touched_off,
+                                                                     unsigned long long* __restrict__ tpacked) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < total; x0 += stride) {  // block-uniform trips
+        const int64_t k = x0 + threadIdx.x;
+        bool take = false;
+        int32_t u = 0;
+        if (k < total) {
+            int q = 0;
+            while (q + 1 < pr.P && pr.off[q + 1] <= k) ++q;
+            const unsigned long long o = rpairs[2 * k], r = rpairs[2 * k + 1];
+            u = send_src[pr.send_off[q] + (int64_t)o];
+            const unsigned long long w = r & ~visited[u];
+            if (w && (w & ~Fnext[u])) take = atomicOr(&Fnext[u], w) == 0ull;
+        }
+        app.append(take, u, 0, touched, touched_off, tpacked);
+    }
+    app.final(touched, touched_off, tpacked);
+}
+
 // v[list[i]] = 0 for i < n: clears the words a level set (its frontier rows, or its halo staging slots)
 // without a pass over the whole vector
 __global__ void msbfs_zero_list_kernel(unsigned long long* __restrict__ v, const int32_t* __restrict__ list, int64_t n) {
@@ -1782,7 +1876,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // a shard pushes its own frontier rows; bits for a peer's vertex collect in its halo slot and
             // go to the owner by the reverse halo exchange (msbfs_td_recv_kernel).
             const bool td_one = g.shards.size() == 1 && g.P == 1 && c0.push != nullptr && tune().msbfs_td != 0;
-            const bool td_shard = g.P > 1 && direction == JG_DIR_BOTH && sh0.halo_both.on && tune().msbfs_td == 1;
+            const bool td_shard = g.P > 1 && g.P <= kMaxPeersMs && direction == JG_DIR_BOTH && sh0.halo_both.on &&
+                                  tune().msbfs_td == 1;
             const bool td_ok = td_one || td_shard;
             struct Td {
                 DevBuf<int32_t> queue[2], touched;
@@ -1793,8 +1888,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> hs;    // sharded: halo staging (compact positions), zero between levels
                 DevBuf<int32_t> hlist;            // sharded: the staging slots a level set
                 DevBuf<int64_t> hlist_off;        // appender scratch
+                DevBuf<unsigned long long> pairs, rpairs, pcnt;  // sparse reverse exchange: sent / received
+                                                                 // (offset, word) pairs, per-peer counts + cursors
                 std::vector<int64_t> src_rows;
                 int64_t nq = 0, mf = 0;
+                int64_t nrp = 0;                  // pairs received by the last sparse exchange
+                PairRuns pv{};                    // their per-peer runs and this shard's send-list offsets
                 int64_t nq_in = 0;                // the last top-down level's input frontier (its queue)
             };
             std::vector<Td> tds(g.shards.size());
@@ -1941,6 +2040,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         JG_HIP(hipMemsetAsync(td.hs.get(), 0, td.hs.bytes(), sh.stream));
                         td.hlist.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
                         td.hlist_off.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
+                        if (tune().msbfs_sparse) {
+                            td.pairs.alloc(2 * std::max<int64_t>(h.recv_off[g.P], 1));
+                            td.rpairs.alloc(2 * std::max<int64_t>(h.send_off[g.P], 1));
+                            td.pcnt.alloc(2 * (size_t)g.P);
+                        }
                     }
                 }
             }
@@ -2002,7 +2106,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    // exactly its input queue (tds[i].queue[qc ^ 1][0, nq_in))
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
             // counted on the device, or every task when the skip is off) and top-down frontier entries
-            int pull_levels = 0;
+            int pull_levels = 0, sparse_levels = 0;
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
                 if (level + 1 >= 255) widen();
@@ -2051,7 +2155,99 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         fv.push_back(td.hs.get());
                         rv.push_back(td.rbuf.get());
                     }
-                    if (td_shard) {
+                    // sparse: only the set staging slots travel, as (offset, word) pairs, when they are fewer
+                    // than half the halo slots over all shards (the tail levels and the first levels from
+                    // the sources set a few thousand)
+                    bool sparse_done = false;
+                    if (td_shard && tune().msbfs_sparse) {
+                        const int P = g.P;
+                        std::vector<std::vector<int64_t>> cnt(g.shards.size(), std::vector<int64_t>((size_t)P, 0));
+                        std::vector<int64_t> mat((size_t)P * P + 1, 0);
+                        for (size_t i = 0; i < g.shards.size(); ++i) {
+                            Shard& sh = *g.shards[i];
+                            DeviceGuard dg(sh.device);
+                            unsigned long long hh = 0;
+                            copy_d2h(&hh, tds[i].ctr.get() + 2, sizeof hh, sh.stream);
+                            const int64_t nh = (int64_t)(hh >> kPackShift);
+                            JG_HIP(hipMemsetAsync(tds[i].pcnt.get(), 0, 2 * (size_t)P * sizeof(unsigned long long), sh.stream));
+                            if (nh > 0) {
+                                msbfs_pair_count_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(
+                                    tds[i].hlist.get(), nh, sh.halo_both.tbits, sh.index, P, tds[i].pcnt.get());
+                                JG_LAUNCH_CHECK();
+                            }
+                            std::vector<unsigned long long> c((size_t)P);
+                            copy_d2h(c.data(), tds[i].pcnt.get(), (size_t)P * sizeof(unsigned long long), sh.stream);
+                            for (int q = 0; q < P; ++q) {
+                                cnt[i][(size_t)q] = (int64_t)c[(size_t)q];
+                                mat[(size_t)sh.index * P + q] = (int64_t)c[(size_t)q];
+                            }
+                            mat[(size_t)P * P] += sh.halo_both.recv_off[(size_t)P];  // the dense exchange's words
+                        }
+                        allreduce_sum_i64(g, mat.data(), P * P + 1);
+                        int64_t pairs_all = 0;
+                        for (int64_t k = 0; k < (int64_t)P * P; ++k) pairs_all += mat[(size_t)k];
+                        if (2 * pairs_all < mat[(size_t)P * P]) {
+                            const size_t ns_ = g.shards.size();
+                            std::vector<const char*> sp(ns_);
+                            std::vector<char*> rp(ns_);
+                            std::vector<std::vector<int64_t>> so(ns_), sc(ns_), ro(ns_), rc(ns_);
+                            for (size_t i = 0; i < ns_; ++i) {
+                                Shard& sh = *g.shards[i];
+                                DeviceGuard dg(sh.device);
+                                so[i].assign((size_t)P + 1, 0);
+                                ro[i].assign((size_t)P + 1, 0);
+                                sc[i].assign((size_t)P, 0);
+                                rc[i].assign((size_t)P, 0);
+                                PairRuns pk{}, pv{};
+                                pk.P = pv.P = P;
+                                for (int q = 0; q < P; ++q) {
+                                    so[i][(size_t)q + 1] = so[i][(size_t)q] + cnt[i][(size_t)q];
+                                    const int64_t from_q = mat[(size_t)q * P + sh.index];
+                                    ro[i][(size_t)q + 1] = ro[i][(size_t)q] + from_q;
+                                    sc[i][(size_t)q] = 2 * cnt[i][(size_t)q];  // uint64 elements: two per pair
+                                    rc[i][(size_t)q] = 2 * from_q;
+                                }
+                                for (int q = 0; q <= P; ++q) {
+                                    pk.off[q] = so[i][(size_t)q];
+                                    pv.off[q] = ro[i][(size_t)q];
+                                    pv.send_off[q] = sh.halo_both.send_off[(size_t)q];
+                                }
+                                const int64_t nh = so[i][(size_t)P];
+                                if (nh > 0) {
+                                    msbfs_pair_pack_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(
+                                        tds[i].hlist.get(), nh, tds[i].hs.get(), sh.halo_both.tbits, sh.index, pk,
+                                        tds[i].pcnt.get() + P, tds[i].pairs.get());
+                                    JG_LAUNCH_CHECK();
+                                }
+                                for (int q = 0; q <= P; ++q) {
+                                    so[i][(size_t)q] *= 2;
+                                    ro[i][(size_t)q] *= 2;
+                                }
+                                sp[i] = reinterpret_cast<const char*>(tds[i].pairs.get());
+                                rp[i] = reinterpret_cast<char*>(tds[i].rpairs.get());
+                                tds[i].nrp = ro[i][(size_t)P] / 2;
+                                tds[i].pv = pv;
+                            }
+                            exchange_runs(g, sp, so, sc, rp, ro, rc, sizeof(unsigned long long), ncclUint64);
+                            for (size_t i = 0; i < ns_; ++i) {
+                                Shard& sh = *g.shards[i];
+                                DeviceGuard dg(sh.device);
+                                if (tds[i].nrp > 0) {
+                                    msbfs_td_recv_pairs_kernel<<<grid_for(tds[i].nrp), kBlock, 0, sh.stream>>>(
+                                        tds[i].rpairs.get(), tds[i].nrp, tds[i].pv, sh.halo_both.send_src.get(),
+                                        st[i].vis.get(), st[i].F[cur ^ 1].get(), tds[i].touched.get(),
+                                        tds[i].touched_off.get(), tds[i].ctr.get() + 1);
+                                    JG_LAUNCH_CHECK();
+                                }
+                            }
+                            sparse_done = true;
+                            ++sparse_levels;
+                            if (std::getenv("JG_DEBUG_BFS"))
+                                std::fprintf(stderr, "[jg msbfs] level %d top-down, sparse reverse exchange: %lld pairs (dense: %lld words)\n",
+                                             level, (long long)pairs_all, (long long)mat[(size_t)P * P]);
+                        }
+                    }
+                    if (td_shard && !sparse_done) {
                         exchange_halo_reverse(g, JG_ADJ_BOTH, fv, rv, sizeof(unsigned long long), ncclUint64);
                         for (size_t i = 0; i < g.shards.size(); ++i) {
                             Shard& sh = *g.shards[i];
