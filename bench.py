@@ -234,8 +234,10 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
         gb.bfs([sv], jg.DIR_BOTH, want=False)
         if ctx.stats()["edges_traversed"] < m // 100:
             continue  # a source in a tiny component: Graph500 resamples
+        ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
         gb.bfs([sv], jg.DIR_BOTH, want=False)  # timed run (the first touched cold pages)
         st = ctx.stats()
+        ctx.set_profiling(False)
         ms = ctl.max(st["compute_ms"])
         srcs.append(sv)
         times.append(ms)
@@ -310,8 +312,10 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     build_ms = ctx.stats()["build_ms"]
     deg = both_degrees(jg, ctl, g)
     g.connected_components()  # warm
+    ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
     comp, it = g.connected_components()
     st = ctx.stats()
+    ctx.set_profiling(False)
     cc_ms = ctl.max(st["compute_ms"])
     cc_rank = ctl.gather([st["compute_ms"], st["exchange_ms"]])
     if ctl.ws > 1:
@@ -337,8 +341,10 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     edges = float(comp_edges[comp[srcs]].sum())
     del comp, counts, comp_edges
     g.bfs(srcs, jg.DIR_BOTH, want=False)  # warm
+    ctx.set_profiling(ctl.ws > 1)
     g.bfs(srcs, jg.DIR_BOTH, want=False)
     st = ctx.stats()
+    ctx.set_profiling(False)
     ms = ctl.max(st["compute_ms"])
     wl_ms = f"msbfs64_rmat{scale}_ef{ef}"
     msb = {"workload": wl_ms, "sources": int(len(srcs)), "ms": round(ms, 3), "levels": st["levels"],

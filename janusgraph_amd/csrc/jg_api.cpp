@@ -53,6 +53,7 @@ void host_exchange(Ctx& c, const std::vector<int>& speer, const std::vector<cons
 }
 
 void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
+    ExchTimer et(g);
     if (g.P == 1) return;
     Ctx& c = *g.ctx;
     const size_t slice = (size_t)g.S * elem_bytes;
@@ -363,6 +364,24 @@ void exch_record(Ctx& c, Shard& sh) {
     JG_HIP(hipEventCreate(&e));
     JG_HIP(hipEventRecord(e, sh.stream));
     sh.exch_events.push_back(e);
+}
+
+ExchTimer::ExchTimer(Graph& gr) : g(gr) {
+    if (!g.ctx->profiling) return;
+    for (auto& sp : g.shards) {
+        DeviceGuard dg(sp->device);
+        exch_record(*g.ctx, *sp);
+    }
+}
+ExchTimer::~ExchTimer() {
+    if (!g.ctx->profiling) return;
+    for (auto& sp : g.shards) {
+        DeviceGuard dg(sp->device);
+        try {
+            exch_record(*g.ctx, *sp);
+        } catch (...) {  // never from a destructor; the pair stays open and prof_collect skips it
+        }
+    }
 }
 
 void prof_collect(Ctx& c, Graph& g) {

@@ -208,6 +208,7 @@ void check_halo_counts(Graph& g, uint32_t adj) {
 }
 
 void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem_bytes, ncclDataType_t type) {
+    ExchTimer et(g);
     if (elem_bytes != 4 && elem_bytes != 8) fail(JG_ERR_UNSUPPORTED, "halo exchange of unsupported element size");
     Ctx& c = *g.ctx;
     for (size_t i = 0; i < g.shards.size(); ++i) {  // pack the runs of own values each peer reads
@@ -302,6 +303,7 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
 void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std::vector<void*>& rbufs,
                            size_t elem_bytes, ncclDataType_t type) {
     if (g.P == 1) return;
+    ExchTimer et(g);
     Ctx& c = *g.ctx;
     // shard r's segment for peer q (the run q sent it) goes back to q, landing at q's send-list
     // position for r
@@ -387,6 +389,7 @@ std::vector<int64_t> halo_word_offsets(const Halo& h, int P) {
 void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, std::vector<uint64_t*>& bitmaps,
                         bool reverse) {
     if (g.P == 1) return;
+    ExchTimer et(g);
     Ctx& c = *g.ctx;
     constexpr size_t W = sizeof(uint64_t);
     // shard i's words about peer q's vertices: its segment for q (receiver side of the forward run)
@@ -480,6 +483,7 @@ void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::ve
                    const std::vector<std::vector<int64_t>>& roff, const std::vector<std::vector<int64_t>>& rcount,
                    size_t eb, ncclDataType_t type) {
     if (g.P == 1) return;
+    ExchTimer et(g);
     Ctx& c = *g.ctx;
     const size_t ns = g.shards.size();
     if (c.logical) {  // every shard here, one device and stream: device copies

@@ -600,6 +600,13 @@ void prof_record_stop(Ctx& c, Shard& sh, int units = 1);
 void prof_collect(Ctx& c, Graph& g);
 // Event pair around an exchange step on the shard's stream (profiling only): exchange_ms.
 void exch_record(Ctx& c, Shard& sh);
+// With profiling on, an exchange step is bracketed by events on every local shard's stream
+// (jg_stats.exchange_ms: the slowest shard's sum); the leaf exchange functions hold one.
+struct ExchTimer {
+    Graph& g;
+    explicit ExchTimer(Graph& gr);
+    ~ExchTimer();
+};
 
 }  // namespace jg
 

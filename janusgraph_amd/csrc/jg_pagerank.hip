@@ -129,17 +129,7 @@ void pagerank_steps(Graph& g, int nsteps) {
             launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get(),
                         skip_empty);
         }
-        if (pc)
-            for (auto& sp : g.shards) {
-                DeviceGuard dg(sp->device);
-                exch_record(*pc, *sp);
-            }
-        exchange_contrib(g, nxt);
-        if (pc)
-            for (auto& sp : g.shards) {
-                DeviceGuard dg(sp->device);
-                exch_record(*pc, *sp);
-            }
+        exchange_contrib(g, nxt);  // timed by the exchange itself (ExchTimer) when profiling
         g.pr_cur = nxt;
         ++g.pr_steps;
     }
