@@ -673,6 +673,8 @@ int jg_tune_set(const char* key, int64_t value) {
             (int)value;
     } else if (k == "cc_push") {
         jg::tune().cc_push = value != 0;
+    } else if (k == "band_sliced_build") {
+        jg::tune().band_sliced_build = value != 0;
     } else if (k == "msbfs_sparse") {
         jg::tune().msbfs_sparse = value != 0;
     } else if (k == "msbfs_td") {

@@ -607,6 +607,70 @@ __global__ void band_len_kernel(const int64_t* __restrict__ rp, const int32_t* _
     }
 }
 
+// Sub-rows from the column-ordered CSR (round 3: the bands used to be cut from a second, sub-slice-
+// ordered build of the whole CSR).  One wave per band row; a sub-row keeps its entries in the row's
+// (column) order.  Wave-private LDS: the fences only keep the compiler from moving LDS accesses across
+// the wave barrier (a wave executes its LDS instructions in order).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// len[h * NR + i] = entries of band row R0 + i in sub-slice h
+__global__ __launch_bounds__(kBlock) void band_count_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                            int64_t R0, int64_t NR, int bits, int32_t* __restrict__ len) {
+    __shared__ uint32_t cnt[kBlock / kWave][256];
+    const int S = 1 << bits;
+    const int wv = (int)(threadIdx.x / kWave), lane = (int)(threadIdx.x % kWave);
+    const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
+    for (int64_t i = (int64_t)blockIdx.x * (kBlock / kWave) + wv; i < NR; i += waves) {
+        for (int h = lane; h < S; h += kWave) cnt[wv][h] = 0u;
+        wave_sync();
+        const int64_t b = rp[R0 + i], e = rp[R0 + i + 1];
+        for (int64_t j = b + lane; j < e; j += kWave) atomicAdd(&cnt[wv][sub_slice(col[j], bits)], 1u);
+        wave_sync();
+        for (int h = lane; h < S; h += kWave) len[(int64_t)h * NR + i] = (int32_t)cnt[wv][h];
+        wave_sync();
+    }
+}
+
+// band col[sp[h][i] + k] = the k-th entry (row order) of band row i in sub-slice h: per 64-entry chunk
+// every lane finds the lanes of its sub-slice by `bits` ballots, takes its rank among them after the
+// sub-row's running position, and the group's highest lane advances that position
+__global__ __launch_bounds__(kBlock) void band_scatter_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                              int64_t R0, int64_t NR, int bits,
+                                                              const int64_t* __restrict__ sp, int32_t* __restrict__ bcol) {
+    __shared__ int64_t run[kBlock / kWave][256];
+    const int S = 1 << bits;
+    const int wv = (int)(threadIdx.x / kWave), lane = (int)(threadIdx.x % kWave);
+    const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));  // lanes below this one
+    for (int64_t i = (int64_t)blockIdx.x * (kBlock / kWave) + wv; i < NR; i += waves) {
+        for (int h = lane; h < S; h += kWave) run[wv][h] = sp[(int64_t)h * (NR + 1) + i];
+        wave_sync();
+        const int64_t b = rp[R0 + i], e = rp[R0 + i + 1];
+        for (int64_t j0 = b; j0 < e; j0 += kWave) {
+            const int64_t j = j0 + lane;
+            const bool valid = j < e;
+            const int32_t c = valid ? col[j] : 0;
+            const int h = valid ? sub_slice(c, bits) : 0;
+            uint64_t mask = __ballot(valid);
+            for (int t = 0; t < bits; ++t) {
+                const uint64_t m = __ballot(valid && ((h >> t) & 1));
+                mask &= ((h >> t) & 1) ? m : ~m;
+            }
+            const int64_t pos = run[wv][h] + (int64_t)__popcll(mask & lt);
+            wave_sync();
+            if (valid) {
+                bcol[pos] = c;
+                if ((mask >> lane) == 1ull) run[wv][h] += (int64_t)__popcll(mask);  // the group's highest lane
+            }
+            wave_sync();
+        }
+    }
+}
+
 // raw[h * NR] for h = 0..S (the sub-slice boundaries of the exclusive scan)
 __global__ void band_bounds_kernel(const int64_t* __restrict__ raw, int64_t NR, int S, int64_t* __restrict__ out) {
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
@@ -749,10 +813,15 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     const int64_t R0 = bd.row_begin, NR = bd.rows();
     const int S = 1 << bd.bits;
     const int64_t NS = NR * S;
-    DevBuf<uint32_t> off(NS);
     DevBuf<int32_t> len(NS);
     DevBuf<int64_t> raw(NS + 1);
-    band_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, off.get(), len.get());
+    DevBuf<uint32_t> off;
+    if (csr.sliced) {  // rows ordered by sub-slice: the sub-rows are runs (binary search)
+        off.alloc(NS);
+        band_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, off.get(), len.get());
+    } else {
+        band_count_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, len.get());
+    }
     JG_LAUNCH_CHECK();
     prim::exclusive_scan(len.get(), raw.get(), NS, s);
     std::vector<int64_t> bounds(S + 1), begin(S), end(S), base(S + 1);
@@ -784,8 +853,12 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     JG_LAUNCH_CHECK();
     bd.col.alloc(at + kMergeTask);  // one task of padding: the last task's aligned loads
     JG_HIP(hipMemsetAsync(bd.col.get(), 0, bd.col.bytes(), s));
-    band_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, S, off.get(),
-                                                             sp.get(), bd.col.get());
+    if (csr.sliced)
+        band_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, S, off.get(),
+                                                                 sp.get(), bd.col.get());
+    else
+        band_scatter_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits,
+                                                                    sp.get(), bd.col.get());
     JG_LAUNCH_CHECK();
     // number the non-empty sub-rows
     DevBuf<int32_t> flag(NS);
@@ -907,8 +980,9 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
     fb[kNumClasses] = 0;  // 1 + last non-empty row
     BandThresholds bt{};
-    // bands only on a sliced CSR, and only when the split is enabled at build time
-    if (tune().pull_split && csr.sliced)
+    // bands only when the split is enabled at build time (cut from a column-ordered CSR by counting, or
+    // from a sub-slice-ordered one by binary search: Tune::band_sliced_build)
+    if (tune().pull_split)
         for (int i = 0; i < 4 && tune().band_deg[i] > 0; ++i) bt.thr[bt.n++] = std::max<int64_t>(tune().band_deg[i], 1);
     for (int i = 0; i < 4; ++i) fb[kNumClasses + 1 + i] = (unsigned long long)rows;
     if (rows > 0) {
@@ -1188,7 +1262,9 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                 vec_entries = sh.rows + halo.recv_off[P];
             }
             a.cbits = std::max(cbits, bits_for((uint64_t)(col_space - 1)));  // compact ids may exceed P*S
-            a.sbits = tune().pull_split ? 8 : 0;
+            // round 3: one column-ordered build, the bands cut from it (band_count / band_scatter); the
+            // sub-slice-ordered first build (band_sliced_build = 1) cost a second select and sort
+            a.sbits = tune().pull_split && tune().band_sliced_build ? 8 : 0;
             build_csr(sh, a, wt, csr, s);
             // the gathered vector of the split: PageRank's fp64 contributions (IN), CC's int32 labels (BOTH)
             build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 2 ? 4 : 8);

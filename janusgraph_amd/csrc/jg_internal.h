@@ -569,6 +569,8 @@ struct Tune {
     int merge_interleave = 1;         // merge blocks take interleaved single tasks, rotating per round (0: chunks of 16)
     int merge_dynamic = 1;            // merge waves take their block's tasks from an LDS counter (0: static)
     int fin_pipe = 1;                 // split finalize: next batch's index words loaded with this batch's partials
+    int band_sliced_build = 0;        // build time: 1 = cut the bands from a sub-slice-ordered first build of the
+                                      // CSR (rounds 1-2; a second select + sort), 0 = from the column-ordered CSR
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
                                       // (0: 32 bits, 24: at least 24; tests)
     int light_runs = 1;               // build time: light rows of degree 1..7 addressed by degree run (no row_ptr load)

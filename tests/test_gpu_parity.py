@@ -399,7 +399,8 @@ def test_errors_are_status_codes(ctx):
 
 @pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
                                   "split_sub1", "split_sub2_4", "split_w24", "split_w32", "split_stage_off",
-                                  "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip", "cc_first3"])
+                                  "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip", "cc_first3",
+                                  "split_sliced_build"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -427,7 +428,8 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "merge_static": [("merge_dynamic", 0)],
              "merge_chunks16": [("merge_interleave", 0)],
              "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)],
-             "cc_first3": [("cc_first", 3)]}[mode]
+             "cc_first3": [("cc_first", 3)],
+             "split_sliced_build": [("band_sliced_build", 1)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -454,6 +456,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("merge_wgs", 1)
         _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
+        _lib.tune_set("band_sliced_build", 0)
         _lib.tune_set("slice_lds", 1)
         _lib.tune_set("merge_pack", 1)
         _lib.tune_set("merge_stage0", -1)
