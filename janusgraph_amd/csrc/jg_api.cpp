@@ -415,6 +415,28 @@ void prof_collect(Ctx& c, Graph& g) {
     c.last.kernel_launches += launches;
 }
 
+const std::vector<int32_t>& Shard::dense_of_local() const {
+    if ((int64_t)dense_of_local_host.size() != rows) {
+        dense_of_local_host.resize((size_t)rows);
+        if (rows > 0) {
+            DeviceGuard dg(device);
+            copy_d2h(dense_of_local_host.data(), dense_rows.get(), (size_t)rows * sizeof(int32_t), stream);
+        }
+    }
+    return dense_of_local_host;
+}
+
+const std::vector<int32_t>& Graph::padded_of_dense() const {
+    if ((int64_t)padded_host.size() != n) {
+        padded_host.resize((size_t)n);
+        if (n > 0) {
+            DeviceGuard dg(id_dev);
+            copy_d2h(padded_host.data(), padded_dev.get(), (size_t)n * sizeof(int32_t), shards[0]->stream);
+        }
+    }
+    return padded_host;
+}
+
 // Host copy of the vertex ids: outputs are indexed like vid[] (vid -> dense lookups and the duplicate
 // check go through the device table the id remap builds: dense_of_vids).
 static void set_vertex_ids(Graph& g, const int64_t* vid, int64_t n) { g.vid.assign(vid, vid + n); }

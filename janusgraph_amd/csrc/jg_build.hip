@@ -142,10 +142,15 @@ __device__ __forceinline__ int32_t id_lookup(const IdSlot* __restrict__ t, uint6
     }
 }
 
-__global__ void id_lookup_kernel(const IdSlot* __restrict__ t, uint64_t mask, const int64_t* __restrict__ q, int64_t k,
-                                 int64_t* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = id_lookup(t, mask, q[i]);
+// t == nullptr: the ids are dense indices (RMAT graphs), valid in [0, n)
+__global__ void id_lookup_kernel(const IdSlot* __restrict__ t, uint64_t mask, int64_t n, const int64_t* __restrict__ q,
+                                 int64_t k, const int32_t* __restrict__ padded, int64_t* __restrict__ out,
+                                 int64_t* __restrict__ pout) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = t ? id_lookup(t, mask, q[i]) : (q[i] >= 0 && q[i] < n ? q[i] : -1);
+        out[i] = d;
+        if (pout) pout[i] = d >= 0 ? (int64_t)padded[d] : -1;
+    }
 }
 
 __global__ void remap_kernel(const IdSlot* __restrict__ t, uint64_t mask, const int64_t* __restrict__ s,
@@ -539,20 +544,19 @@ void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, con
     JG_HIP(hipStreamSynchronize(s));
 }
 
-void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out) {
+void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out, int64_t* padded) {
     if (k <= 0) return;
-    if (g.vid.empty()) {  // RMAT graphs: vid == dense
-        for (int64_t i = 0; i < k; ++i) out[i] = (vids[i] >= 0 && vids[i] < g.n) ? vids[i] : -1;
-        return;
-    }
     DeviceGuard dg(g.id_dev);
     hipStream_t s = g.shards[0]->stream;
-    DevBuf<int64_t> q(k), r(k);
+    DevBuf<int64_t> q(k), r(k), pr(padded ? k : 0);
     copy_h2d(q.get(), vids, (size_t)k * sizeof(int64_t), s);
-    id_lookup_kernel<<<grid_for(k), kBlock, 0, s>>>(g.id_table.get(), (uint64_t)(g.id_table.size() - 1), q.get(), k,
-                                                   r.get());
+    const bool table = g.id_table.size() != 0;
+    id_lookup_kernel<<<grid_for(k), kBlock, 0, s>>>(table ? g.id_table.get() : nullptr,
+                                                   table ? (uint64_t)(g.id_table.size() - 1) : 0ull, g.n, q.get(), k,
+                                                   g.padded_dev.get(), r.get(), padded ? pr.get() : nullptr);
     JG_LAUNCH_CHECK();
     copy_d2h(out, r.get(), (size_t)k * sizeof(int64_t), s);
+    if (padded) copy_d2h(padded, pr.get(), (size_t)k * sizeof(int64_t), s);
 }
 
 static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr& csr, hipStream_t s) {
@@ -1219,18 +1223,13 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         }
         const int r = sh.index;
         sh.rows = std::max<int64_t>(0, std::min<int64_t>(g.S, (n - r + P - 1) / P));
-        // dense index of each owned row (device and host), padded id of every vertex (host, once):
-        // contiguous copies of device arrays (a host loop of n random writes took 87 ms at 2^24)
+        // dense index of each owned row and padded id of every vertex stay on the device; their host
+        // copies are made on first use (Shard::dense_of_local, Graph::padded_of_dense)
         sh.dense_rows.alloc(std::max<int64_t>(sh.rows, 1));
-        sh.dense_of_local.resize(sh.rows);
+        sh.dense_of_local_host.clear();
         if (sh.rows > 0) {
             local_dense_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(order.get(), P, r, sh.rows, sh.dense_rows.get());
             JG_LAUNCH_CHECK();
-            copy_d2h(sh.dense_of_local.data(), sh.dense_rows.get(), sh.rows * sizeof(int32_t), s);
-        }
-        if (first) {
-            g.padded_of_dense.resize(n);
-            if (n) copy_d2h(g.padded_of_dense.data(), padded.get(), n * sizeof(int32_t), s);
         }
         sh.out_degree.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.rows > 0) {
@@ -1296,6 +1295,11 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         }
         if (g.flags & JG_ADJ_BOTH) build_pull_csr(2, all, nullptr, sh.both, sh.plan_both, sh.halo_both);
         JG_HIP(hipStreamSynchronize(s));
+        if (first) {  // the first shard's padded ids stay with the graph (vid -> shard / row lookups)
+            g.padded_dev = std::move(padded);
+            g.padded_host.clear();
+            if (g.id_table.size() == 0) g.id_dev = sh.device;  // RMAT graphs: no id table
+        }
         first = false;
     }
     if (P > 1 && tune().halo) {

@@ -475,7 +475,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
                 JG_LAUNCH_CHECK();
             } else {
                 std::vector<int32_t> lab0(sh.rows);
-                for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local[l]];
+                for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local()[l]];
                 copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
             }
             cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
@@ -628,7 +628,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             std::vector<int32_t> h(sh.rows);
             const int32_t* lab = solved && &sh == &sh0 ? uf_labels : sh.cc_label.get();
             if (sh.rows) copy_d2h(h.data(), lab, sh.rows * sizeof(int32_t), sh.stream);
-            for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local[l]] = vid_of_rank[h[l]];
+            for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local()[l]] = vid_of_rank[h[l]];
         }
     }
     prof_collect(ctx, g);

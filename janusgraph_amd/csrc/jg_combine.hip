@@ -132,7 +132,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
         // owned rows' initial messages at their slots (vertex order: sh.dense_of_local)
         std::vector<int64_t> h(std::max<int64_t>(n, 1));
         for (int64_t l = 0; l < n; ++l) {
-            const int64_t v = init ? init[sh.dense_of_local[l]] : 1;
+            const int64_t v = init ? init[sh.dense_of_local()[l]] : 1;
             h[l] = wrap32 ? (int64_t)(int32_t)v : v;
         }
         if (n) {
@@ -214,11 +214,11 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
         St& t = st[i];
         std::vector<int64_t> h((size_t)n);
         copy_d2h(h.data(), t.x[cur].get() + t.pos.base, n * sizeof(int64_t), sh.stream);
-        for (int64_t l = 0; l < n; ++l) out[sh.dense_of_local[l]] = h[l];
+        for (int64_t l = 0; l < n; ++l) out[sh.dense_of_local()[l]] = h[l];
         if (received_out) {
             std::vector<uint8_t> rc((size_t)n);
             copy_d2h(rc.data(), t.recv.get(), n, sh.stream);
-            for (int64_t l = 0; l < n; ++l) received_out[sh.dense_of_local[l]] = steps > 0 ? rc[l] : 0;
+            for (int64_t l = 0; l < n; ++l) received_out[sh.dense_of_local()[l]] = steps > 0 ? rc[l] : 0;
         }
     }
 }

@@ -212,7 +212,10 @@ struct Shard {
     bool plan_out_built = false;
     Halo halo_in, halo_both;      // sharded graphs: compact vectors of the IN / BOTH pull adjacencies
     DevBuf<int32_t> out_degree;   // [rows] out-degree of owned vertices (PageRank edgeCount)
-    std::vector<int32_t> dense_of_local;  // host: caller's dense index of each owned row
+    // host copy of dense_rows (caller's dense index of each owned row), made on first use
+    // (jg_api.cpp; the build no longer copies it: 67 MB at RMAT-24 through pageable memory)
+    mutable std::vector<int32_t> dense_of_local_host;
+    const std::vector<int32_t>& dense_of_local() const;
     DevBuf<int32_t> dense_rows;           // the same on the device (jg_scatter.h)
 
     // program state (allocated on demand)
@@ -253,7 +256,11 @@ struct Graph {
     DevBuf<IdSlot> id_table;
     int id_dev = 0;
     std::vector<int64_t> vid;           // host: vid[dense] (empty for RMAT graphs: vid == dense)
-    std::vector<int32_t> padded_of_dense;  // host: global padded id of each caller vertex (P*S < 2^31)
+    // global padded id of each caller vertex (P*S < 2^31): on the first shard's device (id_dev), the
+    // host copy made on first use
+    DevBuf<int32_t> padded_dev;
+    mutable std::vector<int32_t> padded_host;
+    const std::vector<int32_t>& padded_of_dense() const;
     jg_graph_info info{};
     bool has_weights = false;
     // PageRank session
@@ -313,8 +320,9 @@ void generate_rmat_device(int scale, uint64_t seed, int64_t m, int32_t* src, int
 // built (nullptr: a temporary); a table that already holds this vid list (size != 0) is reused.
 void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, const int64_t* d_dst, int64_t m,
                       int32_t* dsrc, int32_t* ddst, hipStream_t s, DevBuf<IdSlot>* table = nullptr);
-// out[i] = the dense index of vids[i] (-1 if absent), k host values, one device lookup
-void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out);
+// out[i] = the dense index of vids[i] (-1 if absent), k host values, one device lookup;
+// padded[i] (nullable) = its global padded id (-1 if absent)
+void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out, int64_t* padded = nullptr);
 // out[e] = -1 where masked[e] < 0, else dense[e]
 void mask_ids_device(const int64_t* masked, const int32_t* dense, int64_t m, int32_t* out, hipStream_t s);
 // col_space: length of the gathered vector; vec_entries: entries actually in it, elem_bytes: their

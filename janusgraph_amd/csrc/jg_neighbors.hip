@@ -57,7 +57,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
     for (int64_t k = 0; k < nrows; ++k) {
         const int64_t d = rows[k];
         if (d < 0 || d >= g.n) fail(JG_ERR_ARG, "row outside [0, num_vertices)");
-        const int64_t pg = g.padded_of_dense[(size_t)d];
+        const int64_t pg = g.padded_of_dense()[(size_t)d];
         const int q = (int)(pg / g.S);
         if (!local[q]) continue;  // another rank's row: no entries here
         loc[q].push_back(pg - (int64_t)q * g.S);
@@ -130,7 +130,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
                     p = (int)(c / g.S);
                     l = c - (int64_t)p * g.S;
                 }
-                *o++ = g.shards[p]->dense_of_local[(size_t)l];
+                *o++ = g.shards[p]->dense_of_local()[(size_t)l];
             }
         }
     }

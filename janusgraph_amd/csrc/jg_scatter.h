@@ -34,7 +34,7 @@ void rows_to_dense(const Graph& g, Shard& sh, const Td* dev, Th* out) {
     }
     std::vector<Td> h((size_t)sh.rows);
     copy_d2h(h.data(), dev, (size_t)sh.rows * sizeof(Td), sh.stream);
-    for (int64_t l = 0; l < sh.rows; ++l) out[sh.dense_of_local[l]] = (Th)h[l];
+    for (int64_t l = 0; l < sh.rows; ++l) out[sh.dense_of_local()[l]] = (Th)h[l];
 }
 
 }  // namespace jg

@@ -1342,15 +1342,14 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
 // The owning shard and local row of each caller vid (local -1: not a vertex of the graph), one
 // device lookup for the batch
 void locals_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* local, int* shard) {
-    std::vector<int64_t> d((size_t)k);
-    dense_of_vids(g, vids, k, d.data());
+    std::vector<int64_t> d((size_t)k), pg((size_t)k);
+    dense_of_vids(g, vids, k, d.data(), pg.data());
     for (int64_t i = 0; i < k; ++i) {
         local[i] = -1;
         shard[i] = -1;
         if (d[(size_t)i] < 0) continue;
-        const int64_t pg = g.padded_of_dense[(size_t)d[(size_t)i]];
-        shard[i] = (int)(pg / g.S);
-        local[i] = pg % g.S;
+        shard[i] = (int)(pg[(size_t)i] / g.S);
+        local[i] = pg[(size_t)i] % g.S;
     }
 }
 
@@ -2696,7 +2695,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
     ctx.last.compute_ms = ms;
     ctx.last.levels = levels;
     ctx.last.supersteps = max_depth;  // Fulgora always runs supersteps 0..maxDepth
-    for (int64_t l = 0; l < rows; ++l) dist_out[sh.dense_of_local[l]] = host[l];
+    for (int64_t l = 0; l < rows; ++l) dist_out[sh.dense_of_local()[l]] = host[l];
     prof_collect(ctx, g);
 }
 
