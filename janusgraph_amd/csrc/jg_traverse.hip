@@ -778,6 +778,12 @@ __global__ void degree_bound_kernel(const int64_t* __restrict__ rp, int64_t rows
     *out = lo;
 }
 
+constexpr int kMaxPeersMs = 64;
+__device__ __forceinline__ int slot_peer(int32_t u, int tbits, int r) {
+    const int seg = (int)((uint32_t)u >> tbits);
+    return seg <= r ? seg - 1 : seg;
+}
+
 struct MsTd {
     const int32_t* queue;
     const int64_t* qoff;
@@ -797,11 +803,19 @@ struct MsTd {
     int32_t* hlist;
     int64_t* hlist_off;        // scratch of the appender
     unsigned long long* hpacked;
+    // sparse reverse exchange (nullable): pcnt[q] += the slots about peer q this level set first
+    unsigned long long* pcnt;
+    int r, P;                  // this shard's index, the shard count
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
     __shared__ WaveStage ws, hws;
+    __shared__ unsigned int lpc[kMaxPeersMs];
     WaveApp app{ws}, happ{hws};
+    if (a.pcnt) {
+        for (int q = threadIdx.x; q < a.P; q += blockDim.x) lpc[q] = 0u;
+        __syncthreads();
+    }
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -845,35 +859,22 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
             }
             app.append(take, u, 0, a.touched, a.touched_off, a.tpacked);
             if (a.hstage) happ.append(hfirst, u, 0, a.hlist, a.hlist_off, a.hpacked);
+            if (a.pcnt && hfirst) atomicAdd(&lpc[slot_peer(u, a.tbits, a.r)], 1u);
         }
     }
     app.final(a.touched, a.touched_off, a.tpacked);
     if (a.hstage) happ.final(a.hlist, a.hlist_off, a.hpacked);
+    if (a.pcnt) {
+        __syncthreads();
+        for (int q = threadIdx.x; q < a.P; q += blockDim.x)
+            if (lpc[q]) atomicAdd(&a.pcnt[q], (unsigned long long)lpc[q]);
+    }
 }
 
 // ---- sparse reverse exchange of a sharded top-down level (only the staging slots the level set) ----
 // A staging slot u (compact position, segment u >> tbits >= 1) is about peer q = seg - 1 if seg <= r,
 // else seg (the inverse of Halo::seg_of for shard r); it travels as (offset in the segment, word): the
 // offset is the slot's position in q's send list for r, so q finds its own row as send_src[send_off[r] + o].
-constexpr int kMaxPeersMs = 64;
-__device__ __forceinline__ int slot_peer(int32_t u, int tbits, int r) {
-    const int seg = (int)((uint32_t)u >> tbits);
-    return seg <= r ? seg - 1 : seg;
-}
-
-// cnt[q] += the slots of hlist[0, nh) about peer q (LDS histogram, one global atomic per block and peer)
-__global__ __launch_bounds__(kBlock) void msbfs_pair_count_kernel(const int32_t* __restrict__ hlist, int64_t nh,
-                                                                  int tbits, int r, int P,
-                                                                  unsigned long long* __restrict__ cnt) {
-    __shared__ unsigned int lc[kMaxPeersMs];
-    for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
-    __syncthreads();
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nh; k += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&lc[slot_peer(hlist[k], tbits, r)], 1u);
-    __syncthreads();
-    for (int q = threadIdx.x; q < P; q += blockDim.x)
-        if (lc[q]) atomicAdd(&cnt[q], (unsigned long long)lc[q]);
-}
 
 struct PairRuns {
     int64_t off[kMaxPeersMs + 1];       // pack: the run of peer q starts at pair off[q]; receive: from q at off[q]
@@ -2175,7 +2176,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             MsTd a{td.queue[qc].get(), td.qoff[qc].get(), td.nq, td.mf, c.push->row_ptr.get(),
                                    c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
                                    td.touched_off.get(), td.ctr.get() + 1, td_shard ? sh.halo_both.tbits : 31,
-                                   td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2};
+                                   td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2,
+                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P};
                             msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                   (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                               kBlock, 0, sh.stream>>>(a);
@@ -2195,14 +2197,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         for (size_t i = 0; i < g.shards.size(); ++i) {
                             Shard& sh = *g.shards[i];
                             DeviceGuard dg(sh.device);
-                            unsigned long long hh = 0;
-                            copy_d2h(&hh, tds[i].ctr.get() + 2, sizeof hh, sh.stream);
-                            const int64_t nh = (int64_t)(hh >> kPackShift);
-                            if (nh > 0) {
-                                msbfs_pair_count_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(
-                                    tds[i].hlist.get(), nh, sh.halo_both.tbits, sh.index, P, tds[i].pcnt.get());
-                                JG_LAUNCH_CHECK();
-                            }
+                            // per-peer slot counts: the top-down kernel counted the slots it set first
                             std::vector<unsigned long long> c((size_t)P);
                             copy_d2h(c.data(), tds[i].pcnt.get(), (size_t)P * sizeof(unsigned long long), sh.stream);
                             for (int q = 0; q < P; ++q) {
