@@ -354,8 +354,8 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
         msb["roofline"] = hbm_roofline(st["algorithmic_bytes"], ms, "64-source bit-parallel BFS (MsBfsOp merge / "
                                        "light kernels + msbfs_* kernels)", wl_ms,
                                        "per pull level 12 B per entry of a live merge task and of the light rows "
-                                       "+ 24 B per row; per top-down level 12 B per frontier entry + 16 B per "
-                                       "touched word + 8 B per queued vertex; 4 B per reached (source, row) depth")
+                                       "+ 32 B per row (incl. the level's new-bit word: the depths); per top-down "
+                                       "level 12 B per frontier entry + 24 B per touched word + 8 B per queued vertex")
         msb["entries_examined"] = st["edges_traversed"]
     else:
         msb["per_rank"] = per_rank_rows(ctl.gather([st["compute_ms"], st["exchange_ms"]]))

@@ -444,6 +444,8 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
 }
 
 // ---------------- bit-parallel multi-source BFS (pull, OR semiring) ----------------
+// levels 0 .. kMsLevelWords-1 record their depths as one new-bit word per own row (MsBfsOp::nwl)
+constexpr int kMsLevelWords = 12;
 struct MsBfsOp {
     using T = unsigned long long;
     const T* __restrict__ F;    // frontier words of the previous level, full length
@@ -454,6 +456,10 @@ struct MsBfsOp {
     // scattered depth writes (RMAT-26, 64 sources: 2.1 instead of 8.6 GB); widened to int32 planes on the
     // host's request (output) or when a traversal reaches level 255 (msbfs_widen_kernel)
     uint8_t* __restrict__ depth8;
+    // this level's new-bit words of the own rows ([rows], nullable): levels below kMsLevelWords record
+    // their depths here, one coalesced word per finalised row instead of a scattered byte per (source,
+    // row) (msbfs_levels_to_planes_kernel turns them into planes when the host asks)
+    unsigned long long* __restrict__ nwl;
     int32_t* __restrict__ changed;
     int64_t rows;
     VecPos pos;                 // owned row -> its slot in the gathered vector
@@ -472,13 +478,14 @@ struct MsBfsOp {
     __device__ __forceinline__ void finalize(int64_t row, T acc) const {
         T nw = acc & ~visited[row] & *live;
         Fout[pos(row)] = nw;
+        if (nwl) nwl[row] = nw;
         if (nw) {
             visited[row] |= nw;
             *changed = 1;
             while (nw) {
                 const int s = __ffsll(nw) - 1;
                 if (depth8) depth8[(int64_t)s * rows + row] = (uint8_t)lvl;
-                else depth[(int64_t)s * rows + row] = lvl;
+                else if (depth) depth[(int64_t)s * rows + row] = lvl;
                 nw &= nw - 1;
             }
         }
@@ -589,6 +596,22 @@ __global__ void msbfs_widen_kernel(const uint8_t* __restrict__ d8, int64_t n, in
     }
 }
 
+// Levels recorded as new-bit words ([levels][rows]) into int32 depth planes (plane s, row r = the level
+// whose word holds bit s; pairs no recorded level holds keep what the planes had: a later level's
+// depth, or -1)
+__global__ void msbfs_levels_to_planes_kernel(const unsigned long long* __restrict__ nwl, int levels, int64_t rows,
+                                              int nsrc, int32_t* __restrict__ depth) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
+        for (int L = 0; L < levels; ++L) {
+            unsigned long long w = nwl[(int64_t)L * rows + r];
+            while (w) {
+                const int s = __ffsll(w) - 1;
+                if (s < nsrc) depth[(int64_t)s * rows + r] = L;
+                w &= w - 1;
+            }
+        }
+}
+
 // pairs += the set bits of visited[0, rows) (sources x reached rows: the depth entries written)
 __global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long long* __restrict__ visited, int64_t rows,
                                                              unsigned long long* __restrict__ pairs) {
@@ -600,8 +623,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long
 }
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
-                                  unsigned long long* __restrict__ visited, uint8_t* __restrict__ depth, int64_t rows,
-                                  VecPos pos) {
+                                  unsigned long long* __restrict__ visited, unsigned long long* __restrict__ nw0,
+                                  int64_t rows, VecPos pos) {
     // sequential over the (<= 64) sources: several sources may share a vertex
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     for (int s = 0; s < nsrc; ++s) {
@@ -609,7 +632,7 @@ __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsr
         if (l < 0) continue;
         F[pos(l)] |= 1ull << s;
         visited[l] |= 1ull << s;
-        depth[(int64_t)s * rows + l] = 0;
+        nw0[l] |= 1ull << s;  // level 0's new-bit word
     }
 }
 
@@ -971,6 +994,14 @@ inline void zero_words(std::initializer_list<std::pair<void*, size_t>> bufs, hip
     JG_LAUNCH_CHECK();
 }
 
+// the same with the count in a packed device counter (no host read-back)
+__global__ void msbfs_zero_list_packed_kernel(unsigned long long* __restrict__ v, const int32_t* __restrict__ list,
+                                              const unsigned long long* __restrict__ packed) {
+    const int64_t n = (int64_t)(*packed >> kPackShift);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[list[i]] = 0ull;
+}
+
 // v[list[i]] = 0 for i < n: clears the words a level set (its frontier rows, or its halo staging slots)
 // without a pass over the whole vector
 __global__ void msbfs_zero_list_kernel(unsigned long long* __restrict__ v, const int32_t* __restrict__ list, int64_t n) {
@@ -1019,7 +1050,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_recv_kernel(const unsigned lo
 
 // touched vertex u: its new bits become its next-frontier word (and the visited / depth updates);
 // *live_out |= the OR of the new words (the next pull level's live bits: untouched rows hold zero)
-__global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* __restrict__ touched, int64_t nt,
+__global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* __restrict__ touched,
+                                                                const unsigned long long* __restrict__ tcount,
                                                                 MsBfsOp op, const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
                                                                 unsigned long long* __restrict__ packed,
@@ -1028,6 +1060,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
     __shared__ unsigned long long red[kBlock / kWave];
     WaveApp app{ws};
     unsigned long long lv = 0;
+    // the touched count from the device (packed counter): the host does not wait for it
+    const int64_t nt = (int64_t)(*tcount >> kPackShift);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < nt; x0 += stride) {  // block-uniform trips
         const int64_t x = x0 + threadIdx.x;
@@ -1886,7 +1920,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             struct St {
                 DevBuf<unsigned long long> F[2], vis;
                 DevBuf<int32_t> depth, changed;  // depth: int32 planes once widened
-                DevBuf<uint8_t> depth8;           // byte planes while every level is below 255
+                DevBuf<uint8_t> depth8;           // byte planes of levels kMsLevelWords .. 254 (allocated on reaching them)
+                DevBuf<unsigned long long> nwl;   // [kMsLevelWords][rows] new-bit words of levels 0 .. kMsLevelWords-1
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
@@ -1940,7 +1975,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.F[0].alloc(len);
                 t.F[1].alloc(len);
                 t.vis.alloc(std::max<int64_t>(sh.rows, 1));
-                t.depth8.alloc(std::max<int64_t>(sh.rows * ns, 1));
+                t.nwl.alloc(std::max<int64_t>(sh.rows * kMsLevelWords, 1));
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
@@ -1967,7 +2002,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.depth8.get(), 0xFF, t.depth8.bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.nwl.get(), 0, t.nwl.bytes(), sh.stream));
                 std::vector<int64_t> loc(ns, -1);
                 for (int s = 0; s < ns; ++s)
                     if (src_local[(size_t)s] >= 0 && src_shard[(size_t)s] == sh.index) loc[s] = src_local[(size_t)s];
@@ -1977,7 +2012,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         tds[i].src_rows.push_back(l);
                 DevBuf<int64_t> dloc(ns);
                 copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
-                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.depth8.get(),
+                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.nwl.get(),
                                                           sh.rows, g.vec_pos(sh, adj_of(sh, c)));
                 JG_LAUNCH_CHECK();
                 JG_HIP(hipStreamSynchronize(sh.stream));
@@ -1994,13 +2029,16 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             int cur = 0, level = 0, qc = 0;
             int64_t g_nq = 0, g_mf = 0;  // the current frontier's vertices and push entries, all shards and ranks
-            auto read_frontier = [&]() {
+            // touched (nullable): += the rows the top-down level just applied (its touched counter)
+            auto read_frontier = [&](double* touched = nullptr) {
                 int64_t v[2] = {0, 0};
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
                     DeviceGuard dg(sh.device);
-                    unsigned long long h = 0;
-                    copy_d2h(&h, tds[i].ctr.get(), sizeof h, sh.stream);
+                    unsigned long long hh[2] = {0, 0};
+                    copy_d2h(hh, tds[i].ctr.get(), (touched ? 2 : 1) * sizeof(unsigned long long), sh.stream);
+                    const unsigned long long h = hh[0];
+                    if (touched) *touched += (double)(hh[1] >> kPackShift);
                     tds[i].nq = (int64_t)(h >> kPackShift);
                     tds[i].mf = (int64_t)(h & kEdgeMask);
                     v[0] += tds[i].nq;
@@ -2089,19 +2127,52 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             // queued: tds[i].queue[qc] holds the current frontier; live_ready: live[0] holds its live bits
             // (both from the previous level's end)
-            // byte depth planes hold levels 0..254: a traversal about to write level 255 widens them first
+            // Depths: levels 0 .. kMsLevelWords-1 as new-bit words (nwl), levels up to 254 as byte planes
+            // (allocated, all 255 = unreached, when the traversal reaches them), beyond as int32 planes (a
+            // traversal about to write level 255 widens the byte planes first)
+            auto ensure_depth8 = [&]() {
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    if (t.depth8.size() || t.depth.size()) continue;
+                    DeviceGuard dg(sh.device);
+                    t.depth8.alloc(std::max<int64_t>(sh.rows * ns, 1));
+                    JG_HIP(hipMemsetAsync(t.depth8.get(), 0xFF, t.depth8.bytes(), sh.stream));
+                }
+            };
             auto widen = [&]() {
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
                     St& t = st[i];
-                    if (!t.depth8.size()) continue;
+                    if (t.depth.size()) continue;
                     DeviceGuard dg(sh.device);
                     const int64_t total = std::max<int64_t>(sh.rows * ns, 1);
                     t.depth.alloc(total);
-                    msbfs_widen_kernel<<<grid_for(total), kBlock, 0, sh.stream>>>(t.depth8.get(), total, t.depth.get());
-                    JG_LAUNCH_CHECK();
+                    if (t.depth8.size()) {
+                        msbfs_widen_kernel<<<grid_for(total), kBlock, 0, sh.stream>>>(t.depth8.get(), total, t.depth.get());
+                        JG_LAUNCH_CHECK();
+                    } else {
+                        fill_i32_kernel<<<grid_for(total), kBlock, 0, sh.stream>>>(t.depth.get(), total, -1);
+                        JG_LAUNCH_CHECK();
+                    }
                     JG_HIP(hipStreamSynchronize(sh.stream));
                     t.depth8.reset();
+                }
+            };
+            // the caller's int32 planes: the widened byte / int32 planes, then the word-recorded levels
+            auto materialize = [&](int levels_run) {
+                widen();
+                for (size_t i = 0; i < g.shards.size(); ++i) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    DeviceGuard dg(sh.device);
+                    const int lw = std::min(levels_run + 1, kMsLevelWords);
+                    if (sh.rows > 0) {
+                        msbfs_levels_to_planes_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.nwl.get(), lw, sh.rows,
+                                                                                                   ns, t.depth.get());
+                        JG_LAUNCH_CHECK();
+                    }
+                    JG_HIP(hipStreamSynchronize(sh.stream));
                 }
             };
             // one shard: pull levels whose frontier holds at least msbfs_bu_frac / 1000 of the rows run
@@ -2135,6 +2206,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int pull_levels = 0, sparse_levels = 0;
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
+                if (level + 1 >= kMsLevelWords) ensure_depth8();
                 if (level + 1 >= 255) widen();
                 const bool td_level = td_ok && (double)g_mf < (double)push_nnz / (double)tune().bfs_alpha;
                 if (td_level && !queued) {
@@ -2291,35 +2363,35 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         const BfsCsrs c = pick_csrs(sh, direction);
                         St& t = st[i];
                         Td& td = tds[i];
-                        unsigned long long th[2] = {0, 0};
-                        copy_d2h(th, td.ctr.get() + 1, sizeof th, sh.stream);
-                        const int64_t nt = (int64_t)(th[0] >> kPackShift), nh = (int64_t)(th[1] >> kPackShift);
-                        if (nh > 0) {  // the staging slots went out with the reverse exchange: back to zero
-                            msbfs_zero_list_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(td.hs.get(), td.hlist.get(), nh);
+                        // counts stay on the device (the apply and the clearing read them there): one host
+                        // read-back per level, read_frontier's
+                        if (td_shard) {  // the staging slots went out with the reverse exchange: back to zero
+                            msbfs_zero_list_packed_kernel<<<grid_for(sh.halo_both.recv_off[(size_t)g.P]), kBlock, 0, sh.stream>>>(
+                                td.hs.get(), td.hlist.get(), td.ctr.get() + 2);
                             JG_LAUNCH_CHECK();
                         }
                         td_entries += (double)td.mf;
-                        td_touched += (double)nt;
                         td_queued += (double)td.nq;
-                        if (nt > 0) {
+                        {
                             MsBfsOp op;
                             op.F = t.F[cur].get();
                             op.Fout = t.F[cur ^ 1].get();
                             op.visited = t.vis.get();
                             op.depth = t.depth.get();
-                            op.depth8 = t.depth8.get();
+                            op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
+                            op.nwl = level + 1 < kMsLevelWords && tune().msbfs_diag != 1 ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
                             op.changed = t.changed.get();
                             op.rows = sh.rows;
                             op.pos = g.vec_pos(sh, adj_of(sh, c));
                             op.lvl = level + 1;
                             op.live = t.live.get() + 1;
-                            msbfs_td_apply_kernel<<<grid_for(nt), kBlock, 0, sh.stream>>>(
-                                td.touched.get(), nt, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
+                            msbfs_td_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                td.touched.get(), td.ctr.get() + 1, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
                                 td.qoff[qc ^ 1].get(), td.ctr.get(), t.live.get());
                             JG_LAUNCH_CHECK();
                         }
                     }
-                    read_frontier();
+                    read_frontier(&td_touched);
                     combine_live();
                     qc ^= 1;
                     queued = live_ready = true;
@@ -2345,7 +2417,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.Fout = t.F[cur ^ 1].get();
                         op.visited = t.vis.get();
                         op.depth = t.depth.get();
-                        op.depth8 = t.depth8.get();
+                        op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
+                            op.nwl = level + 1 < kMsLevelWords && tune().msbfs_diag != 1 ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
                         op.changed = t.changed.get();
                         op.rows = sh.rows;
                         op.pos = g.vec_pos(sh, adj_of(sh, c));
@@ -2407,15 +2480,21 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     need_fwd = g.P > 1;
                 }
                 int32_t any = 0;
-                for (size_t i = 0; i < g.shards.size(); ++i) {
-                    Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
-                    int32_t ch = 0;
-                    JG_HIP(hipMemcpyAsync(&ch, st[i].changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
-                    JG_HIP(hipStreamSynchronize(sh.stream));
-                    any |= ch;
+                if (td_ok) {
+                    // the level's new frontier (counted over all shards and ranks by read_frontier) is
+                    // exactly the rows that gained a bit: no read-back of the changed flags
+                    any = g_nq > 0;
+                } else {
+                    for (size_t i = 0; i < g.shards.size(); ++i) {
+                        Shard& sh = *g.shards[i];
+                        DeviceGuard dg(sh.device);
+                        int32_t ch = 0;
+                        JG_HIP(hipMemcpyAsync(&ch, st[i].changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
+                        JG_HIP(hipStreamSynchronize(sh.stream));
+                        any |= ch;
+                    }
+                    any = allreduce_or(g, any);
                 }
-                any = allreduce_or(g, any);
                 cur ^= 1;
                 ++level;
                 if (!any) break;
@@ -2428,9 +2507,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             max_levels = std::max(max_levels, level);
             // the work of this batch, counted after its timed region: per pull level 12 B per entry of a
             // live merge task (col + gathered frontier word; a task streams its 512 slots) and of the light
-            // rows, 24 B per row (visited, the new word, the next level's live scan); per top-down level
-            // 12 B per frontier entry, 16 B per touched word and 8 B per queued vertex; 4 B per reached
-            // (source, row) pair: its depth entry
+            // rows, 32 B per row (visited, the new frontier word, the level's new-bit word, the next
+            // level's live scan); per top-down level 12 B per frontier entry, 24 B per touched word and 8 B
+            // per queued vertex; past kMsLevelWords levels 4 B per reached (source, row) pair (a plane entry)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
@@ -2442,12 +2521,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels : (double)w[0];
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
                 work_entries += entries;
-                work_bytes += 12.0 * entries + 24.0 * (double)sh.rows * (pull_levels + bu_levels) + 4.0 * (double)w[1];
+                work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +
+                              (level >= kMsLevelWords ? 4.0 * (double)w[1] : 0.0);
             }
             work_entries += td_entries;
-            work_bytes += 12.0 * td_entries + 16.0 * td_touched + 8.0 * td_queued;
+            work_bytes += 12.0 * td_entries + 24.0 * td_touched + 8.0 * td_queued;
             if (depth_rows) {
-                widen();  // the caller's int32 rows
+                materialize(level);  // the caller's int32 rows
                 for (size_t i = 0; i < g.shards.size(); ++i)
                     for (int s = 0; s < ns; ++s)
                         if (depth_rows[b0 + s])
