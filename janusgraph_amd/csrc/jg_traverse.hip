@@ -2239,7 +2239,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                     t.F[cur ^ 1].get(), td.queue[qc ^ 1].get(), td.nq_in);
                                 JG_LAUNCH_CHECK();
                             }
-                        } else {
+                        } else if (level > 0) {  // level 0: F[1] is as the init zeroed it
                             JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, (size_t)sh.rows * sizeof(unsigned long long),
                                                   sh.stream));
                         }
