@@ -697,6 +697,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().cc_push = value != 0;
     } else if (k == "band_sliced_build") {
         jg::tune().band_sliced_build = value != 0;
+    } else if (k == "msbfs_skip_first") {
+        jg::tune().msbfs_skip_first = value != 0;
     } else if (k == "msbfs_diag") {
         JG_ARG(value >= 0 && value <= 1, "msbfs_diag must be 0 or 1");
         jg::tune().msbfs_diag = (int)value;

@@ -538,6 +538,7 @@ struct Tune {
                                       // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
+    int msbfs_skip_first = 1;         //         bit-parallel BFS: no task bitmaps on the first pull level
     int msbfs_diag = 0;               //         diagnostic timing (wrong depths): 1 = no depth writes
     int msbfs_sparse = 1;             //         sharded bit-parallel BFS: top-down levels send only the set halo
                                       //         staging slots when they are under half the halo (0: always dense)

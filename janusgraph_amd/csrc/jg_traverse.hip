@@ -2204,6 +2204,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
             // counted on the device, or every task when the skip is off) and top-down frontier entries
             int pull_levels = 0, sparse_levels = 0;
+            int unskipped_levels = 0;  // pull levels that ran every merge task (msbfs_skip_first)
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
                 if (level + 1 >= kMsLevelWords) ensure_depth8();
@@ -2445,7 +2446,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             level_bu = true;
                         } else {
                         std::vector<const uint32_t*> tl;
-                        for (size_t b = 0; b < t.todo.size(); ++b) {
+                        // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows
+                        // can be done there; every task runs, the finalize's live mask keeps it exact)
+                        const bool no_bitmaps = tune().msbfs_skip_first && pull_levels == 0;
+                        if (no_bitmaps && i == 0) ++unskipped_levels;
+                        for (size_t b = 0; b < t.todo.size() && !no_bitmaps; ++b) {
                             const SliceBand& bd = *plan.bands[b];
                             if (bd.tasks == 0 || bd.rows() == 0) {
                                 tl.push_back(nullptr);
@@ -2518,7 +2523,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_LAUNCH_CHECK();
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
-                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels : (double)w[0];
+                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels
+                                                          : (double)w[0] + (double)t.all_tasks * unskipped_levels;
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
                 work_entries += entries;
                 work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +

@@ -222,7 +222,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
 
 @pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
                                          ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
-                                         ("skip_dense_reverse", 3), ("skip_dense", 2)])
+                                         ("skip_dense_reverse", 3), ("skip_dense", 2), ("skip_every_level", 1),
+                                         ("skip_every_level", 3)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -230,7 +231,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     holds every source), on one shard and on logical shards (halo and dense vectors).  On sharded halo
     plans the small-frontier levels run top-down (own rows pushed, peers' bits returned by the reverse
     halo exchange, sparse (offset, word) pairs when few staging slots are set, the whole segments with
-    skip_dense_reverse); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2)."""
+    skip_dense_reverse); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2).
+    The first pull level runs every task by default (msbfs_skip_first); skip_every_level builds the
+    task bitmaps on that level too."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
@@ -238,7 +241,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
                              ("band2_deg", 4), ("band2_bit", 3)],
              "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
              "skip_dense": [("halo", 0)], "skip_sharded_pull_only": [("msbfs_td", 2)],
-             "skip_dense_reverse": [("msbfs_sparse", 0)]}[mode]
+             "skip_dense_reverse": [("msbfs_sparse", 0)], "skip_every_level": [("msbfs_skip_first", 0)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
     vid = np.concatenate([vid0, (np.arange(3, dtype=np.int64) + n0 + 1) << 8 | 7])
