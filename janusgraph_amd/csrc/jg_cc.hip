@@ -12,6 +12,8 @@
 // String order of non-negative ids: compare x*10^(19-digits(x)) (19-digit left-aligned decimal),
 // ties (a prefix such as "1" < "10") broken by fewer digits — computed with two stable radix sorts.
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 
 #include "jg_frontier.h"
 #include "jg_pull.h"
@@ -75,6 +77,10 @@ __global__ void lex_padded_kernel(const int64_t* __restrict__ vid, const uint32_
 __global__ void lex_rank_scatter_kernel(const uint32_t* __restrict__ vals, int64_t n, int32_t* __restrict__ rank_of) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
         rank_of[vals[r]] = (int32_t)r;
+}
+
+__global__ void iota_i32_kernel(int32_t* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = (int32_t)i;
 }
 
 __global__ void iota_i64_kernel(int64_t* __restrict__ p, int64_t n) {
@@ -408,6 +414,394 @@ void exchange_msg(Graph& g, int which) {
     exchange_vec(g, JG_ADJ_BOTH, bufs, sizeof(int32_t), ncclInt32);
 }
 
+// ---- sharded (halo plans): local union-finds, tree labels over the halo, a multi-root sharded BFS ----
+// Each shard runs Afforest over its own rows' BOTH entries in its compact vector space (own rows
+// [0, rows), then one segment per peer), so a local tree joins own rows and halo copies of their
+// neighbours.  A global component is the union of local trees that share a vertex (a copy on one
+// shard, the row on its owner), and each cross edge {v on s, x on q} needs linking on ONE side only,
+// because labels then flow both ways between a copy and its owner:
+//  * a row outside its shard's giant tree (snapshot after the first round) links all its entries, so
+//    an edge with such an endpoint is linked on that endpoint's side;
+//  * an edge between two giant trees (v in s's, x in q's, `flag` bits from q by exchange_halo_bits) is
+//    covered once s's giant tree holds a copy of ANY vertex of q's giant tree: a bounded search over sampled
+//    entries of the hub rows links one and marks the peer found; a peer not found falls back to linking
+//    every flagged entry of the giant rows into its segment;
+// so the giant rows scan nothing on RMAT (one-shard Afforest skips them the same way).
+// Label rounds: own labels go to the copies (forward halo exchange), every tree takes the minimum over
+// its members, own rows take their tree's, copies take their tree's and send it back to the owners
+// (reverse halo exchange, min); until no label changes anywhere.  The superstep count then comes from
+// one sharded DO-BFS started at every component's minimum-rank vertex (cc_root_eccentricity_sharded).
+
+constexpr int kCcSearchRows = 64, kCcSearchEntries = 2048;
+
+struct CcShardLink {
+    int32_t* parent;
+    const int64_t* rp;
+    const int32_t* col;
+    int64_t rows, ne, heavy;
+    int k;
+    const unsigned long long* flag;  // compact bitmap: own rows in this shard's giant tree, copies in their owner's
+    int32_t* found;                  // [P] by segment: a copy of the peer's giant tree is in this shard's
+    int all_found, tbits;
+};
+
+__device__ __forceinline__ bool flag_of(const unsigned long long* f, int32_t x) { return (f[x >> 6] >> (x & 63)) & 1ull; }
+
+// own rows' bits of the flag bitmap (one wave per word): row in the giant tree after the first round
+__global__ __launch_bounds__(kBlock) void cc_own_flags_kernel(const int32_t* __restrict__ parent, int64_t ne,
+                                                               int64_t rows, int32_t giant, unsigned long long* flag) {
+    const int64_t words = (rows + 63) / 64;
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words;
+         w += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+        const int64_t v = w * 64 + lane_id();
+        const uint64_t word = __ballot(v < ne && parent[v] == giant);
+        if (lane_id() == 0) flag[w] = word;
+    }
+}
+
+// send-list words for exchange_halo_bits: bit b of word w = the row at that send-list position is in
+// the giant tree (a thread per word)
+__global__ void cc_pack_flags_kernel(const int32_t* __restrict__ parent, int32_t giant,
+                                     const int32_t* __restrict__ send_src, const int64_t* __restrict__ send_off,
+                                     const int64_t* __restrict__ woff, int P, unsigned long long* __restrict__ sw) {
+    const int64_t words = woff[P];
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+        int q = 0;
+        while (q + 1 < P && woff[q + 1] <= w) ++q;
+        const int64_t x0 = send_off[q] + (w - woff[q]) * 64, x1 = send_off[q + 1];
+        unsigned long long word = 0;
+        for (int b = 0; b < 64 && x0 + b < x1; ++b)
+            if (parent[send_src[x0 + b]] == giant) word |= 1ull << b;
+        sw[w] = word;
+    }
+}
+
+// the bounded search: kCcSearchEntries entries of each of the first kCcSearchRows giant rows (a wave
+// each) link the flagged copies they meet and mark their segments found
+__global__ __launch_bounds__(kBlock) void cc_giant_search_kernel(CcShardLink a) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int64_t nr = a.ne < kCcSearchRows ? a.ne : kCcSearchRows;
+    if (wave >= nr || !flag_of(a.flag, (int32_t)wave)) return;
+    // kCcSearchEntries entries spread evenly over the row (its columns may be ordered by segment)
+    const int64_t e0 = a.rp[wave], deg = a.rp[wave + 1] - e0;
+    const int64_t n = deg < kCcSearchEntries ? deg : kCcSearchEntries;
+    for (int64_t j = lane_id(); j < n; j += kWave) {
+        const int32_t u = a.col[e0 + j * deg / n];
+        if (u >= a.rows && flag_of(a.flag, u)) {
+            uf_link(a.parent, (int32_t)wave, u);
+            a.found[u >> a.tbits] = 1;
+        }
+    }
+}
+
+// the second round: rows outside the giant tree link their remaining entries; giant rows link the
+// flagged copies of peers the search did not find (nothing when all were found).  Rows below `heavy`
+// (degree >= 64) take a wave each, the others a thread.  *linked += the entries scanned.
+__global__ __launch_bounds__(kBlock) void cc_link_rest_sharded_kernel(CcShardLink a,
+                                                                       unsigned long long* __restrict__ linked) {
+    const int lane = lane_id();
+    unsigned long long count = 0;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
+    for (int64_t v = wave; v < a.heavy; v += nwaves) {  // wave-uniform
+        const bool giant = flag_of(a.flag, (int32_t)v);
+        if (giant && a.all_found) continue;
+        if (lane == 0) count += (unsigned long long)(a.rp[v + 1] - a.rp[v] - a.k);
+        for (int64_t e = a.rp[v] + a.k + lane; e < a.rp[v + 1]; e += kWave) {
+            const int32_t u = a.col[e];
+            if (u == (int32_t)v) continue;
+            if (!giant || (u >= a.rows && !a.found[u >> a.tbits] && flag_of(a.flag, u))) uf_link(a.parent, (int32_t)v, u);
+        }
+    }
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = a.heavy + tid; v < a.ne; v += nt) {
+        if (a.rp[v + 1] - a.rp[v] <= a.k) continue;
+        const bool giant = flag_of(a.flag, (int32_t)v);
+        if (giant && a.all_found) continue;
+        count += (unsigned long long)(a.rp[v + 1] - a.rp[v] - a.k);
+        for (int64_t e = a.rp[v] + a.k; e < a.rp[v + 1]; ++e) {
+            const int32_t u = a.col[e];
+            if (u == (int32_t)v) continue;
+            if (!giant || (u >= a.rows && !a.found[u >> a.tbits] && flag_of(a.flag, u))) uf_link(a.parent, (int32_t)v, u);
+        }
+    }
+    count = wave_reduce_add(count);
+    if (lane == 0 && count) atomicAdd(linked, count);
+}
+
+// T[root] = the minimum over the tree's members: own rows with an edge their labels, copies (positions
+// from `rows` on holding a label, i.e. < kNoMsg) their owners'; the giant tree's through a block
+// reduction (one atomic per block)
+__global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(const int32_t* __restrict__ parent,
+                                                              const int32_t* __restrict__ label, int64_t ne,
+                                                              int64_t rows, const int32_t* __restrict__ msg,
+                                                              int64_t len, int32_t giant, int32_t* __restrict__ tmin) {
+    __shared__ int32_t red[kBlock / kWave];
+    int32_t g = INT_MAX;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len; x += (int64_t)gridDim.x * blockDim.x) {
+        if (x < rows && x >= ne) continue;
+        const int32_t m = x < rows ? label[x] : msg[x];
+        if (m >= kNoMsg) continue;
+        const int32_t r = parent[x];
+        if (r == giant) g = m < g ? m : g;
+        else if (m < tmin[r]) atomicMin(&tmin[r], m);
+    }
+    g = wave_reduce_min(g);
+    if (lane_id() == 0) red[wave_id()] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) g = red[w] < g ? red[w] : g;
+        if (g != INT_MAX && giant >= 0) atomicMin(&tmin[giant], g);
+    }
+}
+
+// own rows with an edge take their tree's minimum (labels only decrease); copies take it too, for the
+// reverse exchange
+__global__ void cc_tree_apply_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ tmin, int64_t ne,
+                                     int64_t rows, int64_t len, int32_t* __restrict__ label, int32_t* __restrict__ msg,
+                                     int32_t* __restrict__ changed) {
+    bool ch = false;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len; x += (int64_t)gridDim.x * blockDim.x) {
+        if (x < ne) {
+            const int32_t t = tmin[parent[x]];
+            if (t < label[x]) {
+                label[x] = t;
+                ch = true;
+            }
+        } else if (x >= rows && msg[x] < kNoMsg) {
+            msg[x] = tmin[parent[x]];
+        }
+    }
+    if (__ballot(ch) && lane_id() == 0) *changed = 1;
+}
+
+// the copies' tree minima back at the owners (element j is about own row send_src[j])
+__global__ void cc_reverse_apply_kernel(const int32_t* __restrict__ rbuf, const int32_t* __restrict__ send_src, int64_t n,
+                                        int32_t* __restrict__ label, int32_t* __restrict__ changed) {
+    bool ch = false;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = send_src[j], m = rbuf[j];
+        if (m < label[v]) {
+            atomicMin(&label[v], m);
+            ch = true;
+        }
+    }
+    if (__ballot(ch) && lane_id() == 0) *changed = 1;
+}
+
+// Every shard of the process (halo plans; cc_label holds the ranks).  false (labels untouched, message
+// vectors to be re-initialised) if the superstep count reaches the cap; else each shard's labels are
+// in cc_label.
+bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* work_bytes) {
+    const size_t ns = g.shards.size();
+    const int P = g.P;
+    struct St {
+        DevBuf<int32_t> tmin, label, rank, found, rbuf;
+        DevBuf<int64_t> send_off, woff;
+        DevBuf<unsigned long long> flag, sw;
+        int64_t ne = 0, len = 0, heavy = 0, nsend = 0;
+        int32_t giant = -1;
+        int giant_share = 0, all_found = 0;
+    };
+    std::vector<St> st(ns);
+    const int kFirst = std::max(1, tune().cc_first);
+    double bytes = 0;
+    DevBuf<unsigned long long> linked(ns);
+    auto link_args = [&](size_t i) {
+        Shard& sh = *g.shards[i];
+        St& t = st[i];
+        return CcShardLink{sh.cc_msg[1].get(), sh.both.row_ptr.get(), sh.both.col.get(), sh.rows, t.ne, t.heavy, kFirst,
+                           t.flag.get(), t.found.get(), t.all_found, sh.halo_both.tbits};
+    };
+    // first round, giant sample, own flags, send-list flags
+    std::vector<uint64_t*> swv, flv;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        hipStream_t s = sh.stream;
+        St& t = st[i];
+        const Csr& c = sh.both;
+        const Halo& h = sh.halo_both;
+        t.ne = c.empty_from >= 0 ? std::min(c.empty_from, sh.rows) : sh.rows;
+        t.len = g.vec_len(sh, JG_ADJ_BOTH);
+        t.nsend = h.send_off[(size_t)P];
+        int32_t* parent = sh.cc_msg[1].get();
+        t.tmin.alloc(t.len);
+        t.label.alloc(std::max<int64_t>(sh.rows, 1));
+        t.rank.alloc(std::max<int64_t>(sh.rows, 1));
+        t.found.alloc(P);
+        t.rbuf.alloc(std::max<int64_t>(t.nsend, 1));
+        t.flag.alloc((t.len + 63) / 64);
+        const std::vector<int64_t> woff = halo_word_offsets(h, P);
+        t.sw.alloc(std::max<int64_t>(woff[(size_t)P], 1));
+        t.send_off.alloc(P + 1);
+        t.woff.alloc(P + 1);
+        copy_h2d(t.send_off.get(), h.send_off.data(), (P + 1) * sizeof(int64_t), s);
+        copy_h2d(t.woff.get(), woff.data(), (P + 1) * sizeof(int64_t), s);
+        JG_HIP(hipMemsetAsync(t.found.get(), 0, P * sizeof(int32_t), s));
+        JG_HIP(hipMemsetAsync(t.flag.get(), 0, t.flag.bytes(), s));
+        JG_HIP(hipMemsetAsync(linked.get() + i, 0, sizeof(unsigned long long), s));
+        if (sh.rows) {  // the ranks (cc_label) stay as they are until the labels are final
+            JG_HIP(hipMemcpyAsync(t.label.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+            JG_HIP(hipMemcpyAsync(t.rank.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        }
+        iota_i32_kernel<<<grid_for(t.len), kBlock, 0, s>>>(parent, t.len);
+        JG_LAUNCH_CHECK();
+        if (t.ne > 0) {
+            DevBuf<int32_t> sample(1025);
+            uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), t.ne, kFirst);
+            JG_LAUNCH_CHECK();
+            uf_compress_kernel<<<grid_for(t.len), kBlock, 0, s>>>(parent, t.len);
+            JG_LAUNCH_CHECK();
+            // the most frequent root among 1024 sampled own rows: the giant tree's
+            uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, t.ne, 1024, sample.get());
+            JG_LAUNCH_CHECK();
+            heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), t.ne, sample.get() + 1024);
+            JG_LAUNCH_CHECK();
+            std::vector<int32_t> hs(1025);
+            copy_d2h(hs.data(), sample.get(), hs.size() * sizeof(int32_t), s);
+            t.heavy = hs[1024];
+            hs.pop_back();
+            std::sort(hs.begin(), hs.end());
+            size_t best = 0;
+            for (size_t a = 0; a < hs.size();) {
+                size_t b = a;
+                while (b < hs.size() && hs[b] == hs[a]) ++b;
+                if (b - a > best) {
+                    best = b - a;
+                    t.giant = hs[a];
+                    t.giant_share = (int)best;
+                }
+                a = b;
+            }
+            cc_own_flags_kernel<<<grid_for(((sh.rows + 63) / 64) * kWave), kBlock, 0, s>>>(parent, t.ne, sh.rows, t.giant,
+                                                                                          t.flag.get());
+            JG_LAUNCH_CHECK();
+        }
+        if (woff[(size_t)P] > 0) {
+            cc_pack_flags_kernel<<<grid_for(woff[(size_t)P]), kBlock, 0, s>>>(parent, t.giant, h.send_src.get(),
+                                                                              t.send_off.get(), t.woff.get(), P,
+                                                                              t.sw.get());
+            JG_LAUNCH_CHECK();
+        }
+        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.get()));
+        flv.push_back(reinterpret_cast<uint64_t*>(t.flag.get()));
+    }
+    exchange_halo_bits(g, JG_ADJ_BOTH, swv, flv, false);  // the copies' flags: in their owner's giant tree
+    // the bounded search, then the second round
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        hipStream_t s = sh.stream;
+        St& t = st[i];
+        if (t.ne == 0) continue;
+        cc_giant_search_kernel<<<(kCcSearchRows * kWave + kBlock - 1) / kBlock, kBlock, 0, s>>>(link_args(i));
+        JG_LAUNCH_CHECK();
+        std::vector<int32_t> found((size_t)P);
+        copy_d2h(found.data(), t.found.get(), P * sizeof(int32_t), s);
+        const Halo& h = sh.halo_both;
+        t.all_found = 1;
+        for (int q = 0; q < P; ++q)
+            if (q != sh.index && h.recv_off[(size_t)q + 1] > h.recv_off[(size_t)q] && !found[(size_t)h.seg_of(q, sh.index)])
+                t.all_found = 0;
+        cc_link_rest_sharded_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(link_args(i), linked.get() + i);
+        JG_LAUNCH_CHECK();
+        uf_compress_kernel<<<grid_for(t.len), kBlock, 0, s>>>(sh.cc_msg[1].get(), t.len);
+        JG_LAUNCH_CHECK();
+    }
+    // the label rounds
+    std::vector<void*> mv, rv;
+    for (size_t i = 0; i < ns; ++i) {
+        mv.push_back(g.shards[i]->cc_msg[0].get());
+        rv.push_back(st[i].rbuf.get());
+    }
+    int rounds = 0;
+    for (bool any = true; any;) {
+        ++rounds;
+        for (size_t i = 0; i < ns; ++i) {  // own labels into the message vector's own part
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            if (st[i].ne)
+                JG_HIP(hipMemcpyAsync(sh.cc_msg[0].get(), st[i].label.get(), st[i].ne * sizeof(int32_t),
+                                      hipMemcpyDeviceToDevice, sh.stream));
+        }
+        exchange_msg(g, 0);
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
+            if (t.ne == 0) continue;
+            JG_HIP(hipMemsetAsync(t.tmin.get(), 0x7F, t.len * sizeof(int32_t), sh.stream));
+            cc_tree_min_kernel<<<grid_for(t.len), kBlock, 0, sh.stream>>>(sh.cc_msg[1].get(), t.label.get(), t.ne,
+                                                                          sh.rows, sh.cc_msg[0].get(), t.len, t.giant,
+                                                                          t.tmin.get());
+            JG_LAUNCH_CHECK();
+            cc_tree_apply_kernel<<<grid_for(t.len), kBlock, 0, sh.stream>>>(sh.cc_msg[1].get(), t.tmin.get(), t.ne,
+                                                                            sh.rows, t.len, t.label.get(),
+                                                                            sh.cc_msg[0].get(), sh.cc_changed.get());
+            JG_LAUNCH_CHECK();
+            // memset, parent + label/msg, tree minima; apply; reverse apply
+            bytes += 13.0 * (double)t.len + 12.0 * (double)t.len + 12.0 * (double)t.nsend;
+        }
+        exchange_halo_reverse(g, JG_ADJ_BOTH, mv, rv, sizeof(int32_t), ncclInt32);
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            St& t = st[i];
+            if (t.nsend) {
+                cc_reverse_apply_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
+                    t.rbuf.get(), sh.halo_both.send_src.get(), t.nsend, t.label.get(), sh.cc_changed.get());
+                JG_LAUNCH_CHECK();
+            }
+        }
+        int ch = 0;
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh.device);
+            int32_t c = 0;
+            copy_d2h(&c, sh.cc_changed.get(), sizeof c, sh.stream);
+            ch |= c;
+        }
+        any = allreduce_or(g, ch) != 0;
+    }
+    // the superstep count: one BFS from every component's minimum-rank vertex
+    std::vector<CcRoots> roots(ns);
+    for (size_t i = 0; i < ns; ++i) roots[i] = CcRoots{st[i].label.get(), st[i].rank.get(), nullptr, st[i].ne};
+    double reached = 0;
+    const int d = cc_root_eccentricity_sharded(g, roots.data(), &reached);
+    const int it = d + 1;  // 0 when no vertex has an edge (d = -1)
+    *rounds_out = rounds;
+    static const bool debug = std::getenv("JG_DEBUG_CC") != nullptr;
+    unsigned long long lk = 0;
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        St& t = st[i];
+        unsigned long long l = 0;
+        copy_d2h(&l, linked.get() + i, sizeof l, sh.stream);
+        lk += l;
+        if (debug)
+            std::fprintf(stderr, "[jg cc] shard %d: rows %lld with edges %lld, vector %lld, entries %lld, giant root %d "
+                         "(%d of 1024 sampled), all peers found %d, rest entries scanned %llu; %d label rounds, "
+                         "%d supersteps\n",
+                         sh.index, (long long)sh.rows, (long long)t.ne, (long long)t.len, (long long)sh.both.nnz,
+                         t.giant, t.giant_share, t.all_found, l, rounds, it);
+        // init 4 B, compressions 16 B, flags 1 B per slot; per row with an edge: first links 20 B, BFS
+        // start 17 B, depth and frontier probe 5 B
+        bytes += 21.0 * (double)t.len + 42.0 * (double)t.ne;
+        if (it <= kCcMaxIterations - 1 && sh.rows)
+            JG_HIP(hipMemcpyAsync(sh.cc_label.get(), t.label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                                  sh.stream));
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    if (it > kCcMaxIterations - 1) return false;
+    // 12 B per entry linked (col, both finds), 4 B per adjacency entry of the rows the BFS reached
+    *work_bytes = bytes + 12.0 * (double)lk + 4.0 * reached;
+    *iterations = it;
+    return true;
+}
+
 }  // namespace
 
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
@@ -529,6 +923,29 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
                 sh0.cc_label.get(), sh0.both.row_ptr.get(), sh0.rows, g.vec_pos(sh0, JG_ADJ_BOTH), sh0.cc_label.get(),
                 sh0.cc_msg[0].get());
             JG_LAUNCH_CHECK();
+        }
+    }
+    // Sharded over halo plans: the same from local union-finds, tree labels and a sharded BFS
+    // (cc_union_find_sharded); the sharded BFS takes at most 64 shards (jg_traverse.hip, kMaxShardsBfs).
+    int uf_rounds = 0;
+    if (!solved && g.P > 1 && g.P <= 64 && sh0.halo_both.on && tune().cc_uf && tune().cc_uf_sharded) {
+        solved = cc_union_find_sharded(g, &iteration, &uf_rounds, &uf_bytes);
+        if (solved) {
+            uf_labels = sh0.cc_label.get();
+        } else {  // the cap binds: the propagation runs, from fresh message vectors
+            for (auto& sp : g.shards) {
+                Shard& sh = *sp;
+                DeviceGuard dg(sh.device);
+                for (auto& m : sh.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh.stream));
+                if (sh.rows) {
+                    cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                        sh.cc_label.get(), sh.both.row_ptr.get(), sh.rows, g.vec_pos(sh, JG_ADJ_BOTH),
+                        sh.cc_label.get(), sh.cc_msg[0].get());
+                    JG_LAUNCH_CHECK();
+                }
+            }
+            exchange_msg(g, 0);
+            iteration = 0;
         }
     }
     while (!solved && any && iteration < kCcMaxIterations - 1) {

@@ -484,6 +484,9 @@ struct CcRoots {
 // vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).  *edges_out =
 // adjacency entries of the rows the traversal reached.
 int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out);
+// Sharded (halo plans, every shard of the process): the same from the rows whose label (r.parent) is
+// their rank, r.minr unused, one CcRoots per local shard; -1 if no vertex has an edge (jg_traverse.hip).
+int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);
 // Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
 void bfs_buffers(Shard& sh);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
@@ -553,6 +556,8 @@ struct Tune {
                                       //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
     int msbfs_bu_frac = 100;          //         permille of the rows
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
+    int cc_uf_sharded = 1;            //         sharded (halo plans): local union-find, tree labels over the halo,
+                                      //         multi-root sharded BFS for the superstep count (0: propagation)
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_init_suffix = 1;          //         DO-BFS init: empty rows from the plan's empty suffix (no row_ptr reads)

@@ -1632,8 +1632,35 @@ __global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t rows, int64
     }
 }
 
-// Sharded single-source DO-BFS over BOTH; returns levels run, *edges_out = entries of reached rows.
-int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth, double* edges_out, float* ms_out) {
+// Multi-root start of the sharded traversal (cc_root_eccentricity_sharded): an own row with an edge
+// whose label is its own rank is its component's minimum-rank vertex, a level-0 root.
+__global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(int32_t* __restrict__ dvec, int64_t rows, CcRoots r,
+                                                                 const int64_t* __restrict__ rp, int32_t* queue,
+                                                                 int64_t* qoff, unsigned long long* packed) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t v = x0 + threadIdx.x;
+        bool take = false;
+        int64_t deg = 0;
+        if (v < rows) {
+            if (v < r.ne) {
+                deg = rp[v + 1] - rp[v];
+                take = deg > 0 && r.parent[v] == r.rank[v];
+            }
+            dvec[v] = take ? 0 : -1;
+        }
+        app.append(take, (int32_t)v, deg, queue, qoff, packed);
+    }
+    app.final(queue, qoff, packed);
+}
+
+// Sharded DO-BFS over BOTH from one source (src_shard, src_local) or, with `roots` (one per local
+// shard), from every component's minimum-rank vertex; returns levels run, *edges_out = entries of
+// reached rows.  Depths go to Shard::bfs_depth for a single source only.
+int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth, double* edges_out, float* ms_out,
+                  const CcRoots* roots = nullptr) {
     const size_t ns = g.shards.size();
     struct St {
         DevBuf<int32_t> dvec, stamp, queue[2];
@@ -1643,7 +1670,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     };
     std::vector<St> st(ns);
     int64_t tot[2] = {0, 0};  // entries of all shards, rows of all shards
-    int64_t src_deg = 0;
+    int64_t src_deg = 0, nq0 = 0;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh.device);
@@ -1680,11 +1707,30 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.ctr.alloc(1);
+        if (roots) {
+            JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
+            if (sh.rows) {
+                sbfs_init_roots_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                    t.dvec.get(), sh.rows, roots[i], sh.both.row_ptr.get(), t.queue[0].get(), t.qoff[0].get(),
+                    t.ctr.get());
+                JG_LAUNCH_CHECK();
+            }
+            unsigned long long c = 0;
+            copy_d2h(&c, t.ctr.get(), sizeof c, sh.stream);
+            t.nq = (int64_t)(c >> kPackShift);
+            t.mf = (int64_t)(c & kEdgeMask);
+            nq0 += t.nq;
+            src_deg += t.mf;
+            tot[0] += sh.both.nnz;
+            tot[1] += sh.rows;
+            continue;
+        }
         const int64_t src = sh.index == src_shard ? src_local : -1;
         sbfs_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.dvec.get(), sh.rows, src, t.queue[0].get(),
                                                                       t.qoff[0].get());
         JG_LAUNCH_CHECK();
         t.nq = src >= 0 ? 1 : 0;
+        nq0 += t.nq;
         if (src >= 0) {
             int64_t b[2];
             copy_d2h(b, sh.both.row_ptr.get() + src, 2 * sizeof(int64_t), sh.stream);
@@ -1694,9 +1740,9 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         tot[0] += sh.both.nnz;
         tot[1] += sh.rows;
     }
-    int64_t init[3] = {tot[0], tot[1], src_deg};
-    allreduce_sum_i64(g, init, 3);
-    int64_t mu = init[0] - init[2], nf = 1, mf = init[2], edges = init[2];
+    int64_t init[4] = {tot[0], tot[1], src_deg, nq0};
+    allreduce_sum_i64(g, init, 4);
+    int64_t mu = init[0] - init[2], nf = init[3], mf = init[2], edges = init[2];
     const int64_t nrows = init[1];
     const double alpha = (double)tune().bfs_alpha, beta = (double)tune().bfs_beta;
     bool bu = false;
@@ -1827,7 +1873,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         JG_HIP(hipEventDestroy(t1));
     }
     // depths of the own rows
-    for (size_t i = 0; i < ns; ++i) {
+    for (size_t i = 0; i < ns && !roots; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh.device);
         if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
@@ -1841,6 +1887,11 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
 }
 
 }  // namespace
+
+int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out) {
+    float ms = 0;
+    return dobfs_sharded(g, -1, -1, -1, edges_out, &ms, roots) - 1;
+}
 
 int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out) {
     *edges_out = 0;

@@ -331,6 +331,7 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     comp, it = g.connected_components()
     ref, ref_it = oracle_lib.connected_components(n, ds, dd, vid)
     np.testing.assert_array_equal(comp, ref)
+    assert it == ref_it
     srcs = np.unique(ds)[:5]
     depth = g.bfs(vid[srcs], 3)
     for k in range(len(srcs)):
@@ -346,6 +347,44 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     assert g.info()["num_shards"] == shards
     g.close()
     c.close()
+
+
+@pytest.mark.parametrize("shards,uf", [(2, 1), (3, 1), (8, 1), (3, 0)])
+def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
+    """Logical shards over halo plans: local union-finds, tree labels spread over the halo, and one
+    sharded BFS from every component's minimum-rank vertex for the superstep count (cc_uf_sharded=1),
+    or the label propagation (0).  Components of every kind (isolated vertices, self-loops, small
+    components split across shards, an RMAT giant), a path past the 99-superstep cap (handed to the
+    propagation) and one below it; labels and superstep counts against the oracle."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    rng = np.random.default_rng(12)
+    cases = []
+    n = 400
+    s, d = rng.integers(0, n, 300), rng.integers(0, n, 300)
+    s[:5] = d[:5] = 7  # self-loops
+    cases.append((n, s, d, np.arange(10, 10 + n, dtype=np.int64)))
+    n = 150
+    cases.append((n, np.arange(n - 1), np.arange(1, n), np.arange(10, 10 + n, dtype=np.int64)))  # past the cap
+    cases.append((60, np.arange(59), np.arange(1, 60), np.arange(10, 70, dtype=np.int64)))  # below it
+    n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 13)
+    n = n0 + 5  # + isolated vertices and a 3-vertex chain whose minimum id sits in the middle
+    extra = (np.arange(5, dtype=np.int64) + 7) * 1000003
+    ids = np.concatenate([vid0, extra])
+    cases.append((n, np.concatenate([ds0, [n0 + 2, n0 + 3]]), np.concatenate([dd0, [n0 + 3, n0 + 4]]), ids))
+    try:
+        _lib.tune_set("cc_uf_sharded", uf)
+        c = jg.Context((0,) * shards)
+        for n, s, d, vid in cases:
+            g = c.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
+            comp, it = g.connected_components()
+            want, want_it = oracle_lib.connected_components(n, np.asarray(s, np.int32), np.asarray(d, np.int32), vid)
+            assert it == want_it, f"{shards} shards, n={n}: {it} supersteps, oracle {want_it}"
+            np.testing.assert_array_equal(comp, want)
+            g.close()
+        c.close()
+    finally:
+        _lib.tune_set("cc_uf_sharded", 1)
 
 
 @pytest.mark.parametrize("shards", [2, 3, 8])
