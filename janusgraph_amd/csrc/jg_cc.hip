@@ -79,10 +79,6 @@ __global__ void lex_rank_scatter_kernel(const uint32_t* __restrict__ vals, int64
         rank_of[vals[r]] = (int32_t)r;
 }
 
-__global__ void iota_i32_kernel(int32_t* __restrict__ p, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = (int32_t)i;
-}
-
 __global__ void iota_i64_kernel(int64_t* __restrict__ p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = i;
 }
@@ -434,6 +430,48 @@ void exchange_msg(Graph& g, int which) {
 
 constexpr int kCcSearchRows = 64, kCcSearchEntries = 2048;
 
+// The positions of a shard's compact vector that hold something: own rows with an edge [0, ne), then
+// each peer's run at the start of its segment.  Segments are 2^tbits apart, so at RMAT-26, P = 8 the
+// vector spans 67 M positions for 19 M such slots; the per-slot passes walk these only.
+struct SlotMap {
+    int64_t ne = 0, total = 0;
+    int nseg = 0;
+    int64_t start[64], cum[65];  // run k: positions [start[k], start[k] + cum[k + 1] - cum[k])
+    __device__ __forceinline__ int64_t pos(int64_t j) const {
+        if (j < ne) return j;
+        const int64_t k = j - ne;
+        int s = 0;
+        while (s + 1 < nseg && cum[s + 1] <= k) ++s;
+        return start[s] + (k - cum[s]);
+    }
+};
+
+__global__ void cc_slots_init_kernel(SlotMap m, int32_t* __restrict__ parent) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m.total; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = m.pos(j);
+        parent[x] = (int32_t)x;
+    }
+}
+
+__global__ void cc_slots_compress_kernel(SlotMap m, int32_t* parent) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m.total; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = m.pos(j);
+        parent[x] = uf_find(parent, (int32_t)x);
+    }
+}
+
+// every slot's own value (own rows: label, copies: the owner's) as the start of its tree minimum, so
+// a root (a singleton in particular: most copies next to giant rows only) takes no atomic for itself.
+// Once: later rounds start from the previous round's minima, labels of the same component that every
+// member's label has already reached or passed, so the minima stay exact and only fall faster.
+__global__ void cc_tree_init_kernel(SlotMap m, const int32_t* __restrict__ label, const int32_t* __restrict__ msg,
+                                    int32_t* __restrict__ tmin) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m.total; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = m.pos(j);
+        tmin[x] = j < m.ne ? label[x] : msg[x];
+    }
+}
+
 struct CcShardLink {
     int32_t* parent;
     const int64_t* rp;
@@ -460,19 +498,20 @@ __global__ __launch_bounds__(kBlock) void cc_own_flags_kernel(const int32_t* __r
 }
 
 // send-list words for exchange_halo_bits: bit b of word w = the row at that send-list position is in
-// the giant tree (a thread per word)
-__global__ void cc_pack_flags_kernel(const int32_t* __restrict__ parent, int32_t giant,
-                                     const int32_t* __restrict__ send_src, const int64_t* __restrict__ send_off,
-                                     const int64_t* __restrict__ woff, int P, unsigned long long* __restrict__ sw) {
+// the giant tree (a wave per word)
+__global__ __launch_bounds__(kBlock) void cc_pack_flags_kernel(const int32_t* __restrict__ parent, int32_t giant,
+                                                                const int32_t* __restrict__ send_src,
+                                                                const int64_t* __restrict__ send_off,
+                                                                const int64_t* __restrict__ woff, int P,
+                                                                unsigned long long* __restrict__ sw) {
     const int64_t words = woff[P];
-    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; w < words;
+         w += ((int64_t)gridDim.x * blockDim.x) / kWave) {  // wave-uniform
         int q = 0;
         while (q + 1 < P && woff[q + 1] <= w) ++q;
-        const int64_t x0 = send_off[q] + (w - woff[q]) * 64, x1 = send_off[q + 1];
-        unsigned long long word = 0;
-        for (int b = 0; b < 64 && x0 + b < x1; ++b)
-            if (parent[send_src[x0 + b]] == giant) word |= 1ull << b;
-        sw[w] = word;
+        const int64_t x = send_off[q] + (w - woff[q]) * 64 + lane_id();
+        const uint64_t word = __ballot(x < send_off[q + 1] && parent[send_src[x]] == giant);
+        if (lane_id() == 0) sw[w] = word;
     }
 }
 
@@ -529,18 +568,17 @@ __global__ __launch_bounds__(kBlock) void cc_link_rest_sharded_kernel(CcShardLin
     if (lane == 0 && count) atomicAdd(linked, count);
 }
 
-// T[root] = the minimum over the tree's members: own rows with an edge their labels, copies (positions
-// from `rows` on holding a label, i.e. < kNoMsg) their owners'; the giant tree's through a block
-// reduction (one atomic per block)
-__global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(const int32_t* __restrict__ parent,
-                                                              const int32_t* __restrict__ label, int64_t ne,
-                                                              int64_t rows, const int32_t* __restrict__ msg,
-                                                              int64_t len, int32_t giant, int32_t* __restrict__ tmin) {
+// T[root] = the minimum over the tree's members: own rows with an edge their labels, copies their
+// owners'; the giant tree's through a block reduction (one atomic per block)
+__global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(SlotMap sm, const int32_t* __restrict__ parent,
+                                                              const int32_t* __restrict__ label,
+                                                              const int32_t* __restrict__ msg, int32_t giant,
+                                                              int32_t* __restrict__ tmin) {
     __shared__ int32_t red[kBlock / kWave];
     int32_t g = INT_MAX;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len; x += (int64_t)gridDim.x * blockDim.x) {
-        if (x < rows && x >= ne) continue;
-        const int32_t m = x < rows ? label[x] : msg[x];
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < sm.total; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = sm.pos(j);
+        const int32_t m = j < sm.ne ? label[x] : msg[x];
         if (m >= kNoMsg) continue;
         const int32_t r = parent[x];
         if (r == giant) g = m < g ? m : g;
@@ -557,19 +595,20 @@ __global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(const int32_t* __re
 
 // own rows with an edge take their tree's minimum (labels only decrease); copies take it too, for the
 // reverse exchange
-__global__ void cc_tree_apply_kernel(const int32_t* __restrict__ parent, const int32_t* __restrict__ tmin, int64_t ne,
-                                     int64_t rows, int64_t len, int32_t* __restrict__ label, int32_t* __restrict__ msg,
+__global__ void cc_tree_apply_kernel(SlotMap sm, const int32_t* __restrict__ parent, int32_t* __restrict__ tmin,
+                                     int32_t* __restrict__ label, int32_t* __restrict__ msg,
                                      int32_t* __restrict__ changed) {
     bool ch = false;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len; x += (int64_t)gridDim.x * blockDim.x) {
-        if (x < ne) {
-            const int32_t t = tmin[parent[x]];
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < sm.total; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = sm.pos(j);
+        const int32_t t = tmin[parent[x]];
+        if (j < sm.ne) {
             if (t < label[x]) {
                 label[x] = t;
                 ch = true;
             }
-        } else if (x >= rows && msg[x] < kNoMsg) {
-            msg[x] = tmin[parent[x]];
+        } else {
+            msg[x] = t;
         }
     }
     if (__ballot(ch) && lane_id() == 0) *changed = 1;
@@ -602,6 +641,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         int64_t ne = 0, len = 0, heavy = 0, nsend = 0;
         int32_t giant = -1;
         int giant_share = 0, all_found = 0;
+        SlotMap sm;
     };
     std::vector<St> st(ns);
     const int kFirst = std::max(1, tune().cc_first);
@@ -625,6 +665,16 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         t.ne = c.empty_from >= 0 ? std::min(c.empty_from, sh.rows) : sh.rows;
         t.len = g.vec_len(sh, JG_ADJ_BOTH);
         t.nsend = h.send_off[(size_t)P];
+        t.sm.ne = t.ne;
+        t.sm.cum[0] = 0;
+        for (int q = 0; q < P; ++q) {
+            const int64_t nr = q == sh.index ? 0 : h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q];
+            if (nr == 0) continue;
+            t.sm.start[t.sm.nseg] = (int64_t)h.seg_of(q, sh.index) << h.tbits;
+            t.sm.cum[t.sm.nseg + 1] = t.sm.cum[t.sm.nseg] + nr;
+            ++t.sm.nseg;
+        }
+        t.sm.total = t.ne + t.sm.cum[t.sm.nseg];
         int32_t* parent = sh.cc_msg[1].get();
         t.tmin.alloc(t.len);
         t.label.alloc(std::max<int64_t>(sh.rows, 1));
@@ -645,13 +695,15 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
             JG_HIP(hipMemcpyAsync(t.label.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
             JG_HIP(hipMemcpyAsync(t.rank.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
-        iota_i32_kernel<<<grid_for(t.len), kBlock, 0, s>>>(parent, t.len);
-        JG_LAUNCH_CHECK();
+        if (t.sm.total) {
+            cc_slots_init_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, parent);
+            JG_LAUNCH_CHECK();
+        }
         if (t.ne > 0) {
             DevBuf<int32_t> sample(1025);
             uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), t.ne, kFirst);
             JG_LAUNCH_CHECK();
-            uf_compress_kernel<<<grid_for(t.len), kBlock, 0, s>>>(parent, t.len);
+            cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, parent);
             JG_LAUNCH_CHECK();
             // the most frequent root among 1024 sampled own rows: the giant tree's
             uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, t.ne, 1024, sample.get());
@@ -679,7 +731,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
             JG_LAUNCH_CHECK();
         }
         if (woff[(size_t)P] > 0) {
-            cc_pack_flags_kernel<<<grid_for(woff[(size_t)P]), kBlock, 0, s>>>(parent, t.giant, h.send_src.get(),
+            cc_pack_flags_kernel<<<grid_for(woff[(size_t)P] * kWave), kBlock, 0, s>>>(parent, t.giant, h.send_src.get(),
                                                                               t.send_off.get(), t.woff.get(), P,
                                                                               t.sw.get());
             JG_LAUNCH_CHECK();
@@ -706,7 +758,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
                 t.all_found = 0;
         cc_link_rest_sharded_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(link_args(i), linked.get() + i);
         JG_LAUNCH_CHECK();
-        uf_compress_kernel<<<grid_for(t.len), kBlock, 0, s>>>(sh.cc_msg[1].get(), t.len);
+        cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, sh.cc_msg[1].get());
         JG_LAUNCH_CHECK();
     }
     // the label rounds
@@ -732,17 +784,20 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
             St& t = st[i];
             JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
             if (t.ne == 0) continue;
-            JG_HIP(hipMemsetAsync(t.tmin.get(), 0x7F, t.len * sizeof(int32_t), sh.stream));
-            cc_tree_min_kernel<<<grid_for(t.len), kBlock, 0, sh.stream>>>(sh.cc_msg[1].get(), t.label.get(), t.ne,
-                                                                          sh.rows, sh.cc_msg[0].get(), t.len, t.giant,
-                                                                          t.tmin.get());
+            const unsigned grid = grid_for(t.sm.total);
+            if (rounds == 1) {
+                cc_tree_init_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, t.label.get(), sh.cc_msg[0].get(), t.tmin.get());
+                JG_LAUNCH_CHECK();
+            }
+            cc_tree_min_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, sh.cc_msg[1].get(), t.label.get(), sh.cc_msg[0].get(),
+                                                               t.giant, t.tmin.get());
             JG_LAUNCH_CHECK();
-            cc_tree_apply_kernel<<<grid_for(t.len), kBlock, 0, sh.stream>>>(sh.cc_msg[1].get(), t.tmin.get(), t.ne,
-                                                                            sh.rows, t.len, t.label.get(),
-                                                                            sh.cc_msg[0].get(), sh.cc_changed.get());
+            cc_tree_apply_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, sh.cc_msg[1].get(), t.tmin.get(), t.label.get(),
+                                                                 sh.cc_msg[0].get(), sh.cc_changed.get());
             JG_LAUNCH_CHECK();
-            // memset, parent + label/msg, tree minima; apply; reverse apply
-            bytes += 13.0 * (double)t.len + 12.0 * (double)t.len + 12.0 * (double)t.nsend;
+            // per slot: init 8 B (round 1), tree minima 8 B (parent, label; the atomics of non-root
+            // members), apply 12 B; reverse apply 12 B per send-list element
+            bytes += (rounds == 1 ? 28.0 : 20.0) * (double)t.sm.total + 12.0 * (double)t.nsend;
         }
         exchange_halo_reverse(g, JG_ADJ_BOTH, mv, rv, sizeof(int32_t), ncclInt32);
         for (size_t i = 0; i < ns; ++i) {
@@ -787,9 +842,9 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
                          "%d supersteps\n",
                          sh.index, (long long)sh.rows, (long long)t.ne, (long long)t.len, (long long)sh.both.nnz,
                          t.giant, t.giant_share, t.all_found, l, rounds, it);
-        // init 4 B, compressions 16 B, flags 1 B per slot; per row with an edge: first links 20 B, BFS
-        // start 17 B, depth and frontier probe 5 B
-        bytes += 21.0 * (double)t.len + 42.0 * (double)t.ne;
+        // per slot: init 4 B, two compressions 16 B; flags 1 bit per vector position; per row with an
+        // edge: first links 20 B, BFS start 17 B, depth and frontier probe 5 B
+        bytes += 20.0 * (double)t.sm.total + (double)t.len / 8.0 + 42.0 * (double)t.ne;
         if (it <= kCcMaxIterations - 1 && sh.rows)
             JG_HIP(hipMemcpyAsync(sh.cc_label.get(), t.label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice,
                                   sh.stream));

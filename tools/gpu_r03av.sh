@@ -2,7 +2,7 @@
 # Round 3, session 2: sharded CC by local union-finds + tree labels over the halo + a multi-root
 # sharded DO-BFS — parity (small, multirank, RMAT-26 2/8 shards) and the 8-shard simulation.
 set -o pipefail
-OUT=gpurun_out/r03at
+OUT=gpurun_out/r03av
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "sharded_connected or logical_shards_match or connected_components" > $OUT/pytest.log 2>&1 || exit 2
