@@ -718,6 +718,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().msbfs_bu_frac = (int)value;
     } else if (k == "msbfs_skip") {
         jg::tune().msbfs_skip = value != 0;
+    } else if (k == "cc_uf_search") {
+        jg::tune().cc_uf_search = value != 0;
     } else if (k == "cc_uf_sharded") {
         jg::tune().cc_uf_sharded = value != 0;
     } else if (k == "cc_uf") {

@@ -747,8 +747,10 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         hipStream_t s = sh.stream;
         St& t = st[i];
         if (t.ne == 0) continue;
-        cc_giant_search_kernel<<<(kCcSearchRows * kWave + kBlock - 1) / kBlock, kBlock, 0, s>>>(link_args(i));
-        JG_LAUNCH_CHECK();
+        if (tune().cc_uf_search) {  // 0: every peer takes the fallback (a parity-test variant)
+            cc_giant_search_kernel<<<(kCcSearchRows * kWave + kBlock - 1) / kBlock, kBlock, 0, s>>>(link_args(i));
+            JG_LAUNCH_CHECK();
+        }
         std::vector<int32_t> found((size_t)P);
         copy_d2h(found.data(), t.found.get(), P * sizeof(int32_t), s);
         const Halo& h = sh.halo_both;

@@ -558,6 +558,7 @@ struct Tune {
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int cc_uf_sharded = 1;            //         sharded (halo plans): local union-find, tree labels over the halo,
                                       //         multi-root sharded BFS for the superstep count (0: propagation)
+    int cc_uf_search = 1;             //         ... giant-to-giant links by a bounded search (0: every flagged entry)
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_init_suffix = 1;          //         DO-BFS init: empty rows from the plan's empty suffix (no row_ptr reads)

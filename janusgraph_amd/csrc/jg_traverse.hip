@@ -2254,7 +2254,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    // exactly its input queue (tds[i].queue[qc ^ 1][0, nq_in))
             // work of the levels (jg_stats.algorithmic_bytes): pull levels (per shard: the live merge tasks
             // counted on the device, or every task when the skip is off) and top-down frontier entries
-            int pull_levels = 0, sparse_levels = 0;
+            int pull_levels = 0;
             int unskipped_levels = 0;  // pull levels that ran every merge task (msbfs_skip_first)
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
@@ -2388,7 +2388,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 }
                             }
                             sparse_done = true;
-                            ++sparse_levels;
                             if (std::getenv("JG_DEBUG_BFS"))
                                 std::fprintf(stderr, "[jg msbfs] level %d top-down, sparse reverse exchange: %lld pairs (dense: %lld words)\n",
                                              level, (long long)pairs_all, (long long)mat[(size_t)P * P]);

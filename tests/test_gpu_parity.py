@@ -349,11 +349,12 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     c.close()
 
 
-@pytest.mark.parametrize("shards,uf", [(2, 1), (3, 1), (8, 1), (3, 0)])
+@pytest.mark.parametrize("shards,uf", [(2, 1), (3, 1), (8, 1), (3, 0), (3, "nosearch"), (8, "nosearch")])
 def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
     """Logical shards over halo plans: local union-finds, tree labels spread over the halo, and one
     sharded BFS from every component's minimum-rank vertex for the superstep count (cc_uf_sharded=1),
-    or the label propagation (0).  Components of every kind (isolated vertices, self-loops, small
+    or the label propagation (0); "nosearch" skips the bounded giant-to-giant search, so every peer
+    takes the fallback (giant rows link every flagged copy).  Components of every kind (isolated vertices, self-loops, small
     components split across shards, an RMAT giant), a path past the 99-superstep cap (handed to the
     propagation) and one below it; labels and superstep counts against the oracle."""
     import janusgraph_amd as jg
@@ -373,7 +374,8 @@ def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
     ids = np.concatenate([vid0, extra])
     cases.append((n, np.concatenate([ds0, [n0 + 2, n0 + 3]]), np.concatenate([dd0, [n0 + 3, n0 + 4]]), ids))
     try:
-        _lib.tune_set("cc_uf_sharded", uf)
+        _lib.tune_set("cc_uf_sharded", 0 if uf == 0 else 1)
+        _lib.tune_set("cc_uf_search", 0 if uf == "nosearch" else 1)
         c = jg.Context((0,) * shards)
         for n, s, d, vid in cases:
             g = c.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
@@ -385,6 +387,7 @@ def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
         c.close()
     finally:
         _lib.tune_set("cc_uf_sharded", 1)
+        _lib.tune_set("cc_uf_search", 1)
 
 
 @pytest.mark.parametrize("shards", [2, 3, 8])
