@@ -306,7 +306,8 @@ def required_roofline(m, live, ms):
 
 def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     """CC (configs[3]) and 64-source MS-BFS (configs[4]) on the BOTH adjacency.  N > 1: every rank holds
-    its shard; CC runs the label propagation over the halo, MS-BFS the sharded bit-parallel pull."""
+    its shard; CC runs local union-finds with tree labels over the halo and a multi-root sharded DO-BFS
+    (jg_cc.hip cc_union_find_sharded), MS-BFS the sharded bit-parallel levels."""
     n, m = 1 << scale, ef << scale
     g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
     build_ms = ctx.stats()["build_ms"]
@@ -326,7 +327,9 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
           "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
           "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
                        "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"
-          if ctl.ws == 1 else "label propagation supersteps over the BOTH halo exchange"}
+          if ctl.ws == 1 else "sharded: local Afforest union-finds, tree labels over forward and reverse halo "
+                              "exchanges, one multi-root sharded DO-BFS for the superstep count "
+                              "(jg_cc.hip cc_union_find_sharded)"}
     if ctl.ws == 1:
         cc["roofline"] = hbm_roofline(st["algorithmic_bytes"], cc_ms, "ConnectedComponent run (uf_* kernels + "
                                       "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
