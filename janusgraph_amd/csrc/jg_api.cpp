@@ -765,9 +765,6 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "bfs_grid_mult") {
         JG_ARG(value >= 1 && value <= 64, "bfs_grid_mult must be in [1, 64]");
         jg::tune().bfs_grid_mult = (int)value;
-    } else if (k == "bfs_bu_rows") {
-        JG_ARG(value == 1 || value == 2, "bfs_bu_rows must be 1 or 2");
-        jg::tune().bfs_bu_rows = (int)value;
     } else if (k == "bfs_wave_stage") {
         jg::tune().bfs_wave_stage = value != 0;
     } else if (k == "merge_interleave") {

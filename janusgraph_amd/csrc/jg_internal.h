@@ -574,7 +574,6 @@ struct Tune {
     int bfs_batch0 = 10;              //         DO-BFS: levels in the first batch (then 4, 8, 16, ...)
     int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
     int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)
-    int bfs_bu_rows = 1;              //         DO-BFS bottom-up: vertices each lane scans side by side (1 or 2)
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
     int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power

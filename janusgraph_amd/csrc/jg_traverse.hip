@@ -269,10 +269,8 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
 }
 
 // Bottom-up: one lane per unvisited vertex scans its pull row against the frontier and stops at the
-// first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.  With
-// kRows = 2 a lane scans the vertices of two words (a grid stride apart) side by side, so their
-// dependent round trips (seen byte, row offsets, columns, probes) overlap (Tune::bfs_bu_rows).
-template <bool kFromDepth, int kRows, class App>
+// first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
+template <bool kFromDepth, class App>
 __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, App& app) {
     const int64_t words = (a.rows + 63) / 64;
     constexpr int kWpb = kBlock / kWave;
@@ -281,64 +279,36 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
     // block-uniform trip count when the append is block-wide (words past the end take nothing);
     // wave-staged appends let every wave run its own words
     const int64_t wv0 = App::kWaveUniform ? wave_id() : 0;
-    for (int64_t w0 = (int64_t)blockIdx.x * kWpb + wv0; w0 < words; w0 += wstride * kRows) {
-        int64_t w[kRows], v[kRows], j[kRows], j1[kRows], vdeg[kRows];
-        bool found[kRows], act[kRows];
+    for (int64_t w0 = (int64_t)blockIdx.x * kWpb + wv0; w0 < words; w0 += wstride) {
+        const int64_t w = App::kWaveUniform ? w0 : w0 + wave_id();
+        const int64_t v = w * 64 + lane_id();
+        bool found = false;
+        int64_t vdeg = 0;
+        if (v < a.rows && !a.seen[v]) {
+            // kBuBatch neighbours per step: all column loads, then all frontier probes, then the test,
+            // so a row scanned to its end pays two round trips per batch instead of per neighbour
+            // (which neighbour hits does not matter: the depth is level + 1 either way)
+            const int64_t j1 = a.pull_rp[v + 1];
+            for (int64_t j = a.pull_rp[v]; j < j1 && !found; j += kBuBatch) {
+                int32_t u[kBuBatch];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            w[r] = (App::kWaveUniform ? w0 : w0 + wave_id()) + r * wstride;
-            v[r] = w[r] * 64 + lane_id();
-            found[r] = false;
-            vdeg[r] = 0;
-            act[r] = v[r] < a.rows && !a.seen[v[r]];
-        }
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            j[r] = act[r] ? a.pull_rp[v[r]] : 0;
-            j1[r] = act[r] ? a.pull_rp[v[r] + 1] : 0;
-        }
-        // kBuBatch neighbours per row and step: all column loads, then all frontier probes, then the
-        // test, so a row scanned to its end pays two round trips per batch instead of per neighbour
-        // (which neighbour hits does not matter: the depth is level + 1 either way)
-        for (;;) {
-            bool more = false;
-#pragma unroll
-            for (int r = 0; r < kRows; ++r) more |= !found[r] && j[r] < j1[r];
-            if (!more) break;
-            int32_t u[kRows][kBuBatch];
-#pragma unroll
-            for (int r = 0; r < kRows; ++r) {
-                const bool go = !found[r] && j[r] < j1[r];
+                for (int k = 0; k < kBuBatch; ++k) u[k] = a.pull_col[j + k < j1 ? j + k : j1 - 1];
+                bool hit[kBuBatch];
 #pragma unroll
                 for (int k = 0; k < kBuBatch; ++k)
-                    u[r][k] = go ? a.pull_col[j[r] + k < j1[r] ? j[r] + k : j1[r] - 1] : -1;
+                    hit[k] = kFromDepth ? a.depth[u[k]] == a.level : ((a.bm_in[u[k] >> 6] >> (u[k] & 63)) & 1ull);
+#pragma unroll
+                for (int k = 0; k < kBuBatch; ++k) found |= hit[k];
             }
-#pragma unroll
-            for (int r = 0; r < kRows; ++r) {
-                bool hit = false;
-#pragma unroll
-                for (int k = 0; k < kBuBatch; ++k) {
-                    const int32_t x = u[r][k];
-                    if (x >= 0)
-                        hit |= kFromDepth ? a.depth[x] == a.level : (bool)((a.bm_in[x >> 6] >> (x & 63)) & 1ull);
-                }
-                if (!found[r] && j[r] < j1[r]) {
-                    found[r] = hit;
-                    j[r] += kBuBatch;
-                }
+            if (found) {
+                a.depth[v] = next_depth;
+                a.seen[v] = 1;
+                vdeg = a.deg_rp[v + 1] - a.deg_rp[v];
             }
         }
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            if (found[r]) {
-                a.depth[v[r]] = next_depth;
-                a.seen[v[r]] = 1;
-                vdeg[r] = a.deg_rp[v[r] + 1] - a.deg_rp[v[r]];
-            }
-            const uint64_t word = __ballot(found[r]);
-            if (lane_id() == 0 && w[r] < words) a.bm_out[w[r]] = word;
-            app.append(found[r], (int32_t)v[r], vdeg[r], a.queue_out, a.qoff_out, packed);
-        }
+        const uint64_t word = __ballot(found);
+        if (lane_id() == 0 && w < words) a.bm_out[w] = word;
+        app.append(found, (int32_t)v, vdeg, a.queue_out, a.qoff_out, packed);
     }
 }
 
@@ -348,7 +318,7 @@ __device__ __forceinline__ bool td_split(const BfsLevel& a, long long mf) {
     return a.split && mf >= a.split_min && mf <= a.split_max;
 }
 
-template <bool WAVE, int kRows>
+template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
     __shared__ long long s_nf, s_mf;
@@ -379,9 +349,9 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
         if (td_split(a, s_mf)) bfs_top_down<kTdOwner>(a, s_nf, s_mf, packed, app, s_qs);  // the claim launch appends
         else bfs_top_down<kTdCas>(a, s_nf, s_mf, packed, app, s_qs);
     } else if (s_switch) {
-        bfs_bottom_up<true, kRows>(a, packed, app);
+        bfs_bottom_up<true>(a, packed, app);
     } else {
-        bfs_bottom_up<false, kRows>(a, packed, app);
+        bfs_bottom_up<false>(a, packed, app);
     }
     app.final(a.queue_out, a.qoff_out, packed);
 }
@@ -1379,9 +1349,8 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             a.bm_out = sh.bfs_bm[p ^ 1].get();
             a.split = a.owner && (split_mode == 1 || (split_mode == 2 && level < 16 && ((split_levels >> level) & 1)));
             if (prof_enabled(ctx)) prof_record_start(ctx, sh);
-            if (tune().bfs_wave_stage && tune().bfs_bu_rows == 2) bfs_level_kernel<true, 2><<<grid, kBlock, 0, s>>>(a);
-            else if (tune().bfs_wave_stage) bfs_level_kernel<true, 1><<<grid, kBlock, 0, s>>>(a);
-            else bfs_level_kernel<false, 1><<<grid, kBlock, 0, s>>>(a);
+            if (tune().bfs_wave_stage) bfs_level_kernel<true><<<grid, kBlock, 0, s>>>(a);
+            else bfs_level_kernel<false><<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             if (a.split) {
                 if (tune().bfs_wave_stage) bfs_td_claim_kernel<true><<<grid, kBlock, 0, s>>>(a);

@@ -150,44 +150,6 @@ def test_bfs_rmat_vs_oracle(ctx, oracle_lib, scale):
         np.testing.assert_array_equal(depth, ref)
 
 
-@pytest.mark.parametrize("rows", [1, 2])
-def test_bfs_bottom_up_rows_per_lane(oracle_lib, rows):
-    """Bottom-up levels with one or two vertices per lane scanned side by side (Tune::bfs_bu_rows):
-    depths for BOTH / OUT / IN, edge counts equal to the one-row scan, CC labels and superstep counts
-    (the eccentricity BFS shares the level code), on graphs where the last word is partial."""
-    import janusgraph_amd as jg
-    from janusgraph_amd import _lib
-    c = jg.Context((0,))
-    try:
-        for scale in (13, 17):
-            n, vid, src, dst, ds, dd = rmat_case(oracle_lib, scale)
-            n2 = n - 37  # a partial last frontier word: drop the edges of the top 37 vertices
-            keep = (ds < n2) & (dd < n2)
-            vid2, ds2, dd2 = vid[:n2], ds[keep], dd[keep]
-            g = c.build(vid2, vid2[ds2], vid2[dd2], flags=ALL)
-            deg = np.bincount(ds2, minlength=n2) + np.bincount(dd2, minlength=n2)
-            cand = np.nonzero(deg)[0]
-            for k in range(3):
-                s = int(cand[(k * 7919) % len(cand)])
-                _lib.tune_set("bfs_bu_rows", 1)
-                g.bfs([vid2[s]], 3, want=False)
-                edges1 = c.stats()["edges_traversed"]
-                _lib.tune_set("bfs_bu_rows", rows)
-                for direction in (3, 1, 2):
-                    np.testing.assert_array_equal(g.bfs([vid2[s]], direction)[0],
-                                                  oracle_lib.bfs(n2, ds2, dd2, s, direction))
-                g.bfs([vid2[s]], 3, want=False)
-                assert c.stats()["edges_traversed"] == edges1
-            comp, it = g.connected_components()
-            comp_ref, it_ref = oracle_lib.connected_components(n2, ds2, dd2, vid2)
-            np.testing.assert_array_equal(comp, comp_ref)
-            assert it == it_ref
-            g.close()
-    finally:
-        _lib.tune_set("bfs_bu_rows", 1)
-        c.close()
-
-
 @pytest.mark.parametrize("mode,split_min", [(0, 65536), (1, 1), (1, 4096), (2, 1)])
 def test_bfs_split_top_down_matches_oracle(oracle_lib, mode, split_min):
     """Split top-down levels (owner store + claim launch, Tune::bfs_td_split) against the CAS claims:
