@@ -2,7 +2,7 @@
 # Round 3, session 2, final tree: whole GPU suite, smoke, bench (default command) and its rocprofv3
 # kernel-trace summary.
 set -o pipefail
-OUT=gpurun_out/r03ba
+OUT=gpurun_out/r03bb
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -x -v --timeout 600 --timeout-method thread -m gpu > $OUT/pytest.log 2>&1 || exit 2
