@@ -42,8 +42,11 @@
  *       and memory().getIteration()/getRuntime() (FulgoraMemory.java:97-101)
  *
  * Ownership: host arrays passed in are caller-owned and read only during the call; outputs are
- * caller-allocated.  Device memory is owned by the library (per jg_graph) and freed by
- * jg_graph_destroy.  A jg_ctx is not re-entrant: one call in flight per context.
+ * caller-allocated.  Device memory is owned by the library (per jg_graph) and handed back to the
+ * device by jg_graph_destroy (the library's block cache, which spares a build its ~250 device
+ * synchronising frees, is emptied there and by jg_ctx_trim).  A jg_ctx is not re-entrant: one call in
+ * flight per context, and a jg_graph belongs to its context's caller thread (read-only queries such as
+ * jg_graph_neighbors may run from several threads: their lazily made host copies are locked).
  */
 #ifndef JANUSGPU_H
 #define JANUSGPU_H
@@ -55,9 +58,10 @@
 extern "C" {
 #endif
 
-/* 2: jg_graph_info.exchange_values appended; jg_bfs_rows, jg_graph_neighbors added.  Callers must check
+/* 2: jg_graph_info.exchange_values appended; jg_bfs_rows, jg_graph_neighbors added.
+ * 3: jg_bfs_keep, jg_bfs_kept_row, jg_bfs_kept_release, jg_ctx_trim added.  Callers must check
  * jg_abi_version() == JG_ABI_VERSION before passing any struct across the ABI. */
-#define JG_ABI_VERSION 2
+#define JG_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define JG_OK               0
@@ -148,6 +152,8 @@ typedef struct jg_transport {
 } jg_transport;
 int jg_ctx_create_rank_transport(int device, int nranks, int rank, const jg_transport* t, jg_ctx** out);
 int jg_ctx_destroy(jg_ctx* ctx);
+/* Hands the device memory the library caches for reuse (freed blocks) back to the context's devices. */
+int jg_ctx_trim(jg_ctx* ctx);
 int jg_ctx_last_stats(const jg_ctx* ctx, jg_stats* out);
 /* Record HIP events around every launch of the dominant kernel (costs ~1 us per launch). */
 int jg_ctx_set_profiling(jg_ctx* ctx, int enable);
@@ -293,6 +299,18 @@ int jg_bfs(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direct
  * java/.../GpuGraphComputer.java ShortestPaths). */
 int jg_bfs_rows(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth,
                 int32_t* const* depth_rows);
+
+/* The same traversal (nsrc <= 64: one bit-parallel batch) with its depth rows kept on the device;
+ * jg_bfs_kept_row(g, s, depth_out) then copies row s (n int32, caller order) into a caller buffer, so a
+ * caller that consumes the rows one at a time holds one n-int32 buffer instead of nsrc of them
+ * (ShortestPathVertexProgram's batches at n = 2^26: one 268 MB row instead of 17 GB of direct buffers,
+ * java/.../GpuGraphComputer.java ShortestPaths).  The rows stay until the next jg_bfs_keep, until
+ * jg_bfs_kept_release or until jg_graph_destroy; jg_bfs_kept_row fails with JG_ERR_ARG for s outside
+ * [0, nsrc of the last jg_bfs_keep).  Replaces FulgoraVertexMemory's per-vertex path state
+ * (graphdb/olap/computer/FulgoraVertexMemory.java:52-123) for the bit-parallel batch. */
+int jg_bfs_keep(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth);
+int jg_bfs_kept_row(jg_graph* g, int32_t s, int32_t* depth_out);
+int jg_bfs_kept_release(jg_graph* g);
 
 /* Adjacency of vertices rows[0, nrows) (output-order indices), in output-order indices: the host copy
  * of the snapshot a path walk-back reads where Fulgora re-reads each vertex's preloaded BOTH slice

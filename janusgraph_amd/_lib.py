@@ -41,11 +41,12 @@ EXPORTS = [
     "jg_tune_set", "jg_builder_create", "jg_builder_add_vertices", "jg_builder_add_edges", "jg_builder_set_schema",
     "jg_builder_add_rows", "jg_builder_finish", "jg_builder_destroy", "jg_graph_vertex_ids",
     "jg_builder_set_query_limit", "jg_bfs_rows", "jg_graph_neighbors", "jg_builder_set_weight_key",
+    "jg_bfs_keep", "jg_bfs_kept_row", "jg_bfs_kept_release", "jg_ctx_trim",
 ]
 # JG_PROP_* property value types (jg_builder_set_weight_key)
 PROP_BYTE, PROP_SHORT, PROP_INT, PROP_LONG, PROP_CHAR, PROP_BOOL, PROP_DATE, PROP_FLOAT, PROP_DOUBLE, PROP_UUID, \
     PROP_STRING = range(1, 12)
-ABI_VERSION = 2  # JG_ABI_VERSION of include/janusgpu.h this binding's structs follow
+ABI_VERSION = 3  # JG_ABI_VERSION of include/janusgpu.h this binding's structs follow
 
 
 class GraphInfo(ctypes.Structure):
@@ -184,6 +185,10 @@ def load():
         "jg_bfs_rows": ([_P, _P, _i32, _i32, _i32, _P], ctypes.c_int),
         "jg_graph_neighbors": ([_P, _i32, _P, _i64, _P, _P], ctypes.c_int),
         "jg_builder_set_weight_key": ([_P, _i64, _P, _P, _i32], ctypes.c_int),
+        "jg_bfs_keep": ([_P, _P, _i32, _i32, _i32], ctypes.c_int),
+        "jg_bfs_kept_row": ([_P, _i32, _P], ctypes.c_int),
+        "jg_bfs_kept_release": ([_P], ctypes.c_int),
+        "jg_ctx_trim": ([_P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -265,6 +270,10 @@ class Context:
 
     def set_profiling(self, on=True):
         check(load().jg_ctx_set_profiling(self._h, 1 if on else 0))
+
+    def trim(self):
+        """jg_ctx_trim: the device memory the library caches goes back to the devices."""
+        check(load().jg_ctx_trim(self._h))
 
     def stats(self) -> dict:
         s = Stats()
@@ -497,6 +506,20 @@ class Graph:
         ptrs = (ctypes.c_void_p * len(src))(*[None if r is None else r.ctypes.data for r in rows])
         check(load().jg_bfs_rows(self._h, _ptr(src), len(src), int(direction), int(max_depth), ptrs))
         return rows
+
+    def bfs_keep(self, sources, direction=DIR_BOTH, max_depth=-1):
+        """jg_bfs_keep: the traversal's depth rows (<= 64 sources) stay on the device for bfs_kept_row."""
+        src = np.ascontiguousarray(np.atleast_1d(sources), np.int64)
+        check(load().jg_bfs_keep(self._h, _ptr(src), len(src), int(direction), int(max_depth)))
+
+    def bfs_kept_row(self, s, out=None):
+        """jg_bfs_kept_row: row s of the last bfs_keep, into `out` (n int32) or a new array."""
+        row = self._out(self.n, np.int32) if out is None else out
+        check(load().jg_bfs_kept_row(self._h, int(s), _ptr(row)))
+        return row
+
+    def bfs_kept_release(self):
+        check(load().jg_bfs_kept_release(self._h))
 
     def neighbors(self, rows, direction=DIR_BOTH):
         """jg_graph_neighbors: (off, nbr) CSR of the given output-order rows, in output-order indices."""

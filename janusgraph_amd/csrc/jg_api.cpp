@@ -384,6 +384,15 @@ ExchTimer::~ExchTimer() {
     }
 }
 
+void prof_discard_exchanges(Graph& g) {
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        DeviceGuard dg(sh.device);
+        for (auto e : sh.exch_events) (void)hipEventDestroy(e);
+        sh.exch_events.clear();
+    }
+}
+
 void prof_collect(Ctx& c, Graph& g) {
     double total = 0;
     int64_t launches = 0;
@@ -416,6 +425,7 @@ void prof_collect(Ctx& c, Graph& g) {
 }
 
 const std::vector<int32_t>& Shard::dense_of_local() const {
+    std::lock_guard<std::mutex> lk(lazy_mu);
     if ((int64_t)dense_of_local_host.size() != rows) {
         dense_of_local_host.resize((size_t)rows);
         if (rows > 0) {
@@ -426,7 +436,21 @@ const std::vector<int32_t>& Shard::dense_of_local() const {
     return dense_of_local_host;
 }
 
+const std::vector<int64_t>& Graph::vid_of_rank() const {
+    std::lock_guard<std::mutex> lk(lazy_mu);
+    if ((int64_t)cc_vor_host.size() != n) {
+        cc_vor_host.resize((size_t)n);
+        if (n > 0) {
+            const Shard& sh = *shards[0];
+            DeviceGuard dg(sh.device);
+            copy_d2h(cc_vor_host.data(), cc_vor.get(), (size_t)n * sizeof(int64_t), sh.stream);
+        }
+    }
+    return cc_vor_host;
+}
+
 const std::vector<int32_t>& Graph::padded_of_dense() const {
+    std::lock_guard<std::mutex> lk(lazy_mu);
     if ((int64_t)padded_host.size() != n) {
         padded_host.resize((size_t)n);
         if (n > 0) {
@@ -1281,11 +1305,25 @@ int jg_graph_info_get(const jg_graph* g, jg_graph_info* out) {
 int jg_graph_destroy(jg_graph* g) {
     JG_GUARD_BEGIN
     if (!g) return JG_OK;
+    std::vector<int> devs;
     for (auto& sp : g->impl.shards) {
         jg::DeviceGuard dg(sp->device);
         (void)hipStreamSynchronize(sp->stream);
+        if (std::find(devs.begin(), devs.end(), sp->device) == devs.end()) devs.push_back(sp->device);
     }
     delete g;
+    // the snapshot's device memory goes back to the device, not to the library's block cache (ADVICE r03:
+    // a dropped snapshot must not keep memory from other users of the device for the context's lifetime)
+    for (int d : devs) jg::dev_cache_release(d);
+    JG_GUARD_END
+}
+
+int jg_ctx_trim(jg_ctx* ctx) {
+    JG_GUARD_BEGIN
+    JG_ARG(ctx, "null context");
+    jg::Ctx& c = ctx->impl;
+    for (size_t i = 0; i < c.devices.size(); ++i)
+        if (!(c.logical && i > 0)) jg::dev_cache_release(c.devices[i]);
     JG_GUARD_END
 }
 
@@ -1391,6 +1429,27 @@ int jg_bfs_rows(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t d
     JG_GUARD_BEGIN
     JG_ARG(g && source_vids, "null argument");
     jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, depth_rows);
+    JG_GUARD_END
+}
+
+int jg_bfs_keep(jg_graph* g, const int64_t* source_vids, int32_t nsrc, int32_t direction, int32_t max_depth) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && source_vids, "null argument");
+    jg::bfs_run(g->impl, source_vids, nsrc, direction, max_depth, nullptr, true);
+    JG_GUARD_END
+}
+
+int jg_bfs_kept_row(jg_graph* g, int32_t s, int32_t* depth_out) {
+    JG_GUARD_BEGIN
+    JG_ARG(g && depth_out, "null argument");
+    jg::bfs_kept_row(g->impl, s, depth_out);
+    JG_GUARD_END
+}
+
+int jg_bfs_kept_release(jg_graph* g) {
+    JG_GUARD_BEGIN
+    JG_ARG(g, "null graph");
+    jg::bfs_kept_release(g->impl);
     JG_GUARD_END
 }
 

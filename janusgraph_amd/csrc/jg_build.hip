@@ -1306,6 +1306,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
         if (g.flags & JG_ADJ_IN) check_halo_counts(g, JG_ADJ_IN);
         if (g.flags & JG_ADJ_BOTH) check_halo_counts(g, JG_ADJ_BOTH);
     }
+    if (g.flags & JG_ADJ_BOTH) cc_prepare_ranks(g);  // ConnectedComponent's labels: a property of the ids
     int64_t bytes = 0;
     for (auto& sp : g.shards) bytes += sp->in.bytes() + sp->out.bytes() + sp->both.bytes() + sp->out_degree.bytes();
     g.info.device_bytes = bytes;

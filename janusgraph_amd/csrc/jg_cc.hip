@@ -344,7 +344,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     const int kFirst = std::max(1, tune().cc_first);  // neighbours each vertex links in the first round
     if (rows == 0) {
         *iterations = 0;
-        *labels = sh.cc_label.get();
+        *labels = sh.cc_rank0.get();
         return true;
     }
     const int64_t ne = c.empty_from >= 0 ? std::min(c.empty_from, rows) : rows;
@@ -356,7 +356,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     DevBuf<int32_t> sample(1025);  // 1024 sampled roots, then the heavy-row count
     DevBuf<unsigned long long> linked(1);
     JG_HIP(hipMemsetAsync(linked.get(), 0, sizeof(unsigned long long), s));
-    const int32_t* rank = sh.cc_label.get();  // the initial labels are the ranks
+    const int32_t* rank = sh.cc_rank0.get();  // the initial labels are the ranks (cc_prepare_ranks)
     uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
     JG_LAUNCH_CHECK();
     uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, kFirst);
@@ -638,6 +638,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         DevBuf<int32_t> tmin, label, rank, found, rbuf;
         DevBuf<int64_t> send_off, woff;
         DevBuf<unsigned long long> flag, sw;
+        DevBuf<unsigned long long> linked;  // [1] entries scanned by the second round (on the shard's device)
         int64_t ne = 0, len = 0, heavy = 0, nsend = 0;
         int32_t giant = -1;
         int giant_share = 0, all_found = 0;
@@ -646,7 +647,6 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     std::vector<St> st(ns);
     const int kFirst = std::max(1, tune().cc_first);
     double bytes = 0;
-    DevBuf<unsigned long long> linked(ns);
     auto link_args = [&](size_t i) {
         Shard& sh = *g.shards[i];
         St& t = st[i];
@@ -690,10 +690,11 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         copy_h2d(t.woff.get(), woff.data(), (P + 1) * sizeof(int64_t), s);
         JG_HIP(hipMemsetAsync(t.found.get(), 0, P * sizeof(int32_t), s));
         JG_HIP(hipMemsetAsync(t.flag.get(), 0, t.flag.bytes(), s));
-        JG_HIP(hipMemsetAsync(linked.get() + i, 0, sizeof(unsigned long long), s));
-        if (sh.rows) {  // the ranks (cc_label) stay as they are until the labels are final
-            JG_HIP(hipMemcpyAsync(t.label.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-            JG_HIP(hipMemcpyAsync(t.rank.get(), sh.cc_label.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        t.linked.alloc(1);
+        JG_HIP(hipMemsetAsync(t.linked.get(), 0, sizeof(unsigned long long), s));
+        if (sh.rows) {  // labels start at the ranks (cc_prepare_ranks)
+            JG_HIP(hipMemcpyAsync(t.label.get(), sh.cc_rank0.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+            JG_HIP(hipMemcpyAsync(t.rank.get(), sh.cc_rank0.get(), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
         if (t.sm.total) {
             cc_slots_init_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, parent);
@@ -758,7 +759,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         for (int q = 0; q < P; ++q)
             if (q != sh.index && h.recv_off[(size_t)q + 1] > h.recv_off[(size_t)q] && !found[(size_t)h.seg_of(q, sh.index)])
                 t.all_found = 0;
-        cc_link_rest_sharded_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(link_args(i), linked.get() + i);
+        cc_link_rest_sharded_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(link_args(i), t.linked.get());
         JG_LAUNCH_CHECK();
         cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, sh.cc_msg[1].get());
         JG_LAUNCH_CHECK();
@@ -836,7 +837,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         DeviceGuard dg(sh.device);
         St& t = st[i];
         unsigned long long l = 0;
-        copy_d2h(&l, linked.get() + i, sizeof l, sh.stream);
+        copy_d2h(&l, t.linked.get(), sizeof l, sh.stream);
         lk += l;
         if (debug)
             std::fprintf(stderr, "[jg cc] shard %d: rows %lld with edges %lld, vector %lld, entries %lld, giant root %d "
@@ -861,96 +862,127 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
 
 }  // namespace
 
+// The String-order rank of every vertex id, computed once per snapshot (build_graph_from_dense, graphs
+// with the BOTH adjacency; counted in build_ms): it depends on the ids only.  g.cc_vor[r] = id of the
+// vertex of rank r (on the first shard's device), sh.cc_rank0[l] = rank of own row l (each shard's
+// device).  Negative ids leave them empty; cc_run then fails as before.
+void cc_prepare_ranks(Graph& g) {
+    const int64_t n = g.n;
+    g.cc_ranks = false;
+    for (int64_t d = 0; d < (int64_t)g.vid.size(); ++d)
+        if (g.vid[d] < 0) return;
+    Shard& shr = *g.shards[0];
+    DeviceGuard dg(shr.device);
+    hipStream_t s = shr.stream;
+    DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
+    g.cc_vor.alloc(std::max<int64_t>(n, 1));
+    g.cc_vor_host.clear();
+    if (n > 0) {
+        DevBuf<int64_t> vid(n);
+        DevBuf<uint64_t> keys(n);
+        DevBuf<uint32_t> vals(n);
+        if (g.vid.empty()) {
+            iota_i64_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n);
+            JG_LAUNCH_CHECK();
+        } else {
+            copy_h2d(vid.get(), g.vid.data(), n * sizeof(int64_t), s);
+        }
+        lex_digits_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n, keys.get(), vals.get());
+        JG_LAUNCH_CHECK();
+        prim::radix_sort(keys.get(), vals.get(), n, 5, s);
+        lex_padded_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), vals.get(), n, keys.get());
+        JG_LAUNCH_CHECK();
+        prim::radix_sort(keys.get(), vals.get(), n, 64, s);
+        lex_rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), n, rk.get());
+        JG_LAUNCH_CHECK();
+        vid_of_rank_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), vid.get(), n, g.cc_vor.get());
+        JG_LAUNCH_CHECK();
+    }
+    std::vector<int32_t> rank_of;  // host copy, for shards on other devices
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        sh.cc_rank0.alloc(std::max<int64_t>(sh.rows, 1));
+        if (!sh.rows) continue;
+        if (sh.device == shr.device) {  // the rows' ranks, gathered on the device
+            gather_i32_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(rk.get(), sh.dense_rows.get(), sh.rows,
+                                                                   sh.cc_rank0.get());
+            JG_LAUNCH_CHECK();
+            continue;
+        }
+        if (rank_of.empty()) {
+            rank_of.resize((size_t)n);
+            copy_d2h(rank_of.data(), rk.get(), n * sizeof(int32_t), s);
+        }
+        std::vector<int32_t> lab0((size_t)sh.rows);
+        const std::vector<int32_t>& dl = sh.dense_of_local();
+        for (int64_t l = 0; l < sh.rows; ++l) lab0[(size_t)l] = rank_of[(size_t)dl[(size_t)l]];
+        DeviceGuard dgs(sh.device);
+        copy_h2d(sh.cc_rank0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    JG_HIP(hipStreamSynchronize(s));
+    g.cc_ranks = true;
+}
+
+namespace {
+// Superstep 0 of the propagation: labels = ranks, only vertices with an edge send (every shard), then
+// the exchange step.
+void cc_propagation_init(Graph& g) {
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        DeviceGuard dg(sh.device);
+        for (auto& m : sh.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh.stream));  // ~INT_MAX
+        if (sh.rows) {
+            cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.cc_rank0.get(), sh.both.row_ptr.get(), sh.rows,
+                                                                        g.vec_pos(sh, JG_ADJ_BOTH), sh.cc_label.get(),
+                                                                        sh.cc_msg[0].get());
+            JG_LAUNCH_CHECK();
+        }
+    }
+    exchange_msg(g, 0);
+}
+}  // namespace
+
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     if (!(g.flags & JG_ADJ_BOTH)) fail(JG_ERR_UNSUPPORTED, "connected components need a graph built with JG_ADJ_BOTH");
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
     const int64_t n = g.n;
-    for (int64_t d = 0; d < (int64_t)g.vid.size(); ++d)
-        if (g.vid[d] < 0) fail(JG_ERR_UNSUPPORTED, "connected components need non-negative vertex ids");
-    // String-order rank of every vertex id, on the first shard's device.  One shard keeps everything
-    // there (rank of each vertex, vertex id of each rank, the rows' initial labels and the result in
-    // caller order); sharded graphs take host copies of the two maps.
-    Shard& shr = *g.shards[0];
-    const bool dev_maps = g.shards.size() == 1 && shr.rows == n && shr.dense_rows.size() >= (size_t)n;
-    std::vector<int32_t> rank_of(dev_maps ? 0 : n);
-    std::vector<int64_t> vid_of_rank(dev_maps ? 0 : n);
-    DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
-    DevBuf<int64_t> vor(std::max<int64_t>(n, 1));  // vertex id of each rank
-    {
-        DeviceGuard dg(shr.device);
-        hipStream_t s = shr.stream;
-        DevBuf<int64_t> vid(std::max<int64_t>(n, 1));
-        DevBuf<uint64_t> keys(std::max<int64_t>(n, 1));
-        DevBuf<uint32_t> vals(std::max<int64_t>(n, 1));
-        if (n > 0) {
-            if (g.vid.empty()) {
-                iota_i64_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n);
-                JG_LAUNCH_CHECK();
-            } else {
-                copy_h2d(vid.get(), g.vid.data(), n * sizeof(int64_t), s);
-            }
-            lex_digits_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), n, keys.get(), vals.get());
-            JG_LAUNCH_CHECK();
-            prim::radix_sort(keys.get(), vals.get(), n, 5, s);
-            lex_padded_kernel<<<grid_for(n), kBlock, 0, s>>>(vid.get(), vals.get(), n, keys.get());
-            JG_LAUNCH_CHECK();
-            prim::radix_sort(keys.get(), vals.get(), n, 64, s);
-            lex_rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), n, rk.get());
-            JG_LAUNCH_CHECK();
-            vid_of_rank_kernel<<<grid_for(n), kBlock, 0, s>>>(vals.get(), vid.get(), n, vor.get());
-            JG_LAUNCH_CHECK();
-            if (!dev_maps) {
-                copy_d2h(rank_of.data(), rk.get(), n * sizeof(int32_t), s);
-                copy_d2h(vid_of_rank.data(), vor.get(), n * sizeof(int64_t), s);
-            }
-        }
-    }
+    if (!g.cc_ranks) fail(JG_ERR_UNSUPPORTED, "connected components need non-negative vertex ids");
+    // One shard keeps everything on its device (the labels become ids in caller order there); sharded
+    // graphs map the labels on the host.
+    Shard& sh0 = *g.shards[0];
+    const bool dev_maps = g.shards.size() == 1 && sh0.rows == n;
+    // buffers of the call (allocation only: every kernel of the call runs inside the timed region)
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
         DeviceGuard dg(sh.device);
         const int64_t len = g.vec_len(sh, JG_ADJ_BOTH);
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < 2; ++k)
             if (sh.cc_msg[k].size() != (size_t)len) sh.cc_msg[k].alloc(len);
-            JG_HIP(hipMemsetAsync(sh.cc_msg[k].get(), 0x7F, sh.cc_msg[k].bytes(), sh.stream));  // ~INT_MAX
-        }
-        sh.cc_label.alloc(std::max<int64_t>(sh.rows, 1));
-        sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
-        sh.cc_split_partial.alloc(sh.plan_both.split_partial_len());
-        sh.cc_changed.alloc(1);
-        DevBuf<int32_t> dlab0(std::max<int64_t>(sh.rows, 1));
-        if (sh.rows) {
-            if (dev_maps) {  // the rows' ranks, gathered on the device
-                gather_i32_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(rk.get(), sh.dense_rows.get(), sh.rows,
-                                                                               dlab0.get());
-                JG_LAUNCH_CHECK();
-            } else {
-                std::vector<int32_t> lab0(sh.rows);
-                for (int64_t l = 0; l < sh.rows; ++l) lab0[l] = rank_of[sh.dense_of_local()[l]];
-                copy_h2d(dlab0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
-            }
-            cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dlab0.get(), sh.both.row_ptr.get(), sh.rows,
-                                                                        g.vec_pos(sh, JG_ADJ_BOTH), sh.cc_label.get(),
-                                                                        sh.cc_msg[0].get());
-            JG_LAUNCH_CHECK();
-        }
-        JG_HIP(hipStreamSynchronize(sh.stream));
+        if ((int64_t)sh.cc_label.size() < std::max<int64_t>(sh.rows, 1)) sh.cc_label.alloc(std::max<int64_t>(sh.rows, 1));
+        if ((int64_t)sh.cc_hub_partial.size() < std::max<int64_t>(sh.plan_both.num_chunks, 1))
+            sh.cc_hub_partial.alloc(std::max<int64_t>(sh.plan_both.num_chunks, 1));
+        if ((int64_t)sh.cc_split_partial.size() < sh.plan_both.split_partial_len())
+            sh.cc_split_partial.alloc(sh.plan_both.split_partial_len());
+        if (sh.cc_changed.size() == 0) sh.cc_changed.alloc(1);
     }
-    exchange_msg(g, 0);
     // superstep 0 votes: anyone with an edge sent
     int any = 0;
     for (auto& sp : g.shards) any |= sp->both.nnz > 0;
     any = allreduce_or(g, any);
 
-    Shard& sh0 = *g.shards[0];
     DeviceGuard dg0(sh0.device);
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
-    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf && sh0.rows > 0) {  // the union-find path's scratch
+    const bool uf_one = g.shards.size() == 1 && g.P == 1 && tune().cc_uf;
+    if (uf_one && sh0.rows > 0) {  // the union-find path's scratch
         if ((int64_t)sh0.cc_depth.size() < sh0.rows) sh0.cc_depth.alloc(sh0.rows);
         bfs_buffers(sh0);
     }
+    for (auto& sp : g.shards) JG_HIP(hipStreamSynchronize(sp->stream));
+    prof_discard_exchanges(g);  // exchange pairs count from t0 on only
     JG_HIP(hipEventRecord(t0, sh0.stream));
     int iteration = 0, cur = 0;
     // one shard: supersteps whose senders have few edges run push-style
@@ -972,38 +1004,18 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     bool solved = false;
     const int32_t* uf_labels = nullptr;  // the union-find's labels of shard 0 (when solved)
     double uf_bytes = 0;
-    if (g.shards.size() == 1 && g.P == 1 && tune().cc_uf) {
-        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_bytes);
-        if (!solved && sh0.rows) {  // the cap binds: the propagation runs, from fresh message vectors
-            for (auto& m : sh0.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh0.stream));
-            cc_init_kernel<<<grid_for(sh0.rows), kBlock, 0, sh0.stream>>>(
-                sh0.cc_label.get(), sh0.both.row_ptr.get(), sh0.rows, g.vec_pos(sh0, JG_ADJ_BOTH), sh0.cc_label.get(),
-                sh0.cc_msg[0].get());
-            JG_LAUNCH_CHECK();
-        }
-    }
-    // Sharded over halo plans: the same from local union-finds, tree labels and a sharded BFS
+    if (uf_one) solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_bytes);
+    // Sharded over halo plans: the same from local union-finds, tree labels over the halo and a sharded BFS
     // (cc_union_find_sharded); the sharded BFS takes at most 64 shards (jg_traverse.hip, kMaxShardsBfs).
     int uf_rounds = 0;
-    if (!solved && g.P > 1 && g.P <= 64 && sh0.halo_both.on && tune().cc_uf && tune().cc_uf_sharded) {
+    if (!solved && !uf_one && g.P > 1 && g.P <= 64 && sh0.halo_both.on && tune().cc_uf && tune().cc_uf_sharded) {
         solved = cc_union_find_sharded(g, &iteration, &uf_rounds, &uf_bytes);
-        if (solved) {
-            uf_labels = sh0.cc_label.get();
-        } else {  // the cap binds: the propagation runs, from fresh message vectors
-            for (auto& sp : g.shards) {
-                Shard& sh = *sp;
-                DeviceGuard dg(sh.device);
-                for (auto& m : sh.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh.stream));
-                if (sh.rows) {
-                    cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                        sh.cc_label.get(), sh.both.row_ptr.get(), sh.rows, g.vec_pos(sh, JG_ADJ_BOTH),
-                        sh.cc_label.get(), sh.cc_msg[0].get());
-                    JG_LAUNCH_CHECK();
-                }
-            }
-            exchange_msg(g, 0);
-            iteration = 0;
-        }
+        if (solved) uf_labels = sh0.cc_label.get();
+    }
+    // the propagation (no union-find path, or the 99-superstep cap binds): from superstep 0
+    if (!solved) {
+        iteration = 0;
+        cc_propagation_init(g);
     }
     while (!solved && any && iteration < kCcMaxIterations - 1) {
         ++iteration;
@@ -1092,10 +1104,11 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         DeviceGuard dg(sh.device);
         DevBuf<int64_t> out(n);
         cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(solved ? uf_labels : sh.cc_label.get(),
-                                                                sh.dense_rows.get(), vor.get(), n, out.get());
+                                                                sh.dense_rows.get(), g.cc_vor.get(), n, out.get());
         JG_LAUNCH_CHECK();
         copy_d2h(comp_out, out.get(), n * sizeof(int64_t), sh.stream);
     } else if (comp_out) {
+        const std::vector<int64_t>& vid_of_rank = g.vid_of_rank();
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
             DeviceGuard dg(sh.device);

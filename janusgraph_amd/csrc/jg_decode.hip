@@ -172,11 +172,12 @@ __device__ __forceinline__ void skip_string(const uint8_t* __restrict__ b, int64
         } else if (l != 1) {
             bad = true;
         }
-    } else {  // full UTF: l >> 1 characters of 1 to 3 bytes
+    } else {  // full UTF: l >> 1 characters of 1 to 3 bytes (lead nibble 12/13: 2, 14: 3, any other: 1,
+              // as StringSerializer.java:126-145 consumes them)
         for (int64_t i = 0, nc = l >> 1; i < nc; ++i) {
             if (pos >= len) { bad = true; return; }
             const int hi = b[pos] >> 4;
-            pos += hi < 8 ? 1 : hi == 14 ? 3 : 2;
+            pos += hi == 14 ? 3 : (hi == 12 || hi == 13) ? 2 : 1;
         }
     }
     if (pos > len) bad = true;

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "jg_common.h"
@@ -215,6 +216,7 @@ struct Shard {
     // host copy of dense_rows (caller's dense index of each owned row), made on first use
     // (jg_api.cpp; the build no longer copies it: 67 MB at RMAT-24 through pageable memory)
     mutable std::vector<int32_t> dense_of_local_host;
+    mutable std::mutex lazy_mu;  // guards the lazy host copies (concurrent read-only callers)
     const std::vector<int32_t>& dense_of_local() const;
     DevBuf<int32_t> dense_rows;           // the same on the device (jg_scatter.h)
 
@@ -226,6 +228,7 @@ struct Shard {
     DevBuf<int32_t> cc_split_partial; // [plan_both.split_partial_len()]
     DevBuf<int32_t> cc_msg[2];     // [P*S] label if sent else INT32_MAX
     DevBuf<int32_t> cc_label;      // [rows]
+    DevBuf<int32_t> cc_rank0;      // [rows] String-order rank of each own row's id (cc_prepare_ranks, build time)
     DevBuf<int32_t> cc_depth;      // [rows] one shard's union-find path: the BFS depths
     DevBuf<int32_t> cc_hub_partial;
     DevBuf<int32_t> cc_changed;    // [1]
@@ -238,6 +241,7 @@ struct Shard {
     DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
+    DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
     std::vector<hipEvent_t> exch_events;  // start/stop pairs around the exchange steps
@@ -260,9 +264,17 @@ struct Graph {
     // host copy made on first use
     DevBuf<int32_t> padded_dev;
     mutable std::vector<int32_t> padded_host;
+    mutable std::mutex lazy_mu;  // guards the lazy host copies (padded_host, cc_vor_host)
     const std::vector<int32_t>& padded_of_dense() const;
     jg_graph_info info{};
     bool has_weights = false;
+    // String-order ranks of the ids (graphs with BOTH; jg_cc.hip cc_prepare_ranks, at build): the id of
+    // each rank on the first shard's device, its host copy made on first use (sharded CC output)
+    int kept_nsrc = 0;  // depth rows kept by jg_bfs_keep
+    bool cc_ranks = false;
+    DevBuf<int64_t> cc_vor;
+    mutable std::vector<int64_t> cc_vor_host;
+    const std::vector<int64_t>& vid_of_rank() const;
     // PageRank session
     int pr_cur = 0;
     bool pr_begun = false;
@@ -465,12 +477,18 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count);
 void pagerank_steps(Graph& g, int nsteps);
 void pagerank_end(Graph& g, double* rank_out, double* edge_count_out);
 // depth_rows[s] (each nullable, the array too): source s's depths in caller order (n int32)
-void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows);
+// keep: the depth rows stay on the device (Shard::kept_depth, Graph::kept_nsrc) for bfs_kept_row
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows,
+             bool keep = false);
+void bfs_kept_row(Graph& g, int s, int32_t* depth_out);  // row s in caller order
+void bfs_kept_release(Graph& g);
 // jg_graph_neighbors: the adjacency `direction` of caller vertices rows[0, nrows) in caller order
 void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
                      int64_t* nbr_out);
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out);
 void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out);
+// Build time (graphs with BOTH): the String-order rank of every id (Graph::cc_vor, Shard::cc_rank0).
+void cc_prepare_ranks(Graph& g);
 // The union-find's result on one shard (jg_cc.hip): parent[v] is v's root for v < ne, minr[root] the
 // smallest rank in the root's component; rows [ne, rows) have no edge (Csr::empty_from).
 struct CcRoots {
@@ -618,6 +636,8 @@ void prof_record_stop(Ctx& c, Shard& sh, int units = 1);
 void prof_collect(Ctx& c, Graph& g);
 // Event pair around an exchange step on the shard's stream (profiling only): exchange_ms.
 void exch_record(Ctx& c, Shard& sh);
+// Drops the exchange pairs recorded so far (a program's timed region starts: pairs never straddle it).
+void prof_discard_exchanges(Graph& g);
 // With profiling on, an exchange step is bracketed by events on every local shard's stream
 // (jg_stats.exchange_ms: the slowest shard's sum); the leaf exchange functions hold one.
 struct ExchTimer {

@@ -1903,11 +1903,45 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
 }
 
 
-void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows) {
+void bfs_kept_release(Graph& g) {
+    for (auto& sp : g.shards) {
+        DeviceGuard dg(sp->device);
+        sp->kept_depth.reset();
+    }
+    g.kept_nsrc = 0;
+}
+
+namespace {
+// one source's depths (a single-source traversal's rows) kept as plane 0 of every shard
+template <class F>
+void keep_rows(Graph& g, F rows_of) {
+    for (auto& sp : g.shards) {
+        Shard& sh = *sp;
+        DeviceGuard dg(sh.device);
+        sh.kept_depth.alloc(std::max<int64_t>(sh.rows, 1));
+        if (sh.rows)
+            JG_HIP(hipMemcpyAsync(sh.kept_depth.get(), rows_of(sh), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                                  sh.stream));
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    g.kept_nsrc = 1;
+}
+}  // namespace
+
+void bfs_kept_row(Graph& g, int s, int32_t* depth_out) {
+    if (s < 0 || s >= g.kept_nsrc) fail(JG_ERR_ARG, "no kept depth row with that index (jg_bfs_keep)");
+    for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->kept_depth.get() + (int64_t)s * sp->rows, depth_out);
+}
+
+void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows,
+             bool keep) {
     if (nsrc <= 0) fail(JG_ERR_ARG, "nsrc must be positive");
+    if (keep && nsrc > 64) fail(JG_ERR_ARG, "jg_bfs_keep takes at most 64 sources (one bit-parallel batch)");
+    if (keep) bfs_kept_release(g);
     if (direction < JG_DIR_OUT || direction > JG_DIR_BOTH) fail(JG_ERR_ARG, "bad direction");
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
+    prof_discard_exchanges(g);  // exchange pairs of this call only
     const bool single = nsrc == 1 && g.P == 1;
     const bool sharded_do = nsrc == 1 && g.P > 1 && g.P <= kMaxShardsBfs && direction == JG_DIR_BOTH &&
                             g.shards[0]->halo_both.on && tune().sharded_bfs;
@@ -1928,6 +1962,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
         if (depth_rows && depth_rows[0])
             for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.get(), depth_rows[0]);
+        if (keep) keep_rows(g, [](Shard& sh) { return sh.bfs_depth.get(); });
         prof_collect(ctx, g);
     } else if (single) {
         Shard& sh = sh0;
@@ -1959,6 +1994,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         const Csr* degcsr = c.push ? c.push : c.pull;
         ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
         if (depth_rows && depth_rows[0]) rows_to_dense(g, sh, depth.get(), depth_rows[0]);
+        if (keep) keep_rows(g, [](Shard& s) { return s.bfs_depth.get(); });
         prof_collect(ctx, g);
     } else {
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
@@ -1976,6 +2012,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
+                DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
                 DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs,
                                                   // [2] entries the early-exit bottom-up levels scanned
                 int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
@@ -2050,10 +2087,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         t.tlive[b].alloc(std::max<int64_t>((plan.bands[b]->tasks + 63) / 64, 1));
                     }
                 }
-                JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.nwl.get(), 0, t.nwl.bytes(), sh.stream));
                 std::vector<int64_t> loc(ns, -1);
                 for (int s = 0; s < ns; ++s)
                     if (src_local[(size_t)s] >= 0 && src_shard[(size_t)s] == sh.index) loc[s] = src_local[(size_t)s];
@@ -2061,23 +2094,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 for (int64_t l : loc)
                     if (l >= 0 && std::find(tds[i].src_rows.begin(), tds[i].src_rows.end(), l) == tds[i].src_rows.end())
                         tds[i].src_rows.push_back(l);
-                DevBuf<int64_t> dloc(ns);
-                copy_h2d(dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
-                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(dloc.get(), ns, t.F[0].get(), t.vis.get(), t.nwl.get(),
-                                                          sh.rows, g.vec_pos(sh, adj_of(sh, c)));
-                JG_LAUNCH_CHECK();
+                t.dloc.alloc(ns);
+                copy_h2d(t.dloc.get(), loc.data(), ns * sizeof(int64_t), sh.stream);
                 JG_HIP(hipStreamSynchronize(sh.stream));
             }
             allreduce_sum_i64(g, &push_nnz, 1);
             // need_fwd: the current F's halo segments are stale.  The forward exchange runs lazily, before a
             // pull level: a top-down level reads own frontier words only (and writes own rows only)
             bool need_fwd = g.P > 1;
-            if (!td_ok) {
-                std::vector<void*> bufs;
-                for (auto& t : st) bufs.push_back(t.F[0].get());
-                exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
-                need_fwd = false;
-            }
             int cur = 0, level = 0, qc = 0;
             int64_t g_nq = 0, g_mf = 0;  // the current frontier's vertices and push entries, all shards and ranks
             // touched (nullable): += the rows the top-down level just applied (its touched counter)
@@ -2152,7 +2176,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         const Halo& h = sh.halo_both;
                         td.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
                         td.hs.alloc(g.vec_len(sh, JG_ADJ_BOTH));
-                        JG_HIP(hipMemsetAsync(td.hs.get(), 0, td.hs.bytes(), sh.stream));
                         td.hlist.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
                         td.hlist_off.alloc(std::max<int64_t>(h.recv_off[g.P], 1));
                         if (tune().msbfs_sparse) {
@@ -2163,7 +2186,30 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                 }
             }
+            prof_discard_exchanges(g);  // exchange pairs never straddle t0
             JG_HIP(hipEventRecord(t0, sh0.stream));
+            // the call's state, inside the timed region: frontiers, visited bits, level 0's new-bit words (the
+            // other levels' words are zeroed as their level starts), the halo staging, the sources
+            for (size_t i = 0; i < g.shards.size(); ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh.device);
+                St& t = st[i];
+                const BfsCsrs c = pick_csrs(sh, direction);
+                JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(t.nwl.get(), 0, (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
+                if (tds[i].hs.size()) JG_HIP(hipMemsetAsync(tds[i].hs.get(), 0, tds[i].hs.bytes(), sh.stream));
+                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(t.dloc.get(), ns, t.F[0].get(), t.vis.get(), t.nwl.get(),
+                                                          sh.rows, g.vec_pos(sh, adj_of(sh, c)));
+                JG_LAUNCH_CHECK();
+            }
+            if (!td_ok) {
+                std::vector<void*> bufs;
+                for (auto& t : st) bufs.push_back(t.F[0].get());
+                exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
+                need_fwd = false;
+            }
             if (td_ok) {  // the level-0 frontier is the source rows: queued directly, no scan of F
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
@@ -2258,6 +2304,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int unskipped_levels = 0;  // pull levels that ran every merge task (msbfs_skip_first)
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
+                if (level + 1 < kMsLevelWords)  // the new-bit words this level records (rows it skips read 0)
+                    for (size_t i = 0; i < g.shards.size(); ++i) {
+                        Shard& sh = *g.shards[i];
+                        DeviceGuard dg(sh.device);
+                        JG_HIP(hipMemsetAsync(st[i].nwl.get() + (int64_t)(level + 1) * sh.rows, 0,
+                                              (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
+                    }
                 if (level + 1 >= kMsLevelWords) ensure_depth8();
                 if (level + 1 >= 255) widen();
                 const bool td_level = td_ok && (double)g_mf < (double)push_nnz / (double)tune().bfs_alpha;
@@ -2582,15 +2635,19 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             work_entries += td_entries;
             work_bytes += 12.0 * td_entries + 24.0 * td_touched + 8.0 * td_queued;
-            if (depth_rows) {
+            if (depth_rows || keep) {
                 materialize(level);  // the caller's int32 rows
-                for (size_t i = 0; i < g.shards.size(); ++i)
-                    for (int s = 0; s < ns; ++s)
-                        if (depth_rows[b0 + s])
-                            rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
-                                          depth_rows[b0 + s]);
+                if (depth_rows)
+                    for (size_t i = 0; i < g.shards.size(); ++i)
+                        for (int s = 0; s < ns; ++s)
+                            if (depth_rows[b0 + s])
+                                rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
+                                              depth_rows[b0 + s]);
+                if (keep)  // the planes stay with their shards (jg_bfs_kept_row)
+                    for (size_t i = 0; i < g.shards.size(); ++i) g.shards[i]->kept_depth.swap(st[i].depth);
             }
         }
+        if (keep) g.kept_nsrc = nsrc;
         ctx.last.compute_ms = total_ms;
         ctx.last.levels = max_levels;
         ctx.last.supersteps = max_levels;
@@ -2746,6 +2803,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
+    prof_discard_exchanges(g);  // exchange pairs of this call only
     if (!(g.flags & JG_ADJ_IN)) fail(JG_ERR_UNSUPPORTED, "shortest distance needs a graph built with JG_ADJ_IN");
     if (g.P != 1) {
         shortest_distance_sharded(g, seed_vid, max_depth, dist_out);

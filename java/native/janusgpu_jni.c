@@ -50,6 +50,11 @@ JNIEXPORT jint JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jintArray devices, j
     return st;
 }
 
+JNIEXPORT jint JNICALL FN(ctxTrim)(JNIEnv* env, jclass c, jlong ctx) {
+    (void)env; (void)c;
+    return jg_ctx_trim((jg_ctx*)(intptr_t)ctx);
+}
+
 JNIEXPORT jint JNICALL FN(ctxDestroy)(JNIEnv* env, jclass c, jlong ctx) {
     (void)env; (void)c;
     return jg_ctx_destroy((jg_ctx*)(intptr_t)ctx);
@@ -185,6 +190,22 @@ JNIEXPORT jint JNICALL FN(bfsRows)(JNIEnv* env, jclass c, jlong g, jobject sourc
     int st = jg_bfs_rows((jg_graph*)(intptr_t)g, (const int64_t*)buf(env, sources), nsrc, direction, max_depth, rows);
     free(rows);
     return st;
+}
+
+JNIEXPORT jint JNICALL FN(bfsKeep)(JNIEnv* env, jclass c, jlong g, jobject sources, jint nsrc, jint direction,
+                                   jint max_depth) {
+    (void)c;
+    return jg_bfs_keep((jg_graph*)(intptr_t)g, (const int64_t*)buf(env, sources), nsrc, direction, max_depth);
+}
+
+JNIEXPORT jint JNICALL FN(bfsKeptRow)(JNIEnv* env, jclass c, jlong g, jint s, jobject depth_out) {
+    (void)c;
+    return jg_bfs_kept_row((jg_graph*)(intptr_t)g, s, (int32_t*)buf(env, depth_out));
+}
+
+JNIEXPORT jint JNICALL FN(bfsKeptRelease)(JNIEnv* env, jclass c, jlong g) {
+    (void)env; (void)c;
+    return jg_bfs_kept_release((jg_graph*)(intptr_t)g);
 }
 
 JNIEXPORT jint JNICALL FN(graphNeighbors)(JNIEnv* env, jclass c, jlong g, jint direction, jobject rows, jlong nrows,

@@ -83,8 +83,17 @@ import java.util.function.IntFunction;
  *
  * Entry: {@code graph.compute(GpuGraphComputer.class)} once JanusGraphBlueprintsGraph.compute(Class)
  * (janusgraph-core/.../tinkerpop/JanusGraphBlueprintsGraph.java:155-161) whitelists this class
- * (java/patches/0001); the transaction variant delegates to it. Devices: system property
- * janusgraph.computer.gpu.devices (comma list, default "0"); several devices shard the graph 1D.
+ * (java/patches/0001); the transaction variant delegates to it.
+ *
+ * Configuration (the graph's own, registered by patch 0001 under computer.gpu next to
+ * computer.result-mode, GraphDatabaseConfiguration.java:203-208; MASKABLE, so per graph):
+ * <ul>
+ *   <li>computer.gpu.devices (default "0"): HIP devices; several shard the snapshot 1D by vertex;</li>
+ *   <li>computer.gpu.untruncated (default false): keep every entry instead of Fulgora's 100000-entry
+ *       slice cap;</li>
+ *   <li>computer.gpu.direct-memory (default 1 GiB): most bytes of direct result buffers held at once;</li>
+ *   <li>computer.gpu.default (default false, read by patch 0001): graph.compute() returns this computer.</li>
+ * </ul>
  */
 public class GpuGraphComputer extends FulgoraGraphComputer {
 
@@ -101,6 +110,9 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
 
     private final StandardJanusGraph graph;
     private final int writeBatchSize;
+    private final int[] devices;
+    private final long queryLimit;
+    private final long directMemory;
     private VertexProgram<?> vertexProgram;
     private boolean filtered;
 
@@ -108,6 +120,11 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         super(graph, configuration);
         this.graph = graph;
         this.writeBatchSize = configuration.get(GraphDatabaseConfiguration.BUFFER_SIZE);
+        this.devices = devices(configuration.get(GraphDatabaseConfiguration.COMPUTER_GPU_DEVICES));
+        this.queryLimit = queryLimit(configuration.get(GraphDatabaseConfiguration.COMPUTER_GPU_UNTRUNCATED));
+        this.directMemory = configuration.get(GraphDatabaseConfiguration.COMPUTER_GPU_DIRECT_MEMORY);
+        if (directMemory < (64L << 20))
+            throw new IllegalArgumentException("computer.gpu.direct-memory must be at least 64 MiB");
     }
 
     // ---- the GraphComputer builder: Fulgora records the settings; the GPU path reads them back ----
@@ -148,15 +165,15 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         final long time = System.currentTimeMillis();
         vertexProgram.setup(memory);
         final long[] h = new long[1];
-        JanusGpu.check(JanusGpu.ctxCreate(devices(), h));
+        JanusGpu.check(JanusGpu.ctxCreate(devices, h));
         final long ctx = h[0];
         final Results res;
         try {
-            final long g = GpuSnapshot.scan(graph, ctx, run.adjacency(), run.weightProperty(), queryLimit(),
+            final long g = GpuSnapshot.scan(graph, ctx, run.adjacency(), run.weightProperty(), queryLimit,
                 run.inEntries());
             try {
                 final long[] vid = GpuSnapshot.vertexIds(g);
-                res = run.execute(g, vid, graph, memory);
+                res = run.execute(g, vid, graph, memory, directMemory);
             } finally {
                 JanusGpu.graphDestroy(g);
             }
@@ -175,15 +192,16 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
     /**
      * Fulgora's hard limit on the entries of a non-fitted slice (QueryContainer.DEFAULT_HARD_QUERY_LIMIT,
      * olap/QueryContainer.java:42,133): the snapshot reproduces it, so vertices with more than 100000
-     * edge entries get exactly the truncated adjacency Fulgora computes on.  The system property
-     * janusgraph.computer.gpu.untruncated=true computes on every entry instead.
+     * edge entries get exactly the truncated adjacency Fulgora computes on.  computer.gpu.untruncated=true
+     * computes on every entry instead.
      */
-    private static long queryLimit() {
-        return Boolean.getBoolean("janusgraph.computer.gpu.untruncated") ? 0L : QueryContainer.DEFAULT_HARD_QUERY_LIMIT;
+    static long queryLimit(boolean untruncated) {
+        return untruncated ? 0L : QueryContainer.DEFAULT_HARD_QUERY_LIMIT;
     }
 
-    private static int[] devices() {
-        final String[] parts = System.getProperty("janusgraph.computer.gpu.devices", "0").split(",");
+    /** computer.gpu.devices: HIP device ordinals (a String[] option: "0,1" or a list in the properties file). */
+    static int[] devices(String[] parts) {
+        if (parts == null || parts.length == 0) throw new IllegalArgumentException("computer.gpu.devices is empty");
         final int[] d = new int[parts.length];
         for (int i = 0; i < parts.length; i++) d[i] = Integer.parseInt(parts[i].trim());
         return d;
@@ -383,7 +401,8 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
             return JanusGpu.DIR_IN;
         }
 
-        abstract Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory);
+        /** directMemory: computer.gpu.direct-memory, the most bytes of direct buffers held at once. */
+        abstract Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory, long directMemory);
 
         static GpuProgram recognise(VertexProgram<?> vp, StandardJanusGraph graph) {
             final String name = vp.getClass().getName();
@@ -436,7 +455,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
 
         @Override
-        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory) {
+        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory, long directMemory) {
             final ByteBuffer rank = direct(8L * vid.length), count = direct(8L * vid.length);
             JanusGpu.check(JanusGpu.pageRank(g, damping, vertexCount, iterations, rank, count));
             final Results r = new Results(vid, iterations);
@@ -490,7 +509,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
 
         @Override
-        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory) {
+        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory, long directMemory) {
             final ByteBuffer dist = direct(8L * vid.length);
             JanusGpu.check(JanusGpu.shortestDistance(g, seed, maxDepth, dist));
             final Results r = new Results(vid, maxDepth);
@@ -534,7 +553,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
 
         @Override
-        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory) {
+        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory, long directMemory) {
             final ByteBuffer comp = direct(8L * vid.length);
             final int[] it = new int[1];
             JanusGpu.check(JanusGpu.connectedComponents(g, comp, it));
@@ -597,7 +616,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         }
 
         @Override
-        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory) {
+        Results execute(long g, long[] vid, StandardJanusGraph graph, FulgoraMemory memory, long directMemory) {
             final int n = vid.length;
             final JanusGraphTransaction tx = graph.buildTransaction().readOnly().start();
             try {
@@ -619,23 +638,31 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
                 final Map<Integer, Vertex> detached = new HashMap<>(); // path elements, detached once each
                 final IntFunction<Vertex> element =
                     i -> detached.computeIfAbsent(i, x -> ReferenceFactory.detach(tx.getVertex(vid[x])));
-                final PathDag dag = new PathDag(g, n);
+                // Direct memory: one depth row (4n bytes, reused by every source) and the walk-back's
+                // neighbour batches (PathDag: at most half the budget); the batch's 64 rows stay on the
+                // device (jg_bfs_keep) and come over one at a time (jg_bfs_kept_row).
+                if (4L * n > directMemory / 2)
+                    throw new JanusGraphException("GPU computer: a depth row of " + n + " vertices needs more than half "
+                        + "of computer.gpu.direct-memory (" + directMemory + " bytes)");
+                final PathDag dag = new PathDag(g, n, directMemory / 2);
+                final ByteBuffer row = direct(4L * n);
+                final ByteBuffer src = direct(8L * SOURCES_PER_BFS);
                 final List<Path> paths = new ArrayList<>();
                 int maxLevel = 0;
-                for (int b = 0; b < sources.length; b += SOURCES_PER_BFS) {
-                    final int k = Math.min(SOURCES_PER_BFS, sources.length - b);
-                    final ByteBuffer src = direct(8L * k);
-                    final ByteBuffer[] rows = new ByteBuffer[k];
-                    for (int j = 0; j < k; j++) {
-                        src.putLong(vid[sources[b + j]]);
-                        rows[j] = direct(4L * n);
+                try {
+                    for (int b = 0; b < sources.length; b += SOURCES_PER_BFS) {
+                        final int k = Math.min(SOURCES_PER_BFS, sources.length - b);
+                        src.clear();
+                        for (int j = 0; j < k; j++) src.putLong(vid[sources[b + j]]);
+                        JanusGpu.check(JanusGpu.bfsKeep(g, src, k, JanusGpu.DIR_BOTH, maxDistance));
+                        for (int j = 0; j < k; j++) {
+                            JanusGpu.check(JanusGpu.bfsKeptRow(g, j, row));
+                            maxLevel = Math.max(maxLevel, dag.paths(row.asIntBuffer(), sources[b + j], target, element,
+                                paths));
+                        }
                     }
-                    JanusGpu.check(JanusGpu.bfsRows(g, src, k, JanusGpu.DIR_BOTH, maxDistance, rows));
-                    for (int j = 0; j < k; j++) {
-                        final IntBuffer depth = rows[j].asIntBuffer();
-                        rows[j] = null;
-                        maxLevel = Math.max(maxLevel, dag.paths(depth, sources[b + j], target, element, paths));
-                    }
+                } finally {
+                    JanusGpu.bfsKeptRelease(g);
                 }
                 memory.set(ShortestPathVertexProgram.SHORTEST_PATHS, paths);
                 return new Results(vid, maxLevel + 1);
@@ -656,11 +683,13 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
         private static final int ROWS_PER_CALL = 1 << 14;
         private final long graph;
         private final int[] mark; // de-duplicates a vertex's neighbours (multi-edges, self-loops)
+        private final long budget; // most bytes of the neighbour batch's direct buffers
         private int stamp;
 
-        PathDag(long graph, int n) {
+        PathDag(long graph, int n, long budget) {
             this.graph = graph;
             this.mark = new int[n];
+            this.budget = Math.min(budget, Integer.MAX_VALUE);
         }
 
         /** Adds the source's paths to `out`; returns the deepest target depth (0 when none). */
@@ -729,7 +758,7 @@ public class GpuGraphComputer extends FulgoraGraphComputer {
             JanusGpu.check(JanusGpu.graphNeighbors(graph, JanusGpu.DIR_BOTH, r, k, off, null));
             final long[] o = new long[k + 1];
             off.asLongBuffer().get(o);
-            if (8L * o[k] > Integer.MAX_VALUE && k > 1) { // a hub-heavy batch: split it
+            if (8L * o[k] + 16L * (k + 1) > budget && k > 1) { // a hub-heavy batch: split it
                 final int mid = from + k / 2;
                 final long[][] a = neighbors(rows, from, mid), b = neighbors(rows, mid, to);
                 final long[] oo = Arrays.copyOf(a[0], k + 1);

@@ -19,7 +19,7 @@ import java.nio.ByteBuffer;
  */
 final class JanusGpu {
     /** JG_ABI_VERSION of include/janusgpu.h that these natives and their array layouts follow. */
-    static final int ABI_VERSION = 2;
+    static final int ABI_VERSION = 3;
 
     static {
         System.loadLibrary("janusgpu_jni"); // links libjanusgpu.so
@@ -42,6 +42,8 @@ final class JanusGpu {
     /** jg_ctx_create(devices, ndev, &ctx); handle written to out[0]. */
     static native int ctxCreate(int[] devices, long[] out);
     static native int ctxDestroy(long ctx);
+    /** jg_ctx_trim: the device memory libjanusgpu caches for reuse goes back to the devices. */
+    static native int ctxTrim(long ctx);
     /** jg_ctx_last_stats: supersteps, levels, build_ms, compute_ms, exchange_ms, kernel_ms, launches, bytes, edges. */
     static native int ctxLastStats(long ctx, double[] out9);
 
@@ -80,6 +82,12 @@ final class JanusGpu {
     /** jg_bfs_rows: one int32 direct buffer of n depths per source (null: not wanted). */
     static native int bfsRows(long graph, ByteBuffer sourceVids, int nsrc, int direction, int maxDepth,
                               ByteBuffer[] depthRows);
+    /** jg_bfs_keep: the traversal's depth rows (<= 64 sources) stay on the device for bfsKeptRow. */
+    static native int bfsKeep(long graph, ByteBuffer sourceVids, int nsrc, int direction, int maxDepth);
+    /** jg_bfs_kept_row: row s of the last bfsKeep into an int32 direct buffer of n depths. */
+    static native int bfsKeptRow(long graph, int s, ByteBuffer depthOut);
+    /** jg_bfs_kept_release: frees the kept rows before the graph goes. */
+    static native int bfsKeptRelease(long graph);
     /** jg_graph_neighbors: rows (int64 output-order indices) -> offsets (int64, nrows + 1) and neighbours
      *  (int64 output-order indices; null: offsets only). */
     static native int graphNeighbors(long graph, int direction, ByteBuffer rows, long nrows, ByteBuffer offOut,

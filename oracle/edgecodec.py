@@ -222,8 +222,8 @@ def write_gzip_string_header(nbytes: int) -> bytes:
 
 def write_value(ptype: int, v) -> bytes:
     """StandardSerializer.writeObject: a null flag (0 / -1) unless String, then the serializer's bytes."""
-    if ptype == STRING:
-        return write_string(v)
+    if ptype == STRING:  # bytes: a pre-encoded String (malformed-input tests)
+        return bytes(v) if isinstance(v, (bytes, bytearray)) else write_string(v)
     if v is None:
         return b"\xff"
     if ptype == INT:
@@ -257,9 +257,9 @@ def _skip_string(b: bytes, pos: int) -> int:
                 pos += 1
             pos += 1
         return pos
-    for _ in range(n >> 1):
+    for _ in range(n >> 1):  # StringSerializer.java:126-145: lead nibble 12/13 two bytes, 14 three, else one
         hi = b[pos] >> 4
-        pos += 1 if hi < 8 else 3 if hi == 14 else 2
+        pos += 3 if hi == 14 else 2 if hi in (12, 13) else 1
     return pos
 
 

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_no_gpu_error_is_a_status():
     import janusgraph_amd as jg
     lib = jg.load()
-    assert lib.jg_abi_version() == 2
+    assert lib.jg_abi_version() == 3
     try:
         import torch
         has_gpu = torch.cuda.is_available()

@@ -10,7 +10,9 @@ Every result is checked against the CPU restatement in oracle/ on the same Graph
   configs[3]  ConnectedComponent, RMAT-26 ef16: every String-min label and the iteration count exact, on
               1 shard (union-find + root BFS) and on 2 and 8 logical shards (the label propagation with
               its halo exchange that 2..8 GPUs run), plus the sharded single-source DO-BFS (dobfs_sharded,
-              what a BFS on 2..8 GPUs runs) from 3 degree > 0 sources on the same sharded graphs.
+              what a BFS on 2..8 GPUs runs) from 3 degree > 0 sources on the same sharded graphs (2, 4
+              and 8 shards), and the one-GPU DO-BFS the bench times at this size (3 sources, one
+              depth-bounded, Graph500 validation).
   configs[4]  64-source MS-BFS, RMAT-26 ef16 on 8 logical shards (the 8-GPU layout and halo exchange on
               one device): all 64 depth rows bit-exact, plus Graph500 validation of 3 of them.
 The oracle side uses the parallel checkers of jg_oracle.c (jo_csr_unordered, jo_bfs_csr,
@@ -138,7 +140,41 @@ def test_config3_cc_rmat26(rmat26):
     ctx.close()
 
 
-@pytest.mark.parametrize("shards", [2, 8])
+def test_config3_dobfs_rmat26_one_gpu(oracle_lib, rmat26):
+    """The single-GPU DO-BFS at RMAT-26 that bench.py's rmat26.bfs block times: one shard, BOTH CSR of
+    2.15 G entries (past 2^31: int64 row offsets, the 2^31-entry boundary inside the hub rows).  Sources
+    are the bench's first candidates (same seeded pick among degree > 0 vertices), one depth-bounded;
+    depths bit-exact against the oracle, Graph500 validation of one (SPVP's forced BOTH scope,
+    FulgoraGraphComputer.java:249-253)."""
+    import janusgraph_amd as jg
+    o = oracle_lib
+    r = rmat26
+    n = r["n"]
+    ctx = jg.Context((0,))
+    g = ctx.build_rmat(26, EF, seed_of(26), flags=jg.ADJ_BOTH)
+    assert g.info()["num_shards"] == 1
+    deg = np.diff(r["ptr"])
+    cand = np.flatnonzero(deg > 0)
+    srcs = np.random.default_rng(26).choice(cand, 16, replace=False)[:3]  # bench.py bfs_block's first draws
+    for k, sv in enumerate(srcs.tolist()):
+        got = g.bfs([sv], jg.DIR_BOTH)[0]
+        want = o.bfs_csr(n, r["ptr"], r["adj"], sv)
+        np.testing.assert_array_equal(got, want, err_msg=f"one GPU: DO-BFS from {sv}")
+        if k == 0:
+            err, edges = o.bfs_validate(n, r["s"], r["d"], got, sv, r["label"])
+            assert err == 0 and edges > 0, f"Graph500 validation bits {err} for source {sv}"
+        del got
+        if k == 1:
+            bounded = g.bfs([sv], jg.DIR_BOTH, max_depth=3)[0]
+            np.testing.assert_array_equal(bounded, o.bfs_csr(n, r["ptr"], r["adj"], sv, 3),
+                                          err_msg=f"one GPU: DO-BFS from {sv}, maxDepth 3")
+            del bounded
+        del want
+    g.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("shards", [2, 4, 8])
 def test_config3_sharded_cc_and_dobfs_rmat26(oracle_lib, rmat26, shards):
     """The code paths 2..8 GPUs run at configs[3]'s size: CC by label propagation over the BOTH halo
     (not the one-shard union-find), and single-source DO-BFS by dobfs_sharded (halo refresh for

@@ -93,3 +93,31 @@ def test_bfs_rows_equal_bfs(oracle_lib):
                     assert r is None
         g.close()
         ctx.close()
+
+
+def test_bfs_keep_rows_equal_bfs(oracle_lib):
+    """jg_bfs_keep + jg_bfs_kept_row (ShortestPaths' bounded direct memory): every kept row equals jg_bfs's,
+    on the single-source, sharded single-source and bit-parallel paths; a later keep replaces the rows,
+    release (and a bad index) fails the row read with JG_ERR_ARG."""
+    import janusgraph_amd as jg
+    n, vid, s, t = graph_edges(oracle_lib, scale=12, seed=9)
+    for shards in (1, 3):
+        ctx = jg.Context((0,) * shards)
+        g = ctx.build(vid, vid[s], vid[t], flags=jg.ADJ_BOTH)
+        for srcs, depth in (([vid[3]], -1), (list(vid[:64]), 4), ([vid[7]], 2), (list(vid[5:10]), -1)):
+            full = g.bfs(srcs, jg.DIR_BOTH, max_depth=depth)
+            g.bfs_keep(srcs, jg.DIR_BOTH, depth)
+            out = np.empty(n, np.int32)
+            for k in range(len(srcs)):
+                np.testing.assert_array_equal(g.bfs_kept_row(k, out), full[k], err_msg=f"{shards} shards, row {k}")
+            with pytest.raises(jg.JanusGpuError) as e:
+                g.bfs_kept_row(len(srcs))
+            assert e.value.code == jg._lib.JG_ERR_ARG
+        g.bfs_kept_release()
+        with pytest.raises(jg.JanusGpuError):
+            g.bfs_kept_row(0)
+        with pytest.raises(jg.JanusGpuError):
+            g.bfs_keep(list(vid[:65]), jg.DIR_BOTH)  # one bit-parallel batch at most
+        g.close()
+        ctx.trim()
+        ctx.close()

@@ -25,8 +25,9 @@ KEY_TYPES = {LONG_KEY: ec.LONG, NAME_KEY: ec.STRING, DIST_KEY: ec.INT, SCORE_KEY
 VEXISTS = ec.schema_id(1, "system_key")
 
 
-def weighted_store(n=400, m=3000, seed=0, weight_of=None):
-    """(store arrays, labels table, per-entry host weights); weight_of(e, rng) -> weight or None (absent)."""
+def weighted_store(n=400, m=3000, seed=0, weight_of=None, name_of=None):
+    """(store arrays, labels table, per-entry host weights); weight_of(e, rng) -> weight or None (absent);
+    name_of(rng) -> the String property's value (every edge gets one) or pre-encoded bytes."""
     rng = np.random.default_rng(seed)
     idm = IDManager(5)
     vids = sorted({(((int(c) << 5) + int(p)) << 3) for c, p in zip(rng.integers(1, 1 << 30, n), rng.integers(0, 32, n))})
@@ -41,7 +42,9 @@ def weighted_store(n=400, m=3000, seed=0, weight_of=None):
         props = []
         if rng.random() < 0.5:
             props.append((LONG_KEY, ec.LONG, int(rng.integers(0, 1 << 62))))
-        if rng.random() < 0.5:
+        if name_of is not None:
+            props.append((NAME_KEY, ec.STRING, name_of(rng)))
+        elif rng.random() < 0.5:
             props.append((NAME_KEY, ec.STRING, [None, "", "x", "abc" * 5, "é", "€uro"][int(rng.integers(0, 6))]))
         w = weight_of(e, rng) if weight_of else int(rng.integers(-3, 9))
         if w is not None:
@@ -160,6 +163,30 @@ def test_device_weights_all_present_match_oracle(oracle_lib):
                                       oracle_lib.shortest_distance(len(vid), ds, dd, s, 6, hw[ent].astype(np.int32)))
     g.close()
     ctx.close()
+
+
+def full_utf_raw(body: bytes) -> bytes:
+    """A full-UTF String of len(body) one-byte characters as StringSerializer.write would frame it, with lead
+    bytes the writer never emits (nibbles 8-11 and 15): StringSerializer.read (:126-145) consumes one byte
+    for each, so the property after it is still found."""
+    return ec.write_positive((len(body) << 4) + (1 << 3)) + bytes(body)
+
+
+def test_device_weights_after_odd_utf_lead_bytes(oracle_lib):
+    """skip_string consumed two bytes for lead nibbles 8-11 and 15; the reference one."""
+    odd = [full_utf_raw(bytes([0x85, 0x41])), full_utf_raw(bytes([0x9A, 0xB0, 0xF3])), full_utf_raw(bytes([0xA1]))]
+    # every edge carries one of the odd strings, the weight after it
+    store2, hw2 = weighted_store(n=200, m=1500, seed=11, weight_of=lambda e, rng: int(rng.integers(0, 9)),
+                                 name_of=lambda rng: odd[int(rng.integers(0, len(odd)))])
+    assert (hw2 != ec.WEIGHT_ABSENT).sum() > 1000  # the oracle's parser finds the weight after each
+    ctx_d, gd = build(store2)
+    ctx_h, gh = build(store2, host_weight=hw2)
+    vid = gd.vertex_ids()
+    for s in (0, 17, 101):
+        np.testing.assert_array_equal(gd.shortest_distance(int(vid[s]), 2), gh.shortest_distance(int(vid[s]), 2))
+    for g, c in ((gd, ctx_d), (gh, ctx_h)):
+        g.close()
+        c.close()
 
 
 def test_weight_key_errors():

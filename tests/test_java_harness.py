@@ -89,7 +89,11 @@ MEMBERS = [
     (f"{CORE}/graphdb/olap/computer/FulgoraGraphComputer.java",
      r"public FulgoraGraphComputer\(final StandardJanusGraph graph, final Configuration configuration\)"),
     (f"{CORE}/graphdb/tinkerpop/JanusGraphBlueprintsGraph.java", r"graphComputerClass\.equals\(GpuGraphComputer\.class\)"),
-    (f"{CORE}/graphdb/tinkerpop/JanusGraphBlueprintsGraph.java", r"janusgraph\.computer\.gpu\.default"),
+    (f"{CORE}/graphdb/tinkerpop/JanusGraphBlueprintsGraph.java",
+     r"getConfiguration\(\)\.getConfiguration\(\)\.get\(GraphDatabaseConfiguration\.COMPUTER_GPU_DEFAULT\)"),
+    (f"{CORE}/diskstorage/configuration/ModifiableConfiguration.java",
+     r"public ModifiableConfiguration\(ConfigNamespace root, WriteConfiguration config, Restriction restriction\)"),
+    (f"{CORE}/diskstorage/configuration/BasicConfiguration.java", r"public enum Restriction \{ LOCAL, GLOBAL, NONE \}"),
     (f"{CORE}/graphdb/olap/computer/FulgoraMemory.java", r"public FulgoraMemory\(final VertexProgram<\?> vertexProgram"),
     (f"{CORE}/graphdb/olap/computer/FulgoraMemory.java", r"void attachReferenceElements\(Graph graph\)"),
     (f"{CORE}/graphdb/olap/computer/FulgoraMemory.java", r"void setIteration\(final int iteration\)"),
@@ -120,3 +124,42 @@ MEMBERS = [
 def test_reference_member_exists(patched, path, pattern):
     f = patched / path if path.startswith("janusgraph-core/") else os.path.join(REF, path)
     assert re.search(pattern, open(f).read()), f"{path}: no match for {pattern}"
+
+
+# computer.gpu.* (VERDICT r03 item 7): the options GpuGraphComputer and the harness read
+GPU_OPTIONS = {"COMPUTER_GPU_DEFAULT": ("Boolean", "default"), "COMPUTER_GPU_DEVICES": ("String[]", "devices"),
+               "COMPUTER_GPU_UNTRUNCATED": ("Boolean", "untruncated"),
+               "COMPUTER_GPU_DIRECT_MEMORY": ("Long", "direct-memory")}
+
+
+def test_gpu_options_registered_under_computer_ns(patched):
+    """Every GraphDatabaseConfiguration.COMPUTER_GPU_* that java/ uses is a ConfigOption of the type the code
+    reads, in the computer.gpu namespace (a child of COMPUTER_NS, next to computer.result-mode), MASKABLE
+    (per graph), built with a ConfigOption constructor the reference has; no name collides in the namespace."""
+    gdc = open(patched / CORE / "graphdb/configuration/GraphDatabaseConfiguration.java").read()
+    assert re.search(r'ConfigNamespace COMPUTER_GPU_NS = new ConfigNamespace\(COMPUTER_NS,"gpu",', gdc)
+    used = set()
+    for path in java_sources():
+        used |= set(re.findall(r"GraphDatabaseConfiguration\.(COMPUTER_GPU_\w+)", open(path).read()))
+    used |= set(re.findall(r"GraphDatabaseConfiguration\.(COMPUTER_GPU_\w+)",
+                           open(patched / CORE / "graphdb/tinkerpop/JanusGraphBlueprintsGraph.java").read()))
+    assert used == set(GPU_OPTIONS), used
+    names = []
+    for const, (typ, name) in GPU_OPTIONS.items():
+        m = re.search(r"public static final ConfigOption<" + re.escape(typ) + r"> " + const +
+                      r' = new ConfigOption<>\(COMPUTER_GPU_NS,"([\w-]+)",(.*?);\n', gdc, re.S)
+        assert m, const
+        assert m.group(1) == name and "ConfigOption.Type.MASKABLE" in m.group(2), const
+        names.append(m.group(1))
+    assert len(set(names)) == len(names)
+    opt = open(patched / CORE / "diskstorage/configuration/ConfigOption.java").read()
+    assert re.search(r"public ConfigOption\(ConfigNamespace parent, String name, String description, Type type, "
+                     r"O defaultValue\)", opt)
+    assert re.search(r"enum Type \{", opt) and "MASKABLE" in opt
+
+
+def test_drop_in_reads_no_system_properties():
+    """The drop-in's settings come from the graph's configuration only (two graphs in one JVM may differ)."""
+    for path in java_sources():
+        src = open(path).read()
+        assert "System.getProperty" not in src and "Boolean.getBoolean" not in src, path

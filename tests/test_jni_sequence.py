@@ -147,23 +147,54 @@ def test_connected_components_sequence(oracle_lib, store):
     r.close()
 
 
-def jni_bfs_rows(L, g, src_vids, n, max_depth):
-    """JanusGpu.bfsRows as ShortestPaths.execute calls it: one direct(4L * n) buffer per source."""
+class DirectMemory:
+    """The direct (off-heap) bytes GpuGraphComputer.ShortestPaths holds at once: GpuGraphComputer.direct()
+    buffers, released when the Java code drops them (computer.gpu.direct-memory bounds the peak)."""
+
+    def __init__(self):
+        self.live = self.peak = 0
+
+    def take(self, nbytes):
+        self.live += max(int(nbytes), 8)
+        self.peak = max(self.peak, self.live)
+
+    def drop(self, nbytes):
+        self.live -= max(int(nbytes), 8)
+
+
+def jni_kept_rows(L, g, src_vids, n, max_depth, row, mem=None):
+    """ShortestPaths.execute's batch: JanusGpu.bfsKeep (the 64 rows stay on the device), then bfsKeptRow
+    into ONE reused direct(4L * n) buffer per source; yields that buffer once per source."""
     src = np.ascontiguousarray(src_vids, np.int64)
-    rows = [np.empty(n, np.int32) for _ in range(len(src))]
-    ptrs = (ctypes.c_void_p * len(src))(*[r.ctypes.data for r in rows])
-    _ok(L.jg_bfs_rows(g, _p(src), len(src), 3, max_depth, ptrs))  # JanusGpu.DIR_BOTH
-    return rows
+    _ok(L.jg_bfs_keep(g, _p(src), len(src), 3, max_depth))  # JanusGpu.DIR_BOTH
+    for j in range(len(src)):
+        _ok(L.jg_bfs_kept_row(g, j, _p(row)))
+        yield row
 
 
-def jni_neighbors(L, g):
-    """PathDag.neighbors: JanusGpu.graphNeighbors once for the offsets, once more for the neighbours."""
+def jni_neighbors(L, g, budget=1 << 62, mem=None):
+    """PathDag.neighbors: JanusGpu.graphNeighbors once for the offsets, once more for the neighbours; a batch
+    whose buffers would pass the walk-back's budget (computer.gpu.direct-memory / 2) is split in halves."""
     def call(rows):
         r = np.ascontiguousarray(rows, np.int64)
-        off = np.empty(len(r) + 1, np.int64)
-        _ok(L.jg_graph_neighbors(g, 3, _p(r), len(r), _p(off), None))
+        k = len(r)
+        off = np.empty(k + 1, np.int64)
+        if mem:
+            mem.take(8 * k + 8 * (k + 1))
+        _ok(L.jg_graph_neighbors(g, 3, _p(r), k, _p(off), None))
+        if 8 * int(off[-1]) + 16 * (k + 1) > budget and k > 1:
+            if mem:
+                mem.drop(8 * k + 8 * (k + 1))
+            mid = k // 2
+            oa, na = call(r[:mid])
+            ob, nb_ = call(r[mid:])
+            return np.concatenate([oa, oa[-1] + ob[1:]]), np.concatenate([na, nb_])
         nbr = np.empty(max(int(off[-1]), 1), np.int64)
-        _ok(L.jg_graph_neighbors(g, 3, _p(r), len(r), _p(off), _p(nbr)))
+        if mem:
+            mem.take(8 * int(off[-1]))
+        _ok(L.jg_graph_neighbors(g, 3, _p(r), k, _p(off), _p(nbr)))
+        if mem:
+            mem.drop(8 * int(off[-1]) + 8 * k + 8 * (k + 1))
         return off, nbr[:int(off[-1])]
     return call
 
@@ -194,8 +225,11 @@ def all_shortest_paths(adj, s, t):
 
 
 def test_shortest_path_sequence_batches_of_64(oracle_lib, store):
-    """ShortestPaths.execute: 70 sources -> two jg_bfs_rows calls (64 + 6), DIR_BOTH, maxDistance; paths
-    rebuilt by PathDag (predecessors read through jg_graph_neighbors) -> every shortest path."""
+    """ShortestPaths.execute: 70 sources -> two jg_bfs_keep batches (64 + 6: the bit-parallel and the
+    single-source paths), each row read back by jg_bfs_kept_row into one buffer, DIR_BOTH, maxDistance;
+    paths rebuilt by PathDag (predecessors read through jg_graph_neighbors, batches split under a tiny
+    budget) -> every shortest path."""
+    from janusgraph_amd import _lib
     from janusgraph_amd.computer import PathDag
     ov, ds, dd = oracle_graph(oracle_lib, store)
     r = JavaRun(store[0], flags=4)
@@ -208,14 +242,16 @@ def test_shortest_path_sequence_batches_of_64(oracle_lib, store):
     target = np.zeros(n, bool)
     target[::9] = True
     max_distance = 3
-    dag = PathDag(jni_neighbors(r.L, r.g), n)
+    dag = PathDag(jni_neighbors(r.L, r.g, budget=1 << 12), n)  # a tiny budget: the batch split runs
     got = set()
+    row = np.empty(n, np.int32)
     for b0 in range(0, len(sources), 64):
         batch = sources[b0:b0 + 64]
-        rows = jni_bfs_rows(r.L, r.g, ov[batch], n, max_distance)
-        for s, depth in zip(batch, rows):
+        for s, depth in zip(batch, jni_kept_rows(r.L, r.g, ov[batch], n, max_distance, row)):
             paths, _ = dag.paths(depth, s, target)
             got |= {tuple(p) for p in paths}
+    _ok(r.L.jg_bfs_kept_release(r.g))
+    assert r.L.jg_bfs_kept_row(r.g, 0, _p(row)) == _lib.JG_ERR_ARG  # released
     want = set()
     for s in sources:
         for t in np.flatnonzero(target).tolist():
@@ -227,10 +263,11 @@ def test_shortest_path_sequence_batches_of_64(oracle_lib, store):
 
 
 def test_shortest_path_sequence_rmat24(oracle_lib):
-    """ShortestPaths.execute at BASELINE scale (configs[4]'s program on RMAT-24, n = 2^24): a 64-source
-    batch as 64 separate 4n-byte depth buffers (one 64 x n buffer would be 4 GiB, past Java's 2 GiB
-    direct-buffer limit), vertex ids read back in GpuSnapshot.vertexIds chunks of 2^24; three depth rows
-    against oracle.bfs_csr, and PathDag's predecessor lists and path counts against the oracle's CSR."""
+    """ShortestPaths.execute at RMAT-24 (n = 2^24) from a snapshot built the GpuSnapshot way (vertex and edge
+    ids in chunks under a direct buffer's 2 GiB): a 64-source batch kept on the device and read back one
+    row at a time into one 4n-byte buffer, vertex ids read back in GpuSnapshot.vertexIds chunks of 2^24;
+    three depth rows against oracle.bfs_csr, and PathDag's predecessor lists and path counts against the
+    oracle's CSR."""
     from janusgraph_amd import _lib
     from janusgraph_amd.computer import PathDag
     from test_gpu_configs import host_edges, pick_sources
@@ -261,11 +298,13 @@ def test_shortest_path_sequence_rmat24(oracle_lib):
     ptr, adj = o.csr_unordered(n, s, d, both=True)
     del s, d
     srcs = pick_sources(ptr, 64, scale)
-    rows = jni_bfs_rows(L, g, vid[srcs], n, -1)
-    for k in (0, 31, 63):
-        np.testing.assert_array_equal(rows[k], o.bfs_csr(n, ptr, adj, int(srcs[k])))
-    depth = rows[0]
-    del rows[1:]
+    row = np.empty(n, np.int32)
+    depth = None
+    for k, got in enumerate(jni_kept_rows(L, g, vid[srcs], n, -1, row)):
+        if k in (0, 31, 63):
+            np.testing.assert_array_equal(got, o.bfs_csr(n, ptr, adj, int(srcs[k])))
+        if k == 0:
+            depth = got.copy()
     rng = np.random.default_rng(5)
     reached = np.flatnonzero(depth >= 1)
     target = np.zeros(n, bool)
@@ -284,5 +323,51 @@ def test_shortest_path_sequence_rmat24(oracle_lib):
     assert deepest == 2
     want = sum(len(np.unique(adj[ptr[t]:ptr[t + 1]][depth[adj[ptr[t]:ptr[t + 1]]] == 1])) for t in near.tolist())
     assert len(paths) == want and all(p[0] == srcs[0] and len(p) == 3 for p in paths)
+    _ok(L.jg_graph_destroy(g))
+    _ok(L.jg_ctx_destroy(ctx))
+
+
+def test_shortest_path_buffer_plan_rmat26(oracle_lib):
+    """ShortestPaths.execute's direct memory at configs[4]'s scale (RMAT-26, n = 2^26).
+    The old plan held 64 x direct(4n) = 17.2 GB per batch (an OutOfMemoryError under the JVM's default
+    direct-memory limit); now one 268 MB row is reused (the batch stays on the device, jg_bfs_keep) and the
+    walk-back's neighbour batches split at computer.gpu.direct-memory / 2.  Replays the batch and one
+    source's walk-back with the default 1 GiB budget: peak direct bytes <= 1 GiB (<= 2 GiB asked), three
+    kept rows bit-exact against the oracle, predecessors against the oracle's CSR."""
+    from janusgraph_amd import _lib
+    from janusgraph_amd.computer import PathDag
+    from test_gpu_configs import host_edges, pick_sources, seed_of
+    o = oracle_lib
+    scale = 26
+    n = 1 << scale
+    budget = 1 << 30  # computer.gpu.direct-memory default
+    s, d = host_edges(o, scale)
+    ptr, adj = o.csr_unordered(n, s, d, both=True)
+    del s, d
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    _ok(L.jg_ctx_create((ctypes.c_int * 1)(0), 1, ctypes.byref(ctx)))
+    g = ctypes.c_void_p()
+    _ok(L.jg_graph_build_rmat(ctx, scale, 16, seed_of(scale), 4, ctypes.byref(g)))  # ADJ_BOTH; vid == index
+    mem = DirectMemory()
+    assert 4 * n <= budget // 2  # GpuGraphComputer's own precondition
+    mem.take(4 * n)  # the reused row
+    mem.take(8 * 64)  # the source batch
+    row = np.empty(n, np.int32)
+    srcs = pick_sources(ptr, 64, scale)
+    dag = PathDag(jni_neighbors(L, g, budget // 2, mem), n)
+    for k, got in enumerate(jni_kept_rows(L, g, srcs, n, -1, row)):
+        if k in (0, 17, 63):
+            np.testing.assert_array_equal(got, o.bfs_csr(n, ptr, adj, int(srcs[k])), err_msg=f"kept row {k}")
+        if k == 0:  # one source's walk-back: every reached vertex of depth 3 a target (hubs included)
+            tmask = np.zeros(n, bool)
+            far = np.flatnonzero(got == 3)
+            tmask[far[:: max(1, len(far) // 3000)]] = True
+            pred, targets, deepest = dag.predecessors(got, tmask)
+            assert deepest == 3 and len(targets) > 1000
+            for v in list(pred)[:500]:
+                nb = adj[ptr[v]:ptr[v + 1]]
+                np.testing.assert_array_equal(np.sort(pred[v]), np.unique(nb[got[nb] == got[v] - 1]))
+    assert mem.peak <= budget <= 2 << 30, f"peak direct memory {mem.peak} bytes"
     _ok(L.jg_graph_destroy(g))
     _ok(L.jg_ctx_destroy(ctx))
