@@ -735,8 +735,11 @@ int jg_tune_set(const char* key, int64_t value) {
         JG_ARG(value >= 1 && value <= 64, "cc_first must be in [1, 64]");
         jg::tune().cc_first = (int)value;
     } else if (k == "msbfs_bu") {
-        JG_ARG(value >= 0 && value <= 2, "msbfs_bu must be 0, 1 or 2");
+        JG_ARG(value >= 0 && value <= 3, "msbfs_bu must be 0, 1, 2 or 3");
         jg::tune().msbfs_bu = (int)value;
+    } else if (k == "msbfs_bu_tasks") {
+        JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_tasks must be in [0, 1000]");
+        jg::tune().msbfs_bu_tasks = (int)value;
     } else if (k == "msbfs_bu_frac") {
         JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_frac must be in [0, 1000]");
         jg::tune().msbfs_bu_frac = (int)value;
@@ -752,6 +755,9 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().msbfs_split = value != 0;
     } else if (k == "sharded_bfs") {
         jg::tune().sharded_bfs = value != 0;
+    } else if (k == "bfs_tail_grid") {
+        JG_ARG(value >= 0 && value <= 65536, "bfs_tail_grid must be in [0, 65536]");
+        jg::tune().bfs_tail_grid = (int)value;
     } else if (k == "bfs_grid") {
         JG_ARG(value >= 64 && value <= 65536, "bfs_grid must be in [64, 65536]");
         jg::tune().bfs_grid = (int)value;
@@ -759,6 +765,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().fuse_finalize = value != 0;
     } else if (k == "relabel_ties") {
         jg::tune().relabel_ties = value != 0;
+    } else if (k == "relabel_dead_last") {
+        jg::tune().relabel_dead_last = value != 0;
     } else if (k == "pr_rank_last") {
         jg::tune().pr_rank_last = value != 0;
     } else if (k == "pr_skip_empty") {

@@ -219,22 +219,32 @@ __global__ void nbr_min_kernel(const int32_t* __restrict__ src, const int32_t* _
 }
 
 // pass 1 of the tie-break sort: key = nbr_min << vbits | v (vertices without neighbours last; nbr_min
-// starts at 0x7F7F7F7F, above any rank)
-__global__ void tie_keys_kernel(const int32_t* __restrict__ nbr_min, int64_t n, int vbits, uint64_t* __restrict__ keys) {
+// starts at 0x7F7F7F7F, above any rank).  `gather_deg` (PageRank's IN plan, tune relabel_dead_last):
+// a vertex without pull neighbours (in-degree 0: all of them tie in degree) is ordered by its out-degree
+// instead, descending: the rarely gathered sources among the in-degree-0 rows (~9% of the vertices,
+// <1% of the gathers) sit together at the front of that class instead of spread over all of it
+__global__ void tie_keys_kernel(const int32_t* __restrict__ nbr_min, int64_t n, int vbits,
+                                const int32_t* __restrict__ gather_deg, int64_t max_gather,
+                                uint64_t* __restrict__ keys) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = nbr_min[v] >= n ? n : nbr_min[v];
+        int64_t t = nbr_min[v] >= n ? n : nbr_min[v];
+        if (t == n && gather_deg) t = max_gather - (gather_deg[v] < max_gather ? gather_deg[v] : max_gather);
         keys[v] = ((uint64_t)t << vbits) | (uint64_t)v;
     }
 }
 
-// pass 2: key = (maxdeg - deg(v)) << 32 | position in pass 1 (stable: ties keep the pass-1 order)
+// pass 2: key = (maxdeg - deg(v)) << 33 | dead << 32 | position in pass 1 (stable: ties keep the pass-1
+// order).  dead (PageRank's IN plan, tune relabel_dead_last): v has no out-edge, so no row ever gathers
+// its contribution; such rows go last in their degree class, and the gathered vector's lines hold live
+// contributions only (RMAT: 20% of the in-degree > 0 rows)
 __global__ void tie_deg_keys_kernel(const uint64_t* __restrict__ keys1, int64_t n, uint64_t vmask,
                                     const int32_t* __restrict__ indeg, const int32_t* __restrict__ outdeg, int mode,
-                                    int64_t maxdeg, uint64_t* __restrict__ keys2) {
+                                    int64_t maxdeg, bool dead_last, uint64_t* __restrict__ keys2) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t v = (int64_t)(keys1[i] & vmask);
         const int64_t d = mode == 0 ? indeg[v] : mode == 1 ? (int64_t)indeg[v] + outdeg[v] : outdeg[v];
-        keys2[i] = ((uint64_t)(maxdeg - d) << 32) | (uint64_t)i;
+        const uint64_t dead = dead_last && outdeg[v] == 0 ? 1ull : 0ull;
+        keys2[i] = ((uint64_t)(maxdeg - d) << 33) | (dead << 32) | (uint64_t)i;
     }
 }
 
@@ -1207,13 +1217,15 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                                       rank1.get(), nbr_min.get());
                 JG_LAUNCH_CHECK();
                 DevBuf<uint64_t> k1(n), k2(n);
-                tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, k1.get());
+                const bool dead_last = mode == 0 && tune().relabel_dead_last;  // PageRank's gathered vector
+                tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, dead_last ? dout : nullptr,
+                                                               std::min<int64_t>((int64_t)hc[3], n), k1.get());
                 JG_LAUNCH_CHECK();
                 prim::radix_sort(k1.get(), nullptr, n, vbits + bits_for((uint64_t)n), s);
                 tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, din, dout, mode, maxdeg,
-                                                                   k2.get());
+                                                                   dead_last, k2.get());
                 JG_LAUNCH_CHECK();
-                prim::radix_sort(k2.get(), nullptr, n, 32 + bits_for((uint64_t)maxdeg), s);
+                prim::radix_sort(k2.get(), nullptr, n, 33 + bits_for((uint64_t)maxdeg), s);
                 tie_final_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), k2.get(), n, vmask, rkeys.get());
                 JG_LAUNCH_CHECK();
             }

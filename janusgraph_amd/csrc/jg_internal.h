@@ -241,6 +241,8 @@ struct Shard {
     DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
+    int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
+    int bfs_hist_n = 0;
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
@@ -552,6 +554,8 @@ struct Tune {
                                       // measured: 5% slower than the fused launch at RMAT-24 and 26)
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
+    int relabel_dead_last = 1;        // build time, IN plan: rows without out-edges last in their degree class,
+                                      // in-degree-0 rows by out-degree (the gathered vector's lines hold live values)
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
                                       // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)
     int dobfs_alpha = 30;             // the same for single-source traversals (tools/bfs_sweep.py, RMAT-20:
@@ -568,11 +572,14 @@ struct Tune {
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
                                       //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
-    int msbfs_bu = 0;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
-                                      //         (0 never, 1 every pull level, 2 when the frontier holds >= msbfs_bu_frac;
+    int msbfs_bu = 3;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
+                                      //         (0 never, 1 every pull level, 2 when the frontier holds >= msbfs_bu_frac,
+                                      //         3 sparse levels: fewer than msbfs_bu_tasks permille of the tasks live;
                                       //         measured 2-4x slower than the merge-engine pull: RMAT-26 81.0 / 21.7 ms,
                                       //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
     int msbfs_bu_frac = 100;          //         permille of the rows
+    int msbfs_bu_tasks = 20;          //         msbfs_bu 3: permille of the merge tasks below which a pull level
+                                      //         (after the first) runs bottom-up
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int cc_uf_sharded = 1;            //         sharded (halo plans): local union-find, tree labels over the halo,
                                       //         multi-root sharded BFS for the superstep count (0: propagation)
@@ -593,6 +600,8 @@ struct Tune {
     int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
     int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
+    int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
+                                      //         (0: every launch at the full grid)
     int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
     int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power
                                       // steps only (their rank and contribution are constant after that)

@@ -599,10 +599,11 @@ __global__ void msbfs_widen_kernel(const uint8_t* __restrict__ d8, int64_t n, in
 // Levels recorded as new-bit words ([levels][rows]) into int32 depth planes (plane s, row r = the level
 // whose word holds bit s; pairs no recorded level holds keep what the planes had: a later level's
 // depth, or -1)
-__global__ void msbfs_levels_to_planes_kernel(const unsigned long long* __restrict__ nwl, int levels, int64_t rows,
-                                              int nsrc, int32_t* __restrict__ depth) {
+__global__ void msbfs_levels_to_planes_kernel(const unsigned long long* __restrict__ nwl, int levels, unsigned word_levels,
+                                              int64_t rows, int nsrc, int32_t* __restrict__ depth) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
         for (int L = 0; L < levels; ++L) {
+            if (!((word_levels >> L) & 1u)) continue;  // a top-down level: its (row, word) records instead
             unsigned long long w = nwl[(int64_t)L * rows + r];
             while (w) {
                 const int s = __ffsll(w) - 1;
@@ -624,7 +625,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
                                   unsigned long long* __restrict__ visited, unsigned long long* __restrict__ nw0,
-                                  int64_t rows, VecPos pos) {
+                                  int64_t rows, VecPos pos, int32_t* __restrict__ rec_rows,
+                                  unsigned long long* __restrict__ rec_words) {
     // sequential over the (<= 64) sources: several sources may share a vertex
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     for (int s = 0; s < nsrc; ++s) {
@@ -632,7 +634,42 @@ __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsr
         if (l < 0) continue;
         F[pos(l)] |= 1ull << s;
         visited[l] |= 1ull << s;
-        nw0[l] |= 1ull << s;  // level 0's new-bit word
+        if (nw0) nw0[l] |= 1ull << s;  // level 0's new-bit word
+    }
+    if (rec_rows)  // level 0 as (row, word) records: a shared source row records the same full word twice
+        for (int s = 0; s < nsrc; ++s) {
+            const int64_t l = local_src[s];
+            rec_rows[s] = (int32_t)l;
+            rec_words[s] = l < 0 ? 0ull : F[pos(l)];
+        }
+}
+
+// A top-down level's depths as (row, new-bit word) records: the rows that gained a bit are exactly the
+// next frontier's queue (msbfs_td_apply_kernel queues a touched row iff its new word is nonzero), so the
+// level needs no [rows]-long word array cleared before it
+__global__ void msbfs_td_record_kernel(const int32_t* __restrict__ queue, int64_t n, const unsigned long long* __restrict__ F,
+                                       VecPos pos, int32_t* __restrict__ rec_rows,
+                                       unsigned long long* __restrict__ rec_words) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = queue[i];
+        rec_rows[i] = r;
+        rec_words[i] = F[pos(r)];
+    }
+}
+
+// depth planes from (row, word) records of one level (rows < 0: none)
+__global__ void msbfs_records_to_planes_kernel(const int32_t* __restrict__ rec_rows,
+                                               const unsigned long long* __restrict__ rec_words, int64_t n, int level,
+                                               int64_t rows, int nsrc, int32_t* __restrict__ depth) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = rec_rows[i];
+        if (r < 0) continue;
+        unsigned long long w = rec_words[i];
+        while (w) {
+            const int s = __ffsll(w) - 1;
+            if (s < nsrc) depth[(int64_t)s * rows + r] = level;
+            w &= w - 1;
+        }
     }
 }
 
@@ -1325,6 +1362,14 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     // / 4096 / 8192 / 16384 / 65536): small levels pay less per block, big ones need the parallelism
     const int64_t sq = 1ll << ((bits_for((uint64_t)std::max<int64_t>(rows - 1, 1)) + 1) / 2);
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sq * tune().bfs_grid_mult / 4, 64), tune().bfs_grid);
+    // Launches past the deepest of this shard's last few traversals are almost always no-ops that only
+    // read the device state and exit (RMAT-20: 3-4 of the first batch's 10, ~4.2 us each at the full
+    // grid): they go out with a small grid (bfs_tail_grid workgroups; a level that does have work there
+    // still runs, grid-stride, just slower).  Single-source traversals only (the CC start is not history).
+    int predicted = 0;
+    if (!roots && tune().bfs_tail_grid > 0 && sh.bfs_hist_n >= 2)
+        for (int k = 0; k < std::min(sh.bfs_hist_n, 4); ++k) predicted = std::max(predicted, sh.bfs_hist[k]);
+    const unsigned tail_grid = (unsigned)std::min<int64_t>(std::max(tune().bfs_tail_grid, 1), grid);
     BfsState hs{};
     int level = 0;
     // Levels are enqueued in batches, the host reading the device state once per batch: first
@@ -1349,12 +1394,13 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             a.bm_out = sh.bfs_bm[p ^ 1].get();
             a.split = a.owner && (split_mode == 1 || (split_mode == 2 && level < 16 && ((split_levels >> level) & 1)));
             if (prof_enabled(ctx)) prof_record_start(ctx, sh);
-            if (tune().bfs_wave_stage) bfs_level_kernel<true><<<grid, kBlock, 0, s>>>(a);
-            else bfs_level_kernel<false><<<grid, kBlock, 0, s>>>(a);
+            const unsigned lg = predicted > 0 && level >= predicted ? tail_grid : grid;
+            if (tune().bfs_wave_stage) bfs_level_kernel<true><<<lg, kBlock, 0, s>>>(a);
+            else bfs_level_kernel<false><<<lg, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             if (a.split) {
-                if (tune().bfs_wave_stage) bfs_td_claim_kernel<true><<<grid, kBlock, 0, s>>>(a);
-                else bfs_td_claim_kernel<false><<<grid, kBlock, 0, s>>>(a);
+                if (tune().bfs_wave_stage) bfs_td_claim_kernel<true><<<lg, kBlock, 0, s>>>(a);
+                else bfs_td_claim_kernel<false><<<lg, kBlock, 0, s>>>(a);
                 JG_LAUNCH_CHECK();
             }
             if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
@@ -1371,6 +1417,11 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         if (hs.done) break;
     }
     if (edges_out) *edges_out = (double)hs.edges;
+    if (!roots) {  // the history of level counts (bfs_tail_grid)
+        for (int k = 3; k > 0; --k) sh.bfs_hist[k] = sh.bfs_hist[k - 1];
+        sh.bfs_hist[0] = hs.levels;
+        sh.bfs_hist_n = std::min(sh.bfs_hist_n + 1, 4);
+    }
     return hs.levels;
 }
 
@@ -2013,6 +2064,15 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
                 DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
+                // levels recorded as (row, new word) records instead of nwl words (level 0 from the sources and
+                // every top-down level below kMsLevelWords): {level, count, rows, words}
+                struct Rec {
+                    int level = 0;
+                    int64_t n = 0;
+                    DevBuf<int32_t> rows;
+                    DevBuf<unsigned long long> words;
+                };
+                std::vector<Rec> recs;
                 DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs,
                                                   // [2] entries the early-exit bottom-up levels scanned
                 int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
@@ -2188,8 +2248,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             prof_discard_exchanges(g);  // exchange pairs never straddle t0
             JG_HIP(hipEventRecord(t0, sh0.stream));
-            // the call's state, inside the timed region: frontiers, visited bits, level 0's new-bit words (the
-            // other levels' words are zeroed as their level starts), the halo staging, the sources
+            // the call's state, inside the timed region: frontiers, visited bits, the halo staging, the
+            // sources (and level 0's depth record)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
@@ -2198,10 +2258,21 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.nwl.get(), 0, (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
                 if (tds[i].hs.size()) JG_HIP(hipMemsetAsync(tds[i].hs.get(), 0, tds[i].hs.bytes(), sh.stream));
-                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(t.dloc.get(), ns, t.F[0].get(), t.vis.get(), t.nwl.get(),
-                                                          sh.rows, g.vec_pos(sh, adj_of(sh, c)));
+                St::Rec* r0 = nullptr;
+                if (td_ok && tune().msbfs_diag != 1) {  // level 0 as records of the source rows
+                    t.recs.emplace_back();
+                    r0 = &t.recs.back();
+                    r0->level = 0;
+                    r0->n = ns;
+                    r0->rows.alloc(ns);
+                    r0->words.alloc(ns);
+                } else {  // level 0's words
+                    JG_HIP(hipMemsetAsync(t.nwl.get(), 0, (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
+                }
+                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(t.dloc.get(), ns, t.F[0].get(), t.vis.get(),
+                                                          r0 ? nullptr : t.nwl.get(), sh.rows, g.vec_pos(sh, adj_of(sh, c)),
+                                                          r0 ? r0->rows.get() : nullptr, r0 ? r0->words.get() : nullptr);
                 JG_LAUNCH_CHECK();
             }
             if (!td_ok) {
@@ -2256,6 +2327,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.depth8.reset();
                 }
             };
+            // levels whose depths are nwl words (bit L): a pull level finalises every own row (its word is
+            // written, zero or not); a top-down level records (row, word) pairs of the rows it reached
+            unsigned word_levels = (td_ok && tune().msbfs_diag != 1) ? 0u : 1u;
             // the caller's int32 planes: the widened byte / int32 planes, then the word-recorded levels
             auto materialize = [&](int levels_run) {
                 widen();
@@ -2265,16 +2339,24 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     DeviceGuard dg(sh.device);
                     const int lw = std::min(levels_run + 1, kMsLevelWords);
                     if (sh.rows > 0) {
-                        msbfs_levels_to_planes_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.nwl.get(), lw, sh.rows,
-                                                                                                   ns, t.depth.get());
+                        msbfs_levels_to_planes_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                            t.nwl.get(), lw, word_levels, sh.rows, ns, t.depth.get());
                         JG_LAUNCH_CHECK();
                     }
+                    for (const auto& r : t.recs)
+                        if (r.n > 0 && r.level < lw) {
+                            msbfs_records_to_planes_kernel<<<grid_for(r.n), kBlock, 0, sh.stream>>>(
+                                r.rows.get(), r.words.get(), r.n, r.level, sh.rows, ns, t.depth.get());
+                            JG_LAUNCH_CHECK();
+                        }
                     JG_HIP(hipStreamSynchronize(sh.stream));
                 }
             };
             // one shard: pull levels whose frontier holds at least msbfs_bu_frac / 1000 of the rows run
             // bottom-up with early exit (msbfs_bu_kernel) instead of through the merge engine
             MsBu bu{};
+            // msbfs_bu: 1 every pull level, 2 levels whose frontier holds >= msbfs_bu_frac permille of the rows,
+            // 3 (default) levels where fewer than msbfs_bu_tasks permille of the merge tasks can gain a bit
             const bool bu_ok = td_one && c0.pull == c0.push && tune().msbfs_bu > 0;
             if (bu_ok) {
                 DevBuf<int64_t> bnd(2);
@@ -2295,6 +2377,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             const int64_t bu_rows = bu_ok ? sh0.rows * (int64_t)tune().msbfs_bu_frac / 1000 : 0;
             int bu_levels = 0;
+            unsigned long long bu_task_credit = 0;  // live tasks counted by levels that then ran bottom-up
             bool queued = td_ok, live_ready = false;
             bool prev_td = false;  // the previous level ran top-down: F[cur ^ 1]'s nonzero own words are
                                    // exactly its input queue (tds[i].queue[qc ^ 1][0, nq_in))
@@ -2304,16 +2387,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int unskipped_levels = 0;  // pull levels that ran every merge task (msbfs_skip_first)
             double td_entries = 0, td_touched = 0, td_queued = 0;
             while (max_depth < 0 || level < max_depth) {
-                if (level + 1 < kMsLevelWords)  // the new-bit words this level records (rows it skips read 0)
-                    for (size_t i = 0; i < g.shards.size(); ++i) {
-                        Shard& sh = *g.shards[i];
-                        DeviceGuard dg(sh.device);
-                        JG_HIP(hipMemsetAsync(st[i].nwl.get() + (int64_t)(level + 1) * sh.rows, 0,
-                                              (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
-                    }
                 if (level + 1 >= kMsLevelWords) ensure_depth8();
                 if (level + 1 >= 255) widen();
                 const bool td_level = td_ok && (double)g_mf < (double)push_nnz / (double)tune().bfs_alpha;
+                // a pull level (merge engine or msbfs_bu_kernel) finalises every own row: its words need no clearing
+                if (!td_level && level + 1 < kMsLevelWords) word_levels |= 1u << (level + 1);
                 if (td_level && !queued) {
                     build_frontier(qc ^ 1);
                     qc ^= 1;
@@ -2483,7 +2561,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             op.visited = t.vis.get();
                             op.depth = t.depth.get();
                             op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
-                            op.nwl = level + 1 < kMsLevelWords && tune().msbfs_diag != 1 ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
+                            op.nwl = nullptr;  // recorded from the next queue below (msbfs_td_record_kernel)
                             op.changed = t.changed.get();
                             op.rows = sh.rows;
                             op.pos = g.vec_pos(sh, adj_of(sh, c));
@@ -2496,6 +2574,25 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         }
                     }
                     read_frontier(&td_touched);
+                    if (level + 1 < kMsLevelWords && tune().msbfs_diag != 1)
+                        for (size_t i = 0; i < g.shards.size(); ++i) {  // the level's depths: its new queue
+                            Shard& sh = *g.shards[i];
+                            DeviceGuard dg(sh.device);
+                            St& t = st[i];
+                            const int64_t nq = tds[i].nq;
+                            t.recs.emplace_back();
+                            St::Rec& r = t.recs.back();
+                            r.level = level + 1;
+                            r.n = nq;
+                            r.rows.alloc(std::max<int64_t>(nq, 1));
+                            r.words.alloc(std::max<int64_t>(nq, 1));
+                            if (nq > 0) {
+                                msbfs_td_record_kernel<<<grid_for(nq), kBlock, 0, sh.stream>>>(
+                                    tds[i].queue[qc ^ 1].get(), nq, t.F[cur ^ 1].get(),
+                                    g.vec_pos(sh, adj_of(sh, pick_csrs(sh, direction))), r.rows.get(), r.words.get());
+                                JG_LAUNCH_CHECK();
+                            }
+                        }
                     combine_live();
                     qc ^= 1;
                     queued = live_ready = true;
@@ -2540,7 +2637,43 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                         }
                         op.live = lw;
-                        if (bu_ok && (tune().msbfs_bu == 1 || g_nq >= bu_rows)) {
+                        // sparse levels (msbfs_bu 3): the task bitmaps first; when few tasks hold a row that can
+                        // still gain a bit (RMAT-26's last pull level: ~0.2% of the entries), the early-exit
+                        // bottom-up kernel visits those rows' entries only, instead of the merge engine's
+                        // per-round LDS images over every sub-slice
+                        const bool no_bitmaps = tune().msbfs_skip_first && pull_levels == 0;
+                        std::vector<const uint32_t*> tl;
+                        bool sparse = false;
+                        if (!(bu_ok && (tune().msbfs_bu == 1 || (tune().msbfs_bu == 2 && g_nq >= bu_rows)))) {
+                            unsigned long long before = 0, after = 0;
+                            if (bu_ok && tune().msbfs_bu == 3 && !no_bitmaps && !t.todo.empty())
+                                copy_d2h(&before, t.work.get(), sizeof before, sh.stream);
+                            for (size_t b = 0; b < t.todo.size() && !no_bitmaps; ++b) {
+                                const SliceBand& bd = *plan.bands[b];
+                                if (bd.tasks == 0 || bd.rows() == 0) {
+                                    tl.push_back(nullptr);
+                                    continue;
+                                }
+                                msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
+                                    t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
+                                JG_LAUNCH_CHECK();
+                                msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
+                                    bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
+                                JG_LAUNCH_CHECK();
+                                tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                            }
+                            if (bu_ok && tune().msbfs_bu == 3 && !no_bitmaps && !t.todo.empty()) {
+                                copy_d2h(&after, t.work.get(), sizeof after, sh.stream);
+                                sparse = (double)(after - before) * 1000.0 <
+                                         (double)t.all_tasks * (double)tune().msbfs_bu_tasks;
+                                if (debug_bfs())
+                                    std::fprintf(stderr, "[jg msbfs] level %d pull: %llu of %lld merge tasks live -> %s\n",
+                                                 level, after - before, (long long)t.all_tasks,
+                                                 sparse ? "bottom-up" : "merge");
+                                if (sparse) bu_task_credit += after - before;  // no merge task ran
+                            }
+                        }
+                        if (bu_ok && (tune().msbfs_bu == 1 || (tune().msbfs_bu == 2 && g_nq >= bu_rows) || sparse)) {
                             const int64_t light = sh.rows - bu.wave;
                             const unsigned grid = (unsigned)(bu.blocks_wave +
                                                              std::max<int64_t>(std::min<int64_t>((light + kMergeThreads - 1) / kMergeThreads, 4096), 1));
@@ -2548,25 +2681,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                             level_bu = true;
                         } else {
-                        std::vector<const uint32_t*> tl;
                         // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows
                         // can be done there; every task runs, the finalize's live mask keeps it exact)
-                        const bool no_bitmaps = tune().msbfs_skip_first && pull_levels == 0;
                         if (no_bitmaps && i == 0) ++unskipped_levels;
-                        for (size_t b = 0; b < t.todo.size() && !no_bitmaps; ++b) {
-                            const SliceBand& bd = *plan.bands[b];
-                            if (bd.tasks == 0 || bd.rows() == 0) {
-                                tl.push_back(nullptr);
-                                continue;
-                            }
-                            msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
-                                t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
-                            JG_LAUNCH_CHECK();
-                            msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
-                                bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
-                            JG_LAUNCH_CHECK();
-                            tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
-                        }
                         launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                     t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
                                     tl.empty() ? nullptr : tl.data());
@@ -2627,7 +2744,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels
-                                                          : (double)w[0] + (double)t.all_tasks * unskipped_levels;
+                                                          : (double)(w[0] - (i == 0 ? bu_task_credit : 0ull)) +
+                                                                (double)t.all_tasks * unskipped_levels;
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
                 work_entries += entries;
                 work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +

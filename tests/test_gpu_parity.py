@@ -223,7 +223,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
 @pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
                                          ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
                                          ("skip_dense_reverse", 3), ("skip_dense", 2), ("skip_every_level", 1),
-                                         ("skip_every_level", 3)])
+                                         ("skip_every_level", 3), ("merge_sparse_levels", 1), ("bu_sparse_always", 1),
+                                         ("bu_every_level", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -233,7 +234,8 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     halo exchange, sparse (offset, word) pairs when few staging slots are set, the whole segments with
     skip_dense_reverse); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2).
     The first pull level runs every task by default (msbfs_skip_first); skip_every_level builds the
-    task bitmaps on that level too."""
+    task bitmaps on that level too.  One shard: a later pull level with fewer than msbfs_bu_tasks permille
+    of live tasks runs msbfs_bu_kernel (bottom-up, early exit) instead of the merge engine."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
@@ -241,7 +243,11 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
                              ("band2_deg", 4), ("band2_bit", 3)],
              "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
              "skip_dense": [("halo", 0)], "skip_sharded_pull_only": [("msbfs_td", 2)],
-             "skip_dense_reverse": [("msbfs_sparse", 0)], "skip_every_level": [("msbfs_skip_first", 0)]}[mode]
+             "skip_dense_reverse": [("msbfs_sparse", 0)], "skip_every_level": [("msbfs_skip_first", 0)],
+             # sparse pull levels (msbfs_bu 3, the default): through the merge engine instead, every bitmapped
+             # level bottom-up, every pull level bottom-up
+             "merge_sparse_levels": [("msbfs_bu", 0)], "bu_sparse_always": [("msbfs_bu_tasks", 1000)],
+             "bu_every_level": [("msbfs_bu", 1)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
     vid = np.concatenate([vid0, (np.arange(3, dtype=np.int64) + n0 + 1) << 8 | 7])
@@ -267,6 +273,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_skip", 1)
         _lib.tune_set("msbfs_td", 1)
         _lib.tune_set("msbfs_sparse", 1)
+        _lib.tune_set("msbfs_bu", 3)
+        _lib.tune_set("msbfs_bu_tasks", 20)
+        _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
         for k, v in (("band0_deg", 128), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
                      ("band2_bit", 3)):  # the defaults (Tune::band_deg / band_bits)
@@ -547,3 +556,36 @@ def test_decode_edges_edge_cases(ctx):
     assert list(d) == [0, -1] and o[0] == 1 << 40 and r[0] == 17 and o[1] == -1
     with pytest.raises(jg.JanusGpuError):
         ctx.decode_edges(data, [0, len(data) + 5], [1])
+
+
+@pytest.mark.parametrize("tail", [64, 1, 0])
+def test_bfs_tail_grid_deeper_than_history(oracle_lib, tail):
+    """bfs_tail_grid: launches past the deepest of the last traversals run with a small grid.  Shallow
+    traversals first (history of 2-3 levels), then ones that go 40 levels down a path hanging off the
+    graph: the levels past the prediction do real work on the small grid (one workgroup with tail 1,
+    both directions grid-stride), and every depth still equals the oracle's."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 12)
+    plen = 40
+    n = n0 + plen
+    vid = np.concatenate([vid0, (np.arange(plen, dtype=np.int64) + n0 + 1) << 8 | 3])
+    hub = int(np.bincount(ds0, minlength=n0).argmax())
+    ps = np.concatenate([[hub], np.arange(n0, n - 1)]).astype(ds0.dtype)
+    pd = np.arange(n0, n).astype(ds0.dtype)
+    ds, dd = np.concatenate([ds0, ps]), np.concatenate([dd0, pd])
+    try:
+        _lib.tune_set("bfs_tail_grid", tail)
+        c = jg.Context((0,))
+        g = c.build(vid, vid[ds], vid[dd], flags=4)
+        for sv in (hub, hub, int(ds0[1])):  # shallow: the history
+            np.testing.assert_array_equal(g.bfs([vid[sv]], 3)[0], oracle_lib.bfs(n, ds, dd, sv, 3))
+        for sv in (n - 1, n0 + 5, n - 1):  # the path's far end: ~45 levels
+            np.testing.assert_array_equal(g.bfs([vid[sv]], 3)[0], oracle_lib.bfs(n, ds, dd, sv, 3),
+                                          err_msg=f"tail grid {tail}, source {sv}")
+            assert c.stats()["levels"] > 30
+        np.testing.assert_array_equal(g.bfs([vid[hub]], 3, 2)[0], oracle_lib.bfs(n, ds, dd, hub, 3, 2))
+        g.close()
+        c.close()
+    finally:
+        _lib.tune_set("bfs_tail_grid", 64)
