@@ -484,6 +484,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
              bool keep = false);
 void bfs_kept_row(Graph& g, int s, int32_t* depth_out);  // row s in caller order
 void bfs_kept_release(Graph& g);
+// Zeroes the occupied positions of a shard's gathered vector of adjacency `adj` (own rows + peer runs).
+void zero_gathered(const Graph& g, const Shard& sh, uint32_t adj, void* v, size_t eb);
 // jg_graph_neighbors: the adjacency `direction` of caller vertices rows[0, nrows) in caller order
 void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t nrows, int64_t* off_out,
                      int64_t* nbr_out);

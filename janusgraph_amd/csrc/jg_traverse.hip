@@ -492,32 +492,52 @@ struct MsBfsOp {
     }
 };
 
+// Counters reduced by many workgroups (the live bits, frontier counters, live-task and pair counts):
+// one device atomic per 1024-thread workgroup on a grid of at most kRedBlocks (the CUs).  A device-
+// scope atomic on one word executes at the memory side, ~88 per us (MI355X_MICROARCH.md, dequeue row);
+// one per wave on a 4096-block grid queued 16 K of them, ~0.2 ms, behind kernels of ~20-60 us of work
+// (msbfs_task_live_kernel, msbfs_pairs_kernel in the round-3 8-shard trace).
+constexpr int kRedThreads = 1024, kRedWaves = kRedThreads / kWave;
+constexpr int64_t kRedBlocks = 256;
+inline unsigned red_grid(int64_t work) { return grid_for(work, kRedThreads, kRedBlocks); }
+
+template <class T, class F>
+__device__ __forceinline__ T block_reduce(T v, F op, T* red) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, kWave));
+    if (lane_id() == 0) red[wave_id()] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) v = op(v, red[w]);
+    return v;  // valid in thread 0
+}
+struct OrU64 {
+    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a | b; }
+};
+struct AddU64 {
+    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a + b; }
+};
+
 // *live |= the OR of every word of F (one atomic per block)
-__global__ __launch_bounds__(kBlock) void msbfs_live_kernel(const unsigned long long* __restrict__ F, int64_t len,
-                                                            unsigned long long* __restrict__ live) {
-    __shared__ unsigned long long red[kBlock / kWave];
+__global__ __launch_bounds__(kRedThreads) void msbfs_live_kernel(const unsigned long long* __restrict__ F, int64_t len,
+                                                                 unsigned long long* __restrict__ live) {
+    __shared__ unsigned long long red[kRedWaves];
     unsigned long long m = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x)
         m |= F[i];
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) m |= __shfl_xor(m, o, kWave);
-    if (lane_id() == 0) red[wave_id()] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) m |= red[w];
-        if (m) atomicOr(live, m);
-    }
+    m = block_reduce(m, OrU64{}, red);
+    if (threadIdx.x == 0 && m) atomicOr(live, m);
 }
 
 // After a pull level (one shard): the next level's live bits and its packed frontier counter
 // ((vertices << kPackShift) | push-edge sum: the direction rule's input) in one read of F, without the
 // top-down queue, which msbfs_frontier_kernel builds only if the next level runs top-down
 // (the queue build cost 750 us at RMAT-26's first two pull levels, whose successors pull).
-__global__ __launch_bounds__(kBlock) void msbfs_scan_kernel(const unsigned long long* __restrict__ F, int64_t rows,
-                                                            const int64_t* __restrict__ push_rp,
-                                                            unsigned long long* __restrict__ live,
-                                                            unsigned long long* __restrict__ packed) {
-    __shared__ unsigned long long red_or[kBlock / kWave], red_n[kBlock / kWave];
+__global__ __launch_bounds__(kRedThreads) void msbfs_scan_kernel(const unsigned long long* __restrict__ F, int64_t rows,
+                                                                 const int64_t* __restrict__ push_rp,
+                                                                 unsigned long long* __restrict__ live,
+                                                                 unsigned long long* __restrict__ packed) {
+    __shared__ unsigned long long red_or[kRedWaves], red_n[kRedWaves];
     unsigned long long m = 0, cnt = 0;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         const unsigned long long w = F[v];
@@ -526,21 +546,9 @@ __global__ __launch_bounds__(kBlock) void msbfs_scan_kernel(const unsigned long 
             cnt += (1ull << kPackShift) + (unsigned long long)(push_rp[v + 1] - push_rp[v]);
         }
     }
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-        m |= __shfl_xor(m, o, kWave);
-        cnt += __shfl_xor(cnt, o, kWave);
-    }
-    if (lane_id() == 0) {
-        red_or[wave_id()] = m;
-        red_n[wave_id()] = cnt;
-    }
-    __syncthreads();
+    m = block_reduce(m, OrU64{}, red_or);
+    cnt = block_reduce(cnt, AddU64{}, red_n);
     if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) {
-            m |= red_or[w];
-            cnt += red_n[w];
-        }
         if (m) atomicOr(live, m);
         if (cnt) atomicAdd(packed, cnt);
     }
@@ -562,11 +570,12 @@ __global__ __launch_bounds__(kBlock) void msbfs_todo_kernel(const unsigned long 
 }
 
 // bit t of tlive (MergeArgs::live): merge task t touches a band row that can still gain a bit;
-// *nlive += the live tasks (one atomic per wave; the work counter of jg_stats.algorithmic_bytes)
-__global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* __restrict__ task_rows, int64_t tasks,
-                                                                 const unsigned long long* __restrict__ todo,
-                                                                 unsigned long long* __restrict__ tlive,
-                                                                 unsigned long long* __restrict__ nlive) {
+// *nlive += the live tasks (one atomic per block; the work counter of jg_stats.algorithmic_bytes)
+__global__ __launch_bounds__(kRedThreads) void msbfs_task_live_kernel(const int32_t* __restrict__ task_rows, int64_t tasks,
+                                                                      const unsigned long long* __restrict__ todo,
+                                                                      unsigned long long* __restrict__ tlive,
+                                                                      unsigned long long* __restrict__ nlive) {
+    __shared__ unsigned long long red[kRedWaves];
     unsigned long long count = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tasks; x0 += stride) {  // block-uniform trips
@@ -582,10 +591,13 @@ __global__ __launch_bounds__(kBlock) void msbfs_task_live_kernel(const int32_t* 
             }
         }
         const unsigned long long word = __ballot(b);
-        if (lane_id() == 0 && t < tasks) tlive[t >> 6] = word;
-        count += (unsigned long long)__popcll(word);
+        if (lane_id() == 0 && t < tasks) {
+            tlive[t >> 6] = word;
+            count += (unsigned long long)__popcll(word);
+        }
     }
-    if (lane_id() == 0 && count) atomicAdd(nlive, count);
+    count = block_reduce(count, AddU64{}, red);
+    if (threadIdx.x == 0 && count) atomicAdd(nlive, count);
 }
 
 // int32 planes from byte planes (255 = unreached -> -1)
@@ -614,13 +626,14 @@ __global__ void msbfs_levels_to_planes_kernel(const unsigned long long* __restri
 }
 
 // pairs += the set bits of visited[0, rows) (sources x reached rows: the depth entries written)
-__global__ __launch_bounds__(kBlock) void msbfs_pairs_kernel(const unsigned long long* __restrict__ visited, int64_t rows,
-                                                             unsigned long long* __restrict__ pairs) {
+__global__ __launch_bounds__(kRedThreads) void msbfs_pairs_kernel(const unsigned long long* __restrict__ visited, int64_t rows,
+                                                                  unsigned long long* __restrict__ pairs) {
+    __shared__ unsigned long long red[kRedWaves];
     unsigned long long c = 0;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x)
         c += (unsigned long long)__popcll(visited[v]);
-    c = wave_reduce_add(c);
-    if (lane_id() == 0 && c) atomicAdd(pairs, c);
+    c = block_reduce(c, AddU64{}, red);
+    if (threadIdx.x == 0 && c) atomicAdd(pairs, c);
 }
 
 __global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
@@ -1746,7 +1759,6 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         copy_h2d(t.rlen.get(), rlen.data(), g.P * sizeof(int64_t), sh.stream);
         t.dvec.alloc(std::max<int64_t>(sh.rows, 1));
         t.stamp.alloc(std::max<int64_t>(h.C, 1));
-        JG_HIP(hipMemsetAsync(t.stamp.get(), 0, (size_t)h.C * sizeof(int32_t), sh.stream));  // no level stamps 0
         t.hb.alloc(std::max<int64_t>(t.hb_words, 1));
         t.sw.alloc(std::max<int64_t>(t.sw_words, 1));
         t.send_off.alloc(g.P + 1);
@@ -1758,6 +1770,26 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.ctr.alloc(1);
+    }
+    // the traversal's state, inside its timed region: level stamps (0 = none; the occupied slots of the
+    // compact vector), depths, the level-0 queue
+    Shard& sh0 = *g.shards[0];
+    hipEvent_t t0, t1;
+    {
+        DeviceGuard dg(sh0.device);
+        JG_HIP(hipEventCreate(&t0));
+        JG_HIP(hipEventCreate(&t1));
+        for (auto& sp : g.shards) {
+            DeviceGuard dgs(sp->device);
+            JG_HIP(hipStreamSynchronize(sp->stream));  // the plan copies above; t0 marks the traversal's start
+        }
+        JG_HIP(hipEventRecord(t0, sh0.stream));
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh.device);
+        St& t = st[i];
+        zero_gathered(g, sh, JG_ADJ_BOTH, t.stamp.get(), sizeof(int32_t));
         if (roots) {
             JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
             if (sh.rows) {
@@ -1798,14 +1830,6 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     const double alpha = (double)tune().bfs_alpha, beta = (double)tune().bfs_beta;
     bool bu = false;
     int level = 0, cur = 0;
-    Shard& sh0 = *g.shards[0];
-    hipEvent_t t0, t1;
-    {
-        DeviceGuard dg(sh0.device);
-        JG_HIP(hipEventCreate(&t0));
-        JG_HIP(hipEventCreate(&t1));
-        JG_HIP(hipEventRecord(t0, sh0.stream));
-    }
     std::vector<uint64_t*> swv, hbv;
     for (auto& t : st) {
         swv.push_back(reinterpret_cast<uint64_t*>(t.sw.get()));
@@ -1953,6 +1977,26 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
     return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r) - 1;
 }
 
+
+// Clears the positions of a shard's gathered vector that hold values: its own rows and, on a segmented
+// compact vector (halo plan), each peer's run at the start of its segment.  Nothing reads the rest of a
+// segment (columns and exchanges address the runs only), which at RMAT-26, P = 8 is 83% of the vector's
+// 134 M positions; a dense (allgather) vector is cleared whole.
+void zero_gathered(const Graph& g, const Shard& sh, uint32_t adj, void* v, size_t eb) {
+    const Halo& h = g.halo(sh, adj);
+    char* p = static_cast<char*>(v);
+    if (!h.on) {
+        JG_HIP(hipMemsetAsync(p, 0, (size_t)g.vec_len(sh, adj) * eb, sh.stream));
+        return;
+    }
+    if (sh.rows) JG_HIP(hipMemsetAsync(p, 0, (size_t)sh.rows * eb, sh.stream));
+    for (int q = 0; q < g.P; ++q) {
+        if (q == sh.index) continue;
+        const int64_t nr = h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q];
+        if (nr > 0)
+            JG_HIP(hipMemsetAsync(p + ((size_t)h.seg_of(q, sh.index) << h.tbits) * eb, 0, (size_t)nr * eb, sh.stream));
+    }
+}
 
 void bfs_kept_release(Graph& g) {
     for (auto& sp : g.shards) {
@@ -2255,10 +2299,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DeviceGuard dg(sh.device);
                 St& t = st[i];
                 const BfsCsrs c = pick_csrs(sh, direction);
-                JG_HIP(hipMemsetAsync(t.F[0].get(), 0, t.F[0].bytes(), sh.stream));
-                JG_HIP(hipMemsetAsync(t.F[1].get(), 0, t.F[1].bytes(), sh.stream));
+                zero_gathered(g, sh, adj_of(sh, c), t.F[0].get(), sizeof(unsigned long long));
+                zero_gathered(g, sh, adj_of(sh, c), t.F[1].get(), sizeof(unsigned long long));
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
-                if (tds[i].hs.size()) JG_HIP(hipMemsetAsync(tds[i].hs.get(), 0, tds[i].hs.bytes(), sh.stream));
+                if (tds[i].hs.size()) zero_gathered(g, sh, JG_ADJ_BOTH, tds[i].hs.get(), sizeof(unsigned long long));
                 St::Rec* r0 = nullptr;
                 if (td_ok && tune().msbfs_diag != 1) {  // level 0 as records of the source rows
                     t.recs.emplace_back();
@@ -2633,7 +2677,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         if (!have_live) {
                             const int64_t vlen = g.vec_len(sh, adj_of(sh, c));
                             JG_HIP(hipMemsetAsync(lw, 0, sizeof(unsigned long long), sh.stream));
-                            msbfs_live_kernel<<<grid_for(vlen), kBlock, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
+                            msbfs_live_kernel<<<red_grid(vlen), kRedThreads, 0, sh.stream>>>(t.F[cur].get(), vlen, lw);
                             JG_LAUNCH_CHECK();
                         }
                         op.live = lw;
@@ -2657,7 +2701,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
                                     t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                                 JG_LAUNCH_CHECK();
-                                msbfs_task_live_kernel<<<grid_for(bd.tasks), kBlock, 0, sh.stream>>>(
+                                msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
                                     bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
                                 JG_LAUNCH_CHECK();
                                 tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
@@ -2691,7 +2735,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
                                        sh.stream);
-                            msbfs_scan_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                            msbfs_scan_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
                                 t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), lw, tds[i].ctr.get());
                             JG_LAUNCH_CHECK();
                         }
@@ -2739,8 +2783,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
                 St& t = st[i];
-                msbfs_pairs_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.vis.get(), sh.rows, t.work.get() + 1);
-                JG_LAUNCH_CHECK();
+                if (level >= kMsLevelWords) {  // the plane entries are counted only when planes were written
+                    msbfs_pairs_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(t.vis.get(), sh.rows,
+                                                                                          t.work.get() + 1);
+                    JG_LAUNCH_CHECK();
+                }
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels
