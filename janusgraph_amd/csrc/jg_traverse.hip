@@ -876,19 +876,14 @@ struct MsTd {
     int32_t* hlist;
     int64_t* hlist_off;        // scratch of the appender
     unsigned long long* hpacked;
-    // sparse reverse exchange (nullable): pcnt[q] += the slots about peer q this level set first
+    // (unused: the per-peer counts of the sparse reverse exchange come from msbfs_slot_hist_kernel)
     unsigned long long* pcnt;
     int r, P;                  // this shard's index, the shard count
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
     __shared__ WaveStage ws, hws;
-    __shared__ unsigned int lpc[kMaxPeersMs];
     WaveApp app{ws}, happ{hws};
-    if (a.pcnt) {
-        for (int q = threadIdx.x; q < a.P; q += blockDim.x) lpc[q] = 0u;
-        __syncthreads();
-    }
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
@@ -932,16 +927,12 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
             }
             app.append(take, u, 0, a.touched, a.touched_off, a.tpacked);
             if (a.hstage) happ.append(hfirst, u, 0, a.hlist, a.hlist_off, a.hpacked);
-            if (a.pcnt && hfirst) atomicAdd(&lpc[slot_peer(u, a.tbits, a.r)], 1u);
+
         }
     }
     app.final(a.touched, a.touched_off, a.tpacked);
     if (a.hstage) happ.final(a.hlist, a.hlist_off, a.hpacked);
-    if (a.pcnt) {
-        __syncthreads();
-        for (int q = threadIdx.x; q < a.P; q += blockDim.x)
-            if (lpc[q]) atomicAdd(&a.pcnt[q], (unsigned long long)lpc[q]);
-    }
+
 }
 
 // ---- sparse reverse exchange of a sharded top-down level (only the staging slots the level set) ----
@@ -957,35 +948,67 @@ struct PairRuns {
 
 // the (offset, word) pairs of every set staging slot, grouped by peer (order inside a run is free: the
 // receiver ORs); cursor[P] zeroed by the caller
-__global__ __launch_bounds__(kBlock) void msbfs_pair_pack_kernel(const int32_t* __restrict__ hlist, int64_t nh,
-                                                                 const unsigned long long* __restrict__ hs, int tbits,
-                                                                 int r, PairRuns pr,
-                                                                 unsigned long long* __restrict__ cursor,
-                                                                 unsigned long long* __restrict__ pairs) {
+// Per-peer counts of the halo staging slots a top-down level set first (hlist[0, nh), nh the packed
+// counter's vertices): block b takes the b-th of gridDim.x equal chunks, bcount[b * P + q] = its slots
+// about peer q, pcnt[q] += them (at most gridDim.x atomics per peer; the top-down kernel's one atomic per
+// block and peer, on grids of up to 8192 blocks, queued thousands of them on each counter).
+__global__ __launch_bounds__(kRedThreads) void msbfs_slot_hist_kernel(const int32_t* __restrict__ hlist,
+                                                                      const unsigned long long* __restrict__ hpacked,
+                                                                      int tbits, int r, int P,
+                                                                      unsigned int* __restrict__ bcount,
+                                                                      unsigned long long* __restrict__ pcnt) {
     __shared__ unsigned int lc[kMaxPeersMs];
-    __shared__ unsigned long long base[kMaxPeersMs];
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < nh; k0 += stride) {  // block-uniform trips
+    const int64_t nh = (int64_t)(*hpacked >> kPackShift);
+    const int64_t chunk = (nh + gridDim.x - 1) / gridDim.x;
+    const int64_t k0 = (int64_t)blockIdx.x * chunk, k1 = k0 + chunk < nh ? k0 + chunk : nh;
+    for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+    __syncthreads();
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) atomicAdd(&lc[slot_peer(hlist[k], tbits, r)], 1u);
+    __syncthreads();
+    for (int q = threadIdx.x; q < P; q += blockDim.x) {
+        bcount[(int64_t)blockIdx.x * P + q] = lc[q];
+        if (lc[q]) atomicAdd(&pcnt[q], (unsigned long long)lc[q]);
+    }
+}
+
+// Packs the set staging slots as (offset in the peer's segment, word) pairs, grouped by peer: block b
+// takes the same chunk as msbfs_slot_hist_kernel (the same grid), its runs start after the earlier
+// blocks' (an exclusive sum of bcount), and its slots take their places by LDS cursors: no global atomics.
+__global__ __launch_bounds__(kRedThreads) void msbfs_pair_pack_kernel(const int32_t* __restrict__ hlist, int64_t nh,
+                                                                      const unsigned long long* __restrict__ hs, int tbits,
+                                                                      int r, PairRuns pr,
+                                                                      const unsigned int* __restrict__ bcount,
+                                                                      unsigned long long* __restrict__ pairs) {
+    __shared__ unsigned int lc[kMaxPeersMs];
+    __shared__ int64_t base[kMaxPeersMs];
+    const int64_t chunk = (nh + gridDim.x - 1) / gridDim.x;
+    const int64_t k0 = (int64_t)blockIdx.x * chunk, k1 = k0 + chunk < nh ? k0 + chunk : nh;
+    for (int q = threadIdx.x; q < pr.P; q += blockDim.x) {
+        int64_t b = pr.off[q];
+        for (unsigned x = 0; x < blockIdx.x; ++x) b += bcount[(int64_t)x * pr.P + q];
+        base[q] = b;
+    }
+    __syncthreads();
+    for (int64_t s0 = k0; s0 < k1; s0 += blockDim.x) {  // block-uniform trips
         for (int q = threadIdx.x; q < pr.P; q += blockDim.x) lc[q] = 0u;
         __syncthreads();
-        const int64_t k = k0 + threadIdx.x;
+        const int64_t k = s0 + threadIdx.x;
         int q = 0;
         unsigned int p = 0;
         int32_t u = 0;
-        if (k < nh) {
+        if (k < k1) {
             u = hlist[k];
             q = slot_peer(u, tbits, r);
             p = atomicAdd(&lc[q], 1u);
         }
         __syncthreads();
-        for (int x = threadIdx.x; x < pr.P; x += blockDim.x)
-            base[x] = lc[x] ? atomicAdd(&cursor[x], (unsigned long long)lc[x]) : 0ull;
-        __syncthreads();
-        if (k < nh) {
-            const int64_t j = pr.off[q] + (int64_t)(base[q] + p);
+        if (k < k1) {
+            const int64_t j = base[q] + p;
             pairs[2 * j] = (unsigned long long)((uint32_t)u & ((1u << tbits) - 1u));
             pairs[2 * j + 1] = hs[u];
         }
+        __syncthreads();
+        for (int x = threadIdx.x; x < pr.P; x += blockDim.x) base[x] += lc[x];
         __syncthreads();
     }
 }
@@ -2141,6 +2164,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> hs;    // sharded: halo staging (compact positions), zero between levels
                 DevBuf<int32_t> hlist;            // sharded: the staging slots a level set
                 DevBuf<int64_t> hlist_off;        // appender scratch
+                DevBuf<unsigned int> bcount;      // [kRedBlocks][P] set staging slots per histogram block and peer
                 DevBuf<unsigned long long> pairs, rpairs, pcnt;  // sparse reverse exchange: sent / received
                                                                  // (offset, word) pairs, per-peer counts + cursors
                 std::vector<int64_t> src_rows;
@@ -2286,6 +2310,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             td.pairs.alloc(2 * std::max<int64_t>(h.recv_off[g.P], 1));
                             td.rpairs.alloc(2 * std::max<int64_t>(h.send_off[g.P], 1));
                             td.pcnt.alloc(2 * (size_t)g.P);
+                            td.bcount.alloc((size_t)kRedBlocks * g.P);
                         }
                     }
                 }
@@ -2481,6 +2506,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                                   (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                               kBlock, 0, sh.stream>>>(a);
                             JG_LAUNCH_CHECK();
+                            if (td_shard && td.pcnt.size()) {  // the set slots per peer (the sparse exchange's sizes)
+                                msbfs_slot_hist_kernel<<<(unsigned)kRedBlocks, kRedThreads, 0, sh.stream>>>(
+                                    td.hlist.get(), td.ctr.get() + 2, sh.halo_both.tbits, sh.index, g.P, td.bcount.get(),
+                                    td.pcnt.get());
+                                JG_LAUNCH_CHECK();
+                            }
                         }
                         fv.push_back(td.hs.get());
                         rv.push_back(td.rbuf.get());
@@ -2536,9 +2567,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 }
                                 const int64_t nh = so[i][(size_t)P];
                                 if (nh > 0) {
-                                    msbfs_pair_pack_kernel<<<grid_for(nh), kBlock, 0, sh.stream>>>(
+                                    msbfs_pair_pack_kernel<<<(unsigned)kRedBlocks, kRedThreads, 0, sh.stream>>>(
                                         tds[i].hlist.get(), nh, tds[i].hs.get(), sh.halo_both.tbits, sh.index, pk,
-                                        tds[i].pcnt.get() + P, tds[i].pairs.get());
+                                        tds[i].bcount.get(), tds[i].pairs.get());
                                     JG_LAUNCH_CHECK();
                                 }
                                 for (int q = 0; q <= P; ++q) {
