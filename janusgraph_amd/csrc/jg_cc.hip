@@ -259,10 +259,11 @@ __global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict_
 // giant component and another vertex is linked from the other side).  Rows are degree-sorted: rows
 // below `heavy` (degree >= 64) take a wave each, the others a thread.
 // *linked += the entries linked (one atomic per wave; the work counter of jg_stats.algorithmic_bytes)
-__global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, const int64_t* __restrict__ rp,
-                                                               const int32_t* __restrict__ col, int64_t rows,
-                                                               int64_t heavy, int k, int32_t giant,
-                                                               unsigned long long* __restrict__ linked) {
+__global__ __launch_bounds__(kRedThreads) void uf_link_rest_kernel(int32_t* parent, const int64_t* __restrict__ rp,
+                                                                    const int32_t* __restrict__ col, int64_t rows,
+                                                                    int64_t heavy, int k, int32_t giant,
+                                                                    unsigned long long* __restrict__ linked) {
+    __shared__ unsigned long long red[kRedWaves];
     const int lane = threadIdx.x & (kWave - 1);
     unsigned long long count = 0;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
@@ -284,8 +285,8 @@ __global__ __launch_bounds__(kBlock) void uf_link_rest_kernel(int32_t* parent, c
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
-    count = wave_reduce_add(count);
-    if (lane == 0 && count) atomicAdd(linked, count);
+    count = block_reduce(count, AddU64{}, red);  // one atomic per block: nearly every wave links something
+    if (threadIdx.x == 0 && count) atomicAdd(linked, count);
 }
 
 __global__ void uf_compress_kernel(int32_t* parent, int64_t rows) {
@@ -300,23 +301,18 @@ __global__ void uf_sample_kernel(const int32_t* __restrict__ parent, int64_t row
 
 // minr[root] = the smallest rank of the root's component: the giant component through a block
 // reduction (one atomic per block), the others with an atomicMin each (small components).
-__global__ __launch_bounds__(kBlock) void uf_minrank_kernel(const int32_t* __restrict__ parent,
-                                                             const int32_t* __restrict__ rank, int64_t rows,
-                                                             int32_t giant, int32_t* __restrict__ minr) {
-    __shared__ int32_t red[kBlock / kWave];
+__global__ __launch_bounds__(kRedThreads) void uf_minrank_kernel(const int32_t* __restrict__ parent,
+                                                                  const int32_t* __restrict__ rank, int64_t rows,
+                                                                  int32_t giant, int32_t* __restrict__ minr) {
+    __shared__ int32_t red[kRedWaves];
     int32_t g = INT_MAX;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         const int32_t r = parent[v], k = rank[v];
         if (r == giant) g = k < g ? k : g;
         else atomicMin(&minr[r], k);
     }
-    g = wave_reduce_min(g);
-    if (lane_id() == 0) red[wave_id()] = g;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) g = red[w] < g ? red[w] : g;
-        if (g != INT_MAX) atomicMin(&minr[giant], g);
-    }
+    g = block_reduce(g, MinI32{}, red);
+    if (threadIdx.x == 0 && g != INT_MAX) atomicMin(&minr[giant], g);
 }
 
 // the number of rows of degree >= 64 (rows are degree-sorted: a binary search of the row offsets)
@@ -384,12 +380,12 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
         }
         i = j;
     }
-    uf_link_rest_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
-                                                        giant, linked.get());
+    uf_link_rest_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
+                                                             giant, linked.get());
     JG_LAUNCH_CHECK();
     uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
     JG_LAUNCH_CHECK();
-    uf_minrank_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, rank, ne, giant, minr);
+    uf_minrank_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
     // the BFS start picks the sources and rewrites parent into the labels
     double reached = 0;
@@ -536,8 +532,9 @@ __global__ __launch_bounds__(kBlock) void cc_giant_search_kernel(CcShardLink a) 
 // the second round: rows outside the giant tree link their remaining entries; giant rows link the
 // flagged copies of peers the search did not find (nothing when all were found).  Rows below `heavy`
 // (degree >= 64) take a wave each, the others a thread.  *linked += the entries scanned.
-__global__ __launch_bounds__(kBlock) void cc_link_rest_sharded_kernel(CcShardLink a,
-                                                                       unsigned long long* __restrict__ linked) {
+__global__ __launch_bounds__(kRedThreads) void cc_link_rest_sharded_kernel(CcShardLink a,
+                                                                            unsigned long long* __restrict__ linked) {
+    __shared__ unsigned long long red[kRedWaves];
     const int lane = lane_id();
     unsigned long long count = 0;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
@@ -564,17 +561,17 @@ __global__ __launch_bounds__(kBlock) void cc_link_rest_sharded_kernel(CcShardLin
             if (!giant || (u >= a.rows && !a.found[u >> a.tbits] && flag_of(a.flag, u))) uf_link(a.parent, (int32_t)v, u);
         }
     }
-    count = wave_reduce_add(count);
-    if (lane == 0 && count) atomicAdd(linked, count);
+    count = block_reduce(count, AddU64{}, red);
+    if (threadIdx.x == 0 && count) atomicAdd(linked, count);
 }
 
 // T[root] = the minimum over the tree's members: own rows with an edge their labels, copies their
 // owners'; the giant tree's through a block reduction (one atomic per block)
-__global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(SlotMap sm, const int32_t* __restrict__ parent,
-                                                              const int32_t* __restrict__ label,
-                                                              const int32_t* __restrict__ msg, int32_t giant,
-                                                              int32_t* __restrict__ tmin) {
-    __shared__ int32_t red[kBlock / kWave];
+__global__ __launch_bounds__(kRedThreads) void cc_tree_min_kernel(SlotMap sm, const int32_t* __restrict__ parent,
+                                                                   const int32_t* __restrict__ label,
+                                                                   const int32_t* __restrict__ msg, int32_t giant,
+                                                                   int32_t* __restrict__ tmin) {
+    __shared__ int32_t red[kRedWaves];
     int32_t g = INT_MAX;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < sm.total; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t x = sm.pos(j);
@@ -584,13 +581,8 @@ __global__ __launch_bounds__(kBlock) void cc_tree_min_kernel(SlotMap sm, const i
         if (r == giant) g = m < g ? m : g;
         else if (m < tmin[r]) atomicMin(&tmin[r], m);
     }
-    g = wave_reduce_min(g);
-    if (lane_id() == 0) red[wave_id()] = g;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) g = red[w] < g ? red[w] : g;
-        if (g != INT_MAX && giant >= 0) atomicMin(&tmin[giant], g);
-    }
+    g = block_reduce(g, MinI32{}, red);
+    if (threadIdx.x == 0 && g != INT_MAX && giant >= 0) atomicMin(&tmin[giant], g);
 }
 
 // own rows with an edge take their tree's minimum (labels only decrease); copies take it too, for the
@@ -759,7 +751,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         for (int q = 0; q < P; ++q)
             if (q != sh.index && h.recv_off[(size_t)q + 1] > h.recv_off[(size_t)q] && !found[(size_t)h.seg_of(q, sh.index)])
                 t.all_found = 0;
-        cc_link_rest_sharded_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(link_args(i), t.linked.get());
+        cc_link_rest_sharded_kernel<<<red_grid(t.ne), kRedThreads, 0, s>>>(link_args(i), t.linked.get());
         JG_LAUNCH_CHECK();
         cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, sh.cc_msg[1].get());
         JG_LAUNCH_CHECK();
@@ -792,8 +784,8 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
                 cc_tree_init_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, t.label.get(), sh.cc_msg[0].get(), t.tmin.get());
                 JG_LAUNCH_CHECK();
             }
-            cc_tree_min_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, sh.cc_msg[1].get(), t.label.get(), sh.cc_msg[0].get(),
-                                                               t.giant, t.tmin.get());
+            cc_tree_min_kernel<<<red_grid(t.sm.total), kRedThreads, 0, sh.stream>>>(
+                t.sm, sh.cc_msg[1].get(), t.label.get(), sh.cc_msg[0].get(), t.giant, t.tmin.get());
             JG_LAUNCH_CHECK();
             cc_tree_apply_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, sh.cc_msg[1].get(), t.tmin.get(), t.label.get(),
                                                                  sh.cc_msg[0].get(), sh.cc_changed.get());

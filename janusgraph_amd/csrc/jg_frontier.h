@@ -8,6 +8,37 @@ namespace jg {
 constexpr int kPackShift = 37;  // packed frontier counter: (vertices << 37) | push edges
 constexpr unsigned long long kEdgeMask = (1ull << kPackShift) - 1ull;
 
+// Counters reduced by many workgroups (MS-BFS live bits, frontier counters, live-task and pair counts,
+// CC's linked entries and giant-component minima): one device atomic per 1024-thread workgroup on a
+// grid of at most kRedBlocks (two per CU: 32 waves).  A device-scope atomic on one word executes at
+// the memory side, ~88 per us (MI355X_MICROARCH.md, dequeue row); one per wave on a 4096-block grid
+// queued 16 K of them, ~0.2 ms, behind kernels of ~20-60 us of work (msbfs_task_live_kernel,
+// msbfs_pairs_kernel in the round-3 8-shard trace).
+constexpr int kRedThreads = 1024, kRedWaves = kRedThreads / kWave;
+constexpr int64_t kRedBlocks = 512;
+inline unsigned red_grid(int64_t work) { return grid_for(work, kRedThreads, kRedBlocks); }
+
+// v reduced over the block (every thread calls; `red` holds blockDim.x / kWave elements); valid in thread 0
+template <class T, class F>
+__device__ __forceinline__ T block_reduce(T v, F op, T* red) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, kWave));
+    if (lane_id() == 0) red[wave_id()] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) v = op(v, red[w]);
+    return v;
+}
+struct OrU64 {
+    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a | b; }
+};
+struct AddU64 {
+    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a + b; }
+};
+struct MinI32 {
+    __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; }
+};
+
 // Block-aggregated frontier append: the block's waves combine their counts in LDS and
 // one thread reserves the block's range with a single atomic (a level that finds most of the graph
 // would otherwise put one atomic per wave on one address).  Must be reached by every thread of the

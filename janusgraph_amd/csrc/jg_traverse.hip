@@ -492,32 +492,6 @@ struct MsBfsOp {
     }
 };
 
-// Counters reduced by many workgroups (the live bits, frontier counters, live-task and pair counts):
-// one device atomic per 1024-thread workgroup on a grid of at most kRedBlocks (the CUs).  A device-
-// scope atomic on one word executes at the memory side, ~88 per us (MI355X_MICROARCH.md, dequeue row);
-// one per wave on a 4096-block grid queued 16 K of them, ~0.2 ms, behind kernels of ~20-60 us of work
-// (msbfs_task_live_kernel, msbfs_pairs_kernel in the round-3 8-shard trace).
-constexpr int kRedThreads = 1024, kRedWaves = kRedThreads / kWave;
-constexpr int64_t kRedBlocks = 256;
-inline unsigned red_grid(int64_t work) { return grid_for(work, kRedThreads, kRedBlocks); }
-
-template <class T, class F>
-__device__ __forceinline__ T block_reduce(T v, F op, T* red) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, kWave));
-    if (lane_id() == 0) red[wave_id()] = v;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) v = op(v, red[w]);
-    return v;  // valid in thread 0
-}
-struct OrU64 {
-    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a | b; }
-};
-struct AddU64 {
-    __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a + b; }
-};
-
 // *live |= the OR of every word of F (one atomic per block)
 __global__ __launch_bounds__(kRedThreads) void msbfs_live_kernel(const unsigned long long* __restrict__ F, int64_t len,
                                                                  unsigned long long* __restrict__ live) {
