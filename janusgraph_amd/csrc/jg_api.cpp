@@ -767,6 +767,8 @@ int jg_tune_set(const char* key, int64_t value) {
         jg::tune().relabel_ties = value != 0;
     } else if (k == "relabel_dead_last") {
         jg::tune().relabel_dead_last = value != 0;
+    } else if (k == "relabel_out_ties") {
+        jg::tune().relabel_out_ties = value != 0;
     } else if (k == "pr_rank_last") {
         jg::tune().pr_rank_last = value != 0;
     } else if (k == "pr_skip_empty") {

@@ -223,11 +223,13 @@ __global__ void nbr_min_kernel(const int32_t* __restrict__ src, const int32_t* _
 // a vertex without pull neighbours (in-degree 0: all of them tie in degree) is ordered by its out-degree
 // instead, descending: the rarely gathered sources among the in-degree-0 rows (~9% of the vertices,
 // <1% of the gathers) sit together at the front of that class instead of spread over all of it
+// `out_ties` (tune relabel_out_ties): every tie is ordered by out-degree (gather count), descending, so the
+// gathered vector's lines hold values of like heat (nbr_min unused)
 __global__ void tie_keys_kernel(const int32_t* __restrict__ nbr_min, int64_t n, int vbits,
-                                const int32_t* __restrict__ gather_deg, int64_t max_gather,
+                                const int32_t* __restrict__ gather_deg, int64_t max_gather, bool out_ties,
                                 uint64_t* __restrict__ keys) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
-        int64_t t = nbr_min[v] >= n ? n : nbr_min[v];
+        int64_t t = out_ties ? n : (nbr_min[v] >= n ? n : nbr_min[v]);
         if (t == n && gather_deg) t = max_gather - (gather_deg[v] < max_gather ? gather_deg[v] : max_gather);
         keys[v] = ((uint64_t)t << vbits) | (uint64_t)v;
     }
@@ -1212,14 +1214,17 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                 DevBuf<int32_t> rank1(n), nbr_min(n);
                 rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, vmask, rank1.get());
                 JG_LAUNCH_CHECK();
-                JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
-                nbr_min_kernel<<<grid_for(pull.m, kBlock, 256 * 16), kBlock, 0, s>>>(pull.src, pull.dst, pull.m, mode,
-                                                                                      rank1.get(), nbr_min.get());
-                JG_LAUNCH_CHECK();
-                DevBuf<uint64_t> k1(n), k2(n);
                 const bool dead_last = mode == 0 && tune().relabel_dead_last;  // PageRank's gathered vector
+                const bool out_ties = dead_last && tune().relabel_out_ties;
+                if (!out_ties) {
+                    JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
+                    nbr_min_kernel<<<grid_for(pull.m, kBlock, 256 * 16), kBlock, 0, s>>>(pull.src, pull.dst, pull.m,
+                                                                                          mode, rank1.get(), nbr_min.get());
+                    JG_LAUNCH_CHECK();
+                }
+                DevBuf<uint64_t> k1(n), k2(n);
                 tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, dead_last ? dout : nullptr,
-                                                               std::min<int64_t>((int64_t)hc[3], n), k1.get());
+                                                               std::min<int64_t>((int64_t)hc[3], n), out_ties, k1.get());
                 JG_LAUNCH_CHECK();
                 prim::radix_sort(k1.get(), nullptr, n, vbits + bits_for((uint64_t)n), s);
                 tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, din, dout, mode, maxdeg,

@@ -558,6 +558,8 @@ struct Tune {
     int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
     int relabel_dead_last = 1;        // build time, IN plan: rows without out-edges last in their degree class,
                                       // in-degree-0 rows by out-degree (the gathered vector's lines hold live values)
+    int relabel_out_ties = 0;         // build time, IN plan with relabel_dead_last: every tie by out-degree (not by
+                                      // the hottest pull neighbour)
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
                                       // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)
     int dobfs_alpha = 30;             // the same for single-source traversals (tools/bfs_sweep.py, RMAT-20:
@@ -574,9 +576,11 @@ struct Tune {
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
                                       //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
-    int msbfs_bu = 3;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
+    int msbfs_bu = 0;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
                                       //         (0 never, 1 every pull level, 2 when the frontier holds >= msbfs_bu_frac,
-                                      //         3 sparse levels: fewer than msbfs_bu_tasks permille of the tasks live;
+                                      //         3 sparse levels: fewer than msbfs_bu_tasks permille of the tasks live,
+                                      //         measured slower at RMAT-26's last pull level with 0.25% of its tasks
+                                      //         live: 17.84 / 17.80 vs 17.69 / 17.55 ms, profiles/r04/msbfs_bu3/;
                                       //         measured 2-4x slower than the merge-engine pull: RMAT-26 81.0 / 21.7 ms,
                                       //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
     int msbfs_bu_frac = 100;          //         permille of the rows

@@ -2399,7 +2399,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // bottom-up with early exit (msbfs_bu_kernel) instead of through the merge engine
             MsBu bu{};
             // msbfs_bu: 1 every pull level, 2 levels whose frontier holds >= msbfs_bu_frac permille of the rows,
-            // 3 (default) levels where fewer than msbfs_bu_tasks permille of the merge tasks can gain a bit
+            // 3 levels where fewer than msbfs_bu_tasks permille of the merge tasks can gain a bit (0, the default:
+            // the merge engine skips dead tasks cheaply enough that each variant measured slower)
             const bool bu_ok = td_one && c0.pull == c0.push && tune().msbfs_bu > 0;
             if (bu_ok) {
                 DevBuf<int64_t> bnd(2);

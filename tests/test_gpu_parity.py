@@ -223,7 +223,7 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
 @pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
                                          ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
                                          ("skip_dense_reverse", 3), ("skip_dense", 2), ("skip_every_level", 1),
-                                         ("skip_every_level", 3), ("merge_sparse_levels", 1), ("bu_sparse_always", 1),
+                                         ("skip_every_level", 3), ("bu_sparse_levels", 1), ("bu_sparse_always", 1),
                                          ("bu_every_level", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
@@ -234,8 +234,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     halo exchange, sparse (offset, word) pairs when few staging slots are set, the whole segments with
     skip_dense_reverse); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2).
     The first pull level runs every task by default (msbfs_skip_first); skip_every_level builds the
-    task bitmaps on that level too.  One shard: a later pull level with fewer than msbfs_bu_tasks permille
-    of live tasks runs msbfs_bu_kernel (bottom-up, early exit) instead of the merge engine."""
+    task bitmaps on that level too.  One shard, msbfs_bu 3: a later pull level with fewer than
+    msbfs_bu_tasks permille of live tasks runs msbfs_bu_kernel (bottom-up, early exit) instead of the merge
+    engine."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
@@ -244,9 +245,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
              "skip_dense": [("halo", 0)], "skip_sharded_pull_only": [("msbfs_td", 2)],
              "skip_dense_reverse": [("msbfs_sparse", 0)], "skip_every_level": [("msbfs_skip_first", 0)],
-             # sparse pull levels (msbfs_bu 3, the default): through the merge engine instead, every bitmapped
-             # level bottom-up, every pull level bottom-up
-             "merge_sparse_levels": [("msbfs_bu", 0)], "bu_sparse_always": [("msbfs_bu_tasks", 1000)],
+             # bottom-up pull levels (msbfs_bu; 0, the merge engine, by default): sparse levels only, every
+             # bitmapped level, every pull level
+             "bu_sparse_levels": [("msbfs_bu", 3)], "bu_sparse_always": [("msbfs_bu", 3), ("msbfs_bu_tasks", 1000)],
              "bu_every_level": [("msbfs_bu", 1)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
@@ -273,7 +274,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_skip", 1)
         _lib.tune_set("msbfs_td", 1)
         _lib.tune_set("msbfs_sparse", 1)
-        _lib.tune_set("msbfs_bu", 3)
+        _lib.tune_set("msbfs_bu", 0)
         _lib.tune_set("msbfs_bu_tasks", 20)
         _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
@@ -454,7 +455,7 @@ def test_errors_are_status_codes(ctx):
 @pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
                                   "split_sub1", "split_sub2_4", "split_w24", "split_w32", "split_stage_off",
                                   "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip", "cc_first3",
-                                  "split_sliced_build"])
+                                  "split_sliced_build", "relabel_dead_first", "relabel_out_ties"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
     """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
     LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
@@ -483,7 +484,9 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "merge_chunks16": [("merge_interleave", 0)],
              "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)],
              "cc_first3": [("cc_first", 3)],
-             "split_sliced_build": [("band_sliced_build", 1)]}[mode]
+             "split_sliced_build": [("band_sliced_build", 1)],
+             "relabel_dead_first": [("relabel_dead_last", 0)],
+             "relabel_out_ties": [("relabel_out_ties", 1)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -511,6 +514,8 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
         _lib.tune_set("band_sliced_build", 0)
+        _lib.tune_set("relabel_dead_last", 1)
+        _lib.tune_set("relabel_out_ties", 0)
         _lib.tune_set("slice_lds", 1)
         _lib.tune_set("merge_pack", 1)
         _lib.tune_set("merge_stage0", -1)
