@@ -153,6 +153,31 @@ def pmc_traffic(workload):
     return None, None
 
 
+def trace_kernel_ms(workload):
+    """Kernel time per run of a workload from the newest committed counter-free rocprofv3 trace summary
+    (profiles/<round>/trace/<name>/summary.json, made by tools/gpu_steps.sh "trace" steps with
+    tools/trace_summary.py): the check that a block's kernel_ms is not inflated by counter collection
+    (VERDICT r03 item 6).  None when there is none."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for rnd in sorted(os.listdir(pdir), reverse=True):
+        tdir = os.path.join(pdir, rnd, "trace")
+        if not os.path.isdir(tdir):
+            continue
+        for dirpath, _, files in sorted(os.walk(tdir)):
+            if "summary.json" not in files:
+                continue
+            with open(os.path.join(dirpath, "summary.json")) as f:
+                s = json.load(f)
+            if s.get("workload") != workload:
+                continue
+            return {"kernel_ms_per_run": s.get("kernel_ms_per_run"), "kernel_ms_per_run_steady": s.get("kernel_ms_per_run_steady"),
+                    "event_ms_per_run": s.get("event_ms_per_run"),
+                    "source": os.path.relpath(os.path.join(dirpath, "summary.json"), ROOT)}
+    return None
+
+
 def cpu_baseline(scale, ef, seed, steps):
     """The oracle's PageRank superstep (OpenMP) on the same RMAT graph, rank 0 only."""
     from oracle import oracle as o
@@ -202,6 +227,8 @@ def hbm_roofline(alg_bytes, ms, kernel, workload=None, model=None):
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
          "kernel": kernel, "kernel_ms": round(ms, 4), "bytes_per_launch": alg_bytes}
+    if workload:
+        r["trace"] = trace_kernel_ms(workload)
     if model:
         r["model"] = model
     return r

@@ -934,10 +934,13 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
 // so log2(entries) - 19, within [4, 7], for the 8-byte PageRank vector (IN adjacency).  CC's 4-byte
 // labels (BOTH adjacency; tools/cc_ab.py): RMAT-24 14.3 / 14.9 / 16.2 ms at 4 / 5 / 6 bits, RMAT-26
 // 56.3 / 58.0 / 67.3 ms at 5 / 6 / 7, so 4 + (log2(entries) - 24) / 2.
+// fp64 vectors: log2(entries) - 19, at most 6 (round 4, with rows without out-edges last in their degree
+// class: RMAT-26 at 64 sub-slices 3.552 vs 3.592 ms at 128; RMAT-24 stays at 32: 0.761 vs 0.788 ms at 16;
+// profiles/r04/ab/); int32 vectors: 4 + (log2 - 24) / 2, at most 7
 int auto_band_bits(int64_t vec_entries, int elem_bytes) {
     const int l2 = (int)std::lround(std::log2((double)std::max<int64_t>(vec_entries, 1)));
     const int b = elem_bytes >= 8 ? l2 - 19 : 4 + (l2 - 24) / 2;
-    return std::min(std::max(b, 4), 7);
+    return std::min(std::max(b, 4), elem_bytes >= 8 ? 6 : 7);
 }
 
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
