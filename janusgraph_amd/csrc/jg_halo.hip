@@ -91,8 +91,21 @@ __global__ void list_local_kernel(int32_t* __restrict__ list, int64_t n, int64_t
 template <typename T>
 __global__ __launch_bounds__(kBlock) void halo_pack_kernel(const T* __restrict__ vec, const int32_t* __restrict__ src,
                                                            int64_t n, T* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = vec[src[i]];
+    // four gathers in flight per thread and trip (one per trip left the pack latency-bound: ~60 us for
+    // 14.7 M words at RMAT-26, P = 8)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        int32_t s[4];
+        T v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = src[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = vec[s[k]];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[i + k * stride] = v[k];
+    }
+    for (; i < n; i += stride) out[i] = vec[src[i]];
 }
 
 // Exclusive popcount prefix (words + 1 entries) and per-peer bases of a peer-major bitmap over

@@ -957,10 +957,14 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_pair_pack_kernel(const int3
     __shared__ int64_t base[kMaxPeersMs];
     const int64_t chunk = (nh + gridDim.x - 1) / gridDim.x;
     const int64_t k0 = (int64_t)blockIdx.x * chunk, k1 = k0 + chunk < nh ? k0 + chunk : nh;
-    for (int q = threadIdx.x; q < pr.P; q += blockDim.x) {
-        int64_t b = pr.off[q];
-        for (unsigned x = 0; x < blockIdx.x; ++x) b += bcount[(int64_t)x * pr.P + q];
-        base[q] = b;
+    if (k0 >= k1) return;  // block-uniform: an empty chunk writes nothing
+    // this block's run starts: wave w sums peer q = w (+ kRedWaves ...) over the earlier blocks' counts,
+    // one lane per block (a thread walking up to 511 blocks alone made every launch cost ~50 us)
+    for (int q = wave_id(); q < pr.P; q += kRedWaves) {
+        unsigned int s = 0;
+        for (unsigned x = lane_id(); x < blockIdx.x; x += kWave) s += bcount[(int64_t)x * pr.P + q];
+        s = wave_reduce_add(s);
+        if (lane_id() == 0) base[q] = pr.off[q] + (int64_t)s;
     }
     __syncthreads();
     for (int64_t s0 = k0; s0 < k1; s0 += blockDim.x) {  // block-uniform trips
@@ -1492,40 +1496,21 @@ struct SBfsLevel {
     const int64_t* rlen;            // [P] length of each peer's run in this shard's segment
     int P;
     const int32_t* send_src;  // own row of each send-list position
-    unsigned long long* packed;
+    unsigned long long* packed;       // this level's appends (the host reads it after the level)
+    unsigned long long* packed_next;  // the next level's counter: zeroed by this level's kernels
     int32_t level;
 };
 
-// The per-peer tables of a level (send offsets, word offsets, segment starts and lengths), staged in
-// LDS by every block: a word's peer is a scan over them, and from global memory that scan was up to
-// P dependent loads per word (the pack and apply kernels ran 60-100 us per launch at RMAT-26).
+// shard count the sharded traversal takes (CC checks it too before choosing its sharded path)
 constexpr int kMaxShardsBfs = 64;
-struct PeerTables {
-    int64_t send_off[kMaxShardsBfs + 1], woff[kMaxShardsBfs + 1], rwoff[kMaxShardsBfs + 1];
-    int64_t rseg[kMaxShardsBfs], rlen[kMaxShardsBfs];
-};
-__device__ __forceinline__ void stage_peer_tables(const SBfsLevel& a, PeerTables& t) {
-    for (int i = threadIdx.x; i <= a.P; i += blockDim.x) {
-        t.send_off[i] = a.send_off[i];
-        t.woff[i] = a.woff[i];
-        t.rwoff[i] = a.rwoff[i];
-        if (i < a.P) {
-            t.rseg[i] = a.rseg[i];
-            t.rlen[i] = a.rlen[i];
-        }
-    }
-    __syncthreads();
-}
-// the peer q with offs[q] <= w < offs[q + 1] (offs in LDS)
-__device__ __forceinline__ int peer_of(const int64_t* offs, int P, int64_t w) {
-    int q = 0;
-    while (q + 1 < P && offs[q + 1] <= w) ++q;
-    return q;
-}
 
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
     const int lo = __shfl((int)(uint32_t)v, src, kWave), hi = __shfl((int)(uint32_t)(v >> 32), src, kWave);
     return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ void sbfs_zero_next(const SBfsLevel& a) {
+    if (a.packed_next && blockIdx.x == 0 && threadIdx.x == 0) *a.packed_next = 0ull;
 }
 
 // top-down, edge-parallel over the local frontier's entries (as bfs_top_down): own neighbours are
@@ -1538,6 +1523,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
     const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
     const int32_t nd = a.level + 1;
+    sbfs_zero_next(a);
     for (int64_t t = 0; t < tiles; ++t) {
         if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x + wave_id() * kWave) * kTdEdgesPerThread >= a.mf)
             break;  // wave-uniform
@@ -1580,74 +1566,108 @@ __global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
     app.final(a.queue_out, a.qoff_out, a.packed);
 }
 
-// top-down, reader side: this level's stamps of every peer segment into its compact bitmap words (one
-// wave per word)
+// The per-word kernels below (pack_marks, td_apply, pack_bits) run on a (blocks, P) grid: blockIdx.y
+// is the peer whose run a block works on, so no word has to search the per-peer offset tables (a scan
+// of LDS-staged tables per word, and one wave per word and launch, held them to 45-80 us per launch at
+// RMAT-26, P = 8, for 1.8 M-word send lists).  A wave takes kSbfsWords words per trip with every load
+// issued on a clamped index before any is used.
+constexpr int kSbfsWords = 4;
+constexpr int kSbfsApplyChunk = 16;  // td_apply: words a wave loads at once (lanes 0..15), then walks
+
+// top-down, reader side: this level's stamps of peer q's segment into its compact bitmap words
 __global__ __launch_bounds__(kBlock) void sbfs_pack_marks_kernel(SBfsLevel a) {
-    __shared__ PeerTables pt;
-    stage_peer_tables(a, pt);
-    const int64_t words = pt.rwoff[a.P];
+    sbfs_zero_next(a);
+    const int q = blockIdx.y;
+    const int64_t nw = a.rwoff[q + 1] - a.rwoff[q], len = a.rlen[q], seg = a.rseg[q];
+    const int32_t* __restrict__ stamp = a.stamp + seg;
+    unsigned long long* __restrict__ hb = a.hb + (seg >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
     const int32_t nd = a.level + 1;
-    for (int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w < words; w += nwaves) {
-        const int q = peer_of(pt.rwoff, a.P, w);
-        const int64_t j = (w - pt.rwoff[q]) * 64 + lane_id();
-        const bool bit = j < pt.rlen[q] && a.stamp[pt.rseg[q] + j] == nd;
-        const uint64_t word = __ballot(bit);
-        if (lane_id() == 0) a.hb[(pt.rseg[q] >> 6) + (w - pt.rwoff[q])] = word;
+    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
+        int32_t val[kSbfsWords];
+        bool in[kSbfsWords];
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
+            in[k] = j < len;
+            val[k] = stamp[in[k] ? j : len - 1];  // words exist only for len > 0
+        }
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const uint64_t word = __ballot(in[k] && val[k] == nd);
+            if (lane_id() == 0 && w0 + k * nwaves < nw) hb[w0 + k * nwaves] = word;
+        }
     }
 }
 
-// top-down, owner side: lanes load consecutive received words; the wave walks the non-zero ones, lane
-// b claiming the row of the word's bit b
+// top-down, owner side: received words of peer q's run; a wave loads kSbfsApplyChunk words and claims
+// the rows of their set bits, kSbfsWords non-zero words at a time (lane b: the row of bit b)
 __global__ __launch_bounds__(kBlock) void sbfs_td_apply_kernel(SBfsLevel a) {
     __shared__ WaveStage ws;
-    __shared__ PeerTables pt;
-    stage_peer_tables(a, pt);
+    sbfs_zero_next(a);
     WaveApp app{ws};
-    constexpr int kWpb = kBlock / kWave;
-    const int64_t words = pt.woff[a.P];
+    const int q = blockIdx.y;
+    const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
+    const int32_t* __restrict__ src = a.send_src + so;
+    const int64_t step = (int64_t)gridDim.x * (kBlock / kWave) * kSbfsApplyChunk;
     const int32_t nd = a.level + 1;
-    for (int64_t base = ((int64_t)blockIdx.x * kWpb + wave_id()) * kWave; base < words;
-         base += (int64_t)gridDim.x * kWpb * kWave) {  // wave-uniform
-        const int64_t w = base + lane_id();
-        const unsigned long long mine = w < words ? a.sw[w] : 0ull;
+    for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / kWave) + wave_id()) * kSbfsApplyChunk; c0 < nw;
+         c0 += step) {  // wave-uniform
+        const unsigned long long mine =
+            lane_id() < kSbfsApplyChunk && c0 + lane_id() < nw ? a.sw[wo + c0 + lane_id()] : 0ull;
         uint64_t nz = __ballot(mine != 0ull);
         while (nz) {  // wave-uniform
-            const int l = __ffsll((unsigned long long)nz) - 1;
-            nz &= nz - 1;
-            const unsigned long long word = shfl_u64(mine, l);
-            bool take = false;
-            int32_t u = 0;
-            int64_t deg = 0;
-            if ((word >> lane_id()) & 1ull) {
-                const int64_t ww = base + l;
-                const int q = peer_of(pt.woff, a.P, ww);
-                // bits past a run's end are never set: x < send_off[q + 1]
-                u = a.send_src[pt.send_off[q] + (ww - pt.woff[q]) * 64 + lane_id()];
-                if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
-                    take = true;
-                    deg = a.rp[u + 1] - a.rp[u];
-                }
+            unsigned long long word[kSbfsWords];
+            int32_t u[kSbfsWords];
+#pragma unroll
+            for (int k = 0; k < kSbfsWords; ++k) {
+                const int l = nz ? __ffsll((unsigned long long)nz) - 1 : 0;
+                word[k] = nz ? shfl_u64(mine, l) : 0ull;
+                nz &= nz - 1;
+                const int64_t x = (c0 + l) * 64 + lane_id();
+                u[k] = src[x < cnt ? x : cnt - 1];  // bits past the run's end are never set
             }
-            app.append(take, u, deg, a.queue_out, a.qoff_out, a.packed);
+#pragma unroll
+            for (int k = 0; k < kSbfsWords; ++k) {
+                if (!word[k]) continue;  // wave-uniform
+                bool take = false;
+                int64_t deg = 0;
+                if (((word[k] >> lane_id()) & 1ull) && a.dvec[u[k]] < 0 && atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
+                    take = true;
+                    deg = a.rp[u[k] + 1] - a.rp[u[k]];
+                }
+                app.append(take, u[k], deg, a.queue_out, a.qoff_out, a.packed);
+            }
         }
     }
     app.final(a.queue_out, a.qoff_out, a.packed);
 }
 
-// bottom-up, owner side before the forward exchange: one wave per send-list word, bit b = the depth of
-// the word's row b is this level's
+// bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = the depth of the
+// word's row b is this level's
 __global__ __launch_bounds__(kBlock) void sbfs_pack_bits_kernel(SBfsLevel a) {
-    __shared__ PeerTables pt;
-    stage_peer_tables(a, pt);
-    const int64_t words = pt.woff[a.P];
+    sbfs_zero_next(a);
+    const int q = blockIdx.y;
+    const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
+    const int32_t* __restrict__ src = a.send_src + so;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w < words; w += nwaves) {
-        const int q = peer_of(pt.woff, a.P, w);
-        const int64_t x = pt.send_off[q] + (w - pt.woff[q]) * 64 + lane_id();
-        const bool bit = x < pt.send_off[q + 1] && a.dvec[a.send_src[x]] == a.level;
-        const uint64_t word = __ballot(bit);
-        if (lane_id() == 0) a.sw[w] = word;
+    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
+        int32_t r[kSbfsWords];
+        bool in[kSbfsWords];
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const int64_t x = (w0 + k * nwaves) * 64 + lane_id();
+            in[k] = x < cnt;
+            r[k] = src[in[k] ? x : cnt - 1];  // words exist only for a nonempty run
+        }
+        int32_t d[kSbfsWords];
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) d[k] = a.dvec[r[k]];
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const uint64_t word = __ballot(in[k] && d[k] == a.level);
+            if (lane_id() == 0 && w0 + k * nwaves < nw) a.sw[wo + w0 + k * nwaves] = word;
+        }
     }
 }
 
@@ -1659,6 +1679,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
     constexpr int kWpb = kBlock / kWave;
     const int64_t wstride = (int64_t)gridDim.x * kWpb;
     const int32_t nd = a.level + 1;
+    sbfs_zero_next(a);
     for (int64_t w = (int64_t)blockIdx.x * kWpb + wave_id(); w < words; w += wstride) {  // wave-uniform
         const int64_t v = w * 64 + lane_id();
         bool found = false;
@@ -1727,7 +1748,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         DevBuf<int32_t> dvec, stamp, queue[2];
         DevBuf<int64_t> qoff[2], send_off, woff, rwoff, rseg, rlen;
         DevBuf<unsigned long long> ctr, hb, sw;
-        int64_t nq = 0, mf = 0, hb_words = 0, sw_words = 0, rw_words = 0;
+        int64_t nq = 0, mf = 0, hb_words = 0, sw_words = 0, rw_words = 0, sw_max = 0, rw_max = 0;
     };
     std::vector<St> st(ns);
     int64_t tot[2] = {0, 0};  // entries of all shards, rows of all shards
@@ -1748,6 +1769,10 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             rwoff[(size_t)q + 1] = rwoff[(size_t)q] + (rlen[(size_t)q] + 63) / 64;
         }
         t.rw_words = rwoff[(size_t)g.P];
+        for (int q = 0; q < g.P; ++q) {  // the longest run on each side: the x extent of the (blocks, P) grids
+            t.rw_max = std::max(t.rw_max, rwoff[(size_t)q + 1] - rwoff[(size_t)q]);
+            t.sw_max = std::max(t.sw_max, woff[(size_t)q + 1] - woff[(size_t)q]);
+        }
         t.rwoff.alloc(g.P + 1);
         t.rseg.alloc(g.P);
         t.rlen.alloc(g.P);
@@ -1766,7 +1791,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         t.queue[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
-        t.ctr.alloc(1);
+        t.ctr.alloc(2);  // level L appends to ctr[(L + 1) & 1], the start (roots) to ctr[0]
     }
     // the traversal's state, inside its timed region: level stamps (0 = none; the occupied slots of the
     // compact vector), depths, the level-0 queue
@@ -1787,8 +1812,8 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         DeviceGuard dg(sh.device);
         St& t = st[i];
         zero_gathered(g, sh, JG_ADJ_BOTH, t.stamp.get(), sizeof(int32_t));
+        JG_HIP(hipMemsetAsync(t.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
         if (roots) {
-            JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
             if (sh.rows) {
                 sbfs_init_roots_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
                     t.dvec.get(), sh.rows, roots[i], sh.both.row_ptr.get(), t.queue[0].get(), t.qoff[0].get(),
@@ -1856,13 +1881,19 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         a.rlen = t.rlen.get();
         a.P = g.P;
         a.send_src = sh.halo_both.send_src.get();
-        a.packed = t.ctr.get();
+        a.packed = t.ctr.get() + ((level + 1) & 1);
+        a.packed_next = t.ctr.get() + (level & 1);  // read by the host after the previous level
         a.level = level;
         return a;
     };
-    auto word_grid = [](int64_t words) {  // one wave per word (per 64 words in the apply), no grid-stride cap
-        return (unsigned)std::min<int64_t>(std::max<int64_t>((words + kBlock / kWave - 1) / (kBlock / kWave), 1),
-                                           1 << 20);
+    // (blocks, P) grids over the longest run: kSbfsWords words per wave and trip (the apply: chunks of
+    // kSbfsApplyChunk), at most 2048 blocks in all (the apply, whose blocks each end with one counter
+    // atomic, 1024)
+    auto run_grid = [&](int64_t max_words, int64_t words_per_wave, int64_t cap) {
+        const int64_t per_block = (int64_t)(kBlock / kWave) * words_per_wave;
+        const int64_t x = std::min<int64_t>(std::max<int64_t>((max_words + per_block - 1) / per_block, 1),
+                                            std::max<int64_t>(cap / g.P, 1));
+        return dim3((unsigned)x, (unsigned)g.P);
     };
     while (nf > 0 && (max_depth < 0 || level < max_depth)) {
         if (!bu && (double)mf > (double)mu / alpha) bu = true;
@@ -1872,7 +1903,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             DeviceGuard dg(sh.device);
             St& t = st[i];
             if (bu && t.sw_words > 0) {  // this level's frontier bits of the send lists (before the forward exchange)
-                sbfs_pack_bits_kernel<<<word_grid(t.sw_words), kBlock, 0, sh.stream>>>(level_args(i));
+                sbfs_pack_bits_kernel<<<run_grid(t.sw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
                 JG_LAUNCH_CHECK();
             }
         }
@@ -1881,13 +1912,12 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh.device);
             St& t = st[i];
-            JG_HIP(hipMemsetAsync(t.ctr.get(), 0, sizeof(unsigned long long), sh.stream));
             const SBfsLevel a = level_args(i);
             const unsigned grid = (unsigned)std::min<int64_t>(
                 std::max<int64_t>((((sh.rows + 63) / 64) * kWave + kBlock - 1) / kBlock, 64), tune().bfs_grid);
             if (bu) {
                 sbfs_bu_kernel<<<grid, kBlock, 0, sh.stream>>>(a);
-            } else if (t.mf > 0) {
+            } else if (t.mf > 0 || (t.rw_words == 0 && t.sw_words == 0)) {  // (the last: zeroes the next counter)
                 sbfs_td_push_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                           (t.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                       kBlock, 0, sh.stream>>>(a);
@@ -1899,7 +1929,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh.device);
                 if (st[i].rw_words > 0) {
-                    sbfs_pack_marks_kernel<<<word_grid(st[i].rw_words), kBlock, 0, sh.stream>>>(level_args(i));
+                    sbfs_pack_marks_kernel<<<run_grid(st[i].rw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
                     JG_LAUNCH_CHECK();
                 }
             }
@@ -1909,7 +1939,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
                 DeviceGuard dg(sh.device);
                 St& t = st[i];
                 if (t.sw_words > 0) {
-                    sbfs_td_apply_kernel<<<word_grid((t.sw_words + kWave - 1) / kWave), kBlock, 0, sh.stream>>>(level_args(i));
+                    sbfs_td_apply_kernel<<<run_grid(t.sw_max, kSbfsApplyChunk, 1024), kBlock, 0, sh.stream>>>(level_args(i));
                     JG_LAUNCH_CHECK();
                 }
             }
@@ -1919,7 +1949,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh.device);
             unsigned long long c = 0;
-            copy_d2h(&c, st[i].ctr.get(), sizeof c, sh.stream);
+            copy_d2h(&c, st[i].ctr.get() + ((level + 1) & 1), sizeof c, sh.stream);
             st[i].nq = (int64_t)(c >> kPackShift);
             st[i].mf = (int64_t)(c & kEdgeMask);
             sums[0] += st[i].nq;
@@ -1979,6 +2009,24 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
 // compact vector (halo plan), each peer's run at the start of its segment.  Nothing reads the rest of a
 // segment (columns and exchanges address the runs only), which at RMAT-26, P = 8 is 83% of the vector's
 // 134 M positions; a dense (allgather) vector is cleared whole.
+namespace {
+// The runs of a compact vector a shard gathers into (own rows + one segment per peer), zeroed by one
+// launch: a memset per run was P + 1 fill dispatches of ~5 us each per vector (three vectors per
+// 64-source traversal).  Run starts are 16-byte aligned (rows at 0, segments 2^tbits elements apart).
+constexpr int kZeroRuns = 32;
+struct ZeroRuns {
+    char* p[kZeroRuns];
+    int64_t n[kZeroRuns];  // bytes
+};
+__global__ __launch_bounds__(kBlock) void zero_runs_kernel(ZeroRuns z) {
+    char* p = z.p[blockIdx.y];
+    const int64_t n = z.n[blockIdx.y], n16 = n >> 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = (n16 << 4) + tid; i < n; i += stride) p[i] = 0;
+}
+}  // namespace
+
 void zero_gathered(const Graph& g, const Shard& sh, uint32_t adj, void* v, size_t eb) {
     const Halo& h = g.halo(sh, adj);
     char* p = static_cast<char*>(v);
@@ -1986,12 +2034,25 @@ void zero_gathered(const Graph& g, const Shard& sh, uint32_t adj, void* v, size_
         JG_HIP(hipMemsetAsync(p, 0, (size_t)g.vec_len(sh, adj) * eb, sh.stream));
         return;
     }
-    if (sh.rows) JG_HIP(hipMemsetAsync(p, 0, (size_t)sh.rows * eb, sh.stream));
+    std::vector<std::pair<char*, int64_t>> runs;
+    if (sh.rows) runs.emplace_back(p, sh.rows * (int64_t)eb);
     for (int q = 0; q < g.P; ++q) {
         if (q == sh.index) continue;
         const int64_t nr = h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q];
-        if (nr > 0)
-            JG_HIP(hipMemsetAsync(p + ((size_t)h.seg_of(q, sh.index) << h.tbits) * eb, 0, (size_t)nr * eb, sh.stream));
+        if (nr > 0) runs.emplace_back(p + ((size_t)h.seg_of(q, sh.index) << h.tbits) * eb, nr * (int64_t)eb);
+    }
+    for (size_t r0 = 0; r0 < runs.size(); r0 += kZeroRuns) {
+        ZeroRuns z{};
+        const size_t k = std::min<size_t>(kZeroRuns, runs.size() - r0);
+        int64_t longest = 0;
+        for (size_t j = 0; j < k; ++j) {
+            z.p[j] = runs[r0 + j].first;
+            z.n[j] = runs[r0 + j].second;
+            longest = std::max(longest, z.n[j]);
+        }
+        const dim3 grid(grid_for((longest + 15) / 16, kBlock, 2048), (unsigned)k);
+        zero_runs_kernel<<<grid, kBlock, 0, sh.stream>>>(z);
+        JG_LAUNCH_CHECK();
     }
 }
 
