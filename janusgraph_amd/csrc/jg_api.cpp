@@ -737,6 +737,12 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "msbfs_bu") {
         JG_ARG(value >= 0 && value <= 3, "msbfs_bu must be 0, 1, 2 or 3");
         jg::tune().msbfs_bu = (int)value;
+    } else if (k == "msbfs_exit") {
+        JG_ARG(value >= 0 && value <= 2, "msbfs_exit must be 0, 1 or 2");
+        jg::tune().msbfs_exit = (int)value;
+    } else if (k == "msbfs_exit_live") {
+        JG_ARG(value >= 0 && value <= 1000, "msbfs_exit_live must be in [0, 1000]");
+        jg::tune().msbfs_exit_live = (int)value;
     } else if (k == "msbfs_bu_tasks") {
         JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_tasks must be in [0, 1000]");
         jg::tune().msbfs_bu_tasks = (int)value;

@@ -583,6 +583,13 @@ struct Tune {
                                       //         live: 17.84 / 17.80 vs 17.69 / 17.55 ms, profiles/r04/msbfs_bu3/;
                                       //         measured 2-4x slower than the merge-engine pull: RMAT-26 81.0 / 21.7 ms,
                                       //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
+    int msbfs_exit = 1;               //         bit-parallel BFS, one shard: the split's first band (hub rows) scanned
+                                      //         row by row with early exit instead of merged (0 never, 1 pull levels
+                                      //         where few band-0 tasks are live, 2 every pull level); the other rows
+                                      //         stay merged.  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 /
+                                      //         13.4 ms (profiles/r04/msbfs_exit/)
+    int msbfs_exit_live = 950;        //         msbfs_exit 1: permille of band 0's merge tasks live below which its rows
+                                      //         exit early (the level after the frontier's peak: 45-73%; before it: 100%)
     int msbfs_bu_frac = 100;          //         permille of the rows
     int msbfs_bu_tasks = 20;          //         msbfs_bu 3: permille of the merge tasks below which a pull level
                                       //         (after the first) runs bottom-up

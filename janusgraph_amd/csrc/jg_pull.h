@@ -795,8 +795,9 @@ __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, cons
 }
 
 template <class Op>
-__global__ void pull_slice_finalize_kernel(int64_t rows, Op op, FinalizeBands fb, const typename Op::T* __restrict__ partial) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
+__global__ void pull_slice_finalize_kernel(int64_t row0, int64_t rows, Op op, FinalizeBands fb,
+                                           const typename Op::T* __restrict__ partial) {
+    for (int64_t r = row0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
         slice_finalize_row(r, op, fb, partial);
 }
 
@@ -809,13 +810,13 @@ __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a,
                                                                      FinalizeBands fb,
                                                                      const typename Op::T* __restrict__ partial,
                                                                      int64_t split_rows, int64_t fin_blocks,
-                                                                     int fin_last) {
+                                                                     int fin_last, int64_t fin_row0) {
     // fin_last: the light-row blocks first, the finalize blocks after them (Tune::fin_last)
     const int64_t light_blocks = (int64_t)gridDim.x - fin_blocks;
     const int64_t fb0 = fin_last ? light_blocks : 0;
     const int64_t b = blockIdx.x;
     if (b >= fb0 && b < fb0 + fin_blocks) {
-        const int64_t r = (b - fb0) * kBlock + threadIdx.x;
+        const int64_t r = fin_row0 + (b - fb0) * kBlock + threadIdx.x;
         if (r < split_rows) slice_finalize_row<Op, PIPE>(r, op, fb, partial);
         return;
     }
@@ -829,12 +830,21 @@ constexpr int64_t kMaxLdsBytes = 160 * 1024;
 // `skip_empty`: the rows without entries (the degree-sorted suffix, class kZeroClass) are not
 // finalised, for programs whose value there no longer changes (PageRank after two power steps).
 // `task_live` (nullable): per band, the MergeArgs::live bitmap of its tasks.
+// `caller_rows`: the split rows [0, caller_rows) are the caller's this superstep (it gathers and
+// finalises them itself: the bit-parallel BFS's early-exit rows); it must end a prefix of the bands,
+// which are then neither merged, fixed up nor finalised here.
 template <class Op>
 void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op::T* hub_partial, hipStream_t s,
                  Ctx* prof_ctx = nullptr, Shard* prof_shard = nullptr, typename Op::T* split_partial = nullptr,
-                 bool skip_empty = false, const uint32_t* const* task_live = nullptr) {
+                 bool skip_empty = false, const uint32_t* const* task_live = nullptr, int64_t caller_rows = 0) {
     using T = typename Op::T;
     const bool split = tune().pull_split && plan.split_rows > 0 && split_partial != nullptr;
+    size_t band0 = 0;  // the first band this call merges
+    if (caller_rows > 0) {
+        while (band0 < plan.bands.size() && plan.bands[band0]->row_end <= caller_rows) ++band0;
+        if (!split || band0 == 0 || plan.bands[band0 - 1]->row_end != caller_rows)
+            fail(JG_ERR_UNSUPPORTED, "launch_pull: caller rows must end a prefix of the split bands");
+    }
     PullArgs a = make_pull_args(csr, plan, split);
     if (skip_empty) a.class_block_begin[kNumClasses] = a.class_block_begin[kZeroClass];
     const int64_t blocks = a.class_block_begin[kNumClasses];
@@ -867,7 +877,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             JG_HIP(hipEventRecord(mside->fork, s));
             JG_HIP(hipStreamWaitEvent(mside->stream, mside->fork, 0));
         }
-        for (size_t bi = 0; bi < plan.bands.size(); ++bi) {
+        for (size_t bi = band0; bi < plan.bands.size(); ++bi) {
             const SliceBand& bd = *plan.bands[bi];
             if (bd.tasks == 0) continue;
             const hipStream_t ms = (mside && bi > 0) ? mside->stream : s;
@@ -920,7 +930,8 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             JG_HIP(hipStreamWaitEvent(s, mside->join, 0));
         }
         FixupBands fx{};
-        for (const auto& bp : plan.bands) {
+        for (size_t bi = band0; bi < plan.bands.size(); ++bi) {
+            const auto& bp = plan.bands[bi];
             if (fx.n == kMaxBands) fail(JG_ERR_UNSUPPORTED, "too many split bands");
             fx.meta[fx.n] = bp->meta.get();
             fx.part_off[fx.n] = bp->part_off;
@@ -975,17 +986,17 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                                             (size_t)hot * sizeof(T), s>>>(a, op, hot);
         JG_LAUNCH_CHECK();
     } else if (fuse) {
-        const int64_t fin_blocks = (plan.split_rows + kBlock - 1) / kBlock;
+        const int64_t fin_blocks = (plan.split_rows - caller_rows + kBlock - 1) / kBlock;
         const unsigned grid = (unsigned)(fin_blocks + blocks);
         if (tune().pull_unroll >= 8)
             pull_light_finalize_kernel<Op, 8, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                            plan.split_rows, fin_blocks, tune().fin_last);
+                                                                            plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
         else if (tune().fin_pipe)
             pull_light_finalize_kernel<Op, 4, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                                  plan.split_rows, fin_blocks, tune().fin_last);
+                                                                                  plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
         else
             pull_light_finalize_kernel<Op, 4, false, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                                   plan.split_rows, fin_blocks, tune().fin_last);
+                                                                                   plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
         JG_LAUNCH_CHECK();
     } else if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
         const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
@@ -1016,7 +1027,9 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
         JG_LAUNCH_CHECK();
     }
     if (split && !fuse) {
-        pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows), kBlock, 0, s>>>(plan.split_rows, op, fb, split_partial);
+        if (plan.split_rows > caller_rows)
+            pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows - caller_rows), kBlock, 0, s>>>(
+                caller_rows, plan.split_rows, op, fb, split_partial);
         JG_LAUNCH_CHECK();
     }
     if (side) {

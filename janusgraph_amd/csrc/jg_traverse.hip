@@ -720,11 +720,14 @@ __device__ __forceinline__ unsigned long long wave_or(unsigned long long m) {
     return m;
 }
 
+// The entries scanned are summed per workgroup, one atomic each at the end (a lane-0 atomic per row, as
+// round 3 had it, queued up to a million of them on one counter).
 __global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp op) {
     __shared__ unsigned long long red[kMergeWaves];
     __shared__ int stop;
     const unsigned long long live = *op.live;
     const int lane = lane_id(), wv = threadIdx.x / kWave;
+    unsigned long long scanned = 0;
     if ((int64_t)blockIdx.x < a.blocks_hub) {  // hub rows: a workgroup each
         for (int64_t v = blockIdx.x; v < a.hub; v += a.blocks_hub) {
             const unsigned long long need = ~op.visited[v] & live;  // block-uniform
@@ -754,16 +757,13 @@ __global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp
                     acc = red[0];
                     const int done = stop;
                     __syncthreads();  // red / stop are rewritten by the next step
-                    if (threadIdx.x == 0)
-                        atomicAdd(a.examined, (unsigned long long)min((int64_t)kMsBuUnroll * kMergeThreads, e1 - j));
+                    if (threadIdx.x == 0) scanned += (unsigned long long)min((int64_t)kMsBuUnroll * kMergeThreads, e1 - j);
                     if (done) break;
                 }
             }
             if (threadIdx.x == 0) op.finalize(v, acc);
         }
-        return;
-    }
-    if ((int64_t)blockIdx.x < a.blocks_wave) {  // rows of 64 .. hub entries: a wave each
+    } else if ((int64_t)blockIdx.x < a.blocks_wave) {  // rows of 64 .. hub entries: a wave each
         const int64_t nw = (a.blocks_wave - a.blocks_hub) * kMergeWaves;
         for (int64_t v = a.hub + ((int64_t)blockIdx.x - a.blocks_hub) * kMergeWaves + wv; v < a.wave; v += nw) {
             const unsigned long long need = ~op.visited[v] & live;  // wave-uniform
@@ -783,36 +783,117 @@ __global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp
                     for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
                     acc |= wave_or(m & need);
                 }
-                if (lane == 0) atomicAdd(a.examined, (unsigned long long)(min(j, e1) - e0));
+                if (lane == 0) scanned += (unsigned long long)(min(j, e1) - e0);
             }
             if (lane == 0) op.finalize(v, acc);
         }
-        return;
-    }
-    // light rows: a lane each; rows past ne have no entries
-    const int64_t nt = ((int64_t)gridDim.x - a.blocks_wave) * kMergeThreads;
-    unsigned long long scanned = 0;
-    for (int64_t v = a.wave + ((int64_t)blockIdx.x - a.blocks_wave) * kMergeThreads + threadIdx.x; v < a.rows; v += nt) {
-        unsigned long long acc = 0;
-        if (v < a.ne) {
-            const unsigned long long need = ~op.visited[v] & live;
-            if (need) {
-                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
-                int64_t j = e0;
-                for (; j < e1 && acc != need; j += kMsBuUnroll) {
-                    int32_t c[kMsBuUnroll];
+    } else {  // light rows: a lane each; rows past ne have no entries
+        const int64_t nt = ((int64_t)gridDim.x - a.blocks_wave) * kMergeThreads;
+        for (int64_t v = a.wave + ((int64_t)blockIdx.x - a.blocks_wave) * kMergeThreads + threadIdx.x; v < a.rows;
+             v += nt) {
+            unsigned long long acc = 0;
+            if (v < a.ne) {
+                const unsigned long long need = ~op.visited[v] & live;
+                if (need) {
+                    const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
+                    int64_t j = e0;
+                    for (; j < e1 && acc != need; j += kMsBuUnroll) {
+                        int32_t c[kMsBuUnroll];
 #pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) c[u] = a.col[j + u < e1 ? j + u : e1 - 1];
+                        for (int u = 0; u < kMsBuUnroll; ++u) c[u] = a.col[j + u < e1 ? j + u : e1 - 1];
 #pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) acc |= op.F[c[u]] & need;
+                        for (int u = 0; u < kMsBuUnroll; ++u) acc |= op.F[c[u]] & need;
+                    }
+                    scanned += (unsigned long long)(min(j, e1) - e0);
                 }
-                scanned += (unsigned long long)(min(j, e1) - e0);
+            }
+            op.finalize(v, acc);
+        }
+    }
+    scanned = block_reduce(scanned, AddU64{}, red);  // every role is block-uniform
+    if (threadIdx.x == 0 && scanned) atomicAdd(a.examined, scanned);
+}
+
+// ---- the split's first band with early exit, inside a merged pull level (msbfs_exit) ----
+// On the level after the frontier's peak a hub row typically finds every unvisited live bit within its
+// first two or three entries (RMAT-22: 2.4 on average; tools/msbfs_exit_sim.py), so a 256-entry wave
+// step (msbfs_bu_kernel's wave role) gathers ~100x what the row needs.  Pass A gives each row a lane
+// and its first kExitFirst entries; a row still missing bits leaves its partial word in Fout and a bit
+// in `rest` (one word per 64 rows, a plain store per wave), and pass B scans the remaining entries of
+// those rows a wave each.  Entries scanned are summed per 1024-thread workgroup, one atomic each.
+constexpr int kExitFirst = 8;
+
+__global__ __launch_bounds__(kRedThreads) void msbfs_exit_first_kernel(MsBu a, MsBfsOp op,
+                                                                        unsigned long long* __restrict__ rest) {
+    __shared__ unsigned long long red[kRedWaves];
+    const unsigned long long live = *op.live;
+    const int64_t words = (a.rows + 63) / 64, nwaves = (int64_t)gridDim.x * kRedWaves;
+    unsigned long long scanned = 0;
+    for (int64_t w = (int64_t)blockIdx.x * kRedWaves + wave_id(); w < words; w += nwaves) {  // wave-uniform
+        const int64_t v = w * 64 + lane_id();
+        bool more = false;
+        if (v < a.rows) {
+            const unsigned long long need = ~op.visited[v] & live;
+            unsigned long long acc = 0;
+            if (need) {
+                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1], ek = e1 < e0 + kExitFirst ? e1 : e0 + kExitFirst;
+                int64_t j = e0;
+                for (; j < ek && acc != need; j += 4) {
+                    int32_t c[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) c[u] = a.col[j + u < ek ? j + u : ek - 1];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc |= op.F[c[u]] & need;
+                }
+                scanned += (unsigned long long)((j < ek ? j : ek) - e0);
+                more = acc != need && ek < e1;
+            }
+            if (more) op.Fout[op.pos(v)] = acc;  // pass B's starting word
+            else op.finalize(v, acc);
+        }
+        const uint64_t word = __ballot(more);
+        if (lane_id() == 0) rest[w] = word;
+    }
+    scanned = block_reduce(scanned, AddU64{}, red);
+    if (threadIdx.x == 0 && scanned) atomicAdd(a.examined, scanned);
+}
+
+__global__ __launch_bounds__(kRedThreads) void msbfs_exit_rest_kernel(MsBu a, MsBfsOp op,
+                                                                       const unsigned long long* __restrict__ rest) {
+    __shared__ unsigned long long red[kRedWaves];
+    const unsigned long long live = *op.live;
+    const int lane = lane_id();
+    const int64_t words = (a.rows + 63) / 64, nwaves = (int64_t)gridDim.x * kRedWaves;
+    unsigned long long scanned = 0;
+    for (int64_t w = (int64_t)blockIdx.x * kRedWaves + wave_id(); w < words; w += nwaves) {  // wave-uniform
+        uint64_t bits = rest[w];
+        while (bits) {
+            const int64_t v = w * 64 + (__ffsll((unsigned long long)bits) - 1);
+            bits &= bits - 1;
+            const unsigned long long need = ~op.visited[v] & live;
+            unsigned long long acc = op.Fout[op.pos(v)];
+            const int64_t e0 = a.rp[v] + kExitFirst, e1 = a.rp[v + 1];
+            int64_t j = e0;
+            for (; j < e1 && acc != need; j += kMsBuUnroll * kWave) {
+                int32_t c[kMsBuUnroll];
+#pragma unroll
+                for (int u = 0; u < kMsBuUnroll; ++u) {
+                    const int64_t e = j + u * kWave + lane;
+                    c[u] = e < e1 ? a.col[e] : -1;
+                }
+                unsigned long long m = 0;
+#pragma unroll
+                for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
+                acc |= wave_or(m & need);
+            }
+            if (lane == 0) {
+                scanned += (unsigned long long)((j < e1 ? j : e1) - e0);
+                op.finalize(v, acc);
             }
         }
-        op.finalize(v, acc);
     }
-    scanned = wave_reduce_add(scanned);
-    if (lane == 0 && scanned) atomicAdd(a.examined, scanned);
+    scanned = block_reduce(scanned, AddU64{}, red);
+    if (threadIdx.x == 0 && scanned) atomicAdd(a.examined, scanned);
 }
 
 // the first row whose degree is below d (rows are degree-sorted, descending)
@@ -2164,6 +2245,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> nwl;   // [kMsLevelWords][rows] new-bit words of levels 0 .. kMsLevelWords-1
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
+                DevBuf<unsigned long long> xrest;  // msbfs_exit: the band-0 rows pass B scans (a bit per row)
+                MsBu bx{};                         // msbfs_exit: band 0's rows (bx.rows 0: off on this shard)
+                int64_t exit_tasks = 0;            // band 0's merge tasks
+                int exit_unskipped = 0, exit_levels = 0;  // levels that ran the exit rows (with every task counted)
+                unsigned long long b0_live_merged = 0;     // msbfs_exit 1: band 0's live tasks of levels that merged it
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
                 DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
                 // levels recorded as (row, new word) records instead of nwl words (level 0 from the sources and
@@ -2176,7 +2262,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 };
                 std::vector<Rec> recs;
                 DevBuf<unsigned long long> work;  // [0] live merge tasks over all pull levels, [1] reached pairs,
-                                                  // [2] entries the early-exit bottom-up levels scanned
+                                                  // [2] entries the early-exit bottom-up levels scanned,
+                                                  // [3] band 0's live tasks of this level (msbfs_exit 1)
                 int64_t light_nnz = 0, all_tasks = 0;  // entries outside the split, merge tasks of all bands
             };
             std::vector<St> st(g.shards.size());
@@ -2231,8 +2318,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
                 t.live.alloc(2);
-                t.work.alloc(3);
-                JG_HIP(hipMemsetAsync(t.work.get(), 0, 3 * sizeof(unsigned long long), sh.stream));
+                t.work.alloc(4);
+                JG_HIP(hipMemsetAsync(t.work.get(), 0, 4 * sizeof(unsigned long long), sh.stream));
+                if (tune().msbfs_exit > 0 && t.split.size() && !plan.bands.empty())
+                    t.xrest.alloc(std::max<int64_t>((plan.bands[0]->row_end + 63) / 64, 1));
                 t.light_nnz = c.pull->nnz;
                 if (t.split.size() && plan.split_rows > 0) {
                     int64_t split_nnz = 0;
@@ -2481,6 +2570,27 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 bu.examined = st[0].work.get() + 2;
             }
             const int64_t bu_rows = bu_ok ? sh0.rows * (int64_t)tune().msbfs_bu_frac / 1000 : 0;
+            // msbfs_exit: the split's first band (rows of >= band0_deg entries, hubs first) scans its rows with
+            // early exit (msbfs_exit_first_kernel / msbfs_exit_rest_kernel) on pull levels where few of its
+            // merge tasks are live; every other row stays with the merge engine (launch_pull's caller_rows).
+            // On the level after the frontier's peak a hub row finds all its unvisited live bits within its
+            // first entries: RMAT-22, band 0 examines 0.1% instead of 27.3% of the entries
+            // (tools/msbfs_exit_sim.py).  Each shard decides for its own rows.
+            for (size_t i = 0; i < g.shards.size(); ++i) {
+                Shard& sh = *g.shards[i];
+                const BfsCsrs c = pick_csrs(sh, direction);
+                const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
+                St& t = st[i];
+                if (tune().msbfs_exit > 0 && tune().msbfs_bu == 0 && tune().pull_split && plan.split_rows > 0 &&
+                    !plan.bands.empty() && t.xrest.size() > 0 && plan.bands[0]->row_begin == 0 &&
+                    plan.bands[0]->row_end > 0) {
+                    t.bx.rp = c.pull->row_ptr.get();
+                    t.bx.col = c.pull->col.get();
+                    t.bx.rows = t.bx.wave = t.bx.ne = plan.bands[0]->row_end;  // (the exit kernels use rp, col, rows, examined)
+                    t.bx.examined = t.work.get() + 2;
+                    t.exit_tasks = plan.bands[0]->tasks;
+                }
+            }
             int bu_levels = 0;
             unsigned long long bu_task_credit = 0;  // live tasks counted by levels that then ran bottom-up
             bool queued = td_ok, live_ready = false;
@@ -2753,6 +2863,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // bottom-up kernel visits those rows' entries only, instead of the merge engine's
                         // per-round LDS images over every sub-slice
                         const bool no_bitmaps = tune().msbfs_skip_first && pull_levels == 0;
+                        // msbfs_exit 1: band 0's rows exit early on pull levels where fewer than msbfs_exit_live
+                        // permille of its merge tasks hold a row that can still gain a bit (their live count
+                        // is read back once); 2: on every pull level
+                        const MsBu& bx = t.bx;
+                        int64_t exit_rows = bx.rows > 0 && tune().msbfs_exit == 2 ? bx.rows : 0;
+                        const bool exit_probe = bx.rows > 0 && tune().msbfs_exit == 1 && !no_bitmaps && !t.todo.empty();
                         std::vector<const uint32_t*> tl;
                         bool sparse = false;
                         if (!(bu_ok && (tune().msbfs_bu == 1 || (tune().msbfs_bu == 2 && g_nq >= bu_rows)))) {
@@ -2761,16 +2877,33 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 copy_d2h(&before, t.work.get(), sizeof before, sh.stream);
                             for (size_t b = 0; b < t.todo.size() && !no_bitmaps; ++b) {
                                 const SliceBand& bd = *plan.bands[b];
-                                if (bd.tasks == 0 || bd.rows() == 0) {
+                                if (bd.tasks == 0 || bd.rows() == 0 || bd.row_end <= exit_rows) {  // (exit rows: no merge)
                                     tl.push_back(nullptr);
                                     continue;
                                 }
                                 msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
                                     t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                                 JG_LAUNCH_CHECK();
+                                const bool probe = exit_probe && b == 0 && bd.row_end == bx.rows;
+                                if (probe) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
                                 msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
-                                    bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(), t.work.get());
+                                    bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(),
+                                    t.work.get() + (probe ? 3 : 0));
                                 JG_LAUNCH_CHECK();
+                                if (probe) {
+                                    unsigned long long b0live = 0;
+                                    copy_d2h(&b0live, t.work.get() + 3, sizeof b0live, sh.stream);
+                                    const bool go = (double)b0live * 1000.0 < (double)bd.tasks * (double)tune().msbfs_exit_live;
+                                    if (debug_bfs())
+                                        std::fprintf(stderr, "[jg msbfs] level %d band 0: %llu of %lld merge tasks live -> %s\n",
+                                                     level, b0live, (long long)bd.tasks, go ? "early exit" : "merge");
+                                    if (go) {
+                                        exit_rows = bx.rows;
+                                        tl.push_back(nullptr);
+                                        continue;
+                                    }
+                                    t.b0_live_merged += b0live;  // (work[0] holds the other bands' live tasks)
+                                }
                                 tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
                             }
                             if (bu_ok && tune().msbfs_bu == 3 && !no_bitmaps && !t.todo.empty()) {
@@ -2795,9 +2928,25 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows
                         // can be done there; every task runs, the finalize's live mask keeps it exact)
                         if (no_bitmaps && i == 0) ++unskipped_levels;
+                        if (no_bitmaps && exit_rows) ++t.exit_unskipped;
+                        if (exit_rows) {
+                            ++t.exit_levels;
+                            unsigned long long before = 0, after = 0;
+                            if (debug_bfs()) copy_d2h(&before, bx.examined, sizeof before, sh.stream);
+                            const unsigned xg = red_grid((bx.rows + 63) / 64 * kWave);
+                            msbfs_exit_first_kernel<<<xg, kRedThreads, 0, sh.stream>>>(bx, op, t.xrest.get());
+                            JG_LAUNCH_CHECK();
+                            msbfs_exit_rest_kernel<<<xg, kRedThreads, 0, sh.stream>>>(bx, op, t.xrest.get());
+                            JG_LAUNCH_CHECK();
+                            if (debug_bfs()) {
+                                copy_d2h(&after, bx.examined, sizeof after, sh.stream);
+                                std::fprintf(stderr, "[jg msbfs] level %d exit rows [0, %lld): %llu entries examined\n",
+                                             level, (long long)bx.rows, after - before);
+                            }
+                        }
                         launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                     t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
-                                    tl.empty() ? nullptr : tl.data());
+                                    tl.empty() ? nullptr : tl.data(), exit_rows);
                         }
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
@@ -2857,9 +3006,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
-                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels
+                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels - (double)t.exit_tasks * t.exit_levels
                                                           : (double)(w[0] - (i == 0 ? bu_task_credit : 0ull)) +
-                                                                (double)t.all_tasks * unskipped_levels;
+                                                                (double)t.b0_live_merged +
+                                                                (double)t.all_tasks * unskipped_levels -
+                                                                (double)t.exit_tasks * t.exit_unskipped;
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
                 work_entries += entries;
                 work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +

@@ -224,7 +224,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
                                          ("skip_dense_reverse", 3), ("skip_dense", 2), ("skip_every_level", 1),
                                          ("skip_every_level", 3), ("bu_sparse_levels", 1), ("bu_sparse_always", 1),
-                                         ("bu_every_level", 1)])
+                                         ("bu_every_level", 1), ("exit_off", 1), ("exit_every_bitmapped_level", 1),
+                                         ("exit_every_level", 1), ("exit_no_skip", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -248,7 +249,12 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              # bottom-up pull levels (msbfs_bu; 0, the merge engine, by default): sparse levels only, every
              # bitmapped level, every pull level
              "bu_sparse_levels": [("msbfs_bu", 3)], "bu_sparse_always": [("msbfs_bu", 3), ("msbfs_bu_tasks", 1000)],
-             "bu_every_level": [("msbfs_bu", 1)]}[mode]
+             "bu_every_level": [("msbfs_bu", 1)],
+             # the split's first band through the early-exit rows (msbfs_exit: 1, the default, on levels where
+             # few of its tasks are live), the rest merged
+             "exit_off": [("msbfs_exit", 0)], "exit_every_bitmapped_level": [("msbfs_exit_live", 1000)],
+             "exit_every_level": [("msbfs_exit", 2)],
+             "exit_no_skip": [("msbfs_exit", 2), ("msbfs_skip", 0)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
     vid = np.concatenate([vid0, (np.arange(3, dtype=np.int64) + n0 + 1) << 8 | 7])
@@ -275,6 +281,8 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_td", 1)
         _lib.tune_set("msbfs_sparse", 1)
         _lib.tune_set("msbfs_bu", 0)
+        _lib.tune_set("msbfs_exit", 1)
+        _lib.tune_set("msbfs_exit_live", 950)
         _lib.tune_set("msbfs_bu_tasks", 20)
         _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)

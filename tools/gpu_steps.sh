@@ -9,7 +9,7 @@
 #   tests <pytest args>  a subset of it
 #   smoke                __graft_entry__.smoke()
 #   bench <args>         bench.py; the JSON line goes to <name>.json as well
-#   trace <workload>     rocprofv3 --kernel-trace --stats of tools/workload.py <workload> (no counters),
+#   trace <workload> [workload.py args]  rocprofv3 --kernel-trace --stats of tools/workload.py <workload> (no counters),
 #                        summarised by tools/trace_summary.py into gpurun_out/<tag>/<name>/summary.json
 #   pmc <workload>       the PMC passes of tools/pmc_workloads.sh for one workload
 # Anything else runs as written (bash -c).
@@ -29,7 +29,8 @@ for step in "$@"; do
         tests) shift; cmd="python -u -m pytest -x -v --timeout 600 --timeout-method thread $*" ;;
         smoke) cmd="python -c 'import __graft_entry__ as g; g.smoke()'" ;;
         bench) shift; cmd="python bench.py $* | tee $OUT/$name.json" ;;
-        trace) shift; cmd="rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o $1 -- python3 tools/workload.py $1 && python3 tools/trace_summary.py $OUT/$name $1" ;;
+        trace) shift; w=$1; shift
+               cmd="rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o $w -- python3 tools/workload.py $w $* && python3 tools/trace_summary.py $OUT/$name $w" ;;
         pmc) shift; cmd="bash tools/pmc_workloads.sh $TAG/$name $1" ;;
     esac
     echo "[$(date +%T)] $name ($secs s): $cmd"

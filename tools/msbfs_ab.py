@@ -2,6 +2,7 @@
 timing only (parity: tests/test_gpu_configs.py, tests/test_gpu_parity.py).  One line per setting:
 median HIP-event ms over `reps` runs after one warm run, levels, entries examined.
     python tools/msbfs_ab.py --scale 26 msbfs_bu 0 1 2
+    python tools/msbfs_ab.py --scale 26 --tune msbfs_exit=1 msbfs_exit_live 0 700 1000
 """
 import argparse
 import json
@@ -18,11 +19,15 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--tune", action="append", default=[], help="a fixed jg_tune_set knob (key=value; repeatable)")
     p.add_argument("key")
     p.add_argument("values", type=int, nargs="+")
     a = p.parse_args()
     import bench
     import janusgraph_amd as jg
+    for kv in a.tune:
+        k, _, v = kv.partition("=")
+        jg._lib.tune_set(k, int(v))
     ctx = jg.Context((0,))
     g = ctx.build_rmat(a.scale, 16, 0x5EED + a.scale, flags=jg.ADJ_BOTH)
     srcs = bench.pick_sources(g.degrees(jg.DIR_BOTH), 64, 7)

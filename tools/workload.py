@@ -4,7 +4,7 @@ time and the library's algorithmic bytes of every run.  tools/pmc_workloads.sh p
 tools/pmc_summary.py turns the counters into bytes per run (profiles/<round>/<workload>/summary.json),
 which bench.py reads for the block's roofline "traffic".
 
-  python tools/workload.py bfs20|bfs26|cc26|msbfs26|pr24|pr26 [--runs R]
+  python tools/workload.py bfs20|bfs26|cc26|msbfs26|pr24|pr26 [--runs R] [--tune key=value ...]
 """
 import argparse
 import json
@@ -34,13 +34,17 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("workload", choices=["bfs20", "bfs26", "cc26", "msbfs26", "pr24", "pr26"])
     p.add_argument("--runs", type=int, default=5)
+    p.add_argument("--tune", action="append", default=[], help="a jg_tune_set knob (key=value; repeatable) applied before the build")
     a = p.parse_args()
     import janusgraph_amd as jg
+    for kv in a.tune:
+        k, _, v = kv.partition("=")
+        jg._lib.tune_set(k, int(v))
     ctx = jg.Context((0,))
     kind, scale = a.workload.rstrip("0123456789"), int(a.workload[-2:])
     ef = 16
     n, m = 1 << scale, ef << scale
-    out = {"workload": a.workload, "runs": a.runs, "warm_runs": 1, "kernels": KERNELS[kind], "ms": [], "bytes": []}
+    out = {"workload": a.workload, "tune": a.tune, "runs": a.runs, "warm_runs": 1, "kernels": KERNELS[kind], "ms": [], "bytes": []}
     if kind == "pr":
         g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_IN)
         g.pagerank_begin(0.85, n)
