@@ -740,6 +740,11 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "msbfs_exit") {
         JG_ARG(value >= 0 && value <= 2, "msbfs_exit must be 0, 1 or 2");
         jg::tune().msbfs_exit = (int)value;
+    } else if (k == "msbfs_exit_bands") {
+        JG_ARG(value >= 1 && value <= 4, "msbfs_exit_bands must be in [1, 4]");
+        jg::tune().msbfs_exit_bands = (int)value;
+    } else if (k == "msbfs_exit_all") {
+        jg::tune().msbfs_exit_all = value != 0;
     } else if (k == "msbfs_exit_live") {
         JG_ARG(value >= 0 && value <= 1000, "msbfs_exit_live must be in [0, 1000]");
         jg::tune().msbfs_exit_live = (int)value;

@@ -588,6 +588,10 @@ struct Tune {
                                       //         where few band-0 tasks are live, 2 every pull level); the other rows
                                       //         stay merged.  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 /
                                       //         13.4 ms (profiles/r04/msbfs_exit/)
+    int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
+                                      //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
+                                      //         1.47 / 3.48 / 12.46 ms)
+    int msbfs_exit_all = 0;           //         msbfs_exit: every row (the light rows too) takes the early exit
     int msbfs_exit_live = 950;        //         msbfs_exit 1: permille of band 0's merge tasks live below which its rows
                                       //         exit early (the level after the frontier's peak: 45-73%; before it: 100%)
     int msbfs_bu_frac = 100;          //         permille of the rows

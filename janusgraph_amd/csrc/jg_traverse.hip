@@ -2247,7 +2247,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 DevBuf<unsigned long long> xrest;  // msbfs_exit: the band-0 rows pass B scans (a bit per row)
                 MsBu bx{};                         // msbfs_exit: band 0's rows (bx.rows 0: off on this shard)
-                int64_t exit_tasks = 0;            // band 0's merge tasks
+                int64_t exit_tasks = 0;            // the exit bands' merge tasks
+                size_t exit_nbands = 0;
+                bool exit_all = false;  // msbfs_exit_all: the exit rows are every row
+                int exit_all_levels = 0;
                 int exit_unskipped = 0, exit_levels = 0;  // levels that ran the exit rows (with every task counted)
                 unsigned long long b0_live_merged = 0;     // msbfs_exit 1: band 0's live tasks of levels that merged it
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
@@ -2321,7 +2324,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.work.alloc(4);
                 JG_HIP(hipMemsetAsync(t.work.get(), 0, 4 * sizeof(unsigned long long), sh.stream));
                 if (tune().msbfs_exit > 0 && t.split.size() && !plan.bands.empty())
-                    t.xrest.alloc(std::max<int64_t>((plan.bands[0]->row_end + 63) / 64, 1));
+                    t.xrest.alloc(std::max<int64_t>(
+                        ((tune().msbfs_exit_all ? sh.rows
+                                                : plan.bands[std::min<size_t>(plan.bands.size(), (size_t)tune().msbfs_exit_bands) - 1]->row_end) +
+                         63) / 64, 1));
                 t.light_nnz = c.pull->nnz;
                 if (t.split.size() && plan.split_rows > 0) {
                     int64_t split_nnz = 0;
@@ -2586,9 +2592,15 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     plan.bands[0]->row_end > 0) {
                     t.bx.rp = c.pull->row_ptr.get();
                     t.bx.col = c.pull->col.get();
-                    t.bx.rows = t.bx.wave = t.bx.ne = plan.bands[0]->row_end;  // (the exit kernels use rp, col, rows, examined)
+                    // the first msbfs_exit_bands bands (their rows: a prefix of the split)
+                    // (msbfs_exit_all: every row; the level then runs no merge engine and no light kernel)
+                    const size_t k = tune().msbfs_exit_all ? plan.bands.size()
+                                                           : std::min<size_t>(plan.bands.size(), (size_t)tune().msbfs_exit_bands);
+                    t.exit_all = tune().msbfs_exit_all != 0;
+                    t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? sh.rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
                     t.bx.examined = t.work.get() + 2;
-                    t.exit_tasks = plan.bands[0]->tasks;
+                    t.exit_nbands = k;
+                    for (size_t b = 0; b < k; ++b) t.exit_tasks += plan.bands[b]->tasks;
                 }
             }
             int bu_levels = 0;
@@ -2884,25 +2896,27 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
                                     t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                                 JG_LAUNCH_CHECK();
-                                const bool probe = exit_probe && b == 0 && bd.row_end == bx.rows;
-                                if (probe) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
+                                // the exit bands count their live tasks apart (work[3]); after the last of them the
+                                // count decides (launch_pull then skips those bands, whatever their bitmaps say)
+                                const bool probe = exit_probe && b < t.exit_nbands;
+                                if (probe && b == 0) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
                                 msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
                                     bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(),
                                     t.work.get() + (probe ? 3 : 0));
                                 JG_LAUNCH_CHECK();
-                                if (probe) {
-                                    unsigned long long b0live = 0;
-                                    copy_d2h(&b0live, t.work.get() + 3, sizeof b0live, sh.stream);
-                                    const bool go = (double)b0live * 1000.0 < (double)bd.tasks * (double)tune().msbfs_exit_live;
+                                if (probe && b + 1 == t.exit_nbands) {
+                                    unsigned long long xlive = 0;
+                                    copy_d2h(&xlive, t.work.get() + 3, sizeof xlive, sh.stream);
+                                    const bool go = (double)xlive * 1000.0 < (double)t.exit_tasks * (double)tune().msbfs_exit_live;
                                     if (debug_bfs())
-                                        std::fprintf(stderr, "[jg msbfs] level %d band 0: %llu of %lld merge tasks live -> %s\n",
-                                                     level, b0live, (long long)bd.tasks, go ? "early exit" : "merge");
+                                        std::fprintf(stderr, "[jg msbfs] level %d bands 0..%zu: %llu of %lld merge tasks live -> %s\n",
+                                                     level, b, xlive, (long long)t.exit_tasks, go ? "early exit" : "merge");
                                     if (go) {
                                         exit_rows = bx.rows;
                                         tl.push_back(nullptr);
                                         continue;
                                     }
-                                    t.b0_live_merged += b0live;  // (work[0] holds the other bands' live tasks)
+                                    t.b0_live_merged += xlive;  // (work[0] holds the other bands' live tasks)
                                 }
                                 tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
                             }
@@ -2944,9 +2958,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                              level, (long long)bx.rows, after - before);
                             }
                         }
-                        launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                    t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
-                                    tl.empty() ? nullptr : tl.data(), exit_rows);
+                        if (exit_rows && t.exit_all) {
+                            ++t.exit_all_levels;  // every row went through the exit kernels
+                        } else {
+                            launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
+                                        t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
+                                        tl.empty() ? nullptr : tl.data(), exit_rows);
+                        }
                         }
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
@@ -3011,7 +3029,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                                                 (double)t.b0_live_merged +
                                                                 (double)t.all_tasks * unskipped_levels -
                                                                 (double)t.exit_tasks * t.exit_unskipped;
-                const double entries = live_tasks * kMergeTask + (double)t.light_nnz * pull_levels + (double)w[2];
+                const double entries = live_tasks * kMergeTask + (double)t.light_nnz * (pull_levels - t.exit_all_levels) + (double)w[2];
                 work_entries += entries;
                 work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +
                               (level >= kMsLevelWords ? 4.0 * (double)w[1] : 0.0);
