@@ -25,7 +25,8 @@ KERNELS = {
            "uf_minrank_kernel", "heavy_rows_kernel", "bfs_init_roots_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
     "msbfs": ["MsBfsOp", "msbfs_live_kernel", "msbfs_scan_kernel", "msbfs_todo_kernel", "msbfs_task_live_kernel",
               "msbfs_init_kernel", "msbfs_frontier_kernel", "msbfs_source_queue_kernel", "msbfs_td_kernel",
-              "msbfs_td_apply_kernel", "msbfs_zero_list_kernel", "msbfs_td_recv_kernel", "msbfs_td_record_kernel"],
+              "msbfs_td_apply_kernel", "msbfs_zero_list_kernel", "msbfs_td_recv_kernel", "msbfs_td_record_kernel",
+              "msbfs_exit_first_kernel", "msbfs_exit_rest_kernel", "zero_words_kernel"],
     "pr": ["PrOp"],
 }
 
