@@ -196,6 +196,56 @@ def test_multi_source_bfs_past_255_levels(oracle_lib, shards):
     c.close()
 
 
+@pytest.mark.parametrize("shards,exit_mode", [(1, 1), (1, 2), (3, 1), (3, 2)])
+def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode):
+    """The 64-source BFS's early-exit rows (msbfs_exit; the split's hub bands scanned row by row) on a
+    graph made for it: four hubs of 300-900 leaves joined in a ring, leaves cross-linked to each other's
+    hubs, a 150-vertex tail hanging off one leaf, a small separate component and an isolated vertex.  Hub
+    rows then need every live source at once while some sources sit at the end of the tail, so some
+    levels exit and others must scan whole rows.  All 64 depth rows against the oracle, unbounded and
+    bounded, with the adaptive rule (1) and the exit forced on every pull level (2), on 1 and 3 shards."""
+    import janusgraph_amd as jg
+    from janusgraph_amd import _lib
+    rng = np.random.default_rng(5)
+    src, dst = [], []
+    hubs = [0, 1, 2, 3]
+    nxt = 4
+    leaves = []
+    for h, k in zip(hubs, (300, 500, 700, 900)):
+        for _ in range(k):
+            src.append(h); dst.append(nxt); leaves.append(nxt); nxt += 1
+    for a, b in zip(hubs, hubs[1:] + hubs[:1]):
+        src.append(a); dst.append(b)
+    leaves = np.array(leaves)
+    for _ in range(2000):  # leaves linked to other hubs and to each other
+        a, b = rng.choice(leaves, 2)
+        src.append(int(a)); dst.append(int(rng.choice(hubs)) if rng.random() < 0.5 else int(b))
+    prev = int(leaves[7])
+    for _ in range(150):  # the tail
+        src.append(prev); dst.append(nxt); prev = nxt; nxt += 1
+    tail_end = prev
+    for a, b in ((nxt, nxt + 1), (nxt + 1, nxt + 2)):  # a small component
+        src.append(a); dst.append(b)
+    small = nxt
+    n = nxt + 4  # + an isolated vertex
+    s, t = np.array(src, np.int32), np.array(dst, np.int32)
+    vid = (np.arange(n, dtype=np.int64) + 1) << 8
+    try:
+        _lib.tune_set("msbfs_exit", exit_mode)
+        c = jg.Context((0,) * shards)
+        g = c.build(vid, vid[s], vid[t], flags=jg.ADJ_BOTH)
+        srcs = np.concatenate([[0, 3, tail_end, small, n - 1], rng.choice(leaves, 59, replace=False)])
+        for max_depth in (-1, 3):
+            got = g.bfs(vid[srcs], jg.DIR_BOTH, max_depth=max_depth)
+            for k, sv in enumerate(srcs):
+                np.testing.assert_array_equal(got[k], oracle_lib.bfs(n, s, t, int(sv), oracle_lib.DIR_BOTH, max_depth),
+                                              err_msg=f"shards {shards} exit {exit_mode} max_depth {max_depth} source {sv}")
+        g.close()
+        c.close()
+    finally:
+        _lib.tune_set("msbfs_exit", 1)
+
+
 def test_vertex_id_remap_arbitrary_ids(ctx, oracle_lib, rmat12):
     """The device id table (jg_build.hip remap_ids_device): arbitrary int64 ids (negative, huge, clustered
     in a few high-bit groups like JanusGraph's partitioned ids), ghost endpoints among them, a duplicate
