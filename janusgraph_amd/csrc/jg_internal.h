@@ -588,6 +588,13 @@ struct Tune {
                                       //         where few band-0 tasks are live, 2 every pull level); the other rows
                                       //         stay merged.  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 /
                                       //         13.4 ms (profiles/r04/msbfs_exit/)
+    int msbfs_srcsplit = 0;           //         bit-parallel BFS, one shard: the first pull level's small-frontier sources
+                                      //         go top-down (0 never, 1 the first pull level, 2 every pull level).
+                                      //         Measured slower: RMAT-24 3.50 -> 4.16 ms (the small sources' push,
+                                      //         34.7 M entries, 0.7 ms + 0.33 ms apply; band 0 still scanned 17.8 M
+                                      //         entries), RMAT-26 12.44 -> 12.60 (the split did not apply: 10 small
+                                      //         sources held 7.4% of the entries), profiles/r04/msbfs_srcsplit/
+    int msbfs_srcsplit_permille = 20; //         msbfs_srcsplit: a source is small below this permille of the push entries
     int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
                                       //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
                                       //         1.47 / 3.48 / 12.46 ms)

@@ -667,17 +667,78 @@ __global__ void msbfs_records_to_planes_kernel(const int32_t* __restrict__ rec_r
 __global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned long long* __restrict__ F, int64_t rows,
                                                                 const int64_t* __restrict__ push_rp,
                                                                 int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
-                                                                unsigned long long* __restrict__ packed) {
+                                                                unsigned long long* __restrict__ packed,
+                                                                unsigned long long mask = ~0ull) {
     __shared__ WaveStage ws;
     WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
-        const bool take = v < rows && F[v] != 0ull;
+        const bool take = v < rows && (F[v] & mask) != 0ull;
         const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
         app.append(take, (int32_t)v, deg, queue, qoff, packed);
     }
     app.final(queue, qoff, packed);
+}
+
+// ---- split pull levels (msbfs_srcsplit): the sources whose frontier is small go top-down ----
+// A pull row can stop early only when every live source it lacks arrives this level; a source whose
+// frontier is still small (a few rows two hops out) reaches almost no row yet, so on the first pull
+// level it keeps every hub row scanning its whole row.  A split level pulls with live' = the big
+// sources only (the hub band exits early: RMAT-22, band 0 scans 0.2% instead of 60% of the entries,
+// tools/msbfs_split_sim.py) and pushes the small sources' bits top-down into a scratch vector, which
+// msbfs_split_apply_kernel merges into the pulled words.
+
+// out[s] += the push entries of the rows whose word holds source s (one LDS histogram per workgroup)
+__global__ __launch_bounds__(kRedThreads) void msbfs_source_entries_kernel(const unsigned long long* __restrict__ F,
+                                                                          int64_t rows,
+                                                                          const int64_t* __restrict__ push_rp,
+                                                                          unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long cnt[64];
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0ull;
+    __syncthreads();
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        unsigned long long w = F[v];
+        if (!w) continue;
+        const unsigned long long d = (unsigned long long)(push_rp[v + 1] - push_rp[v]);
+        while (w) {
+            atomicAdd(&cnt[__ffsll(w) - 1], d);
+            w &= w - 1;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64 && cnt[threadIdx.x]) atomicAdd(&out[threadIdx.x], cnt[threadIdx.x]);
+}
+
+// *dst = *src & mask (the split level's pull live bits, on the device: the host never reads live)
+__global__ void msbfs_mask_word_kernel(const unsigned long long* __restrict__ src, unsigned long long mask,
+                                      unsigned long long* __restrict__ dst) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dst = *src & mask;
+}
+
+// The small sources' bits of the split level, pushed into T: merged into the pulled words.  A touched
+// row's bits are disjoint from the pulled ones (other sources), so its word, visited bits and new-bit
+// word are ORed, and T is cleared behind.
+__global__ __launch_bounds__(kBlock) void msbfs_split_apply_kernel(const int32_t* __restrict__ touched,
+                                                                   const unsigned long long* __restrict__ tcount,
+                                                                   unsigned long long* __restrict__ T, MsBfsOp op) {
+    const int64_t nt = (int64_t)(*tcount >> kPackShift);
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nt; x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = touched[x];
+        unsigned long long nw = T[u] & ~op.visited[u];
+        T[u] = 0ull;
+        if (!nw) continue;
+        op.Fout[op.pos(u)] |= nw;
+        op.visited[u] |= nw;
+        if (op.nwl) op.nwl[u] |= nw;
+        *op.changed = 1;
+        while (nw) {
+            const int s = __ffsll(nw) - 1;
+            if (op.depth8) op.depth8[(int64_t)s * op.rows + u] = (uint8_t)op.lvl;
+            else if (op.depth) op.depth[(int64_t)s * op.rows + u] = op.lvl;
+            nw &= nw - 1;
+        }
+    }
 }
 
 // The first top-down queue: the distinct source rows with their push-edge offsets, and the packed
@@ -934,6 +995,7 @@ struct MsTd {
     // (unused: the per-peer counts of the sparse reverse exchange come from msbfs_slot_hist_kernel)
     unsigned long long* pcnt;
     int r, P;                  // this shard's index, the shard count
+    unsigned long long mask;   // the sources this push carries (~0: all; a split level: its small sources)
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
@@ -968,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 }
                 const int32_t v = a.queue[i];
                 u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
-                const unsigned long long fv = a.F[v];
+                const unsigned long long fv = a.F[v] & a.mask;
                 if ((u >> a.tbits) == 0) {
                     const unsigned long long w = fv & ~a.visited[u];
                     // a plain read first: a hub neighbour already holding these bits takes no atomic (the
@@ -2247,12 +2309,17 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
                 DevBuf<unsigned long long> xrest;  // msbfs_exit: the band-0 rows pass B scans (a bit per row)
                 MsBu bx{};                         // msbfs_exit: band 0's rows (bx.rows 0: off on this shard)
+                MsBu bx1{};                        // the same over band 0 only (split levels)
+                DevBuf<unsigned long long> tnext;  // msbfs_srcsplit: the small sources' pushed words (one shard)
+                DevBuf<unsigned long long> srcent; // msbfs_srcsplit: push entries per source
                 int64_t exit_tasks = 0;            // the exit bands' merge tasks
                 size_t exit_nbands = 0;
                 bool exit_all = false;  // msbfs_exit_all: the exit rows are every row
                 int exit_all_levels = 0;
-                int exit_unskipped = 0, exit_levels = 0;  // levels that ran the exit rows (with every task counted)
+                // merge tasks of the bands the exit kernels took instead (on levels that count every task, and on all)
+                double exit_unskipped_tasks = 0, exit_level_tasks = 0;
                 unsigned long long b0_live_merged = 0;     // msbfs_exit 1: band 0's live tasks of levels that merged it
+                bool tnext_zero = false;                   // tnext cleared in this call
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
                 DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
                 // levels recorded as (row, new word) records instead of nwl words (level 0 from the sources and
@@ -2320,9 +2387,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.changed.alloc(1);
                 t.hub.alloc(std::max<int64_t>(plan.num_chunks, 1));
                 if (tune().msbfs_split && plan.split_rows > 0) t.split.alloc(plan.split_partial_len());
-                t.live.alloc(2);
+                t.live.alloc(3);  // [2]: a split level's pull live bits
                 t.work.alloc(4);
                 JG_HIP(hipMemsetAsync(t.work.get(), 0, 4 * sizeof(unsigned long long), sh.stream));
+                if (tune().msbfs_srcsplit > 0 && g.shards.size() == 1 && g.P == 1 && c.push) {
+                    t.tnext.alloc(std::max<int64_t>(sh.rows, 1));
+                    t.srcent.alloc(64);
+                }
                 if (tune().msbfs_exit > 0 && t.split.size() && !plan.bands.empty())
                     t.xrest.alloc(std::max<int64_t>(
                         ((tune().msbfs_exit_all ? sh.rows
@@ -2599,6 +2670,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.exit_all = tune().msbfs_exit_all != 0;
                     t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? sh.rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
                     t.bx.examined = t.work.get() + 2;
+                    t.bx1 = t.bx;
+                    t.bx1.rows = t.bx1.wave = t.bx1.ne = plan.bands[0]->row_end;
                     t.exit_nbands = k;
                     for (size_t b = 0; b < k; ++b) t.exit_tasks += plan.bands[b]->tasks;
                 }
@@ -2659,7 +2732,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
                                    td.touched_off.get(), td.ctr.get() + 1, td_shard ? sh.halo_both.tbits : 31,
                                    td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2,
-                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P};
+                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P, ~0ull};
                             msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                   (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                               kBlock, 0, sh.stream>>>(a);
@@ -2870,6 +2943,42 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                         }
                         op.live = lw;
+                        // msbfs_srcsplit: sources whose frontier holds fewer than msbfs_srcsplit_permille of the push
+                        // entries go top-down after the pull (their bits pushed into tnext); the pull then
+                        // runs on the other sources' live bits, and band 0 exits early
+                        unsigned long long small = 0;
+                        if (t.tnext.size() && t.bx1.rows > 0 && td_ok &&
+                            (tune().msbfs_srcsplit == 2 || (tune().msbfs_srcsplit == 1 && pull_levels == 0))) {
+                            JG_HIP(hipMemsetAsync(t.srcent.get(), 0, 64 * sizeof(unsigned long long), sh.stream));
+                            msbfs_source_entries_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
+                                t.F[cur].get(), sh.rows, c.push->row_ptr.get(), t.srcent.get());
+                            JG_LAUNCH_CHECK();
+                            unsigned long long ent[64];
+                            copy_d2h(ent, t.srcent.get(), sizeof ent, sh.stream);
+                            const double lim = (double)push_nnz * (double)tune().msbfs_srcsplit_permille / 1000.0;
+                            double small_sum = 0;
+                            unsigned long long big = 0;
+                            for (int b = 0; b < 64; ++b) {
+                                if (!ent[b]) continue;
+                                if ((double)ent[b] < lim) {
+                                    small |= 1ull << b;
+                                    small_sum += (double)ent[b];
+                                } else {
+                                    big |= 1ull << b;
+                                }
+                            }
+                            // all small: the level would have run top-down; too many small entries: plain pull
+                            if (!big || small_sum * (double)tune().bfs_alpha > (double)push_nnz) small = 0;
+                            if (debug_bfs())
+                                std::fprintf(stderr, "[jg msbfs] level %d pull: %d big, %d small sources (%.0f push entries) -> %s\n",
+                                             level, __builtin_popcountll(big), __builtin_popcountll(small), small_sum,
+                                             small ? "split" : "pull");
+                            if (small) {
+                                msbfs_mask_word_kernel<<<1, 1, 0, sh.stream>>>(lw, ~small, lw + 2);
+                                JG_LAUNCH_CHECK();
+                                op.live = lw + 2;
+                            }
+                        }
                         // sparse levels (msbfs_bu 3): the task bitmaps first; when few tasks hold a row that can
                         // still gain a bit (RMAT-26's last pull level: ~0.2% of the entries), the early-exit
                         // bottom-up kernel visits those rows' entries only, instead of the merge engine's
@@ -2878,8 +2987,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // msbfs_exit 1: band 0's rows exit early on pull levels where fewer than msbfs_exit_live
                         // permille of its merge tasks hold a row that can still gain a bit (their live count
                         // is read back once); 2: on every pull level
-                        const MsBu& bx = t.bx;
-                        int64_t exit_rows = bx.rows > 0 && tune().msbfs_exit == 2 ? bx.rows : 0;
+                        const MsBu& bx = small ? t.bx1 : t.bx;  // a split level: band 0 exits early, always
+                        int64_t exit_rows = bx.rows > 0 && (tune().msbfs_exit == 2 || small) ? bx.rows : 0;
                         const bool exit_probe = bx.rows > 0 && tune().msbfs_exit == 1 && !no_bitmaps && !t.todo.empty();
                         std::vector<const uint32_t*> tl;
                         bool sparse = false;
@@ -2942,9 +3051,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows
                         // can be done there; every task runs, the finalize's live mask keeps it exact)
                         if (no_bitmaps && i == 0) ++unskipped_levels;
-                        if (no_bitmaps && exit_rows) ++t.exit_unskipped;
                         if (exit_rows) {
-                            ++t.exit_levels;
+                            double xt = 0;
+                            for (const auto& bp : plan.bands)
+                                if (bp->row_end <= exit_rows) xt += (double)bp->tasks;
+                            t.exit_level_tasks += xt;
+                            if (no_bitmaps) t.exit_unskipped_tasks += xt;
                             unsigned long long before = 0, after = 0;
                             if (debug_bfs()) copy_d2h(&before, bx.examined, sizeof before, sh.stream);
                             const unsigned xg = red_grid((bx.rows + 63) / 64 * kWave);
@@ -2958,13 +3070,43 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                              level, (long long)bx.rows, after - before);
                             }
                         }
-                        if (exit_rows && t.exit_all) {
-                            ++t.exit_all_levels;  // every row went through the exit kernels
+                        if (exit_rows && exit_rows == sh.rows) {  // msbfs_exit_all: every row went through the exit kernels
+                            ++t.exit_all_levels;
                         } else {
                             launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
                                         t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
                                         tl.empty() ? nullptr : tl.data(), exit_rows);
                         }
+                        }
+                        if (small) {  // the split level's small sources, top-down into tnext, merged into the pulled words
+                            Td& td = tds[i];
+                            if (!t.tnext_zero) {  // first use in this call
+                                JG_HIP(hipMemsetAsync(t.tnext.get(), 0, t.tnext.bytes(), sh.stream));
+                                t.tnext_zero = true;
+                            }
+                            zero_words({{td.ctr.get(), 3 * sizeof(unsigned long long)}}, sh.stream);
+                            msbfs_frontier_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                t.F[cur].get(), sh.rows, c.push->row_ptr.get(), td.queue[qc].get(), td.qoff[qc].get(),
+                                td.ctr.get(), small);
+                            JG_LAUNCH_CHECK();
+                            unsigned long long qc0 = 0;
+                            copy_d2h(&qc0, td.ctr.get(), sizeof qc0, sh.stream);
+                            const int64_t snq = (int64_t)(qc0 >> kPackShift), smf = (int64_t)(qc0 & kEdgeMask);
+                            if (smf > 0) {
+                                MsTd a{td.queue[qc].get(), td.qoff[qc].get(), snq, smf, c.push->row_ptr.get(),
+                                       c.push->col.get(), t.F[cur].get(), t.vis.get(), t.tnext.get(), td.touched.get(),
+                                       td.touched_off.get(), td.ctr.get() + 1, 31, nullptr, td.hlist.get(), td.hlist_off.get(),
+                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small};
+                                msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
+                                                      (smf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
+                                                  kBlock, 0, sh.stream>>>(a);
+                                JG_LAUNCH_CHECK();
+                                msbfs_split_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                    td.touched.get(), td.ctr.get() + 1, t.tnext.get(), op);
+                                JG_LAUNCH_CHECK();
+                            }
+                            td_entries += (double)smf;
+                            td_queued += (double)snq;
                         }
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
@@ -3024,11 +3166,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
-                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels - (double)t.exit_tasks * t.exit_levels
+                const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels - t.exit_level_tasks
                                                           : (double)(w[0] - (i == 0 ? bu_task_credit : 0ull)) +
                                                                 (double)t.b0_live_merged +
                                                                 (double)t.all_tasks * unskipped_levels -
-                                                                (double)t.exit_tasks * t.exit_unskipped;
+                                                                t.exit_unskipped_tasks;
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * (pull_levels - t.exit_all_levels) + (double)w[2];
                 work_entries += entries;
                 work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +

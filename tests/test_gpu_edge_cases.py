@@ -196,14 +196,15 @@ def test_multi_source_bfs_past_255_levels(oracle_lib, shards):
     c.close()
 
 
-@pytest.mark.parametrize("shards,exit_mode", [(1, 1), (1, 2), (3, 1), (3, 2)])
-def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode):
+@pytest.mark.parametrize("shards,exit_mode,srcsplit", [(1, 1, 0), (1, 2, 0), (1, 1, 2), (3, 1, 0), (3, 2, 0)])
+def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode, srcsplit):
     """The 64-source BFS's early-exit rows (msbfs_exit; the split's hub bands scanned row by row) on a
     graph made for it: four hubs of 300-900 leaves joined in a ring, leaves cross-linked to each other's
     hubs, a 150-vertex tail hanging off one leaf, a small separate component and an isolated vertex.  Hub
     rows then need every live source at once while some sources sit at the end of the tail, so some
     levels exit and others must scan whole rows.  All 64 depth rows against the oracle, unbounded and
-    bounded, with the adaptive rule (1) and the exit forced on every pull level (2), on 1 and 3 shards."""
+    bounded, with the adaptive rule (1) and the exit forced on every pull level (2), on 1 and 3 shards, and
+    with the tail's and the small component's sources pushed top-down on pull levels (msbfs_srcsplit 2)."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     rng = np.random.default_rng(5)
@@ -232,6 +233,7 @@ def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode):
     vid = (np.arange(n, dtype=np.int64) + 1) << 8
     try:
         _lib.tune_set("msbfs_exit", exit_mode)
+        _lib.tune_set("msbfs_srcsplit", srcsplit)
         c = jg.Context((0,) * shards)
         g = c.build(vid, vid[s], vid[t], flags=jg.ADJ_BOTH)
         srcs = np.concatenate([[0, 3, tail_end, small, n - 1], rng.choice(leaves, 59, replace=False)])
@@ -244,6 +246,7 @@ def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode):
         c.close()
     finally:
         _lib.tune_set("msbfs_exit", 1)
+        _lib.tune_set("msbfs_srcsplit", 0)
 
 
 def test_vertex_id_remap_arbitrary_ids(ctx, oracle_lib, rmat12):
