@@ -536,8 +536,10 @@ struct Tune {
     int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_merge_kernel): 0 off, 1 on
                           // (read at build time too: the sliced in-CSR and split plan need it)
     // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
-    // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light
-    int64_t band_deg[4] = {128, 8, 0, 0};
+    // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light.  Band 0 from 96
+    // entries (round 4, tools/pr_ab.py: PageRank RMAT-22 / 24 -1% against 128, RMAT-26 and the 64-source
+    // BFS unchanged; profiles/r04/band0_deg/)
+    int64_t band_deg[4] = {96, 8, 0, 0};
     int band_bits[4] = {-1, 3, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits of the vector)
     int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
     int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
