@@ -2859,6 +2859,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                         }
                         td_entries += (double)td.mf;
+                        if (debug_bfs())
+                            std::fprintf(stderr, "[jg msbfs] level %d top-down (shard %d): %lld frontier rows, %lld push entries\n",
+                                         level, sh.index, (long long)td.nq, (long long)td.mf);
                         td_queued += (double)td.nq;
                         {
                             MsBfsOp op;
