@@ -996,6 +996,7 @@ struct MsTd {
     unsigned long long* pcnt;
     int r, P;                  // this shard's index, the shard count
     unsigned long long mask;   // the sources this push carries (~0: all; a split level: its small sources)
+    int probe_visited;         // 0: no visited probe before the OR (the apply masks with visited anyway)
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
@@ -1032,7 +1033,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
                 const unsigned long long fv = a.F[v] & a.mask;
                 if ((u >> a.tbits) == 0) {
-                    const unsigned long long w = fv & ~a.visited[u];
+                    const unsigned long long w = fv & ~(a.probe_visited ? a.visited[u] : 0ull);
                     // a plain read first: a hub neighbour already holding these bits takes no atomic (the
                     // atomics on one word serialise at the memory side); a stale read only costs the atomic
                     if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull;
@@ -2732,7 +2733,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
                                    td.touched_off.get(), td.ctr.get() + 1, td_shard ? sh.halo_both.tbits : 31,
                                    td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2,
-                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P, ~0ull};
+                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P, ~0ull,
+                                   // the first top-down levels skip the visited probe: next to nothing is visited
+                                   // yet, and it is a random 8-byte read per edge (RMAT-26 level 1: 33.6 M)
+                                   level >= tune().msbfs_td_noprobe ? 1 : 0};
                             msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                   (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                               kBlock, 0, sh.stream>>>(a);
@@ -3099,7 +3103,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 MsTd a{td.queue[qc].get(), td.qoff[qc].get(), snq, smf, c.push->row_ptr.get(),
                                        c.push->col.get(), t.F[cur].get(), t.vis.get(), t.tnext.get(), td.touched.get(),
                                        td.touched_off.get(), td.ctr.get() + 1, 31, nullptr, td.hlist.get(), td.hlist_off.get(),
-                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small};
+                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small, 1};
                                 msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                       (smf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                                   kBlock, 0, sh.stream>>>(a);

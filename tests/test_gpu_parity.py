@@ -228,7 +228,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("exit_every_level", 1), ("exit_no_skip", 1), ("exit_one_band", 1),
                                          ("exit_all_rows", 1), ("exit_all_rows", 3), ("srcsplit_first_level", 1),
                                          ("srcsplit_every_level", 1), ("srcsplit_many_small", 1),
-                                         ("srcsplit_exit_all", 1)])
+                                         ("srcsplit_exit_all", 1), ("td_probe_always", 1), ("td_probe_never", 1),
+                                         ("td_probe_never", 3)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -263,6 +264,8 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "srcsplit_first_level": [("msbfs_srcsplit", 1)], "srcsplit_every_level": [("msbfs_srcsplit", 2)],
              "srcsplit_many_small": [("msbfs_srcsplit", 2), ("msbfs_srcsplit_permille", 300)],
              "srcsplit_exit_all": [("msbfs_srcsplit", 2), ("msbfs_exit_all", 1)],
+             # the visited probe of top-down edges (skipped below level msbfs_td_noprobe, 2 by default)
+             "td_probe_always": [("msbfs_td_noprobe", 0)], "td_probe_never": [("msbfs_td_noprobe", 1000)],
              "exit_no_skip": [("msbfs_exit", 2), ("msbfs_skip", 0)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
@@ -296,6 +299,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_exit_all", 0)
         _lib.tune_set("msbfs_srcsplit", 0)
         _lib.tune_set("msbfs_srcsplit_permille", 20)
+        _lib.tune_set("msbfs_td_noprobe", 2)
         _lib.tune_set("msbfs_bu_tasks", 20)
         _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
