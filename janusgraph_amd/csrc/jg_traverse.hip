@@ -772,6 +772,7 @@ struct MsBu {
     int64_t rows, hub, wave, ne;
     int64_t blocks_hub, blocks_wave;  // first blocks of the wave and lane roles
     unsigned long long* examined;     // += the entries scanned (work counter, jg_stats.algorithmic_bytes)
+    int first = 16;                   // msbfs_exit_first_kernel: entries a lane scans before pass B takes the row
 };
 constexpr int kMsBuUnroll = 4;
 
@@ -879,10 +880,9 @@ __global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp
 // On the level after the frontier's peak a hub row typically finds every unvisited live bit within its
 // first two or three entries (RMAT-22: 2.4 on average; tools/msbfs_exit_sim.py), so a 256-entry wave
 // step (msbfs_bu_kernel's wave role) gathers ~100x what the row needs.  Pass A gives each row a lane
-// and its first kExitFirst entries; a row still missing bits leaves its partial word in Fout and a bit
+// and its first `first` entries (MsBu::first, Tune::msbfs_exit_first; 16 by default); a row still missing bits leaves its partial word in Fout and a bit
 // in `rest` (one word per 64 rows, a plain store per wave), and pass B scans the remaining entries of
 // those rows a wave each.  Entries scanned are summed per 1024-thread workgroup, one atomic each.
-constexpr int kExitFirst = 8;
 
 __global__ __launch_bounds__(kRedThreads) void msbfs_exit_first_kernel(MsBu a, MsBfsOp op,
                                                                         unsigned long long* __restrict__ rest) {
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_exit_first_kernel(MsBu a, M
             const unsigned long long need = ~op.visited[v] & live;
             unsigned long long acc = 0;
             if (need) {
-                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1], ek = e1 < e0 + kExitFirst ? e1 : e0 + kExitFirst;
+                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1], ek = e1 < e0 + a.first ? e1 : e0 + a.first;
                 int64_t j = e0;
                 for (; j < ek && acc != need; j += 4) {
                     int32_t c[4];
@@ -933,7 +933,7 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_exit_rest_kernel(MsBu a, Ms
             bits &= bits - 1;
             const unsigned long long need = ~op.visited[v] & live;
             unsigned long long acc = op.Fout[op.pos(v)];
-            const int64_t e0 = a.rp[v] + kExitFirst, e1 = a.rp[v + 1];
+            const int64_t e0 = a.rp[v] + a.first, e1 = a.rp[v + 1];
             int64_t j = e0;
             for (; j < e1 && acc != need; j += kMsBuUnroll * kWave) {
                 int32_t c[kMsBuUnroll];
@@ -2671,6 +2671,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.exit_all = tune().msbfs_exit_all != 0;
                     t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? sh.rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
                     t.bx.examined = t.work.get() + 2;
+                    t.bx.first = tune().msbfs_exit_first;
                     t.bx1 = t.bx;
                     t.bx1.rows = t.bx1.wave = t.bx1.ne = plan.bands[0]->row_end;
                     t.exit_nbands = k;

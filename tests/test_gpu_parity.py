@@ -229,7 +229,7 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("exit_all_rows", 1), ("exit_all_rows", 3), ("srcsplit_first_level", 1),
                                          ("srcsplit_every_level", 1), ("srcsplit_many_small", 1),
                                          ("srcsplit_exit_all", 1), ("td_probe_always", 1), ("td_probe_never", 1),
-                                         ("td_probe_never", 3)])
+                                         ("td_probe_never", 3), ("exit_first3", 1), ("exit_first32", 3)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -266,6 +266,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "srcsplit_exit_all": [("msbfs_srcsplit", 2), ("msbfs_exit_all", 1)],
              # the visited probe of top-down edges (skipped below level msbfs_td_noprobe, 2 by default)
              "td_probe_always": [("msbfs_td_noprobe", 0)], "td_probe_never": [("msbfs_td_noprobe", 1000)],
+             # the early exit's lane pass over 3 / 32 entries per row (16 by default)
+             "exit_first3": [("msbfs_exit_first", 3), ("msbfs_exit_live", 1000)],
+             "exit_first32": [("msbfs_exit_first", 32), ("msbfs_exit_live", 1000)],
              "exit_no_skip": [("msbfs_exit", 2), ("msbfs_skip", 0)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
@@ -300,6 +303,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_srcsplit", 0)
         _lib.tune_set("msbfs_srcsplit_permille", 20)
         _lib.tune_set("msbfs_td_noprobe", 2)
+        _lib.tune_set("msbfs_exit_first", 16)
         _lib.tune_set("msbfs_bu_tasks", 20)
         _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
@@ -314,6 +318,24 @@ def test_directed_bfs(ctx, oracle_lib, direction):
     g = ctx.build(vid, src, dst, flags=3)
     s = int(ds[5])
     np.testing.assert_array_equal(g.bfs([vid[s]], direction)[0], oracle_lib.bfs(n, ds, dd, s, direction))
+
+
+@pytest.mark.parametrize("exit_mode", [0, 1, 2])
+def test_directed_multi_source_bfs(ctx, oracle_lib, exit_mode):
+    """The 64-source BFS along OUT edges (pulling over the IN adjacency, pushing over OUT) with the early
+    exit off, adaptive and forced on every pull level: all depth rows against the oracle."""
+    from janusgraph_amd import _lib
+    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 15)
+    try:
+        _lib.tune_set("msbfs_exit", exit_mode)
+        g = ctx.build(vid, src, dst, flags=3)
+        srcs = np.unique(ds)[::97][:64]
+        depth = g.bfs(vid[srcs], 1)
+        for k in range(len(srcs)):
+            np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 1), err_msg=f"source {k}")
+        g.close()
+    finally:
+        _lib.tune_set("msbfs_exit", 1)
 
 
 @pytest.mark.parametrize("scale", [12, 16])
