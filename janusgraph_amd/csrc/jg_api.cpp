@@ -752,6 +752,9 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "msbfs_srcsplit_permille") {
         JG_ARG(value >= 0 && value <= 1000, "msbfs_srcsplit_permille must be in [0, 1000]");
         jg::tune().msbfs_srcsplit_permille = (int)value;
+    } else if (k == "msbfs_scan_queue") {
+        JG_ARG(value >= 0 && value <= 1001, "msbfs_scan_queue must be in [0, 1001]");
+        jg::tune().msbfs_scan_queue = (int)value;
     } else if (k == "msbfs_exit_first") {
         JG_ARG(value >= 1 && value <= 256, "msbfs_exit_first must be in [1, 256]");
         jg::tune().msbfs_exit_first = (int)value;

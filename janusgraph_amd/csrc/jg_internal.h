@@ -602,6 +602,9 @@ struct Tune {
     int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
                                       //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
                                       //         1.47 / 3.48 / 12.46 ms)
+    int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose exit bands had fewer
+                                      //         live tasks than this permille builds the next top-down queue in its
+                                      //         frontier scan (one pass instead of two); 0: never
     int msbfs_exit_first = 16;        //         msbfs_exit: entries a lane scans per row before a wave takes it
                                       //         (RMAT-26 12.29-12.35 / 12.14-12.21 / 12.14-12.18 ms at 8 / 16 / 32,
                                       //         RMAT-24 -1% at 16; profiles/r04/msbfs_exit/first_*.log)

@@ -741,6 +741,32 @@ __global__ __launch_bounds__(kBlock) void msbfs_split_apply_kernel(const int32_t
     }
 }
 
+// msbfs_frontier_kernel and msbfs_scan_kernel in one pass, after a pull level whose successor is
+// expected to run top-down (its exit bands had almost no live task): the queue, the packed counter
+// and the live bits (*live |= the OR of the words, one atomic per block)
+__global__ __launch_bounds__(kBlock) void msbfs_frontier_live_kernel(const unsigned long long* __restrict__ F, int64_t rows,
+                                                                     const int64_t* __restrict__ push_rp,
+                                                                     int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                                     unsigned long long* __restrict__ packed,
+                                                                     unsigned long long* __restrict__ live) {
+    __shared__ WaveStage ws;
+    __shared__ unsigned long long red[kBlock / kWave];
+    WaveApp app{ws};
+    unsigned long long m = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t v = x0 + threadIdx.x;
+        const unsigned long long w = v < rows ? F[v] : 0ull;
+        m |= w;
+        const bool take = w != 0ull;
+        const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
+        app.append(take, (int32_t)v, deg, queue, qoff, packed);
+    }
+    app.final(queue, qoff, packed);
+    m = block_reduce(m, OrU64{}, red);
+    if (threadIdx.x == 0 && m) atomicOr(live, m);
+}
+
 // The first top-down queue: the distinct source rows with their push-edge offsets, and the packed
 // frontier counter (one thread: at most 64 sources)
 __global__ void msbfs_source_queue_kernel(const int64_t* __restrict__ rows, int cnt, const int64_t* __restrict__ push_rp,
@@ -2321,6 +2347,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 double exit_unskipped_tasks = 0, exit_level_tasks = 0;
                 unsigned long long b0_live_merged = 0;     // msbfs_exit 1: band 0's live tasks of levels that merged it
                 bool tnext_zero = false;                   // tnext cleared in this call
+                double xlive_permille = 1000.0;            // the last probe's live share of the exit bands' tasks
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
                 DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
                 // levels recorded as (row, new word) records instead of nwl words (level 0 from the sources and
@@ -2701,6 +2728,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 const bool have_live = live_ready;
                 queued = live_ready = false;
                 bool level_bu = false;  // this pull level ran msbfs_bu_kernel
+                bool queued_next = false;  // this pull level built the next level's top-down queue
                 if (td_level) {
                     std::vector<void*> fv, rv;
                     for (size_t i = 0; i < g.shards.size(); ++i) {
@@ -3025,6 +3053,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                     unsigned long long xlive = 0;
                                     copy_d2h(&xlive, t.work.get() + 3, sizeof xlive, sh.stream);
                                     const bool go = (double)xlive * 1000.0 < (double)t.exit_tasks * (double)tune().msbfs_exit_live;
+                                    t.xlive_permille = t.exit_tasks ? (double)xlive * 1000.0 / (double)t.exit_tasks : 1000.0;
                                     if (debug_bfs())
                                         std::fprintf(stderr, "[jg msbfs] level %d bands 0..%zu: %llu of %lld merge tasks live -> %s\n",
                                                      level, b, xlive, (long long)t.exit_tasks, go ? "early exit" : "merge");
@@ -3119,8 +3148,19 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
                                        sh.stream);
-                            msbfs_scan_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
-                                t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), lw, tds[i].ctr.get());
+                            // a level whose exit bands had (almost) no live task leaves a small frontier, which
+                            // the next level pushes top-down: its queue is built here, in the same pass
+                            const bool qnext = td_one && !t.todo.empty() && t.xlive_permille < (double)tune().msbfs_scan_queue;
+                            t.xlive_permille = 1000.0;
+                            if (qnext) {
+                                msbfs_frontier_live_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), tds[i].queue[qc ^ 1].get(),
+                                    tds[i].qoff[qc ^ 1].get(), tds[i].ctr.get(), lw);
+                                queued_next = true;
+                            } else {
+                                msbfs_scan_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), lw, tds[i].ctr.get());
+                            }
                             JG_LAUNCH_CHECK();
                         }
                     }
@@ -3128,6 +3168,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         read_frontier();
                         combine_live();
                         live_ready = true;
+                        if (queued_next) {  // the queue is in slot qc ^ 1 (one shard): the next top-down level's
+                            qc ^= 1;
+                            queued = true;
+                        }
                     }
                     ++(level_bu ? bu_levels : pull_levels);
                     need_fwd = g.P > 1;
