@@ -752,6 +752,8 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "msbfs_srcsplit_permille") {
         JG_ARG(value >= 0 && value <= 1000, "msbfs_srcsplit_permille must be in [0, 1000]");
         jg::tune().msbfs_srcsplit_permille = (int)value;
+    } else if (k == "msbfs_skip_empty") {
+        jg::tune().msbfs_skip_empty = value != 0;
     } else if (k == "msbfs_scan_queue") {
         JG_ARG(value >= 0 && value <= 1001, "msbfs_scan_queue must be in [0, 1001]");
         jg::tune().msbfs_scan_queue = (int)value;

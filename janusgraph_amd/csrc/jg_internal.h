@@ -602,6 +602,7 @@ struct Tune {
     int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
                                       //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
                                       //         1.47 / 3.48 / 12.46 ms)
+    int msbfs_skip_empty = 1;         //         bit-parallel BFS pull levels skip the rows without entries (no finalise)
     int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose exit bands had fewer
                                       //         live tasks than this permille builds the next top-down queue in its
                                       //         frontier scan (one pass instead of two); 0: never

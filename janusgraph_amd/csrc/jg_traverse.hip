@@ -585,11 +585,14 @@ __global__ void msbfs_widen_kernel(const uint8_t* __restrict__ d8, int64_t n, in
 // Levels recorded as new-bit words ([levels][rows]) into int32 depth planes (plane s, row r = the level
 // whose word holds bit s; pairs no recorded level holds keep what the planes had: a later level's
 // depth, or -1)
+// Rows [ne, rows) have no pull entries, so no level after 0 reaches them; pull levels do not finalise
+// them (msbfs_skip_empty) and their words of levels >= 1 are never written.
 __global__ void msbfs_levels_to_planes_kernel(const unsigned long long* __restrict__ nwl, int levels, unsigned word_levels,
-                                              int64_t rows, int nsrc, int32_t* __restrict__ depth) {
+                                              int64_t rows, int64_t ne, int nsrc, int32_t* __restrict__ depth) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
         for (int L = 0; L < levels; ++L) {
             if (!((word_levels >> L) & 1u)) continue;  // a top-down level: its (row, word) records instead
+            if (L > 0 && r >= ne) break;
             unsigned long long w = nwl[(int64_t)L * rows + r];
             while (w) {
                 const int s = __ffsll(w) - 1;
@@ -2637,8 +2640,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     DeviceGuard dg(sh.device);
                     const int lw = std::min(levels_run + 1, kMsLevelWords);
                     if (sh.rows > 0) {
+                        const Csr* pc = pick_csrs(sh, direction).pull;
+                        const int64_t ne = tune().msbfs_skip_empty && pc->empty_from >= 0 ? std::min(pc->empty_from, sh.rows)
+                                                                                            : sh.rows;
                         msbfs_levels_to_planes_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                            t.nwl.get(), lw, word_levels, sh.rows, ns, t.depth.get());
+                            t.nwl.get(), lw, word_levels, sh.rows, ne, ns, t.depth.get());
                         JG_LAUNCH_CHECK();
                     }
                     for (const auto& r : t.recs)
@@ -3110,9 +3116,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         if (exit_rows && exit_rows == sh.rows) {  // msbfs_exit_all: every row went through the exit kernels
                             ++t.exit_all_levels;
                         } else {
+                            // rows without pull entries are not finalised (msbfs_skip_empty): they gain nothing,
+                            // their words are zero on every output vector, and their new-bit words are masked
+                            // at output (msbfs_levels_to_planes_kernel)
                             launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                        t.split.size() ? t.split.get() : (unsigned long long*)nullptr, false,
-                                        tl.empty() ? nullptr : tl.data(), exit_rows);
+                                        t.split.size() ? t.split.get() : (unsigned long long*)nullptr,
+                                        tune().msbfs_skip_empty != 0, tl.empty() ? nullptr : tl.data(), exit_rows);
                         }
                         }
                         if (small) {  // the split level's small sources, top-down into tnext, merged into the pulled words

@@ -89,7 +89,8 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_exit_bands", 1), ("msbfs_exit_bands", 2), ("msbfs_exit_all", 1), ("msbfs_exit_all", 0),
                  ("msbfs_srcsplit", 1), ("msbfs_srcsplit", 2), ("msbfs_srcsplit", 0), ("msbfs_srcsplit_permille", 20),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
-                 ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50)):
+                 ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
+                 ("msbfs_skip_empty", 0), ("msbfs_skip_empty", 1)):
         _lib.tune_set(k, v)
     for k, v in (("light_lds", -1), ("pull_unroll", 5), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
                  ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 5), ("merge_nt", 0),
