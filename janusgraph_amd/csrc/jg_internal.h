@@ -590,6 +590,8 @@ struct Tune {
                                       //         where few band-0 tasks are live, 2 every pull level); the other rows
                                       //         stay merged.  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 /
                                       //         13.4 ms (profiles/r04/msbfs_exit/)
+    int msbfs_td_rowapply = 4;        //         bit-parallel BFS, one shard: a top-down level with >= rows / this frontier
+                                      //         edges applies over every row in order, not its touched list (0: never)
     int msbfs_td_noprobe = 2;         //         bit-parallel BFS: top-down levels below this skip the visited probe
                                       //         (RMAT-26 12.49-12.60 -> 12.32 ms, RMAT-24 -1%; profiles/r04/msbfs_td_dense/)
     int msbfs_srcsplit = 0;           //         bit-parallel BFS, one shard: the first pull level's small-frontier sources

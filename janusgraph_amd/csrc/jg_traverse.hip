@@ -1026,6 +1026,7 @@ struct MsTd {
     int r, P;                  // this shard's index, the shard count
     unsigned long long mask;   // the sources this push carries (~0: all; a split level: its small sources)
     int probe_visited;         // 0: no visited probe before the OR (the apply masks with visited anyway)
+    int no_touched;            // 1: no touched list (the level's apply passes over every row instead)
 };
 
 __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
@@ -1065,7 +1066,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                     const unsigned long long w = fv & ~(a.probe_visited ? a.visited[u] : 0ull);
                     // a plain read first: a hub neighbour already holding these bits takes no atomic (the
                     // atomics on one word serialise at the memory side); a stale read only costs the atomic
-                    if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull;
+                    if (w && (w & ~a.Fnext[u])) take = atomicOr(&a.Fnext[u], w) == 0ull && !a.no_touched;
                 } else if (fv & ~a.hstage[u]) {
                     // a peer's vertex: its halo slot collects the bits; the reverse exchange takes them to
                     // the owner, which masks them with its visited bits (msbfs_td_recv_kernel)
@@ -1312,6 +1313,47 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_kernel(const int32_t* _
         for (int w = 1; w < kBlock / kWave; ++w) lv |= red[w];
         // a plain read first: once every source is live (most levels) no block takes the atomic, which
         // serialises at the memory side (one per block was +1.5 ms over a sharded RMAT-26 traversal)
+        if (lv & ~*(volatile unsigned long long*)live_out) atomicOr(live_out, lv);
+    }
+}
+
+// The same over every own row in row order (msbfs_td_rowapply): a big top-down level touches a good
+// part of the rows (RMAT-26 level 1: 33.6 M edges), and its touched list, in append order, made every
+// word, visited and next-word access of the apply a random 8-byte one (0.48 ms); the pass reads the
+// words sequentially and finalises the nonzero ones.
+__global__ __launch_bounds__(kBlock) void msbfs_td_apply_rows_kernel(int64_t rows, MsBfsOp op,
+                                                                     const int64_t* __restrict__ push_rp,
+                                                                     int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                                     unsigned long long* __restrict__ packed,
+                                                                     unsigned long long* __restrict__ live_out) {
+    __shared__ WaveStage ws;
+    __shared__ unsigned long long red[kBlock / kWave];
+    WaveApp app{ws};
+    unsigned long long lv = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+        const int64_t u = x0 + threadIdx.x;
+        bool take = false;
+        int64_t deg = 0;
+        if (u < rows) {
+            const unsigned long long acc = op.Fout[op.pos(u)];
+            if (acc) {
+                op.finalize(u, acc);
+                const unsigned long long nw = op.Fout[op.pos(u)];
+                lv |= nw;
+                take = nw != 0ull;
+                if (take) deg = push_rp[u + 1] - push_rp[u];
+            }
+        }
+        app.append(take, (int32_t)u, deg, queue, qoff, packed);
+    }
+    app.final(queue, qoff, packed);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) lv |= __shfl_xor(lv, o, kWave);
+    if (lane_id() == 0) red[wave_id()] = lv;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) lv |= red[w];
         if (lv & ~*(volatile unsigned long long*)live_out) atomicOr(live_out, lv);
     }
 }
@@ -2395,6 +2437,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 int64_t nrp = 0;                  // pairs received by the last sparse exchange
                 PairRuns pv{};                    // their per-peer runs and this shard's send-list offsets
                 int64_t nq_in = 0;                // the last top-down level's input frontier (its queue)
+                bool rowapply = false;            // this level's apply passes over every row (no touched list)
             };
             std::vector<Td> tds(g.shards.size());
             std::vector<int64_t> src_local((size_t)ns);
@@ -2721,6 +2764,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int pull_levels = 0;
             int unskipped_levels = 0;  // pull levels that ran every merge task (msbfs_skip_first)
             double td_entries = 0, td_touched = 0, td_queued = 0;
+            double td_row_passes = 0;  // rows the row-order applies read (8 B each)
             while (max_depth < 0 || level < max_depth) {
                 if (level + 1 >= kMsLevelWords) ensure_depth8();
                 if (level + 1 >= 255) widen();
@@ -2763,6 +2807,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                                   sh.stream));
                         }
                         td.nq_in = td.nq;
+                        // a big level (one shard): the apply passes over every row instead of a touched list
+                        td.rowapply = !td_shard && tune().msbfs_td_rowapply > 0 &&
+                                      td.mf * tune().msbfs_td_rowapply >= sh.rows;
                         if (td.mf > 0) {
                             MsTd a{td.queue[qc].get(), td.qoff[qc].get(), td.nq, td.mf, c.push->row_ptr.get(),
                                    c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
@@ -2771,7 +2818,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P, ~0ull,
                                    // the first top-down levels skip the visited probe: next to nothing is visited
                                    // yet, and it is a random 8-byte read per edge (RMAT-26 level 1: 33.6 M)
-                                   level >= tune().msbfs_td_noprobe ? 1 : 0};
+                                   level >= tune().msbfs_td_noprobe ? 1 : 0, td.rowapply ? 1 : 0};
                             msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                   (td.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                               kBlock, 0, sh.stream>>>(a);
@@ -2902,6 +2949,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             std::fprintf(stderr, "[jg msbfs] level %d top-down (shard %d): %lld frontier rows, %lld push entries\n",
                                          level, sh.index, (long long)td.nq, (long long)td.mf);
                         td_queued += (double)td.nq;
+                        if (td.rowapply) td_row_passes += (double)sh.rows;
                         {
                             MsBfsOp op;
                             op.F = t.F[cur].get();
@@ -2915,9 +2963,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             op.pos = g.vec_pos(sh, adj_of(sh, c));
                             op.lvl = level + 1;
                             op.live = t.live.get() + 1;
-                            msbfs_td_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                                td.touched.get(), td.ctr.get() + 1, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
-                                td.qoff[qc ^ 1].get(), td.ctr.get(), t.live.get());
+                            if (td.rowapply)
+                                msbfs_td_apply_rows_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                    sh.rows, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(), td.qoff[qc ^ 1].get(),
+                                    td.ctr.get(), t.live.get());
+                            else
+                                msbfs_td_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
+                                    td.touched.get(), td.ctr.get() + 1, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
+                                    td.qoff[qc ^ 1].get(), td.ctr.get(), t.live.get());
                             JG_LAUNCH_CHECK();
                         }
                     }
@@ -3142,7 +3195,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 MsTd a{td.queue[qc].get(), td.qoff[qc].get(), snq, smf, c.push->row_ptr.get(),
                                        c.push->col.get(), t.F[cur].get(), t.vis.get(), t.tnext.get(), td.touched.get(),
                                        td.touched_off.get(), td.ctr.get() + 1, 31, nullptr, td.hlist.get(), td.hlist_off.get(),
-                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small, 1};
+                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small, 1, 0};
                                 msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
                                                       (smf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
                                                   kBlock, 0, sh.stream>>>(a);
@@ -3238,7 +3291,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                               (level >= kMsLevelWords ? 4.0 * (double)w[1] : 0.0);
             }
             work_entries += td_entries;
-            work_bytes += 12.0 * td_entries + 24.0 * td_touched + 8.0 * td_queued;
+            work_bytes += 12.0 * td_entries + 24.0 * td_touched + 8.0 * td_queued + 8.0 * td_row_passes;
             if (depth_rows || keep) {
                 materialize(level);  // the caller's int32 rows
                 if (depth_rows)

@@ -90,13 +90,13 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_srcsplit", 1), ("msbfs_srcsplit", 2), ("msbfs_srcsplit", 0), ("msbfs_srcsplit_permille", 20),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
-                 ("msbfs_skip_empty", 0), ("msbfs_skip_empty", 1)):
+                 ("msbfs_skip_empty", 0), ("msbfs_skip_empty", 1), ("msbfs_td_rowapply", 0), ("msbfs_td_rowapply", 4)):
         _lib.tune_set(k, v)
     for k, v in (("light_lds", -1), ("pull_unroll", 5), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
                  ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 5), ("merge_nt", 0),
                  ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("msbfs_bu", 4), ("msbfs_bu_tasks", 1001), ("bfs_tail_grid", -1),
                  ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_exit_bands", 0), ("msbfs_exit_bands", 5),
-                 ("msbfs_srcsplit", 3), ("msbfs_srcsplit_permille", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0), ("msbfs_scan_queue", 1002),
+                 ("msbfs_srcsplit", 3), ("msbfs_srcsplit_permille", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0), ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1),
                  ("msbfs_bu_frac", 1001), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1), ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31)):
         with pytest.raises(jg.JanusGpuError) as e:
             _lib.tune_set(k, v)

@@ -230,7 +230,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("srcsplit_every_level", 1), ("srcsplit_many_small", 1),
                                          ("srcsplit_exit_all", 1), ("td_probe_always", 1), ("td_probe_never", 1),
                                          ("td_probe_never", 3), ("exit_first3", 1), ("exit_first32", 3), ("scan_queue_off", 1),
-                                         ("scan_queue_always", 1), ("finalize_empty_rows", 1), ("finalize_empty_rows", 3)])
+                                         ("scan_queue_always", 1), ("finalize_empty_rows", 1), ("finalize_empty_rows", 3),
+                                         ("td_rowapply_off", 1), ("td_rowapply_always", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -274,6 +275,8 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "scan_queue_off": [("msbfs_scan_queue", 0)], "scan_queue_always": [("msbfs_scan_queue", 1001)],
              # pull levels finalise the rows without entries too (msbfs_skip_empty 0; 1 by default)
              "finalize_empty_rows": [("msbfs_skip_empty", 0)],
+             # top-down applies in row order (msbfs_td_rowapply: never / every one-shard level)
+             "td_rowapply_off": [("msbfs_td_rowapply", 0)], "td_rowapply_always": [("msbfs_td_rowapply", 1024)],
              "exit_no_skip": [("msbfs_exit", 2), ("msbfs_skip", 0)]}[mode]
     n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 15)
     n = n0 + 3  # + an isolated vertex and a two-vertex component
@@ -311,6 +314,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_exit_first", 16)
         _lib.tune_set("msbfs_scan_queue", 50)
         _lib.tune_set("msbfs_skip_empty", 1)
+        _lib.tune_set("msbfs_td_rowapply", 4)
         _lib.tune_set("msbfs_bu_tasks", 20)
         _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
