@@ -611,7 +611,9 @@ struct Tune {
     int msbfs_exit_first = 16;        //         msbfs_exit: entries a lane scans per row before a wave takes it
                                       //         (RMAT-26 12.29-12.35 / 12.14-12.21 / 12.14-12.18 ms at 8 / 16 / 32,
                                       //         RMAT-24 -1% at 16; profiles/r04/msbfs_exit/first_*.log)
-    int msbfs_exit_all = 0;           //         msbfs_exit: every row (the light rows too) takes the early exit
+    int msbfs_exit_all = 1;           //         msbfs_exit: every row with entries (the light rows too) takes the early
+                                      //         exit; no merge launch on such levels (RMAT-26 11.42-11.46 -> 11.19-11.21
+                                      //         ms, RMAT-24 -1%, once the empty rows were skipped; neutral before)
     int msbfs_exit_live = 950;        //         msbfs_exit 1: permille of band 0's merge tasks live below which its rows
                                       //         exit early (the level after the frontier's peak: 45-73%; before it: 100%)
     int msbfs_bu_frac = 100;          //         permille of the rows

@@ -2387,6 +2387,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 int64_t exit_tasks = 0;            // the exit bands' merge tasks
                 size_t exit_nbands = 0;
                 bool exit_all = false;  // msbfs_exit_all: the exit rows are every row
+                int64_t all_rows = 0;   // the rows a pull level finalises (those with entries under msbfs_skip_empty)
                 int exit_all_levels = 0;
                 // merge tasks of the bands the exit kernels took instead (on levels that count every task, and on all)
                 double exit_unskipped_tasks = 0, exit_level_tasks = 0;
@@ -2745,7 +2746,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     const size_t k = tune().msbfs_exit_all ? plan.bands.size()
                                                            : std::min<size_t>(plan.bands.size(), (size_t)tune().msbfs_exit_bands);
                     t.exit_all = tune().msbfs_exit_all != 0;
-                    t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? sh.rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
+                    // (exit_all: every row with entries when the pull levels skip the empty ones, else every row)
+                    const int64_t all_rows = tune().msbfs_skip_empty && c.pull->empty_from >= 0
+                                                 ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
+                    t.all_rows = all_rows;
+                    t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? all_rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
                     t.bx.examined = t.work.get() + 2;
                     t.bx.first = tune().msbfs_exit_first;
                     t.bx1 = t.bx;
@@ -3166,7 +3171,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                              level, (long long)bx.rows, after - before);
                             }
                         }
-                        if (exit_rows && exit_rows == sh.rows) {  // msbfs_exit_all: every row went through the exit kernels
+                        if (exit_rows && exit_rows == t.all_rows) {  // msbfs_exit_all: every row went through the exit kernels
                             ++t.exit_all_levels;
                         } else {
                             // rows without pull entries are not finalised (msbfs_skip_empty): they gain nothing,

@@ -226,9 +226,9 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("skip_every_level", 3), ("bu_sparse_levels", 1), ("bu_sparse_always", 1),
                                          ("bu_every_level", 1), ("exit_off", 1), ("exit_every_bitmapped_level", 1),
                                          ("exit_every_level", 1), ("exit_no_skip", 1), ("exit_one_band", 1),
-                                         ("exit_all_rows", 1), ("exit_all_rows", 3), ("srcsplit_first_level", 1),
+                                         ("exit_light_merged", 1), ("exit_light_merged", 3), ("srcsplit_first_level", 1),
                                          ("srcsplit_every_level", 1), ("srcsplit_many_small", 1),
-                                         ("srcsplit_exit_all", 1), ("td_probe_always", 1), ("td_probe_never", 1),
+                                         ("srcsplit_exit_bands", 1), ("td_probe_always", 1), ("td_probe_never", 1),
                                          ("td_probe_never", 3), ("exit_first3", 1), ("exit_first32", 3), ("scan_queue_off", 1),
                                          ("scan_queue_always", 1), ("finalize_empty_rows", 1), ("finalize_empty_rows", 3),
                                          ("td_rowapply_off", 1), ("td_rowapply_always", 1)])
@@ -261,11 +261,11 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "exit_off": [("msbfs_exit", 0)], "exit_every_bitmapped_level": [("msbfs_exit_live", 1000)],
              "exit_every_level": [("msbfs_exit", 2)],
              "exit_one_band": [("msbfs_exit_bands", 1), ("msbfs_exit_live", 1000)],
-             "exit_all_rows": [("msbfs_exit_all", 1), ("msbfs_exit_live", 1000)],
+             "exit_light_merged": [("msbfs_exit_all", 0), ("msbfs_exit_live", 1000)],
              # the first pull level's small-frontier sources top-down (msbfs_srcsplit; 0, off, by default)
              "srcsplit_first_level": [("msbfs_srcsplit", 1)], "srcsplit_every_level": [("msbfs_srcsplit", 2)],
              "srcsplit_many_small": [("msbfs_srcsplit", 2), ("msbfs_srcsplit_permille", 300)],
-             "srcsplit_exit_all": [("msbfs_srcsplit", 2), ("msbfs_exit_all", 1)],
+             "srcsplit_exit_bands": [("msbfs_srcsplit", 2), ("msbfs_exit_all", 0)],
              # the visited probe of top-down edges (skipped below level msbfs_td_noprobe, 2 by default)
              "td_probe_always": [("msbfs_td_noprobe", 0)], "td_probe_never": [("msbfs_td_noprobe", 1000)],
              # the early exit's lane pass over 3 / 32 entries per row (16 by default)
@@ -307,7 +307,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_exit", 1)
         _lib.tune_set("msbfs_exit_live", 950)
         _lib.tune_set("msbfs_exit_bands", 2)
-        _lib.tune_set("msbfs_exit_all", 0)
+        _lib.tune_set("msbfs_exit_all", 1)
         _lib.tune_set("msbfs_srcsplit", 0)
         _lib.tune_set("msbfs_srcsplit_permille", 20)
         _lib.tune_set("msbfs_td_noprobe", 2)
