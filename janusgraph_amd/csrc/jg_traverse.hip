@@ -613,25 +613,31 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_pairs_kernel(const unsigned
     if (threadIdx.x == 0 && c) atomicAdd(pairs, c);
 }
 
-__global__ void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc, unsigned long long* __restrict__ F,
-                                  unsigned long long* __restrict__ visited, unsigned long long* __restrict__ nw0,
-                                  int64_t rows, VecPos pos, int32_t* __restrict__ rec_rows,
-                                  unsigned long long* __restrict__ rec_words) {
-    // sequential over the (<= 64) sources: several sources may share a vertex
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    for (int s = 0; s < nsrc; ++s) {
-        const int64_t l = local_src[s];
-        if (l < 0) continue;
-        F[pos(l)] |= 1ull << s;
-        visited[l] |= 1ull << s;
-        if (nw0) nw0[l] |= 1ull << s;  // level 0's new-bit word
+__global__ __launch_bounds__(kWave) void msbfs_init_kernel(const int64_t* __restrict__ local_src, int nsrc,
+                                                           unsigned long long* __restrict__ F,
+                                                           unsigned long long* __restrict__ visited,
+                                                           unsigned long long* __restrict__ nw0, int64_t rows, VecPos pos,
+                                                           int32_t* __restrict__ rec_rows,
+                                                           unsigned long long* __restrict__ rec_words) {
+    // one wave, lane s = source s (nsrc <= 64: the caller walks the sources in batches of 64).  Several
+    // sources may share a vertex: each lane ORs in the bits of every source on its row, so lanes sharing
+    // a row store the same words (one thread walking the sources took ~46 us: 128 dependent round trips)
+    const int s = (int)threadIdx.x;
+    const int64_t l = s < nsrc ? local_src[s] : -1;
+    unsigned long long word = 0;
+    for (int t = 0; t < nsrc; ++t)
+        if (__shfl(l, t, kWave) == l) word |= 1ull << t;
+    if (l >= 0) {
+        const unsigned long long f = F[pos(l)] | word;
+        F[pos(l)] = f;
+        visited[l] |= word;
+        if (nw0) nw0[l] |= word;  // level 0's new-bit word
+        if (rec_rows) rec_words[s] = f;
+    } else if (rec_rows && s < nsrc) {
+        rec_words[s] = 0ull;
     }
-    if (rec_rows)  // level 0 as (row, word) records: a shared source row records the same full word twice
-        for (int s = 0; s < nsrc; ++s) {
-            const int64_t l = local_src[s];
-            rec_rows[s] = (int32_t)l;
-            rec_words[s] = l < 0 ? 0ull : F[pos(l)];
-        }
+    // level 0 as (row, word) records: a shared source row records the same full word twice
+    if (rec_rows && s < nsrc) rec_rows[s] = (int32_t)l;
 }
 
 // A top-down level's depths as (row, new-bit word) records: the rows that gained a bit are exactly the
@@ -772,18 +778,21 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_live_kernel(const unsig
 
 // The first top-down queue: the distinct source rows with their push-edge offsets, and the packed
 // frontier counter (one thread: at most 64 sources)
-__global__ void msbfs_source_queue_kernel(const int64_t* __restrict__ rows, int cnt, const int64_t* __restrict__ push_rp,
-                                          int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
-                                          unsigned long long* __restrict__ packed) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    int64_t off = 0;
-    for (int i = 0; i < cnt; ++i) {
-        const int64_t v = rows[i];
+__global__ __launch_bounds__(kWave) void msbfs_source_queue_kernel(const int64_t* __restrict__ rows, int cnt,
+                                                                   const int64_t* __restrict__ push_rp,
+                                                                   int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
+                                                                   unsigned long long* __restrict__ packed) {
+    // one wave, lane i = distinct source row i (cnt <= 64: one batch's distinct rows); the entry offsets are
+    // the wave's exclusive scan of the row degrees
+    const int i = (int)threadIdx.x;
+    const int64_t v = i < cnt ? rows[i] : 0;
+    const int64_t d = i < cnt ? push_rp[v + 1] - push_rp[v] : 0;
+    const int64_t inc = wave_inclusive_scan_add(d);
+    if (i < cnt) {
         queue[i] = (int32_t)v;
-        qoff[i] = off;
-        off += push_rp[v + 1] - push_rp[v];
+        qoff[i] = inc - d;
     }
-    packed[0] = ((unsigned long long)cnt << kPackShift) | (unsigned long long)off;
+    if (i == kWave - 1) packed[0] = ((unsigned long long)cnt << kPackShift) | (unsigned long long)inc;
 }
 
 // ---- bottom-up pull levels of the bit-parallel BFS with early exit (one shard) ----
@@ -2615,7 +2624,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 } else {  // level 0's words
                     JG_HIP(hipMemsetAsync(t.nwl.get(), 0, (size_t)sh.rows * sizeof(unsigned long long), sh.stream));
                 }
-                msbfs_init_kernel<<<1, 1, 0, sh.stream>>>(t.dloc.get(), ns, t.F[0].get(), t.vis.get(),
+                msbfs_init_kernel<<<1, kWave, 0, sh.stream>>>(t.dloc.get(), ns, t.F[0].get(), t.vis.get(),
                                                           r0 ? nullptr : t.nwl.get(), sh.rows, g.vec_pos(sh, adj_of(sh, c)),
                                                           r0 ? r0->rows.get() : nullptr, r0 ? r0->words.get() : nullptr);
                 JG_LAUNCH_CHECK();
@@ -2631,7 +2640,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     Shard& sh = *g.shards[i];
                     DeviceGuard dg(sh.device);
                     const BfsCsrs c = pick_csrs(sh, direction);
-                    msbfs_source_queue_kernel<<<1, 1, 0, sh.stream>>>(tds[i].srcs.get(), (int)tds[i].src_rows.size(),
+                    msbfs_source_queue_kernel<<<1, kWave, 0, sh.stream>>>(tds[i].srcs.get(), (int)tds[i].src_rows.size(),
                                                                        c.push->row_ptr.get(), tds[i].queue[0].get(),
                                                                        tds[i].qoff[0].get(), tds[i].ctr.get());
                     JG_LAUNCH_CHECK();
