@@ -743,6 +743,9 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "msbfs_exit_bands") {
         JG_ARG(value >= 1 && value <= 4, "msbfs_exit_bands must be in [1, 4]");
         jg::tune().msbfs_exit_bands = (int)value;
+    } else if (k == "msbfs_exit_probe") {
+        JG_ARG(value >= 0 && value <= 4, "msbfs_exit_probe must be in [0, 4]");
+        jg::tune().msbfs_exit_probe = (int)value;
     } else if (k == "msbfs_td_rowapply") {
         JG_ARG(value >= 0 && value <= 1024, "msbfs_td_rowapply must be in [0, 1024]");
         jg::tune().msbfs_td_rowapply = (int)value;

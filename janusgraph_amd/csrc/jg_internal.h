@@ -604,6 +604,10 @@ struct Tune {
     int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
                                       //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
                                       //         1.47 / 3.48 / 12.46 ms)
+    int msbfs_exit_probe = 1;         //         msbfs_exit: how many leading exit bands' live tasks decide a level's exit
+                                      //         (0: all of them; at 1 an exit level builds no band-1 bitmaps: RMAT-22
+                                      //         / 24 / 26 at 0 / 1: 1.384 / 3.131 / 11.23 -> 1.385 / 3.102 / 11.12 ms,
+                                      //         the same decisions, profiles/r04/msbfs_exit/probe_band0.jsonl)
     int msbfs_skip_empty = 1;         //         bit-parallel BFS pull levels skip the rows without entries (no finalise)
     int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose exit bands had fewer
                                       //         live tasks than this permille builds the next top-down queue in its

@@ -2393,8 +2393,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 MsBu bx1{};                        // the same over band 0 only (split levels)
                 DevBuf<unsigned long long> tnext;  // msbfs_srcsplit: the small sources' pushed words (one shard)
                 DevBuf<unsigned long long> srcent; // msbfs_srcsplit: push entries per source
-                int64_t exit_tasks = 0;            // the exit bands' merge tasks
+                int64_t exit_tasks = 0;            // the probed exit bands' merge tasks
                 size_t exit_nbands = 0;
+                size_t probe_nbands = 0;           // the leading exit bands whose live tasks decide (msbfs_exit_probe)
                 bool exit_all = false;  // msbfs_exit_all: the exit rows are every row
                 int64_t all_rows = 0;   // the rows a pull level finalises (those with entries under msbfs_skip_empty)
                 int exit_all_levels = 0;
@@ -2765,7 +2766,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.bx1 = t.bx;
                     t.bx1.rows = t.bx1.wave = t.bx1.ne = plan.bands[0]->row_end;
                     t.exit_nbands = k;
-                    for (size_t b = 0; b < k; ++b) t.exit_tasks += plan.bands[b]->tasks;
+                    t.probe_nbands = tune().msbfs_exit_probe > 0 ? std::min<size_t>(k, (size_t)tune().msbfs_exit_probe) : k;
+                    for (size_t b = 0; b < t.probe_nbands; ++b) t.exit_tasks += plan.bands[b]->tasks;
                 }
             }
             int bu_levels = 0;
@@ -3114,15 +3116,16 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
                                     t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                                 JG_LAUNCH_CHECK();
-                                // the exit bands count their live tasks apart (work[3]); after the last of them the
-                                // count decides (launch_pull then skips those bands, whatever their bitmaps say)
-                                const bool probe = exit_probe && b < t.exit_nbands;
+                                // the probed exit bands count their live tasks apart (work[3]); after the last of them
+                                // the count decides (launch_pull then skips the exit bands, whatever their bitmaps
+                                // say, and an exit level builds no bitmaps for the bands after the probed ones)
+                                const bool probe = exit_probe && b < t.probe_nbands;
                                 if (probe && b == 0) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
                                 msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
                                     bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(),
                                     t.work.get() + (probe ? 3 : 0));
                                 JG_LAUNCH_CHECK();
-                                if (probe && b + 1 == t.exit_nbands) {
+                                if (probe && b + 1 == t.probe_nbands) {
                                     unsigned long long xlive = 0;
                                     copy_d2h(&xlive, t.work.get() + 3, sizeof xlive, sh.stream);
                                     const bool go = (double)xlive * 1000.0 < (double)t.exit_tasks * (double)tune().msbfs_exit_live;

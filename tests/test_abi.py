@@ -87,6 +87,7 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_bu_frac", 100), ("msbfs_sparse", 1), ("msbfs_skip_first", 1), ("msbfs_skip_first", 0), ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("band_sliced_build", 0), ("msbfs_td", 2), ("msbfs_td", 1), ("bfs_td_split", 2), ("bfs_td_split_levels", 2), ("bfs_td_split_min", 65536), ("bfs_td_split_max", 1 << 20), ("relabel_dead_last", 0), ("relabel_dead_last", 1), ("msbfs_bu", 3), ("msbfs_bu_tasks", 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64), ("relabel_out_ties", 1), ("relabel_out_ties", 0),
                  ("msbfs_exit", 0), ("msbfs_exit", 2), ("msbfs_exit", 1), ("msbfs_exit_live", 1000), ("msbfs_exit_live", 950),
                  ("msbfs_exit_bands", 1), ("msbfs_exit_bands", 2), ("msbfs_exit_all", 1), ("msbfs_exit_all", 0),
+                 ("msbfs_exit_probe", 0), ("msbfs_exit_probe", 1),
                  ("msbfs_srcsplit", 1), ("msbfs_srcsplit", 2), ("msbfs_srcsplit", 0), ("msbfs_srcsplit_permille", 20),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
@@ -96,6 +97,7 @@ def test_tune_keys_validate_without_a_gpu():
                  ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 5), ("merge_nt", 0),
                  ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("msbfs_bu", 4), ("msbfs_bu_tasks", 1001), ("bfs_tail_grid", -1),
                  ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_exit_bands", 0), ("msbfs_exit_bands", 5),
+                 ("msbfs_exit_probe", -1), ("msbfs_exit_probe", 5),
                  ("msbfs_srcsplit", 3), ("msbfs_srcsplit_permille", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0), ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1),
                  ("msbfs_bu_frac", 1001), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1), ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31)):
         with pytest.raises(jg.JanusGpuError) as e:

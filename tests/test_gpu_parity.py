@@ -231,7 +231,8 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
                                          ("srcsplit_exit_bands", 1), ("td_probe_always", 1), ("td_probe_never", 1),
                                          ("td_probe_never", 3), ("exit_first3", 1), ("exit_first32", 3), ("scan_queue_off", 1),
                                          ("scan_queue_always", 1), ("finalize_empty_rows", 1), ("finalize_empty_rows", 3),
-                                         ("td_rowapply_off", 1), ("td_rowapply_always", 1)])
+                                         ("td_rowapply_off", 1), ("td_rowapply_always", 1), ("exit_probe_all", 1),
+                                         ("exit_probe_all", 3), ("exit_probe_all_merged", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -262,6 +263,9 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "exit_every_level": [("msbfs_exit", 2)],
              "exit_one_band": [("msbfs_exit_bands", 1), ("msbfs_exit_live", 1000)],
              "exit_light_merged": [("msbfs_exit_all", 0), ("msbfs_exit_live", 1000)],
+             # the exit decided by every exit band's live tasks (msbfs_exit_probe 0; 1, band 0 alone, by default)
+             "exit_probe_all": [("msbfs_exit_probe", 0)],
+             "exit_probe_all_merged": [("msbfs_exit_probe", 0), ("msbfs_exit_all", 0), ("msbfs_exit_live", 1000)],
              # the first pull level's small-frontier sources top-down (msbfs_srcsplit; 0, off, by default)
              "srcsplit_first_level": [("msbfs_srcsplit", 1)], "srcsplit_every_level": [("msbfs_srcsplit", 2)],
              "srcsplit_many_small": [("msbfs_srcsplit", 2), ("msbfs_srcsplit_permille", 300)],
@@ -308,6 +312,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_exit_live", 950)
         _lib.tune_set("msbfs_exit_bands", 2)
         _lib.tune_set("msbfs_exit_all", 1)
+        _lib.tune_set("msbfs_exit_probe", 1)
         _lib.tune_set("msbfs_srcsplit", 0)
         _lib.tune_set("msbfs_srcsplit_permille", 20)
         _lib.tune_set("msbfs_td_noprobe", 2)
