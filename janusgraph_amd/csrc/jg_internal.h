@@ -607,7 +607,8 @@ struct Tune {
     int msbfs_exit_probe = 1;         //         msbfs_exit: how many leading exit bands' live tasks decide a level's exit
                                       //         (0: all of them; at 1 an exit level builds no band-1 bitmaps: RMAT-22
                                       //         / 24 / 26 at 0 / 1: 1.384 / 3.131 / 11.23 -> 1.385 / 3.102 / 11.12 ms,
-                                      //         the same decisions, profiles/r04/msbfs_exit/probe_band0.jsonl)
+                                      //         the same decisions; a repeat: 24 / 26 3.079 / 11.11 -> 3.066 / 11.11,
+                                      //         profiles/r04/msbfs_exit/probe_band0*.jsonl)
     int msbfs_skip_empty = 1;         //         bit-parallel BFS pull levels skip the rows without entries (no finalise)
     int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose exit bands had fewer
                                       //         live tasks than this permille builds the next top-down queue in its

@@ -1243,6 +1243,15 @@ __global__ void msbfs_zero_list_kernel(unsigned long long* __restrict__ v, const
         v[list[i]] = 0ull;
 }
 
+// The source rows at or past from (rows without pull entries) of a frontier vector: the only such rows
+// whose word can be nonzero after level 0 (one wave; n <= 64 distinct source rows)
+__global__ __launch_bounds__(kWave) void msbfs_zero_tail_sources_kernel(unsigned long long* __restrict__ v,
+                                                                       const int64_t* __restrict__ src, int n,
+                                                                       int64_t from) {
+    const int i = (int)threadIdx.x;
+    if (i < n && src[i] >= from) v[src[i]] = 0ull;
+}
+
 // Sharded top-down level, owner side: the peers' halo slots for own rows, received at the send-list
 // positions (rbuf[k] is about own row send_src[k]); own rows that gain a bit join the touched list
 // the local top-down kernel started (the first toucher of a word appends it, as there)
@@ -2819,8 +2828,17 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 JG_LAUNCH_CHECK();
                             }
                         } else if (level > 0) {  // level 0: F[1] is as the init zeroed it
-                            JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, (size_t)sh.rows * sizeof(unsigned long long),
-                                                  sh.stream));
+                            // rows without pull entries (msbfs_skip_empty) are never written after level 0: their
+                            // words are zero except an isolated source's level-0 word, cleared apart (RMAT-26:
+                            // 215 of 537 MB cleared)
+                            const int64_t ne = tune().msbfs_skip_empty && c.pull && c.pull->empty_from >= 0
+                                                   ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
+                            JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, (size_t)ne * sizeof(unsigned long long), sh.stream));
+                            if (ne < sh.rows && !td.src_rows.empty()) {
+                                msbfs_zero_tail_sources_kernel<<<1, kWave, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), td.srcs.get(), (int)td.src_rows.size(), ne);
+                                JG_LAUNCH_CHECK();
+                            }
                         }
                         td.nq_in = td.nq;
                         // a big level (one shard): the apply passes over every row instead of a touched list
