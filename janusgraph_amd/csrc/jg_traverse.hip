@@ -481,7 +481,7 @@ struct MsBfsOp {
         if (nwl) nwl[row] = nw;
         if (nw) {
             visited[row] |= nw;
-            *changed = 1;
+            if (changed) *changed = 1;
             while (nw) {
                 const int s = __ffsll(nw) - 1;
                 if (depth8) depth8[(int64_t)s * rows + row] = (uint8_t)lvl;
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_split_apply_kernel(const int32_t
         op.Fout[op.pos(u)] |= nw;
         op.visited[u] |= nw;
         if (op.nwl) op.nwl[u] |= nw;
-        *op.changed = 1;
+        if (op.changed) *op.changed = 1;
         while (nw) {
             const int s = __ffsll(nw) - 1;
             if (op.depth8) op.depth8[(int64_t)s * op.rows + u] = (uint8_t)op.lvl;
@@ -3047,7 +3047,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         const BfsCsrs c = pick_csrs(sh, direction);
                         const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
                         St& t = st[i];
-                        JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
+                        // (with the top-down path the frontier count ends the traversal: no changed flag, whose
+                        // one-word store every gaining row's wave would repeat)
+                        if (!td_ok) JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
                         MsBfsOp op;
                         op.F = t.F[cur].get();
                         op.Fout = t.F[cur ^ 1].get();
@@ -3055,7 +3057,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.depth = t.depth.get();
                         op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
                             op.nwl = level + 1 < kMsLevelWords && tune().msbfs_diag != 1 ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
-                        op.changed = t.changed.get();
+                        op.changed = td_ok ? nullptr : t.changed.get();
                         op.rows = sh.rows;
                         op.pos = g.vec_pos(sh, adj_of(sh, c));
                         op.lvl = level + 1;
