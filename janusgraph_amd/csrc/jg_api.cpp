@@ -717,6 +717,14 @@ int jg_tune_set(const char* key, int64_t value) {
         JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta / dobfs_alpha must be in [1, 1e6]");
         (k == "bfs_alpha" ? jg::tune().bfs_alpha : k == "bfs_beta" ? jg::tune().bfs_beta : jg::tune().dobfs_alpha) =
             (int)value;
+    } else if (k == "bfs_narrow") {
+        jg::tune().bfs_narrow = value != 0;
+    } else if (k == "nb_alpha") {
+        JG_ARG(value >= 1 && value <= 1000000, "nb_alpha must be in [1, 1e6]");
+        jg::tune().nb_alpha = (int)value;
+    } else if (k == "nb_first") {
+        JG_ARG(value >= 4 && value <= 4096, "nb_first must be in [4, 4096]");
+        jg::tune().nb_first = (int)value;
     } else if (k == "cc_push") {
         jg::tune().cc_push = value != 0;
     } else if (k == "band_sliced_build") {

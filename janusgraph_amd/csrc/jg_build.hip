@@ -1328,7 +1328,9 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
     }
     if (g.flags & JG_ADJ_BOTH) cc_prepare_ranks(g);  // ConnectedComponent's labels: a property of the ids
     int64_t bytes = 0;
-    for (auto& sp : g.shards) bytes += sp->in.bytes() + sp->out.bytes() + sp->both.bytes() + sp->out_degree.bytes();
+    for (auto& sp : g.shards)
+        bytes += sp->in.bytes() + sp->out.bytes() + sp->both.bytes() + sp->out_degree.bytes() + sp->cc_rank0.bytes();
+    bytes += g.cc_vor.bytes();  // the String-order id of each rank (~0.5 GB at RMAT-26)
     g.info.device_bytes = bytes;
     g.info.num_shards = P;
     g.info.flags = g.flags;

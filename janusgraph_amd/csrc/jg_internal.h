@@ -244,6 +244,15 @@ struct Shard {
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
+    // narrow bit-parallel BFS scratch (<= 8 sources, one shard; jg_narrow.hip), kept across calls
+    std::vector<DevBuf<uint8_t>> nb_level;   // [levels][rows + pad] each level's frontier byte (= its new bits)
+    DevBuf<uint8_t> nb_vis;                  // [rows] visited bits
+    DevBuf<unsigned long long> nb_rest;      // [ceil(rows/64)] rows the bottom-up first pass left unfinished
+    DevBuf<int32_t> nb_queue[2];             // [rows] top-down queues (level parity)
+    DevBuf<int64_t> nb_qoff[2];
+    DevBuf<unsigned long long> nb_ctr;       // per-level counters (NbCtr ring)
+    DevBuf<unsigned char> nb_state;          // per-level decisions (NbState ring)
+    DevBuf<const uint8_t*> nb_table;         // device copy of the level pointers (depth output)
 
     std::vector<hipEvent_t> prof_events;  // start/stop pairs for the dominant kernel
     std::vector<hipEvent_t> exch_events;  // start/stop pairs around the exchange steps
@@ -511,6 +520,20 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
 int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);
 // Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
 void bfs_buffers(Shard& sh);
+// Narrow bit-parallel direction-optimising BFS (jg_narrow.hip): 2..kNarrowMax sources on one shard,
+// one frontier byte per row, each source choosing its own direction every level.  push / pull: the
+// traversal's adjacencies (both present); src[s]: source s's local row (-1: not a vertex).  planes
+// (device, [ns][rows], nullable): the depths (-1 unreached).  Returns the levels run.
+constexpr int kNarrowMax = 8;
+struct NarrowRun {
+    int levels = 0;
+    float ms = 0;            // HIP-event time of the traversal (init to the last level)
+    double entries = 0;      // adjacency entries examined (top-down pushes + bottom-up scans)
+    double bytes = 0;        // algorithmic bytes of the examined work
+    double reached = 0;      // reached (source, row) pairs
+};
+NarrowRun narrow_bfs(Ctx& ctx, Shard& sh, const Csr& push, const Csr& pull, const int64_t* src, int ns, int max_depth,
+                     int32_t* planes);
 void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_t* init, int steps, int64_t* out,
                  uint8_t* received_out);
 
@@ -568,6 +591,9 @@ struct Tune {
                                       // 0.147 / 0.146 / 0.137 / 0.136 / 0.137 ms at 14 / 20 / 30 / 45 / 70;
                                       // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
+    int bfs_narrow = 1;               //         2..8 sources on one shard: the narrow byte-word engine (jg_narrow.hip)
+    int nb_alpha = 14;                //         its per-source top-down -> bottom-up threshold
+    int nb_first = 16;                //         its bottom-up first pass: entries a lane scans before a wave takes the row
     int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
     int msbfs_skip_first = 1;         //         bit-parallel BFS: no task bitmaps on the first pull level
     int msbfs_diag = 0;               //         diagnostic timing (wrong depths): 1 = no depth writes

@@ -2382,6 +2382,31 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         if (depth_rows && depth_rows[0]) rows_to_dense(g, sh, depth.get(), depth_rows[0]);
         if (keep) keep_rows(g, [](Shard& s) { return s.bfs_depth.get(); });
         prof_collect(ctx, g);
+    } else if (nsrc <= kNarrowMax && g.P == 1 && g.shards.size() == 1 && tune().bfs_narrow &&
+               pick_csrs(sh0, direction).push && pick_csrs(sh0, direction).pull) {
+        // 2..8 sources on one shard: the narrow engine (jg_narrow.hip), one frontier byte per row
+        Shard& sh = sh0;
+        const BfsCsrs c = pick_csrs(sh, direction);
+        std::vector<int64_t> loc((size_t)nsrc);
+        std::vector<int> shard((size_t)nsrc);
+        locals_of_vids(g, source_vids, nsrc, loc.data(), shard.data());
+        DevBuf<int32_t> planes;
+        if (depth_rows || keep) planes.alloc(std::max<int64_t>((int64_t)nsrc * sh.rows, 1));
+        const NarrowRun r = narrow_bfs(ctx, sh, *c.push, *c.pull, loc.data(), nsrc, max_depth,
+                                       planes.size() ? planes.get() : nullptr);
+        ctx.last.compute_ms = r.ms;
+        ctx.last.levels = r.levels;
+        ctx.last.supersteps = r.levels;
+        ctx.last.edges_traversed = r.entries;
+        ctx.last.algorithmic_bytes = r.bytes;
+        if (depth_rows)
+            for (int s = 0; s < nsrc; ++s)
+                if (depth_rows[s]) rows_to_dense(g, sh, planes.get() + (size_t)s * sh.rows, depth_rows[s]);
+        if (keep) {
+            sh.kept_depth.swap(planes);
+            g.kept_nsrc = nsrc;
+        }
+        prof_collect(ctx, g);
     } else {
         // bit-parallel BFS in batches of 64 sources; works sharded (frontier words allgathered)
         float total_ms = 0;
@@ -3050,6 +3075,15 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // (with the top-down path the frontier count ends the traversal: no changed flag, whose
                         // one-word store every gaining row's wave would repeat)
                         if (!td_ok) JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
+                        // rows without pull entries are not written by a pull level (msbfs_skip_empty): a source
+                        // among them keeps its level-0 word in this output vector unless cleared here, and the
+                        // frontier scan would count it (one extra level)
+                        if (td_ok && tune().msbfs_skip_empty && c.pull->empty_from >= 0 &&
+                            c.pull->empty_from < sh.rows && !tds[i].src_rows.empty()) {
+                            msbfs_zero_tail_sources_kernel<<<1, kWave, 0, sh.stream>>>(
+                                t.F[cur ^ 1].get(), tds[i].srcs.get(), (int)tds[i].src_rows.size(), c.pull->empty_from);
+                            JG_LAUNCH_CHECK();
+                        }
                         MsBfsOp op;
                         op.F = t.F[cur].get();
                         op.Fout = t.F[cur ^ 1].get();
