@@ -215,9 +215,9 @@ def _ptr(a):
 
 
 def tune_set(key: str, value: int):
-    """Process-wide performance knob (results are unaffected): pull_unroll, pull_nt, pull_lds,
-    slice_lds, pull_short, pull_overlap, and at graph build time pull_split, band<i>_deg, band<i>_bit,
-    halo (sharded graphs: compact vectors + sparse halo exchange instead of the dense allgather)."""
+    """Process-wide performance knob (results are unaffected; the list is jg_api.cpp jg_tune_set), e.g.
+    msbfs_exit, bfs_narrow, and at graph build time pull_split, band<i>_deg, band<i>_bit, halo (sharded
+    graphs: compact vectors + sparse halo exchange instead of the dense allgather)."""
     check(load().jg_tune_set(key.encode(), int(value)))
 
 

@@ -12,6 +12,7 @@
 #include <map>
 #include <mutex>
 
+#include "jg_cache.h"
 #include "jg_internal.h"
 
 namespace jg {
@@ -135,50 +136,29 @@ void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
     JG_HIP(hipStreamSynchronize(sh.stream));
 }
 
-// ---- the caching device allocator behind DevBuf (jg_common.h) ----
+// ---- the caching device allocator behind DevBuf (jg_common.h): jg_cache.h over HIP ----
 namespace {
-constexpr size_t kCacheBlockMax = 1ull << 30;  // larger blocks go straight to hipMalloc / hipFree
-constexpr size_t kCacheBytesMax = 16ull << 30; // per device: beyond it, synchronise and free half
-struct DevCache {
-    std::multimap<size_t, void*> ready;           // synchronised since their free: reusable
-    std::vector<std::pair<size_t, void*>> pending; // freed since the device's last synchronisation
-    size_t bytes = 0;                              // ready + pending
-};
-// never destroyed: a DevBuf released during process exit (after static destructors) still finds them
-std::mutex& g_cache_mu = *new std::mutex;
-std::map<int, DevCache>& g_cache = *new std::map<int, DevCache>;
-bool cache_off() {
-    static const bool off = std::getenv("JG_NO_DEVCACHE") != nullptr;
-    return off;
-}
-// size class: at most 1/8 above the request (granularity = a power of two >= 4 KiB, 1/8 of the
-// request's leading power of two)
-size_t cache_round(size_t b) {
-    size_t top = 1;
-    while (top * 2 <= b) top *= 2;
-    const size_t g = std::max<size_t>(4096, top / 8);
-    return (b + g - 1) / g * g;
-}
-void free_on(int dev, void* p) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    if (cur != dev) (void)hipSetDevice(dev);
-    (void)hipFree(p);
-    if (cur != dev) (void)hipSetDevice(cur);
-}
-// synchronise every device that holds cached memory (a block of one device may be read by another's
-// peer copy) and move dev's pending blocks taken before the synchronisation to ready; with `trim`, free
-// ready blocks until the cache holds at most half its cap
-void cache_sync_dev(int dev, bool trim) {
-    std::vector<std::pair<size_t, void*>> snap;
-    std::vector<int> devs;
-    {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        snap.swap(g_cache[dev].pending);
-        for (auto& kv : g_cache) devs.push_back(kv.first);
+struct HipBackend {
+    void* alloc(int dev, size_t bytes) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+        }
+        if (cur != dev) (void)hipSetDevice(cur);
+        return p;
     }
-    if (snap.empty() && !trim) return;
-    {
+    void release(int dev, void* p) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        (void)hipFree(p);
+        if (cur != dev) (void)hipSetDevice(cur);
+    }
+    void synchronize(const std::vector<int>& devs) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         for (int d : devs) {
@@ -187,92 +167,35 @@ void cache_sync_dev(int dev, bool trim) {
         }
         (void)hipSetDevice(cur);
     }
-    std::vector<void*> drop;
-    {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        DevCache& c = g_cache[dev];
-        for (auto& b : snap) c.ready.emplace(b.first, b.second);
-        while (trim && c.bytes > kCacheBytesMax / 2 && !c.ready.empty()) {
-            auto it = std::prev(c.ready.end());  // the largest first
-            c.bytes -= it->first;
-            drop.push_back(it->second);
-            c.ready.erase(it);
-        }
-    }
-    for (void* p : drop) free_on(dev, p);
+};
+// never destroyed: a DevBuf released during process exit (after static destructors) still finds it
+BlockCache<HipBackend>& cache() {
+    static BlockCache<HipBackend>* c = [] {
+        auto* b = new BlockCache<HipBackend>();
+        b->set_off(std::getenv("JG_NO_DEVCACHE") != nullptr);  // plain hipMalloc / hipFree
+        return b;
+    }();
+    return *c;
 }
+thread_local bool t_direct_free = false;  // DirectFree scope (jg_graph_destroy)
 }  // namespace
+
+DirectFree::DirectFree() : prev(t_direct_free) { t_direct_free = true; }
+DirectFree::~DirectFree() { t_direct_free = prev; }
 
 void* dev_alloc(size_t bytes) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const bool cached = !cache_off() && bytes <= kCacheBlockMax;
-    const size_t rb = cached ? cache_round(bytes) : bytes;
-    if (cached) {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        DevCache& c = g_cache[dev];
-        auto it = c.ready.find(rb);
-        if (it != c.ready.end()) {
-            void* p = it->second;
-            c.ready.erase(it);
-            c.bytes -= rb;
-            return p;
-        }
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, rb) != hipSuccess) {
-        (void)hipGetLastError();
-        dev_cache_release(dev);  // hand the cached blocks back, then try once more
-        p = nullptr;
-        if (hipMalloc(&p, rb) != hipSuccess) {
-            (void)hipGetLastError();
-            return nullptr;
-        }
-    }
-    return p;
+    return cache().alloc(dev, bytes);
 }
 
-void dev_free(void* p, size_t bytes, int dev) {
-    if (!p) return;
-    if (cache_off() || bytes > kCacheBlockMax) {
-        free_on(dev, p);
-        return;
-    }
-    bool over = false;
-    {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        DevCache& c = g_cache[dev];
-        const size_t rb = cache_round(bytes);
-        c.pending.emplace_back(rb, p);
-        c.bytes += rb;
-        over = c.bytes > kCacheBytesMax;
-    }
-    if (over) cache_sync_dev(dev, true);
-}
+void dev_free(void* p, size_t bytes, int dev) { cache().free(dev, p, bytes, t_direct_free); }
 
-void dev_cache_sync() {
-    std::vector<int> devs;
-    {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        for (auto& kv : g_cache)
-            if (!kv.second.pending.empty()) devs.push_back(kv.first);
-    }
-    for (int d : devs) cache_sync_dev(d, false);
-}
+void dev_cache_sync() { cache().sync(); }
 
-void dev_cache_release(int dev) {
-    cache_sync_dev(dev, false);
-    std::vector<void*> drop;
-    {
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        DevCache& c = g_cache[dev];
-        for (auto& kv : c.ready) drop.push_back(kv.second);
-        c.ready.clear();
-        c.bytes = 0;
-        for (auto& b : c.pending) c.bytes += b.first;
-    }
-    for (void* p : drop) free_on(dev, p);
-}
+void dev_cache_release(int dev) { cache().release(dev); }
+
+void dev_cache_drop_ready(int dev) { cache().drop_ready(dev); }
 
 uint64_t allreduce_or_u64(Graph& g, uint64_t v) {
     Ctx& c = *g.ctx;
@@ -322,18 +245,6 @@ Tune& tune() {
     return t;
 }
 
-SideStream& side_stream() {
-    static SideStream cache[64];
-    int dev = 0;
-    JG_HIP(hipGetDevice(&dev));
-    SideStream& ss = cache[dev & 63];
-    if (!ss.stream) {
-        JG_HIP(hipStreamCreateWithFlags(&ss.stream, hipStreamNonBlocking));
-        JG_HIP(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
-        JG_HIP(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
-    }
-    return ss;
-}
 
 int device_cu_count() {
     static int cache[64] = {0};
@@ -668,198 +579,80 @@ int jg_tune_set(const char* key, int64_t value) {
     JG_GUARD_BEGIN
     JG_ARG(key, "null key");
     const std::string k(key);
-    if (k == "pull_unroll") {
-        JG_ARG(value == 4 || value == 8, "pull_unroll must be 4 or 8");
-        jg::tune().pull_unroll = (int)value;
-    } else if (k == "pull_nt") {
-        jg::tune().pull_nt = value != 0;
-    } else if (k == "pull_lds") {
-        JG_ARG(value >= 0, "pull_lds must be >= 0");
-        jg::tune().pull_lds = value;
-    } else if (k == "fin_last") {
-        jg::tune().fin_last = value != 0;
-    } else if (k == "merge_wgs") {
-        JG_ARG(value == 1 || value == 2, "merge_wgs must be 1 or 2");
-        jg::tune().merge_wgs = (int)value;
-    } else if (k == "merge_overlap") {
-        jg::tune().merge_overlap = value != 0;
-    } else if (k == "light_lds") {
-        JG_ARG(value >= 0, "light_lds must be >= 0");
-        jg::tune().light_lds = value;
-    } else if (k.rfind("band", 0) == 0 && k.size() == 9 && k[4] >= '0' && k[4] <= '3' &&
-               (k.substr(5) == "_deg" || k.substr(5) == "_bit" || k.substr(5) == "_sub")) {
+    jg::Tune& t = jg::tune();
+    // int knobs: name, field, allowed range
+    struct Knob {
+        const char* name;
+        int* field;
+        int64_t lo, hi;
+    };
+    const Knob knobs[] = {
+        {"pull_split", &t.pull_split, 0, 1},
+        {"halo", &t.halo, 0, 1},
+        {"bfs_alpha", &t.bfs_alpha, 1, 1000000},
+        {"dobfs_alpha", &t.dobfs_alpha, 1, 1000000},
+        {"bfs_beta", &t.bfs_beta, 1, 1000000},
+        {"bfs_narrow", &t.bfs_narrow, 0, 1},
+        {"nb_alpha", &t.nb_alpha, 1, 1000000},
+        {"nb_first", &t.nb_first, 4, 4096},
+        {"cc_push", &t.cc_push, 0, 1},
+        {"msbfs_sparse", &t.msbfs_sparse, 0, 1},
+        {"msbfs_td", &t.msbfs_td, 0, 2},
+        {"cc_first", &t.cc_first, 1, 64},
+        {"msbfs_skip", &t.msbfs_skip, 0, 1},
+        {"msbfs_exit", &t.msbfs_exit, 0, 2},
+        {"msbfs_td_rowapply", &t.msbfs_td_rowapply, 0, 1024},
+        {"msbfs_td_noprobe", &t.msbfs_td_noprobe, 0, 1000},
+        {"msbfs_scan_queue", &t.msbfs_scan_queue, 0, 1001},
+        {"msbfs_exit_first", &t.msbfs_exit_first, 1, 256},
+        {"msbfs_exit_live", &t.msbfs_exit_live, 0, 1000},
+        {"cc_uf", &t.cc_uf, 0, 1},
+        {"cc_uf_sharded", &t.cc_uf_sharded, 0, 1},
+        {"cc_uf_search", &t.cc_uf_search, 0, 1},
+        {"msbfs_split", &t.msbfs_split, 0, 1},
+        {"sharded_bfs", &t.sharded_bfs, 0, 1},
+        {"bfs_td_split", &t.bfs_td_split, 0, 2},
+        {"bfs_td_split_levels", &t.bfs_td_split_levels, 0, 0xffff},
+        {"bfs_batch0", &t.bfs_batch0, 1, 64},
+        {"bfs_grid_mult", &t.bfs_grid_mult, 1, 64},
+        {"bfs_grid", &t.bfs_grid, 64, 65536},
+        {"bfs_tail_grid", &t.bfs_tail_grid, 0, 65536},
+        {"merge_temporal", &t.merge_temporal, 0, 2},
+    };
+    for (const Knob& kn : knobs) {
+        if (k != kn.name) continue;
+        if (value < kn.lo || value > kn.hi)
+            jg::fail(JG_ERR_ARG, k + " must be in [" + std::to_string(kn.lo) + ", " + std::to_string(kn.hi) + "]");
+        *kn.field = (int)value;
+        return JG_OK;
+    }
+    if (k.rfind("band", 0) == 0 && k.size() == 9 && k[4] >= '0' && k[4] <= '3' &&
+        (k.substr(5) == "_deg" || k.substr(5) == "_bit" || k.substr(5) == "_sub")) {
         // band<i>_deg: minimum degree (0: band unused); band<i>_bit: log2 sub-slices (0: automatic);
         // band<i>_sub: sub-slices, a power of two in [1, 256]
         const int i = k[4] - '0';
         if (k.substr(5) == "_deg") {
             JG_ARG(value >= 0, "band degree must be >= 0");
-            jg::tune().band_deg[i] = value;
+            t.band_deg[i] = value;
         } else if (k.substr(5) == "_bit") {
             JG_ARG(value == 0 || (value >= 3 && value <= 8), "band bits must be 0 (automatic) or in [3, 8]");
-            jg::tune().band_bits[i] = value == 0 ? -1 : (int)value;
+            t.band_bits[i] = value == 0 ? -1 : (int)value;
         } else {
             JG_ARG(value >= 1 && value <= 256 && (value & (value - 1)) == 0, "band sub-slices must be a power of two in [1, 256]");
             int b = 0;
             while ((1 << b) < value) ++b;
-            jg::tune().band_bits[i] = b;
+            t.band_bits[i] = b;
         }
-    } else if (k == "pull_split") {
-        jg::tune().pull_split = value != 0;
-    } else if (k == "pull_short") {
-        jg::tune().pull_short = value != 0;
-    } else if (k == "pull_overlap") {
-        jg::tune().pull_overlap = value != 0;
-    } else if (k == "slice_lds") {
-        jg::tune().slice_lds = value != 0;
-    } else if (k == "halo") {
-        jg::tune().halo = value != 0;
-    } else if (k == "bfs_alpha" || k == "bfs_beta" || k == "dobfs_alpha") {
-        JG_ARG(value >= 1 && value <= 1000000, "bfs_alpha / bfs_beta / dobfs_alpha must be in [1, 1e6]");
-        (k == "bfs_alpha" ? jg::tune().bfs_alpha : k == "bfs_beta" ? jg::tune().bfs_beta : jg::tune().dobfs_alpha) =
-            (int)value;
-    } else if (k == "bfs_narrow") {
-        jg::tune().bfs_narrow = value != 0;
-    } else if (k == "nb_alpha") {
-        JG_ARG(value >= 1 && value <= 1000000, "nb_alpha must be in [1, 1e6]");
-        jg::tune().nb_alpha = (int)value;
-    } else if (k == "nb_first") {
-        JG_ARG(value >= 4 && value <= 4096, "nb_first must be in [4, 4096]");
-        jg::tune().nb_first = (int)value;
-    } else if (k == "cc_push") {
-        jg::tune().cc_push = value != 0;
-    } else if (k == "band_sliced_build") {
-        jg::tune().band_sliced_build = value != 0;
-    } else if (k == "msbfs_skip_first") {
-        jg::tune().msbfs_skip_first = value != 0;
-    } else if (k == "msbfs_diag") {
-        JG_ARG(value >= 0 && value <= 1, "msbfs_diag must be 0 or 1");
-        jg::tune().msbfs_diag = (int)value;
-    } else if (k == "msbfs_sparse") {
-        jg::tune().msbfs_sparse = value != 0;
-    } else if (k == "msbfs_td") {
-        JG_ARG(value >= 0 && value <= 2, "msbfs_td must be 0 (off), 1 (one shard and sharded) or 2 (one shard only)");
-        jg::tune().msbfs_td = (int)value;
-    } else if (k == "cc_first") {
-        JG_ARG(value >= 1 && value <= 64, "cc_first must be in [1, 64]");
-        jg::tune().cc_first = (int)value;
-    } else if (k == "msbfs_bu") {
-        JG_ARG(value >= 0 && value <= 3, "msbfs_bu must be 0, 1, 2 or 3");
-        jg::tune().msbfs_bu = (int)value;
-    } else if (k == "msbfs_exit") {
-        JG_ARG(value >= 0 && value <= 2, "msbfs_exit must be 0, 1 or 2");
-        jg::tune().msbfs_exit = (int)value;
-    } else if (k == "msbfs_exit_bands") {
-        JG_ARG(value >= 1 && value <= 4, "msbfs_exit_bands must be in [1, 4]");
-        jg::tune().msbfs_exit_bands = (int)value;
-    } else if (k == "msbfs_exit_probe") {
-        JG_ARG(value >= 0 && value <= 4, "msbfs_exit_probe must be in [0, 4]");
-        jg::tune().msbfs_exit_probe = (int)value;
-    } else if (k == "msbfs_td_rowapply") {
-        JG_ARG(value >= 0 && value <= 1024, "msbfs_td_rowapply must be in [0, 1024]");
-        jg::tune().msbfs_td_rowapply = (int)value;
-    } else if (k == "msbfs_td_noprobe") {
-        JG_ARG(value >= 0 && value <= 1000, "msbfs_td_noprobe must be in [0, 1000]");
-        jg::tune().msbfs_td_noprobe = (int)value;
-    } else if (k == "msbfs_srcsplit") {
-        JG_ARG(value >= 0 && value <= 2, "msbfs_srcsplit must be 0, 1 or 2");
-        jg::tune().msbfs_srcsplit = (int)value;
-    } else if (k == "msbfs_srcsplit_permille") {
-        JG_ARG(value >= 0 && value <= 1000, "msbfs_srcsplit_permille must be in [0, 1000]");
-        jg::tune().msbfs_srcsplit_permille = (int)value;
-    } else if (k == "msbfs_skip_empty") {
-        jg::tune().msbfs_skip_empty = value != 0;
-    } else if (k == "msbfs_scan_queue") {
-        JG_ARG(value >= 0 && value <= 1001, "msbfs_scan_queue must be in [0, 1001]");
-        jg::tune().msbfs_scan_queue = (int)value;
-    } else if (k == "msbfs_exit_first") {
-        JG_ARG(value >= 1 && value <= 256, "msbfs_exit_first must be in [1, 256]");
-        jg::tune().msbfs_exit_first = (int)value;
-    } else if (k == "msbfs_exit_all") {
-        jg::tune().msbfs_exit_all = value != 0;
-    } else if (k == "msbfs_exit_live") {
-        JG_ARG(value >= 0 && value <= 1000, "msbfs_exit_live must be in [0, 1000]");
-        jg::tune().msbfs_exit_live = (int)value;
-    } else if (k == "msbfs_bu_tasks") {
-        JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_tasks must be in [0, 1000]");
-        jg::tune().msbfs_bu_tasks = (int)value;
-    } else if (k == "msbfs_bu_frac") {
-        JG_ARG(value >= 0 && value <= 1000, "msbfs_bu_frac must be in [0, 1000]");
-        jg::tune().msbfs_bu_frac = (int)value;
-    } else if (k == "msbfs_skip") {
-        jg::tune().msbfs_skip = value != 0;
-    } else if (k == "cc_uf_search") {
-        jg::tune().cc_uf_search = value != 0;
-    } else if (k == "cc_uf_sharded") {
-        jg::tune().cc_uf_sharded = value != 0;
-    } else if (k == "cc_uf") {
-        jg::tune().cc_uf = value != 0;
-    } else if (k == "msbfs_split") {
-        jg::tune().msbfs_split = value != 0;
-    } else if (k == "sharded_bfs") {
-        jg::tune().sharded_bfs = value != 0;
-    } else if (k == "bfs_tail_grid") {
-        JG_ARG(value >= 0 && value <= 65536, "bfs_tail_grid must be in [0, 65536]");
-        jg::tune().bfs_tail_grid = (int)value;
-    } else if (k == "bfs_grid") {
-        JG_ARG(value >= 64 && value <= 65536, "bfs_grid must be in [64, 65536]");
-        jg::tune().bfs_grid = (int)value;
-    } else if (k == "fuse_finalize") {
-        jg::tune().fuse_finalize = value != 0;
-    } else if (k == "relabel_ties") {
-        jg::tune().relabel_ties = value != 0;
-    } else if (k == "relabel_dead_last") {
-        jg::tune().relabel_dead_last = value != 0;
-    } else if (k == "relabel_out_ties") {
-        jg::tune().relabel_out_ties = value != 0;
-    } else if (k == "pr_rank_last") {
-        jg::tune().pr_rank_last = value != 0;
-    } else if (k == "pr_skip_empty") {
-        jg::tune().pr_skip_empty = value != 0;
     } else if (k.size() == 12 && k.compare(0, 11, "merge_stage") == 0 && k[11] >= '0' && k[11] <= '3') {
         JG_ARG(value == -1 || value == 0 || value == 64 || value == 128 || value == 256 || value == 512,
                "merge_stage<i> must be -1 (automatic), 0, 64, 128, 256 or 512");
-        jg::tune().merge_stage[k[11] - '0'] = (int)value;
-    } else if (k == "bfs_init_suffix") {
-        jg::tune().bfs_init_suffix = value != 0;
-    } else if (k == "bfs_grow_rule") {
-        jg::tune().bfs_grow_rule = value != 0;
-    } else if (k == "bfs_td_split") {
-        JG_ARG(value >= 0 && value <= 2, "bfs_td_split must be 0, 1 or 2");
-        jg::tune().bfs_td_split = (int)value;
-    } else if (k == "bfs_td_split_levels") {
-        JG_ARG(value >= 0 && value <= 0xffff, "bfs_td_split_levels must be a mask of levels 0..15");
-        jg::tune().bfs_td_split_levels = (int)value;
-    } else if (k == "bfs_td_split_min") {
-        JG_ARG(value >= 1 && value <= INT32_MAX, "bfs_td_split_min must be in [1, 2^31)");
-        jg::tune().bfs_td_split_min = value;
-    } else if (k == "bfs_td_split_max") {
-        JG_ARG(value >= 1 && value <= INT32_MAX, "bfs_td_split_max must be in [1, 2^31)");
-        jg::tune().bfs_td_split_max = value;
-    } else if (k == "bfs_batch0") {
-        JG_ARG(value >= 1 && value <= 64, "bfs_batch0 must be in [1, 64]");
-        jg::tune().bfs_batch0 = (int)value;
-    } else if (k == "bfs_grid_mult") {
-        JG_ARG(value >= 1 && value <= 64, "bfs_grid_mult must be in [1, 64]");
-        jg::tune().bfs_grid_mult = (int)value;
-    } else if (k == "bfs_wave_stage") {
-        jg::tune().bfs_wave_stage = value != 0;
-    } else if (k == "merge_interleave") {
-        jg::tune().merge_interleave = value != 0;
-    } else if (k == "merge_dynamic") {
-        jg::tune().merge_dynamic = value != 0;
-    } else if (k == "fin_pipe") {
-        jg::tune().fin_pipe = value != 0;
+        t.merge_stage[k[11] - '0'] = (int)value;
+    } else if (k == "bfs_td_split_min" || k == "bfs_td_split_max") {
+        JG_ARG(value >= 1 && value <= INT32_MAX, "bfs_td_split_min / _max must be in [1, 2^31)");
+        (k == "bfs_td_split_min" ? t.bfs_td_split_min : t.bfs_td_split_max) = value;
     } else if (k == "merge_pack") {
         JG_ARG(value == 0 || value == 1 || value == 24, "merge_pack must be 0 (32 bits), 1 (automatic) or 24 (at least 24)");
-        jg::tune().merge_pack = (int)value;
-    } else if (k == "light_runs") {
-        jg::tune().light_runs = value != 0;
-    } else if (k == "merge_diag") {
-        JG_ARG(value >= 0 && value <= 4, "merge_diag must be in [0, 4]");
-        jg::tune().merge_diag = (int)value;
-    } else if (k == "merge_temporal") {
-        JG_ARG(value >= 0 && value <= 2, "merge_temporal must be 0, 1 (automatic) or 2");
-        jg::tune().merge_temporal = (int)value;
+        t.merge_pack = (int)value;
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }
@@ -1363,10 +1156,16 @@ int jg_graph_destroy(jg_graph* g) {
         (void)hipStreamSynchronize(sp->stream);
         if (std::find(devs.begin(), devs.end(), sp->device) == devs.end()) devs.push_back(sp->device);
     }
-    delete g;
-    // the snapshot's device memory goes back to the device, not to the library's block cache (ADVICE r03:
-    // a dropped snapshot must not keep memory from other users of the device for the context's lifetime)
-    for (int d : devs) jg::dev_cache_release(d);
+    // The snapshot's device memory goes back to the device, not to the library's block cache (ADVICE r03:
+    // a dropped snapshot must not keep memory from other users of the device for the context's lifetime).
+    // Its streams are synchronised above, so its blocks are freed directly, and the cache's ready blocks
+    // go back without a device-wide synchronisation (that blocked on other contexts' work);
+    // blocks other callers freed and not yet synchronised stay pending.
+    {
+        jg::DirectFree direct;
+        delete g;
+    }
+    for (int d : devs) jg::dev_cache_drop_ready(d);
     JG_GUARD_END
 }
 

@@ -223,13 +223,12 @@ __global__ void nbr_min_kernel(const int32_t* __restrict__ src, const int32_t* _
 // a vertex without pull neighbours (in-degree 0: all of them tie in degree) is ordered by its out-degree
 // instead, descending: the rarely gathered sources among the in-degree-0 rows (~9% of the vertices,
 // <1% of the gathers) sit together at the front of that class instead of spread over all of it
-// `out_ties` (tune relabel_out_ties): every tie is ordered by out-degree (gather count), descending, so the
-// gathered vector's lines hold values of like heat (nbr_min unused)
+// (Ordering every tie by out-degree instead measured +0.9% / +0.6% at RMAT-24 / 26, round 4.)
 __global__ void tie_keys_kernel(const int32_t* __restrict__ nbr_min, int64_t n, int vbits,
-                                const int32_t* __restrict__ gather_deg, int64_t max_gather, bool out_ties,
+                                const int32_t* __restrict__ gather_deg, int64_t max_gather,
                                 uint64_t* __restrict__ keys) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
-        int64_t t = out_ties ? n : (nbr_min[v] >= n ? n : nbr_min[v]);
+        int64_t t = nbr_min[v] >= n ? n : nbr_min[v];
         if (t == n && gather_deg) t = max_gather - (gather_deg[v] < max_gather ? gather_deg[v] : max_gather);
         keys[v] = ((uint64_t)t << vbits) | (uint64_t)v;
     }
@@ -307,7 +306,6 @@ struct SelectArgs {
     int r;
     int which;
     int cbits;
-    int sbits;  // 0, or 8: entries of a row ordered by (sub_key(col), col)
     CompactMap cm;  // sharded pull adjacency with a halo plan: columns become compact ids
 };
 
@@ -382,15 +380,13 @@ __global__ __launch_bounds__(kBlock) void select_write_kernel(SelectArgs a, cons
         const bool own_d = (gd / a.S) == a.r, own_s = (gs / a.S) == a.r;
         if ((a.which == 1 || a.which == 2) && own_s) {
             const int64_t c = a.cm.on() ? (int64_t)a.cm(gd) : gd;
-            keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? sub_key(c) : 0) << a.cbits) | (uint64_t)c;
+            keys[pos] = ((uint64_t)(gs - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)c;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
         if ((a.which == 0 || a.which == 2) && own_d) {
             const int64_t c = a.cm.on() ? (int64_t)a.cm(gs) : gs;
-            keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << (a.cbits + a.sbits)) |
-                        ((uint64_t)(a.sbits ? sub_key(c) : 0) << a.cbits) | (uint64_t)c;
+            keys[pos] = ((uint64_t)(gd - (int64_t)a.r * a.S) << a.cbits) | (uint64_t)c;
             if (eidx) eidx[pos] = (uint32_t)e;
             ++pos;
         }
@@ -576,18 +572,17 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
     DevBuf<uint32_t> eidx;
     const int64_t nnz = select_keys(a, keys, eidx, weight != nullptr, s);
     const int rbits = bits_for((uint64_t)std::max<int64_t>(sh.rows - 1, 0));
-    if (rbits + a.cbits + a.sbits > 64) fail(JG_ERR_UNSUPPORTED, "CSR sort key exceeds 64 bits");
-    prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits + a.sbits, s);
+    if (rbits + a.cbits > 64) fail(JG_ERR_UNSUPPORTED, "CSR sort key exceeds 64 bits");
+    prim::radix_sort(keys.get(), weight ? eidx.get() : nullptr, nnz, rbits + a.cbits, s);
     csr.rows = sh.rows;
     csr.nnz = nnz;
-    csr.sliced = a.sbits != 0;
     csr.row_ptr.alloc(sh.rows + 1);
     csr.col.alloc(std::max<int64_t>(nnz, 1));
     if (weight) csr.weight.alloc(std::max<int64_t>(nnz, 1));
     fill_i64_kernel<<<grid_for(sh.rows + 1), kBlock, 0, s>>>(csr.row_ptr.get(), sh.rows + 1, nnz);
     JG_LAUNCH_CHECK();
     if (nnz > 0) {
-        csr_from_sorted_kernel<<<grid_for(nnz), kBlock, 0, s>>>(keys.get(), nnz, a.cbits, a.cbits + a.sbits,
+        csr_from_sorted_kernel<<<grid_for(nnz), kBlock, 0, s>>>(keys.get(), nnz, a.cbits, a.cbits,
                                                                 csr.row_ptr.get(),
                                                                 csr.col.get(), weight ? eidx.get() : nullptr, weight,
                                                                 weight ? csr.weight.get() : nullptr);
@@ -597,32 +592,6 @@ static void build_csr(Shard& sh, const SelectArgs& a, const int32_t* weight, Csr
 }
 
 // ---------------- the sliced split (SliceBand) ----------------
-// len[h * NR + i] = entries of band row R0 + i in sub-slice h (the row's entries are ordered by
-// sub_key = bit-reversed hash, so sub-slice h of a 2^b band is the key range brev_b(h) << (8 - b)).
-__global__ void band_len_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t R0,
-                                int64_t NR, int bits, uint32_t* __restrict__ off, int32_t* __restrict__ len) {
-    const int64_t S = 1ll << bits;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < S * NR; x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = x % NR;
-        const int h = (int)(x / NR);
-        const int64_t b = rp[R0 + i], e = rp[R0 + i + 1];
-        const uint32_t k0 = brev_bits((uint32_t)h, bits) << (8 - bits);
-        const uint32_t k1 = k0 + (1u << (8 - bits));
-        auto first_at_least = [&](uint32_t key) {
-            int64_t lo = b, hi = e;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (sub_key(col[mid]) < key) lo = mid + 1; else hi = mid;
-            }
-            return lo;
-        };
-        const int64_t j0 = first_at_least(k0);
-        const int64_t j1 = k1 >= 256 ? e : first_at_least(k1);
-        off[x] = (uint32_t)(j0 - b);
-        len[x] = (int32_t)(j1 - j0);
-    }
-}
-
 // Sub-rows from the column-ordered CSR (round 3: the bands used to be cut from a second, sub-slice-
 // ordered build of the whole CSR).  One wave per band row; a sub-row keeps its entries in the row's
 // (column) order.  Wave-private LDS: the fences only keep the compiler from moving LDS accesses across
@@ -702,19 +671,6 @@ __global__ void band_ptr_kernel(const int64_t* __restrict__ raw, int64_t NR, int
     }
 }
 
-// band col[sp[h][i] ...] = the sub-slice-h entries of band row i (one wave per sub-row)
-__global__ void band_copy_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t R0,
-                                 int64_t NR, int S, const uint32_t* __restrict__ off, const int64_t* __restrict__ sp,
-                                 int32_t* __restrict__ bcol) {
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; x < NR * S; x += waves) {
-        const int64_t h = x / NR, i = x % NR;
-        const int64_t src = rp[R0 + i] + off[x];
-        const int64_t* p = sp + h * (NR + 1) + i;
-        const int64_t dst = p[0], n = p[1] - p[0];
-        for (int64_t k = lane_id(); k < n; k += kWave) bcol[dst + k] = col[src + k];
-    }
-}
 
 __global__ void nonempty_kernel(const int32_t* __restrict__ len, int64_t n, int32_t* __restrict__ flag) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -831,13 +787,7 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     const int64_t NS = NR * S;
     DevBuf<int32_t> len(NS);
     DevBuf<int64_t> raw(NS + 1);
-    DevBuf<uint32_t> off;
-    if (csr.sliced) {  // rows ordered by sub-slice: the sub-rows are runs (binary search)
-        off.alloc(NS);
-        band_len_kernel<<<grid_for(NS), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, off.get(), len.get());
-    } else {
-        band_count_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, len.get());
-    }
+    band_count_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits, len.get());
     JG_LAUNCH_CHECK();
     prim::exclusive_scan(len.get(), raw.get(), NS, s);
     std::vector<int64_t> bounds(S + 1), begin(S), end(S), base(S + 1);
@@ -869,12 +819,8 @@ static void build_band(Shard& sh, const Csr& csr, SliceBand& bd, int64_t col_spa
     JG_LAUNCH_CHECK();
     bd.col.alloc(at + kMergeTask);  // one task of padding: the last task's aligned loads
     JG_HIP(hipMemsetAsync(bd.col.get(), 0, bd.col.bytes(), s));
-    if (csr.sliced)
-        band_copy_kernel<<<grid_for(NS * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, S, off.get(),
-                                                                 sp.get(), bd.col.get());
-    else
-        band_scatter_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits,
-                                                                    sp.get(), bd.col.get());
+    band_scatter_kernel<<<grid_for(NR * kWave), kBlock, 0, s>>>(csr.row_ptr.get(), csr.col.get(), R0, NR, bd.bits,
+                                                                sp.get(), bd.col.get());
     JG_LAUNCH_CHECK();
     // number the non-empty sub-rows
     DevBuf<int32_t> flag(NS);
@@ -999,8 +945,8 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     for (int c = 0; c < kNumClasses; ++c) fb[c] = (unsigned long long)rows;
     fb[kNumClasses] = 0;  // 1 + last non-empty row
     BandThresholds bt{};
-    // bands only when the split is enabled at build time (cut from a column-ordered CSR by counting, or
-    // from a sub-slice-ordered one by binary search: Tune::band_sliced_build)
+    // bands only when the split is enabled at build time (cut from the column-ordered CSR by counting;
+    // cutting them from a second, sub-slice-ordered build cost a select and a sort more, round 3)
     if (tune().pull_split)
         for (int i = 0; i < 4 && tune().band_deg[i] > 0; ++i) bt.thr[bt.n++] = std::max<int64_t>(tune().band_deg[i], 1);
     for (int i = 0; i < 4; ++i) fb[kNumClasses + 1 + i] = (unsigned long long)rows;
@@ -1066,7 +1012,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     plan.runs = false;
     {
         const int64_t lo = plan.light_row_begin[kZeroClass - 1], hi = plan.light_row_end[kZeroClass - 1];
-        if (tune().light_runs && hi > lo && c_class_thr_host[kZeroClass - 2] == kRunMax + 1) {
+        if (hi > lo && c_class_thr_host[kZeroClass - 2] == kRunMax + 1) {
             int64_t st[17];
             for (int i = 0; i < 17; ++i) st[i] = -1;
             st[0] = 0;
@@ -1211,23 +1157,20 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
             relabel_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(din, dout, n, mode, maxdeg, vbits, rkeys.get());
             JG_LAUNCH_CHECK();
             prim::radix_sort(rkeys.get(), nullptr, n, vbits + bits_for((uint64_t)maxdeg), s);
-            if (tune().relabel_ties && mode != 2 && pull.m > 0) {
+            if (mode != 2 && pull.m > 0) {
                 // equal-degree vertices ordered by their hottest pull neighbour (then id)
                 const uint64_t vmask = (1ull << vbits) - 1ull;
                 DevBuf<int32_t> rank1(n), nbr_min(n);
                 rank_scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(rkeys.get(), n, vmask, rank1.get());
                 JG_LAUNCH_CHECK();
-                const bool dead_last = mode == 0 && tune().relabel_dead_last;  // PageRank's gathered vector
-                const bool out_ties = dead_last && tune().relabel_out_ties;
-                if (!out_ties) {
-                    JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
-                    nbr_min_kernel<<<grid_for(pull.m, kBlock, 256 * 16), kBlock, 0, s>>>(pull.src, pull.dst, pull.m,
-                                                                                          mode, rank1.get(), nbr_min.get());
-                    JG_LAUNCH_CHECK();
-                }
+                const bool dead_last = mode == 0;  // PageRank's gathered vector
+                JG_HIP(hipMemsetAsync(nbr_min.get(), 0x7F, nbr_min.bytes(), s));  // > any rank
+                nbr_min_kernel<<<grid_for(pull.m, kBlock, 256 * 16), kBlock, 0, s>>>(pull.src, pull.dst, pull.m,
+                                                                                      mode, rank1.get(), nbr_min.get());
+                JG_LAUNCH_CHECK();
                 DevBuf<uint64_t> k1(n), k2(n);
                 tie_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(nbr_min.get(), n, vbits, dead_last ? dout : nullptr,
-                                                               std::min<int64_t>((int64_t)hc[3], n), out_ties, k1.get());
+                                                               std::min<int64_t>((int64_t)hc[3], n), k1.get());
                 JG_LAUNCH_CHECK();
                 prim::radix_sort(k1.get(), nullptr, n, vbits + bits_for((uint64_t)n), s);
                 tie_deg_keys_kernel<<<grid_for(n), kBlock, 0, s>>>(k1.get(), n, vmask, din, dout, mode, maxdeg,
@@ -1257,7 +1200,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                                                                      r, sh.rows, sh.out_degree.get());
             JG_LAUNCH_CHECK();
         }
-        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, 0, CompactMap{}};
+        SelectArgs a{e.src[li], e.dst[li], padded.get(), m, g.S, r, 0, cbits, CompactMap{}};
         const int32_t* w = (e.weight.size() > li) ? e.weight[li] : nullptr;
         auto use = [&](const EdgeList& l) {
             a.src = l.src;
@@ -1281,9 +1224,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                 vec_entries = sh.rows + halo.recv_off[P];
             }
             a.cbits = std::max(cbits, bits_for((uint64_t)(col_space - 1)));  // compact ids may exceed P*S
-            // round 3: one column-ordered build, the bands cut from it (band_count / band_scatter); the
-            // sub-slice-ordered first build (band_sliced_build = 1) cost a second select and sort
-            a.sbits = tune().pull_split && tune().band_sliced_build ? 8 : 0;
+            // round 3: one column-ordered build, the bands cut from it (band_count / band_scatter)
             build_csr(sh, a, wt, csr, s);
             // the gathered vector of the split: PageRank's fp64 contributions (IN), CC's int32 labels (BOTH)
             build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 2 ? 4 : 8);
@@ -1291,10 +1232,6 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
                 plan.lds_ok = true;
                 plan.seg_tbits = halo.tbits;
                 plan.nseg = P;
-            }
-            if (a.sbits) {
-                a.sbits = 0;
-                build_csr(sh, a, wt, csr, s);
             }
             if (halo.on) release_halo_maps(halo);
             a.cm = CompactMap{};

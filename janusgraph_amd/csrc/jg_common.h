@@ -28,17 +28,25 @@ void hip_check(hipError_t e, const char* what, const char* file, int line);
 #define JG_HIP(call) ::jg::hip_check((call), #call, __FILE__, __LINE__)
 #define JG_LAUNCH_CHECK() ::jg::hip_check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)
 
-// Device memory behind DevBuf (jg_api.cpp).  hipFree synchronises the whole device, and a snapshot
-// build frees ~240 temporaries (RMAT-20: 9.6 ms of a 49 ms build went to hipFree), so freed blocks of
-// up to 1 GiB are kept per device and size class instead.  A freed block is "pending" until the
-// device has been synchronised once after its free (dev_cache_sync: at the end of every entry point
-// that left blocks pending); only synchronised blocks are handed out again, so a block is never reused
-// while work queued before its free may still touch it (what hipFree guaranteed per call).
+// Device memory behind DevBuf (jg_api.cpp over jg_cache.h).  hipFree synchronises the whole device,
+// and a snapshot build frees ~240 temporaries (RMAT-20: 9.6 ms of a 49 ms build went to hipFree), so
+// freed blocks of up to 1 GiB are kept per device and size class instead.  A freed block is "pending"
+// until the device has been synchronised once after its free (dev_cache_sync: at the end of every entry
+// point that left blocks pending); only synchronised blocks are handed out again, so a block is never
+// reused while work queued before its free may still touch it (what hipFree guaranteed per call).
 // JG_NO_DEVCACHE=1 in the environment restores plain hipMalloc / hipFree.
 void* dev_alloc(size_t bytes);                 // current device; nullptr when the device is out of memory
 void dev_free(void* p, size_t bytes, int dev);
 void dev_cache_sync();                          // pending blocks of every device become reusable
 void dev_cache_release(int dev);                // synchronise and return every cached block of dev
+void dev_cache_drop_ready(int dev);             // return dev's synchronised blocks (no synchronisation)
+// While one is alive on a thread, DevBuf frees on that thread bypass the cache (the caller has
+// synchronised every stream that used the blocks).
+struct DirectFree {
+    bool prev;
+    DirectFree();
+    ~DirectFree();
+};
 
 // Owning device allocation (dev_alloc on the current device).
 template <typename T>

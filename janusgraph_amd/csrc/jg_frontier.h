@@ -39,112 +39,6 @@ struct MinI32 {
     __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; }
 };
 
-// Block-aggregated frontier append: the block's waves combine their counts in LDS and
-// one thread reserves the block's range with a single atomic (a level that finds most of the graph
-// would otherwise put one atomic per wave on one address).  Must be reached by every thread of the
-// block (block-uniform call sites); queue positions and edge offsets stay monotone.
-struct AppendScratch {
-    unsigned long long cnt[kBlock / kWave], deg[kBlock / kWave];
-    unsigned long long base;
-};
-__device__ __forceinline__ void block_append_frontier(bool take, int32_t v, int64_t deg, int32_t* __restrict__ queue,
-                                                      int64_t* __restrict__ qoff, unsigned long long* __restrict__ packed,
-                                                      AppendScratch& sc) {
-    const uint64_t mask = __ballot(take);
-    const int64_t d = take ? deg : 0;
-    const int64_t dinc = wave_inclusive_scan_add(d);
-    const int wv = wave_id();
-    if (lane_id() == kWave - 1) {
-        sc.cnt[wv] = (unsigned long long)__popcll(mask);
-        sc.deg[wv] = (unsigned long long)dinc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long c = 0, e = 0;
-        for (int k = 0; k < kBlock / kWave; ++k) {
-            const unsigned long long ck = sc.cnt[k], ek = sc.deg[k];
-            sc.cnt[k] = c;  // exclusive prefixes
-            sc.deg[k] = e;
-            c += ck;
-            e += ek;
-        }
-        sc.base = c ? atomicAdd(packed, (c << kPackShift) | e) : 0ull;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long base = sc.base;
-        const uint64_t pos = (base >> kPackShift) + sc.cnt[wv] + (uint64_t)__popcll(mask & lanemask_lt());
-        queue[pos] = v;
-        qoff[pos] = (int64_t)(base & kEdgeMask) + (int64_t)sc.deg[wv] + dinc - d;
-    }
-    __syncthreads();  // the scratch is reused by the next call
-}
-
-// LDS-staged frontier append: a block collects its appends in LDS (positions and edge offsets
-// relative to the block's staged run) and reserves global queue space with ONE atomic per flush —
-// normally once per kernel, at the end.  A single device-scope counter saturates near 90 atomics
-// per microsecond (MI355X_MICROARCH.md price list, dequeue row), so one atomic per block and wave
-// iteration made the frontier counter the bottleneck of large levels (RMAT-26 level 2: ~230 K appends).
-// Calls must be block-uniform; staged_flush must be called by the whole block before it exits.
-struct StagedAppend {
-    static constexpr int kCap = 2048;  // at least one full block of appends fits after a flush check
-    int32_t v[kCap];
-    int64_t off[kCap];                 // edge offset of entry i inside the staged run
-    unsigned long long wcnt[kBlock / kWave], wdeg[kBlock / kWave];
-    unsigned long long n, dsum, base;
-};
-__device__ __forceinline__ void staged_init(StagedAppend& sa) {
-    if (threadIdx.x == 0) sa.n = sa.dsum = 0;
-    __syncthreads();
-}
-__device__ __forceinline__ void staged_flush(StagedAppend& sa, int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
-                                             unsigned long long* __restrict__ packed) {
-    __syncthreads();
-    if (threadIdx.x == 0) sa.base = sa.n ? atomicAdd(packed, (sa.n << kPackShift) | sa.dsum) : 0ull;
-    __syncthreads();
-    const unsigned long long n = sa.n, qb = sa.base >> kPackShift, eb = sa.base & kEdgeMask;
-    for (unsigned long long i = threadIdx.x; i < n; i += blockDim.x) {
-        queue[qb + i] = sa.v[i];
-        qoff[qb + i] = (int64_t)eb + sa.off[i];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) sa.n = sa.dsum = 0;
-    __syncthreads();
-}
-__device__ __forceinline__ void staged_append(bool take, int32_t v, int64_t deg, StagedAppend& sa,
-                                              int32_t* __restrict__ queue, int64_t* __restrict__ qoff,
-                                              unsigned long long* __restrict__ packed) {
-    const uint64_t mask = __ballot(take);
-    const int64_t d = take ? deg : 0;
-    const int64_t dinc = wave_inclusive_scan_add(d);
-    const int wv = wave_id();
-    if (lane_id() == kWave - 1) {
-        sa.wcnt[wv] = (unsigned long long)__popcll(mask);
-        sa.wdeg[wv] = (unsigned long long)dinc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long c = sa.n, e = sa.dsum;
-        for (int k = 0; k < kBlock / kWave; ++k) {
-            const unsigned long long ck = sa.wcnt[k], ek = sa.wdeg[k];
-            sa.wcnt[k] = c;  // positions and offsets after the staged run
-            sa.wdeg[k] = e;
-            c += ck;
-            e += ek;
-        }
-        sa.n = c;
-        sa.dsum = e;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long p = sa.wcnt[wv] + (unsigned long long)__popcll(mask & lanemask_lt());
-        sa.v[p] = v;
-        sa.off[p] = (int64_t)sa.wdeg[wv] + dinc - d;
-    }
-    __syncthreads();
-    if (sa.n > (unsigned long long)(StagedAppend::kCap - kBlock)) staged_flush(sa, queue, qoff, packed);
-}
-
 // Wave-staged frontier append: every wave collects its appends in its own LDS region and keeps its
 // count in registers, so appending needs no block barrier and the waves of a block run their loops
 // independently (a block-wide append made every wave wait, every iteration, for the block's slowest
@@ -222,17 +116,9 @@ __device__ __forceinline__ void wave_stage_final(WaveStage& sa, WaveRun& run, in
     run.n = run.ds = 0;
 }
 
-// The two frontier appenders behind one interface: block-staged (every call block-uniform) and
-// wave-staged (every call wave-uniform; Tune::bfs_wave_stage).
-struct BlockApp {
-    static constexpr bool kWaveUniform = false;
-    StagedAppend& sa;
-    __device__ void init() { staged_init(sa); }
-    __device__ void append(bool take, int32_t v, int64_t deg, int32_t* q, int64_t* qo, unsigned long long* packed) {
-        staged_append(take, v, deg, sa, q, qo, packed);
-    }
-    __device__ void final(int32_t* q, int64_t* qo, unsigned long long* packed) { staged_flush(sa, q, qo, packed); }
-};
+// The wave-staged appender behind the interface the traversal kernels use (init / append / final).
+// (A block-wide staged append, one LDS flush per block, made every wave wait each step for the block's
+// slowest lane scan: RMAT-20 DO-BFS 0.145-0.157 -> 0.119-0.129 ms with per-wave runs, round 2.)
 struct WaveApp {
     static constexpr bool kWaveUniform = true;
     WaveStage& sa;

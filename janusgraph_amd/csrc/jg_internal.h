@@ -34,7 +34,6 @@ struct Csr {
     DevBuf<int64_t> row_ptr;
     DevBuf<int32_t> col;
     DevBuf<int32_t> weight;  // optional (SD weights)
-    bool sliced = false;     // entries of each row ordered by (sub_key(col), col) instead of col
     // rows [empty_from, rows) have no entries (set with the pull plan: 1 + the last non-empty row;
     // -1 when unknown)
     mutable int64_t empty_from = -1;
@@ -96,7 +95,7 @@ struct PullPlan {
     DevBuf<int64_t> hub_chunk_ptr;  // [num_hub_rows+1] chunks of hub row r: [ptr[r], ptr[r+1])
     int64_t total_blocks() const { return class_block_begin[kNumClasses]; }
 
-    // XCD-sliced split of the heavy rows [0, split_rows) of a sliced CSR, in degree bands (rows are
+    // XCD-sliced split of the heavy rows [0, split_rows) of a CSR, in degree bands (rows are
     // degree-sorted, so every band is a row range): see SliceBand and pull_merge_kernel (jg_pull.h).
     // The light rows keep the degree classes above (the light_* table covers [split_rows, rows)).
     int64_t split_rows = 0;
@@ -551,11 +550,10 @@ bool pull_split_launches();
 bool debug_plan();
 bool debug_bfs();  // JG_DEBUG_BFS=1: synchronise and print every DO-BFS level's decision
 
-// Performance knobs (jg_tune_set): variants of the pull kernel selectable at run time so that they
-// can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).
+// Performance knobs (jg_tune_set): algorithm variants and thresholds selectable at run time so that
+// they can be A/B-timed in one process (cdna_hip_programming.md §5.4 rule 24).  Variants measured
+// slower or equal were deleted with their code (round 5; DESIGN.md §5-6 keep their measurements).
 struct Tune {
-    int pull_unroll = 4;  // gathers in flight per lane: 4 or 8
-    int pull_nt = 0;      // 1: non-temporal loads for the streamed col[] array
     int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_merge_kernel): 0 off, 1 on
                           // (read at build time too: the sliced in-CSR and split plan need it)
     // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
@@ -564,27 +562,7 @@ struct Tune {
     // BFS unchanged; profiles/r04/band0_deg/)
     int64_t band_deg[4] = {96, 8, 0, 0};
     int band_bits[4] = {-1, 3, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits of the vector)
-    int slice_lds = 1;                // stage each sub-slice's hottest lines in LDS (single shard)
-    int pull_short = 1;               // 1-lane rows of <= 8 entries: one exec-masked batch (fold_short)
-    int fuse_finalize = 1;            // light rows and the split's finalize in one launch
-    int pull_overlap = 0;             // run the light rows on a side stream beside the split kernels (measured: no gain)
-    int64_t pull_lds = 0;             // >0: stage this many hottest elements of the gathered vector in LDS
-    int fin_last = 0;                 // fused light+finalize launch: light-row blocks first (1) or last (0)
-                                      // (measured: no difference at RMAT-24 or 26)
-    int merge_wgs = 1;                // merge workgroups per CU (1 or 2): 2 halves each one's LDS image
-                                      // (measured: 2 is 17% slower at RMAT-24, 11% at RMAT-26)
-    int merge_overlap = 0;            // with the split: band i > 0 merge launches run on the side stream
-                                      // beside band 0's (disjoint partial/carry ranges), joined before the fixup
-                                      // (measured: RMAT-24 +0.1%, RMAT-26 -0.8%, within box noise)
-    int64_t light_lds = 0;            // >0, with the split: the light rows run persistent with this many
-                                      // hottest elements in LDS (unfused from the split's finalize;
-                                      // measured: 5% slower than the fused launch at RMAT-24 and 26)
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
-    int relabel_ties = 1;             // build time: equal-degree vertices ordered by their hottest pull neighbour
-    int relabel_dead_last = 1;        // build time, IN plan: rows without out-edges last in their degree class,
-                                      // in-degree-0 rows by out-degree (the gathered vector's lines hold live values)
-    int relabel_out_ties = 0;         // build time, IN plan with relabel_dead_last: every tie by out-degree (not by
-                                      // the hottest pull neighbour)
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
                                       // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)
     int dobfs_alpha = 30;             // the same for single-source traversals (tools/bfs_sweep.py, RMAT-20:
@@ -592,11 +570,11 @@ struct Tune {
                                       // RMAT-26: 2.147 / 2.143 / 2.431 at 14 / 30 / 70)
     int bfs_beta = 24;                //         bottom-up -> top-down when frontier vertices < rows / beta
     int bfs_narrow = 1;               //         2..8 sources on one shard: the narrow byte-word engine (jg_narrow.hip)
-    int nb_alpha = 14;                //         its per-source top-down -> bottom-up threshold
+    int nb_alpha = 30;                //         its per-source top-down -> bottom-up threshold (RMAT-26, 8 groups of 8
+                                      //         sources: slowest group 6.61 / 5.79 / 6.61 / 6.85 ms at 14 / 30 / 60 / 120,
+                                      //         profiles/r05/groups/narrow_alpha_sweep_s26.jsonl)
     int nb_first = 16;                //         its bottom-up first pass: entries a lane scans before a wave takes the row
-    int cc_push = 1;                  // CC on one shard: push supersteps when the senders have few edges
-    int msbfs_skip_first = 1;         //         bit-parallel BFS: no task bitmaps on the first pull level
-    int msbfs_diag = 0;               //         diagnostic timing (wrong depths): 1 = no depth writes
+    int cc_push = 1;                  // CC propagation on one shard: push supersteps when the senders have few edges
     int msbfs_sparse = 1;             //         sharded bit-parallel BFS: top-down levels send only the set halo
                                       //         staging slots when they are under half the halo (0: always dense)
     int msbfs_td = 1;                 //         bit-parallel BFS: top-down levels for small frontiers (1: one shard
@@ -604,61 +582,28 @@ struct Tune {
     int cc_first = 1;                 //         one-shard CC union-find: neighbours linked by every vertex in the first round
                                       //         (RMAT-26: 2.82 / 3.05 / 3.31 / 3.53 ms at 1 / 2 / 3 / 4)
     int msbfs_skip = 1;               //         bit-parallel BFS pull levels skip the merge tasks of rows that can gain no bit
-    int msbfs_bu = 0;                 //         bit-parallel BFS, one shard: pull levels bottom-up with early exit
-                                      //         (0 never, 1 every pull level, 2 when the frontier holds >= msbfs_bu_frac,
-                                      //         3 sparse levels: fewer than msbfs_bu_tasks permille of the tasks live,
-                                      //         measured slower at RMAT-26's last pull level with 0.25% of its tasks
-                                      //         live: 17.84 / 17.80 vs 17.69 / 17.55 ms, profiles/r04/msbfs_bu3/;
-                                      //         measured 2-4x slower than the merge-engine pull: RMAT-26 81.0 / 21.7 ms,
-                                      //         RMAT-22 11.9 / 2.58 ms at 1 / 0, profiles/r03/msbfs/)
-    int msbfs_exit = 1;               //         bit-parallel BFS, one shard: the split's first band (hub rows) scanned
-                                      //         row by row with early exit instead of merged (0 never, 1 pull levels
-                                      //         where few band-0 tasks are live, 2 every pull level); the other rows
-                                      //         stay merged.  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 /
-                                      //         13.4 ms (profiles/r04/msbfs_exit/)
+    int msbfs_exit = 1;               //         bit-parallel BFS, one shard: rows scanned with early exit instead of merged
+                                      //         (0 never, 1 pull levels where few band-0 tasks are live, 2 every pull
+                                      //         level).  RMAT-22 / 24 / 26: 1.83 / 4.46 / 17.6 -> 1.67 / 3.83 / 13.4 ms
+                                      //         with band 0 alone (profiles/r04/msbfs_exit/); every row since
     int msbfs_td_rowapply = 4;        //         bit-parallel BFS, one shard: a top-down level with >= rows / this frontier
                                       //         edges applies over every row in order, not its touched list (0: never)
     int msbfs_td_noprobe = 2;         //         bit-parallel BFS: top-down levels below this skip the visited probe
                                       //         (RMAT-26 12.49-12.60 -> 12.32 ms, RMAT-24 -1%; profiles/r04/msbfs_td_dense/)
-    int msbfs_srcsplit = 0;           //         bit-parallel BFS, one shard: the first pull level's small-frontier sources
-                                      //         go top-down (0 never, 1 the first pull level, 2 every pull level).
-                                      //         Measured slower: RMAT-24 3.50 -> 4.16 ms (the small sources' push,
-                                      //         34.7 M entries, 0.7 ms + 0.33 ms apply; band 0 still scanned 17.8 M
-                                      //         entries), RMAT-26 12.44 -> 12.60 (the split did not apply: 10 small
-                                      //         sources held 7.4% of the entries), profiles/r04/msbfs_srcsplit/
-    int msbfs_srcsplit_permille = 20; //         msbfs_srcsplit: a source is small below this permille of the push entries
-    int msbfs_exit_bands = 2;         //         msbfs_exit: how many leading split bands take the early exit (2: both of
-                                      //         the BOTH plan's; RMAT-22 / 24 / 26 at 1 / 2: 1.57 / 3.82 / 13.5 ->
-                                      //         1.47 / 3.48 / 12.46 ms)
-    int msbfs_exit_probe = 1;         //         msbfs_exit: how many leading exit bands' live tasks decide a level's exit
-                                      //         (0: all of them; at 1 an exit level builds no band-1 bitmaps: RMAT-22
-                                      //         / 24 / 26 at 0 / 1: 1.384 / 3.131 / 11.23 -> 1.385 / 3.102 / 11.12 ms,
-                                      //         the same decisions; a repeat: 24 / 26 3.079 / 11.11 -> 3.066 / 11.11,
-                                      //         profiles/r04/msbfs_exit/probe_band0*.jsonl)
-    int msbfs_skip_empty = 1;         //         bit-parallel BFS pull levels skip the rows without entries (no finalise)
-    int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose exit bands had fewer
-                                      //         live tasks than this permille builds the next top-down queue in its
+    int msbfs_scan_queue = 50;        //         bit-parallel BFS, one shard: a pull level whose band 0 had fewer live
+                                      //         tasks than this permille builds the next top-down queue in its
                                       //         frontier scan (one pass instead of two); 0: never
     int msbfs_exit_first = 16;        //         msbfs_exit: entries a lane scans per row before a wave takes it
                                       //         (RMAT-26 12.29-12.35 / 12.14-12.21 / 12.14-12.18 ms at 8 / 16 / 32,
                                       //         RMAT-24 -1% at 16; profiles/r04/msbfs_exit/first_*.log)
-    int msbfs_exit_all = 1;           //         msbfs_exit: every row with entries (the light rows too) takes the early
-                                      //         exit; no merge launch on such levels (RMAT-26 11.42-11.46 -> 11.19-11.21
-                                      //         ms, RMAT-24 -1%, once the empty rows were skipped; neutral before)
-    int msbfs_exit_live = 950;        //         msbfs_exit 1: permille of band 0's merge tasks live below which its rows
+    int msbfs_exit_live = 950;        //         msbfs_exit 1: permille of band 0's merge tasks live below which the rows
                                       //         exit early (the level after the frontier's peak: 45-73%; before it: 100%)
-    int msbfs_bu_frac = 100;          //         permille of the rows
-    int msbfs_bu_tasks = 20;          //         msbfs_bu 3: permille of the merge tasks below which a pull level
-                                      //         (after the first) runs bottom-up
     int cc_uf = 1;                    //         connected components on one shard: union-find + BFS superstep count
     int cc_uf_sharded = 1;            //         sharded (halo plans): local union-find, tree labels over the halo,
                                       //         multi-root sharded BFS for the superstep count (0: propagation)
     int cc_uf_search = 1;             //         ... giant-to-giant links by a bounded search (0: every flagged entry)
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
-    int bfs_init_suffix = 1;          //         DO-BFS init: empty rows from the plan's empty suffix (no row_ptr reads)
-    int bfs_grow_rule = 0;            //         DO-BFS: top-down -> bottom-up only while the frontier grows
-                                      //         (measured: RMAT-26 -0.6%, RMAT-20 +2.5%; off)
     int bfs_td_split = 2;             //         DO-BFS top-down levels of >= bfs_td_split_min frontier entries in two
                                       //         launches (targets' owner written, then claimed) instead of one CAS
                                       //         per entry: 0 never, 1 every level, 2 the level(s) in bfs_td_split_levels
@@ -668,29 +613,15 @@ struct Tune {
                                       //         1.2 ms; RMAT-20's 329 K-entry level 1 went 64 -> 26 us)
     int bfs_batch0 = 10;              //         DO-BFS: levels in the first batch (then 4, 8, 16, ...)
     int bfs_grid_mult = 4;            //         DO-BFS level grid = sqrt(rows) * bfs_grid_mult / 4 workgroups
-    int bfs_wave_stage = 1;           //         DO-BFS levels append through per-wave LDS runs (no block barrier per step)
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
                                       //         (0: every launch at the full grid)
-    int pr_rank_last = 1;             // PageRank: store the rank vector on a call's last superstep only
-    int pr_skip_empty = 1;            // PageRank: rows without in-edges are finalised in the first two power
-                                      // steps only (their rank and contribution are constant after that)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
                                           // stores, -1 = automatic from the band's heads per task)
-    int merge_interleave = 1;         // merge blocks take interleaved single tasks, rotating per round (0: chunks of 16)
-    int merge_dynamic = 1;            // merge waves take their block's tasks from an LDS counter (0: static)
-    int fin_pipe = 1;                 // split finalize: next batch's index words loaded with this batch's partials
-    int band_sliced_build = 0;        // build time: 1 = cut the bands from a sub-slice-ordered first build of the
-                                      // CSR (rounds 1-2; a second select + sort), 0 = from the column-ordered CSR
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
                                       // (0: 32 bits, 24: at least 24; tests)
-    int light_runs = 1;               // build time: light rows of degree 1..7 addressed by degree run (no row_ptr load)
-    int merge_diag = 0;               // diagnostic timing of the merge kernel (wrong results for 1, 3, 4):
-                                      // 1 staging only, 3 no partial stores, 4 no cold (non-LDS) gathers
-                                      // (round 2: a second col-sized
-                                      // stream cost +28% / +10% in the band 0 / 1 merges at RMAT-26)
 };
 Tune& tune();
 // rank mode over jg_transport callbacks (jg_api.cpp)
@@ -699,14 +630,6 @@ void host_exchange(Ctx& c, const std::vector<int>& speer, const std::vector<cons
                    const std::vector<size_t>& sbytes, const std::vector<int>& rpeer, const std::vector<void*>& rbuf,
                    const std::vector<size_t>& rbytes);
 int device_cu_count();  // compute units of the current device
-// A second stream of the current device (created on first use, lives for the process) with a fork
-// and a join event: work independent of the main stream's runs beside it, e.g. the light rows of a
-// pull superstep next to the sliced split's merge kernels.
-struct SideStream {
-    hipStream_t stream = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream& side_stream();
 
 // Profiling of the dominant kernel (HIP events on the shard's stream).
 bool prof_enabled(const Ctx& c);

@@ -121,11 +121,11 @@ void pagerank_steps(Graph& g, int nsteps) {
             op.teleport = teleport;
             // the rank property is read only after the call (jg_pagerank_end): earlier supersteps' ranks
             // are dead stores, except on steps 0 and 1, which also write the rows later steps skip
-            op.write_rank = t == nsteps - 1 || g.pr_steps < 2 || !tune().pr_rank_last;
+            op.write_rank = t == nsteps - 1 || g.pr_steps < 2;
             // Rows without in-edges: rank = (1-d)/N and contrib = rank/edgeCount from the first power step
             // on.  Steps 0 and 1 write that constant into both contrib buffers (step 0 must still gather
             // the initial values), later steps leave those rows alone.
-            const bool skip_empty = g.pr_steps >= 2 && tune().pr_skip_empty;
+            const bool skip_empty = g.pr_steps >= 2;
             launch_pull(sh.in, sh.plan_in, op, sh.pr_hub_partial.get(), sh.stream, pc, &sh, sh.pr_split_partial.get(),
                         skip_empty);
         }

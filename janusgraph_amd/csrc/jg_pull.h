@@ -34,7 +34,6 @@ struct PullArgs {
     int64_t class_block_begin[kNumClasses + 1];
     int64_t block_offset;  // diagnostic split launches (JG_PULL_SPLIT=1): first block of this launch
     int64_t skip_rows;     // rows [0, skip_rows) are folded by the XCD split: their hub chunks are skipped
-    int short_rows;        // 1-lane rows of <= 8 entries use fold_short (Tune::pull_short)
     int runs;              // 1-lane rows from run_begin[kRunMax] on are addressed by degree run (PullPlan::runs)
     int64_t run_begin[kRunMax + 1];
     int64_t run_ptr[kRunMax + 1];
@@ -57,8 +56,7 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = f
     for (int c = 0; c <= kNumClasses; ++c) a.class_block_begin[c] = light ? p.light_block_begin[c] : p.class_block_begin[c];
     a.block_offset = 0;
     a.skip_rows = light ? p.split_rows : 0;
-    a.short_rows = tune().pull_short;
-    a.runs = p.runs && a.short_rows;
+    a.runs = p.runs;
     for (int d = 0; d <= kRunMax; ++d) {
         a.run_begin[d] = p.run_begin[d];
         a.run_ptr[d] = p.run_ptr[d];
@@ -66,14 +64,7 @@ inline PullArgs make_pull_args(const Csr& csr, const PullPlan& p, bool light = f
     return a;
 }
 
-template <bool NT>
-__device__ __forceinline__ int32_t load_col(const int32_t* __restrict__ col, int64_t j) {
-    if constexpr (NT) return __builtin_nontemporal_load(col + j);  // streamed once: don't keep it in cache
-    else return col[j];
-}
-
-// How a fold reads the gathered vector: straight from global memory, or from an LDS copy of its
-// hottest prefix (the degree-sorted first `hot` ids) with global memory for the rest.
+// How a fold reads the gathered vector (the class rows: straight from global memory).
 template <class Op>
 struct GlobalGather {
     const Op& op;
@@ -84,43 +75,35 @@ struct GlobalGather {
 template <class T>
 using lds_ptr = __attribute__((address_space(3))) T*;
 
-template <class Op>
-struct LdsGather {
-    const Op& op;
-    lds_ptr<const typename Op::T> lds;
-    int32_t hot;
-    __device__ __forceinline__ typename Op::T operator()(int32_t c) const { return c < hot ? lds[c] : op.gather(c); }
-};
-
 // Fold col[j..j1) with stride `stride`; U gathers in flight per lane, folded in index order.
 // Software-pipelined: the col batch of iteration i+1 is loaded while the gathers of iteration i are
 // in flight, so a long row pays one round trip per batch instead of two.  The last, partial batch is
 // not walked one entry at a time: its out-of-range slots re-read the row's last entry (a cache hit)
 // and are dropped from the fold by a select, so every batch is branch-free.
-template <class Op, int U, bool NT>
+template <class Op, int U>
 __device__ __forceinline__ void load_cols(const int32_t* __restrict__ col, int64_t j, int64_t j1, int stride,
                                           int32_t (&c)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t k = j + u * (int64_t)stride;
-        c[u] = load_col<NT>(col, k < j1 ? k : j1 - 1);
+        c[u] = col[k < j1 ? k : j1 - 1];
     }
 }
 
-template <class Op, int U, bool NT, class G>
+template <class Op, int U, class G>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& gather, const int32_t* __restrict__ col,
                                                        int64_t j, int64_t j1, int stride) {
     using T = typename Op::T;
     T acc = op.identity();
     if (j >= j1) return acc;
     int32_t c[U];
-    load_cols<Op, U, NT>(col, j, j1, stride, c);
+    load_cols<Op, U>(col, j, j1, stride, c);
     for (;;) {
         T v[U];
         const int64_t jn = j + U * (int64_t)stride;
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = gather(c[u]);
-        load_cols<Op, U, NT>(col, jn, j1, stride, c);  // clamped: unconditional keeps vmcnt counting exact
+        load_cols<Op, U>(col, jn, j1, stride, c);  // clamped: unconditional keeps vmcnt counting exact
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const T t = op.combine(acc, v[u]);
@@ -135,7 +118,7 @@ __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const G& ga
 // Short rows (one lane per row, < 8 entries): all entries in one masked batch of 8.  Out-of-range
 // slots issue no load at all (exec-masked), instead of re-reading the last entry: a duplicate lane
 // still costs the TA/TD its cycles (tools/micro/td_mask.hip: cost scales with active lanes).
-template <class Op, bool NT, class G>
+template <class Op, class G>
 __device__ __forceinline__ typename Op::T fold_short(const Op& op, const G& gather, const int32_t* __restrict__ col,
                                                      int64_t j, int64_t j1) {
     using T = typename Op::T;
@@ -145,7 +128,7 @@ __device__ __forceinline__ typename Op::T fold_short(const Op& op, const G& gath
 #pragma unroll
     for (int u = 0; u < kMax; ++u) {
         c[u] = 0;
-        if (u < n) c[u] = load_col<NT>(col, j + u);
+        if (u < n) c[u] = col[j + u];
     }
     T v[kMax];
 #pragma unroll
@@ -160,14 +143,14 @@ __device__ __forceinline__ typename Op::T fold_short(const Op& op, const G& gath
     return acc;
 }
 
-template <class Op, int U, bool NT>
+template <class Op, int U>
 __device__ __forceinline__ typename Op::T fold_strided(const Op& op, const int32_t* __restrict__ col, int64_t j,
                                                        int64_t j1, int stride) {
-    return fold_strided<Op, U, NT>(op, GlobalGather<Op>{op}, col, j, j1, stride);
+    return fold_strided<Op, U>(op, GlobalGather<Op>{op}, col, j, j1, stride);
 }
 
 // `tid` is the thread's index inside its (virtual) 256-thread block.
-template <class Op, int L, int U, bool NT, class G>
+template <class Op, int L, int U, class G>
 __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op, const G& gather, int c,
                                                 int64_t local_block, int tid) {
     using T = typename Op::T;
@@ -186,7 +169,7 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
                 d = k;
                 j0 = a.run_ptr[k] + (row - a.run_begin[k]) * k;
             }
-        if (op.active(row)) acc = fold_short<Op, NT>(op, gather, a.col, j0, j0 + d);
+        if (op.active(row)) acc = fold_short<Op>(op, gather, a.col, j0, j0 + d);
         op.finalize(row, acc);
         return;
     }
@@ -194,8 +177,8 @@ __device__ __forceinline__ void pull_rows_class(const PullArgs& a, const Op& op,
         const int64_t j0 = a.row_ptr[row], j1 = a.row_ptr[row + 1];
         hub = (j1 - j0) >= kHubDegree;  // folded by the chunk path
         if (!hub && op.active(row)) {
-            if (L == 1 && a.short_rows && j1 - j0 <= 8) acc = fold_short<Op, NT>(op, gather, a.col, j0, j1);
-            else acc = fold_strided<Op, U, NT>(op, gather, a.col, j0 + sub, j1, L);
+            if (L == 1 && j1 - j0 <= 8) acc = fold_short<Op>(op, gather, a.col, j0, j1);
+            else acc = fold_strided<Op, U>(op, gather, a.col, j0 + sub, j1, L);
         }
     }
 #pragma unroll
@@ -211,7 +194,7 @@ __device__ __forceinline__ void pull_rows_empty(const PullArgs& a, const Op& op,
 }
 
 // Class dispatch of (virtual) block b >= num_chunks.
-template <class Op, int U, bool NT, class G>
+template <class Op, int U, class G>
 __device__ __forceinline__ void pull_block_rows(const PullArgs& a, const Op& op, const G& gather, int64_t b, int tid) {
     int c = 1;
 #pragma unroll
@@ -219,18 +202,18 @@ __device__ __forceinline__ void pull_block_rows(const PullArgs& a, const Op& op,
         if (b >= a.class_block_begin[k + 1]) c = k + 1;
     const int64_t lb = b - a.class_block_begin[c];
     switch (c) {
-        case 1: pull_rows_class<Op, 64, U, NT>(a, op, gather, c, lb, tid); break;
-        case 2: pull_rows_class<Op, 32, U, NT>(a, op, gather, c, lb, tid); break;
-        case 3: pull_rows_class<Op, 16, U, NT>(a, op, gather, c, lb, tid); break;
-        case 4: pull_rows_class<Op, 8, U, NT>(a, op, gather, c, lb, tid); break;
-        case 5: pull_rows_class<Op, 4, U, NT>(a, op, gather, c, lb, tid); break;
-        case 6: pull_rows_class<Op, 2, U, NT>(a, op, gather, c, lb, tid); break;
-        case 7: pull_rows_class<Op, 1, U, NT>(a, op, gather, c, lb, tid); break;
+        case 1: pull_rows_class<Op, 64, U>(a, op, gather, c, lb, tid); break;
+        case 2: pull_rows_class<Op, 32, U>(a, op, gather, c, lb, tid); break;
+        case 3: pull_rows_class<Op, 16, U>(a, op, gather, c, lb, tid); break;
+        case 4: pull_rows_class<Op, 8, U>(a, op, gather, c, lb, tid); break;
+        case 5: pull_rows_class<Op, 4, U>(a, op, gather, c, lb, tid); break;
+        case 6: pull_rows_class<Op, 2, U>(a, op, gather, c, lb, tid); break;
+        case 7: pull_rows_class<Op, 1, U>(a, op, gather, c, lb, tid); break;
         default: pull_rows_empty<Op>(a, op, lb, tid); break;
     }
 }
 
-template <class Op, int U, bool NT>
+template <class Op, int U>
 __device__ __forceinline__ void pull_block(const PullArgs& a, const Op& op, typename Op::T* __restrict__ hub_partial,
                                            int64_t b) {
     using T = typename Op::T;
@@ -238,7 +221,7 @@ __device__ __forceinline__ void pull_block(const PullArgs& a, const Op& op, type
         __shared__ T red[kBlock / kWave];
         const int64_t j0 = a.chunk_begin[b], j1 = a.chunk_end[b];
         const int64_t crow = a.chunk_row[b];
-        T acc = (crow >= a.skip_rows && op.active(crow)) ? fold_strided<Op, U, NT>(op, a.col, j0 + threadIdx.x, j1, kBlock)
+        T acc = (crow >= a.skip_rows && op.active(crow)) ? fold_strided<Op, U>(op, a.col, j0 + threadIdx.x, j1, kBlock)
                                                          : op.identity();
 #pragma unroll
         for (int o = kWave / 2; o > 0; o >>= 1) acc = op.combine(acc, op.shfl_xor(acc, o));
@@ -252,36 +235,12 @@ __device__ __forceinline__ void pull_block(const PullArgs& a, const Op& op, type
         }
         return;
     }
-    pull_block_rows<Op, U, NT>(a, op, GlobalGather<Op>{op}, b, (int)threadIdx.x);
+    pull_block_rows<Op, U>(a, op, GlobalGather<Op>{op}, b, (int)threadIdx.x);
 }
 
-template <class Op, int U, bool NT>
+template <class Op, int U>
 __global__ __launch_bounds__(kBlock) void pull_kernel(PullArgs a, Op op, typename Op::T* __restrict__ hub_partial) {
-    pull_block<Op, U, NT>(a, op, hub_partial, (int64_t)blockIdx.x + a.block_offset);
-}
-
-// LDS-cached variant (persistent, 1024 threads = 4 virtual 256-thread blocks, one workgroup per
-// CU): the gathered vector's hottest prefix [0, hot) — the highest-degree vertices after the
-// degree-sorted relabel — is staged once per superstep into LDS (up to 160 KiB), so those gathers
-// never become L2 requests (the pull superstep is bound by L2 request rate, not bytes:
-// tools/pr_locality.py).  Virtual blocks >= num_chunks are dealt round-robin; hub chunks stay with
-// pull_kernel.  No block-wide barrier after the staging one, so the four virtual blocks run freely.
-constexpr int kLdsThreads = 1024;
-template <class Op, int U, bool NT>
-__global__ __launch_bounds__(kLdsThreads) void pull_lds_kernel(PullArgs a, Op op, int32_t hot) {
-    using T = typename Op::T;
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    lds_ptr<T> lds = (lds_ptr<T>)lds_raw;
-    const T* src = op.vec();
-    for (int i = threadIdx.x; i < hot; i += kLdsThreads) lds[i] = src[i];
-    __syncthreads();
-    const LdsGather<Op> gather{op, lds, hot};
-    constexpr int kVirt = kLdsThreads / kBlock;
-    const int tid = threadIdx.x % kBlock;
-    const int64_t last = a.class_block_begin[kNumClasses];
-    for (int64_t b = a.class_block_begin[1] + (int64_t)blockIdx.x * kVirt + threadIdx.x / kBlock; b < last;
-         b += (int64_t)gridDim.x * kVirt)
-        pull_block_rows<Op, U, NT>(a, op, gather, b, tid);
+    pull_block<Op, U>(a, op, hub_partial, (int64_t)blockIdx.x + a.block_offset);
 }
 
 template <class Op>
@@ -332,9 +291,6 @@ struct MergeArgs {
     int64_t tasks;
     int bits;
     int stage;         // LDS staging slots per wave for a task's partials (0: direct stores)
-    int dynamic;       // LDS image kernels: waves take their block's tasks from an LDS counter
-    int interleave;    // a block's tasks interleaved with its sub-slice's other blocks (rotating per round)
-    int diag;          // Tune::merge_diag (diagnostic timing variants; 0 in production)
     // nullable: bit t (of the band's tasks) clear = task t is skipped, its partials and carry left as
     // they are.  A program passes it only when every row the task touches would discard what the task
     // folds (the multi-source BFS: rows that can gain no bit; see msbfs_task_live_kernel).
@@ -394,16 +350,10 @@ __device__ __forceinline__ uint32_t unpack_entry(const uint32_t (&d)[W / 4], int
     return v;
 }
 
-// NT: bit 0 = the streamed band arrays are loaded non-temporally, bit 1 = the partials are stored
-// non-temporally.  Every launch uses 0: the merge_nt knob measured no gain at RMAT-24/26 (round 2,
-// 4.12-4.25 vs 4.12 ms) and was removed; the parameter stays for such experiments.  Bands of fewer than 8 sub-slices (2^bits < 8) share each sub-slice among
-// 8 / 2^bits XCDs.
-template <class T>
-__device__ __forceinline__ void store_nt(T* p, T v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-template <class Op, bool LDS, int NT, int PW>
+// Bands of fewer than 8 sub-slices (2^bits < 8) share each sub-slice among 8 / 2^bits XCDs.
+// (Non-temporal band loads / partial stores measured no gain at RMAT-24/26 in round 2: 4.12-4.25 vs
+// 4.12 ms.)
+template <class Op, bool LDS, int PW>
 __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, Op op, typename Op::T* __restrict__ partial,
                                                                    typename Op::T* __restrict__ carry, HotSegs hs,
                                                                    int temporal) {
@@ -484,20 +434,16 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     const int64_t base = a.sub_base[h];
     const int64_t ntask = a.sub_base[h + 1] - base;
     const int64_t hbegin = a.sub_begin[h], hend = a.sub_end[h];
-    const int64_t step = G * kMergeWaves;
-    // The block's j-th task, j = 0, 1, ...: interleaved (a.interleave), k = j * G + (g + rd) mod G, so
-    // the G blocks of a sub-slice differ by at most one task per round and the rotation spreads the
-    // extra tasks over the blocks round by round; otherwise chunks of 16, k = g * 16 + (j mod 16) +
-    // (j / 16) * step, which gave the low blocks up to one more chunk in every round (~4% more work
-    // by the kernel's end).  Static: wave w takes j = w, w + 16, ...; dynamic (LDS image kernels,
-    // a.dynamic): the waves take j from the block's LDS counter, so a wave that drew cheaper tasks takes
-    // more and the round's barrier waits less for the slowest wave.  Any order gives the same result
-    // (tasks are independent).
-    const bool dyn = LDS && a.dynamic;
+    // The block's j-th task, j = 0, 1, ...: interleaved, k = j * G + (g + rd) mod G, so the G blocks of
+    // a sub-slice differ by at most one task per round and the rotation spreads the extra tasks over
+    // the blocks round by round (chunks of 16 per block gave the low blocks up to one more chunk in
+    // every round, ~4% more work by the kernel's end).  Without an LDS image, wave w takes j = w, w +
+    // 16, ...; the LDS image kernels' waves take j from the block's LDS counter, so a wave that drew
+    // cheaper tasks takes more and the round's barrier waits less for the slowest wave (RMAT-24 0.848
+    // -> 0.800 ms).  Any order gives the same result (tasks are independent).
+    constexpr bool dyn = LDS;
     const int64_t grot = (g + rd) % G;
-    auto task_of = [&](int64_t j) {
-        return a.interleave ? j * G + grot : (j / kMergeWaves) * step + g * kMergeWaves + (j % kMergeWaves);
-    };
+    auto task_of = [&](int64_t j) { return j * G + grot; };
     auto grab = [&]() -> int64_t {
         uint32_t j = 0;
         if (lane == 0) j = __hip_atomic_fetch_add(tctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -519,7 +465,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     };
     int64_t k = dyn ? grab() : task_of(jstat);
     while (dead(k)) k = advance();
-    if (k >= ntask || a.diag == 1) continue;
+    if (k >= ntask) continue;
     // The next task's entries and metadata are loaded while this task's gathers are in flight.  The
     // loop carries the raw load registers (the packed lane chunk, head byte, meta word) and unpacks
     // them at the top, so a prefetch writes straight into them and nothing waits on it until the next
@@ -530,10 +476,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
     auto chunk = [&](int64_t kk) { return (hbegin >> 3) + kk * kWave + lane; };
     auto meta_idx = [&](int64_t kk) { return 2 * (base + kk) + (lane & 1); };
     auto head_idx = [&](int64_t kk) { return (base + kk) * kWave + lane; };
-    auto ld = [](const auto* p) {
-        if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(p);
-        else return *p;
-    };
+    auto ld = [](const auto* p) { return *p; };
     using v4u = uint32_t __attribute__((ext_vector_type(4)));
     using v2u = uint32_t __attribute__((ext_vector_type(2)));
     auto load_chunk = [&](int64_t kk, uint32_t (&d)[PW / 4]) {
@@ -570,7 +513,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) vl[u] = lg.hot(loc[u], kMergeEpl * lane + u < n);
 #pragma unroll
-            for (int u = 0; u < kMergeEpl; ++u) vg[u] = lg.cold(loc[u], a.diag != 4 && kMergeEpl * lane + u < n, true);
+            for (int u = 0; u < kMergeEpl; ++u) vg[u] = lg.cold(loc[u], kMergeEpl * lane + u < n, true);
 #pragma unroll
             for (int u = 0; u < kMergeEpl; ++u) v[u] = op.combine(vl[u], vg[u]);
         } else {
@@ -596,17 +539,16 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         const bool valid_lane = kMergeEpl * lane < n;
         // A task's partials are consecutive slots: with at most `stage` heads they are collected in the
         // wave's LDS window and written by one coalesced store per 64, instead of up to 10 exec-masked
-        // scattered stores per lane (the stores cost ~20% of the merge kernel: merge_diag 3).
+        // scattered stores per lane (the stores cost ~20% of the merge kernel, round 2).
         const int H = __builtin_amdgcn_readlane(incl, kWave - 1);
         const bool staged = LDS && H <= a.stage;
         auto emit = [&](int hh, T val) {  // segment of head hh
-            if (a.diag == 3) return;  // diag 3: no partial stores (timing only)
             if (staged) {
                 stg[hh] = val;
                 return;
             }
-            if (hh == 0 && carry_in) store_nt(carry + t, val, (NT & 2) != 0);
-            else store_nt(partial + j0 + hh, val, (NT & 2) != 0);
+            if (hh == 0 && carry_in) carry[t] = val;
+            else partial[j0 + hh] = val;
         };
         // lane-local: the part before the first head (continues the segment on the left), inner
         // segments (emitted here) and the segment of the last head (continues to the right)
@@ -651,7 +593,7 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
                 else emit(in_h, lane > 0 ? op.combine(in_x, pre) : pre);
             }
         }
-        if (staged && a.diag != 3) {
+        if (staged) {
             // the window is wave-private and LDS runs a wave's instructions in order: the fences only
             // keep the compiler from moving these reads above the writes (or the next task's writes
             // above these reads)
@@ -660,8 +602,8 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             for (int i = lane; i < H; i += kWave) {
                 const T val = stg[i];
-                if (i == 0 && carry_in) store_nt(carry + t, val, (NT & 2) != 0);
-                else store_nt(partial + j0 + i, val, (NT & 2) != 0);
+                if (i == 0 && carry_in) carry[t] = val;
+                else partial[j0 + i] = val;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -724,74 +666,50 @@ struct FinalizeBands {
     int bits[kMaxBands];
     int n;
 };
-template <class Op, bool PIPE = true>
+template <class Op>
 __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, const FinalizeBands& fb,
                                                    const typename Op::T* __restrict__ partial) {
     using T = typename Op::T;
-    {
-        int b = 0;
-        while (b < fb.n - 1 && r >= fb.row_end[b]) ++b;
-        const int64_t NR = fb.row_end[b] - fb.row_begin[b], i = r - fb.row_begin[b];
-        const int64_t W = (NR + 31) / 32, wi = i >> 5;
-        const uint32_t below = (1u << (i & 31)) - 1u, me = 1u << (i & 31);
-        const int S = 1 << fb.bits[b];
-        const uint2* __restrict__ sw = fb.sub_word[b];
-        const T* __restrict__ part = partial + fb.part_off[b];
-        T acc = op.identity();
-        bool first = true;
-        // batches of 8 sub-slices: all index loads, then all partial loads, then the fold in h order,
-        // and the next batch's index words are loaded with this batch's partials, so a hub row's 128
-        // sub-slices cost 17 round trips instead of 128 dependent pairs.  The index words are shared by
-        // 32 rows (1/16 of the bytes of an int32 index per sub-row).
-        if constexpr (PIPE) {
-            uint2 wc[8], wn[8];
-            auto load_words = [&](int h0, uint2 (&wd)[8]) {
+    int b = 0;
+    while (b < fb.n - 1 && r >= fb.row_end[b]) ++b;
+    const int64_t NR = fb.row_end[b] - fb.row_begin[b], i = r - fb.row_begin[b];
+    const int64_t W = (NR + 31) / 32, wi = i >> 5;
+    const uint32_t below = (1u << (i & 31)) - 1u, me = 1u << (i & 31);
+    const int S = 1 << fb.bits[b];
+    const uint2* __restrict__ sw = fb.sub_word[b];
+    const T* __restrict__ part = partial + fb.part_off[b];
+    T acc = op.identity();
+    bool first = true;
+    // batches of 8 sub-slices: all index loads, then all partial loads, then the fold in h order, and
+    // the next batch's index words are loaded with this batch's partials, so a hub row's 128 sub-slices
+    // cost 17 round trips instead of 128 dependent pairs (the unpipelined batches: RMAT-26 light+finalize
+    // 858 -> 771 us).  The index words are shared by 32 rows (1/16 of the bytes of an int32 index per
+    // sub-row).
+    uint2 wc[8], wn[8];
+    auto load_words = [&](int h0, uint2 (&wd)[8]) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u)  // bands of fewer than 8 sub-slices: empty words
-                    wd[u] = h0 + u < S ? sw[(int64_t)(h0 + u) * W + wi] : make_uint2(0u, 0u);
-            };
-            load_words(0, wc);
-            for (int h0 = 0; h0 < S; h0 += 8) {
-                int32_t j[8];
-                T v[8];
+        for (int u = 0; u < 8; ++u)  // bands of fewer than 8 sub-slices: empty words
+            wd[u] = h0 + u < S ? sw[(int64_t)(h0 + u) * W + wi] : make_uint2(0u, 0u);
+    };
+    load_words(0, wc);
+    for (int h0 = 0; h0 < S; h0 += 8) {
+        int32_t j[8];
+        T v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) j[u] = (wc[u].x & me) ? (int32_t)wc[u].y + __popc(wc[u].x & below) : -1;
-                if (h0 + 8 < S) load_words(h0 + 8, wn);
+        for (int u = 0; u < 8; ++u) j[u] = (wc[u].x & me) ? (int32_t)wc[u].y + __popc(wc[u].x & below) : -1;
+        if (h0 + 8 < S) load_words(h0 + 8, wn);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
+        for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (j[u] >= 0) {
-                        acc = first ? v[u] : op.combine(acc, v[u]);
-                        first = false;
-                    }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) wc[u] = wn[u];
+        for (int u = 0; u < 8; ++u)
+            if (j[u] >= 0) {
+                acc = first ? v[u] : op.combine(acc, v[u]);
+                first = false;
             }
-        } else {  // round 1: index loads and partial loads of one batch, then the next batch
-            for (int h0 = 0; h0 < S; h0 += 8) {
-                int32_t j[8];
-                T v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    j[u] = -1;
-                    if (h0 + u < S) {
-                        const uint2 w = sw[(int64_t)(h0 + u) * W + wi];
-                        j[u] = (w.x & me) ? (int32_t)w.y + __popc(w.x & below) : -1;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = j[u] >= 0 ? part[j[u]] : op.identity();
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (j[u] >= 0) {
-                        acc = first ? v[u] : op.combine(acc, v[u]);
-                        first = false;
-                    }
-            }
-        }
-        op.finalize(r, acc);
+        for (int u = 0; u < 8; ++u) wc[u] = wn[u];
     }
+    op.finalize(r, acc);
 }
 
 template <class Op>
@@ -801,31 +719,28 @@ __global__ void pull_slice_finalize_kernel(int64_t row0, int64_t rows, Op op, Fi
         slice_finalize_row(r, op, fb, partial);
 }
 
-// The light rows and the split's finalize in one launch (tune fuse_finalize): blocks [0, fin_blocks)
-// finalise split rows (one per thread), the rest run light-row blocks.  Both are latency-bound and
-// independent, so interleaving their blocks hides one's stalls behind the other's.
-template <class Op, int U, bool NT, bool PIPE>
+// The light rows and the split's finalize in one launch: blocks [0, fin_blocks) finalise split rows
+// (one per thread), the rest run light-row blocks.  Both are latency-bound and independent, so
+// interleaving their blocks hides one's stalls behind the other's (the order of the two block ranges
+// measured equal at RMAT-24 and 26, round 1).
+template <class Op, int U>
 __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a, Op op,
                                                                      typename Op::T* __restrict__ hub_partial,
                                                                      FinalizeBands fb,
                                                                      const typename Op::T* __restrict__ partial,
                                                                      int64_t split_rows, int64_t fin_blocks,
-                                                                     int fin_last, int64_t fin_row0) {
-    // fin_last: the light-row blocks first, the finalize blocks after them (Tune::fin_last)
-    const int64_t light_blocks = (int64_t)gridDim.x - fin_blocks;
-    const int64_t fb0 = fin_last ? light_blocks : 0;
+                                                                     int64_t fin_row0) {
     const int64_t b = blockIdx.x;
-    if (b >= fb0 && b < fb0 + fin_blocks) {
-        const int64_t r = fin_row0 + (b - fb0) * kBlock + threadIdx.x;
-        if (r < split_rows) slice_finalize_row<Op, PIPE>(r, op, fb, partial);
+    if (b < fin_blocks) {
+        const int64_t r = fin_row0 + b * kBlock + threadIdx.x;
+        if (r < split_rows) slice_finalize_row<Op>(r, op, fb, partial);
         return;
     }
-    pull_block<Op, U, NT>(a, op, hub_partial, (fin_last ? b : b - fin_blocks) + a.block_offset);
+    pull_block<Op, U>(a, op, hub_partial, b - fin_blocks + a.block_offset);
 }
 
 // Enqueue one pull superstep on `s`.
 // `split_partial` ([8 * plan.split_rows], nullable) enables the XCD split of the heavy rows.
-constexpr int64_t kMaxLdsBytes = 160 * 1024;
 
 // `skip_empty`: the rows without entries (the degree-sorted suffix, class kZeroClass) are not
 // finalised, for programs whose value there no longer changes (PageRank after two power steps).
@@ -849,38 +764,23 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     if (skip_empty) a.class_block_begin[kNumClasses] = a.class_block_begin[kZeroClass];
     const int64_t blocks = a.class_block_begin[kNumClasses];
     if (prof_ctx) prof_record_start(*prof_ctx, *prof_shard);
-    // With the split, the light rows (and hub finalize) run on the side stream beside the merge
-    // kernels: they touch other rows, and their 256-thread, LDS-free blocks fit next to a merge
-    // workgroup on every CU, filling its memory stalls.
-    hipStream_t ls = s;
-    SideStream* side = nullptr;
-    if (split && tune().pull_overlap) {
-        side = &side_stream();
-        JG_HIP(hipEventRecord(side->fork, s));
-        JG_HIP(hipStreamWaitEvent(side->stream, side->fork, 0));
-        ls = side->stream;
-    }
+    // (Measured and removed: the light rows on a side stream beside the merge kernels, band 1's merge on
+    // a side stream beside band 0's, two merge workgroups per CU with half the LDS image each, the light
+    // rows through a persistent LDS-prefix kernel: no gain or slower at RMAT-24 and 26)
     if (split) {
         static bool attr = false;
         if (!attr) {
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 20>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 20>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 24>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 24>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
-            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 0, 32>,
+            JG_HIP(hipFuncSetAttribute((const void*)pull_merge_kernel<Op, true, 32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsBytes));
             attr = true;
-        }
-        SideStream* mside = nullptr;
-        if (tune().merge_overlap && side == nullptr && plan.bands.size() > 1) {
-            mside = &side_stream();
-            JG_HIP(hipEventRecord(mside->fork, s));
-            JG_HIP(hipStreamWaitEvent(mside->stream, mside->fork, 0));
         }
         for (size_t bi = band0; bi < plan.bands.size(); ++bi) {
             const SliceBand& bd = *plan.bands[bi];
             if (bd.tasks == 0) continue;
-            const hipStream_t ms = (mside && bi > 0) ? mside->stream : s;
             // staging window: -1 = automatic, the power of two >= 4x the band's mean heads per task,
             // within [128, 256] (RMAT-24 band 0 ~21 heads: 128; RMAT-26 band 0 ~73 and band 1 ~110:
             // 256).  Heads per task are heavy-tailed (tasks of short sub-rows near the band's degree
@@ -893,41 +793,35 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
                 while (stage < 4.0 * heads && stage < 256) stage *= 2;
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
-                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage, tune().merge_dynamic, tune().merge_interleave, tune().merge_diag,
+                         bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage,
                          task_live ? task_live[bi] : nullptr};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
             const int64_t S = 1ll << bd.bits, gsz = 16 * S;
-            // a multiple of S workgroups: every sub-slice gets grid / S of them
-            const int wpc = tune().merge_wgs;
-            const unsigned grid = (unsigned)std::max<int64_t>(S, (int64_t)device_cu_count() * wpc / S * S);
+            // one workgroup per CU, a multiple of S: every sub-slice gets grid / S of them
+            const unsigned grid = (unsigned)std::max<int64_t>(S, (int64_t)device_cu_count() / S * S);
             // shared equally by the segments; a segment's hot part stays below its stride
             const int64_t stage_bytes = (int64_t)kMergeWaves * stage * (int64_t)sizeof(T);
-            const int64_t hot_max = (int64_t)((kMergeLdsBytes / wpc - stage_bytes - 16) / (int64_t)sizeof(T) - 16) * S;
-            const bool lds_ok = plan.lds_ok && tune().slice_lds;
+            const int64_t hot_max = (int64_t)((kMergeLdsBytes - stage_bytes - 16) / (int64_t)sizeof(T) - 16) * S;
             HotSegs hs;
             hs.tbits = plan.seg_tbits;
             hs.nseg = plan.nseg;
             const int64_t seg_cap = plan.nseg == 1 ? plan.col_space : (1ll << plan.seg_tbits) - gsz;
-            hs.hs = lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
+            hs.hs = plan.lds_ok ? (int32_t)(std::min<int64_t>(hot_max / plan.nseg, seg_cap) / gsz * gsz) : 0;
             const int temporal = tune().merge_temporal == 2 || (tune().merge_temporal == 1 && plan.temporal);
             const size_t lds = hs.hs > 0 ? (size_t)(hs.nseg * (hs.hs / S) + 1) * sizeof(T) + (size_t)stage_bytes + 16 : 0;
-            auto go = [&](auto kern) { kern<<<grid, kMergeThreads, lds, ms>>>(ma, op, part, carry, hs, temporal); };
+            auto go = [&](auto kern) { kern<<<grid, kMergeThreads, lds, s>>>(ma, op, part, carry, hs, temporal); };
             if (hs.hs > 0) {
-                if (bd.width == 20) go(pull_merge_kernel<Op, true, 0, 20>);
-                else if (bd.width == 24) go(pull_merge_kernel<Op, true, 0, 24>);
-                else go(pull_merge_kernel<Op, true, 0, 32>);
+                if (bd.width == 20) go(pull_merge_kernel<Op, true, 20>);
+                else if (bd.width == 24) go(pull_merge_kernel<Op, true, 24>);
+                else go(pull_merge_kernel<Op, true, 32>);
             } else {
-                if (bd.width == 20) go(pull_merge_kernel<Op, false, 0, 20>);
-                else if (bd.width == 24) go(pull_merge_kernel<Op, false, 0, 24>);
-                else go(pull_merge_kernel<Op, false, 0, 32>);
+                if (bd.width == 20) go(pull_merge_kernel<Op, false, 20>);
+                else if (bd.width == 24) go(pull_merge_kernel<Op, false, 24>);
+                else go(pull_merge_kernel<Op, false, 32>);
             }
             JG_LAUNCH_CHECK();
-        }
-        if (mside) {
-            JG_HIP(hipEventRecord(mside->join, mside->stream));
-            JG_HIP(hipStreamWaitEvent(s, mside->join, 0));
         }
         FixupBands fx{};
         for (size_t bi = band0; bi < plan.bands.size(); ++bi) {
@@ -944,16 +838,9 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             JG_LAUNCH_CHECK();
         }
     }
+    // 4 gathers in flight per lane (8 measured no faster: RMAT-26 4.36 vs 4.32 ms, round 1)
     auto launch = [&](unsigned grid) {
-        const int u = tune().pull_unroll;
-        const bool nt = tune().pull_nt != 0;
-        if (u >= 8) {
-            if (nt) pull_kernel<Op, 8, true><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
-            else pull_kernel<Op, 8, false><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
-        } else {
-            if (nt) pull_kernel<Op, 4, true><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
-            else pull_kernel<Op, 4, false><<<grid, kBlock, 0, ls>>>(a, op, hub_partial);
-        }
+        pull_kernel<Op, 4><<<grid, kBlock, 0, s>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     };
     FinalizeBands fb{};
@@ -968,48 +855,12 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             ++fb.n;
         }
     }
-    // light rows through the persistent LDS-prefix kernel (every hub row is inside the split, so the
-    // light args hold no chunk work)
-    const bool light_lds = split && tune().light_lds > 0 && plan.lds_ok && plan.nseg == 1 &&
-                           plan.max_hub_row < plan.split_rows && !pull_split_launches() && side == nullptr;
-    const bool fuse = split && tune().fuse_finalize && !pull_split_launches() && side == nullptr && !light_lds;
-    if (light_lds) {
-        const int32_t hot = (int32_t)std::min<int64_t>(tune().light_lds, kMaxLdsBytes / (int64_t)sizeof(T));
-        static bool attr_l = false;
-        if (!attr_l) {
-            JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
-            attr_l = true;
-        }
-        if (a.class_block_begin[kNumClasses] > a.class_block_begin[1])
-            pull_lds_kernel<Op, 4, false><<<(unsigned)device_cu_count() * (hot <= 8192 ? 2u : 1u), kLdsThreads,
-                                            (size_t)hot * sizeof(T), s>>>(a, op, hot);
-        JG_LAUNCH_CHECK();
-    } else if (fuse) {
+    const bool fuse = split && !pull_split_launches();
+    if (fuse) {
         const int64_t fin_blocks = (plan.split_rows - caller_rows + kBlock - 1) / kBlock;
         const unsigned grid = (unsigned)(fin_blocks + blocks);
-        if (tune().pull_unroll >= 8)
-            pull_light_finalize_kernel<Op, 8, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                            plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
-        else if (tune().fin_pipe)
-            pull_light_finalize_kernel<Op, 4, false, true><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                                  plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
-        else
-            pull_light_finalize_kernel<Op, 4, false, false><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial,
-                                                                                   plan.split_rows, fin_blocks, tune().fin_last, caller_rows);
-        JG_LAUNCH_CHECK();
-    } else if (!split && tune().pull_lds > 0 && plan.lds_ok && plan.nseg == 1) {  // LDS-cached hot prefix (unsliced)
-        const int32_t hot = (int32_t)std::min<int64_t>(tune().pull_lds, kMaxLdsBytes / (int64_t)sizeof(T));
-        if (plan.num_chunks > 0) launch((unsigned)plan.num_chunks);  // hub chunks: blocks [0, num_chunks)
-        const size_t bytes = (size_t)hot * sizeof(T);
-        const unsigned grid = (unsigned)device_cu_count();
-        static bool attr = false;
-        if (!attr) {
-            JG_HIP(hipFuncSetAttribute((const void*)pull_lds_kernel<Op, 4, false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes));
-            attr = true;
-        }
-        pull_lds_kernel<Op, 4, false><<<grid, kLdsThreads, bytes, s>>>(a, op, hot);
+        pull_light_finalize_kernel<Op, 4><<<grid, kBlock, 0, s>>>(a, op, hub_partial, fb, split_partial, plan.split_rows,
+                                                                  fin_blocks, caller_rows);
         JG_LAUNCH_CHECK();
     } else if (pull_split_launches()) {  // diagnostic: one launch per degree class (per-class rocprof times)
         for (int c = 0; c < kNumClasses; ++c) {
@@ -1023,7 +874,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
     }
     // with the split, hub rows inside it are finalised by it (skip the launch when that is all of them)
     if (plan.num_hub_rows > 0 && !(split && plan.max_hub_row < plan.split_rows)) {
-        pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, ls>>>(a, op, hub_partial);
+        pull_hub_finalize_kernel<Op><<<grid_for(plan.num_hub_rows), kBlock, 0, s>>>(a, op, hub_partial);
         JG_LAUNCH_CHECK();
     }
     if (split && !fuse) {
@@ -1031,10 +882,6 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             pull_slice_finalize_kernel<Op><<<grid_for(plan.split_rows - caller_rows), kBlock, 0, s>>>(
                 caller_rows, plan.split_rows, op, fb, split_partial);
         JG_LAUNCH_CHECK();
-    }
-    if (side) {
-        JG_HIP(hipEventRecord(side->join, side->stream));
-        JG_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
     if (prof_ctx) prof_record_stop(*prof_ctx, *prof_shard);  // the whole superstep: every launch above
 }

@@ -108,7 +108,6 @@ struct BfsLevel {
     BfsState* st;             // [kBfsRing]
     int level, max_depth;
     double alpha, beta;
-    int grow_rule;  // switch to bottom-up only while the frontier grows (Tune::bfs_grow_rule)
 };
 
 // Direction choice (Beamer et al.): go bottom-up when the frontier's edges outweigh the unexplored
@@ -131,12 +130,9 @@ __device__ BfsState bfs_decide(const BfsLevel& a, int64_t* nf_out, int64_t* mf_o
         c.levels = a.level;
         return c;
     }
-    // top-down -> bottom-up only while the frontier grows (Beamer et al.: a small, shrinking frontier
-    // late in the traversal has few unexplored edges left, yet a bottom-up level would scan every
-    // unvisited row: RMAT-26's 4-vertex level took 83 us bottom-up)
-    const int64_t nf_prev = a.level >= 1 ? (int64_t)(a.ctr[(a.level + kBfsRing - 2) % kBfsRing] >> kPackShift) : 0;
-    const bool growing = !a.grow_rule || nf > nf_prev;
-    if (!p.bottom_up && a.pull_rp && (!a.push_rp || ((double)mf > (double)c.mu / a.alpha && growing))) {
+    // (Beamer's growth condition, bottom-up only while the frontier grows, measured RMAT-26 -0.6% and
+    // RMAT-20 +2.5%, round 2: not used)
+    if (!p.bottom_up && a.pull_rp && (!a.push_rp || (double)mf > (double)c.mu / a.alpha)) {
         c.bottom_up = 1;
         *switch_in = true;  // the previous frontier exists only as a queue: test depth == level instead
     } else if (p.bottom_up && a.push_rp && (double)nf < (double)a.rows / a.beta) {
@@ -318,14 +314,14 @@ __device__ __forceinline__ bool td_split(const BfsLevel& a, long long mf) {
     return a.split && mf >= a.split_min && mf <= a.split_max;
 }
 
-template <bool WAVE>
+// Appends are wave-staged (WaveStage: no block barrier per step; the block-wide staged append measured
+// RMAT-20 0.145-0.157 -> 0.119-0.129 ms, round 2).
 __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
     __shared__ BfsState s_st;
     __shared__ long long s_nf, s_mf;
     __shared__ int s_switch;
-    using Stage = std::conditional_t<WAVE, WaveStage, StagedAppend>;
-    using App = std::conditional_t<WAVE, WaveApp, BlockApp>;
-    __shared__ Stage s_app;
+    using App = WaveApp;
+    __shared__ WaveStage s_app;
     if (threadIdx.x == 0) {
         int64_t nf, mf;
         bool sw;
@@ -358,13 +354,11 @@ __global__ __launch_bounds__(kBlock) void bfs_level_kernel(BfsLevel a) {
 
 // Second launch of a split top-down level: the level's state (bfs_level_kernel wrote it) and input
 // frontier counter say whether the level was split; if so, every entry re-reads its target's owner.
-template <bool WAVE>
 __global__ __launch_bounds__(kBlock) void bfs_td_claim_kernel(BfsLevel a) {
     __shared__ long long s_nf, s_mf;
     __shared__ int s_run;
-    using Stage = std::conditional_t<WAVE, WaveStage, StagedAppend>;
-    using App = std::conditional_t<WAVE, WaveApp, BlockApp>;
-    __shared__ Stage s_app;
+    using App = WaveApp;
+    __shared__ WaveStage s_app;
     if (threadIdx.x == 0) {
         const BfsState c = a.st[a.level % kBfsRing];
         const unsigned long long h = a.ctr[(a.level + kBfsRing - 1) % kBfsRing];
@@ -690,66 +684,6 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_kernel(const unsigned l
     app.final(queue, qoff, packed);
 }
 
-// ---- split pull levels (msbfs_srcsplit): the sources whose frontier is small go top-down ----
-// A pull row can stop early only when every live source it lacks arrives this level; a source whose
-// frontier is still small (a few rows two hops out) reaches almost no row yet, so on the first pull
-// level it keeps every hub row scanning its whole row.  A split level pulls with live' = the big
-// sources only (the hub band exits early: RMAT-22, band 0 scans 0.2% instead of 60% of the entries,
-// tools/msbfs_split_sim.py) and pushes the small sources' bits top-down into a scratch vector, which
-// msbfs_split_apply_kernel merges into the pulled words.
-
-// out[s] += the push entries of the rows whose word holds source s (one LDS histogram per workgroup)
-__global__ __launch_bounds__(kRedThreads) void msbfs_source_entries_kernel(const unsigned long long* __restrict__ F,
-                                                                          int64_t rows,
-                                                                          const int64_t* __restrict__ push_rp,
-                                                                          unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long cnt[64];
-    if (threadIdx.x < 64) cnt[threadIdx.x] = 0ull;
-    __syncthreads();
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
-        unsigned long long w = F[v];
-        if (!w) continue;
-        const unsigned long long d = (unsigned long long)(push_rp[v + 1] - push_rp[v]);
-        while (w) {
-            atomicAdd(&cnt[__ffsll(w) - 1], d);
-            w &= w - 1;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64 && cnt[threadIdx.x]) atomicAdd(&out[threadIdx.x], cnt[threadIdx.x]);
-}
-
-// *dst = *src & mask (the split level's pull live bits, on the device: the host never reads live)
-__global__ void msbfs_mask_word_kernel(const unsigned long long* __restrict__ src, unsigned long long mask,
-                                      unsigned long long* __restrict__ dst) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *dst = *src & mask;
-}
-
-// The small sources' bits of the split level, pushed into T: merged into the pulled words.  A touched
-// row's bits are disjoint from the pulled ones (other sources), so its word, visited bits and new-bit
-// word are ORed, and T is cleared behind.
-__global__ __launch_bounds__(kBlock) void msbfs_split_apply_kernel(const int32_t* __restrict__ touched,
-                                                                   const unsigned long long* __restrict__ tcount,
-                                                                   unsigned long long* __restrict__ T, MsBfsOp op) {
-    const int64_t nt = (int64_t)(*tcount >> kPackShift);
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nt; x += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t u = touched[x];
-        unsigned long long nw = T[u] & ~op.visited[u];
-        T[u] = 0ull;
-        if (!nw) continue;
-        op.Fout[op.pos(u)] |= nw;
-        op.visited[u] |= nw;
-        if (op.nwl) op.nwl[u] |= nw;
-        if (op.changed) *op.changed = 1;
-        while (nw) {
-            const int s = __ffsll(nw) - 1;
-            if (op.depth8) op.depth8[(int64_t)s * op.rows + u] = (uint8_t)op.lvl;
-            else if (op.depth) op.depth[(int64_t)s * op.rows + u] = op.lvl;
-            nw &= nw - 1;
-        }
-    }
-}
-
 // msbfs_frontier_kernel and msbfs_scan_kernel in one pass, after a pull level whose successor is
 // expected to run top-down (its exit bands had almost no live task): the queue, the packed counter
 // and the live bits (*live |= the OR of the words, one atomic per block)
@@ -795,24 +729,20 @@ __global__ __launch_bounds__(kWave) void msbfs_source_queue_kernel(const int64_t
     if (i == kWave - 1) packed[0] = ((unsigned long long)cnt << kPackShift) | (unsigned long long)inc;
 }
 
-// ---- bottom-up pull levels of the bit-parallel BFS with early exit (one shard) ----
+// ---- bottom-up rows of the bit-parallel BFS with early exit (one shard) ----
 // A row's gain this level is the OR of its neighbours' frontier words masked by need = ~visited & live;
 // once the OR covers need, no further entry can add a bit, so the scan stops (Beamer's bottom-up
-// early exit, per 64-bit word).  On a level whose frontier is large (most sources reach most rows)
-// nearly every row stops within its first entries (the CSR rows are column-ordered, hubs first):
-// RMAT-22, the level after the frontier's peak: 53 M -> 2.4 M entries (tools/msbfs_bu_sim).
-// The result equals the merge engine's: the same OR, the same finalize.  Rows [0, hub) take a
-// workgroup each (4 x 1024 entries in flight per step, a block-wide OR), [hub, wave) a wave each
-// (4 x 64), [wave, ne) a lane each (4 at a time), [ne, rows) have no entries and gain nothing.
+// early exit, per 64-bit word).  The result equals the merge engine's: the same OR, the same finalize.
+// (Every pull level bottom-up, rows [0, ne) by workgroup / wave / lane roles, measured 2-4x slower than
+// the merge engine at RMAT-22 / 26, round 3: the exit pays only on the levels after the frontier's peak.)
+constexpr int kMsBuUnroll = 4;  // pass B: 4 x 64 entries in flight per wave step
 struct MsBu {
     const int64_t* rp;
     const int32_t* col;
-    int64_t rows, hub, wave, ne;
-    int64_t blocks_hub, blocks_wave;  // first blocks of the wave and lane roles
+    int64_t rows;                     // rows [0, rows) take the early exit
     unsigned long long* examined;     // += the entries scanned (work counter, jg_stats.algorithmic_bytes)
     int first = 16;                   // msbfs_exit_first_kernel: entries a lane scans before pass B takes the row
 };
-constexpr int kMsBuUnroll = 4;
 
 __device__ __forceinline__ unsigned long long wave_or(unsigned long long m) {
 #pragma unroll
@@ -820,104 +750,10 @@ __device__ __forceinline__ unsigned long long wave_or(unsigned long long m) {
     return m;
 }
 
-// The entries scanned are summed per workgroup, one atomic each at the end (a lane-0 atomic per row, as
-// round 3 had it, queued up to a million of them on one counter).
-__global__ __launch_bounds__(kMergeThreads) void msbfs_bu_kernel(MsBu a, MsBfsOp op) {
-    __shared__ unsigned long long red[kMergeWaves];
-    __shared__ int stop;
-    const unsigned long long live = *op.live;
-    const int lane = lane_id(), wv = threadIdx.x / kWave;
-    unsigned long long scanned = 0;
-    if ((int64_t)blockIdx.x < a.blocks_hub) {  // hub rows: a workgroup each
-        for (int64_t v = blockIdx.x; v < a.hub; v += a.blocks_hub) {
-            const unsigned long long need = ~op.visited[v] & live;  // block-uniform
-            unsigned long long acc = 0;
-            if (need) {
-                const int64_t e1 = a.rp[v + 1];
-                for (int64_t j = a.rp[v]; j < e1; j += kMsBuUnroll * kMergeThreads) {
-                    int32_t c[kMsBuUnroll];
-#pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) {
-                        const int64_t e = j + u * kMergeThreads + threadIdx.x;
-                        c[u] = e < e1 ? a.col[e] : -1;
-                    }
-                    unsigned long long m = 0;
-#pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
-                    m = wave_or(m & need);
-                    if (lane == 0) red[wv] = m;
-                    __syncthreads();
-                    if (threadIdx.x == 0) {
-                        unsigned long long t = acc;
-                        for (int w = 0; w < kMergeWaves; ++w) t |= red[w];
-                        red[0] = t;
-                        stop = t == need;
-                    }
-                    __syncthreads();
-                    acc = red[0];
-                    const int done = stop;
-                    __syncthreads();  // red / stop are rewritten by the next step
-                    if (threadIdx.x == 0) scanned += (unsigned long long)min((int64_t)kMsBuUnroll * kMergeThreads, e1 - j);
-                    if (done) break;
-                }
-            }
-            if (threadIdx.x == 0) op.finalize(v, acc);
-        }
-    } else if ((int64_t)blockIdx.x < a.blocks_wave) {  // rows of 64 .. hub entries: a wave each
-        const int64_t nw = (a.blocks_wave - a.blocks_hub) * kMergeWaves;
-        for (int64_t v = a.hub + ((int64_t)blockIdx.x - a.blocks_hub) * kMergeWaves + wv; v < a.wave; v += nw) {
-            const unsigned long long need = ~op.visited[v] & live;  // wave-uniform
-            unsigned long long acc = 0;
-            if (need) {
-                const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
-                int64_t j = e0;
-                for (; j < e1 && acc != need; j += kMsBuUnroll * kWave) {
-                    int32_t c[kMsBuUnroll];
-#pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) {
-                        const int64_t e = j + u * kWave + lane;
-                        c[u] = e < e1 ? a.col[e] : -1;
-                    }
-                    unsigned long long m = 0;
-#pragma unroll
-                    for (int u = 0; u < kMsBuUnroll; ++u) m |= c[u] >= 0 ? op.F[c[u]] : 0ull;
-                    acc |= wave_or(m & need);
-                }
-                if (lane == 0) scanned += (unsigned long long)(min(j, e1) - e0);
-            }
-            if (lane == 0) op.finalize(v, acc);
-        }
-    } else {  // light rows: a lane each; rows past ne have no entries
-        const int64_t nt = ((int64_t)gridDim.x - a.blocks_wave) * kMergeThreads;
-        for (int64_t v = a.wave + ((int64_t)blockIdx.x - a.blocks_wave) * kMergeThreads + threadIdx.x; v < a.rows;
-             v += nt) {
-            unsigned long long acc = 0;
-            if (v < a.ne) {
-                const unsigned long long need = ~op.visited[v] & live;
-                if (need) {
-                    const int64_t e0 = a.rp[v], e1 = a.rp[v + 1];
-                    int64_t j = e0;
-                    for (; j < e1 && acc != need; j += kMsBuUnroll) {
-                        int32_t c[kMsBuUnroll];
-#pragma unroll
-                        for (int u = 0; u < kMsBuUnroll; ++u) c[u] = a.col[j + u < e1 ? j + u : e1 - 1];
-#pragma unroll
-                        for (int u = 0; u < kMsBuUnroll; ++u) acc |= op.F[c[u]] & need;
-                    }
-                    scanned += (unsigned long long)(min(j, e1) - e0);
-                }
-            }
-            op.finalize(v, acc);
-        }
-    }
-    scanned = block_reduce(scanned, AddU64{}, red);  // every role is block-uniform
-    if (threadIdx.x == 0 && scanned) atomicAdd(a.examined, scanned);
-}
-
 // ---- the split's first band with early exit, inside a merged pull level (msbfs_exit) ----
 // On the level after the frontier's peak a hub row typically finds every unvisited live bit within its
 // first two or three entries (RMAT-22: 2.4 on average; tools/msbfs_exit_sim.py), so a 256-entry wave
-// step (msbfs_bu_kernel's wave role) gathers ~100x what the row needs.  Pass A gives each row a lane
+// step gathers ~100x what the row needs.  Pass A gives each row a lane
 // and its first `first` entries (MsBu::first, Tune::msbfs_exit_first; 16 by default); a row still missing bits leaves its partial word in Fout and a bit
 // in `rest` (one word per 64 rows, a plain store per wave), and pass B scans the remaining entries of
 // those rows a wave each.  Entries scanned are summed per 1024-thread workgroup, one atomic each.
@@ -995,16 +831,6 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_exit_rest_kernel(MsBu a, Ms
     if (threadIdx.x == 0 && scanned) atomicAdd(a.examined, scanned);
 }
 
-// the first row whose degree is below d (rows are degree-sorted, descending)
-__global__ void degree_bound_kernel(const int64_t* __restrict__ rp, int64_t rows, int64_t d, int64_t* __restrict__ out) {
-    int64_t lo = 0, hi = rows;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (rp[mid + 1] - rp[mid] >= d) lo = mid + 1; else hi = mid;
-    }
-    *out = lo;
-}
-
 constexpr int kMaxPeersMs = 64;
 __device__ __forceinline__ int slot_peer(int32_t u, int tbits, int r) {
     const int seg = (int)((uint32_t)u >> tbits);
@@ -1021,7 +847,7 @@ struct MsTd {
     const unsigned long long* visited;
     unsigned long long* Fnext;
     int32_t* touched;
-    int64_t* touched_off;  // scratch (block_append_frontier writes edge offsets)
+    int64_t* touched_off;  // scratch (the appender writes edge offsets)
     unsigned long long* tpacked;
     int tbits;             // sharded (compact BOTH columns): u >> tbits != 0 is a peer's vertex; 31 on one shard
     // sharded: the halo staging vector (compact positions; zero outside a level) and the list of its
@@ -1033,7 +859,6 @@ struct MsTd {
     // (unused: the per-peer counts of the sparse reverse exchange come from msbfs_slot_hist_kernel)
     unsigned long long* pcnt;
     int r, P;                  // this shard's index, the shard count
-    unsigned long long mask;   // the sources this push carries (~0: all; a split level: its small sources)
     int probe_visited;         // 0: no visited probe before the OR (the apply masks with visited anyway)
     int no_touched;            // 1: no touched list (the level's apply passes over every row instead)
 };
@@ -1070,7 +895,7 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_kernel(MsTd a) {
                 }
                 const int32_t v = a.queue[i];
                 u = a.push_col[a.push_rp[v] + (e - a.qoff[i])];
-                const unsigned long long fv = a.F[v] & a.mask;
+                const unsigned long long fv = a.F[v];
                 if ((u >> a.tbits) == 0) {
                     const unsigned long long w = fv & ~(a.probe_visited ? a.visited[u] : 0ull);
                     // a plain read first: a hub neighbour already holding these bits takes no atomic (the
@@ -1581,7 +1406,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
                                                           sh.bfs_qoff[0].get(), degcsr->row_ptr.get(),
                                                           (long long)degcsr->nnz, sh.bfs_ctr.get(), st,
                                                           sh.bfs_seen.get(), pull ? pull->row_ptr.get() : nullptr,
-                                                          pull && tune().bfs_init_suffix ? pull->empty_from : -1);
+                                                          pull ? pull->empty_from : -1);
     }
     JG_LAUNCH_CHECK();
     BfsLevel a{};
@@ -1598,7 +1423,6 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.max_depth = max_depth;
     a.alpha = (double)(roots ? tune().bfs_alpha : tune().dobfs_alpha);
     a.beta = (double)tune().bfs_beta;
-    a.grow_rule = tune().bfs_grow_rule;
     a.owner = sh.bfs_owner.get();
     a.split_min = (long long)tune().bfs_td_split_min;
     a.split_max = (long long)tune().bfs_td_split_max;
@@ -1642,12 +1466,10 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             a.split = a.owner && (split_mode == 1 || (split_mode == 2 && level < 16 && ((split_levels >> level) & 1)));
             if (prof_enabled(ctx)) prof_record_start(ctx, sh);
             const unsigned lg = predicted > 0 && level >= predicted ? tail_grid : grid;
-            if (tune().bfs_wave_stage) bfs_level_kernel<true><<<lg, kBlock, 0, s>>>(a);
-            else bfs_level_kernel<false><<<lg, kBlock, 0, s>>>(a);
+            bfs_level_kernel<<<lg, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             if (a.split) {
-                if (tune().bfs_wave_stage) bfs_td_claim_kernel<true><<<lg, kBlock, 0, s>>>(a);
-                else bfs_td_claim_kernel<false><<<lg, kBlock, 0, s>>>(a);
+                bfs_td_claim_kernel<<<lg, kBlock, 0, s>>>(a);
                 JG_LAUNCH_CHECK();
             }
             if (prof_enabled(ctx)) prof_record_stop(ctx, sh);
@@ -2422,22 +2244,15 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DevBuf<unsigned long long> nwl;   // [kMsLevelWords][rows] new-bit words of levels 0 .. kMsLevelWords-1
                 DevBuf<unsigned long long> hub, split;
                 DevBuf<unsigned long long> live;  // [0] the pull level's live bits, [1] all sources (top-down)
-                DevBuf<unsigned long long> xrest;  // msbfs_exit: the band-0 rows pass B scans (a bit per row)
-                MsBu bx{};                         // msbfs_exit: band 0's rows (bx.rows 0: off on this shard)
-                MsBu bx1{};                        // the same over band 0 only (split levels)
-                DevBuf<unsigned long long> tnext;  // msbfs_srcsplit: the small sources' pushed words (one shard)
-                DevBuf<unsigned long long> srcent; // msbfs_srcsplit: push entries per source
-                int64_t exit_tasks = 0;            // the probed exit bands' merge tasks
-                size_t exit_nbands = 0;
-                size_t probe_nbands = 0;           // the leading exit bands whose live tasks decide (msbfs_exit_probe)
-                bool exit_all = false;  // msbfs_exit_all: the exit rows are every row
-                int64_t all_rows = 0;   // the rows a pull level finalises (those with entries under msbfs_skip_empty)
+                DevBuf<unsigned long long> xrest;  // msbfs_exit: the rows pass B scans (a bit per row)
+                MsBu bx{};                         // msbfs_exit: every row with entries (bx.rows 0: off on this shard)
+                int64_t exit_tasks = 0;            // band 0's merge tasks (its live count decides an exit level)
+                int64_t all_rows = 0;   // the rows a pull level finalises (those with entries)
                 int exit_all_levels = 0;
                 // merge tasks of the bands the exit kernels took instead (on levels that count every task, and on all)
                 double exit_unskipped_tasks = 0, exit_level_tasks = 0;
                 unsigned long long b0_live_merged = 0;     // msbfs_exit 1: band 0's live tasks of levels that merged it
-                bool tnext_zero = false;                   // tnext cleared in this call
-                double xlive_permille = 1000.0;            // the last probe's live share of the exit bands' tasks
+                double xlive_permille = 1000.0;            // the last probe's live share of band 0's tasks
                 std::vector<DevBuf<unsigned long long>> todo, tlive;  // per band: row and task bitmaps
                 DevBuf<int64_t> dloc;             // [64] each source's own row (-1: another shard's)
                 // levels recorded as (row, new word) records instead of nwl words (level 0 from the sources and
@@ -2509,15 +2324,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 t.live.alloc(3);  // [2]: a split level's pull live bits
                 t.work.alloc(4);
                 JG_HIP(hipMemsetAsync(t.work.get(), 0, 4 * sizeof(unsigned long long), sh.stream));
-                if (tune().msbfs_srcsplit > 0 && g.shards.size() == 1 && g.P == 1 && c.push) {
-                    t.tnext.alloc(std::max<int64_t>(sh.rows, 1));
-                    t.srcent.alloc(64);
-                }
                 if (tune().msbfs_exit > 0 && t.split.size() && !plan.bands.empty())
-                    t.xrest.alloc(std::max<int64_t>(
-                        ((tune().msbfs_exit_all ? sh.rows
-                                                : plan.bands[std::min<size_t>(plan.bands.size(), (size_t)tune().msbfs_exit_bands) - 1]->row_end) +
-                         63) / 64, 1));
+                    t.xrest.alloc(std::max<int64_t>((sh.rows + 63) / 64, 1));
                 t.light_nnz = c.pull->nnz;
                 if (t.split.size() && plan.split_rows > 0) {
                     int64_t split_nnz = 0;
@@ -2649,7 +2457,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
                 if (tds[i].hs.size()) zero_gathered(g, sh, JG_ADJ_BOTH, tds[i].hs.get(), sizeof(unsigned long long));
                 St::Rec* r0 = nullptr;
-                if (td_ok && tune().msbfs_diag != 1) {  // level 0 as records of the source rows
+                if (td_ok) {  // level 0 as records of the source rows
                     t.recs.emplace_back();
                     r0 = &t.recs.back();
                     r0->level = 0;
@@ -2718,7 +2526,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             };
             // levels whose depths are nwl words (bit L): a pull level finalises every own row (its word is
             // written, zero or not); a top-down level records (row, word) pairs of the rows it reached
-            unsigned word_levels = (td_ok && tune().msbfs_diag != 1) ? 0u : 1u;
+            unsigned word_levels = td_ok ? 0u : 1u;
             // the caller's int32 planes: the widened byte / int32 planes, then the word-recorded levels
             auto materialize = [&](int levels_run) {
                 widen();
@@ -2729,8 +2537,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     const int lw = std::min(levels_run + 1, kMsLevelWords);
                     if (sh.rows > 0) {
                         const Csr* pc = pick_csrs(sh, direction).pull;
-                        const int64_t ne = tune().msbfs_skip_empty && pc->empty_from >= 0 ? std::min(pc->empty_from, sh.rows)
-                                                                                            : sh.rows;
+                        const int64_t ne = pc->empty_from >= 0 ? std::min(pc->empty_from, sh.rows) : sh.rows;
                         msbfs_levels_to_planes_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
                             t.nwl.get(), lw, word_levels, sh.rows, ne, ns, t.depth.get());
                         JG_LAUNCH_CHECK();
@@ -2744,68 +2551,29 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     JG_HIP(hipStreamSynchronize(sh.stream));
                 }
             };
-            // one shard: pull levels whose frontier holds at least msbfs_bu_frac / 1000 of the rows run
-            // bottom-up with early exit (msbfs_bu_kernel) instead of through the merge engine
-            MsBu bu{};
-            // msbfs_bu: 1 every pull level, 2 levels whose frontier holds >= msbfs_bu_frac permille of the rows,
-            // 3 levels where fewer than msbfs_bu_tasks permille of the merge tasks can gain a bit (0, the default:
-            // the merge engine skips dead tasks cheaply enough that each variant measured slower)
-            const bool bu_ok = td_one && c0.pull == c0.push && tune().msbfs_bu > 0;
-            if (bu_ok) {
-                DevBuf<int64_t> bnd(2);
-                degree_bound_kernel<<<1, 1, 0, sh0.stream>>>(c0.pull->row_ptr.get(), sh0.rows, 4096, bnd.get());
-                degree_bound_kernel<<<1, 1, 0, sh0.stream>>>(c0.pull->row_ptr.get(), sh0.rows, kWave, bnd.get() + 1);
-                JG_LAUNCH_CHECK();
-                int64_t hb[2] = {0, 0};
-                copy_d2h(hb, bnd.get(), sizeof hb, sh0.stream);
-                bu.rp = c0.pull->row_ptr.get();
-                bu.col = c0.pull->col.get();
-                bu.rows = sh0.rows;
-                bu.hub = hb[0];
-                bu.wave = hb[1];
-                bu.ne = c0.pull->empty_from >= 0 ? std::min(c0.pull->empty_from, sh0.rows) : sh0.rows;
-                bu.blocks_hub = std::min<int64_t>(bu.hub, 256);
-                bu.blocks_wave = bu.blocks_hub + std::min<int64_t>((bu.wave - bu.hub + kMergeWaves - 1) / kMergeWaves, 2048);
-                bu.examined = st[0].work.get() + 2;
-            }
-            const int64_t bu_rows = bu_ok ? sh0.rows * (int64_t)tune().msbfs_bu_frac / 1000 : 0;
-            // msbfs_exit: the split's first band (rows of >= band0_deg entries, hubs first) scans its rows with
-            // early exit (msbfs_exit_first_kernel / msbfs_exit_rest_kernel) on pull levels where few of its
-            // merge tasks are live; every other row stays with the merge engine (launch_pull's caller_rows).
-            // On the level after the frontier's peak a hub row finds all its unvisited live bits within its
-            // first entries: RMAT-22, band 0 examines 0.1% instead of 27.3% of the entries
-            // (tools/msbfs_exit_sim.py).  Each shard decides for its own rows.
+            // msbfs_exit: every row with entries scans its row with early exit (msbfs_exit_first_kernel /
+            // msbfs_exit_rest_kernel) on pull levels where few of band 0's merge tasks are live, and such a
+            // level runs no merge launch at all.  On the level after the frontier's peak a hub row finds all
+            // its unvisited live bits within its first entries: RMAT-22, band 0 examines 0.1% instead of
+            // 27.3% of the entries (tools/msbfs_exit_sim.py).  Band 0's live tasks alone decide
+            // (every exit band's bitmaps took the same decisions, round 4); each shard decides for its own
+            // rows.  (Only the exit bands through the exit, the light rows merged: RMAT-26 11.42 vs 11.20 ms.)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
                 const BfsCsrs c = pick_csrs(sh, direction);
                 const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
                 St& t = st[i];
-                if (tune().msbfs_exit > 0 && tune().msbfs_bu == 0 && tune().pull_split && plan.split_rows > 0 &&
-                    !plan.bands.empty() && t.xrest.size() > 0 && plan.bands[0]->row_begin == 0 &&
-                    plan.bands[0]->row_end > 0) {
+                if (tune().msbfs_exit > 0 && tune().pull_split && plan.split_rows > 0 && !plan.bands.empty() &&
+                    t.xrest.size() > 0 && plan.bands[0]->row_begin == 0 && plan.bands[0]->row_end > 0) {
                     t.bx.rp = c.pull->row_ptr.get();
                     t.bx.col = c.pull->col.get();
-                    // the first msbfs_exit_bands bands (their rows: a prefix of the split)
-                    // (msbfs_exit_all: every row; the level then runs no merge engine and no light kernel)
-                    const size_t k = tune().msbfs_exit_all ? plan.bands.size()
-                                                           : std::min<size_t>(plan.bands.size(), (size_t)tune().msbfs_exit_bands);
-                    t.exit_all = tune().msbfs_exit_all != 0;
-                    // (exit_all: every row with entries when the pull levels skip the empty ones, else every row)
-                    const int64_t all_rows = tune().msbfs_skip_empty && c.pull->empty_from >= 0
-                                                 ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
-                    t.all_rows = all_rows;
-                    t.bx.rows = t.bx.wave = t.bx.ne = t.exit_all ? all_rows : plan.bands[k - 1]->row_end;  // (the exit kernels use rp, col, rows, examined)
+                    t.all_rows = c.pull->empty_from >= 0 ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
+                    t.bx.rows = t.all_rows;
                     t.bx.examined = t.work.get() + 2;
                     t.bx.first = tune().msbfs_exit_first;
-                    t.bx1 = t.bx;
-                    t.bx1.rows = t.bx1.wave = t.bx1.ne = plan.bands[0]->row_end;
-                    t.exit_nbands = k;
-                    t.probe_nbands = tune().msbfs_exit_probe > 0 ? std::min<size_t>(k, (size_t)tune().msbfs_exit_probe) : k;
-                    for (size_t b = 0; b < t.probe_nbands; ++b) t.exit_tasks += plan.bands[b]->tasks;
+                    t.exit_tasks = plan.bands[0]->tasks;
                 }
             }
-            int bu_levels = 0;
-            unsigned long long bu_task_credit = 0;  // live tasks counted by levels that then ran bottom-up
             bool queued = td_ok, live_ready = false;
             bool prev_td = false;  // the previous level ran top-down: F[cur ^ 1]'s nonzero own words are
                                    // exactly its input queue (tds[i].queue[qc ^ 1][0, nq_in))
@@ -2819,7 +2587,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 if (level + 1 >= kMsLevelWords) ensure_depth8();
                 if (level + 1 >= 255) widen();
                 const bool td_level = td_ok && (double)g_mf < (double)push_nnz / (double)tune().bfs_alpha;
-                // a pull level (merge engine or msbfs_bu_kernel) finalises every own row: its words need no clearing
+                // a pull level (merge engine or the exit kernels) finalises every own row: its words need no clearing
                 if (!td_level && level + 1 < kMsLevelWords) word_levels |= 1u << (level + 1);
                 if (td_level && !queued) {
                     build_frontier(qc ^ 1);
@@ -2827,7 +2595,6 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
                 const bool have_live = live_ready;
                 queued = live_ready = false;
-                bool level_bu = false;  // this pull level ran msbfs_bu_kernel
                 bool queued_next = false;  // this pull level built the next level's top-down queue
                 if (td_level) {
                     std::vector<void*> fv, rv;
@@ -2853,11 +2620,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 JG_LAUNCH_CHECK();
                             }
                         } else if (level > 0) {  // level 0: F[1] is as the init zeroed it
-                            // rows without pull entries (msbfs_skip_empty) are never written after level 0: their
-                            // words are zero except an isolated source's level-0 word, cleared apart (RMAT-26:
-                            // 215 of 537 MB cleared)
-                            const int64_t ne = tune().msbfs_skip_empty && c.pull && c.pull->empty_from >= 0
-                                                   ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
+                            // rows without pull entries are never written after level 0: their words are zero
+                            // except an isolated source's level-0 word, cleared apart (RMAT-26: 215 of 537 MB
+                            // cleared)
+                            const int64_t ne = c.pull && c.pull->empty_from >= 0 ? std::min(c.pull->empty_from, sh.rows)
+                                                                                 : sh.rows;
                             JG_HIP(hipMemsetAsync(t.F[cur ^ 1].get(), 0, (size_t)ne * sizeof(unsigned long long), sh.stream));
                             if (ne < sh.rows && !td.src_rows.empty()) {
                                 msbfs_zero_tail_sources_kernel<<<1, kWave, 0, sh.stream>>>(
@@ -2874,7 +2641,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                    c.push->col.get(), t.F[cur].get(), t.vis.get(), t.F[cur ^ 1].get(), td.touched.get(),
                                    td.touched_off.get(), td.ctr.get() + 1, td_shard ? sh.halo_both.tbits : 31,
                                    td_shard ? td.hs.get() : nullptr, td.hlist.get(), td.hlist_off.get(), td.ctr.get() + 2,
-                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P, ~0ull,
+                                   td_shard && td.pcnt.size() ? td.pcnt.get() : nullptr, sh.index, g.P,
                                    // the first top-down levels skip the visited probe: next to nothing is visited
                                    // yet, and it is a random 8-byte read per edge (RMAT-26 level 1: 33.6 M)
                                    level >= tune().msbfs_td_noprobe ? 1 : 0, td.rowapply ? 1 : 0};
@@ -3015,7 +2782,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             op.Fout = t.F[cur ^ 1].get();
                             op.visited = t.vis.get();
                             op.depth = t.depth.get();
-                            op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
+                            op.depth8 = t.depth8.get();
                             op.nwl = nullptr;  // recorded from the next queue below (msbfs_td_record_kernel)
                             op.changed = t.changed.get();
                             op.rows = sh.rows;
@@ -3034,7 +2801,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         }
                     }
                     read_frontier(&td_touched);
-                    if (level + 1 < kMsLevelWords && tune().msbfs_diag != 1)
+                    if (level + 1 < kMsLevelWords)
                         for (size_t i = 0; i < g.shards.size(); ++i) {  // the level's depths: its new queue
                             Shard& sh = *g.shards[i];
                             DeviceGuard dg(sh.device);
@@ -3075,10 +2842,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         // (with the top-down path the frontier count ends the traversal: no changed flag, whose
                         // one-word store every gaining row's wave would repeat)
                         if (!td_ok) JG_HIP(hipMemsetAsync(t.changed.get(), 0, sizeof(int32_t), sh.stream));
-                        // rows without pull entries are not written by a pull level (msbfs_skip_empty): a source
-                        // among them keeps its level-0 word in this output vector unless cleared here, and the
-                        // frontier scan would count it (one extra level)
-                        if (td_ok && tune().msbfs_skip_empty && c.pull->empty_from >= 0 &&
+                        // rows without pull entries are not written by a pull level: a source among them keeps
+                        // its level-0 word in this output vector unless cleared here, and the frontier scan would
+                        // count it (one extra level)
+                        if (td_ok && c.pull->empty_from >= 0 &&
                             c.pull->empty_from < sh.rows && !tds[i].src_rows.empty()) {
                             msbfs_zero_tail_sources_kernel<<<1, kWave, 0, sh.stream>>>(
                                 t.F[cur ^ 1].get(), tds[i].srcs.get(), (int)tds[i].src_rows.size(), c.pull->empty_from);
@@ -3089,8 +2856,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         op.Fout = t.F[cur ^ 1].get();
                         op.visited = t.vis.get();
                         op.depth = t.depth.get();
-                        op.depth8 = tune().msbfs_diag == 1 ? nullptr : t.depth8.get();
-                            op.nwl = level + 1 < kMsLevelWords && tune().msbfs_diag != 1 ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
+                        op.depth8 = t.depth8.get();
+                        op.nwl = level + 1 < kMsLevelWords ? t.nwl.get() + (int64_t)(level + 1) * sh.rows : nullptr;
                         op.changed = td_ok ? nullptr : t.changed.get();
                         op.rows = sh.rows;
                         op.pos = g.vec_pos(sh, adj_of(sh, c));
@@ -3108,122 +2875,53 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                         }
                         op.live = lw;
-                        // msbfs_srcsplit: sources whose frontier holds fewer than msbfs_srcsplit_permille of the push
-                        // entries go top-down after the pull (their bits pushed into tnext); the pull then
-                        // runs on the other sources' live bits, and band 0 exits early
-                        unsigned long long small = 0;
-                        if (t.tnext.size() && t.bx1.rows > 0 && td_ok &&
-                            (tune().msbfs_srcsplit == 2 || (tune().msbfs_srcsplit == 1 && pull_levels == 0))) {
-                            JG_HIP(hipMemsetAsync(t.srcent.get(), 0, 64 * sizeof(unsigned long long), sh.stream));
-                            msbfs_source_entries_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
-                                t.F[cur].get(), sh.rows, c.push->row_ptr.get(), t.srcent.get());
-                            JG_LAUNCH_CHECK();
-                            unsigned long long ent[64];
-                            copy_d2h(ent, t.srcent.get(), sizeof ent, sh.stream);
-                            const double lim = (double)push_nnz * (double)tune().msbfs_srcsplit_permille / 1000.0;
-                            double small_sum = 0;
-                            unsigned long long big = 0;
-                            for (int b = 0; b < 64; ++b) {
-                                if (!ent[b]) continue;
-                                if ((double)ent[b] < lim) {
-                                    small |= 1ull << b;
-                                    small_sum += (double)ent[b];
-                                } else {
-                                    big |= 1ull << b;
-                                }
-                            }
-                            // all small: the level would have run top-down; too many small entries: plain pull
-                            if (!big || small_sum * (double)tune().bfs_alpha > (double)push_nnz) small = 0;
-                            if (debug_bfs())
-                                std::fprintf(stderr, "[jg msbfs] level %d pull: %d big, %d small sources (%.0f push entries) -> %s\n",
-                                             level, __builtin_popcountll(big), __builtin_popcountll(small), small_sum,
-                                             small ? "split" : "pull");
-                            if (small) {
-                                msbfs_mask_word_kernel<<<1, 1, 0, sh.stream>>>(lw, ~small, lw + 2);
-                                JG_LAUNCH_CHECK();
-                                op.live = lw + 2;
-                            }
-                        }
-                        // sparse levels (msbfs_bu 3): the task bitmaps first; when few tasks hold a row that can
-                        // still gain a bit (RMAT-26's last pull level: ~0.2% of the entries), the early-exit
-                        // bottom-up kernel visits those rows' entries only, instead of the merge engine's
-                        // per-round LDS images over every sub-slice
-                        const bool no_bitmaps = tune().msbfs_skip_first && pull_levels == 0;
-                        // msbfs_exit 1: band 0's rows exit early on pull levels where fewer than msbfs_exit_live
-                        // permille of its merge tasks hold a row that can still gain a bit (their live count
-                        // is read back once); 2: on every pull level
-                        const MsBu& bx = small ? t.bx1 : t.bx;  // a split level: band 0 exits early, always
-                        int64_t exit_rows = bx.rows > 0 && (tune().msbfs_exit == 2 || small) ? bx.rows : 0;
+                        // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows can be
+                        // done there; every task runs, the finalize's live mask keeps it exact)
+                        const bool no_bitmaps = pull_levels == 0;
+                        // msbfs_exit 1: every row with entries exits early on pull levels where fewer than
+                        // msbfs_exit_live permille of band 0's merge tasks hold a row that can still gain a bit
+                        // (their live count is read back once); 2: on every pull level
+                        const MsBu& bx = t.bx;
+                        int64_t exit_rows = bx.rows > 0 && tune().msbfs_exit == 2 ? bx.rows : 0;
                         const bool exit_probe = bx.rows > 0 && tune().msbfs_exit == 1 && !no_bitmaps && !t.todo.empty();
                         std::vector<const uint32_t*> tl;
-                        bool sparse = false;
-                        if (!(bu_ok && (tune().msbfs_bu == 1 || (tune().msbfs_bu == 2 && g_nq >= bu_rows)))) {
-                            unsigned long long before = 0, after = 0;
-                            if (bu_ok && tune().msbfs_bu == 3 && !no_bitmaps && !t.todo.empty())
-                                copy_d2h(&before, t.work.get(), sizeof before, sh.stream);
-                            for (size_t b = 0; b < t.todo.size() && !no_bitmaps; ++b) {
-                                const SliceBand& bd = *plan.bands[b];
-                                if (bd.tasks == 0 || bd.rows() == 0 || bd.row_end <= exit_rows) {  // (exit rows: no merge)
-                                    tl.push_back(nullptr);
-                                    continue;
-                                }
-                                msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
-                                    t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
-                                JG_LAUNCH_CHECK();
-                                // the probed exit bands count their live tasks apart (work[3]); after the last of them
-                                // the count decides (launch_pull then skips the exit bands, whatever their bitmaps
-                                // say, and an exit level builds no bitmaps for the bands after the probed ones)
-                                const bool probe = exit_probe && b < t.probe_nbands;
-                                if (probe && b == 0) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
-                                msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
-                                    bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(),
-                                    t.work.get() + (probe ? 3 : 0));
-                                JG_LAUNCH_CHECK();
-                                if (probe && b + 1 == t.probe_nbands) {
-                                    unsigned long long xlive = 0;
-                                    copy_d2h(&xlive, t.work.get() + 3, sizeof xlive, sh.stream);
-                                    const bool go = (double)xlive * 1000.0 < (double)t.exit_tasks * (double)tune().msbfs_exit_live;
-                                    t.xlive_permille = t.exit_tasks ? (double)xlive * 1000.0 / (double)t.exit_tasks : 1000.0;
-                                    if (debug_bfs())
-                                        std::fprintf(stderr, "[jg msbfs] level %d bands 0..%zu: %llu of %lld merge tasks live -> %s\n",
-                                                     level, b, xlive, (long long)t.exit_tasks, go ? "early exit" : "merge");
-                                    if (go) {
-                                        exit_rows = bx.rows;
-                                        tl.push_back(nullptr);
-                                        continue;
-                                    }
-                                    t.b0_live_merged += xlive;  // (work[0] holds the other bands' live tasks)
-                                }
-                                tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                        for (size_t b = 0; b < t.todo.size() && !no_bitmaps && !exit_rows; ++b) {
+                            const SliceBand& bd = *plan.bands[b];
+                            if (bd.tasks == 0 || bd.rows() == 0) {
+                                tl.push_back(nullptr);
+                                continue;
                             }
-                            if (bu_ok && tune().msbfs_bu == 3 && !no_bitmaps && !t.todo.empty()) {
-                                copy_d2h(&after, t.work.get(), sizeof after, sh.stream);
-                                sparse = (double)(after - before) * 1000.0 <
-                                         (double)t.all_tasks * (double)tune().msbfs_bu_tasks;
-                                if (debug_bfs())
-                                    std::fprintf(stderr, "[jg msbfs] level %d pull: %llu of %lld merge tasks live -> %s\n",
-                                                 level, after - before, (long long)t.all_tasks,
-                                                 sparse ? "bottom-up" : "merge");
-                                if (sparse) bu_task_credit += after - before;  // no merge task ran
-                            }
-                        }
-                        if (bu_ok && (tune().msbfs_bu == 1 || (tune().msbfs_bu == 2 && g_nq >= bu_rows) || sparse)) {
-                            const int64_t light = sh.rows - bu.wave;
-                            const unsigned grid = (unsigned)(bu.blocks_wave +
-                                                             std::max<int64_t>(std::min<int64_t>((light + kMergeThreads - 1) / kMergeThreads, 4096), 1));
-                            msbfs_bu_kernel<<<grid, kMergeThreads, 0, sh.stream>>>(bu, op);
+                            msbfs_todo_kernel<<<grid_for(bd.rows()), kBlock, 0, sh.stream>>>(
+                                t.vis.get(), bd.row_begin, bd.rows(), lw, t.todo[b].get());
                             JG_LAUNCH_CHECK();
-                            level_bu = true;
-                        } else {
-                        // msbfs_skip_first: no task bitmaps on the traversal's first pull level (few rows
-                        // can be done there; every task runs, the finalize's live mask keeps it exact)
+                            // band 0 counts its live tasks apart (work[3]), and the count decides: an exit level
+                            // builds no bitmaps for the other bands
+                            const bool probe = exit_probe && b == 0;
+                            if (probe) JG_HIP(hipMemsetAsync(t.work.get() + 3, 0, sizeof(unsigned long long), sh.stream));
+                            msbfs_task_live_kernel<<<red_grid(bd.tasks), kRedThreads, 0, sh.stream>>>(
+                                bd.task_rows.get(), bd.tasks, t.todo[b].get(), t.tlive[b].get(),
+                                t.work.get() + (probe ? 3 : 0));
+                            JG_LAUNCH_CHECK();
+                            if (probe) {
+                                unsigned long long xlive = 0;
+                                copy_d2h(&xlive, t.work.get() + 3, sizeof xlive, sh.stream);
+                                const bool go = (double)xlive * 1000.0 < (double)t.exit_tasks * (double)tune().msbfs_exit_live;
+                                t.xlive_permille = t.exit_tasks ? (double)xlive * 1000.0 / (double)t.exit_tasks : 1000.0;
+                                if (debug_bfs())
+                                    std::fprintf(stderr, "[jg msbfs] level %d band 0: %llu of %lld merge tasks live -> %s\n",
+                                                 level, xlive, (long long)t.exit_tasks, go ? "early exit" : "merge");
+                                if (go) {
+                                    exit_rows = bx.rows;
+                                    break;
+                                }
+                                t.b0_live_merged += xlive;  // (work[0] holds the other bands' live tasks)
+                            }
+                            tl.push_back(reinterpret_cast<const uint32_t*>(t.tlive[b].get()));
+                        }
                         if (no_bitmaps && i == 0) ++unskipped_levels;
-                        if (exit_rows) {
-                            double xt = 0;
-                            for (const auto& bp : plan.bands)
-                                if (bp->row_end <= exit_rows) xt += (double)bp->tasks;
-                            t.exit_level_tasks += xt;
-                            if (no_bitmaps) t.exit_unskipped_tasks += xt;
+                        if (exit_rows) {  // every row with entries through the exit kernels, no merge launch
+                            t.exit_level_tasks += (double)t.all_tasks;
+                            if (no_bitmaps) t.exit_unskipped_tasks += (double)t.all_tasks;
                             unsigned long long before = 0, after = 0;
                             if (debug_bfs()) copy_d2h(&before, bx.examined, sizeof before, sh.stream);
                             const unsigned xg = red_grid((bx.rows + 63) / 64 * kWave);
@@ -3231,52 +2929,19 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             JG_LAUNCH_CHECK();
                             msbfs_exit_rest_kernel<<<xg, kRedThreads, 0, sh.stream>>>(bx, op, t.xrest.get());
                             JG_LAUNCH_CHECK();
+                            ++t.exit_all_levels;
                             if (debug_bfs()) {
                                 copy_d2h(&after, bx.examined, sizeof after, sh.stream);
                                 std::fprintf(stderr, "[jg msbfs] level %d exit rows [0, %lld): %llu entries examined\n",
                                              level, (long long)bx.rows, after - before);
                             }
-                        }
-                        if (exit_rows && exit_rows == t.all_rows) {  // msbfs_exit_all: every row went through the exit kernels
-                            ++t.exit_all_levels;
                         } else {
-                            // rows without pull entries are not finalised (msbfs_skip_empty): they gain nothing,
-                            // their words are zero on every output vector, and their new-bit words are masked
-                            // at output (msbfs_levels_to_planes_kernel)
+                            // rows without pull entries are not finalised: they gain nothing, their words are zero
+                            // on every output vector, and their new-bit words are masked at output
+                            // (msbfs_levels_to_planes_kernel)
                             launch_pull(*c.pull, plan, op, t.hub.get(), sh.stream, ctx.profiling ? &ctx : nullptr, &sh,
-                                        t.split.size() ? t.split.get() : (unsigned long long*)nullptr,
-                                        tune().msbfs_skip_empty != 0, tl.empty() ? nullptr : tl.data(), exit_rows);
-                        }
-                        }
-                        if (small) {  // the split level's small sources, top-down into tnext, merged into the pulled words
-                            Td& td = tds[i];
-                            if (!t.tnext_zero) {  // first use in this call
-                                JG_HIP(hipMemsetAsync(t.tnext.get(), 0, t.tnext.bytes(), sh.stream));
-                                t.tnext_zero = true;
-                            }
-                            zero_words({{td.ctr.get(), 3 * sizeof(unsigned long long)}}, sh.stream);
-                            msbfs_frontier_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                                t.F[cur].get(), sh.rows, c.push->row_ptr.get(), td.queue[qc].get(), td.qoff[qc].get(),
-                                td.ctr.get(), small);
-                            JG_LAUNCH_CHECK();
-                            unsigned long long qc0 = 0;
-                            copy_d2h(&qc0, td.ctr.get(), sizeof qc0, sh.stream);
-                            const int64_t snq = (int64_t)(qc0 >> kPackShift), smf = (int64_t)(qc0 & kEdgeMask);
-                            if (smf > 0) {
-                                MsTd a{td.queue[qc].get(), td.qoff[qc].get(), snq, smf, c.push->row_ptr.get(),
-                                       c.push->col.get(), t.F[cur].get(), t.vis.get(), t.tnext.get(), td.touched.get(),
-                                       td.touched_off.get(), td.ctr.get() + 1, 31, nullptr, td.hlist.get(), td.hlist_off.get(),
-                                       td.ctr.get() + 2, nullptr, sh.index, g.P, small, 1, 0};
-                                msbfs_td_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
-                                                      (smf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
-                                                  kBlock, 0, sh.stream>>>(a);
-                                JG_LAUNCH_CHECK();
-                                msbfs_split_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                                    td.touched.get(), td.ctr.get() + 1, t.tnext.get(), op);
-                                JG_LAUNCH_CHECK();
-                            }
-                            td_entries += (double)smf;
-                            td_queued += (double)snq;
+                                        t.split.size() ? t.split.get() : (unsigned long long*)nullptr, true,
+                                        tl.empty() ? nullptr : tl.data());
                         }
                         if (td_ok) {  // the next level's frontier counter (its direction) and, on one shard, live bits
                             zero_words({{tds[i].ctr.get(), sizeof(unsigned long long)}, {lw, sizeof(unsigned long long)}},
@@ -3306,7 +2971,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             queued = true;
                         }
                     }
-                    ++(level_bu ? bu_levels : pull_levels);
+                    ++pull_levels;
                     need_fwd = g.P > 1;
                 }
                 int32_t any = 0;
@@ -3352,13 +3017,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels - t.exit_level_tasks
-                                                          : (double)(w[0] - (i == 0 ? bu_task_credit : 0ull)) +
+                                                          : (double)w[0] +
                                                                 (double)t.b0_live_merged +
                                                                 (double)t.all_tasks * unskipped_levels -
                                                                 t.exit_unskipped_tasks;
                 const double entries = live_tasks * kMergeTask + (double)t.light_nnz * (pull_levels - t.exit_all_levels) + (double)w[2];
                 work_entries += entries;
-                work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * (pull_levels + bu_levels) +
+                work_bytes += 12.0 * entries + 32.0 * (double)sh.rows * pull_levels +
                               (level >= kMsLevelWords ? 4.0 * (double)w[1] : 0.0);
             }
             work_entries += td_entries;

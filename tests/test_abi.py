@@ -80,26 +80,27 @@ def test_tune_keys_validate_without_a_gpu():
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     jg.load()
-    for k, v in (("pull_lds", 0), ("light_lds", 0), ("pull_unroll", 4), ("merge_temporal", 1), ("band1_bit", 3),
-                 ("merge_pack", 1), ("merge_stage0", -1), ("merge_stage1", -1), ("light_runs", 1), ("merge_diag", 0),
-                 ("merge_dynamic", 1), ("fin_pipe", 1), ("bfs_wave_stage", 1), ("bfs_grid_mult", 4), ("bfs_init_suffix", 1), ("bfs_grow_rule", 0),
-                 ("bfs_batch0", 10), ("msbfs_skip", 1), ("cc_first", 1), ("msbfs_bu", 0),
-                 ("msbfs_bu_frac", 100), ("msbfs_sparse", 1), ("msbfs_skip_first", 1), ("msbfs_skip_first", 0), ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("band_sliced_build", 0), ("msbfs_td", 2), ("msbfs_td", 1), ("bfs_td_split", 2), ("bfs_td_split_levels", 2), ("bfs_td_split_min", 65536), ("bfs_td_split_max", 1 << 20), ("relabel_dead_last", 0), ("relabel_dead_last", 1), ("msbfs_bu", 3), ("msbfs_bu_tasks", 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64), ("relabel_out_ties", 1), ("relabel_out_ties", 0),
+    for k, v in (("merge_temporal", 1), ("band1_bit", 3), ("merge_pack", 1), ("merge_stage0", -1), ("merge_stage1", -1),
+                 ("bfs_grid_mult", 4), ("bfs_batch0", 10), ("msbfs_skip", 1), ("cc_first", 1), ("msbfs_sparse", 1),
+                 ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("msbfs_td", 2),
+                 ("msbfs_td", 1), ("bfs_td_split", 2), ("bfs_td_split_levels", 2), ("bfs_td_split_min", 65536),
+                 ("bfs_td_split_max", 1 << 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64),
                  ("msbfs_exit", 0), ("msbfs_exit", 2), ("msbfs_exit", 1), ("msbfs_exit_live", 1000), ("msbfs_exit_live", 950),
-                 ("msbfs_exit_bands", 1), ("msbfs_exit_bands", 2), ("msbfs_exit_all", 1), ("msbfs_exit_all", 0),
-                 ("msbfs_exit_probe", 0), ("msbfs_exit_probe", 1),
-                 ("msbfs_srcsplit", 1), ("msbfs_srcsplit", 2), ("msbfs_srcsplit", 0), ("msbfs_srcsplit_permille", 20),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
-                 ("msbfs_skip_empty", 0), ("msbfs_skip_empty", 1), ("msbfs_td_rowapply", 0), ("msbfs_td_rowapply", 4)):
+                 ("msbfs_td_rowapply", 0), ("msbfs_td_rowapply", 4), ("bfs_narrow", 0), ("bfs_narrow", 1),
+                 ("nb_alpha", 14), ("nb_alpha", 30), ("nb_first", 16), ("halo", 1), ("pull_split", 1), ("band0_sub", 64),
+                 ("band0_bit", 0), ("band0_deg", 96)):
         _lib.tune_set(k, v)
-    for k, v in (("light_lds", -1), ("pull_unroll", 5), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
-                 ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 5), ("merge_nt", 0),
-                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("msbfs_bu", 4), ("msbfs_bu_tasks", 1001), ("bfs_tail_grid", -1),
-                 ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_exit_bands", 0), ("msbfs_exit_bands", 5),
-                 ("msbfs_exit_probe", -1), ("msbfs_exit_probe", 5),
-                 ("msbfs_srcsplit", 3), ("msbfs_srcsplit_permille", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0), ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1),
-                 ("msbfs_bu_frac", 1001), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1), ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31)):
+    # unknown keys (including the variants deleted in round 5: measured slower or equal) and bad values
+    for k, v in (("light_lds", 0), ("pull_unroll", 4), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
+                 ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 0), ("merge_nt", 0), ("msbfs_srcsplit", 0),
+                 ("msbfs_bu", 0), ("fin_pipe", 1), ("relabel_out_ties", 0), ("band_sliced_build", 0),
+                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("bfs_tail_grid", -1),
+                 ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0),
+                 ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1), ("nb_first", 3), ("nb_alpha", 0),
+                 ("bfs_narrow", 2), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1),
+                 ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31)):
         with pytest.raises(jg.JanusGpuError) as e:
             _lib.tune_set(k, v)
         assert e.value.code == -1

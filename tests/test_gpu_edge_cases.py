@@ -196,15 +196,17 @@ def test_multi_source_bfs_past_255_levels(oracle_lib, shards):
     c.close()
 
 
-@pytest.mark.parametrize("shards,exit_mode,srcsplit", [(1, 1, 0), (1, 2, 0), (1, 1, 2), (3, 1, 0), (3, 2, 0)])
-def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode, srcsplit):
+@pytest.mark.parametrize("shards,exit_mode", [(1, 1), (1, 2), (1, 0), (3, 1), (3, 2)])
+def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode):
     """The 64-source BFS's early-exit rows (msbfs_exit; the split's hub bands scanned row by row) on a
     graph made for it: four hubs of 300-900 leaves joined in a ring, leaves cross-linked to each other's
     hubs, a 150-vertex tail hanging off one leaf, a small separate component and an isolated vertex.  Hub
     rows then need every live source at once while some sources sit at the end of the tail, so some
     levels exit and others must scan whole rows.  All 64 depth rows against the oracle, unbounded and
-    bounded, with the adaptive rule (1) and the exit forced on every pull level (2), on 1 and 3 shards, and
-    with the tail's and the small component's sources pushed top-down on pull levels (msbfs_srcsplit 2)."""
+    bounded, with the adaptive rule (1), the exit forced on every pull level (2) and off (0), on 1 and 3
+    shards.  The traversal's level count is the deepest source's depth + 1 (the level that finds nothing
+    new), capped by max_depth: an isolated source's level-0 word must not survive into a later frontier
+    (ADVICE r04)."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     rng = np.random.default_rng(5)
@@ -233,20 +235,23 @@ def test_multi_source_bfs_hubs_and_tails(oracle_lib, shards, exit_mode, srcsplit
     vid = (np.arange(n, dtype=np.int64) + 1) << 8
     try:
         _lib.tune_set("msbfs_exit", exit_mode)
-        _lib.tune_set("msbfs_srcsplit", srcsplit)
         c = jg.Context((0,) * shards)
         g = c.build(vid, vid[s], vid[t], flags=jg.ADJ_BOTH)
         srcs = np.concatenate([[0, 3, tail_end, small, n - 1], rng.choice(leaves, 59, replace=False)])
         for max_depth in (-1, 3):
             got = g.bfs(vid[srcs], jg.DIR_BOTH, max_depth=max_depth)
+            levels = c.stats()["levels"]
+            deepest = 0
             for k, sv in enumerate(srcs):
-                np.testing.assert_array_equal(got[k], oracle_lib.bfs(n, s, t, int(sv), oracle_lib.DIR_BOTH, max_depth),
+                want = oracle_lib.bfs(n, s, t, int(sv), oracle_lib.DIR_BOTH, max_depth)
+                np.testing.assert_array_equal(got[k], want,
                                               err_msg=f"shards {shards} exit {exit_mode} max_depth {max_depth} source {sv}")
+                deepest = max(deepest, int(want.max()))
+            assert levels == (deepest + 1 if max_depth < 0 else min(deepest + 1, max_depth)), (levels, deepest)
         g.close()
         c.close()
     finally:
         _lib.tune_set("msbfs_exit", 1)
-        _lib.tune_set("msbfs_srcsplit", 0)
 
 
 def test_vertex_id_remap_arbitrary_ids(ctx, oracle_lib, rmat12):

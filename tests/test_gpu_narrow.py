@@ -35,7 +35,7 @@ def knobs(pairs):
         _lib.tune_set(k, v)
 
 
-DEFAULTS = [("bfs_narrow", 1), ("nb_alpha", 14), ("nb_first", 16), ("bfs_beta", 24)]
+DEFAULTS = [("bfs_narrow", 1), ("nb_alpha", 30), ("nb_first", 16), ("bfs_beta", 24)]
 
 
 @pytest.fixture(scope="module")
@@ -53,9 +53,15 @@ def case15(oracle_lib):
 def check_rows(o, c, srcs, direction=3, max_depth=-1):
     g = c["g"]
     got = g.bfs(c["vid"][srcs], direction, max_depth)
+    levels = c["ctx"].stats()["levels"]
+    deepest = 0
     for k, s in enumerate(srcs):
-        np.testing.assert_array_equal(got[k], o.bfs(c["n"], c["ds"], c["dd"], int(s), direction, max_depth),
+        want = o.bfs(c["n"], c["ds"], c["dd"], int(s), direction, max_depth)
+        np.testing.assert_array_equal(got[k], want,
                                       err_msg=f"source {k} ({s}), direction {direction}, max_depth {max_depth}")
+        deepest = max(deepest, int(want.max()))
+    # the level that finds nothing new ends the traversal; a bound stops it at max_depth
+    assert levels == (deepest + 1 if max_depth < 0 else min(deepest + 1, max_depth)), (levels, deepest)
     return got
 
 

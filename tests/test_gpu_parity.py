@@ -222,17 +222,11 @@ def test_multisource_bfs_rmat(ctx, oracle_lib):
 
 @pytest.mark.parametrize("mode,shards", [("skip", 1), ("noskip", 1), ("skip_pull_only", 1), ("skip_bands3", 1),
                                          ("skip_wide", 1), ("skip", 3), ("skip", 8), ("skip_sharded_pull_only", 3),
-                                         ("skip_dense_reverse", 3), ("skip_dense", 2), ("skip_every_level", 1),
-                                         ("skip_every_level", 3), ("bu_sparse_levels", 1), ("bu_sparse_always", 1),
-                                         ("bu_every_level", 1), ("exit_off", 1), ("exit_every_bitmapped_level", 1),
-                                         ("exit_every_level", 1), ("exit_no_skip", 1), ("exit_one_band", 1),
-                                         ("exit_light_merged", 1), ("exit_light_merged", 3), ("srcsplit_first_level", 1),
-                                         ("srcsplit_every_level", 1), ("srcsplit_many_small", 1),
-                                         ("srcsplit_exit_bands", 1), ("td_probe_always", 1), ("td_probe_never", 1),
-                                         ("td_probe_never", 3), ("exit_first3", 1), ("exit_first32", 3), ("scan_queue_off", 1),
-                                         ("scan_queue_always", 1), ("finalize_empty_rows", 1), ("finalize_empty_rows", 3),
-                                         ("td_rowapply_off", 1), ("td_rowapply_always", 1), ("exit_probe_all", 1),
-                                         ("exit_probe_all", 3), ("exit_probe_all_merged", 1)])
+                                         ("skip_dense_reverse", 3), ("skip_dense", 2), ("exit_off", 1),
+                                         ("exit_every_bitmapped_level", 1), ("exit_every_level", 1), ("exit_no_skip", 1),
+                                         ("td_probe_always", 1), ("td_probe_never", 1), ("td_probe_never", 3),
+                                         ("exit_first3", 1), ("exit_first32", 3), ("scan_queue_off", 1),
+                                         ("scan_queue_always", 1), ("td_rowapply_off", 1), ("td_rowapply_always", 1)])
 def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     """The 64-source BFS's pull levels skip merge tasks whose rows can gain no live bit
     (MergeArgs::live): all 64 depth rows equal the oracle's, with sources in the giant component, an
@@ -241,10 +235,7 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
     plans the small-frontier levels run top-down (own rows pushed, peers' bits returned by the reverse
     halo exchange, sparse (offset, word) pairs when few staging slots are set, the whole segments with
     skip_dense_reverse); skip_sharded_pull_only keeps every sharded level a pull level (msbfs_td 2).
-    The first pull level runs every task by default (msbfs_skip_first); skip_every_level builds the
-    task bitmaps on that level too.  One shard, msbfs_bu 3: a later pull level with fewer than
-    msbfs_bu_tasks permille of live tasks runs msbfs_bu_kernel (bottom-up, early exit) instead of the merge
-    engine."""
+    One shard: levels after the frontier's peak scan every row with early exit (msbfs_exit)."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"skip": [], "noskip": [("msbfs_skip", 0)], "skip_pull_only": [("msbfs_td", 0)],
@@ -252,24 +243,10 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
                              ("band2_deg", 4), ("band2_bit", 3)],
              "skip_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
              "skip_dense": [("halo", 0)], "skip_sharded_pull_only": [("msbfs_td", 2)],
-             "skip_dense_reverse": [("msbfs_sparse", 0)], "skip_every_level": [("msbfs_skip_first", 0)],
-             # bottom-up pull levels (msbfs_bu; 0, the merge engine, by default): sparse levels only, every
-             # bitmapped level, every pull level
-             "bu_sparse_levels": [("msbfs_bu", 3)], "bu_sparse_always": [("msbfs_bu", 3), ("msbfs_bu_tasks", 1000)],
-             "bu_every_level": [("msbfs_bu", 1)],
-             # the split's first band through the early-exit rows (msbfs_exit: 1, the default, on levels where
-             # few of its tasks are live), the rest merged
+             "skip_dense_reverse": [("msbfs_sparse", 0)],
+             # the early exit (msbfs_exit: 1, the default, on levels where few band-0 tasks are live)
              "exit_off": [("msbfs_exit", 0)], "exit_every_bitmapped_level": [("msbfs_exit_live", 1000)],
              "exit_every_level": [("msbfs_exit", 2)],
-             "exit_one_band": [("msbfs_exit_bands", 1), ("msbfs_exit_live", 1000)],
-             "exit_light_merged": [("msbfs_exit_all", 0), ("msbfs_exit_live", 1000)],
-             # the exit decided by every exit band's live tasks (msbfs_exit_probe 0; 1, band 0 alone, by default)
-             "exit_probe_all": [("msbfs_exit_probe", 0)],
-             "exit_probe_all_merged": [("msbfs_exit_probe", 0), ("msbfs_exit_all", 0), ("msbfs_exit_live", 1000)],
-             # the first pull level's small-frontier sources top-down (msbfs_srcsplit; 0, off, by default)
-             "srcsplit_first_level": [("msbfs_srcsplit", 1)], "srcsplit_every_level": [("msbfs_srcsplit", 2)],
-             "srcsplit_many_small": [("msbfs_srcsplit", 2), ("msbfs_srcsplit_permille", 300)],
-             "srcsplit_exit_bands": [("msbfs_srcsplit", 2), ("msbfs_exit_all", 0)],
              # the visited probe of top-down edges (skipped below level msbfs_td_noprobe, 2 by default)
              "td_probe_always": [("msbfs_td_noprobe", 0)], "td_probe_never": [("msbfs_td_noprobe", 1000)],
              # the early exit's lane pass over 3 / 32 entries per row (16 by default)
@@ -277,8 +254,6 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
              "exit_first32": [("msbfs_exit_first", 32), ("msbfs_exit_live", 1000)],
              # the next top-down queue built by the frontier scan (msbfs_scan_queue: never / after every probe)
              "scan_queue_off": [("msbfs_scan_queue", 0)], "scan_queue_always": [("msbfs_scan_queue", 1001)],
-             # pull levels finalise the rows without entries too (msbfs_skip_empty 0; 1 by default)
-             "finalize_empty_rows": [("msbfs_skip_empty", 0)],
              # top-down applies in row order (msbfs_td_rowapply: never / every one-shard level)
              "td_rowapply_off": [("msbfs_td_rowapply", 0)], "td_rowapply_always": [("msbfs_td_rowapply", 1024)],
              "exit_no_skip": [("msbfs_exit", 2), ("msbfs_skip", 0)]}[mode]
@@ -307,21 +282,12 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_skip", 1)
         _lib.tune_set("msbfs_td", 1)
         _lib.tune_set("msbfs_sparse", 1)
-        _lib.tune_set("msbfs_bu", 0)
         _lib.tune_set("msbfs_exit", 1)
         _lib.tune_set("msbfs_exit_live", 950)
-        _lib.tune_set("msbfs_exit_bands", 2)
-        _lib.tune_set("msbfs_exit_all", 1)
-        _lib.tune_set("msbfs_exit_probe", 1)
-        _lib.tune_set("msbfs_srcsplit", 0)
-        _lib.tune_set("msbfs_srcsplit_permille", 20)
         _lib.tune_set("msbfs_td_noprobe", 2)
         _lib.tune_set("msbfs_exit_first", 16)
         _lib.tune_set("msbfs_scan_queue", 50)
-        _lib.tune_set("msbfs_skip_empty", 1)
         _lib.tune_set("msbfs_td_rowapply", 4)
-        _lib.tune_set("msbfs_bu_tasks", 20)
-        _lib.tune_set("msbfs_skip_first", 1)
         _lib.tune_set("halo", 1)
         for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
                      ("band2_bit", 3)):  # the defaults (Tune::band_deg / band_bits)
@@ -347,8 +313,13 @@ def test_directed_multi_source_bfs(ctx, oracle_lib, exit_mode):
         g = ctx.build(vid, src, dst, flags=3)
         srcs = np.unique(ds)[::97][:64]
         depth = g.bfs(vid[srcs], 1)
+        levels = ctx.stats()["levels"]
+        deepest = 0
         for k in range(len(srcs)):
-            np.testing.assert_array_equal(depth[k], oracle_lib.bfs(n, ds, dd, int(srcs[k]), 1), err_msg=f"source {k}")
+            want = oracle_lib.bfs(n, ds, dd, int(srcs[k]), 1)
+            np.testing.assert_array_equal(depth[k], want, err_msg=f"source {k}")
+            deepest = max(deepest, int(want.max()))
+        assert levels == deepest + 1  # the level that finds nothing new ends the traversal
         g.close()
     finally:
         _lib.tune_set("msbfs_exit", 1)
@@ -515,26 +486,18 @@ def test_errors_are_status_codes(ctx):
         g.pagerank_step(1)
 
 
-@pytest.mark.parametrize("mode", ["plain", "lds", "split_nolds", "split_lds", "split_bands3", "split_wide", "split_light_lds", "split_merge_overlap", "split_merge_wgs2", "split_fin_last",
-                                  "split_sub1", "split_sub2_4", "split_w24", "split_w32", "split_stage_off",
-                                  "split_stage512", "light_noruns", "merge_static", "merge_chunks16", "pr_noskip", "cc_first3",
-                                  "split_sliced_build", "relabel_dead_first", "relabel_out_ties"])
+@pytest.mark.parametrize("mode", ["plain", "split", "split_bands3", "split_wide", "split_sub1", "split_sub2_4",
+                                  "split_w24", "split_w32", "split_stage_off", "split_stage512", "cc_first3"])
 def test_pull_engine_variants_match_oracle(oracle_lib, mode):
-    """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes,
-    LDS-staged hot prefix, XCD-sliced split without / with the LDS-resident hot slice."""
+    """Every pull-engine variant (jg_tune_set knobs) gives oracle parity: plain degree classes, the
+    XCD-sliced split with its band layouts, entry packings and partial staging windows."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     knobs = {"plain": [("pull_split", 0)],
-             "lds": [("pull_split", 0), ("pull_lds", 20480)],
-             "split_nolds": [("pull_split", 1), ("slice_lds", 0)],
-             "split_lds": [("pull_split", 1), ("slice_lds", 1)],
+             "split": [("pull_split", 1)],
              "split_bands3": [("band0_deg", 64), ("band0_bit", 8), ("band1_deg", 16), ("band1_bit", 5),
                               ("band2_deg", 4), ("band2_bit", 3)],
              "split_wide": [("band0_deg", 2), ("band0_bit", 7), ("band1_deg", 0)],
-             "split_light_lds": [("pull_split", 1), ("light_lds", 8192)],
-             "split_merge_overlap": [("pull_split", 1), ("merge_overlap", 1)],
-             "split_merge_wgs2": [("pull_split", 1), ("merge_wgs", 2)],
-             "split_fin_last": [("pull_split", 1), ("fin_last", 1)],
              "split_sub1": [("band1_sub", 1)],
              "split_sub2_4": [("band0_deg", 64), ("band0_sub", 4), ("band1_deg", 16), ("band1_sub", 2),
                               ("band2_deg", 4), ("band2_sub", 1)],
@@ -542,14 +505,7 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
              "split_w32": [("merge_pack", 0)],
              "split_stage_off": [("merge_stage0", 0), ("merge_stage1", 0)],
              "split_stage512": [("merge_stage0", 512), ("merge_stage1", 512)],
-             "light_noruns": [("light_runs", 0)],
-             "merge_static": [("merge_dynamic", 0)],
-             "merge_chunks16": [("merge_interleave", 0)],
-             "pr_noskip": [("pr_skip_empty", 0), ("pr_rank_last", 0)],
-             "cc_first3": [("cc_first", 3)],
-             "split_sliced_build": [("band_sliced_build", 1)],
-             "relabel_dead_first": [("relabel_dead_last", 0)],
-             "relabel_out_ties": [("relabel_out_ties", 1)]}[mode]
+             "cc_first3": [("cc_first", 3)]}[mode]
     try:
         for k, v in knobs:
             _lib.tune_set(k, v)
@@ -570,24 +526,10 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         g.close()
         c.close()
     finally:
-        _lib.tune_set("pull_lds", 0)
-        _lib.tune_set("light_lds", 0)
-        _lib.tune_set("merge_overlap", 0)
-        _lib.tune_set("merge_wgs", 1)
-        _lib.tune_set("fin_last", 0)
         _lib.tune_set("pull_split", 1)
-        _lib.tune_set("band_sliced_build", 0)
-        _lib.tune_set("relabel_dead_last", 1)
-        _lib.tune_set("relabel_out_ties", 0)
-        _lib.tune_set("slice_lds", 1)
         _lib.tune_set("merge_pack", 1)
         _lib.tune_set("merge_stage0", -1)
         _lib.tune_set("merge_stage1", -1)
-        _lib.tune_set("light_runs", 1)
-        _lib.tune_set("merge_dynamic", 1)
-        _lib.tune_set("merge_interleave", 1)
-        _lib.tune_set("pr_skip_empty", 1)
-        _lib.tune_set("pr_rank_last", 1)
         _lib.tune_set("cc_first", 1)
         for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 3), ("band2_deg", 0),
                      ("band2_bit", 3)):

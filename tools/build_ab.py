@@ -2,7 +2,7 @@
 RMAT graph (jg_tune_set knobs "name:key=value,..." applied before the build, as in tools/pr_ab.py),
 then CC and the bench's 64-source BFS are timed in interleaved rounds.  Reports median HIP-event ms and
 whether every variant's CC labels and BFS depths equal the first's.
-    python tools/build_ab.py --scale 26 col: sliced:band_sliced_build=1
+    python tools/build_ab.py --scale 26 col: nopack:merge_pack=0
 """
 import argparse
 import json

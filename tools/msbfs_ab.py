@@ -1,7 +1,7 @@
 """A/B of bit-parallel BFS knobs on the bench's 64-source workload (bench.pick_sources(deg, 64, 7)),
 timing only (parity: tests/test_gpu_configs.py, tests/test_gpu_parity.py).  One line per setting:
 median HIP-event ms over `reps` runs after one warm run, levels, entries examined.
-    python tools/msbfs_ab.py --scale 26 msbfs_bu 0 1 2
+    python tools/msbfs_ab.py --scale 26 msbfs_exit 0 1 2
     python tools/msbfs_ab.py --scale 26 --tune msbfs_exit=1 msbfs_exit_live 0 700 1000
 """
 import argparse

@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import janusgraph_amd as jg  # noqa: E402
 from janusgraph_amd import _lib  # noqa: E402
 
-DEFAULTS = {"pull_split": 1, "slice_lds": 1, "merge_temporal": 1, "relabel_ties": 1, "relabel_dead_last": 1, "relabel_out_ties": 0, "fuse_finalize": 1, "pull_lds": 0, "light_lds": 0, "merge_overlap": 0, "merge_wgs": 1, "fin_last": 0, "pull_unroll": 4, "pull_nt": 0, "pr_skip_empty": 1, "pr_rank_last": 1, "merge_diag": 0, "band_sliced_build": 0, "fin_pipe": 1, "merge_dynamic": 1, "merge_interleave": 1, "merge_pack": 1, "light_runs": 1, "merge_stage0": -1, "merge_stage1": -1, "merge_stage2": -1, "merge_stage3": -1,
+DEFAULTS = {"pull_split": 1, "merge_temporal": 1, "merge_pack": 1, "merge_stage0": -1, "merge_stage1": -1,
+            "merge_stage2": -1, "merge_stage3": -1,
             "band0_deg": 96, "band0_bit": 0, "band1_deg": 8, "band1_bit": 3, "band2_deg": 0, "band2_bit": 3,
             "band3_deg": 0, "band3_bit": 3}
 

@@ -53,10 +53,7 @@ def main():
         g.close()
         _lib.tune_set("pull_split", 1)
         g = ctx.build(vid, s2, dst, flags=jg.ADJ_IN)
-        _lib.tune_set("slice_lds", 0)
-        r["split"] = round(time_steps(g, n), 4)
-        _lib.tune_set("slice_lds", 1)
-        r["split_lds"] = round(time_steps(g, n), 4)
+        r["split_lds"] = round(time_steps(g, n), 4)  # (the split without LDS images was removed in round 5)
         _lib.tune_set("pull_split", 0)
         r["sliced_nosplit"] = round(time_steps(g, n), 4)
         _lib.tune_set("pull_split", 1)
