@@ -6,6 +6,7 @@ entry point raises — there is no CPU fallback in the product.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -259,6 +260,9 @@ class Context:
 
     def close(self):
         if self._h:
+            # the graphs first: a graph destroyed after its context would touch freed streams
+            for g in list(getattr(self, "_graphs", ())):
+                g.close()
             check(load().jg_ctx_destroy(self._h))
             self._h = ctypes.c_void_p()
 
@@ -434,6 +438,9 @@ class Graph:
 
     def __init__(self, ctx: Context, handle, n):
         self.ctx, self._h, self.n = ctx, handle, n
+        if not hasattr(ctx, "_graphs"):
+            ctx._graphs = weakref.WeakSet()
+        ctx._graphs.add(self)
 
     def _out(self, size, dtype):
         """An output array; in rank mode pre-filled so the other ranks' vertices are recognisable."""

@@ -5,7 +5,11 @@
 // Error style mirrors FulgoraGraphComputer's "Computer is aborting" failures
 // (janusgraph-core/.../olap/computer/FulgoraGraphComputer.java:269-286): any failure aborts the
 // whole program run; callers wrap a non-zero status in a JanusGraphException.
+#include <dlfcn.h>
+#include <execinfo.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -60,7 +64,7 @@ void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, n
     const size_t slice = (size_t)g.S * elem_bytes;
     if (c.host_transport) {  // rank mode over host callbacks: one shard per process
         Shard& sh = *g.shards[0];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         std::vector<char> mine(slice), all(slice * (size_t)c.nranks);
         char* base = static_cast<char*>(bufs[0]);
         copy_d2h(mine.data(), base + (size_t)sh.index * slice, slice, sh.stream);
@@ -85,7 +89,7 @@ void exchange_allgather(Graph& g, std::vector<void*>& bufs, size_t elem_bytes, n
     rccl_check(ncclGroupStart(), "ncclGroupStart");
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         char* base = static_cast<char*>(bufs[i]);
         rccl_check(ncclAllGather(base + (size_t)sh.index * slice, base, (size_t)g.S,
                                  type, sh.comm, sh.stream),
@@ -98,7 +102,7 @@ int allreduce_or(Graph& g, int flag) {
     Ctx& c = *g.ctx;
     if (c.nranks == 1) return flag;  // in-process shards already combined by the caller
     Shard& sh = *g.shards[0];
-    DeviceGuard dg(sh.device);
+    DeviceGuard dg(sh);
     if (c.host_transport) {
         const int32_t mine = flag ? 1 : 0;
         std::vector<int32_t> all((size_t)c.nranks);
@@ -118,7 +122,7 @@ void allreduce_sum_i64(Graph& g, int64_t* vals, int n) {
     Ctx& c = *g.ctx;
     if (c.nranks == 1) return;  // in-process shards already summed by the caller
     Shard& sh = *g.shards[0];
-    DeviceGuard dg(sh.device);
+    DeviceGuard dg(sh);
     if (c.host_transport) {
         std::vector<int64_t> all((size_t)n * c.nranks);
         host_allgather(c, vals, all.data(), (size_t)n * sizeof(int64_t));
@@ -180,6 +184,52 @@ BlockCache<HipBackend>& cache() {
 thread_local bool t_direct_free = false;  // DirectFree scope (jg_graph_destroy)
 }  // namespace
 
+namespace {
+std::atomic<int> g_vdev_mode{-1};  // JG_VDEV_CHECK, re-read at every context creation (tests toggle it)
+int vdev_env() {
+    const char* v = std::getenv("JG_VDEV_CHECK");
+    return v && *v ? std::atoi(v) : 0;
+}
+}  // namespace
+
+int vdev_mode() {
+    int m = g_vdev_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        m = vdev_env();
+        g_vdev_mode.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
+void vdev_refresh() { g_vdev_mode.store(vdev_env(), std::memory_order_relaxed); }
+
+void vdev_violation(int buffer_tag, int current_tag) {
+    const std::string msg = "virtual-device check: a buffer of shard " + std::to_string(buffer_tag) + " used under shard " +
+                            std::to_string(current_tag) +
+                            "'s device guard (on distinct devices this is a cross-device access)";
+    if (vdev_mode() == 2 || std::getenv("JG_VDEV_TRACE")) {  // return addresses as library offsets
+        void* pcs[16];
+        const int k = backtrace(pcs, 16);
+        std::string where;
+        for (int i = 1; i < k && i < 6; ++i) {
+            Dl_info di{};
+            if (dladdr(pcs[i], &di) && di.dli_fname && std::strstr(di.dli_fname, "libjanusgpu")) {
+                char b[32];
+                std::snprintf(b, sizeof b, " +0x%lx", (unsigned long)((const char*)pcs[i] - (const char*)di.dli_fbase));
+                where += b;
+            }
+        }
+        static std::mutex mu;
+        static std::vector<std::string> seen;
+        std::lock_guard<std::mutex> lk(mu);
+        if (std::find(seen.begin(), seen.end(), where) == seen.end()) {
+            seen.push_back(where);
+            std::fprintf(stderr, "[jg vdev] %s at libjanusgpu.so%s\n", msg.c_str(), where.c_str());
+        }
+        if (vdev_mode() == 2) return;
+    }
+    fail(JG_ERR_STATE, msg);
+}
+
 DirectFree::DirectFree() : prev(t_direct_free) { t_direct_free = true; }
 DirectFree::~DirectFree() { t_direct_free = prev; }
 
@@ -201,7 +251,7 @@ uint64_t allreduce_or_u64(Graph& g, uint64_t v) {
     Ctx& c = *g.ctx;
     if (c.nranks == 1) return v;
     Shard& sh = *g.shards[0];
-    DeviceGuard dg(sh.device);
+    DeviceGuard dg(sh);
     if (c.host_transport) {
         std::vector<uint64_t> all((size_t)c.nranks);
         host_allgather(c, &v, all.data(), sizeof v);
@@ -280,14 +330,14 @@ void exch_record(Ctx& c, Shard& sh) {
 ExchTimer::ExchTimer(Graph& gr) : g(gr) {
     if (!g.ctx->profiling) return;
     for (auto& sp : g.shards) {
-        DeviceGuard dg(sp->device);
+        DeviceGuard dg(*sp);
         exch_record(*g.ctx, *sp);
     }
 }
 ExchTimer::~ExchTimer() {
     if (!g.ctx->profiling) return;
     for (auto& sp : g.shards) {
-        DeviceGuard dg(sp->device);
+        DeviceGuard dg(*sp);
         try {
             exch_record(*g.ctx, *sp);
         } catch (...) {  // never from a destructor; the pair stays open and prof_collect skips it
@@ -298,7 +348,7 @@ ExchTimer::~ExchTimer() {
 void prof_discard_exchanges(Graph& g) {
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         for (auto e : sh.exch_events) (void)hipEventDestroy(e);
         sh.exch_events.clear();
     }
@@ -309,7 +359,7 @@ void prof_collect(Ctx& c, Graph& g) {
     int64_t launches = 0;
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         double ex = 0;
         for (size_t i = 0; i + 1 < sh.exch_events.size(); i += 2) {
             JG_HIP(hipEventSynchronize(sh.exch_events[i + 1]));
@@ -340,7 +390,7 @@ const std::vector<int32_t>& Shard::dense_of_local() const {
     if ((int64_t)dense_of_local_host.size() != rows) {
         dense_of_local_host.resize((size_t)rows);
         if (rows > 0) {
-            DeviceGuard dg(device);
+            DeviceGuard dg(*this);
             copy_d2h(dense_of_local_host.data(), dense_rows.get(), (size_t)rows * sizeof(int32_t), stream);
         }
     }
@@ -353,7 +403,7 @@ const std::vector<int64_t>& Graph::vid_of_rank() const {
         cc_vor_host.resize((size_t)n);
         if (n > 0) {
             const Shard& sh = *shards[0];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             copy_d2h(cc_vor_host.data(), cc_vor.get(), (size_t)n * sizeof(int64_t), sh.stream);
         }
     }
@@ -382,6 +432,7 @@ static void make_shards(Ctx& c, Graph& g) {
         auto sh = std::make_unique<Shard>();
         sh->device = c.devices[i];
         sh->index = c.rank * (int)c.devices.size() + (int)i;
+        sh->vtag = c.vdev ? sh->index : -1;
         sh->stream = c.streams[i];
         sh->comm = c.comms.empty() ? nullptr : c.comms[i];
         g.shards.push_back(std::move(sh));
@@ -428,12 +479,13 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
     }
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const int64_t *v = d_vid, *a = d_src, *b = d_dst;
         auto peer = [&](void* dst, const void* src, size_t bytes) {
             if (bytes) JG_HIP(hipMemcpyPeerAsync(dst, sh.device, src, dev0, bytes, sh.stream));
         };
-        if (sh.device != dev0) {
+        const bool other = !same_device(sh, dev0);  // a virtual device in the check mode counts as another
+        if (other) {
             pv[i].alloc(std::max<int64_t>(n, 1));
             ps[i].alloc(std::max<int64_t>(m, 1));
             pd[i].alloc(std::max<int64_t>(m, 1));
@@ -450,24 +502,24 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
         // device; shards on other devices build a temporary one
         if (i == 0) g.id_dev = sh.device;
         DevBuf<IdSlot> tmp_table;
-        DevBuf<IdSlot>& table = sh.device == g.id_dev ? g.id_table : tmp_table;
+        DevBuf<IdSlot>& table = same_device(sh, g.id_dev) ? g.id_table : tmp_table;
         remap_ids_device(v, n, a, b, m, ds[i].get(), dd[i].get(), sh.stream, &table);
-        e.src.push_back(ds[i].get());
-        e.dst.push_back(dd[i].get());
+        e.src.push_back(ds[i].peer());
+        e.dst.push_back(dd[i].peer());
         if (cap) {
             DevBuf<int64_t> po, pis, pid;
             const int64_t *o = cap->osrc, *is = cap->isrc, *id = cap->idst;
-            if (sh.device != dev0) {
+            if (other) {
                 po.alloc(std::max<int64_t>(m, 1));
                 peer(po.get(), cap->osrc, (size_t)m * sizeof(int64_t));
                 o = po.get();
             }
             dos[i].alloc(std::max<int64_t>(m, 1));
             mask_ids_device(o, ds[i].get(), m, dos[i].get(), sh.stream);
-            e.out_src.push_back(dos[i].get());
+            e.out_src.push_back(dos[i].peer());
             if (cap->in_from_in) {
                 const int64_t mi = cap->mi;
-                if (sh.device != dev0) {
+                if (other) {
                     pis.alloc(std::max<int64_t>(mi, 1));
                     pid.alloc(std::max<int64_t>(mi, 1));
                     peer(pis.get(), cap->isrc, (size_t)mi * sizeof(int64_t));
@@ -478,16 +530,16 @@ static void build_from_device_ids(Graph& g, int dev0, hipStream_t s0, const int6
                 dis[i].alloc(std::max<int64_t>(mi, 1));
                 did[i].alloc(std::max<int64_t>(mi, 1));
                 remap_ids_device(v, n, is, id, mi, dis[i].get(), did[i].get(), sh.stream, &table);
-                e.in_src.push_back(dis[i].get());
-                e.in_dst.push_back(did[i].get());
+                e.in_src.push_back(dis[i].peer());
+                e.in_dst.push_back(did[i].peer());
             }
             JG_HIP(hipStreamSynchronize(sh.stream));  // the peer staging buffers are freed here
         }
         if (d_w) {
             dw[i].alloc(std::max<int64_t>(m, 1));
-            if (sh.device != dev0) peer(dw[i].get(), d_w, (size_t)m * sizeof(int32_t));
+            if (other) peer(dw[i].get(), d_w, (size_t)m * sizeof(int32_t));
             else if (m) JG_HIP(hipMemcpyAsync(dw[i].get(), d_w, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToDevice, sh.stream));
-            e.weight.push_back(dw[i].get());
+            e.weight.push_back(dw[i].peer());
         } else {
             e.weight.push_back(nullptr);
         }
@@ -685,6 +737,8 @@ int jg_ctx_create(const int* devices, int ndev, jg_ctx** out) {
     bool all_same = true;
     for (int i = 1; i < ndev; ++i) all_same &= devices[i] == devices[0];
     c.logical = ndev > 1 && all_same;
+    jg::vdev_refresh();
+    c.vdev = c.logical && jg::vdev_mode() != 0;
     if (ndev > 1 && !all_same) {
         std::vector<int> sorted(c.devices);
         std::sort(sorted.begin(), sorted.end());
@@ -1102,12 +1156,12 @@ int jg_graph_build_rmat(jg_ctx* ctx, int scale, int edgefactor, uint64_t seed, u
     e.m = m;
     for (size_t i = 0; i < g.shards.size(); ++i) {
         jg::Shard& sh = *g.shards[i];
-        jg::DeviceGuard dg(sh.device);
+        jg::DeviceGuard dg(sh);
         ds[i].alloc(m);
         dd[i].alloc(m);
         jg::generate_rmat_device(scale, seed, m, ds[i].get(), dd[i].get(), sh.stream);
-        e.src.push_back(ds[i].get());
-        e.dst.push_back(dd[i].get());
+        e.src.push_back(ds[i].peer());
+        e.dst.push_back(dd[i].peer());
         e.weight.push_back(nullptr);
     }
     jg::build_graph_from_dense(g, e);
@@ -1152,7 +1206,7 @@ int jg_graph_destroy(jg_graph* g) {
     if (!g) return JG_OK;
     std::vector<int> devs;
     for (auto& sp : g->impl.shards) {
-        jg::DeviceGuard dg(sp->device);
+        jg::DeviceGuard dg(*sp);
         (void)hipStreamSynchronize(sp->stream);
         if (std::find(devs.begin(), devs.end(), sp->device) == devs.end()) devs.push_back(sp->device);
     }
@@ -1182,7 +1236,7 @@ int jg_graph_sync(jg_graph* g) {
     JG_GUARD_BEGIN
     JG_ARG(g, "null graph");
     for (auto& sp : g->impl.shards) {
-        jg::DeviceGuard dg(sp->device);
+        jg::DeviceGuard dg(*sp);
         JG_HIP(hipStreamSynchronize(sp->stream));
     }
     JG_GUARD_END

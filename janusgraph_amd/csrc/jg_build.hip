@@ -1084,7 +1084,7 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
     bool first = true;
     for (size_t li = 0; li < g.shards.size(); ++li) {
         Shard& sh = *g.shards[li];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         hipStream_t s = sh.stream;
         // The edge list of each adjacency: all of them, unless the snapshot was taken under Fulgora's
         // slice cap (then OUT: the capped OUT entries; IN: the capped IN entries or the capped OUT list).

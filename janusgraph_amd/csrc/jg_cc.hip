@@ -402,7 +402,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
 
 void exchange_msg(Graph& g, int which) {
     std::vector<void*> bufs;
-    for (auto& sp : g.shards) bufs.push_back(sp->cc_msg[which].get());
+    for (auto& sp : g.shards) bufs.push_back(sp->cc_msg[which].peer());
     exchange_vec(g, JG_ADJ_BOTH, bufs, sizeof(int32_t), ncclInt32);
 }
 
@@ -649,7 +649,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     std::vector<uint64_t*> swv, flv;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         hipStream_t s = sh.stream;
         St& t = st[i];
         const Csr& c = sh.both;
@@ -736,7 +736,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     // the bounded search, then the second round
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         hipStream_t s = sh.stream;
         St& t = st[i];
         if (t.ne == 0) continue;
@@ -759,15 +759,15 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     // the label rounds
     std::vector<void*> mv, rv;
     for (size_t i = 0; i < ns; ++i) {
-        mv.push_back(g.shards[i]->cc_msg[0].get());
-        rv.push_back(st[i].rbuf.get());
+        mv.push_back(g.shards[i]->cc_msg[0].peer());
+        rv.push_back(st[i].rbuf.peer());
     }
     int rounds = 0;
     for (bool any = true; any;) {
         ++rounds;
         for (size_t i = 0; i < ns; ++i) {  // own labels into the message vector's own part
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             if (st[i].ne)
                 JG_HIP(hipMemcpyAsync(sh.cc_msg[0].get(), st[i].label.get(), st[i].ne * sizeof(int32_t),
                                       hipMemcpyDeviceToDevice, sh.stream));
@@ -775,7 +775,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         exchange_msg(g, 0);
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
             if (t.ne == 0) continue;
@@ -797,7 +797,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         exchange_halo_reverse(g, JG_ADJ_BOTH, mv, rv, sizeof(int32_t), ncclInt32);
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             if (t.nsend) {
                 cc_reverse_apply_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
@@ -808,7 +808,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         int ch = 0;
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             int32_t c = 0;
             copy_d2h(&c, sh.cc_changed.get(), sizeof c, sh.stream);
             ch |= c;
@@ -817,7 +817,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     }
     // the superstep count: one BFS from every component's minimum-rank vertex
     std::vector<CcRoots> roots(ns);
-    for (size_t i = 0; i < ns; ++i) roots[i] = CcRoots{st[i].label.get(), st[i].rank.get(), nullptr, st[i].ne};
+    for (size_t i = 0; i < ns; ++i) roots[i] = CcRoots{st[i].label.peer(), st[i].rank.peer(), nullptr, st[i].ne};  // (used under shard i)
     double reached = 0;
     const int d = cc_root_eccentricity_sharded(g, roots.data(), &reached);
     const int it = d + 1;  // 0 when no vertex has an edge (d = -1)
@@ -826,7 +826,7 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
     unsigned long long lk = 0;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         St& t = st[i];
         unsigned long long l = 0;
         copy_d2h(&l, t.linked.get(), sizeof l, sh.stream);
@@ -864,7 +864,7 @@ void cc_prepare_ranks(Graph& g) {
     for (int64_t d = 0; d < (int64_t)g.vid.size(); ++d)
         if (g.vid[d] < 0) return;
     Shard& shr = *g.shards[0];
-    DeviceGuard dg(shr.device);
+    DeviceGuard dg(shr.device);  // graph-level arrays (untagged in the virtual-device check)
     hipStream_t s = shr.stream;
     DevBuf<int32_t> rk(std::max<int64_t>(n, 1));
     g.cc_vor.alloc(std::max<int64_t>(n, 1));
@@ -893,9 +893,14 @@ void cc_prepare_ranks(Graph& g) {
     std::vector<int32_t> rank_of;  // host copy, for shards on other devices
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        sh.cc_rank0.alloc(std::max<int64_t>(sh.rows, 1));
+        {
+            // on the shard's own device (found by the virtual-device check: round 4 allocated every shard's
+            // ranks on the first device, where shards on other devices would have read them across xGMI)
+            DeviceGuard dgs(sh);
+            sh.cc_rank0.alloc(std::max<int64_t>(sh.rows, 1));
+        }
         if (!sh.rows) continue;
-        if (sh.device == shr.device) {  // the rows' ranks, gathered on the device
+        if (same_device(sh, shr.device)) {  // the rows' ranks, gathered on the device
             gather_i32_kernel<<<grid_for(sh.rows), kBlock, 0, s>>>(rk.get(), sh.dense_rows.get(), sh.rows,
                                                                    sh.cc_rank0.get());
             JG_LAUNCH_CHECK();
@@ -908,7 +913,7 @@ void cc_prepare_ranks(Graph& g) {
         std::vector<int32_t> lab0((size_t)sh.rows);
         const std::vector<int32_t>& dl = sh.dense_of_local();
         for (int64_t l = 0; l < sh.rows; ++l) lab0[(size_t)l] = rank_of[(size_t)dl[(size_t)l]];
-        DeviceGuard dgs(sh.device);
+        DeviceGuard dgs(sh);
         copy_h2d(sh.cc_rank0.get(), lab0.data(), sh.rows * sizeof(int32_t), sh.stream);
         JG_HIP(hipStreamSynchronize(sh.stream));
     }
@@ -922,7 +927,7 @@ namespace {
 void cc_propagation_init(Graph& g) {
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         for (auto& m : sh.cc_msg) JG_HIP(hipMemsetAsync(m.get(), 0x7F, m.bytes(), sh.stream));  // ~INT_MAX
         if (sh.rows) {
             cc_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(sh.cc_rank0.get(), sh.both.row_ptr.get(), sh.rows,
@@ -948,7 +953,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     // buffers of the call (allocation only: every kernel of the call runs inside the timed region)
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const int64_t len = g.vec_len(sh, JG_ADJ_BOTH);
         for (int k = 0; k < 2; ++k)
             if (sh.cc_msg[k].size() != (size_t)len) sh.cc_msg[k].alloc(len);
@@ -1052,7 +1057,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         if (!pushed)
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
             CcOp op;
             op.msg = sh.cc_msg[cur].get();
@@ -1067,7 +1072,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         any = 0;
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             int32_t ch = 0;
             JG_HIP(hipMemcpyAsync(&ch, sh.cc_changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
             JG_HIP(hipStreamSynchronize(sh.stream));
@@ -1093,7 +1098,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     if (iterations_out) *iterations_out = iteration;
     if (comp_out && dev_maps && n > 0) {  // comp[dense of row l] = id of rank label[l], on the device
         Shard& sh = *g.shards[0];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         DevBuf<int64_t> out(n);
         cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(solved ? uf_labels : sh.cc_label.get(),
                                                                 sh.dense_rows.get(), g.cc_vor.get(), n, out.get());
@@ -1103,7 +1108,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         const std::vector<int64_t>& vid_of_rank = g.vid_of_rank();
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             std::vector<int32_t> h(sh.rows);
             const int32_t* lab = solved && &sh == &sh0 ? uf_labels : sh.cc_label.get();
             if (sh.rows) copy_d2h(h.data(), lab, sh.rows * sizeof(int32_t), sh.stream);

@@ -107,7 +107,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
     std::vector<St> st(ns);
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         hipStream_t s = sh.stream;
         St& t = st[i];
         const Csr& c = adj == JG_ADJ_OUT ? sh.out : adj == JG_ADJ_IN ? sh.in : sh.both;
@@ -143,7 +143,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
     }
     auto exchange = [&](int which) {
         std::vector<void*> bufs;
-        for (auto& t : st) bufs.push_back(t.x[which].get());
+        for (auto& t : st) bufs.push_back(t.x[which].peer());
         if (adj == JG_ADJ_OUT)
             exchange_allgather(g, bufs, sizeof(int64_t), ncclInt64);
         else
@@ -163,7 +163,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
             if (sh.rows == 0) continue;
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& s_ = st[i];
             const Csr& c = adj == JG_ADJ_OUT ? sh.out : adj == JG_ADJ_IN ? sh.in : sh.both;
             const PullPlan& plan = adj == JG_ADJ_OUT ? sh.plan_out : adj == JG_ADJ_IN ? sh.plan_in : sh.plan_both;
@@ -210,7 +210,7 @@ void combine_run(Graph& g, int direction, int combiner, int wrap32, const int64_
         Shard& sh = *g.shards[i];
         const int64_t n = sh.rows;
         if (n == 0) continue;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         St& t = st[i];
         std::vector<int64_t> h((size_t)n);
         copy_d2h(h.data(), t.x[cur].get() + t.pos.base, n * sizeof(int64_t), sh.stream);

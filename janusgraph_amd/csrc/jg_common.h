@@ -48,6 +48,23 @@ struct DirectFree {
     ~DirectFree();
 };
 
+// Virtual-device check (JG_VDEV_CHECK=1, logical shards).  A context that drives
+// several devices in one process (computer.gpu.devices=0,1,...) must keep every shard's buffers on that
+// shard's device.  Logical shards share one device, so there a misplaced buffer works and no test sees
+// it.  In the check mode every logical shard is a "virtual device": DeviceGuard(shard) makes the shard's
+// tag current on the thread, each DevBuf records the tag current at its allocation, and DevBuf::get()
+// under another shard's guard fails the call (vdev_violation: JG_ERR_STATE) instead of handing a kernel
+// or copy on that shard's stream a pointer of another device.  A plain DeviceGuard(int) is graph-level
+// work on the first device: tag 0 (the first shard's) in the check mode, so a per-shard buffer
+// allocated there is caught too.  Tag -1 (outside the check mode) checks nothing.  peer() is the
+// unchecked accessor for deliberate accesses across devices (the exchange's peer copies) and for
+// collecting pointers that another shard's guard will use.  JG_VDEV_CHECK=2 reports every violation
+// (return addresses as library offsets) and continues.
+inline thread_local int t_vtag = -1;
+int vdev_mode();     // JG_VDEV_CHECK: 0 off, 1 fail, 2 report and continue
+void vdev_refresh();  // re-read JG_VDEV_CHECK (jg_ctx_create)
+void vdev_violation(int buffer_tag, int current_tag);
+
 // Owning device allocation (dev_alloc on the current device).
 template <typename T>
 class DevBuf {
@@ -57,14 +74,15 @@ class DevBuf {
     ~DevBuf() { reset(); }
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p_(o.p_), n_(o.n_), dev_(o.dev_) { o.p_ = nullptr; o.n_ = 0; }
+    DevBuf(DevBuf&& o) noexcept : p_(o.p_), n_(o.n_), dev_(o.dev_), tag_(o.tag_) { o.p_ = nullptr; o.n_ = 0; }
     DevBuf& operator=(DevBuf&& o) noexcept {
-        if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; dev_ = o.dev_; o.p_ = nullptr; o.n_ = 0; }
+        if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; dev_ = o.dev_; tag_ = o.tag_; o.p_ = nullptr; o.n_ = 0; }
         return *this;
     }
     void alloc(size_t n) {
         reset();
         n_ = n;
+        tag_ = t_vtag;
         JG_HIP(hipGetDevice(&dev_));
         if (n) {
             p_ = static_cast<T*>(dev_alloc(n * sizeof(T)));
@@ -79,15 +97,26 @@ class DevBuf {
         p_ = nullptr;
         n_ = 0;
     }
-    T* get() const { return p_; }
+    T* get() const {
+        if (tag_ >= 0 && t_vtag >= 0 && tag_ != t_vtag) vdev_violation(tag_, t_vtag);
+        return p_;
+    }
+    T* peer() const { return p_; }  // a deliberate access from another shard's device (peer copies)
     size_t size() const { return n_; }
     size_t bytes() const { return n_ * sizeof(T); }
-    void swap(DevBuf& o) { std::swap(p_, o.p_); std::swap(n_, o.n_); std::swap(dev_, o.dev_); }
+    int tag() const { return tag_; }
+    void swap(DevBuf& o) {
+        std::swap(p_, o.p_);
+        std::swap(n_, o.n_);
+        std::swap(dev_, o.dev_);
+        std::swap(tag_, o.tag_);
+    }
 
    private:
     T* p_ = nullptr;
     size_t n_ = 0;
     int dev_ = 0;
+    int tag_ = -1;  // the virtual device current at allocation (-1: none)
 };
 
 inline unsigned grid_for(int64_t work, int per_block = kBlock, int64_t cap = 256 * 16) {
@@ -116,14 +145,23 @@ inline void copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
     JG_HIP(hipStreamSynchronize(s));
 }
 
-// RAII device switch.
+// RAII device switch.  DeviceGuard(shard) also makes the shard's virtual-device tag current (the
+// check mode above); DeviceGuard(int) clears it (graph-level work, unchecked).
 struct DeviceGuard {
-    int prev = 0;
-    explicit DeviceGuard(int dev) {
+    int prev = 0, prev_tag = -1;
+    explicit DeviceGuard(int dev) : prev_tag(t_vtag) {
         JG_HIP(hipGetDevice(&prev));
         if (prev != dev) JG_HIP(hipSetDevice(dev));
+        t_vtag = vdev_mode() ? 0 : -1;
     }
-    ~DeviceGuard() { (void)hipSetDevice(prev); }
+    template <class S, class = decltype(std::declval<const S&>().vtag)>
+    explicit DeviceGuard(const S& sh) : DeviceGuard(sh.device) {
+        t_vtag = sh.vtag;
+    }
+    ~DeviceGuard() {
+        (void)hipSetDevice(prev);
+        t_vtag = prev_tag;
+    }
 };
 
 }  // namespace jg

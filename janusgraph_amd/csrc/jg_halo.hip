@@ -226,7 +226,7 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
     Ctx& c = *g.ctx;
     for (size_t i = 0; i < g.shards.size(); ++i) {  // pack the runs of own values each peer reads
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const Halo& h = g.halo(sh, adj);
         const int64_t n = h.send_off[g.P];
         if (n == 0) continue;
@@ -257,7 +257,7 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
                 const int64_t n = hd.recv_off[q + 1] - hd.recv_off[q];
                 if (n == 0) continue;
                 JG_HIP(hipMemcpyAsync(seg_ptr(di, q),
-                                      reinterpret_cast<const char*>(hs.send_buf.get()) + hs.send_off[r] * elem_bytes,
+                                      reinterpret_cast<const char*>(hs.send_buf.peer()) + hs.send_off[r] * elem_bytes,
                                       n * elem_bytes, hipMemcpyDeviceToDevice, s0.stream));
             }
         }
@@ -266,7 +266,7 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
     if (c.host_transport) {  // rank mode over host callbacks (one shard per process): staged runs
         Shard& sh = *g.shards[0];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         std::vector<char> sbuf((size_t)h.send_off[g.P] * elem_bytes);
         copy_d2h(sbuf.data(), h.send_buf.get(), sbuf.size(), sh.stream);  // after the pack kernel
         std::vector<int> sp, rp;
@@ -298,7 +298,7 @@ void exchange_halo(Graph& g, uint32_t adj, std::vector<void*>& bufs, size_t elem
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         for (int q = 0; q < g.P; ++q) {
             if (q == sh.index) continue;
             const int64_t ns = h.send_off[q + 1] - h.send_off[q];
@@ -345,7 +345,7 @@ void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std
     if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
         Shard& sh = *g.shards[0];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         std::vector<int> sp, rp;
         std::vector<const void*> sv;
         std::vector<void*> rv;
@@ -378,7 +378,7 @@ void exchange_halo_reverse(Graph& g, uint32_t adj, std::vector<void*>& vecs, std
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         for (int q = 0; q < g.P; ++q) {
             if (q == sh.index) continue;
             const int64_t ns = h.recv_off[q + 1] - h.recv_off[q];  // my segment for q goes back to q
@@ -434,7 +434,7 @@ void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, s
     if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
         Shard& sh = *g.shards[0];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
         std::vector<int> sp, rp;
         std::vector<const void*> sv;
@@ -471,7 +471,7 @@ void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, s
     for (size_t i = 0; i < g.shards.size(); ++i) {
         Shard& sh = *g.shards[i];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
         for (int q = 0; q < g.P; ++q) {
             if (q == sh.index) continue;
@@ -516,7 +516,7 @@ void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::ve
     }
     if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
         Shard& sh = *g.shards[0];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         std::vector<int> sp, rp;
         std::vector<const void*> sv;
         std::vector<void*> rv;
@@ -547,7 +547,7 @@ void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::ve
     rccl_check(ncclGroupStart(), "ncclGroupStart");
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         for (int q = 0; q < g.P; ++q) {
             if (q == sh.index) continue;
             const int64_t n_s = scount[i][(size_t)q], n_r = rcount[i][(size_t)q];

@@ -203,6 +203,7 @@ struct VecPos {
 struct Shard {
     int device = 0;
     int index = 0;           // shard id r in [0, P)
+    int vtag = -1;           // virtual-device tag (JG_VDEV_CHECK=1 on logical shards: the index; jg_common.h)
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;  // borrowed from the context (may be null)
     int64_t rows = 0;        // owned rows (<= S)
@@ -258,6 +259,11 @@ struct Shard {
     std::vector<int> prof_units;          // supersteps each pair spans
 };
 
+// Whether shard sh is on physical device dev as far as data placement goes: in the virtual-device check
+// mode every logical shard but the first counts as a device of its own (jg_common.h), so the
+// multi-device paths (peer copies, per-device tables) run on one GPU.
+inline bool same_device(const Shard& sh, int dev) { return sh.device == dev && sh.vtag <= 0; }
+
 struct Graph {
     Ctx* ctx = nullptr;
     int64_t n = 0;         // caller vertices
@@ -312,6 +318,7 @@ struct Ctx {
     int nranks = 1;             // processes (rank mode) — total shards = nranks * devices.size()
     int rank = 0;
     bool logical = false;       // several shards on one device: exchange by device copies
+    bool vdev = false;          // logical shards checked as virtual devices (JG_VDEV_CHECK=1, jg_common.h)
     std::vector<ncclComm_t> comms;
     bool host_transport = false;  // rank mode over jg_transport callbacks (tests) instead of RCCL
     jg_transport transport{};

@@ -71,7 +71,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
         if (!k) continue;
         const Shard& sh = *local[q];
         const Csr& c = pick(sh, direction);
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         DevBuf<int64_t> drows(k), dlen(k);
         copy_h2d(drows.get(), loc[q].data(), (size_t)k * sizeof(int64_t), sh.stream);
         row_bounds_kernel<<<grid_for(k), kBlock, 0, sh.stream>>>(c.row_ptr.get(), drows.get(), k, dlen.get());
@@ -103,7 +103,7 @@ void graph_neighbors(const Graph& g, int direction, const int64_t* rows, int64_t
         for (int p = 0; p < g.P; ++p) {
             const Shard& sh = *g.shards[p];
             const Halo& h = g.halo(sh, adj);
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             send[p].resize((size_t)h.send_off[g.P]);
             if (!send[p].empty())
                 copy_d2h(send[p].data(), h.send_src.get(), send[p].size() * sizeof(int32_t), sh.stream);

@@ -12,6 +12,8 @@
 // contrib_in at col[] (full length, or the shard's compact vector); then the exchange step
 // (allgather or halo exchange, RCCL) refreshes every shard's copy.
 // Algorithmic bytes per superstep: 12*m + 32*n.
+#include <cstdlib>
+
 #include "jg_pull.h"
 #include "jg_scatter.h"
 
@@ -54,7 +56,7 @@ __global__ void pr_init_kernel(const int32_t* __restrict__ outdeg, int64_t rows,
 
 void exchange_contrib(Graph& g, int which) {
     std::vector<void*> bufs;
-    for (auto& sp : g.shards) bufs.push_back(sp->pr_contrib[which].get());
+    for (auto& sp : g.shards) bufs.push_back(sp->pr_contrib[which].peer());
     exchange_vec(g, JG_ADJ_IN, bufs, sizeof(double), ncclFloat64);
 }
 
@@ -65,13 +67,23 @@ void pagerank_begin(Graph& g, double damping, int64_t vertex_count) {
     if (vertex_count == 0) fail(JG_ERR_ARG, "vertexCount must be non-zero");
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const int64_t len = g.vec_len(sh, JG_ADJ_IN);
         for (int k = 0; k < 2; ++k) {
             if (sh.pr_contrib[k].size() != (size_t)len) sh.pr_contrib[k].alloc(len);
             JG_HIP(hipMemsetAsync(sh.pr_contrib[k].get(), 0, sh.pr_contrib[k].bytes(), sh.stream));
         }
-        if (sh.pr_rank.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
+        if (sh.pr_rank.size() != (size_t)std::max<int64_t>(sh.rows, 1)) {
+            // JG_VDEV_FAULT=1 (tests/test_gpu_vdev.py): the rank vector of shards > 0 allocated under the first
+            // shard's guard, the misplacement the virtual-device check must report (ADVICE r03's bug class)
+            const char* f = std::getenv("JG_VDEV_FAULT");
+            if (f && *f && *f != '0' && sh.index > 0) {
+                DeviceGuard d0(*g.shards[0]);
+                sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
+            } else {
+                sh.pr_rank.alloc(std::max<int64_t>(sh.rows, 1));
+            }
+        }
         if (sh.pr_hub_partial.size() != (size_t)std::max<int64_t>(sh.plan_in.num_chunks, 1))
             sh.pr_hub_partial.alloc(std::max<int64_t>(sh.plan_in.num_chunks, 1));
         if (sh.pr_split_partial.size() != (size_t)sh.plan_in.split_partial_len()) {
@@ -110,7 +122,7 @@ void pagerank_steps(Graph& g, int nsteps) {
         const int cur = g.pr_cur, nxt = cur ^ 1;
         for (auto& sp : g.shards) {
             Shard& sh = *sp;
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             PrOp op;
             op.x = sh.pr_contrib[cur].get();
             op.contrib_out = sh.pr_contrib[nxt].get();
@@ -143,7 +155,7 @@ void pagerank_end(Graph& g, double* rank_out, double* edge_count_out) {
     if (!g.pr_begun) fail(JG_ERR_STATE, "jg_pagerank_end before jg_pagerank_begin");
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         JG_HIP(hipStreamSynchronize(sh.stream));
         if (sh.rows == 0) continue;
         if (rank_out) rows_to_dense(g, sh, sh.pr_rank.get(), rank_out);

@@ -23,7 +23,7 @@ __global__ void rows_to_dense_kernel(const Td* __restrict__ in, const int32_t* _
 template <class Td, class Th>
 void rows_to_dense(const Graph& g, Shard& sh, const Td* dev, Th* out) {
     if (sh.rows == 0) return;
-    DeviceGuard dg(sh.device);
+    DeviceGuard dg(sh);
     if (g.shards.size() == 1 && sh.rows == g.n && sh.dense_rows.size() >= (size_t)sh.rows) {
         DevBuf<Th> tmp(sh.rows);
         rows_to_dense_kernel<Td, Th><<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(dev, sh.dense_rows.get(), sh.rows,

@@ -1810,7 +1810,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     int64_t src_deg = 0, nq0 = 0;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const Halo& h = sh.halo_both;
         St& t = st[i];
         const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
@@ -1857,14 +1857,14 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         JG_HIP(hipEventCreate(&t0));
         JG_HIP(hipEventCreate(&t1));
         for (auto& sp : g.shards) {
-            DeviceGuard dgs(sp->device);
+            DeviceGuard dgs(*sp);
             JG_HIP(hipStreamSynchronize(sp->stream));  // the plan copies above; t0 marks the traversal's start
         }
         JG_HIP(hipEventRecord(t0, sh0.stream));
     }
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         St& t = st[i];
         zero_gathered(g, sh, JG_ADJ_BOTH, t.stamp.get(), sizeof(int32_t));
         JG_HIP(hipMemsetAsync(t.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
@@ -1909,8 +1909,8 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     int level = 0, cur = 0;
     std::vector<uint64_t*> swv, hbv;
     for (auto& t : st) {
-        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.get()));
-        hbv.push_back(reinterpret_cast<uint64_t*>(t.hb.get()));
+        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.peer()));  // (the exchange uses them under each shard)
+        hbv.push_back(reinterpret_cast<uint64_t*>(t.hb.peer()));
     }
     auto level_args = [&](size_t i) {
         Shard& sh = *g.shards[i];
@@ -1955,7 +1955,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         else if (bu && (double)nf < (double)nrows / beta) bu = false;
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             if (bu && t.sw_words > 0) {  // this level's frontier bits of the send lists (before the forward exchange)
                 sbfs_pack_bits_kernel<<<run_grid(t.sw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
@@ -1965,7 +1965,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         if (bu) exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, false);
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             const SBfsLevel a = level_args(i);
             const unsigned grid = (unsigned)std::min<int64_t>(
@@ -1982,7 +1982,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         if (!bu) {
             for (size_t i = 0; i < ns; ++i) {  // the stamps of this level into the segment words
                 Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh.device);
+                DeviceGuard dg(sh);
                 if (st[i].rw_words > 0) {
                     sbfs_pack_marks_kernel<<<run_grid(st[i].rw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
                     JG_LAUNCH_CHECK();
@@ -1991,7 +1991,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, true);
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh.device);
+                DeviceGuard dg(sh);
                 St& t = st[i];
                 if (t.sw_words > 0) {
                     sbfs_td_apply_kernel<<<run_grid(t.sw_max, kSbfsApplyChunk, 1024), kBlock, 0, sh.stream>>>(level_args(i));
@@ -2002,7 +2002,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         int64_t sums[2] = {0, 0};
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             unsigned long long c = 0;
             copy_d2h(&c, st[i].ctr.get() + ((level + 1) & 1), sizeof c, sh.stream);
             st[i].nq = (int64_t)(c >> kPackShift);
@@ -2032,7 +2032,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     // depths of the own rows
     for (size_t i = 0; i < ns && !roots; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.rows)
             JG_HIP(hipMemcpyAsync(sh.bfs_depth.get(), st[i].dvec.get(), sh.rows * sizeof(int32_t),
@@ -2113,7 +2113,7 @@ void zero_gathered(const Graph& g, const Shard& sh, uint32_t adj, void* v, size_
 
 void bfs_kept_release(Graph& g) {
     for (auto& sp : g.shards) {
-        DeviceGuard dg(sp->device);
+        DeviceGuard dg(*sp);
         sp->kept_depth.reset();
     }
     g.kept_nsrc = 0;
@@ -2125,7 +2125,7 @@ template <class F>
 void keep_rows(Graph& g, F rows_of) {
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         sh.kept_depth.alloc(std::max<int64_t>(sh.rows, 1));
         if (sh.rows)
             JG_HIP(hipMemcpyAsync(sh.kept_depth.get(), rows_of(sh), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice,
@@ -2138,7 +2138,7 @@ void keep_rows(Graph& g, F rows_of) {
 
 void bfs_kept_row(Graph& g, int s, int32_t* depth_out) {
     if (s < 0 || s >= g.kept_nsrc) fail(JG_ERR_ARG, "no kept depth row with that index (jg_bfs_keep)");
-    for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->kept_depth.get() + (int64_t)s * sp->rows, depth_out);
+    for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->kept_depth.peer() + (int64_t)s * sp->rows, depth_out);
 }
 
 void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int max_depth, int32_t* const* depth_rows,
@@ -2169,7 +2169,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.supersteps = levels;
         ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
         if (depth_rows && depth_rows[0])
-            for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.get(), depth_rows[0]);
+            for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.peer(), depth_rows[0]);
         if (keep) keep_rows(g, [](Shard& sh) { return sh.bfs_depth.get(); });
         prof_collect(ctx, g);
     } else if (single) {
@@ -2306,7 +2306,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             int64_t push_nnz = 0;  // entries of the push adjacency, all shards and ranks (the direction rule)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh.device);
+                DeviceGuard dg(sh);
                 const BfsCsrs c = pick_csrs(sh, direction);
                 if (!c.pull) fail(JG_ERR_UNSUPPORTED, "multi-source BFS needs the pull adjacency");
                 const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
@@ -2365,7 +2365,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 int64_t v[2] = {0, 0};
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     unsigned long long hh[2] = {0, 0};
                     copy_d2h(hh, tds[i].ctr.get(), (touched ? 2 : 1) * sizeof(unsigned long long), sh.stream);
                     const unsigned long long h = hh[0];
@@ -2387,7 +2387,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 uint64_t v = 0;
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     uint64_t w = 0;
                     copy_d2h(&w, st[i].live.get(), sizeof w, sh.stream);
                     v |= w;
@@ -2395,14 +2395,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 v = allreduce_or_u64(g, v);
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     copy_h2d(st[i].live.get(), &v, sizeof v, sh.stream);
                 }
             };
             auto build_frontier = [&](int qslot) {
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     const BfsCsrs c = pick_csrs(sh, direction);
                     JG_HIP(hipMemsetAsync(tds[i].ctr.get(), 0, sizeof(unsigned long long), sh.stream));
                     msbfs_frontier_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
@@ -2415,7 +2415,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             if (td_ok) {  // allocated before the timed region (~2.3 GB at RMAT-26 on one shard)
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     Td& td = tds[i];
                     const size_t r1 = (size_t)std::max<int64_t>(sh.rows, 1);
                     for (int k = 0; k < 2; ++k) {
@@ -2449,7 +2449,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // sources (and level 0's depth record)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh.device);
+                DeviceGuard dg(sh);
                 St& t = st[i];
                 const BfsCsrs c = pick_csrs(sh, direction);
                 zero_gathered(g, sh, adj_of(sh, c), t.F[0].get(), sizeof(unsigned long long));
@@ -2474,14 +2474,14 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             }
             if (!td_ok) {
                 std::vector<void*> bufs;
-                for (auto& t : st) bufs.push_back(t.F[0].get());
+                for (auto& t : st) bufs.push_back(t.F[0].peer());
                 exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
                 need_fwd = false;
             }
             if (td_ok) {  // the level-0 frontier is the source rows: queued directly, no scan of F
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     const BfsCsrs c = pick_csrs(sh, direction);
                     msbfs_source_queue_kernel<<<1, kWave, 0, sh.stream>>>(tds[i].srcs.get(), (int)tds[i].src_rows.size(),
                                                                        c.push->row_ptr.get(), tds[i].queue[0].get(),
@@ -2500,7 +2500,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     Shard& sh = *g.shards[i];
                     St& t = st[i];
                     if (t.depth8.size() || t.depth.size()) continue;
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     t.depth8.alloc(std::max<int64_t>(sh.rows * ns, 1));
                     JG_HIP(hipMemsetAsync(t.depth8.get(), 0xFF, t.depth8.bytes(), sh.stream));
                 }
@@ -2510,7 +2510,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     Shard& sh = *g.shards[i];
                     St& t = st[i];
                     if (t.depth.size()) continue;
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     const int64_t total = std::max<int64_t>(sh.rows * ns, 1);
                     t.depth.alloc(total);
                     if (t.depth8.size()) {
@@ -2533,7 +2533,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 for (size_t i = 0; i < g.shards.size(); ++i) {
                     Shard& sh = *g.shards[i];
                     St& t = st[i];
-                    DeviceGuard dg(sh.device);
+                    DeviceGuard dg(sh);
                     const int lw = std::min(levels_run + 1, kMsLevelWords);
                     if (sh.rows > 0) {
                         const Csr* pc = pick_csrs(sh, direction).pull;
@@ -2560,6 +2560,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // rows.  (Only the exit bands through the exit, the light rows merged: RMAT-26 11.42 vs 11.20 ms.)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
                 const BfsCsrs c = pick_csrs(sh, direction);
                 const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
                 St& t = st[i];
@@ -2600,7 +2601,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     std::vector<void*> fv, rv;
                     for (size_t i = 0; i < g.shards.size(); ++i) {
                         Shard& sh = *g.shards[i];
-                        DeviceGuard dg(sh.device);
+                        DeviceGuard dg(sh);
                         const BfsCsrs c = pick_csrs(sh, direction);
                         St& t = st[i];
                         Td& td = tds[i];
@@ -2656,8 +2657,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                                 JG_LAUNCH_CHECK();
                             }
                         }
-                        fv.push_back(td.hs.get());
-                        rv.push_back(td.rbuf.get());
+                        fv.push_back(td.hs.peer());
+                        rv.push_back(td.rbuf.peer());
                     }
                     // sparse: only the set staging slots travel, as (offset, word) pairs, when they are fewer
                     // than half the halo slots over all shards (the tail levels and the first levels from
@@ -2669,7 +2670,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         std::vector<int64_t> mat((size_t)P * P + 1, 0);
                         for (size_t i = 0; i < g.shards.size(); ++i) {
                             Shard& sh = *g.shards[i];
-                            DeviceGuard dg(sh.device);
+                            DeviceGuard dg(sh);
                             // per-peer slot counts: the top-down kernel counted the slots it set first
                             std::vector<unsigned long long> c((size_t)P);
                             copy_d2h(c.data(), tds[i].pcnt.get(), (size_t)P * sizeof(unsigned long long), sh.stream);
@@ -2689,7 +2690,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             std::vector<std::vector<int64_t>> so(ns_), sc(ns_), ro(ns_), rc(ns_);
                             for (size_t i = 0; i < ns_; ++i) {
                                 Shard& sh = *g.shards[i];
-                                DeviceGuard dg(sh.device);
+                                DeviceGuard dg(sh);
                                 so[i].assign((size_t)P + 1, 0);
                                 ro[i].assign((size_t)P + 1, 0);
                                 sc[i].assign((size_t)P, 0);
@@ -2727,7 +2728,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             exchange_runs(g, sp, so, sc, rp, ro, rc, sizeof(unsigned long long), ncclUint64);
                             for (size_t i = 0; i < ns_; ++i) {
                                 Shard& sh = *g.shards[i];
-                                DeviceGuard dg(sh.device);
+                                DeviceGuard dg(sh);
                                 if (tds[i].nrp > 0) {
                                     msbfs_td_recv_pairs_kernel<<<grid_for(tds[i].nrp), kBlock, 0, sh.stream>>>(
                                         tds[i].rpairs.get(), tds[i].nrp, tds[i].pv, sh.halo_both.send_src.get(),
@@ -2746,7 +2747,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                         exchange_halo_reverse(g, JG_ADJ_BOTH, fv, rv, sizeof(unsigned long long), ncclUint64);
                         for (size_t i = 0; i < g.shards.size(); ++i) {
                             Shard& sh = *g.shards[i];
-                            DeviceGuard dg(sh.device);
+                            DeviceGuard dg(sh);
                             const int64_t nrecv = sh.halo_both.send_off[g.P];
                             if (nrecv > 0) {
                                 msbfs_td_recv_kernel<<<grid_for(nrecv, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
@@ -2759,7 +2760,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                     for (size_t i = 0; i < g.shards.size(); ++i) {
                         Shard& sh = *g.shards[i];
-                        DeviceGuard dg(sh.device);
+                        DeviceGuard dg(sh);
                         const BfsCsrs c = pick_csrs(sh, direction);
                         St& t = st[i];
                         Td& td = tds[i];
@@ -2804,7 +2805,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     if (level + 1 < kMsLevelWords)
                         for (size_t i = 0; i < g.shards.size(); ++i) {  // the level's depths: its new queue
                             Shard& sh = *g.shards[i];
-                            DeviceGuard dg(sh.device);
+                            DeviceGuard dg(sh);
                             St& t = st[i];
                             const int64_t nq = tds[i].nq;
                             t.recs.emplace_back();
@@ -2829,13 +2830,13 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     prev_td = false;
                     if (need_fwd) {  // stale halo segments: the lazy forward exchange
                         std::vector<void*> bufs;
-                        for (auto& t : st) bufs.push_back(t.F[cur].get());
+                        for (auto& t : st) bufs.push_back(t.F[cur].peer());
                         exchange_vec(g, adj0, bufs, sizeof(unsigned long long), ncclUint64);
                         need_fwd = false;
                     }
                     for (size_t i = 0; i < g.shards.size(); ++i) {
                         Shard& sh = *g.shards[i];
-                        DeviceGuard dg(sh.device);
+                        DeviceGuard dg(sh);
                         const BfsCsrs c = pick_csrs(sh, direction);
                         const PullPlan& plan = (c.pull == &sh.both) ? sh.plan_both : sh.plan_in;
                         St& t = st[i];
@@ -2982,7 +2983,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 } else {
                     for (size_t i = 0; i < g.shards.size(); ++i) {
                         Shard& sh = *g.shards[i];
-                        DeviceGuard dg(sh.device);
+                        DeviceGuard dg(sh);
                         int32_t ch = 0;
                         JG_HIP(hipMemcpyAsync(&ch, st[i].changed.get(), sizeof ch, hipMemcpyDeviceToHost, sh.stream));
                         JG_HIP(hipStreamSynchronize(sh.stream));
@@ -3007,7 +3008,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             // per queued vertex; past kMsLevelWords levels 4 B per reached (source, row) pair (a plane entry)
             for (size_t i = 0; i < g.shards.size(); ++i) {
                 Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh.device);
+                DeviceGuard dg(sh);
                 St& t = st[i];
                 if (level >= kMsLevelWords) {  // the plane entries are counted only when planes were written
                     msbfs_pairs_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(t.vis.get(), sh.rows,
@@ -3034,7 +3035,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     for (size_t i = 0; i < g.shards.size(); ++i)
                         for (int s = 0; s < ns; ++s)
                             if (depth_rows[b0 + s])
-                                rows_to_dense(g, *g.shards[i], st[i].depth.get() + (size_t)s * g.shards[i]->rows,
+                                rows_to_dense(g, *g.shards[i], st[i].depth.peer() + (size_t)s * g.shards[i]->rows,
                                               depth_rows[b0 + s]);
                 if (keep)  // the planes stay with their shards (jg_bfs_kept_row)
                     for (size_t i = 0; i < g.shards.size(); ++i) g.shards[i]->kept_depth.swap(st[i].depth);
@@ -3080,7 +3081,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     std::vector<void*> bv, rv;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         const Halo& h = sh.halo_in;
         St& t = st[i];
         const int64_t rows = std::max<int64_t>(sh.rows, 1);
@@ -3105,8 +3106,8 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
             copy_h2d(t.fa.get(), &seed32, sizeof seed32, sh.stream);
             t.fsize = 1;
         }
-        bv.push_back(t.best.get());
-        rv.push_back(t.rbuf.get());
+        bv.push_back(t.best.peer());
+        rv.push_back(t.rbuf.peer());
     }
     int64_t total = seed_local >= 0 ? 1 : 0;
     allreduce_sum_i64(g, &total, 1);
@@ -3122,7 +3123,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     for (int lv = 1; lv <= max_depth && total > 0; ++lv) {
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             JG_HIP(hipMemsetAsync(t.sizes.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
             if (t.fsize > 0) {
@@ -3136,7 +3137,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         int64_t next = 0;
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh.device);
+            DeviceGuard dg(sh);
             St& t = st[i];
             const Halo& h = sh.halo_in;
             const int64_t nrecv = h.send_off[g.P];
@@ -3181,7 +3182,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     int missing = 0;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
-        DeviceGuard dg(sh.device);
+        DeviceGuard dg(sh);
         int32_t e = 0;
         copy_d2h(&e, st[i].err.get(), sizeof e, sh.stream);
         missing |= e;
@@ -3203,7 +3204,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         return;
     }
     Shard& sh = *g.shards[0];
-    DeviceGuard dg(sh.device);
+    DeviceGuard dg(sh);
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     int shard = 0;

@@ -100,6 +100,54 @@ def _worker(rank, world, port, halo, errfile):
         raise
 
 
+def _worker_msbfs(rank, world, port, errfile):
+    """64 sources, unbounded, rank mode (the driver's N-GPU bench runs this path): top-down levels with the
+    sparse pair exchange, pull levels after the frontier's peak, the last levels top-down again; every row
+    against the oracle, and the level count."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import janusgraph_amd as jg
+        from janusgraph_amd.transport import GlooTransport
+        from oracle import oracle as o
+        scale = 14
+        n = 1 << scale
+        s, d = o.rmat_edges(scale, 16, 0x5EED + scale)
+        ds, dd = s.astype(np.int32), d.astype(np.int32)
+        vid = (np.arange(n, dtype=np.int64) + 1) << 8
+        ctx = jg.Context((0,), rank=rank, nranks=world, transport=GlooTransport(dist, world))
+        g = ctx.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
+        deg = np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n)
+        # 62 sources with an edge, an isolated vertex and a hub
+        srcs = np.concatenate([np.random.default_rng(14).choice(np.flatnonzero(deg > 0), 62, replace=False),
+                               [np.flatnonzero(deg == 0)[0], int(np.argmax(deg))]]).astype(np.int64)
+        for max_depth in (-1, 2):
+            got = g.bfs(vid[srcs], jg.DIR_BOTH, max_depth=max_depth)
+            levels = ctx.stats()["levels"]
+            got, own = _combine(dist, world, got.ravel(), np.iinfo(np.int32).min)
+            if rank == 0:
+                assert (own == 1).all(), "every (source, vertex) owned once"
+                got = got.reshape(len(srcs), n)
+                ptr, adj = o.csr_unordered(n, ds, dd, both=True)
+                want = o.msbfs_csr(n, ptr, adj, srcs, max_depth)
+                for k in range(len(srcs)):
+                    np.testing.assert_array_equal(got[k], want[k], err_msg=f"source {k}, max_depth {max_depth}")
+                deepest = int(want.max())
+                assert levels == (deepest + 1 if max_depth < 0 else min(deepest + 1, max_depth)), (levels, deepest)
+        g.close()
+        ctx.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}:\n" + traceback.format_exc())
+        raise
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -114,6 +162,25 @@ def test_ranks_over_host_transport(tmp_path, world, halo):
     errfile = str(tmp_path / "err.txt")
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, halo, errfile)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    err = open(errfile).read() if os.path.exists(errfile) else ""
+    assert all(p.exitcode == 0 for p in procs), f"exit codes {[p.exitcode for p in procs]}\n{err}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_msbfs64_unbounded_ranks_over_host_transport(tmp_path, world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errfile = str(tmp_path / "err.txt")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_msbfs, args=(r, world, port, errfile)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
