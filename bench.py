@@ -290,10 +290,12 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
 def per_rank_rows(rows):
     """Each rank's (compute_ms, exchange_ms) of a program call.  The exchange pairs are recorded inside the
     call's timed region only (prof_discard_exchanges at its start), so exchange_ms <= compute_ms must hold;
-    a row that breaks it means the timing is wrong, and the run fails loudly instead of reporting it."""
+    a row that breaks it is flagged `timing_suspect` (the other blocks' results stay), and
+    tests/test_bench_host.py fails on such a row."""
     out = [{"rank": r, "compute_ms": round(x[0], 4), "exchange_ms": round(x[1], 4)} for r, x in enumerate(rows)]
-    bad = [o for o in out if o["exchange_ms"] > o["compute_ms"] * 1.001 + 0.01]
-    assert not bad, f"exchange time exceeds the call's compute time: {bad}"
+    for o in out:
+        if o["exchange_ms"] > o["compute_ms"] * 1.001 + 0.01:
+            o["timing_suspect"] = "exchange_ms exceeds the call's compute_ms"
     return out
 
 

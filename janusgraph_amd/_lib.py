@@ -521,6 +521,9 @@ class Graph:
 
     def bfs_kept_row(self, s, out=None):
         """jg_bfs_kept_row: row s of the last bfs_keep, into `out` (n int32) or a new array."""
+        if out is not None and not (isinstance(out, np.ndarray) and out.dtype == np.int32 and out.ndim == 1
+                                    and out.flags.c_contiguous and out.size >= self.n):
+            raise ValueError("out must be a C-contiguous int32 array of at least n elements")  # (ADVICE r04)
         row = self._out(self.n, np.int32) if out is None else out
         check(load().jg_bfs_kept_row(self._h, int(s), _ptr(row)))
         return row

@@ -33,10 +33,11 @@ def test_required_bytes_below_model():
     assert abs(r["frac"] - r["bytes_per_launch"] / 0.8e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-4
 
 
-def test_per_rank_rows_refuse_exchange_beyond_compute():
-    """VERDICT r03 weak #2: a rank's exchange time inside a call cannot exceed the call's time."""
-    import pytest
+def test_per_rank_rows_flag_exchange_beyond_compute():
+    """a rank's exchange time inside a call cannot exceed the call's time; such a row
+    is flagged (the other blocks' results are kept) and this test is where it fails."""
     rows = bench.per_rank_rows([[10.0, 2.5], [9.5, 3.0]])
     assert rows[1] == {"rank": 1, "compute_ms": 9.5, "exchange_ms": 3.0}
-    with pytest.raises(AssertionError):
-        bench.per_rank_rows([[936.9, 1302.0]])
+    assert not any("timing_suspect" in r for r in rows)
+    bad = bench.per_rank_rows([[936.9, 1302.0]])
+    assert "timing_suspect" in bad[0]
