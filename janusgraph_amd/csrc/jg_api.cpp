@@ -669,6 +669,8 @@ int jg_tune_set(const char* key, int64_t value) {
         {"bfs_grid_mult", &t.bfs_grid_mult, 1, 64},
         {"bfs_grid", &t.bfs_grid, 64, 65536},
         {"bfs_tail_grid", &t.bfs_tail_grid, 0, 65536},
+        {"bfs_persistent", &t.bfs_persistent, 0, 1},
+        {"bfs_persistent_grid", &t.bfs_persistent_grid, 0, 8192},
         {"merge_temporal", &t.merge_temporal, 0, 2},
     };
     for (const Knob& kn : knobs) {

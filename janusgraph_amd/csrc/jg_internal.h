@@ -243,6 +243,7 @@ struct Shard {
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;
+    DevBuf<unsigned char> bfs_sync;          // persistent DO-BFS: grid-barrier counters, abort flag, final state
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
     // narrow bit-parallel BFS scratch (<= 8 sources, one shard; jg_narrow.hip), kept across calls
     std::vector<DevBuf<uint8_t>> nb_level;   // [levels][rows + pad] each level's frontier byte (= its new bits)
@@ -623,6 +624,9 @@ struct Tune {
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
                                       //         (0: every launch at the full grid)
+    int bfs_persistent = 0;           //         DO-BFS: every level in one launch, a grid barrier between levels
+                                      //         (measured slower, profiles/r05/persistent/)
+    int bfs_persistent_grid = 0;      //         its workgroups (0: the level grid, capped at the co-resident count)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
