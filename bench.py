@@ -27,6 +27,19 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
+# Host-clock windows of every timed region (block, start ns, end ns, runs), CLOCK_MONOTONIC: printed with
+# --trace-windows so tools/bench_trace.py can cut a rocprofv3 kernel trace of this same process into the
+# blocks' timed runs
+WINDOWS = []
+
+
+def window_start():
+    return time.monotonic_ns()
+
+
+def window_end(block, t0, runs=1):
+    WINDOWS.append([block, t0, time.monotonic_ns(), runs])
+
 
 def parse():
     p = argparse.ArgumentParser()
@@ -43,6 +56,8 @@ def parse():
     p.add_argument("--no-big", action="store_true", help="skip the RMAT-26 blocks (PageRank, BFS, CC, MS-BFS)")
     p.add_argument("--big-scale", type=int, default=26)
     p.add_argument("--big-steps", type=int, default=10)
+    p.add_argument("--trace-windows", action="store_true",
+                   help="add the timed regions' host-clock windows to the JSON line (tools/bench_trace.py)")
     p.add_argument("--host-transport", action="store_true",
                    help="N > 1 rehearsal on one GPU: every rank on device 0, exchanges over gloo through the "
                         "library's host transport instead of RCCL (not a performance measurement)")
@@ -178,6 +193,30 @@ def trace_kernel_ms(workload):
     return None
 
 
+def bench_trace_block(workload):
+    """This workload's block from the newest committed trace of a whole bench process
+    (profiles/<round>/bench_trace/summary.json, tools/bench_trace.py): the trace's span and kernel sum per
+    run against that process's own event figure, and the roofline fraction on each.
+    None when there is none."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for rnd in sorted(os.listdir(pdir), reverse=True):
+        fn = os.path.join(pdir, rnd, "bench_trace", "summary.json")
+        if not os.path.exists(fn):
+            continue
+        with open(fn) as f:
+            blk = json.load(f).get("blocks", {}).get(workload)
+        if blk is None:
+            continue
+        keep = ("event_ms", "trace_span_ms", "trace_kernel_ms", "frac_event", "frac_trace_span", "frac_trace_kernel",
+                "span_over_event", "agree", "within_step")
+        out = {k: blk[k] for k in keep if k in blk}
+        out["source"] = os.path.relpath(fn, ROOT)
+        return out
+    return None
+
+
 def cpu_baseline(scale, ef, seed, steps):
     """The oracle's PageRank superstep (OpenMP) on the same RMAT graph, rank 0 only."""
     from oracle import oracle as o
@@ -229,6 +268,7 @@ def hbm_roofline(alg_bytes, ms, kernel, workload=None, model=None):
          "kernel": kernel, "kernel_ms": round(ms, 4), "bytes_per_launch": alg_bytes}
     if workload:
         r["trace"] = trace_kernel_ms(workload)
+        r["bench_trace"] = bench_trace_block(workload)
     if model:
         r["model"] = model
     return r
@@ -262,7 +302,9 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
         if ctx.stats()["edges_traversed"] < m // 100:
             continue  # a source in a tiny component: Graph500 resamples
         ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
+        w0 = window_start()
         gb.bfs([sv], jg.DIR_BOTH, want=False)  # timed run (the first touched cold pages)
+        window_end(f"bfs_spvp_rmat{scale}_ef{ef}", w0)
         st = ctx.stats()
         ctx.set_profiling(False)
         ms = ctl.max(st["compute_ms"])
@@ -274,7 +316,10 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
     ms = float(np.median(times))
     workload = f"bfs_spvp_rmat{scale}_ef{ef}"
     blk = {"workload": workload, "gteps_median": round(float(np.median(teps)), 3), "ms_median": round(ms, 4),
-           "runs": len(times), "sources": [int(x) for x in srcs]}
+           "runs": len(times), "sources": [int(x) for x in srcs],
+           "timed_region": "HIP events from the init launch to the end of the last level batch; the source's id "
+                           "lookup, the host's read of the final level state and the depth output (want=False: "
+                           "none) are outside"}
     if ctl.ws == 1:
         blk["roofline"] = hbm_roofline(8.0 * m + 12.0 * n, ms, "direction-optimising BFS, one traversal "
                                        "(bfs_init_kernel + bfs_level_kernel launches)", workload,
@@ -308,10 +353,12 @@ def pagerank_block(jg, ctx, scale, ef, steps, warmup):
     g.pagerank_step(warmup)
     g.sync()
     ctx.set_profiling(True)
+    w0 = window_start()
     t0 = time.perf_counter()
     g.pagerank_step(steps)
     g.sync()
     dt = time.perf_counter() - t0
+    window_end(f"pagerank_fp64_rmat{scale}_ef{ef}", w0, steps)
     g.pagerank_end(want=False)
     st = ctx.stats()
     ctx.set_profiling(False)
@@ -349,7 +396,9 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     deg = both_degrees(jg, ctl, g)
     g.connected_components()  # warm
     ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
+    w0 = window_start()
     comp, it = g.connected_components()
+    window_end(f"cc_rmat{scale}_ef{ef}", w0)
     st = ctx.stats()
     ctx.set_profiling(False)
     cc_ms = ctl.max(st["compute_ms"])
@@ -359,6 +408,8 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     counts = np.bincount(comp, minlength=n)  # RMAT ids are 0..n-1: labels are vertex ids
     wl_cc = f"cc_rmat{scale}_ef{ef}"
     cc = {"workload": wl_cc, "ms": round(cc_ms, 3), "iterations": it,
+          "timed_region": "HIP events around the union-find passes and the superstep-count BFS; the label output "
+                          "(cc_output_kernel: rank labels to vertex ids, scattered to caller order) is outside",
           "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
           "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
                        "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"
@@ -380,12 +431,17 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
     del comp, counts, comp_edges
     g.bfs(srcs, jg.DIR_BOTH, want=False)  # warm
     ctx.set_profiling(ctl.ws > 1)
+    w0 = window_start()
     g.bfs(srcs, jg.DIR_BOTH, want=False)
+    window_end(f"msbfs64_rmat{scale}_ef{ef}", w0)
     st = ctx.stats()
     ctx.set_profiling(False)
     ms = ctl.max(st["compute_ms"])
     wl_ms = f"msbfs64_rmat{scale}_ef{ef}"
     msb = {"workload": wl_ms, "sources": int(len(srcs)), "ms": round(ms, 3), "levels": st["levels"],
+           "timed_region": "HIP events from the state fills to the last level; the sources' id lookup and the depth "
+                           "rows (want=False: not materialised; the per-level words are an exact encoding) are "
+                           "outside",
            "gteps": round(edges / (ms * 1e-3) / 1e9, 1),
            "gteps_note": "sum over the 64 sources (degree > 0) of the input edges in the source's component / time"}
     if ctl.ws == 1:
@@ -428,10 +484,12 @@ def main():
     g.sync()
     ctl.barrier()
     ctx.set_profiling(True)
+    w0 = window_start()
     t0 = time.perf_counter()
     g.pagerank_step(args.steps)
     g.sync()
     t1 = time.perf_counter()
+    window_end(f"pagerank_fp64_rmat{args.scale}_ef{args.edgefactor}", w0, args.steps)
     ctl.barrier()
     elapsed = ctl.max(t1 - t0)
     g.pagerank_end(want=False)
@@ -498,6 +556,8 @@ def main():
         if per_rank is not None:
             line["per_rank"] = per_rank
         line.update(extra)
+        if args.trace_windows:
+            line["trace_windows"] = {"clock": "CLOCK_MONOTONIC ns", "windows": WINDOWS}
         print(json.dumps(line), flush=True)
     ctx.close()
     ctl.close()

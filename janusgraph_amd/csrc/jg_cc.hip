@@ -980,6 +980,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     }
     for (auto& sp : g.shards) JG_HIP(hipStreamSynchronize(sp->stream));
     prof_discard_exchanges(g);  // exchange pairs count from t0 on only
+    region_mark(sh0.stream, true);
     JG_HIP(hipEventRecord(t0, sh0.stream));
     int iteration = 0, cur = 0;
     // one shard: supersteps whose senders have few edges run push-style
@@ -1082,6 +1083,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         cur ^= 1;
     }
     JG_HIP(hipEventRecord(t1, sh0.stream));
+    region_mark(sh0.stream, false);
     JG_HIP(hipEventSynchronize(t1));
     float ms = 0;
     JG_HIP(hipEventElapsedTime(&ms, t0, t1));

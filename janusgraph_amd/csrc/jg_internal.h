@@ -527,6 +527,8 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
 int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);
 // Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
 void bfs_buffers(Shard& sh);
+// JG_TRACE_MARKS=1: an empty named dispatch before a program's t0 / after its t1 (tools/bench_trace.py)
+void region_mark(hipStream_t s, bool begin);
 // Narrow bit-parallel direction-optimising BFS (jg_narrow.hip): 2..kNarrowMax sources on one shard,
 // one frontier byte per row, each source choosing its own direction every level.  push / pull: the
 // traversal's adjacencies (both present); src[s]: source s's local row (-1: not a vertex).  planes

@@ -1478,6 +1478,22 @@ uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ?
 
 // The single-shard traversal's scratch, kept with the shard (callers allocate it before their timed
 // region: a first call would otherwise time ~1 ms of allocations at RMAT-26).
+// Trace markers (JG_TRACE_MARKS=1): an empty dispatch just before a program's t0 event and just after its
+// t1 event, so tools/bench_trace.py cuts a rocprofv3 kernel trace of the bench process to exactly the
+// event-timed regions.  Unset: no launch.
+__global__ void region_begin_kernel() {}
+__global__ void region_end_kernel() {}
+void region_mark(hipStream_t s, bool begin) {
+    static const bool on = [] {
+        const char* e = std::getenv("JG_TRACE_MARKS");
+        return e && std::atoi(e) != 0;
+    }();
+    if (!on) return;
+    if (begin) region_begin_kernel<<<1, kWave, 0, s>>>();
+    else region_end_kernel<<<1, kWave, 0, s>>>();
+    JG_LAUNCH_CHECK();
+}
+
 void bfs_buffers(Shard& sh) {
     const int64_t rows = sh.rows;
     const int64_t words = (rows + 63) / 64;
@@ -1495,8 +1511,10 @@ void bfs_buffers(Shard& sh) {
 
 namespace {
 
+// end_ev (nullable) is recorded behind the last level launch, before the host reads the final state:
+// the traversal's GPU span ends there (the state read-back is the host's control, not traversal work)
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out, const CcRoots* roots = nullptr) {
+                 double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr* push = c.push;
@@ -1577,6 +1595,10 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         p.split_levels = split_levels;
         bfs_persistent_kernel<<<pg, kBlock, 0, s>>>(a, p);
         JG_LAUNCH_CHECK();
+        if (end_ev) {
+            JG_HIP(hipEventRecord(end_ev, s));
+            region_mark(s, false);
+        }
         unsigned abort_word = 0;
         copy_d2h(&abort_word, sh.bfs_sync.get() + kSyncAbort * sizeof(unsigned), sizeof abort_word, s);
         if (abort_word) fail(JG_ERR_STATE, "persistent BFS: grid barrier timed out (grid not co-resident)");
@@ -1622,6 +1644,10 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
                 std::fprintf(stderr, "[jg bfs] level %d %s done %d next frontier %llu vertices %llu edges\n", level,
                              ds.bottom_up ? "bottom-up" : "top-down", ds.done, dc >> kPackShift, dc & kEdgeMask);
             }
+        }
+        if (end_ev) {
+            JG_HIP(hipEventRecord(end_ev, s));
+            region_mark(s, false);
         }
         copy_d2h(&hs, st + (level - 1) % kBfsRing, sizeof hs, s);
         if (hs.done) break;
@@ -2001,6 +2027,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             DeviceGuard dgs(*sp);
             JG_HIP(hipStreamSynchronize(sp->stream));  // the plan copies above; t0 marks the traversal's start
         }
+        region_mark(sh0.stream, true);
         JG_HIP(hipEventRecord(t0, sh0.stream));
     }
     for (size_t i = 0; i < ns; ++i) {
@@ -2165,6 +2192,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     {
         DeviceGuard dg(sh0.device);
         JG_HIP(hipEventRecord(t1, sh0.stream));
+        region_mark(sh0.stream, false);
         JG_HIP(hipEventSynchronize(t1));
         JG_HIP(hipEventElapsedTime(ms_out, t0, t1));
         JG_HIP(hipEventDestroy(t0));
@@ -2329,9 +2357,9 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventRecord(t1, sh.stream));
         } else {
             bfs_buffers(sh);
+            region_mark(sh.stream, true);
             JG_HIP(hipEventRecord(t0, sh.stream));
-            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges);
-            JG_HIP(hipEventRecord(t1, sh.stream));
+            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1);
         }
         JG_HIP(hipEventSynchronize(t1));
         float ms = 0;
@@ -2585,6 +2613,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 }
             }
             prof_discard_exchanges(g);  // exchange pairs never straddle t0
+            region_mark(sh0.stream, true);
             JG_HIP(hipEventRecord(t0, sh0.stream));
             // the call's state, inside the timed region: frontiers, visited bits, the halo staging, the
             // sources (and level 0's depth record)
@@ -3137,6 +3166,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 if (!any) break;
             }
             JG_HIP(hipEventRecord(t1, sh0.stream));
+            region_mark(sh0.stream, false);
             JG_HIP(hipEventSynchronize(t1));
             float ms = 0;
             JG_HIP(hipEventElapsedTime(&ms, t0, t1));
@@ -3258,6 +3288,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         DeviceGuard dg(sh0.device);
         JG_HIP(hipEventCreate(&t0));
         JG_HIP(hipEventCreate(&t1));
+        region_mark(sh0.stream, true);
         JG_HIP(hipEventRecord(t0, sh0.stream));
     }
     int levels = 0;
@@ -3315,6 +3346,7 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     {
         DeviceGuard dg(sh0.device);
         JG_HIP(hipEventRecord(t1, sh0.stream));
+        region_mark(sh0.stream, false);
         JG_HIP(hipEventSynchronize(t1));
         JG_HIP(hipEventElapsedTime(&ms, t0, t1));
         (void)hipEventDestroy(t0);
@@ -3355,6 +3387,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
     if (seed >= 0 && !g.has_weights) bfs_buffers(sh);
+    region_mark(s, true);
     JG_HIP(hipEventRecord(t0, s));
     int levels = 0;
     if (seed >= 0 && !g.has_weights) {
@@ -3411,6 +3444,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         if (e) fail(JG_ERR_ARG, kMissingWeight);
     }
     JG_HIP(hipEventRecord(t1, s));
+    region_mark(s, false);
     JG_HIP(hipEventSynchronize(t1));
     float ms = 0;
     JG_HIP(hipEventElapsedTime(&ms, t0, t1));

@@ -1,7 +1,12 @@
 """bench.py host helpers (CPU): the CPU-baseline leg, the PMC traffic lookup and the source pick."""
+import os
+
 import numpy as np
+import pytest
 
 import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_cpu_baseline_small():
@@ -41,3 +46,40 @@ def test_per_rank_rows_flag_exchange_beyond_compute():
     assert not any("timing_suspect" in r for r in rows)
     bad = bench.per_rank_rows([[936.9, 1302.0]])
     assert "timing_suspect" in bad[0]
+
+
+def test_bench_trace_cuts_windows_at_the_markers(tmp_path):
+    """tools/bench_trace.py: a window's dispatches outside the library's region markers (id lookups,
+    argument copies, output kernels) do not count; the span runs from the begin mark to the last end mark
+    (the DO-BFS marks the end of every level batch); a window without marks counts whole."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    us = 1000
+    rows = [("id_lookup_kernel", 0, 2), ("jg::region_begin_kernel()", 3, 4), ("bfs_init_kernel", 5, 8),
+            ("bfs_level_kernel", 9, 19), ("jg::region_end_kernel()", 20, 21), ("copyBuffer", 22, 24),
+            ("bfs_level_kernel", 25, 30), ("jg::region_end_kernel()", 31, 32), ("cc_output_kernel", 33, 90),
+            ("pull_merge_kernel", 100, 110), ("pull_light_finalize_kernel", 111, 120),
+            ("pull_merge_kernel", 121, 131), ("pull_light_finalize_kernel", 132, 140)]
+    with open(tmp_path / "b_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for n, s, e in rows:
+            w.writerow([n, s * us, e * us])
+    line = {"metric": "m", "ms_per_step": 0.02, "config": {"workload": "pr"},
+            "roofline": {"kernel_ms": 0.02, "bytes_per_launch": 8e6},
+            "bfs": {"workload": "bfs", "ms_median": 0.025, "roofline": {"bytes_per_launch": 1e6}},
+            "trace_windows": {"windows": [["bfs", 0, 95 * us, 1], ["pr", 99 * us, 141 * us, 2]]}}
+    (tmp_path / "b.json").write_text(json.dumps(line) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_trace.py"), str(tmp_path), "b",
+                          str(tmp_path / "b.json")], capture_output=True, text=True, check=True).stdout
+    blk = json.loads(out)["blocks"]
+    b = blk["bfs"]
+    assert b["marked"] and b["dispatches_per_run"] == 4  # init, two levels, the copy between batches
+    assert b["trace_span_ms"] == pytest.approx(0.025)  # init start 5 -> last level end 30 us
+    assert b["trace_kernel_ms"] == pytest.approx((3 + 10 + 2 + 5) / 1000)
+    assert b["agree"]
+    p = blk["pr"]
+    assert not p["marked"] and p["dispatches_per_run"] == 2
+    assert p["trace_span_ms"] == pytest.approx(0.020) and p["within_step"]

@@ -9,6 +9,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -40,6 +41,7 @@ def main():
         if ctx.stats()["edges_traversed"] >= m // 100:
             srcs.append(sv)
     times = {s: {sv: [] for sv in srcs} for s in a.settings}
+    wall = {s: [] for s in a.settings}  # host wall time of the call (launches, read-backs, no depth output)
     levels = {}
     for _ in range(a.rounds):
         for s in a.settings:
@@ -48,13 +50,16 @@ def main():
                 jg._lib.tune_set(k, v)
             for sv in srcs:
                 g.bfs([sv], jg.DIR_BOTH, want=False)  # warm (the bench drops the first run too)
+                t = time.perf_counter()
                 g.bfs([sv], jg.DIR_BOTH, want=False)
+                wall[s].append((time.perf_counter() - t) * 1e3)
                 st = ctx.stats()
                 times[s][sv].append(st["compute_ms"])
                 levels[sv] = st["levels"]
     for s in a.settings:
         allv = [x for v in times[s].values() for x in v]
         print(json.dumps({"setting": s, "scale": a.scale, "ms_median": round(float(np.median(allv)), 4),
+                          "wall_ms_median": round(float(np.median(wall[s])), 4),
                           "per_source": {str(sv): round(float(np.median(v)), 4) for sv, v in times[s].items()},
                           "levels": {str(sv): levels[sv] for sv in srcs}}), flush=True)
     g.close()
