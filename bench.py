@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-big", action="store_true", help="skip the RMAT-26 blocks (PageRank, BFS, CC, MS-BFS)")
     p.add_argument("--big-scale", type=int, default=26)
     p.add_argument("--big-steps", type=int, default=10)
+    p.add_argument("--cc-plan", choices=["replicated", "sharded"], default="replicated",
+                   help="N > 1: CC on a whole-graph copy per GPU (default) or over the ranks' shards")
     p.add_argument("--trace-windows", action="store_true",
                    help="add the timed regions' host-clock windows to the JSON line (tools/bench_trace.py)")
     p.add_argument("--host-transport", action="store_true",
@@ -386,24 +388,34 @@ def required_roofline(m, live, ms):
             "frac": round(a / HBM_PEAK_GBS, 4)}
 
 
-def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
+def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
     """CC (configs[3]) and 64-source MS-BFS (configs[4]) on the BOTH adjacency.  N > 1: every rank holds
-    its shard; CC runs local union-finds with tree labels over the halo and a multi-root sharded DO-BFS
-    (jg_cc.hip cc_union_find_sharded), MS-BFS the sharded bit-parallel levels."""
+    its shard and MS-BFS runs the sharded bit-parallel levels; CC runs replicated: every GPU builds the
+    whole BOTH graph (9 GB of 288 GB at RMAT-26) and runs the one-GPU union-find, because the sharded CC
+    (local union-finds, tree labels over the halo, a multi-root sharded DO-BFS: jg_cc.hip
+    cc_union_find_sharded) models below one GPU's time at P = 8."""
     n, m = 1 << scale, ef << scale
     g = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
     build_ms = ctx.stats()["build_ms"]
     deg = both_degrees(jg, ctl, g)
-    g.connected_components()  # warm
-    ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
+    cctx, cg = ctx, g
+    replicated = ctl.ws > 1 and cc_plan == "replicated"
+    if replicated:
+        cctx = jg.Context((local,))
+        cg = cctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
+    cg.connected_components()  # warm
+    cctx.set_profiling(ctl.ws > 1 and not replicated)  # sharded: exchange_ms from events around every exchange
     w0 = window_start()
-    comp, it = g.connected_components()
+    comp, it = cg.connected_components()
     window_end(f"cc_rmat{scale}_ef{ef}", w0)
-    st = ctx.stats()
-    ctx.set_profiling(False)
+    st = cctx.stats()
+    cctx.set_profiling(False)
     cc_ms = ctl.max(st["compute_ms"])
     cc_rank = ctl.gather([st["compute_ms"], st["exchange_ms"]])
-    if ctl.ws > 1:
+    if replicated:
+        cg.close()
+        cctx.close()
+    elif ctl.ws > 1:
         comp = ctl.min_array(comp)  # each rank filled its own rows (the others hold INT64_MAX)
     counts = np.bincount(comp, minlength=n)  # RMAT ids are 0..n-1: labels are vertex ids
     wl_cc = f"cc_rmat{scale}_ef{ef}"
@@ -413,9 +425,12 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef):
           "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
           "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
                        "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"
-          if ctl.ws == 1 else "sharded: local Afforest union-finds, tree labels over forward and reverse halo "
-                              "exchanges, one multi-root sharded DO-BFS for the superstep count "
-                              "(jg_cc.hip cc_union_find_sharded)"}
+          if ctl.ws == 1 else "replicated: every GPU holds the whole BOTH graph and runs the one-GPU union-find "
+                              "+ DO-BFS (the sharded cc_union_find_sharded models at 0.85-0.9x of one GPU at P = 8, "
+                              "DESIGN.md section 7)" if replicated else
+                              "sharded: local Afforest union-finds, tree labels over forward and reverse halo "
+                              "exchanges (pairs of the labels that fell after the first rounds), one multi-root "
+                              "sharded DO-BFS for the superstep count (jg_cc.hip cc_union_find_sharded)"}
     if ctl.ws == 1:
         cc["roofline"] = hbm_roofline(st["algorithmic_bytes"], cc_ms, "ConnectedComponent run (uf_* kernels + "
                                       "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
@@ -532,7 +547,8 @@ def main():
         if ws == 1:
             blk["pagerank"] = pagerank_block(jg, ctx, big, args.edgefactor, args.big_steps, 3)
         blk["bfs"] = bfs_block(jg, ctx, ctl, big, args.edgefactor, nsrc=4, cpu=False)
-        blk["cc"], blk["msbfs64"] = rmat26_both_blocks(jg, ctx, ctl, big, args.edgefactor)
+        blk["cc"], blk["msbfs64"] = rmat26_both_blocks(jg, ctx, ctl, big, args.edgefactor,
+                                                       0 if args.host_transport else local, args.cc_plan)
         extra[f"rmat{big}"] = blk
 
     cpu = None

@@ -661,6 +661,7 @@ int jg_tune_set(const char* key, int64_t value) {
         {"cc_uf", &t.cc_uf, 0, 1},
         {"cc_uf_sharded", &t.cc_uf_sharded, 0, 1},
         {"cc_uf_search", &t.cc_uf_search, 0, 1},
+        {"cc_sparse", &t.cc_sparse, 0, 1},
         {"msbfs_split", &t.msbfs_split, 0, 1},
         {"sharded_bfs", &t.sharded_bfs, 0, 1},
         {"bfs_td_split", &t.bfs_td_split, 0, 2},
@@ -669,8 +670,7 @@ int jg_tune_set(const char* key, int64_t value) {
         {"bfs_grid_mult", &t.bfs_grid_mult, 1, 64},
         {"bfs_grid", &t.bfs_grid, 64, 65536},
         {"bfs_tail_grid", &t.bfs_tail_grid, 0, 65536},
-        {"bfs_persistent", &t.bfs_persistent, 0, 1},
-        {"bfs_persistent_grid", &t.bfs_persistent_grid, 0, 8192},
+        {"bfs_persistent", &t.bfs_persistent, 0, 8192},
         {"merge_temporal", &t.merge_temporal, 0, 2},
     };
     for (const Knob& kn : knobs) {

@@ -511,19 +511,22 @@ __global__ __launch_bounds__(kBlock) void cc_pack_flags_kernel(const int32_t* __
     }
 }
 
-// the bounded search: kCcSearchEntries entries of each of the first kCcSearchRows giant rows (a wave
-// each) link the flagged copies they meet and mark their segments found
+// the bounded search: kCcSearchEntries entries of each of the first kCcSearchRows giant rows (kCcSearchSplit
+// waves each, every lane a few entries: one wave per row walked 32 dependent col -> flag -> link steps,
+// 114 us per shard at RMAT-26, P = 8) link the flagged copies they meet and mark their segments found
+constexpr int kCcSearchSplit = 8;
 __global__ __launch_bounds__(kBlock) void cc_giant_search_kernel(CcShardLink a) {
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int64_t row = wave / kCcSearchSplit, part = wave % kCcSearchSplit;
     const int64_t nr = a.ne < kCcSearchRows ? a.ne : kCcSearchRows;
-    if (wave >= nr || !flag_of(a.flag, (int32_t)wave)) return;
+    if (row >= nr || !flag_of(a.flag, (int32_t)row)) return;
     // kCcSearchEntries entries spread evenly over the row (its columns may be ordered by segment)
-    const int64_t e0 = a.rp[wave], deg = a.rp[wave + 1] - e0;
+    const int64_t e0 = a.rp[row], deg = a.rp[row + 1] - e0;
     const int64_t n = deg < kCcSearchEntries ? deg : kCcSearchEntries;
-    for (int64_t j = lane_id(); j < n; j += kWave) {
+    for (int64_t j = part * kWave + lane_id(); j < n; j += kWave * kCcSearchSplit) {
         const int32_t u = a.col[e0 + j * deg / n];
         if (u >= a.rows && flag_of(a.flag, u)) {
-            uf_link(a.parent, (int32_t)wave, u);
+            uf_link(a.parent, (int32_t)row, u);
             a.found[u >> a.tbits] = 1;
         }
     }
@@ -585,39 +588,300 @@ __global__ __launch_bounds__(kRedThreads) void cc_tree_min_kernel(SlotMap sm, co
     if (threadIdx.x == 0 && g != INT_MAX && giant >= 0) atomicMin(&tmin[giant], g);
 }
 
-// own rows with an edge take their tree's minimum (labels only decrease); copies take it too, for the
-// reverse exchange
-__global__ void cc_tree_apply_kernel(SlotMap sm, const int32_t* __restrict__ parent, int32_t* __restrict__ tmin,
-                                     int32_t* __restrict__ label, int32_t* __restrict__ msg,
-                                     int32_t* __restrict__ changed) {
-    bool ch = false;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < sm.total; j += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = sm.pos(j);
-        const int32_t t = tmin[parent[x]];
-        if (j < sm.ne) {
-            if (t < label[x]) {
-                label[x] = t;
-                ch = true;
+__device__ __forceinline__ bool bit_at(const unsigned long long* b, int64_t i) { return (b[i >> 6] >> (i & 63)) & 1ull; }
+
+// Counters of rows whose label fell: kFellLines counters on lines of their own, a block adds its sum to
+// counter (block mod kFellLines) (one counter for every wave of the grid cost ~40-100 us per launch in
+// same-address atomics); the host sums them.  Every thread of the block calls this.
+constexpr int kFellLines = 64, kFellStride = 16;
+__device__ __forceinline__ void add_fell(unsigned long long* ctr, unsigned long long c) {
+    __shared__ unsigned long long s;
+    if (threadIdx.x == 0) s = 0;
+    __syncthreads();
+    if (c) atomicAdd(&s, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && s) atomicAdd(&ctr[(blockIdx.x % kFellLines) * kFellStride], s);
+}
+__device__ __forceinline__ void set_bit_at(unsigned long long* b, int64_t i) {
+    const unsigned long long m = 1ull << (i & 63);
+    if (!(b[i >> 6] & m)) atomicOr(&b[i >> 6], m);
+}
+
+// own rows with an edge take their tree's minimum (labels only decrease; a row whose label fell is
+// marked in `dirty` for the next round's sparse forward); copies take it too, for the reverse exchange
+// (A wave's 64 consecutive slots below ne are one aligned dirty word: the wave's ballot, ORed in by one
+// lane; no other wave of the launch touches that word.)  nchg += own rows whose label fell.
+__global__ __launch_bounds__(kBlock) void cc_tree_apply_kernel(SlotMap sm, const int32_t* __restrict__ parent,
+                                                                int32_t* __restrict__ tmin, int32_t* __restrict__ label,
+                                                                int32_t* __restrict__ msg, int32_t* __restrict__ changed,
+                                                                unsigned long long* __restrict__ dirty,
+                                                                unsigned long long* __restrict__ nchg) {
+    unsigned long long cnt = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + wave_id() * kWave; j0 < sm.total; j0 += stride) {  // wave-uniform
+        const int64_t j = j0 + lane_id();
+        bool fell = false;
+        if (j < sm.total) {
+            const int64_t x = sm.pos(j);
+            const int32_t t = tmin[parent[x]];
+            if (j < sm.ne) {
+                if (t < label[x]) {
+                    label[x] = t;
+                    fell = true;
+                }
+            } else {
+                msg[x] = t;
             }
-        } else {
-            msg[x] = t;
+        }
+        const unsigned long long m = __ballot(fell);
+        if (m && lane_id() == 0) {
+            // j0 is 64-aligned and below ne wherever a bit is set; the word is zero (cleared for this
+            // round, no other wave writes it, the reverse apply runs after): a plain store, no read
+            dirty[j0 >> 6] = m;
+            cnt += (unsigned long long)__popcll(m);
         }
     }
-    if (__ballot(ch) && lane_id() == 0) *changed = 1;
+    if (lane_id() == 0 && cnt) *changed = 1;
+    add_fell(nchg, cnt);
 }
 
 // the copies' tree minima back at the owners (element j is about own row send_src[j])
 __global__ void cc_reverse_apply_kernel(const int32_t* __restrict__ rbuf, const int32_t* __restrict__ send_src, int64_t n,
-                                        int32_t* __restrict__ label, int32_t* __restrict__ changed) {
-    bool ch = false;
+                                        int32_t* __restrict__ label, int32_t* __restrict__ changed,
+                                        unsigned long long* __restrict__ dirty, unsigned long long* __restrict__ nchg) {
+    unsigned long long cnt = 0;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const int32_t v = send_src[j], m = rbuf[j];
-        if (m < label[v]) {
-            atomicMin(&label[v], m);
-            ch = true;
+        if (m < label[v]) {  // non-returning atomics (a returning one stalls the lane on every changed row);
+            atomicMin(&label[v], m);  // a row lowered by two elements is counted twice (the count only has to
+            atomicOr(&dirty[v >> 6], 1ull << (v & 63));  // be non-zero exactly when something fell)
+            ++cnt;
         }
     }
-    if (__ballot(ch) && lane_id() == 0) *changed = 1;
+    if (__ballot(cnt != 0) && lane_id() == 0) *changed = 1;
+    add_fell(nchg, cnt);
+}
+
+// ---- sparse label rounds (cc_sparse) ----
+// After the first round a label only moves when it fell in the previous one.  Own rows whose label fell
+// are marked in `dirty` (the apply and the reverse apply above and below); the next round sends only
+// their send-list entries, as (offset in the run to the peer) << 32 | label pairs (forward), feeds only
+// them and the received copies into the tree minima (marking each root whose minimum fell in `rootb`),
+// applies only the slots of those roots, and sends back only the copies whose minimum fell (reverse
+// pairs, `cb` marks them).  A direction goes dense when its pairs over all shards are at least half the
+// dense run (a pair is two int32 elements).  Unchanged values change no minimum, so the rounds, their
+// count and the labels are the dense rounds' exactly.
+constexpr int kMaxPeersCc = 64;
+
+// peer of send-list element j (offsets in LDS)
+__device__ __forceinline__ int run_peer(const int64_t* off, int P, int64_t j) {
+    int q = 0;
+    while (q + 1 < P && off[q + 1] <= j) ++q;
+    return q;
+}
+// the peer whose run sits in segment s of shard r's compact vector (inverse of Halo::seg_of)
+__device__ __forceinline__ int seg_peer(int s, int r) { return s <= r ? s - 1 : s; }
+
+// pass 1 of a forward: dirty send-list elements per peer (pcnt[q] +=)
+__global__ __launch_bounds__(kBlock) void cc_fwd_count_kernel(const int32_t* __restrict__ send_src,
+                                                               const int64_t* __restrict__ send_off, int P,
+                                                               const unsigned long long* __restrict__ dirty,
+                                                               unsigned long long* __restrict__ pcnt) {
+    __shared__ int64_t so[kMaxPeersCc + 1];
+    __shared__ unsigned int lc[kMaxPeersCc];
+    for (int q = threadIdx.x; q <= P; q += blockDim.x) so[q] = send_off[q];
+    for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+    __syncthreads();
+    const int64_t n = so[P];
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        if (bit_at(dirty, send_src[j])) atomicAdd(&lc[run_peer(so, P, j)], 1u);
+    __syncthreads();
+    for (int q = threadIdx.x; q < P; q += blockDim.x)
+        if (lc[q]) atomicAdd(&pcnt[q], (unsigned long long)lc[q]);
+}
+
+// pass 2: the pairs, grouped by peer at pbase[q] (order inside a group: any)
+__global__ __launch_bounds__(kBlock) void cc_fwd_pack_kernel(const int32_t* __restrict__ send_src,
+                                                              const int64_t* __restrict__ send_off, int P,
+                                                              const unsigned long long* __restrict__ dirty,
+                                                              const int32_t* __restrict__ label,
+                                                              const int64_t* __restrict__ pbase,
+                                                              unsigned long long* __restrict__ cursor,
+                                                              unsigned long long* __restrict__ pairs) {
+    __shared__ int64_t so[kMaxPeersCc + 1];
+    __shared__ unsigned int lc[kMaxPeersCc];
+    __shared__ int64_t gb[kMaxPeersCc];
+    for (int q = threadIdx.x; q <= P; q += blockDim.x) so[q] = send_off[q];
+    __syncthreads();
+    const int64_t n = so[P];
+    // one tile of blockDim elements per trip (block-uniform trips): LDS counters rank the tile's pairs per
+    // peer, one global add per (tile, peer) reserves their slots (a global add per pair serialised on the
+    // P cursors: 1.4 ms for 126 K pairs)
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
+        for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+        __syncthreads();
+        const int64_t j = j0 + threadIdx.x;
+        int q = -1;
+        unsigned int li = 0;
+        int32_t v = 0;
+        if (j < n) {
+            v = send_src[j];
+            if (bit_at(dirty, v)) {
+                q = run_peer(so, P, j);
+                li = atomicAdd(&lc[q], 1u);
+            }
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < P; x += blockDim.x)
+            gb[x] = lc[x] ? pbase[x] + (int64_t)atomicAdd(&cursor[x], (unsigned long long)lc[x]) : 0;
+        __syncthreads();
+        if (q >= 0) pairs[gb[q] + li] = ((unsigned long long)(j - so[q]) << 32) | (uint32_t)label[v];
+        __syncthreads();
+    }
+}
+
+// receiver of a forward: each pair's copy slot takes the owner's label and lowers its tree's minimum
+// (roff[q]: where sender q's pairs start)
+__global__ __launch_bounds__(kBlock) void cc_fwd_recv_kernel(const unsigned long long* __restrict__ rpairs,
+                                                              const int64_t* __restrict__ roff, int P, int r, int tbits,
+                                                              const int32_t* __restrict__ parent,
+                                                              int32_t* __restrict__ msg, int32_t* __restrict__ tmin,
+                                                              unsigned long long* __restrict__ rootb) {
+    __shared__ int64_t ro[kMaxPeersCc + 1];
+    for (int q = threadIdx.x; q <= P; q += blockDim.x) ro[q] = roff[q];
+    __syncthreads();
+    const int64_t n = ro[P];
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int q = run_peer(ro, P, k);
+        const unsigned long long p = rpairs[k];
+        const int32_t val = (int32_t)(uint32_t)p;
+        const int64_t x = ((int64_t)(q < r ? q + 1 : q) << tbits) + (int64_t)(p >> 32);
+        msg[x] = val;
+        const int32_t root = parent[x];
+        if (val < tmin[root] && val < atomicMin(&tmin[root], val)) set_bit_at(rootb, root);
+    }
+}
+
+// own rows whose label fell last round lower their tree's minimum
+__global__ void cc_own_tree_min_kernel(const unsigned long long* __restrict__ dirty, int64_t ne,
+                                       const int32_t* __restrict__ label, const int32_t* __restrict__ parent,
+                                       int32_t* __restrict__ tmin, unsigned long long* __restrict__ rootb) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < ne; v += (int64_t)gridDim.x * blockDim.x) {
+        if (!bit_at(dirty, v)) continue;
+        const int32_t val = label[v], root = parent[v];
+        if (val < tmin[root] && val < atomicMin(&tmin[root], val)) set_bit_at(rootb, root);
+    }
+}
+
+// the slots of roots whose minimum fell: own rows take it (dirty), copies take it when it is lower (cb,
+// counted per peer for the reverse pairs)
+__global__ __launch_bounds__(kBlock) void cc_apply_sparse_kernel(SlotMap sm, const int32_t* __restrict__ parent,
+                                                                  const int32_t* __restrict__ tmin,
+                                                                  const unsigned long long* __restrict__ rootb,
+                                                                  int32_t* __restrict__ label, int32_t* __restrict__ msg,
+                                                                  unsigned long long* __restrict__ dirty,
+                                                                  unsigned long long* __restrict__ cb, int r, int P,
+                                                                  int tbits, unsigned long long* __restrict__ pcnt,
+                                                                  int32_t* __restrict__ changed,
+                                                                  unsigned long long* __restrict__ nchg) {
+    __shared__ unsigned int lc[kMaxPeersCc];
+    for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+    __syncthreads();
+    unsigned long long cnt = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + wave_id() * kWave; j0 < sm.total; j0 += stride) {  // wave-uniform
+        const int64_t j = j0 + lane_id();
+        bool fell = false;
+        if (j < sm.total) {
+            const int64_t x = sm.pos(j);
+            const int32_t root = parent[x];
+            if (bit_at(rootb, root)) {
+                const int32_t t = tmin[root];
+                if (j < sm.ne) {
+                    if (t < label[x]) {
+                        label[x] = t;
+                        fell = true;
+                    }
+                } else if (t < msg[x]) {
+                    msg[x] = t;
+                    set_bit_at(cb, x);
+                    atomicAdd(&lc[seg_peer((int)(x >> tbits), r)], 1u);
+                }
+            }
+        }
+        const unsigned long long m = __ballot(fell);
+        if (m && lane_id() == 0) {
+            dirty[j0 >> 6] = m;  // as in cc_tree_apply_kernel
+            cnt += (unsigned long long)__popcll(m);
+        }
+    }
+    if (lane_id() == 0 && cnt) *changed = 1;
+    add_fell(nchg, cnt);
+    __syncthreads();
+    for (int q = threadIdx.x; q < P; q += blockDim.x)
+        if (lc[q]) atomicAdd(&pcnt[q], (unsigned long long)lc[q]);
+}
+
+// the reverse pairs: marked copies, grouped by owner at pbase[q]
+__global__ __launch_bounds__(kBlock) void cc_rev_pack_kernel(SlotMap sm, const unsigned long long* __restrict__ cb,
+                                                              const int32_t* __restrict__ msg, int r, int P, int tbits,
+                                                              const int64_t* __restrict__ pbase,
+                                                              unsigned long long* __restrict__ cursor,
+                                                              unsigned long long* __restrict__ pairs) {
+    __shared__ unsigned int lc[kMaxPeersCc];
+    __shared__ int64_t gb[kMaxPeersCc];
+    for (int64_t j0 = sm.ne + (int64_t)blockIdx.x * blockDim.x; j0 < sm.total; j0 += (int64_t)gridDim.x * blockDim.x) {
+        for (int q = threadIdx.x; q < P; q += blockDim.x) lc[q] = 0u;
+        __syncthreads();
+        const int64_t j = j0 + threadIdx.x;
+        int q = -1;
+        unsigned int li = 0;
+        int64_t x = 0;
+        if (j < sm.total) {
+            x = sm.pos(j);
+            if (bit_at(cb, x)) {
+                q = seg_peer((int)(x >> tbits), r);
+                li = atomicAdd(&lc[q], 1u);
+            }
+        }
+        __syncthreads();
+        for (int y = threadIdx.x; y < P; y += blockDim.x)
+            gb[y] = lc[y] ? pbase[y] + (int64_t)atomicAdd(&cursor[y], (unsigned long long)lc[y]) : 0;
+        __syncthreads();
+        if (q >= 0) {
+            const int64_t s0 = (x >> tbits) << tbits;
+            pairs[gb[q] + li] = ((unsigned long long)(x - s0) << 32) | (uint32_t)msg[x];
+        }
+        __syncthreads();
+    }
+}
+
+// the owner's side of the reverse pairs (sender q's pairs at roff[q]; its run offset names own row
+// send_src[send_off[q] + offset])
+__global__ __launch_bounds__(kBlock) void cc_rev_recv_kernel(const unsigned long long* __restrict__ rpairs,
+                                                              const int64_t* __restrict__ roff, int P,
+                                                              const int32_t* __restrict__ send_src,
+                                                              const int64_t* __restrict__ send_off,
+                                                              int32_t* __restrict__ label,
+                                                              unsigned long long* __restrict__ dirty,
+                                                              int32_t* __restrict__ changed,
+                                                              unsigned long long* __restrict__ nchg) {
+    __shared__ int64_t ro[kMaxPeersCc + 1];
+    for (int q = threadIdx.x; q <= P; q += blockDim.x) ro[q] = roff[q];
+    __syncthreads();
+    const int64_t n = ro[P];
+    unsigned long long cnt = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int q = run_peer(ro, P, k);
+        const unsigned long long p = rpairs[k];
+        const int32_t val = (int32_t)(uint32_t)p, v = send_src[send_off[q] + (int64_t)(p >> 32)];
+        if (val < label[v] && val < atomicMin(&label[v], val)) {
+            set_bit_at(dirty, v);
+            ++cnt;
+        }
+    }
+    if (__ballot(cnt != 0) && lane_id() == 0) *changed = 1;
+    add_fell(nchg, cnt);
 }
 
 // Every shard of the process (halo plans; cc_label holds the ranks).  false (labels untouched, message
@@ -631,6 +895,12 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         DevBuf<int64_t> send_off, woff;
         DevBuf<unsigned long long> flag, sw;
         DevBuf<unsigned long long> linked;  // [1] entries scanned by the second round (on the shard's device)
+        // sparse rounds: own rows whose label fell (this round's / the last round's), roots whose minimum
+        // fell, copies whose value fell; per-peer pair counts [2P] (forward, reverse) and cursors [P];
+        // the pair buffers and their per-peer offsets (pbase: send, roffd: receive)
+        DevBuf<unsigned long long> dirty[2], rootb, cb, pcnt, cursor, spairs, rpairs;
+        DevBuf<unsigned long long> nchg;  // [kFellLines * kFellStride] own rows whose label fell this round
+        DevBuf<int64_t> pbase, roffd;
         int64_t ne = 0, len = 0, heavy = 0, nsend = 0;
         int32_t giant = -1;
         int giant_share = 0, all_found = 0;
@@ -741,7 +1011,8 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         St& t = st[i];
         if (t.ne == 0) continue;
         if (tune().cc_uf_search) {  // 0: every peer takes the fallback (a parity-test variant)
-            cc_giant_search_kernel<<<(kCcSearchRows * kWave + kBlock - 1) / kBlock, kBlock, 0, s>>>(link_args(i));
+            cc_giant_search_kernel<<<(kCcSearchRows * kCcSearchSplit * kWave + kBlock - 1) / kBlock, kBlock, 0, s>>>(
+                link_args(i));
             JG_LAUNCH_CHECK();
         }
         std::vector<int32_t> found((size_t)P);
@@ -762,24 +1033,162 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         mv.push_back(g.shards[i]->cc_msg[0].peer());
         rv.push_back(st[i].rbuf.peer());
     }
-    int rounds = 0;
-    for (bool any = true; any;) {
-        ++rounds;
-        for (size_t i = 0; i < ns; ++i) {  // own labels into the message vector's own part
+    for (size_t i = 0; i < ns; ++i) {  // the sparse rounds' marks and counters
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh);
+        St& t = st[i];
+        for (int k = 0; k < 2; ++k) {
+            t.dirty[k].alloc((size_t)std::max<int64_t>((sh.rows + 63) / 64, 1));
+            JG_HIP(hipMemsetAsync(t.dirty[k].get(), 0, t.dirty[k].bytes(), sh.stream));
+        }
+        t.rootb.alloc((size_t)std::max<int64_t>((t.len + 63) / 64, 1));
+        t.cb.alloc((size_t)std::max<int64_t>((t.len + 63) / 64, 1));
+        JG_HIP(hipMemsetAsync(t.rootb.get(), 0, t.rootb.bytes(), sh.stream));
+        JG_HIP(hipMemsetAsync(t.cb.get(), 0, t.cb.bytes(), sh.stream));
+        t.pcnt.alloc(2 * (size_t)P);
+        t.nchg.alloc((size_t)kFellLines * kFellStride);
+        t.cursor.alloc((size_t)P);
+        t.pbase.alloc((size_t)P);
+        t.roffd.alloc((size_t)P + 1);
+    }
+    // One sparse exchange step (the pair counts are in pcnt + cofs per shard): the P x P count matrix
+    // and the dense volume are summed over ranks, so every rank takes the same decision; false = dense
+    // is cheaper (nothing sent).  pack(i) packs shard i's pairs, recv(i) consumes what it received.
+    int64_t dense_fwd = 0;  // elements of one dense exchange over all shards
+    for (size_t i = 0; i < ns; ++i) dense_fwd += st[i].nsend;
+    auto sparse_step = [&](int cofs, auto&& pack, auto&& recv) -> bool {
+        std::vector<std::vector<int64_t>> cnt(ns, std::vector<int64_t>((size_t)P, 0));
+        std::vector<int64_t> mat((size_t)P * P + 1, 0);
+        for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh);
-            if (st[i].ne)
-                JG_HIP(hipMemcpyAsync(sh.cc_msg[0].get(), st[i].label.get(), st[i].ne * sizeof(int32_t),
-                                      hipMemcpyDeviceToDevice, sh.stream));
+            std::vector<unsigned long long> c((size_t)P);
+            copy_d2h(c.data(), st[i].pcnt.get() + cofs, (size_t)P * sizeof(unsigned long long), sh.stream);
+            for (int q = 0; q < P; ++q) mat[(size_t)sh.index * P + q] = cnt[i][(size_t)q] = (int64_t)c[(size_t)q];
         }
-        exchange_msg(g, 0);
+        mat[(size_t)P * P] = dense_fwd;
+        allreduce_sum_i64(g, mat.data(), P * P + 1);
+        int64_t pairs_all = 0;
+        for (int64_t k = 0; k < (int64_t)P * P; ++k) pairs_all += mat[(size_t)k];
+        if (2 * pairs_all >= mat[(size_t)P * P]) return false;
+        std::vector<const char*> sp(ns);
+        std::vector<char*> rp(ns);
+        std::vector<std::vector<int64_t>> so(ns), sc(ns), ro(ns), rc(ns);
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh);
+            St& t = st[i];
+            so[i].assign((size_t)P + 1, 0);
+            ro[i].assign((size_t)P + 1, 0);
+            sc[i].assign((size_t)P, 0);
+            rc[i].assign((size_t)P, 0);
+            for (int q = 0; q < P; ++q) {
+                sc[i][(size_t)q] = cnt[i][(size_t)q];
+                rc[i][(size_t)q] = mat[(size_t)q * P + sh.index];
+                so[i][(size_t)q + 1] = so[i][(size_t)q] + sc[i][(size_t)q];
+                ro[i][(size_t)q + 1] = ro[i][(size_t)q] + rc[i][(size_t)q];
+            }
+            if ((int64_t)t.spairs.size() < std::max<int64_t>(so[i][(size_t)P], 1)) t.spairs.alloc(std::max<int64_t>(so[i][(size_t)P], 1));
+            if ((int64_t)t.rpairs.size() < std::max<int64_t>(ro[i][(size_t)P], 1)) t.rpairs.alloc(std::max<int64_t>(ro[i][(size_t)P], 1));
+            copy_h2d(t.pbase.get(), so[i].data(), (size_t)P * sizeof(int64_t), sh.stream);
+            copy_h2d(t.roffd.get(), ro[i].data(), ((size_t)P + 1) * sizeof(int64_t), sh.stream);
+            JG_HIP(hipMemsetAsync(t.cursor.get(), 0, (size_t)P * sizeof(unsigned long long), sh.stream));
+            if (so[i][(size_t)P] > 0) pack(i);
+            sp[i] = reinterpret_cast<const char*>(t.spairs.peer());
+            rp[i] = reinterpret_cast<char*>(t.rpairs.peer());
+        }
+        exchange_runs(g, sp, so, sc, rp, ro, rc, sizeof(unsigned long long), ncclUint64);
+        for (size_t i = 0; i < ns; ++i) {
+            Shard& sh = *g.shards[i];
+            DeviceGuard dg(sh);
+            if (ro[i][(size_t)P] > 0) recv(i, ro[i][(size_t)P]);
+        }
+        return true;
+    };
+    static const bool debug_rounds = std::getenv("JG_DEBUG_CC") != nullptr;
+    int64_t own_all = 0;  // own rows with an edge, all shards and ranks
+    for (size_t i = 0; i < ns; ++i) own_all += st[i].ne;
+    allreduce_sum_i64(g, &own_all, 1);
+    int64_t dense_all = dense_fwd;
+    allreduce_sum_i64(g, &dense_all, 1);
+    int64_t fell = 0;         // own rows whose label fell last round, all shards and ranks
+    int rounds = 0, cur = 0;  // dirty[cur]: own rows whose label fell last round
+    for (bool any = true; any;) {
+        ++rounds;
+        const int nxt = cur ^ 1;
+        bool fwd_sparse = false;
+        // a sparse forward is tried when the rows that fell, at the mean send-list fan-out, would make
+        // fewer pairs than half the dense run (the counts then decide; rounds 2-3 of RMAT move most labels)
+        const bool try_sparse = rounds > 1 && tune().cc_sparse && P <= kMaxPeersCc &&
+                                2.0 * (double)fell * (double)dense_all / (double)std::max<int64_t>(own_all, 1) <
+                                    (double)dense_all;
+        if (try_sparse) {
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                St& t = st[i];
+                JG_HIP(hipMemsetAsync(t.pcnt.get(), 0, 2 * (size_t)P * sizeof(unsigned long long), sh.stream));
+                if (t.nsend) {
+                    cc_fwd_count_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
+                        sh.halo_both.send_src.get(), t.send_off.get(), P, t.dirty[cur].get(), t.pcnt.get());
+                    JG_LAUNCH_CHECK();
+                }
+                bytes += 4.0 * (double)t.nsend;  // send_src (the dirty bits are 1/32 of it)
+            }
+            fwd_sparse = sparse_step(
+                0,
+                [&](size_t i) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    cc_fwd_pack_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
+                        sh.halo_both.send_src.get(), t.send_off.get(), P, t.dirty[cur].get(), t.label.get(), t.pbase.get(),
+                        t.cursor.get(), t.spairs.get());
+                    JG_LAUNCH_CHECK();
+                },
+                [&](size_t i, int64_t n) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    cc_fwd_recv_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(t.rpairs.get(), t.roffd.get(), P, sh.index,
+                                                                             sh.halo_both.tbits, sh.cc_msg[1].get(),
+                                                                             sh.cc_msg[0].get(), t.tmin.get(), t.rootb.get());
+                    JG_LAUNCH_CHECK();
+                    bytes += 24.0 * (double)n;  // pair, parent, msg, tmin
+                });
+        }
+        if (!fwd_sparse) {
+            for (size_t i = 0; i < ns; ++i) {  // own labels into the message vector's own part
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                if (st[i].ne)
+                    JG_HIP(hipMemcpyAsync(sh.cc_msg[0].get(), st[i].label.get(), st[i].ne * sizeof(int32_t),
+                                          hipMemcpyDeviceToDevice, sh.stream));
+            }
+            exchange_msg(g, 0);
+        }
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh);
             St& t = st[i];
             JG_HIP(hipMemsetAsync(sh.cc_changed.get(), 0, sizeof(int32_t), sh.stream));
+            JG_HIP(hipMemsetAsync(t.dirty[nxt].get(), 0, t.dirty[nxt].bytes(), sh.stream));
+            JG_HIP(hipMemsetAsync(t.nchg.get(), 0, t.nchg.bytes(), sh.stream));
+            if (!fwd_sparse) JG_HIP(hipMemsetAsync(t.pcnt.get(), 0, 2 * (size_t)P * sizeof(unsigned long long), sh.stream));
             if (t.ne == 0) continue;
             const unsigned grid = grid_for(t.sm.total);
+            if (fwd_sparse) {
+                cc_own_tree_min_kernel<<<grid_for(t.ne), kBlock, 0, sh.stream>>>(t.dirty[cur].get(), t.ne, t.label.get(),
+                                                                                 sh.cc_msg[1].get(), t.tmin.get(),
+                                                                                 t.rootb.get());
+                JG_LAUNCH_CHECK();
+                cc_apply_sparse_kernel<<<grid, kBlock, 0, sh.stream>>>(
+                    t.sm, sh.cc_msg[1].get(), t.tmin.get(), t.rootb.get(), t.label.get(), sh.cc_msg[0].get(),
+                    t.dirty[nxt].get(), t.cb.get(), sh.index, P, sh.halo_both.tbits, t.pcnt.get() + P, sh.cc_changed.get(),
+                    t.nchg.get());
+                JG_LAUNCH_CHECK();
+                // dirty bits of own rows, parent + root bit per slot (the applied slots' tmin and values are few)
+                bytes += (double)t.ne / 8.0 + 4.5 * (double)t.sm.total;
+                continue;
+            }
             if (rounds == 1) {
                 cc_tree_init_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, t.label.get(), sh.cc_msg[0].get(), t.tmin.get());
                 JG_LAUNCH_CHECK();
@@ -788,32 +1197,85 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
                 t.sm, sh.cc_msg[1].get(), t.label.get(), sh.cc_msg[0].get(), t.giant, t.tmin.get());
             JG_LAUNCH_CHECK();
             cc_tree_apply_kernel<<<grid, kBlock, 0, sh.stream>>>(t.sm, sh.cc_msg[1].get(), t.tmin.get(), t.label.get(),
-                                                                 sh.cc_msg[0].get(), sh.cc_changed.get());
+                                                                 sh.cc_msg[0].get(), sh.cc_changed.get(), t.dirty[nxt].get(),
+                                                                 t.nchg.get());
             JG_LAUNCH_CHECK();
             // per slot: init 8 B (round 1), tree minima 8 B (parent, label; the atomics of non-root
-            // members), apply 12 B; reverse apply 12 B per send-list element
-            bytes += (rounds == 1 ? 28.0 : 20.0) * (double)t.sm.total + 12.0 * (double)t.nsend;
+            // members), apply 12 B
+            bytes += (rounds == 1 ? 28.0 : 20.0) * (double)t.sm.total;
         }
-        exchange_halo_reverse(g, JG_ADJ_BOTH, mv, rv, sizeof(int32_t), ncclInt32);
-        for (size_t i = 0; i < ns; ++i) {
-            Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh);
-            St& t = st[i];
-            if (t.nsend) {
-                cc_reverse_apply_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
-                    t.rbuf.get(), sh.halo_both.send_src.get(), t.nsend, t.label.get(), sh.cc_changed.get());
-                JG_LAUNCH_CHECK();
+        // reverse: after a sparse apply only the marked copies moved (pairs, unless dense is cheaper);
+        // after a dense one every copy holds its tree's minimum (the whole run)
+        bool rev_sparse = false;
+        if (fwd_sparse)
+            rev_sparse = sparse_step(
+                P,
+                [&](size_t i) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    if (t.sm.total > t.ne) {
+                        cc_rev_pack_kernel<<<grid_for(t.sm.total - t.ne), kBlock, 0, sh.stream>>>(
+                            t.sm, t.cb.get(), sh.cc_msg[0].get(), sh.index, P, sh.halo_both.tbits, t.pbase.get(),
+                            t.cursor.get(), t.spairs.get());
+                        JG_LAUNCH_CHECK();
+                    }
+                },
+                [&](size_t i, int64_t n) {
+                    Shard& sh = *g.shards[i];
+                    St& t = st[i];
+                    cc_rev_recv_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(t.rpairs.get(), t.roffd.get(), P,
+                                                                             sh.halo_both.send_src.get(), t.send_off.get(),
+                                                                             t.label.get(), t.dirty[nxt].get(),
+                                                                             sh.cc_changed.get(), t.nchg.get());
+                    JG_LAUNCH_CHECK();
+                    bytes += 20.0 * (double)n;  // pair, send_src, label
+                });
+        if (!rev_sparse) {
+            exchange_halo_reverse(g, JG_ADJ_BOTH, mv, rv, sizeof(int32_t), ncclInt32);
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                St& t = st[i];
+                if (t.nsend) {
+                    cc_reverse_apply_kernel<<<grid_for(t.nsend), kBlock, 0, sh.stream>>>(
+                        t.rbuf.get(), sh.halo_both.send_src.get(), t.nsend, t.label.get(), sh.cc_changed.get(),
+                        t.dirty[nxt].get(), t.nchg.get());
+                    JG_LAUNCH_CHECK();
+                }
+                bytes += 12.0 * (double)t.nsend;  // reverse apply per send-list element
             }
         }
-        int ch = 0;
+        if (fwd_sparse)
+            for (size_t i = 0; i < ns; ++i) {  // the marks of this round's sparse apply
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                JG_HIP(hipMemsetAsync(st[i].rootb.get(), 0, st[i].rootb.bytes(), sh.stream));
+                JG_HIP(hipMemsetAsync(st[i].cb.get(), 0, st[i].cb.bytes(), sh.stream));
+            }
+        if (debug_rounds) {
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                std::vector<unsigned long long> c(2 * (size_t)P, 0);
+                copy_d2h(c.data(), st[i].pcnt.get(), c.size() * sizeof(unsigned long long), sh.stream);
+                unsigned long long f = 0, rv2 = 0;
+                for (int q = 0; q < P; ++q) f += c[(size_t)q], rv2 += c[(size_t)P + q];
+                std::fprintf(stderr, "[jg cc] round %d shard %d: forward %s %llu pairs, reverse %s %llu pairs (rows fell "
+                             "last round, all shards: %lld)\n", rounds, sh.index, fwd_sparse ? "sparse" : "dense", f,
+                             rev_sparse ? "sparse" : "dense", rv2, (long long)fell);
+            }
+        }
+        fell = 0;  // (cc_changed is set exactly when a shard's count is non-zero)
         for (size_t i = 0; i < ns; ++i) {
             Shard& sh = *g.shards[i];
             DeviceGuard dg(sh);
-            int32_t c = 0;
-            copy_d2h(&c, sh.cc_changed.get(), sizeof c, sh.stream);
-            ch |= c;
+            std::vector<unsigned long long> c((size_t)kFellLines * kFellStride);
+            copy_d2h(c.data(), st[i].nchg.get(), c.size() * sizeof(unsigned long long), sh.stream);
+            for (int k = 0; k < kFellLines; ++k) fell += (int64_t)c[(size_t)k * kFellStride];
         }
-        any = allreduce_or(g, ch) != 0;
+        allreduce_sum_i64(g, &fell, 1);
+        any = fell > 0;
+        cur = nxt;
     }
     // the superstep count: one BFS from every component's minimum-rank vertex
     std::vector<CcRoots> roots(ns);

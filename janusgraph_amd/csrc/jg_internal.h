@@ -612,6 +612,8 @@ struct Tune {
     int cc_uf_sharded = 1;            //         sharded (halo plans): local union-find, tree labels over the halo,
                                       //         multi-root sharded BFS for the superstep count (0: propagation)
     int cc_uf_search = 1;             //         ... giant-to-giant links by a bounded search (0: every flagged entry)
+    int cc_sparse = 1;                //         ... label rounds after the first move only the labels that fell
+                                      //         ((offset, label) pairs) when that is under half the run (0: dense)
     int msbfs_split = 1;              //         bit-parallel BFS pull levels through the sliced split (merge engine)
     int sharded_bfs = 1;              //         single-source BOTH BFS on a sharded graph: DO-BFS over the halo
     int bfs_td_split = 2;             //         DO-BFS top-down levels of >= bfs_td_split_min frontier entries in two
@@ -627,8 +629,9 @@ struct Tune {
     int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
                                       //         (0: every launch at the full grid)
     int bfs_persistent = 0;           //         DO-BFS: every level in one launch, a grid barrier between levels
-                                      //         (measured slower, profiles/r05/persistent/)
-    int bfs_persistent_grid = 0;      //         its workgroups (0: the level grid, capped at the co-resident count)
+                                      //         (measured slower, profiles/r05/persistent/):
+                                      //         0 off, 1 at the level grid, N > 1 at N workgroups (capped at the
+                                      //         co-resident count)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct

@@ -1580,7 +1580,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
             JG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sh.device));
             resident = std::max(per_cu, 1) * std::max(cus, 1);
         }
-        const int want = tune().bfs_persistent_grid > 0 ? tune().bfs_persistent_grid : (int)grid;
+        const int want = tune().bfs_persistent > 1 ? tune().bfs_persistent : (int)grid;
         const unsigned pg = (unsigned)std::min(want, resident);
         if (sh.bfs_sync.size() != kSyncBytes) sh.bfs_sync.alloc(kSyncBytes);
         JG_HIP(hipMemsetAsync(sh.bfs_sync.get(), 0, kSyncBytes, s));

@@ -82,10 +82,10 @@ def test_tune_keys_validate_without_a_gpu():
     jg.load()
     for k, v in (("merge_temporal", 1), ("band1_bit", 3), ("merge_pack", 1), ("merge_stage0", -1), ("merge_stage1", -1),
                  ("bfs_grid_mult", 4), ("bfs_batch0", 10), ("msbfs_skip", 1), ("cc_first", 1), ("msbfs_sparse", 1),
-                 ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("msbfs_td", 2),
+                 ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("cc_sparse", 0), ("cc_sparse", 1), ("msbfs_td", 2),
                  ("msbfs_td", 1), ("bfs_td_split", 2), ("bfs_td_split_levels", 2), ("bfs_td_split_min", 65536),
-                 ("bfs_td_split_max", 1 << 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64), ("bfs_persistent", 1), ("bfs_persistent", 0),
-                 ("bfs_persistent_grid", 256), ("bfs_persistent_grid", 0),
+                 ("bfs_td_split_max", 1 << 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64), ("bfs_persistent", 1), ("bfs_persistent", 256),
+                 ("bfs_persistent", 0),
                  ("msbfs_exit", 0), ("msbfs_exit", 2), ("msbfs_exit", 1), ("msbfs_exit_live", 1000), ("msbfs_exit_live", 950),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
@@ -97,7 +97,7 @@ def test_tune_keys_validate_without_a_gpu():
     for k, v in (("light_lds", 0), ("pull_unroll", 4), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
                  ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 0), ("merge_nt", 0), ("msbfs_srcsplit", 0),
                  ("msbfs_bu", 0), ("fin_pipe", 1), ("relabel_out_ties", 0), ("band_sliced_build", 0),
-                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("bfs_tail_grid", -1), ("bfs_persistent", 2),
+                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("cc_first", 0), ("cc_first", 65), ("bfs_tail_grid", -1), ("bfs_persistent", -1),
                  ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0),
                  ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1), ("nb_first", 3), ("nb_alpha", 0),
                  ("bfs_narrow", 2), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1),

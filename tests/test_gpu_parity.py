@@ -393,12 +393,14 @@ def test_logical_shards_match_single(oracle_lib, shards, scale, halo):
     c.close()
 
 
-@pytest.mark.parametrize("shards,uf", [(2, 1), (3, 1), (8, 1), (3, 0), (3, "nosearch"), (8, "nosearch")])
+@pytest.mark.parametrize("shards,uf", [(2, 1), (3, 1), (8, 1), (3, 0), (3, "nosearch"), (8, "nosearch"), (3, "dense"),
+                                       (8, "dense")])
 def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
     """Logical shards over halo plans: local union-finds, tree labels spread over the halo, and one
     sharded BFS from every component's minimum-rank vertex for the superstep count (cc_uf_sharded=1),
     or the label propagation (0); "nosearch" skips the bounded giant-to-giant search, so every peer
-    takes the fallback (giant rows link every flagged copy).  Components of every kind (isolated vertices, self-loops, small
+    takes the fallback (giant rows link every flagged copy); "dense" moves every label in every label
+    round (cc_sparse=0; the default sends only the labels that fell, as pairs).  Components of every kind (isolated vertices, self-loops, small
     components split across shards, an RMAT giant), a path past the 99-superstep cap (handed to the
     propagation) and one below it; labels and superstep counts against the oracle."""
     import janusgraph_amd as jg
@@ -420,6 +422,7 @@ def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
     try:
         _lib.tune_set("cc_uf_sharded", 0 if uf == 0 else 1)
         _lib.tune_set("cc_uf_search", 0 if uf == "nosearch" else 1)
+        _lib.tune_set("cc_sparse", 0 if uf == "dense" else 1)
         c = jg.Context((0,) * shards)
         for n, s, d, vid in cases:
             g = c.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
@@ -432,6 +435,7 @@ def test_sharded_connected_components_union_find(oracle_lib, shards, uf):
     finally:
         _lib.tune_set("cc_uf_sharded", 1)
         _lib.tune_set("cc_uf_search", 1)
+        _lib.tune_set("cc_sparse", 1)
 
 
 @pytest.mark.parametrize("shards", [2, 3, 8])
@@ -601,12 +605,13 @@ def test_bfs_tail_grid_deeper_than_history(oracle_lib, tail):
         _lib.tune_set("bfs_tail_grid", 64)
 
 
-@pytest.mark.parametrize("grid", [0, 256, 8])
+@pytest.mark.parametrize("grid", [1, 256, 8])
 def test_bfs_persistent_matches_oracle(oracle_lib, grid):
     """bfs_persistent: every DO-BFS level in one launch with a grid barrier between levels (the A/B of
     VERDICT r04 item 4).  Depths and edge counts equal the launch-per-level path's and the oracle's over
     RMAT graphs (both directions, split and CAS top-down levels), a 45-level path (many barriers on a
-    tiny frontier), a depth bound, and OUT/IN adjacencies; grid 8 is one workgroup per barrier group."""
+    tiny frontier), a depth bound, and OUT/IN adjacencies; grid 1 = the level grid, 8 = one workgroup per
+    barrier group."""
     import janusgraph_amd as jg
     from janusgraph_amd import _lib
     c = jg.Context((0,))
@@ -620,8 +625,7 @@ def test_bfs_persistent_matches_oracle(oracle_lib, grid):
                 _lib.tune_set("bfs_persistent", 0)
                 g.bfs([vid[s]], 3, want=False)
                 st0 = c.stats()
-                _lib.tune_set("bfs_persistent", 1)
-                _lib.tune_set("bfs_persistent_grid", grid)
+                _lib.tune_set("bfs_persistent", grid)
                 got = g.bfs([vid[s]], 3)[0]
                 st1 = c.stats()
                 np.testing.assert_array_equal(got, oracle_lib.bfs(n, ds, dd, s, 3), err_msg=f"scale {scale} src {s}")
@@ -643,5 +647,4 @@ def test_bfs_persistent_matches_oracle(oracle_lib, grid):
         g.close()
     finally:
         _lib.tune_set("bfs_persistent", 0)
-        _lib.tune_set("bfs_persistent_grid", 0)
         c.close()

@@ -31,7 +31,7 @@ def main():
     g = ctx.build(vid, vid[s], vid[s + 1], flags=jg.ADJ_BOTH)
     settings = [("launch", {"bfs_persistent": 0, "bfs_grid": 8192}),
                 ("launch_g256", {"bfs_persistent": 0, "bfs_grid": 256})]
-    settings += [(f"persistent_g{pg}", {"bfs_persistent": 1, "bfs_persistent_grid": pg, "bfs_grid": 8192})
+    settings += [(f"persistent_g{pg}", {"bfs_persistent": pg, "bfs_grid": 8192})
                  for pg in (1024, 512, 256, 64)]
     jg._lib.tune_set("bfs_tail_grid", 0)  # every launch at the level grid
     res = {name: [] for name, _ in settings}
@@ -45,7 +45,7 @@ def main():
             st = ctx.stats()
             res[name].append(st["compute_ms"])
             lv[name] = st["levels"]
-    for k, v in (("bfs_persistent", 0), ("bfs_persistent_grid", 0), ("bfs_grid", 8192), ("bfs_tail_grid", 64)):
+    for k, v in (("bfs_persistent", 0), ("bfs_grid", 8192), ("bfs_tail_grid", 64)):
         jg._lib.tune_set(k, v)
     for name, _ in settings:
         ms = float(np.median(res[name]))
