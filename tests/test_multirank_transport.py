@@ -148,6 +148,61 @@ def _worker_msbfs(rank, world, port, errfile):
         raise
 
 
+def _worker_cc(rank, world, port, errfile, logfile):
+    """Sharded CC in rank mode on a graph of many cross-shard chains (many label rounds, few labels moving
+    in each after the first): the sparse pair rounds over the host transport (the library's JG_DEBUG_CC
+    log must show a sparse forward) and the dense rounds (cc_sparse 0), both against the oracle."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["JG_DEBUG_CC"] = "1"
+        fd = os.open(f"{logfile}.{rank}", os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+        os.dup2(fd, 2)  # the library's per-round log
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import janusgraph_amd as jg
+        from janusgraph_amd import _lib
+        from janusgraph_amd.transport import GlooTransport
+        from oracle import oracle as o
+        rng = np.random.default_rng(5)
+        n, plen = 4000, 40
+        perm = rng.permutation(n)
+        s, d = [], []
+        for c0 in range(0, 3200, plen):  # 80 chains of 40 vertices with scattered ids
+            ch = perm[c0:c0 + plen]
+            s += list(ch[:-1])
+            d += list(ch[1:])
+        s += list(rng.integers(3200, n, 900))  # a random part: small components and a few larger ones
+        d += list(rng.integers(3200, n, 900))
+        s, d = np.array(s, np.int32), np.array(d, np.int32)
+        vid = (np.arange(n, dtype=np.int64) + 3) * 7
+        ctx = jg.Context((0,), rank=rank, nranks=world, transport=GlooTransport(dist, world))
+        g = ctx.build(vid, vid[s], vid[d], flags=jg.ADJ_BOTH)
+        out = []
+        for sparse in (1, 0):
+            _lib.tune_set("cc_sparse", sparse)
+            comp, it = g.connected_components()
+            comp, own = _combine(dist, world, comp, np.iinfo(np.int64).max)
+            out.append((comp, it, own))
+        _lib.tune_set("cc_sparse", 1)
+        if rank == 0:
+            cref, cit = o.connected_components(n, s, d, vid)
+            for comp, it, own in out:
+                assert (own == 1).all()
+                np.testing.assert_array_equal(comp, cref)
+                assert it == cit, (it, cit)
+        g.close()
+        ctx.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}:\n" + traceback.format_exc())
+        raise
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -190,3 +245,25 @@ def test_msbfs64_unbounded_ranks_over_host_transport(tmp_path, world):
             p.kill()
     err = open(errfile).read() if os.path.exists(errfile) else ""
     assert all(p.exitcode == 0 for p in procs), f"exit codes {[p.exitcode for p in procs]}\n{err}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_cc_sparse_rounds_ranks_over_host_transport(tmp_path, world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errfile = str(tmp_path / "err.txt")
+    logfile = str(tmp_path / "cc.log")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cc, args=(r, world, port, errfile, logfile)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    err = open(errfile).read() if os.path.exists(errfile) else ""
+    assert all(p.exitcode == 0 for p in procs), f"exit codes {[p.exitcode for p in procs]}\n{err}"
+    log = open(f"{logfile}.0").read()
+    assert "forward sparse" in log, log[-2000:]
