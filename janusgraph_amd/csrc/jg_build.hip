@@ -888,6 +888,13 @@ int auto_band_bits(int64_t vec_entries, int elem_bytes) {
     const int b = elem_bytes >= 8 ? l2 - 19 : 4 + (l2 - 24) / 2;
     return std::min(std::max(b, 4), elem_bytes >= 8 ? 6 : 7);
 }
+// Bands after the first (in-degree 8-95): 4 sub-slices (each shared by two XCDs) when the whole 8-byte
+// vector fits the Infinity Cache on one shard (<= 2^24 entries, 128 MB), 8 otherwise (round 5,
+// tools/pr_ab.py: RMAT-24 0.7426 / 0.751 / 0.7654 ms at 4 / 8 / 2, RMAT-26 3.623 / 3.508 / 4.028 ms;
+// profiles/r05/ab/): fewer sub-row partials where the gathers hit the cache anyway
+int auto_band1_bits(int64_t vec_entries, int elem_bytes, bool sharded_vec) {
+    return elem_bytes >= 8 && !sharded_vec && vec_entries <= (1ll << 24) ? 2 : 3;
+}
 
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
                      int elem_bytes) {
@@ -968,9 +975,9 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         const int64_t end = std::min<int64_t>((int64_t)fb[kNumClasses + 1 + i], zero_begin);
         if (end <= row_at) continue;
         auto bd = std::make_unique<SliceBand>();
-        bd->bits = tune().band_bits[i] >= 0
-                       ? std::min(tune().band_bits[i], 8)
-                       : std::min(std::max(auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
+        bd->bits = tune().band_bits[i] >= 0 ? std::min(tune().band_bits[i], 8)
+                   : i > 0 ? auto_band1_bits(vec_entries, elem_bytes, sharded_vec)
+                           : std::min(std::max(auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
         bd->row_begin = row_at;
         bd->row_end = end;
         row_at = end;

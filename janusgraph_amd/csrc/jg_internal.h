@@ -571,7 +571,8 @@ struct Tune {
     // entries (round 4, tools/pr_ab.py: PageRank RMAT-22 / 24 -1% against 128, RMAT-26 and the 64-source
     // BFS unchanged; profiles/r04/band0_deg/)
     int64_t band_deg[4] = {96, 8, 0, 0};
-    int band_bits[4] = {-1, 3, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits of the vector)
+    int band_bits[4] = {-1, -1, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits /
+                                        // auto_band1_bits of the vector)
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
                                       // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)
