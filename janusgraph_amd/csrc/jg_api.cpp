@@ -686,7 +686,7 @@ int jg_tune_set(const char* key, int64_t value) {
         // band<i>_sub: sub-slices, a power of two in [1, 256]
         const int i = k[4] - '0';
         if (k.substr(5) == "_deg") {
-            JG_ARG(value >= 0, "band degree must be >= 0");
+            JG_ARG(value >= -1, "band degree must be >= 0 (0: unused) or -1 (automatic)");
             t.band_deg[i] = value;
         } else if (k.substr(5) == "_bit") {
             JG_ARG(value == 0 || (value >= 3 && value <= 8), "band bits must be 0 (automatic) or in [3, 8]");

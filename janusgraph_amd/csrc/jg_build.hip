@@ -888,12 +888,22 @@ int auto_band_bits(int64_t vec_entries, int elem_bytes) {
     const int b = elem_bytes >= 8 ? l2 - 19 : 4 + (l2 - 24) / 2;
     return std::min(std::max(b, 4), elem_bytes >= 8 ? 6 : 7);
 }
-// Bands after the first (in-degree 8-95): 4 sub-slices (each shared by two XCDs) when the whole 8-byte
-// vector fits the Infinity Cache on one shard (<= 2^24 entries, 128 MB), 8 otherwise (round 5,
-// tools/pr_ab.py: RMAT-24 0.7426 / 0.751 / 0.7654 ms at 4 / 8 / 2, RMAT-26 3.623 / 3.508 / 4.028 ms;
-// profiles/r05/ab/): fewer sub-row partials where the gathers hit the cache anyway
-int auto_band1_bits(int64_t vec_entries, int elem_bytes, bool sharded_vec) {
-    return elem_bytes >= 8 && !sharded_vec && vec_entries <= (1ll << 24) ? 2 : 3;
+// Bands after the first (round 5, tools/pr_ab.py, profiles/r05/ab/).  When the whole 8-byte vector fits
+// the Infinity Cache on one shard (<= 2^24 entries, 128 MB) one band of in-degree 8-95 with 4 sub-slices
+// (each shared by two XCDs): half the sub-row partials where the gathers hit the cache anyway (RMAT-24
+// 0.743 / 0.751 / 0.765 ms at 4 / 8 / 2 sub-slices; a third band: no gain).  A larger one-shard 8-byte
+// vector: in-degree 16-95 with 8 sub-slices and 8-15 with 4 (RMAT-26 3.473-3.484 against 3.520-3.559 ms
+// with one band of 8-95 at 8; 4 sub-slices for all of 8-95: 3.623).  Otherwise (sharded or 4-byte
+// vectors: not re-measured) one band of 8-95 with 8.  -> (degree floor, log2 sub-slices) of band i >= 1.
+struct AutoBand {
+    int64_t deg;
+    int bits;
+};
+AutoBand auto_bands(int i, int64_t vec_entries, int elem_bytes, bool sharded_vec) {
+    const bool one8 = elem_bytes >= 8 && !sharded_vec;
+    if (one8 && vec_entries <= (1ll << 24)) return i == 1 ? AutoBand{8, 2} : AutoBand{0, 2};
+    if (one8) return i == 1 ? AutoBand{16, 3} : i == 2 ? AutoBand{8, 2} : AutoBand{0, 2};
+    return i == 1 ? AutoBand{8, 3} : AutoBand{0, 3};
 }
 
 void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_space, int64_t vec_entries,
@@ -954,8 +964,12 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
     BandThresholds bt{};
     // bands only when the split is enabled at build time (cut from the column-ordered CSR by counting;
     // cutting them from a second, sub-slice-ordered build cost a select and a sort more, round 3)
+    // a band's degree floor: the knob, or automatic (-1); the first unused band (0) ends the list
+    auto band_floor = [&](int i) {
+        return tune().band_deg[i] >= 0 ? tune().band_deg[i] : i == 0 ? 96 : auto_bands(i, vec_entries, elem_bytes, sharded_vec).deg;
+    };
     if (tune().pull_split)
-        for (int i = 0; i < 4 && tune().band_deg[i] > 0; ++i) bt.thr[bt.n++] = std::max<int64_t>(tune().band_deg[i], 1);
+        for (int i = 0; i < 4 && band_floor(i) > 0; ++i) bt.thr[bt.n++] = std::max<int64_t>(band_floor(i), 1);
     for (int i = 0; i < 4; ++i) fb[kNumClasses + 1 + i] = (unsigned long long)rows;
     if (rows > 0) {
         DevBuf<unsigned long long> d_fb(kNumClasses + 1 + 4);
@@ -976,7 +990,7 @@ void build_pull_plan(Shard& sh, const Csr& csr, PullPlan& plan, int64_t col_spac
         if (end <= row_at) continue;
         auto bd = std::make_unique<SliceBand>();
         bd->bits = tune().band_bits[i] >= 0 ? std::min(tune().band_bits[i], 8)
-                   : i > 0 ? auto_band1_bits(vec_entries, elem_bytes, sharded_vec)
+                   : i > 0 ? auto_bands(i, vec_entries, elem_bytes, sharded_vec).bits
                            : std::min(std::max(auto_band_bits(vec_entries, elem_bytes) + (sharded_vec ? 1 : 0), 3), 8);
         bd->row_begin = row_at;
         bd->row_end = end;

@@ -567,12 +567,12 @@ struct Tune {
     int pull_split = 1;   // XCD-sliced split of the heavy rows (pull_merge_kernel): 0 off, 1 on
                           // (read at build time too: the sliced in-CSR and split plan need it)
     // build time: degree bands of the split, highest first: rows of degree >= band_deg[i] (and below
-    // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light.  Band 0 from 96
-    // entries (round 4, tools/pr_ab.py: PageRank RMAT-22 / 24 -1% against 128, RMAT-26 and the 64-source
-    // BFS unchanged; profiles/r04/band0_deg/)
-    int64_t band_deg[4] = {96, 8, 0, 0};
-    int band_bits[4] = {-1, -1, 3, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits /
-                                        // auto_band1_bits of the vector)
+    // band i-1) get 2^band_bits[i] sub-slices; rows below the last used band stay light (0: unused).  Band
+    // 0 from 96 entries (round 4, tools/pr_ab.py: PageRank RMAT-22 / 24 -1% against 128, RMAT-26 and the
+    // 64-source BFS unchanged; profiles/r04/band0_deg/).  -1: automatic (auto_bands in jg_build.hip: bands
+    // 1 and 2 depend on whether the vector fits the Infinity Cache)
+    int64_t band_deg[4] = {96, -1, -1, 0};
+    int band_bits[4] = {-1, -1, -1, 3};  // log2 sub-slices (0..8); -1: automatic (auto_band_bits, auto_bands)
     int halo = 1;                     // build time, P > 1: compact vectors + halo exchange (0: dense allgather)
     int bfs_alpha = 14;               // DO-BFS: top-down -> bottom-up when frontier edges > unexplored / alpha
                                       // (multi-source starts: CC's eccentricity BFS, MS-BFS and CC push levels)

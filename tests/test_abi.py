@@ -91,7 +91,8 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
                  ("msbfs_td_rowapply", 0), ("msbfs_td_rowapply", 4), ("bfs_narrow", 0), ("bfs_narrow", 1),
                  ("nb_alpha", 14), ("nb_alpha", 30), ("nb_first", 16), ("halo", 1), ("pull_split", 1), ("band0_sub", 64),
-                 ("band0_bit", 0), ("band0_deg", 96), ("band1_bit", 0)):
+                 ("band0_bit", 0), ("band0_deg", 96), ("band1_bit", 0), ("band1_deg", -1), ("band2_deg", -1),
+                 ("band2_bit", 0)):
         _lib.tune_set(k, v)
     # unknown keys (including the variants deleted in round 5: measured slower or equal) and bad values
     for k, v in (("light_lds", 0), ("pull_unroll", 4), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),

@@ -289,8 +289,8 @@ def test_msbfs_task_skip_matches_oracle(oracle_lib, mode, shards):
         _lib.tune_set("msbfs_scan_queue", 50)
         _lib.tune_set("msbfs_td_rowapply", 4)
         _lib.tune_set("halo", 1)
-        for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 0), ("band2_deg", 0),
-                     ("band2_bit", 3)):  # the defaults (Tune::band_deg / band_bits)
+        for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", -1), ("band1_bit", 0), ("band2_deg", -1),
+                     ("band2_bit", 0), ("band3_deg", 0)):  # the defaults (Tune::band_deg / band_bits)
             _lib.tune_set(k, v)
 
 
@@ -535,8 +535,8 @@ def test_pull_engine_variants_match_oracle(oracle_lib, mode):
         _lib.tune_set("merge_stage0", -1)
         _lib.tune_set("merge_stage1", -1)
         _lib.tune_set("cc_first", 1)
-        for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", 8), ("band1_bit", 0), ("band2_deg", 0),
-                     ("band2_bit", 3)):
+        for k, v in (("band0_deg", 96), ("band0_bit", 0), ("band1_deg", -1), ("band1_bit", 0), ("band2_deg", -1),
+                     ("band2_bit", 0), ("band3_deg", 0)):
             _lib.tune_set(k, v)
 
 
