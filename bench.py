@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--bfs-scale", type=int, default=20)
     p.add_argument("--no-bfs", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU work of each cpu_baseline sample (whole supersteps / BFS rounds until then)")
     p.add_argument("--no-big", action="store_true", help="skip the RMAT-26 blocks (PageRank, BFS, CC, MS-BFS)")
     p.add_argument("--big-scale", type=int, default=26)
     p.add_argument("--big-steps", type=int, default=10)
@@ -219,8 +220,9 @@ def bench_trace_block(workload):
     return None
 
 
-def cpu_baseline(scale, ef, seed, steps):
-    """The oracle's PageRank superstep (OpenMP) on the same RMAT graph, rank 0 only."""
+def cpu_baseline(scale, ef, seed, seconds, min_steps=2):
+    """The oracle's PageRank superstep (OpenMP) on the same RMAT graph, rank 0 only: whole supersteps until
+    `seconds` of CPU work (a bounded sample of the workload)."""
     from oracle import oracle as o
     o.build()
     n, m = 1 << scale, ef << scale
@@ -233,33 +235,39 @@ def cpu_baseline(scale, ef, seed, steps):
     with np.errstate(divide="ignore"):  # sinks: never gathered (no out-edges), as in the kernels
         contrib = (1.0 / n) / outdeg
     t0 = time.perf_counter()
-    for _ in range(steps):
+    steps = 0
+    while steps < min_steps or time.perf_counter() - t0 < seconds:
         contrib = o.pagerank_superstep_csr(n, ptr, col, contrib, outdeg, 0.85, n)
+        steps += 1
     dt = time.perf_counter() - t0
     return {"value": round(m * steps / dt / 1e9, 4), "unit": "GTEPS", "cores": o.num_threads(), "kind": "port",
             "sample": f"oracle/jg_oracle.c jo_pagerank_superstep_csr (OpenMP), {steps} full power supersteps on "
-                      f"the same RMAT-{scale} ef{ef} graph (seed {seed}); CSR build untimed"}
+                      f"the same RMAT-{scale} ef{ef} graph (seed {seed}), {dt:.1f} s; CSR build untimed"}
 
 
-def cpu_baseline_bfs(scale, ef, seed, sources):
+def cpu_baseline_bfs(scale, ef, seed, sources, seconds):
     """The oracle's level-synchronous parallel BFS (jo_bfs_csr, OpenMP) from the bench's sources on the same
-    symmetrised RMAT graph, Graph500 TEPS (input edges of the source's component / time)."""
+    symmetrised RMAT graph, Graph500 TEPS (input edges of the source's component / time), rounds over the
+    sources until `seconds` of CPU work."""
     from oracle import oracle as o
     o.build()
     n = 1 << scale
     s, d = o.rmat_edges(scale, ef, seed)
     s, d = s.astype(np.int32), d.astype(np.int32)
     ptr, adj = o.csr_unordered(n, s, d, both=True)
-    teps, total = [], 0.0
-    for sv in sources:
-        t0 = time.perf_counter()
-        depth = o.bfs_csr(n, ptr, adj, int(sv))
-        dt = time.perf_counter() - t0
-        total += dt
-        teps.append(int(np.count_nonzero(depth[s] >= 0)) / dt / 1e9)
+    teps, total, rounds = [], 0.0, 0
+    while rounds == 0 or total < seconds:
+        for sv in sources:
+            t0 = time.perf_counter()
+            depth = o.bfs_csr(n, ptr, adj, int(sv))
+            dt = time.perf_counter() - t0
+            total += dt
+            teps.append(int(np.count_nonzero(depth[s] >= 0)) / dt / 1e9)
+        rounds += 1
     return {"value": round(float(np.median(teps)), 4), "unit": "GTEPS", "cores": o.num_threads(), "kind": "port",
-            "sample": f"oracle/jg_oracle.c jo_bfs_csr (OpenMP, top-down level-synchronous), the {len(sources)} bench "
-                      f"sources on the same RMAT-{scale} ef{ef} graph, {total:.2f} s of CPU BFS; CSR build untimed"}
+            "sample": f"oracle/jg_oracle.c jo_bfs_csr (OpenMP, top-down level-synchronous), {rounds} rounds over the "
+                      f"{len(sources)} bench sources on the same RMAT-{scale} ef{ef} graph, {total:.1f} s of CPU BFS; "
+                      f"CSR build untimed"}
 
 
 def hbm_roofline(alg_bytes, ms, kernel, workload=None, model=None):
@@ -288,7 +296,7 @@ def both_degrees(jg, ctl, g):
     return ctl.sum_array(deg) if ctl.ws > 1 else deg
 
 
-def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
+def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True, cpu_seconds=10.0):
     """Single-source DO-BFS (SPVP depth, BOTH edges) from seeded sources of degree > 0, Graph500 TEPS (input
     edges of the source's component / time); roofline of one traversal: 8*m + 12*n algorithmic bytes
     (one full pass) / its HIP-event time.  N > 1: the sharded DO-BFS (dobfs_sharded)."""
@@ -330,7 +338,7 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True):
     else:
         blk["per_rank"] = per_rank_rows(ranks[len(ranks) // 2])
     if cpu and ctl.ws == 1:
-        blk["cpu_baseline"] = cpu_baseline_bfs(scale, ef, 0x5EED + scale, srcs[:3])
+        blk["cpu_baseline"] = cpu_baseline_bfs(scale, ef, 0x5EED + scale, srcs, cpu_seconds)
     return blk
 
 
@@ -539,7 +547,8 @@ def main():
 
     extra = {}
     if not args.no_bfs and ws == 1:
-        extra["bfs"] = bfs_block(jg, ctx, ctl, args.bfs_scale, args.edgefactor, cpu=not args.no_cpu)
+        extra["bfs"] = bfs_block(jg, ctx, ctl, args.bfs_scale, args.edgefactor, cpu=not args.no_cpu,
+                                 cpu_seconds=args.cpu_seconds)
     if not args.no_big:
         # N > 1: the configs[3] / [4] workloads on N GPUs (sharded DO-BFS, CC propagation, sharded MS-BFS)
         big = args.big_scale
@@ -553,7 +562,7 @@ def main():
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.scale, args.edgefactor, args.seed, args.cpu_steps)
+        cpu = cpu_baseline(args.scale, args.edgefactor, args.seed, args.cpu_seconds)
 
     if rank == 0:
         line = {

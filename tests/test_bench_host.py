@@ -10,9 +10,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_cpu_baseline_small():
-    cpu = bench.cpu_baseline(12, 16, 7, 1)
+    cpu = bench.cpu_baseline(12, 16, 7, 0.0, min_steps=1)
     assert set(cpu) >= {"value", "unit", "cores", "kind", "sample"}
     assert cpu["kind"] == "port" and cpu["unit"] == "GTEPS" and cpu["value"] > 0 and cpu["cores"] >= 1
+
+
+def test_cpu_baseline_bfs_rounds_until_the_budget():
+    b = bench.cpu_baseline_bfs(12, 16, 7, [1, 2], 0.0)
+    assert b["value"] > 0 and "1 rounds over the 2 bench sources" in b["sample"]
 
 
 def test_pmc_traffic_lookup():
