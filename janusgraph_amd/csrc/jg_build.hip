@@ -1247,8 +1247,11 @@ void build_graph_from_dense(Graph& g, DenseEdges& e) {
             a.cbits = std::max(cbits, bits_for((uint64_t)(col_space - 1)));  // compact ids may exceed P*S
             // round 3: one column-ordered build, the bands cut from it (band_count / band_scatter)
             build_csr(sh, a, wt, csr, s);
-            // the gathered vector of the split: PageRank's fp64 contributions (IN), CC's int32 labels (BOTH)
-            build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 2 ? 4 : 8);
+            // the gathered vector of the split: PageRank's fp64 contributions (IN); on BOTH the 64-source
+            // BFS's uint64 frontier words on one shard (its main user since CC runs a union-find there:
+            // RMAT-26 11.0 -> 10.35 ms with 64 band-0 sub-slices instead of 32, CC unchanged; round 5,
+            // profiles/r05/ab/msbfs26_bands.txt), CC's int32 labels on sharded graphs (not re-measured)
+            build_pull_plan(sh, csr, plan, col_space, vec_entries, which == 2 && P > 1 ? 4 : 8);
             if (halo.on) {  // segmented compact vector: every segment's hot entries are its prefix
                 plan.lds_ok = true;
                 plan.seg_tbits = halo.tbits;
