@@ -285,14 +285,24 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
             // so a row scanned to its end pays two round trips per batch instead of per neighbour
             // (which neighbour hits does not matter: the depth is level + 1 either way)
             const int64_t j1 = a.pull_rp[v + 1];
-            for (int64_t j = a.pull_rp[v]; j < j1 && !found; j += kBuBatch) {
+            int64_t j = a.pull_rp[v];
+            auto probe = [&](int32_t x) -> bool {
+                return kFromDepth ? a.depth[x] == a.level : ((a.bm_in[x >> 6] >> (x & 63)) & 1ull);
+            };
+            // the first neighbour alone (a row before the empty suffix may still be empty on a directed
+            // pull adjacency, so the bound is checked): columns are in relabelled order, so it is
+            // the row's highest-degree neighbour, the likeliest to be in the frontier (a row still unvisited
+            // at level L has no neighbour of depth < L); one column load and one probe instead of four each
+            // for most rows of the big levels (RMAT-26 DO-BFS 1.730 -> 1.625 ms, CC 2.97 -> 2.88 ms; first
+            // two: 1.675 / 2.94; round 5, profiles/r05/ab/bfs_bu_first_*)
+            if (j < j1) found = probe(a.pull_col[j++]);
+            for (; j < j1 && !found; j += kBuBatch) {
                 int32_t u[kBuBatch];
 #pragma unroll
                 for (int k = 0; k < kBuBatch; ++k) u[k] = a.pull_col[j + k < j1 ? j + k : j1 - 1];
                 bool hit[kBuBatch];
 #pragma unroll
-                for (int k = 0; k < kBuBatch; ++k)
-                    hit[k] = kFromDepth ? a.depth[u[k]] == a.level : ((a.bm_in[u[k] >> 6] >> (u[k] & 63)) & 1ull);
+                for (int k = 0; k < kBuBatch; ++k) hit[k] = probe(u[k]);
 #pragma unroll
                 for (int k = 0; k < kBuBatch; ++k) found |= hit[k];
             }
@@ -1907,18 +1917,22 @@ __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
         bool found = false;
         int64_t deg = 0;
         if (v < a.rows && a.dvec[v] < 0) {
-            const int64_t j1 = a.rp[v + 1];
-            for (int64_t j = a.rp[v]; j < j1 && !found; j += kBuBatch) {
+            const int64_t j0 = a.rp[v], j1 = a.rp[v + 1];
+            auto in_frontier = [&](int32_t x) -> bool {
+                return x < a.rows ? a.dvec[x] == a.level : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
+            };
+            int64_t j = j0;
+            if (j < j1) found = in_frontier(a.col[j++]);  // the first neighbour alone (bfs_bottom_up)
+            for (; j < j1 && !found; j += kBuBatch) {
                 int32_t u[kBuBatch];
 #pragma unroll
                 for (int k = 0; k < kBuBatch; ++k) u[k] = a.col[j + k < j1 ? j + k : j1 - 1];
 #pragma unroll
-                for (int k = 0; k < kBuBatch; ++k)
-                    found |= u[k] < a.rows ? a.dvec[u[k]] == a.level : (bool)((a.hb[u[k] >> 6] >> (u[k] & 63)) & 1ull);
+                for (int k = 0; k < kBuBatch; ++k) found |= in_frontier(u[k]);
             }
             if (found) {
                 a.dvec[v] = nd;
-                deg = j1 - a.rp[v];
+                deg = j1 - j0;
             }
         }
         app.append(found, (int32_t)v, deg, a.queue_out, a.qoff_out, a.packed);
