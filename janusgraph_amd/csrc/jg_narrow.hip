@@ -204,6 +204,10 @@ __global__ __launch_bounds__(kBlock) void nb_bu_kernel(NbLevel a) {
             const int64_t j0 = a.pull_rp[v], j1 = a.pull_rp[v + 1];
             const int64_t je = j0 + a.first < j1 ? j0 + a.first : j1;
             int64_t j = j0;
+            if (j < je) {  // the first (highest-degree) neighbour alone, as in bfs_bottom_up
+                const int32_t u0 = a.pull_col[j++];
+                acc |= (u0 < fdef ? a.Fc[u0] : 0u) & need;
+            }
             for (; j < je && acc != need; j += 4) {
                 int32_t u[4];
 #pragma unroll
