@@ -1439,6 +1439,7 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     if (uf_one && sh0.rows > 0) {  // the union-find path's scratch
         if ((int64_t)sh0.cc_depth.size() < sh0.rows) sh0.cc_depth.alloc(sh0.rows);
         bfs_buffers(sh0);
+        bfs_first_col(sh0, sh0.both);
     }
     for (auto& sp : g.shards) JG_HIP(hipStreamSynchronize(sp->stream));
     prof_discard_exchanges(g);  // exchange pairs count from t0 on only

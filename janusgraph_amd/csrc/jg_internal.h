@@ -37,6 +37,9 @@ struct Csr {
     // rows [empty_from, rows) have no entries (set with the pull plan: 1 + the last non-empty row;
     // -1 when unknown)
     mutable int64_t empty_from = -1;
+    // each row's first column (-1: empty row), built on a traversal's first use (bfs_first_col): a
+    // bottom-up level probes it with one coalesced load instead of a row_ptr pair and a scattered column
+    mutable DevBuf<int32_t> first_col;
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
 };
@@ -527,6 +530,8 @@ int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, 
 int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);
 // Allocate the single-shard traversal's scratch (no-op when present; jg_traverse.hip).
 void bfs_buffers(Shard& sh);
+// Csr::first_col of a traversal's pull adjacency (built on first use, on the shard's stream)
+const int32_t* bfs_first_col(Shard& sh, const Csr& c);
 // JG_TRACE_MARKS=1: an empty named dispatch before a program's t0 / after its t1 (tools/bench_trace.py)
 void region_mark(hipStream_t s, bool begin);
 // Narrow bit-parallel direction-optimising BFS (jg_narrow.hip): 2..kNarrowMax sources on one shard,

@@ -90,6 +90,7 @@ struct BfsLevel {
     const int32_t* push_col;
     const int64_t* pull_rp;  // null when there is no pull adjacency
     const int32_t* pull_col;
+    const int32_t* pull_first;  // [rows] each pull row's first column, -1 when empty (Csr::first_col)
     const int64_t* deg_rp;   // push_rp, else pull_rp (frontier edge counts)
     int32_t* depth;
     int64_t rows;
@@ -284,18 +285,20 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
             // kBuBatch neighbours per step: all column loads, then all frontier probes, then the test,
             // so a row scanned to its end pays two round trips per batch instead of per neighbour
             // (which neighbour hits does not matter: the depth is level + 1 either way)
-            const int64_t j1 = a.pull_rp[v + 1];
-            int64_t j = a.pull_rp[v];
             auto probe = [&](int32_t x) -> bool {
                 return kFromDepth ? a.depth[x] == a.level : ((a.bm_in[x >> 6] >> (x & 63)) & 1ull);
             };
-            // the first neighbour alone (a row before the empty suffix may still be empty on a directed
-            // pull adjacency, so the bound is checked): columns are in relabelled order, so it is
-            // the row's highest-degree neighbour, the likeliest to be in the frontier (a row still unvisited
-            // at level L has no neighbour of depth < L); one column load and one probe instead of four each
-            // for most rows of the big levels (RMAT-26 DO-BFS 1.730 -> 1.625 ms, CC 2.97 -> 2.88 ms; first
-            // two: 1.675 / 2.94; round 5, profiles/r05/ab/bfs_bu_first_*)
-            if (j < j1) found = probe(a.pull_col[j++]);
+            // the first neighbour alone, from the dense first-column array (one coalesced load per wave;
+            // -1: an empty row, which a directed pull adjacency may hold before its empty suffix): columns
+            // are in relabelled order, so it is the row's highest-degree neighbour, the likeliest to be in
+            // the frontier (a row still unvisited at level L has no neighbour of depth < L); for most rows
+            // of the big levels one probe is all, with no row_ptr or column load (round 5: probing the
+            // first column alone took RMAT-26 DO-BFS 1.730 -> 1.625 ms and CC 2.97 -> 2.88 ms,
+            // profiles/r05/ab/bfs_bu_first_*; the dense array: profiles/r05/ab/bfs_first_col_*)
+            const int32_t u0 = a.pull_first[v];
+            if (u0 >= 0) found = probe(u0);
+            const int64_t j1 = found ? 0 : a.pull_rp[v + 1];
+            int64_t j = found ? 0 : a.pull_rp[v] + 1;
             for (; j < j1 && !found; j += kBuBatch) {
                 int32_t u[kBuBatch];
 #pragma unroll
@@ -1507,6 +1510,29 @@ void region_mark(hipStream_t s, bool begin) {
     JG_LAUNCH_CHECK();
 }
 
+__global__ void first_col_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t rows,
+                                 int32_t* __restrict__ first) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = rp[v];
+        first[v] = rp[v + 1] > j ? col[j] : -1;
+    }
+}
+
+// Csr::first_col of a traversal's pull adjacency, built on first use (outside any timed region: the
+// callers run it before their t0 event)
+const int32_t* bfs_first_col(Shard& sh, const Csr& c) {
+    if (c.first_col.size() != (size_t)std::max<int64_t>(c.rows, 1)) {
+        DeviceGuard dg(sh);
+        c.first_col.alloc(std::max<int64_t>(c.rows, 1));
+        if (c.rows > 0) {
+            first_col_kernel<<<grid_for(c.rows), kBlock, 0, sh.stream>>>(c.row_ptr.get(), c.col.get(), c.rows,
+                                                                         c.first_col.get());
+            JG_LAUNCH_CHECK();
+        }
+    }
+    return c.first_col.get();
+}
+
 void bfs_buffers(Shard& sh) {
     const int64_t rows = sh.rows;
     const int64_t words = (rows + 63) / 64;
@@ -1556,6 +1582,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.push_col = push ? push->col.get() : nullptr;
     a.pull_rp = pull ? pull->row_ptr.get() : nullptr;
     a.pull_col = pull ? pull->col.get() : nullptr;
+    a.pull_first = pull ? bfs_first_col(sh, *pull) : nullptr;  // (the callers build it before their t0)
     a.deg_rp = degcsr->row_ptr.get();
     a.depth = depth;
     a.rows = rows;
@@ -2374,6 +2401,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             JG_HIP(hipEventRecord(t1, sh.stream));
         } else {
             bfs_buffers(sh);
+            if (c.pull) bfs_first_col(sh, *c.pull);
             region_mark(sh.stream, true);
             JG_HIP(hipEventRecord(t0, sh.stream));
             levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1);
@@ -3403,7 +3431,10 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
     hipEvent_t t0, t1;
     JG_HIP(hipEventCreate(&t0));
     JG_HIP(hipEventCreate(&t1));
-    if (seed >= 0 && !g.has_weights) bfs_buffers(sh);
+    if (seed >= 0 && !g.has_weights) {
+        bfs_buffers(sh);
+        if (sh.out.present()) bfs_first_col(sh, sh.out);  // the traversal's pull adjacency
+    }
     region_mark(s, true);
     JG_HIP(hipEventRecord(t0, s));
     int levels = 0;
