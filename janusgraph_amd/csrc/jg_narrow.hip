@@ -58,6 +58,7 @@ struct NbLevel {
     const int32_t* push_col;
     const int64_t* pull_rp;
     const int32_t* pull_col;
+    const int32_t* pull_first;  // [rows] each pull row's first column (Csr::first_col)
     const uint8_t* Fc;  // F_L: this level's frontier (rows [0, ne) defined; level 0: every row)
     uint8_t* Fn;        // F_{L+1}
     uint8_t* vis;
@@ -205,7 +206,8 @@ __global__ __launch_bounds__(kBlock) void nb_bu_kernel(NbLevel a) {
             const int64_t je = j0 + a.first < j1 ? j0 + a.first : j1;
             int64_t j = j0;
             if (j < je) {  // the first (highest-degree) neighbour alone, as in bfs_bottom_up
-                const int32_t u0 = a.pull_col[j++];
+                const int32_t u0 = a.pull_first[v];  // (the dense array: one coalesced load)
+                ++j;
                 acc |= (u0 < fdef ? a.Fc[u0] : 0u) & need;
             }
             for (; j < je && acc != need; j += 4) {
@@ -525,6 +527,7 @@ NarrowRun narrow_bfs(Ctx& ctx, Shard& sh, const Csr& push, const Csr& pull, cons
     a.push_col = push.col.get();
     a.pull_rp = pull.row_ptr.get();
     a.pull_col = pull.col.get();
+    a.pull_first = bfs_first_col(sh, pull);
     a.vis = sh.nb_vis.get();
     a.rest = sh.nb_rest.get();
     a.ctr = ctr;

@@ -863,6 +863,7 @@ constexpr int kMsBuUnroll = 4;  // pass B: 4 x 64 entries in flight per wave ste
 struct MsBu {
     const int64_t* rp;
     const int32_t* col;
+    const int32_t* first_col;         // [rows] each row's first column (Csr::first_col)
     int64_t rows;                     // rows [0, rows) take the early exit
     unsigned long long* examined;     // += the entries scanned (work counter, jg_stats.algorithmic_bytes)
     int first = 16;                   // msbfs_exit_first_kernel: entries a lane scans before pass B takes the row
@@ -899,7 +900,10 @@ __global__ __launch_bounds__(kRedThreads) void msbfs_exit_first_kernel(MsBu a, M
                 int64_t j = e0;
                 // the first entry alone (the row's highest-degree neighbour: often every bit the row needs; as
                 // in bfs_bottom_up): RMAT-26 64-source BFS 10.50 -> 10.04-10.17 ms (profiles/r05/ab/msbfs_first1.log)
-                if (j < ek) acc |= op.F[a.col[j++]] & need;
+                if (j < ek) {  // (its column from the dense array: one coalesced load)
+                    acc |= op.F[a.first_col[v]] & need;
+                    ++j;
+                }
                 for (; j < ek && acc != need; j += 4) {
                     int32_t c[4];
 #pragma unroll
@@ -2657,6 +2661,11 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     }
                 }
             }
+            for (size_t i = 0; i < g.shards.size(); ++i) {  // the early exit's first columns (before t0)
+                Shard& sh = *g.shards[i];
+                const BfsCsrs c = pick_csrs(sh, direction);
+                if (c.pull) bfs_first_col(sh, *c.pull);
+            }
             prof_discard_exchanges(g);  // exchange pairs never straddle t0
             region_mark(sh0.stream, true);
             JG_HIP(hipEventRecord(t0, sh0.stream));
@@ -2783,6 +2792,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     t.xrest.size() > 0 && plan.bands[0]->row_begin == 0 && plan.bands[0]->row_end > 0) {
                     t.bx.rp = c.pull->row_ptr.get();
                     t.bx.col = c.pull->col.get();
+                    t.bx.first_col = bfs_first_col(sh, *c.pull);
                     t.all_rows = c.pull->empty_from >= 0 ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
                     t.bx.rows = t.all_rows;
                     t.bx.examined = t.work.get() + 2;
