@@ -1534,7 +1534,7 @@ const int32_t* bfs_first_col(Shard& sh, const Csr& c) {
             JG_LAUNCH_CHECK();
         }
     }
-    return c.first_col.get();
+    return c.first_col.peer();  // (the callers pass it to kernels under the shard's own guard)
 }
 
 void bfs_buffers(Shard& sh) {
@@ -1745,6 +1745,7 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
 struct SBfsLevel {
     const int64_t* rp;
     const int32_t* col;
+    const int32_t* first_col;       // [rows] each row's first column (Csr::first_col)
     int64_t rows;
     int32_t* dvec;                  // [rows] own depths
     int32_t* stamp;                 // [C] top-down: level + 1 on the halo vertices this level reached
@@ -1951,12 +1952,14 @@ __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
         bool found = false;
         int64_t deg = 0;
         if (v < a.rows && a.dvec[v] < 0) {
-            const int64_t j0 = a.rp[v], j1 = a.rp[v + 1];
             auto in_frontier = [&](int32_t x) -> bool {
                 return x < a.rows ? a.dvec[x] == a.level : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
             };
-            int64_t j = j0;
-            if (j < j1) found = in_frontier(a.col[j++]);  // the first neighbour alone (bfs_bottom_up)
+            // the first neighbour alone, from the dense first-column array (bfs_bottom_up)
+            const int32_t u0 = a.first_col[v];
+            if (u0 >= 0) found = in_frontier(u0);
+            const int64_t j0 = a.rp[v], j1 = a.rp[v + 1];
+            int64_t j = found ? j1 : j0 + 1;
             for (; j < j1 && !found; j += kBuBatch) {
                 int32_t u[kBuBatch];
 #pragma unroll
@@ -2062,6 +2065,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
         t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
         t.ctr.alloc(2);  // level L appends to ctr[(L + 1) & 1], the start (roots) to ctr[0]
+        bfs_first_col(sh, sh.both);  // the bottom-up's first columns (before t0)
     }
     // the traversal's state, inside its timed region: level stamps (0 = none; the occupied slots of the
     // compact vector), depths, the level-0 queue
@@ -2134,6 +2138,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         SBfsLevel a{};
         a.rp = sh.both.row_ptr.get();
         a.col = sh.both.col.get();
+        a.first_col = sh.both.first_col.get();
         a.rows = sh.rows;
         a.dvec = t.dvec.get();
         a.stamp = t.stamp.get();
