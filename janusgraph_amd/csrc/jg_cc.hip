@@ -243,9 +243,17 @@ __global__ void uf_init_kernel(int32_t* __restrict__ parent, int32_t* __restrict
     }
 }
 
-// Afforest's first round: every vertex links to its first k neighbours.
+// Afforest's first round: every vertex links to its first k neighbours.  k = 1 (the default) reads
+// the dense first-column array (Csr::first_col: one coalesced load, no row_ptr pair or scattered column).
 __global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                     int64_t rows, int k) {
+                                     const int32_t* __restrict__ first, int64_t rows, int k) {
+    if (k == 1 && first) {
+        for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+            const int32_t u = first[v];
+            if (u >= 0 && u != (int32_t)v) uf_link(parent, (int32_t)v, u);
+        }
+        return;
+    }
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = rp[v], e1 = rp[v + 1] < rp[v] + k ? rp[v + 1] : rp[v] + k;
         for (int64_t e = e0; e < e1; ++e) {
@@ -355,7 +363,8 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     const int32_t* rank = sh.cc_rank0.get();  // the initial labels are the ranks (cc_prepare_ranks)
     uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
     JG_LAUNCH_CHECK();
-    uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, kFirst);
+    uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), c.first_col.get(), ne,
+                                                         kFirst);
     JG_LAUNCH_CHECK();
     uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
     JG_LAUNCH_CHECK();
@@ -964,7 +973,8 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         }
         if (t.ne > 0) {
             DevBuf<int32_t> sample(1025);
-            uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), t.ne, kFirst);
+            uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), nullptr, t.ne,
+                                                                   kFirst);
             JG_LAUNCH_CHECK();
             cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, parent);
             JG_LAUNCH_CHECK();
