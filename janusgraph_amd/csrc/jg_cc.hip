@@ -973,8 +973,8 @@ bool cc_union_find_sharded(Graph& g, int* iterations, int* rounds_out, double* w
         }
         if (t.ne > 0) {
             DevBuf<int32_t> sample(1025);
-            uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), nullptr, t.ne,
-                                                                   kFirst);
+            uf_link_first_kernel<<<grid_for(t.ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(),
+                                                                   c.first_col.get(), t.ne, kFirst);
             JG_LAUNCH_CHECK();
             cc_slots_compress_kernel<<<grid_for(t.sm.total), kBlock, 0, s>>>(t.sm, parent);
             JG_LAUNCH_CHECK();
@@ -1451,6 +1451,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         bfs_buffers(sh0);
         bfs_first_col(sh0, sh0.both);
     }
+    if (!uf_one && g.P > 1)  // the sharded union-find's first round reads each row's first column
+        for (auto& sp : g.shards)
+            if (sp->both.present()) bfs_first_col(*sp, sp->both);
     for (auto& sp : g.shards) JG_HIP(hipStreamSynchronize(sp->stream));
     prof_discard_exchanges(g);  // exchange pairs count from t0 on only
     region_mark(sh0.stream, true);
