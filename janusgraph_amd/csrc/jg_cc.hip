@@ -338,9 +338,9 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // The union-find runs over the rows that have an edge (those before Csr::empty_from): an edgeless row
 // is its own component, with its own rank as label, and is never linked.
 // *work_bytes: the bytes the passes need (the §8d-style model of this algorithm): per row
-// with an edge 98 B (init 8, first links 20, two compressions 16, rest-link scan 12, minimum rank 8, BFS
-// start 29, BFS depth and seen 5), 12 B per entry linked in the second round (col, both finds) and 4 B
-// per adjacency entry of the rows the BFS reached.
+// with an edge 86 B (init 8, first links 8: the dense first column and the parent probe, two compressions
+// 16, rest-link scan 12, minimum rank 8, BFS start 29, BFS depth and seen 5), 12 B per entry linked in the
+// second round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.
 bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, double* work_bytes) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
@@ -403,7 +403,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     if (it > kCcMaxIterations - 1) return false;
     unsigned long long rest = 0;
     copy_d2h(&rest, linked.get(), sizeof rest, s);
-    *work_bytes = 98.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
+    *work_bytes = 86.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
     *iterations = it;
     *labels = parent;
     return true;
