@@ -442,7 +442,7 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
     if ctl.ws == 1:
         cc["roofline"] = hbm_roofline(st["algorithmic_bytes"], cc_ms, "ConnectedComponent run (uf_* kernels + "
                                       "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
-                                      "86 B per row with an edge (union-find passes + BFS start), 12 B per entry "
+                                      "58 B per row with an edge (union-find passes + BFS start), 12 B per entry "
                                       "linked in the second round, 4 B per entry of the rows the BFS reached "
                                       "(jg_cc.hip cc_union_find)")
     else:

@@ -263,6 +263,38 @@ __global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict_
     }
 }
 
+// One shard, k = 1: the first round without atomics.  Every row hooks under its first neighbour when
+// that neighbour has the smaller index (a plain store of the row's own entry: the parents then all point
+// to smaller indices, a forest), the rest keep themselves; uf_link_up_compress_kernel then links the
+// rows whose first neighbour has the larger index (rows are degree-sorted and the columns ascending, so
+// nearly every row's first neighbour is a hub of smaller index: only the local degree maxima are left).
+// The union of the two is the first round's: every row joined to its first neighbour.  Fuses uf_init.
+__global__ void uf_hook_first_kernel(int32_t* __restrict__ parent, int32_t* __restrict__ minr,
+                                     const int32_t* __restrict__ first, int64_t rows) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = first[v];
+        parent[v] = u >= 0 && u < (int32_t)v ? u : (int32_t)v;
+        minr[v] = INT_MAX;
+    }
+}
+
+// The rest of the first round (rows whose first neighbour has the larger index) and the compression in
+// one pass.  A row's compression stores its root only when the row is no root itself: a root's entry is
+// only ever written by a hook's atomicCAS, so no plain store can undo a concurrent hook, and a non-root
+// stays one.  A root found here may be hooked later in the pass, so the entries end up pointing at
+// ancestors, not always roots: the finds that follow (rest links, minimum ranks) walk what is left.
+__global__ void uf_link_up_compress_kernel(int32_t* parent, const int32_t* __restrict__ first, int64_t rows) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = first[v];
+        if (u > (int32_t)v) uf_link(parent, (int32_t)v, u);
+        const int32_t p = parent[v];
+        if (p != (int32_t)v) {
+            const int32_t r = uf_find(parent, p);
+            if (r != p) parent[v] = r;
+        }
+    }
+}
+
 // Vertices outside the sampled giant component link their remaining neighbours (an edge between the
 // giant component and another vertex is linked from the other side).  Rows are degree-sorted: rows
 // below `heavy` (degree >= 64) take a wave each, the others a thread.
@@ -277,7 +309,8 @@ __global__ __launch_bounds__(kRedThreads) void uf_link_rest_kernel(int32_t* pare
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
     for (int64_t v = wave; v < heavy; v += nwaves) {  // wave-uniform
-        if (uf_find(parent, (int32_t)v) == giant) continue;
+        const int32_t p = parent[v];
+        if (p == giant || uf_find(parent, p) == giant) continue;
         if (lane == 0) count += (unsigned long long)(rp[v + 1] - rp[v] - k);
         for (int64_t e = rp[v] + k + lane; e < rp[v + 1]; e += kWave) {
             const int32_t u = col[e];
@@ -286,9 +319,13 @@ __global__ __launch_bounds__(kRedThreads) void uf_link_rest_kernel(int32_t* pare
     }
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
     for (int64_t v = heavy + tid; v < rows; v += nt) {
-        if (rp[v + 1] - rp[v] <= k || uf_find(parent, (int32_t)v) == giant) continue;
-        count += (unsigned long long)(rp[v + 1] - rp[v] - k);
-        for (int64_t e = rp[v] + k; e < rp[v + 1]; ++e) {
+        // the giant test first: the rows of the giant component (nearly all) then never read row_ptr
+        const int32_t p = parent[v];
+        if (p == giant || uf_find(parent, p) == giant) continue;
+        const int64_t e0 = rp[v], e1 = rp[v + 1];
+        if (e1 - e0 <= k) continue;
+        count += (unsigned long long)(e1 - e0 - k);
+        for (int64_t e = e0 + k; e < e1; ++e) {
             const int32_t u = col[e];
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
@@ -308,14 +345,18 @@ __global__ void uf_sample_kernel(const int32_t* __restrict__ parent, int64_t row
 }
 
 // minr[root] = the smallest rank of the root's component: the giant component through a block
-// reduction (one atomic per block), the others with an atomicMin each (small components).
-__global__ __launch_bounds__(kRedThreads) void uf_minrank_kernel(const int32_t* __restrict__ parent,
-                                                                  const int32_t* __restrict__ rank, int64_t rows,
-                                                                  int32_t giant, int32_t* __restrict__ minr) {
+// reduction (one atomic per block), the others with an atomicMin each (small components).  The final
+// path compression rides along: each row finds its root and stores it when it differs (no hook runs
+// here, so a concurrent find reading a rewritten entry still meets an ancestor).
+__global__ __launch_bounds__(kRedThreads) void uf_minrank_kernel(int32_t* parent, const int32_t* __restrict__ rank,
+                                                                  int64_t rows, int32_t giant,
+                                                                  int32_t* __restrict__ minr) {
     __shared__ int32_t red[kRedWaves];
     int32_t g = INT_MAX;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t r = parent[v], k = rank[v];
+        const int32_t p = parent[v], k = rank[v];
+        const int32_t r = uf_find(parent, p);  // not `p == giant`: the rest links may have hooked it
+        if (r != p) parent[v] = r;
         if (r == giant) g = k < g ? k : g;
         else atomicMin(&minr[r], k);
     }
@@ -338,9 +379,12 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // The union-find runs over the rows that have an edge (those before Csr::empty_from): an edgeless row
 // is its own component, with its own rank as label, and is never linked.
 // *work_bytes: the bytes the passes need (the §8d-style model of this algorithm): per row
-// with an edge 86 B (init 8, first links 8: the dense first column and the parent probe, two compressions
-// 16, rest-link scan 12, minimum rank 8, BFS start 29, BFS depth and seen 5), 12 B per entry linked in the
-// second round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.
+// with an edge 58 B (first hooks 12: the dense first column, the parent and minimum-rank initial values;
+// the remaining first links with the first compression 8: the first column again and the parent;
+// rest-link giant test 4; minimum rank with the second compression 8; BFS start 21: rank, parent, the
+// component minimum, depth, label and seen; BFS depth and seen 5), 12 B per entry linked in the second
+// round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.  k > 1 (Tune::cc_first)
+// runs the atomic first round of uf_link_first_kernel instead, under the same model.
 bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, double* work_bytes) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
@@ -361,13 +405,20 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     DevBuf<unsigned long long> linked(1);
     JG_HIP(hipMemsetAsync(linked.get(), 0, sizeof(unsigned long long), s));
     const int32_t* rank = sh.cc_rank0.get();  // the initial labels are the ranks (cc_prepare_ranks)
-    uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
-    JG_LAUNCH_CHECK();
-    uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), c.first_col.get(), ne,
-                                                         kFirst);
-    JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
-    JG_LAUNCH_CHECK();
+    if (kFirst == 1 && c.first_col.get()) {
+        uf_hook_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, c.first_col.get(), ne);
+        JG_LAUNCH_CHECK();
+        uf_link_up_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.first_col.get(), ne);
+        JG_LAUNCH_CHECK();
+    } else {
+        uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
+        JG_LAUNCH_CHECK();
+        uf_link_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), c.first_col.get(),
+                                                             ne, kFirst);
+        JG_LAUNCH_CHECK();
+        uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
+        JG_LAUNCH_CHECK();
+    }
     // the most frequent root among 1024 sampled vertices: the giant component's
     uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, std::max<int64_t>(ne, 1), 1024, sample.get());
     JG_LAUNCH_CHECK();
@@ -392,8 +443,6 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     uf_link_rest_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
                                                              giant, linked.get());
     JG_LAUNCH_CHECK();
-    uf_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, ne);
-    JG_LAUNCH_CHECK();
     uf_minrank_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
     // the BFS start picks the sources and rewrites parent into the labels
@@ -403,7 +452,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     if (it > kCcMaxIterations - 1) return false;
     unsigned long long rest = 0;
     copy_d2h(&rest, linked.get(), sizeof rest, s);
-    *work_bytes = 86.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
+    *work_bytes = 58.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
     *iterations = it;
     *labels = parent;
     return true;

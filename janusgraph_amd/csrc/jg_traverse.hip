@@ -546,15 +546,21 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
         int64_t deg = 0;
         if (v < rows) {
             int32_t lab = r.rank[v];
+            bool least = true;
             if (v < r.ne) {
-                deg = deg_rp[v + 1] - deg_rp[v];
                 const int32_t m = r.minr[r.parent[v]];
-                take = deg > 0 && lab == m;
+                least = lab == m;
+                // A row whose component minimum is another row has an edge, so only the component minima
+                // read the row pointers: an edgeless row is its own singleton component.
+                if (least) {
+                    deg = deg_rp[v + 1] - deg_rp[v];
+                    take = deg > 0;
+                }
                 lab = m;
                 depth[v] = take ? 0 : -1;  // only the traversal reads the depths: the edgeless rows need none
             }
             r.parent[v] = lab;
-            seen[v] = take || deg == 0;  // BOTH: push and pull rows are the same (bfs_init_kernel)
+            seen[v] = least;  // = take || deg == 0; BOTH: push and pull rows are the same (bfs_init_kernel)
         }
         app.append(take, (int32_t)v, deg, queue, qoff, packed);
     }

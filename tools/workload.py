@@ -21,8 +21,9 @@ import bench  # noqa: E402
 # kernels of each workload's timed region (name substrings; tools/pmc_summary.py filters on them)
 KERNELS = {
     "bfs": ["bfs_init_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
-    "cc": ["uf_init_kernel", "uf_link_first_kernel", "uf_link_rest_kernel", "uf_compress_kernel", "uf_sample_kernel",
-           "uf_minrank_kernel", "heavy_rows_kernel", "bfs_init_roots_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
+    "cc": ["uf_init_kernel", "uf_link_first_kernel", "uf_hook_first_kernel", "uf_link_up_compress_kernel",
+           "uf_link_rest_kernel", "uf_compress_kernel", "uf_sample_kernel", "uf_minrank_kernel",
+           "heavy_rows_kernel", "bfs_init_roots_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
     "msbfs": ["MsBfsOp", "msbfs_live_kernel", "msbfs_scan_kernel", "msbfs_todo_kernel", "msbfs_task_live_kernel",
               "msbfs_init_kernel", "msbfs_frontier_kernel", "msbfs_source_queue_kernel", "msbfs_td_kernel",
               "msbfs_td_apply_kernel", "msbfs_zero_list_kernel", "msbfs_td_recv_kernel", "msbfs_td_record_kernel",
