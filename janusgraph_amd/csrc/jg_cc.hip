@@ -236,6 +236,42 @@ __device__ __forceinline__ void uf_link(int32_t* parent, int32_t a, int32_t b) {
     }
 }
 
+// Four rows per thread for the streaming union-find passes: 16-byte loads put four times the bytes in
+// flight per lane, and the four finds walk in lock step, one dependent load per step for all four (one
+// row per lane left these passes bound by load latency: 4.5 TB/s at best, RMAT-26).
+constexpr int kQuad = 4;
+__device__ __forceinline__ void uf_find4(const int32_t* parent, int32_t (&x)[kQuad]) {
+    bool act[kQuad];
+#pragma unroll
+    for (int k = 0; k < kQuad; ++k) act[k] = true;
+    for (;;) {
+        int32_t y[kQuad];
+#pragma unroll
+        for (int k = 0; k < kQuad; ++k) y[k] = act[k] ? parent[x[k]] : x[k];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < kQuad; ++k) {
+            if (y[k] == x[k]) act[k] = false;
+            else {
+                x[k] = y[k];
+                any = true;
+            }
+        }
+        if (!any) return;
+    }
+}
+// the four entries of a[v0, v0 + 4) (16-byte aligned when v0 is a multiple of 4: DevBuf bases are)
+__device__ __forceinline__ void load4(const int32_t* a, int64_t v0, int32_t (&x)[kQuad]) {
+    const int4 q = *reinterpret_cast<const int4*>(a + v0);
+    x[0] = q.x;
+    x[1] = q.y;
+    x[2] = q.z;
+    x[3] = q.w;
+}
+__device__ __forceinline__ void store4(int32_t* a, int64_t v0, const int32_t (&x)[kQuad]) {
+    *reinterpret_cast<int4*>(a + v0) = make_int4(x[0], x[1], x[2], x[3]);
+}
+
 __global__ void uf_init_kernel(int32_t* __restrict__ parent, int32_t* __restrict__ minr, int64_t rows) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
         parent[v] = (int32_t)v;
@@ -271,10 +307,23 @@ __global__ void uf_link_first_kernel(int32_t* parent, const int64_t* __restrict_
 // The union of the two is the first round's: every row joined to its first neighbour.  Fuses uf_init.
 __global__ void uf_hook_first_kernel(int32_t* __restrict__ parent, int32_t* __restrict__ minr,
                                      const int32_t* __restrict__ first, int64_t rows) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t u = first[v];
-        parent[v] = u >= 0 && u < (int32_t)v ? u : (int32_t)v;
-        minr[v] = INT_MAX;
+    const int64_t quads = (rows + kQuad - 1) / kQuad;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v0 = q * kQuad;
+        if (v0 + kQuad <= rows) {
+            int32_t u[kQuad], p[kQuad];
+            load4(first, v0, u);
+#pragma unroll
+            for (int k = 0; k < kQuad; ++k) p[k] = u[k] >= 0 && u[k] < (int32_t)(v0 + k) ? u[k] : (int32_t)(v0 + k);
+            store4(parent, v0, p);
+            *reinterpret_cast<int4*>(minr + v0) = make_int4(INT_MAX, INT_MAX, INT_MAX, INT_MAX);
+        } else {
+            for (int64_t v = v0; v < rows; ++v) {
+                const int32_t u = first[v];
+                parent[v] = u >= 0 && u < (int32_t)v ? u : (int32_t)v;
+                minr[v] = INT_MAX;
+            }
+        }
     }
 }
 
@@ -284,13 +333,31 @@ __global__ void uf_hook_first_kernel(int32_t* __restrict__ parent, int32_t* __re
 // stays one.  A root found here may be hooked later in the pass, so the entries end up pointing at
 // ancestors, not always roots: the finds that follow (rest links, minimum ranks) walk what is left.
 __global__ void uf_link_up_compress_kernel(int32_t* parent, const int32_t* __restrict__ first, int64_t rows) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t u = first[v];
-        if (u > (int32_t)v) uf_link(parent, (int32_t)v, u);
-        const int32_t p = parent[v];
-        if (p != (int32_t)v) {
-            const int32_t r = uf_find(parent, p);
-            if (r != p) parent[v] = r;
+    const int64_t quads = (rows + kQuad - 1) / kQuad;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v0 = q * kQuad;
+        if (v0 + kQuad <= rows) {
+            int32_t u[kQuad], p[kQuad], r[kQuad];
+            load4(first, v0, u);
+            for (int k = 0; k < kQuad; ++k)  // (rare: the local degree maxima)
+                if (u[k] > (int32_t)(v0 + k)) uf_link(parent, (int32_t)(v0 + k), u[k]);
+            load4(parent, v0, p);  // after the links: a row's own hook shows in its entry
+#pragma unroll
+            for (int k = 0; k < kQuad; ++k) r[k] = p[k];
+            uf_find4(parent, r);
+#pragma unroll
+            for (int k = 0; k < kQuad; ++k)
+                if (p[k] != (int32_t)(v0 + k) && r[k] != p[k]) parent[v0 + k] = r[k];
+        } else {
+            for (int64_t v = v0; v < rows; ++v) {
+                const int32_t u = first[v];
+                if (u > (int32_t)v) uf_link(parent, (int32_t)v, u);
+                const int32_t p = parent[v];
+                if (p != (int32_t)v) {
+                    const int32_t r = uf_find(parent, p);
+                    if (r != p) parent[v] = r;
+                }
+            }
         }
     }
 }
@@ -317,17 +384,33 @@ __global__ __launch_bounds__(kRedThreads) void uf_link_rest_kernel(int32_t* pare
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
         }
     }
+    // light rows four per thread, from the first multiple of four at or past `heavy` (the rows between
+    // take a thread each below): the giant test first, so the rows of the giant component (nearly all)
+    // never read row_ptr
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t v = heavy + tid; v < rows; v += nt) {
-        // the giant test first: the rows of the giant component (nearly all) then never read row_ptr
-        const int32_t p = parent[v];
-        if (p == giant || uf_find(parent, p) == giant) continue;
+    const int64_t h4 = (heavy + kQuad - 1) / kQuad * kQuad;
+    auto light = [&](int64_t v, int32_t p) {
+        if (p == giant || uf_find(parent, p) == giant) return;
         const int64_t e0 = rp[v], e1 = rp[v + 1];
-        if (e1 - e0 <= k) continue;
+        if (e1 - e0 <= k) return;
         count += (unsigned long long)(e1 - e0 - k);
         for (int64_t e = e0 + k; e < e1; ++e) {
             const int32_t u = col[e];
             if (u != (int32_t)v) uf_link(parent, (int32_t)v, u);
+        }
+    };
+    for (int64_t v = heavy + tid; v < h4 && v < rows; v += nt) light(v, parent[v]);
+    const int64_t quads = (rows - h4 + kQuad - 1) / kQuad;
+    for (int64_t q = tid; q < quads; q += nt) {
+        const int64_t v0 = h4 + q * kQuad;
+        if (v0 + kQuad <= rows) {
+            int32_t p[kQuad];
+            load4(parent, v0, p);
+            if (p[0] == giant && p[1] == giant && p[2] == giant && p[3] == giant) continue;
+#pragma unroll
+            for (int j = 0; j < kQuad; ++j) light(v0 + j, p[j]);
+        } else {
+            for (int64_t v = v0; v < rows; ++v) light(v, parent[v]);
         }
     }
     count = block_reduce(count, AddU64{}, red);  // one atomic per block: nearly every wave links something
@@ -353,12 +436,31 @@ __global__ __launch_bounds__(kRedThreads) void uf_minrank_kernel(int32_t* parent
                                                                   int32_t* __restrict__ minr) {
     __shared__ int32_t red[kRedWaves];
     int32_t g = INT_MAX;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < rows; v += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t p = parent[v], k = rank[v];
-        const int32_t r = uf_find(parent, p);  // not `p == giant`: the rest links may have hooked it
-        if (r != p) parent[v] = r;
-        if (r == giant) g = k < g ? k : g;
-        else atomicMin(&minr[r], k);
+    const int64_t quads = (rows + kQuad - 1) / kQuad;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v0 = q * kQuad;
+        if (v0 + kQuad <= rows) {
+            int32_t p[kQuad], r[kQuad], k[kQuad];
+            load4(parent, v0, p);
+            load4(rank, v0, k);
+#pragma unroll
+            for (int j = 0; j < kQuad; ++j) r[j] = p[j];
+            uf_find4(parent, r);  // not `p == giant`: the rest links may have hooked it
+#pragma unroll
+            for (int j = 0; j < kQuad; ++j) {
+                if (r[j] != p[j]) parent[v0 + j] = r[j];
+                if (r[j] == giant) g = k[j] < g ? k[j] : g;
+                else atomicMin(&minr[r[j]], k[j]);
+            }
+        } else {
+            for (int64_t v = v0; v < rows; ++v) {
+                const int32_t p = parent[v], k = rank[v];
+                const int32_t r = uf_find(parent, p);
+                if (r != p) parent[v] = r;
+                if (r == giant) g = k < g ? k : g;
+                else atomicMin(&minr[r], k);
+            }
+        }
     }
     g = block_reduce(g, MinI32{}, red);
     if (threadIdx.x == 0 && g != INT_MAX) atomicMin(&minr[giant], g);
@@ -406,9 +508,9 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     JG_HIP(hipMemsetAsync(linked.get(), 0, sizeof(unsigned long long), s));
     const int32_t* rank = sh.cc_rank0.get();  // the initial labels are the ranks (cc_prepare_ranks)
     if (kFirst == 1 && c.first_col.get()) {
-        uf_hook_first_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, c.first_col.get(), ne);
+        uf_hook_first_kernel<<<grid_for((ne + kQuad - 1) / kQuad), kBlock, 0, s>>>(parent, minr, c.first_col.get(), ne);
         JG_LAUNCH_CHECK();
-        uf_link_up_compress_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, c.first_col.get(), ne);
+        uf_link_up_compress_kernel<<<grid_for((ne + kQuad - 1) / kQuad), kBlock, 0, s>>>(parent, c.first_col.get(), ne);
         JG_LAUNCH_CHECK();
     } else {
         uf_init_kernel<<<grid_for(ne), kBlock, 0, s>>>(parent, minr, ne);
@@ -443,7 +545,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     uf_link_rest_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
                                                              giant, linked.get());
     JG_LAUNCH_CHECK();
-    uf_minrank_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, rank, ne, giant, minr);
+    uf_minrank_kernel<<<red_grid((ne + kQuad - 1) / kQuad), kRedThreads, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
     // the BFS start picks the sources and rewrites parent into the labels
     double reached = 0;

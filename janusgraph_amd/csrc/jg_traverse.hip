@@ -537,32 +537,69 @@ __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restr
                                                                 const int64_t* __restrict__ deg_rp, int32_t* queue,
                                                                 int64_t* qoff, unsigned long long* packed,
                                                                 uint8_t* __restrict__ seen) {
+    // Four rows per thread (16-byte loads and stores: one row per lane left the pass bound by load
+    // latency, 218 us at RMAT-26).  A row whose component minimum is another row has an edge, so only
+    // the component minima read the row pointers: an edgeless row is its own singleton component.
+    constexpr int kQ = 4;
     __shared__ WaveStage ws;
     WaveApp app{ws};
+    const int64_t quads = (rows + kQ - 1) / kQ;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
-        const int64_t v = x0 + threadIdx.x;
-        bool take = false;
-        int64_t deg = 0;
-        if (v < rows) {
-            int32_t lab = r.rank[v];
-            bool least = true;
-            if (v < r.ne) {
-                const int32_t m = r.minr[r.parent[v]];
-                least = lab == m;
-                // A row whose component minimum is another row has an edge, so only the component minima
-                // read the row pointers: an edgeless row is its own singleton component.
-                if (least) {
-                    deg = deg_rp[v + 1] - deg_rp[v];
-                    take = deg > 0;
-                }
-                lab = m;
-                depth[v] = take ? 0 : -1;  // only the traversal reads the depths: the edgeless rows need none
+    for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x; q0 < quads; q0 += stride) {  // block-uniform trips
+        const int64_t q = q0 + threadIdx.x, v0 = q * kQ;
+        bool take[kQ] = {false, false, false, false};
+        int64_t deg[kQ] = {0, 0, 0, 0};
+        if (q < quads) {
+            int32_t lab[kQ], par[kQ], dep[kQ];
+            uint8_t sn[kQ];
+            const bool full = v0 + kQ <= rows, in = v0 + kQ <= r.ne;
+            if (full) {
+                const int4 x = *reinterpret_cast<const int4*>(r.rank + v0);
+                lab[0] = x.x, lab[1] = x.y, lab[2] = x.z, lab[3] = x.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < kQ; ++k) lab[k] = v0 + k < rows ? r.rank[v0 + k] : 0;
             }
-            r.parent[v] = lab;
-            seen[v] = least;  // = take || deg == 0; BOTH: push and pull rows are the same (bfs_init_kernel)
+            if (in) {
+                const int4 x = *reinterpret_cast<const int4*>(r.parent + v0);
+                par[0] = x.x, par[1] = x.y, par[2] = x.z, par[3] = x.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < kQ; ++k) par[k] = v0 + k < r.ne ? r.parent[v0 + k] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kQ; ++k) {
+                const int64_t v = v0 + k;
+                bool least = true;
+                dep[k] = -1;
+                if (v < r.ne) {
+                    const int32_t m = r.minr[par[k]];
+                    least = lab[k] == m;
+                    if (least) {
+                        deg[k] = deg_rp[v + 1] - deg_rp[v];
+                        take[k] = deg[k] > 0;
+                    }
+                    lab[k] = m;
+                    dep[k] = take[k] ? 0 : -1;  // only the traversal reads the depths: the edgeless rows need none
+                }
+                sn[k] = least;  // = take || deg == 0; BOTH: push and pull rows are the same (bfs_init_kernel)
+            }
+            if (full) {
+                *reinterpret_cast<int4*>(r.parent + v0) = make_int4(lab[0], lab[1], lab[2], lab[3]);
+                *reinterpret_cast<uint32_t*>(seen + v0) =
+                    (uint32_t)sn[0] | (uint32_t)sn[1] << 8 | (uint32_t)sn[2] << 16 | (uint32_t)sn[3] << 24;
+            } else {
+                for (int k = 0; k < kQ && v0 + k < rows; ++k) {
+                    r.parent[v0 + k] = lab[k];
+                    seen[v0 + k] = sn[k];
+                }
+            }
+            if (in) *reinterpret_cast<int4*>(depth + v0) = make_int4(dep[0], dep[1], dep[2], dep[3]);
+            else
+                for (int k = 0; k < kQ && v0 + k < r.ne; ++k) depth[v0 + k] = dep[k];
         }
-        app.append(take, (int32_t)v, deg, queue, qoff, packed);
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) app.append(take[k], (int32_t)(v0 + k), deg[k], queue, qoff, packed);
     }
     app.final(queue, qoff, packed);
 }
@@ -1576,7 +1613,7 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         BfsState s0{};
         s0.mu = (long long)degcsr->nnz;
         copy_h2d(st + kBfsRing - 1, &s0, sizeof s0, s);
-        bfs_init_roots_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, *roots, degcsr->row_ptr.get(),
+        bfs_init_roots_kernel<<<grid_for((rows + 3) / 4), kBlock, 0, s>>>(depth, rows, *roots, degcsr->row_ptr.get(),
                                                                 sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
                                                                 sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
     } else {
