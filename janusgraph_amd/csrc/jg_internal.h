@@ -40,6 +40,10 @@ struct Csr {
     // each row's first column (-1: empty row), built on a traversal's first use (bfs_first_col): a
     // bottom-up level probes it with one coalesced load instead of a row_ptr pair and a scattered column
     mutable DevBuf<int32_t> first_col;
+    // weight statistics (smallest, sum, count of the non-absent weights), computed on the first weighted
+    // shortest distance that needs them (sd_weight_stats)
+    mutable long long wstat[3] = {0, 0, 0};
+    mutable bool wstat_ok = false;
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
 };
@@ -638,6 +642,9 @@ struct Tune {
                                       //         (measured slower, profiles/r05/persistent/):
                                       //         0 off, 1 at the level grid, N > 1 at N workgroups (capped at the
                                       //         co-resident count)
+    int sd_delta = -1;                // weighted shortest distance with an unbounded hop count (maxDepth >= rows - 1)
+                                      // and no negative weight: near-far delta-stepping with this delta (-1:
+                                      // automatic, 0: the frontier Bellman-Ford supersteps)
     int merge_temporal = 1;           // merge blocks sweep their XCD's sub-slices one at a time (L2 locality):
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct

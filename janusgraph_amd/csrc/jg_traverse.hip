@@ -1379,49 +1379,6 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_rows_kernel(int64_t row
 // An edge without the weight property carries kWeightAbsent: a message crossing it is an error, as
 // in Fulgora; distances may be negative, so an absent DISTANCE is reported as INT64_MIN.
 constexpr int32_t kWeightAbsent = INT32_MIN;
-__global__ __launch_bounds__(kBlock) void sd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                         const int32_t* __restrict__ wt,
-                                                         const int32_t* __restrict__ frontier, int64_t fsize,
-                                                         const long long* __restrict__ msg, long long* __restrict__ best,
-                                                         int32_t* __restrict__ touched,
-                                                         unsigned long long* __restrict__ tsize,
-                                                         int32_t* __restrict__ err) {
-    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
-    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
-    const int sub = threadIdx.x % kTdLanes;
-    const int64_t iters = (fsize + ngroups - 1) / ngroups;
-    for (int64_t it = 0; it < iters; ++it) {
-        const int64_t qi = group + it * ngroups;
-        const bool have = qi < fsize;
-        const int32_t w = have ? frontier[qi] : 0;
-        const int64_t j0 = have ? rp[w] : 0, j1 = have ? rp[w + 1] : 0;
-        const long long mw = have ? msg[w] : 0;
-        const int64_t len = j1 - j0;
-        int64_t maxlen = len;
-#pragma unroll
-        for (int o = kTdLanes; o < kWave; o <<= 1) {
-            const int64_t t = __shfl_xor(maxlen, o, kWave);
-            maxlen = t > maxlen ? t : maxlen;
-        }
-        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
-            const int64_t k = k0 + sub;
-            bool first = false;
-            int32_t u = 0;
-            if (k < len) {
-                u = col[j0 + k];
-                const int32_t wk = wt ? wt[j0 + k] : 1;
-                if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
-                    *err = 1;
-                } else {
-                    const long long old = atomicMin(&best[u], mw + (long long)wk);
-                    first = old == LLONG_MAX;
-                }
-            }
-            wave_append(first, u, touched, tsize);
-        }
-    }
-}
-
 __global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsize, long long* __restrict__ best,
                                 long long* __restrict__ dist, long long* __restrict__ msg,
                                 int32_t* __restrict__ next_frontier, unsigned long long* __restrict__ nsize) {
@@ -1444,7 +1401,257 @@ __global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsi
     }
 }
 
-// Sharded SD push: like sd_push_kernel, but the columns are compact ids of the IN halo plan (own rows
+// One shard: the same superstep edge-balanced.  The frontier carries each row's first edge number
+// (qoff), and each thread takes kTdEdgesPerThread consecutive edges of the whole frontier after one
+// binary search, so a hub row's 10^5 in-entries are spread over the grid instead of holding one lane
+// group for the superstep (RMAT-20, weights 1..255, unbounded: 15.8 ms with the lane groups).
+struct SdPush {
+    const int64_t* rp;
+    const int32_t* col;
+    const int32_t* wt;
+    const int32_t* frontier;
+    const int64_t* qoff;
+    int64_t nq, mf;
+    const long long* msg;
+    long long* best;
+    int32_t* touched;
+    unsigned long long* tsize;
+    int32_t* err;
+};
+__global__ __launch_bounds__(kBlock) void sd_push_q_kernel(SdPush a) {
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+        }
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
+            bool first = false;
+            int32_t u = 0;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                }
+                const int32_t w = a.frontier[i];
+                const int64_t j = a.rp[w] + (e - a.qoff[i]);
+                u = a.col[j];
+                const int32_t wk = a.wt ? a.wt[j] : 1;
+                if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
+                    *a.err = 1;
+                } else {
+                    const long long cand = a.msg[w] + (long long)wk;
+                    // a read first (past L1, as in sd_near_kernel): a candidate no better than the best so far
+                    // takes no atomic
+                    if (cand < __hip_atomic_load(&a.best[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        first = atomicMin(&a.best[u], cand) == LLONG_MAX;
+                }
+            }
+            wave_append(first, u, a.touched, a.tsize);
+        }
+    }
+}
+
+// sd_apply_kernel with the next frontier's first edge numbers (for sd_push_q_kernel)
+__global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(const int32_t* __restrict__ touched, int64_t tsize,
+                                                            long long* __restrict__ best, long long* __restrict__ dist,
+                                                            long long* __restrict__ msg, const int64_t* __restrict__ rp,
+                                                            int32_t* next_frontier, int64_t* next_qoff,
+                                                            unsigned long long* packed) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tsize; x0 += stride) {  // block-uniform trips
+        const int64_t i = x0 + threadIdx.x;
+        bool improved = false;
+        int32_t u = 0;
+        int64_t du = 0;
+        if (i < tsize) {
+            u = touched[i];
+            const long long b = best[u];
+            best[u] = LLONG_MAX;
+            if (dist[u] == LLONG_MIN || dist[u] > b) {
+                dist[u] = b;
+                msg[u] = b;
+                improved = true;
+                du = rp[u + 1] - rp[u];
+            }
+        }
+        app.append(improved, u, du, next_frontier, next_qoff, packed);
+    }
+    app.final(next_frontier, next_qoff, packed);
+}
+
+// ---------------- weighted shortest distance, unbounded hops (near-far delta-stepping) ----------------
+// When the hop bound cannot bind (maxDepth >= rows - 1) and no weight is negative, the hop-bounded
+// minimum is the plain shortest distance (a shortest path can be taken simple: <= rows - 1 hops), so
+// the supersteps can be replaced by delta-stepping (Meyer & Sanders; the GPU
+// near-far pile of Davidson et al.): the rows below the threshold T are relaxed pass by pass (the near
+// queue), the rest wait in a far pile, and T rises by delta once the near queue is empty.  The frontier
+// Bellman-Ford above re-relaxes a row every time a longer-hop path improves it; here a row is relaxed
+// only while its distance is below T, so most rows are relaxed once.  The reported distances are the
+// Bellman-Ford ones bit for bit (integers, a min); an absent weight on an edge out of a reached row
+// fails the run as there (every reached row is relaxed at least once, at its final distance).
+// Queues hold each row at most once: near entries by a pass stamp, far entries by a flag.
+struct SdNear {
+    const int64_t* rp;
+    const int32_t* col;
+    const int32_t* wt;
+    const int32_t* near;  // the pass's rows and their first edge numbers (edge-balanced: hub rows of
+    const int64_t* qoff;  // 10^5 entries would otherwise hold one lane group for the whole pass)
+    int64_t nq, mf;       // rows, edges
+    long long* dist;      // LLONG_MAX: unreached
+    long long T;
+    int32_t* stamp;
+    int32_t pass;
+    int32_t* near_next;
+    int64_t* qoff_next;
+    unsigned long long* packed;  // near_next: (rows << kPackShift) | edges
+    int32_t* far_flag;
+    int32_t* far;
+    unsigned long long* far_size;
+    int32_t* err;
+};
+__global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear a) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+        }
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
+            bool to_near = false, to_far = false;
+            int32_t u = 0;
+            int64_t du = 0;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                }
+                const int32_t w = a.near[i];
+                const int64_t j = a.rp[w] + (e - a.qoff[i]);
+                u = a.col[j];
+                const int32_t wk = a.wt ? a.wt[j] : 1;
+                if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
+                    *a.err = 1;
+                } else {
+                    // dist[w] now: it only fell since w was queued
+                    const long long nd = a.dist[w] + (long long)wk;
+                    // the prefilter reads past L1 (agent scope): a hub row's entry is hit from every XCD at
+                    // once, and a stale L1 copy would send each of those lanes to the atomic
+                    if (nd < __hip_atomic_load(&a.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                        nd < atomicMin(&a.dist[u], nd)) {
+                        if (nd < a.T) {
+                            to_near = atomicExch(&a.stamp[u], a.pass) != a.pass;
+                            if (to_near) du = a.rp[u + 1] - a.rp[u];
+                        } else {
+                            to_far = atomicExch(&a.far_flag[u], 1) == 0;
+                        }
+                    }
+                }
+            }
+            app.append(to_near, u, du, a.near_next, a.qoff_next, a.packed);
+            wave_append(to_far, u, a.far, a.far_size);
+        }
+    }
+    app.final(a.near_next, a.qoff_next, a.packed);
+}
+
+// The far pile at a threshold change: rows now below T go to the near queue, rows below the previous
+// threshold were relaxed at their final distance already (dropped), the others stay; *minkept gets the
+// smallest distance kept (the next threshold when the near queue comes out empty).
+__global__ __launch_bounds__(kBlock) void sd_far_split_kernel(const int32_t* __restrict__ far, int64_t fsize,
+                                                              const long long* __restrict__ dist,
+                                                              const int64_t* __restrict__ rp, long long t_prev,
+                                                              long long T, int32_t* __restrict__ far_flag,
+                                                              int32_t* near, int64_t* qoff, unsigned long long* packed,
+                                                              int32_t* __restrict__ far_next,
+                                                              unsigned long long* __restrict__ far_size,
+                                                              unsigned long long* __restrict__ minkept) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long mk = ULLONG_MAX;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < fsize; x0 += stride) {  // block-uniform trips
+        const int64_t i = x0 + threadIdx.x;
+        bool to_near = false, keep = false;
+        int32_t u = 0;
+        int64_t du = 0;
+        if (i < fsize) {
+            u = far[i];
+            const long long d = dist[u];
+            keep = d >= T;
+            to_near = !keep && d >= t_prev;
+            if (keep) mk = (unsigned long long)d < mk ? (unsigned long long)d : mk;
+            else far_flag[u] = 0;
+            if (to_near) du = rp[u + 1] - rp[u];
+        }
+        app.append(to_near, u, du, near, qoff, packed);
+        wave_append(keep, u, far_next, far_size);
+    }
+    app.final(near, qoff, packed);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(mk, o, kWave);
+        mk = t < mk ? t : mk;
+    }
+    if (lane_id() == 0 && mk != ULLONG_MAX) atomicMin(minkept, mk);
+}
+
+// Weight statistics of a CSR for the delta-stepping gate and its automatic delta: [0] the smallest
+// weight, [1] the sum, [2] the count (absent weights excluded).
+__global__ void sd_weight_stats_kernel(const int32_t* __restrict__ wt, int64_t nnz, long long* __restrict__ out) {
+    long long mn = LLONG_MAX, sum = 0, cnt = 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t w = wt[j];
+        if (w == kWeightAbsent) continue;
+        mn = w < mn ? w : mn;
+        sum += w;
+        ++cnt;
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const long long a = __shfl_xor(mn, o, kWave);
+        mn = a < mn ? a : mn;
+        sum += __shfl_xor(sum, o, kWave);
+        cnt += __shfl_xor(cnt, o, kWave);
+    }
+    if (lane_id() == 0) {
+        atomicMin(&out[0], mn);
+        atomicAdd((unsigned long long*)&out[1], (unsigned long long)sum);
+        atomicAdd((unsigned long long*)&out[2], (unsigned long long)cnt);
+    }
+}
+
+// Sharded SD push: like sd_push_q_kernel (one lane group per frontier row), but the columns are compact ids of the IN halo plan (own rows
 // in segment 0, peers' vertices in their segments): only own rows enter the touched list; remote
 // candidates wait in the halo slots for the reverse exchange.
 __global__ __launch_bounds__(kBlock) void ssd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
@@ -3470,6 +3677,121 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     ctx.last.supersteps = max_depth;
 }
 
+// The weight statistics of c (sd_weight_stats_kernel), cached on the CSR.
+const long long* sd_weight_stats(Shard& sh, const Csr& c) {
+    if (!c.wstat_ok) {
+        hipStream_t s = sh.stream;
+        DevBuf<long long> out(3);
+        const long long init[3] = {LLONG_MAX, 0, 0};
+        copy_h2d(out.get(), init, sizeof init, s);
+        if (c.nnz > 0 && c.weight.get()) {
+            sd_weight_stats_kernel<<<grid_for(c.nnz), kBlock, 0, s>>>(c.weight.get(), c.nnz, out.get());
+            JG_LAUNCH_CHECK();
+        }
+        copy_d2h(c.wstat, out.get(), sizeof c.wstat, s);
+        c.wstat_ok = true;
+    }
+    return c.wstat;
+}
+
+// delta: Tune::sd_delta when set, else kSdDeltaScale x the mean weight / the mean in-degree, at least 1
+// (the near-far rule of thumb, delta ~ c w / d; RMAT-20 / 22 with weights 1..255 and c = 32, 128: 1.50 /
+// 3.40 and 1.23 / 3.05 ms, c = 512 equal to 128: profiles/r05/sssp/)
+constexpr double kSdDeltaScale = 128.0;
+long long sd_auto_delta(const long long* ws, int64_t nnz, int64_t rows) {
+    if (tune().sd_delta > 0) return tune().sd_delta;
+    const double mean_w = ws[2] > 0 ? (double)ws[1] / (double)ws[2] : 1.0;
+    const double mean_deg = std::max(1.0, (double)nnz / (double)std::max<int64_t>(rows, 1));
+    return std::max<long long>(1, (long long)std::llround(kSdDeltaScale * mean_w / mean_deg));
+}
+
+// Near-far delta-stepping from `seed` over sh.in (see sd_near_kernel); host[] gets the distances
+// (INT64_MIN: absent); end_ev is recorded once the distances are final, before they are copied out.
+// Returns the near passes run.
+int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, hipEvent_t end_ev) {
+    hipStream_t s = sh.stream;
+    const int64_t rows = sh.rows, cap = std::max<int64_t>(rows, 1);
+    const Csr& c = sh.in;
+    DevBuf<long long> dist(cap);
+    DevBuf<int32_t> nq[2] = {DevBuf<int32_t>(cap), DevBuf<int32_t>(cap)};
+    DevBuf<int64_t> qo[2] = {DevBuf<int64_t>(cap), DevBuf<int64_t>(cap)};
+    DevBuf<int32_t> far[2] = {DevBuf<int32_t>(cap), DevBuf<int32_t>(cap)};
+    DevBuf<int32_t> stamp(cap), far_flag(cap), err(1);
+    DevBuf<unsigned long long> ctr(3);  // near packed (rows, edges), far entries, the smallest distance kept
+    fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MAX);
+    JG_LAUNCH_CHECK();
+    JG_HIP(hipMemsetAsync(stamp.get(), 0, rows * sizeof(int32_t), s));
+    JG_HIP(hipMemsetAsync(far_flag.get(), 0, rows * sizeof(int32_t), s));
+    JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
+    const long long zero = 0;
+    const int32_t seed32 = (int32_t)seed;
+    int64_t srp[2];
+    copy_d2h(srp, c.row_ptr.get() + seed, sizeof srp, s);
+    JG_HIP(hipMemcpyAsync(dist.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+    JG_HIP(hipMemcpyAsync(nq[0].get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
+    JG_HIP(hipMemcpyAsync(qo[0].get(), &zero, sizeof zero, hipMemcpyHostToDevice, s));
+    int64_t nsize = 1, medges = srp[1] - srp[0], fsize = 0;
+    int cur = 0, fc = 0;
+    int32_t pass = 0;
+    long long T = delta;  // every row below the previous threshold is final
+    unsigned long long h[3];
+    auto unpack = [&]() {
+        nsize = (int64_t)(h[0] >> kPackShift);
+        medges = (int64_t)(h[0] & kEdgeMask);
+        fsize = (int64_t)h[1];
+    };
+    for (;;) {
+        while (nsize > 0) {  // near passes: relax the rows below T until none falls below it again
+            ++pass;
+            if (medges > 0) {
+                h[0] = 0;
+                h[1] = (unsigned long long)fsize;
+                copy_h2d(ctr.get(), h, 2 * sizeof(unsigned long long), s);
+                SdNear a{c.row_ptr.get(), c.col.get(), c.weight.get(), nq[cur].get(), qo[cur].get(), nsize, medges,
+                         dist.get(), T, stamp.get(), pass, nq[cur ^ 1].get(), qo[cur ^ 1].get(), ctr.get(),
+                         far_flag.get(), far[fc].get(), ctr.get() + 1, err.get()};
+                const unsigned grid = (unsigned)std::min<int64_t>(
+                    std::max<int64_t>((medges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
+                    8192);
+                sd_near_kernel<<<grid, kBlock, 0, s>>>(a);
+                JG_LAUNCH_CHECK();
+                copy_d2h(h, ctr.get(), 2 * sizeof(unsigned long long), s);
+                unpack();
+            } else {
+                nsize = 0;  // rows without entries relax nothing
+            }
+            cur ^= 1;
+        }
+        if (fsize == 0) break;
+        // the next threshold: T + delta, or past the smallest far distance when that bucket is empty
+        long long T2 = T + delta;
+        for (int k = 0; k < 2 && nsize == 0 && fsize > 0; ++k) {
+            h[0] = 0;
+            h[1] = 0;
+            h[2] = ULLONG_MAX;
+            copy_h2d(ctr.get(), h, sizeof h, s);
+            sd_far_split_kernel<<<grid_for(fsize, kBlock, 4096), kBlock, 0, s>>>(
+                far[fc].get(), fsize, dist.get(), c.row_ptr.get(), T, T2, far_flag.get(), nq[cur].get(), qo[cur].get(),
+                ctr.get(), far[fc ^ 1].get(), ctr.get() + 1, ctr.get() + 2);
+            JG_LAUNCH_CHECK();
+            copy_d2h(h, ctr.get(), sizeof h, s);
+            unpack();
+            fc ^= 1;
+            if (nsize == 0 && fsize > 0) T2 = ((long long)h[2] / delta + 1) * delta;
+        }
+        T = T2;
+    }
+    JG_HIP(hipEventRecord(end_ev, s));  // the distances are final: their copy-out is the caller's
+    region_mark(s, false);
+    std::vector<long long> hd(rows);
+    if (rows) copy_d2h(hd.data(), dist.get(), rows * sizeof(long long), s);
+    for (int64_t l = 0; l < rows; ++l) host[l] = hd[l] == LLONG_MAX ? LLONG_MIN : hd[l];
+    int32_t e = 0;
+    copy_d2h(&e, err.get(), sizeof e, s);
+    if (e) fail(JG_ERR_ARG, kMissingWeight);
+    return pass;
+}
+
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
     Ctx& ctx = *g.ctx;
     ctx.last = jg_stats{};
@@ -3493,23 +3815,35 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         bfs_buffers(sh);
         if (sh.out.present()) bfs_first_col(sh, sh.out);  // the traversal's pull adjacency
     }
+    // weighted with an unbounded hop count and no negative weight: delta-stepping (the weight
+    // statistics are taken once per graph, outside the timed region)
+    long long delta = 0;
+    if (seed >= 0 && g.has_weights && tune().sd_delta != 0 && (int64_t)max_depth >= rows - 1) {
+        const long long* ws = sd_weight_stats(sh, sh.in);
+        if (ws[0] >= 0) delta = sd_auto_delta(ws, sh.in.nnz, rows);
+    }
     region_mark(s, true);
     JG_HIP(hipEventRecord(t0, s));
     int levels = 0;
+    bool timed_end = false;  // t1 recorded by the branch (before its output copy)
     if (seed >= 0 && !g.has_weights) {
         // unit weights: min over <= maxDepth-hop paths == BFS depth along IN edges, capped
         DevBuf<int32_t> depth(std::max<int64_t>(rows, 1));
         BfsCsrs c{&sh.in, sh.out.present() ? &sh.out : nullptr};
-        levels = dobfs_single(ctx, sh, c, seed, max_depth, depth.get(), nullptr);
+        levels = dobfs_single(ctx, sh, c, seed, max_depth, depth.get(), nullptr, nullptr, t1);
+        timed_end = true;
         std::vector<int32_t> h(rows);
         if (rows) copy_d2h(h.data(), depth.get(), rows * sizeof(int32_t), s);
         for (int64_t l = 0; l < rows; ++l) host[l] = h[l] >= 0 ? h[l] : LLONG_MIN;
+    } else if (seed >= 0 && delta > 0) {
+        levels = sd_delta_stepping(sh, seed, delta, host.data(), t1);
+        timed_end = true;
     } else if (seed >= 0) {
-        DevBuf<long long> dist(std::max<int64_t>(rows, 1)), msg(std::max<int64_t>(rows, 1)),
-            best(std::max<int64_t>(rows, 1));
-        DevBuf<int32_t> fa(std::max<int64_t>(rows, 1)), fb(std::max<int64_t>(rows, 1)),
-            touched(std::max<int64_t>(rows, 1));
-        DevBuf<unsigned long long> sizes(2);
+        const int64_t cap = std::max<int64_t>(rows, 1);
+        DevBuf<long long> dist(cap), msg(cap), best(cap);
+        DevBuf<int32_t> fa(cap), fb(cap), touched(cap);
+        DevBuf<int64_t> qa(cap), qb(cap);
+        DevBuf<unsigned long long> sizes(2);  // touched rows, the next frontier packed (rows, edges)
         DevBuf<int32_t> err(1);
         JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
         fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MIN);  // absent
@@ -3517,31 +3851,46 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         JG_LAUNCH_CHECK();
         const long long zero = 0;
         const int32_t seed32 = (int32_t)seed;
+        int64_t srp[2];
+        copy_d2h(srp, sh.in.row_ptr.get() + seed, sizeof srp, s);
         JG_HIP(hipMemcpyAsync(dist.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
         JG_HIP(hipMemcpyAsync(msg.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
         JG_HIP(hipMemcpyAsync(fa.get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
-        int64_t fsize = 1;
+        JG_HIP(hipMemcpyAsync(qa.get(), &zero, sizeof zero, hipMemcpyHostToDevice, s));
+        int64_t fsize = 1, fedges = srp[1] - srp[0];
         for (int t = 1; t <= max_depth && fsize > 0; ++t) {
+            if (fedges == 0) {  // the frontier's rows have no entries: the superstep sends nothing
+                fsize = 0;
+                levels = t;
+                break;
+            }
             JG_HIP(hipMemsetAsync(sizes.get(), 0, 2 * sizeof(unsigned long long), s));
-            sd_push_kernel<<<grid_for(fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, s>>>(
-                sh.in.row_ptr.get(), sh.in.col.get(), sh.in.weight.get(), fa.get(), fsize, msg.get(), best.get(),
-                touched.get(), sizes.get(), err.get());
+            SdPush a{sh.in.row_ptr.get(), sh.in.col.get(), sh.in.weight.get(), fa.get(), qa.get(), fsize, fedges,
+                     msg.get(), best.get(), touched.get(), sizes.get(), err.get()};
+            const unsigned grid = (unsigned)std::min<int64_t>(
+                std::max<int64_t>((fedges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
+                8192);
+            sd_push_q_kernel<<<grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
             unsigned long long ts = 0;
-            JG_HIP(hipMemcpyAsync(&ts, sizes.get(), sizeof ts, hipMemcpyDeviceToHost, s));
-            JG_HIP(hipStreamSynchronize(s));
+            copy_d2h(&ts, sizes.get(), sizeof ts, s);
+            unsigned long long np = 0;
             if (ts > 0) {
-                sd_apply_kernel<<<grid_for((int64_t)ts, kBlock, 256 * 8), kBlock, 0, s>>>(
-                    touched.get(), (int64_t)ts, best.get(), dist.get(), msg.get(), fb.get(), sizes.get() + 1);
+                sd_apply_q_kernel<<<grid_for((int64_t)ts, kBlock, 4096), kBlock, 0, s>>>(
+                    touched.get(), (int64_t)ts, best.get(), dist.get(), msg.get(), sh.in.row_ptr.get(), fb.get(), qb.get(),
+                    sizes.get() + 1);
                 JG_LAUNCH_CHECK();
+                copy_d2h(&np, sizes.get() + 1, sizeof np, s);
             }
-            unsigned long long ns = 0;
-            JG_HIP(hipMemcpyAsync(&ns, sizes.get() + 1, sizeof ns, hipMemcpyDeviceToHost, s));
-            JG_HIP(hipStreamSynchronize(s));
-            fsize = (int64_t)ns;
+            fsize = (int64_t)(np >> kPackShift);
+            fedges = (int64_t)(np & kEdgeMask);
             fa.swap(fb);
+            qa.swap(qb);
             levels = t;
         }
+        JG_HIP(hipEventRecord(t1, s));  // the distances are final: the copy-out is outside the timed region
+        region_mark(s, false);
+        timed_end = true;
         std::vector<long long> h(rows);
         if (rows) copy_d2h(h.data(), dist.get(), rows * sizeof(long long), s);
         for (int64_t l = 0; l < rows; ++l) host[l] = h[l];
@@ -3549,8 +3898,10 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         copy_d2h(&e, err.get(), sizeof e, s);
         if (e) fail(JG_ERR_ARG, kMissingWeight);
     }
-    JG_HIP(hipEventRecord(t1, s));
-    region_mark(s, false);
+    if (!timed_end) {
+        JG_HIP(hipEventRecord(t1, s));
+        region_mark(s, false);
+    }
     JG_HIP(hipEventSynchronize(t1));
     float ms = 0;
     JG_HIP(hipEventElapsedTime(&ms, t0, t1));
