@@ -94,6 +94,7 @@ struct BfsLevel {
     const int64_t* deg_rp;   // push_rp, else pull_rp (frontier edge counts)
     int32_t* depth;
     int64_t rows;
+    int64_t bu_rows;  // the bottom-up probes rows [0, bu_rows): the pull adjacency's empty suffix is never found
     const int32_t* queue_in;
     const int64_t* qoff_in;
     int32_t* queue_out;
@@ -269,6 +270,8 @@ __device__ __forceinline__ void bfs_top_down(const BfsLevel& a, int64_t nf, int6
 // first hit; 64 consecutive vertices per wave so the next frontier word is the wave's ballot.
 template <bool kFromDepth, class App>
 __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long long* packed, App& app) {
+    // every word of the output bitmap is written (a word past bu_rows comes out zero: a stale bit there
+    // would put a row in the next level's frontier); rows from bu_rows on read nothing
     const int64_t words = (a.rows + 63) / 64;
     constexpr int kWpb = kBlock / kWave;
     const int64_t wstride = (int64_t)gridDim.x * kWpb;
@@ -281,7 +284,7 @@ __device__ __forceinline__ void bfs_bottom_up(const BfsLevel& a, unsigned long l
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t vdeg = 0;
-        if (v < a.rows && !a.seen[v]) {
+        if (v < a.bu_rows && !a.seen[v]) {
             // kBuBatch neighbours per step: all column loads, then all frontier probes, then the test,
             // so a row scanned to its end pays two round trips per batch instead of per neighbour
             // (which neighbour hits does not matter: the depth is level + 1 either way)
@@ -1840,6 +1843,10 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     a.deg_rp = degcsr->row_ptr.get();
     a.depth = depth;
     a.rows = rows;
+    // rows from the pull adjacency's empty suffix on have no pull entries: no bottom-up level finds them
+    // (their seen bytes are set at the start), so its probes skip them without reading their seen bytes
+    // (RMAT-26 BOTH: ~34 M of 67 M rows)
+    a.bu_rows = pull && pull->empty_from >= 0 ? std::min(rows, pull->empty_from) : rows;
     a.seen = sh.bfs_seen.get();
     a.ctr = sh.bfs_ctr.get();
     a.st = st;
