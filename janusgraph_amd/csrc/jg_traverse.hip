@@ -521,6 +521,8 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
         seen[i] = i == source || empty;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        depth[source] = 0;  // (also when the source lies past `rows`: the caller's init_rows skipped the suffix)
+        seen[source] = 1;
         queue[0] = (int32_t)source;
         qoff[0] = 0;
         ctr[kBfsRing - 1] = (1ull << kPackShift) | (unsigned long long)(deg_rp[source + 1] - deg_rp[source]);
@@ -1809,8 +1811,10 @@ namespace {
 
 // end_ev (nullable) is recorded behind the last level launch, before the host reads the final state:
 // the traversal's GPU span ends there (the state read-back is the host's control, not traversal work)
+// tail = false: no caller reads the depths of the empty suffix (no depth output, no kept rows); on a BOTH
+// traversal the traversal itself never does either, so the init skips those rows.
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr) {
+                 double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr, bool tail = true) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr* push = c.push;
@@ -1827,7 +1831,12 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
                                                                 sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
                                                                 sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
     } else {
-        bfs_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(depth, rows, source, sh.bfs_queue[0].get(),
+        // BOTH (push = pull): rows from the empty suffix on have no entry at all, so no bottom-up probe or
+        // top-down claim reads their depth or seen byte, only the caller's depth output does.  (Directed,
+        // a row without pull entries may still be a pull neighbour whose depth a bottom-up level probes.)
+        const int64_t live = pull && pull->empty_from >= 0 ? std::min(rows, pull->empty_from) : rows;
+        const int64_t init_rows = tail || push != pull ? rows : live;
+        bfs_init_kernel<<<grid_for(init_rows), kBlock, 0, s>>>(depth, init_rows, source, sh.bfs_queue[0].get(),
                                                           sh.bfs_qoff[0].get(), degcsr->row_ptr.get(),
                                                           (long long)degcsr->nnz, sh.bfs_ctr.get(), st,
                                                           sh.bfs_seen.get(), pull ? pull->row_ptr.get() : nullptr,
@@ -2670,7 +2679,8 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
             if (c.pull) bfs_first_col(sh, *c.pull);
             region_mark(sh.stream, true);
             JG_HIP(hipEventRecord(t0, sh.stream));
-            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1);
+            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1,
+                                  (depth_rows && depth_rows[0]) || keep);
         }
         JG_HIP(hipEventSynchronize(t1));
         float ms = 0;

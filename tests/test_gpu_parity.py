@@ -150,6 +150,27 @@ def test_bfs_rmat_vs_oracle(ctx, oracle_lib, scale):
         np.testing.assert_array_equal(depth, ref)
 
 
+def test_bfs_without_depth_output_skips_the_empty_suffix(ctx, oracle_lib):
+    """want=False on a BOTH traversal: the init skips the empty suffix's rows (dobfs_single `tail`), which
+    the traversal never reads.  Isolated sources (in that suffix) and connected ones alternate, so stale
+    depths of an earlier source would show: every want=False run must count the levels and edges of the
+    want=True run from the same source, and a later want=True run must still match the oracle."""
+    import janusgraph_amd as jg
+    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 15)
+    g = ctx.build(vid, src, dst, flags=ALL)
+    deg = np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n)
+    iso = np.flatnonzero(deg == 0)[:3]
+    conn = np.flatnonzero(deg > 0)[[0, 11, 257]]
+    assert len(iso) == 3
+    for s in [int(x) for pair in zip(iso, conn) for x in pair]:
+        g.bfs([vid[s]], jg.DIR_BOTH, want=False)
+        quiet = (ctx.stats()["levels"], ctx.stats()["edges_traversed"])
+        got = g.bfs([vid[s]], jg.DIR_BOTH)[0]
+        assert (ctx.stats()["levels"], ctx.stats()["edges_traversed"]) == quiet
+        np.testing.assert_array_equal(got, oracle_lib.bfs(n, ds, dd, s, 3))
+    g.close()
+
+
 @pytest.mark.parametrize("mode,split_min", [(0, 65536), (1, 1), (1, 4096), (2, 1)])
 def test_bfs_split_top_down_matches_oracle(oracle_lib, mode, split_min):
     """Split top-down levels (owner store + claim launch, Tune::bfs_td_split) against the CAS claims:
