@@ -97,10 +97,12 @@ __global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t
 }
 
 // comp[dense[l]] = vor[label[l]]: each row's component id, in caller order
-__global__ void cc_output_kernel(const int32_t* __restrict__ label, const int32_t* __restrict__ dense,
+// rows from label_rows on take their own rank as label (the union-find's edgeless suffix, not written)
+__global__ void cc_output_kernel(const int32_t* __restrict__ label, const int32_t* __restrict__ rank,
+                                 int64_t label_rows, const int32_t* __restrict__ dense,
                                  const int64_t* __restrict__ vor, int64_t rows, int64_t* __restrict__ comp) {
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < rows; l += (int64_t)gridDim.x * blockDim.x)
-        comp[dense[l]] = vor[label[l]];
+        comp[dense[l]] = vor[l < label_rows ? label[l] : rank[l]];
 }
 
 __global__ void cc_init_kernel(const int32_t* __restrict__ lab0, const int64_t* __restrict__ rp, int64_t rows,
@@ -487,7 +489,8 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // component minimum, depth, label and seen; BFS depth and seen 5), 12 B per entry linked in the second
 // round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.  k > 1 (Tune::cc_first)
 // runs the atomic first round of uf_link_first_kernel instead, under the same model.
-bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, double* work_bytes) {
+bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, int64_t* label_rows,
+                   double* work_bytes) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
@@ -495,9 +498,11 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     if (rows == 0) {
         *iterations = 0;
         *labels = sh.cc_rank0.get();
+        *label_rows = 0;
         return true;
     }
     const int64_t ne = c.empty_from >= 0 ? std::min(c.empty_from, rows) : rows;
+    *label_rows = ne;  // an edgeless row's label is its own rank: the BFS start writes the rows before ne only
     // scratch: the message vectors (re-initialised if the propagation has to run), a rows array kept
     // with the shard
     int32_t* parent = sh.cc_msg[0].get();
@@ -1628,8 +1633,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     // One shard: the same labels and superstep count from a union-find and one BFS (cc_union_find).
     bool solved = false;
     const int32_t* uf_labels = nullptr;  // the union-find's labels of shard 0 (when solved)
+    int64_t uf_label_rows = sh0.rows;      // its rows from here on take their rank (cc_union_find)
     double uf_bytes = 0;
-    if (uf_one) solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_bytes);
+    if (uf_one) solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_label_rows, &uf_bytes);
     // Sharded over halo plans: the same from local union-finds, tree labels over the halo and a sharded BFS
     // (cc_union_find_sharded); the sharded BFS takes at most 64 shards (jg_traverse.hip, kMaxShardsBfs).
     int uf_rounds = 0;
@@ -1729,8 +1735,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         Shard& sh = *g.shards[0];
         DeviceGuard dg(sh);
         DevBuf<int64_t> out(n);
-        cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(solved ? uf_labels : sh.cc_label.get(),
-                                                                sh.dense_rows.get(), g.cc_vor.get(), n, out.get());
+        cc_output_kernel<<<grid_for(n), kBlock, 0, sh.stream>>>(
+            solved ? uf_labels : sh.cc_label.get(), sh.cc_rank0.get(), solved ? uf_label_rows : n, sh.dense_rows.get(),
+            g.cc_vor.get(), n, out.get());
         JG_LAUNCH_CHECK();
         copy_d2h(comp_out, out.get(), n * sizeof(int64_t), sh.stream);
     } else if (comp_out) {
@@ -1739,8 +1746,12 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
             Shard& sh = *sp;
             DeviceGuard dg(sh);
             std::vector<int32_t> h(sh.rows);
-            const int32_t* lab = solved && &sh == &sh0 ? uf_labels : sh.cc_label.get();
-            if (sh.rows) copy_d2h(h.data(), lab, sh.rows * sizeof(int32_t), sh.stream);
+            const bool uf = solved && &sh == &sh0;
+            const int32_t* lab = uf ? uf_labels : sh.cc_label.get();
+            const int64_t lr = uf ? std::min(uf_label_rows, sh.rows) : sh.rows;
+            if (lr) copy_d2h(h.data(), lab, lr * sizeof(int32_t), sh.stream);
+            if (lr < sh.rows)  // the union-find's edgeless suffix: its ranks
+                copy_d2h(h.data() + lr, sh.cc_rank0.get() + lr, (sh.rows - lr) * sizeof(int32_t), sh.stream);
             for (int64_t l = 0; l < sh.rows; ++l) comp_out[sh.dense_of_local()[l]] = vid_of_rank[h[l]];
         }
     }

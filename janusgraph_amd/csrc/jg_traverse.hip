@@ -1827,9 +1827,11 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
         BfsState s0{};
         s0.mu = (long long)degcsr->nnz;
         copy_h2d(st + kBfsRing - 1, &s0, sizeof s0, s);
-        bfs_init_roots_kernel<<<grid_for((rows + 3) / 4), kBlock, 0, s>>>(depth, rows, *roots, degcsr->row_ptr.get(),
-                                                                sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
-                                                                sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
+        // rows from roots->ne on (no edge) are neither read by the traversal (BOTH: no entry) nor labelled here
+        // (cc_output_kernel gives them their rank)
+        bfs_init_roots_kernel<<<grid_for((roots->ne + 3) / 4), kBlock, 0, s>>>(
+            depth, roots->ne, *roots, degcsr->row_ptr.get(), sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
+            sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
     } else {
         // BOTH (push = pull): rows from the empty suffix on have no entry at all, so no bottom-up probe or
         // top-down claim reads their depth or seen byte, only the caller's depth output does.  (Directed,
