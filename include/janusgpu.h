@@ -151,6 +151,9 @@ typedef struct jg_transport {
                     int nrecv, const int* recv_peer, void* const* recv, const size_t* recv_bytes);
 } jg_transport;
 int jg_ctx_create_rank_transport(int device, int nranks, int rank, const jg_transport* t, jg_ctx** out);
+/* Lifetime: every jg_graph and jg_builder made from a context uses its streams and communicators, so
+ * destroy them before the context.  While any is alive jg_ctx_destroy changes nothing and returns
+ * JG_ERR_STATE (the context stays valid: destroy the graphs/builders, then call it again). */
 int jg_ctx_destroy(jg_ctx* ctx);
 /* Hands the device memory the library caches for reuse (freed blocks) back to the context's devices. */
 int jg_ctx_trim(jg_ctx* ctx);
@@ -357,13 +360,22 @@ int jg_decode_edges(jg_ctx* ctx, const uint8_t* bytes, int64_t nbytes, const int
 /* Block until all work enqueued on the graph's streams is complete. */
 int jg_graph_sync(jg_graph* g);
 
-/* Process-wide performance knobs (no effect on results): "pull_unroll" (4 | 8 gathers in flight per
- * lane), "pull_nt" (0 | 1: non-temporal loads of the streamed adjacency), "pull_lds", "light_lds",
- * "slice_lds", "pull_short", "pull_overlap"; read when a graph is built: "pull_split", "band<i>_deg",
- * "band<i>_bit", "halo" (sharded graphs: sparse halo exchange, 0 = dense allgather).  Every key with
- * its default and measurement is listed in `struct Tune` (janusgraph_amd/csrc/jg_internal.h), e.g.
- * "msbfs_skip" (bit-parallel BFS merge-task skip), "cc_first" (CC union-find first-round links).
- * Unknown key: JG_ERR_ARG. */
+/* Process-wide performance knobs (no effect on results).  Every key, its default and the measurement
+ * behind it is in `struct Tune` (janusgraph_amd/csrc/jg_internal.h); the ranges are checked here:
+ *   0/1 switches (any other value: JG_ERR_ARG): "pull_split", "halo" (read at build; sharded graphs:
+ *     0 = dense allgather), "bfs_narrow", "cc_push", "cc_uf", "cc_uf_sharded", "cc_uf_search",
+ *     "cc_sparse", "msbfs_sparse", "msbfs_skip", "msbfs_split", "sharded_bfs";
+ *   integers: "bfs_alpha", "dobfs_alpha", "bfs_beta", "nb_alpha" [1, 1e6]; "nb_first" [4, 4096];
+ *     "msbfs_td" [0, 2]; "msbfs_exit" [0, 2]; "cc_first" [1, 64]; "msbfs_td_rowapply" [0, 1024];
+ *     "msbfs_td_noprobe", "msbfs_exit_live" [0, 1000]; "msbfs_scan_queue" [0, 1001];
+ *     "msbfs_exit_first" [1, 256]; "bfs_td_split" [0, 2]; "bfs_td_split_levels" [0, 0xffff];
+ *     "bfs_td_split_min" / "_max" [1, 2^31); "bfs_batch0" [1, 64]; "bfs_grid_mult" [1, 64];
+ *     "bfs_grid" [64, 65536]; "bfs_tail_grid" [0, 65536]; "merge_temporal" [0, 2];
+ *     "sd_delta" [-1, 2^30]; "merge_pack" 0 | 1 | 24; "merge_stage<i>" -1 | 0 | 64 | 128 | 256 | 512;
+ *     read at build: "band<i>_deg" (>= -1), "band<i>_bit" (0 or [3, 8]), "band<i>_sub" (power of two <= 256);
+ *   retired (their variants were measured slower and removed; accepted and ignored): "pull_unroll",
+ *     "pull_nt", "pull_lds", "light_lds", "slice_lds", "pull_short", "pull_overlap", "bfs_persistent".
+ * Unknown key or value out of range: JG_ERR_ARG. */
 int jg_tune_set(const char* key, int64_t value);
 
 #ifdef __cplusplus

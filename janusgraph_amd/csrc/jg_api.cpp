@@ -577,6 +577,10 @@ struct BuildTimer {
 // decoded there chunk by chunk (EdgestoreDecoder: copy and decode overlap the caller's next chunk).
 struct jg_builder {
     jg::Ctx* ctx = nullptr;
+    explicit jg_builder(jg::Ctx* c) : ctx(c) { c->live.fetch_add(1); }
+    ~jg_builder() { ctx->live.fetch_sub(1); }
+    jg_builder(const jg_builder&) = delete;
+    jg_builder& operator=(const jg_builder&) = delete;
     int mode = 0;  // 0 empty, 1 ids (vertices / edges), 2 edgestore rows
     int weights = -1;  // ids mode: -1 unknown, 0 no edge weights, 1 every edge weighted
     bool finished = false;
@@ -670,7 +674,6 @@ int jg_tune_set(const char* key, int64_t value) {
         {"bfs_grid_mult", &t.bfs_grid_mult, 1, 64},
         {"bfs_grid", &t.bfs_grid, 64, 65536},
         {"bfs_tail_grid", &t.bfs_tail_grid, 0, 65536},
-        {"bfs_persistent", &t.bfs_persistent, 0, 8192},
         {"merge_temporal", &t.merge_temporal, 0, 2},
         {"sd_delta", &t.sd_delta, -1, 1 << 30},
     };
@@ -708,6 +711,9 @@ int jg_tune_set(const char* key, int64_t value) {
     } else if (k == "merge_pack") {
         JG_ARG(value == 0 || value == 1 || value == 24, "merge_pack must be 0 (32 bits), 1 (automatic) or 24 (at least 24)");
         t.merge_pack = (int)value;
+    } else if (k == "pull_unroll" || k == "pull_nt" || k == "pull_lds" || k == "light_lds" || k == "slice_lds" ||
+               k == "pull_short" || k == "pull_overlap" || k == "bfs_persistent") {
+        // retired knobs (their variants were measured and removed, rounds 4-6): accepted, no effect
     } else {
         jg::fail(JG_ERR_ARG, "unknown tuning key: " + k);
     }
@@ -818,6 +824,12 @@ int jg_ctx_destroy(jg_ctx* ctx) {
     JG_GUARD_BEGIN
     if (!ctx) return JG_OK;
     jg::Ctx& c = ctx->impl;
+    // graphs and builders hold the context's streams and communicators (a graph destroyed after its
+    // context synchronised a destroyed stream: gpurun_out/r05f): the caller destroys them first
+    const int live = c.live.load();
+    if (live > 0)
+        jg::fail(JG_ERR_STATE, ("jg_ctx_destroy: " + std::to_string(live) +
+                                " graph(s)/builder(s) of this context are still alive; destroy them first").c_str());
     for (auto cm : c.comms) ncclCommDestroy(cm);
     for (size_t i = 0; i < c.streams.size(); ++i) {
         if (c.logical && i > 0) continue;
@@ -856,9 +868,8 @@ int jg_graph_build(jg_ctx* ctx, const int64_t* vid, int64_t n, const int64_t* sr
     JG_ARG((flags & (JG_ADJ_IN | JG_ADJ_OUT | JG_ADJ_BOTH)) != 0 && (flags & ~7u) == 0, "bad adjacency flags");
     *out = nullptr;
     jg::Ctx& c = ctx->impl;
-    auto gh = std::make_unique<jg_graph>();
+    auto gh = std::make_unique<jg_graph>(&c);
     jg::Graph& g = gh->impl;
-    g.ctx = &c;
     g.flags = flags;
     jg::make_shards(c, g);
     jg::BuildTimer timer(g);
@@ -898,9 +909,8 @@ int jg_graph_build_edgestore(jg_ctx* ctx, const uint64_t* row_keys, int64_t nrow
                               value_pos, nentries, type_ids,      type_mult, ntypes,       partition_bits};
     *out = nullptr;  // the decoder validates the rows and entries as it stages them
     jg::Ctx& c = ctx->impl;
-    auto gh = std::make_unique<jg_graph>();
+    auto gh = std::make_unique<jg_graph>(&c);
     jg::Graph& g = gh->impl;
-    g.ctx = &c;
     g.flags = flags;
     jg::make_shards(c, g);
     jg::BuildTimer timer(g);
@@ -934,8 +944,7 @@ int jg_builder_create(jg_ctx* ctx, jg_builder** out) {
     JG_GUARD_BEGIN
     JG_ARG(ctx && out, "null argument");
     *out = nullptr;
-    auto b = std::make_unique<jg_builder>();
-    b->ctx = &ctx->impl;
+    auto b = std::make_unique<jg_builder>(&ctx->impl);
     *out = b.release();
     JG_GUARD_END
 }
@@ -1065,9 +1074,8 @@ int jg_builder_finish(jg_builder* b, uint32_t flags, jg_graph** out) {
     if (b->finished) jg::fail(JG_ERR_STATE, "builder already finished");
     *out = nullptr;
     jg::Ctx& c = *b->ctx;
-    auto gh = std::make_unique<jg_graph>();
+    auto gh = std::make_unique<jg_graph>(&c);
     jg::Graph& g = gh->impl;
-    g.ctx = &c;
     g.flags = flags;
     jg::make_shards(c, g);
     jg::BuildTimer timer(g);
@@ -1141,9 +1149,8 @@ int jg_graph_build_rmat(jg_ctx* ctx, int scale, int edgefactor, uint64_t seed, u
     const int64_t n = 1ll << scale, m = (int64_t)edgefactor << scale;
     JG_ARG(m < (int64_t)UINT32_MAX, "too many edges");
     jg::Ctx& c = ctx->impl;
-    auto gh = std::make_unique<jg_graph>();
+    auto gh = std::make_unique<jg_graph>(&c);
     jg::Graph& g = gh->impl;
-    g.ctx = &c;
     g.n = n;
     g.flags = flags;
     jg::make_shards(c, g);

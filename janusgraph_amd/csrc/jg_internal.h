@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -248,9 +249,9 @@ struct Shard {
     DevBuf<unsigned long long> bfs_ctr;      // [kBfsRing] packed per-level frontier counters
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
+    bool bfs_depth_tail_clean = false;       // BOTH: bfs_depth's empty suffix holds -1 (the init skips it)
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;
-    DevBuf<unsigned char> bfs_sync;          // persistent DO-BFS: grid-barrier counters, abort flag, final state
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
     // narrow bit-parallel BFS scratch (<= 8 sources, one shard; jg_narrow.hip), kept across calls
     std::vector<DevBuf<uint8_t>> nb_level;   // [levels][rows + pad] each level's frontier byte (= its new bits)
@@ -333,6 +334,9 @@ struct Ctx {
     std::vector<hipStream_t> streams;
     bool profiling = false;
     jg_stats last{};
+    // graphs and builders made from this context and not yet destroyed: they use its streams and
+    // communicators, so jg_ctx_destroy refuses while any is alive (JG_ERR_STATE)
+    std::atomic<int> live{0};
     int total_shards() const { return nranks * (int)devices.size(); }
 };
 
@@ -638,10 +642,6 @@ struct Tune {
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
                                       //         (0: every launch at the full grid)
-    int bfs_persistent = 0;           //         DO-BFS: every level in one launch, a grid barrier between levels
-                                      //         (measured slower, profiles/r05/persistent/):
-                                      //         0 off, 1 at the level grid, N > 1 at N workgroups (capped at the
-                                      //         co-resident count)
     int sd_delta = -1;                // weighted shortest distance with an unbounded hop count (maxDepth >= rows - 1)
                                       // and no negative weight: near-far delta-stepping with this delta (-1:
                                       // automatic, 0: the frontier Bellman-Ford supersteps)
@@ -684,4 +684,11 @@ struct jg_ctx {
 };
 struct jg_graph {
     jg::Graph impl;
+    explicit jg_graph(jg::Ctx* c) {
+        impl.ctx = c;
+        c->live.fetch_add(1);
+    }
+    ~jg_graph() { impl.ctx->live.fetch_sub(1); }
+    jg_graph(const jg_graph&) = delete;
+    jg_graph& operator=(const jg_graph&) = delete;
 };

@@ -391,117 +391,6 @@ __global__ __launch_bounds__(kBlock) void bfs_td_claim_kernel(BfsLevel a) {
     app.final(a.queue_out, a.qoff_out, a.ctr + a.level % kBfsRing);
 }
 
-// ---- persistent DO-BFS (bfs_persistent) ----
-// Every level in one launch of a co-resident grid, levels separated by a grid barrier instead of a
-// kernel boundary.  The barrier follows MI355X_MICROARCH.md's barrier-xcd row: each workgroup drains
-// its stores, releases them to memory (agent fence) and arrives on one of 8 group counters (group =
-// block mod 8, so the release is per workgroup: the protocol does not depend on where blocks are
-// placed); the last arriver of a group arrives on the top counter, whose last arriver publishes the
-// generation; every workgroup polls the generation with relaxed agent loads and acquires.  Counters
-// are monotonic (epoch e waits for e arrivals per member).  Every spin is bounded in wall time: past
-// kSyncSpinTicks a workgroup raises the abort word and leaves, and every spinner leaves on it, so a
-// grid that is not co-resident ends the launch with an error instead of hanging the GPU.
-constexpr int kSyncGroupStride = 32;                // unsigned words: one 128-B line per group counter
-constexpr int kSyncTop = 8 * kSyncGroupStride, kSyncGen = kSyncTop + kSyncGroupStride,
-              kSyncAbort = kSyncGen + kSyncGroupStride, kSyncWords = kSyncAbort + kSyncGroupStride;
-constexpr size_t kSyncFinalOff = kSyncWords * sizeof(unsigned);  // BfsState of the last level
-constexpr size_t kSyncBytes = kSyncFinalOff + sizeof(BfsState);
-constexpr unsigned long long kSyncSpinTicks = 100000000ull;  // 1 s of the 100 MHz wall clock
-
-__device__ bool grid_barrier(unsigned* sync, unsigned epoch) {
-    __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned g = blockIdx.x & 7u;
-        const unsigned gsize = (gridDim.x >> 3) + (g < (gridDim.x & 7u) ? 1u : 0u);
-        const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
-        if (atomicAdd(sync + g * kSyncGroupStride, 1u) + 1u == epoch * gsize &&
-            atomicAdd(sync + kSyncTop, 1u) + 1u == epoch * groups)
-            __hip_atomic_store(sync + kSyncGen, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(sync + kSyncGen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
-            if (__hip_atomic_load(sync + kSyncAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                wall_clock64() - t0 > kSyncSpinTicks) {
-                __hip_atomic_store(sync + kSyncAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-struct BfsPersist {
-    int32_t* queue[2];
-    int64_t* qoff[2];
-    unsigned long long* bm[2];
-    unsigned* sync;  // [kSyncBytes] zeroed before the launch
-    int split_mode, split_levels;
-};
-
-__global__ __launch_bounds__(kBlock) void bfs_persistent_kernel(BfsLevel a, BfsPersist p) {
-    __shared__ BfsState s_st;
-    __shared__ long long s_nf, s_mf;
-    __shared__ int s_switch;
-    __shared__ WaveStage s_app;
-    __shared__ int64_t s_qs[kQoffSamples];
-    unsigned epoch = 0;
-    for (int level = 0;; ++level) {
-        const int q = level & 1;
-        a.level = level;
-        a.queue_in = p.queue[q];
-        a.qoff_in = p.qoff[q];
-        a.queue_out = p.queue[q ^ 1];
-        a.qoff_out = p.qoff[q ^ 1];
-        a.bm_in = p.bm[q];
-        a.bm_out = p.bm[q ^ 1];
-        a.split = a.owner && (p.split_mode == 1 || (p.split_mode == 2 && level < 16 && ((p.split_levels >> level) & 1)));
-        if (threadIdx.x == 0) {
-            int64_t nf, mf;
-            bool sw;
-            const BfsState c = bfs_decide(a, &nf, &mf, &sw);
-            s_st = c;
-            s_nf = nf;
-            s_mf = mf;
-            s_switch = sw;
-            if (blockIdx.x == 0) {
-                a.st[level % kBfsRing] = c;
-                if (!c.done) a.ctr[(level + 1) % kBfsRing] = 0ull;
-                else *reinterpret_cast<BfsState*>(reinterpret_cast<unsigned char*>(p.sync) + kSyncFinalOff) = c;
-            }
-        }
-        __syncthreads();
-        if (s_st.done) return;  // every workgroup read the same state: all leave together
-        unsigned long long* packed = a.ctr + level % kBfsRing;
-        WaveApp app{s_app};
-        app.init();
-        if (!s_st.bottom_up) {
-            if (td_split(a, s_mf)) {
-                bfs_top_down<kTdOwner>(a, s_nf, s_mf, packed, app, s_qs);
-                if (!grid_barrier(p.sync, ++epoch)) return;
-                bfs_top_down<kTdClaim>(a, s_nf, s_mf, packed, app, s_qs);
-            } else {
-                bfs_top_down<kTdCas>(a, s_nf, s_mf, packed, app, s_qs);
-            }
-        } else if (s_switch) {
-            bfs_bottom_up<true>(a, packed, app);
-        } else {
-            bfs_bottom_up<false>(a, packed, app);
-        }
-        app.final(a.queue_out, a.qoff_out, packed);
-        if (!grid_barrier(p.sync, ++epoch)) return;
-    }
-}
-
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -1811,8 +1700,9 @@ namespace {
 
 // end_ev (nullable) is recorded behind the last level launch, before the host reads the final state:
 // the traversal's GPU span ends there (the state read-back is the host's control, not traversal work)
-// tail = false: no caller reads the depths of the empty suffix (no depth output, no kept rows); on a BOTH
-// traversal the traversal itself never does either, so the init skips those rows.
+// tail = false: the depths of the empty suffix already hold -1 (bfs_run keeps them so: Shard::
+// bfs_depth_tail_clean); on a BOTH traversal the traversal itself never reads or writes those rows, so the
+// init skips them.
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
                  double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr, bool tail = true) {
     hipStream_t s = sh.stream;
@@ -1884,40 +1774,9 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     const unsigned tail_grid = (unsigned)std::min<int64_t>(std::max(tune().bfs_tail_grid, 1), grid);
     BfsState hs{};
     int level = 0;
-    if (!roots && tune().bfs_persistent) {  // one launch for every level (grid_barrier)
-        static int resident = 0;  // co-resident workgroups of the persistent kernel (LDS-bound: 4 per CU)
-        if (!resident) {
-            int per_cu = 0, cus = 0;
-            JG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfs_persistent_kernel, kBlock, 0));
-            JG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sh.device));
-            resident = std::max(per_cu, 1) * std::max(cus, 1);
-        }
-        const int want = tune().bfs_persistent > 1 ? tune().bfs_persistent : (int)grid;
-        const unsigned pg = (unsigned)std::min(want, resident);
-        if (sh.bfs_sync.size() != kSyncBytes) sh.bfs_sync.alloc(kSyncBytes);
-        JG_HIP(hipMemsetAsync(sh.bfs_sync.get(), 0, kSyncBytes, s));
-        BfsPersist p{};
-        for (int k = 0; k < 2; ++k) {
-            p.queue[k] = sh.bfs_queue[k].get();
-            p.qoff[k] = sh.bfs_qoff[k].get();
-            p.bm[k] = sh.bfs_bm[k].get();
-        }
-        p.sync = reinterpret_cast<unsigned*>(sh.bfs_sync.get());
-        p.split_mode = split_mode;
-        p.split_levels = split_levels;
-        bfs_persistent_kernel<<<pg, kBlock, 0, s>>>(a, p);
-        JG_LAUNCH_CHECK();
-        if (end_ev) {
-            JG_HIP(hipEventRecord(end_ev, s));
-            region_mark(s, false);
-        }
-        unsigned abort_word = 0;
-        copy_d2h(&abort_word, sh.bfs_sync.get() + kSyncAbort * sizeof(unsigned), sizeof abort_word, s);
-        if (abort_word) fail(JG_ERR_STATE, "persistent BFS: grid barrier timed out (grid not co-resident)");
-        copy_d2h(&hs, sh.bfs_sync.get() + kSyncFinalOff, sizeof hs, s);
-        if (edges_out) *edges_out = (double)hs.edges;
-        return hs.levels;
-    }
+    // (A persistent kernel running every level in one launch with a grid barrier between levels was
+    // built in round 5 and measured slower: the barrier cost 6-19 us per level, profiles/r05/persistent/;
+    // deleted in round 6.)
     // Levels are enqueued in batches, the host reading the device state once per batch: first
     // bfs_batch0 (RMAT traversals end within ~10 levels plus the one that finds the frontier empty),
     // then 4, 8, 16, ... (levels past the end are launched anyway and cost ~4 us each: a second batch
@@ -2667,22 +2526,38 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         const BfsCsrs c = pick_csrs(sh, direction);
         int shard = 0;
         const int64_t l = local_of_vid(g, source_vids[0], &shard);
-        if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
+        if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) {
+            sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
+            sh.bfs_depth_tail_clean = false;
+        }
         DevBuf<int32_t>& depth = sh.bfs_depth;
         int levels = 0;
         double edges = 0;
         if (l < 0) {
             fill_i32_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(depth.get(), sh.rows, -1);
             JG_LAUNCH_CHECK();
+            sh.bfs_depth_tail_clean = true;
             JG_HIP(hipEventRecord(t0, sh.stream));
             JG_HIP(hipEventRecord(t1, sh.stream));
         } else {
             bfs_buffers(sh);
             if (c.pull) bfs_first_col(sh, *c.pull);
+            // BOTH: rows of the empty suffix (no entry) are never reached, so their depths stay -1 from one
+            // traversal to the next and the init skips them, whatever the caller wants back (the
+            // depth output and kept rows no longer pay a longer init than want=False).  The suffix is filled
+            // once, before t0; a source inside it (an isolated vertex) takes the full init and leaves its 0
+            // behind, so the next traversal refills.
+            const int64_t live = c.push == c.pull && c.pull->empty_from >= 0 ? std::min(sh.rows, c.pull->empty_from)
+                                                                              : sh.rows;
+            if (live < sh.rows && !sh.bfs_depth_tail_clean) {
+                fill_i32_kernel<<<grid_for(sh.rows - live), kBlock, 0, sh.stream>>>(depth.get() + live, sh.rows - live, -1);
+                JG_LAUNCH_CHECK();
+            }
+            const bool full_init = l >= live;
             region_mark(sh.stream, true);
             JG_HIP(hipEventRecord(t0, sh.stream));
-            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1,
-                                  (depth_rows && depth_rows[0]) || keep);
+            levels = dobfs_single(ctx, sh, c, l, max_depth, depth.get(), &edges, nullptr, t1, full_init);
+            sh.bfs_depth_tail_clean = !full_init || live == sh.rows;
         }
         JG_HIP(hipEventSynchronize(t1));
         float ms = 0;

@@ -84,8 +84,9 @@ def test_tune_keys_validate_without_a_gpu():
                  ("bfs_grid_mult", 4), ("bfs_batch0", 10), ("msbfs_skip", 1), ("cc_first", 1), ("msbfs_sparse", 1),
                  ("cc_uf_sharded", 0), ("cc_uf_sharded", 1), ("cc_uf_search", 0), ("cc_uf_search", 1), ("cc_sparse", 0), ("cc_sparse", 1), ("msbfs_td", 2),
                  ("msbfs_td", 1), ("bfs_td_split", 2), ("bfs_td_split_levels", 2), ("bfs_td_split_min", 65536),
-                 ("bfs_td_split_max", 1 << 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64), ("bfs_persistent", 1), ("bfs_persistent", 256),
-                 ("bfs_persistent", 0),
+                 ("bfs_td_split_max", 1 << 20), ("bfs_tail_grid", 0), ("bfs_tail_grid", 64),
+                 # retired knobs (variants measured slower and removed): accepted as no-ops
+                 ("bfs_persistent", 1), ("light_lds", 0), ("pull_unroll", 4), ("pull_nt", 1), ("pull_overlap", 0),
                  ("msbfs_exit", 0), ("msbfs_exit", 2), ("msbfs_exit", 1), ("msbfs_exit_live", 1000), ("msbfs_exit_live", 950),
                  ("msbfs_td_noprobe", 0), ("msbfs_td_noprobe", 2), ("msbfs_exit_first", 3), ("msbfs_exit_first", 16),
                  ("msbfs_scan_queue", 0), ("msbfs_scan_queue", 1001), ("msbfs_scan_queue", 50),
@@ -95,10 +96,10 @@ def test_tune_keys_validate_without_a_gpu():
                  ("band2_bit", 0), ("sd_delta", 0), ("sd_delta", 64), ("sd_delta", -1)):
         _lib.tune_set(k, v)
     # unknown keys (including the variants deleted in round 5: measured slower or equal) and bad values
-    for k, v in (("light_lds", 0), ("pull_unroll", 4), ("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
+    for k, v in (("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
                  ("merge_stage0", 100), ("merge_stage4", 64), ("merge_diag", 0), ("merge_nt", 0), ("msbfs_srcsplit", 0),
                  ("msbfs_bu", 0), ("fin_pipe", 1), ("relabel_out_ties", 0), ("band_sliced_build", 0),
-                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("sd_delta", -2), ("cc_first", 0), ("cc_first", 65), ("bfs_tail_grid", -1), ("bfs_persistent", -1),
+                 ("bfs_grid_mult", 0), ("bfs_batch0", 0), ("sd_delta", -2), ("cc_first", 0), ("cc_first", 65), ("bfs_tail_grid", -1),
                  ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0),
                  ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1), ("nb_first", 3), ("nb_alpha", 0),
                  ("bfs_narrow", 2), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1),

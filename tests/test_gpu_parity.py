@@ -168,6 +168,16 @@ def test_bfs_without_depth_output_skips_the_empty_suffix(ctx, oracle_lib):
         got = g.bfs([vid[s]], jg.DIR_BOTH)[0]
         assert (ctx.stats()["levels"], ctx.stats()["edges_traversed"]) == quiet
         np.testing.assert_array_equal(got, oracle_lib.bfs(n, ds, dd, s, 3))
+    # want=True skips the suffix too now, and CC shares the seen bytes; alternate want=False BFS,
+    # connected_components and want=True / kept rows from isolated and connected sources
+    comp_ref, _ = oracle_lib.connected_components(n, ds, dd, vid)
+    for s in [int(x) for pair in zip(conn, iso) for x in pair]:
+        g.bfs([vid[s]], jg.DIR_BOTH, want=False)
+        comp, _ = g.connected_components()
+        np.testing.assert_array_equal(comp, comp_ref)
+        np.testing.assert_array_equal(g.bfs([vid[s]], jg.DIR_BOTH)[0], oracle_lib.bfs(n, ds, dd, s, 3))
+        g.bfs_keep([vid[s]], jg.DIR_BOTH)
+        np.testing.assert_array_equal(g.bfs_kept_row(0), oracle_lib.bfs(n, ds, dd, s, 3))
     g.close()
 
 
@@ -624,48 +634,3 @@ def test_bfs_tail_grid_deeper_than_history(oracle_lib, tail):
         c.close()
     finally:
         _lib.tune_set("bfs_tail_grid", 64)
-
-
-@pytest.mark.parametrize("grid", [1, 256, 8])
-def test_bfs_persistent_matches_oracle(oracle_lib, grid):
-    """bfs_persistent: every DO-BFS level in one launch with a grid barrier between levels (the A/B of
-    VERDICT r04 item 4).  Depths and edge counts equal the launch-per-level path's and the oracle's over
-    RMAT graphs (both directions, split and CAS top-down levels), a 45-level path (many barriers on a
-    tiny frontier), a depth bound, and OUT/IN adjacencies; grid 1 = the level grid, 8 = one workgroup per
-    barrier group."""
-    import janusgraph_amd as jg
-    from janusgraph_amd import _lib
-    c = jg.Context((0,))
-    try:
-        for scale in (12, 16):
-            n, vid, src, dst, ds, dd = rmat_case(oracle_lib, scale)
-            g = c.build(vid, src, dst, flags=ALL)
-            deg = np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n)
-            cand = np.flatnonzero(deg > 0)
-            for s in (int(deg.argmax()), int(cand[len(cand) // 2]), int(cand[-1])):
-                _lib.tune_set("bfs_persistent", 0)
-                g.bfs([vid[s]], 3, want=False)
-                st0 = c.stats()
-                _lib.tune_set("bfs_persistent", grid)
-                got = g.bfs([vid[s]], 3)[0]
-                st1 = c.stats()
-                np.testing.assert_array_equal(got, oracle_lib.bfs(n, ds, dd, s, 3), err_msg=f"scale {scale} src {s}")
-                assert st1["edges_traversed"] == st0["edges_traversed"] and st1["levels"] == st0["levels"]
-                for d in (1, 2):  # OUT / IN
-                    np.testing.assert_array_equal(g.bfs([vid[s]], d)[0], oracle_lib.bfs(n, ds, dd, s, d))
-                np.testing.assert_array_equal(g.bfs([vid[s]], 3, 2)[0], oracle_lib.bfs(n, ds, dd, s, 3, 2))
-            g.close()
-        n0, vid0, src0, dst0, ds0, dd0 = rmat_case(oracle_lib, 10)
-        plen = 45
-        n = n0 + plen
-        vid = np.concatenate([vid0, (np.arange(plen, dtype=np.int64) + n0 + 1) << 8 | 3])
-        hub = int(np.bincount(ds0, minlength=n0).argmax())
-        ds = np.concatenate([ds0, [hub], np.arange(n0, n - 1)]).astype(ds0.dtype)
-        dd = np.concatenate([dd0, np.arange(n0, n)]).astype(ds0.dtype)
-        g = c.build(vid, vid[ds], vid[dd], flags=ALL)
-        np.testing.assert_array_equal(g.bfs([vid[n - 1]], 3)[0], oracle_lib.bfs(n, ds, dd, n - 1, 3))
-        assert c.stats()["levels"] > 40
-        g.close()
-    finally:
-        _lib.tune_set("bfs_persistent", 0)
-        c.close()

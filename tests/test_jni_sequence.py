@@ -371,3 +371,32 @@ def test_shortest_path_buffer_plan_rmat26(oracle_lib):
     assert mem.peak <= budget <= 2 << 30, f"peak direct memory {mem.peak} bytes"
     _ok(L.jg_graph_destroy(g))
     _ok(L.jg_ctx_destroy(ctx))
+
+
+def test_ctx_destroy_before_graph_is_refused(oracle_lib):
+    """VERDICT r05 item 3 (the r05f segfault): jg_ctx_destroy while a graph or builder of the context is
+    alive returns JG_ERR_STATE and leaves the context usable; the graph still runs, then everything tears
+    down in the right order.  (Before: the context destroyed its streams and a later jg_graph_destroy
+    synchronised a destroyed stream.)  Error style: FulgoraGraphComputer.java:241-243."""
+    from janusgraph_amd import _lib
+    o = oracle_lib
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    _ok(L.jg_ctx_create((ctypes.c_int * 1)(0), 1, ctypes.byref(ctx)))
+    g = ctypes.c_void_p()
+    _ok(L.jg_graph_build_rmat(ctx, 10, 16, 7, 2, ctypes.byref(g)))  # ADJ_IN
+    b = ctypes.c_void_p()
+    _ok(L.jg_builder_create(ctx, ctypes.byref(b)))
+    assert L.jg_ctx_destroy(ctx) == _lib.JG_ERR_STATE
+    assert b"still alive" in L.jg_last_error()
+    _ok(L.jg_builder_destroy(b))
+    assert L.jg_ctx_destroy(ctx) == _lib.JG_ERR_STATE  # the graph is still alive
+    n = 1 << 10
+    rank = np.empty(n, np.float64)
+    cnt = np.empty(n, np.float64)
+    _ok(L.jg_pagerank(g, ctypes.c_double(0.85), n, 10, _p(rank), _p(cnt)))  # the context still works
+    s, t = o.rmat_edges(10, 16, 7)
+    ref, _ = o.pagerank(n, s.astype(np.int32), t.astype(np.int32), 0.85, n, 10)
+    assert (np.abs(rank - ref) / np.abs(ref)).max() <= 1e-9
+    _ok(L.jg_graph_destroy(g))
+    _ok(L.jg_ctx_destroy(ctx))
