@@ -41,6 +41,22 @@ def window_end(block, t0, runs=1):
     WINDOWS.append([block, t0, time.monotonic_ns(), runs])
 
 
+def code_identity():
+    """What this line was measured with: the commit the tree was at (JG_BENCH_HEAD, set by the GPU scripts:
+    the box gets the tree without .git) and content hashes of bench.py and the library it loaded."""
+    import hashlib
+
+    def sha16(path):
+        try:
+            with open(path, "rb") as f:
+                return hashlib.sha256(f.read()).hexdigest()[:16]
+        except OSError:
+            return None
+    return os.environ.get("JG_BENCH_HEAD"), {"bench_py_sha16": sha16(os.path.join(ROOT, "bench.py")),
+                                             "libjanusgpu_sha16": sha16(os.path.join(ROOT, "janusgraph_amd",
+                                                                                     "libjanusgpu.so"))}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -304,7 +320,7 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True, cpu_seconds=10.0):
     gb = ctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
     deg = both_degrees(jg, ctl, gb)
     cand = pick_sources(deg, 4 * nsrc, scale)
-    times, teps, srcs, ranks = [], [], [], []
+    times, teps, srcs, ranks, walls, keep_ms, keep_walls = [], [], [], [], [], [], []
     for sv in cand.tolist():
         if len(srcs) == nsrc:
             break
@@ -312,24 +328,41 @@ def bfs_block(jg, ctx, ctl, scale, ef, nsrc=6, cpu=True, cpu_seconds=10.0):
         if ctx.stats()["edges_traversed"] < m // 100:
             continue  # a source in a tiny component: Graph500 resamples
         ctx.set_profiling(ctl.ws > 1)  # N > 1: exchange_ms from events around every exchange step
+        ctl.barrier()
         w0 = window_start()
+        t0 = time.perf_counter()
         gb.bfs([sv], jg.DIR_BOTH, want=False)  # timed run (the first touched cold pages)
+        wall = (time.perf_counter() - t0) * 1e3
         window_end(f"bfs_spvp_rmat{scale}_ef{ef}", w0)
         st = ctx.stats()
         ctx.set_profiling(False)
         ms = ctl.max(st["compute_ms"])
         srcs.append(sv)
         times.append(ms)
+        walls.append(ctl.max(wall))
         teps.append(st["edges_traversed"] / (ms * 1e-3) / 1e9)
         ranks.append(ctl.gather([st["compute_ms"], st["exchange_ms"]]))
+        # the ShortestPathVertexProgram drop-in's call (GpuGraphComputer: jg_bfs_keep, the depth row kept on
+        # the device for the walk-back), entry to return
+        ctl.barrier()
+        t0 = time.perf_counter()
+        gb.bfs_keep([sv], jg.DIR_BOTH)
+        keep_walls.append(ctl.max((time.perf_counter() - t0) * 1e3))
+        keep_ms.append(ctl.max(ctx.stats()["compute_ms"]))
     gb.close()
     ms = float(np.median(times))
     workload = f"bfs_spvp_rmat{scale}_ef{ef}"
     blk = {"workload": workload, "gteps_median": round(float(np.median(teps)), 3), "ms_median": round(ms, 4),
+           "wall_ms_median": round(float(np.median(walls)), 4),
            "runs": len(times), "sources": [int(x) for x in srcs],
-           "timed_region": "HIP events from the init launch to the end of the last level batch; the source's id "
-                           "lookup, the host's read of the final level state and the depth output (want=False: "
-                           "none) are outside"}
+           "timed_region": "ms: HIP events from the init launch to the end of the last level batch (the depth init "
+                           "covers every row a BOTH traversal can reach; the empty suffix keeps -1 between calls); "
+                           "wall_ms: the call from entry to return (source id lookup, level launches, the host's "
+                           "read of the final level state), max over ranks",
+           "spvp_keep": {"ms_median": round(float(np.median(keep_ms)), 4),
+                         "wall_ms_median": round(float(np.median(keep_walls)), 4),
+                         "call": "jg_bfs_keep (GpuGraphComputer's ShortestPathVertexProgram path: the depth row kept "
+                                 "on the device), same sources; wall_ms from entry to return"}}
     if ctl.ws == 1:
         blk["roofline"] = hbm_roofline(8.0 * m + 12.0 * n, ms, "direction-optimising BFS, one traversal "
                                        "(bfs_init_kernel + bfs_level_kernel launches)", workload,
@@ -413,8 +446,11 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
         cg = cctx.build_rmat(scale, ef, 0x5EED + scale, flags=jg.ADJ_BOTH)
     cg.connected_components()  # warm
     cctx.set_profiling(ctl.ws > 1 and not replicated)  # sharded: exchange_ms from events around every exchange
+    ctl.barrier()
     w0 = window_start()
+    t0 = time.perf_counter()
     comp, it = cg.connected_components()
+    cc_wall = ctl.max((time.perf_counter() - t0) * 1e3)
     window_end(f"cc_rmat{scale}_ef{ef}", w0)
     st = cctx.stats()
     cctx.set_profiling(False)
@@ -427,9 +463,11 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
         comp = ctl.min_array(comp)  # each rank filled its own rows (the others hold INT64_MAX)
     counts = np.bincount(comp, minlength=n)  # RMAT ids are 0..n-1: labels are vertex ids
     wl_cc = f"cc_rmat{scale}_ef{ef}"
-    cc = {"workload": wl_cc, "ms": round(cc_ms, 3), "iterations": it,
-          "timed_region": "HIP events around the union-find passes and the superstep-count BFS; the label output "
-                          "(cc_output_kernel: rank labels to vertex ids, scattered to caller order) is outside",
+    cc = {"workload": wl_cc, "ms": round(cc_ms, 3), "iterations": it, "wall_ms": round(cc_wall, 3),
+          "timed_region": "ms: HIP events around the union-find passes, the superstep-count BFS and (one GPU) the "
+                          "caller-order output (cc_output_kernel: every vertex's component id, edgeless rows "
+                          "included, gathered into caller order on the device); wall_ms: the call from entry to "
+                          "return, which adds the copy of the n int64 ids to the caller's host array",
           "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
           "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
                        "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"
@@ -444,7 +482,7 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
                                       "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
                                       "58 B per row with an edge (union-find passes + BFS start), 12 B per entry "
                                       "linked in the second round, 4 B per entry of the rows the BFS reached "
-                                      "(jg_cc.hip cc_union_find)")
+                                      "(jg_cc.hip cc_union_find), 24 B per vertex of the caller-order output")
     else:
         cc["per_rank"] = per_rank_rows(cc_rank)
     # 64 sources among the degree > 0 vertices; TEPS counts each source's component edges
@@ -454,17 +492,21 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
     del comp, counts, comp_edges
     g.bfs(srcs, jg.DIR_BOTH, want=False)  # warm
     ctx.set_profiling(ctl.ws > 1)
+    ctl.barrier()
     w0 = window_start()
+    t0 = time.perf_counter()
     g.bfs(srcs, jg.DIR_BOTH, want=False)
+    ms_wall = ctl.max((time.perf_counter() - t0) * 1e3)
     window_end(f"msbfs64_rmat{scale}_ef{ef}", w0)
     st = ctx.stats()
     ctx.set_profiling(False)
     ms = ctl.max(st["compute_ms"])
     wl_ms = f"msbfs64_rmat{scale}_ef{ef}"
     msb = {"workload": wl_ms, "sources": int(len(srcs)), "ms": round(ms, 3), "levels": st["levels"],
-           "timed_region": "HIP events from the state fills to the last level; the sources' id lookup and the depth "
-                           "rows (want=False: not materialised; the per-level words are an exact encoding) are "
-                           "outside",
+           "wall_ms": round(ms_wall, 3),
+           "timed_region": "ms: HIP events from the state fills to the last level; the depth rows (want=False: not "
+                           "materialised; the per-level words are an exact encoding) are outside; wall_ms: the call "
+                           "from entry to return (the sources' id lookup, launches, level-control reads)",
            "gteps": round(edges / (ms * 1e-3) / 1e9, 1),
            "gteps_note": "sum over the 64 sources (degree > 0) of the input edges in the source's component / time"}
     if ctl.ws == 1:
@@ -580,6 +622,7 @@ def main():
         }
         if per_rank is not None:
             line["per_rank"] = per_rank
+        line["head"], line["code"] = code_identity()
         line.update(extra)
         if args.trace_windows:
             line["trace_windows"] = {"clock": "CLOCK_MONOTONIC ns", "windows": WINDOWS}

@@ -111,7 +111,10 @@ typedef struct jg_graph_info {
 
 typedef struct jg_stats {
     int32_t supersteps;          /* memory().getIteration() of the equivalent Fulgora run           */
-    int32_t levels;              /* BFS/SSSP levels or CC sweeps actually executed on the GPU       */
+    int32_t levels;              /* passes actually executed on the GPU; the unit depends on the path:
+                                  * BFS: levels; CC: union-find BFS levels or propagation sweeps;
+                                  * shortest distance: supersteps (hop-bounded Bellman-Ford) or, on the
+                                  * unbounded delta-stepping path, near-far passes      */
     double  build_ms;            /* last jg_graph_build*: snapshot -> CSR on device                 */
     double  compute_ms;          /* last program: HIP-event time of the superstep loop              */
     double  exchange_ms;         /* HIP-event time of the exchange steps (profiling on, sharded)    */

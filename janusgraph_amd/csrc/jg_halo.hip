@@ -491,6 +491,40 @@ void exchange_halo_bits(Graph& g, uint32_t adj, std::vector<uint64_t*>& sends, s
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
+void exchange_halo_bits_both(Graph& g, uint32_t adj, std::vector<uint64_t*>& fsend, std::vector<uint64_t*>& fbitmap,
+                             std::vector<uint64_t*>& rbitmap, std::vector<uint64_t*>& rsend) {
+    if (g.P == 1) return;
+    Ctx& c = *g.ctx;
+    if (c.logical || c.host_transport) {  // (the sharded DO-BFS copies one direction by kernel on one device)
+        exchange_halo_bits(g, adj, fsend, fbitmap, false);
+        exchange_halo_bits(g, adj, rsend, rbitmap, true);
+        return;
+    }
+    ExchTimer et(g);
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        const Halo& h = g.halo(sh, adj);
+        DeviceGuard dg(sh);
+        const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
+        for (int q = 0; q < g.P; ++q) {
+            if (q == sh.index) continue;
+            const int64_t mine = (h.send_off[(size_t)q + 1] - h.send_off[(size_t)q] + 63) / 64;    // my vertices q reads
+            const int64_t theirs = (h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q] + 63) / 64;  // q's vertices I read
+            const int64_t seg = (((int64_t)h.seg_of(q, sh.index) << h.tbits) >> 6);
+            if (mine > 0) {
+                rccl_check(ncclSend(fsend[i] + woff[(size_t)q], (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
+                rccl_check(ncclRecv(rsend[i] + woff[(size_t)q], (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
+            }
+            if (theirs > 0) {
+                rccl_check(ncclRecv(fbitmap[i] + seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
+                rccl_check(ncclSend(rbitmap[i] + seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
+            }
+        }
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::vector<std::vector<int64_t>>& soff,
                    const std::vector<std::vector<int64_t>>& scount, const std::vector<char*>& recv,
                    const std::vector<std::vector<int64_t>>& roff, const std::vector<std::vector<int64_t>>& rcount,

@@ -87,6 +87,8 @@ struct SliceBand {
     // whether band row i has entries in sub-slice h; its number is w.y + the set bits of w.x below it
     DevBuf<uint2> sub_word;     // [S][words], words = ceil(rows of the band / 32)
     DevBuf<int32_t> task_rows;  // [tasks][2]: band rows of the task's first and last entry
+    mutable DevBuf<int32_t> ab_srow;        // Tune::ab_fold experiment: band row of each sub-row
+    mutable DevBuf<unsigned char> ab_acc;   // Tune::ab_fold experiment: [8][rows] accumulators
     int64_t rows() const { return row_end - row_begin; }
 };
 
@@ -400,6 +402,10 @@ void exchange_runs(Graph& g, const std::vector<const char*>& send, const std::ve
                    const std::vector<std::vector<int64_t>>& scount, const std::vector<char*>& recv,
                    const std::vector<std::vector<int64_t>>& roff, const std::vector<std::vector<int64_t>>& rcount,
                    size_t eb, ncclDataType_t type);
+// Both directions of exchange_halo_bits in one grouped step (the sharded DO-BFS, whose level direction is
+// decided on the device): forward fsend -> fbitmap segments, and reverse rbitmap segments -> rsend.
+void exchange_halo_bits_both(Graph& g, uint32_t adj, std::vector<uint64_t*>& fsend, std::vector<uint64_t*>& fbitmap,
+                             std::vector<uint64_t*>& rbitmap, std::vector<uint64_t*>& rsend);
 // word offsets of the per-peer send-list runs of exchange_halo_bits ([P + 1])
 std::vector<int64_t> halo_word_offsets(const Halo& h, int P);
 // Builds shard sh's halo plan for adjacency `which` (0 IN, 2 BOTH) from the full edge list.
@@ -649,6 +655,9 @@ struct Tune {
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
                                           // stores, -1 = automatic from the band's heads per task)
+    int ab_fold = 0;                  // A/B EXPERIMENT ONLY (results are not PageRank):
+                                      // band 0's sub-row sums go to one accumulator per (row, XCD), read-
+                                      // modified-written round by round, instead of a partial per sub-row
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
                                       // (0: 32 bits, 24: at least 24; tests)
 };

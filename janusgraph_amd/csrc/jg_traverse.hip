@@ -1636,6 +1636,12 @@ BfsCsrs pick_csrs(const Shard& sh, int direction) {
 // the pull adjacency of a traversal, as the key of its gathered vector's layout (Graph::vec_pos)
 uint32_t adj_of(const Shard& sh, const BfsCsrs& c) { return c.pull == &sh.both ? JG_ADJ_BOTH : JG_ADJ_IN; }
 
+// rows [0, live) of the pull adjacency have entries; from there on none (the degree-sorted empty suffix):
+// no level after 0 reaches or finalises them
+int64_t pull_live_rows(const Shard& sh, const BfsCsrs& c) {
+    return c.pull && c.pull->empty_from >= 0 ? std::min(c.pull->empty_from, sh.rows) : sh.rows;
+}
+
 // Direction-optimising single-source BFS on one shard; depth (device, [rows]) receives the result.
 // Returns levels run; *edges_out = adjacency entries of reached vertices (degree CSR).
 }  // namespace
@@ -1855,192 +1861,114 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
 }
 
 // ---------------- sharded direction-optimising BFS (BOTH adjacency, halo plan) ----------------
-// Each shard owns its rows and their depths (dvec, [rows]).  Column ids of the BOTH CSR are compact:
-// own rows [0, rows), then one segment per peer (its vertices this shard's rows touch).  Frontiers cross
-// shards as bits (exchange_halo_bits: a 14.7 M-vertex halo per shard at RMAT-26, P = 8, is 1.8 MB of
-// words instead of 59 MB of int32 depths, moved every level):
-//  * bottom-up: each owner packs "depth == level" of its send lists into words, the forward exchange
-//    lands them in the readers' compact bitmaps, and own unvisited rows probe own depths and those bits;
-//  * top-down: edge-parallel over the local frontier; own targets are claimed by CAS, remote ones are
-//    stamped with the level (a plain store: same-address CAS or atomicOr would queue at the memory side
-//    behind the hub targets every shard's frontier reaches), the stamps are packed into the compact
-//    bitmap's segment words, and the reverse exchange hands those to the owners, which claim the marked
-//    send-list rows.
-// One packed counter per shard and level ((vertices << 37) | degree sum), summed over shards and ranks,
-// drives Beamer's direction rule on the host.  Appends are wave-staged (WaveApp), as in the one-shard
-// traversal; a block-wide append cost three barriers per 256 rows or words.
+// Each shard owns its rows and their depths (Shard::bfs_depth, [rows]).  Column ids of the BOTH CSR are
+// compact: own rows [0, rows), then one segment per peer (its vertices this shard's rows touch).
+// Frontiers cross shards as bits (a 14.7 M-vertex halo per shard at RMAT-26, P = 8, is 1.8 MB of words
+// instead of 59 MB of int32 depths):
+//  * bottom-up: each owner packs "depth == level" of its send lists into words (sw), the forward
+//    exchange lands them in the readers' compact bitmaps (hb), and own unvisited rows probe own depths
+//    and those bits;
+//  * top-down: edge-parallel over the local frontier; own targets are claimed by CAS, a remote target is
+//    stamped with a plain byte store (st8, zero between levels: a same-word atomicOr into a bitmap
+//    queued behind the hub targets, RMAT-26 level 2 61 -> 146 us per shard), the stamps are packed into
+//    the compact mark bitmap's segment words (mk) and cleared, the reverse exchange hands the marks to
+//    the owners (rm), which claim the marked send-list rows.
+// Level control lives on the device: one packed counter per shard and level
+// ((vertices << 37) | entries) is summed over shards and ranks on the stream -- by the deciding kernels
+// themselves over the shards' counter rings when the shards share a device, by a stream-ordered
+// ncclAllReduce otherwise (over the host only in host-transport mode) -- and every kernel of level L takes
+// Beamer's decision from level L-1's state and global counter, so the host enqueues whole batches of
+// levels and reads the state once per batch (as dobfs_single does).  Both directions' words travel in
+// every level's exchange (a few MB), so the host never needs the direction.  A level is four steps:
+// sbfs_pre_kernel (pack the send-list bits | top-down push), sbfs_mid_kernel (- | pack the stamps), the
+// exchange, sbfs_post_kernel (bottom-up probes | claim the received marks), then the counter reduction.
+// Appends are wave-staged (WaveApp); the appending launches stay at ~2 K workgroups, since every
+// workgroup ends with one device atomic on the level's counter (~88 per us at the memory side).
+constexpr int kSRing = 4;  // level-state ring: level L reads slot L-1, writes L, zeroes L+1
+// shard count the sharded traversal takes (CC checks it too before choosing its sharded path)
+constexpr int kMaxShardsBfs = 64;
+
+struct SBfsState {
+    long long mu;     // entries of all shards not yet in any frontier (after this level's input frontier)
+    long long edges;  // entries summed over every frontier so far (all shards)
+    int bottom_up;    // direction this level runs in
+    int done;         // traversal finished: this level and all later ones do nothing
+    int levels;       // levels run (valid once done)
+    int pad;
+};
+
 struct SBfsLevel {
     const int64_t* rp;
     const int32_t* col;
     const int32_t* first_col;       // [rows] each row's first column (Csr::first_col)
     int64_t rows;
+    int64_t bu_rows;                // rows [bu_rows, rows) have no entry (BOTH empty suffix): never probed
     int32_t* dvec;                  // [rows] own depths
-    int32_t* stamp;                 // [C] top-down: level + 1 on the halo vertices this level reached
-    unsigned long long* hb;         // compact bitmap: halo frontier bits (bottom-up) / remote marks (top-down)
+    unsigned long long* hb;         // compact bitmap: the peers' frontier bits, received forward (bottom-up)
+    unsigned long long* mk;         // compact bitmap: this level's remote marks (top-down), packed from st8
+    uint8_t* st8;                   // compact byte map: remote targets stamped by the top-down push
+    unsigned long long* sw;         // send-list words: own frontier bits for the peers (bottom-up)
+    const unsigned long long* rm;   // send-list words: the peers' marks of own rows, received back (top-down)
     const int32_t* queue_in;
     const int64_t* qoff_in;   // first frontier edge of each queue entry (edge-parallel top-down)
-    int64_t nq, mf;           // local frontier: vertices, entries
     int32_t* queue_out;
     int64_t* qoff_out;
-    unsigned long long* sw;         // send-list words (packed bottom-up bits / received top-down marks)
     const int64_t* send_off;        // [P + 1] send-list element offsets per peer
     const int64_t* woff;            // [P + 1] send-list word offsets per peer
-    const int64_t* rwoff;           // [P + 1] receive-run word offsets per peer (segment words, packed)
     const int64_t* rseg;            // [P] first position of each peer's segment in the compact vector
     const int64_t* rlen;            // [P] length of each peer's run in this shard's segment
     int P;
-    const int32_t* send_src;  // own row of each send-list position
-    unsigned long long* packed;       // this level's appends (the host reads it after the level)
-    unsigned long long* packed_next;  // the next level's counter: zeroed by this level's kernels
-    int32_t level;
+    const int32_t* send_src;        // own row of each send-list position
+    unsigned long long* ctr;        // [kSRing] this shard's packed counters: slot L = level L's appends
+    const unsigned long long* gsum[kMaxShardsBfs];  // counter rings whose sum is the global counter (by
+    int nsum;                                       // value: the decision's loads issue together)
+    SBfsState* st;                  // [kSRing] this shard's copy of the (identical) level decisions
+    int32_t level, max_depth;
+    double alpha, beta;
+    int64_t nrows;                  // rows of all shards (the beta rule)
 };
-
-// shard count the sharded traversal takes (CC checks it too before choosing its sharded path)
-constexpr int kMaxShardsBfs = 64;
 
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
     const int lo = __shfl((int)(uint32_t)v, src, kWave), hi = __shfl((int)(uint32_t)(v >> 32), src, kWave);
     return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-__device__ __forceinline__ void sbfs_zero_next(const SBfsLevel& a) {
-    if (a.packed_next && blockIdx.x == 0 && threadIdx.x == 0) *a.packed_next = 0ull;
-}
-
-// top-down, edge-parallel over the local frontier's entries (as bfs_top_down): own neighbours are
-// claimed by CAS, remote ones stamped
-__global__ __launch_bounds__(kBlock) void sbfs_td_push_kernel(SBfsLevel a) {
-    __shared__ WaveStage ws;
-    WaveApp app{ws};
-    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t per_tile = nthreads * kTdEdgesPerThread;
-    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
-    const int32_t nd = a.level + 1;
-    sbfs_zero_next(a);
-    for (int64_t t = 0; t < tiles; ++t) {
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x + wave_id() * kWave) * kTdEdgesPerThread >= a.mf)
-            break;  // wave-uniform
-        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
-        int64_t i = 0, next_bound = 0;
-        if (e0 < a.mf) {
-            int64_t lo = 0, hi = a.nq - 1;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) >> 1;
-                if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
-            }
-            i = lo;
-            next_bound = i + 1 < a.nq ? a.qoff_in[i + 1] : a.mf;
-        }
-#pragma unroll
-        for (int k = 0; k < kTdEdgesPerThread; ++k) {
-            const int64_t e = e0 + k;
-            bool take = false;
-            int32_t u = 0;
-            int64_t deg = 0;
-            if (e < a.mf) {
-                while (e >= next_bound) {
-                    ++i;
-                    next_bound = i + 1 < a.nq ? a.qoff_in[i + 1] : a.mf;
-                }
-                const int32_t v = a.queue_in[i];
-                u = a.col[a.rp[v] + (e - a.qoff_in[i])];
-                if (u < a.rows) {
-                    if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
-                        take = true;
-                        deg = a.rp[u + 1] - a.rp[u];
-                    }
-                } else {
-                    a.stamp[u] = nd;
-                }
-            }
-            app.append(take, u, deg, a.queue_out, a.qoff_out, a.packed);
-        }
+// Level L's decision from level L-1's state and global counter (Beamer: bottom-up when the frontier's
+// entries outweigh the unexplored ones / alpha, back top-down when the frontier falls below rows / beta);
+// *nq / *mf = this shard's own input frontier.  Every shard and rank computes the same state.
+__device__ SBfsState sbfs_decide(const SBfsLevel& a, long long* nq, long long* mf) {
+    const int pl = (a.level + kSRing - 1) % kSRing;
+    const SBfsState p = a.st[pl];
+    const unsigned long long own = a.ctr[pl];
+    *nq = (long long)(own >> kPackShift);
+    *mf = (long long)(own & kEdgeMask);
+    if (p.done) return p;
+    unsigned long long h = 0;
+    for (int k = 0; k < kMaxShardsBfs; ++k)
+        if (k < a.nsum) h += a.gsum[k][pl];
+    const long long gnf = (long long)(h >> kPackShift), gmf = (long long)(h & kEdgeMask);
+    SBfsState c = p;
+    c.mu = p.mu - gmf;
+    c.edges = p.edges + gmf;
+    if (gnf == 0 || (a.max_depth >= 0 && a.level >= a.max_depth)) {
+        c.done = 1;
+        c.levels = a.level;
+        return c;
     }
-    app.final(a.queue_out, a.qoff_out, a.packed);
+    if (!p.bottom_up && (double)gmf > (double)c.mu / a.alpha) c.bottom_up = 1;
+    else if (p.bottom_up && (double)gnf < (double)a.nrows / a.beta) c.bottom_up = 0;
+    return c;
 }
 
-// The per-word kernels below (pack_marks, td_apply, pack_bits) run on a (blocks, P) grid: blockIdx.y
-// is the peer whose run a block works on, so no word has to search the per-peer offset tables (a scan
-// of LDS-staged tables per word, and one wave per word and launch, held them to 45-80 us per launch at
-// RMAT-26, P = 8, for 1.8 M-word send lists).  A wave takes kSbfsWords words per trip with every load
-// issued on a clamped index before any is used.
+// The per-word passes run on a (blocks, P) grid: blockIdx.y is the peer whose run a block works on, so
+// no word searches the per-peer offset tables (a scan of LDS-staged tables per word held them to 45-80 us
+// per launch at RMAT-26, P = 8, round 4).  The row-parallel passes use the same grid flattened.
 constexpr int kSbfsWords = 4;
-constexpr int kSbfsApplyChunk = 16;  // td_apply: words a wave loads at once (lanes 0..15), then walks
-
-// top-down, reader side: this level's stamps of peer q's segment into its compact bitmap words
-__global__ __launch_bounds__(kBlock) void sbfs_pack_marks_kernel(SBfsLevel a) {
-    sbfs_zero_next(a);
-    const int q = blockIdx.y;
-    const int64_t nw = a.rwoff[q + 1] - a.rwoff[q], len = a.rlen[q], seg = a.rseg[q];
-    const int32_t* __restrict__ stamp = a.stamp + seg;
-    unsigned long long* __restrict__ hb = a.hb + (seg >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-    const int32_t nd = a.level + 1;
-    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
-        int32_t val[kSbfsWords];
-        bool in[kSbfsWords];
-#pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
-            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
-            in[k] = j < len;
-            val[k] = stamp[in[k] ? j : len - 1];  // words exist only for len > 0
-        }
-#pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
-            const uint64_t word = __ballot(in[k] && val[k] == nd);
-            if (lane_id() == 0 && w0 + k * nwaves < nw) hb[w0 + k * nwaves] = word;
-        }
-    }
-}
-
-// top-down, owner side: received words of peer q's run; a wave loads kSbfsApplyChunk words and claims
-// the rows of their set bits, kSbfsWords non-zero words at a time (lane b: the row of bit b)
-__global__ __launch_bounds__(kBlock) void sbfs_td_apply_kernel(SBfsLevel a) {
-    __shared__ WaveStage ws;
-    sbfs_zero_next(a);
-    WaveApp app{ws};
-    const int q = blockIdx.y;
-    const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
-    const int32_t* __restrict__ src = a.send_src + so;
-    const int64_t step = (int64_t)gridDim.x * (kBlock / kWave) * kSbfsApplyChunk;
-    const int32_t nd = a.level + 1;
-    for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / kWave) + wave_id()) * kSbfsApplyChunk; c0 < nw;
-         c0 += step) {  // wave-uniform
-        const unsigned long long mine =
-            lane_id() < kSbfsApplyChunk && c0 + lane_id() < nw ? a.sw[wo + c0 + lane_id()] : 0ull;
-        uint64_t nz = __ballot(mine != 0ull);
-        while (nz) {  // wave-uniform
-            unsigned long long word[kSbfsWords];
-            int32_t u[kSbfsWords];
-#pragma unroll
-            for (int k = 0; k < kSbfsWords; ++k) {
-                const int l = nz ? __ffsll((unsigned long long)nz) - 1 : 0;
-                word[k] = nz ? shfl_u64(mine, l) : 0ull;
-                nz &= nz - 1;
-                const int64_t x = (c0 + l) * 64 + lane_id();
-                u[k] = src[x < cnt ? x : cnt - 1];  // bits past the run's end are never set
-            }
-#pragma unroll
-            for (int k = 0; k < kSbfsWords; ++k) {
-                if (!word[k]) continue;  // wave-uniform
-                bool take = false;
-                int64_t deg = 0;
-                if (((word[k] >> lane_id()) & 1ull) && a.dvec[u[k]] < 0 && atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
-                    take = true;
-                    deg = a.rp[u[k] + 1] - a.rp[u[k]];
-                }
-                app.append(take, u[k], deg, a.queue_out, a.qoff_out, a.packed);
-            }
-        }
-    }
-    app.final(a.queue_out, a.qoff_out, a.packed);
-}
 
 // bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = the depth of the
-// word's row b is this level's
-__global__ __launch_bounds__(kBlock) void sbfs_pack_bits_kernel(SBfsLevel a) {
-    sbfs_zero_next(a);
+// word's row b is this level's.  A wave takes kSbfsWords words per trip, every load issued on a clamped
+// index before any is used.
+__device__ __forceinline__ void sbfs_pack_bits(const SBfsLevel& a) {
     const int q = blockIdx.y;
     const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
     const int32_t* __restrict__ src = a.send_src + so;
@@ -2065,20 +1993,70 @@ __global__ __launch_bounds__(kBlock) void sbfs_pack_bits_kernel(SBfsLevel a) {
     }
 }
 
-// bottom-up over own rows: a neighbour is in the frontier if its depth (own) or bit (halo) says so
-__global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
-    __shared__ WaveStage ws;
-    WaveApp app{ws};
-    const int64_t words = (a.rows + 63) / 64;
-    constexpr int kWpb = kBlock / kWave;
-    const int64_t wstride = (int64_t)gridDim.x * kWpb;
+// top-down, edge-parallel over the local frontier's nq vertices and mf entries (as bfs_top_down): own
+// neighbours are claimed by CAS, remote ones marked
+__device__ __forceinline__ void sbfs_td_push(const SBfsLevel& a, int64_t nq, int64_t mf, WaveApp& app) {
+    const int64_t bid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t nthreads = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+    const int64_t tid = bid * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (mf + per_tile - 1) / per_tile;
     const int32_t nd = a.level + 1;
-    sbfs_zero_next(a);
-    for (int64_t w = (int64_t)blockIdx.x * kWpb + wave_id(); w < words; w += wstride) {  // wave-uniform
+    unsigned long long* packed = a.ctr + a.level % kSRing;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + bid * blockDim.x + wave_id() * kWave) * kTdEdgesPerThread >= mf) break;  // wave-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < mf) {
+            int64_t lo = 0, hi = nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff_in[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < nq ? a.qoff_in[i + 1] : mf;
+        }
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
+            bool take = false;
+            int32_t u = 0;
+            int64_t deg = 0;
+            if (e < mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < nq ? a.qoff_in[i + 1] : mf;
+                }
+                const int32_t v = a.queue_in[i];
+                u = a.col[a.rp[v] + (e - a.qoff_in[i])];
+                if (u < a.rows) {
+                    if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                        take = true;
+                        deg = a.rp[u + 1] - a.rp[u];
+                    }
+                } else {
+                    a.st8[u] = 1;
+                }
+            }
+            app.append(take, u, deg, a.queue_out, a.qoff_out, packed);
+        }
+    }
+}
+
+// bottom-up over own rows [0, bu_rows): a neighbour is in the frontier if its depth (own) or bit (halo)
+// says so; the flattened grid walks 64-row words, one per wave
+__device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app) {
+    const int64_t words = (a.bu_rows + 63) / 64;
+    constexpr int kWpb = kBlock / kWave;
+    const int64_t bid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t wstride = (int64_t)gridDim.x * gridDim.y * kWpb;
+    const int32_t nd = a.level + 1;
+    unsigned long long* packed = a.ctr + a.level % kSRing;
+    for (int64_t w = bid * kWpb + wave_id(); w < words; w += wstride) {  // wave-uniform
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t deg = 0;
-        if (v < a.rows && a.dvec[v] < 0) {
+        if (v < a.bu_rows && a.dvec[v] < 0) {
             auto in_frontier = [&](int32_t x) -> bool {
                 return x < a.rows ? a.dvec[x] == a.level : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
             };
@@ -2099,60 +2077,256 @@ __global__ __launch_bounds__(kBlock) void sbfs_bu_kernel(SBfsLevel a) {
                 deg = j1 - j0;
             }
         }
-        app.append(found, (int32_t)v, deg, a.queue_out, a.qoff_out, a.packed);
-    }
-    app.final(a.queue_out, a.qoff_out, a.packed);
-}
-
-__global__ void sbfs_init_kernel(int32_t* __restrict__ dvec, int64_t rows, int64_t src, int32_t* __restrict__ queue,
-                                 int64_t* __restrict__ qoff) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x)
-        dvec[i] = i == src ? 0 : -1;
-    if (src >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-        queue[0] = (int32_t)src;
-        qoff[0] = 0;
+        app.append(found, (int32_t)v, deg, a.queue_out, a.qoff_out, packed);
     }
 }
 
-// Multi-root start of the sharded traversal (cc_root_eccentricity_sharded): an own row with an edge
-// whose label is its own rank is its component's minimum-rank vertex, a level-0 root.
-__global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(int32_t* __restrict__ dvec, int64_t rows, CcRoots r,
-                                                                 const int64_t* __restrict__ rp, int32_t* queue,
-                                                                 int64_t* qoff, unsigned long long* packed) {
+// top-down, owner side: the received words of peer q's run, 64 per wave and trip (lane l loads word l);
+// the rows of the set bits are claimed kSbfsWords non-zero words at a time (lane b: the row of bit b).
+__device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) {
+    const int q = blockIdx.y;
+    const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
+    const int32_t* __restrict__ src = a.send_src + so;
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+    const int32_t nd = a.level + 1;
+    unsigned long long* packed = a.ctr + a.level % kSRing;
+    for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / kWave) + wave_id()) * kWave; c0 < nw; c0 += nwaves * kWave) {
+        const unsigned long long mine = c0 + lane_id() < nw ? a.rm[wo + c0 + lane_id()] : 0ull;
+        uint64_t nz = __ballot(mine != 0ull);
+        while (nz) {  // wave-uniform
+            unsigned long long word[kSbfsWords];
+            int32_t u[kSbfsWords];
+#pragma unroll
+            for (int k = 0; k < kSbfsWords; ++k) {
+                const int l = nz ? __ffsll((unsigned long long)nz) - 1 : 0;
+                word[k] = nz ? shfl_u64(mine, l) : 0ull;
+                nz &= nz - 1;
+                const int64_t x = (c0 + l) * 64 + lane_id();
+                u[k] = src[x < cnt ? x : cnt - 1];  // bits past the run's end are never set
+            }
+#pragma unroll
+            for (int k = 0; k < kSbfsWords; ++k) {
+                if (!word[k]) continue;  // wave-uniform
+                bool take = false;
+                int64_t deg = 0;
+                if (((word[k] >> lane_id()) & 1ull) && a.dvec[u[k]] < 0 && atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
+                    take = true;
+                    deg = a.rp[u[k] + 1] - a.rp[u[k]];
+                }
+                app.append(take, u[k], deg, a.queue_out, a.qoff_out, packed);
+            }
+        }
+    }
+}
+
+// First kernel of a level: the decision (block (0, 0) publishes it and zeroes the next level's counter),
+// then this shard's send-list bits (bottom-up) or its top-down push.
+__global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
+    __shared__ SBfsState s_st;
+    __shared__ long long s_nq, s_mf;
+    __shared__ WaveStage ws;
+    if (threadIdx.x == 0) {
+        long long nq, mf;
+        const SBfsState c = sbfs_decide(a, &nq, &mf);
+        s_st = c;
+        s_nq = nq;
+        s_mf = mf;
+        if (blockIdx.x == 0 && blockIdx.y == 0) {
+            a.st[a.level % kSRing] = c;
+            if (!c.done) a.ctr[(a.level + 1) % kSRing] = 0ull;
+        }
+    }
+    __syncthreads();
+    if (s_st.done) return;
+    if (s_st.bottom_up) {
+        sbfs_pack_bits(a);
+    } else {
+        WaveApp app{ws};
+        sbfs_td_push(a, s_nq, s_mf, app);
+        app.final(a.queue_out, a.qoff_out, a.ctr + a.level % kSRing);
+    }
+}
+
+// Second kernel of a top-down level (a bottom-up level leaves at once): peer q's segment of stamp bytes
+// into its mark words, every word written (zero or not: the words are the exchange's payload) and every
+// set byte cleared for the next top-down level; a wave takes kSbfsWords words per trip.
+__global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
+    __shared__ int s_run;
+    if (threadIdx.x == 0) {
+        const SBfsState c = a.st[a.level % kSRing];
+        s_run = !c.done && !c.bottom_up;
+    }
+    __syncthreads();
+    if (!s_run) return;
+    const int q = blockIdx.y;
+    const int64_t len = a.rlen[q], seg = a.rseg[q], nw = (len + 63) / 64;
+    uint8_t* __restrict__ stamp = a.st8 + seg;
+    unsigned long long* __restrict__ mk = a.mk + (seg >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
+        uint8_t b[kSbfsWords];
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
+            b[k] = j < len ? stamp[j] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int k = 0; k < kSbfsWords; ++k) {
+            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
+            const uint64_t word = __ballot(b[k] != 0);
+            if (b[k]) stamp[j] = 0;
+            if (lane_id() == 0 && w0 + k * nwaves < nw) mk[w0 + k * nwaves] = word;
+        }
+    }
+}
+
+// Last kernel of a level (after the exchange): bottom-up probes, or the claims of the received marks.
+__global__ __launch_bounds__(kBlock) void sbfs_post_kernel(SBfsLevel a) {
+    __shared__ SBfsState s_st;
+    __shared__ WaveStage ws;
+    if (threadIdx.x == 0) s_st = a.st[a.level % kSRing];
+    __syncthreads();
+    if (s_st.done) return;
+    WaveApp app{ws};
+    if (s_st.bottom_up) sbfs_bottom_up(a, app);
+    else sbfs_td_apply(a, app);
+    app.final(a.queue_out, a.qoff_out, a.ctr + a.level % kSRing);
+}
+
+// Shards on one device: the exchange as one kernel that copies, for every (owner, reader) pair, the
+// direction this level runs in (bottom-up: the owner's send-list words to the reader's segment; top-down:
+// the reader's marks back to the owner's received words), with the decision read from the first shard.
+struct SBfsCopyRun {
+    const unsigned long long* fsrc;  // forward: owner's send-list words for the reader
+    unsigned long long* fdst;        //          reader's bitmap segment for the owner
+    const unsigned long long* rsrc;  // reverse: reader's marks about the owner's vertices
+    unsigned long long* rdst;        //          owner's received words from the reader
+    int64_t n;                       // words
+};
+__global__ __launch_bounds__(kBlock) void sbfs_copy_kernel(const SBfsCopyRun* __restrict__ runs, const SBfsState* st,
+                                                           int slot) {
+    const SBfsState c = st[slot];
+    if (c.done) return;
+    const SBfsCopyRun r = runs[blockIdx.y];
+    const unsigned long long* __restrict__ s = c.bottom_up ? r.fsrc : r.rsrc;
+    unsigned long long* __restrict__ d = c.bottom_up ? r.fdst : r.rdst;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = s[i];
+}
+
+// the stamp bytes of every peer segment's run cleared (grid-stride)
+__device__ __forceinline__ void sbfs_zero_stamps(const SBfsLevel& a) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int q = 0; q < a.P; ++q) {
+        uint8_t* __restrict__ p = a.st8 + a.rseg[q];
+        const int64_t len = a.rlen[q], n4 = len >> 2;  // segments start 2^tbits apart: 4-byte aligned
+        for (int64_t i = tid; i < n4; i += stride) reinterpret_cast<uint32_t*>(p)[i] = 0u;
+        for (int64_t i = (n4 << 2) + tid; i < len; i += stride) p[i] = 0;
+    }
+}
+
+// Single-source start: depths (rows [0, init_rows): the caller keeps the empty suffix at -1), the
+// level-0 queue, the counter ring (level -1's slot: the source's own frontier) and the level -1 state;
+// the stamp bytes are cleared.
+__global__ __launch_bounds__(kBlock) void sbfs_init_kernel(SBfsLevel a, int64_t init_rows, int64_t src, long long total) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = tid; i < init_rows; i += stride) a.dvec[i] = i == src ? 0 : -1;
+    sbfs_zero_stamps(a);
+    if (tid == 0) {
+        const long long deg = src >= 0 ? (long long)(a.rp[src + 1] - a.rp[src]) : 0;
+        if (src >= 0) {
+            a.dvec[src] = 0;  // (also when the source lies in the skipped suffix: the caller refills it)
+            const_cast<int32_t*>(a.queue_in)[0] = (int32_t)src;
+            const_cast<int64_t*>(a.qoff_in)[0] = 0;
+        }
+        for (int k = 0; k < kSRing; ++k) a.ctr[k] = 0ull;
+        a.ctr[kSRing - 1] = src >= 0 ? (1ull << kPackShift) | (unsigned long long)deg : 0ull;
+        SBfsState s0{};
+        s0.mu = total;
+        a.st[kSRing - 1] = s0;
+    }
+}
+
+// Multi-root start (cc_root_eccentricity_sharded): an own row with an edge whose label is its own rank is
+// its component's minimum-rank vertex, a level-0 root; appended to level -1's counter slot (zeroed by
+// the caller).  Rows from r.ne on have no edge.
+__global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(SBfsLevel a, CcRoots r, long long total) {
     __shared__ WaveStage ws;
     WaveApp app{ws};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
+    int32_t* queue = const_cast<int32_t*>(a.queue_in);
+    int64_t* qoff = const_cast<int64_t*>(a.qoff_in);
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < a.rows; x0 += stride) {  // block-uniform trips
         const int64_t v = x0 + threadIdx.x;
         bool take = false;
         int64_t deg = 0;
-        if (v < rows) {
+        if (v < a.rows) {
             if (v < r.ne) {
-                deg = rp[v + 1] - rp[v];
+                deg = a.rp[v + 1] - a.rp[v];
                 take = deg > 0 && r.parent[v] == r.rank[v];
             }
-            dvec[v] = take ? 0 : -1;
+            a.dvec[v] = take ? 0 : -1;
         }
-        app.append(take, (int32_t)v, deg, queue, qoff, packed);
+        app.append(take, (int32_t)v, deg, queue, qoff, a.ctr + kSRing - 1);
     }
-    app.final(queue, qoff, packed);
+    app.final(queue, qoff, a.ctr + kSRing - 1);
+    sbfs_zero_stamps(a);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        SBfsState s0{};
+        s0.mu = total;
+        a.st[kSRing - 1] = s0;
+    }
+}
+
+// The level counters of slot `slot` summed into every shard's global slot (gctr), on the streams: a
+// grouped ncclAllReduce, or over the host in host-transport mode.  Shards sharing one device need no
+// step (the deciding kernels sum the shards' rings).
+void sbfs_reduce(Graph& g, const std::vector<unsigned long long*>& ctr, const std::vector<unsigned long long*>& gctr,
+                 int slot) {
+    Ctx& c = *g.ctx;
+    if (c.logical) return;
+    if (c.host_transport) {
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh);
+        unsigned long long v = 0;
+        copy_d2h(&v, ctr[0] + slot, sizeof v, sh.stream);
+        int64_t s = (int64_t)v;  // packed: the fields sum independently (neither overflows)
+        allreduce_sum_i64(g, &s, 1);
+        v = (unsigned long long)s;
+        copy_h2d(gctr[0] + slot, &v, sizeof v, sh.stream);
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh);
+        rccl_check(ncclAllReduce(ctr[i] + slot, gctr[i] + slot, 1, ncclUint64, ncclSum, sh.comm, sh.stream),
+                   "ncclAllReduce");
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
 // Sharded DO-BFS over BOTH from one source (src_shard, src_local) or, with `roots` (one per local
 // shard), from every component's minimum-rank vertex; returns levels run, *edges_out = entries of
-// reached rows.  Depths go to Shard::bfs_depth for a single source only.
+// reached rows.  Depths go to Shard::bfs_depth (rows of the empty suffix stay -1 between calls:
+// Shard::bfs_depth_tail_clean).
 int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth, double* edges_out, float* ms_out,
                   const CcRoots* roots = nullptr) {
+    Ctx& ctx = *g.ctx;
     const size_t ns = g.shards.size();
     struct St {
-        DevBuf<int32_t> dvec, stamp, queue[2];
-        DevBuf<int64_t> qoff[2], send_off, woff, rwoff, rseg, rlen;
-        DevBuf<unsigned long long> ctr, hb, sw;
-        int64_t nq = 0, mf = 0, hb_words = 0, sw_words = 0, rw_words = 0, sw_max = 0, rw_max = 0;
+        DevBuf<int32_t> queue[2];
+        DevBuf<int64_t> qoff[2], send_off, woff, rseg, rlen;
+        DevBuf<unsigned long long> ctr, gctr, hb, mk, sw, rm;
+        DevBuf<uint8_t> st8;
+        DevBuf<SBfsState> st;
+        int64_t hb_words = 0, sw_max = 0, rw_max = 0, live = 0;
+        bool full_init = false;
     };
     std::vector<St> st(ns);
     int64_t tot[2] = {0, 0};  // entries of all shards, rows of all shards
-    int64_t src_deg = 0, nq0 = 0;
+    std::vector<unsigned long long*> ctrv, gctrv;
+    std::vector<uint64_t*> swv, hbv, mkv, rmv;
     for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh);
@@ -2160,43 +2334,146 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         St& t = st[i];
         const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
         t.hb_words = (h.C + 63) / 64;
-        t.sw_words = woff[(size_t)g.P];
-        // this shard's segments (receive runs): first position, length, packed word offsets
-        std::vector<int64_t> rwoff((size_t)g.P + 1, 0), rseg((size_t)g.P, 0), rlen((size_t)g.P, 0);
+        std::vector<int64_t> rseg((size_t)g.P, 0), rlen((size_t)g.P, 0);
         for (int q = 0; q < g.P; ++q) {
             rlen[(size_t)q] = q == sh.index ? 0 : h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q];
             rseg[(size_t)q] = (int64_t)h.seg_of(q, sh.index) << h.tbits;
-            rwoff[(size_t)q + 1] = rwoff[(size_t)q] + (rlen[(size_t)q] + 63) / 64;
-        }
-        t.rw_words = rwoff[(size_t)g.P];
-        for (int q = 0; q < g.P; ++q) {  // the longest run on each side: the x extent of the (blocks, P) grids
-            t.rw_max = std::max(t.rw_max, rwoff[(size_t)q + 1] - rwoff[(size_t)q]);
+            t.rw_max = std::max(t.rw_max, (rlen[(size_t)q] + 63) / 64);
             t.sw_max = std::max(t.sw_max, woff[(size_t)q + 1] - woff[(size_t)q]);
         }
-        t.rwoff.alloc(g.P + 1);
         t.rseg.alloc(g.P);
         t.rlen.alloc(g.P);
-        copy_h2d(t.rwoff.get(), rwoff.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
-        copy_h2d(t.rseg.get(), rseg.data(), g.P * sizeof(int64_t), sh.stream);
-        copy_h2d(t.rlen.get(), rlen.data(), g.P * sizeof(int64_t), sh.stream);
-        t.dvec.alloc(std::max<int64_t>(sh.rows, 1));
-        t.stamp.alloc(std::max<int64_t>(h.C, 1));
-        t.hb.alloc(std::max<int64_t>(t.hb_words, 1));
-        t.sw.alloc(std::max<int64_t>(t.sw_words, 1));
         t.send_off.alloc(g.P + 1);
         t.woff.alloc(g.P + 1);
+        copy_h2d(t.rseg.get(), rseg.data(), g.P * sizeof(int64_t), sh.stream);
+        copy_h2d(t.rlen.get(), rlen.data(), g.P * sizeof(int64_t), sh.stream);
         copy_h2d(t.send_off.get(), h.send_off.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
         copy_h2d(t.woff.get(), woff.data(), (g.P + 1) * sizeof(int64_t), sh.stream);
-        t.queue[0].alloc(std::max<int64_t>(sh.rows, 1));
-        t.queue[1].alloc(std::max<int64_t>(sh.rows, 1));
-        t.qoff[0].alloc(std::max<int64_t>(sh.rows, 1));
-        t.qoff[1].alloc(std::max<int64_t>(sh.rows, 1));
-        t.ctr.alloc(2);  // level L appends to ctr[(L + 1) & 1], the start (roots) to ctr[0]
+        const int64_t r1 = std::max<int64_t>(sh.rows, 1);
+        for (int k = 0; k < 2; ++k) {
+            t.queue[k].alloc(r1);
+            t.qoff[k].alloc(r1);
+        }
+        t.hb.alloc(std::max<int64_t>(t.hb_words, 1));
+        t.mk.alloc(std::max<int64_t>(t.hb_words, 1));
+        t.st8.alloc(std::max<int64_t>(t.hb_words * 64, 1));
+        t.sw.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
+        t.rm.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
+        t.ctr.alloc(kSRing);
+        t.gctr.alloc(kSRing);
+        t.st.alloc(kSRing);
         bfs_first_col(sh, sh.both);  // the bottom-up's first columns (before t0)
+        // depths live in bfs_depth; the BOTH empty suffix is never reached, so it keeps -1 between calls
+        if (sh.bfs_depth.size() != (size_t)r1) {
+            sh.bfs_depth.alloc(r1);
+            sh.bfs_depth_tail_clean = false;
+        }
+        t.live = sh.both.empty_from >= 0 ? std::min(sh.rows, sh.both.empty_from) : sh.rows;
+        if (t.live < sh.rows && !sh.bfs_depth_tail_clean) {
+            fill_i32_kernel<<<grid_for(sh.rows - t.live), kBlock, 0, sh.stream>>>(sh.bfs_depth.get() + t.live,
+                                                                                  sh.rows - t.live, -1);
+            JG_LAUNCH_CHECK();
+        }
+        t.full_init = !roots && sh.index == src_shard && src_local >= t.live;
+        tot[0] += sh.both.nnz;
+        tot[1] += sh.rows;
+        ctrv.push_back(t.ctr.peer());  // (collected for the exchange / reduction / peers' kernels)
+        gctrv.push_back(t.gctr.peer());
+        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.peer()));
+        hbv.push_back(reinterpret_cast<uint64_t*>(t.hb.peer()));
+        mkv.push_back(reinterpret_cast<uint64_t*>(t.mk.peer()));
+        rmv.push_back(reinterpret_cast<uint64_t*>(t.rm.peer()));
     }
-    // the traversal's state, inside its timed region: level stamps (0 = none; the occupied slots of the
-    // compact vector), depths, the level-0 queue
+    allreduce_sum_i64(g, tot, 2);
+    // shards on one device: the exchange's (owner, reader) runs for sbfs_copy_kernel
     Shard& sh0 = *g.shards[0];
+    DevBuf<SBfsCopyRun> runs;
+    int nruns = 0;
+    int64_t run_max = 0;
+    if (ctx.logical) {
+        std::vector<SBfsCopyRun> rv;
+        for (size_t oi = 0; oi < ns; ++oi) {
+            const Halo& ho = g.shards[oi]->halo_both;
+            const std::vector<int64_t> woff = halo_word_offsets(ho, g.P);
+            for (size_t ri = 0; ri < ns; ++ri) {
+                if (ri == oi) continue;
+                const Shard& rs = *g.shards[ri];
+                const Halo& hr = rs.halo_both;
+                const int q = g.shards[oi]->index, r = rs.index;
+                const int64_t n = (ho.send_off[(size_t)r + 1] - ho.send_off[(size_t)r] + 63) / 64;
+                if (n == 0) continue;
+                const int64_t seg = ((int64_t)hr.seg_of(q, r) << hr.tbits) >> 6;
+                using U = unsigned long long;
+                rv.push_back({reinterpret_cast<const U*>(swv[oi] + woff[(size_t)r]), reinterpret_cast<U*>(hbv[ri] + seg),
+                              reinterpret_cast<const U*>(mkv[ri] + seg), reinterpret_cast<U*>(rmv[oi] + woff[(size_t)r]), n});
+                run_max = std::max(run_max, n);
+            }
+        }
+        nruns = (int)rv.size();
+        DeviceGuard dg(sh0.device);
+        runs.alloc(std::max<size_t>(rv.size(), 1));
+        if (nruns) copy_h2d(runs.get(), rv.data(), rv.size() * sizeof(SBfsCopyRun), sh0.stream);
+    }
+    // the direction thresholds of dobfs_single: a single source switches to bottom-up at dobfs_alpha, the
+    // multi-root start (CC) at bfs_alpha
+    const double alpha = (double)(roots ? tune().bfs_alpha : tune().dobfs_alpha), beta = (double)tune().bfs_beta;
+    auto level_args = [&](size_t i, int level) {
+        Shard& sh = *g.shards[i];
+        St& t = st[i];
+        SBfsLevel a{};
+        a.rp = sh.both.row_ptr.get();
+        a.col = sh.both.col.get();
+        a.first_col = sh.both.first_col.get();
+        a.rows = sh.rows;
+        a.bu_rows = t.live;
+        a.dvec = sh.bfs_depth.get();
+        a.hb = t.hb.get();
+        a.mk = t.mk.get();
+        a.st8 = t.st8.get();
+        a.sw = t.sw.get();
+        a.rm = t.rm.get();
+        a.queue_in = t.queue[level & 1].get();
+        a.qoff_in = t.qoff[level & 1].get();
+        a.queue_out = t.queue[(level & 1) ^ 1].get();
+        a.qoff_out = t.qoff[(level & 1) ^ 1].get();
+        a.send_off = t.send_off.get();
+        a.woff = t.woff.get();
+        a.rseg = t.rseg.get();
+        a.rlen = t.rlen.get();
+        a.P = g.P;
+        a.send_src = sh.halo_both.send_src.get();
+        a.ctr = t.ctr.get();
+        // the global counter: the sum of every shard's ring on one device, else this shard's reduced ring
+        if (ctx.logical) {
+            a.nsum = (int)ns;
+            for (size_t k = 0; k < ns; ++k) a.gsum[k] = ctrv[k];
+        } else {
+            a.nsum = 1;
+            a.gsum[0] = gctrv[i];
+        }
+        a.st = t.st.get();
+        a.level = level;
+        a.max_depth = max_depth;
+        a.alpha = alpha;
+        a.beta = beta;
+        a.nrows = tot[1];
+        return a;
+    };
+    // (blocks, P) grids.  The appending launches (top-down push, bottom-up probes, mark claims) keep to
+    // about kSbfsAppendBlocks workgroups, grid-stride, sized from the shard alone (the frontier is on the
+    // device); the per-peer word passes cover the longest run with kSbfsWords words per wave and trip.
+    constexpr int64_t kSbfsAppendBlocks = 2048;
+    std::vector<dim3> gpre(ns), gmid(ns), gpost(ns);
+    for (size_t i = 0; i < ns; ++i) {
+        const St& t = st[i];
+        const int64_t per_wave_trip = (kBlock / kWave) * kSbfsWords;
+        const int64_t fx = std::max<int64_t>(kSbfsAppendBlocks / g.P, 1);
+        const int64_t pack_x = std::min<int64_t>((t.sw_max + per_wave_trip - 1) / per_wave_trip, 256);
+        const int64_t mid_x = std::min<int64_t>((t.rw_max + per_wave_trip - 1) / per_wave_trip, 256);
+        gpre[i] = dim3((unsigned)std::max<int64_t>({pack_x, fx, 1}), (unsigned)g.P);
+        gmid[i] = dim3((unsigned)std::max<int64_t>(mid_x, 1), (unsigned)g.P);
+        gpost[i] = dim3((unsigned)fx, (unsigned)g.P);
+    }
     hipEvent_t t0, t1;
     {
         DeviceGuard dg(sh0.device);
@@ -2213,183 +2490,99 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh);
         St& t = st[i];
-        zero_gathered(g, sh, JG_ADJ_BOTH, t.stamp.get(), sizeof(int32_t));
-        JG_HIP(hipMemsetAsync(t.ctr.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
+        const SBfsLevel a = level_args(i, 0);
         if (roots) {
-            if (sh.rows) {
-                sbfs_init_roots_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                    t.dvec.get(), sh.rows, roots[i], sh.both.row_ptr.get(), t.queue[0].get(), t.qoff[0].get(),
-                    t.ctr.get());
-                JG_LAUNCH_CHECK();
-            }
-            unsigned long long c = 0;
-            copy_d2h(&c, t.ctr.get(), sizeof c, sh.stream);
-            t.nq = (int64_t)(c >> kPackShift);
-            t.mf = (int64_t)(c & kEdgeMask);
-            nq0 += t.nq;
-            src_deg += t.mf;
-            tot[0] += sh.both.nnz;
-            tot[1] += sh.rows;
-            continue;
+            JG_HIP(hipMemsetAsync(t.ctr.get(), 0, kSRing * sizeof(unsigned long long), sh.stream));
+            sbfs_init_roots_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(a, roots[i], (long long)tot[0]);
+        } else {
+            const int64_t init_rows = t.full_init ? sh.rows : t.live;
+            sbfs_init_kernel<<<grid_for(std::max(init_rows, t.hb_words * 16)), kBlock, 0, sh.stream>>>(
+                a, init_rows, sh.index == src_shard ? src_local : -1, (long long)tot[0]);
         }
-        const int64_t src = sh.index == src_shard ? src_local : -1;
-        sbfs_init_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(t.dvec.get(), sh.rows, src, t.queue[0].get(),
-                                                                      t.qoff[0].get());
         JG_LAUNCH_CHECK();
-        t.nq = src >= 0 ? 1 : 0;
-        nq0 += t.nq;
-        if (src >= 0) {
-            int64_t b[2];
-            copy_d2h(b, sh.both.row_ptr.get() + src, 2 * sizeof(int64_t), sh.stream);
-            src_deg = b[1] - b[0];
-            t.mf = src_deg;
-        }
-        tot[0] += sh.both.nnz;
-        tot[1] += sh.rows;
     }
-    int64_t init[4] = {tot[0], tot[1], src_deg, nq0};
-    allreduce_sum_i64(g, init, 4);
-    int64_t mu = init[0] - init[2], nf = init[3], mf = init[2], edges = init[2];
-    const int64_t nrows = init[1];
-    const double alpha = (double)tune().bfs_alpha, beta = (double)tune().bfs_beta;
-    bool bu = false;
-    int level = 0, cur = 0;
-    std::vector<uint64_t*> swv, hbv;
-    for (auto& t : st) {
-        swv.push_back(reinterpret_cast<uint64_t*>(t.sw.peer()));  // (the exchange uses them under each shard)
-        hbv.push_back(reinterpret_cast<uint64_t*>(t.hb.peer()));
-    }
-    auto level_args = [&](size_t i) {
-        Shard& sh = *g.shards[i];
-        St& t = st[i];
-        SBfsLevel a{};
-        a.rp = sh.both.row_ptr.get();
-        a.col = sh.both.col.get();
-        a.first_col = sh.both.first_col.get();
-        a.rows = sh.rows;
-        a.dvec = t.dvec.get();
-        a.stamp = t.stamp.get();
-        a.hb = t.hb.get();
-        a.queue_in = t.queue[cur].get();
-        a.qoff_in = t.qoff[cur].get();
-        a.nq = t.nq;
-        a.mf = t.mf;
-        a.queue_out = t.queue[cur ^ 1].get();
-        a.qoff_out = t.qoff[cur ^ 1].get();
-        a.sw = t.sw.get();
-        a.send_off = t.send_off.get();
-        a.woff = t.woff.get();
-        a.rwoff = t.rwoff.get();
-        a.rseg = t.rseg.get();
-        a.rlen = t.rlen.get();
-        a.P = g.P;
-        a.send_src = sh.halo_both.send_src.get();
-        a.packed = t.ctr.get() + ((level + 1) & 1);
-        a.packed_next = t.ctr.get() + (level & 1);  // read by the host after the previous level
-        a.level = level;
-        return a;
-    };
-    // (blocks, P) grids over the longest run: kSbfsWords words per wave and trip (the apply: chunks of
-    // kSbfsApplyChunk), at most 2048 blocks in all (the apply, whose blocks each end with one counter
-    // atomic, 1024)
-    auto run_grid = [&](int64_t max_words, int64_t words_per_wave, int64_t cap) {
-        const int64_t per_block = (int64_t)(kBlock / kWave) * words_per_wave;
-        const int64_t x = std::min<int64_t>(std::max<int64_t>((max_words + per_block - 1) / per_block, 1),
-                                            std::max<int64_t>(cap / g.P, 1));
-        return dim3((unsigned)x, (unsigned)g.P);
-    };
-    while (nf > 0 && (max_depth < 0 || level < max_depth)) {
-        if (!bu && (double)mf > (double)mu / alpha) bu = true;
-        else if (bu && (double)nf < (double)nrows / beta) bu = false;
-        for (size_t i = 0; i < ns; ++i) {
-            Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh);
-            St& t = st[i];
-            if (bu && t.sw_words > 0) {  // this level's frontier bits of the send lists (before the forward exchange)
-                sbfs_pack_bits_kernel<<<run_grid(t.sw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
-                JG_LAUNCH_CHECK();
-            }
-        }
-        if (bu) exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, false);
-        for (size_t i = 0; i < ns; ++i) {
-            Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh);
-            St& t = st[i];
-            const SBfsLevel a = level_args(i);
-            const unsigned grid = (unsigned)std::min<int64_t>(
-                std::max<int64_t>((((sh.rows + 63) / 64) * kWave + kBlock - 1) / kBlock, 64), tune().bfs_grid);
-            if (bu) {
-                sbfs_bu_kernel<<<grid, kBlock, 0, sh.stream>>>(a);
-            } else if (t.mf > 0 || (t.rw_words == 0 && t.sw_words == 0)) {  // (the last: zeroes the next counter)
-                sbfs_td_push_kernel<<<(unsigned)std::min<int64_t>(std::max<int64_t>(
-                                          (t.mf / kTdEdgesPerThread + kBlock - 1) / kBlock, 1), tune().bfs_grid),
-                                      kBlock, 0, sh.stream>>>(a);
-            }
-            JG_LAUNCH_CHECK();
-        }
-        if (!bu) {
-            for (size_t i = 0; i < ns; ++i) {  // the stamps of this level into the segment words
-                Shard& sh = *g.shards[i];
-                DeviceGuard dg(sh);
-                if (st[i].rw_words > 0) {
-                    sbfs_pack_marks_kernel<<<run_grid(st[i].rw_max, kSbfsWords, 2048), kBlock, 0, sh.stream>>>(level_args(i));
-                    JG_LAUNCH_CHECK();
-                }
-            }
-            exchange_halo_bits(g, JG_ADJ_BOTH, swv, hbv, true);
+    sbfs_reduce(g, ctrv, gctrv, kSRing - 1);
+    // Levels in batches, the state read back once per batch: the first batch covers the deepest of the
+    // last traversals plus the level that finds the frontier empty (a level enqueued past the end costs an
+    // exchange and an all-reduce on N GPUs), then 4, 8, 16, ...
+    int predicted = 0;
+    for (int k = 0; k < std::min(sh0.bfs_hist_n, 4); ++k) predicted = std::max(predicted, sh0.bfs_hist[k]);
+    int level = 0;
+    SBfsState hs{};
+    for (int batch = predicted > 0 ? predicted + 1 : std::max(1, tune().bfs_batch0), next_batch = 4;;
+         batch = next_batch, next_batch = std::min(next_batch * 2, 64)) {
+        if (max_depth >= 0) batch = std::min(batch, max_depth + 1 - level);
+        if (batch <= 0) fail(JG_ERR_STATE, "sharded BFS level control did not terminate");  // level max_depth stops
+        for (int k = 0; k < batch; ++k, ++level) {
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh);
-                St& t = st[i];
-                if (t.sw_words > 0) {
-                    sbfs_td_apply_kernel<<<run_grid(t.sw_max, kSbfsApplyChunk, 1024), kBlock, 0, sh.stream>>>(level_args(i));
+                sbfs_pre_kernel<<<gpre[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                JG_LAUNCH_CHECK();
+            }
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                sbfs_mid_kernel<<<gmid[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                JG_LAUNCH_CHECK();
+            }
+            if (ctx.logical) {
+                if (nruns) {
+                    ExchTimer et(g);
+                    DeviceGuard dg(sh0.device);
+                    const dim3 grid((unsigned)std::min<int64_t>((run_max + kBlock - 1) / kBlock, 64), (unsigned)nruns);
+                    sbfs_copy_kernel<<<grid, kBlock, 0, sh0.stream>>>(runs.get(), st[0].st.peer(), level % kSRing);
                     JG_LAUNCH_CHECK();
                 }
+            } else {
+                exchange_halo_bits_both(g, JG_ADJ_BOTH, swv, hbv, mkv, rmv);
+            }
+            for (size_t i = 0; i < ns; ++i) {
+                Shard& sh = *g.shards[i];
+                DeviceGuard dg(sh);
+                sbfs_post_kernel<<<gpost[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                JG_LAUNCH_CHECK();
+            }
+            sbfs_reduce(g, ctrv, gctrv, level % kSRing);
+            if (debug_bfs()) {
+                SBfsState ds{};
+                unsigned long long dc = 0;
+                DeviceGuard dg(sh0);
+                copy_d2h(&ds, st[0].st.get() + level % kSRing, sizeof ds, sh0.stream);
+                copy_d2h(&dc, st[0].ctr.get() + level % kSRing, sizeof dc, sh0.stream);
+                std::fprintf(stderr, "[jg sbfs] level %d %s done %d shard-0 next frontier %llu vertices %llu entries\n",
+                             level, ds.bottom_up ? "bottom-up" : "top-down", ds.done, dc >> kPackShift, dc & kEdgeMask);
             }
         }
-        int64_t sums[2] = {0, 0};
-        for (size_t i = 0; i < ns; ++i) {
-            Shard& sh = *g.shards[i];
-            DeviceGuard dg(sh);
-            unsigned long long c = 0;
-            copy_d2h(&c, st[i].ctr.get() + ((level + 1) & 1), sizeof c, sh.stream);
-            st[i].nq = (int64_t)(c >> kPackShift);
-            st[i].mf = (int64_t)(c & kEdgeMask);
-            sums[0] += st[i].nq;
-            sums[1] += st[i].mf;
+        {
+            DeviceGuard dg(sh0);
+            JG_HIP(hipEventRecord(t1, sh0.stream));
+            copy_d2h(&hs, st[0].st.get() + (level - 1) % kSRing, sizeof hs, sh0.stream);
         }
-        allreduce_sum_i64(g, sums, 2);
-        nf = sums[0];
-        mf = sums[1];
-        mu -= mf;
-        edges += mf;
-        cur ^= 1;
-        ++level;
-        if (debug_bfs())
-            std::fprintf(stderr, "[jg sbfs] level %d %s next frontier %lld vertices %lld entries\n", level - 1,
-                         bu ? "bottom-up" : "top-down", (long long)nf, (long long)mf);
+        if (hs.done) break;
     }
     {
         DeviceGuard dg(sh0.device);
-        JG_HIP(hipEventRecord(t1, sh0.stream));
         region_mark(sh0.stream, false);
         JG_HIP(hipEventSynchronize(t1));
         JG_HIP(hipEventElapsedTime(ms_out, t0, t1));
         JG_HIP(hipEventDestroy(t0));
         JG_HIP(hipEventDestroy(t1));
     }
-    // depths of the own rows
-    for (size_t i = 0; i < ns && !roots; ++i) {
+    for (size_t i = 0; i < ns; ++i) {
         Shard& sh = *g.shards[i];
         DeviceGuard dg(sh);
-        if (sh.bfs_depth.size() != (size_t)std::max<int64_t>(sh.rows, 1)) sh.bfs_depth.alloc(std::max<int64_t>(sh.rows, 1));
-        if (sh.rows)
-            JG_HIP(hipMemcpyAsync(sh.bfs_depth.get(), st[i].dvec.get(), sh.rows * sizeof(int32_t),
-                                  hipMemcpyDeviceToDevice, sh.stream));
         JG_HIP(hipStreamSynchronize(sh.stream));
+        // a source in the skipped suffix left its 0 there: the next call refills the suffix
+        sh.bfs_depth_tail_clean = !st[i].full_init || st[i].live == sh.rows;
     }
-    *edges_out = (double)edges;
-    return level;  // levels run, as dobfs_single counts them
+    if (!roots) {  // the level counts of the last traversals (the first batch's size)
+        for (int k = 3; k > 0; --k) sh0.bfs_hist[k] = sh0.bfs_hist[k - 1];
+        sh0.bfs_hist[0] = hs.levels;
+        sh0.bfs_hist_n = std::min(sh0.bfs_hist_n + 1, 4);
+    }
+    *edges_out = (double)hs.edges;
+    return hs.levels;  // levels run, as dobfs_single counts them
 }
 
 }  // namespace
@@ -2469,17 +2662,16 @@ void bfs_kept_release(Graph& g) {
 }
 
 namespace {
-// one source's depths (a single-source traversal's rows) kept as plane 0 of every shard
-template <class F>
-void keep_rows(Graph& g, F rows_of) {
+// one source's depths (a single-source traversal's bfs_depth) kept as plane 0 of every shard: the buffers
+// swap (no copy); the next traversal finds bfs_depth of another size or with a stale suffix and refills
+// it before its timed region
+void keep_depth_rows(Graph& g) {
     for (auto& sp : g.shards) {
         Shard& sh = *sp;
         DeviceGuard dg(sh);
-        sh.kept_depth.alloc(std::max<int64_t>(sh.rows, 1));
-        if (sh.rows)
-            JG_HIP(hipMemcpyAsync(sh.kept_depth.get(), rows_of(sh), sh.rows * sizeof(int32_t), hipMemcpyDeviceToDevice,
-                                  sh.stream));
         JG_HIP(hipStreamSynchronize(sh.stream));
+        sh.kept_depth.swap(sh.bfs_depth);
+        sh.bfs_depth_tail_clean = false;
     }
     g.kept_nsrc = 1;
 }
@@ -2519,7 +2711,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         ctx.last.edges_traversed = l >= 0 ? edges / 2 : 0;
         if (depth_rows && depth_rows[0])
             for (auto& sp : g.shards) rows_to_dense(g, *sp, sp->bfs_depth.peer(), depth_rows[0]);
-        if (keep) keep_rows(g, [](Shard& sh) { return sh.bfs_depth.get(); });
+        if (keep) keep_depth_rows(g);
         prof_collect(ctx, g);
     } else if (single) {
         Shard& sh = sh0;
@@ -2569,7 +2761,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
         const Csr* degcsr = c.push ? c.push : c.pull;
         ctx.last.algorithmic_bytes = 4.0 * (double)degcsr->nnz + 12.0 * (double)sh.rows;
         if (depth_rows && depth_rows[0]) rows_to_dense(g, sh, depth.get(), depth_rows[0]);
-        if (keep) keep_rows(g, [](Shard& s) { return s.bfs_depth.get(); });
+        if (keep) keep_depth_rows(g);
         prof_collect(ctx, g);
     } else if (nsrc <= kNarrowMax && g.P == 1 && g.shards.size() == 1 && tune().bfs_narrow &&
                pick_csrs(sh0, direction).push && pick_csrs(sh0, direction).pull) {
@@ -2771,9 +2963,10 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                     Shard& sh = *g.shards[i];
                     DeviceGuard dg(sh);
                     const BfsCsrs c = pick_csrs(sh, direction);
+                    const int64_t ne = pull_live_rows(sh, c);
                     JG_HIP(hipMemsetAsync(tds[i].ctr.get(), 0, sizeof(unsigned long long), sh.stream));
-                    msbfs_frontier_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                        st[i].F[cur].get(), sh.rows, c.push->row_ptr.get(), tds[i].queue[qslot].get(),
+                    msbfs_frontier_kernel<<<grid_for(ne), kBlock, 0, sh.stream>>>(
+                        st[i].F[cur].get(), ne, c.push->row_ptr.get(), tds[i].queue[qslot].get(),
                         tds[i].qoff[qslot].get(), tds[i].ctr.get());
                     JG_LAUNCH_CHECK();
                 }
@@ -3325,14 +3518,17 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             // the next level pushes top-down: its queue is built here, in the same pass
                             const bool qnext = td_one && !t.todo.empty() && t.xlive_permille < (double)tune().msbfs_scan_queue;
                             t.xlive_permille = 1000.0;
+                            // rows without pull entries gained nothing (a pull level does not finalise them):
+                            // the scans stop at the empty suffix (RMAT-26 BOTH: 34 M of 67 M rows)
+                            const int64_t ne = pull_live_rows(sh, c);
                             if (qnext) {
-                                msbfs_frontier_live_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                                    t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), tds[i].queue[qc ^ 1].get(),
+                                msbfs_frontier_live_kernel<<<grid_for(ne), kBlock, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), ne, c.push->row_ptr.get(), tds[i].queue[qc ^ 1].get(),
                                     tds[i].qoff[qc ^ 1].get(), tds[i].ctr.get(), lw);
                                 queued_next = true;
                             } else {
-                                msbfs_scan_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(
-                                    t.F[cur ^ 1].get(), sh.rows, c.push->row_ptr.get(), lw, tds[i].ctr.get());
+                                msbfs_scan_kernel<<<red_grid(ne), kRedThreads, 0, sh.stream>>>(
+                                    t.F[cur ^ 1].get(), ne, c.push->row_ptr.get(), lw, tds[i].ctr.get());
                             }
                             JG_LAUNCH_CHECK();
                         }

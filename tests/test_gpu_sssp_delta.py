@@ -172,3 +172,25 @@ def test_delta_stepping_rmat16(ctx, oracle_lib):
     np.testing.assert_array_equal(got, want)
     assert (got > 0).sum() > n // 4
     g.close()
+
+
+@pytest.mark.parametrize("delta", [-1, 32])
+def test_delta_stepping_rmat20_matches_oracle(ctx, oracle_lib, delta):
+    """delta-stepping at RMAT-20 (the smallest size README and tools/sd_bench.py time),
+    weights 1..255 (Graph500 SSSP style), unbounded hops, seeded at the row of largest in-degree, against
+    the oracle's superstep restatement bit for bit (until now only the GPU superstep path was compared
+    at this size: a self-comparison)."""
+    import janusgraph_amd as jg
+    n = 1 << 20
+    s, t = oracle_lib.rmat_edges(20, 16, 0x55D + 20)
+    s, t = s.astype(np.int32), t.astype(np.int32)
+    w = np.random.default_rng(20).integers(1, 256, len(s)).astype(np.int32)
+    vid = (np.arange(n, dtype=np.int64) + 1) << 8
+    seed = int(np.bincount(t, minlength=n).argmax())
+    g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN)
+    want = oracle_lib.shortest_distance(n, s, t, seed, DEPTH_INF, w)
+    got = run_sd(g, vid[seed], DEPTH_INF, delta)
+    np.testing.assert_array_equal(got, want)
+    assert (want >= 0).sum() > n // 4  # most of the graph reached
+    assert ctx.stats()["levels"] > 1
+    g.close()

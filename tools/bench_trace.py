@@ -120,7 +120,7 @@ def main():
         d["kernel"].append(kern / runs / 1e6)
         d["span"].append(span / runs / 1e6)
         d["dispatches"].append(nd / runs)
-    out = {"bench_head": line.get("head"), "trace_files": [os.path.relpath(x) for x in files], "blocks": {}}
+    out = {"bench_head": line.get("head"), "bench_code": line.get("code"), "trace_files": [os.path.relpath(x) for x in files], "blocks": {}}
     for name, d in per.items():
         kern, span = float(np.median(d["kernel"])), float(np.median(d["span"]))
         blk = {"windows": len(d["kernel"]), "runs_per_window": d["runs"], "marked": d["marked"],

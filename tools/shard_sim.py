@@ -56,7 +56,7 @@ def run_pr(jg, scale, shards, halo, steps, warmup):
             "gteps_single_gpu_equiv": round(m / (dt / steps) / 1e9, 2)}, rank
 
 
-def run_both(jg, program, scale, shards, reps):
+def run_both(jg, program, scale, shards, reps, groups=1, group=0):
     import bench
     ctx = jg.Context((0,) * shards)
     g = ctx.build_rmat(scale, 16, 0x5EED + scale, flags=jg.ADJ_BOTH)
@@ -80,8 +80,12 @@ def run_both(jg, program, scale, shards, reps):
             if len(rows) >= 3 * reps:
                 break
     else:
+        # msbfs --groups G: the bench's 64 sources split into G groups of 64 / G (a 2D plan: G source
+        # groups x P vertex shards); this run is group `group`
+        srcs = np.array_split(bench.pick_sources(deg, 64, 7), groups)[group]
+        out.update({"sources": int(len(srcs)), "groups": groups, "group": group})
         call = g.connected_components if program == "cc" else (
-            lambda: g.bfs(bench.pick_sources(deg, 64, 7), jg.DIR_BOTH, want=False))
+            lambda: g.bfs(srcs, jg.DIR_BOTH, want=False))
         call()
         for _ in range(reps):
             ctx.set_profiling(True)
@@ -109,6 +113,9 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--halo", type=int, nargs="+", default=[1, 0], help="halo settings tried for P > 1 (pr)")
     p.add_argument("--tune", nargs="*", default=[], help="jg_tune_set knobs key=value applied first")
+    p.add_argument("--groups", type=int, default=1, help="msbfs: split the 64 sources into this many groups "
+                                                          "and run each (a groups x shards 2D plan)")
+    p.add_argument("--only-group", type=int, default=-1, help="msbfs --groups: run this group alone (traces)")
     a = p.parse_args()
     import janusgraph_amd as jg
     for kv in a.tune:
@@ -116,7 +123,10 @@ def main():
         jg._lib.tune_set(k, int(v))
     if a.program != "pr":
         for P in a.shards:
-            print(json.dumps(run_both(jg, a.program, a.scale, P, a.reps)), flush=True)
+            for grp in range(a.groups if a.program == "msbfs" else 1):
+                if a.only_group >= 0 and grp != a.only_group:
+                    continue
+                print(json.dumps(run_both(jg, a.program, a.scale, P, a.reps, a.groups, grp)), flush=True)
         return
     ref = None
     for P in a.shards:

@@ -4,6 +4,7 @@
 # the build container) takes the difference, so build kernels and warm-up calls cancel out.
 #   bash tools/shard_traces.sh <out dir> <scale> <shards> [programs...]   (default: pr bfs cc msbfs)
 # -> <out dir>/<program>_{a,b}/ (traces) and <program>_{a,b}.json (shard_sim's line: its "runs")
+# SIM_ARGS (environment): extra shard_sim.py arguments, e.g. "--groups 2 --only-group 1" (a 2D plan's group)
 set -o pipefail
 OUT=${1:?out dir}
 SCALE=${2:-26}
@@ -23,7 +24,7 @@ for prog in $PROGS; do
         fi
         echo "[shard_traces] $prog $v: $args"
         timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${prog}_$v" -o t -- \
-            python3 tools/shard_sim.py --scale "$SCALE" --shards "$P" $args > "$OUT/${prog}_$v.json" 2> "$OUT/${prog}_$v.err" || exit 3
+            python3 tools/shard_sim.py --scale "$SCALE" --shards "$P" $args $SIM_ARGS > "$OUT/${prog}_$v.json" 2> "$OUT/${prog}_$v.err" || exit 3
         tail -n 1 "$OUT/${prog}_$v.json"
     done
 done
