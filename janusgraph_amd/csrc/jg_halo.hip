@@ -495,32 +495,71 @@ void exchange_halo_bits_both(Graph& g, uint32_t adj, std::vector<uint64_t*>& fse
                              std::vector<uint64_t*>& rbitmap, std::vector<uint64_t*>& rsend) {
     if (g.P == 1) return;
     Ctx& c = *g.ctx;
-    if (c.logical || c.host_transport) {  // (the sharded DO-BFS copies one direction by kernel on one device)
+    if (c.logical) {  // (the sharded DO-BFS copies the level's one direction by kernel on one device)
         exchange_halo_bits(g, adj, fsend, fbitmap, false);
         exchange_halo_bits(g, adj, rsend, rbitmap, true);
         return;
     }
     ExchTimer et(g);
-    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    // The transfers of every local shard, in the order RCCL matches them: two each way per peer pair,
+    // both sides sending [forward, reverse] and receiving [forward, reverse].  My forward send (my send
+    // list for q: `mine` words) is q's forward receive (its segment for me); my reverse send (my marks
+    // about q's vertices: `theirs` words) is q's reverse receive (its send-list words from me).  The
+    // host-transport mode hands the same ordered lists to the transport, whose point-to-point messages
+    // also match in issue order per peer pair (gloo), so the rank-mode tests check this plan.
+    struct Op {
+        int peer;
+        uint64_t* p;
+        int64_t words;
+    };
+    std::vector<std::vector<Op>> sends(g.shards.size()), recvs(g.shards.size());
     for (size_t i = 0; i < g.shards.size(); ++i) {
-        Shard& sh = *g.shards[i];
+        const Shard& sh = *g.shards[i];
         const Halo& h = g.halo(sh, adj);
-        DeviceGuard dg(sh);
         const std::vector<int64_t> woff = halo_word_offsets(h, g.P);
         for (int q = 0; q < g.P; ++q) {
             if (q == sh.index) continue;
             const int64_t mine = (h.send_off[(size_t)q + 1] - h.send_off[(size_t)q] + 63) / 64;    // my vertices q reads
             const int64_t theirs = (h.recv_off[(size_t)q + 1] - h.recv_off[(size_t)q] + 63) / 64;  // q's vertices I read
             const int64_t seg = (((int64_t)h.seg_of(q, sh.index) << h.tbits) >> 6);
-            if (mine > 0) {
-                rccl_check(ncclSend(fsend[i] + woff[(size_t)q], (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
-                rccl_check(ncclRecv(rsend[i] + woff[(size_t)q], (size_t)mine, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
-            }
-            if (theirs > 0) {
-                rccl_check(ncclRecv(fbitmap[i] + seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclRecv");
-                rccl_check(ncclSend(rbitmap[i] + seg, (size_t)theirs, ncclUint64, q, sh.comm, sh.stream), "ncclSend");
-            }
+            if (mine > 0) sends[i].push_back({q, fsend[i] + woff[(size_t)q], mine});
+            if (theirs > 0) sends[i].push_back({q, rbitmap[i] + seg, theirs});
+            if (theirs > 0) recvs[i].push_back({q, fbitmap[i] + seg, theirs});
+            if (mine > 0) recvs[i].push_back({q, rsend[i] + woff[(size_t)q], mine});
         }
+    }
+    constexpr size_t W = sizeof(uint64_t);
+    if (c.host_transport) {  // rank mode over host callbacks (one shard per process)
+        Shard& sh = *g.shards[0];
+        DeviceGuard dg(sh);
+        std::vector<int> sp, rp;
+        std::vector<std::vector<uint64_t>> out, in;
+        std::vector<const void*> sv;
+        std::vector<void*> rv;
+        std::vector<size_t> sb, rb;
+        for (const Op& o : sends[0]) {
+            sp.push_back(o.peer);
+            out.emplace_back((size_t)o.words);
+            copy_d2h(out.back().data(), o.p, (size_t)o.words * W, sh.stream);
+            sb.push_back((size_t)o.words * W);
+        }
+        for (const Op& o : recvs[0]) {
+            rp.push_back(o.peer);
+            in.emplace_back((size_t)o.words);
+            rb.push_back((size_t)o.words * W);
+        }
+        for (auto& v : out) sv.push_back(v.data());
+        for (auto& v : in) rv.push_back(v.data());
+        host_exchange(c, sp, sv, sb, rp, rv, rb);
+        for (size_t k = 0; k < recvs[0].size(); ++k) copy_h2d(recvs[0][k].p, rv[k], rb[k], sh.stream);
+        return;
+    }
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t i = 0; i < g.shards.size(); ++i) {
+        Shard& sh = *g.shards[i];
+        DeviceGuard dg(sh);
+        for (const Op& o : sends[i]) rccl_check(ncclSend(o.p, (size_t)o.words, ncclUint64, o.peer, sh.comm, sh.stream), "ncclSend");
+        for (const Op& o : recvs[i]) rccl_check(ncclRecv(o.p, (size_t)o.words, ncclUint64, o.peer, sh.comm, sh.stream), "ncclRecv");
     }
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }

@@ -87,8 +87,6 @@ struct SliceBand {
     // whether band row i has entries in sub-slice h; its number is w.y + the set bits of w.x below it
     DevBuf<uint2> sub_word;     // [S][words], words = ceil(rows of the band / 32)
     DevBuf<int32_t> task_rows;  // [tasks][2]: band rows of the task's first and last entry
-    mutable DevBuf<int32_t> ab_srow;        // Tune::ab_fold experiment: band row of each sub-row
-    mutable DevBuf<unsigned char> ab_acc;   // Tune::ab_fold experiment: [8][rows] accumulators
     int64_t rows() const { return row_end - row_begin; }
 };
 
@@ -252,6 +250,8 @@ struct Shard {
     DevBuf<unsigned char> bfs_state;         // [kBfsRing * sizeof(BfsState)] per-level decisions
     DevBuf<int32_t> bfs_depth;               // [rows] depth of the last traversal
     bool bfs_depth_tail_clean = false;       // BOTH: bfs_depth's empty suffix holds -1 (the init skips it)
+    DevBuf<uint8_t> sbfs_stamp;              // sharded DO-BFS: remote-target stamps per compact position
+    bool sbfs_stamp_clean = false;           // ... all zero (set when a traversal completes)
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
@@ -655,9 +655,6 @@ struct Tune {
                                       // 0 off, 1 when an XCD's eighth of the vector exceeds 8 MB, 2 always
     int merge_stage[4] = {-1, -1, -1, -1};  // per band: LDS window of a wave's task partials (slots; 0 = direct
                                           // stores, -1 = automatic from the band's heads per task)
-    int ab_fold = 0;                  // A/B EXPERIMENT ONLY (results are not PageRank):
-                                      // band 0's sub-row sums go to one accumulator per (row, XCD), read-
-                                      // modified-written round by round, instead of a partial per sub-row
     int merge_pack = 1;               // build time: band entries packed in 20/24 bits when the vector allows
                                       // (0: 32 bits, 24: at least 24; tests)
 };

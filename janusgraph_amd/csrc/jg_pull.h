@@ -295,11 +295,6 @@ struct MergeArgs {
     // they are.  A program passes it only when every row the task touches would discard what the task
     // folds (the multi-source BFS: rows that can gain no bit; see msbfs_task_live_kernel).
     const uint32_t* __restrict__ live;
-    // Tune::ab_fold experiment (null: off): a sub-row's sum goes to fold[xcd][srow[j]], stored in the
-    // first temporal round and read-modified-written in the later ones
-    void* fold;
-    const int32_t* __restrict__ srow;
-    int64_t fold_rows;
 };
 
 // The hot entries of a gathered vector: the first `hs` entries of each of its `nseg` segments
@@ -547,14 +542,9 @@ __global__ __launch_bounds__(kMergeThreads) void pull_merge_kernel(MergeArgs a, 
         // scattered stores per lane (the stores cost ~20% of the merge kernel, round 2).
         const int H = __builtin_amdgcn_readlane(incl, kWave - 1);
         const bool staged = LDS && H <= a.stage;
-        auto store_partial = [&](int64_t j, T val) {
-            if (a.fold) {
-                T* p = static_cast<T*>(a.fold) + (int64_t)xcd * a.fold_rows + a.srow[j];
-                *p = rd == 0 ? val : op.combine(*p, val);
-            } else {
-                partial[j] = val;
-            }
-        };
+        // (Folding band 0 into one accumulator per (row, XCD), read-modified-written round by round, was
+        // measured 7-9% slower than these partials: profiles/r06/abfold/.)
+        auto store_partial = [&](int64_t j, T val) { partial[j] = val; };
         auto emit = [&](int hh, T val) {  // segment of head hh
             if (staged) {
                 stg[hh] = val;
@@ -678,7 +668,6 @@ struct FinalizeBands {
     int64_t part_off[kMaxBands];
     int bits[kMaxBands];
     int n;
-    const void* fold;  // Tune::ab_fold experiment: band 0's [8][rows] accumulators (null: off)
 };
 template <class Op>
 __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, const FinalizeBands& fb,
@@ -693,17 +682,6 @@ __device__ __forceinline__ void slice_finalize_row(int64_t r, const Op& op, cons
     const uint2* __restrict__ sw = fb.sub_word[b];
     const T* __restrict__ part = partial + fb.part_off[b];
     T acc = op.identity();
-    if (b == 0 && fb.fold) {  // Tune::ab_fold experiment: the 8 per-XCD accumulators
-        const T* __restrict__ f = static_cast<const T*>(fb.fold);
-        T v[kXcds];
-#pragma unroll
-        for (int x = 0; x < kXcds; ++x) v[x] = f[(int64_t)x * NR + i];
-        acc = v[0];
-#pragma unroll
-        for (int x = 1; x < kXcds; ++x) acc = op.combine(acc, v[x]);
-        op.finalize(r, acc);
-        return;
-    }
     bool first = true;
     // batches of 8 sub-slices: all index loads, then all partial loads, then the fold in h order, and
     // the next batch's index words are loaded with this batch's partials, so a hub row's 128 sub-slices
@@ -764,22 +742,6 @@ __global__ __launch_bounds__(kBlock) void pull_light_finalize_kernel(PullArgs a,
     pull_block<Op, U>(a, op, hub_partial, b - fin_blocks + a.block_offset);
 }
 
-// Tune::ab_fold experiment: srow[j] = band row of sub-row j (from the sub_word index)
-static __global__ void ab_srow_kernel(const uint2* __restrict__ sw, int64_t W, int S, int32_t* __restrict__ srow) {
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < (int64_t)S * W; x += (int64_t)gridDim.x * blockDim.x) {
-        const uint2 w = sw[x];
-        const int64_t wi = x % W;
-        uint32_t m = w.x;
-        int k = 0;
-        while (m) {
-            const int b = __ffs(m) - 1;
-            srow[w.y + k] = (int32_t)(wi * 32 + b);
-            ++k;
-            m &= m - 1;
-        }
-    }
-}
-
 // Enqueue one pull superstep on `s`.
 // `split_partial` ([8 * plan.split_rows], nullable) enables the XCD split of the heavy rows.
 
@@ -835,23 +797,7 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             }
             MergeArgs ma{bd.pack_a.get(), bd.pack_b.get(), bd.heads.get(), bd.meta.get(), bd.sub_begin.get(),
                          bd.sub_end.get(), bd.sub_base.get(), bd.tasks, bd.bits, stage,
-                         task_live ? task_live[bi] : nullptr, nullptr, nullptr, 0};
-            if (bi == 0 && tune().ab_fold) {  // A/B experiment only: band 0 folds per (row, XCD)
-                if (bd.ab_srow.size() != (size_t)std::max<int64_t>(bd.subrows, 1)) {
-                    bd.ab_srow.alloc(std::max<int64_t>(bd.subrows, 1));
-                    const int64_t W = (bd.rows() + 31) / 32;
-                    ab_srow_kernel<<<grid_for((1ll << bd.bits) * W), kBlock, 0, s>>>(bd.sub_word.get(), W, 1 << bd.bits,
-                                                                                     bd.ab_srow.get());
-                    JG_LAUNCH_CHECK();
-                }
-                if (bd.ab_acc.size() != (size_t)(kXcds * bd.rows() * (int64_t)sizeof(T))) {
-                    bd.ab_acc.alloc(kXcds * bd.rows() * (int64_t)sizeof(T));
-                    JG_HIP(hipMemsetAsync(bd.ab_acc.get(), 0, bd.ab_acc.bytes(), s));
-                }
-                ma.fold = bd.ab_acc.get();
-                ma.srow = bd.ab_srow.get();
-                ma.fold_rows = bd.rows();
-            }
+                         task_live ? task_live[bi] : nullptr};
             T* part = split_partial + bd.part_off;
             T* carry = split_partial + bd.carry_off;
             // LDS image: kMergeLdsBytes / sizeof(T) - 16 elements (1 identity line) per sub-slice
@@ -911,7 +857,6 @@ void launch_pull(const Csr& csr, const PullPlan& plan, const Op& op, typename Op
             fb.bits[fb.n] = bp->bits;
             ++fb.n;
         }
-        if (tune().ab_fold && !plan.bands.empty() && plan.bands[0]->ab_acc.size()) fb.fold = plan.bands[0]->ab_acc.get();
     }
     const bool fuse = split && !pull_split_launches();
     if (fuse) {

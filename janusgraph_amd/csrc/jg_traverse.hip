@@ -1923,6 +1923,7 @@ struct SBfsLevel {
     const unsigned long long* gsum[kMaxShardsBfs];  // counter rings whose sum is the global counter (by
     int nsum;                                       // value: the decision's loads issue together)
     SBfsState* st;                  // [kSRing] this shard's copy of the (identical) level decisions
+    int64_t apply_x;                // workgroups per peer of the mark claims (the post kernel's x extent may be larger)
     int32_t level, max_depth;
     double alpha, beta;
     int64_t nrows;                  // rows of all shards (the beta rule)
@@ -1935,17 +1936,20 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 
 // Level L's decision from level L-1's state and global counter (Beamer: bottom-up when the frontier's
 // entries outweigh the unexplored ones / alpha, back top-down when the frontier falls below rows / beta);
-// *nq / *mf = this shard's own input frontier.  Every shard and rank computes the same state.
+// *nq / *mf = this shard's own input frontier.  Every shard and rank computes the same state.  Called by
+// every lane of wave 0 (lane k < nsum loads counter ring k: one round trip for all the loads); the result
+// is valid in lane 0.
 __device__ SBfsState sbfs_decide(const SBfsLevel& a, long long* nq, long long* mf) {
     const int pl = (a.level + kSRing - 1) % kSRing;
+    const int l = lane_id();
     const SBfsState p = a.st[pl];
     const unsigned long long own = a.ctr[pl];
+    unsigned long long h = l < a.nsum ? a.gsum[l][pl] : 0ull;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) h += shfl_u64(h, l ^ o);
     *nq = (long long)(own >> kPackShift);
     *mf = (long long)(own & kEdgeMask);
     if (p.done) return p;
-    unsigned long long h = 0;
-    for (int k = 0; k < kMaxShardsBfs; ++k)
-        if (k < a.nsum) h += a.gsum[k][pl];
     const long long gnf = (long long)(h >> kPackShift), gmf = (long long)(h & kEdgeMask);
     SBfsState c = p;
     c.mu = p.mu - gmf;
@@ -1963,30 +1967,30 @@ __device__ SBfsState sbfs_decide(const SBfsLevel& a, long long* nq, long long* m
 // The per-word passes run on a (blocks, P) grid: blockIdx.y is the peer whose run a block works on, so
 // no word searches the per-peer offset tables (a scan of LDS-staged tables per word held them to 45-80 us
 // per launch at RMAT-26, P = 8, round 4).  The row-parallel passes use the same grid flattened.
-constexpr int kSbfsWords = 4;
 
 // bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = the depth of the
-// word's row b is this level's.  A wave takes kSbfsWords words per trip, every load issued on a clamped
+// word's row b is this level's.  A wave takes PW words per trip, every load issued on a clamped
 // index before any is used.
+template <int PW>
 __device__ __forceinline__ void sbfs_pack_bits(const SBfsLevel& a) {
     const int q = blockIdx.y;
     const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
     const int32_t* __restrict__ src = a.send_src + so;
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
-        int32_t r[kSbfsWords];
-        bool in[kSbfsWords];
+    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * PW) {
+        int32_t r[PW];
+        bool in[PW];
 #pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
+        for (int k = 0; k < PW; ++k) {
             const int64_t x = (w0 + k * nwaves) * 64 + lane_id();
             in[k] = x < cnt;
             r[k] = src[in[k] ? x : cnt - 1];  // words exist only for a nonempty run
         }
-        int32_t d[kSbfsWords];
+        int32_t d[PW];
 #pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) d[k] = a.dvec[r[k]];
+        for (int k = 0; k < PW; ++k) d[k] = a.dvec[r[k]];
 #pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
+        for (int k = 0; k < PW; ++k) {
             const uint64_t word = __ballot(in[k] && d[k] == a.level);
             if (lane_id() == 0 && w0 + k * nwaves < nw) a.sw[wo + w0 + k * nwaves] = word;
         }
@@ -2081,23 +2085,35 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
     }
 }
 
-// top-down, owner side: the received words of peer q's run, 64 per wave and trip (lane l loads word l);
-// the rows of the set bits are claimed kSbfsWords non-zero words at a time (lane b: the row of bit b).
+// top-down, owner side: the received words of peer q's run, kSbfsApplyChunk per wave and trip (lanes
+// 0 .. 15 load); the rows of the set bits are claimed AW non-zero words at a time (lane b: the
+// row of bit b).  Blocks from apply_x on leave: the claims end with one counter atomic per block.
+// (64 words per wave and trip on 2048 workgroups measured 43 / 124 us per shard at RMAT-26's levels 1 and
+// 2 against 21 / 100 us for this shape, round 6.)
+constexpr int kSbfsApplyChunk = 16;
+// Round-6 A/B at RMAT-26, P = 8 (tools/shard_sim.py, event time per shard; profiles/r06/sbfs/variants.log):
+// 4 -> 8 words per trip in the send-list pack 0.606 -> 0.583 ms, in the claims 0.601; 1024 -> 2048 /
+// 4096 claim workgroups 0.578 / 0.573.
+constexpr int kSbfsPackWords = 8, kSbfsApplyWords = 8;
+constexpr int64_t kSbfsApplyBlocks = 4096;
+template <int AW>
 __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) {
     const int q = blockIdx.y;
     const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
     const int32_t* __restrict__ src = a.send_src + so;
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+    const int64_t nwaves = (int64_t)a.apply_x * (kBlock / kWave);
     const int32_t nd = a.level + 1;
     unsigned long long* packed = a.ctr + a.level % kSRing;
-    for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / kWave) + wave_id()) * kWave; c0 < nw; c0 += nwaves * kWave) {
-        const unsigned long long mine = c0 + lane_id() < nw ? a.rm[wo + c0 + lane_id()] : 0ull;
+    for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / kWave) + wave_id()) * kSbfsApplyChunk; c0 < nw;
+         c0 += nwaves * kSbfsApplyChunk) {
+        const unsigned long long mine =
+            lane_id() < kSbfsApplyChunk && c0 + lane_id() < nw ? a.rm[wo + c0 + lane_id()] : 0ull;
         uint64_t nz = __ballot(mine != 0ull);
         while (nz) {  // wave-uniform
-            unsigned long long word[kSbfsWords];
-            int32_t u[kSbfsWords];
+            unsigned long long word[AW];
+            int32_t u[AW];
 #pragma unroll
-            for (int k = 0; k < kSbfsWords; ++k) {
+            for (int k = 0; k < AW; ++k) {
                 const int l = nz ? __ffsll((unsigned long long)nz) - 1 : 0;
                 word[k] = nz ? shfl_u64(mine, l) : 0ull;
                 nz &= nz - 1;
@@ -2105,7 +2121,7 @@ __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) 
                 u[k] = src[x < cnt ? x : cnt - 1];  // bits past the run's end are never set
             }
 #pragma unroll
-            for (int k = 0; k < kSbfsWords; ++k) {
+            for (int k = 0; k < AW; ++k) {
                 if (!word[k]) continue;  // wave-uniform
                 bool take = false;
                 int64_t deg = 0;
@@ -2121,13 +2137,15 @@ __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) 
 
 // First kernel of a level: the decision (block (0, 0) publishes it and zeroes the next level's counter),
 // then this shard's send-list bits (bottom-up) or its top-down push.
+template <int PW>
 __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
     __shared__ SBfsState s_st;
     __shared__ long long s_nq, s_mf;
     __shared__ WaveStage ws;
+    long long nq = 0, mf = 0;
+    SBfsState c{};
+    if (threadIdx.x < kWave) c = sbfs_decide(a, &nq, &mf);  // (wave 0: its lanes' loads issue together)
     if (threadIdx.x == 0) {
-        long long nq, mf;
-        const SBfsState c = sbfs_decide(a, &nq, &mf);
         s_st = c;
         s_nq = nq;
         s_mf = mf;
@@ -2139,7 +2157,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
     __syncthreads();
     if (s_st.done) return;
     if (s_st.bottom_up) {
-        sbfs_pack_bits(a);
+        sbfs_pack_bits<PW>(a);
     } else {
         WaveApp app{ws};
         sbfs_td_push(a, s_nq, s_mf, app);
@@ -2149,7 +2167,9 @@ __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
 
 // Second kernel of a top-down level (a bottom-up level leaves at once): peer q's segment of stamp bytes
 // into its mark words, every word written (zero or not: the words are the exchange's payload) and every
-// set byte cleared for the next top-down level; a wave takes kSbfsWords words per trip.
+// set byte cleared for the next top-down level.  Lane l loads bytes [8l, 8l + 8) of a 512-byte chunk
+// (eight mark words) as one 8-byte load; word k is the byte masks of lanes 8k .. 8k + 7.  (One byte per
+// lane and load ran 13-19 us per level and shard at RMAT-26, P = 8.)
 __global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
     __shared__ int s_run;
     if (threadIdx.x == 0) {
@@ -2159,37 +2179,58 @@ __global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
     __syncthreads();
     if (!s_run) return;
     const int q = blockIdx.y;
-    const int64_t len = a.rlen[q], seg = a.rseg[q], nw = (len + 63) / 64;
-    uint8_t* __restrict__ stamp = a.st8 + seg;
+    const int64_t len = a.rlen[q], seg = a.rseg[q], nw = (len + 63) / 64, nchunks = (nw + 7) / 8;
+    uint8_t* __restrict__ stamp = a.st8 + seg;  // seg: a multiple of 2^tbits, so 8-byte aligned
     unsigned long long* __restrict__ mk = a.mk + (seg >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * kSbfsWords) {
-        uint8_t b[kSbfsWords];
+    const int l = lane_id();
+    for (int64_t c0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); c0 < nchunks; c0 += nwaves * 2) {
+        unsigned long long x[2];
+        bool in[2];
 #pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
-            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
-            b[k] = j < len ? stamp[j] : (uint8_t)0;
+        for (int k = 0; k < 2; ++k) {  // two chunks per trip, both loads issued first
+            const int64_t b0 = (c0 + k * nwaves) * 512 + 8 * l;  // this lane's first byte
+            in[k] = c0 + k * nwaves < nchunks && b0 < len;
+            x[k] = 0ull;
+            if (in[k]) {
+                if (b0 + 8 <= len) {
+                    x[k] = *reinterpret_cast<const unsigned long long*>(stamp + b0);
+                } else {
+                    for (int64_t j = b0; j < len; ++j) x[k] |= (unsigned long long)stamp[j] << (8 * (j - b0));
+                }
+            }
         }
 #pragma unroll
-        for (int k = 0; k < kSbfsWords; ++k) {
-            const int64_t j = (w0 + k * nwaves) * 64 + lane_id();
-            const uint64_t word = __ballot(b[k] != 0);
-            if (b[k]) stamp[j] = 0;
-            if (lane_id() == 0 && w0 + k * nwaves < nw) mk[w0 + k * nwaves] = word;
+        for (int k = 0; k < 2; ++k) {
+            unsigned m = 0;  // bit i: byte i of this lane's eight is set
+#pragma unroll
+            for (int i = 0; i < 8; ++i) m |= ((x[k] >> (8 * i)) & 0xffull) ? (1u << i) : 0u;
+            unsigned long long word = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) word |= (unsigned long long)__shfl((int)m, 8 * (l & 7) + i, kWave) << (8 * i);
+            const int64_t w = (c0 + k * nwaves) * 8 + l;  // lanes 0..7 write words 8c .. 8c + 7
+            if (l < 8 && c0 + k * nwaves < nchunks && w < nw) mk[w] = word;
+            if (m) {  // clear this lane's stamps (the tail of the run byte by byte)
+                const int64_t b0 = (c0 + k * nwaves) * 512 + 8 * l;
+                if (b0 + 8 <= len) *reinterpret_cast<unsigned long long*>(stamp + b0) = 0ull;
+                else for (int64_t j = b0; j < len; ++j) stamp[j] = 0;
+            }
         }
     }
 }
 
 // Last kernel of a level (after the exchange): bottom-up probes, or the claims of the received marks.
+template <int AW>
 __global__ __launch_bounds__(kBlock) void sbfs_post_kernel(SBfsLevel a) {
     __shared__ SBfsState s_st;
     __shared__ WaveStage ws;
     if (threadIdx.x == 0) s_st = a.st[a.level % kSRing];
     __syncthreads();
     if (s_st.done) return;
+    if (!s_st.bottom_up && blockIdx.x >= a.apply_x) return;  // (block-uniform)
     WaveApp app{ws};
     if (s_st.bottom_up) sbfs_bottom_up(a, app);
-    else sbfs_td_apply(a, app);
+    else sbfs_td_apply<AW>(a, app);
     app.final(a.queue_out, a.qoff_out, a.ctr + a.level % kSRing);
 }
 
@@ -2214,24 +2255,11 @@ __global__ __launch_bounds__(kBlock) void sbfs_copy_kernel(const SBfsCopyRun* __
         d[i] = s[i];
 }
 
-// the stamp bytes of every peer segment's run cleared (grid-stride)
-__device__ __forceinline__ void sbfs_zero_stamps(const SBfsLevel& a) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int q = 0; q < a.P; ++q) {
-        uint8_t* __restrict__ p = a.st8 + a.rseg[q];
-        const int64_t len = a.rlen[q], n4 = len >> 2;  // segments start 2^tbits apart: 4-byte aligned
-        for (int64_t i = tid; i < n4; i += stride) reinterpret_cast<uint32_t*>(p)[i] = 0u;
-        for (int64_t i = (n4 << 2) + tid; i < len; i += stride) p[i] = 0;
-    }
-}
-
 // Single-source start: depths (rows [0, init_rows): the caller keeps the empty suffix at -1), the
-// level-0 queue, the counter ring (level -1's slot: the source's own frontier) and the level -1 state;
-// the stamp bytes are cleared.
+// level-0 queue, the counter ring (level -1's slot: the source's own frontier) and the level -1 state.
 __global__ __launch_bounds__(kBlock) void sbfs_init_kernel(SBfsLevel a, int64_t init_rows, int64_t src, long long total) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = tid; i < init_rows; i += stride) a.dvec[i] = i == src ? 0 : -1;
-    sbfs_zero_stamps(a);
     if (tid == 0) {
         const long long deg = src >= 0 ? (long long)(a.rp[src + 1] - a.rp[src]) : 0;
         if (src >= 0) {
@@ -2270,7 +2298,6 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(SBfsLevel a, Cc
         app.append(take, (int32_t)v, deg, queue, qoff, a.ctr + kSRing - 1);
     }
     app.final(queue, qoff, a.ctr + kSRing - 1);
-    sbfs_zero_stamps(a);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         SBfsState s0{};
         s0.mu = total;
@@ -2318,9 +2345,8 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         DevBuf<int32_t> queue[2];
         DevBuf<int64_t> qoff[2], send_off, woff, rseg, rlen;
         DevBuf<unsigned long long> ctr, gctr, hb, mk, sw, rm;
-        DevBuf<uint8_t> st8;
         DevBuf<SBfsState> st;
-        int64_t hb_words = 0, sw_max = 0, rw_max = 0, live = 0;
+        int64_t hb_words = 0, sw_max = 0, rw_max = 0, live = 0, apply_x = 1;
         bool full_init = false;
     };
     std::vector<St> st(ns);
@@ -2356,7 +2382,14 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         }
         t.hb.alloc(std::max<int64_t>(t.hb_words, 1));
         t.mk.alloc(std::max<int64_t>(t.hb_words, 1));
-        t.st8.alloc(std::max<int64_t>(t.hb_words * 64, 1));
+        // the stamp bytes stay with the shard, zero between traversals (each top-down level's mid kernel
+        // clears what its push set), so the start clears them only after an allocation or a failed call
+        if (sh.sbfs_stamp.size() != (size_t)std::max<int64_t>(t.hb_words * 64, 1)) {
+            sh.sbfs_stamp.alloc(std::max<int64_t>(t.hb_words * 64, 1));
+            sh.sbfs_stamp_clean = false;
+        }
+        if (!sh.sbfs_stamp_clean) JG_HIP(hipMemsetAsync(sh.sbfs_stamp.get(), 0, sh.sbfs_stamp.bytes(), sh.stream));
+        sh.sbfs_stamp_clean = false;  // until this traversal completes
         t.sw.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
         t.rm.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
         t.ctr.alloc(kSRing);
@@ -2429,7 +2462,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         a.dvec = sh.bfs_depth.get();
         a.hb = t.hb.get();
         a.mk = t.mk.get();
-        a.st8 = t.st8.get();
+        a.st8 = sh.sbfs_stamp.get();
         a.sw = t.sw.get();
         a.rm = t.rm.get();
         a.queue_in = t.queue[level & 1].get();
@@ -2452,6 +2485,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             a.gsum[0] = gctrv[i];
         }
         a.st = t.st.get();
+        a.apply_x = t.apply_x;
         a.level = level;
         a.max_depth = max_depth;
         a.alpha = alpha;
@@ -2461,18 +2495,23 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     };
     // (blocks, P) grids.  The appending launches (top-down push, bottom-up probes, mark claims) keep to
     // about kSbfsAppendBlocks workgroups, grid-stride, sized from the shard alone (the frontier is on the
-    // device); the per-peer word passes cover the longest run with kSbfsWords words per wave and trip.
+    // device); the per-peer word passes cover the longest run (at most 256 workgroups per peer).
     constexpr int64_t kSbfsAppendBlocks = 2048;
     std::vector<dim3> gpre(ns), gmid(ns), gpost(ns);
     for (size_t i = 0; i < ns; ++i) {
-        const St& t = st[i];
-        const int64_t per_wave_trip = (kBlock / kWave) * kSbfsWords;
+        St& t = st[i];
+        const int64_t pack_trip = (kBlock / kWave) * kSbfsPackWords, mid_trip = (kBlock / kWave) * 16;
         const int64_t fx = std::max<int64_t>(kSbfsAppendBlocks / g.P, 1);
-        const int64_t pack_x = std::min<int64_t>((t.sw_max + per_wave_trip - 1) / per_wave_trip, 256);
-        const int64_t mid_x = std::min<int64_t>((t.rw_max + per_wave_trip - 1) / per_wave_trip, 256);
+        const int64_t pack_x = std::min<int64_t>((t.sw_max + pack_trip - 1) / pack_trip, 256);
+        const int64_t mid_x = std::min<int64_t>((t.rw_max + mid_trip - 1) / mid_trip, 256);
         gpre[i] = dim3((unsigned)std::max<int64_t>({pack_x, fx, 1}), (unsigned)g.P);
         gmid[i] = dim3((unsigned)std::max<int64_t>(mid_x, 1), (unsigned)g.P);
-        gpost[i] = dim3((unsigned)fx, (unsigned)g.P);
+        // the claims: kSbfsApplyChunk words per wave and trip, at most kSbfsApplyBlocks workgroups in all
+        st[i].apply_x = std::max<int64_t>(std::min<int64_t>((t.sw_max + (kBlock / kWave) * kSbfsApplyChunk - 1) /
+                                                                ((kBlock / kWave) * kSbfsApplyChunk),
+                                                            std::max<int64_t>(kSbfsApplyBlocks / g.P, 1)),
+                                          1);
+        gpost[i] = dim3((unsigned)std::max(fx, st[i].apply_x), (unsigned)g.P);
     }
     hipEvent_t t0, t1;
     {
@@ -2496,7 +2535,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             sbfs_init_roots_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(a, roots[i], (long long)tot[0]);
         } else {
             const int64_t init_rows = t.full_init ? sh.rows : t.live;
-            sbfs_init_kernel<<<grid_for(std::max(init_rows, t.hb_words * 16)), kBlock, 0, sh.stream>>>(
+            sbfs_init_kernel<<<grid_for(init_rows), kBlock, 0, sh.stream>>>(
                 a, init_rows, sh.index == src_shard ? src_local : -1, (long long)tot[0]);
         }
         JG_LAUNCH_CHECK();
@@ -2517,7 +2556,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh);
-                sbfs_pre_kernel<<<gpre[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                sbfs_pre_kernel<kSbfsPackWords><<<gpre[i], kBlock, 0, sh.stream>>>(level_args(i, level));
                 JG_LAUNCH_CHECK();
             }
             for (size_t i = 0; i < ns; ++i) {
@@ -2540,7 +2579,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh);
-                sbfs_post_kernel<<<gpost[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                sbfs_post_kernel<kSbfsApplyWords><<<gpost[i], kBlock, 0, sh.stream>>>(level_args(i, level));
                 JG_LAUNCH_CHECK();
             }
             sbfs_reduce(g, ctrv, gctrv, level % kSRing);
@@ -2575,6 +2614,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         JG_HIP(hipStreamSynchronize(sh.stream));
         // a source in the skipped suffix left its 0 there: the next call refills the suffix
         sh.bfs_depth_tail_clean = !st[i].full_init || st[i].live == sh.rows;
+        sh.sbfs_stamp_clean = true;  // every top-down level cleared its stamps
     }
     if (!roots) {  // the level counts of the last traversals (the first batch's size)
         for (int k = 3; k > 0; --k) sh0.bfs_hist[k] = sh0.bfs_hist[k - 1];

@@ -6,5 +6,3 @@ timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-metho
 tail -3 $OUT/pytest.log
 timeout -k 10 600 bash tools/shard_traces.sh $OUT/st 26 8 bfs > $OUT/st.log 2>&1 || { tail -20 $OUT/st.log; exit 4; }
 tail -5 $OUT/st.log
-timeout -k 10 900 bash tools/gpu_ab_fold.sh ${1:-r06b}/abfold > $OUT/abfold.log 2>&1 || { tail -20 $OUT/abfold.log; exit 5; }
-tail -4 $OUT/abfold.log

@@ -21,7 +21,7 @@ from janusgraph_amd import _lib  # noqa: E402
 DEFAULTS = {"pull_split": 1, "merge_temporal": 1, "merge_pack": 1, "merge_stage0": -1, "merge_stage1": -1,
             "merge_stage2": -1, "merge_stage3": -1,
             "band0_deg": 96, "band0_bit": 0, "band1_deg": -1, "band1_bit": 0, "band2_deg": -1, "band2_bit": 0,
-            "band3_deg": 0, "band3_bit": 3, "ab_fold": 0}
+            "band3_deg": 0, "band3_bit": 3}
 
 
 def apply(knobs):
