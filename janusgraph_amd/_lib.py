@@ -260,9 +260,12 @@ class Context:
 
     def close(self):
         if self._h:
-            # the graphs first: a graph destroyed after its context would touch freed streams
+            # the graphs and builders first: they use the context's streams, and jg_ctx_destroy refuses
+            # (JG_ERR_STATE) while any is alive
             for g in list(getattr(self, "_graphs", ())):
                 g.close()
+            for b in list(getattr(self, "_builders", ())):
+                b.close()
             check(load().jg_ctx_destroy(self._h))
             self._h = ctypes.c_void_p()
 
@@ -360,6 +363,9 @@ class Builder:
         self.ctx = ctx
         self._h = ctypes.c_void_p()
         check(load().jg_builder_create(ctx.handle, ctypes.byref(self._h)))
+        if not hasattr(ctx, "_builders"):
+            ctx._builders = weakref.WeakSet()
+        ctx._builders.add(self)
 
     def close(self):
         if self._h:
