@@ -487,7 +487,8 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
                                       "bfs_init_roots_kernel + bfs_level_kernel)", wl_cc,
                                       "58 B per row with an edge (union-find passes + BFS start), 12 B per entry "
                                       "linked in the second round, 4 B per entry of the rows the BFS reached "
-                                      "(jg_cc.hip cc_union_find), 24 B per vertex of the caller-order output")
+                                      "(jg_cc.hip cc_union_find); the caller-order output: 4 B per row with an edge (giant-component bits) + "
+                                      "12 B per vertex")
     else:
         cc["per_rank"] = per_rank_rows(cc_rank)
     # 64 sources among the degree > 0 vertices; TEPS counts each source's component edges

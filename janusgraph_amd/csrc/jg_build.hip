@@ -554,6 +554,16 @@ void remap_ids_device(const int64_t* d_vid, int64_t n, const int64_t* d_src, con
 
 void dense_of_vids(const Graph& g, const int64_t* vids, int64_t k, int64_t* out, int64_t* padded) {
     if (k <= 0) return;
+    if (g.id_table.size() == 0 && k <= 4096) {
+        // no id table (vid == dense index): a few sources are looked up on the host, without the device
+        // round trip (two synchronised copies and a launch: ~40 us of a 0.2 ms RMAT-20 BFS call)
+        const std::vector<int32_t>* pad = padded ? &g.padded_of_dense() : nullptr;
+        for (int64_t i = 0; i < k; ++i) {
+            out[i] = vids[i] >= 0 && vids[i] < g.n ? vids[i] : -1;
+            if (padded) padded[i] = out[i] >= 0 ? (int64_t)(*pad)[(size_t)out[i]] : -1;
+        }
+        return;
+    }
     DeviceGuard dg(g.id_dev);
     hipStream_t s = g.shards[0]->stream;
     DevBuf<int64_t> q(k), r(k), pr(padded ? k : 0);

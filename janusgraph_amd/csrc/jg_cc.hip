@@ -98,14 +98,35 @@ __global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t
 
 // comp[d] = vor[label[local[d]]]: each caller vertex's component id, in caller order, gathered through
 // the inverse of the degree order (a coalesced store per vertex; the scatter through dense_rows it
-// replaces wrote one 8-byte value per 64-byte line: ~1.5 ms at RMAT-26, round 5).  Rows from
-// label_rows on take their own rank as label (the union-find's edgeless suffix, not written).
+// replaced wrote one 8-byte value per 64-byte line: ~1.5 ms at RMAT-26, round 5).  The random reads are
+// avoided where the answer is known without them: a row of the giant component (one bit per row with an
+// edge, `giant`: 4 MB at RMAT-26, cache-resident) takes the giant's id, and a row without an edge (from
+// label_rows on) is its own component, whose id is its own (vid_is_dense: the graph's ids are its dense
+// indices) or vor[its rank].  Only the other rows gather their label (round 6: 0.78 ms with every row
+// gathering its label at RMAT-26).
+__global__ void cc_giant_bits_kernel(const int32_t* __restrict__ label, int64_t label_rows, const int32_t* giant_label,
+                                     unsigned long long* __restrict__ giant) {
+    const int32_t gl = *giant_label;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < label_rows; x0 += stride) {  // block-uniform trips
+        const int64_t l = x0 + threadIdx.x;
+        const uint64_t w = __ballot(l < label_rows && label[l] == gl);
+        if (lane_id() == 0 && l < label_rows) giant[l >> 6] = w;
+    }
+}
 __global__ void cc_output_kernel(const int32_t* __restrict__ label, const int32_t* __restrict__ rank,
                                  int64_t label_rows, const int32_t* __restrict__ local_of_dense,
-                                 const int64_t* __restrict__ vor, int64_t n, int64_t* __restrict__ comp) {
+                                 const int64_t* __restrict__ vor, int64_t n, int64_t* __restrict__ comp,
+                                 const unsigned long long* __restrict__ giant, const int32_t* giant_label,
+                                 int vid_is_dense) {
+    const int64_t giant_id = vor[*giant_label];
     for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
         const int32_t l = local_of_dense[d];
-        comp[d] = vor[l < label_rows ? label[l] : rank[l]];
+        int64_t v;
+        if (l >= label_rows) v = vid_is_dense ? d : vor[rank[l]];
+        else if ((giant[l >> 6] >> (l & 63)) & 1ull) v = giant_id;
+        else v = vor[label[l]];
+        comp[d] = v;
     }
 }
 
@@ -1730,9 +1751,17 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         Shard& sh = *g.shards[0];
         DeviceGuard dg(sh);
         out.alloc(n);
+        const int32_t* lab = solved ? uf_labels : sh.cc_label.get();
+        const int64_t lrows = solved ? uf_label_rows : n;
+        // the giant component's label: row 0's (the highest-degree row; any row would be correct)
+        DevBuf<unsigned long long> giant(std::max<int64_t>((lrows + 63) / 64, 1));
+        if (lrows > 0) {
+            cc_giant_bits_kernel<<<grid_for(lrows), kBlock, 0, sh.stream>>>(lab, lrows, lab, giant.get());
+            JG_LAUNCH_CHECK();
+        }
         cc_output_kernel<<<grid_for(n, kBlock, 8192), kBlock, 0, sh.stream>>>(
-            solved ? uf_labels : sh.cc_label.get(), sh.cc_rank0.get(), solved ? uf_label_rows : n, g.padded_dev.get(),
-            g.cc_vor.get(), n, out.get());
+            lab, sh.cc_rank0.get(), lrows, g.padded_dev.get(), g.cc_vor.get(), n, out.get(), giant.get(),
+            lrows > 0 ? lab : sh.cc_rank0.get(), g.vid.empty() ? 1 : 0);
         JG_LAUNCH_CHECK();
     }
     JG_HIP(hipEventRecord(t1, sh0.stream));
@@ -1750,8 +1779,9 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     ctx.last.edges_traversed = nnz * iteration;
     // the propagation: 16m + 16n per superstep; the union-find: its own pass model
     ctx.last.algorithmic_bytes = solved ? uf_bytes : (8.0 * nnz + 16.0 * (double)n) * iteration;
-    // the output pass: local index (4 B), label or rank (4 B), id (8 B) gathered, id stored (8 B) per vertex
-    if (dev_out) ctx.last.algorithmic_bytes += 24.0 * (double)n;
+    // the output pass: the giant bits (a 4-byte label read per row with an edge), then per vertex its local
+    // index (4 B) and the id stored (8 B); the other rows' label and id gathers are not counted
+    if (dev_out) ctx.last.algorithmic_bytes += 12.0 * (double)n + 4.0 * (double)(solved ? uf_label_rows : n);
     if (iterations_out) *iterations_out = iteration;
     if (dev_out) {
         Shard& sh = *g.shards[0];

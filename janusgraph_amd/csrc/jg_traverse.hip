@@ -1887,6 +1887,12 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
 constexpr int kSRing = 4;  // level-state ring: level L reads slot L-1, writes L, zeroes L+1
 // shard count the sharded traversal takes (CC checks it too before choosing its sharded path)
 constexpr int kMaxShardsBfs = 64;
+constexpr uint8_t kLevUnseen = 255, kLevFar = 254;
+__device__ __forceinline__ uint8_t lev8(int32_t d) { return d >= kLevFar ? kLevFar : (uint8_t)d; }
+// own row x is in level L's frontier (exact: byte depths are exact below kLevFar)
+__device__ __forceinline__ bool own_at_level(const int32_t* dvec, const uint8_t* dlev, int64_t x, int32_t L) {
+    return L < kLevFar ? dlev[x] == (uint8_t)L : dvec[x] == L;
+}
 
 struct SBfsState {
     long long mu;     // entries of all shards not yet in any frontier (after this level's input frontier)
@@ -1904,6 +1910,9 @@ struct SBfsLevel {
     int64_t rows;
     int64_t bu_rows;                // rows [bu_rows, rows) have no entry (BOTH empty suffix): never probed
     int32_t* dvec;                  // [rows] own depths
+    // [rows] own depths as bytes for the probes (a 8 MB map at 2^23 rows stays in the caches where the
+    // 32 MB int32 depths do not): 255 unvisited, 254 any depth >= 254 (levels from 254 on compare dvec)
+    uint8_t* dlev;
     unsigned long long* hb;         // compact bitmap: the peers' frontier bits, received forward (bottom-up)
     unsigned long long* mk;         // compact bitmap: this level's remote marks (top-down), packed from st8
     uint8_t* st8;                   // compact byte map: remote targets stamped by the top-down push
@@ -1986,12 +1995,12 @@ __device__ __forceinline__ void sbfs_pack_bits(const SBfsLevel& a) {
             in[k] = x < cnt;
             r[k] = src[in[k] ? x : cnt - 1];  // words exist only for a nonempty run
         }
-        int32_t d[PW];
+        bool at[PW];
 #pragma unroll
-        for (int k = 0; k < PW; ++k) d[k] = a.dvec[r[k]];
+        for (int k = 0; k < PW; ++k) at[k] = own_at_level(a.dvec, a.dlev, r[k], a.level);
 #pragma unroll
         for (int k = 0; k < PW; ++k) {
-            const uint64_t word = __ballot(in[k] && d[k] == a.level);
+            const uint64_t word = __ballot(in[k] && at[k]);
             if (lane_id() == 0 && w0 + k * nwaves < nw) a.sw[wo + w0 + k * nwaves] = word;
         }
     }
@@ -2034,7 +2043,8 @@ __device__ __forceinline__ void sbfs_td_push(const SBfsLevel& a, int64_t nq, int
                 const int32_t v = a.queue_in[i];
                 u = a.col[a.rp[v] + (e - a.qoff_in[i])];
                 if (u < a.rows) {
-                    if (a.dvec[u] < 0 && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                    if (a.dlev[u] == kLevUnseen && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                        a.dlev[u] = lev8(nd);
                         take = true;
                         deg = a.rp[u + 1] - a.rp[u];
                     }
@@ -2060,9 +2070,9 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t deg = 0;
-        if (v < a.bu_rows && a.dvec[v] < 0) {
+        if (v < a.bu_rows && a.dlev[v] == kLevUnseen) {
             auto in_frontier = [&](int32_t x) -> bool {
-                return x < a.rows ? a.dvec[x] == a.level : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
+                return x < a.rows ? own_at_level(a.dvec, a.dlev, x, a.level) : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
             };
             // the first neighbour alone, from the dense first-column array (bfs_bottom_up)
             const int32_t u0 = a.first_col[v];
@@ -2078,6 +2088,7 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
             }
             if (found) {
                 a.dvec[v] = nd;
+                a.dlev[v] = lev8(nd);
                 deg = j1 - j0;
             }
         }
@@ -2125,7 +2136,9 @@ __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) 
                 if (!word[k]) continue;  // wave-uniform
                 bool take = false;
                 int64_t deg = 0;
-                if (((word[k] >> lane_id()) & 1ull) && a.dvec[u[k]] < 0 && atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
+                if (((word[k] >> lane_id()) & 1ull) && a.dlev[u[k]] == kLevUnseen &&
+                    atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
+                    a.dlev[u[k]] = lev8(nd);
                     take = true;
                     deg = a.rp[u[k] + 1] - a.rp[u[k]];
                 }
@@ -2259,11 +2272,15 @@ __global__ __launch_bounds__(kBlock) void sbfs_copy_kernel(const SBfsCopyRun* __
 // level-0 queue, the counter ring (level -1's slot: the source's own frontier) and the level -1 state.
 __global__ __launch_bounds__(kBlock) void sbfs_init_kernel(SBfsLevel a, int64_t init_rows, int64_t src, long long total) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t i = tid; i < init_rows; i += stride) a.dvec[i] = i == src ? 0 : -1;
+    for (int64_t i = tid; i < init_rows; i += stride) {
+        a.dvec[i] = i == src ? 0 : -1;
+        a.dlev[i] = i == src ? (uint8_t)0 : kLevUnseen;  // (rows past the empty suffix are never read)
+    }
     if (tid == 0) {
         const long long deg = src >= 0 ? (long long)(a.rp[src + 1] - a.rp[src]) : 0;
         if (src >= 0) {
             a.dvec[src] = 0;  // (also when the source lies in the skipped suffix: the caller refills it)
+            a.dlev[src] = 0;
             const_cast<int32_t*>(a.queue_in)[0] = (int32_t)src;
             const_cast<int64_t*>(a.qoff_in)[0] = 0;
         }
@@ -2294,6 +2311,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(SBfsLevel a, Cc
                 take = deg > 0 && r.parent[v] == r.rank[v];
             }
             a.dvec[v] = take ? 0 : -1;
+            a.dlev[v] = take ? (uint8_t)0 : kLevUnseen;
         }
         app.append(take, (int32_t)v, deg, queue, qoff, a.ctr + kSRing - 1);
     }
@@ -2345,6 +2363,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         DevBuf<int32_t> queue[2];
         DevBuf<int64_t> qoff[2], send_off, woff, rseg, rlen;
         DevBuf<unsigned long long> ctr, gctr, hb, mk, sw, rm;
+        DevBuf<uint8_t> dlev;
         DevBuf<SBfsState> st;
         int64_t hb_words = 0, sw_max = 0, rw_max = 0, live = 0, apply_x = 1;
         bool full_init = false;
@@ -2394,6 +2413,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         t.rm.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
         t.ctr.alloc(kSRing);
         t.gctr.alloc(kSRing);
+        t.dlev.alloc(r1);
         t.st.alloc(kSRing);
         bfs_first_col(sh, sh.both);  // the bottom-up's first columns (before t0)
         // depths live in bfs_depth; the BOTH empty suffix is never reached, so it keeps -1 between calls
@@ -2460,6 +2480,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         a.rows = sh.rows;
         a.bu_rows = t.live;
         a.dvec = sh.bfs_depth.get();
+        a.dlev = t.dlev.get();
         a.hb = t.hb.get();
         a.mk = t.mk.get();
         a.st8 = sh.sbfs_stamp.get();
