@@ -23,11 +23,13 @@ KERNELS = {
     "bfs": ["bfs_init_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
     "cc": ["uf_init_kernel", "uf_link_first_kernel", "uf_hook_first_kernel", "uf_link_up_compress_kernel",
            "uf_link_rest_kernel", "uf_compress_kernel", "uf_sample_kernel", "uf_minrank_kernel",
-           "heavy_rows_kernel", "bfs_init_roots_kernel", "bfs_level_kernel", "bfs_td_claim_kernel"],
+           "heavy_rows_kernel", "bfs_init_roots_kernel", "bfs_level_kernel", "bfs_td_claim_kernel",
+           "cc_giant_bits_kernel", "cc_output_kernel"],  # (round 6: the caller-order output is in the region)
     "msbfs": ["MsBfsOp", "msbfs_live_kernel", "msbfs_scan_kernel", "msbfs_todo_kernel", "msbfs_task_live_kernel",
               "msbfs_init_kernel", "msbfs_frontier_kernel", "msbfs_source_queue_kernel", "msbfs_td_kernel",
               "msbfs_td_apply_kernel", "msbfs_zero_list_kernel", "msbfs_td_recv_kernel", "msbfs_td_record_kernel",
-              "msbfs_exit_first_kernel", "msbfs_exit_rest_kernel", "zero_words_kernel"],
+              "msbfs_exit_first_kernel", "msbfs_exit_rest_kernel", "zero_words_kernel", "msbfs_frontier_live_kernel",
+              "msbfs_td_apply_rows_kernel", "msbfs_zero_tail_sources_kernel"],
     "pr": ["PrOp"],
 }
 
