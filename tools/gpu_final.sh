@@ -15,5 +15,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 15; }
 JG_TRACE_MARKS=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_trace -o bench -- python3 bench.py --no-cpu --trace-windows > $OUT/bench_traced.json 2> $OUT/bench_traced.err || { tail -20 $OUT/bench_traced.err; exit 16; }
 timeout -k 10 600 bash tools/shard_traces.sh $OUT/st 26 8 bfs > $OUT/st.log 2>&1 || { tail -20 $OUT/st.log; exit 17; }
-timeout -k 10 1500 bash tools/pmc_workloads.sh $T/pmc bfs20 bfs26 cc26 pr24 pr26 > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 18; }
+[ -n "$PMC" ] && { timeout -k 10 1500 bash tools/pmc_workloads.sh $T/pmc $PMC > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 18; }; }
 echo all-done
