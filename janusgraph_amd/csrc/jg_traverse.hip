@@ -1887,11 +1887,16 @@ int64_t local_of_vid(const Graph& g, int64_t vid, int* shard_out) {
 constexpr int kSRing = 4;  // level-state ring: level L reads slot L-1, writes L, zeroes L+1
 // shard count the sharded traversal takes (CC checks it too before choosing its sharded path)
 constexpr int kMaxShardsBfs = 64;
-constexpr uint8_t kLevUnseen = 255, kLevFar = 254;
-__device__ __forceinline__ uint8_t lev8(int32_t d) { return d >= kLevFar ? kLevFar : (uint8_t)d; }
-// own row x is in level L's frontier (exact: byte depths are exact below kLevFar)
-__device__ __forceinline__ bool own_at_level(const int32_t* dvec, const uint8_t* dlev, int64_t x, int32_t L) {
-    return L < kLevFar ? dlev[x] == (uint8_t)L : dvec[x] == L;
+// bits of x at the set positions of m, packed into the low popc(m) bits (x's set bits only are visited)
+__device__ __forceinline__ unsigned long long pext_u64(unsigned long long x, unsigned long long m) {
+    x &= m;
+    unsigned long long r = 0;
+    while (x) {
+        const int b = __ffsll(x) - 1;
+        r |= 1ull << __popcll(m & ((1ull << b) - 1ull));
+        x &= x - 1;
+    }
+    return r;
 }
 
 struct SBfsState {
@@ -1910,12 +1915,23 @@ struct SBfsLevel {
     int64_t rows;
     int64_t bu_rows;                // rows [bu_rows, rows) have no entry (BOTH empty suffix): never probed
     int32_t* dvec;                  // [rows] own depths
-    // [rows] own depths as bytes for the probes (a 8 MB map at 2^23 rows stays in the caches where the
-    // 32 MB int32 depths do not): 255 unvisited, 254 any depth >= 254 (levels from 254 on compare dvec)
-    uint8_t* dlev;
+    uint8_t* seen;                  // [rows] 1: the row's depth is set (a byte probe instead of an int32 one)
+    // Own frontiers as bitmaps over own rows, rotating by level: fb[L % 3] = the rows of depth L (set by
+    // level L-1's claims: the bottom-up's ballot words, the top-down claims' atomicOr), fb[(L + 1) % 3]
+    // receives level L's claims, fb[(L + 2) % 3] (level L-1's, read by nothing any more) is cleared by
+    // level L's first kernel for level L+1.
+    unsigned long long* fb[3];
+    int64_t fw;                     // words per bitmap
+    // Send lists as bitmaps over own rows: bit v of bq[q] = own row v is in peer q's send list (which
+    // holds its rows in ascending order), bpre[q][w] = the send-list position of word w's first set bit,
+    // bfirst[woff[q] + k] = the first row word contributing to peer q's send-list word k
+    const unsigned long long* bq;   // [P][fw]
+    const int32_t* bpre;            // [P][fw + 1]
+    const int32_t* bfirst;          // [woff[P]]
     unsigned long long* hb;         // compact bitmap: the peers' frontier bits, received forward (bottom-up)
     unsigned long long* mk;         // compact bitmap: this level's remote marks (top-down), packed from st8
     uint8_t* st8;                   // compact byte map: remote targets stamped by the top-down push
+    uint8_t* dirty;                 // [C / 512] a stamp was set in this 512-byte chunk (zero between levels)
     unsigned long long* sw;         // send-list words: own frontier bits for the peers (bottom-up)
     const unsigned long long* rm;   // send-list words: the peers' marks of own rows, received back (top-down)
     const int32_t* queue_in;
@@ -1937,6 +1953,10 @@ struct SBfsLevel {
     double alpha, beta;
     int64_t nrows;                  // rows of all shards (the beta rule)
 };
+
+__device__ __forceinline__ void sbfs_claim_bit(const SBfsLevel& a, int64_t v) {  // v joins level L+1's frontier
+    atomicOr(&a.fb[(a.level + 1) % 3][v >> 6], 1ull << (v & 63));
+}
 
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
     const int lo = __shfl((int)(uint32_t)v, src, kWave), hi = __shfl((int)(uint32_t)(v >> 32), src, kWave);
@@ -1977,32 +1997,30 @@ __device__ SBfsState sbfs_decide(const SBfsLevel& a, long long* nq, long long* m
 // no word searches the per-peer offset tables (a scan of LDS-staged tables per word held them to 45-80 us
 // per launch at RMAT-26, P = 8, round 4).  The row-parallel passes use the same grid flattened.
 
-// bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = the depth of the
-// word's row b is this level's.  A wave takes PW words per trip, every load issued on a clamped
-// index before any is used.
-template <int PW>
+// bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = send-list row b is
+// in this level's frontier.  A thread per word: the word's bits are the frontier bits of the row words it
+// spans, extracted at peer q's membership bits (a send list holds its rows in ascending order) and shifted
+// to their send-list positions.  Reads 1 MB bitmaps instead of the 59 MB list of rows and their depths
+// (RMAT-26, P = 8: 42 us per bottom-up level and shard through the list, round 6).
 __device__ __forceinline__ void sbfs_pack_bits(const SBfsLevel& a) {
     const int q = blockIdx.y;
-    const int64_t so = a.send_off[q], cnt = a.send_off[q + 1] - so, wo = a.woff[q], nw = a.woff[q + 1] - wo;
-    const int32_t* __restrict__ src = a.send_src + so;
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t w0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); w0 < nw; w0 += nwaves * PW) {
-        int32_t r[PW];
-        bool in[PW];
-#pragma unroll
-        for (int k = 0; k < PW; ++k) {
-            const int64_t x = (w0 + k * nwaves) * 64 + lane_id();
-            in[k] = x < cnt;
-            r[k] = src[in[k] ? x : cnt - 1];  // words exist only for a nonempty run
+    const int64_t wo = a.woff[q], nw = a.woff[q + 1] - wo;
+    const unsigned long long* __restrict__ F = a.fb[a.level % 3];
+    const unsigned long long* __restrict__ B = a.bq + (int64_t)q * a.fw;
+    const int32_t* __restrict__ pre = a.bpre + (int64_t)q * (a.fw + 1);
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nw; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t lo = 64 * k, hi = lo + 64;
+        unsigned long long out = 0;
+        for (int64_t w = a.bfirst[wo + k]; w < a.fw; ++w) {
+            const int64_t p = pre[w];
+            if (p >= hi) break;
+            const unsigned long long m = B[w], f = F[w] & m;
+            if (!f) continue;
+            const unsigned long long bits = pext_u64(f, m);
+            const int64_t sh = p - lo;
+            out |= sh >= 0 ? bits << sh : bits >> (-sh);
         }
-        bool at[PW];
-#pragma unroll
-        for (int k = 0; k < PW; ++k) at[k] = own_at_level(a.dvec, a.dlev, r[k], a.level);
-#pragma unroll
-        for (int k = 0; k < PW; ++k) {
-            const uint64_t word = __ballot(in[k] && at[k]);
-            if (lane_id() == 0 && w0 + k * nwaves < nw) a.sw[wo + w0 + k * nwaves] = word;
-        }
+        a.sw[wo + k] = out;
     }
 }
 
@@ -2043,13 +2061,15 @@ __device__ __forceinline__ void sbfs_td_push(const SBfsLevel& a, int64_t nq, int
                 const int32_t v = a.queue_in[i];
                 u = a.col[a.rp[v] + (e - a.qoff_in[i])];
                 if (u < a.rows) {
-                    if (a.dlev[u] == kLevUnseen && atomicCAS(&a.dvec[u], -1, nd) == -1) {
-                        a.dlev[u] = lev8(nd);
+                    if (!a.seen[u] && atomicCAS(&a.dvec[u], -1, nd) == -1) {
+                        a.seen[u] = 1;
+                        sbfs_claim_bit(a, u);
                         take = true;
                         deg = a.rp[u + 1] - a.rp[u];
                     }
                 } else {
                     a.st8[u] = 1;
+                    a.dirty[u >> 9] = 1;
                 }
             }
             app.append(take, u, deg, a.queue_out, a.qoff_out, packed);
@@ -2070,9 +2090,10 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
         const int64_t v = w * 64 + lane_id();
         bool found = false;
         int64_t deg = 0;
-        if (v < a.bu_rows && a.dlev[v] == kLevUnseen) {
+        if (v < a.bu_rows && !a.seen[v]) {
+            const unsigned long long* __restrict__ F = a.fb[a.level % 3];
             auto in_frontier = [&](int32_t x) -> bool {
-                return x < a.rows ? own_at_level(a.dvec, a.dlev, x, a.level) : (bool)((a.hb[x >> 6] >> (x & 63)) & 1ull);
+                return (bool)(((x < a.rows ? F[x >> 6] : a.hb[x >> 6]) >> (x & 63)) & 1ull);
             };
             // the first neighbour alone, from the dense first-column array (bfs_bottom_up)
             const int32_t u0 = a.first_col[v];
@@ -2088,10 +2109,12 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
             }
             if (found) {
                 a.dvec[v] = nd;
-                a.dlev[v] = lev8(nd);
+                a.seen[v] = 1;
                 deg = j1 - j0;
             }
         }
+        const uint64_t word = __ballot(found);  // level L+1's frontier word (words past bu_rows stay zero)
+        if (lane_id() == 0) a.fb[(a.level + 1) % 3][w] = word;
         app.append(found, (int32_t)v, deg, a.queue_out, a.qoff_out, packed);
     }
 }
@@ -2103,9 +2126,9 @@ __device__ __forceinline__ void sbfs_bottom_up(const SBfsLevel& a, WaveApp& app)
 // 2 against 21 / 100 us for this shape, round 6.)
 constexpr int kSbfsApplyChunk = 16;
 // Round-6 A/B at RMAT-26, P = 8 (tools/shard_sim.py, event time per shard; profiles/r06/sbfs/variants.log):
-// 4 -> 8 words per trip in the send-list pack 0.606 -> 0.583 ms, in the claims 0.601; 1024 -> 2048 /
-// 4096 claim workgroups 0.578 / 0.573.
-constexpr int kSbfsPackWords = 8, kSbfsApplyWords = 8;
+// 4 -> 8 words per trip in the claims 0.606 -> 0.601 ms (in the list-walking pack, since replaced, 0.583);
+// 1024 -> 2048 / 4096 claim workgroups 0.578 / 0.573.
+constexpr int kSbfsApplyWords = 8;
 constexpr int64_t kSbfsApplyBlocks = 4096;
 template <int AW>
 __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) {
@@ -2136,9 +2159,9 @@ __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) 
                 if (!word[k]) continue;  // wave-uniform
                 bool take = false;
                 int64_t deg = 0;
-                if (((word[k] >> lane_id()) & 1ull) && a.dlev[u[k]] == kLevUnseen &&
-                    atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
-                    a.dlev[u[k]] = lev8(nd);
+                if (((word[k] >> lane_id()) & 1ull) && !a.seen[u[k]] && atomicCAS(&a.dvec[u[k]], -1, nd) == -1) {
+                    a.seen[u[k]] = 1;
+                    sbfs_claim_bit(a, u[k]);
                     take = true;
                     deg = a.rp[u[k] + 1] - a.rp[u[k]];
                 }
@@ -2150,7 +2173,6 @@ __device__ __forceinline__ void sbfs_td_apply(const SBfsLevel& a, WaveApp& app) 
 
 // First kernel of a level: the decision (block (0, 0) publishes it and zeroes the next level's counter),
 // then this shard's send-list bits (bottom-up) or its top-down push.
-template <int PW>
 __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
     __shared__ SBfsState s_st;
     __shared__ long long s_nq, s_mf;
@@ -2169,8 +2191,14 @@ __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
     }
     __syncthreads();
     if (s_st.done) return;
+    {  // level L-1's frontier bitmap becomes level L+1's (cleared before level L+1's claims)
+        unsigned long long* __restrict__ z = a.fb[(a.level + 2) % 3];
+        const int64_t stride = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+        for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < a.fw; i += stride)
+            z[i] = 0ull;
+    }
     if (s_st.bottom_up) {
-        sbfs_pack_bits<PW>(a);
+        sbfs_pack_bits(a);
     } else {
         WaveApp app{ws};
         sbfs_td_push(a, s_nq, s_mf, app);
@@ -2180,7 +2208,8 @@ __global__ __launch_bounds__(kBlock) void sbfs_pre_kernel(SBfsLevel a) {
 
 // Second kernel of a top-down level (a bottom-up level leaves at once): peer q's segment of stamp bytes
 // into its mark words, every word written (zero or not: the words are the exchange's payload) and every
-// set byte cleared for the next top-down level.  Lane l loads bytes [8l, 8l + 8) of a 512-byte chunk
+// set byte cleared for the next top-down level.  Chunks the push left clean (no dirty flag) are not read:
+// the small top-down levels (a few thousand stamps) write zero words only.  Lane l loads bytes [8l, 8l + 8) of a 512-byte chunk
 // (eight mark words) as one 8-byte load; word k is the byte masks of lanes 8k .. 8k + 7.  (One byte per
 // lane and load ran 13-19 us per level and shard at RMAT-26, P = 8.)
 __global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
@@ -2197,13 +2226,17 @@ __global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
     unsigned long long* __restrict__ mk = a.mk + (seg >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
     const int l = lane_id();
+    uint8_t* __restrict__ dirty = a.dirty + (seg >> 9);  // one flag per 512-byte chunk (segments start on one)
     for (int64_t c0 = (int64_t)blockIdx.x * (kBlock / kWave) + wave_id(); c0 < nchunks; c0 += nwaves * 2) {
         unsigned long long x[2];
         bool in[2];
+        uint8_t dc[2];  // the chunk's dirty flag: a clean chunk's words are zero, its stamps are not read
+#pragma unroll
+        for (int k = 0; k < 2; ++k) dc[k] = c0 + k * nwaves < nchunks ? dirty[c0 + k * nwaves] : (uint8_t)0;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // two chunks per trip, both loads issued first
             const int64_t b0 = (c0 + k * nwaves) * 512 + 8 * l;  // this lane's first byte
-            in[k] = c0 + k * nwaves < nchunks && b0 < len;
+            in[k] = dc[k] && b0 < len;
             x[k] = 0ull;
             if (in[k]) {
                 if (b0 + 8 <= len) {
@@ -2223,6 +2256,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_mid_kernel(SBfsLevel a) {
             for (int i = 0; i < 8; ++i) word |= (unsigned long long)__shfl((int)m, 8 * (l & 7) + i, kWave) << (8 * i);
             const int64_t w = (c0 + k * nwaves) * 8 + l;  // lanes 0..7 write words 8c .. 8c + 7
             if (l < 8 && c0 + k * nwaves < nchunks && w < nw) mk[w] = word;
+            if (l == 0 && dc[k]) dirty[c0 + k * nwaves] = 0;
             if (m) {  // clear this lane's stamps (the tail of the run byte by byte)
                 const int64_t b0 = (c0 + k * nwaves) * 512 + 8 * l;
                 if (b0 + 8 <= len) *reinterpret_cast<unsigned long long*>(stamp + b0) = 0ull;
@@ -2274,13 +2308,17 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_kernel(SBfsLevel a, int64_t 
     const int64_t stride = (int64_t)gridDim.x * blockDim.x, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = tid; i < init_rows; i += stride) {
         a.dvec[i] = i == src ? 0 : -1;
-        a.dlev[i] = i == src ? (uint8_t)0 : kLevUnseen;  // (rows past the empty suffix are never read)
+        a.seen[i] = i == src ? 1 : 0;  // (rows past the empty suffix are never read)
+    }
+    for (int64_t i = tid; i < a.fw; i += stride) {  // level 0's frontier bitmap: the source; level 1's: empty
+        a.fb[0][i] = src >= 0 && i == (src >> 6) ? 1ull << (src & 63) : 0ull;
+        a.fb[1][i] = 0ull;
     }
     if (tid == 0) {
         const long long deg = src >= 0 ? (long long)(a.rp[src + 1] - a.rp[src]) : 0;
         if (src >= 0) {
             a.dvec[src] = 0;  // (also when the source lies in the skipped suffix: the caller refills it)
-            a.dlev[src] = 0;
+            a.seen[src] = 1;
             const_cast<int32_t*>(a.queue_in)[0] = (int32_t)src;
             const_cast<int64_t*>(a.qoff_in)[0] = 0;
         }
@@ -2311,16 +2349,82 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(SBfsLevel a, Cc
                 take = deg > 0 && r.parent[v] == r.rank[v];
             }
             a.dvec[v] = take ? 0 : -1;
-            a.dlev[v] = take ? (uint8_t)0 : kLevUnseen;
+            a.seen[v] = take ? 1 : 0;
         }
+        const uint64_t word = __ballot(take);  // level 0's frontier bitmap (64 consecutive rows per wave)
+        if (lane_id() == 0 && v < a.rows) a.fb[0][v >> 6] = word;
         app.append(take, (int32_t)v, deg, queue, qoff, a.ctr + kSRing - 1);
     }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.fw; i += stride) a.fb[1][i] = 0ull;
     app.final(queue, qoff, a.ctr + kSRing - 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         SBfsState s0{};
         s0.mu = total;
         a.st[kSRing - 1] = s0;
     }
+}
+
+// bq[q][w]: the membership bitmap of peer q's send list (grid (blocks, P))
+__global__ __launch_bounds__(kBlock) void sbfs_bq_kernel(const int32_t* __restrict__ send_src,
+                                                         const int64_t* __restrict__ send_off, int64_t fw,
+                                                         unsigned long long* __restrict__ bq) {
+    const int q = blockIdx.y;
+    for (int64_t x = send_off[q] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < send_off[q + 1];
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = send_src[x];
+        atomicOr(&bq[(int64_t)q * fw + (v >> 6)], 1ull << (v & 63));
+    }
+}
+
+// The send lists as bitmaps (SBfsLevel::bq / bpre / bfirst), built on a shard's first sharded traversal
+// (before its timed region) and kept: the bitmaps on the device, the prefixes and first words from a host
+// pass over them.
+void sbfs_send_bitmaps(Graph& g, Shard& sh) {
+    const int64_t fw = std::max<int64_t>((sh.rows + 63) / 64, 1);
+    const int P = g.P;
+    if (sh.sbfs_bq.size() == (size_t)P * fw) return;
+    const Halo& h = sh.halo_both;
+    DeviceGuard dg(sh);
+    sh.sbfs_bq.alloc((size_t)P * fw);
+    JG_HIP(hipMemsetAsync(sh.sbfs_bq.get(), 0, sh.sbfs_bq.bytes(), sh.stream));
+    {
+        DevBuf<int64_t> so(P + 1);
+        copy_h2d(so.get(), h.send_off.data(), (P + 1) * sizeof(int64_t), sh.stream);
+        int64_t longest = 0;
+        for (int q = 0; q < P; ++q) longest = std::max(longest, h.send_off[(size_t)q + 1] - h.send_off[(size_t)q]);
+        if (longest > 0) {
+            sbfs_bq_kernel<<<dim3(grid_for(longest, kBlock, 1024), (unsigned)P), kBlock, 0, sh.stream>>>(
+                h.send_src.get(), so.get(), fw, sh.sbfs_bq.get());
+            JG_LAUNCH_CHECK();
+        }
+        JG_HIP(hipStreamSynchronize(sh.stream));
+    }
+    std::vector<unsigned long long> bq((size_t)P * fw);
+    copy_d2h(bq.data(), sh.sbfs_bq.get(), bq.size() * sizeof(unsigned long long), sh.stream);
+    const std::vector<int64_t> woff = halo_word_offsets(h, P);
+    std::vector<int32_t> pre((size_t)P * (fw + 1)), first((size_t)std::max<int64_t>(woff[(size_t)P], 1), 0);
+    for (int q = 0; q < P; ++q) {
+        const unsigned long long* b = bq.data() + (size_t)q * fw;
+        int32_t* pq = pre.data() + (size_t)q * (fw + 1);
+        int64_t c = 0;
+        for (int64_t w = 0; w < fw; ++w) {
+            pq[w] = (int32_t)c;
+            c += __builtin_popcountll(b[w]);
+        }
+        pq[fw] = (int32_t)c;
+        if (c != h.send_off[(size_t)q + 1] - h.send_off[(size_t)q])
+            fail(JG_ERR_STATE, "sharded BFS: a send list repeats a row");
+        // first row word contributing to send-list word k: the first w whose bits reach position 64 k
+        int64_t w = 0;
+        for (int64_t k = 0; k < woff[(size_t)q + 1] - woff[(size_t)q]; ++k) {
+            while (w < fw && pq[w + 1] <= 64 * k) ++w;
+            first[(size_t)(woff[(size_t)q] + k)] = (int32_t)w;
+        }
+    }
+    sh.sbfs_bpre.alloc(pre.size());
+    copy_h2d(sh.sbfs_bpre.get(), pre.data(), pre.size() * sizeof(int32_t), sh.stream);
+    sh.sbfs_bfirst.alloc(first.size());
+    copy_h2d(sh.sbfs_bfirst.get(), first.data(), first.size() * sizeof(int32_t), sh.stream);
 }
 
 // The level counters of slot `slot` summed into every shard's global slot (gctr), on the streams: a
@@ -2362,8 +2466,8 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     struct St {
         DevBuf<int32_t> queue[2];
         DevBuf<int64_t> qoff[2], send_off, woff, rseg, rlen;
-        DevBuf<unsigned long long> ctr, gctr, hb, mk, sw, rm;
-        DevBuf<uint8_t> dlev;
+        DevBuf<unsigned long long> ctr, gctr, hb, mk, sw, rm, fb;
+        DevBuf<uint8_t> seen;
         DevBuf<SBfsState> st;
         int64_t hb_words = 0, sw_max = 0, rw_max = 0, live = 0, apply_x = 1;
         bool full_init = false;
@@ -2405,15 +2509,21 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         // clears what its push set), so the start clears them only after an allocation or a failed call
         if (sh.sbfs_stamp.size() != (size_t)std::max<int64_t>(t.hb_words * 64, 1)) {
             sh.sbfs_stamp.alloc(std::max<int64_t>(t.hb_words * 64, 1));
+            sh.sbfs_dirty.alloc(std::max<int64_t>(t.hb_words / 8 + 1, 1));
             sh.sbfs_stamp_clean = false;
         }
-        if (!sh.sbfs_stamp_clean) JG_HIP(hipMemsetAsync(sh.sbfs_stamp.get(), 0, sh.sbfs_stamp.bytes(), sh.stream));
+        if (!sh.sbfs_stamp_clean) {
+            JG_HIP(hipMemsetAsync(sh.sbfs_stamp.get(), 0, sh.sbfs_stamp.bytes(), sh.stream));
+            JG_HIP(hipMemsetAsync(sh.sbfs_dirty.get(), 0, sh.sbfs_dirty.bytes(), sh.stream));
+        }
         sh.sbfs_stamp_clean = false;  // until this traversal completes
         t.sw.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
         t.rm.alloc(std::max<int64_t>(woff[(size_t)g.P], 1));
         t.ctr.alloc(kSRing);
         t.gctr.alloc(kSRing);
-        t.dlev.alloc(r1);
+        t.seen.alloc(r1);
+        t.fb.alloc(3 * (size_t)((r1 + 63) / 64));
+        sbfs_send_bitmaps(g, sh);
         t.st.alloc(kSRing);
         bfs_first_col(sh, sh.both);  // the bottom-up's first columns (before t0)
         // depths live in bfs_depth; the BOTH empty suffix is never reached, so it keeps -1 between calls
@@ -2480,10 +2590,16 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         a.rows = sh.rows;
         a.bu_rows = t.live;
         a.dvec = sh.bfs_depth.get();
-        a.dlev = t.dlev.get();
+        a.seen = t.seen.get();
+        a.fw = (std::max<int64_t>(sh.rows, 1) + 63) / 64;
+        for (int k = 0; k < 3; ++k) a.fb[k] = t.fb.get() + k * a.fw;
+        a.bq = sh.sbfs_bq.get();
+        a.bpre = sh.sbfs_bpre.get();
+        a.bfirst = sh.sbfs_bfirst.get();
         a.hb = t.hb.get();
         a.mk = t.mk.get();
         a.st8 = sh.sbfs_stamp.get();
+        a.dirty = sh.sbfs_dirty.get();
         a.sw = t.sw.get();
         a.rm = t.rm.get();
         a.queue_in = t.queue[level & 1].get();
@@ -2521,7 +2637,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     std::vector<dim3> gpre(ns), gmid(ns), gpost(ns);
     for (size_t i = 0; i < ns; ++i) {
         St& t = st[i];
-        const int64_t pack_trip = (kBlock / kWave) * kSbfsPackWords, mid_trip = (kBlock / kWave) * 16;
+        const int64_t pack_trip = kBlock, mid_trip = (kBlock / kWave) * 16;  // (the pack: a send-list word per thread)
         const int64_t fx = std::max<int64_t>(kSbfsAppendBlocks / g.P, 1);
         const int64_t pack_x = std::min<int64_t>((t.sw_max + pack_trip - 1) / pack_trip, 256);
         const int64_t mid_x = std::min<int64_t>((t.rw_max + mid_trip - 1) / mid_trip, 256);
@@ -2577,7 +2693,7 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
             for (size_t i = 0; i < ns; ++i) {
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh);
-                sbfs_pre_kernel<kSbfsPackWords><<<gpre[i], kBlock, 0, sh.stream>>>(level_args(i, level));
+                sbfs_pre_kernel<<<gpre[i], kBlock, 0, sh.stream>>>(level_args(i, level));
                 JG_LAUNCH_CHECK();
             }
             for (size_t i = 0; i < ns; ++i) {
