@@ -253,7 +253,7 @@ struct Shard {
     DevBuf<uint8_t> sbfs_stamp;              // sharded DO-BFS: remote-target stamps per compact position
     DevBuf<uint8_t> sbfs_dirty;              //   a flag per 512 stamps: the chunk holds a set stamp
     DevBuf<unsigned long long> sbfs_bq;      // sharded DO-BFS: send lists as row bitmaps [P][rows / 64]
-    DevBuf<int32_t> sbfs_bpre, sbfs_bfirst;  //   their bit prefixes per word, first row word per list word
+    DevBuf<int32_t> sbfs_bpre;               //   their bit prefixes per word
     bool sbfs_stamp_clean = false;           // ... all zero (set when a traversal completes)
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;

@@ -1923,11 +1923,9 @@ struct SBfsLevel {
     unsigned long long* fb[3];
     int64_t fw;                     // words per bitmap
     // Send lists as bitmaps over own rows: bit v of bq[q] = own row v is in peer q's send list (which
-    // holds its rows in ascending order), bpre[q][w] = the send-list position of word w's first set bit,
-    // bfirst[woff[q] + k] = the first row word contributing to peer q's send-list word k
+    // holds its rows in ascending order), bpre[q][w] = the send-list position of word w's first set bit
     const unsigned long long* bq;   // [P][fw]
     const int32_t* bpre;            // [P][fw + 1]
-    const int32_t* bfirst;          // [woff[P]]
     unsigned long long* hb;         // compact bitmap: the peers' frontier bits, received forward (bottom-up)
     unsigned long long* mk;         // compact bitmap: this level's remote marks (top-down), packed from st8
     uint8_t* st8;                   // compact byte map: remote targets stamped by the top-down push
@@ -1998,29 +1996,26 @@ __device__ SBfsState sbfs_decide(const SBfsLevel& a, long long* nq, long long* m
 // per launch at RMAT-26, P = 8, round 4).  The row-parallel passes use the same grid flattened.
 
 // bottom-up, owner side before the forward exchange: peer q's send-list words, bit b = send-list row b is
-// in this level's frontier.  A thread per word: the word's bits are the frontier bits of the row words it
-// spans, extracted at peer q's membership bits (a send list holds its rows in ascending order) and shifted
-// to their send-list positions.  Reads 1 MB bitmaps instead of the 59 MB list of rows and their depths
-// (RMAT-26, P = 8: 42 us per bottom-up level and shard through the list, round 6).
+// in this level's frontier.  A thread per row word: its frontier bits at peer q's membership bits are
+// extracted and ORed in at their send-list position (a send list holds its rows in ascending order), one or
+// two atomics per word with a frontier row in q's list; the words start zero (the post kernel clears them
+// after the exchange).  Reads 1 MB bitmaps instead of the 59 MB list of rows and their depths (RMAT-26,
+// P = 8: 42 us per bottom-up level and shard through the list; a thread per send-list word that walked
+// the row words it spans took 25 ms: the sparse tail of a list spans thousands of row words, round 6).
 __device__ __forceinline__ void sbfs_pack_bits(const SBfsLevel& a) {
     const int q = blockIdx.y;
-    const int64_t wo = a.woff[q], nw = a.woff[q + 1] - wo;
+    unsigned long long* __restrict__ out = a.sw + a.woff[q];
     const unsigned long long* __restrict__ F = a.fb[a.level % 3];
     const unsigned long long* __restrict__ B = a.bq + (int64_t)q * a.fw;
     const int32_t* __restrict__ pre = a.bpre + (int64_t)q * (a.fw + 1);
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nw; k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t lo = 64 * k, hi = lo + 64;
-        unsigned long long out = 0;
-        for (int64_t w = a.bfirst[wo + k]; w < a.fw; ++w) {
-            const int64_t p = pre[w];
-            if (p >= hi) break;
-            const unsigned long long m = B[w], f = F[w] & m;
-            if (!f) continue;
-            const unsigned long long bits = pext_u64(f, m);
-            const int64_t sh = p - lo;
-            out |= sh >= 0 ? bits << sh : bits >> (-sh);
-        }
-        a.sw[wo + k] = out;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < a.fw; w += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long m = B[w], f = F[w] & m;
+        if (!f) continue;
+        const unsigned long long bits = pext_u64(f, m);
+        const int64_t p = pre[w];
+        const int o = (int)(p & 63);
+        atomicOr(&out[p >> 6], bits << o);
+        if (o && (bits >> (64 - o))) atomicOr(&out[(p >> 6) + 1], bits >> (64 - o));
     }
 }
 
@@ -2274,6 +2269,12 @@ __global__ __launch_bounds__(kBlock) void sbfs_post_kernel(SBfsLevel a) {
     if (threadIdx.x == 0) s_st = a.st[a.level % kSRing];
     __syncthreads();
     if (s_st.done) return;
+    if (s_st.bottom_up) {  // the send-list words went out with the exchange: clear them for the next pack
+        const int64_t nw = a.woff[a.P];
+        const int64_t stride = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+        for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < nw; i += stride)
+            a.sw[i] = 0ull;
+    }
     if (!s_st.bottom_up && blockIdx.x >= a.apply_x) return;  // (block-uniform)
     WaveApp app{ws};
     if (s_st.bottom_up) sbfs_bottom_up(a, app);
@@ -2314,6 +2315,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_kernel(SBfsLevel a, int64_t 
         a.fb[0][i] = src >= 0 && i == (src >> 6) ? 1ull << (src & 63) : 0ull;
         a.fb[1][i] = 0ull;
     }
+    for (int64_t i = tid; i < a.woff[a.P]; i += stride) a.sw[i] = 0ull;  // the pack ORs into zero words
     if (tid == 0) {
         const long long deg = src >= 0 ? (long long)(a.rp[src + 1] - a.rp[src]) : 0;
         if (src >= 0) {
@@ -2356,6 +2358,7 @@ __global__ __launch_bounds__(kBlock) void sbfs_init_roots_kernel(SBfsLevel a, Cc
         app.append(take, (int32_t)v, deg, queue, qoff, a.ctr + kSRing - 1);
     }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.fw; i += stride) a.fb[1][i] = 0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.woff[a.P]; i += stride) a.sw[i] = 0ull;
     app.final(queue, qoff, a.ctr + kSRing - 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         SBfsState s0{};
@@ -2376,9 +2379,8 @@ __global__ __launch_bounds__(kBlock) void sbfs_bq_kernel(const int32_t* __restri
     }
 }
 
-// The send lists as bitmaps (SBfsLevel::bq / bpre / bfirst), built on a shard's first sharded traversal
-// (before its timed region) and kept: the bitmaps on the device, the prefixes and first words from a host
-// pass over them.
+// The send lists as bitmaps (SBfsLevel::bq / bpre), built on a shard's first sharded traversal (before
+// its timed region) and kept: the bitmaps on the device, the prefixes from a host pass over them.
 void sbfs_send_bitmaps(Graph& g, Shard& sh) {
     const int64_t fw = std::max<int64_t>((sh.rows + 63) / 64, 1);
     const int P = g.P;
@@ -2401,8 +2403,7 @@ void sbfs_send_bitmaps(Graph& g, Shard& sh) {
     }
     std::vector<unsigned long long> bq((size_t)P * fw);
     copy_d2h(bq.data(), sh.sbfs_bq.get(), bq.size() * sizeof(unsigned long long), sh.stream);
-    const std::vector<int64_t> woff = halo_word_offsets(h, P);
-    std::vector<int32_t> pre((size_t)P * (fw + 1)), first((size_t)std::max<int64_t>(woff[(size_t)P], 1), 0);
+    std::vector<int32_t> pre((size_t)P * (fw + 1));
     for (int q = 0; q < P; ++q) {
         const unsigned long long* b = bq.data() + (size_t)q * fw;
         int32_t* pq = pre.data() + (size_t)q * (fw + 1);
@@ -2414,17 +2415,9 @@ void sbfs_send_bitmaps(Graph& g, Shard& sh) {
         pq[fw] = (int32_t)c;
         if (c != h.send_off[(size_t)q + 1] - h.send_off[(size_t)q])
             fail(JG_ERR_STATE, "sharded BFS: a send list repeats a row");
-        // first row word contributing to send-list word k: the first w whose bits reach position 64 k
-        int64_t w = 0;
-        for (int64_t k = 0; k < woff[(size_t)q + 1] - woff[(size_t)q]; ++k) {
-            while (w < fw && pq[w + 1] <= 64 * k) ++w;
-            first[(size_t)(woff[(size_t)q] + k)] = (int32_t)w;
-        }
     }
     sh.sbfs_bpre.alloc(pre.size());
     copy_h2d(sh.sbfs_bpre.get(), pre.data(), pre.size() * sizeof(int32_t), sh.stream);
-    sh.sbfs_bfirst.alloc(first.size());
-    copy_h2d(sh.sbfs_bfirst.get(), first.data(), first.size() * sizeof(int32_t), sh.stream);
 }
 
 // The level counters of slot `slot` summed into every shard's global slot (gctr), on the streams: a
@@ -2595,7 +2588,6 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
         for (int k = 0; k < 3; ++k) a.fb[k] = t.fb.get() + k * a.fw;
         a.bq = sh.sbfs_bq.get();
         a.bpre = sh.sbfs_bpre.get();
-        a.bfirst = sh.sbfs_bfirst.get();
         a.hb = t.hb.get();
         a.mk = t.mk.get();
         a.st8 = sh.sbfs_stamp.get();
@@ -2637,9 +2629,10 @@ int dobfs_sharded(Graph& g, int64_t src_shard, int64_t src_local, int max_depth,
     std::vector<dim3> gpre(ns), gmid(ns), gpost(ns);
     for (size_t i = 0; i < ns; ++i) {
         St& t = st[i];
-        const int64_t pack_trip = kBlock, mid_trip = (kBlock / kWave) * 16;  // (the pack: a send-list word per thread)
+        const Shard& sh = *g.shards[i];
+        const int64_t mid_trip = (kBlock / kWave) * 16;
         const int64_t fx = std::max<int64_t>(kSbfsAppendBlocks / g.P, 1);
-        const int64_t pack_x = std::min<int64_t>((t.sw_max + pack_trip - 1) / pack_trip, 256);
+        const int64_t pack_x = std::min<int64_t>((((sh.rows + 63) / 64) + kBlock - 1) / kBlock, 256);  // a row word per thread
         const int64_t mid_x = std::min<int64_t>((t.rw_max + mid_trip - 1) / mid_trip, 256);
         gpre[i] = dim3((unsigned)std::max<int64_t>({pack_x, fx, 1}), (unsigned)g.P);
         gmid[i] = dim3((unsigned)std::max<int64_t>(mid_x, 1), (unsigned)g.P);

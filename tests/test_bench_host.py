@@ -88,3 +88,21 @@ def test_bench_trace_cuts_windows_at_the_markers(tmp_path):
     p = blk["pr"]
     assert not p["marked"] and p["dispatches_per_run"] == 2
     assert p["trace_span_ms"] == pytest.approx(0.020) and p["within_step"]
+
+
+def test_roofline_reports_fabric_fraction_beside_the_model():
+    """a block whose workload has a committed PMC summary carries frac_fabric (the
+    counters' fabric bytes over the run's time) beside the model's work-equivalent frac."""
+    r = bench.hbm_roofline(3.758e9, 0.75, "k", "pagerank_fp64_rmat24_ef16", "m")
+    assert r["traffic"] is not None and "frac_fabric" in r
+    assert abs(r["frac_fabric"] - r["traffic"] / 0.75e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-4
+    assert "frac_fabric" not in bench.hbm_roofline(1e9, 1.0, "k")
+
+
+def test_code_identity(monkeypatch):
+    """The bench line names what it measured: JG_BENCH_HEAD (the GPU box gets the tree without .git) and
+    content hashes of bench.py and the library (bench_trace.py copies both into its summary)."""
+    monkeypatch.setenv("JG_BENCH_HEAD", "abc1234")
+    head, code = bench.code_identity()
+    assert head == "abc1234" and len(code["bench_py_sha16"]) == 16
+    assert set(code) == {"bench_py_sha16", "libjanusgpu_sha16"}
