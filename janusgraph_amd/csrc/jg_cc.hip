@@ -103,30 +103,57 @@ __global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t
 // edge, `giant`: 4 MB at RMAT-26, cache-resident) takes the giant's id, and a row without an edge (from
 // label_rows on) is its own component, whose id is its own (vid_is_dense: the graph's ids are its dense
 // indices) or vor[its rank].  Only the other rows gather their label (round 6: 0.78 ms with every row
-// gathering its label at RMAT-26).
+// gathering its label at RMAT-26, 0.388 ms with the giant bits, 0.345 ms with the loads in phases).
 __global__ void cc_giant_bits_kernel(const int32_t* __restrict__ label, int64_t label_rows, const int32_t* giant_label,
                                      unsigned long long* __restrict__ giant) {
     const int32_t gl = *giant_label;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < label_rows; x0 += stride) {  // block-uniform trips
-        const int64_t l = x0 + threadIdx.x;
-        const uint64_t w = __ballot(l < label_rows && label[l] == gl);
-        if (lane_id() == 0 && l < label_rows) giant[l >> 6] = w;
+    constexpr int R = 4;  // bitmap words per wave and trip, their label loads issued together
+    const int64_t span = (int64_t)blockDim.x * R;
+    for (int64_t x0 = (int64_t)blockIdx.x * span; x0 < label_rows; x0 += (int64_t)gridDim.x * span) {  // block-uniform
+        int32_t lab[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t l = x0 + (int64_t)k * blockDim.x + threadIdx.x;
+            lab[k] = l < label_rows ? label[l] : gl ^ 1;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t l = x0 + (int64_t)k * blockDim.x + threadIdx.x;
+            const uint64_t w = __ballot(l < label_rows && lab[k] == gl);
+            if (lane_id() == 0 && l < label_rows) giant[l >> 6] = w;
+        }
     }
 }
+constexpr int kCcOutRun = 8;
 __global__ void cc_output_kernel(const int32_t* __restrict__ label, const int32_t* __restrict__ rank,
                                  int64_t label_rows, const int32_t* __restrict__ local_of_dense,
                                  const int64_t* __restrict__ vor, int64_t n, int64_t* __restrict__ comp,
                                  const unsigned long long* __restrict__ giant, const int32_t* giant_label,
                                  int vid_is_dense) {
     const int64_t giant_id = vor[*giant_label];
-    for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t l = local_of_dense[d];
-        int64_t v;
-        if (l >= label_rows) v = vid_is_dense ? d : vor[rank[l]];
-        else if ((giant[l >> 6] >> (l & 63)) & 1ull) v = giant_id;
-        else v = vor[label[l]];
-        comp[d] = v;
+    // kCcOutRun vertices per thread and trip, in phases (every local index, then every giant-bit word, then
+    // the rare label gathers), so a lane keeps several random reads in flight instead of one dependent chain
+    const int64_t span = (int64_t)blockDim.x * kCcOutRun;
+    for (int64_t d0 = (int64_t)blockIdx.x * span + threadIdx.x; d0 < n; d0 += (int64_t)gridDim.x * span) {
+        int32_t l[kCcOutRun];
+        unsigned long long gw[kCcOutRun];
+#pragma unroll
+        for (int k = 0; k < kCcOutRun; ++k) {
+            const int64_t d = d0 + (int64_t)k * blockDim.x;
+            l[k] = d < n ? local_of_dense[d] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kCcOutRun; ++k) gw[k] = l[k] >= 0 && l[k] < label_rows ? giant[l[k] >> 6] : 0ull;
+#pragma unroll
+        for (int k = 0; k < kCcOutRun; ++k) {
+            const int64_t d = d0 + (int64_t)k * blockDim.x;
+            if (l[k] < 0) continue;
+            int64_t v;
+            if (l[k] >= label_rows) v = vid_is_dense ? d : vor[rank[l[k]]];
+            else if ((gw[k] >> (l[k] & 63)) & 1ull) v = giant_id;
+            else v = vor[label[l[k]]];
+            comp[d] = v;
+        }
     }
 }
 
@@ -1756,10 +1783,10 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         // the giant component's label: row 0's (the highest-degree row; any row would be correct)
         DevBuf<unsigned long long> giant(std::max<int64_t>((lrows + 63) / 64, 1));
         if (lrows > 0) {
-            cc_giant_bits_kernel<<<grid_for(lrows), kBlock, 0, sh.stream>>>(lab, lrows, lab, giant.get());
+            cc_giant_bits_kernel<<<grid_for((lrows + 3) / 4), kBlock, 0, sh.stream>>>(lab, lrows, lab, giant.get());
             JG_LAUNCH_CHECK();
         }
-        cc_output_kernel<<<grid_for(n, kBlock, 8192), kBlock, 0, sh.stream>>>(
+        cc_output_kernel<<<grid_for((n + kCcOutRun - 1) / kCcOutRun, kBlock, 8192), kBlock, 0, sh.stream>>>(
             lab, sh.cc_rank0.get(), lrows, g.padded_dev.get(), g.cc_vor.get(), n, out.get(), giant.get(),
             lrows > 0 ? lab : sh.cc_rank0.get(), g.vid.empty() ? 1 : 0);
         JG_LAUNCH_CHECK();
