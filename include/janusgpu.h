@@ -374,7 +374,7 @@ int jg_graph_sync(jg_graph* g);
  *     "msbfs_exit_first" [1, 256]; "bfs_td_split" [0, 2]; "bfs_td_split_levels" [0, 0xffff];
  *     "bfs_td_split_min" / "_max" [1, 2^31); "bfs_batch0" [1, 64]; "bfs_grid_mult" [1, 64];
  *     "bfs_grid" [64, 65536]; "bfs_tail_grid" [0, 65536]; "merge_temporal" [0, 2];
- *     "sd_delta" [-1, 2^30]; "merge_pack" 0 | 1 | 24; "merge_stage<i>" -1 | 0 | 64 | 128 | 256 | 512;
+ *     "sd_delta" [-1, 2^30]; "sd_dist32" [0, 2]; "merge_pack" 0 | 1 | 24; "merge_stage<i>" -1 | 0 | 64 | 128 | 256 | 512;
  *     read at build: "band<i>_deg" (>= -1), "band<i>_bit" (0 or [3, 8]), "band<i>_sub" (power of two <= 256);
  *   retired (their variants were measured slower and removed; accepted and ignored): "pull_unroll",
  *     "pull_nt", "pull_lds", "light_lds", "slice_lds", "pull_short", "pull_overlap", "bfs_persistent".

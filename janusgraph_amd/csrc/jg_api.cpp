@@ -676,6 +676,7 @@ int jg_tune_set(const char* key, int64_t value) {
         {"bfs_tail_grid", &t.bfs_tail_grid, 0, 65536},
         {"merge_temporal", &t.merge_temporal, 0, 2},
         {"sd_delta", &t.sd_delta, -1, 1 << 30},
+        {"sd_dist32", &t.sd_dist32, 0, 2},
     };
     for (const Knob& kn : knobs) {
         if (k != kn.name) continue;

@@ -43,7 +43,7 @@ struct Csr {
     mutable DevBuf<int32_t> first_col;
     // weight statistics (smallest, sum, count of the non-absent weights), computed on the first weighted
     // shortest distance that needs them (sd_weight_stats)
-    mutable long long wstat[3] = {0, 0, 0};
+    mutable long long wstat[4] = {0, 0, 0, 0};  // sd_weight_stats: min, sum, count, max
     mutable bool wstat_ok = false;
     bool present() const { return row_ptr.size() > 0; }
     int64_t bytes() const { return (int64_t)(row_ptr.bytes() + col.bytes() + weight.bytes()); }
@@ -651,6 +651,8 @@ struct Tune {
     int bfs_grid = 8192;              //         most workgroups of a level launch (sqrt(rows) below; grid-stride)
     int bfs_tail_grid = 64;           //         workgroups of the launches past the deepest of the last 4 traversals
                                       //         (0: every launch at the full grid)
+    int sd_dist32 = 1;                // delta-stepping: 32-bit distances when they cannot overflow (0 never,
+                                      // 1 from 2^23 rows on, 2 at any size; sd_delta_stepping)
     int sd_delta = -1;                // weighted shortest distance with an unbounded hop count (maxDepth >= rows - 1)
                                       // and no negative weight: near-far delta-stepping with this delta (-1:
                                       // automatic, 0: the frontier Bellman-Ford supersteps)

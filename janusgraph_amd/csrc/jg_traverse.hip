@@ -1400,6 +1400,7 @@ __global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(const int32_t* __res
 // Bellman-Ford ones bit for bit (integers, a min); an absent weight on an edge out of a reached row
 // fails the run as there (every reached row is relaxed at least once, at its final distance).
 // Queues hold each row at most once: near entries by a pass stamp, far entries by a flag.
+template <class D>
 struct SdNear {
     const int64_t* rp;
     const int32_t* col;
@@ -1407,7 +1408,7 @@ struct SdNear {
     const int32_t* near;  // the pass's rows and their first edge numbers (edge-balanced: hub rows of
     const int64_t* qoff;  // 10^5 entries would otherwise hold one lane group for the whole pass)
     int64_t nq, mf;       // rows, edges
-    long long* dist;      // LLONG_MAX: unreached
+    D* dist;              // DistTraits<D>::kNone: unreached
     long long T;
     int32_t* stamp;
     int32_t pass;
@@ -1419,7 +1420,15 @@ struct SdNear {
     unsigned long long* far_size;
     int32_t* err;
 };
-__global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear a) {
+// Distances are 64-bit, or 32-bit when every distance the run can store fits (sd_delta_stepping: a row's
+// first distance is a path of at most rows - 1 entries, later ones only fall): half the bytes per
+// random distance read and atomicMin, so twice the rows per cached line.
+template <class D> struct DistTraits;
+template <> struct DistTraits<long long> { static constexpr long long kNone = LLONG_MAX; };
+template <> struct DistTraits<unsigned int> { static constexpr unsigned int kNone = UINT_MAX; };
+
+template <class D>
+__global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear<D> a) {
     __shared__ WaveStage ws;
     WaveApp app{ws};
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
@@ -1458,11 +1467,11 @@ __global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear a) {
                     *a.err = 1;
                 } else {
                     // dist[w] now: it only fell since w was queued
-                    const long long nd = a.dist[w] + (long long)wk;
+                    const long long nd = (long long)a.dist[w] + (long long)wk;
                     // the prefilter reads past L1 (agent scope): a hub row's entry is hit from every XCD at
                     // once, and a stale L1 copy would send each of those lanes to the atomic
-                    if (nd < __hip_atomic_load(&a.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
-                        nd < atomicMin(&a.dist[u], nd)) {
+                    if (nd < (long long)__hip_atomic_load(&a.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                        nd < (long long)atomicMin(&a.dist[u], (D)nd)) {
                         if (nd < a.T) {
                             to_near = atomicExch(&a.stamp[u], a.pass) != a.pass;
                             if (to_near) du = a.rp[u + 1] - a.rp[u];
@@ -1482,8 +1491,9 @@ __global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear a) {
 // The far pile at a threshold change: rows now below T go to the near queue, rows below the previous
 // threshold were relaxed at their final distance already (dropped), the others stay; *minkept gets the
 // smallest distance kept (the next threshold when the near queue comes out empty).
+template <class D>
 __global__ __launch_bounds__(kBlock) void sd_far_split_kernel(const int32_t* __restrict__ far, int64_t fsize,
-                                                              const long long* __restrict__ dist,
+                                                              const D* __restrict__ dist,
                                                               const int64_t* __restrict__ rp, long long t_prev,
                                                               long long T, int32_t* __restrict__ far_flag,
                                                               int32_t* near, int64_t* qoff, unsigned long long* packed,
@@ -1501,7 +1511,7 @@ __global__ __launch_bounds__(kBlock) void sd_far_split_kernel(const int32_t* __r
         int64_t du = 0;
         if (i < fsize) {
             u = far[i];
-            const long long d = dist[u];
+            const long long d = (long long)dist[u];
             keep = d >= T;
             to_near = !keep && d >= t_prev;
             if (keep) mk = (unsigned long long)d < mk ? (unsigned long long)d : mk;
@@ -1521,25 +1531,28 @@ __global__ __launch_bounds__(kBlock) void sd_far_split_kernel(const int32_t* __r
 }
 
 // Weight statistics of a CSR for the delta-stepping gate and its automatic delta: [0] the smallest
-// weight, [1] the sum, [2] the count (absent weights excluded).
+// weight, [1] the sum, [2] the count, [3] the largest (absent weights excluded).
 __global__ void sd_weight_stats_kernel(const int32_t* __restrict__ wt, int64_t nnz, long long* __restrict__ out) {
-    long long mn = LLONG_MAX, sum = 0, cnt = 0;
+    long long mn = LLONG_MAX, mx = LLONG_MIN, sum = 0, cnt = 0;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * blockDim.x) {
         const int32_t w = wt[j];
         if (w == kWeightAbsent) continue;
         mn = w < mn ? w : mn;
+        mx = w > mx ? w : mx;
         sum += w;
         ++cnt;
     }
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
-        const long long a = __shfl_xor(mn, o, kWave);
+        const long long a = __shfl_xor(mn, o, kWave), b = __shfl_xor(mx, o, kWave);
         mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
         sum += __shfl_xor(sum, o, kWave);
         cnt += __shfl_xor(cnt, o, kWave);
     }
     if (lane_id() == 0) {
         atomicMin(&out[0], mn);
+        atomicMax(&out[3], mx);
         atomicAdd((unsigned long long*)&out[1], (unsigned long long)sum);
         atomicAdd((unsigned long long*)&out[2], (unsigned long long)cnt);
     }
@@ -3941,8 +3954,8 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
 const long long* sd_weight_stats(Shard& sh, const Csr& c) {
     if (!c.wstat_ok) {
         hipStream_t s = sh.stream;
-        DevBuf<long long> out(3);
-        const long long init[3] = {LLONG_MAX, 0, 0};
+        DevBuf<long long> out(4);
+        const long long init[4] = {LLONG_MAX, 0, 0, LLONG_MIN};
         copy_h2d(out.get(), init, sizeof init, s);
         if (c.nnz > 0 && c.weight.get()) {
             sd_weight_stats_kernel<<<grid_for(c.nnz), kBlock, 0, s>>>(c.weight.get(), c.nnz, out.get());
@@ -3968,26 +3981,32 @@ long long sd_auto_delta(const long long* ws, int64_t nnz, int64_t rows) {
 // Near-far delta-stepping from `seed` over sh.in (see sd_near_kernel); host[] gets the distances
 // (INT64_MIN: absent); end_ev is recorded once the distances are final, before they are copied out.
 // Returns the near passes run.
-int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, hipEvent_t end_ev) {
+template <class D>
+int sd_delta_stepping_t(Shard& sh, int64_t seed, long long delta, int64_t* host, hipEvent_t end_ev) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows, cap = std::max<int64_t>(rows, 1);
     const Csr& c = sh.in;
-    DevBuf<long long> dist(cap);
+    DevBuf<D> dist(cap);
     DevBuf<int32_t> nq[2] = {DevBuf<int32_t>(cap), DevBuf<int32_t>(cap)};
     DevBuf<int64_t> qo[2] = {DevBuf<int64_t>(cap), DevBuf<int64_t>(cap)};
     DevBuf<int32_t> far[2] = {DevBuf<int32_t>(cap), DevBuf<int32_t>(cap)};
     DevBuf<int32_t> stamp(cap), far_flag(cap), err(1);
     DevBuf<unsigned long long> ctr(3);  // near packed (rows, edges), far entries, the smallest distance kept
-    fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MAX);
-    JG_LAUNCH_CHECK();
+    if constexpr (sizeof(D) == 8) {
+        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(reinterpret_cast<long long*>(dist.get()), rows, LLONG_MAX);
+        JG_LAUNCH_CHECK();
+    } else {
+        JG_HIP(hipMemsetAsync(dist.get(), 0xff, rows * sizeof(D), s));  // UINT_MAX
+    }
     JG_HIP(hipMemsetAsync(stamp.get(), 0, rows * sizeof(int32_t), s));
     JG_HIP(hipMemsetAsync(far_flag.get(), 0, rows * sizeof(int32_t), s));
     JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
     const long long zero = 0;
+    const D dzero = 0;
     const int32_t seed32 = (int32_t)seed;
     int64_t srp[2];
     copy_d2h(srp, c.row_ptr.get() + seed, sizeof srp, s);
-    JG_HIP(hipMemcpyAsync(dist.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+    JG_HIP(hipMemcpyAsync(dist.get() + seed, &dzero, sizeof dzero, hipMemcpyHostToDevice, s));
     JG_HIP(hipMemcpyAsync(nq[0].get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
     JG_HIP(hipMemcpyAsync(qo[0].get(), &zero, sizeof zero, hipMemcpyHostToDevice, s));
     int64_t nsize = 1, medges = srp[1] - srp[0], fsize = 0;
@@ -4007,13 +4026,13 @@ int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, h
                 h[0] = 0;
                 h[1] = (unsigned long long)fsize;
                 copy_h2d(ctr.get(), h, 2 * sizeof(unsigned long long), s);
-                SdNear a{c.row_ptr.get(), c.col.get(), c.weight.get(), nq[cur].get(), qo[cur].get(), nsize, medges,
+                SdNear<D> a{c.row_ptr.get(), c.col.get(), c.weight.get(), nq[cur].get(), qo[cur].get(), nsize, medges,
                          dist.get(), T, stamp.get(), pass, nq[cur ^ 1].get(), qo[cur ^ 1].get(), ctr.get(),
                          far_flag.get(), far[fc].get(), ctr.get() + 1, err.get()};
                 const unsigned grid = (unsigned)std::min<int64_t>(
                     std::max<int64_t>((medges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
                     8192);
-                sd_near_kernel<<<grid, kBlock, 0, s>>>(a);
+                sd_near_kernel<D><<<grid, kBlock, 0, s>>>(a);
                 JG_LAUNCH_CHECK();
                 copy_d2h(h, ctr.get(), 2 * sizeof(unsigned long long), s);
                 unpack();
@@ -4030,7 +4049,7 @@ int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, h
             h[1] = 0;
             h[2] = ULLONG_MAX;
             copy_h2d(ctr.get(), h, sizeof h, s);
-            sd_far_split_kernel<<<grid_for(fsize, kBlock, 4096), kBlock, 0, s>>>(
+            sd_far_split_kernel<D><<<grid_for(fsize, kBlock, 4096), kBlock, 0, s>>>(
                 far[fc].get(), fsize, dist.get(), c.row_ptr.get(), T, T2, far_flag.get(), nq[cur].get(), qo[cur].get(),
                 ctr.get(), far[fc ^ 1].get(), ctr.get() + 1, ctr.get() + 2);
             JG_LAUNCH_CHECK();
@@ -4043,13 +4062,29 @@ int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, h
     }
     JG_HIP(hipEventRecord(end_ev, s));  // the distances are final: their copy-out is the caller's
     region_mark(s, false);
-    std::vector<long long> hd(rows);
-    if (rows) copy_d2h(hd.data(), dist.get(), rows * sizeof(long long), s);
-    for (int64_t l = 0; l < rows; ++l) host[l] = hd[l] == LLONG_MAX ? LLONG_MIN : hd[l];
+    std::vector<D> hd(rows);
+    if (rows) copy_d2h(hd.data(), dist.get(), rows * sizeof(D), s);
+    for (int64_t l = 0; l < rows; ++l) host[l] = hd[l] == DistTraits<D>::kNone ? LLONG_MIN : (int64_t)hd[l];
     int32_t e = 0;
     copy_d2h(&e, err.get(), sizeof e, s);
     if (e) fail(JG_ERR_ARG, kMissingWeight);
     return pass;
+}
+
+// 32-bit distances when no stored distance can reach UINT_MAX: a row's first distance is the length of a
+// path of at most rows - 1 entries (the first-touch tree has no cycle), every later one is smaller, and a
+// candidate adds one more weight (ws: sd_weight_stats).  Tune::sd_dist32: 0 keeps 64 bits, 2 takes 32 when
+// safe, 1 (default) when safe and rows >= 2^23: weights 1..255, tools/sd_bench.py, median ms 64 / 32 bits,
+// RMAT-20 1.197 / 1.249, RMAT-22 3.036 / 3.130, RMAT-24 10.715 / 10.228 (fabric reads -18% at RMAT-22, but
+// the near pass is bound by its random round trips and atomics more than by the lines they move;
+// profiles/r06/sssp32/)
+int sd_delta_stepping(Shard& sh, int64_t seed, long long delta, int64_t* host, hipEvent_t end_ev, const long long* ws) {
+    const unsigned long long wmax = ws[3] > 0 ? (unsigned long long)ws[3] : 0ull;
+    const unsigned long long bound = (unsigned long long)std::max<int64_t>(sh.rows, 1) * wmax;  // rows * wmax
+    const bool want32 = tune().sd_dist32 == 2 || (tune().sd_dist32 == 1 && sh.rows >= (1ll << 23));
+    if (want32 && wmax < (1ull << 31) && (uint64_t)sh.rows < (1ull << 32) && bound < (unsigned long long)UINT_MAX)
+        return sd_delta_stepping_t<unsigned int>(sh, seed, delta, host, end_ev);
+    return sd_delta_stepping_t<long long>(sh, seed, delta, host, end_ev);
 }
 
 void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* dist_out) {
@@ -4096,7 +4131,7 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         if (rows) copy_d2h(h.data(), depth.get(), rows * sizeof(int32_t), s);
         for (int64_t l = 0; l < rows; ++l) host[l] = h[l] >= 0 ? h[l] : LLONG_MIN;
     } else if (seed >= 0 && delta > 0) {
-        levels = sd_delta_stepping(sh, seed, delta, host.data(), t1);
+        levels = sd_delta_stepping(sh, seed, delta, host.data(), t1, sd_weight_stats(sh, sh.in));
         timed_end = true;
     } else if (seed >= 0) {
         const int64_t cap = std::max<int64_t>(rows, 1);

@@ -93,7 +93,8 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_td_rowapply", 0), ("msbfs_td_rowapply", 4), ("bfs_narrow", 0), ("bfs_narrow", 1),
                  ("nb_alpha", 14), ("nb_alpha", 30), ("nb_first", 16), ("halo", 1), ("pull_split", 1), ("band0_sub", 64),
                  ("band0_bit", 0), ("band0_deg", 96), ("band1_bit", 0), ("band1_deg", -1), ("band2_deg", -1),
-                 ("band2_bit", 0), ("sd_delta", 0), ("sd_delta", 64), ("sd_delta", -1)):
+                 ("band2_bit", 0), ("sd_delta", 0), ("sd_delta", 64), ("sd_delta", -1),
+                 ("sd_dist32", 0), ("sd_dist32", 1), ("sd_dist32", 2)):
         _lib.tune_set(k, v)
     # unknown keys (including the variants deleted in round 5: measured slower or equal) and bad values
     for k, v in (("band1_bit", 2), ("no_such_knob", 1), ("merge_pack", 20),
@@ -103,7 +104,7 @@ def test_tune_keys_validate_without_a_gpu():
                  ("msbfs_exit", 3), ("msbfs_exit_live", 1001), ("msbfs_td_noprobe", -1), ("msbfs_exit_first", 0),
                  ("msbfs_scan_queue", 1002), ("msbfs_td_rowapply", -1), ("nb_first", 3), ("nb_alpha", 0),
                  ("bfs_narrow", 2), ("msbfs_td", 3), ("bfs_td_split", 3), ("bfs_td_split_levels", -1),
-                 ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31)):
+                 ("bfs_td_split_min", 0), ("bfs_td_split_max", 1 << 31), ("sd_dist32", 3)):
         with pytest.raises(jg.JanusGpuError) as e:
             _lib.tune_set(k, v)
         assert e.value.code == -1

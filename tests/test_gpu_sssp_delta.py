@@ -31,13 +31,15 @@ def rmat12(oracle_lib):
     return n, vid, s.astype(np.int32), t.astype(np.int32)
 
 
-def run_sd(g, seed_vid, max_depth, delta):
+def run_sd(g, seed_vid, max_depth, delta, dist32=2):
     from janusgraph_amd import _lib
     try:
         _lib.tune_set("sd_delta", delta)
+        _lib.tune_set("sd_dist32", dist32)
         return g.shortest_distance(seed_vid, max_depth)
     finally:
         _lib.tune_set("sd_delta", -1)
+        _lib.tune_set("sd_dist32", 1)
 
 
 @pytest.mark.parametrize("delta", [-1, 1, 3, 64, 100000])
@@ -174,8 +176,8 @@ def test_delta_stepping_rmat16(ctx, oracle_lib):
     g.close()
 
 
-@pytest.mark.parametrize("delta", [-1, 32])
-def test_delta_stepping_rmat20_matches_oracle(ctx, oracle_lib, delta):
+@pytest.mark.parametrize("delta,dist32", [(-1, 2), (32, 2), (-1, 0)])
+def test_delta_stepping_rmat20_matches_oracle(ctx, oracle_lib, delta, dist32):
     """delta-stepping at RMAT-20 (the smallest size README and tools/sd_bench.py time),
     weights 1..255 (Graph500 SSSP style), unbounded hops, seeded at the row of largest in-degree, against
     the oracle's superstep restatement bit for bit (until now only the GPU superstep path was compared
@@ -189,8 +191,31 @@ def test_delta_stepping_rmat20_matches_oracle(ctx, oracle_lib, delta):
     seed = int(np.bincount(t, minlength=n).argmax())
     g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN)
     want = oracle_lib.shortest_distance(n, s, t, seed, DEPTH_INF, w)
-    got = run_sd(g, vid[seed], DEPTH_INF, delta)
+    got = run_sd(g, vid[seed], DEPTH_INF, delta, dist32)
     np.testing.assert_array_equal(got, want)
     assert (want >= 0).sum() > n // 4  # most of the graph reached
     assert ctx.stats()["levels"] > 1
+    g.close()
+
+
+@pytest.mark.parametrize("wexp", [28, 30])
+def test_distance_width_gate(ctx, oracle_lib, wexp):
+    """Tune::sd_dist32 (2: 32 bits at any size when safe, 0: never, 1: from 2^23 rows): 32-bit distances only
+    when rows x the largest weight stays below 2^32 - 1.  A
+    12-row path of weight-2^wexp edges plus a few edges that shorten nothing: 2^28 keeps 32 bits with distances past
+    2^31 (unsigned), 2^30 needs 64 bits (distances past 2^32); both equal the oracle, with 32 bits off too."""
+    import janusgraph_amd as jg
+    n = 12
+    rng = np.random.default_rng(wexp)
+    a, b = rng.integers(0, n, 6), rng.integers(0, n, 6)
+    s = list(range(1, n)) + list(np.minimum(a, b))  # extra edges from a lower to a higher row: no shortcut
+    t = list(range(0, n - 1)) + list(np.maximum(a, b))
+    w = [1 << wexp] * (n - 1) + list(rng.integers(1 << (wexp - 1), 1 << wexp, 6))
+    s, t, w = np.array(s, np.int32), np.array(t, np.int32), np.array(w, np.int32)
+    vid = (np.arange(n, dtype=np.int64) + 5) << 8
+    g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN | jg.ADJ_OUT)
+    want = oracle_lib.shortest_distance(n, s, t, 0, DEPTH_INF, w)
+    assert want.max() > (1 << 31)
+    for dist32 in (2, 0, 1):
+        np.testing.assert_array_equal(run_sd(g, vid[0], DEPTH_INF, -1, dist32), want)
     g.close()

@@ -3,7 +3,7 @@ supersteps (sd_delta = 0) against near-far delta-stepping at several deltas (-1:
 Prints one JSON line: per delta the HIP-event times of `runs` calls, the pass / superstep count, and
 whether the distances equal the supersteps' bit for bit.
 
-  python tools/sd_bench.py [--scale 20] [--runs 5] [--deltas 0,-1,8,32,128] [--wmax 255]
+  python tools/sd_bench.py [--scale 20] [--runs 5] [--deltas 0,-1,8,32,128] [--wmax 255] [--tune k=v ...]
 
 The graph: Graph500 Kronecker edges (A, B, C = 0.57, 0.19, 0.19) drawn here with numpy, weights uniform
 in [1, wmax] (Graph500 SSSP style), built with JG_ADJ_IN; the seed is the row of largest in-degree.
@@ -45,6 +45,7 @@ def main():
     p.add_argument("--runs", type=int, default=5)
     p.add_argument("--deltas", default="0,-1,8,32,128")
     p.add_argument("--wmax", type=int, default=255)
+    p.add_argument("--tune", nargs="*", default=[], help="jg_tune_set knobs key=value applied first (e.g. sd_dist32=0)")
     a = p.parse_args()
     import janusgraph_amd as jg
     n = 1 << a.scale
@@ -53,9 +54,12 @@ def main():
     vid = (np.arange(n, dtype=np.int64) + 1) << 8
     seed = int(np.bincount(t, minlength=n).argmax())
     ctx = jg.Context((0,))
+    for kv in a.tune:
+        k, v = kv.split("=")
+        jg._lib.tune_set(k, int(v))
     g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN)
     out = {"workload": f"sssp_unbounded_rmat{a.scale}_ef{a.ef}_w1-{a.wmax}", "n": n, "m": len(s), "seed_row": seed,
-           "runs": a.runs, "results": []}
+           "runs": a.runs, "tune": a.tune, "results": []}
     ref = None
     for d in [int(x) for x in a.deltas.split(",")]:
         jg._lib.tune_set("sd_delta", d)
