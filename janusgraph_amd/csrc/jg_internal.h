@@ -257,6 +257,8 @@ struct Shard {
     bool sbfs_stamp_clean = false;           // ... all zero (set when a traversal completes)
     int bfs_hist[4] = {0, 0, 0, 0};          // level counts of the last single-source traversals (newest first)
     int bfs_hist_n = 0;
+    int sd_hist[4] = {0, 0, 0, 0};  // delta-stepping: steps of the last calls (the first batch's size)
+    int sd_hist_n = 0;
     DevBuf<int32_t> kept_depth;              // [kept_nsrc][rows] jg_bfs_keep's depth planes (jg_bfs_kept_row)
     // narrow bit-parallel BFS scratch (<= 8 sources, one shard; jg_narrow.hip), kept across calls
     std::vector<DevBuf<uint8_t>> nb_level;   // [levels][rows + pad] each level's frontier byte (= its new bits)

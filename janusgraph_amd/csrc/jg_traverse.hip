@@ -1400,26 +1400,21 @@ __global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(const int32_t* __res
 // Bellman-Ford ones bit for bit (integers, a min); an absent weight on an edge out of a reached row
 // fails the run as there (every reached row is relaxed at least once, at its final distance).
 // Queues hold each row at most once: near entries by a pass stamp, far entries by a flag.
-template <class D>
-struct SdNear {
-    const int64_t* rp;
-    const int32_t* col;
-    const int32_t* wt;
-    const int32_t* near;  // the pass's rows and their first edge numbers (edge-balanced: hub rows of
-    const int64_t* qoff;  // 10^5 entries would otherwise hold one lane group for the whole pass)
-    int64_t nq, mf;       // rows, edges
-    D* dist;              // DistTraits<D>::kNone: unreached
-    long long T;
-    int32_t* stamp;
-    int32_t pass;
-    int32_t* near_next;
-    int64_t* qoff_next;
-    unsigned long long* packed;  // near_next: (rows << kPackShift) | edges
-    int32_t* far_flag;
-    int32_t* far;
-    unsigned long long* far_size;
-    int32_t* err;
+//
+// The passes are controlled on the device (round 6): a step is sd_split_kernel (which moves the far pile
+// when the near queue came out empty) and sd_near_kernel (one near pass); both take the step's decision
+// from the state ring and the previous step's counters, as the DO-BFS levels do, and the host enqueues
+// steps in batches and reads the state once per batch.  (A host read per pass cost ~50 us of every pass:
+// RMAT-22, 10 passes, 0.5 of 3.0 ms.)
+struct SdState {     // a step's decision, ring slot = step % kSdRing
+    long long T;     // the threshold: the near pass relaxes rows below it
+    int32_t fc;      // the far pile rows join (far[fc], its size fsz[fc])
+    int32_t split;   // this step moved the far pile before its near pass
+    int32_t done;
+    int32_t end_step;  // done: the step that found nothing left
 };
+constexpr int kSdRing = 4;
+
 // Distances are 64-bit, or 32-bit when every distance the run can store fits (sd_delta_stepping: a row's
 // first distance is a path of at most rows - 1 entries, later ones only fall): half the bytes per
 // random distance read and atomicMin, so twice the rows per cached line.
@@ -1428,25 +1423,160 @@ template <> struct DistTraits<long long> { static constexpr long long kNone = LL
 template <> struct DistTraits<unsigned int> { static constexpr unsigned int kNone = UINT_MAX; };
 
 template <class D>
-__global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear<D> a) {
+struct SdStep {
+    const int64_t* rp;
+    const int32_t* col;
+    const int32_t* wt;
+    D* dist;                    // DistTraits<D>::kNone: unreached
+    int32_t* nq[2];             // near queues: step s relaxes nq[s & 1] (and its first-edge offsets qo),
+    int64_t* qo[2];             // its near pass appends to nq[(s + 1) & 1]
+    unsigned long long* nctr;   // [kSdRing] step s's near queue, packed (rows << kPackShift) | edges
+    int32_t* far[2];            // far piles and their sizes
+    unsigned long long* fsz;    // [2]
+    int32_t* far_flag;
+    int32_t* stamp;             // near-queue stamps (pass = step + 1)
+    unsigned long long* fmin;   // [kSdRing] smallest distance seen in the far pile up to step s
+    SdState* st;                // [kSdRing]
+    unsigned long long* passes; // near passes run (a near queue with rows)
+    int32_t* err;
+    long long delta;
+    int32_t step;
+};
+
+// Step s's decision (every block of both kernels computes it from the same completed inputs): relax the
+// near queue when it has entries; else stop when the far pile is empty; else move the far pile, with the
+// threshold past the previous one by delta, or to the bucket of the smallest far distance seen when that
+// lies further (the host version's two split attempts; any threshold sequence gives the same distances,
+// the bucket only decides how much is relaxed again)
+template <class D>
+__device__ SdState sd_decide(const SdStep<D>& a) {
+    const int ps = (a.step + kSdRing - 1) % kSdRing;
+    const SdState p = a.st[ps];
+    SdState c = p;
+    c.split = 0;
+    if (p.done) return c;
+    if ((a.nctr[a.step % kSdRing] & kEdgeMask) > 0) return c;
+    if (a.fsz[p.fc] == 0) {
+        c.done = 1;
+        c.end_step = a.step;
+        return c;
+    }
+    long long t2 = p.T + a.delta;
+    const unsigned long long m = a.fmin[ps];
+    if (m != ULLONG_MAX) {
+        const long long jump = ((long long)m / a.delta + 1) * a.delta;
+        t2 = jump > t2 ? jump : t2;
+    }
+    c.T = t2;
+    c.fc = p.fc ^ 1;
+    c.split = 1;
+    return c;
+}
+
+// The far pile at a threshold change: rows now below T join the step's near queue, rows below the previous
+// threshold were relaxed at their final distance already (dropped), the others stay (their smallest
+// distance goes to fmin[step]).
+template <class D>
+__global__ __launch_bounds__(kBlock) void sd_split_kernel(SdStep<D> a) {
+    __shared__ SdState s_st;
+    __shared__ long long s_tprev;
     __shared__ WaveStage ws;
+    if (threadIdx.x == 0) {
+        s_st = sd_decide(a);
+        s_tprev = a.st[(a.step + kSdRing - 1) % kSdRing].T;
+        if (blockIdx.x == 0) a.st[a.step % kSdRing] = s_st;
+    }
+    __syncthreads();
+    if (!s_st.split) return;
     WaveApp app{ws};
+    const int from = s_st.fc ^ 1;
+    const int64_t fsize = (int64_t)a.fsz[from];
+    const int32_t* __restrict__ far = a.far[from];
+    const long long T = s_st.T, t_prev = s_tprev;
+    int32_t* nq = a.nq[a.step & 1];
+    int64_t* qo = a.qo[a.step & 1];
+    unsigned long long* packed = a.nctr + a.step % kSdRing;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long mk = ULLONG_MAX;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < fsize; x0 += stride) {  // block-uniform trips
+        const int64_t i = x0 + threadIdx.x;
+        bool to_near = false, keep = false;
+        int32_t u = 0;
+        int64_t du = 0;
+        if (i < fsize) {
+            u = far[i];
+            const long long d = (long long)a.dist[u];
+            keep = d >= T;
+            to_near = !keep && d >= t_prev;
+            if (keep) mk = (unsigned long long)d < mk ? (unsigned long long)d : mk;
+            else a.far_flag[u] = 0;
+            if (to_near) du = a.rp[u + 1] - a.rp[u];
+        }
+        app.append(to_near, u, du, nq, qo, packed);
+        wave_append(keep, u, a.far[s_st.fc], a.fsz + s_st.fc);
+    }
+    app.final(nq, qo, packed);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(mk, o, kWave);
+        mk = t < mk ? t : mk;
+    }
+    if (lane_id() == 0 && mk != ULLONG_MAX) atomicMin(a.fmin + a.step % kSdRing, mk);
+}
+
+// One near pass, edge-balanced over the step's near queue (first-edge numbers, one binary search per 4
+// edges per thread).  Block 0 also keeps the rings: the next step's output counter and far minimum start
+// empty, the far minimum carries over a step without a split, and after a split the emptied pile's size
+// is reset.
+template <class D>
+__global__ __launch_bounds__(kBlock) void sd_near_kernel(SdStep<D> a) {
+    __shared__ SdState s_st;
+    __shared__ long long s_nq, s_mf;
+    __shared__ WaveStage ws;
+    const int cs = a.step % kSdRing;
+    if (threadIdx.x == 0) {
+        s_st = a.st[cs];
+        const unsigned long long h = a.nctr[cs];
+        s_nq = (long long)(h >> kPackShift);
+        s_mf = (long long)(h & kEdgeMask);
+        if (blockIdx.x == 0 && !s_st.done) {
+            a.nctr[(a.step + 2) % kSdRing] = 0ull;
+            a.fmin[(a.step + 2) % kSdRing] = ULLONG_MAX;
+            if (s_st.split) a.fsz[s_st.fc ^ 1] = 0ull;
+            else atomicMin(a.fmin + cs, a.fmin[(a.step + kSdRing - 1) % kSdRing]);
+            if (s_nq > 0) a.passes[0] += 1;  // (as the host-driven passes counted: a queue with rows)
+        }
+    }
+    __syncthreads();
+    if (s_st.done || s_mf == 0) return;
+    WaveApp app{ws};
+    const int64_t nq = s_nq, mf = s_mf;
+    const long long T = s_st.T;
+    const int32_t pass = a.step + 1;
+    const int32_t* __restrict__ near = a.nq[a.step & 1];
+    const int64_t* __restrict__ qoff = a.qo[a.step & 1];
+    int32_t* near_next = a.nq[(a.step + 1) & 1];
+    int64_t* qoff_next = a.qo[(a.step + 1) & 1];
+    unsigned long long* packed = a.nctr + (a.step + 1) % kSdRing;
+    int32_t* far = a.far[s_st.fc];
+    unsigned long long* far_size = a.fsz + s_st.fc;
+    unsigned long long fm = ULLONG_MAX;  // this lane's smallest distance that stays in the far pile
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
-    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    const int64_t tiles = (mf + per_tile - 1) / per_tile;
     for (int64_t t = 0; t < tiles; ++t) {
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= mf) break;  // block-uniform
         const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
         int64_t i = 0, next_bound = 0;
-        if (e0 < a.mf) {
-            int64_t lo = 0, hi = a.nq - 1;
+        if (e0 < mf) {
+            int64_t lo = 0, hi = nq - 1;
             while (lo < hi) {
                 const int64_t mid = (lo + hi + 1) >> 1;
-                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+                if (qoff[mid] <= e0) lo = mid; else hi = mid - 1;
             }
             i = lo;
-            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+            next_bound = i + 1 < nq ? qoff[i + 1] : mf;
         }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) {
@@ -1454,13 +1584,13 @@ __global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear<D> a) {
             bool to_near = false, to_far = false;
             int32_t u = 0;
             int64_t du = 0;
-            if (e < a.mf) {
+            if (e < mf) {
                 while (e >= next_bound) {
                     ++i;
-                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                    next_bound = i + 1 < nq ? qoff[i + 1] : mf;
                 }
-                const int32_t w = a.near[i];
-                const int64_t j = a.rp[w] + (e - a.qoff[i]);
+                const int32_t w = near[i];
+                const int64_t j = a.rp[w] + (e - qoff[i]);
                 u = a.col[j];
                 const int32_t wk = a.wt ? a.wt[j] : 1;
                 if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
@@ -1472,62 +1602,51 @@ __global__ __launch_bounds__(kBlock) void sd_near_kernel(SdNear<D> a) {
                     // once, and a stale L1 copy would send each of those lanes to the atomic
                     if (nd < (long long)__hip_atomic_load(&a.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
                         nd < (long long)atomicMin(&a.dist[u], (D)nd)) {
-                        if (nd < a.T) {
-                            to_near = atomicExch(&a.stamp[u], a.pass) != a.pass;
+                        if (nd < T) {
+                            to_near = atomicExch(&a.stamp[u], pass) != pass;
                             if (to_near) du = a.rp[u + 1] - a.rp[u];
                         } else {
                             to_far = atomicExch(&a.far_flag[u], 1) == 0;
+                            fm = (unsigned long long)nd < fm ? (unsigned long long)nd : fm;
                         }
                     }
                 }
             }
-            app.append(to_near, u, du, a.near_next, a.qoff_next, a.packed);
-            wave_append(to_far, u, a.far, a.far_size);
+            app.append(to_near, u, du, near_next, qoff_next, packed);
+            wave_append(to_far, u, far, far_size);
         }
     }
-    app.final(a.near_next, a.qoff_next, a.packed);
-}
-
-// The far pile at a threshold change: rows now below T go to the near queue, rows below the previous
-// threshold were relaxed at their final distance already (dropped), the others stay; *minkept gets the
-// smallest distance kept (the next threshold when the near queue comes out empty).
-template <class D>
-__global__ __launch_bounds__(kBlock) void sd_far_split_kernel(const int32_t* __restrict__ far, int64_t fsize,
-                                                              const D* __restrict__ dist,
-                                                              const int64_t* __restrict__ rp, long long t_prev,
-                                                              long long T, int32_t* __restrict__ far_flag,
-                                                              int32_t* near, int64_t* qoff, unsigned long long* packed,
-                                                              int32_t* __restrict__ far_next,
-                                                              unsigned long long* __restrict__ far_size,
-                                                              unsigned long long* __restrict__ minkept) {
-    __shared__ WaveStage ws;
-    WaveApp app{ws};
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    unsigned long long mk = ULLONG_MAX;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < fsize; x0 += stride) {  // block-uniform trips
-        const int64_t i = x0 + threadIdx.x;
-        bool to_near = false, keep = false;
-        int32_t u = 0;
-        int64_t du = 0;
-        if (i < fsize) {
-            u = far[i];
-            const long long d = (long long)dist[u];
-            keep = d >= T;
-            to_near = !keep && d >= t_prev;
-            if (keep) mk = (unsigned long long)d < mk ? (unsigned long long)d : mk;
-            else far_flag[u] = 0;
-            if (to_near) du = rp[u + 1] - rp[u];
-        }
-        app.append(to_near, u, du, near, qoff, packed);
-        wave_append(keep, u, far_next, far_size);
-    }
-    app.final(near, qoff, packed);
+    app.final(near_next, qoff_next, packed);
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
-        const unsigned long long t = __shfl_xor(mk, o, kWave);
-        mk = t < mk ? t : mk;
+        const unsigned long long x = __shfl_xor(fm, o, kWave);
+        fm = x < fm ? x : fm;
     }
-    if (lane_id() == 0 && mk != ULLONG_MAX) atomicMin(minkept, mk);
+    if (lane_id() == 0 && fm != ULLONG_MAX) atomicMin(a.fmin + cs, fm);
+}
+
+// The start: every row unreached, no stamps or far flags, the seed at 0 as step 0's near queue, the ring
+// empty, the state before step 0: threshold delta, far pile 0.
+template <class D>
+__global__ void sd_init_kernel(SdStep<D> a, int64_t rows, int32_t seed, long long delta) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
+        a.dist[i] = i == seed ? (D)0 : DistTraits<D>::kNone;
+        a.stamp[i] = 0;
+        a.far_flag[i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.nq[0][0] = seed;
+        a.qo[0][0] = 0;
+        a.nctr[0] = (1ull << kPackShift) | (unsigned long long)(a.rp[seed + 1] - a.rp[seed]);
+        for (int k = 1; k < kSdRing; ++k) a.nctr[k] = 0ull;
+        for (int k = 0; k < kSdRing; ++k) a.fmin[k] = ULLONG_MAX;
+        a.fsz[0] = a.fsz[1] = 0ull;
+        a.passes[0] = 0ull;
+        *a.err = 0;
+        SdState s0{};
+        s0.T = delta;
+        a.st[kSdRing - 1] = s0;
+    }
 }
 
 // Weight statistics of a CSR for the delta-stepping gate and its automatic delta: [0] the smallest
@@ -3991,84 +4110,67 @@ int sd_delta_stepping_t(Shard& sh, int64_t seed, long long delta, int64_t* host,
     DevBuf<int64_t> qo[2] = {DevBuf<int64_t>(cap), DevBuf<int64_t>(cap)};
     DevBuf<int32_t> far[2] = {DevBuf<int32_t>(cap), DevBuf<int32_t>(cap)};
     DevBuf<int32_t> stamp(cap), far_flag(cap), err(1);
-    DevBuf<unsigned long long> ctr(3);  // near packed (rows, edges), far entries, the smallest distance kept
-    if constexpr (sizeof(D) == 8) {
-        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(reinterpret_cast<long long*>(dist.get()), rows, LLONG_MAX);
-        JG_LAUNCH_CHECK();
-    } else {
-        JG_HIP(hipMemsetAsync(dist.get(), 0xff, rows * sizeof(D), s));  // UINT_MAX
+    DevBuf<unsigned long long> ring(2 * kSdRing + 3);  // nctr[kSdRing], fmin[kSdRing], fsz[2], passes
+    DevBuf<SdState> st(kSdRing);
+    SdStep<D> a{};
+    a.rp = c.row_ptr.get();
+    a.col = c.col.get();
+    a.wt = c.weight.get();
+    a.dist = dist.get();
+    for (int k = 0; k < 2; ++k) {
+        a.nq[k] = nq[k].get();
+        a.qo[k] = qo[k].get();
+        a.far[k] = far[k].get();
     }
-    JG_HIP(hipMemsetAsync(stamp.get(), 0, rows * sizeof(int32_t), s));
-    JG_HIP(hipMemsetAsync(far_flag.get(), 0, rows * sizeof(int32_t), s));
-    JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
-    const long long zero = 0;
-    const D dzero = 0;
-    const int32_t seed32 = (int32_t)seed;
-    int64_t srp[2];
-    copy_d2h(srp, c.row_ptr.get() + seed, sizeof srp, s);
-    JG_HIP(hipMemcpyAsync(dist.get() + seed, &dzero, sizeof dzero, hipMemcpyHostToDevice, s));
-    JG_HIP(hipMemcpyAsync(nq[0].get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
-    JG_HIP(hipMemcpyAsync(qo[0].get(), &zero, sizeof zero, hipMemcpyHostToDevice, s));
-    int64_t nsize = 1, medges = srp[1] - srp[0], fsize = 0;
-    int cur = 0, fc = 0;
-    int32_t pass = 0;
-    long long T = delta;  // every row below the previous threshold is final
-    unsigned long long h[3];
-    auto unpack = [&]() {
-        nsize = (int64_t)(h[0] >> kPackShift);
-        medges = (int64_t)(h[0] & kEdgeMask);
-        fsize = (int64_t)h[1];
-    };
-    for (;;) {
-        while (nsize > 0) {  // near passes: relax the rows below T until none falls below it again
-            ++pass;
-            if (medges > 0) {
-                h[0] = 0;
-                h[1] = (unsigned long long)fsize;
-                copy_h2d(ctr.get(), h, 2 * sizeof(unsigned long long), s);
-                SdNear<D> a{c.row_ptr.get(), c.col.get(), c.weight.get(), nq[cur].get(), qo[cur].get(), nsize, medges,
-                         dist.get(), T, stamp.get(), pass, nq[cur ^ 1].get(), qo[cur ^ 1].get(), ctr.get(),
-                         far_flag.get(), far[fc].get(), ctr.get() + 1, err.get()};
-                const unsigned grid = (unsigned)std::min<int64_t>(
-                    std::max<int64_t>((medges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
-                    8192);
-                sd_near_kernel<D><<<grid, kBlock, 0, s>>>(a);
-                JG_LAUNCH_CHECK();
-                copy_d2h(h, ctr.get(), 2 * sizeof(unsigned long long), s);
-                unpack();
-            } else {
-                nsize = 0;  // rows without entries relax nothing
-            }
-            cur ^= 1;
-        }
-        if (fsize == 0) break;
-        // the next threshold: T + delta, or past the smallest far distance when that bucket is empty
-        long long T2 = T + delta;
-        for (int k = 0; k < 2 && nsize == 0 && fsize > 0; ++k) {
-            h[0] = 0;
-            h[1] = 0;
-            h[2] = ULLONG_MAX;
-            copy_h2d(ctr.get(), h, sizeof h, s);
-            sd_far_split_kernel<D><<<grid_for(fsize, kBlock, 4096), kBlock, 0, s>>>(
-                far[fc].get(), fsize, dist.get(), c.row_ptr.get(), T, T2, far_flag.get(), nq[cur].get(), qo[cur].get(),
-                ctr.get(), far[fc ^ 1].get(), ctr.get() + 1, ctr.get() + 2);
+    a.nctr = ring.get();
+    a.fmin = ring.get() + kSdRing;
+    a.fsz = ring.get() + 2 * kSdRing;
+    a.passes = ring.get() + 2 * kSdRing + 2;
+    a.far_flag = far_flag.get();
+    a.stamp = stamp.get();
+    a.st = st.get();
+    a.err = err.get();
+    a.delta = delta;
+    sd_init_kernel<D><<<grid_for(rows), kBlock, 0, s>>>(a, rows, (int32_t)seed, delta);
+    JG_LAUNCH_CHECK();
+    // Fixed grids (the host does not know a pass's size): the near pass grid-strides over its edges, a
+    // workgroup whose slice of a tile is past the end leaves at once.  tools/sd_bench.py, weights 1..255,
+    // median ms at a cap of 4096 / 8192 / 16384 / 32768 / 65536 near workgroups: RMAT-24 10.25 / 9.94 / 9.68 /
+    // 9.95 / 10.41, RMAT-22 2.84 / 2.74 / 2.72 (its entries / 4096 = 16384); split 1024 -> 256: equal
+    // (profiles/r06/sssp_ctl/)
+    const unsigned near_grid = (unsigned)std::min<int64_t>(std::max<int64_t>(c.nnz / ((int64_t)kBlock * kTdEdgesPerThread * 4), 64), 16384);
+    const unsigned split_grid = (unsigned)std::min<int64_t>(std::max<int64_t>(rows / ((int64_t)kBlock * 8), 16), 256);
+    // Steps in batches, the state read once per batch: the first sized from the last calls' step counts
+    int step = 0, predicted = 0;
+    for (int k = 0; k < std::min(sh.sd_hist_n, 4); ++k) predicted = std::max(predicted, sh.sd_hist[k]);
+    SdState hs{};
+    for (int batch = predicted > 0 ? predicted + 1 : 16, next_batch = 8;; batch = next_batch, next_batch = std::min(next_batch * 2, 64)) {
+        if (step > (1 << 26)) fail(JG_ERR_STATE, "delta-stepping control did not terminate");
+        for (int k = 0; k < batch; ++k, ++step) {
+            a.step = step;
+            sd_split_kernel<D><<<split_grid, kBlock, 0, s>>>(a);
             JG_LAUNCH_CHECK();
-            copy_d2h(h, ctr.get(), sizeof h, s);
-            unpack();
-            fc ^= 1;
-            if (nsize == 0 && fsize > 0) T2 = ((long long)h[2] / delta + 1) * delta;
+            sd_near_kernel<D><<<near_grid, kBlock, 0, s>>>(a);
+            JG_LAUNCH_CHECK();
         }
-        T = T2;
+        copy_d2h(&hs, st.get() + (step - 1) % kSdRing, sizeof hs, s);
+        if (hs.done) break;
     }
     JG_HIP(hipEventRecord(end_ev, s));  // the distances are final: their copy-out is the caller's
     region_mark(s, false);
+    unsigned long long passes = 0;
+    copy_d2h(&passes, a.passes, sizeof passes, s);
+    // the steps this call needed: up to the one that found nothing left (the next call's first batch)
+    for (int k = 3; k > 0; --k) sh.sd_hist[k] = sh.sd_hist[k - 1];
+    sh.sd_hist[0] = hs.end_step + 1;
+    sh.sd_hist_n = std::min(sh.sd_hist_n + 1, 4);
     std::vector<D> hd(rows);
     if (rows) copy_d2h(hd.data(), dist.get(), rows * sizeof(D), s);
     for (int64_t l = 0; l < rows; ++l) host[l] = hd[l] == DistTraits<D>::kNone ? LLONG_MIN : (int64_t)hd[l];
     int32_t e = 0;
     copy_d2h(&e, err.get(), sizeof e, s);
     if (e) fail(JG_ERR_ARG, kMissingWeight);
-    return pass;
+    return (int)passes;
 }
 
 // 32-bit distances when no stored distance can reach UINT_MAX: a row's first distance is the length of a
