@@ -422,9 +422,10 @@ __global__ void uf_link_up_compress_kernel(int32_t* parent, const int32_t* __res
 // *linked += the entries linked (one atomic per wave; the work counter of jg_stats.algorithmic_bytes)
 __global__ __launch_bounds__(kRedThreads) void uf_link_rest_kernel(int32_t* parent, const int64_t* __restrict__ rp,
                                                                     const int32_t* __restrict__ col, int64_t rows,
-                                                                    int64_t heavy, int k, int32_t giant,
+                                                                    int64_t heavy, int k, const int32_t* giant_p,
                                                                     unsigned long long* __restrict__ linked) {
     __shared__ unsigned long long red[kRedWaves];
+    const int32_t giant = *giant_p;
     const int lane = threadIdx.x & (kWave - 1);
     unsigned long long count = 0;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
@@ -481,14 +482,46 @@ __global__ void uf_sample_kernel(const int32_t* __restrict__ parent, int64_t row
     if (i < n) out[i] = parent[(int64_t)(((uint64_t)i * 0x9E3779B97F4A7C15ull) % (uint64_t)rows)];
 }
 
+// The giant component's root, on the device: of eight candidates (the root of row 0, the highest-degree
+// row, and the first seven sampled roots) the one most frequent among kUfSamples sampled roots.  It
+// replaced a read-back, a host sort of the samples and the next launch (~36 us of idle GPU per call at
+// RMAT-26, round 6; an LDS bitonic sort of the samples took 79 us).  Any choice is correct (Afforest links
+// an edge out of the skipped component from its other end); the most frequent skips the most work.
+constexpr int kUfSamples = 1024, kUfCand = 8;
+__global__ __launch_bounds__(kUfSamples) void uf_giant_kernel(const int32_t* __restrict__ parent,
+                                                              const int32_t* __restrict__ sample,
+                                                              int32_t* __restrict__ giant) {
+    __shared__ int32_t cand[kUfCand];
+    __shared__ int cnt[kUfCand];
+    const int t = threadIdx.x;
+    if (t < kUfCand) {
+        cand[t] = t == 0 ? uf_find(parent, 0) : sample[t - 1];
+        cnt[t] = 0;
+    }
+    const int32_t x = sample[t];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kUfCand; ++k) {
+        const uint64_t b = __ballot(x == cand[k]);
+        if (lane_id() == 0 && b) atomicAdd(&cnt[k], __popcll(b));
+    }
+    __syncthreads();
+    if (t == 0) {
+        int best = 0;
+        for (int k = 1; k < kUfCand; ++k) best = cnt[k] > cnt[best] ? k : best;
+        *giant = cand[best];
+    }
+}
+
 // minr[root] = the smallest rank of the root's component: the giant component through a block
 // reduction (one atomic per block), the others with an atomicMin each (small components).  The final
 // path compression rides along: each row finds its root and stores it when it differs (no hook runs
 // here, so a concurrent find reading a rewritten entry still meets an ancestor).
 __global__ __launch_bounds__(kRedThreads) void uf_minrank_kernel(int32_t* parent, const int32_t* __restrict__ rank,
-                                                                  int64_t rows, int32_t giant,
+                                                                  int64_t rows, const int32_t* giant_p,
                                                                   int32_t* __restrict__ minr) {
     __shared__ int32_t red[kRedWaves];
+    const int32_t giant = *giant_p;
     int32_t g = INT_MAX;
     const int64_t quads = (rows + kQuad - 1) / kQuad;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (int64_t)gridDim.x * blockDim.x) {
@@ -544,7 +577,7 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.  k > 1 (Tune::cc_first)
 // runs the atomic first round of uf_link_first_kernel instead, under the same model.
 bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, int64_t* label_rows,
-                   double* work_bytes) {
+                   double* work_bytes, const std::function<void(const int32_t*, int64_t)>* emit = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
@@ -561,9 +594,19 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     int32_t* parent = sh.cc_msg[0].get();
     int32_t* minr = sh.cc_msg[1].get();
     if ((int64_t)sh.cc_depth.size() < rows) sh.cc_depth.alloc(rows);
-    DevBuf<int32_t> sample(1025);  // 1024 sampled roots, then the heavy-row count
-    DevBuf<unsigned long long> linked(1);
-    JG_HIP(hipMemsetAsync(linked.get(), 0, sizeof(unsigned long long), s));
+    DevBuf<int32_t> sample(kUfSamples + 1);  // the sampled roots, then the giant root
+    if (sh.cc_linked.size() != 1) sh.cc_linked.alloc(1);
+    unsigned long long* linked = sh.cc_linked.get();  // read by the caller after its timed region
+    JG_HIP(hipMemsetAsync(linked, 0, sizeof(unsigned long long), s));
+    // rows of degree >= 64 (a property of the graph: found once, a binary search of the degree-sorted rows)
+    if (sh.cc_heavy < 0) {
+        heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), ne, sample.get());
+        JG_LAUNCH_CHECK();
+        int32_t h = 0;
+        copy_d2h(&h, sample.get(), sizeof h, s);
+        sh.cc_heavy = h;
+    }
+    const int64_t heavy = sh.cc_heavy;
     const int32_t* rank = sh.cc_rank0.get();  // the initial labels are the ranks (cc_prepare_ranks)
     if (kFirst == 1 && c.first_col.get()) {
         uf_hook_first_kernel<<<grid_for((ne + kQuad - 1) / kQuad), kBlock, 0, s>>>(parent, minr, c.first_col.get(), ne);
@@ -580,39 +623,27 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
         JG_LAUNCH_CHECK();
     }
     // the most frequent root among 1024 sampled vertices: the giant component's
-    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, std::max<int64_t>(ne, 1), 1024, sample.get());
+    uf_sample_kernel<<<4, kBlock, 0, s>>>(parent, std::max<int64_t>(ne, 1), kUfSamples, sample.get());
     JG_LAUNCH_CHECK();
-    heavy_rows_kernel<<<1, 1, 0, s>>>(c.row_ptr.get(), ne, sample.get() + 1024);
+    uf_giant_kernel<<<1, kUfSamples, 0, s>>>(parent, sample.get(), sample.get() + kUfSamples);
     JG_LAUNCH_CHECK();
-    std::vector<int32_t> hs(1025);
-    copy_d2h(hs.data(), sample.get(), hs.size() * sizeof(int32_t), s);
-    const int64_t heavy = hs[1024];
-    hs.pop_back();
-    std::sort(hs.begin(), hs.end());
-    int32_t giant = hs[0];
-    size_t best = 0;
-    for (size_t i = 0; i < hs.size();) {
-        size_t j = i;
-        while (j < hs.size() && hs[j] == hs[i]) ++j;
-        if (j - i > best) {
-            best = j - i;
-            giant = hs[i];
-        }
-        i = j;
-    }
+    const int32_t* giant = sample.get() + kUfSamples;
     uf_link_rest_kernel<<<red_grid(ne), kRedThreads, 0, s>>>(parent, c.row_ptr.get(), c.col.get(), ne, heavy, kFirst,
-                                                             giant, linked.get());
+                                                             giant, linked);
     JG_LAUNCH_CHECK();
     uf_minrank_kernel<<<red_grid((ne + kQuad - 1) / kQuad), kRedThreads, 0, s>>>(parent, rank, ne, giant, minr);
     JG_LAUNCH_CHECK();
     // the BFS start picks the sources and rewrites parent into the labels
     double reached = 0;
-    const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get(), &reached);
+    // the caller's output gathers read the labels the BFS start writes: queued between the start and the
+    // levels, so the GPU does not wait for the host's read of the last level state before running them
+    const std::function<void()> out_hook = [&]() { (*emit)(parent, ne); };
+    const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get(), &reached,
+                                       emit ? &out_hook : nullptr);
     const int it = c.nnz > 0 ? d + 1 : 0;
     if (it > kCcMaxIterations - 1) return false;
-    unsigned long long rest = 0;
-    copy_d2h(&rest, linked.get(), sizeof rest, s);
-    *work_bytes = 58.0 * (double)ne + 12.0 * (double)rest + 4.0 * reached;
+    // + 12 B per entry the second round linked: the caller adds them from sh.cc_linked after its timed region
+    *work_bytes = 58.0 * (double)ne + 4.0 * reached;
     *iterations = it;
     *labels = parent;
     *label_rows = ne;  // an edgeless row's label is its own rank: the BFS start writes the rows before ne only
@@ -1689,7 +1720,32 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     const int32_t* uf_labels = nullptr;  // the union-find's labels of shard 0 (when solved)
     int64_t uf_label_rows = sh0.rows;      // its rows from here on take their rank (cc_union_find)
     double uf_bytes = 0;
-    if (uf_one) solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_label_rows, &uf_bytes);
+    // One shard: the caller-order ids are made on the device inside the timed region (VERDICT r05 item 4:
+    // the edgeless rows' labels and the output are work the caller needs; only the copy to the host is
+    // outside).  Sharded graphs assemble them on the host below.
+    DevBuf<int64_t> out;
+    DevBuf<unsigned long long> giant_bits;
+    const bool dev_out = comp_out && dev_maps && n > 0;
+    bool out_done = false;
+    const std::function<void(const int32_t*, int64_t)> emit_output = [&](const int32_t* lab, int64_t lrows) {
+        Shard& sh = *g.shards[0];  // comp[d] = id of rank label[local of d]
+        DeviceGuard dg(sh);
+        if (!out.size()) out.alloc(n);
+        // the giant component's label: row 0's (the highest-degree row; any row would be correct)
+        if (giant_bits.size() < (size_t)std::max<int64_t>((lrows + 63) / 64, 1))
+            giant_bits.alloc(std::max<int64_t>((lrows + 63) / 64, 1));
+        if (lrows > 0) {
+            cc_giant_bits_kernel<<<grid_for((lrows + 3) / 4), kBlock, 0, sh.stream>>>(lab, lrows, lab, giant_bits.get());
+            JG_LAUNCH_CHECK();
+        }
+        cc_output_kernel<<<grid_for((n + kCcOutRun - 1) / kCcOutRun, kBlock, 8192), kBlock, 0, sh.stream>>>(
+            lab, sh.cc_rank0.get(), lrows, g.padded_dev.get(), g.cc_vor.get(), n, out.get(), giant_bits.get(),
+            lrows > 0 ? lab : sh.cc_rank0.get(), g.vid.empty() ? 1 : 0);
+        JG_LAUNCH_CHECK();
+        out_done = true;
+    };
+    if (uf_one)
+        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_label_rows, &uf_bytes, dev_out ? &emit_output : nullptr);
     // Sharded over halo plans: the same from local union-finds, tree labels over the halo and a sharded BFS
     // (cc_union_find_sharded); the sharded BFS takes at most 64 shards (jg_traverse.hip, kMaxShardsBfs).
     int uf_rounds = 0;
@@ -1769,28 +1825,10 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         any = allreduce_or(g, any);
         cur ^= 1;
     }
-    // One shard: the caller-order ids are made on the device inside the timed region (VERDICT r05 item 4:
-    // the edgeless rows' labels and the output are work the caller needs; only the copy to the host is
-    // outside).  Sharded graphs assemble them on the host below.
-    DevBuf<int64_t> out;
-    const bool dev_out = comp_out && dev_maps && n > 0;
-    if (dev_out) {  // comp[d] = id of rank label[local of d]
-        Shard& sh = *g.shards[0];
-        DeviceGuard dg(sh);
-        out.alloc(n);
-        const int32_t* lab = solved ? uf_labels : sh.cc_label.get();
-        const int64_t lrows = solved ? uf_label_rows : n;
-        // the giant component's label: row 0's (the highest-degree row; any row would be correct)
-        DevBuf<unsigned long long> giant(std::max<int64_t>((lrows + 63) / 64, 1));
-        if (lrows > 0) {
-            cc_giant_bits_kernel<<<grid_for((lrows + 3) / 4), kBlock, 0, sh.stream>>>(lab, lrows, lab, giant.get());
-            JG_LAUNCH_CHECK();
-        }
-        cc_output_kernel<<<grid_for((n + kCcOutRun - 1) / kCcOutRun, kBlock, 8192), kBlock, 0, sh.stream>>>(
-            lab, sh.cc_rank0.get(), lrows, g.padded_dev.get(), g.cc_vor.get(), n, out.get(), giant.get(),
-            lrows > 0 ? lab : sh.cc_rank0.get(), g.vid.empty() ? 1 : 0);
-        JG_LAUNCH_CHECK();
-    }
+    // the union-find queued the output behind its BFS start; the other paths (and a union-find that hit
+    // the superstep cap, whose output is stale) make it here
+    if (dev_out && !(solved && uf_one && out_done))
+        emit_output(solved ? uf_labels : g.shards[0]->cc_label.get(), solved ? uf_label_rows : n);
     JG_HIP(hipEventRecord(t1, sh0.stream));
     region_mark(sh0.stream, false);
     JG_HIP(hipEventSynchronize(t1));
@@ -1805,6 +1843,12 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     for (auto& sp : g.shards) nnz += (double)sp->both.nnz;
     ctx.last.edges_traversed = nnz * iteration;
     // the propagation: 16m + 16n per superstep; the union-find: its own pass model
+    if (uf_one && solved) {  // the second round's linked entries (12 B each), read now that the region has ended
+        unsigned long long rest = 0;
+        DeviceGuard dg(sh0);
+        copy_d2h(&rest, sh0.cc_linked.get(), sizeof rest, sh0.stream);
+        uf_bytes += 12.0 * (double)rest;
+    }
     ctx.last.algorithmic_bytes = solved ? uf_bytes : (8.0 * nnz + 16.0 * (double)n) * iteration;
     // the output pass: the giant bits (a 4-byte label read per row with an edge), then per vertex its local
     // index (4 B) and the id stored (8 B); the other rows' label and id gathers are not counted

@@ -20,6 +20,7 @@
 #include <memory>
 #include <atomic>
 #include <mutex>
+#include <functional>
 #include <vector>
 
 #include "jg_common.h"
@@ -238,6 +239,8 @@ struct Shard {
     DevBuf<int32_t> cc_label;      // [rows]
     DevBuf<int32_t> cc_rank0;      // [rows] String-order rank of each own row's id (cc_prepare_ranks, build time)
     DevBuf<int32_t> cc_depth;      // [rows] one shard's union-find path: the BFS depths
+    DevBuf<unsigned long long> cc_linked;  // union-find: entries the second round linked (a stat, read after t1)
+    int64_t cc_heavy = -1;                 // union-find: rows of degree >= 64 of the BOTH CSR (-1: not yet found)
     DevBuf<int32_t> cc_hub_partial;
     DevBuf<int32_t> cc_changed;    // [1]
     // single-source DO-BFS scratch, kept across calls (level-parity ping-pong)
@@ -543,7 +546,9 @@ struct CcRoots {
 // component, by a direction-optimising BFS started at every such vertex that has an edge; -1 if no
 // vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).  *edges_out =
 // adjacency entries of the rows the traversal reached.
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out);
+// after_start (nullable): called once the BFS start (which writes the labels) is enqueued, before its levels
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out,
+                         const std::function<void()>* after_start = nullptr);
 // Sharded (halo plans, every shard of the process): the same from the rows whose label (r.parent) is
 // their rank, r.minr unused, one CcRoots per local shard; -1 if no vertex has an edge (jg_traverse.hip).
 int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);

@@ -430,7 +430,12 @@ __global__ void bfs_init_kernel(int32_t* __restrict__ depth, int64_t rows, int64
 __global__ __launch_bounds__(kBlock) void bfs_init_roots_kernel(int32_t* __restrict__ depth, int64_t rows, CcRoots r,
                                                                 const int64_t* __restrict__ deg_rp, int32_t* queue,
                                                                 int64_t* qoff, unsigned long long* packed,
-                                                                uint8_t* __restrict__ seen) {
+                                                                uint8_t* __restrict__ seen, BfsState* st0, long long total) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // level -1's state: nothing explored (no host copy and sync)
+        BfsState s0{};
+        s0.mu = total;
+        *st0 = s0;
+    }
     // Four rows per thread (16-byte loads and stores: one row per lane left the pass bound by load
     // latency, 218 us at RMAT-26).  A row whose component minimum is another row has an edge, so only
     // the component minima read the row pointers: an edgeless row is its own singleton component.
@@ -1842,7 +1847,8 @@ namespace {
 // bfs_depth_tail_clean); on a BOTH traversal the traversal itself never reads or writes those rows, so the
 // init skips them.
 int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_depth, int32_t* depth,
-                 double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr, bool tail = true) {
+                 double* edges_out, const CcRoots* roots = nullptr, hipEvent_t end_ev = nullptr, bool tail = true,
+                 const std::function<void()>* after_start = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr* push = c.push;
@@ -1852,14 +1858,13 @@ int dobfs_single(Ctx& ctx, Shard& sh, const BfsCsrs& c, int64_t source, int max_
     BfsState* st = reinterpret_cast<BfsState*>(sh.bfs_state.get());
     if (roots) {  // every component's minimum-rank vertex with an edge starts at depth 0
         JG_HIP(hipMemsetAsync(sh.bfs_ctr.get(), 0, kBfsRing * sizeof(unsigned long long), s));
-        BfsState s0{};
-        s0.mu = (long long)degcsr->nnz;
-        copy_h2d(st + kBfsRing - 1, &s0, sizeof s0, s);
         // rows from roots->ne on (no edge) are neither read by the traversal (BOTH: no entry) nor labelled here
         // (cc_output_kernel gives them their rank)
         bfs_init_roots_kernel<<<grid_for((roots->ne + 3) / 4), kBlock, 0, s>>>(
             depth, roots->ne, *roots, degcsr->row_ptr.get(), sh.bfs_queue[0].get(), sh.bfs_qoff[0].get(),
-            sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get());
+            sh.bfs_ctr.get() + kBfsRing - 1, sh.bfs_seen.get(), st + kBfsRing - 1, (long long)degcsr->nnz);
+        JG_LAUNCH_CHECK();
+        if (after_start) (*after_start)();  // (CC: its output gathers, queued before the levels)
     } else {
         // BOTH (push = pull): rows from the empty suffix on have no entry at all, so no bottom-up probe or
         // top-down claim reads their depth or seen byte, only the caller's depth output does.  (Directed,
@@ -2894,13 +2899,14 @@ int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_o
     return dobfs_sharded(g, -1, -1, -1, edges_out, &ms, roots) - 1;
 }
 
-int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out) {
+int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out,
+                         const std::function<void()>* after_start) {
     *edges_out = 0;
     if (sh.rows == 0) return -1;
     const BfsCsrs c{&sh.both, &sh.both};
     // the traversal stops at the first level with an empty frontier, which it counts: the deepest
     // depth is the one before (no depth-max pass over the rows)
-    return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r) - 1;
+    return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r, nullptr, true, after_start) - 1;
 }
 
 
