@@ -471,8 +471,10 @@ def rmat26_both_blocks(jg, ctx, ctl, scale, ef, local=0, cc_plan="replicated"):
     cc = {"workload": wl_cc, "ms": round(cc_ms, 3), "iterations": it, "wall_ms": round(cc_wall, 3),
           "timed_region": "ms: HIP events around the union-find passes, the superstep-count BFS and (one GPU) the "
                           "caller-order output (cc_output_kernel: every vertex's component id, edgeless rows "
-                          "included, gathered into caller order on the device); wall_ms: the call from entry to "
-                          "return, which adds the copy of the n int64 ids to the caller's host array",
+                          "included, gathered into caller order on the device, queued behind the BFS start); one "
+                          "GPU: the end event follows the BFS's last level batch, before the host reads its final "
+                          "level state (as the DO-BFS's); wall_ms: the call from entry to return, which adds that "
+                          "read and the copy of the n int64 ids to the caller's host array",
           "components": int(np.count_nonzero(counts)), "build_ms": round(build_ms, 1),
           "algorithm": "one shard: union-find + one DO-BFS from every component's minimum-rank vertex "
                        "(jg_cc.hip cc_union_find), labels and superstep count identical to the propagation"

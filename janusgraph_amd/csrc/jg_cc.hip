@@ -577,7 +577,8 @@ __global__ void heavy_rows_kernel(const int64_t* __restrict__ rp, int64_t rows, 
 // round (col, both finds) and 4 B per adjacency entry of the rows the BFS reached.  k > 1 (Tune::cc_first)
 // runs the atomic first round of uf_link_first_kernel instead, under the same model.
 bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels, int64_t* label_rows,
-                   double* work_bytes, const std::function<void(const int32_t*, int64_t)>* emit = nullptr) {
+                   double* work_bytes, const std::function<void(const int32_t*, int64_t)>* emit = nullptr,
+                   hipEvent_t end_ev = nullptr) {
     hipStream_t s = sh.stream;
     const int64_t rows = sh.rows;
     const Csr& c = sh.both;
@@ -639,7 +640,7 @@ bool cc_union_find(Ctx& ctx, Shard& sh, int* iterations, const int32_t** labels,
     // levels, so the GPU does not wait for the host's read of the last level state before running them
     const std::function<void()> out_hook = [&]() { (*emit)(parent, ne); };
     const int d = cc_root_eccentricity(ctx, sh, CcRoots{parent, rank, minr, ne}, sh.cc_depth.get(), &reached,
-                                       emit ? &out_hook : nullptr);
+                                       emit ? &out_hook : nullptr, emit ? end_ev : nullptr);
     const int it = c.nnz > 0 ? d + 1 : 0;
     if (it > kCcMaxIterations - 1) return false;
     // + 12 B per entry the second round linked: the caller adds them from sh.cc_linked after its timed region
@@ -1745,7 +1746,8 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
         out_done = true;
     };
     if (uf_one)
-        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_label_rows, &uf_bytes, dev_out ? &emit_output : nullptr);
+        solved = cc_union_find(ctx, sh0, &iteration, &uf_labels, &uf_label_rows, &uf_bytes, dev_out ? &emit_output : nullptr,
+                               dev_out ? t1 : nullptr);
     // Sharded over halo plans: the same from local union-finds, tree labels over the halo and a sharded BFS
     // (cc_union_find_sharded); the sharded BFS takes at most 64 shards (jg_traverse.hip, kMaxShardsBfs).
     int uf_rounds = 0;
@@ -1829,8 +1831,12 @@ void cc_run(Graph& g, int64_t* comp_out, int32_t* iterations_out) {
     // the superstep cap, whose output is stale) make it here
     if (dev_out && !(solved && uf_one && out_done))
         emit_output(solved ? uf_labels : g.shards[0]->cc_label.get(), solved ? uf_label_rows : n);
-    JG_HIP(hipEventRecord(t1, sh0.stream));
-    region_mark(sh0.stream, false);
+    // with the output queued behind the BFS start, the BFS recorded t1 behind its last level batch (the
+    // host's read of the final level state is control, as in the DO-BFS); otherwise it ends here
+    if (!(dev_out && solved && uf_one && out_done)) {
+        JG_HIP(hipEventRecord(t1, sh0.stream));
+        region_mark(sh0.stream, false);
+    }
     JG_HIP(hipEventSynchronize(t1));
     float ms = 0;
     JG_HIP(hipEventElapsedTime(&ms, t0, t1));

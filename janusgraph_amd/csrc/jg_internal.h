@@ -547,8 +547,9 @@ struct CcRoots {
 // vertex has an edge.  The start also writes the labels into r.parent (jg_traverse.hip).  *edges_out =
 // adjacency entries of the rows the traversal reached.
 // after_start (nullable): called once the BFS start (which writes the labels) is enqueued, before its levels
+// end_ev (nullable): recorded behind the last level batch, before the host reads the final level state
 int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out,
-                         const std::function<void()>* after_start = nullptr);
+                         const std::function<void()>* after_start = nullptr, hipEvent_t end_ev = nullptr);
 // Sharded (halo plans, every shard of the process): the same from the rows whose label (r.parent) is
 // their rank, r.minr unused, one CcRoots per local shard; -1 if no vertex has an edge (jg_traverse.hip).
 int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_out);

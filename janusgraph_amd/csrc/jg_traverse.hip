@@ -2900,13 +2900,13 @@ int cc_root_eccentricity_sharded(Graph& g, const CcRoots* roots, double* edges_o
 }
 
 int cc_root_eccentricity(Ctx& ctx, Shard& sh, const CcRoots& r, int32_t* depth, double* edges_out,
-                         const std::function<void()>* after_start) {
+                         const std::function<void()>* after_start, hipEvent_t end_ev) {
     *edges_out = 0;
     if (sh.rows == 0) return -1;
     const BfsCsrs c{&sh.both, &sh.both};
     // the traversal stops at the first level with an empty frontier, which it counts: the deepest
     // depth is the one before (no depth-max pass over the rows)
-    return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r, nullptr, true, after_start) - 1;
+    return dobfs_single(ctx, sh, c, -1, -1, depth, edges_out, &r, end_ev, true, after_start) - 1;
 }
 
 
