@@ -1304,49 +1304,100 @@ __global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsi
 // (qoff), and each thread takes kTdEdgesPerThread consecutive edges of the whole frontier after one
 // binary search, so a hub row's 10^5 in-entries are spread over the grid instead of holding one lane
 // group for the superstep (RMAT-20, weights 1..255, unbounded: 15.8 ms with the lane groups).
+//
+// The supersteps are controlled on the device (round 6, as the delta-stepping steps): superstep t's push
+// and apply take the frontier count from a ring the previous apply filled, and its state (done, the
+// superstep count) from the push's decision; the host enqueues supersteps in batches and reads the state
+// once per batch instead of twice per superstep.
+constexpr int kSdRing = 4;  // decision / counter rings of the device-controlled SD loops
+struct SdSuper {      // superstep t's decision, ring slot t % kSdRing
+    int32_t done;     // no superstep from t on
+    int32_t levels;   // the supersteps counted so far (as the host loop counted them)
+};
 struct SdPush {
     const int64_t* rp;
     const int32_t* col;
     const int32_t* wt;
-    const int32_t* frontier;
-    const int64_t* qoff;
-    int64_t nq, mf;
-    const long long* msg;
+    int32_t* frontier[2];         // superstep t reads frontier[t & 1] (+ qoff), its apply writes [(t + 1) & 1]
+    int64_t* qoff[2];
+    unsigned long long* fr;       // [kSdRing] superstep t's frontier, packed (rows << kPackShift) | edges
+    unsigned long long* tsz;      // [kSdRing] rows superstep t touched
+    SdSuper* st;                  // [kSdRing]
+    long long* msg;
     long long* best;
+    long long* dist;
     int32_t* touched;
-    unsigned long long* tsize;
     int32_t* err;
+    int32_t t;
 };
+__device__ __forceinline__ SdSuper sd_super_decide(const SdPush& a, int64_t* nq, int64_t* mf) {
+    const SdSuper p = a.st[(a.t + kSdRing - 1) % kSdRing];
+    const unsigned long long h = a.fr[a.t % kSdRing];
+    *nq = (int64_t)(h >> kPackShift);
+    *mf = (int64_t)(h & kEdgeMask);
+    SdSuper c = p;
+    if (p.done) return c;
+    if (*nq == 0) {
+        c.done = 1;
+    } else if (*mf == 0) {  // the frontier's rows have no entries: the superstep sends nothing, the run ends
+        c.done = 1;
+        c.levels = a.t;
+    } else {
+        c.levels = a.t;
+    }
+    return c;
+}
 __global__ __launch_bounds__(kBlock) void sd_push_q_kernel(SdPush a) {
+    __shared__ SdSuper s_c;
+    __shared__ int64_t s_nq, s_mf;
+    if (threadIdx.x == 0) {
+        int64_t nq, mf;
+        s_c = sd_super_decide(a, &nq, &mf);
+        s_nq = nq;
+        s_mf = mf;
+        if (blockIdx.x == 0) {
+            a.st[a.t % kSdRing] = s_c;
+            if (!s_c.done) {  // the apply's next frontier and the next push's touched count start at zero
+                a.fr[(a.t + 1) % kSdRing] = 0ull;
+                a.tsz[(a.t + 1) % kSdRing] = 0ull;
+            }
+        }
+    }
+    __syncthreads();
+    if (s_c.done) return;
+    const int64_t nq = s_nq, mf = s_mf;
+    const int32_t* __restrict__ frontier = a.frontier[a.t & 1];
+    const int64_t* __restrict__ qoff = a.qoff[a.t & 1];
+    unsigned long long* tsize = a.tsz + a.t % kSdRing;
     const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per_tile = nthreads * kTdEdgesPerThread;
-    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    const int64_t tiles = (mf + per_tile - 1) / per_tile;
     for (int64_t t = 0; t < tiles; ++t) {
-        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= mf) break;  // block-uniform
         const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
         int64_t i = 0, next_bound = 0;
-        if (e0 < a.mf) {
-            int64_t lo = 0, hi = a.nq - 1;
+        if (e0 < mf) {
+            int64_t lo = 0, hi = nq - 1;
             while (lo < hi) {
                 const int64_t mid = (lo + hi + 1) >> 1;
-                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+                if (qoff[mid] <= e0) lo = mid; else hi = mid - 1;
             }
             i = lo;
-            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+            next_bound = i + 1 < nq ? qoff[i + 1] : mf;
         }
 #pragma unroll
         for (int k = 0; k < kTdEdgesPerThread; ++k) {
             const int64_t e = e0 + k;
             bool first = false;
             int32_t u = 0;
-            if (e < a.mf) {
+            if (e < mf) {
                 while (e >= next_bound) {
                     ++i;
-                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                    next_bound = i + 1 < nq ? qoff[i + 1] : mf;
                 }
-                const int32_t w = a.frontier[i];
-                const int64_t j = a.rp[w] + (e - a.qoff[i]);
+                const int32_t w = frontier[i];
+                const int64_t j = a.rp[w] + (e - qoff[i]);
                 u = a.col[j];
                 const int32_t wk = a.wt ? a.wt[j] : 1;
                 if (wk == kWeightAbsent) {  // the edge function would throw (ShortestDistanceVertexProgram.java:69)
@@ -1359,19 +1410,25 @@ __global__ __launch_bounds__(kBlock) void sd_push_q_kernel(SdPush a) {
                         first = atomicMin(&a.best[u], cand) == LLONG_MAX;
                 }
             }
-            wave_append(first, u, a.touched, a.tsize);
+            wave_append(first, u, a.touched, tsize);
         }
     }
 }
 
 // sd_apply_kernel with the next frontier's first edge numbers (for sd_push_q_kernel)
-__global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(const int32_t* __restrict__ touched, int64_t tsize,
-                                                            long long* __restrict__ best, long long* __restrict__ dist,
-                                                            long long* __restrict__ msg, const int64_t* __restrict__ rp,
-                                                            int32_t* next_frontier, int64_t* next_qoff,
-                                                            unsigned long long* packed) {
+__global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(SdPush a) {
     __shared__ WaveStage ws;
+    if (a.st[a.t % kSdRing].done) return;
     WaveApp app{ws};
+    const int32_t* __restrict__ touched = a.touched;
+    const int64_t tsize = (int64_t)a.tsz[a.t % kSdRing];
+    long long* __restrict__ best = a.best;
+    long long* __restrict__ dist = a.dist;
+    long long* __restrict__ msg = a.msg;
+    const int64_t* __restrict__ rp = a.rp;
+    int32_t* next_frontier = a.frontier[(a.t + 1) & 1];
+    int64_t* next_qoff = a.qoff[(a.t + 1) & 1];
+    unsigned long long* packed = a.fr + (a.t + 1) % kSdRing;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tsize; x0 += stride) {  // block-uniform trips
         const int64_t i = x0 + threadIdx.x;
@@ -1418,7 +1475,6 @@ struct SdState {     // a step's decision, ring slot = step % kSdRing
     int32_t done;
     int32_t end_step;  // done: the step that found nothing left
 };
-constexpr int kSdRing = 4;
 
 // Distances are 64-bit, or 32-bit when every distance the run can store fits (sd_delta_stepping: a row's
 // first distance is a path of at most rows - 1 entries, later ones only fall): half the bytes per
@@ -1628,6 +1684,26 @@ __global__ __launch_bounds__(kBlock) void sd_near_kernel(SdStep<D> a) {
         fm = x < fm ? x : fm;
     }
     if (lane_id() == 0 && fm != ULLONG_MAX) atomicMin(a.fmin + cs, fm);
+}
+
+// The superstep start: distances absent, best empty, the seed at 0 as superstep 1's frontier.
+__global__ void sd_super_init_kernel(SdPush a, int64_t rows, int32_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
+        a.dist[i] = i == seed ? 0ll : LLONG_MIN;
+        a.best[i] = LLONG_MAX;
+        if (i == seed) a.msg[i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.frontier[1][0] = seed;
+        a.qoff[1][0] = 0;
+        for (int k = 0; k < kSdRing; ++k) {
+            a.fr[k] = 0ull;
+            a.tsz[k] = 0ull;
+        }
+        a.fr[1 % kSdRing] = (1ull << kPackShift) | (unsigned long long)(a.rp[seed + 1] - a.rp[seed]);
+        a.st[0] = SdSuper{0, 0};
+        *a.err = 0;
+    }
 }
 
 // The start: every row unreached, no stamps or far flags, the seed at 0 as step 0's near queue, the ring
@@ -4246,51 +4322,46 @@ void shortest_distance_run(Graph& g, int64_t seed_vid, int max_depth, int64_t* d
         DevBuf<long long> dist(cap), msg(cap), best(cap);
         DevBuf<int32_t> fa(cap), fb(cap), touched(cap);
         DevBuf<int64_t> qa(cap), qb(cap);
-        DevBuf<unsigned long long> sizes(2);  // touched rows, the next frontier packed (rows, edges)
+        DevBuf<unsigned long long> ring(2 * kSdRing);  // frontier counts, touched counts
+        DevBuf<SdSuper> sst(kSdRing);
         DevBuf<int32_t> err(1);
-        JG_HIP(hipMemsetAsync(err.get(), 0, sizeof(int32_t), s));
-        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(dist.get(), rows, LLONG_MIN);  // absent
-        fill_ll_kernel<<<grid_for(rows), kBlock, 0, s>>>(best.get(), rows, LLONG_MAX);
+        SdPush a{};
+        a.rp = sh.in.row_ptr.get();
+        a.col = sh.in.col.get();
+        a.wt = sh.in.weight.get();
+        a.frontier[0] = fa.get();
+        a.frontier[1] = fb.get();
+        a.qoff[0] = qa.get();
+        a.qoff[1] = qb.get();
+        a.fr = ring.get();
+        a.tsz = ring.get() + kSdRing;
+        a.st = sst.get();
+        a.msg = msg.get();
+        a.best = best.get();
+        a.dist = dist.get();
+        a.touched = touched.get();
+        a.err = err.get();
+        sd_super_init_kernel<<<grid_for(rows), kBlock, 0, s>>>(a, rows, (int32_t)seed);
         JG_LAUNCH_CHECK();
-        const long long zero = 0;
-        const int32_t seed32 = (int32_t)seed;
-        int64_t srp[2];
-        copy_d2h(srp, sh.in.row_ptr.get() + seed, sizeof srp, s);
-        JG_HIP(hipMemcpyAsync(dist.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
-        JG_HIP(hipMemcpyAsync(msg.get() + seed, &zero, sizeof zero, hipMemcpyHostToDevice, s));
-        JG_HIP(hipMemcpyAsync(fa.get(), &seed32, sizeof seed32, hipMemcpyHostToDevice, s));
-        JG_HIP(hipMemcpyAsync(qa.get(), &zero, sizeof zero, hipMemcpyHostToDevice, s));
-        int64_t fsize = 1, fedges = srp[1] - srp[0];
-        for (int t = 1; t <= max_depth && fsize > 0; ++t) {
-            if (fedges == 0) {  // the frontier's rows have no entries: the superstep sends nothing
-                fsize = 0;
-                levels = t;
-                break;
-            }
-            JG_HIP(hipMemsetAsync(sizes.get(), 0, 2 * sizeof(unsigned long long), s));
-            SdPush a{sh.in.row_ptr.get(), sh.in.col.get(), sh.in.weight.get(), fa.get(), qa.get(), fsize, fedges,
-                     msg.get(), best.get(), touched.get(), sizes.get(), err.get()};
-            const unsigned grid = (unsigned)std::min<int64_t>(
-                std::max<int64_t>((fedges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
-                8192);
-            sd_push_q_kernel<<<grid, kBlock, 0, s>>>(a);
-            JG_LAUNCH_CHECK();
-            unsigned long long ts = 0;
-            copy_d2h(&ts, sizes.get(), sizeof ts, s);
-            unsigned long long np = 0;
-            if (ts > 0) {
-                sd_apply_q_kernel<<<grid_for((int64_t)ts, kBlock, 4096), kBlock, 0, s>>>(
-                    touched.get(), (int64_t)ts, best.get(), dist.get(), msg.get(), sh.in.row_ptr.get(), fb.get(), qb.get(),
-                    sizes.get() + 1);
+        // fixed grids (the host does not know a superstep's size): the push grid-strides over its edges
+        const unsigned push_grid = (unsigned)std::min<int64_t>(
+            std::max<int64_t>(sh.in.nnz / ((int64_t)kBlock * kTdEdgesPerThread * 4), 64), 16384);
+        const unsigned apply_grid = grid_for(rows, kBlock, 4096);
+        SdSuper hs{};
+        int t = 1;
+        for (int batch = std::min(max_depth, 16), next_batch = 8; t <= max_depth;
+             batch = std::min(next_batch, max_depth - t + 1), next_batch = std::min(next_batch * 2, 64)) {
+            for (int k = 0; k < batch; ++k, ++t) {
+                a.t = t;
+                sd_push_q_kernel<<<push_grid, kBlock, 0, s>>>(a);
                 JG_LAUNCH_CHECK();
-                copy_d2h(&np, sizes.get() + 1, sizeof np, s);
+                sd_apply_q_kernel<<<apply_grid, kBlock, 0, s>>>(a);
+                JG_LAUNCH_CHECK();
             }
-            fsize = (int64_t)(np >> kPackShift);
-            fedges = (int64_t)(np & kEdgeMask);
-            fa.swap(fb);
-            qa.swap(qb);
-            levels = t;
+            copy_d2h(&hs, sst.get() + (t - 1) % kSdRing, sizeof hs, s);
+            if (hs.done) break;
         }
+        levels = hs.levels;
         JG_HIP(hipEventRecord(t1, s));  // the distances are final: the copy-out is outside the timed region
         region_mark(s, false);
         timed_end = true;
