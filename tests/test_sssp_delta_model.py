@@ -1,8 +1,11 @@
-"""CPU model of the near-far delta-stepping queue discipline (jg_traverse.hip sd_delta_stepping,
-sd_near_kernel, sd_far_split_kernel) against the oracle's supersteps (oracle/jg_oracle.c
-jo_shortest_distance), no GPU: the pass stamps, the far flags, the drop of far entries below the previous
-threshold and the jump past an empty bucket are restated here step for step, with the passes' relaxations
-applied in a shuffled order (the kernel's lanes race; the result must not depend on the order)."""
+"""CPU model of the near-far delta-stepping step discipline (jg_traverse.hip sd_delta_stepping_t,
+sd_decide, sd_split_kernel, sd_near_kernel: the passes controlled on the device, round 6) against the
+oracle's supersteps (oracle/jg_oracle.c jo_shortest_distance), no GPU: each step relaxes its near queue
+when that has entries, else stops when the far pile is empty, else moves the far pile with the threshold
+past the previous one by delta or at the bucket of the smallest far distance seen (the split's kept
+minimum and every far relaxation since); pass stamps, far flags and the drop of far entries below the
+previous threshold are restated step for step, with each pass's relaxations applied in a shuffled order
+(the kernel's lanes race; the result must not depend on the order)."""
 import numpy as np
 import pytest
 
@@ -25,45 +28,49 @@ def delta_stepping_model(n, s, t, w, seed, delta, rng):
     far_flag = np.zeros(n, bool)
     dist[seed] = 0
     near, far = [seed], []
-    T, npass = delta, 0
+    T, npass, step, fmin_prev = delta, 0, 0, INF
     while True:
-        while near:  # sd_near_kernel passes
-            npass += 1
-            edges = [(x, j) for x in near for j in range(rp[x], rp[x + 1])]
-            rng.shuffle(edges)
-            nxt = []
-            for x, j in edges:
-                u, nd = col[j], dist[x] + int(wt[j])
-                if nd < dist[u]:
-                    dist[u] = nd
-                    if nd < T:
-                        if stamp[u] != npass:
-                            stamp[u] = npass
-                            nxt.append(u)
-                    elif not far_flag[u]:
-                        far_flag[u] = True
-                        far.append(u)
-            near = nxt
-        if not far:
+        # sd_decide / sd_split_kernel
+        if sum(rp[x + 1] - rp[x] for x in near) > 0:
+            fmin = fmin_prev  # no split: the far minimum carries over
+        elif not far:
             break
-        T2 = T + delta
-        for _ in range(2):  # sd_far_split_kernel, again past the smallest kept distance if the bucket is empty
-            if near or not far:
-                break
-            keep, minkept = [], INF
+        else:
+            t2 = T + delta
+            if fmin_prev != INF:
+                t2 = max(t2, (fmin_prev // delta + 1) * delta)
+            keep, fmin = [], INF
             for u in far:
                 d = dist[u]
-                if d >= T2:
+                if d >= t2:
                     keep.append(u)
-                    minkept = min(minkept, d)
+                    fmin = min(fmin, d)
                 else:
                     far_flag[u] = False
                     if d >= T:
                         near.append(u)
-            far = keep
-            if not near and far:
-                T2 = (minkept // delta + 1) * delta
-        T = T2
+            far, T = keep, t2
+        # sd_near_kernel (pass = step + 1); a queue with rows counts as a pass
+        if near:
+            npass += 1
+        edges = [(x, j) for x in near for j in range(rp[x], rp[x + 1])]
+        rng.shuffle(edges)
+        nxt = []
+        for x, j in edges:
+            u, nd = col[j], dist[x] + int(wt[j])
+            if nd < dist[u]:
+                dist[u] = nd
+                if nd < T:
+                    if stamp[u] != step + 1:
+                        stamp[u] = step + 1
+                        nxt.append(u)
+                else:
+                    fmin = min(fmin, nd)
+                    if not far_flag[u]:
+                        far_flag[u] = True
+                        far.append(u)
+        near, fmin_prev = nxt, fmin
+        step += 1
     out = dist.copy()
     out[out == INF] = np.iinfo(np.int64).min
     return out, npass
@@ -89,7 +96,8 @@ def test_delta_stepping_model_matches_oracle(oracle_lib, delta, case):
 
 def test_delta_one_is_one_pass_per_distance(oracle_lib):
     """Weights >= 1 and delta = 1: each pass settles exactly one distance value (what
-    tests/test_gpu_sssp_delta.py::test_delta_path_runs checks on the GPU's pass count)."""
+    tests/test_gpu_sssp_delta.py::test_delta_path_runs checks on the GPU's pass count: at least one pass per
+    distinct distance)."""
     rng = np.random.default_rng(4)
     n, m = 200, 1200
     s, t = rng.integers(0, n, m).astype(np.int32), rng.integers(0, n, m).astype(np.int32)
