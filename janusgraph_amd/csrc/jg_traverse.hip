@@ -33,7 +33,6 @@ namespace jg {
 
 namespace {
 
-constexpr int kTdLanes = 16;         // lanes per frontier vertex in the weighted-SD push
 constexpr int kTdEdgesPerThread = 4;
 constexpr int kBuBatch = 4;             // bottom-up: neighbours probed per step
 constexpr int kBfsRing = 4;            // level-state ring: a level touches slots L-1, L, L+1
@@ -1278,29 +1277,8 @@ __global__ __launch_bounds__(kBlock) void msbfs_td_apply_rows_kernel(int64_t row
 // An edge without the weight property carries kWeightAbsent: a message crossing it is an error, as
 // in Fulgora; distances may be negative, so an absent DISTANCE is reported as INT64_MIN.
 constexpr int32_t kWeightAbsent = INT32_MIN;
-__global__ void sd_apply_kernel(const int32_t* __restrict__ touched, int64_t tsize, long long* __restrict__ best,
-                                long long* __restrict__ dist, long long* __restrict__ msg,
-                                int32_t* __restrict__ next_frontier, unsigned long long* __restrict__ nsize) {
-    const int64_t iters = (tsize + (int64_t)gridDim.x * blockDim.x - 1) / ((int64_t)gridDim.x * blockDim.x);
-    for (int64_t it = 0; it < iters; ++it) {
-        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + it * (int64_t)gridDim.x * blockDim.x;
-        bool improved = false;
-        int32_t u = 0;
-        if (i < tsize) {
-            u = touched[i];
-            const long long b = best[u];
-            best[u] = LLONG_MAX;
-            if (dist[u] == LLONG_MIN || dist[u] > b) {
-                dist[u] = b;
-                msg[u] = b;
-                improved = true;
-            }
-        }
-        wave_append(improved, u, next_frontier, nsize);
-    }
-}
 
-// One shard: the same superstep edge-balanced.  The frontier carries each row's first edge number
+// A superstep edge-balanced: the frontier carries each row's first edge number
 // (qoff), and each thread takes kTdEdgesPerThread consecutive edges of the whole frontier after one
 // binary search, so a hub row's 10^5 in-entries are spread over the grid instead of holding one lane
 // group for the superstep (RMAT-20, weights 1..255, unbounded: 15.8 ms with the lane groups).
@@ -1415,7 +1393,8 @@ __global__ __launch_bounds__(kBlock) void sd_push_q_kernel(SdPush a) {
     }
 }
 
-// sd_apply_kernel with the next frontier's first edge numbers (for sd_push_q_kernel)
+// The apply of a superstep: touched rows whose candidate beats their distance take it and form the next
+// frontier, with its first edge numbers (for sd_push_q_kernel)
 __global__ __launch_bounds__(kBlock) void sd_apply_q_kernel(SdPush a) {
     __shared__ WaveStage ws;
     if (a.st[a.t % kSdRing].done) return;
@@ -1758,53 +1737,101 @@ __global__ void sd_weight_stats_kernel(const int32_t* __restrict__ wt, int64_t n
     }
 }
 
-// Sharded SD push: like sd_push_q_kernel (one lane group per frontier row), but the columns are compact ids of the IN halo plan (own rows
-// in segment 0, peers' vertices in their segments): only own rows enter the touched list; remote
-// candidates wait in the halo slots for the reverse exchange.
-__global__ __launch_bounds__(kBlock) void ssd_push_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                          const int32_t* __restrict__ wt,
-                                                          const int32_t* __restrict__ frontier, int64_t fsize,
-                                                          const long long* __restrict__ msg, long long* __restrict__ best,
-                                                          int tbits, int32_t* __restrict__ touched,
-                                                          unsigned long long* __restrict__ tsize,
-                                                          int32_t* __restrict__ err) {
-    const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTdLanes;
-    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / kTdLanes;
-    const int sub = threadIdx.x % kTdLanes;
-    const int64_t iters = (fsize + ngroups - 1) / ngroups;
-    for (int64_t it = 0; it < iters; ++it) {
-        const int64_t qi = group + it * ngroups;
-        const bool have = qi < fsize;
-        const int32_t w = have ? frontier[qi] : 0;
-        const int64_t j0 = have ? rp[w] : 0, j1 = have ? rp[w + 1] : 0;
-        const long long mw = have ? msg[w] : 0;
-        const int64_t len = j1 - j0;
-        int64_t maxlen = len;
-#pragma unroll
-        for (int o = kTdLanes; o < kWave; o <<= 1) {
-            const int64_t t = __shfl_xor(maxlen, o, kWave);
-            maxlen = t > maxlen ? t : maxlen;
+
+// The peers' candidates for own rows, received at the send-list positions (send_src[k] = own row)
+// Sharded supersteps, edge-balanced as sd_push_q_kernel (round 6; the 16-lane row groups of
+// ssd_push_kernel held a hub row's group for the superstep): the frontier carries each row's first edge
+// number, targets are compact positions, a candidate for a peer's row stays in its halo slot of best
+// (the reverse exchange takes it to the owner), only own rows are listed as touched.
+struct SsdPushQ {
+    const int64_t* rp;
+    const int32_t* col;
+    const int32_t* wt;
+    const int32_t* frontier;
+    const int64_t* qoff;
+    int64_t nq, mf;
+    const long long* msg;
+    long long* best;
+    int tbits;
+    int32_t* touched;
+    unsigned long long* tsize;
+    int32_t* err;
+};
+__global__ __launch_bounds__(kBlock) void ssd_push_q_kernel(SsdPushQ a) {
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = nthreads * kTdEdgesPerThread;
+    const int64_t tiles = (a.mf + per_tile - 1) / per_tile;
+    for (int64_t t = 0; t < tiles; ++t) {
+        if ((t * nthreads + (int64_t)blockIdx.x * blockDim.x) * kTdEdgesPerThread >= a.mf) break;  // block-uniform
+        const int64_t e0 = (t * nthreads + tid) * kTdEdgesPerThread;
+        int64_t i = 0, next_bound = 0;
+        if (e0 < a.mf) {
+            int64_t lo = 0, hi = a.nq - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (a.qoff[mid] <= e0) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
         }
-        for (int64_t k0 = 0; k0 < maxlen; k0 += kTdLanes) {  // wave-uniform trip count
-            const int64_t k = k0 + sub;
+#pragma unroll
+        for (int k = 0; k < kTdEdgesPerThread; ++k) {
+            const int64_t e = e0 + k;
             bool first = false;
             int32_t u = 0;
-            if (k < len) {
-                u = col[j0 + k];
-                const int32_t wk = wt ? wt[j0 + k] : 1;
+            if (e < a.mf) {
+                while (e >= next_bound) {
+                    ++i;
+                    next_bound = i + 1 < a.nq ? a.qoff[i + 1] : a.mf;
+                }
+                const int32_t w = a.frontier[i];
+                const int64_t j = a.rp[w] + (e - a.qoff[i]);
+                u = a.col[j];
+                const int32_t wk = a.wt ? a.wt[j] : 1;
                 if (wk == kWeightAbsent) {
-                    *err = 1;
+                    *a.err = 1;
                 } else {
-                    const long long old = atomicMin(&best[u], mw + (long long)wk);
-                    first = old == LLONG_MAX && (u >> tbits) == 0;
+                    const long long cand = a.msg[w] + (long long)wk;
+                    if (cand < __hip_atomic_load(&a.best[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        first = atomicMin(&a.best[u], cand) == LLONG_MAX && (u >> a.tbits) == 0;
                 }
             }
-            wave_append(first, u, touched, tsize);
+            wave_append(first, u, a.touched, a.tsize);
         }
     }
 }
 
-// The peers' candidates for own rows, received at the send-list positions (send_src[k] = own row)
+// sd_apply_q_kernel's apply with the counts from the host (for ssd_push_q_kernel)
+__global__ __launch_bounds__(kBlock) void ssd_apply_q_kernel(const int32_t* __restrict__ touched, int64_t tsize,
+                                                             long long* __restrict__ best, long long* __restrict__ dist,
+                                                             long long* __restrict__ msg, const int64_t* __restrict__ rp,
+                                                             int32_t* next_frontier, int64_t* next_qoff,
+                                                             unsigned long long* packed) {
+    __shared__ WaveStage ws;
+    WaveApp app{ws};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < tsize; x0 += stride) {  // block-uniform trips
+        const int64_t i = x0 + threadIdx.x;
+        bool improved = false;
+        int32_t u = 0;
+        int64_t du = 0;
+        if (i < tsize) {
+            u = touched[i];
+            const long long b = best[u];
+            best[u] = LLONG_MAX;
+            if (dist[u] == LLONG_MIN || dist[u] > b) {
+                dist[u] = b;
+                msg[u] = b;
+                improved = true;
+                du = rp[u + 1] - rp[u];
+            }
+        }
+        app.append(improved, u, du, next_frontier, next_qoff, packed);
+    }
+    app.final(next_frontier, next_qoff, packed);
+}
+
 __global__ void ssd_recv_kernel(const long long* __restrict__ rbuf, const int32_t* __restrict__ send_src, int64_t nrecv,
                                 long long* __restrict__ best, int32_t* __restrict__ touched,
                                 unsigned long long* __restrict__ tsize) {
@@ -4028,9 +4055,10 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
     struct St {
         DevBuf<long long> best, dist, msg, rbuf;
         DevBuf<int32_t> fa, fb, touched;
+        DevBuf<int64_t> qa, qb;  // the frontier's first edge numbers
         DevBuf<unsigned long long> sizes;
         DevBuf<int32_t> err;
-        int64_t fsize = 0;
+        int64_t fsize = 0, fedges = 0;
     };
     std::vector<St> st(ns);
     std::vector<void*> bv, rv;
@@ -4045,6 +4073,8 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
         t.msg.alloc(rows);
         t.fa.alloc(rows);
         t.fb.alloc(rows);
+        t.qa.alloc(rows);
+        t.qb.alloc(rows);
         t.touched.alloc(rows);
         t.rbuf.alloc(std::max<int64_t>(h.send_off[g.P], 1));
         t.sizes.alloc(2);
@@ -4059,7 +4089,12 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
             copy_h2d(t.dist.get() + seed_local, &zero, sizeof zero, sh.stream);
             copy_h2d(t.msg.get() + seed_local, &zero, sizeof zero, sh.stream);
             copy_h2d(t.fa.get(), &seed32, sizeof seed32, sh.stream);
+            const int64_t zero64 = 0;
+            copy_h2d(t.qa.get(), &zero64, sizeof zero64, sh.stream);
+            int64_t srp[2];
+            copy_d2h(srp, sh.in.row_ptr.get() + seed_local, sizeof srp, sh.stream);
             t.fsize = 1;
+            t.fedges = srp[1] - srp[0];
         }
         bv.push_back(t.best.peer());
         rv.push_back(t.rbuf.peer());
@@ -4082,10 +4117,14 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
             DeviceGuard dg(sh);
             St& t = st[i];
             JG_HIP(hipMemsetAsync(t.sizes.get(), 0, 2 * sizeof(unsigned long long), sh.stream));
-            if (t.fsize > 0) {
-                ssd_push_kernel<<<grid_for(t.fsize * kTdLanes, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
-                    sh.in.row_ptr.get(), sh.in.col.get(), g.has_weights ? sh.in.weight.get() : nullptr, t.fa.get(),
-                    t.fsize, t.msg.get(), t.best.get(), sh.halo_in.tbits, t.touched.get(), t.sizes.get(), t.err.get());
+            if (t.fsize > 0 && t.fedges > 0) {
+                SsdPushQ a{sh.in.row_ptr.get(), sh.in.col.get(), g.has_weights ? sh.in.weight.get() : nullptr, t.fa.get(),
+                           t.qa.get(), t.fsize, t.fedges, t.msg.get(), t.best.get(), sh.halo_in.tbits, t.touched.get(),
+                           t.sizes.get(), t.err.get()};
+                const unsigned grid = (unsigned)std::min<int64_t>(
+                    std::max<int64_t>((t.fedges + (int64_t)kBlock * kTdEdgesPerThread - 1) / ((int64_t)kBlock * kTdEdgesPerThread), 1),
+                    8192);
+                ssd_push_q_kernel<<<grid, kBlock, 0, sh.stream>>>(a);
                 JG_LAUNCH_CHECK();
             }
         }
@@ -4112,14 +4151,17 @@ static void shortest_distance_sharded(Graph& g, int64_t seed_vid, int max_depth,
             unsigned long long ts = 0;
             copy_d2h(&ts, t.sizes.get(), sizeof ts, sh.stream);
             if (ts > 0) {
-                sd_apply_kernel<<<grid_for((int64_t)ts, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
-                    t.touched.get(), (int64_t)ts, t.best.get(), t.dist.get(), t.msg.get(), t.fb.get(), t.sizes.get() + 1);
+                ssd_apply_q_kernel<<<grid_for((int64_t)ts, kBlock, 256 * 8), kBlock, 0, sh.stream>>>(
+                    t.touched.get(), (int64_t)ts, t.best.get(), t.dist.get(), t.msg.get(), sh.in.row_ptr.get(), t.fb.get(),
+                    t.qb.get(), t.sizes.get() + 1);
                 JG_LAUNCH_CHECK();
             }
             unsigned long long nn = 0;
             copy_d2h(&nn, t.sizes.get() + 1, sizeof nn, sh.stream);
-            t.fsize = (int64_t)nn;
+            t.fsize = (int64_t)(nn >> kPackShift);
+            t.fedges = (int64_t)(nn & kEdgeMask);
             t.fa.swap(t.fb);
+            t.qa.swap(t.qb);
             next += t.fsize;
         }
         allreduce_sum_i64(g, &next, 1);

@@ -2,12 +2,13 @@
 The shards run one after another on one stream, so the kernel time per shard is the P-GPU compute
 estimate; the halo volume is what each shard would receive over xGMI per exchange step.
 
-    python tools/shard_sim.py --scale 26 --shards 1 8 [--program pr|bfs|cc|msbfs] [--steps 10]
+    python tools/shard_sim.py --scale 26 --shards 1 8 [--program pr|bfs|cc|msbfs|sd] [--steps 10]
 
 pr:    PageRank supersteps (halo vs the dense allgather layout), per-shard superstep kernel time
 bfs:   sharded single-source DO-BFS from the bench's sources: levels, exchange steps, kernel time
 cc:    the sharded CC propagation (one shard: the union-find path), supersteps and time
 msbfs: the 64-source bit-parallel BFS, levels and time
+sd:    weighted shortest distance, 6 hops (the supersteps; sharded over the IN halo plan), weights 1..255
 Each line carries exchange_values (values all shards receive per exchange step) and its bytes.
 """
 from __future__ import annotations
@@ -103,11 +104,41 @@ def run_both(jg, program, scale, shards, reps, groups=1, group=0):
     return out
 
 
+def run_sd(jg, scale, shards, reps, max_depth=6):
+    """Weighted shortest distance, hop-bounded (the supersteps; sharded: the IN halo plan with the reverse
+    exchange of candidates), Graph500 Kronecker edges with weights 1..255 as tools/sd_bench.py draws them,
+    seeded at the row of largest in-degree."""
+    from sd_bench import kronecker
+    n = 1 << scale
+    s, t = kronecker(scale, 16, 0x55D + scale)
+    w = np.random.default_rng(scale).integers(1, 256, len(s)).astype(np.int32)
+    vid = (np.arange(n, dtype=np.int64) + 1) << 8
+    seed = int(np.bincount(t, minlength=n).argmax())
+    ctx = jg.Context((0,) * shards)
+    g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN)
+    xv = g.info()["exchange_values"]
+    g.shortest_distance(vid[seed], max_depth)
+    rows = []
+    for _ in range(reps):
+        ctx.set_profiling(True)
+        g.shortest_distance(vid[seed], max_depth)
+        st = ctx.stats()
+        ctx.set_profiling(False)
+        rows.append((st["compute_ms"], st["exchange_ms"], st["levels"]))
+    g.close()
+    ctx.close()
+    r = np.array(rows)
+    return {"program": "sd", "shards": shards, "max_depth": max_depth, "exchange_values_all_shards": xv,
+            "runs": len(rows), "compute_ms_all_shards": round(float(np.median(r[:, 0])), 4),
+            "exchange_ms_all_shards": round(float(np.median(r[:, 1])), 4), "levels": int(np.median(r[:, 2])),
+            "kernel_ms_per_shard": round(float(np.median(r[:, 0] - r[:, 1])) / shards, 4)}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=22)
     p.add_argument("--shards", type=int, nargs="+", default=[1, 8])
-    p.add_argument("--program", default="pr", choices=["pr", "bfs", "cc", "msbfs"])
+    p.add_argument("--program", default="pr", choices=["pr", "bfs", "cc", "msbfs", "sd"])
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--reps", type=int, default=3)
@@ -121,6 +152,11 @@ def main():
     for kv in a.tune:
         k, v = kv.split("=")
         jg._lib.tune_set(k, int(v))
+    if a.program == "sd":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        for P in a.shards:
+            print(json.dumps(run_sd(jg, a.scale, P, a.reps)), flush=True)
+        return
     if a.program != "pr":
         for P in a.shards:
             for grp in range(a.groups if a.program == "msbfs" else 1):
