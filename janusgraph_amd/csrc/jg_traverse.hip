@@ -3767,7 +3767,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             std::fprintf(stderr, "[jg msbfs] level %d top-down (shard %d): %lld frontier rows, %lld push entries\n",
                                          level, sh.index, (long long)td.nq, (long long)td.mf);
                         td_queued += (double)td.nq;
-                        if (td.rowapply) td_row_passes += (double)sh.rows;
+                        if (td.rowapply) td_row_passes += (double)pull_live_rows(sh, c);
                         {
                             MsBfsOp op;
                             op.F = t.F[cur].get();
@@ -3781,10 +3781,12 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             op.pos = g.vec_pos(sh, adj_of(sh, c));
                             op.lvl = level + 1;
                             op.live = t.live.get() + 1;
+                            // (the row-order apply stops at the pull adjacency's empty suffix: a push target has a
+                            // pull entry, so no row past it gains a bit after level 0; RMAT-26 BOTH: 34 of 67 M rows)
                             if (td.rowapply)
-                                msbfs_td_apply_rows_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
-                                    sh.rows, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(), td.qoff[qc ^ 1].get(),
-                                    td.ctr.get(), t.live.get());
+                                msbfs_td_apply_rows_kernel<<<grid_for(pull_live_rows(sh, c)), kBlock, 0, sh.stream>>>(
+                                    pull_live_rows(sh, c), op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
+                                    td.qoff[qc ^ 1].get(), td.ctr.get(), t.live.get());
                             else
                                 msbfs_td_apply_kernel<<<grid_for(sh.rows), kBlock, 0, sh.stream>>>(
                                     td.touched.get(), td.ctr.get() + 1, op, c.push->row_ptr.get(), td.queue[qc ^ 1].get(),
