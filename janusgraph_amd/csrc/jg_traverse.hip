@@ -686,12 +686,11 @@ __global__ __launch_bounds__(kWave) void msbfs_init_kernel(const int64_t* __rest
     unsigned long long word = 0;
     for (int t = 0; t < nsrc; ++t)
         if (__shfl(l, t, kWave) == l) word |= 1ull << t;
-    if (l >= 0) {
-        const unsigned long long f = F[pos(l)] | word;
-        F[pos(l)] = f;
-        visited[l] |= word;
-        if (nw0) nw0[l] |= word;  // level 0's new-bit word
-        if (rec_rows) rec_words[s] = f;
+    if (l >= 0) {  // stores, not ORs: a source row past the empty suffix is not cleared first (one shard)
+        F[pos(l)] = word;
+        visited[l] = word;
+        if (nw0) nw0[l] = word;  // level 0's new-bit word
+        if (rec_rows) rec_words[s] = word;
     } else if (rec_rows && s < nsrc) {
         rec_words[s] = 0ull;
     }
@@ -3442,9 +3441,27 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 DeviceGuard dg(sh);
                 St& t = st[i];
                 const BfsCsrs c = pick_csrs(sh, direction);
-                zero_gathered(g, sh, adj_of(sh, c), t.F[0].get(), sizeof(unsigned long long));
-                zero_gathered(g, sh, adj_of(sh, c), t.F[1].get(), sizeof(unsigned long long));
-                JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
+                if (td_one && c.pull == c.push) {
+                    // one shard, BOTH: only rows before the empty suffix are read after level 0 (no gather,
+                    // push target, scan, apply or finalise reaches the rows past it, §5; a directed traversal
+                    // gathers columns without pull entries of their own, so it clears everything); the source
+                    // rows among them get their words stored by the init below.  RMAT-26 BOTH: 34 of 67 M rows,
+                    // three 537 MB clears halved
+                    const int64_t ne = pull_live_rows(sh, c), base = g.vec_pos(sh, adj_of(sh, c)).base;
+                    if (std::getenv("JG_MSBFS_POISON") && ne < sh.rows) {  // (test switch: garbage past the suffix)
+                        const size_t tail = (size_t)(sh.rows - ne) * sizeof(unsigned long long);
+                        JG_HIP(hipMemsetAsync(t.F[0].get() + base + ne, 0xA5, tail, sh.stream));
+                        JG_HIP(hipMemsetAsync(t.F[1].get() + base + ne, 0x5A, tail, sh.stream));
+                        JG_HIP(hipMemsetAsync(t.vis.get() + ne, 0xC3, tail, sh.stream));
+                    }
+                    JG_HIP(hipMemsetAsync(t.F[0].get() + base, 0, (size_t)ne * sizeof(unsigned long long), sh.stream));
+                    JG_HIP(hipMemsetAsync(t.F[1].get() + base, 0, (size_t)ne * sizeof(unsigned long long), sh.stream));
+                    JG_HIP(hipMemsetAsync(t.vis.get(), 0, (size_t)ne * sizeof(unsigned long long), sh.stream));
+                } else {
+                    zero_gathered(g, sh, adj_of(sh, c), t.F[0].get(), sizeof(unsigned long long));
+                    zero_gathered(g, sh, adj_of(sh, c), t.F[1].get(), sizeof(unsigned long long));
+                    JG_HIP(hipMemsetAsync(t.vis.get(), 0, t.vis.bytes(), sh.stream));
+                }
                 if (tds[i].hs.size()) zero_gathered(g, sh, JG_ADJ_BOTH, tds[i].hs.get(), sizeof(unsigned long long));
                 St::Rec* r0 = nullptr;
                 if (td_ok) {  // level 0 as records of the source rows
@@ -4007,13 +4024,20 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                 Shard& sh = *g.shards[i];
                 DeviceGuard dg(sh);
                 St& t = st[i];
+                // one shard, BOTH: the visited words past the empty suffix were not cleared (the init); there only
+                // the source rows hold bits, one per source
+                const BfsCsrs cp = pick_csrs(sh, direction);
+                const int64_t prow = td_one && cp.pull == cp.push ? pull_live_rows(sh, cp) : sh.rows;
                 if (level >= kMsLevelWords) {  // the plane entries are counted only when planes were written
-                    msbfs_pairs_kernel<<<red_grid(sh.rows), kRedThreads, 0, sh.stream>>>(t.vis.get(), sh.rows,
-                                                                                          t.work.get() + 1);
+                    msbfs_pairs_kernel<<<red_grid(prow), kRedThreads, 0, sh.stream>>>(t.vis.get(), prow,
+                                                                                       t.work.get() + 1);
                     JG_LAUNCH_CHECK();
                 }
                 unsigned long long w[3] = {0, 0, 0};
                 copy_d2h(w, t.work.get(), sizeof w, sh.stream);
+                if (level >= kMsLevelWords && prow < sh.rows)
+                    for (int q = 0; q < ns; ++q)
+                        if (src_local[(size_t)q] >= prow && src_shard[(size_t)q] == sh.index) ++w[1];
                 const double live_tasks = t.todo.empty() ? (double)t.all_tasks * pull_levels - t.exit_level_tasks
                                                           : (double)w[0] +
                                                                 (double)t.b0_live_merged +

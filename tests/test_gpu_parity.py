@@ -333,6 +333,31 @@ def test_directed_bfs(ctx, oracle_lib, direction):
     np.testing.assert_array_equal(g.bfs([vid[s]], direction)[0], oracle_lib.bfs(n, ds, dd, s, direction))
 
 
+def test_msbfs_rows_past_the_suffix_are_never_read(ctx, oracle_lib, monkeypatch):
+    """One shard, BOTH: the 64-source BFS clears its frontier and visited words only before the empty suffix
+    (the rows past it are never read after level 0; the source rows among them are stored by the init).
+    With JG_MSBFS_POISON those rows hold garbage instead of whatever the allocator left: every depth row
+    must still match the oracle, isolated sources (in the suffix) included, and so must the level count."""
+    import janusgraph_amd as jg
+    monkeypatch.setenv("JG_MSBFS_POISON", "1")
+    n, vid, src, dst, ds, dd = rmat_case(oracle_lib, 15)
+    g = ctx.build(vid, src, dst, flags=ALL)
+    deg = np.bincount(ds, minlength=n) + np.bincount(dd, minlength=n)
+    iso = np.flatnonzero(deg == 0)[:5]
+    live = np.flatnonzero(deg > 0)
+    conn = live[np.linspace(0, len(live) - 1, 59).astype(np.int64)]
+    srcs = np.concatenate([conn[:20], iso, conn[20:]])
+    assert len(iso) == 5 and len(srcs) == 64
+    depth = g.bfs(vid[srcs], jg.DIR_BOTH)
+    deepest = 0
+    for k, s0 in enumerate(srcs):
+        want = oracle_lib.bfs(n, ds, dd, int(s0), 3)
+        np.testing.assert_array_equal(depth[k], want, err_msg=f"source {k}")
+        deepest = max(deepest, int(want.max()))
+    assert ctx.stats()["levels"] == deepest + 1
+    g.close()
+
+
 @pytest.mark.parametrize("exit_mode", [0, 1, 2])
 def test_directed_multi_source_bfs(ctx, oracle_lib, exit_mode):
     """The 64-source BFS along OUT edges (pulling over the IN adjacency, pushing over OUT) with the early
