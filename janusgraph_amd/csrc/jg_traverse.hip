@@ -760,14 +760,27 @@ __global__ __launch_bounds__(kBlock) void msbfs_frontier_live_kernel(const unsig
     __shared__ unsigned long long red[kBlock / kWave];
     WaveApp app{ws};
     unsigned long long m = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x0 = (int64_t)blockIdx.x * blockDim.x; x0 < rows; x0 += stride) {  // block-uniform trips
-        const int64_t v = x0 + threadIdx.x;
-        const unsigned long long w = v < rows ? F[v] : 0ull;
-        m |= w;
-        const bool take = w != 0ull;
-        const int64_t deg = take ? push_rp[v + 1] - push_rp[v] : 0;
-        app.append(take, (int32_t)v, deg, queue, qoff, packed);
+    // four rows per thread and trip, their loads issued together (one per trip: 217 -> 196 us at RMAT-26,
+    // round 6; the pass reads the frontier words and the row pointers of the frontier rows)
+    constexpr int R = 4;
+    const int64_t span = (int64_t)blockDim.x * R;
+    for (int64_t x0 = (int64_t)blockIdx.x * span; x0 < rows; x0 += (int64_t)gridDim.x * span) {  // block-uniform trips
+        unsigned long long w[R];
+        int64_t deg[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t v = x0 + (int64_t)k * blockDim.x + threadIdx.x;
+            w[k] = v < rows ? F[v] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t v = x0 + (int64_t)k * blockDim.x + threadIdx.x;
+            m |= w[k];
+            deg[k] = w[k] ? push_rp[v + 1] - push_rp[v] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            app.append(w[k] != 0ull, (int32_t)(x0 + (int64_t)k * blockDim.x + threadIdx.x), deg[k], queue, qoff, packed);
     }
     app.final(queue, qoff, packed);
     m = block_reduce(m, OrU64{}, red);
@@ -3965,7 +3978,7 @@ void bfs_run(Graph& g, const int64_t* source_vids, int nsrc, int direction, int 
                             // the scans stop at the empty suffix (RMAT-26 BOTH: 34 M of 67 M rows)
                             const int64_t ne = pull_live_rows(sh, c);
                             if (qnext) {
-                                msbfs_frontier_live_kernel<<<grid_for(ne), kBlock, 0, sh.stream>>>(
+                                msbfs_frontier_live_kernel<<<grid_for((ne + 3) / 4), kBlock, 0, sh.stream>>>(
                                     t.F[cur ^ 1].get(), ne, c.push->row_ptr.get(), tds[i].queue[qc ^ 1].get(),
                                     tds[i].qoff[qc ^ 1].get(), tds[i].ctr.get(), lw);
                                 queued_next = true;
