@@ -198,6 +198,37 @@ def test_delta_stepping_rmat20_matches_oracle(ctx, oracle_lib, delta, dist32):
     g.close()
 
 
+@pytest.mark.parametrize("wpath", [0, 1, 5])
+def test_long_path_crosses_many_batches(ctx, oracle_lib, wpath):
+    """A 3000-row path (the hop-gate test's edge direction) in shuffled ids, plus random edges of weight
+    0..63 that shorten nothing: thousands of buckets (weight 1, delta 1) or of passes inside one bucket
+    (weight 0), so the device-side step rings wrap many times and each call runs many host batches.  The
+    delta path (auto delta and delta = 1, 32- and 64-bit distances) and the Bellman-Ford supersteps
+    (delta = 0, one superstep per hop: the superstep ring wraps too; also with a hop bound that binds)
+    all equal the oracle."""
+    import janusgraph_amd as jg
+    n = 3000
+    rng = np.random.default_rng(40 + wpath)
+    a, b = rng.integers(0, n, 400), rng.integers(0, n, 400)
+    # the extra edges run from a lower to a higher row: against the path's flow, so they shorten nothing
+    s = np.concatenate([np.arange(1, n), np.minimum(a, b)]).astype(np.int32)
+    t = np.concatenate([np.arange(0, n - 1), np.maximum(a, b)]).astype(np.int32)
+    w = np.concatenate([np.full(n - 1, wpath), rng.integers(0, 64, 400)]).astype(np.int32)
+    keep = s != t
+    s, t, w = s[keep], t[keep], w[keep]
+    vid = (rng.permutation(n).astype(np.int64) + 3) << 8
+    g = ctx.build(vid, vid[s], vid[t], weight=w, flags=jg.ADJ_IN | jg.ADJ_OUT)
+    want = oracle_lib.shortest_distance(n, s, t, 0, DEPTH_INF, w)
+    np.testing.assert_array_equal(want, wpath * np.arange(n))
+    for delta in (-1, 1, 0):
+        np.testing.assert_array_equal(run_sd(g, vid[0], DEPTH_INF, delta), want)
+    np.testing.assert_array_equal(run_sd(g, vid[0], DEPTH_INF, 1, 0), want)  # 64-bit distances
+    bounded = oracle_lib.shortest_distance(n, s, t, 0, n // 2, w)
+    assert (bounded == jg.DIST_ABSENT).sum() == n - 1 - n // 2
+    np.testing.assert_array_equal(run_sd(g, vid[0], n // 2, -1), bounded)
+    g.close()
+
+
 @pytest.mark.parametrize("wexp", [28, 30])
 def test_distance_width_gate(ctx, oracle_lib, wexp):
     """Tune::sd_dist32 (2: 32 bits at any size when safe, 0: never, 1: from 2^23 rows): 32-bit distances only
